@@ -1,0 +1,130 @@
+#!/usr/bin/env python
+"""Headline benchmark: CLIP ViT-L/14 image embedding throughput (whole node).
+
+One step = one serving batch per GPU: host-pinned decoded uint8 images (256x256
+RGB, synthetic) -> H2D -> fused resize/normalise/patchify kernel -> ViT-L/14
+image tower (bf16, random-init weights of the real architecture: 24 layers,
+width 1024, 16 heads, patch 14, 224x224) -> fp32 L2-normalised 768-d
+embeddings -> RCCL all-gather of every rank's embeddings (the DP result
+gather).  Weak scaling: the per-GPU batch is fixed, so the global batch grows
+with N.  JPEG decode is not in the timed region (reported separately by
+``--include-decode`` runs, off by default).
+
+Launch: ``python bench.py --gpus 1`` or
+``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``.
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from lumen_amd.models.clip import CLIPModel, PRESETS  # noqa: E402
+
+METRIC = "CLIP ViT-L/14 images/sec (whole node)"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=512, help="images per GPU per step")
+    ap.add_argument("--model", default="ViT-L-14")
+    ap.add_argument("--src-size", type=int, default=256, help="synthetic decoded image side")
+    ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = PRESETS[args.model]
+    model = CLIPModel.random(cfg, seed=0, device=dev, with_text=False)
+    B = args.batch
+    g = torch.Generator().manual_seed(1234 + rank)
+    host = torch.randint(0, 256, (B, args.src_size, args.src_size, 3), generator=g, dtype=torch.uint8).pin_memory()
+    dimg = torch.empty_like(host, device=dev)
+    gathered = torch.empty((world * B, cfg.embed_dim), device=dev, dtype=torch.float32)
+
+    def step():
+        dimg.copy_(host, non_blocking=True)
+        emb = model.encode_image_uint8(dimg)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, emb)
+        else:
+            gathered.copy_(emb)
+        return emb
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    ok = bool(torch.isfinite(gathered).all().item())
+    if rank == 0:
+        ms = dt / args.steps * 1e3
+        total = world * B * args.steps / dt
+        v = cfg.vision
+        S = (v.image_size // v.patch_size) ** 2 + 1
+        W = v.width
+        gemm_flops = 2 * S * (v.layers * (4 * W * W + 2 * W * int(W * v.mlp_ratio))) + 2 * (S - 1) * W * 3 * v.patch_size ** 2
+        attn_flops = v.layers * 4 * S * S * W
+        flops_img = gemm_flops + attn_flops
+        out = {
+            "metric": METRIC,
+            "value": round(total, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random uint8 256x256 RGB images, random-init weights)",
+            "config": {
+                "model": f"CLIP {args.model} image tower",
+                "global_batch": world * B,
+                "seq_len": S,
+                "parallelism": f"dp{world}",
+                "image_size": v.image_size,
+                "per_gpu_batch": B,
+                "includes": "H2D + resize/normalise/patchify + tower + L2 + all-gather",
+            },
+            "tflops_per_gpu": round(flops_img * total / world / 1e12, 1),
+            "finite": ok,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

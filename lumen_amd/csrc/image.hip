@@ -1,0 +1,209 @@
+// Image preprocessing kernels (resize / pad / normalise / layout) for gfx950.
+//
+// A ragged batch of decoded uint8 HWC images (one flat buffer + per-image
+// offset/height/width) is resampled straight into the tensor layout the next
+// kernel wants: NCHW, NHWC, or ViT patch rows [B*P, Kpad] (im2col of the
+// patch-embedding convolution, so the patch GEMM reads it as a plain A matrix).
+//
+// Two geometries cover every preprocessor of the reference:
+//   canvas  : the image is first placed at (ox, oy) in a (cw x ch) canvas filled
+//             with `pad` and the canvas is resized to the output
+//             (VLM pad-to-square, packages/lumen-vlm/.../onnxrt_backend.py:661-719)
+//   dst rect: the image is resized into (dw x dh) at (dx, dy) of the output and
+//             the rest is `pad` (SCRFD letterbox, lumen-face onnxrt_backend.py:749-808;
+//             OCR det resize, lumen-ocr onnxrt_backend.py:338-378)
+// Filters: 0 = PIL BICUBIC (a=-0.5, antialiased on downscale; CLIP
+// onnxrt_backend.py:410-431), 1 = PIL BILINEAR (antialiased), 2 = cv2
+// INTER_LINEAR (half-pixel, no antialias), 3 = cv2 INTER_CUBIC (a=-0.75).
+// Resampling is separable: pass 1 filters rows into an fp32 scratch, pass 2
+// filters columns, normalises ((x/255 - mean)/std, or (x - mean)/std in 0..255
+// units) and writes the layout.
+#include "common.h"
+
+namespace lumen {
+
+// 11 x int64 per image (host passes a [B, 11] int64 tensor)
+struct ImgGeomRaw {
+  int64_t ih, iw, off, cw, ch, ox, oy, dx, dy, dw, dh;
+};
+struct ImgGeom {
+  int ih, iw;        // input image size
+  int64_t off;       // byte offset of image in the flat buffer
+  int cw, ch, ox, oy;  // source canvas: image at (ox, oy) inside (cw x ch)
+  int dx, dy, dw, dh;  // destination rect inside the (OH x OW) output
+};
+__device__ __forceinline__ ImgGeom load_geom(const ImgGeomRaw* r) {
+  ImgGeom g;
+  g.ih = (int)r->ih; g.iw = (int)r->iw; g.off = r->off;
+  g.cw = (int)r->cw; g.ch = (int)r->ch; g.ox = (int)r->ox; g.oy = (int)r->oy;
+  g.dx = (int)r->dx; g.dy = (int)r->dy; g.dw = (int)r->dw; g.dh = (int)r->dh;
+  return g;
+}
+
+struct PrepArgs {
+  const uint8_t* src;
+  const ImgGeomRaw* geom;   // device array [B]
+  float* tmp;            // [B, max_ch, max_dw, 3]
+  int tmp_h, tmp_w;      // scratch dims
+  void* out;
+  int OH, OW;
+  int filter;
+  int swap_rb;           // output channel order reversed (RGB <-> BGR)
+  float mean[3], inv_std[3];
+  float scale;           // 1/255 or 1
+  float pad;             // raw pad value (0..255)
+  int layout;            // 0 NCHW, 1 NHWC, 2 patches
+  int patch;             // patch size for layout 2
+  int kpad;              // padded K (row length) for layout 2
+  int out_bf16;
+};
+
+__device__ __forceinline__ float cubic_w(float x, float a) {
+  x = fabsf(x);
+  if (x < 1.f) return ((a + 2.f) * x - (a + 3.f)) * x * x + 1.f;
+  if (x < 2.f) return (((x - 5.f) * x + 8.f) * x - 4.f) * a;
+  return 0.f;
+}
+__device__ __forceinline__ float filt(float x, int f) {
+  if (f == 0) return cubic_w(x, -0.5f);
+  if (f == 3) return cubic_w(x, -0.75f);
+  x = fabsf(x);
+  return x < 1.f ? 1.f - x : 0.f;
+}
+__device__ __forceinline__ float support(int f) { return (f == 0 || f == 3) ? 2.f : 1.f; }
+
+// 1-D window for output index i of a (in_len -> out_len) resample
+__device__ __forceinline__ void window(int i, int in_len, int out_len, int f, int& x0, int& x1,
+                                       float& center, float& inv_ss) {
+  const float scale = (float)in_len / (float)out_len;
+  if (f >= 2) {  // cv2: no antialias, half-pixel centres, replicate border
+    center = (i + 0.5f) * scale - 0.5f;
+    const int r = (f == 3) ? 2 : 1;
+    x0 = (int)floorf(center) - r + 1;
+    x1 = x0 + 2 * r;
+    inv_ss = 1.f;
+    return;
+  }
+  const float ss = fmaxf(scale, 1.f);
+  const float sup = support(f) * ss;
+  center = (i + 0.5f) * scale;
+  x0 = max((int)(center - sup + 0.5f), 0);
+  x1 = min((int)(center + sup + 0.5f), in_len);
+  inv_ss = 1.f / ss;
+}
+
+// canvas pixel fetch (raw 0..255), pad outside the image
+__device__ __forceinline__ void canvas_px(const uint8_t* img, const ImgGeom& g, int x, int y, float pad, float* c) {
+  const int ix = x - g.ox, iy = y - g.oy;
+  if (ix < 0 || iy < 0 || ix >= g.iw || iy >= g.ih) { c[0] = c[1] = c[2] = pad; return; }
+  const uint8_t* p = img + ((int64_t)iy * g.iw + ix) * 3;
+  c[0] = p[0]; c[1] = p[1]; c[2] = p[2];
+}
+
+// pass 1: horizontal resample of every canvas row into tmp[b][y][x'][3], x' in [0, dw)
+__global__ void prep_h_kernel(PrepArgs a) {
+  const int b = blockIdx.z;
+  const ImgGeom g = load_geom(a.geom + b);
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  const int y = blockIdx.y;
+  if (x >= g.dw || y >= g.ch) return;
+  const uint8_t* img = a.src + g.off;
+  int x0, x1; float center, inv_ss;
+  window(x, g.cw, g.dw, a.filter, x0, x1, center, inv_ss);
+  float acc[3] = {0.f, 0.f, 0.f}, ws = 0.f;
+  for (int sx = x0; sx < x1; ++sx) {
+    float w;
+    int cx = sx;
+    if (a.filter >= 2) { w = filt((float)sx - center, a.filter); cx = min(max(sx, 0), g.cw - 1); }
+    else w = filt(((float)sx - center + 0.5f) * inv_ss, a.filter);
+    float c[3];
+    canvas_px(img, g, cx, y, a.pad, c);
+    acc[0] += w * c[0]; acc[1] += w * c[1]; acc[2] += w * c[2];
+    ws += w;
+  }
+  const float inv = ws != 0.f ? 1.f / ws : 0.f;
+  float* t = a.tmp + (((int64_t)b * a.tmp_h + y) * a.tmp_w + x) * 3;
+  if (a.filter < 2) {  // PIL rounds/clips to uint8 between the two passes
+    for (int k = 0; k < 3; ++k) t[k] = fminf(fmaxf(rintf(acc[k] * inv), 0.f), 255.f);
+  } else {
+    t[0] = acc[0] * inv; t[1] = acc[1] * inv; t[2] = acc[2] * inv;
+  }
+}
+
+// pass 2: vertical resample + normalise + layout
+__global__ void prep_v_kernel(PrepArgs a) {
+  const int b = blockIdx.z;
+  const ImgGeom g = load_geom(a.geom + b);
+  const int ox = blockIdx.x * blockDim.x + threadIdx.x;
+  const int oy = blockIdx.y;
+  if (ox >= a.OW || oy >= a.OH) return;
+  float c[3];
+  const int rx = ox - g.dx, ry = oy - g.dy;
+  if (rx < 0 || ry < 0 || rx >= g.dw || ry >= g.dh) {
+    c[0] = c[1] = c[2] = a.pad;
+  } else {
+    int y0, y1; float center, inv_ss;
+    window(ry, g.ch, g.dh, a.filter, y0, y1, center, inv_ss);
+    float acc[3] = {0.f, 0.f, 0.f}, ws = 0.f;
+    for (int sy = y0; sy < y1; ++sy) {
+      float w;
+      int cy = sy;
+      if (a.filter >= 2) { w = filt((float)sy - center, a.filter); cy = min(max(sy, 0), g.ch - 1); }
+      else w = filt(((float)sy - center + 0.5f) * inv_ss, a.filter);
+      const float* t = a.tmp + (((int64_t)b * a.tmp_h + cy) * a.tmp_w + rx) * 3;
+      acc[0] += w * t[0]; acc[1] += w * t[1]; acc[2] += w * t[2];
+      ws += w;
+    }
+    const float inv = ws != 0.f ? 1.f / ws : 0.f;
+    // PIL / cv2 round and clip to uint8 after each resample pass
+    for (int k = 0; k < 3; ++k) c[k] = fminf(fmaxf(rintf(acc[k] * inv), 0.f), 255.f);
+  }
+  float v[3];
+  for (int k = 0; k < 3; ++k) {
+    const int sk = a.swap_rb ? 2 - k : k;
+    v[k] = (c[sk] * a.scale - a.mean[k]) * a.inv_std[k];
+  }
+  int64_t idx[3];
+  if (a.layout == 0) {
+    for (int k = 0; k < 3; ++k) idx[k] = (((int64_t)b * 3 + k) * a.OH + oy) * a.OW + ox;
+  } else if (a.layout == 1) {
+    for (int k = 0; k < 3; ++k) idx[k] = (((int64_t)b * a.OH + oy) * a.OW + ox) * 3 + k;
+  } else {
+    const int p = a.patch, gw = a.OW / p;
+    const int64_t prow = (int64_t)b * (a.OH / p) * gw + (oy / p) * gw + (ox / p);
+    for (int k = 0; k < 3; ++k) idx[k] = prow * a.kpad + k * p * p + (oy % p) * p + (ox % p);
+  }
+  if (a.out_bf16) {
+    uint16_t* o = (uint16_t*)a.out;
+    for (int k = 0; k < 3; ++k) o[idx[k]] = f2bf(v[k]);
+  } else {
+    float* o = (float*)a.out;
+    for (int k = 0; k < 3; ++k) o[idx[k]] = v[k];
+  }
+}
+
+// zero the K padding columns of patch rows (k in [3p^2, kpad))
+__global__ void patch_pad_kernel(uint16_t* out, int64_t rows, int k0, int kpad) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  for (int k = k0 + (threadIdx.x & 63); k < kpad; k += 64) out[r * kpad + k] = 0;
+}
+
+hipError_t image_prep(const PrepArgs& a, int B, int max_ch, int max_dw, hipStream_t stream) {
+  {
+    dim3 block(128), grid((max_dw + 127) / 128, max_ch, B);
+    hipLaunchKernelGGL(prep_h_kernel, grid, block, 0, stream, a);
+  }
+  {
+    dim3 block(128), grid((a.OW + 127) / 128, a.OH, B);
+    hipLaunchKernelGGL(prep_v_kernel, grid, block, 0, stream, a);
+  }
+  if (a.layout == 2 && a.kpad > 3 * a.patch * a.patch) {
+    const int64_t rows = (int64_t)B * (a.OH / a.patch) * (a.OW / a.patch);
+    hipLaunchKernelGGL(patch_pad_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream,
+                       (uint16_t*)a.out, rows, 3 * a.patch * a.patch, a.kpad);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace lumen

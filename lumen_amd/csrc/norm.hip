@@ -1,0 +1,192 @@
+// Row normalisation kernels: LayerNorm, RMSNorm (optionally fused with the
+// residual add that precedes it), row L2-normalise, and the small CLIP
+// token-assembly helpers.  One wave64 per row, 16-byte vector loads.
+//
+// Reference ops replaced: the LayerNorm / RMSNorm nodes inside the ONNX
+// towers and the numpy `embedding / ||embedding||` at
+// packages/lumen-clip/src/lumen_clip/backends/onnxrt_backend.py:458,545-546 and
+// packages/lumen-face/src/lumen_face/backends/onnxrt_backend.py:1341-1343.
+#include "common.h"
+
+namespace lumen {
+
+// mode 0 = LayerNorm (mean/var, weight, bias), 1 = RMSNorm (weight only)
+template <int CPL>
+__global__ void __launch_bounds__(256)
+norm_rows_kernel(const uint16_t* __restrict__ x, int64_t x_stride, const int64_t* __restrict__ row_idx,
+                 const uint16_t* __restrict__ add, int64_t add_stride,
+                 uint16_t* __restrict__ resid_out, int64_t resid_stride,
+                 const uint16_t* __restrict__ w, const uint16_t* __restrict__ b,
+                 void* __restrict__ out, int64_t out_stride, int out_f32,
+                 int rows, int D, float eps, int mode) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int64_t src_row = row_idx ? row_idx[row] : row;
+  const uint16_t* xr = x + src_row * x_stride;
+  const int nch = D >> 3;
+  float v[CPL][8];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      unpack8(*(const uint4*)(xr + ch * 8), v[c]);
+      if (add) {
+        float a[8];
+        unpack8(*(const uint4*)(add + src_row * add_stride + ch * 8), a);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[c][i] += a[i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[c][i] = 0.f;
+    }
+  }
+  if (resid_out) {
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) *(uint4*)(resid_out + (int64_t)row * resid_stride + ch * 8) = pack8(v[c]);
+    }
+  }
+  float mean = 0.f;
+  if (mode == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[c][i];
+    mean = wave_sum(s) / (float)D;
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float d = v[c][i] - mean;
+        ss += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / (float)D + eps);
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + c * 64;
+    if (ch >= nch) continue;
+    float wf[8], bfv[8];
+    unpack8(*(const uint4*)(w + ch * 8), wf);
+    if (b) unpack8(*(const uint4*)(b + ch * 8), bfv);
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      o[i] = (v[c][i] - mean) * rstd * wf[i];
+      if (b) o[i] += bfv[i];
+    }
+    if (out_f32) {
+      float* op = (float*)out + (int64_t)row * out_stride + ch * 8;
+      *(f32x4_t*)op = (f32x4_t){o[0], o[1], o[2], o[3]};
+      *(f32x4_t*)(op + 4) = (f32x4_t){o[4], o[5], o[6], o[7]};
+    } else {
+      *(uint4*)((uint16_t*)out + (int64_t)row * out_stride + ch * 8) = pack8(o);
+    }
+  }
+}
+
+hipError_t norm_rows(const uint16_t* x, int64_t x_stride, const int64_t* row_idx, const uint16_t* add,
+                     int64_t add_stride, uint16_t* resid_out, int64_t resid_stride, const uint16_t* w,
+                     const uint16_t* b, void* out, int64_t out_stride, int out_f32, int rows, int D,
+                     float eps, int mode, hipStream_t stream) {
+  const int cpl = (D / 8 + 63) / 64;
+  dim3 grid((rows + 3) / 4), block(256);
+#define LN_CASE(N)                                                                                     \
+  case N:                                                                                              \
+    hipLaunchKernelGGL(norm_rows_kernel<N>, grid, block, 0, stream, x, x_stride, row_idx, add,        \
+                       add_stride, resid_out, resid_stride, w, b, out, out_stride, out_f32, rows, D, \
+                       eps, mode);                                                                     \
+    break;
+  switch (cpl) {
+    LN_CASE(1) LN_CASE(2) LN_CASE(3) LN_CASE(4) LN_CASE(6) LN_CASE(8) LN_CASE(16)
+    default:
+      if (cpl == 5) { hipLaunchKernelGGL(norm_rows_kernel<6>, grid, block, 0, stream, x, x_stride, row_idx, add, add_stride, resid_out, resid_stride, w, b, out, out_stride, out_f32, rows, D, eps, mode); }
+      else if (cpl == 7) { hipLaunchKernelGGL(norm_rows_kernel<8>, grid, block, 0, stream, x, x_stride, row_idx, add, add_stride, resid_out, resid_stride, w, b, out, out_stride, out_f32, rows, D, eps, mode); }
+      else if (cpl <= 16) { hipLaunchKernelGGL(norm_rows_kernel<16>, grid, block, 0, stream, x, x_stride, row_idx, add, add_stride, resid_out, resid_stride, w, b, out, out_stride, out_f32, rows, D, eps, mode); }
+      else return hipErrorInvalidValue;
+  }
+#undef LN_CASE
+  return hipGetLastError();
+}
+
+// Row L2 normalisation of fp32 rows in place (embedding epilogue).
+__global__ void __launch_bounds__(256) l2norm_f32_kernel(float* __restrict__ x, int rows, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float* xr = x + (int64_t)row * D;
+  float s = 0.f;
+  for (int i = lane; i < D; i += 64) s += xr[i] * xr[i];
+  s = wave_sum(s);
+  const float inv = 1.0f / fmaxf(sqrtf(s), eps);
+  for (int i = lane; i < D; i += 64) xr[i] *= inv;
+}
+
+hipError_t l2norm_f32(float* x, int rows, int D, float eps, hipStream_t stream) {
+  hipLaunchKernelGGL(l2norm_f32_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, x, rows, D, eps);
+  return hipGetLastError();
+}
+
+// x[b * S + 0, :] = cls[:] + pos[0, :]   (class token row of a ViT token buffer)
+__global__ void cls_fill_kernel(uint16_t* __restrict__ x, int64_t seq_stride, const uint16_t* __restrict__ cls,
+                                const uint16_t* __restrict__ pos, int D) {
+  const int b = blockIdx.x;
+  uint16_t* xr = x + (int64_t)b * seq_stride;
+  for (int ch = threadIdx.x; ch < D / 8; ch += blockDim.x) {
+    float c[8], p[8];
+    unpack8(*(const uint4*)(cls + ch * 8), c);
+    unpack8(*(const uint4*)(pos + ch * 8), p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] += p[i];
+    *(uint4*)(xr + ch * 8) = pack8(c);
+  }
+}
+
+hipError_t cls_fill(uint16_t* x, int64_t seq_stride, const uint16_t* cls, const uint16_t* pos, int B, int D,
+                    hipStream_t stream) {
+  hipLaunchKernelGGL(cls_fill_kernel, dim3(B), dim3(128), 0, stream, x, seq_stride, cls, pos, D);
+  return hipGetLastError();
+}
+
+// out[r, :] = table[ids[r], :] (+ pos[r % S, :])    token / position embedding gather
+__global__ void embed_gather_kernel(const int64_t* __restrict__ ids, const uint16_t* __restrict__ table,
+                                    const uint16_t* __restrict__ pos, int S, uint16_t* __restrict__ out,
+                                    int rows, int D, int64_t vocab, int64_t id_offset) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  int64_t id = ids[row] - id_offset;
+  const bool valid = id >= 0 && id < vocab;
+  const uint16_t* tr = table + (valid ? id : 0) * D;
+  const uint16_t* pr = pos ? pos + (int64_t)(row % S) * D : nullptr;
+  for (int ch = lane; ch < D / 8; ch += 64) {
+    float t[8];
+    if (valid) unpack8(*(const uint4*)(tr + ch * 8), t);
+    else for (int i = 0; i < 8; ++i) t[i] = 0.f;
+    if (pr) {
+      float p[8];
+      unpack8(*(const uint4*)(pr + ch * 8), p);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[i] += p[i];
+    }
+    *(uint4*)(out + (int64_t)row * D + ch * 8) = pack8(t);
+  }
+}
+
+hipError_t embed_gather(const int64_t* ids, const uint16_t* table, const uint16_t* pos, int S, uint16_t* out,
+                        int rows, int D, int64_t vocab, int64_t id_offset, hipStream_t stream) {
+  hipLaunchKernelGGL(embed_gather_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, ids, table, pos, S, out,
+                     rows, D, vocab, id_offset);
+  return hipGetLastError();
+}
+
+}  // namespace lumen

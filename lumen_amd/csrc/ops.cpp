@@ -1,0 +1,275 @@
+// PyTorch-ROCm operator registration for the lumen_amd HIP kernel library.
+//
+// Every op is registered under the `lumen` namespace (torch.ops.lumen.*) with
+// a CUDA (= HIP on ROCm) implementation only: on a GPU tensor the hand-written
+// gfx950 kernel runs on the current HIP stream (so the ops compose with
+// torch.cuda graphs and stream semantics); CPU tensors are rejected here and
+// handled by the Python reference path in lumen_amd.ops.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <ATen/DeviceGuard.h>
+#include <torch/library.h>
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+namespace lumen {
+struct GemmEpi {
+  const void* bias; const uint16_t* residual; const uint16_t* table;
+  int64_t ldr; int64_t ldt; int table_period; int table_offset; int act; int bias_f32;
+  float alpha; int out_group; int64_t out_group_stride; int out_row_offset; int out_f32;
+};
+hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
+                     int64_t ldc, int M, int N, int K, const GemmEpi& ep, int tile, hipStream_t stream);
+hipError_t norm_rows(const uint16_t* x, int64_t x_stride, const int64_t* row_idx, const uint16_t* add,
+                     int64_t add_stride, uint16_t* resid_out, int64_t resid_stride, const uint16_t* w,
+                     const uint16_t* b, void* out, int64_t out_stride, int out_f32, int rows, int D,
+                     float eps, int mode, hipStream_t stream);
+hipError_t l2norm_f32(float* x, int rows, int D, float eps, hipStream_t stream);
+hipError_t cls_fill(uint16_t* x, int64_t seq_stride, const uint16_t* cls, const uint16_t* pos, int B, int D,
+                    hipStream_t stream);
+hipError_t embed_gather(const int64_t* ids, const uint16_t* table, const uint16_t* pos, int S, uint16_t* out,
+                        int rows, int D, int64_t vocab, int64_t id_offset, hipStream_t stream);
+struct AttnArgs {
+  const uint16_t* q; const uint16_t* k; const uint16_t* v; uint16_t* o;
+  int64_t q_sb, q_ss, q_sh; int64_t k_sb, k_ss, k_sh; int64_t v_sb, v_ss, v_sh; int64_t o_sb, o_ss, o_sh;
+  const int* kv_len; int Sq, Sk, H, Hkv; float scale_log2; int causal;
+};
+hipError_t attn_fwd(const AttnArgs& a, int B, int D, hipStream_t stream);
+struct ImgGeomRaw;
+struct PrepArgs {
+  const uint8_t* src; const ImgGeomRaw* geom; float* tmp; int tmp_h, tmp_w; void* out; int OH, OW;
+  int filter; int swap_rb; float mean[3], inv_std[3]; float scale; float pad; int layout; int patch;
+  int kpad; int out_bf16;
+};
+hipError_t image_prep(const PrepArgs& a, int B, int max_ch, int max_dw, hipStream_t stream);
+}  // namespace lumen
+
+namespace {
+
+#define LUMEN_CHECK_HIP(expr)                                                          \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    TORCH_CHECK(_e == hipSuccess, "lumen HIP error: ", hipGetErrorString(_e), " @ ", #expr); \
+  } while (0)
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+inline const uint16_t* bf(const at::Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+inline uint16_t* bfm(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+void check_gpu(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "lumen op: ", name, " must be a GPU tensor");
+}
+void check_bf16_rows(const at::Tensor& t, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, name, " must be 2-D with unit inner stride");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && (reinterpret_cast<uintptr_t>(t.data_ptr()) % 16) == 0,
+              name, " rows must be 16-byte aligned");
+}
+
+// ---------------------------------------------------------------- gemm
+void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+          const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& table,
+          int64_t table_period, int64_t table_offset, int64_t act, double alpha, at::Tensor out,
+          int64_t out_group, int64_t out_group_stride, int64_t out_row_offset, int64_t tile) {
+  check_bf16_rows(a, "a");
+  check_bf16_rows(w, "w");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "gemm: K mismatch ", w.size(1), " vs ", K);
+  TORCH_CHECK(K % 64 == 0, "gemm: K must be a multiple of 64 (pad weights), got ", K);
+  TORCH_CHECK(N % 16 == 0, "gemm: N must be a multiple of 16, got ", N);
+  check_gpu(out, "out");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) >= N, "gemm: bad out");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "gemm: out dtype");
+  const int64_t last = M - 1;
+  const int64_t need_rows = out_group > 0 ? (last / out_group) * out_group_stride + out_row_offset + last % out_group + 1 : M;
+  TORCH_CHECK(out.size(0) >= need_rows, "gemm: out has ", out.size(0), " rows, needs ", need_rows);
+  lumen::GemmEpi ep{};
+  ep.alpha = (float)alpha;
+  ep.act = (int)act;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->numel() >= N && bias->is_contiguous(), "gemm: bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16, "gemm: bias dtype");
+    ep.bias = bias->data_ptr();
+    ep.bias_f32 = bias->scalar_type() == at::kFloat;
+  }
+  if (residual.has_value() && residual->defined()) {
+    check_bf16_rows(*residual, "residual");
+    ep.residual = bf(*residual);
+    ep.ldr = residual->stride(0);
+  }
+  if (table.has_value() && table->defined()) {
+    check_bf16_rows(*table, "table");
+    TORCH_CHECK(table_period > 0, "gemm: table_period");
+    ep.table = bf(*table);
+    ep.ldt = table->stride(0);
+    ep.table_period = (int)table_period;
+    ep.table_offset = (int)table_offset;
+  }
+  ep.out_group = (int)out_group;
+  ep.out_group_stride = out_group_stride;
+  ep.out_row_offset = (int)out_row_offset;
+  ep.out_f32 = out.scalar_type() == at::kFloat;
+  const at::DeviceGuard guard(a.device());
+  LUMEN_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
+                                   (int)M, (int)N, (int)K, ep, (int)tile, cur_stream()));
+}
+
+// ---------------------------------------------------------------- norms
+void norm(const at::Tensor& x, const c10::optional<at::Tensor>& row_idx, const c10::optional<at::Tensor>& add,
+          const c10::optional<at::Tensor>& resid_out, const at::Tensor& w, const c10::optional<at::Tensor>& b,
+          at::Tensor out, double eps, int64_t mode) {
+  check_bf16_rows(x, "x");
+  const int64_t D = x.size(1);
+  TORCH_CHECK(D % 8 == 0 && D <= 8192, "norm: D must be a multiple of 8 and <= 8192");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.numel() == D, "norm: weight");
+  const int64_t rows = out.size(0);
+  const int64_t* idx = nullptr;
+  if (row_idx.has_value() && row_idx->defined()) {
+    TORCH_CHECK(row_idx->scalar_type() == at::kLong && row_idx->numel() == rows, "norm: row_idx");
+    idx = row_idx->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(x.size(0) >= rows, "norm: rows");
+  }
+  const uint16_t* addp = nullptr; int64_t add_stride = 0;
+  if (add.has_value() && add->defined()) { check_bf16_rows(*add, "add"); addp = bf(*add); add_stride = add->stride(0); }
+  uint16_t* rp = nullptr; int64_t r_stride = 0;
+  if (resid_out.has_value() && resid_out->defined()) { check_bf16_rows(*resid_out, "resid_out"); rp = bfm(*resid_out); r_stride = resid_out->stride(0); }
+  const uint16_t* bp = nullptr;
+  if (b.has_value() && b->defined()) { TORCH_CHECK(b->scalar_type() == at::kBFloat16 && b->numel() == D); bp = bf(*b); }
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) == D, "norm: out");
+  const at::DeviceGuard guard(x.device());
+  LUMEN_CHECK_HIP(lumen::norm_rows(bf(x), x.stride(0), idx, addp, add_stride, rp, r_stride, bf(w), bp,
+                                   out.data_ptr(), out.stride(0), out.scalar_type() == at::kFloat, (int)rows,
+                                   (int)D, (float)eps, (int)mode, cur_stream()));
+}
+
+void l2norm_(at::Tensor x, double eps) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 2, "l2norm_: f32 2-D contiguous");
+  const at::DeviceGuard guard(x.device());
+  LUMEN_CHECK_HIP(lumen::l2norm_f32(x.data_ptr<float>(), (int)x.size(0), (int)x.size(1), (float)eps, cur_stream()));
+}
+
+void cls_fill(at::Tensor x, const at::Tensor& cls, const at::Tensor& pos, int64_t seq) {
+  check_bf16_rows(x, "x");
+  const int64_t D = x.size(1);
+  TORCH_CHECK(x.size(0) % seq == 0, "cls_fill: rows % seq");
+  TORCH_CHECK(cls.numel() == D && pos.size(-1) == D, "cls_fill: shapes");
+  const at::DeviceGuard guard(x.device());
+  LUMEN_CHECK_HIP(lumen::cls_fill(bfm(x), seq * x.stride(0), bf(cls), bf(pos), (int)(x.size(0) / seq), (int)D,
+                                  cur_stream()));
+}
+
+void embed_gather(const at::Tensor& ids, const at::Tensor& table, const c10::optional<at::Tensor>& pos,
+                  at::Tensor out, int64_t seq, int64_t id_offset) {
+  check_gpu(ids, "ids");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous(), "embed_gather: ids int64");
+  TORCH_CHECK(table.scalar_type() == at::kBFloat16 && table.is_contiguous(), "embed_gather: table");
+  const int64_t D = table.size(1);
+  TORCH_CHECK(out.is_contiguous() && out.numel() == ids.numel() * D, "embed_gather: out");
+  const uint16_t* pp = nullptr;
+  if (pos.has_value() && pos->defined()) { TORCH_CHECK(pos->is_contiguous() && pos->size(-1) == D); pp = bf(*pos); }
+  const at::DeviceGuard guard(ids.device());
+  LUMEN_CHECK_HIP(lumen::embed_gather(ids.data_ptr<int64_t>(), bf(table), pp, (int)seq, bfm(out), (int)ids.numel(),
+                                      (int)D, table.size(0), id_offset, cur_stream()));
+}
+
+// ---------------------------------------------------------------- attention
+// q: [B, Sq, H, D], k/v: [B, Sk, Hkv, D], o: [B, Sq, H, D]  (any strides, unit inner)
+void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor o,
+               const c10::optional<at::Tensor>& kv_len, double scale, bool causal) {
+  for (auto* t : {&q, &k, &v}) {
+    check_gpu(*t, "qkv");
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 4 && t->stride(3) == 1, "attention: bf16 4-D");
+  }
+  TORCH_CHECK(o.scalar_type() == at::kBFloat16 && o.dim() == 4 && o.stride(3) == 1, "attention: out");
+  const int64_t B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
+  const int64_t Sk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(k.size(3) == D && v.size(3) == D && v.size(1) == Sk && v.size(2) == Hkv, "attention: kv shape");
+  TORCH_CHECK(H % Hkv == 0, "attention: H % Hkv");
+  TORCH_CHECK(D == 32 || D == 64 || D == 128, "attention: head dim must be 32/64/128");
+  lumen::AttnArgs a{};
+  a.q = bf(q); a.k = bf(k); a.v = bf(v); a.o = bfm(o);
+  a.q_sb = q.stride(0); a.q_ss = q.stride(1); a.q_sh = q.stride(2);
+  a.k_sb = k.stride(0); a.k_ss = k.stride(1); a.k_sh = k.stride(2);
+  a.v_sb = v.stride(0); a.v_ss = v.stride(1); a.v_sh = v.stride(2);
+  a.o_sb = o.stride(0); a.o_ss = o.stride(1); a.o_sh = o.stride(2);
+  if (kv_len.has_value() && kv_len->defined()) {
+    TORCH_CHECK(kv_len->scalar_type() == at::kInt && kv_len->numel() == B, "attention: kv_len int32 [B]");
+    a.kv_len = kv_len->data_ptr<int>();
+  }
+  a.Sq = (int)Sq; a.Sk = (int)Sk; a.H = (int)H; a.Hkv = (int)Hkv;
+  a.scale_log2 = (float)(scale * 1.4426950408889634);
+  a.causal = causal ? 1 : 0;
+  const at::DeviceGuard guard(q.device());
+  LUMEN_CHECK_HIP(lumen::attn_fwd(a, (int)B, (int)D, cur_stream()));
+}
+
+// ---------------------------------------------------------------- image prep
+void image_prep2(const at::Tensor& src, const at::Tensor& geom, at::Tensor out, at::Tensor tmp, int64_t out_h,
+                 int64_t out_w, int64_t filter, bool swap_rb, std::vector<double> mean, std::vector<double> std_,
+                 double scale, double pad, int64_t layout, int64_t patch, int64_t kpad, int64_t max_ch,
+                 int64_t max_dw) {
+  check_gpu(src, "src");
+  check_gpu(out, "out");
+  TORCH_CHECK(src.scalar_type() == at::kByte, "image_prep: uint8 src");
+  TORCH_CHECK(geom.is_cuda() && geom.scalar_type() == at::kLong && geom.dim() == 2 && geom.size(1) == 11 &&
+                  geom.is_contiguous(), "image_prep: geom int64 [B, 11] on device");
+  TORCH_CHECK(tmp.scalar_type() == at::kFloat && tmp.dim() == 4 && tmp.size(3) == 3 && tmp.is_contiguous(),
+              "image_prep: tmp f32 [B, H, W, 3]");
+  TORCH_CHECK(mean.size() == 3 && std_.size() == 3, "image_prep: mean/std");
+  TORCH_CHECK(out.is_contiguous(), "image_prep: out contiguous");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "image_prep: out dtype");
+  const int64_t B = geom.size(0);
+  lumen::PrepArgs a{};
+  a.src = src.data_ptr<uint8_t>();
+  a.geom = reinterpret_cast<const lumen::ImgGeomRaw*>(geom.data_ptr<int64_t>());
+  a.tmp = tmp.data_ptr<float>();
+  a.tmp_h = (int)tmp.size(1); a.tmp_w = (int)tmp.size(2);
+  TORCH_CHECK(tmp.size(0) >= B && a.tmp_h >= max_ch && a.tmp_w >= max_dw, "image_prep: tmp too small");
+  a.out = out.data_ptr();
+  a.out_bf16 = out.scalar_type() == at::kBFloat16;
+  a.OH = (int)out_h; a.OW = (int)out_w;
+  if (layout == 2) {
+    TORCH_CHECK(patch > 0 && out_h % patch == 0 && out_w % patch == 0, "image_prep: patch grid");
+    TORCH_CHECK(kpad >= 3 * patch * patch, "image_prep: kpad");
+    TORCH_CHECK(out.numel() == B * (out_h / patch) * (out_w / patch) * kpad, "image_prep: patch out size");
+  } else {
+    TORCH_CHECK(out.numel() == B * 3 * out_h * out_w, "image_prep: out size");
+  }
+  a.filter = (int)filter; a.swap_rb = swap_rb ? 1 : 0;
+  for (int i = 0; i < 3; ++i) { a.mean[i] = (float)mean[i]; a.inv_std[i] = (float)(1.0 / std_[i]); }
+  a.scale = (float)scale; a.pad = (float)pad;
+  a.layout = (int)layout; a.patch = (int)patch; a.kpad = (int)kpad;
+  const at::DeviceGuard guard(src.device());
+  LUMEN_CHECK_HIP(lumen::image_prep(a, (int)B, (int)max_ch, (int)max_dw, cur_stream()));
+}
+
+}  // namespace
+
+TORCH_LIBRARY(lumen, m) {
+  m.def("gemm(Tensor a, Tensor w, Tensor? bias, Tensor? residual, Tensor? table, int table_period, "
+        "int table_offset, int act, float alpha, Tensor(o!) out, int out_group, int out_group_stride, "
+        "int out_row_offset, int tile) -> ()");
+  m.def("norm(Tensor x, Tensor? row_idx, Tensor? add, Tensor(r!)? resid_out, Tensor w, Tensor? b, "
+        "Tensor(o!) out, float eps, int mode) -> ()");
+  m.def("l2norm_(Tensor(a!) x, float eps) -> ()");
+  m.def("cls_fill(Tensor(a!) x, Tensor cls, Tensor pos, int seq) -> ()");
+  m.def("embed_gather(Tensor ids, Tensor table, Tensor? pos, Tensor(o!) out, int seq, int id_offset) -> ()");
+  m.def("attention(Tensor q, Tensor k, Tensor v, Tensor(o!) o, Tensor? kv_len, float scale, bool causal) -> ()");
+  m.def("image_prep(Tensor src, Tensor geom, Tensor(o!) out, Tensor(t!) tmp, int out_h, int out_w, int filter, "
+        "bool swap_rb, float[] mean, float[] std, float scale, float pad, int layout, int patch, int kpad, "
+        "int max_ch, int max_dw) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
+  m.impl("gemm", &gemm);
+  m.impl("norm", &norm);
+  m.impl("l2norm_", &l2norm_);
+  m.impl("cls_fill", &cls_fill);
+  m.impl("embed_gather", &embed_gather);
+  m.impl("attention", &attention);
+  m.impl("image_prep", &image_prep2);
+}

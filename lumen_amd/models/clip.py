@@ -1,0 +1,387 @@
+"""CLIP model family (OpenAI / OpenCLIP / HF CLIP naming, BioCLIP-2, ViT-B/L).
+
+The towers are written directly against :mod:`lumen_amd.ops`, i.e. every hot op
+is one hand-written gfx950 kernel on the GPU:
+
+  image_prep (resize+normalise+im2col)  -> patch GEMM (epilogue: +pos-emb, row
+  scatter into the token buffer) -> cls_fill -> ln_pre -> L x [LN -> QKV GEMM ->
+  fused attention (reads the packed QKV in place) -> out-proj GEMM (+bias
+  +residual in place) -> LN -> fc1 GEMM (+bias, GELU/QuickGELU) -> fc2 GEMM (+bias
+  +residual)] -> ln_post on CLS rows (row gather) -> projection GEMM (fp32 out) ->
+  L2 normalise.
+
+Reference behaviour reproduced: image embedding = normalised projection of the
+CLS token (packages/lumen-clip/src/lumen_clip/backends/onnxrt_backend.py:466-495,
+torch_backend.py:520-535); text embedding pools the EOT token (argmax id) for
+OpenAI-style towers (torch_backend.py:340-393).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field, asdict
+from typing import Optional
+
+import torch
+from torch import nn
+
+from .. import ops
+
+
+@dataclass
+class VisionConfig:
+    image_size: int = 224
+    patch_size: int = 14
+    width: int = 1024
+    layers: int = 24
+    heads: int = 16
+    mlp_ratio: float = 4.0
+    act: str = "quick_gelu"
+    ln_eps: float = 1e-5
+
+
+@dataclass
+class TextConfig:
+    context_length: int = 77
+    vocab_size: int = 49408
+    width: int = 768
+    layers: int = 12
+    heads: int = 12
+    mlp_ratio: float = 4.0
+    act: str = "quick_gelu"
+    ln_eps: float = 1e-5
+    eot_token_id: Optional[int] = None  # None -> argmax(ids) pooling (OpenAI BPE: EOT is the max id)
+
+
+@dataclass
+class CLIPConfig:
+    embed_dim: int = 768
+    vision: VisionConfig = field(default_factory=VisionConfig)
+    text: TextConfig = field(default_factory=TextConfig)
+    image_mean: tuple = (0.48145466, 0.4578275, 0.40821073)
+    image_std: tuple = (0.26862954, 0.26130258, 0.27577711)
+    logit_scale: float = math.log(100.0)
+
+    def to_dict(self):
+        return asdict(self)
+
+    @staticmethod
+    def from_dict(d: dict) -> "CLIPConfig":
+        v = VisionConfig(**d.get("vision", {}))
+        t = TextConfig(**d.get("text", {}))
+        rest = {k: d[k] for k in ("embed_dim", "image_mean", "image_std", "logit_scale") if k in d}
+        if "image_mean" in rest:
+            rest["image_mean"] = tuple(rest["image_mean"])
+        if "image_std" in rest:
+            rest["image_std"] = tuple(rest["image_std"])
+        return CLIPConfig(vision=v, text=t, **rest)
+
+
+PRESETS = {
+    # OpenAI ViT-L/14 (also the BioCLIP-2 geometry), 768-d embeddings
+    "ViT-L-14": CLIPConfig(),
+    "ViT-B-32": CLIPConfig(
+        embed_dim=512,
+        vision=VisionConfig(patch_size=32, width=768, layers=12, heads=12),
+        text=TextConfig(width=512, layers=12, heads=8),
+    ),
+    "ViT-B-16": CLIPConfig(
+        embed_dim=512,
+        vision=VisionConfig(patch_size=16, width=768, layers=12, heads=12),
+        text=TextConfig(width=512, layers=12, heads=8),
+    ),
+    "ViT-L-14-336": CLIPConfig(vision=VisionConfig(image_size=336)),
+    # tiny geometry used by CPU tests and synthetic model directories
+    "tiny": CLIPConfig(
+        embed_dim=64,
+        vision=VisionConfig(image_size=32, patch_size=8, width=64, layers=2, heads=2),
+        text=TextConfig(context_length=16, vocab_size=512, width=64, layers=2, heads=2),
+    ),
+}
+
+
+def _pad64(k: int) -> int:
+    return (k + 63) // 64 * 64
+
+
+class _Block(nn.Module):
+    """Pre-LN transformer block parameters (weights stored [out, in], bf16)."""
+
+    def __init__(self, width: int, mlp: int, dtype, device):
+        super().__init__()
+        kw = dict(dtype=dtype, device=device)
+        self.ln1_w = nn.Parameter(torch.ones(width, **kw), requires_grad=False)
+        self.ln1_b = nn.Parameter(torch.zeros(width, **kw), requires_grad=False)
+        self.qkv_w = nn.Parameter(torch.empty(3 * width, width, **kw), requires_grad=False)
+        self.qkv_b = nn.Parameter(torch.zeros(3 * width, **kw), requires_grad=False)
+        self.out_w = nn.Parameter(torch.empty(width, width, **kw), requires_grad=False)
+        self.out_b = nn.Parameter(torch.zeros(width, **kw), requires_grad=False)
+        self.ln2_w = nn.Parameter(torch.ones(width, **kw), requires_grad=False)
+        self.ln2_b = nn.Parameter(torch.zeros(width, **kw), requires_grad=False)
+        self.fc1_w = nn.Parameter(torch.empty(mlp, width, **kw), requires_grad=False)
+        self.fc1_b = nn.Parameter(torch.zeros(mlp, **kw), requires_grad=False)
+        self.fc2_w = nn.Parameter(torch.empty(width, mlp, **kw), requires_grad=False)
+        self.fc2_b = nn.Parameter(torch.zeros(width, **kw), requires_grad=False)
+
+    def random_init(self, gen: torch.Generator, layers: int):
+        w = self.qkv_w.shape[1]
+        attn_std = w ** -0.5
+        proj_std = (w ** -0.5) * ((2 * layers) ** -0.5)
+        fc_std = (2 * w) ** -0.5
+        for p, s in ((self.qkv_w, attn_std), (self.out_w, proj_std), (self.fc1_w, fc_std), (self.fc2_w, proj_std)):
+            p.data.copy_(torch.randn(p.shape, generator=gen) * s)
+
+
+def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float,
+               causal: bool = False, kv_len: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Run pre-LN blocks over the flat residual stream x [B*S, W] (updated in place)."""
+    T, W = x.shape
+    D = W // heads
+    h = torch.empty_like(x)
+    o = torch.empty_like(x)
+    for blk in blocks:
+        ops.layer_norm(x, blk.ln1_w, blk.ln1_b, eps, out=h)
+        qkv = ops.linear(h, blk.qkv_w, blk.qkv_b)
+        q5 = qkv.view(B, S, 3, heads, D)
+        ops.attention(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], causal=causal, kv_len=kv_len,
+                      out=o.view(B, S, heads, D))
+        del qkv, q5
+        ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x)
+        ops.layer_norm(x, blk.ln2_w, blk.ln2_b, eps, out=h)
+        f = ops.linear(h, blk.fc1_w, blk.fc1_b, act=act)
+        ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x)
+        del f
+    return x
+
+
+class VisionTower(nn.Module):
+    def __init__(self, cfg: VisionConfig, embed_dim: int, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.cfg = cfg
+        self.embed_dim = embed_dim
+        kw = dict(dtype=dtype, device=device)
+        p = cfg.patch_size
+        self.grid = cfg.image_size // p
+        self.num_patches = self.grid * self.grid
+        self.seq = self.num_patches + 1
+        self.kdim = 3 * p * p
+        self.kpad = _pad64(self.kdim)
+        W = cfg.width
+        self.patch_w = nn.Parameter(torch.zeros(W, self.kpad, **kw), requires_grad=False)
+        self.class_emb = nn.Parameter(torch.zeros(W, **kw), requires_grad=False)
+        self.pos_emb = nn.Parameter(torch.zeros(self.seq, W, **kw), requires_grad=False)
+        self.ln_pre_w = nn.Parameter(torch.ones(W, **kw), requires_grad=False)
+        self.ln_pre_b = nn.Parameter(torch.zeros(W, **kw), requires_grad=False)
+        self.blocks = nn.ModuleList([_Block(W, int(W * cfg.mlp_ratio), dtype, device) for _ in range(cfg.layers)])
+        self.ln_post_w = nn.Parameter(torch.ones(W, **kw), requires_grad=False)
+        self.ln_post_b = nn.Parameter(torch.zeros(W, **kw), requires_grad=False)
+        self.proj_w = nn.Parameter(torch.zeros(embed_dim, W, **kw), requires_grad=False)  # [E, W]
+
+    def random_init(self, gen: torch.Generator):
+        W = self.cfg.width
+        s = W ** -0.5
+        w = torch.randn(W, self.kdim, generator=gen) * (self.kdim ** -0.5)
+        self.patch_w.data.zero_()
+        self.patch_w.data[:, : self.kdim] = w.to(self.patch_w.dtype)
+        self.class_emb.data.copy_(torch.randn(W, generator=gen) * s)
+        self.pos_emb.data.copy_(torch.randn(self.seq, W, generator=gen) * 0.01)
+        for b in self.blocks:
+            b.random_init(gen, self.cfg.layers)
+        self.proj_w.data.copy_(torch.randn(self.embed_dim, W, generator=gen) * s)
+
+    @torch.no_grad()
+    def forward_patches(self, patches: torch.Tensor, B: int) -> torch.Tensor:
+        """patches [B*P, kpad] (bf16) -> L2-normalised fp32 embeddings [B, E]."""
+        cfg = self.cfg
+        S, P, W = self.seq, self.num_patches, cfg.width
+        dev, dt = patches.device, self.patch_w.dtype
+        x = torch.empty((B * S, W), device=dev, dtype=dt)
+        # patch GEMM: row m = b*P + p -> token row b*S + 1 + p, + pos_emb[1 + p]
+        ops.linear(patches, self.patch_w, table=self.pos_emb, table_period=P, table_offset=1, out=x,
+                   out_group=P, out_group_stride=S, out_row_offset=1)
+        ops.cls_fill(x, self.class_emb, self.pos_emb, S)
+        ops.layer_norm(x, self.ln_pre_w, self.ln_pre_b, cfg.ln_eps, out=x)
+        run_blocks(x, self.blocks, B, S, cfg.heads, cfg.act, cfg.ln_eps)
+        cls_rows = torch.arange(B, device=dev, dtype=torch.long) * S
+        pooled = ops.layer_norm(x, self.ln_post_w, self.ln_post_b, cfg.ln_eps, row_idx=cls_rows)
+        emb = ops.linear(pooled, self.proj_w, out_dtype=torch.float32)
+        return ops.l2_normalize_(emb)
+
+    def preprocess(self, images, mean, std, filter: str = "pil_bicubic") -> torch.Tensor:
+        """uint8 HWC images -> patch rows [B*P, kpad] (squash resize, no crop: the ONNX path)."""
+        s = self.cfg.image_size
+        return ops.image_prep(images, (s, s), mean=mean, std=std, filter=filter, layout="patches",
+                              patch=self.cfg.patch_size, kpad=self.kpad, out_dtype=self.patch_w.dtype,
+                              device=self.patch_w.device)
+
+    def preprocess_nchw_to_patches(self, pix: torch.Tensor) -> torch.Tensor:
+        """Already-normalised NCHW float pixels -> patch rows (used for parity tests)."""
+        B = pix.shape[0]
+        p, g = self.cfg.patch_size, self.grid
+        x = pix.reshape(B, 3, g, p, g, p).permute(0, 2, 4, 1, 3, 5).reshape(B * g * g, self.kdim)
+        out = torch.zeros((B * g * g, self.kpad), device=pix.device, dtype=self.patch_w.dtype)
+        out[:, : self.kdim] = x.to(out.dtype)
+        return out
+
+
+class TextTower(nn.Module):
+    """OpenAI-style causal text transformer with EOT pooling."""
+
+    def __init__(self, cfg: TextConfig, embed_dim: int, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.cfg = cfg
+        self.embed_dim = embed_dim
+        kw = dict(dtype=dtype, device=device)
+        W = cfg.width
+        self.token_emb = nn.Parameter(torch.zeros(cfg.vocab_size, W, **kw), requires_grad=False)
+        self.pos_emb = nn.Parameter(torch.zeros(cfg.context_length, W, **kw), requires_grad=False)
+        self.blocks = nn.ModuleList([_Block(W, int(W * cfg.mlp_ratio), dtype, device) for _ in range(cfg.layers)])
+        self.ln_final_w = nn.Parameter(torch.ones(W, **kw), requires_grad=False)
+        self.ln_final_b = nn.Parameter(torch.zeros(W, **kw), requires_grad=False)
+        self.proj_w = nn.Parameter(torch.zeros(embed_dim, W, **kw), requires_grad=False)
+
+    def random_init(self, gen: torch.Generator):
+        W = self.cfg.width
+        self.token_emb.data.copy_(torch.randn(self.token_emb.shape, generator=gen) * 0.02)
+        self.pos_emb.data.copy_(torch.randn(self.pos_emb.shape, generator=gen) * 0.01)
+        for b in self.blocks:
+            b.random_init(gen, self.cfg.layers)
+        self.proj_w.data.copy_(torch.randn(self.embed_dim, W, generator=gen) * W ** -0.5)
+
+    @torch.no_grad()
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        """ids [B, ctx] int64 -> L2-normalised fp32 embeddings [B, E]."""
+        cfg = self.cfg
+        B, S = ids.shape
+        dev = self.token_emb.device
+        ids = ids.to(dev)
+        x = ops.embed(ids, self.token_emb, self.pos_emb[:S]).view(B * S, cfg.width)
+        run_blocks(x, self.blocks, B, S, cfg.heads, cfg.act, cfg.ln_eps, causal=True)
+        if cfg.eot_token_id is None:
+            eot = ids.argmax(dim=-1)
+        else:
+            eot = (ids == cfg.eot_token_id).int().argmax(dim=-1)
+        rows = torch.arange(B, device=dev) * S + eot
+        pooled = ops.layer_norm(x, self.ln_final_w, self.ln_final_b, cfg.ln_eps, row_idx=rows.long())
+        emb = ops.linear(pooled, self.proj_w, out_dtype=torch.float32)
+        return ops.l2_normalize_(emb)
+
+
+class CLIPModel(nn.Module):
+    def __init__(self, cfg: CLIPConfig, dtype=torch.bfloat16, device=None, with_text: bool = True):
+        super().__init__()
+        self.cfg = cfg
+        self.visual = VisionTower(cfg.vision, cfg.embed_dim, dtype, device)
+        self.text = TextTower(cfg.text, cfg.embed_dim, dtype, device) if with_text else None
+        self.logit_scale = cfg.logit_scale
+
+    @staticmethod
+    def random(cfg: CLIPConfig | str, seed: int = 0, dtype=torch.bfloat16, device=None, with_text=True):
+        if isinstance(cfg, str):
+            cfg = PRESETS[cfg]
+        m = CLIPModel(cfg, dtype=dtype, device="cpu", with_text=with_text)
+        g = torch.Generator().manual_seed(seed)
+        m.visual.random_init(g)
+        if m.text is not None:
+            m.text.random_init(g)
+        return m.to(device) if device is not None else m
+
+    # ---- public API (mirrors the reference backend contract: unit-norm fp32 vectors)
+    @torch.no_grad()
+    def encode_image_uint8(self, images) -> torch.Tensor:
+        patches = self.visual.preprocess(images, self.cfg.image_mean, self.cfg.image_std)
+        B = patches.shape[0] // self.visual.num_patches
+        return self.visual.forward_patches(patches, B)
+
+    @torch.no_grad()
+    def encode_text_ids(self, ids: torch.Tensor) -> torch.Tensor:
+        assert self.text is not None
+        return self.text(ids)
+
+    # ---- weight ingestion
+    def load_state_dict_any(self, sd: dict) -> None:
+        """Load OpenCLIP / OpenAI (``visual.*``) or HF ``CLIPModel`` naming."""
+        if any(k.startswith("vision_model.") for k in sd):
+            sd = _hf_to_openclip(sd, self.cfg)
+        _load_openclip(self, sd)
+
+
+def _cp(dst: torch.Tensor, src: torch.Tensor):
+    if tuple(dst.shape) != tuple(src.shape):
+        raise ValueError(f"shape mismatch {tuple(dst.shape)} vs {tuple(src.shape)}")
+    dst.data.copy_(src.to(dst.dtype))
+
+
+def _load_blocks(blocks, sd, prefix):
+    for i, b in enumerate(blocks):
+        p = f"{prefix}.resblocks.{i}."
+        _cp(b.ln1_w, sd[p + "ln_1.weight"]); _cp(b.ln1_b, sd[p + "ln_1.bias"])
+        _cp(b.qkv_w, sd[p + "attn.in_proj_weight"]); _cp(b.qkv_b, sd[p + "attn.in_proj_bias"])
+        _cp(b.out_w, sd[p + "attn.out_proj.weight"]); _cp(b.out_b, sd[p + "attn.out_proj.bias"])
+        _cp(b.ln2_w, sd[p + "ln_2.weight"]); _cp(b.ln2_b, sd[p + "ln_2.bias"])
+        _cp(b.fc1_w, sd[p + "mlp.c_fc.weight"]); _cp(b.fc1_b, sd[p + "mlp.c_fc.bias"])
+        _cp(b.fc2_w, sd[p + "mlp.c_proj.weight"]); _cp(b.fc2_b, sd[p + "mlp.c_proj.bias"])
+
+
+def _load_openclip(m: CLIPModel, sd: dict) -> None:
+    v = m.visual
+    conv = sd["visual.conv1.weight"]
+    v.patch_w.data.zero_()
+    v.patch_w.data[:, : v.kdim] = conv.reshape(conv.shape[0], -1).to(v.patch_w.dtype)
+    _cp(v.class_emb, sd["visual.class_embedding"])
+    _cp(v.pos_emb, sd["visual.positional_embedding"])
+    _cp(v.ln_pre_w, sd["visual.ln_pre.weight"]); _cp(v.ln_pre_b, sd["visual.ln_pre.bias"])
+    _load_blocks(v.blocks, sd, "visual.transformer")
+    _cp(v.ln_post_w, sd["visual.ln_post.weight"]); _cp(v.ln_post_b, sd["visual.ln_post.bias"])
+    _cp(v.proj_w, sd["visual.proj"].t())
+    if m.text is not None and "token_embedding.weight" in sd:
+        t = m.text
+        _cp(t.token_emb, sd["token_embedding.weight"])
+        _cp(t.pos_emb, sd["positional_embedding"])
+        _load_blocks(t.blocks, sd, "transformer")
+        _cp(t.ln_final_w, sd["ln_final.weight"]); _cp(t.ln_final_b, sd["ln_final.bias"])
+        _cp(t.proj_w, sd["text_projection"].t())
+    if "logit_scale" in sd:
+        m.logit_scale = float(sd["logit_scale"])
+
+
+def _hf_to_openclip(sd: dict, cfg: CLIPConfig) -> dict:
+    """Rename HF transformers CLIPModel weights to the OpenCLIP layout."""
+    out = {}
+    vm, tm = "vision_model.", "text_model."
+    out["visual.conv1.weight"] = sd[vm + "embeddings.patch_embedding.weight"]
+    out["visual.class_embedding"] = sd[vm + "embeddings.class_embedding"]
+    out["visual.positional_embedding"] = sd[vm + "embeddings.position_embedding.weight"]
+    out["visual.ln_pre.weight"] = sd[vm + "pre_layrnorm.weight"]
+    out["visual.ln_pre.bias"] = sd[vm + "pre_layrnorm.bias"]
+    out["visual.ln_post.weight"] = sd[vm + "post_layernorm.weight"]
+    out["visual.ln_post.bias"] = sd[vm + "post_layernorm.bias"]
+    out["visual.proj"] = sd["visual_projection.weight"].t()
+
+    def blocks(src_prefix, dst_prefix, n):
+        for i in range(n):
+            s = f"{src_prefix}encoder.layers.{i}."
+            d = f"{dst_prefix}.resblocks.{i}."
+            out[d + "ln_1.weight"] = sd[s + "layer_norm1.weight"]
+            out[d + "ln_1.bias"] = sd[s + "layer_norm1.bias"]
+            out[d + "ln_2.weight"] = sd[s + "layer_norm2.weight"]
+            out[d + "ln_2.bias"] = sd[s + "layer_norm2.bias"]
+            out[d + "attn.in_proj_weight"] = torch.cat([sd[s + f"self_attn.{x}_proj.weight"] for x in "qkv"])
+            out[d + "attn.in_proj_bias"] = torch.cat([sd[s + f"self_attn.{x}_proj.bias"] for x in "qkv"])
+            out[d + "attn.out_proj.weight"] = sd[s + "self_attn.out_proj.weight"]
+            out[d + "attn.out_proj.bias"] = sd[s + "self_attn.out_proj.bias"]
+            out[d + "mlp.c_fc.weight"] = sd[s + "mlp.fc1.weight"]
+            out[d + "mlp.c_fc.bias"] = sd[s + "mlp.fc1.bias"]
+            out[d + "mlp.c_proj.weight"] = sd[s + "mlp.fc2.weight"]
+            out[d + "mlp.c_proj.bias"] = sd[s + "mlp.fc2.bias"]
+
+    blocks(vm, "visual.transformer", cfg.vision.layers)
+    if tm + "embeddings.token_embedding.weight" in sd:
+        out["token_embedding.weight"] = sd[tm + "embeddings.token_embedding.weight"]
+        out["positional_embedding"] = sd[tm + "embeddings.position_embedding.weight"]
+        out["ln_final.weight"] = sd[tm + "final_layer_norm.weight"]
+        out["ln_final.bias"] = sd[tm + "final_layer_norm.bias"]
+        out["text_projection"] = sd["text_projection.weight"].t()
+        blocks(tm, "transformer", cfg.text.layers)
+    if "logit_scale" in sd:
+        out["logit_scale"] = sd["logit_scale"]
+    return out

@@ -1,0 +1,407 @@
+"""Compute ops of lumen_amd.
+
+Every op has exactly two implementations:
+
+* GPU tensors -> the hand-written gfx950 HIP kernel (``torch.ops.lumen.*``); the
+  native library is *required* (no silent PyTorch fallback on a GPU).
+* CPU tensors -> a plain PyTorch fp32 reference with identical semantics.  This
+  is the "CPU reference path" used for plumbing tests (BASELINE config #1) and
+  as the numerical oracle the GPU kernels are tested against.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence
+
+import torch
+import torch.nn.functional as F
+
+from .._native import hip_ops
+
+ACTS = {
+    None: 0, "none": 0, "gelu": 1, "quick_gelu": 2, "relu": 3, "silu": 4, "gelu_tanh": 5,
+    "hardswish": 6, "sigmoid": 7, "leaky": 8, "hardsigmoid": 9,
+}
+
+
+def _act_ref(x: torch.Tensor, act: int) -> torch.Tensor:
+    if act == 0:
+        return x
+    if act == 1:
+        return F.gelu(x)
+    if act == 2:
+        return x * torch.sigmoid(1.702 * x)
+    if act == 3:
+        return F.relu(x)
+    if act == 4:
+        return F.silu(x)
+    if act == 5:
+        return F.gelu(x, approximate="tanh")
+    if act == 6:
+        return F.hardswish(x)
+    if act == 7:
+        return torch.sigmoid(x)
+    if act == 8:
+        return F.leaky_relu(x, 0.1)
+    if act == 9:
+        return torch.clamp(x / 6.0 + 0.5, 0.0, 1.0)
+    raise ValueError(act)
+
+
+def act_id(act) -> int:
+    if isinstance(act, int):
+        return act
+    return ACTS[act]
+
+
+def apply_act(x: torch.Tensor, act) -> torch.Tensor:
+    """Standalone activation (reference semantics) — used by conv paths on CPU."""
+    return _act_ref(x.float(), act_id(act)).to(x.dtype)
+
+
+# --------------------------------------------------------------------------- GEMM
+def linear(
+    x: torch.Tensor,
+    w: torch.Tensor,
+    bias: Optional[torch.Tensor] = None,
+    act=None,
+    residual: Optional[torch.Tensor] = None,
+    table: Optional[torch.Tensor] = None,
+    table_period: int = 0,
+    table_offset: int = 0,
+    alpha: float = 1.0,
+    out: Optional[torch.Tensor] = None,
+    out_dtype: Optional[torch.dtype] = None,
+    out_group: int = 0,
+    out_group_stride: int = 0,
+    out_row_offset: int = 0,
+    tile: int = -1,
+) -> torch.Tensor:
+    """y = epi(alpha * x @ w.T): (+bias) -> act -> (+table[m % P + off]) -> (+residual[orow]).
+
+    ``x`` is [M, K] (or [..., K]), ``w`` is [N, K].  With ``out_group`` > 0 row m is
+    written to ``(m // G) * GS + RO + m % G`` of ``out`` (patch rows into a token
+    buffer).  ``residual`` is indexed by the *output* row.
+    """
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, x.shape[-1])
+    M, K = x2.shape
+    N = w.shape[0]
+    a = act_id(act)
+    if out is None:
+        assert out_group == 0, "out_group needs an explicit out tensor"
+        out = torch.empty((M, N), device=x.device, dtype=out_dtype or x.dtype)
+        ret_shape = (*lead, N)
+    else:
+        ret_shape = None
+    out2 = out if out.dim() == 2 else out.view(-1, out.shape[-1])
+    if x.is_cuda:
+        if x2.stride(-1) != 1 or x2.stride(0) % 8 != 0:
+            x2 = x2.contiguous()
+        res2 = residual.reshape(-1, residual.shape[-1]) if residual is not None else None
+        hip_ops().gemm(x2, w, bias, res2, table, int(table_period), int(table_offset), a, float(alpha), out2,
+                       int(out_group), int(out_group_stride), int(out_row_offset), int(tile))
+    else:
+        y = (x2.float() @ w.float().t()) * alpha
+        if bias is not None:
+            y = y + bias.float()
+        y = _act_ref(y, a)
+        m = torch.arange(M)
+        orow = (m // out_group) * out_group_stride + out_row_offset + m % out_group if out_group > 0 else m
+        if table is not None:
+            y = y + table.float()[(m % table_period) + table_offset, :N]
+        if residual is not None:
+            r2 = residual.reshape(-1, residual.shape[-1])
+            y = y + r2.float()[orow, :N]
+        out2[orow, :N] = y.to(out2.dtype)
+    if ret_shape is not None:
+        return out.view(ret_shape)
+    return out
+
+
+# --------------------------------------------------------------------------- norms
+def _norm_ref(x, w, b, eps, mode):
+    xf = x.float()
+    if mode == 0:
+        mu = xf.mean(-1, keepdim=True)
+        var = ((xf - mu) ** 2).mean(-1, keepdim=True)
+        y = (xf - mu) * torch.rsqrt(var + eps) * w.float()
+        if b is not None:
+            y = y + b.float()
+    else:
+        y = xf * torch.rsqrt((xf * xf).mean(-1, keepdim=True) + eps) * w.float()
+    return y
+
+
+def _norm(x, w, b, eps, mode, row_idx=None, add=None, resid_out=None, out=None, out_dtype=None):
+    D = x.shape[-1]
+    x2 = x.reshape(-1, D)
+    rows = row_idx.numel() if row_idx is not None else x2.shape[0]
+    if out is None:
+        out = torch.empty((rows, D), device=x.device, dtype=out_dtype or x.dtype)
+    if x.is_cuda:
+        add2 = add.reshape(-1, D) if add is not None else None
+        hip_ops().norm(x2, row_idx, add2, resid_out, w, b, out.view(-1, D), float(eps), int(mode))
+    else:
+        src = x2[row_idx] if row_idx is not None else x2
+        h = src.float()
+        if add is not None:
+            a2 = add.reshape(-1, D)
+            h = h + (a2[row_idx] if row_idx is not None else a2).float()
+        if resid_out is not None:
+            resid_out.copy_(h.to(resid_out.dtype))
+        out.view(-1, D).copy_(_norm_ref(h, w, b, eps, mode).to(out.dtype))
+    return out
+
+
+def layer_norm(x, w, b=None, eps=1e-5, row_idx=None, out=None, out_dtype=None):
+    out = _norm(x, w, b, eps, 0, row_idx=row_idx, out=out, out_dtype=out_dtype)
+    if row_idx is None and out.shape != x.shape and out.numel() == x.numel():
+        return out.view(x.shape)
+    return out
+
+
+def rms_norm(x, w, eps=1e-6, add=None, resid_out=None, out=None, out_dtype=None):
+    """RMSNorm(x [+ add]); when ``resid_out`` is given the pre-norm sum is stored there."""
+    o = _norm(x, w, None, eps, 1, add=add, resid_out=resid_out, out=out, out_dtype=out_dtype)
+    return o.view(*x.shape[:-1], x.shape[-1]) if o.numel() == x.numel() else o
+
+
+def l2_normalize_(x: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:
+    """In-place row L2 normalisation of an fp32 [R, D] tensor."""
+    if x.is_cuda:
+        hip_ops().l2norm_(x, float(eps))
+    else:
+        x.div_(x.norm(dim=-1, keepdim=True).clamp_min(eps))
+    return x
+
+
+def cls_fill(x: torch.Tensor, cls: torch.Tensor, pos: torch.Tensor, seq: int) -> None:
+    """x[b*seq + 0] = cls + pos[0] for every sequence in the flat [B*seq, D] buffer."""
+    if x.is_cuda:
+        hip_ops().cls_fill(x, cls, pos, int(seq))
+    else:
+        B = x.shape[0] // seq
+        x.view(B, seq, -1)[:, 0] = (cls.float() + pos.reshape(-1, x.shape[-1])[0].float()).to(x.dtype)
+
+
+def embed(ids: torch.Tensor, table: torch.Tensor, pos: Optional[torch.Tensor] = None, id_offset: int = 0,
+          out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Token-embedding gather (+ positional row ``pos[s]`` for position s of each sequence)."""
+    S = ids.shape[-1]
+    D = table.shape[1]
+    if out is None:
+        out = torch.empty((*ids.shape, D), device=table.device, dtype=table.dtype)
+    if table.is_cuda:
+        hip_ops().embed_gather(ids.contiguous().to(torch.long), table, pos, out, int(S), int(id_offset))
+    else:
+        idx = ids.long() - id_offset
+        valid = (idx >= 0) & (idx < table.shape[0])
+        e = table.float()[idx.clamp(0, table.shape[0] - 1)] * valid.unsqueeze(-1)
+        if pos is not None:
+            e = e + pos.float().reshape(-1, D)[:S]
+        out.copy_(e.to(out.dtype))
+    return out
+
+
+# --------------------------------------------------------------------------- attention
+def attention(q, k, v, scale: Optional[float] = None, causal: bool = False, kv_len=None, out=None):
+    """Fused softmax(q k^T * scale [+mask]) v.
+
+    q: [B, Sq, H, D]; k, v: [B, Sk, Hkv, D] (GQA when Hkv < H); any strides with unit
+    inner stride (e.g. views into a packed QKV projection).  Returns [B, Sq, H, D].
+    ``kv_len`` (int32 [B]) masks padded keys; ``causal`` aligns the last query with
+    the last key (prefill with a KV-cache prefix).
+    """
+    B, Sq, H, D = q.shape
+    Sk, Hkv = k.shape[1], k.shape[2]
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if out is None:
+        out = torch.empty((B, Sq, H, D), device=q.device, dtype=q.dtype)
+    if q.is_cuda:
+        kl = kv_len.to(torch.int32) if kv_len is not None else None
+        hip_ops().attention(q, k, v, out, kl, float(scale), bool(causal))
+        return out
+    qf = q.float().transpose(1, 2)
+    rep = H // Hkv
+    kf = k.float().transpose(1, 2).repeat_interleave(rep, dim=1)
+    vf = v.float().transpose(1, 2).repeat_interleave(rep, dim=1)
+    s = (qf @ kf.transpose(-1, -2)) * scale
+    mask = torch.zeros((B, 1, Sq, Sk), dtype=torch.bool)
+    if kv_len is not None:
+        kl = kv_len.long().view(B, 1, 1, 1)
+        mask |= torch.arange(Sk).view(1, 1, 1, Sk) >= kl
+    if causal:
+        qi = torch.arange(Sq).view(Sq, 1) + (Sk - Sq)
+        mask |= (torch.arange(Sk).view(1, Sk) > qi).view(1, 1, Sq, Sk)
+    s = s.masked_fill(mask, float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    p = torch.nan_to_num(p, nan=0.0)
+    o = (p @ vf).transpose(1, 2)
+    out.copy_(o.to(out.dtype))
+    return out
+
+
+# --------------------------------------------------------------------------- image prep
+FILTERS = {"pil_bicubic": 0, "bicubic": 0, "pil_bilinear": 1, "cv2_linear": 2, "linear": 2, "cv2_cubic": 3}
+LAYOUTS = {"nchw": 0, "nhwc": 1, "patches": 2}
+
+
+class ImageGeom:
+    """Geometry of one image in a ragged preprocessing batch."""
+
+    __slots__ = ("ih", "iw", "off", "cw", "ch", "ox", "oy", "dx", "dy", "dw", "dh")
+
+    def __init__(self, ih, iw, off, cw, ch, ox, oy, dx, dy, dw, dh):
+        self.ih, self.iw, self.off = ih, iw, off
+        self.cw, self.ch, self.ox, self.oy = cw, ch, ox, oy
+        self.dx, self.dy, self.dw, self.dh = dx, dy, dw, dh
+
+    def row(self):
+        return [self.ih, self.iw, self.off, self.cw, self.ch, self.ox, self.oy, self.dx, self.dy, self.dw, self.dh]
+
+    @staticmethod
+    def resize(ih, iw, off, oh, ow):
+        """Plain resize of the whole image to (oh, ow)."""
+        return ImageGeom(ih, iw, off, iw, ih, 0, 0, 0, 0, ow, oh)
+
+    @staticmethod
+    def letterbox(ih, iw, off, oh, ow, rh, rw):
+        """Resize to (rh, rw) placed top-left in an (oh, ow) canvas, rest padded."""
+        return ImageGeom(ih, iw, off, iw, ih, 0, 0, 0, 0, rw, rh)
+
+    @staticmethod
+    def pad_square(ih, iw, off, out):
+        """Centre on a black max(h, w) square, then resize the square to out x out."""
+        s = max(ih, iw)
+        return ImageGeom(ih, iw, off, s, s, (s - iw) // 2, (s - ih) // 2, 0, 0, out, out)
+
+
+def _ref_resample_axis(img: torch.Tensor, out_len: int, axis: int, filt: int) -> torch.Tensor:
+    """1-D resample of float image [H, W, 3] along axis (0=H, 1=W) matching the kernel."""
+    in_len = img.shape[axis]
+    scale = in_len / out_len
+    res = []
+    for i in range(out_len):
+        if filt >= 2:
+            center = (i + 0.5) * scale - 0.5
+            r = 2 if filt == 3 else 1
+            x0 = math.floor(center) - r + 1
+            xs = list(range(x0, x0 + 2 * r))
+            ws = [_filt(float(x) - center, filt) for x in xs]
+            xs = [min(max(x, 0), in_len - 1) for x in xs]
+        else:
+            ss = max(scale, 1.0)
+            sup = (2.0 if filt == 0 else 1.0) * ss
+            center = (i + 0.5) * scale
+            x0 = max(int(center - sup + 0.5), 0)
+            x1 = min(int(center + sup + 0.5), in_len)
+            xs = list(range(x0, x1))
+            ws = [_filt((x - center + 0.5) / ss, filt) for x in xs]
+        wt = torch.tensor(ws, dtype=torch.float32)
+        wt = wt / wt.sum() if float(wt.sum()) != 0 else wt * 0
+        sl = img.index_select(axis, torch.tensor(xs))
+        shape = [1, 1, 1]
+        shape[axis] = len(xs)
+        res.append((sl * wt.view(shape)).sum(axis, keepdim=True))
+    out = torch.cat(res, axis)
+    if filt < 2 or axis == 0:
+        out = out.round().clamp(0, 255)
+    return out
+
+
+def _filt(x, f):
+    a = -0.5 if f == 0 else -0.75
+    x = abs(x)
+    if f in (0, 3):
+        if x < 1:
+            return ((a + 2) * x - (a + 3)) * x * x + 1
+        if x < 2:
+            return (((x - 5) * x + 8) * x - 4) * a
+        return 0.0
+    return 1 - x if x < 1 else 0.0
+
+
+def image_prep(
+    images: Sequence[torch.Tensor] | torch.Tensor,
+    out_hw: tuple[int, int],
+    mean=(0.0, 0.0, 0.0),
+    std=(1.0, 1.0, 1.0),
+    scale: float = 1.0 / 255.0,
+    filter: str = "pil_bicubic",
+    layout: str = "nchw",
+    patch: int = 0,
+    kpad: int = 0,
+    swap_rb: bool = False,
+    pad: float = 0.0,
+    geoms: Optional[Sequence[ImageGeom]] = None,
+    out_dtype: torch.dtype = torch.float32,
+    device=None,
+) -> torch.Tensor:
+    """Resize/pad/normalise a batch of uint8 HWC RGB images into one tensor.
+
+    ``images`` is a list of [H, W, 3] uint8 tensors (ragged sizes allowed) or a
+    [B, H, W, 3] uint8 tensor.  Output value = ((px * scale) - mean) / std with the
+    channel order optionally reversed (``swap_rb``).
+    """
+    if isinstance(images, torch.Tensor) and images.dim() == 4:
+        imgs = list(images.unbind(0))
+        flat_src = images.reshape(-1)
+    else:
+        imgs = list(images)
+        flat_src = None
+    B = len(imgs)
+    OH, OW = out_hw
+    device = device or imgs[0].device
+    if geoms is None:
+        off = 0
+        geoms = []
+        for im in imgs:
+            geoms.append(ImageGeom.resize(im.shape[0], im.shape[1], off, OH, OW))
+            off += im.numel()
+    lay = LAYOUTS[layout]
+    filt = FILTERS[filter]
+    if lay == 2:
+        P = (OH // patch) * (OW // patch)
+        kpad = kpad or 3 * patch * patch
+        out = torch.empty((B * P, kpad), device=device, dtype=out_dtype)
+    elif lay == 0:
+        out = torch.empty((B, 3, OH, OW), device=device, dtype=out_dtype)
+    else:
+        out = torch.empty((B, OH, OW, 3), device=device, dtype=out_dtype)
+    if torch.device(device).type == "cuda":
+        src = flat_src if flat_src is not None else torch.cat([im.reshape(-1) for im in imgs])
+        src = src.to(device, non_blocking=True)
+        g = torch.tensor([gg.row() for gg in geoms], dtype=torch.long).to(device, non_blocking=True)
+        max_ch = max(gg.ch for gg in geoms)
+        max_dw = max(gg.dw for gg in geoms)
+        tmp = torch.empty((B, max_ch, max_dw, 3), device=device, dtype=torch.float32)
+        hip_ops().image_prep(src, g, out, tmp, OH, OW, filt, bool(swap_rb), [float(m) for m in mean],
+                             [float(s) for s in std], float(scale), float(pad), lay, int(patch), int(kpad),
+                             int(max_ch), int(max_dw))
+        return out
+    # CPU reference
+    outs = []
+    for im, gg in zip(imgs, geoms):
+        canvas = torch.full((gg.ch, gg.cw, 3), float(pad))
+        canvas[gg.oy:gg.oy + gg.ih, gg.ox:gg.ox + gg.iw] = im.float()
+        t = _ref_resample_axis(canvas, gg.dw, 1, filt)
+        t = _ref_resample_axis(t, gg.dh, 0, filt)
+        full = torch.full((OH, OW, 3), float(pad))
+        full[gg.dy:gg.dy + gg.dh, gg.dx:gg.dx + gg.dw] = t
+        if swap_rb:
+            full = full.flip(-1)
+        v = (full * scale - torch.tensor(mean, dtype=torch.float32)) / torch.tensor(std, dtype=torch.float32)
+        outs.append(v)
+    v = torch.stack(outs)  # B, OH, OW, 3
+    if lay == 0:
+        out.copy_(v.permute(0, 3, 1, 2).to(out_dtype))
+    elif lay == 1:
+        out.copy_(v.to(out_dtype))
+    else:
+        p = patch
+        gh, gw = OH // p, OW // p
+        x = v.permute(0, 3, 1, 2).reshape(B, 3, gh, p, gw, p).permute(0, 2, 4, 1, 3, 5).reshape(B * gh * gw, 3 * p * p)
+        out.zero_()
+        out[:, : 3 * p * p] = x.to(out_dtype)
+    return out

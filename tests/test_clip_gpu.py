@@ -1,0 +1,36 @@
+"""CLIP towers on the GPU (HIP kernels) vs the CPU fp32 reference path."""
+import pytest
+import torch
+
+from lumen_amd.models.clip import CLIPModel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("preset", ["tiny", "ViT-B-32"])
+def test_clip_image_text_gpu_matches_cpu(preset):
+    m_cpu = CLIPModel.random(preset, seed=3, dtype=torch.float32)
+    m_gpu = CLIPModel.random(preset, seed=3, dtype=torch.bfloat16, device="cuda")
+    s = m_cpu.cfg.vision.image_size
+    imgs = torch.randint(0, 256, (4, s + 13, s + 7, 3), dtype=torch.uint8)
+    e_ref = m_cpu.encode_image_uint8(imgs)
+    e = m_gpu.encode_image_uint8(imgs.cuda()).cpu()
+    assert torch.allclose(e.norm(dim=-1), torch.ones(4), atol=1e-3)
+    cos = (e * e_ref).sum(-1)
+    assert cos.min().item() > 0.995, cos
+    ctx = m_cpu.cfg.text.context_length
+    ids = torch.randint(1, 400, (3, ctx))
+    ids[:, 5] = m_cpu.cfg.text.vocab_size - 1
+    t_ref = m_cpu.encode_text_ids(ids)
+    t = m_gpu.encode_text_ids(ids.cuda()).cpu()
+    assert (t * t_ref).sum(-1).min().item() > 0.995
+
+
+def test_vit_l14_batch_runs():
+    m = CLIPModel.random("ViT-L-14", seed=0, device="cuda", with_text=False)
+    imgs = torch.randint(0, 256, (8, 256, 256, 3), dtype=torch.uint8, device="cuda")
+    e = m.encode_image_uint8(imgs)
+    assert e.shape == (8, 768) and torch.isfinite(e).all()
+    # batch invariance: an image's embedding does not depend on its batch mates
+    e1 = m.encode_image_uint8(imgs[:1])
+    assert (e1[0] * e[0]).sum().item() > 0.999

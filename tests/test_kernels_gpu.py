@@ -1,0 +1,142 @@
+"""Numerics of the hand-written gfx950 kernels vs the PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+from lumen_amd import ops
+from lumen_amd._native import native_status
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-6)).item()
+
+
+def test_native_library_loaded():
+    ops.linear(torch.zeros(16, 64, device=DEV, dtype=torch.bfloat16), torch.zeros(16, 64, device=DEV, dtype=torch.bfloat16))
+    st = native_status()
+    assert st["hip_loaded"], st
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 768, 1024), (131, 3072, 1024), (512, 4096, 1024),
+                                   (37, 64, 128), (4096, 1024, 4096), (2, 512, 512), (2570, 1024, 640)])
+@pytest.mark.parametrize("act", [None, "gelu", "quick_gelu"])
+def test_gemm_vs_fp32(M, N, K, act):
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
+    b = torch.randn(N, generator=g).bfloat16()
+    r = torch.randn(M, N, generator=g).bfloat16()
+    ref = ops.linear(x, w, b, act=act, residual=r)
+    got = ops.linear(x.to(DEV), w.to(DEV), b.to(DEV), act=act, residual=r.to(DEV))
+    assert _rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+def test_gemm_tiles_asymmetric(tile):
+    # A = I, asymmetric B: catches a transposed C write
+    M = N = K = 256
+    x = torch.eye(M, K).bfloat16()
+    w = torch.arange(N * K, dtype=torch.float32).reshape(N, K).remainder(97).sub(48).bfloat16()
+    got = ops.linear(x.to(DEV), w.to(DEV), tile=tile).cpu().float()
+    assert torch.equal(got, w.float().t())
+
+
+def test_gemm_row_scatter_table_f32out():
+    B, P, S, W, K = 3, 16, 17, 128, 192
+    x = torch.randn(B * P, K).bfloat16()
+    w = (torch.randn(W, K) * 0.1).bfloat16()
+    pos = torch.randn(S, W).bfloat16()
+    out_ref = torch.zeros(B * S, W).bfloat16()
+    ops.linear(x, w, table=pos, table_period=P, table_offset=1, out=out_ref, out_group=P, out_group_stride=S,
+               out_row_offset=1)
+    out = torch.zeros(B * S, W, device=DEV).bfloat16()
+    ops.linear(x.to(DEV), w.to(DEV), table=pos.to(DEV), table_period=P, table_offset=1, out=out, out_group=P,
+               out_group_stride=S, out_row_offset=1)
+    assert _rel(out, out_ref) < 1e-2
+    f = ops.linear(x.to(DEV), w.to(DEV), out_dtype=torch.float32)
+    assert f.dtype == torch.float32 and _rel(f, x.float() @ w.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("rows,D", [(1, 64), (257, 1024), (1000, 768), (33, 4096), (7, 896), (5, 3584)])
+def test_layernorm_rmsnorm(rows, D):
+    x = torch.randn(rows, D).bfloat16() * 3
+    w = torch.randn(D).bfloat16()
+    b = torch.randn(D).bfloat16()
+    assert _rel(ops.layer_norm(x.to(DEV), w.to(DEV), b.to(DEV)), ops.layer_norm(x, w, b)) < 1e-2
+    add = torch.randn(rows, D).bfloat16()
+    ro_ref = torch.empty_like(x)
+    ro = torch.empty_like(x, device=DEV)
+    ref = ops.rms_norm(x, w, add=add, resid_out=ro_ref)
+    got = ops.rms_norm(x.to(DEV), w.to(DEV), add=add.to(DEV), resid_out=ro)
+    assert _rel(got, ref) < 1e-2 and _rel(ro, ro_ref) < 1e-2
+
+
+def test_layernorm_row_gather_and_l2():
+    x = torch.randn(5 * 17, 256).bfloat16()
+    w = torch.ones(256).bfloat16()
+    idx = torch.arange(5) * 17
+    ref = ops.layer_norm(x, w, row_idx=idx)
+    got = ops.layer_norm(x.to(DEV), w.to(DEV), row_idx=idx.to(DEV))
+    assert _rel(got, ref) < 1e-2
+    e = torch.randn(9, 768)
+    ops.l2_normalize_(e_d := e.to(DEV))
+    assert torch.allclose(e_d.cpu(), e / e.norm(dim=-1, keepdim=True), atol=1e-5)
+
+
+@pytest.mark.parametrize("B,Sq,Sk,H,Hkv,D,causal", [
+    (2, 257, 257, 16, 16, 64, False), (3, 77, 77, 8, 8, 64, True), (1, 197, 197, 12, 12, 64, False),
+    (2, 130, 130, 14, 2, 64, True), (1, 33, 300, 8, 2, 128, True), (2, 65, 65, 4, 4, 128, False),
+    (2, 20, 20, 4, 4, 32, False)])
+def test_attention_vs_fp32(B, Sq, Sk, H, Hkv, D, causal):
+    g = torch.Generator().manual_seed(Sq * H + D)
+    q = torch.randn(B, Sq, H, D, generator=g).bfloat16()
+    k = torch.randn(B, Sk, Hkv, D, generator=g).bfloat16()
+    v = torch.randn(B, Sk, Hkv, D, generator=g).bfloat16()
+    ref = ops.attention(q, k, v, causal=causal)
+    got = ops.attention(q.to(DEV), k.to(DEV), v.to(DEV), causal=causal)
+    assert _rel(got, ref) < 2e-2
+
+
+def test_attention_packed_qkv_and_kv_len():
+    B, S, H, D = 3, 52, 12, 64
+    qkv = torch.randn(B, S, 3, H, D).bfloat16()
+    kl = torch.tensor([52, 10, 31], dtype=torch.int32)
+    ref = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], kv_len=kl)
+    qd = qkv.to(DEV)
+    got = ops.attention(qd[:, :, 0], qd[:, :, 1], qd[:, :, 2], kv_len=kl.to(DEV))
+    assert _rel(got, ref) < 2e-2
+
+
+@pytest.mark.parametrize("filt", ["pil_bicubic", "pil_bilinear", "cv2_linear", "cv2_cubic"])
+def test_image_prep_matches_reference(filt):
+    g = torch.Generator().manual_seed(1)
+    imgs = [torch.randint(0, 256, (45, 61, 3), generator=g, dtype=torch.uint8),
+            torch.randint(0, 256, (20, 16, 3), generator=g, dtype=torch.uint8)]
+    kw = dict(mean=(0.48, 0.45, 0.40), std=(0.26, 0.26, 0.27), filter=filt)
+    ref = ops.image_prep(imgs, (32, 32), **kw)
+    got = ops.image_prep([i.to(DEV) for i in imgs], (32, 32), **kw)
+    # one uint8 LSB of rounding slack
+    assert (got.cpu() - ref).abs().max().item() <= 1.01 / (255 * 0.26)
+
+
+def test_image_prep_patches_layout():
+    imgs = torch.randint(0, 256, (2, 30, 30, 3), dtype=torch.uint8)
+    ref = ops.image_prep(imgs, (16, 16), layout="patches", patch=8, kpad=256, out_dtype=torch.bfloat16)
+    got = ops.image_prep(imgs.to(DEV), (16, 16), layout="patches", patch=8, kpad=256, out_dtype=torch.bfloat16)
+    assert got.shape == (8, 256)
+    assert (got.cpu().float() - ref.float()).abs().max().item() < 0.05
+    assert got[:, 192:].abs().max().item() == 0
+
+
+def test_embed_gather():
+    table = torch.randn(100, 64).bfloat16()
+    pos = torch.randn(9, 64).bfloat16()
+    ids = torch.randint(0, 100, (3, 9))
+    ref = ops.embed(ids, table, pos)
+    got = ops.embed(ids.to(DEV), table.to(DEV), pos.to(DEV))
+    assert _rel(got, ref) < 1e-2
