@@ -83,14 +83,14 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     for (int id = tid; id < KC * NCH; id += 256) {
       const int r = id / NCH, c = id % NCH;
       const int kr = min(k0 + r, a.Sk - 1);
-      uint4 val = *(const uint4*)(kb + (int64_t)kr * a.k_ss + c * 8);
-      *(uint4*)(sK + r * D * 2 + (kswz(r, c, NCH) << 4)) = val;
+      u32x4_t val = *(const u32x4_t*)(kb + (int64_t)kr * a.k_ss + c * 8);
+      *(u32x4_t*)(sK + r * D * 2 + (kswz(r, c, NCH) << 4)) = val;
     }
     // stage V transposed: thread loads 8 dims of one key, scatters 8 bf16
     for (int id = tid; id < KC * NCH; id += 256) {
       const int r = id / NCH, c = id % NCH;   // key r, dims c*8..c*8+7
       const int kr = min(k0 + r, a.Sk - 1);
-      uint4 val = *(const uint4*)(vb + (int64_t)kr * a.v_ss + c * 8);
+      u32x4_t val = *(const u32x4_t*)(vb + (int64_t)kr * a.v_ss + c * 8);
       const uint16_t* e = (const uint16_t*)&val;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {

@@ -17,8 +17,25 @@ typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef uint16_t bf16_raw;
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 namespace lumen {
+
+// Compile-time unrolled loop: f(I) for I in [B, E) with I a literal after
+// inlining (keeps register-array indices static so arrays never hit scratch).
+template <int B, int E>
+struct Unroll {
+  template <typename F>
+  __device__ __forceinline__ static void run(F&& f) {
+    f(B);
+    Unroll<B + 1, E>::run(f);
+  }
+};
+template <int E>
+struct Unroll<E, E> {
+  template <typename F>
+  __device__ __forceinline__ static void run(F&&) {}
+};
 
 // ---- bf16 <-> f32 -------------------------------------------------------
 __device__ __forceinline__ float bf2f(uint16_t v) {
@@ -34,16 +51,16 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
 }
 
 // 16-byte vector of 8 bf16 <-> 8 floats
-__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
-  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
-  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
-  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
-  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+__device__ __forceinline__ void unpack8(const u32x4_t v, float* f) {
+  f[0] = __uint_as_float(v[0] << 16); f[1] = __uint_as_float(v[0] & 0xffff0000u);
+  f[2] = __uint_as_float(v[1] << 16); f[3] = __uint_as_float(v[1] & 0xffff0000u);
+  f[4] = __uint_as_float(v[2] << 16); f[5] = __uint_as_float(v[2] & 0xffff0000u);
+  f[6] = __uint_as_float(v[3] << 16); f[7] = __uint_as_float(v[3] & 0xffff0000u);
 }
-__device__ __forceinline__ uint4 pack8(const float* f) {
-  uint4 v;
-  v.x = pack2bf(f[0], f[1]); v.y = pack2bf(f[2], f[3]);
-  v.z = pack2bf(f[4], f[5]); v.w = pack2bf(f[6], f[7]);
+__device__ __forceinline__ u32x4_t pack8(const float* f) {
+  u32x4_t v;
+  v[0] = pack2bf(f[0], f[1]); v[1] = pack2bf(f[2], f[3]);
+  v[2] = pack2bf(f[4], f[5]); v[3] = pack2bf(f[6], f[7]);
   return v;
 }
 

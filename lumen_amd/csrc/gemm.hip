@@ -105,18 +105,18 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda,
 #pragma unroll
     for (int j = 0; j < NR; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[CA], rb[CB];
+  u32x4_t ra[CA], rb[CB];
   const int nk = K / BK;
 
   // prologue: tile 0 -> buffer 0
 #pragma unroll
-  for (int i = 0; i < CA; ++i) ra[i] = *(const uint4*)(pa[i]);
+  for (int i = 0; i < CA; ++i) ra[i] = *(const u32x4_t*)(pa[i]);
 #pragma unroll
-  for (int i = 0; i < CB; ++i) rb[i] = *(const uint4*)(pb[i]);
+  for (int i = 0; i < CB; ++i) rb[i] = *(const u32x4_t*)(pb[i]);
 #pragma unroll
-  for (int i = 0; i < CA; ++i) *(uint4*)(sA + la[i]) = ra[i];
+  for (int i = 0; i < CA; ++i) *(u32x4_t*)(sA + la[i]) = ra[i];
 #pragma unroll
-  for (int i = 0; i < CB; ++i) *(uint4*)(sB + lb[i]) = rb[i];
+  for (int i = 0; i < CB; ++i) *(u32x4_t*)(sB + lb[i]) = rb[i];
   __syncthreads();
 
   // per-lane fragment read offsets (row low bits = lane & 15)
@@ -127,9 +127,9 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda,
     if (kt + 1 < nk) {
       const int koff = (kt + 1) * BK;
 #pragma unroll
-      for (int i = 0; i < CA; ++i) ra[i] = *(const uint4*)(pa[i] + koff);
+      for (int i = 0; i < CA; ++i) ra[i] = *(const u32x4_t*)(pa[i] + koff);
 #pragma unroll
-      for (int i = 0; i < CB; ++i) rb[i] = *(const uint4*)(pb[i] + koff);
+      for (int i = 0; i < CB; ++i) rb[i] = *(const u32x4_t*)(pb[i] + koff);
     }
     const char* tA = sA + cur * BM * 128;
     const char* tB = sB + cur * BN * 128;
@@ -156,9 +156,9 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda,
       char* nA = sA + (cur ^ 1) * BM * 128;
       char* nB = sB + (cur ^ 1) * BN * 128;
 #pragma unroll
-      for (int i = 0; i < CA; ++i) *(uint4*)(nA + la[i]) = ra[i];
+      for (int i = 0; i < CA; ++i) *(u32x4_t*)(nA + la[i]) = ra[i];
 #pragma unroll
-      for (int i = 0; i < CB; ++i) *(uint4*)(nB + lb[i]) = rb[i];
+      for (int i = 0; i < CB; ++i) *(u32x4_t*)(nB + lb[i]) = rb[i];
     }
     __syncthreads();
   }
@@ -171,8 +171,8 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda,
   constexpr int NPASS = RPP >= 16 ? 1 : 16 / RPP;
   static_assert(TN % 16 == 0 && 64 % LPR == 0, "epilogue tiling");
 
-#pragma unroll
-  for (int i = 0; i < MR; ++i) {
+  // static unroll over accumulator slabs: acc is only ever indexed by constants
+  Unroll<0, MR>::run([&](const int i) {
 #pragma unroll
     for (int j = 0; j < NR; ++j)
 #pragma unroll
@@ -204,13 +204,14 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda,
             const uint16_t* b = (const uint16_t*)ep.bias + n;
             if (full) {
               float f[8];
-              unpack8(*(const uint4*)b, f);
+              unpack8(*(const u32x4_t*)b, f);
 #pragma unroll
               for (int q = 0; q < 8; ++q) v[q] += f[q];
-              unpack8(*(const uint4*)(b + 8), f);
+              unpack8(*(const u32x4_t*)(b + 8), f);
 #pragma unroll
               for (int q = 0; q < 8; ++q) v[8 + q] += f[q];
             } else {
+#pragma unroll
               for (int q = 0; q < 16; ++q) if (n + q < N) v[q] += bf2f(b[q]);
             }
           }
@@ -226,13 +227,14 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda,
           const uint16_t* t = ep.table + (int64_t)((m % ep.table_period) + ep.table_offset) * ep.ldt + n;
           if (full) {
             float f[8];
-            unpack8(*(const uint4*)t, f);
+            unpack8(*(const u32x4_t*)t, f);
 #pragma unroll
             for (int q = 0; q < 8; ++q) v[q] += f[q];
-            unpack8(*(const uint4*)(t + 8), f);
+            unpack8(*(const u32x4_t*)(t + 8), f);
 #pragma unroll
             for (int q = 0; q < 8; ++q) v[8 + q] += f[q];
           } else {
+#pragma unroll
             for (int q = 0; q < 16; ++q) if (n + q < N) v[q] += bf2f(t[q]);
           }
         }
@@ -240,13 +242,14 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda,
           const uint16_t* t = ep.residual + orow * ep.ldr + n;
           if (full) {
             float f[8];
-            unpack8(*(const uint4*)t, f);
+            unpack8(*(const u32x4_t*)t, f);
 #pragma unroll
             for (int q = 0; q < 8; ++q) v[q] += f[q];
-            unpack8(*(const uint4*)(t + 8), f);
+            unpack8(*(const u32x4_t*)(t + 8), f);
 #pragma unroll
             for (int q = 0; q < 8; ++q) v[8 + q] += f[q];
           } else {
+#pragma unroll
             for (int q = 0; q < 16; ++q) if (n + q < N) v[q] += bf2f(t[q]);
           }
         }
@@ -256,21 +259,23 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda,
 #pragma unroll
             for (int q = 0; q < 4; ++q) *(f32x4_t*)(o + 4 * q) = (f32x4_t){v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
           } else {
+#pragma unroll
             for (int q = 0; q < 16; ++q) if (n + q < N) o[q] = v[q];
           }
         } else {
           uint16_t* o = (uint16_t*)C + orow * ldc + n;
           if (full) {
-            *(uint4*)o = pack8(v);
-            *(uint4*)(o + 8) = pack8(v + 8);
+            *(u32x4_t*)o = pack8(v);
+            *(u32x4_t*)(o + 8) = pack8(v + 8);
           } else {
+#pragma unroll
             for (int q = 0; q < 16; ++q) if (n + q < N) o[q] = f2bf(v[q]);
           }
         }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
+  });
 }
 
 template <int BM, int BN, int WM, int WN>

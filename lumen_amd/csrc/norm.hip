@@ -30,10 +30,10 @@ norm_rows_kernel(const uint16_t* __restrict__ x, int64_t x_stride, const int64_t
   for (int c = 0; c < CPL; ++c) {
     const int ch = lane + c * 64;
     if (ch < nch) {
-      unpack8(*(const uint4*)(xr + ch * 8), v[c]);
+      unpack8(*(const u32x4_t*)(xr + ch * 8), v[c]);
       if (add) {
         float a[8];
-        unpack8(*(const uint4*)(add + src_row * add_stride + ch * 8), a);
+        unpack8(*(const u32x4_t*)(add + src_row * add_stride + ch * 8), a);
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[c][i] += a[i];
       }
@@ -46,7 +46,7 @@ norm_rows_kernel(const uint16_t* __restrict__ x, int64_t x_stride, const int64_t
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int ch = lane + c * 64;
-      if (ch < nch) *(uint4*)(resid_out + (int64_t)row * resid_stride + ch * 8) = pack8(v[c]);
+      if (ch < nch) *(u32x4_t*)(resid_out + (int64_t)row * resid_stride + ch * 8) = pack8(v[c]);
     }
   }
   float mean = 0.f;
@@ -76,8 +76,8 @@ norm_rows_kernel(const uint16_t* __restrict__ x, int64_t x_stride, const int64_t
     const int ch = lane + c * 64;
     if (ch >= nch) continue;
     float wf[8], bfv[8];
-    unpack8(*(const uint4*)(w + ch * 8), wf);
-    if (b) unpack8(*(const uint4*)(b + ch * 8), bfv);
+    unpack8(*(const u32x4_t*)(w + ch * 8), wf);
+    if (b) unpack8(*(const u32x4_t*)(b + ch * 8), bfv);
     float o[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -89,7 +89,7 @@ norm_rows_kernel(const uint16_t* __restrict__ x, int64_t x_stride, const int64_t
       *(f32x4_t*)op = (f32x4_t){o[0], o[1], o[2], o[3]};
       *(f32x4_t*)(op + 4) = (f32x4_t){o[4], o[5], o[6], o[7]};
     } else {
-      *(uint4*)((uint16_t*)out + (int64_t)row * out_stride + ch * 8) = pack8(o);
+      *(u32x4_t*)((uint16_t*)out + (int64_t)row * out_stride + ch * 8) = pack8(o);
     }
   }
 }
@@ -143,11 +143,11 @@ __global__ void cls_fill_kernel(uint16_t* __restrict__ x, int64_t seq_stride, co
   uint16_t* xr = x + (int64_t)b * seq_stride;
   for (int ch = threadIdx.x; ch < D / 8; ch += blockDim.x) {
     float c[8], p[8];
-    unpack8(*(const uint4*)(cls + ch * 8), c);
-    unpack8(*(const uint4*)(pos + ch * 8), p);
+    unpack8(*(const u32x4_t*)(cls + ch * 8), c);
+    unpack8(*(const u32x4_t*)(pos + ch * 8), p);
 #pragma unroll
     for (int i = 0; i < 8; ++i) c[i] += p[i];
-    *(uint4*)(xr + ch * 8) = pack8(c);
+    *(u32x4_t*)(xr + ch * 8) = pack8(c);
   }
 }
 
@@ -170,15 +170,15 @@ __global__ void embed_gather_kernel(const int64_t* __restrict__ ids, const uint1
   const uint16_t* pr = pos ? pos + (int64_t)(row % S) * D : nullptr;
   for (int ch = lane; ch < D / 8; ch += 64) {
     float t[8];
-    if (valid) unpack8(*(const uint4*)(tr + ch * 8), t);
+    if (valid) unpack8(*(const u32x4_t*)(tr + ch * 8), t);
     else for (int i = 0; i < 8; ++i) t[i] = 0.f;
     if (pr) {
       float p[8];
-      unpack8(*(const uint4*)(pr + ch * 8), p);
+      unpack8(*(const u32x4_t*)(pr + ch * 8), p);
 #pragma unroll
       for (int i = 0; i < 8; ++i) t[i] += p[i];
     }
-    *(uint4*)(out + (int64_t)row * D + ch * 8) = pack8(t);
+    *(u32x4_t*)(out + (int64_t)row * D + ch * 8) = pack8(t);
   }
 }
 
