@@ -1,10 +1,19 @@
 // Fused multi-head attention forward (flash-style, online softmax) for gfx950.
 //
-// One workgroup = 4 waves = 64 query rows of one (batch, head); each wave owns
-// 16 query rows.  K/V stream through LDS in 64-key chunks: K as an XOR-swizzled
-// row-major image (B operand of S = Q.K^T, one ds_read_b128 per fragment), V
-// transposed into [d][key] (B operand of O += P.V).  P is re-laid from the
-// accumulator layout into an A fragment through a per-wave LDS tile.
+// Transposed-score formulation so that P never leaves registers:
+//   S^T[key][q]  = K . Q^T          (A = K rows from LDS via ds_read_b128,
+//                                    B = Q^T fragment held in registers)
+//   O^T[d][q]   += V^T . P^T        (A = V^T via ds_read_b64_tr_b16 hardware
+//                                    transpose reads of the row-major V image,
+//                                    B = P^T packed straight from the S^T
+//                                    accumulators: the k-order of the two
+//                                    operands is permuted identically)
+// Each lane owns one query column (lane & 15), so the online-softmax row
+// statistics are per-lane values reduced over the 4 lanes {l, l^16, l^32, l^48}.
+//
+// One workgroup = 4 waves = 64 queries of one (batch, head); each wave owns 16.
+// K/V stream through LDS in 64-key chunks, double-buffered and filled by
+// LDS-DMA (global_load_lds_dwordx4) with the XOR swizzle on the source address.
 //
 // Covers every attention the reference runs inside its ONNX graphs:
 // non-causal ViT (CLIP/BioCLIP vision, seq 197/257/577), causal CLIP text (77),
@@ -27,26 +36,44 @@ struct AttnArgs {
   int causal;                 // query i attends keys j <= i + (Sk - Sq)
 };
 
-__device__ __forceinline__ int kswz(int row, int chunk, int nchunk) {
-  // rows of nchunk 16-byte chunks; XOR keeps a ds_read_b128 lane group on
-  // distinct bank slots for both 128-B (D=64) and 256-B (D=128) rows.
-  return nchunk == 8 ? (chunk ^ ((row >> 1) & 7))
-                     : nchunk == 16 ? (chunk ^ (row & 15)) : (chunk ^ ((row >> 1) & 3));
+typedef short s16x4v __attribute__((ext_vector_type(4)));
+
+// K image: rows of D bf16; 16-byte chunk XOR so the ds_read_b128 A-fragment
+// reads of 16 consecutive rows are conflict-free.
+template <int D>
+__device__ __forceinline__ int k_phys(int row, int chunk) {
+  if constexpr (D == 64) return chunk ^ ((row >> 1) & 7);
+  else if constexpr (D == 128) return chunk ^ (row & 15);
+  else return chunk ^ ((row >> 2) & 3);
+}
+// V image: rows of D bf16; chunk XOR so that a 32-lane half of
+// ds_read_b64_tr_b16 (8 rows x 32 bytes) covers all 64 banks.
+template <int D>
+__device__ __forceinline__ int v_phys(int row, int chunk) {
+  if constexpr (D == 64) return chunk ^ (((row >> 1) & 3) << 1);
+  else if constexpr (D == 128) return chunk ^ ((row & 7) << 1);
+  else return chunk ^ (((row >> 2) & 1) << 1);
+}
+
+__device__ __forceinline__ s16x4v ds_read_tr16(const char* p) {
+  typedef __attribute__((address_space(3))) s16x4v* lp;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(p));
 }
 
 template <int D>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
-  constexpr int NCH = D / 8;        // 16-byte chunks per K row
-  constexpr int KS = D / 32;        // MFMA k-steps over head dim
-  constexpr int NB = D / 16;        // 16-wide output column blocks
+  constexpr int NCH = D / 8;        // 16-byte chunks per row
+  constexpr int KS = D / 32;        // MFMA k-steps over head dim (S^T)
+  constexpr int NB = D / 16;        // 16-wide d blocks (O^T)
   constexpr int KC = 64;            // keys per chunk
-  __shared__ __attribute__((aligned(16))) char smem[KC * D * 2 * 2 + 4 * 16 * KC * 2];
-  char* sK = smem;                        // [KC][D]      swizzled
-  char* sV = smem + KC * D * 2;           // [D][KC]      swizzled (8 chunks per row)
-  char* sP = smem + KC * D * 2 * 2;       // [4 waves][16][KC]
+  constexpr int IMG = KC * D * 2;   // bytes per K (or V) chunk image
+  constexpr int RPI = 1024 / (D * 2);  // rows per 1 KiB DMA wave-instruction
+  constexpr int NI = KC / RPI / 4;  // DMA instructions per wave per image
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * IMG];  // [buf][K,V]
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int frow = lane & 15, fq = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, g = lane >> 4;
   const int b = blockIdx.z, h = blockIdx.y;
   const int hk = h / (a.H / a.Hkv);
   const int q0 = blockIdx.x * 64 + wid * 16;
@@ -57,135 +84,164 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const uint16_t* kb = a.k + b * a.k_sb + hk * a.k_sh;
   const uint16_t* vb = a.v + b * a.v_sb + hk * a.v_sh;
 
-  // Q fragments (A operand): row q0 + frow, dims 32s + 8fq .. +8
+  // ---- Q^T fragments (B operand): query q0 + col, dims 32t + 8g .. +8
   bf16x8_t qf[KS];
   {
-    const int qr = min(q0 + frow, a.Sq - 1);
+    const int qr = min(q0 + col, a.Sq - 1);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) qf[s] = *(const bf16x8_t*)(qb + (int64_t)qr * a.q_ss + s * 32 + fq * 8);
+    for (int t = 0; t < KS; ++t) qf[t] = *(const bf16x8_t*)(qb + (int64_t)qr * a.q_ss + t * 32 + g * 8);
   }
+
+  // ---- DMA staging: wave wid fills rows [wid*NI*RPI, +NI*RPI) of each image.
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  typedef const __attribute__((address_space(1))) void* g_ptr_t;
+  int srow[NI], kch[NI], vch[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int r = (wid * NI + i) * RPI + lane / NCH;
+    const int pc = lane % NCH;               // physical chunk this lane lands in
+    srow[i] = r;
+    kch[i] = k_phys<D>(r, pc);               // XOR is an involution: logical = phys ^ f
+    vch[i] = v_phys<D>(r, pc);
+  }
+  auto stage = [&](int chunk, int buf) {
+    const int k0 = chunk * KC;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int kr = min(k0 + srow[i], a.Sk - 1);
+      char* dk = smem + buf * 2 * IMG + (wid * NI + i) * 1024;
+      __builtin_amdgcn_global_load_lds((g_ptr_t)(kb + (int64_t)kr * a.k_ss + kch[i] * 8), (lds_ptr_t)dk, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((g_ptr_t)(vb + (int64_t)kr * a.v_ss + vch[i] * 8), (lds_ptr_t)(dk + IMG), 16,
+                                       0, 0);
+    }
+  };
 
   f32x4_t o[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) o[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  float mrow[4], lrow[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) { mrow[r] = -INFINITY; lrow[r] = 0.f; }
+  float mrow = -INFINITY, lrow = 0.f;   // stats of query q0 + col (replicated over g)
+  const int qi = q0 + col;
 
   int kend = kv_len;
-  if (a.causal) kend = min(kend, blockIdx.x * 64 + 64 + causal_off);
+  if (a.causal) kend = min(kend, min(blockIdx.x * 64 + 64, a.Sq) + causal_off);
   const int nkc = (kend + KC - 1) / KC;
 
-  for (int kc = 0; kc < nkc; ++kc) {
-    const int k0 = kc * KC;
-    __syncthreads();  // previous chunk fully consumed
-    // stage K chunk: KC*NCH 16-byte chunks over 256 threads
-    for (int id = tid; id < KC * NCH; id += 256) {
-      const int r = id / NCH, c = id % NCH;
-      const int kr = min(k0 + r, a.Sk - 1);
-      u32x4_t val = *(const u32x4_t*)(kb + (int64_t)kr * a.k_ss + c * 8);
-      *(u32x4_t*)(sK + r * D * 2 + (kswz(r, c, NCH) << 4)) = val;
-    }
-    // stage V transposed: thread loads 8 dims of one key, scatters 8 bf16
-    for (int id = tid; id < KC * NCH; id += 256) {
-      const int r = id / NCH, c = id % NCH;   // key r, dims c*8..c*8+7
-      const int kr = min(k0 + r, a.Sk - 1);
-      u32x4_t val = *(const u32x4_t*)(vb + (int64_t)kr * a.v_ss + c * 8);
-      const uint16_t* e = (const uint16_t*)&val;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int d = c * 8 + i;
-        const int kch = r >> 3;
-        *(uint16_t*)(sV + d * KC * 2 + (kswz(d, kch, 8) << 4) + (r & 7) * 2) = e[i];
-      }
-    }
-    __syncthreads();
+  // waves whose 16 queries are all past the end (the ragged last q-block, e.g.
+  // 257 = 4*64 + 1) still stage K/V and join the barriers but skip all math.
+  const bool active = q0 < a.Sq;
+  // causal: last key any query of this wave may see
+  const int wave_kend = a.causal ? min(kend, min(q0 + 16, a.Sq) + causal_off) : kend;
 
-    // S = Q K^T for 4 key blocks of 16
+  if (nkc > 0) stage(0, 0);
+  for (int kc = 0; kc < nkc; ++kc) {
+    const int buf = kc & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();                       // chunk kc landed; chunk kc-1 fully consumed
+    if (kc + 1 < nkc) stage(kc + 1, buf ^ 1);
+    const int k0 = kc * KC;
+    if (!active || k0 >= wave_kend) continue;
+    const char* sK = smem + buf * 2 * IMG;
+    const char* sV = sK + IMG;
+    // live 16-key blocks of this chunk (wave-uniform): the ragged tail chunk
+    // (257 keys -> 1 live key) only pays for the blocks it needs
+    const int nblk = min(4, (wave_kend - k0 + 15) >> 4);
+
+    // S^T = K Q^T : 4 key blocks of 16; lane holds keys kb*16 + 4g + r, query col
     f32x4_t sc[4];
 #pragma unroll
     for (int kb16 = 0; kb16 < 4; ++kb16) {
       sc[kb16] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-      const int kr = kb16 * 16 + frow;
+      if (kb16 < nblk) {
+        const int kr = kb16 * 16 + col;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        bf16x8_t kf = *(const bf16x8_t*)(sK + kr * D * 2 + (kswz(kr, s * 4 + fq, NCH) << 4));
-        sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[s], kf, sc[kb16], 0, 0, 0);
+        for (int t = 0; t < KS; ++t) {
+          bf16x8_t kf = *(const bf16x8_t*)(sK + kr * D * 2 + (k_phys<D>(kr, t * 4 + g) << 4));
+          sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[t], sc[kb16], 0, 0, 0);
+        }
       }
     }
-    // mask + online softmax.  lane holds S[row fq*4+r][key kb16*16+frow]
-    float mnew[4];
+    // mask (only on chunks that need it) + online softmax (per lane = per query)
+    const bool need_mask = (k0 + KC > kv_len) || (a.causal && k0 + KC - 1 > q0 + causal_off);
+    float mx = mrow;
+    if (need_mask) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int qi = q0 + fq * 4 + r;
-      float mx = mrow[r];
+      for (int kb16 = 0; kb16 < 4; ++kb16)
 #pragma unroll
-      for (int kb16 = 0; kb16 < 4; ++kb16) {
-        const int kj = k0 + kb16 * 16 + frow;
-        bool ok = kj < kv_len;
-        if (a.causal) ok = ok && (kj <= qi + causal_off);
-        float sv = ok ? sc[kb16][r] * a.scale_log2 : -INFINITY;
-        sc[kb16][r] = sv;
-        mx = fmaxf(mx, sv);
-      }
+        for (int r = 0; r < 4; ++r) {
+          const int kj = k0 + kb16 * 16 + g * 4 + r;
+          bool ok = kj < kv_len;
+          if (a.causal) ok = ok && (kj <= qi + causal_off);
+          const float sv = ok ? sc[kb16][r] * a.scale_log2 : -INFINITY;
+          sc[kb16][r] = sv;
+          mx = fmaxf(mx, sv);
+        }
+    } else {
 #pragma unroll
-      for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
-      mnew[r] = mx;
+      for (int kb16 = 0; kb16 < 4; ++kb16)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float sv = sc[kb16][r] * a.scale_log2;
+          sc[kb16][r] = sv;
+          mx = fmaxf(mx, sv);
+        }
     }
-    float alpha[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float mbase = mnew[r] == -INFINITY ? 0.f : mnew[r];
-      alpha[r] = exp2f(mrow[r] - mbase);
-      float rs = 0.f;
-#pragma unroll
-      for (int kb16 = 0; kb16 < 4; ++kb16) {
-        float p = exp2f(sc[kb16][r] - mbase);
-        sc[kb16][r] = p;
-        rs += p;
-      }
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) rs += __shfl_xor(rs, off, 64);
-      lrow[r] = lrow[r] * alpha[r] + rs;
-      mrow[r] = mnew[r];
-    }
-#pragma unroll
-    for (int j = 0; j < NB; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[j][r] *= alpha[r];
-
-    // P (bf16) -> wave-private LDS tile [16][64], swizzled like K (8 chunks/row)
-    char* pw = sP + wid * 16 * KC * 2;
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mbase = mx == -INFINITY ? 0.f : mx;
+    const float alpha = exp2f(mrow - mbase);
+    float rs = 0.f;
 #pragma unroll
     for (int kb16 = 0; kb16 < 4; ++kb16)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int pr = fq * 4 + r, key = kb16 * 16 + frow;
-        *(uint16_t*)(pw + pr * KC * 2 + (kswz(pr, key >> 3, 8) << 4) + (key & 7) * 2) = f2bf(sc[kb16][r]);
+        const float p = exp2f(sc[kb16][r] - mbase);
+        sc[kb16][r] = p;
+        rs += p;
       }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // O += P V : A = P[16 rows][32 keys] (2 k-steps), B = V[key][d] from sV (transposed image)
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    lrow = lrow * alpha + rs;
+    mrow = mx;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) o[j] *= alpha;
+
+    // O^T += V^T P^T over two 32-key steps
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8_t pf = *(const bf16x8_t*)(pw + frow * KC * 2 + (kswz(frow, s * 4 + fq, 8) << 4));
+      if (2 * s >= nblk) break;
+      bf16x8_t pf;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pf[r] = (__bf16)sc[2 * s][r];
+        pf[4 + r] = (__bf16)sc[2 * s + 1][r];
+      }
+      // tr-read rows (keys): s*32 + 4g + q  and  s*32 + 16 + 4g + q ; lane 4q+p
+      const int q = col >> 2, p = col & 3;
+      const int r0 = s * 32 + 4 * g + q, r1 = r0 + 16;
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        const int d = j * 16 + frow;
-        bf16x8_t vf = *(const bf16x8_t*)(sV + d * KC * 2 + (kswz(d, s * 4 + fq, 8) << 4));
-        o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[j], 0, 0, 0);
+        const int c0 = j * 16 + 4 * p;           // column (d) of this lane's 8-byte piece
+        const char* a0 = sV + r0 * D * 2 + (v_phys<D>(r0, c0 >> 3) << 4) + (c0 & 7) * 2;
+        const char* a1 = sV + r1 * D * 2 + (v_phys<D>(r1, c0 >> 3) << 4) + (c0 & 7) * 2;
+        const s16x4v lo = ds_read_tr16(a0);
+        const s16x4v hi = ds_read_tr16(a1);
+        s16x8_t vv = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, vv), pf, o[j], 0, 0, 0);
       }
     }
   }
 
-  // normalise and store O[b, q, h, :]
-  uint16_t* ob = a.o + b * a.o_sb + h * a.o_sh;
+  // ---- normalise and store O[b, q, h, d]: lane holds d = 16j + 4g + r for query col
+  if (qi < a.Sq) {
+    const float inv = lrow > 0.f ? 1.0f / lrow : 0.f;
+    uint16_t* orow = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qi * a.o_ss;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int qi = q0 + fq * 4 + r;
-    if (qi >= a.Sq) continue;
-    const float inv = lrow[r] > 0.f ? 1.0f / lrow[r] : 0.f;
-#pragma unroll
-    for (int j = 0; j < NB; ++j) ob[(int64_t)qi * a.o_ss + j * 16 + frow] = f2bf(o[j][r] * inv);
+    for (int j = 0; j < NB; ++j) {
+      uint2 w;
+      w.x = pack2bf(o[j][0] * inv, o[j][1] * inv);
+      w.y = pack2bf(o[j][2] * inv, o[j][3] * inv);
+      *(uint2*)(orow + j * 16 + 4 * g) = w;
+    }
   }
 }
 

@@ -344,6 +344,40 @@ def _load_openclip(m: CLIPModel, sd: dict) -> None:
         m.logit_scale = float(sd["logit_scale"])
 
 
+def export_openclip_state_dict(m: CLIPModel) -> dict:
+    """Inverse of the OpenCLIP loader (used to write synthetic model directories)."""
+    sd = {}
+    v = m.visual
+    W, p = v.cfg.width, v.cfg.patch_size
+    sd["visual.conv1.weight"] = v.patch_w[:, : v.kdim].reshape(W, 3, p, p)
+    sd["visual.class_embedding"] = v.class_emb
+    sd["visual.positional_embedding"] = v.pos_emb
+    sd["visual.ln_pre.weight"], sd["visual.ln_pre.bias"] = v.ln_pre_w, v.ln_pre_b
+    sd["visual.ln_post.weight"], sd["visual.ln_post.bias"] = v.ln_post_w, v.ln_post_b
+    sd["visual.proj"] = v.proj_w.t()
+
+    def blocks(bl, prefix):
+        for i, b in enumerate(bl):
+            q = f"{prefix}.resblocks.{i}."
+            sd[q + "ln_1.weight"], sd[q + "ln_1.bias"] = b.ln1_w, b.ln1_b
+            sd[q + "attn.in_proj_weight"], sd[q + "attn.in_proj_bias"] = b.qkv_w, b.qkv_b
+            sd[q + "attn.out_proj.weight"], sd[q + "attn.out_proj.bias"] = b.out_w, b.out_b
+            sd[q + "ln_2.weight"], sd[q + "ln_2.bias"] = b.ln2_w, b.ln2_b
+            sd[q + "mlp.c_fc.weight"], sd[q + "mlp.c_fc.bias"] = b.fc1_w, b.fc1_b
+            sd[q + "mlp.c_proj.weight"], sd[q + "mlp.c_proj.bias"] = b.fc2_w, b.fc2_b
+
+    blocks(v.blocks, "visual.transformer")
+    if m.text is not None:
+        t = m.text
+        sd["token_embedding.weight"] = t.token_emb
+        sd["positional_embedding"] = t.pos_emb
+        blocks(t.blocks, "transformer")
+        sd["ln_final.weight"], sd["ln_final.bias"] = t.ln_final_w, t.ln_final_b
+        sd["text_projection"] = t.proj_w.t()
+    sd["logit_scale"] = torch.tensor(m.logit_scale)
+    return {k: val.detach().contiguous().cpu() for k, val in sd.items()}
+
+
 def _hf_to_openclip(sd: dict, cfg: CLIPConfig) -> dict:
     """Rename HF transformers CLIPModel weights to the OpenCLIP layout."""
     out = {}

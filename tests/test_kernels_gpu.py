@@ -25,18 +25,19 @@ def test_native_library_loaded():
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 768, 1024), (131, 3072, 1024), (512, 4096, 1024),
                                    (37, 64, 128), (4096, 1024, 4096), (2, 512, 512), (2570, 1024, 640)])
 @pytest.mark.parametrize("act", [None, "gelu", "quick_gelu"])
-def test_gemm_vs_fp32(M, N, K, act):
+@pytest.mark.parametrize("tile", [-1, 4, 5, 6])
+def test_gemm_vs_fp32(M, N, K, act, tile):
     g = torch.Generator().manual_seed(M + N + K)
     x = torch.randn(M, K, generator=g).bfloat16()
     w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
     b = torch.randn(N, generator=g).bfloat16()
     r = torch.randn(M, N, generator=g).bfloat16()
     ref = ops.linear(x, w, b, act=act, residual=r)
-    got = ops.linear(x.to(DEV), w.to(DEV), b.to(DEV), act=act, residual=r.to(DEV))
+    got = ops.linear(x.to(DEV), w.to(DEV), b.to(DEV), act=act, residual=r.to(DEV), tile=tile)
     assert _rel(got, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6])
 def test_gemm_tiles_asymmetric(tile):
     # A = I, asymmetric B: catches a transposed C write
     M = N = K = 256

@@ -15,12 +15,15 @@ for M, N, K in shapes:
     x = torch.randn(M, K, device="cuda").bfloat16()
     w = torch.randn(N, K, device="cuda").bfloat16() * 0.05
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    def run_l():
-        ops.linear(x, w, out=out)
     def run_t():
         torch.matmul(x, w.t(), out=out)
     r = {"M": M, "N": N, "K": K}
-    for name, fn in (("lumen", run_l), ("torch", run_t)):
+    variants = [("g1", lambda: ops.linear(x, w, out=out, tile=15)), ("g2", lambda: ops.linear(x, w, out=out, tile=25)),
+                ("g4", lambda: ops.linear(x, w, out=out, tile=45)), ("g8", lambda: ops.linear(x, w, out=out, tile=85)),
+                ("torch", run_t), ("g1b", lambda: ops.linear(x, w, out=out, tile=15)),
+                ("g4b", lambda: ops.linear(x, w, out=out, tile=45)), ("g8b", lambda: ops.linear(x, w, out=out, tile=85)),
+                ("g16", lambda: ops.linear(x, w, out=out, tile=165))]
+    for name, fn in variants:
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -35,7 +38,7 @@ for M, N, K in shapes:
         r[name + "_ms"] = round(ms, 3)
         r[name + "_tflops"] = round(2 * M * N * K / ms / 1e9, 1)
     ref = (x[:256].float() @ w.float().t())
-    ops.linear(x, w, out=out)
+    ops.linear(x, w, out=out, tile=4)
     r["rel_err"] = float(((out[:256].float() - ref).norm() / ref.norm()).item())
     print(json.dumps(r), flush=True)
     res.append(r)
