@@ -86,10 +86,7 @@ __device__ __forceinline__ void epi_store16(float* v, int m, int n, int M, int N
       }
     }
   }
-  if (ep.act) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = apply_act(v[q], ep.act);
-  }
+  if (ep.act) apply_act_n<16>(v, ep.act);
   int64_t orow = m;
   if (ep.out_group > 0)
     orow = (int64_t)(m / ep.out_group) * ep.out_group_stride + ep.out_row_offset + (m % ep.out_group);

@@ -43,6 +43,8 @@ struct PrepArgs {
   int kpad; int out_bf16;
 };
 hipError_t image_prep(const PrepArgs& a, int B, int max_ch, int max_dw, hipStream_t stream);
+hipError_t row_topk(const float* scores, int64_t ld, int B, int N, int k, float scale, float* out_v, int* out_i,
+                    float* out_lse, int index_offset, hipStream_t stream);
 }  // namespace lumen
 
 namespace {
@@ -247,6 +249,26 @@ void image_prep2(const at::Tensor& src, const at::Tensor& geom, at::Tensor out, 
   LUMEN_CHECK_HIP(lumen::image_prep(a, (int)B, (int)max_ch, (int)max_dw, cur_stream()));
 }
 
+// ---------------------------------------------------------------- top-k
+void row_topk(const at::Tensor& scores, int64_t k, double scale, at::Tensor out_v, at::Tensor out_i,
+              const c10::optional<at::Tensor>& out_lse, int64_t index_offset) {
+  check_gpu(scores, "scores");
+  TORCH_CHECK(scores.scalar_type() == at::kFloat && scores.dim() == 2 && scores.stride(1) == 1, "row_topk: f32 [B, N]");
+  TORCH_CHECK(k >= 1 && k <= 64 && k <= scores.size(1), "row_topk: 1 <= k <= min(64, N)");
+  const int64_t B = scores.size(0);
+  TORCH_CHECK(out_v.scalar_type() == at::kFloat && out_v.is_contiguous() && out_v.numel() == B * k, "row_topk: out_v");
+  TORCH_CHECK(out_i.scalar_type() == at::kInt && out_i.is_contiguous() && out_i.numel() == B * k, "row_topk: out_i");
+  float* lse = nullptr;
+  if (out_lse.has_value() && out_lse->defined()) {
+    TORCH_CHECK(out_lse->scalar_type() == at::kFloat && out_lse->numel() == B, "row_topk: out_lse");
+    lse = out_lse->data_ptr<float>();
+  }
+  const at::DeviceGuard guard(scores.device());
+  LUMEN_CHECK_HIP(lumen::row_topk(scores.data_ptr<float>(), scores.stride(0), (int)B, (int)scores.size(1), (int)k,
+                                  (float)scale, out_v.data_ptr<float>(), out_i.data_ptr<int>(), lse, (int)index_offset,
+                                  cur_stream()));
+}
+
 }  // namespace
 
 TORCH_LIBRARY(lumen, m) {
@@ -262,6 +284,8 @@ TORCH_LIBRARY(lumen, m) {
   m.def("image_prep(Tensor src, Tensor geom, Tensor(o!) out, Tensor(t!) tmp, int out_h, int out_w, int filter, "
         "bool swap_rb, float[] mean, float[] std, float scale, float pad, int layout, int patch, int kpad, "
         "int max_ch, int max_dw) -> ()");
+  m.def("row_topk(Tensor scores, int k, float scale, Tensor(v!) out_v, Tensor(i!) out_i, Tensor(l!)? out_lse, "
+        "int index_offset) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
@@ -272,4 +296,5 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("embed_gather", &embed_gather);
   m.impl("attention", &attention);
   m.impl("image_prep", &image_prep2);
+  m.impl("row_topk", &row_topk);
 }

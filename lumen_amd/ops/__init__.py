@@ -242,6 +242,37 @@ def attention(q, k, v, scale: Optional[float] = None, causal: bool = False, kv_l
     return out
 
 
+# --------------------------------------------------------------------------- top-k
+def row_topk(scores: torch.Tensor, k: int, scale: float = 1.0, with_lse: bool = False, index_offset: int = 0):
+    """Per-row top-k (descending) of fp32 scores [B, N]; optionally the row logsumexp(scale*s).
+
+    Returns (values [B,k] f32, indices [B,k] int32, lse [B] f32 | None).
+    """
+    B, N = scores.shape
+    k = min(k, N)
+    if scores.is_cuda:
+        v = torch.empty((B, k), device=scores.device, dtype=torch.float32)
+        i = torch.empty((B, k), device=scores.device, dtype=torch.int32)
+        lse = torch.empty((B,), device=scores.device, dtype=torch.float32) if with_lse else None
+        hip_ops().row_topk(scores.contiguous().float(), int(k), float(scale), v, i, lse, int(index_offset))
+        return v, i, lse
+    s = scores.float()
+    v, i = torch.topk(s, k, dim=-1, largest=True, sorted=True)
+    lse = torch.logsumexp(s * scale, dim=-1) if with_lse else None
+    return v, (i + index_offset).to(torch.int32), lse
+
+
+def bank_scores(q: torch.Tensor, bank: torch.Tensor) -> torch.Tensor:
+    """cosine scores [B, N] (fp32) of unit query rows q [B, D] against a unit label bank [N, D]."""
+    if q.is_cuda:
+        D = q.shape[1]
+        qb = q.to(bank.dtype) if bank.dtype == torch.bfloat16 else q
+        if D % 64 != 0 or bank.dtype != torch.bfloat16:
+            return (q.float() @ bank.float().t())
+        return linear(qb.contiguous(), bank, out_dtype=torch.float32)
+    return q.float() @ bank.float().t()
+
+
 # --------------------------------------------------------------------------- image prep
 FILTERS = {"pil_bicubic": 0, "bicubic": 0, "pil_bilinear": 1, "cv2_linear": 2, "linear": 2, "cv2_cubic": 3}
 LAYOUTS = {"nchw": 0, "nhwc": 1, "patches": 2}

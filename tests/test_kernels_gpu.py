@@ -141,3 +141,22 @@ def test_embed_gather():
     ref = ops.embed(ids, table, pos)
     got = ops.embed(ids.to(DEV), table.to(DEV), pos.to(DEV))
     assert _rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,N,k", [(1, 1000, 5), (3, 100000, 10), (2, 37, 37), (4, 5000, 64)])
+def test_row_topk_and_lse(B, N, k):
+    s = torch.randn(B, N)
+    v_ref, i_ref, lse_ref = ops.row_topk(s, k, scale=100.0, with_lse=True)
+    v, i, lse = ops.row_topk(s.to(DEV), k, scale=100.0, with_lse=True)
+    assert torch.allclose(v.cpu(), v_ref, atol=1e-6)
+    assert torch.equal(i.cpu(), i_ref)
+    assert torch.allclose(lse.cpu(), lse_ref, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("act", ["gelu", "quick_gelu", "silu", "gelu_tanh", "relu", "hardswish", "sigmoid"])
+def test_gemm_activations(act):
+    x = torch.randn(300, 128).bfloat16()
+    w = (torch.randn(256, 128) * 0.2).bfloat16()
+    ref = ops.linear(x, w, act=act)
+    got = ops.linear(x.to(DEV), w.to(DEV), act=act)
+    assert _rel(got, ref) < 1e-2
