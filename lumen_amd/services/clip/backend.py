@@ -1,0 +1,204 @@
+"""MI355X CLIP backend (L2): weights -> CLIPModel on the GPU, tokenizer, preprocessing.
+
+Contract of the reference ``BaseClipBackend`` (packages/lumen-clip/src/lumen_clip/
+backends/base.py:47-292): ``initialize``, ``image_to_vector``, ``text_to_vector``,
+``image_batch_to_vectors``, ``text_batch_to_vectors``, ``get_info``,
+``get_temperature``; vectors are unit-normalised fp32 numpy arrays.
+
+MI355X specifics: image decode on CPU threads, then ONE fused
+resize+normalise+patchify HIP kernel for the whole batch, the bf16 tower on
+MFMA kernels and the L2-normalise epilogue on device; concurrent requests from
+all gRPC streams are merged by a :class:`~lumen_amd.runtime.batcher.DynamicBatcher`
+that owns the device.  The same backend serves runtime ``torch`` and ``onnx``
+configs (one native execution path, no multi-backend dispatch); ``device: cpu``
+selects the fp32 PyTorch reference path (BASELINE config #1).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import time
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from ...models.clip import CLIPModel
+from ...runtime.batcher import DynamicBatcher
+from ...utils.image import decode_many
+from .resources import ModelResources, load_weights
+
+log = logging.getLogger("lumen.clip.backend")
+
+
+class BackendError(Exception):
+    pass
+
+
+class BackendNotInitializedError(BackendError):
+    pass
+
+
+class InvalidInputError(BackendError):
+    pass
+
+
+@dataclass
+class BackendInfo:
+    runtime: str
+    device: Optional[str]
+    model_id: str
+    model_name: str
+    version: str = "1.0.0"
+    precisions: tuple = ("bf16",)
+    image_embedding_dim: Optional[int] = None
+    text_embedding_dim: Optional[int] = None
+    supports_image_batch: bool = True
+    extra_metadata: Optional[dict] = None
+
+
+def pick_device(pref: Optional[str]) -> torch.device:
+    if pref and pref.startswith("cpu"):
+        return torch.device("cpu")
+    if torch.cuda.is_available():
+        if pref and pref.startswith("cuda"):
+            return torch.device(pref)
+        return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1))
+    return torch.device("cpu")
+
+
+class MI355XClipBackend:
+    def __init__(self, resources: ModelResources, device: Optional[str] = None, batch_size: int = 8,
+                 max_batch: int = 256, max_wait_ms: float = 2.0, precision: Optional[str] = None):
+        self.resources = resources
+        self.device_pref = device
+        self.batch_size = batch_size
+        self.max_batch = max_batch
+        self.max_wait_ms = max_wait_ms
+        self.precision = precision
+        self.model: Optional[CLIPModel] = None
+        self.tokenizer = None
+        self.context_length = 77
+        self.load_time = 0.0
+        self._img_batcher: Optional[DynamicBatcher] = None
+        self._txt_batcher: Optional[DynamicBatcher] = None
+        self.is_initialized = False
+
+    # ------------------------------------------------------------------ lifecycle
+    def initialize(self) -> None:
+        if self.is_initialized:
+            return
+        t0 = time.time()
+        self.device = pick_device(self.device_pref)
+        dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        cfg = self.resources.clip_config()
+        mean, std = self.resources.get_normalization_stats()
+        cfg.image_mean, cfg.image_std = tuple(mean), tuple(std)
+        self.cfg = cfg
+        self.context_length = cfg.text.context_length
+        m = CLIPModel(cfg, dtype=dtype, device="cpu")
+        m.load_state_dict_any(load_weights(self.resources.model_root_path))
+        self.model = m.to(self.device)
+        self._load_tokenizer()
+        self._img_batcher = DynamicBatcher(self._encode_images, self.max_batch, self.max_wait_ms, "clip-image")
+        self._txt_batcher = DynamicBatcher(self._encode_texts, self.max_batch, self.max_wait_ms, "clip-text")
+        self.load_time = time.time() - t0
+        self.is_initialized = True
+        log.info("CLIP %s ready on %s in %.2fs", self.resources.model_name, self.device, self.load_time)
+
+    def close(self) -> None:
+        for b in (self._img_batcher, self._txt_batcher):
+            if b is not None:
+                b.close()
+
+    def _load_tokenizer(self) -> None:
+        p = self.resources.tokenizer_path
+        if p is None:
+            raise BackendError(f"tokenizer.json missing in {self.resources.model_root_path}")
+        from tokenizers import Tokenizer
+
+        tok = Tokenizer.from_file(str(p))
+        tok.enable_truncation(max_length=self.context_length)
+        tok.enable_padding(pad_id=0, pad_token="<pad>", length=self.context_length)
+        self.tokenizer = tok
+
+    def _ensure(self):
+        if not self.is_initialized:
+            raise BackendNotInitializedError("backend not initialized")
+
+    # ------------------------------------------------------------------ batched workers
+    def tokenize(self, texts: Sequence[str]) -> torch.Tensor:
+        encs = self.tokenizer.encode_batch(list(texts))
+        ids = np.array([e.ids[: self.context_length] for e in encs], dtype=np.int64)
+        return torch.from_numpy(ids)
+
+    def _encode_texts(self, texts: Sequence[str]) -> list:
+        with torch.no_grad():
+            ids = self.tokenize(texts).to(self.device)
+            emb = self.model.encode_text_ids(ids).float().cpu().numpy()
+        return list(emb)
+
+    def _encode_images(self, payloads: Sequence[bytes]) -> list:
+        imgs = decode_many(payloads)
+        with torch.no_grad():
+            tens = [torch.from_numpy(i) for i in imgs]
+            emb = self.model.encode_image_uint8(tens).float().cpu().numpy()
+        return list(emb)
+
+    # ------------------------------------------------------------------ public API
+    def image_to_vector(self, image_bytes: bytes) -> np.ndarray:
+        self._ensure()
+        if not image_bytes:
+            raise InvalidInputError("empty image payload")
+        return self._img_batcher(image_bytes)
+
+    def image_batch_to_vectors(self, images: Sequence[bytes]) -> np.ndarray:
+        self._ensure()
+        out = []
+        for i in range(0, len(images), self.max_batch):
+            out.extend(self._encode_images(images[i:i + self.max_batch]))
+        return np.stack(out).astype(np.float32)
+
+    def text_to_vector(self, text: str) -> np.ndarray:
+        self._ensure()
+        return self._txt_batcher(text)
+
+    def text_batch_to_vectors(self, texts: Sequence[str]) -> np.ndarray:
+        self._ensure()
+        out = []
+        for i in range(0, len(texts), self.max_batch):
+            out.extend(self._encode_texts(texts[i:i + self.max_batch]))
+        return np.stack(out).astype(np.float32) if out else np.zeros((0, self.cfg.embed_dim), np.float32)
+
+    def get_temperature(self) -> float:
+        return float(np.exp(self.model.logit_scale)) if self.model is not None else 100.0
+
+    def get_info(self) -> BackendInfo:
+        r = self.resources
+        dim = self.cfg.embed_dim if self.is_initialized else r.get_embedding_dim()
+        return BackendInfo(runtime="mi355x-hip" if getattr(self, "device", None) is not None and self.device.type == "cuda"
+                           else "torch-cpu-reference", device=str(getattr(self, "device", self.device_pref)),
+                           model_id=r.model_id, model_name=r.model_name, image_embedding_dim=dim,
+                           text_embedding_dim=dim,
+                           precisions=("bf16",) if getattr(self, "device", None) is not None and self.device.type == "cuda"
+                           else ("fp32",),
+                           extra_metadata={"image_size": str(r.get_image_size()),
+                                           "context_length": str(self.context_length)})
+
+
+def create_backend(backend_settings, resources: ModelResources, runtime: Optional[str] = None,
+                   precision: Optional[str] = None) -> MI355XClipBackend:
+    """Factory (reference backends/factory.py:21-141): runtime must be onnx|torch|rknn."""
+    rt = runtime or resources.runtime
+    if rt not in ("onnx", "torch", "rknn"):
+        raise ValueError(f"unsupported runtime '{rt}' (expected onnx|torch|rknn)")
+    if rt == "rknn":
+        raise ImportError("RKNN runtime is not available on MI355X builds")
+    from ...resources.config import AmdRuntimeSettings
+
+    amd = AmdRuntimeSettings.from_env()
+    dev = getattr(backend_settings, "device", None) if backend_settings is not None else None
+    bs = getattr(backend_settings, "batch_size", 8) if backend_settings is not None else 8
+    return MI355XClipBackend(resources, device=dev, batch_size=bs or 8, max_batch=amd.max_batch,
+                             max_wait_ms=amd.max_wait_ms, precision=precision)

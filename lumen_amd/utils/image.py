@@ -40,7 +40,7 @@ def decode_rgb(data: bytes, draft_to: Optional[tuple[int, int]] = None, exif_tra
         im = im.convert("RGB")
     except Exception as e:
         raise ValueError(f"cannot decode image: {e}") from e
-    return np.asarray(im, dtype=np.uint8)
+    return np.array(im, dtype=np.uint8)  # writable copy (torch.from_numpy-safe)
 
 
 def decode_bgr(data: bytes) -> np.ndarray:

@@ -1,0 +1,156 @@
+"""In-process gRPC tests of the CLIP services + hub router on the CPU reference path."""
+import json
+import threading
+
+import grpc
+import numpy as np
+import pytest
+import yaml
+
+from lumen_amd.hub.router import HubRouter
+from lumen_amd.hub.server import AppService, build_server
+from lumen_amd.proto import ml_service as pb
+from lumen_amd.resources.synthetic import write_clip_model
+from lumen_amd.resources.validator import config_from_dict
+from lumen_amd.utils.image import encode_jpeg, encode_png
+
+
+def _cfg(cache, mode="hub"):
+    return {
+        "metadata": {"version": "1.0.0", "region": "other", "cache_dir": str(cache)},
+        "deployment": {"mode": "hub", "services": ["clip", "bioclip"]} if mode == "hub" else {"mode": "single", "service": "clip"},
+        "server": {"port": 50551, "host": "127.0.0.1"},
+        "services": {
+            "clip": {"enabled": True, "package": "lumen_clip",
+                     "import_info": {"registry_class": "lumen_clip.general_clip.clip_service.GeneralCLIPService",
+                                     "add_to_server": "lumen_clip.proto.ml_service_pb2_grpc.add_InferenceServicer_to_server"},
+                     "backend_settings": {"device": "cpu", "batch_size": 4},
+                     "models": {"general": {"model": "clip-tiny", "runtime": "torch", "dataset": "ImageNet_1k"}}},
+            "bioclip": {"enabled": True, "package": "lumen_clip",
+                        "import_info": {"registry_class": "lumen_clip.expert_bioclip.bioclip_service.BioCLIPService",
+                                        "add_to_server": "lumen_clip.proto.ml_service_pb2_grpc.add_InferenceServicer_to_server"},
+                        "backend_settings": {"device": "cpu"},
+                        "models": {"bioclip": {"model": "bioclip-tiny", "runtime": "onnx", "dataset": "TreeOfLife-10M"}}},
+        },
+    }
+
+
+@pytest.fixture(scope="module")
+def hub(tmp_path_factory):
+    cache = tmp_path_factory.mktemp("cache")
+    write_clip_model(cache / "models" / "clip-tiny", "clip-tiny", preset="tiny", dataset="ImageNet_1k", n_labels=40)
+    write_clip_model(cache / "models" / "bioclip-tiny", "bioclip-tiny", preset="tiny", dataset="TreeOfLife-10M",
+                     n_labels=60, bio=True)
+    cfg = config_from_dict(_cfg(cache))
+    app = AppService.from_app_config(cfg)
+    router = HubRouter(app.services)
+    server, port = build_server(router, "127.0.0.1", 0)
+    server.start()
+    ch = grpc.insecure_channel(f"127.0.0.1:{port}")
+    yield pb.InferenceStub(ch), router, cache
+    ch.close()
+    server.stop(0)
+    app.close()
+
+
+def _img(seed=0, png=False):
+    a = np.random.default_rng(seed).integers(0, 255, (48, 40, 3), dtype=np.uint8)
+    return encode_png(a) if png else encode_jpeg(a)
+
+
+def _one(stub, task, payload, mime, meta=None, cid="c1"):
+    rs = list(stub.Infer(iter([pb.InferRequest(correlation_id=cid, task=task, payload=payload, payload_mime=mime,
+                                               meta=meta or {})])))
+    assert len(rs) == 1
+    return rs[0]
+
+
+def test_route_table(hub):
+    _, router, _ = hub
+    assert set(router.route_table) >= {"clip_text_embed", "clip_image_embed", "clip_classify", "clip_scene_classify",
+                                       "bioclip_text_embed", "bioclip_image_embed", "bioclip_classify"}
+
+
+def test_image_and_text_embed(hub):
+    stub, _, _ = hub
+    r = _one(stub, "clip_image_embed", _img(), "image/jpeg")
+    assert not r.HasField("error") and r.is_final and r.correlation_id == "c1"
+    assert r.result_mime == "application/json;schema=embedding_v1"
+    d = json.loads(r.result)
+    assert d["dim"] == 64 and len(d["vector"]) == 64 and d["model_id"] == "clip-tiny_torch"
+    assert abs(np.linalg.norm(d["vector"]) - 1) < 1e-4
+    assert "lat_ms" in r.meta and r.meta["dim"] == "64"
+    t = json.loads(_one(stub, "clip_text_embed", b"a cat", "text/plain").result)
+    assert t["model_id"] == "clip-tiny:clip-tiny_torch"
+
+
+def test_classify_and_scene(hub):
+    stub, _, _ = hub
+    r = _one(stub, "clip_classify", _img(1, png=True), "image/png", {"topk": "3"})
+    d = json.loads(r.result)
+    assert len(d["labels"]) == 3 and r.meta["labels_count"] == "3"
+    scores = [x["score"] for x in d["labels"]]
+    assert scores == sorted(scores, reverse=True) and 0 < sum(scores) <= 1.0001
+    s = json.loads(_one(stub, "clip_scene_classify", _img(2), "image/jpeg").result)
+    assert len(s["labels"]) == 1 and "photo" not in s["labels"][0]["label"]
+
+
+def test_bioclip(hub):
+    stub, _, _ = hub
+    r = _one(stub, "bioclip_classify", _img(3), "image/jpeg", {"namespace": "bioatlas", "topk": "4"})
+    d = json.loads(r.result)
+    assert len(d["labels"]) == 4 and d["model_id"] == "bioclip-tiny_onnx"
+    bad = _one(stub, "bioclip_text_embed", b"x", "image/jpeg")
+    assert bad.error.code == pb.ERROR_CODE_INTERNAL
+    bad = _one(stub, "bioclip_classify", _img(3), "image/jpeg", {"namespace": "zoo"})
+    assert bad.HasField("error")
+
+
+def test_chunked_upload_and_errors(hub):
+    stub, _, _ = hub
+    data = _img(4)
+    parts = [data[i:i + 100] for i in range(0, len(data), 100)]
+    reqs = [pb.InferRequest(correlation_id="big", task="clip_image_embed", payload=p, payload_mime="image/jpeg",
+                            seq=i, total=len(parts), offset=i * 100) for i, p in enumerate(parts)]
+    rs = list(stub.Infer(iter(reqs)))
+    assert len(rs) == 1 and json.loads(rs[0].result)["dim"] == 64
+    ref = json.loads(_one(stub, "clip_image_embed", data, "image/jpeg").result)["vector"]
+    assert np.allclose(json.loads(rs[0].result)["vector"], ref, atol=1e-5)
+    # unknown task routed by the hub -> NOT_FOUND status
+    with pytest.raises(grpc.RpcError) as e:
+        list(stub.Infer(iter([pb.InferRequest(task="nope", payload=b"x")])))
+    assert e.value.code() == grpc.StatusCode.NOT_FOUND
+    # garbage image -> INTERNAL error payload, stream continues
+    rs = list(stub.Infer(iter([pb.InferRequest(task="clip_image_embed", payload=b"notanimage"),
+                               pb.InferRequest(task="clip_image_embed", payload=data, payload_mime="image/jpeg")])))
+    assert rs[0].error.code == pb.ERROR_CODE_INTERNAL and rs[0].correlation_id.startswith("cid-")
+    assert not rs[1].HasField("error")
+
+
+def test_capabilities_and_health(hub):
+    stub, _, _ = hub
+    cap = stub.GetCapabilities(pb.Empty())
+    names = {t.name for t in cap.tasks}
+    assert "clip_image_embed" in names and "bioclip_classify" in names
+    caps = list(stub.StreamCapabilities(pb.Empty()))
+    assert {c.service_name for c in caps} == {"lumen_clip", "lumen_bioclip"}
+    assert all(c.protocol_version == "1.0" for c in caps)
+    t = [t for t in caps[0].tasks][0]
+    assert t.limits["max_payload_size"] == "52428800"
+    stub.Health(pb.Empty())
+
+
+def test_concurrent_streams_batched(hub):
+    stub, router, _ = hub
+    svc = router.route_table["clip_image_embed"]
+    out = []
+
+    def work(i):
+        out.append(json.loads(_one(stub, "clip_image_embed", _img(10 + i), "image/jpeg", cid=f"t{i}").result))
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(8)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert len(out) == 8
+    b = svc.backend._img_batcher
+    assert b.items >= 8
