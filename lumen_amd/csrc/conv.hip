@@ -1,0 +1,434 @@
+// Convolution and CNN-support kernels (NHWC bf16) for the face (SCRFD/RetinaFace,
+// IResNet ArcFace) and OCR (DBNet, LCNet/SVTR recogniser) towers.
+//
+// conv2d_igemm: implicit-GEMM convolution on MFMA.  GEMM view:
+//   M = N*Ho*Wo output pixels, N = Cout, K = KH*KW*Cin,
+//   A[m][k] = x[n, ho*sh-ph+ky*dh, wo*sw-pw+kx*dw, ci]  (zero outside),
+//   B[n][k] = w[cout][ky][kx][ci]                       ([Cout, KH, KW, Cin] layout)
+// A 16-byte A-chunk is 8 consecutive input channels of one tap (Cin % 8 == 0),
+// gathered straight from NHWC memory into the XOR-swizzled LDS tile (no im2col
+// buffer); the tap / channel cursor of every staging slot advances
+// incrementally per K-tile.  The output tile is NHWC = the GEMM C layout, so the
+// shared epilogue fuses bias (folded BN), activation, per-channel PReLU and the
+// residual add, and can write into a channel slice of a wider tensor (concat).
+//
+// Replaces the Conv / BatchNormalization / Relu / PRelu / Add ONNX nodes of the
+// reference's detection.*.onnx / recognition.*.onnx graphs.
+#include "conv.h"
+#include "gemm_epi.h"
+
+namespace lumen {
+
+constexpr int CBK = 64;
+
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(WM* WN * 64) conv_igemm_kernel(ConvArgs a, GemmEpi ep) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MR = TM / 16, NR = TN / 16;
+  constexpr int CA = BM * 8 / NT;
+  constexpr int CB = BN * 8 / NT;
+  static_assert(CA >= 1 && CB >= 1 && BM * 8 % NT == 0 && BN * 8 % NT == 0, "tiling");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* sA = smem;
+  char* sB = smem + 2 * BM * 128;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int M = a.N * a.Ho * a.Wo, Nn = a.Cout, K = a.KH * a.KW * a.Cin;
+  const int tiles_n = (Nn + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_n * tiles_m);
+  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+
+  // ---- A staging slots: output pixel + incremental (tap, ci) cursor
+  const uint16_t* xb[CA];
+  int hb[CA], wb[CA], ci[CA], ky[CA], kx[CA], kk[CA], la[CA];
+  bool mv[CA];
+#pragma unroll
+  for (int i = 0; i < CA; ++i) {
+    const int id = tid + i * NT, r = id >> 3, c = id & 7;
+    const int m = m0 + r;
+    mv[i] = m < M;
+    const int mm = mv[i] ? m : 0;
+    const int img = mm / (a.Ho * a.Wo), rem = mm % (a.Ho * a.Wo);
+    const int ho = rem / a.Wo, wo = rem % a.Wo;
+    xb[i] = a.x + (int64_t)img * a.H * a.W * a.ldx;
+    hb[i] = ho * a.sh - a.ph;
+    wb[i] = wo * a.sw - a.pw;
+    kk[i] = c * 8;
+    const int tap = kk[i] / a.Cin;
+    ci[i] = kk[i] % a.Cin;
+    ky[i] = tap / a.KW;
+    kx[i] = tap % a.KW;
+    la[i] = swz(r, c);
+  }
+  const uint16_t* pb[CB];
+  int lb[CB], kb[CB];
+#pragma unroll
+  for (int i = 0; i < CB; ++i) {
+    const int id = tid + i * NT, r = id >> 3, c = id & 7;
+    pb[i] = a.w + (int64_t)min(n0 + r, Nn - 1) * K + c * 8;
+    kb[i] = c * 8;
+    lb[i] = swz(r, c);
+  }
+
+  auto load_a = [&](int i) -> u32x4_t {
+    const int hi = hb[i] + ky[i] * a.dh, wi = wb[i] + kx[i] * a.dw;
+    const bool ok = mv[i] && kk[i] < K && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+    u32x4_t v = (u32x4_t){0u, 0u, 0u, 0u};
+    if (ok) v = *(const u32x4_t*)(xb[i] + ((int64_t)hi * a.W + wi) * a.ldx + ci[i]);
+    return v;
+  };
+  auto advance_a = [&](int i) {
+    kk[i] += CBK;
+    ci[i] += CBK;
+    while (ci[i] >= a.Cin) {
+      ci[i] -= a.Cin;
+      if (++kx[i] == a.KW) { kx[i] = 0; ++ky[i]; }
+    }
+  };
+  auto load_b = [&](int i, int koff) -> u32x4_t {
+    u32x4_t v = (u32x4_t){0u, 0u, 0u, 0u};
+    if (kb[i] + koff < K) v = *(const u32x4_t*)(pb[i] + koff);
+    return v;
+  };
+
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  u32x4_t ra[CA], rb[CB];
+  const int nk = (K + CBK - 1) / CBK;
+#pragma unroll
+  for (int i = 0; i < CA; ++i) ra[i] = load_a(i);
+#pragma unroll
+  for (int i = 0; i < CB; ++i) rb[i] = load_b(i, 0);
+#pragma unroll
+  for (int i = 0; i < CA; ++i) *(u32x4_t*)(sA + la[i]) = ra[i];
+#pragma unroll
+  for (int i = 0; i < CB; ++i) *(u32x4_t*)(sB + lb[i]) = rb[i];
+  __syncthreads();
+
+  const int frow = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+#pragma unroll
+      for (int i = 0; i < CA; ++i) { advance_a(i); ra[i] = load_a(i); }
+#pragma unroll
+      for (int i = 0; i < CB; ++i) rb[i] = load_b(i, (kt + 1) * CBK);
+    }
+    const char* tA = sA + cur * BM * 128;
+    const char* tB = sB + cur * BN * 128;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8_t fa[MR], fb[NR];
+#pragma unroll
+      for (int i = 0; i < MR; ++i) fa[i] = *(const bf16x8_t*)(tA + swz(wm * TM + i * 16 + frow, s * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < NR; ++j) fb[j] = *(const bf16x8_t*)(tB + swz(wn * TN + j * 16 + frow, s * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      char* nA = sA + (cur ^ 1) * BM * 128;
+      char* nB = sB + (cur ^ 1) * BN * 128;
+#pragma unroll
+      for (int i = 0; i < CA; ++i) *(u32x4_t*)(nA + la[i]) = ra[i];
+#pragma unroll
+      for (int i = 0; i < CB; ++i) *(u32x4_t*)(nB + lb[i]) = rb[i];
+    }
+    __syncthreads();
+  }
+
+  constexpr int LDSTR = TN + 4;
+  float* es = (float*)smem + wid * 16 * LDSTR;
+  constexpr int LPR = TN / 16;
+  constexpr int RPP = 64 / LPR;
+  constexpr int NPASS = RPP >= 16 ? 1 : 16 / RPP;
+  Unroll<0, MR>::run([&](const int i) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) es[(fq * 4 + r) * LDSTR + j * 16 + frow] = acc[i][j][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const int rr = p * RPP + lane / LPR;
+      const int cc = (lane % LPR) * 16;
+      if (rr < 16) {
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cc + q * 4);
+          v[q * 4 + 0] = t[0]; v[q * 4 + 1] = t[1]; v[q * 4 + 2] = t[2]; v[q * 4 + 3] = t[3];
+        }
+        epi_store16(v, m0 + wm * TM + i * 16 + rr, n0 + wn * TN + cc, M, Nn, a.out, a.ldo, ep);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  });
+}
+
+template <int BM, int BN, int WM, int WN>
+static hipError_t launch_conv(const ConvArgs& a, const GemmEpi& ep, hipStream_t stream) {
+  const int M = a.N * a.Ho * a.Wo;
+  const int tiles = ((M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
+  size_t lds = 2 * (size_t)(BM + BN) * 128;
+  const size_t epi = (size_t)WM * WN * 16 * (BN / WN + 4) * 4;
+  if (epi > lds) lds = epi;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_igemm_kernel<BM, BN, WM, WN>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN>), dim3(tiles), dim3(WM * WN * 64), lds, stream, a, ep);
+  return hipGetLastError();
+}
+
+hipError_t conv2d_igemm(const ConvArgs& a, const GemmEpi& ep, int tile, hipStream_t stream) {
+  const int64_t M = (int64_t)a.N * a.Ho * a.Wo;
+  if (tile < 0) {
+    const int64_t t128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
+    if (a.Cout >= 128 && t128 >= 256) tile = 0;
+    else if (a.Cout >= 64) tile = 1;
+    else tile = 2;
+  }
+  switch (tile) {
+    case 0: return launch_conv<128, 128, 2, 2>(a, ep, stream);
+    case 1: return launch_conv<128, 64, 2, 2>(a, ep, stream);
+    default: return launch_conv<128, 32, 4, 1>(a, ep, stream);
+  }
+}
+
+// ---------------------------------------------------------------------------- depthwise
+// one thread = 8 channels of one output pixel; weights [KH, KW, C]
+__global__ void __launch_bounds__(256)
+dw_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, const void* __restrict__ bias,
+               int bias_f32, void* __restrict__ out, int N, int H, int W, int C, int KH, int KW, int sh, int sw,
+               int ph, int pw, int dh, int dw, int Ho, int Wo, int act, int out_f32) {
+  const int CG = C >> 3;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)N * Ho * Wo * CG;
+  if (gid >= total) return;
+  const int cg = gid % CG;
+  const int64_t pix = gid / CG;
+  const int wo = pix % Wo, ho = (pix / Wo) % Ho, n = pix / ((int64_t)Wo * Ho);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const uint16_t* xn = x + (int64_t)n * H * W * C + cg * 8;
+  for (int ky = 0; ky < KH; ++ky) {
+    const int hi = ho * sh - ph + ky * dh;
+    if (hi < 0 || hi >= H) continue;
+    for (int kx = 0; kx < KW; ++kx) {
+      const int wi = wo * sw - pw + kx * dw;
+      if (wi < 0 || wi >= W) continue;
+      float xv[8], wv[8];
+      unpack8(*(const u32x4_t*)(xn + ((int64_t)hi * W + wi) * C), xv);
+      unpack8(*(const u32x4_t*)(w + (ky * KW + kx) * C + cg * 8), wv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += xv[i] * wv[i];
+    }
+  }
+  if (bias) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      acc[i] += bias_f32 ? ((const float*)bias)[cg * 8 + i] : bf2f(((const uint16_t*)bias)[cg * 8 + i]);
+  }
+  apply_act_n<8>(acc, act);
+  if (out_f32) {
+    float* o = (float*)out + pix * C + cg * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = acc[i];
+  } else {
+    *(u32x4_t*)((uint16_t*)out + pix * C + cg * 8) = pack8(acc);
+  }
+}
+
+hipError_t conv2d_depthwise(const uint16_t* x, const uint16_t* w, const void* bias, int bias_f32, void* out, int N,
+                            int H, int W, int C, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw,
+                            int Ho, int Wo, int act, int out_f32, hipStream_t stream) {
+  const int64_t total = (int64_t)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(dw_conv_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, x, w, bias,
+                     bias_f32, out, N, H, W, C, KH, KW, sh, sw, ph, pw, dh, dw, Ho, Wo, act, out_f32);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- per-channel affine (+act/PReLU)
+__global__ void channel_affine_kernel(const uint16_t* __restrict__ x, const float* __restrict__ scale,
+                                      const float* __restrict__ shift, uint16_t* __restrict__ out, int64_t rows,
+                                      int C, int act, const uint16_t* __restrict__ prelu) {
+  const int CG = C >> 3;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= rows * CG) return;
+  const int cg = gid % CG;
+  float v[8];
+  unpack8(*(const u32x4_t*)(x + gid * 8), v);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = v[i] * scale[cg * 8 + i] + shift[cg * 8 + i];
+  apply_act_n<8>(v, act);
+  if (prelu) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float s = bf2f(prelu[cg * 8 + i]);
+      v[i] = v[i] > 0.f ? v[i] : v[i] * s;
+    }
+  }
+  *(u32x4_t*)(out + gid * 8) = pack8(v);
+}
+
+hipError_t channel_affine(const uint16_t* x, const float* scale, const float* shift, uint16_t* out, int64_t rows,
+                          int C, int act, const uint16_t* prelu, hipStream_t stream) {
+  const int64_t total = rows * (C / 8);
+  hipLaunchKernelGGL(channel_affine_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, x, scale,
+                     shift, out, rows, C, act, prelu);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- pooling
+__global__ void pool2d_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ out, int N, int H, int W, int C,
+                              int KH, int KW, int sh, int sw, int ph, int pw, int Ho, int Wo, int is_max) {
+  const int CG = C >> 3;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)N * Ho * Wo * CG;
+  if (gid >= total) return;
+  const int cg = gid % CG;
+  const int64_t pix = gid / CG;
+  const int wo = pix % Wo, ho = (pix / Wo) % Ho, n = pix / ((int64_t)Wo * Ho);
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = is_max ? -INFINITY : 0.f;
+  int cnt = 0;
+  for (int ky = 0; ky < KH; ++ky) {
+    const int hi = ho * sh - ph + ky;
+    if (hi < 0 || hi >= H) continue;
+    for (int kx = 0; kx < KW; ++kx) {
+      const int wi = wo * sw - pw + kx;
+      if (wi < 0 || wi >= W) continue;
+      float v[8];
+      unpack8(*(const u32x4_t*)(x + (((int64_t)n * H + hi) * W + wi) * C + cg * 8), v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = is_max ? fmaxf(acc[i], v[i]) : acc[i] + v[i];
+      ++cnt;
+    }
+  }
+  if (!is_max) {
+    const float inv = 1.f / (float)(KH * KW);  // count_include_pad=True (ONNX/PyTorch default)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] *= inv;
+  }
+  *(u32x4_t*)(out + pix * C + cg * 8) = pack8(acc);
+}
+
+hipError_t pool2d(const uint16_t* x, uint16_t* out, int N, int H, int W, int C, int KH, int KW, int sh, int sw, int ph,
+                  int pw, int Ho, int Wo, int is_max, hipStream_t stream) {
+  const int64_t total = (int64_t)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(pool2d_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, x, out, N, H, W, C,
+                     KH, KW, sh, sw, ph, pw, Ho, Wo, is_max);
+  return hipGetLastError();
+}
+
+// mean over HW per (n, c) -> f32 [N, C]; one block per (n, 256-channel group)
+__global__ void global_avgpool_kernel(const uint16_t* __restrict__ x, float* __restrict__ out, int HW, int C) {
+  const int n = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int part = threadIdx.x >> 6;  // 4 row-partitions
+  __shared__ float red[4][64];
+  float s = 0.f;
+  if (c < C) {
+    const uint16_t* xn = x + (int64_t)n * HW * C + c;
+    for (int p = part; p < HW; p += 4) s += bf2f(xn[(int64_t)p * C]);
+  }
+  red[part][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (part == 0 && c < C)
+    out[(int64_t)n * C + c] = (red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]) / HW;
+}
+
+hipError_t global_avgpool(const uint16_t* x, float* out, int N, int HW, int C, hipStream_t stream) {
+  hipLaunchKernelGGL(global_avgpool_kernel, dim3((C + 63) / 64, N), dim3(256), 0, stream, x, out, HW, C);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- FPN helpers
+// out[n, h, w, :] (pixel stride ldo) = x[n, h/f, w/f, :] (+ add[n, h, w, :])   nearest upsample
+__global__ void upsample_add_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ add,
+                                    uint16_t* __restrict__ out, int N, int H, int W, int C, int f, int64_t ldo) {
+  const int CG = C >> 3;
+  const int Ho = H * f, Wo = W * f;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (int64_t)N * Ho * Wo * CG) return;
+  const int cg = gid % CG;
+  const int64_t pix = gid / CG;
+  const int wo = pix % Wo, ho = (pix / Wo) % Ho, n = pix / ((int64_t)Wo * Ho);
+  float v[8];
+  unpack8(*(const u32x4_t*)(x + (((int64_t)n * H + ho / f) * W + wo / f) * C + cg * 8), v);
+  if (add) {
+    float a2[8];
+    unpack8(*(const u32x4_t*)(add + pix * C + cg * 8), a2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] += a2[i];
+  }
+  *(u32x4_t*)(out + pix * ldo + cg * 8) = pack8(v);
+}
+
+hipError_t upsample_add(const uint16_t* x, const uint16_t* add, uint16_t* out, int N, int H, int W, int C, int f,
+                        int64_t ldo, hipStream_t stream) {
+  const int64_t total = (int64_t)N * H * f * W * f * (C / 8);
+  hipLaunchKernelGGL(upsample_add_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, x, add, out,
+                     N, H, W, C, f, ldo);
+  return hipGetLastError();
+}
+
+// SE channel re-weighting: x[n, p, c] *= s[n, c]
+__global__ void channel_scale_kernel(uint16_t* __restrict__ x, const float* __restrict__ s, int HW, int C,
+                                     int64_t total) {
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= total) return;
+  const int CG = C >> 3;
+  const int cg = gid % CG;
+  const int64_t n = gid / ((int64_t)HW * CG);
+  float v[8];
+  unpack8(*(const u32x4_t*)(x + gid * 8), v);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] *= s[n * C + cg * 8 + i];
+  *(u32x4_t*)(x + gid * 8) = pack8(v);
+}
+
+hipError_t channel_scale(uint16_t* x, const float* s, int N, int HW, int C, hipStream_t stream) {
+  const int64_t total = (int64_t)N * HW * (C / 8);
+  hipLaunchKernelGGL(channel_scale_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, x, s, HW, C,
+                     total);
+  return hipGetLastError();
+}
+
+// ConvTranspose(k=f, s=f) as GEMM + depth-to-space: y [N, H, W, f*f*C] (GEMM output,
+// channel index (dy*f + dx)*C + c) -> out [N, H*f, W*f, C]
+__global__ void pixel_shuffle_kernel(const uint16_t* __restrict__ y, uint16_t* __restrict__ out, int N, int H, int W,
+                                     int C, int f) {
+  const int CG = C >> 3;
+  const int Ho = H * f, Wo = W * f;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (int64_t)N * Ho * Wo * CG) return;
+  const int cg = gid % CG;
+  const int64_t pix = gid / CG;
+  const int wo = pix % Wo, ho = (pix / Wo) % Ho, n = pix / ((int64_t)Wo * Ho);
+  const int h = ho / f, dy = ho % f, w = wo / f, dx = wo % f;
+  const uint16_t* src = y + (((int64_t)n * H + h) * W + w) * (f * f * C) + (dy * f + dx) * C + cg * 8;
+  *(u32x4_t*)(out + pix * C + cg * 8) = *(const u32x4_t*)src;
+}
+
+hipError_t pixel_shuffle_up(const uint16_t* y, uint16_t* out, int N, int H, int W, int C, int f, hipStream_t stream) {
+  const int64_t total = (int64_t)N * H * f * W * f * (C / 8);
+  hipLaunchKernelGGL(pixel_shuffle_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, y, out, N, H,
+                     W, C, f);
+  return hipGetLastError();
+}
+
+}  // namespace lumen

@@ -13,12 +13,10 @@
 
 #include <vector>
 
+#include "gemm_epi.h"
+#include "conv.h"
+
 namespace lumen {
-struct GemmEpi {
-  const void* bias; const uint16_t* residual; const uint16_t* table;
-  int64_t ldr; int64_t ldt; int table_period; int table_offset; int act; int bias_f32;
-  float alpha; int out_group; int64_t out_group_stride; int out_row_offset; int out_f32;
-};
 hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
                      int64_t ldc, int M, int N, int K, const GemmEpi& ep, int tile, hipStream_t stream);
 hipError_t norm_rows(const uint16_t* x, int64_t x_stride, const int64_t* row_idx, const uint16_t* add,
@@ -74,7 +72,8 @@ void check_bf16_rows(const at::Tensor& t, const char* name) {
 void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
           const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& table,
           int64_t table_period, int64_t table_offset, int64_t act, double alpha, at::Tensor out,
-          int64_t out_group, int64_t out_group_stride, int64_t out_row_offset, int64_t tile) {
+          int64_t out_group, int64_t out_group_stride, int64_t out_row_offset, int64_t tile,
+          const c10::optional<at::Tensor>& prelu) {
   check_bf16_rows(a, "a");
   check_bf16_rows(w, "w");
   const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
@@ -113,6 +112,10 @@ void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tens
   ep.out_group_stride = out_group_stride;
   ep.out_row_offset = (int)out_row_offset;
   ep.out_f32 = out.scalar_type() == at::kFloat;
+  if (prelu.has_value() && prelu->defined()) {
+    TORCH_CHECK(prelu->scalar_type() == at::kBFloat16 && prelu->numel() >= N && prelu->is_contiguous(), "gemm: prelu");
+    ep.prelu = bf(*prelu);
+  }
   const at::DeviceGuard guard(a.device());
   LUMEN_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
                                    (int)M, (int)N, (int)K, ep, (int)tile, cur_stream()));
@@ -269,12 +272,143 @@ void row_topk(const at::Tensor& scores, int64_t k, double scale, at::Tensor out_
                                   cur_stream()));
 }
 
+// ---------------------------------------------------------------- convolution / CNN support (NHWC)
+static int64_t pixel_stride(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1, name, ": NHWC 4-D with unit channel stride");
+  const int64_t ld = t.stride(2);
+  TORCH_CHECK(t.stride(1) == t.size(2) * ld && t.stride(0) == t.size(1) * t.stride(1), name,
+              ": pixels must be uniformly strided (channel-slice views allowed)");
+  TORCH_CHECK(ld % 8 == 0 && (reinterpret_cast<uintptr_t>(t.data_ptr()) % 16) == 0, name, ": 16-byte aligned pixels");
+  return ld;
+}
+
+void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+            const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& prelu, int64_t act,
+            std::vector<int64_t> stride, std::vector<int64_t> padding, std::vector<int64_t> dilation, at::Tensor out,
+            int64_t tile) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv2d: bf16");
+  const int64_t ldx = pixel_stride(x, "x");
+  TORCH_CHECK(w.dim() == 4 && w.is_contiguous(), "conv2d: w [Cout, KH, KW, Cin] contiguous");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3);
+  const int64_t Cout = w.size(0), KH = w.size(1), KW = w.size(2);
+  TORCH_CHECK(w.size(3) == Cin && Cin % 8 == 0, "conv2d: Cin mismatch or not a multiple of 8");
+  TORCH_CHECK(Cout % 16 == 0, "conv2d: Cout must be a multiple of 16");
+  TORCH_CHECK(stride.size() == 2 && padding.size() == 2 && dilation.size() == 2, "conv2d: 2-D params");
+  const int64_t Ho = (H + 2 * padding[0] - dilation[0] * (KH - 1) - 1) / stride[0] + 1;
+  const int64_t Wo = (W + 2 * padding[1] - dilation[1] * (KW - 1) - 1) / stride[1] + 1;
+  const int64_t ldo = pixel_stride(out, "out");
+  TORCH_CHECK(out.size(0) == N && out.size(1) == Ho && out.size(2) == Wo && out.size(3) == Cout, "conv2d: out shape");
+  lumen::GemmEpi ep{};
+  ep.alpha = 1.f;
+  ep.act = (int)act;
+  ep.out_f32 = out.scalar_type() == at::kFloat;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->numel() == Cout && bias->is_contiguous(), "conv2d: bias");
+    ep.bias = bias->data_ptr();
+    ep.bias_f32 = bias->scalar_type() == at::kFloat;
+  }
+  if (residual.has_value() && residual->defined()) {
+    ep.ldr = pixel_stride(*residual, "residual");
+    ep.residual = bf(*residual);
+  }
+  if (prelu.has_value() && prelu->defined()) {
+    TORCH_CHECK(prelu->scalar_type() == at::kBFloat16 && prelu->numel() == Cout, "conv2d: prelu");
+    ep.prelu = bf(*prelu);
+  }
+  lumen::ConvArgs a{};
+  a.x = bf(x); a.w = bf(w); a.out = out.data_ptr(); a.ldx = ldx; a.ldo = ldo;
+  a.N = (int)N; a.H = (int)H; a.W = (int)W; a.Cin = (int)Cin; a.Cout = (int)Cout; a.KH = (int)KH; a.KW = (int)KW;
+  a.sh = (int)stride[0]; a.sw = (int)stride[1]; a.ph = (int)padding[0]; a.pw = (int)padding[1];
+  a.dh = (int)dilation[0]; a.dw = (int)dilation[1]; a.Ho = (int)Ho; a.Wo = (int)Wo;
+  const at::DeviceGuard guard(x.device());
+  LUMEN_CHECK_HIP(lumen::conv2d_igemm(a, ep, (int)tile, cur_stream()));
+}
+
+void conv2d_dw(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t act,
+               std::vector<int64_t> stride, std::vector<int64_t> padding, std::vector<int64_t> dilation,
+               at::Tensor out) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.is_contiguous() && x.dim() == 4 && x.scalar_type() == at::kBFloat16, "conv2d_dw: x NHWC contiguous");
+  TORCH_CHECK(w.is_contiguous() && w.dim() == 3, "conv2d_dw: w [KH, KW, C]");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && w.size(2) == C, "conv2d_dw: C % 8 / mismatch");
+  TORCH_CHECK(out.is_contiguous() && out.dim() == 4 && out.size(3) == C, "conv2d_dw: out");
+  const void* bp = nullptr; int bf32 = 0;
+  if (bias.has_value() && bias->defined()) { bp = bias->data_ptr(); bf32 = bias->scalar_type() == at::kFloat; }
+  const at::DeviceGuard guard(x.device());
+  LUMEN_CHECK_HIP(lumen::conv2d_depthwise(bf(x), bf(w), bp, bf32, out.data_ptr(), (int)N, (int)H, (int)W, (int)C,
+                                          (int)w.size(0), (int)w.size(1), (int)stride[0], (int)stride[1],
+                                          (int)padding[0], (int)padding[1], (int)dilation[0], (int)dilation[1],
+                                          (int)out.size(1), (int)out.size(2), (int)act,
+                                          out.scalar_type() == at::kFloat, cur_stream()));
+}
+
+void channel_affine(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift, at::Tensor out,
+                    int64_t act, const c10::optional<at::Tensor>& prelu) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.scalar_type() == at::kBFloat16, "channel_affine: x/out");
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(C % 8 == 0 && scale.numel() == C && shift.numel() == C && scale.scalar_type() == at::kFloat, "channel_affine: C");
+  const uint16_t* pp = nullptr;
+  if (prelu.has_value() && prelu->defined()) pp = bf(*prelu);
+  const at::DeviceGuard guard(x.device());
+  LUMEN_CHECK_HIP(lumen::channel_affine(bf(x), scale.data_ptr<float>(), shift.data_ptr<float>(), bfm(out),
+                                        x.numel() / C, (int)C, (int)act, pp, cur_stream()));
+}
+
+void pool2d(const at::Tensor& x, at::Tensor out, std::vector<int64_t> kernel, std::vector<int64_t> stride,
+            std::vector<int64_t> padding, bool is_max) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.dim() == 4 && x.size(3) % 8 == 0, "pool2d: NHWC");
+  const at::DeviceGuard guard(x.device());
+  LUMEN_CHECK_HIP(lumen::pool2d(bf(x), bfm(out), (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3),
+                                (int)kernel[0], (int)kernel[1], (int)stride[0], (int)stride[1], (int)padding[0],
+                                (int)padding[1], (int)out.size(1), (int)out.size(2), is_max ? 1 : 0, cur_stream()));
+}
+
+void global_avgpool(const at::Tensor& x, at::Tensor out) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.is_contiguous() && x.dim() == 4 && out.scalar_type() == at::kFloat, "global_avgpool");
+  const at::DeviceGuard guard(x.device());
+  LUMEN_CHECK_HIP(lumen::global_avgpool(bf(x), out.data_ptr<float>(), (int)x.size(0), (int)(x.size(1) * x.size(2)),
+                                        (int)x.size(3), cur_stream()));
+}
+
+void upsample_add(const at::Tensor& x, const c10::optional<at::Tensor>& add, at::Tensor out, int64_t factor) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.is_contiguous() && x.dim() == 4 && x.size(3) % 8 == 0, "upsample_add: x");
+  const int64_t ldo = pixel_stride(out, "out");
+  const uint16_t* ap = nullptr;
+  if (add.has_value() && add->defined()) { TORCH_CHECK(add->is_contiguous()); ap = bf(*add); }
+  const at::DeviceGuard guard(x.device());
+  LUMEN_CHECK_HIP(lumen::upsample_add(bf(x), ap, bfm(out), (int)x.size(0), (int)x.size(1), (int)x.size(2),
+                                      (int)x.size(3), (int)factor, ldo, cur_stream()));
+}
+
+void channel_scale_(at::Tensor x, const at::Tensor& s) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.is_contiguous() && x.dim() == 4 && s.scalar_type() == at::kFloat, "channel_scale_");
+  const at::DeviceGuard guard(x.device());
+  LUMEN_CHECK_HIP(lumen::channel_scale(bfm(x), s.data_ptr<float>(), (int)x.size(0), (int)(x.size(1) * x.size(2)),
+                                       (int)x.size(3), cur_stream()));
+}
+
+void pixel_shuffle_up(const at::Tensor& y, at::Tensor out, int64_t factor) {
+  check_gpu(y, "y");
+  TORCH_CHECK(y.is_contiguous() && out.is_contiguous(), "pixel_shuffle_up");
+  const int64_t C = out.size(3);
+  const at::DeviceGuard guard(y.device());
+  LUMEN_CHECK_HIP(lumen::pixel_shuffle_up(bf(y), bfm(out), (int)y.size(0), (int)y.size(1), (int)y.size(2), (int)C,
+                                          (int)factor, cur_stream()));
+}
+
 }  // namespace
 
 TORCH_LIBRARY(lumen, m) {
   m.def("gemm(Tensor a, Tensor w, Tensor? bias, Tensor? residual, Tensor? table, int table_period, "
         "int table_offset, int act, float alpha, Tensor(o!) out, int out_group, int out_group_stride, "
-        "int out_row_offset, int tile) -> ()");
+        "int out_row_offset, int tile, Tensor? prelu=None) -> ()");
   m.def("norm(Tensor x, Tensor? row_idx, Tensor? add, Tensor(r!)? resid_out, Tensor w, Tensor? b, "
         "Tensor(o!) out, float eps, int mode) -> ()");
   m.def("l2norm_(Tensor(a!) x, float eps) -> ()");
@@ -286,6 +420,16 @@ TORCH_LIBRARY(lumen, m) {
         "int max_ch, int max_dw) -> ()");
   m.def("row_topk(Tensor scores, int k, float scale, Tensor(v!) out_v, Tensor(i!) out_i, Tensor(l!)? out_lse, "
         "int index_offset) -> ()");
+  m.def("conv2d(Tensor x, Tensor w, Tensor? bias, Tensor? residual, Tensor? prelu, int act, int[] stride, "
+        "int[] padding, int[] dilation, Tensor(o!) out, int tile) -> ()");
+  m.def("conv2d_dw(Tensor x, Tensor w, Tensor? bias, int act, int[] stride, int[] padding, int[] dilation, "
+        "Tensor(o!) out) -> ()");
+  m.def("channel_affine(Tensor x, Tensor scale, Tensor shift, Tensor(o!) out, int act, Tensor? prelu) -> ()");
+  m.def("pool2d(Tensor x, Tensor(o!) out, int[] kernel, int[] stride, int[] padding, bool is_max) -> ()");
+  m.def("global_avgpool(Tensor x, Tensor(o!) out) -> ()");
+  m.def("upsample_add(Tensor x, Tensor? add, Tensor(o!) out, int factor) -> ()");
+  m.def("channel_scale_(Tensor(a!) x, Tensor s) -> ()");
+  m.def("pixel_shuffle_up(Tensor y, Tensor(o!) out, int factor) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
@@ -297,4 +441,12 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("attention", &attention);
   m.impl("image_prep", &image_prep2);
   m.impl("row_topk", &row_topk);
+  m.impl("conv2d", &conv2d);
+  m.impl("conv2d_dw", &conv2d_dw);
+  m.impl("channel_affine", &channel_affine);
+  m.impl("pool2d", &pool2d);
+  m.impl("global_avgpool", &global_avgpool);
+  m.impl("upsample_add", &upsample_add);
+  m.impl("channel_scale_", &channel_scale_);
+  m.impl("pixel_shuffle_up", &pixel_shuffle_up);
 }

@@ -1,0 +1,153 @@
+"""CNN ops on NHWC activations (HIP kernels on GPU, PyTorch fp32 reference on CPU).
+
+Layout conventions: activations are NHWC ``[N, H, W, C]`` (C a multiple of 8 on the
+GPU path, 16-byte channel vectors); dense conv weights are ``[Cout, KH, KW, Cin]``
+(K-contiguous, the implicit-GEMM B operand); depthwise weights are ``[KH, KW, C]``.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .._native import hip_ops
+from . import _act_ref, act_id
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+def conv_out_hw(H, W, KH, KW, stride, padding, dilation):
+    s, p, d = _pair(stride), _pair(padding), _pair(dilation)
+    return ((H + 2 * p[0] - d[0] * (KH - 1) - 1) // s[0] + 1, (W + 2 * p[1] - d[1] * (KW - 1) - 1) // s[1] + 1)
+
+
+def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride=1, padding=0, dilation=1,
+           act=None, residual: Optional[torch.Tensor] = None, prelu: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None, out_dtype=None, tile: int = -1) -> torch.Tensor:
+    """out = prelu(act(conv(x, w) + bias)) + residual   (NHWC; w [Cout, KH, KW, Cin])."""
+    N, H, W, Cin = x.shape
+    Cout, KH, KW, _ = w.shape
+    Ho, Wo = conv_out_hw(H, W, KH, KW, stride, padding, dilation)
+    if out is None:
+        out = torch.empty((N, Ho, Wo, Cout), device=x.device, dtype=out_dtype or x.dtype)
+    a = act_id(act)
+    if x.is_cuda:
+        hip_ops().conv2d(x, w, bias, residual, prelu, a, list(_pair(stride)), list(_pair(padding)),
+                         list(_pair(dilation)), out, int(tile))
+        return out
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, _pair(stride), _pair(padding),
+                 _pair(dilation)).permute(0, 2, 3, 1)
+    if bias is not None:
+        y = y + bias.float()
+    y = _act_ref(y, a)
+    if prelu is not None:
+        y = torch.where(y > 0, y, y * prelu.float())
+    if residual is not None:
+        y = y + residual.float()
+    out.copy_(y.to(out.dtype))
+    return out
+
+
+def conv2d_dw(x, w, bias=None, stride=1, padding=0, dilation=1, act=None, out=None):
+    """Depthwise conv, NHWC; w [KH, KW, C]."""
+    N, H, W, C = x.shape
+    KH, KW, _ = w.shape
+    Ho, Wo = conv_out_hw(H, W, KH, KW, stride, padding, dilation)
+    if out is None:
+        out = torch.empty((N, Ho, Wo, C), device=x.device, dtype=x.dtype)
+    a = act_id(act)
+    if x.is_cuda:
+        hip_ops().conv2d_dw(x.contiguous(), w.contiguous(), bias, a, list(_pair(stride)), list(_pair(padding)),
+                            list(_pair(dilation)), out)
+        return out
+    wt = w.float().permute(2, 0, 1).unsqueeze(1)  # [C, 1, KH, KW]
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), wt, None, _pair(stride), _pair(padding), _pair(dilation), groups=C)
+    y = y.permute(0, 2, 3, 1)
+    if bias is not None:
+        y = y + bias.float()
+    out.copy_(_act_ref(y, a).to(out.dtype))
+    return out
+
+
+def channel_affine(x, scale, shift, act=None, prelu=None, out=None):
+    """y = x * scale[c] + shift[c] (-> act -> PReLU) — un-foldable BatchNorm (pre-conv BN)."""
+    if out is None:
+        out = torch.empty_like(x)
+    a = act_id(act)
+    if x.is_cuda:
+        hip_ops().channel_affine(x.contiguous(), scale.float().contiguous(), shift.float().contiguous(), out, a, prelu)
+        return out
+    y = _act_ref(x.float() * scale.float() + shift.float(), a)
+    if prelu is not None:
+        y = torch.where(y > 0, y, y * prelu.float())
+    out.copy_(y.to(out.dtype))
+    return out
+
+
+def pool2d(x, kernel, stride, padding=0, is_max=True):
+    N, H, W, C = x.shape
+    k, s, p = _pair(kernel), _pair(stride), _pair(padding)
+    Ho, Wo = (H + 2 * p[0] - k[0]) // s[0] + 1, (W + 2 * p[1] - k[1]) // s[1] + 1
+    if x.is_cuda:
+        out = torch.empty((N, Ho, Wo, C), device=x.device, dtype=x.dtype)
+        hip_ops().pool2d(x.contiguous(), out, list(k), list(s), list(p), bool(is_max))
+        return out
+    xn = x.float().permute(0, 3, 1, 2)
+    y = F.max_pool2d(xn, k, s, p) if is_max else F.avg_pool2d(xn, k, s, p, count_include_pad=True)
+    return y.permute(0, 2, 3, 1).to(x.dtype).contiguous()
+
+
+def global_avgpool(x) -> torch.Tensor:
+    """NHWC -> fp32 [N, C]."""
+    if x.is_cuda:
+        out = torch.empty((x.shape[0], x.shape[3]), device=x.device, dtype=torch.float32)
+        hip_ops().global_avgpool(x.contiguous(), out)
+        return out
+    return x.float().mean(dim=(1, 2))
+
+
+def upsample_add(x, add=None, factor=2, out=None):
+    """nearest-upsample x by ``factor`` (+ add) -> out (may be a channel slice of a concat buffer)."""
+    N, H, W, C = x.shape
+    if out is None:
+        out = torch.empty((N, H * factor, W * factor, C), device=x.device, dtype=x.dtype)
+    if x.is_cuda:
+        hip_ops().upsample_add(x.contiguous(), add, out, int(factor))
+        return out
+    y = x.float().repeat_interleave(factor, 1).repeat_interleave(factor, 2)
+    if add is not None:
+        y = y + add.float()
+    out.copy_(y.to(out.dtype))
+    return out
+
+
+def channel_scale_(x, s):
+    """SE re-weighting in place: x[n, h, w, c] *= s[n, c] (s fp32 [N, C])."""
+    if x.is_cuda:
+        hip_ops().channel_scale_(x, s.float().contiguous())
+        return x
+    x.copy_((x.float() * s.float()[:, None, None, :]).to(x.dtype))
+    return x
+
+
+def pixel_shuffle_up(y, C, factor=2):
+    """[N, H, W, f*f*C] (ConvTranspose-as-GEMM output) -> [N, H*f, W*f, C]."""
+    N, H, W, _ = y.shape
+    out = torch.empty((N, H * factor, W * factor, C), device=y.device, dtype=y.dtype)
+    if y.is_cuda:
+        hip_ops().pixel_shuffle_up(y.contiguous(), out, int(factor))
+        return out
+    t = y.reshape(N, H, W, factor, factor, C).permute(0, 1, 3, 2, 4, 5).reshape(N, H * factor, W * factor, C)
+    out.copy_(t)
+    return out
+
+
+def conv_weight_from_torch(w: torch.Tensor, cin_pad: Optional[int] = None) -> torch.Tensor:
+    """[Cout, Cin, KH, KW] -> [Cout, KH, KW, Cin(_pad)] (zero-padded input channels)."""
+    wt = w.permute(0, 2, 3, 1).contiguous()
+    if cin_pad is not None and cin_pad > wt.shape[3]:
+        wt = F.pad(wt, (0, cin_pad - wt.shape[3]))
+    return wt.contiguous()

@@ -1,0 +1,73 @@
+"""Implicit-GEMM conv / depthwise / pooling / FPN kernels vs the PyTorch fp32 reference."""
+import pytest
+import torch
+
+from lumen_amd.ops import cnn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-6)).item()
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,K,s,p,d", [
+    (2, 33, 31, 8, 16, 3, 1, 1, 1), (1, 64, 64, 32, 64, 3, 2, 1, 1), (2, 20, 20, 64, 128, 1, 1, 0, 1),
+    (1, 17, 19, 16, 32, 5, 1, 2, 1), (1, 40, 40, 24, 48, 3, 1, 2, 2), (3, 28, 28, 128, 256, 3, 2, 1, 1),
+    (1, 112, 112, 8, 64, 3, 1, 1, 1), (2, 7, 7, 512, 512, 3, 1, 1, 1)])
+@pytest.mark.parametrize("tile", [-1, 0, 1, 2])
+def test_conv2d(N, H, W, Cin, Cout, K, s, p, d, tile):
+    g = torch.Generator().manual_seed(H * Cin + K)
+    x = torch.randn(N, H, W, Cin, generator=g).bfloat16()
+    w = (torch.randn(Cout, K, K, Cin, generator=g) * (K * K * Cin) ** -0.5).bfloat16()
+    b = torch.randn(Cout, generator=g).bfloat16()
+    pr = (torch.rand(Cout, generator=g) * 0.3).bfloat16()
+    ref = cnn.conv2d(x, w, b, s, p, d, act=None, prelu=pr)
+    got = cnn.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), s, p, d, prelu=pr.to(DEV), tile=tile)
+    assert got.shape == ref.shape
+    assert _rel(got, ref) < 1e-2
+    r = torch.randn(*ref.shape, generator=g).bfloat16()
+    ref2 = cnn.conv2d(x, w, b, s, p, d, act="relu", residual=r)
+    got2 = cnn.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), s, p, d, act="relu", residual=r.to(DEV), tile=tile)
+    assert _rel(got2, ref2) < 1e-2
+
+
+def test_conv2d_into_channel_slice():
+    x = torch.randn(1, 16, 16, 32).bfloat16()
+    w = (torch.randn(16, 3, 3, 32) * 0.05).bfloat16()
+    big = torch.zeros(1, 16, 16, 64, device=DEV).bfloat16()
+    cnn.conv2d(x.to(DEV), w.to(DEV), None, 1, 1, out=big[..., 16:32])
+    ref = cnn.conv2d(x, w, None, 1, 1)
+    assert _rel(big[..., 16:32], ref) < 1e-2
+    assert big[..., :16].abs().max().item() == 0 and big[..., 32:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("C,K,s", [(16, 3, 1), (64, 3, 2), (128, 5, 1), (24, 3, 1)])
+def test_depthwise(C, K, s):
+    x = torch.randn(2, 30, 26, C).bfloat16()
+    w = torch.randn(K, K, C).bfloat16() * 0.2
+    b = torch.randn(C).bfloat16()
+    ref = cnn.conv2d_dw(x, w, b, s, K // 2, act="hardswish")
+    got = cnn.conv2d_dw(x.to(DEV), w.to(DEV), b.to(DEV), s, K // 2, act="hardswish")
+    assert _rel(got, ref) < 1e-2
+
+
+def test_pool_affine_upsample_scale_shuffle():
+    x = torch.randn(2, 17, 15, 32).bfloat16()
+    for mx in (True, False):
+        assert _rel(cnn.pool2d(x.to(DEV), 3, 2, 1, mx), cnn.pool2d(x, 3, 2, 1, mx)) < 1e-2
+    assert _rel(cnn.global_avgpool(x.to(DEV)), cnn.global_avgpool(x)) < 1e-3
+    sc, sh = torch.rand(32) + 0.5, torch.randn(32)
+    pr = torch.rand(32).bfloat16()
+    assert _rel(cnn.channel_affine(x.to(DEV), sc.to(DEV), sh.to(DEV), prelu=pr.to(DEV)),
+                cnn.channel_affine(x, sc, sh, prelu=pr)) < 1e-2
+    add = torch.randn(2, 34, 30, 32).bfloat16()
+    assert _rel(cnn.upsample_add(x.to(DEV), add.to(DEV), 2), cnn.upsample_add(x, add, 2)) < 1e-2
+    s = torch.rand(2, 32)
+    a = x.clone()
+    b = x.to(DEV)
+    assert _rel(cnn.channel_scale_(b, s.to(DEV)), cnn.channel_scale_(a, s)) < 1e-2
+    y = torch.randn(2, 5, 6, 4 * 16).bfloat16()
+    assert torch.equal(cnn.pixel_shuffle_up(y.to(DEV), 16, 2).cpu(), cnn.pixel_shuffle_up(y, 16, 2))
