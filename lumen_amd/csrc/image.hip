@@ -168,6 +168,15 @@ __global__ void prep_v_kernel(PrepArgs a) {
     for (int k = 0; k < 3; ++k) idx[k] = (((int64_t)b * 3 + k) * a.OH + oy) * a.OW + ox;
   } else if (a.layout == 1) {
     for (int k = 0; k < 3; ++k) idx[k] = (((int64_t)b * a.OH + oy) * a.OW + ox) * 3 + k;
+  } else if (a.layout == 3) {  // NHWC with channels padded to 8 (implicit-GEMM conv input, Cin % 8 == 0)
+    const int64_t base = (((int64_t)b * a.OH + oy) * a.OW + ox) * 8;
+    for (int k = 0; k < 3; ++k) idx[k] = base + k;
+    if (a.out_bf16) {
+      u32x4_t z = (u32x4_t){0u, 0u, 0u, 0u};
+      *(u32x4_t*)((uint16_t*)a.out + base) = z;  // zero the pad lanes first (same thread writes 0..2 below)
+    } else {
+      for (int k = 3; k < 8; ++k) ((float*)a.out)[base + k] = 0.f;
+    }
   } else {
     const int p = a.patch, gw = a.OW / p;
     const int64_t prow = (int64_t)b * (a.OH / p) * gw + (oy / p) * gw + (ox / p);

@@ -242,7 +242,7 @@ void image_prep2(const at::Tensor& src, const at::Tensor& geom, at::Tensor out, 
     TORCH_CHECK(kpad >= 3 * patch * patch, "image_prep: kpad");
     TORCH_CHECK(out.numel() == B * (out_h / patch) * (out_w / patch) * kpad, "image_prep: patch out size");
   } else {
-    TORCH_CHECK(out.numel() == B * 3 * out_h * out_w, "image_prep: out size");
+    TORCH_CHECK(out.numel() == B * (layout == 3 ? 8 : 3) * out_h * out_w, "image_prep: out size");
   }
   a.filter = (int)filter; a.swap_rb = swap_rb ? 1 : 0;
   for (int i = 0; i < 3; ++i) { a.mean[i] = (float)mean[i]; a.inv_std[i] = (float)(1.0 / std_[i]); }

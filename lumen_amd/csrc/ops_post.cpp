@@ -1,0 +1,122 @@
+// torch.ops.lumen.* registration of the detection / recognition post-processing
+// kernels (postproc.hip): anchor/prior decode, NMS, batched affine/perspective
+// warps into recogniser batches, CTC greedy decode.
+#include <ATen/ATen.h>
+#include <ATen/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+#include <torch/library.h>
+
+namespace lumen {
+struct DetDecodeArgs {
+  const float* scores; const float* bbox; const float* kps; const float* priors;
+  int N, H, W, A, stride; int P; float thresh; const float* img_scale; const float* img_hw;
+  float min_size, max_size; float var0, var1; float in_w, in_h; float* cand; int* count; int max_cand;
+  int64_t sN, sL; int apply_sigmoid;
+};
+hipError_t det_decode(const DetDecodeArgs& a, hipStream_t stream);
+hipError_t nms(const float* cand, const int* count, int N, int max_cand, float iou_thr, int max_out, int* keep,
+               int* keep_n, hipStream_t stream);
+struct WarpArgs {
+  const uint8_t* src; const int64_t* meta; const float* minv; uint16_t* out; int F, OH, OW, cpad;
+  float scale, mean, inv_std; int swap_rb; int cubic;
+};
+hipError_t warp_batch(const WarpArgs& a, hipStream_t stream);
+hipError_t ctc_greedy(const float* probs, int B, int T, int C, int blank, int* tmp_idx, float* tmp_conf,
+                      int* out_ids, int* out_len, float* out_conf, hipStream_t stream);
+}  // namespace lumen
+
+namespace {
+
+#define CHECK_HIP2(expr)                                                                   \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    TORCH_CHECK(_e == hipSuccess, "lumen HIP error: ", hipGetErrorString(_e), " @ ", #expr); \
+  } while (0)
+
+inline hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void f32c(const at::Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), n, ": f32 contiguous GPU tensor");
+}
+
+// scores [N, P], bbox [N, P, 4], kps [N, P, 10]?; priors [P, 4]? ; cand [N, max_cand, 16]; count [N] (int32, zeroed)
+void det_decode(const at::Tensor& scores, const at::Tensor& bbox, const c10::optional<at::Tensor>& kps,
+                const c10::optional<at::Tensor>& priors, int64_t H, int64_t W, int64_t A, int64_t stride_,
+                double thresh, const at::Tensor& img_scale, const at::Tensor& img_hw, double min_size,
+                double max_size, double var0, double var1, double in_w, double in_h, at::Tensor cand,
+                at::Tensor count, int64_t P, int64_t sN, int64_t sL, bool apply_sigmoid) {
+  f32c(img_scale, "img_scale"); f32c(img_scale, "img_scale"); f32c(img_hw, "img_hw"); f32c(cand, "cand");
+  TORCH_CHECK(count.scalar_type() == at::kInt && count.is_contiguous(), "count int32");
+  lumen::DetDecodeArgs a{};
+  TORCH_CHECK(scores.is_cuda() && scores.scalar_type() == at::kFloat && bbox.scalar_type() == at::kFloat, "f32 GPU");
+  a.scores = scores.data_ptr<float>(); a.bbox = bbox.data_ptr<float>();
+  if (kps.has_value() && kps->defined()) a.kps = kps->data_ptr<float>();
+  if (priors.has_value() && priors->defined()) { f32c(*priors, "priors"); a.priors = priors->data_ptr<float>(); }
+  a.N = (int)img_scale.size(0); a.P = (int)P;
+  a.sN = sN; a.sL = sL; a.apply_sigmoid = apply_sigmoid ? 1 : 0;
+  a.H = (int)H; a.W = (int)W; a.A = (int)A; a.stride = (int)stride_;
+  a.thresh = (float)thresh; a.img_scale = img_scale.data_ptr<float>(); a.img_hw = img_hw.data_ptr<float>();
+  a.min_size = (float)min_size; a.max_size = (float)max_size; a.var0 = (float)var0; a.var1 = (float)var1;
+  a.in_w = (float)in_w; a.in_h = (float)in_h;
+  a.cand = cand.data_ptr<float>(); a.count = count.data_ptr<int>(); a.max_cand = (int)cand.size(1);
+  TORCH_CHECK(cand.size(2) == 16 && cand.size(0) == a.N, "cand [N, max_cand, 16]");
+  const at::DeviceGuard g(scores.device());
+  CHECK_HIP2(lumen::det_decode(a, stream()));
+}
+
+void nms(const at::Tensor& cand, const at::Tensor& count, double iou_thr, at::Tensor keep, at::Tensor keep_n) {
+  f32c(cand, "cand");
+  TORCH_CHECK(cand.size(1) <= 1024, "nms: at most 1024 candidates per image");
+  TORCH_CHECK(keep.scalar_type() == at::kInt && keep_n.scalar_type() == at::kInt, "nms: int32 outputs");
+  const at::DeviceGuard g(cand.device());
+  CHECK_HIP2(lumen::nms(cand.data_ptr<float>(), count.data_ptr<int>(), (int)cand.size(0), (int)cand.size(1),
+                        (float)iou_thr, (int)keep.size(1), keep.data_ptr<int>(), keep_n.data_ptr<int>(), stream()));
+}
+
+// src flat uint8; meta int64 [F, 4] (offset, h, w, out_w); minv f32 [F, 9]; out bf16 [F, OH, OW, cpad]
+void warp_batch(const at::Tensor& src, const at::Tensor& meta, const at::Tensor& minv, at::Tensor out, double scale,
+                double mean, double std_, bool swap_rb, bool cubic) {
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte, "warp: uint8 src");
+  TORCH_CHECK(meta.is_cuda() && meta.scalar_type() == at::kLong && meta.is_contiguous() && meta.size(1) == 4, "meta");
+  f32c(minv, "minv");
+  TORCH_CHECK(out.is_contiguous() && out.scalar_type() == at::kBFloat16 && out.dim() == 4, "warp: out bf16 [F,H,W,C]");
+  lumen::WarpArgs a{};
+  a.src = src.data_ptr<uint8_t>(); a.meta = meta.data_ptr<int64_t>(); a.minv = minv.data_ptr<float>();
+  a.out = reinterpret_cast<uint16_t*>(out.data_ptr());
+  a.F = (int)out.size(0); a.OH = (int)out.size(1); a.OW = (int)out.size(2); a.cpad = (int)out.size(3);
+  a.scale = (float)scale; a.mean = (float)mean; a.inv_std = (float)(1.0 / std_);
+  a.swap_rb = swap_rb ? 1 : 0; a.cubic = cubic ? 1 : 0;
+  const at::DeviceGuard g(src.device());
+  CHECK_HIP2(lumen::warp_batch(a, stream()));
+}
+
+void ctc_greedy(const at::Tensor& probs, int64_t blank, at::Tensor out_ids, at::Tensor out_len, at::Tensor out_conf) {
+  f32c(probs, "probs");
+  const int B = (int)probs.size(0), T = (int)probs.size(1), C = (int)probs.size(2);
+  auto idx = at::empty({B, T}, probs.options().dtype(at::kInt));
+  auto conf = at::empty({B, T}, probs.options());
+  const at::DeviceGuard g(probs.device());
+  CHECK_HIP2(lumen::ctc_greedy(probs.data_ptr<float>(), B, T, C, (int)blank, idx.data_ptr<int>(),
+                               conf.data_ptr<float>(), out_ids.data_ptr<int>(), out_len.data_ptr<int>(),
+                               out_conf.data_ptr<float>(), stream()));
+}
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(lumen, m) {
+  m.def("det_decode(Tensor scores, Tensor bbox, Tensor? kps, Tensor? priors, int H, int W, int A, int stride, "
+        "float thresh, Tensor img_scale, Tensor img_hw, float min_size, float max_size, float var0, float var1, "
+        "float in_w, float in_h, Tensor(c!) cand, Tensor(n!) count, int P, int sN, int sL, bool apply_sigmoid) -> ()");
+  m.def("nms(Tensor cand, Tensor count, float iou_thr, Tensor(k!) keep, Tensor(n!) keep_n) -> ()");
+  m.def("warp_batch(Tensor src, Tensor meta, Tensor minv, Tensor(o!) out, float scale, float mean, float std, "
+        "bool swap_rb, bool cubic) -> ()");
+  m.def("ctc_greedy(Tensor probs, int blank, Tensor(i!) out_ids, Tensor(l!) out_len, Tensor(c!) out_conf) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
+  m.impl("det_decode", &det_decode);
+  m.impl("nms", &nms);
+  m.impl("warp_batch", &warp_batch);
+  m.impl("ctc_greedy", &ctc_greedy);
+}

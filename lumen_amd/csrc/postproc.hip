@@ -1,0 +1,315 @@
+// Detection / recognition post-processing kernels.
+//
+//  * det_decode: SCRFD-style anchor decode of one FPN stride, fused with the
+//    score threshold, distance2bbox / distance2kps, un-letterbox rescale, clip
+//    and face-size filter; survivors are appended to a per-image candidate list
+//    through an atomic counter (reference face onnxrt_backend.py:425-468,
+//    882-1153, 1208-1259; SURVEY F-3/F-5).  Also decodes RetinaFace-style
+//    prior-box outputs (F-4: centre/size regression with variances).
+//  * nms: per-image greedy NMS on the candidate list (one workgroup per image:
+//    bitonic sort by score in LDS, then the kept set is swept in score order
+//    with a block-parallel IoU suppression per kept box; reference _nms
+//    onnxrt_backend.py:391-422).
+//  * warp_affine_batch: bilinear warpAffine (cv2 INTER_LINEAR, constant-0
+//    border) of every detected face into the 112x112 recogniser batch, fused
+//    with RGB->BGR and (x/255 - 0.5)/0.5 (F-7/F-8), and the same kernel with a
+//    3x3 matrix for OCR perspective crops into the padded recogniser batch (O-5/O-6).
+//  * ctc_greedy: per (sequence, timestep) arg-max over the class axis and the
+//    blank/repeat collapse with the mean confidence (O-8).
+#include "common.h"
+
+namespace lumen {
+
+struct DetDecodeArgs {
+  const float* scores;   // [N, H*W*A]           (already sigmoid'ed) — or [N, P] priors mode
+  const float* bbox;     // [N, H*W*A, 4]        distances (in stride units) or prior deltas
+  const float* kps;      // [N, H*W*A, 10] or null
+  const float* priors;   // [P, 4] (cx, cy, w, h) normalised, RetinaFace mode; null = SCRFD anchors
+  int N, H, W, A, stride;
+  int P;                 // candidates per image in this level
+  float thresh;
+  const float* img_scale;  // [N] letterbox scale (det size / original)
+  const float* img_hw;     // [N, 2] original (h, w)
+  float min_size, max_size;
+  float var0, var1;        // RetinaFace variances
+  float in_w, in_h;        // network input size (priors mode)
+  float* cand;             // [N, max_cand, 16]: x1 y1 x2 y2 score kps*10 pad
+  int* count;              // [N]
+  int max_cand;
+  // generalised addressing (fused head conv outputs, NHWC): element (n, loc, a, j) of
+  // scores/bbox/kps lives at base + n*sN + loc*sL + a*{1,4,10} + j
+  int64_t sN, sL;
+  int apply_sigmoid;
+};
+
+__global__ void det_decode_kernel(DetDecodeArgs a) {
+  const int n = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.P) return;
+  const int loc_i = i / a.A, anc = i % a.A;
+  const bool strided = a.sL > 0;
+  float s = strided ? a.scores[n * a.sN + loc_i * a.sL + anc] : a.scores[(int64_t)n * a.P + i];
+  if (a.apply_sigmoid) s = 1.f / (1.f + __expf(-s));
+  if (!(s >= a.thresh)) return;
+  const float* bb = strided ? a.bbox + n * a.sN + loc_i * a.sL + anc * 4 : a.bbox + ((int64_t)n * a.P + i) * 4;
+  float x1, y1, x2, y2, cx, cy, pw = 0.f, ph = 0.f;
+  if (a.priors == nullptr) {
+    const int loc = i / a.A;
+    cx = (float)((loc % a.W) * a.stride);
+    cy = (float)((loc / a.W) * a.stride);
+    x1 = cx - bb[0] * a.stride; y1 = cy - bb[1] * a.stride;
+    x2 = cx + bb[2] * a.stride; y2 = cy + bb[3] * a.stride;
+  } else {
+    const float* pr = a.priors + (int64_t)i * 4;
+    cx = pr[0] + bb[0] * a.var0 * pr[2];
+    cy = pr[1] + bb[1] * a.var0 * pr[3];
+    pw = pr[2] * __expf(bb[2] * a.var1);
+    ph = pr[3] * __expf(bb[3] * a.var1);
+    x1 = (cx - pw * 0.5f) * a.in_w; y1 = (cy - ph * 0.5f) * a.in_h;
+    x2 = (cx + pw * 0.5f) * a.in_w; y2 = (cy + ph * 0.5f) * a.in_h;
+  }
+  const float sc = a.img_scale[n];
+  const float ih = a.img_hw[n * 2 + 0], iw = a.img_hw[n * 2 + 1];
+  x1 = fminf(fmaxf(x1 / sc, 0.f), iw); x2 = fminf(fmaxf(x2 / sc, 0.f), iw);
+  y1 = fminf(fmaxf(y1 / sc, 0.f), ih); y2 = fminf(fmaxf(y2 / sc, 0.f), ih);
+  const float fw = x2 - x1, fh = y2 - y1;
+  const float side = fminf(fw, fh);
+  if (side < a.min_size || fmaxf(fw, fh) > a.max_size) return;
+  const int slot = atomicAdd(&a.count[n], 1);
+  if (slot >= a.max_cand) return;
+  float* o = a.cand + ((int64_t)n * a.max_cand + slot) * 16;
+  o[0] = x1; o[1] = y1; o[2] = x2; o[3] = y2; o[4] = s;
+  if (a.kps) {
+    const float* kp = strided ? a.kps + n * a.sN + loc_i * a.sL + anc * 10 : a.kps + ((int64_t)n * a.P + i) * 10;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      float kx, ky;
+      if (a.priors == nullptr) {
+        kx = cx + kp[2 * k] * a.stride; ky = cy + kp[2 * k + 1] * a.stride;
+      } else {
+        const float* pr = a.priors + (int64_t)i * 4;
+        kx = (pr[0] + kp[2 * k] * a.var0 * pr[2]) * a.in_w;
+        ky = (pr[1] + kp[2 * k + 1] * a.var0 * pr[3]) * a.in_h;
+      }
+      o[5 + 2 * k] = kx / sc; o[6 + 2 * k] = ky / sc;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) o[5 + k] = -1.f;
+  }
+  o[15] = 0.f;
+}
+
+hipError_t det_decode(const DetDecodeArgs& a, hipStream_t stream) {
+  dim3 grid((a.P + 255) / 256, a.N), block(256);
+  hipLaunchKernelGGL(det_decode_kernel, grid, block, 0, stream, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- NMS
+// one workgroup (256 threads) per image; up to 1024 candidates
+__global__ void __launch_bounds__(256)
+nms_kernel(const float* __restrict__ cand, const int* __restrict__ count, int max_cand, float iou_thr, int max_out,
+           int* __restrict__ keep, int* __restrict__ keep_n) {
+  constexpr int CAP = 1024;
+  __shared__ float sc[CAP];
+  __shared__ int id[CAP];
+  __shared__ float bx[CAP][4];
+  __shared__ unsigned char alive[CAP];
+  __shared__ int nkeep;
+  const int n = blockIdx.x;
+  const int cnt = min(min(count[n], max_cand), CAP);
+  int P2 = 1;
+  while (P2 < cnt) P2 <<= 1;
+  for (int i = threadIdx.x; i < P2; i += 256) {
+    sc[i] = i < cnt ? cand[((int64_t)n * max_cand + i) * 16 + 4] : -INFINITY;
+    id[i] = i;
+  }
+  __syncthreads();
+  // bitonic sort descending by score
+  for (int k = 2; k <= P2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P2; i += 256) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const bool desc = (i & k) == 0;
+          const bool sw = desc ? (sc[i] < sc[ixj]) : (sc[i] > sc[ixj]);
+          if (sw) {
+            float t = sc[i]; sc[i] = sc[ixj]; sc[ixj] = t;
+            int u = id[i]; id[i] = id[ixj]; id[ixj] = u;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < cnt; i += 256) {
+    const float* c = cand + ((int64_t)n * max_cand + id[i]) * 16;
+    bx[i][0] = c[0]; bx[i][1] = c[1]; bx[i][2] = c[2]; bx[i][3] = c[3];
+    alive[i] = 1;
+  }
+  if (threadIdx.x == 0) nkeep = 0;
+  __syncthreads();
+  for (int i = 0; i < cnt; ++i) {
+    if (!alive[i]) continue;  // uniform: alive[] only changes between barriers
+    if (threadIdx.x == 0) {
+      if (nkeep < max_out) keep[n * max_out + nkeep] = id[i];
+      nkeep++;
+    }
+    const float ax1 = bx[i][0], ay1 = bx[i][1], ax2 = bx[i][2], ay2 = bx[i][3];
+    const float aa = (ax2 - ax1) * (ay2 - ay1);  // continuous-area IoU, +1e-8 (reference _nms)
+    for (int j = i + 1 + threadIdx.x; j < cnt; j += 256) {
+      if (!alive[j]) continue;
+      const float xx1 = fmaxf(ax1, bx[j][0]), yy1 = fmaxf(ay1, bx[j][1]);
+      const float xx2 = fminf(ax2, bx[j][2]), yy2 = fminf(ay2, bx[j][3]);
+      const float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
+      const float inter = w * h;
+      const float ab = (bx[j][2] - bx[j][0]) * (bx[j][3] - bx[j][1]);
+      if (inter / (aa + ab - inter + 1e-8f) > iou_thr) alive[j] = 0;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) keep_n[n] = min(nkeep, max_out);
+}
+
+hipError_t nms(const float* cand, const int* count, int N, int max_cand, float iou_thr, int max_out, int* keep,
+               int* keep_n, hipStream_t stream) {
+  hipLaunchKernelGGL(nms_kernel, dim3(N), dim3(256), 0, stream, cand, count, max_cand, iou_thr, max_out, keep, keep_n);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- warps
+// out[f, y, x, c] for c < 3 (channel-padded to cpad) =
+//   ((sample(src_f, Minv * (x, y, 1)) [c or 2-c]) * scale - mean) * inv_std
+// M is a 3x3 inverse map (affine: last row 0 0 1).  bilinear, constant 0 border
+// (cv2 warpAffine/warpPerspective defaults).  Output region [0, ow_f) x [0, OH)
+// of a (OH x OW) canvas; columns beyond ow_f are zero (OCR width bucketing).
+struct WarpArgs {
+  const uint8_t* src;
+  const int64_t* meta;   // [F, 4]: byte offset, h, w, out_w (valid output width)
+  const float* minv;     // [F, 9]
+  uint16_t* out;         // [F, OH, OW, cpad] bf16
+  int F, OH, OW, cpad;
+  float scale, mean, inv_std;
+  int swap_rb;
+  int cubic;             // 0 bilinear, 1 bicubic (cv2 a=-0.75)
+};
+
+__device__ __forceinline__ float cub(float x) {
+  const float a = -0.75f;
+  x = fabsf(x);
+  if (x < 1.f) return ((a + 2.f) * x - (a + 3.f)) * x * x + 1.f;
+  if (x < 2.f) return (((x - 5.f) * x + 8.f) * x - 4.f) * a;
+  return 0.f;
+}
+
+__global__ void warp_kernel(WarpArgs a) {
+  const int f = blockIdx.z;
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= a.OW || y >= a.OH) return;
+  const int64_t off = a.meta[f * 4 + 0];
+  const int h = (int)a.meta[f * 4 + 1], w = (int)a.meta[f * 4 + 2], ow = (int)a.meta[f * 4 + 3];
+  const float* M = a.minv + f * 9;
+  float v[3] = {0.f, 0.f, 0.f};
+  bool inside = x < ow;
+  if (inside) {
+    const float X = M[0] * x + M[1] * y + M[2], Y = M[3] * x + M[4] * y + M[5];
+    const float Z = M[6] * x + M[7] * y + M[8];
+    const float sx = X / Z, sy = Y / Z;
+    const uint8_t* img = a.src + off;
+    if (!a.cubic) {
+      const int x0 = (int)floorf(sx), y0 = (int)floorf(sy);
+      const float fx = sx - x0, fy = sy - y0;
+      for (int dy = 0; dy < 2; ++dy)
+        for (int dx = 0; dx < 2; ++dx) {
+          const int xx = x0 + dx, yy = y0 + dy;
+          if (xx < 0 || yy < 0 || xx >= w || yy >= h) continue;
+          const float wt = (dx ? fx : 1.f - fx) * (dy ? fy : 1.f - fy);
+          const uint8_t* p = img + ((int64_t)yy * w + xx) * 3;
+          v[0] += wt * p[0]; v[1] += wt * p[1]; v[2] += wt * p[2];
+        }
+    } else {
+      const int x0 = (int)floorf(sx), y0 = (int)floorf(sy);
+      const float fx = sx - x0, fy = sy - y0;
+      for (int dy = -1; dy < 3; ++dy)
+        for (int dx = -1; dx < 3; ++dx) {
+          const int xx = x0 + dx, yy = y0 + dy;
+          if (xx < 0 || yy < 0 || xx >= w || yy >= h) continue;
+          const float wt = cub(dx - fx) * cub(dy - fy);
+          const uint8_t* p = img + ((int64_t)yy * w + xx) * 3;
+          v[0] += wt * p[0]; v[1] += wt * p[1]; v[2] += wt * p[2];
+        }
+    }
+  }
+  uint16_t* o = a.out + (((int64_t)f * a.OH + y) * a.OW + x) * a.cpad;
+  for (int c = 0; c < a.cpad; ++c) {
+    float r = 0.f;
+    if (c < 3 && inside) {
+      const float px = fminf(fmaxf(rintf(v[a.swap_rb ? 2 - c : c]), 0.f), 255.f);
+      r = (px * a.scale - a.mean) * a.inv_std;
+    }
+    o[c] = f2bf(r);
+  }
+}
+
+hipError_t warp_batch(const WarpArgs& a, hipStream_t stream) {
+  dim3 grid((a.OW + 127) / 128, a.OH, a.F), block(128);
+  hipLaunchKernelGGL(warp_kernel, grid, block, 0, stream, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- CTC
+// probs [B, T, C] fp32 -> idx [B, T] (arg-max), conf [B, T] (max prob)
+__global__ void ctc_argmax_kernel(const float* __restrict__ probs, int rows, int C, int* __restrict__ idx,
+                                  float* __restrict__ conf) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;  // wave-uniform
+  const float* p = probs + (int64_t)row * C;
+  float best = -INFINITY;
+  int bi = 0;
+  for (int c = lane; c < C; c += 64) {
+    const float v = p[c];
+    if (v > best) { best = v; bi = c; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  if (lane == 0) { idx[row] = bi; conf[row] = best; }
+}
+
+// collapse: one thread per sequence; out_ids [B, T] (-1 padded), out_len [B], out_conf [B] (mean prob)
+__global__ void ctc_collapse_kernel(const int* __restrict__ idx, const float* __restrict__ conf, int B, int T,
+                                    int blank, int* __restrict__ out_ids, int* __restrict__ out_len,
+                                    float* __restrict__ out_conf) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  int n = 0, prev = -1;
+  float s = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const int c = idx[b * T + t];
+    if (c != blank && c != prev) {
+      out_ids[b * T + n] = c;
+      s += conf[b * T + t];
+      ++n;
+    }
+    prev = c;
+  }
+  for (int t = n; t < T; ++t) out_ids[b * T + t] = -1;
+  out_len[b] = n;
+  out_conf[b] = n > 0 ? s / n : 0.f;
+}
+
+hipError_t ctc_greedy(const float* probs, int B, int T, int C, int blank, int* tmp_idx, float* tmp_conf,
+                      int* out_ids, int* out_len, float* out_conf, hipStream_t stream) {
+  const int rows = B * T;
+  hipLaunchKernelGGL(ctc_argmax_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, probs, rows, C, tmp_idx, tmp_conf);
+  hipLaunchKernelGGL(ctc_collapse_kernel, dim3((B + 63) / 64), dim3(64), 0, stream, tmp_idx, tmp_conf, B, T, blank,
+                     out_ids, out_len, out_conf);
+  return hipGetLastError();
+}
+
+}  // namespace lumen

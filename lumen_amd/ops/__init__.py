@@ -275,7 +275,7 @@ def bank_scores(q: torch.Tensor, bank: torch.Tensor) -> torch.Tensor:
 
 # --------------------------------------------------------------------------- image prep
 FILTERS = {"pil_bicubic": 0, "bicubic": 0, "pil_bilinear": 1, "cv2_linear": 2, "linear": 2, "cv2_cubic": 3}
-LAYOUTS = {"nchw": 0, "nhwc": 1, "patches": 2}
+LAYOUTS = {"nchw": 0, "nhwc": 1, "patches": 2, "nhwc8": 3}
 
 
 class ImageGeom:
@@ -398,6 +398,8 @@ def image_prep(
         out = torch.empty((B * P, kpad), device=device, dtype=out_dtype)
     elif lay == 0:
         out = torch.empty((B, 3, OH, OW), device=device, dtype=out_dtype)
+    elif lay == 3:
+        out = torch.empty((B, OH, OW, 8), device=device, dtype=out_dtype)
     else:
         out = torch.empty((B, OH, OW, 3), device=device, dtype=out_dtype)
     if torch.device(device).type == "cuda":
@@ -429,6 +431,9 @@ def image_prep(
         out.copy_(v.permute(0, 3, 1, 2).to(out_dtype))
     elif lay == 1:
         out.copy_(v.to(out_dtype))
+    elif lay == 3:
+        out.zero_()
+        out[..., :3] = v.to(out_dtype)
     else:
         p = patch
         gh, gw = OH // p, OW // p
