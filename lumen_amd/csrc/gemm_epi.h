@@ -22,6 +22,7 @@ struct GemmEpi {
   int out_row_offset;
   int out_f32;
   const uint16_t* prelu;     // [N] per-channel PReLU slopes (bf16) or null; applied after act
+  int post_act;              // activation applied AFTER the residual add (ResNet: relu(conv + x))
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) {
@@ -96,6 +97,7 @@ __device__ __forceinline__ void epi_store16(float* v, int m, int n, int M, int N
       for (int q = 0; q < 16; ++q) if (n + q < N) v[q] += bf2f(t[q]);
     }
   }
+  if (ep.post_act) apply_act_n<16>(v, ep.post_act);
   if (ep.out_f32) {
     float* o = (float*)C + orow * ldc + n;
     if (full) {

@@ -285,7 +285,7 @@ static int64_t pixel_stride(const at::Tensor& t, const char* name) {
 void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
             const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& prelu, int64_t act,
             std::vector<int64_t> stride, std::vector<int64_t> padding, std::vector<int64_t> dilation, at::Tensor out,
-            int64_t tile) {
+            int64_t tile, int64_t post_act) {
   check_gpu(x, "x");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv2d: bf16");
   const int64_t ldx = pixel_stride(x, "x");
@@ -316,6 +316,7 @@ void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Te
     TORCH_CHECK(prelu->scalar_type() == at::kBFloat16 && prelu->numel() == Cout, "conv2d: prelu");
     ep.prelu = bf(*prelu);
   }
+  ep.post_act = (int)post_act;
   lumen::ConvArgs a{};
   a.x = bf(x); a.w = bf(w); a.out = out.data_ptr(); a.ldx = ldx; a.ldo = ldo;
   a.N = (int)N; a.H = (int)H; a.W = (int)W; a.Cin = (int)Cin; a.Cout = (int)Cout; a.KH = (int)KH; a.KW = (int)KW;
@@ -421,7 +422,7 @@ TORCH_LIBRARY(lumen, m) {
   m.def("row_topk(Tensor scores, int k, float scale, Tensor(v!) out_v, Tensor(i!) out_i, Tensor(l!)? out_lse, "
         "int index_offset) -> ()");
   m.def("conv2d(Tensor x, Tensor w, Tensor? bias, Tensor? residual, Tensor? prelu, int act, int[] stride, "
-        "int[] padding, int[] dilation, Tensor(o!) out, int tile) -> ()");
+        "int[] padding, int[] dilation, Tensor(o!) out, int tile, int post_act=0) -> ()");
   m.def("conv2d_dw(Tensor x, Tensor w, Tensor? bias, int act, int[] stride, int[] padding, int[] dilation, "
         "Tensor(o!) out) -> ()");
   m.def("channel_affine(Tensor x, Tensor scale, Tensor shift, Tensor(o!) out, int act, Tensor? prelu) -> ()");

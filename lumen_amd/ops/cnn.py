@@ -26,8 +26,8 @@ def conv_out_hw(H, W, KH, KW, stride, padding, dilation):
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride=1, padding=0, dilation=1,
            act=None, residual: Optional[torch.Tensor] = None, prelu: Optional[torch.Tensor] = None,
-           out: Optional[torch.Tensor] = None, out_dtype=None, tile: int = -1) -> torch.Tensor:
-    """out = prelu(act(conv(x, w) + bias)) + residual   (NHWC; w [Cout, KH, KW, Cin])."""
+           out: Optional[torch.Tensor] = None, out_dtype=None, tile: int = -1, post_act=None) -> torch.Tensor:
+    """out = post_act(prelu(act(conv(x, w) + bias)) + residual)   (NHWC; w [Cout, KH, KW, Cin])."""
     N, H, W, Cin = x.shape
     Cout, KH, KW, _ = w.shape
     Ho, Wo = conv_out_hw(H, W, KH, KW, stride, padding, dilation)
@@ -36,7 +36,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     a = act_id(act)
     if x.is_cuda:
         hip_ops().conv2d(x, w, bias, residual, prelu, a, list(_pair(stride)), list(_pair(padding)),
-                         list(_pair(dilation)), out, int(tile))
+                         list(_pair(dilation)), out, int(tile), act_id(post_act))
         return out
     y = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, _pair(stride), _pair(padding),
                  _pair(dilation)).permute(0, 2, 3, 1)
@@ -47,6 +47,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         y = torch.where(y > 0, y, y * prelu.float())
     if residual is not None:
         y = y + residual.float()
+    y = _act_ref(y, act_id(post_act))
     out.copy_(y.to(out.dtype))
     return out
 
