@@ -1,0 +1,339 @@
+"""MI355X face backend (L2): SCRFD detection + ArcFace IResNet embedding.
+
+Contract of the reference ``FaceRecognitionBackend``
+(packages/lumen-face/src/lumen_face/backends/base.py:107-308) and behaviour of its
+ONNX backend (backends/onnxrt_backend.py:701-1417):
+
+detection  decode -> letterbox (aspect kept, top-left, pad 0, cv2 linear) to the
+           detector size -> (x - 127.5) / 128 -> SCRFD -> anchor-centre
+           distance2bbox / distance2kps -> score >= threshold -> un-letterbox, clip ->
+           size filter (min <= w, h <= max) -> greedy NMS (IoU <= thr kept).
+embedding  optional 5-point similarity alignment onto the ArcFace 112x112 template,
+           else a plain resize of the (cropped) face -> (x/255 - 0.5) / 0.5 ->
+           IResNet -> L2-normalised fp32 vector.
+
+MI355X design: ONE fused letterbox+normalise kernel for the whole image batch into
+NHWC8 bf16, the detector's convs as implicit-GEMM MFMA kernels with BN/ReLU/residual
+in the epilogue, all three strides' heads decoded+thresholded+size-filtered by one
+kernel each and NMS'd on device; every face of every image in a batch is aligned by
+ONE batched warp kernel straight from the decoded original (no PIL re-decode per face
+— reference face_model.py:429-470) and embedded as ONE recogniser batch.  Concurrent
+requests from all gRPC streams are merged by :class:`DynamicBatcher` (one device-owning
+thread per model).
+
+Deliberate fixes of reference quirks: alignment uses the landmarks in
+the coordinate frame of the image they were detected in (the reference applies
+original-image landmarks to the bbox crop), and the canonical insightface 112x112
+ArcFace template (the reference's template is the 96-wide one without the +8 px x
+offset, onnxrt_backend.py:1388-1397) — ``LUMEN_FACE_REFERENCE_TEMPLATE=1`` restores it.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from ... import ops
+from ...models.face import IRESNET_PRESETS, SCRFD_PRESETS, IResNet, IResNetConfig, SCRFD, SCRFDConfig
+from ...ops import vision
+from ...resources.exceptions import ResourceNotFoundError
+from ...runtime.batcher import DynamicBatcher
+from ...utils.image import decode_rgb
+from ..common import BackendInfo, GenericResources, load_safetensors, pick_device, runtime_name
+
+log = logging.getLogger("lumen.face.backend")
+
+MAX_CAND = 1024
+REFERENCE_TEMPLATE = vision.ARCFACE_DST - np.array([8.0, 0.0], np.float32)
+
+
+class BackendError(Exception):
+    pass
+
+
+class BackendNotInitializedError(BackendError):
+    pass
+
+
+class InvalidInputError(BackendError):
+    pass
+
+
+class InferenceError(BackendError):
+    pass
+
+
+class DeviceUnavailableError(BackendError):
+    pass
+
+
+@dataclass
+class FaceDetection:
+    """bbox (x1, y1, x2, y2) in original-image pixels, optional 5 landmarks, confidence."""
+
+    bbox: tuple
+    confidence: float
+    landmarks: Optional[list] = None
+
+
+@dataclass
+class DetParams:
+    conf: float = 0.7
+    nms: float = 0.4
+    size_min: float = 50.0
+    size_max: float = 1000.0
+
+    def key(self):
+        return (self.conf, self.nms, self.size_min, self.size_max)
+
+
+@dataclass
+class FaceSpec:
+    det_size: int = 640
+    det_mean: float = 127.5
+    det_std: float = 128.0
+    rec_size: int = 112
+    rec_mean: float = 127.5
+    rec_std: float = 127.5
+    rec_color: str = "rgb"
+    align_landmarks: bool = True
+    extra: dict = field(default_factory=dict)
+
+
+def letterbox_geom(h: int, w: int, off: int, S: int):
+    """Reference _preprocess_detection sizes (onnxrt_backend.py:756-770): top-left, int()."""
+    if h / w > 1.0:
+        nh, nw = S, int(S / (h / w))
+    else:
+        nw, nh = S, int(S * (h / w))
+    nh, nw = max(nh, 1), max(nw, 1)
+    return ops.ImageGeom.letterbox(h, w, off, S, S, nh, nw), nh / h
+
+
+def crop_minv(bbox, out: int) -> np.ndarray:
+    """dst (out x out) -> src map of an integer bbox crop resized with cv2 linear (half-pixel)."""
+    x1, y1, x2, y2 = [int(v) for v in bbox]
+    bw, bh = max(x2 - x1, 1), max(y2 - y1, 1)
+    sx, sy = bw / out, bh / out
+    return np.array([[sx, 0, x1 + 0.5 * sx - 0.5], [0, sy, y1 + 0.5 * sy - 0.5], [0, 0, 1]], np.float32)
+
+
+class MI355XFaceBackend:
+    def __init__(self, resources: GenericResources, device: Optional[str] = None, max_batch: int = 64,
+                 max_wait_ms: float = 2.0, max_faces_batch: int = 512):
+        self.resources = resources
+        self.device_pref = device
+        self.max_batch = max_batch
+        self.max_wait_ms = max_wait_ms
+        self.max_faces_batch = max_faces_batch
+        self.det: Optional[SCRFD] = None
+        self.rec: Optional[IResNet] = None
+        self.spec = FaceSpec()
+        self.is_initialized = False
+        self.load_time = 0.0
+        self._det_batcher: Optional[DynamicBatcher] = None
+        self._emb_batcher: Optional[DynamicBatcher] = None
+        self.template = REFERENCE_TEMPLATE if os.environ.get("LUMEN_FACE_REFERENCE_TEMPLATE") == "1" \
+            else vision.ARCFACE_DST
+
+    # ------------------------------------------------------------------ lifecycle
+    def initialize(self) -> None:
+        if self.is_initialized:
+            return
+        t0 = time.time()
+        self.device = pick_device(self.device_pref)
+        r = self.resources
+        cfgp = r.model_root_path / "lumen_face_config.json"
+        if not cfgp.exists():
+            raise ResourceNotFoundError(
+                f"{r.model_name}: lumen_face_config.json missing — MI355X face weights are loaded from "
+                "detection/recognition.safetensors (ONNX initializer import is not available in this build)")
+        import json
+
+        meta = json.loads(cfgp.read_text())
+        dcfg = SCRFDConfig(**{k: tuple(v) if isinstance(v, list) else v for k, v in meta["det"].items()})
+        rcfg = IResNetConfig(**{k: tuple(v) if isinstance(v, list) else v for k, v in meta["rec"].items()})
+        ins = (r.extra.get("insightface") or {})
+        d, rc = ins.get("detection", {}), ins.get("recognition", {})
+        self.spec = FaceSpec(det_size=dcfg.input_size, det_mean=float(np.mean(d.get("mean", 127.5))),
+                             det_std=float(np.mean(d.get("std", 128.0))), rec_size=rcfg.input_size,
+                             rec_mean=float(np.mean(rc.get("mean", 127.5))), rec_std=float(np.mean(rc.get("std", 127.5))),
+                             rec_color=rc.get("color_order", "rgb"), align_landmarks=rc.get("align_landmarks", True))
+        det, rec = SCRFD(dcfg), IResNet(rcfg)
+        det.load_state_dict(load_safetensors(r.get_model_file("detection.safetensors")))
+        rec.load_state_dict(load_safetensors(r.get_model_file("recognition.safetensors")))
+        self.det, self.rec = det.to(self.device).eval(), rec.to(self.device).eval()
+        self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        self._det_batcher = DynamicBatcher(self._detect_batch, self.max_batch, self.max_wait_ms, "face-det")
+        self._emb_batcher = DynamicBatcher(self._embed_batch, self.max_faces_batch, self.max_wait_ms, "face-emb")
+        self.load_time = time.time() - t0
+        self.is_initialized = True
+        log.info("face pack %s ready on %s in %.2fs", r.model_name, self.device, self.load_time)
+
+    def close(self) -> None:
+        for b in (self._det_batcher, self._emb_batcher):
+            if b is not None:
+                b.close()
+
+    def _ensure(self):
+        if not self.is_initialized:
+            raise BackendNotInitializedError("Backend not initialized")
+
+    # ------------------------------------------------------------------ batched device work
+    @torch.no_grad()
+    def detect_images(self, images: Sequence[np.ndarray], params: Sequence[DetParams]) -> list[list[FaceDetection]]:
+        """Batched detection of decoded uint8 RGB images (one DetParams per image)."""
+        N = len(images)
+        if N == 0:
+            return []
+        S = self.spec.det_size
+        geoms, scales, off = [], [], 0
+        for im in images:
+            g, s = letterbox_geom(im.shape[0], im.shape[1], off, S)
+            geoms.append(g)
+            scales.append(s)
+            off += im.size
+        tens = [torch.from_numpy(np.ascontiguousarray(im)) for im in images]
+        if self.device.type == "cuda":
+            tens = [t.pin_memory() for t in tens] if len(tens) > 1 else tens
+        x = ops.image_prep(tens, (S, S), mean=(self.spec.det_mean,) * 3, std=(self.spec.det_std,) * 3, scale=1.0,
+                           filter="cv2_linear", layout="nhwc8", pad=0.0, geoms=geoms, out_dtype=self.dtype,
+                           device=self.device)
+        heads = self.det(x)
+        img_scale = torch.tensor(scales, dtype=torch.float32, device=self.device)
+        img_hw = torch.tensor([[im.shape[0], im.shape[1]] for im in images], dtype=torch.float32, device=self.device)
+        A = self.det.cfg.anchors
+        results: list[Optional[list[FaceDetection]]] = [None] * N
+        groups: dict = {}
+        for i, p in enumerate(params):
+            groups.setdefault(p.key(), []).append(i)
+        for key, idx in groups.items():
+            p = params[idx[0]]
+            sel = torch.tensor(idx, device=self.device) if len(groups) > 1 else None
+            n = len(idx)
+            cand = torch.zeros((n, MAX_CAND, 16), dtype=torch.float32, device=self.device)
+            count = torch.zeros((n,), dtype=torch.int32, device=self.device)
+            for h, stride in zip(heads, self.det.cfg.strides):
+                hh = h if sel is None else h.index_select(0, sel)
+                vision.det_decode_head(hh, A, stride, p.conf,
+                                       img_scale if sel is None else img_scale.index_select(0, sel),
+                                       img_hw if sel is None else img_hw.index_select(0, sel), cand, count,
+                                       float(p.size_min), float(p.size_max))
+            kept = vision.nms(cand, count, p.nms)
+            for j, rows in zip(idx, kept):
+                faces = []
+                for r in rows.tolist():
+                    lm = [(r[5 + 2 * k], r[6 + 2 * k]) for k in range(5)]
+                    faces.append(FaceDetection(bbox=(r[0], r[1], r[2], r[3]), confidence=min(max(r[4], 0.0), 1.0),
+                                               landmarks=lm))
+                results[j] = faces
+        return results  # type: ignore[return-value]
+
+    def _minv_for(self, img: np.ndarray, landmarks, bbox) -> np.ndarray:
+        out = self.spec.rec_size
+        if landmarks is not None and len(landmarks) == 5 and self.spec.align_landmarks:
+            dst = self.template * (out / 112.0)
+            M = vision.similarity_transform(np.asarray(landmarks, np.float32), dst)
+            return vision.invert_affine(M)
+        if bbox is None:
+            bbox = (0, 0, img.shape[1], img.shape[0])
+        return crop_minv(bbox, out)
+
+    @torch.no_grad()
+    def embed_faces(self, images: Sequence[np.ndarray], img_index: Sequence[int], minv: np.ndarray) -> np.ndarray:
+        """Warp + embed F faces -> [F, D] fp32 (L2-normalised)."""
+        if len(img_index) == 0:
+            return np.zeros((0, self.rec.cfg.embedding), np.float32)
+        R = self.spec.rec_size
+        x = vision.warp_batch(images, img_index, minv, (R, R), cpad=8, scale=1.0 / self.spec.rec_std,
+                              mean=self.spec.rec_mean / self.spec.rec_std, std=1.0,
+                              swap_rb=self.spec.rec_color.lower() == "bgr", device=self.device)
+        if x.dtype != self.dtype:
+            x = x.to(self.dtype)
+        return self.rec(x).float().cpu().numpy()
+
+    def _detect_batch(self, items):
+        imgs = [it[0] for it in items]
+        return self.detect_images(imgs, [it[1] for it in items])
+
+    def _embed_batch(self, items):
+        # items: (image, landmarks, bbox); identical image objects are uploaded once
+        uniq: dict = {}
+        images, index, minvs = [], [], []
+        for img, lm, bb in items:
+            k = id(img)
+            if k not in uniq:
+                uniq[k] = len(images)
+                images.append(img)
+            index.append(uniq[k])
+            minvs.append(self._minv_for(img, lm, bb))
+        emb = self.embed_faces(images, index, np.stack(minvs))
+        return list(emb)
+
+    # ------------------------------------------------------------------ public API (reference contract)
+    def decode(self, image_bytes: bytes) -> np.ndarray:
+        if not image_bytes:
+            raise InvalidInputError("image_bytes cannot be empty")
+        try:
+            return decode_rgb(image_bytes)
+        except ValueError as e:
+            raise InvalidInputError(f"Failed to decode image bytes: {e}") from e
+
+    def image_to_faces(self, image_bytes: bytes, detection_confidence_threshold: float = 0.7,
+                       nms_threshold: float = 0.4, face_size_min: int = 50, face_size_max: int = 1000
+                       ) -> list[FaceDetection]:
+        self._ensure()
+        img = self.decode(image_bytes)
+        return self.detect_decoded(img, DetParams(detection_confidence_threshold, nms_threshold, face_size_min,
+                                                  face_size_max))
+
+    def detect_decoded(self, img: np.ndarray, params: DetParams) -> list[FaceDetection]:
+        self._ensure()
+        return self._det_batcher((img, params))
+
+    def face_to_embedding(self, face_image: Optional[bytes] = None, cropped_face_array: Optional[np.ndarray] = None,
+                          landmarks: Optional[list] = None) -> np.ndarray:
+        self._ensure()
+        if face_image is None and cropped_face_array is None:
+            raise InvalidInputError("Either face_image or cropped_face_array must be provided")
+        img = self.decode(face_image) if face_image is not None else \
+            np.ascontiguousarray(np.clip(cropped_face_array, 0, 255).astype(np.uint8))
+        return self._emb_batcher((img, landmarks, None))
+
+    def embed_detections(self, img: np.ndarray, faces: Sequence[FaceDetection]) -> list[np.ndarray]:
+        """Embed detected faces of one decoded image (aligned from the full image)."""
+        self._ensure()
+        return self._emb_batcher.map([(img, f.landmarks, f.bbox) for f in faces])
+
+    def get_runtime_info(self) -> BackendInfo:
+        return self.get_info()
+
+    def get_info(self) -> BackendInfo:
+        r = self.resources
+        dev = getattr(self, "device", None)
+        cuda = dev is not None and dev.type == "cuda"
+        emb = self.rec.cfg.embedding if self.rec is not None else (r.get_embedding_dim() or 512)
+        return BackendInfo(runtime=runtime_name(dev) if dev is not None else "mi355x-hip", device=str(dev or self.device_pref),
+                           model_id=r.model_id, model_name=r.model_name, version=r.model_info.version,
+                           precisions=("bf16",) if cuda or dev is None else ("fp32",), embedding_dim=emb,
+                           extra={"det_size": str(self.spec.det_size), "rec_size": str(self.spec.rec_size),
+                                  "detector": "scrfd", "max_batch": str(self.max_batch)})
+
+
+def create_backend(settings, resources: GenericResources, runtime: Optional[str] = None) -> MI355XFaceBackend:
+    """Factory (reference backends/factory.py:21-141 registers only onnx)."""
+    rt = runtime or resources.runtime
+    if rt not in ("onnx", "torch", "rknn"):
+        raise ValueError(f"unsupported runtime '{rt}'")
+    if rt == "rknn":
+        raise DeviceUnavailableError("RKNN runtime is not available on MI355X builds")
+    from ...resources.config import AmdRuntimeSettings
+
+    amd = AmdRuntimeSettings.from_env()
+    dev = getattr(settings, "device", None) if settings is not None else None
+    return MI355XFaceBackend(resources, device=dev, max_batch=min(amd.max_batch, 64), max_wait_ms=amd.max_wait_ms)

@@ -32,6 +32,10 @@ def test_conv2d(N, H, W, Cin, Cout, K, s, p, d, tile):
     ref2 = cnn.conv2d(x, w, b, s, p, d, act="relu", residual=r)
     got2 = cnn.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), s, p, d, act="relu", residual=r.to(DEV), tile=tile)
     assert _rel(got2, ref2) < 1e-2
+    # ResNet tail: relu(conv + bias + shortcut)
+    ref3 = cnn.conv2d(x, w, b, s, p, d, residual=r, post_act="relu")
+    got3 = cnn.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), s, p, d, residual=r.to(DEV), tile=tile, post_act="relu")
+    assert _rel(got3, ref3) < 1e-2 and got3.min().item() >= 0
 
 
 def test_conv2d_into_channel_slice():

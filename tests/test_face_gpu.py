@@ -1,0 +1,86 @@
+"""Face models and service on the MI355X path vs the fp32 CPU reference."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from lumen_amd.models.face import IRESNET_PRESETS, SCRFD, SCRFD_PRESETS, IResNet, write_face_model
+from lumen_amd.resources.validator import config_from_dict
+from lumen_amd.services.face import GeneralFaceService
+from lumen_amd.utils.image import encode_jpeg
+
+pytestmark = pytest.mark.gpu
+
+
+def _cos(a, b):
+    a, b = a.float().flatten(1), b.float().flatten(1)
+    return torch.nn.functional.cosine_similarity(a, b, dim=1)
+
+
+def test_iresnet50_full_size():
+    g = torch.Generator().manual_seed(0)
+    m = IResNet(IRESNET_PRESETS["r50"])
+    m.random_init(g)
+    x = torch.randn(4, 112, 112, 8, generator=g)
+    x[..., 3:] = 0
+    ref = m(x)
+    got = m.to("cuda")(x.to("cuda", torch.bfloat16)).cpu()
+    assert got.shape == (4, 512)
+    assert _cos(got, ref).min() > 0.99
+
+
+def test_scrfd_10g_full_size():
+    g = torch.Generator().manual_seed(1)
+    m = SCRFD(SCRFD_PRESETS["10g"])
+    m.random_init(g)
+    x = torch.randn(1, 640, 640, 8, generator=g)
+    x[..., 3:] = 0
+    ref = m(x)
+    got = m.to("cuda")(x.to("cuda", torch.bfloat16))
+    for r, o in zip(ref, got):
+        assert o.shape == r.shape
+        assert _cos(o.cpu(), r).min() > 0.99
+
+
+def _cfg(cache, device):
+    return {
+        "metadata": {"version": "1.0.0", "region": "other", "cache_dir": str(cache)},
+        "deployment": {"mode": "single", "service": "face"},
+        "server": {"port": 50553, "host": "127.0.0.1"},
+        "services": {"face": {"enabled": True, "package": "lumen_face",
+                              "import_info": {"registry_class": "lumen_face.general_face.GeneralFaceService",
+                                              "add_to_server": "x.y"},
+                              "backend_settings": {"device": device},
+                              "models": {"general": {"model": "buffalo_tiny", "runtime": "onnx"}}}},
+    }
+
+
+def test_face_service_gpu_vs_cpu(tmp_path):
+    write_face_model(tmp_path / "models" / "buffalo_tiny", "buffalo_tiny")
+    svcs = {}
+    for dev in ("cpu", "cuda"):
+        cfg = config_from_dict(_cfg(tmp_path, dev))
+        svcs[dev] = GeneralFaceService.from_config(cfg.services["face"], tmp_path)
+        svcs[dev].initialize()
+    try:
+        rng = np.random.default_rng(0)
+        img = encode_jpeg(rng.integers(0, 255, (96, 160, 3), dtype=np.uint8))
+        face = encode_jpeg(rng.integers(0, 255, (130, 120, 3), dtype=np.uint8))
+        lm = json.dumps([{"x": 40, "y": 50}, {"x": 72, "y": 50}, {"x": 56, "y": 70}, {"x": 42, "y": 90},
+                         {"x": 70, "y": 90}])
+        for meta in ({}, {"landmarks": lm}):
+            a = np.array(json.loads(svcs["cpu"].handle("face_embed", face, "image/jpeg", meta)[0])["vector"])
+            b = np.array(json.loads(svcs["cuda"].handle("face_embed", face, "image/jpeg", meta)[0])["vector"])
+            assert float(a @ b) > 0.98
+        low = {"detection_confidence_threshold": "0.0", "face_size_min": "0", "nms_threshold": "0.3"}
+        dc = json.loads(svcs["cpu"].handle("face_detect", img, "image/jpeg", low)[0])
+        dg = json.loads(svcs["cuda"].handle("face_detect", img, "image/jpeg", low)[0])
+        assert dg["count"] > 0 and abs(dg["count"] - dc["count"]) <= max(2, dc["count"] // 5)
+        bc, bg = np.array(dc["faces"][0]["bbox"]), np.array(dg["faces"][0]["bbox"])
+        assert np.abs(bc - bg).max() < 4.0
+        de = json.loads(svcs["cuda"].handle("face_detect_and_embed", img, "image/jpeg", dict(low, max_faces="4"))[0])
+        assert de["count"] == 4 and all(abs(np.linalg.norm(f["embedding"]) - 1) < 1e-2 for f in de["faces"])
+    finally:
+        for s in svcs.values():
+            s.close()

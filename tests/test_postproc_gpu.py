@@ -1,0 +1,83 @@
+"""Detection / recognition post-processing HIP kernels vs the numpy / PyTorch references."""
+import numpy as np
+import pytest
+import torch
+
+from lumen_amd.ops import vision
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _sorted_rows(t):
+    a = t.float().cpu().numpy()
+    return a[np.lexsort((a[:, 1], a[:, 0], -a[:, 4]))] if len(a) else a
+
+
+@pytest.mark.parametrize("H,W,A,stride", [(80, 80, 2, 8), (20, 20, 2, 32), (13, 17, 1, 16)])
+def test_det_decode_head(H, W, A, stride):
+    g = torch.Generator().manual_seed(H + A)
+    N, Ch = 2, 32
+    head = torch.randn(N, H, W, Ch, generator=g)
+    head[..., A:5 * A] = head[..., A:5 * A].abs() * 2
+    img_scale = torch.tensor([0.5, 1.25])
+    img_hw = torch.tensor([[900.0, 1200.0], [500.0, 400.0]])
+    cand_r = torch.zeros(N, 4096, 16)
+    cnt_r = torch.zeros(N, dtype=torch.int32)
+    vision.det_decode_head(head, A, stride, 0.8, img_scale, img_hw, cand_r, cnt_r, 4.0, 600.0)
+    cand = torch.zeros(N, 4096, 16, device=DEV)
+    cnt = torch.zeros(N, dtype=torch.int32, device=DEV)
+    vision.det_decode_head(head.to(DEV), A, stride, 0.8, img_scale.to(DEV), img_hw.to(DEV), cand, cnt, 4.0, 600.0)
+    assert cnt.cpu().tolist() == cnt_r.tolist()
+    for n in range(N):
+        c = int(cnt_r[n])
+        got, ref = _sorted_rows(cand[n, :c]), _sorted_rows(cand_r[n, :c])
+        np.testing.assert_allclose(got[:, :15], ref[:, :15], rtol=1e-4, atol=1e-3)
+
+
+def test_nms_matches_reference():
+    rng = np.random.default_rng(0)
+    N, MC = 3, 1024
+    cand = torch.zeros(N, MC, 16)
+    count = torch.tensor([700, 37, 0], dtype=torch.int32)
+    for n in range(N):
+        c = int(count[n])
+        xy = rng.uniform(0, 500, (c, 2))
+        wh = rng.uniform(10, 80, (c, 2))
+        cand[n, :c, 0:2] = torch.from_numpy(xy)
+        cand[n, :c, 2:4] = torch.from_numpy(xy + wh)
+        cand[n, :c, 4] = torch.from_numpy(rng.permutation(c) / max(c, 1)).float()
+    got = vision.nms(cand.to(DEV), count.to(DEV), 0.4)
+    ref = vision.nms(cand, count, 0.4)
+    for g_, r_ in zip(got, ref):
+        assert g_.shape == r_.shape
+        np.testing.assert_allclose(g_.numpy(), r_.numpy(), atol=1e-5)
+
+
+@pytest.mark.parametrize("cubic", [False, True])
+def test_warp_batch(cubic):
+    rng = np.random.default_rng(1)
+    imgs = [rng.integers(0, 255, (120, 160, 3), dtype=np.uint8), rng.integers(0, 255, (300, 200, 3), dtype=np.uint8)]
+    lms = [np.array([[50, 60], [90, 58], [70, 80], [55, 100], [88, 99]], np.float32),
+           np.array([[80, 120], [130, 125], [100, 160], [85, 190], [125, 195]], np.float32),
+           np.array([[10, 10], [60, 12], [30, 40], [15, 70], [55, 72]], np.float32)]
+    idx = [0, 1, 1]
+    minv = np.stack([vision.invert_affine(vision.similarity_transform(l)) for l in lms])
+    ref = vision.warp_batch(imgs, idx, minv, (112, 112), cubic=cubic)
+    got = vision.warp_batch(imgs, idx, minv, (112, 112), cubic=cubic, device=DEV).cpu()
+    diff = (got.float() - ref.float()).abs()
+    # 1 LSB of the uint8 rounding (2/255 after normalisation) + bf16 rounding
+    assert diff.max().item() < 0.03, diff.max()
+    assert diff.mean().item() < 2e-3
+
+
+def test_ctc_greedy():
+    g = torch.Generator().manual_seed(3)
+    B, T, C = 37, 40, 97
+    logits = torch.randn(B, T, C, generator=g) * 3
+    logits[:, ::3, 0] += 6  # plenty of blanks
+    probs = torch.softmax(logits, -1)
+    ids_r, cf_r = vision.ctc_greedy(probs)
+    ids, cf = vision.ctc_greedy(probs.to(DEV))
+    assert ids == ids_r
+    np.testing.assert_allclose(cf, cf_r, rtol=1e-4, atol=1e-5)
