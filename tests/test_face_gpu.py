@@ -50,7 +50,7 @@ def _cfg(cache, device):
         "server": {"port": 50553, "host": "127.0.0.1"},
         "services": {"face": {"enabled": True, "package": "lumen_face",
                               "import_info": {"registry_class": "lumen_face.general_face.GeneralFaceService",
-                                              "add_to_server": "x.y"},
+                                              "add_to_server": "lumen_face.proto.ml_service_pb2_grpc.add_InferenceServicer_to_server"},
                               "backend_settings": {"device": device},
                               "models": {"general": {"model": "buffalo_tiny", "runtime": "onnx"}}}},
     }
