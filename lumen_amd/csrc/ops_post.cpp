@@ -7,24 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <torch/library.h>
 
-namespace lumen {
-struct DetDecodeArgs {
-  const float* scores; const float* bbox; const float* kps; const float* priors;
-  int N, H, W, A, stride; int P; float thresh; const float* img_scale; const float* img_hw;
-  float min_size, max_size; float var0, var1; float in_w, in_h; float* cand; int* count; int max_cand;
-  int64_t sN, sL; int apply_sigmoid;
-};
-hipError_t det_decode(const DetDecodeArgs& a, hipStream_t stream);
-hipError_t nms(const float* cand, const int* count, int N, int max_cand, float iou_thr, int max_out, int* keep,
-               int* keep_n, hipStream_t stream);
-struct WarpArgs {
-  const uint8_t* src; const int64_t* meta; const float* minv; uint16_t* out; int F, OH, OW, cpad;
-  float scale, mean, inv_std; int swap_rb; int cubic;
-};
-hipError_t warp_batch(const WarpArgs& a, hipStream_t stream);
-hipError_t ctc_greedy(const float* probs, int B, int T, int C, int blank, int* tmp_idx, float* tmp_conf,
-                      int* out_ids, int* out_len, float* out_conf, hipStream_t stream);
-}  // namespace lumen
+#include "postproc.h"
 
 namespace {
 
@@ -76,7 +59,7 @@ void nms(const at::Tensor& cand, const at::Tensor& count, double iou_thr, at::Te
 
 // src flat uint8; meta int64 [F, 4] (offset, h, w, out_w); minv f32 [F, 9]; out bf16 [F, OH, OW, cpad]
 void warp_batch(const at::Tensor& src, const at::Tensor& meta, const at::Tensor& minv, at::Tensor out, double scale,
-                double mean, double std_, bool swap_rb, bool cubic) {
+                double mean, double std_, bool swap_rb, bool cubic, bool replicate) {
   TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte, "warp: uint8 src");
   TORCH_CHECK(meta.is_cuda() && meta.scalar_type() == at::kLong && meta.is_contiguous() && meta.size(1) == 4, "meta");
   f32c(minv, "minv");
@@ -86,18 +69,27 @@ void warp_batch(const at::Tensor& src, const at::Tensor& meta, const at::Tensor&
   a.out = reinterpret_cast<uint16_t*>(out.data_ptr());
   a.F = (int)out.size(0); a.OH = (int)out.size(1); a.OW = (int)out.size(2); a.cpad = (int)out.size(3);
   a.scale = (float)scale; a.mean = (float)mean; a.inv_std = (float)(1.0 / std_);
-  a.swap_rb = swap_rb ? 1 : 0; a.cubic = cubic ? 1 : 0;
+  a.swap_rb = swap_rb ? 1 : 0; a.cubic = cubic ? 1 : 0; a.replicate = replicate ? 1 : 0;
   const at::DeviceGuard g(src.device());
   CHECK_HIP2(lumen::warp_batch(a, stream()));
 }
 
-void ctc_greedy(const at::Tensor& probs, int64_t blank, at::Tensor out_ids, at::Tensor out_len, at::Tensor out_conf) {
+void ctc_greedy(const at::Tensor& probs, int64_t blank, at::Tensor out_ids, at::Tensor out_len, at::Tensor out_conf,
+                bool from_logits, const c10::optional<at::Tensor>& tlen) {
   f32c(probs, "probs");
   const int B = (int)probs.size(0), T = (int)probs.size(1), C = (int)probs.size(2);
+  TORCH_CHECK(out_ids.is_contiguous() && out_ids.scalar_type() == at::kInt && out_ids.numel() == (int64_t)B * T, "ids");
+  TORCH_CHECK(out_len.scalar_type() == at::kInt && out_len.numel() == B, "len");
+  TORCH_CHECK(out_conf.scalar_type() == at::kFloat && out_conf.numel() == B, "conf");
+  const int* tl = nullptr;
+  if (tlen.has_value()) {
+    TORCH_CHECK(tlen->is_cuda() && tlen->scalar_type() == at::kInt && tlen->numel() == B && tlen->is_contiguous(), "tlen");
+    tl = tlen->data_ptr<int>();
+  }
   auto idx = at::empty({B, T}, probs.options().dtype(at::kInt));
   auto conf = at::empty({B, T}, probs.options());
   const at::DeviceGuard g(probs.device());
-  CHECK_HIP2(lumen::ctc_greedy(probs.data_ptr<float>(), B, T, C, (int)blank, idx.data_ptr<int>(),
+  CHECK_HIP2(lumen::ctc_greedy(probs.data_ptr<float>(), B, T, C, (int)blank, from_logits ? 1 : 0, tl, idx.data_ptr<int>(),
                                conf.data_ptr<float>(), out_ids.data_ptr<int>(), out_len.data_ptr<int>(),
                                out_conf.data_ptr<float>(), stream()));
 }
@@ -110,8 +102,9 @@ TORCH_LIBRARY_FRAGMENT(lumen, m) {
         "float in_w, float in_h, Tensor(c!) cand, Tensor(n!) count, int P, int sN, int sL, bool apply_sigmoid) -> ()");
   m.def("nms(Tensor cand, Tensor count, float iou_thr, Tensor(k!) keep, Tensor(n!) keep_n) -> ()");
   m.def("warp_batch(Tensor src, Tensor meta, Tensor minv, Tensor(o!) out, float scale, float mean, float std, "
-        "bool swap_rb, bool cubic) -> ()");
-  m.def("ctc_greedy(Tensor probs, int blank, Tensor(i!) out_ids, Tensor(l!) out_len, Tensor(c!) out_conf) -> ()");
+        "bool swap_rb, bool cubic, bool replicate=False) -> ()");
+  m.def("ctc_greedy(Tensor probs, int blank, Tensor(i!) out_ids, Tensor(l!) out_len, Tensor(c!) out_conf, "
+        "bool from_logits=False, Tensor? tlen=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(lumen, CUDA, m) {

@@ -17,30 +17,11 @@
 //  * ctc_greedy: per (sequence, timestep) arg-max over the class axis and the
 //    blank/repeat collapse with the mean confidence (O-8).
 #include "common.h"
+#include "postproc.h"
 
 namespace lumen {
 
-struct DetDecodeArgs {
-  const float* scores;   // [N, H*W*A]           (already sigmoid'ed) — or [N, P] priors mode
-  const float* bbox;     // [N, H*W*A, 4]        distances (in stride units) or prior deltas
-  const float* kps;      // [N, H*W*A, 10] or null
-  const float* priors;   // [P, 4] (cx, cy, w, h) normalised, RetinaFace mode; null = SCRFD anchors
-  int N, H, W, A, stride;
-  int P;                 // candidates per image in this level
-  float thresh;
-  const float* img_scale;  // [N] letterbox scale (det size / original)
-  const float* img_hw;     // [N, 2] original (h, w)
-  float min_size, max_size;
-  float var0, var1;        // RetinaFace variances
-  float in_w, in_h;        // network input size (priors mode)
-  float* cand;             // [N, max_cand, 16]: x1 y1 x2 y2 score kps*10 pad
-  int* count;              // [N]
-  int max_cand;
-  // generalised addressing (fused head conv outputs, NHWC): element (n, loc, a, j) of
-  // scores/bbox/kps lives at base + n*sN + loc*sL + a*{1,4,10} + j
-  int64_t sN, sL;
-  int apply_sigmoid;
-};
+
 
 __global__ void det_decode_kernel(DetDecodeArgs a) {
   const int n = blockIdx.y;
@@ -182,18 +163,9 @@ hipError_t nms(const float* cand, const int* count, int N, int max_cand, float i
 // out[f, y, x, c] for c < 3 (channel-padded to cpad) =
 //   ((sample(src_f, Minv * (x, y, 1)) [c or 2-c]) * scale - mean) * inv_std
 // M is a 3x3 inverse map (affine: last row 0 0 1).  bilinear, constant 0 border
-// (cv2 warpAffine/warpPerspective defaults).  Output region [0, ow_f) x [0, OH)
+// (cv2 warpAffine/warpPerspective defaults) or replicate.  Output region [0, ow_f) x [0, OH)
 // of a (OH x OW) canvas; columns beyond ow_f are zero (OCR width bucketing).
-struct WarpArgs {
-  const uint8_t* src;
-  const int64_t* meta;   // [F, 4]: byte offset, h, w, out_w (valid output width)
-  const float* minv;     // [F, 9]
-  uint16_t* out;         // [F, OH, OW, cpad] bf16
-  int F, OH, OW, cpad;
-  float scale, mean, inv_std;
-  int swap_rb;
-  int cubic;             // 0 bilinear, 1 bicubic (cv2 a=-0.75)
-};
+
 
 __device__ __forceinline__ float cub(float x) {
   const float a = -0.75f;
@@ -222,8 +194,9 @@ __global__ void warp_kernel(WarpArgs a) {
       const float fx = sx - x0, fy = sy - y0;
       for (int dy = 0; dy < 2; ++dy)
         for (int dx = 0; dx < 2; ++dx) {
-          const int xx = x0 + dx, yy = y0 + dy;
-          if (xx < 0 || yy < 0 || xx >= w || yy >= h) continue;
+          int xx = x0 + dx, yy = y0 + dy;
+          if (a.replicate) { xx = min(max(xx, 0), w - 1); yy = min(max(yy, 0), h - 1); }
+          else if (xx < 0 || yy < 0 || xx >= w || yy >= h) continue;
           const float wt = (dx ? fx : 1.f - fx) * (dy ? fy : 1.f - fy);
           const uint8_t* p = img + ((int64_t)yy * w + xx) * 3;
           v[0] += wt * p[0]; v[1] += wt * p[1]; v[2] += wt * p[2];
@@ -233,8 +206,9 @@ __global__ void warp_kernel(WarpArgs a) {
       const float fx = sx - x0, fy = sy - y0;
       for (int dy = -1; dy < 3; ++dy)
         for (int dx = -1; dx < 3; ++dx) {
-          const int xx = x0 + dx, yy = y0 + dy;
-          if (xx < 0 || yy < 0 || xx >= w || yy >= h) continue;
+          int xx = x0 + dx, yy = y0 + dy;
+          if (a.replicate) { xx = min(max(xx, 0), w - 1); yy = min(max(yy, 0), h - 1); }
+          else if (xx < 0 || yy < 0 || xx >= w || yy >= h) continue;
           const float wt = cub(dx - fx) * cub(dy - fy);
           const uint8_t* p = img + ((int64_t)yy * w + xx) * 3;
           v[0] += wt * p[0]; v[1] += wt * p[1]; v[2] += wt * p[2];
@@ -259,37 +233,52 @@ hipError_t warp_batch(const WarpArgs& a, hipStream_t stream) {
 }
 
 // ---------------------------------------------------------------------------- CTC
-// probs [B, T, C] fp32 -> idx [B, T] (arg-max), conf [B, T] (max prob)
-__global__ void ctc_argmax_kernel(const float* __restrict__ probs, int rows, int C, int* __restrict__ idx,
-                                  float* __restrict__ conf) {
+// probs [B, T, C] fp32 -> idx [B, T] (arg-max), conf [B, T] (max prob).  With from_logits
+// the row holds raw logits and conf = softmax(row)[argmax] = 1 / sum_j exp(l_j - l_max),
+// computed with a per-lane online sum — the recogniser's softmax is fused away.
+__global__ void ctc_argmax_kernel(const float* __restrict__ probs, int rows, int C, int from_logits,
+                                  int* __restrict__ idx, float* __restrict__ conf) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;  // wave-uniform
   const float* p = probs + (int64_t)row * C;
-  float best = -INFINITY;
+  float best = -INFINITY, sum = 0.f;
   int bi = 0;
   for (int c = lane; c < C; c += 64) {
     const float v = p[c];
-    if (v > best) { best = v; bi = c; }
+    if (v > best) {
+      if (from_logits) sum = sum * __expf(best - v) + 1.f;
+      best = v;
+      bi = c;
+    } else if (from_logits) {
+      sum += __expf(v - best);
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float ov = __shfl_xor(best, o, 64);
     const int oi = __shfl_xor(bi, o, 64);
+    const float os = __shfl_xor(sum, o, 64);
+    if (from_logits) {
+      const float m = fmaxf(best, ov);
+      sum = (best == -INFINITY ? 0.f : sum * __expf(best - m)) + (ov == -INFINITY ? 0.f : os * __expf(ov - m));
+    }
     if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
   }
-  if (lane == 0) { idx[row] = bi; conf[row] = best; }
+  if (lane == 0) { idx[row] = bi; conf[row] = from_logits ? 1.f / sum : best; }
 }
 
-// collapse: one thread per sequence; out_ids [B, T] (-1 padded), out_len [B], out_conf [B] (mean prob)
+// collapse: one thread per sequence; out_ids [B, T] (-1 padded), out_len [B], out_conf [B] (mean prob).
+// tlen (optional) = valid time steps per sequence (width-bucketed batches).
 __global__ void ctc_collapse_kernel(const int* __restrict__ idx, const float* __restrict__ conf, int B, int T,
-                                    int blank, int* __restrict__ out_ids, int* __restrict__ out_len,
-                                    float* __restrict__ out_conf) {
+                                    int blank, const int* __restrict__ tlen, int* __restrict__ out_ids,
+                                    int* __restrict__ out_len, float* __restrict__ out_conf) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
+  const int Tb = tlen ? min(max(tlen[b], 0), T) : T;
   int n = 0, prev = -1;
   float s = 0.f;
-  for (int t = 0; t < T; ++t) {
+  for (int t = 0; t < Tb; ++t) {
     const int c = idx[b * T + t];
     if (c != blank && c != prev) {
       out_ids[b * T + n] = c;
@@ -303,12 +292,13 @@ __global__ void ctc_collapse_kernel(const int* __restrict__ idx, const float* __
   out_conf[b] = n > 0 ? s / n : 0.f;
 }
 
-hipError_t ctc_greedy(const float* probs, int B, int T, int C, int blank, int* tmp_idx, float* tmp_conf,
-                      int* out_ids, int* out_len, float* out_conf, hipStream_t stream) {
+hipError_t ctc_greedy(const float* probs, int B, int T, int C, int blank, int from_logits, const int* tlen,
+                      int* tmp_idx, float* tmp_conf, int* out_ids, int* out_len, float* out_conf, hipStream_t stream) {
   const int rows = B * T;
-  hipLaunchKernelGGL(ctc_argmax_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, probs, rows, C, tmp_idx, tmp_conf);
+  hipLaunchKernelGGL(ctc_argmax_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, probs, rows, C, from_logits,
+                     tmp_idx, tmp_conf);
   hipLaunchKernelGGL(ctc_collapse_kernel, dim3((B + 63) / 64), dim3(64), 0, stream, tmp_idx, tmp_conf, B, T, blank,
-                     out_ids, out_len, out_conf);
+                     tlen, out_ids, out_len, out_conf);
   return hipGetLastError();
 }
 

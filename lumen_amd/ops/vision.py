@@ -177,10 +177,12 @@ def invert_affine(M: np.ndarray) -> np.ndarray:
 
 def warp_batch(images: Sequence[np.ndarray], img_index: Sequence[int], minv: np.ndarray, out_hw: tuple,
                out_w: Optional[Sequence[int]] = None, cpad: int = 8, scale: float = 1 / 127.5, mean: float = 1.0,
-               std: float = 1.0, swap_rb: bool = True, cubic: bool = False, device=None) -> torch.Tensor:
+               std: float = 1.0, swap_rb: bool = True, cubic: bool = False, device=None,
+               replicate: bool = False) -> torch.Tensor:
     """Warp F crops (inverse 3x3 maps ``minv`` [F, 3, 3], dst->src) from uint8 RGB images into
     bf16 NHWC [F, OH, OW, cpad]: value = (px * scale - mean) / std, channels reversed if swap_rb.
-    Default = ArcFace preprocessing (x/127.5 - 1 == (x/255 - 0.5)/0.5, BGR)."""
+    Default = ArcFace preprocessing (x/127.5 - 1 == (x/255 - 0.5)/0.5, BGR).  ``replicate``
+    selects cv2 BORDER_REPLICATE instead of the constant-0 border."""
     F = len(img_index)
     OH, OW = out_hw
     ow = list(out_w) if out_w is not None else [OW] * F
@@ -197,7 +199,8 @@ def warp_batch(images: Sequence[np.ndarray], img_index: Sequence[int], minv: np.
                             dtype=torch.long).to(device)
         mv = torch.from_numpy(np.ascontiguousarray(minv, np.float32).reshape(F, 9)).to(device)
         out = torch.empty((F, OH, OW, cpad), device=device, dtype=torch.bfloat16)
-        hip_ops().warp_batch(src, meta, mv, out, float(scale), float(mean), float(std), bool(swap_rb), bool(cubic))
+        hip_ops().warp_batch(src, meta, mv, out, float(scale), float(mean), float(std), bool(swap_rb), bool(cubic),
+                             bool(replicate))
         return out
     out = torch.zeros((F, OH, OW, cpad), dtype=torch.float32)
     ys, xs = np.mgrid[0:OH, 0:OW].astype(np.float32)
@@ -217,6 +220,8 @@ def warp_batch(images: Sequence[np.ndarray], img_index: Sequence[int], minv: np.
             for dx in taps:
                 xx, yy = x0 + dx, y0 + dy
                 ok = (xx >= 0) & (yy >= 0) & (xx < w) & (yy < h)
+                if replicate:
+                    ok = np.ones_like(ok)
                 if cubic:
                     wt = _cub(dx - fx) * _cub(dy - fy)
                 else:
@@ -239,22 +244,26 @@ def _cub(x):
 
 
 # --------------------------------------------------------------------------- CTC
-def ctc_greedy(probs: torch.Tensor, blank: int = 0):
-    """probs [B, T, C] (softmax output) -> (ids list per sequence, mean confidence per sequence)."""
+def ctc_greedy(probs: torch.Tensor, blank: int = 0, from_logits: bool = False,
+               tlen: Optional[Sequence[int]] = None):
+    """probs [B, T, C] (softmax output, or raw logits with ``from_logits``) -> (ids list per
+    sequence, mean confidence per sequence).  ``tlen`` limits each sequence to its valid
+    time steps (width-padded recogniser batches)."""
     B, T, C = probs.shape
     if probs.is_cuda:
         ids = torch.empty((B, T), dtype=torch.int32, device=probs.device)
         ln = torch.empty((B,), dtype=torch.int32, device=probs.device)
         cf = torch.empty((B,), dtype=torch.float32, device=probs.device)
-        hip_ops().ctc_greedy(probs.float().contiguous(), int(blank), ids, ln, cf)
+        tl = torch.tensor(list(tlen), dtype=torch.int32).to(probs.device) if tlen is not None else None
+        hip_ops().ctc_greedy(probs.float().contiguous(), int(blank), ids, ln, cf, bool(from_logits), tl)
         ids, ln, cf = ids.cpu(), ln.cpu(), cf.cpu()
         return [ids[b, : int(ln[b])].tolist() for b in range(B)], cf.tolist()
-    p = probs.float()
+    p = torch.softmax(probs.float(), -1) if from_logits else probs.float()
     conf, idx = p.max(dim=-1)
     seqs, confs = [], []
     for b in range(B):
         out, cs, prev = [], [], -1
-        for t in range(T):
+        for t in range(T if tlen is None else min(int(tlen[b]), T)):
             c = int(idx[b, t])
             if c != blank and c != prev:
                 out.append(c)

@@ -1,0 +1,335 @@
+"""MI355X OCR backend (L2): DBNet detection -> geometry -> batched crops -> SVTR CTC.
+
+Behaviour of the reference ``OnnxOcrBackend``
+(packages/lumen-ocr/src/lumen_ocr/backends/onnxrt_backend.py:43-632):
+
+* configs from ``model_info.extra_metadata.{det_config, rec_config}`` with the same
+  defaults (det ImageNet mean/std on BGR, scale 1/255, ``limit_side_len`` 960,
+  ``thresh`` 0.3, ``box_thresh`` 0.6, ``unclip_ratio`` 1.5; rec mean/std 0.5,
+  ``image_shape`` [3, 48, 320]) — :242-268;
+* vocabulary file + optional space, blank inserted at index 0 — :103-114;
+* det: resize so the long side <= limit, each side rounded to x32 (cv2 linear),
+  normalise, DBNet, threshold bitmap -> components -> min-area rect -> box score ->
+  unclip -> min-area rect -> rescale/clip (host C++ ``lumen_db_boxes``) — :318-476;
+* reading-order sort — :478-494;
+* crop: perspective warp of each quad (cubic, border replicate), rotate 90 deg if
+  h/w >= 1.5, resize to height 48 keeping aspect — :496-594;
+* greedy CTC, mean max-prob confidence, ``score >= rec_threshold`` kept — :596-632.
+
+MI355X design: detection images of equal resized shape share one forward; the prob
+map is the only D2H copy on the det side; every text crop of every image in the
+batch is produced by ONE perspective-warp kernel that fuses the crop, the optional
+rotation and the height-48 resize into a single 3x3 inverse map (one cubic
+resampling instead of the reference's warp + resize pair) and writes bf16 NHWC8
+directly into width-bucketed recogniser batches; the recogniser runs per bucket
+with padded time steps masked in attention (kv_len) and in the CTC collapse (tlen);
+softmax is fused into the CTC arg-max kernel.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from ... import ops
+from ...models.ocr import DBNet, DBNetConfig, RecConfig, SVTRRecognizer
+from ...ops import vision
+from ...resources.exceptions import ResourceNotFoundError
+from ...runtime.batcher import DynamicBatcher
+from ...utils.image import decode_rgb
+from ..common import BackendInfo, GenericResources, load_safetensors, pick_device, runtime_name
+
+log = logging.getLogger("lumen.ocr.backend")
+
+
+class BackendError(Exception):
+    pass
+
+
+class BackendNotInitializedError(BackendError):
+    pass
+
+
+class InvalidInputError(BackendError):
+    pass
+
+
+class ModelLoadingError(BackendError):
+    pass
+
+
+@dataclass
+class OcrResult:
+    box: list            # [(x, y)] * 4, clockwise from top-left, source-image pixels
+    text: str
+    confidence: float
+
+
+@dataclass
+class OcrParams:
+    det_thresh: float = 0.3
+    rec_thresh: float = 0.5
+    box_thresh: float = 0.6
+    unclip_ratio: float = 1.5
+    use_angle_cls: bool = False
+
+
+DET_DEFAULTS = {"mean": [0.485, 0.456, 0.406], "std": [0.229, 0.224, 0.225], "scale": 1.0 / 255.0,
+                "limit_side_len": 960, "thresh": 0.3, "box_thresh": 0.6, "unclip_ratio": 1.5}
+REC_DEFAULTS = {"mean": [0.5, 0.5, 0.5], "std": [0.5, 0.5, 0.5], "scale": 1.0 / 255.0, "image_shape": [3, 48, 320]}
+
+
+def det_resize_shape(h: int, w: int, limit: int) -> tuple[int, int]:
+    """Reference _det_preprocess (onnxrt_backend.py:338-360)."""
+    ratio = 1.0
+    if max(h, w) > limit:
+        ratio = float(limit) / h if h > w else float(limit) / w
+    rh, rw = int(h * ratio), int(w * ratio)
+    rh = max(int(round(rh / 32) * 32), 32)
+    rw = max(int(round(rw / 32) * 32), 32)
+    return rh, rw
+
+
+def sorted_boxes(boxes: Sequence[np.ndarray]) -> list[np.ndarray]:
+    """Reference _sorted_boxes (:478-494): by (y, x) of the first point, then a bubble pass
+    swapping neighbours on the same line (|dy| < 10) into left-to-right order."""
+    b = sorted(boxes, key=lambda x: (x[0][1], x[0][0]))
+    for i in range(len(b) - 1):
+        for j in range(i, -1, -1):
+            if abs(b[j + 1][0][1] - b[j][0][1]) < 10 and b[j + 1][0][0] < b[j][0][0]:
+                b[j], b[j + 1] = b[j + 1], b[j]
+            else:
+                break
+    return b
+
+
+def _perspective(src: np.ndarray, dst: np.ndarray) -> np.ndarray:
+    """3x3 homography mapping 4 src points to 4 dst points (cv2.getPerspectiveTransform)."""
+    A, bvec = [], []
+    for (x, y), (u, v) in zip(src.astype(np.float64), dst.astype(np.float64)):
+        A.append([x, y, 1, 0, 0, 0, -u * x, -u * y]); bvec.append(u)
+        A.append([0, 0, 0, x, y, 1, -v * x, -v * y]); bvec.append(v)
+    try:
+        h = np.linalg.solve(np.array(A), np.array(bvec))
+    except np.linalg.LinAlgError:
+        h = np.linalg.lstsq(np.array(A), np.array(bvec), rcond=None)[0]
+    return np.append(h, 1.0).reshape(3, 3)
+
+
+def crop_map(box: np.ndarray, rec_h: int) -> tuple[np.ndarray, int]:
+    """Inverse map (rec-input pixel -> source pixel) fusing the reference's perspective crop,
+    rot90 for tall crops and the height-``rec_h`` resize; returns (minv 3x3, resize_w)."""
+    pts = box.astype(np.float32)
+    cw = int(max(np.linalg.norm(pts[0] - pts[1]), np.linalg.norm(pts[2] - pts[3])))
+    ch = int(max(np.linalg.norm(pts[0] - pts[3]), np.linalg.norm(pts[1] - pts[2])))
+    cw, ch = max(cw, 1), max(ch, 1)
+    dst = np.array([[0, 0], [cw, 0], [cw, ch], [0, ch]], np.float32)
+    Minv = np.linalg.inv(_perspective(pts, dst))            # crop pixel -> source pixel
+    rot = ch * 1.0 / cw >= 1.5
+    if rot:   # np.rot90 (CCW): rotated (x, y) = crop (cw - 1 - y, x); rotated is ch wide, cw high
+        R = np.array([[0, -1, cw - 1], [1, 0, 0], [0, 0, 1]], np.float64)
+        wr, hr = ch, cw
+    else:
+        R = np.eye(3)
+        wr, hr = cw, ch
+    resize_w = max(1, math.ceil(wr * rec_h / hr))
+    sx, sy = wr / resize_w, hr / rec_h                       # cv2 linear resize, half-pixel centres
+    S = np.array([[sx, 0, 0.5 * sx - 0.5], [0, sy, 0.5 * sy - 0.5], [0, 0, 1]], np.float64)
+    return (Minv @ R @ S).astype(np.float32), resize_w
+
+
+class MI355XOcrBackend:
+    def __init__(self, resources: GenericResources, device: Optional[str] = None, max_batch: int = 16,
+                 max_wait_ms: float = 2.0, rec_batch: int = 256, bucket: int = 32):
+        self.resources = resources
+        self.device_pref = device
+        self.max_batch = max_batch
+        self.max_wait_ms = max_wait_ms
+        self.rec_batch = rec_batch
+        self.bucket = bucket
+        self.is_initialized = False
+        self.load_time = 0.0
+        self.det: Optional[DBNet] = None
+        self.rec: Optional[SVTRRecognizer] = None
+        self._batcher: Optional[DynamicBatcher] = None
+        self.character_str: list[str] = []
+
+    # ------------------------------------------------------------------ lifecycle
+    def initialize(self) -> None:
+        if self.is_initialized:
+            return
+        t0 = time.time()
+        r = self.resources
+        extra = r.extra
+        self.det_config = {**DET_DEFAULTS, **(extra.get("det_config") or {})}
+        self.rec_config = {**REC_DEFAULTS, **(extra.get("rec_config") or {})}
+        try:
+            vocab_path = r.get_model_file(self.rec_config.get("character_dict_path", "ppocr_keys_v1.txt"))
+            lines = vocab_path.read_bytes().decode("utf-8").split("\n")
+            if lines and lines[-1] == "":
+                lines = lines[:-1]
+            chars = [ln.strip("\r") for ln in lines]
+        except Exception as e:
+            raise ModelLoadingError(f"Failed to load vocab file: {e}") from e
+        if self.rec_config.get("use_space_char", True):
+            chars.append(" ")
+        self.character_str = ["blank"] + chars
+        cfgp = r.model_root_path / "lumen_ocr_config.json"
+        if not cfgp.exists():
+            raise ResourceNotFoundError(f"{r.model_name}: lumen_ocr_config.json missing (MI355X OCR weights are "
+                                        "loaded from detection/recognition.safetensors)")
+        meta = json.loads(cfgp.read_text())
+        dcfg = DBNetConfig(**{k: _tup(v) for k, v in meta["det"].items()})
+        rcfg = RecConfig(**{k: _tup(v) for k, v in meta["rec"].items()})
+        self.device = pick_device(self.device_pref)
+        self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        det, rec = DBNet(dcfg), SVTRRecognizer(rcfg)
+        try:
+            det.load_state_dict(load_safetensors(r.get_model_file("detection.safetensors")))
+            rec.load_state_dict(load_safetensors(r.get_model_file("recognition.safetensors")))
+        except Exception as e:
+            raise ModelLoadingError(f"Initialization failed: {e}") from e
+        self.det, self.rec = det.to(self.device).eval(), rec.to(self.device).eval()
+        self.rec_h = int(self.rec_config["image_shape"][1])
+        self._batcher = DynamicBatcher(self._predict_batch, self.max_batch, self.max_wait_ms, "ocr")
+        self.load_time = time.time() - t0
+        self.is_initialized = True
+        log.info("OCR %s ready on %s in %.2fs (%d classes)", r.model_name, self.device, self.load_time,
+                 len(self.character_str))
+
+    def close(self) -> None:
+        if self._batcher is not None:
+            self._batcher.close()
+
+    # ------------------------------------------------------------------ detection
+    @torch.no_grad()
+    def detect(self, images: Sequence[np.ndarray], params: Sequence[OcrParams]) -> list[list[np.ndarray]]:
+        """decoded RGB images -> per image list of int boxes [4, 2] in reading order."""
+        dc = self.det_config
+        limit = int(dc["limit_side_len"])
+        shapes = [det_resize_shape(im.shape[0], im.shape[1], limit) for im in images]
+        groups: dict = {}
+        for i, s in enumerate(shapes):
+            groups.setdefault(s, []).append(i)
+        out: list = [None] * len(images)
+        for (rh, rw), idx in groups.items():
+            geoms, off, tens = [], 0, []
+            for i in idx:
+                h, w = images[i].shape[:2]
+                geoms.append(ops.ImageGeom.resize(h, w, off, rh, rw))
+                off += images[i].size
+                tens.append(torch.from_numpy(np.ascontiguousarray(images[i])))
+            x = ops.image_prep(tens, (rh, rw), mean=dc["mean"], std=dc["std"], scale=float(dc["scale"]),
+                               filter="cv2_linear", layout="nhwc8", swap_rb=True, geoms=geoms, out_dtype=self.dtype,
+                               device=self.device)
+            prob = self.det(x).float().cpu().numpy()
+            for j, i in enumerate(idx):
+                h, w = images[i].shape[:2]
+                p = params[i]
+                boxes, _ = vision.db_boxes(prob[j], thresh=p.det_thresh, box_thresh=p.box_thresh,
+                                           unclip_ratio=p.unclip_ratio, scale_xy=(w / rw, h / rh), src_wh=(w, h))
+                out[i] = sorted_boxes(list(boxes))
+        return out
+
+    # ------------------------------------------------------------------ recognition
+    @torch.no_grad()
+    def recognize(self, images: Sequence[np.ndarray], crops: Sequence[tuple[int, np.ndarray]]
+                  ) -> list[tuple[str, float]]:
+        """crops: (image index, box [4, 2]) -> (text, confidence) per crop."""
+        if not crops:
+            return []
+        rc = self.rec_config
+        H = self.rec_h
+        maps = [crop_map(b, H) for _, b in crops]
+        order = sorted(range(len(crops)), key=lambda k: maps[k][1])
+        res: list = [None] * len(crops)
+        mean = float(np.mean(rc["mean"]))
+        std = float(np.mean(rc["std"]))
+        scale = float(rc["scale"])
+        for s in range(0, len(order), self.rec_batch):
+            chunk = order[s:s + self.rec_batch]
+            widths = [maps[k][1] for k in chunk]
+            Wb = max(self.bucket, -(-max(widths) // self.bucket) * self.bucket)
+            minv = np.stack([maps[k][0] for k in chunk])
+            x = vision.warp_batch(images, [crops[k][0] for k in chunk], minv, (H, Wb), out_w=widths, cpad=8,
+                                  scale=scale / std, mean=mean / std, std=1.0, swap_rb=True, cubic=True,
+                                  replicate=True, device=self.device)
+            if x.dtype != self.dtype:
+                x = x.to(self.dtype)
+            logits = self.rec(x, valid_w=widths)
+            ts = self.rec.time_stride
+            ids, conf = vision.ctc_greedy(logits, blank=0, from_logits=True,
+                                          tlen=[-(-w // ts) for w in widths])
+            for k, seq, c in zip(chunk, ids, conf):
+                res[k] = ("".join(self.character_str[i] for i in seq if 0 < i < len(self.character_str)), float(c))
+        return res
+
+    # ------------------------------------------------------------------ end to end
+    def _predict_batch(self, items):
+        imgs = [it[0] for it in items]
+        params = [it[1] for it in items]
+        boxes = self.detect(imgs, params)
+        crops = [(i, b) for i, bs in enumerate(boxes) for b in bs]
+        texts = self.recognize(imgs, crops)
+        outs: list = [[] for _ in items]
+        for (i, b), (text, score) in zip(crops, texts):
+            if score >= params[i].rec_thresh:
+                outs[i].append(OcrResult(box=[(int(x), int(y)) for x, y in b.tolist()], text=text,
+                                         confidence=min(max(score, 0.0), 1.0)))
+        return outs
+
+    def _ensure(self):
+        if not self.is_initialized:
+            raise BackendNotInitializedError("Backend not initialized")
+
+    def predict(self, image_bytes: bytes, det_threshold: float = 0.3, rec_threshold: float = 0.5,
+                use_angle_cls: bool = False, **kwargs) -> list[OcrResult]:
+        self._ensure()
+        if not image_bytes:
+            raise InvalidInputError("Failed to decode image bytes")
+        try:
+            img = decode_rgb(image_bytes)
+        except ValueError as e:
+            raise InvalidInputError(f"Failed to decode image bytes: {e}") from e
+        p = OcrParams(det_thresh=float(det_threshold), rec_thresh=float(rec_threshold),
+                      box_thresh=float(kwargs.get("box_thresh", self.det_config["box_thresh"])),
+                      unclip_ratio=float(kwargs.get("unclip_ratio", self.det_config["unclip_ratio"])),
+                      use_angle_cls=bool(use_angle_cls))
+        return self._batcher((img, p))
+
+    def get_info(self) -> BackendInfo:
+        r = self.resources
+        dev = getattr(self, "device", None)
+        cuda = dev is not None and dev.type == "cuda"
+        return BackendInfo(runtime=runtime_name(dev) if dev is not None else "mi355x-hip",
+                           device=str(dev or self.device_pref), model_id=r.model_id, model_name=r.model_name,
+                           version=r.model_info.version, precisions=("bf16",) if cuda or dev is None else ("fp32",),
+                           extra={"det_model_id": f"{r.model_info.name}_det", "rec_model_id": f"{r.model_info.name}_rec",
+                                  "num_classes": str(len(self.character_str)),
+                                  "limit_side_len": str(getattr(self, "det_config", DET_DEFAULTS)["limit_side_len"])})
+
+
+def _tup(v):
+    if isinstance(v, list):
+        return tuple(_tup(x) for x in v)
+    return v
+
+
+def create_backend(settings, resources: GenericResources, runtime: Optional[str] = None) -> MI355XOcrBackend:
+    """Factory (reference backends/factory.py:75-146: only onnx registered; torch accepted here)."""
+    rt = runtime or resources.runtime
+    if rt not in ("onnx", "torch", "rknn"):
+        raise ValueError(f"unsupported runtime '{rt}'")
+    if rt == "rknn":
+        raise BackendError("RKNN runtime is not available on MI355X builds")
+    from ...resources.config import AmdRuntimeSettings
+
+    amd = AmdRuntimeSettings.from_env()
+    dev = getattr(settings, "device", None) if settings is not None else None
+    return MI355XOcrBackend(resources, device=dev, max_batch=min(amd.max_batch, 16), max_wait_ms=amd.max_wait_ms)

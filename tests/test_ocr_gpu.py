@@ -1,0 +1,72 @@
+"""OCR models / service on the MI355X path vs the fp32 CPU reference."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from lumen_amd.models.ocr import DBNET_PRESETS, REC_PRESETS, DBNet, SVTRRecognizer, write_ocr_model
+from lumen_amd.resources.validator import config_from_dict
+from lumen_amd.services.ocr import GeneralOcrService
+from lumen_amd.utils.image import encode_png
+
+pytestmark = pytest.mark.gpu
+
+
+def test_dbnet_mobile_full_size():
+    g = torch.Generator().manual_seed(0)
+    m = DBNet(DBNET_PRESETS["mobile"])
+    m.random_init(g)
+    x = torch.randn(2, 320, 480, 8, generator=g)
+    x[..., 3:] = 0
+    ref = m(x)
+    got = m.to("cuda")(x.to("cuda", torch.bfloat16)).cpu()
+    assert got.shape == ref.shape == (2, 320, 480)
+    assert (got - ref).abs().max().item() < 0.05
+    assert ((got > 0.3) == (ref > 0.3)).float().mean().item() > 0.98
+
+
+def test_svtr_mobile():
+    g = torch.Generator().manual_seed(1)
+    m = SVTRRecognizer(REC_PRESETS["mobile"])
+    m.random_init(g)
+    x = torch.randn(6, 48, 320, 8, generator=g)
+    x[..., 3:] = 0
+    vw = [320, 300, 200, 96, 64, 33]
+    ref = m(x, valid_w=vw)
+    got = m.to("cuda")(x.to("cuda", torch.bfloat16), valid_w=vw).cpu()
+    C = REC_PRESETS["mobile"].num_classes
+    a, b = got[..., :C].flatten(0, 1), ref[..., :C].flatten(0, 1)
+    cos = torch.nn.functional.cosine_similarity(a, b, dim=-1)
+    assert cos.min().item() > 0.99
+
+
+def _cfg(cache, device):
+    return {
+        "metadata": {"version": "1.0.0", "region": "other", "cache_dir": str(cache)},
+        "deployment": {"mode": "single", "service": "ocr"},
+        "server": {"port": 50555, "host": "127.0.0.1"},
+        "services": {"ocr": {"enabled": True, "package": "lumen_ocr",
+                             "import_info": {"registry_class": "lumen_ocr.general_ocr.GeneralOcrService",
+                                             "add_to_server": "lumen_ocr.proto.ml_service_pb2_grpc.add_InferenceServicer_to_server"},
+                             "backend_settings": {"device": device},
+                             "models": {"general": {"model": "ppocr-tiny", "runtime": "onnx"}}}},
+    }
+
+
+def test_ocr_service_gpu_vs_cpu(tmp_path):
+    write_ocr_model(tmp_path / "models" / "ppocr-tiny", "ppocr-tiny")
+    svcs = {d: GeneralOcrService.from_config(config_from_dict(_cfg(tmp_path, d)).services["ocr"], tmp_path)
+            for d in ("cpu", "cuda")}
+    try:
+        img = encode_png(np.random.default_rng(0).integers(0, 255, (90, 200, 3), dtype=np.uint8))
+        meta = {"detection_threshold": "0.0", "ocr.box_thresh": "0.0", "recognition_threshold": "0.0"}
+        dc = json.loads(svcs["cpu"].handle("ocr", img, "image/png", meta)[0])
+        dg = json.loads(svcs["cuda"].handle("ocr", img, "image/png", meta)[0])
+        assert dg["count"] == dc["count"] >= 1
+        for a, b in zip(dc["items"], dg["items"]):
+            assert np.abs(np.array(a["box"]) - np.array(b["box"])).max() <= 2
+            assert abs(a["confidence"] - b["confidence"]) < 0.05
+    finally:
+        for s in svcs.values():
+            s.close()

@@ -54,8 +54,8 @@ def test_nms_matches_reference():
         np.testing.assert_allclose(g_.numpy(), r_.numpy(), atol=1e-5)
 
 
-@pytest.mark.parametrize("cubic", [False, True])
-def test_warp_batch(cubic):
+@pytest.mark.parametrize("cubic,replicate", [(False, False), (True, False), (True, True)])
+def test_warp_batch(cubic, replicate):
     rng = np.random.default_rng(1)
     imgs = [rng.integers(0, 255, (120, 160, 3), dtype=np.uint8), rng.integers(0, 255, (300, 200, 3), dtype=np.uint8)]
     lms = [np.array([[50, 60], [90, 58], [70, 80], [55, 100], [88, 99]], np.float32),
@@ -63,8 +63,8 @@ def test_warp_batch(cubic):
            np.array([[10, 10], [60, 12], [30, 40], [15, 70], [55, 72]], np.float32)]
     idx = [0, 1, 1]
     minv = np.stack([vision.invert_affine(vision.similarity_transform(l)) for l in lms])
-    ref = vision.warp_batch(imgs, idx, minv, (112, 112), cubic=cubic)
-    got = vision.warp_batch(imgs, idx, minv, (112, 112), cubic=cubic, device=DEV).cpu()
+    ref = vision.warp_batch(imgs, idx, minv, (112, 112), cubic=cubic, replicate=replicate)
+    got = vision.warp_batch(imgs, idx, minv, (112, 112), cubic=cubic, replicate=replicate, device=DEV).cpu()
     diff = (got.float() - ref.float()).abs()
     # 1 LSB of the uint8 rounding (2/255 after normalisation) + bf16 rounding
     assert diff.max().item() < 0.03, diff.max()
@@ -79,5 +79,11 @@ def test_ctc_greedy():
     probs = torch.softmax(logits, -1)
     ids_r, cf_r = vision.ctc_greedy(probs)
     ids, cf = vision.ctc_greedy(probs.to(DEV))
+    assert ids == ids_r
+    np.testing.assert_allclose(cf, cf_r, rtol=1e-4, atol=1e-5)
+    # fused softmax from logits + per-sequence valid lengths
+    tl = [T - (b % 7) * 3 for b in range(B)]
+    ids_r, cf_r = vision.ctc_greedy(logits, from_logits=True, tlen=tl)
+    ids, cf = vision.ctc_greedy(logits.to(DEV), from_logits=True, tlen=tl)
     assert ids == ids_r
     np.testing.assert_allclose(cf, cf_r, rtol=1e-4, atol=1e-5)
