@@ -23,6 +23,8 @@ struct GemmEpi {
   int out_f32;
   const uint16_t* prelu;     // [N] per-channel PReLU slopes (bf16) or null; applied after act
   int post_act;              // activation applied AFTER the residual add (ResNet: relu(conv + x))
+  int glu;                   // SwiGLU: columns interleaved [gate 8 | up 8] per 16; writes silu(g) * u to
+                             // column n/2 .. n/2+8 of C (C has N/2 columns)
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) {
@@ -60,6 +62,14 @@ __device__ __forceinline__ void epi_store16(float* v, int m, int n, int M, int N
         for (int q = 0; q < 16; ++q) if (n + q < N) v[q] += bf2f(b[q]);
       }
     }
+  }
+  if (ep.glu) {
+    float r[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) r[q] = v[q] * fast_rcp(1.f + __expf(-v[q])) * v[8 + q];
+    uint16_t* o = (uint16_t*)C + (int64_t)m * ldc + (n >> 1);
+    *(u32x4_t*)o = pack8(r);
+    return;
   }
   if (ep.act) apply_act_n<16>(v, ep.act);
   if (ep.prelu) {

@@ -1,0 +1,50 @@
+// Decoder-LLM kernels (llm.hip) shared with their torch bindings (ops_llm.cpp).
+//
+// Paged KV cache layout (block = 64 tokens of one sequence):
+//   k_cache [num_blocks, Hkv, 64, D]   token-major rows: the S^T = K Q^T MFMA A-operand
+//                                      reads 16-byte pieces of K rows directly from HBM
+//   v_cache [num_blocks, Hkv, D, 64]   transposed (d-major): the O^T = V^T P^T A-operand
+//                                      needs 8 consecutive tokens of one d -> one 16-byte load
+// so the decode kernel streams both straight from global memory into MFMA
+// fragments with no LDS staging and no transposing reads.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace lumen {
+
+constexpr int KV_BLOCK = 64;
+
+struct RopeKVArgs {
+  uint16_t* qkv;          // [T, ld] bf16: q heads | k heads | v heads (rotated in place)
+  int64_t ld;
+  const int* pos;         // [T] positions
+  const float* cos_sin;   // [max_pos, D/2, 2] (cos, sin)
+  const int64_t* slots;   // [T] cache slot = block * 64 + offset, < 0 = do not cache; null = no cache write
+  uint16_t* k_cache;
+  uint16_t* v_cache;
+  int T, H, Hkv, D;
+};
+hipError_t rope_kv(const RopeKVArgs& a, hipStream_t stream);
+
+struct DecodeArgs {
+  const uint16_t* q;      // [B, q_sb] rows; head h at h * D
+  int64_t q_sb;
+  const uint16_t* k_cache;
+  const uint16_t* v_cache;
+  const int* block_table; // [B, bt_stride]
+  int bt_stride;
+  const int* ctx_len;     // [B] tokens in cache (including the current one)
+  uint16_t* o;            // [B, o_sb] rows; head h at h * D
+  int64_t o_sb;
+  float* part_o;          // [B, H, nsplit, D]   (nsplit > 1)
+  float* part_ml;         // [B, H, nsplit, 2]
+  int H, Hkv, nsplit, blocks_per_split;
+  float scale_log2;
+};
+hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream);
+
+hipError_t rep_penalty(float* logits, int64_t ld, const int* ids, int maxn, const float* penalty, int B, int V,
+                       hipStream_t stream);
+
+}  // namespace lumen

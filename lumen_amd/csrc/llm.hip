@@ -1,0 +1,254 @@
+// Decoder-LLM kernels for the VLM (Qwen2 / Llama family):
+//
+//  * rope_kv: rotary embedding (rotate-half, HF convention) applied in place to
+//    the q and k heads of the packed QKV projection, fused with the paged KV
+//    cache write (k token-major, v transposed; layouts in llm.h).  Prefill
+//    attention then reads q/k/v straight from the rotated QKV buffer.
+//  * paged_decode: flash-decoding over the paged cache.  One workgroup per
+//    (split, kv-head, sequence); the G = H / Hkv query heads sharing a kv head
+//    are the 16 MFMA columns, each wave walks its own 64-token blocks with an
+//    online softmax, the 4 wave states are merged through LDS and — when the
+//    context is split across workgroups — a combine kernel merges the splits.
+//    Both MFMA operands come straight from HBM: S^T = K Q^T reads K rows in a
+//    permuted token order chosen so that each lane's 8 P values are 8
+//    consecutive tokens, which the transposed V cache serves with one 16-byte
+//    load per MFMA (O^T = V^T P^T).
+//  * rep_penalty: repetition penalty on the logits of previously generated
+//    tokens (the reference accepts and ignores it, SURVEY V-7).
+#include "common.h"
+#include "llm.h"
+
+namespace lumen {
+
+// ------------------------------------------------------------------------------ RoPE + KV write
+__global__ void __launch_bounds__(256) rope_kv_kernel(RopeKVArgs a) {
+  const int t = blockIdx.x;
+  const int half = a.D >> 1;
+  const int p = a.pos[t];
+  const float2* cs = reinterpret_cast<const float2*>(a.cos_sin) + (int64_t)p * half;
+  uint16_t* row = a.qkv + (int64_t)t * a.ld;
+  const int64_t slot = a.slots ? a.slots[t] : -1;
+  const int64_t blk = slot >= 0 ? (slot >> 6) : 0;
+  const int off = (int)(slot & 63);
+  const int nrot = (a.H + a.Hkv) * half;
+  for (int idx = threadIdx.x; idx < nrot; idx += blockDim.x) {
+    const int hh = idx / half, i = idx - hh * half;
+    uint16_t* hp = row + hh * a.D;
+    const float x1 = bf2f(hp[i]), x2 = bf2f(hp[i + half]);
+    const float2 c = cs[i];
+    const float y1 = x1 * c.x - x2 * c.y, y2 = x2 * c.x + x1 * c.y;
+    const uint16_t b1 = f2bf(y1), b2 = f2bf(y2);
+    hp[i] = b1;
+    hp[i + half] = b2;
+    if (hh >= a.H && slot >= 0) {
+      uint16_t* kr = a.k_cache + ((blk * a.Hkv + (hh - a.H)) * KV_BLOCK + off) * a.D;
+      kr[i] = b1;
+      kr[i + half] = b2;
+    }
+  }
+  if (slot >= 0) {
+    const uint16_t* vr = row + (a.H + a.Hkv) * a.D;
+    for (int idx = threadIdx.x; idx < a.Hkv * a.D; idx += blockDim.x) {
+      const int kh = idx / a.D, d = idx - kh * a.D;
+      a.v_cache[((blk * a.Hkv + kh) * a.D + d) * KV_BLOCK + off] = vr[idx];
+    }
+  }
+}
+
+hipError_t rope_kv(const RopeKVArgs& a, hipStream_t stream) {
+  if (a.T == 0) return hipSuccess;
+  hipLaunchKernelGGL(rope_kv_kernel, dim3(a.T), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ paged decode attention
+template <int D>
+__global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
+  constexpr int KS = D / 32;   // k-steps of S^T over the head dim
+  constexpr int NB = D / 16;   // 16-wide d blocks of O^T
+  __shared__ float sm_ml[4][2][16];
+  __shared__ float sm_o[4][D][17];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int G = a.H / a.Hkv;
+  const int ctx = a.ctx_len[b];
+  const int nblk = (ctx + KV_BLOCK - 1) / KV_BLOCK;
+  const int blk0 = split * a.blocks_per_split;
+  const int blk1 = min(blk0 + a.blocks_per_split, nblk);
+
+  // Q^T fragment (B operand): column = query head hk*G + col (zero beyond G)
+  bf16x8_t qf[KS];
+  {
+    const bool qv = col < G;
+    const uint16_t* qp = a.q + (int64_t)b * a.q_sb + (int64_t)(hk * G + (qv ? col : 0)) * D;
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+      u32x4_t w = *(const u32x4_t*)(qp + t * 32 + g * 8);
+      if (!qv) w = (u32x4_t){0u, 0u, 0u, 0u};
+      qf[t] = __builtin_bit_cast(bf16x8_t, w);
+    }
+  }
+  f32x4_t o[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) o[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  float mrow = -INFINITY, lrow = 0.f;
+
+  for (int bi = blk0 + wid; bi < blk1; bi += 4) {
+    const int phys = a.block_table[(int64_t)b * a.bt_stride + bi];
+    const uint16_t* kb = a.k_cache + ((int64_t)phys * a.Hkv + hk) * KV_BLOCK * D;
+    const uint16_t* vb = a.v_cache + ((int64_t)phys * a.Hkv + hk) * D * KV_BLOCK;
+    const int valid = min(KV_BLOCK, ctx - bi * KV_BLOCK);
+
+    // S^T tiles: tile kb16 = (s = kb16 >> 1, hf = kb16 & 1); MFMA row i <-> token
+    // 32s + 8(i >> 2) + 4hf + (i & 3), so C row 4g + r holds token 32s + 8g + 4hf + r.
+    f32x4_t sc[4];
+#pragma unroll
+    for (int kb16 = 0; kb16 < 4; ++kb16) {
+      const int tok = 32 * (kb16 >> 1) + 8 * (col >> 2) + 4 * (kb16 & 1) + (col & 3);
+      const uint16_t* kr = kb + (int64_t)tok * D + g * 8;
+      bf16x8_t kf[KS];
+#pragma unroll
+      for (int t = 0; t < KS; ++t) kf[t] = *(const bf16x8_t*)(kr + t * 32);
+      sc[kb16] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < KS; ++t) sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t], qf[t], sc[kb16], 0, 0, 0);
+    }
+    float mx = mrow;
+#pragma unroll
+    for (int kb16 = 0; kb16 < 4; ++kb16)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tok = 32 * (kb16 >> 1) + 8 * g + 4 * (kb16 & 1) + r;
+        const float sv = tok < valid ? sc[kb16][r] * a.scale_log2 : -INFINITY;
+        sc[kb16][r] = sv;
+        mx = fmaxf(mx, sv);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mbase = mx == -INFINITY ? 0.f : mx;
+    const float alpha = exp2f(mrow - mbase);
+    float rs = 0.f;
+#pragma unroll
+    for (int kb16 = 0; kb16 < 4; ++kb16)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(sc[kb16][r] - mbase);
+        sc[kb16][r] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    lrow = lrow * alpha + rs;
+    mrow = mx;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) o[j] *= alpha;
+
+    // O^T += V^T P^T over two 32-token steps; lane's P k-slots 8g + j = tokens 32s + 8g + j
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (32 * s >= valid) break;
+      bf16x8_t pf;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pf[r] = (__bf16)sc[2 * s][r];
+        pf[4 + r] = (__bf16)sc[2 * s + 1][r];
+      }
+      const uint16_t* vr = vb + (int64_t)col * KV_BLOCK + 32 * s + 8 * g;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const bf16x8_t vf = *(const bf16x8_t*)(vr + (int64_t)j * 16 * KV_BLOCK);
+        o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[j], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- merge the 4 wave states through LDS
+  if (g == 0) {
+    sm_ml[wid][0][col] = mrow;
+    sm_ml[wid][1][col] = lrow;
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sm_o[wid][j * 16 + 4 * g + r][col] = o[j][r];
+  __syncthreads();
+  for (int idx = tid; idx < G * D; idx += 256) {
+    const int q = idx / D, d = idx - q * D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm_ml[w][0][q]);
+    float L = 0.f, O = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float e = exp2f(sm_ml[w][0][q] - M);
+        L += sm_ml[w][1][q] * e;
+        O += sm_o[w][d][q] * e;
+      }
+    }
+    const int h = hk * G + q;
+    if (a.nsplit == 1) {
+      a.o[(int64_t)b * a.o_sb + (int64_t)h * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+    } else {
+      const int64_t pi = ((int64_t)b * a.H + h) * a.nsplit + split;
+      a.part_o[pi * D + d] = O;
+      if (d == 0) {
+        a.part_ml[pi * 2] = M;
+        a.part_ml[pi * 2 + 1] = L;
+      }
+    }
+  }
+}
+
+__global__ void decode_combine_kernel(DecodeArgs a, int D) {
+  const int bh = blockIdx.x;
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int64_t base = (int64_t)bh * a.nsplit;
+  float M = -INFINITY;
+  for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, a.part_ml[(base + s) * 2]);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float L = 0.f, O = 0.f;
+    if (M != -INFINITY) {
+      for (int s = 0; s < a.nsplit; ++s) {
+        const float e = exp2f(a.part_ml[(base + s) * 2] - M);
+        L += a.part_ml[(base + s) * 2 + 1] * e;
+        O += a.part_o[(base + s) * D + d] * e;
+      }
+    }
+    a.o[(int64_t)b * a.o_sb + (int64_t)h * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+  }
+}
+
+hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream) {
+  dim3 grid(a.nsplit, a.Hkv, B), block(256);
+  if (D == 64) hipLaunchKernelGGL(paged_decode_kernel<64>, grid, block, 0, stream, a);
+  else if (D == 128) hipLaunchKernelGGL(paged_decode_kernel<128>, grid, block, 0, stream, a);
+  else return hipErrorInvalidValue;
+  if (a.nsplit > 1) hipLaunchKernelGGL(decode_combine_kernel, dim3(B * a.H), dim3(128), 0, stream, a, D);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ repetition penalty
+__global__ void rep_penalty_kernel(float* logits, int64_t ld, const int* ids, int maxn, const float* penalty, int V) {
+  const int b = blockIdx.x;
+  const float p = penalty[b];
+  for (int j = threadIdx.x; j < maxn; j += blockDim.x) {
+    const int id = ids[(int64_t)b * maxn + j];
+    if (id < 0 || id >= V) continue;
+    float* l = logits + (int64_t)b * ld + id;
+    const float v = *l;
+    *l = v > 0.f ? v / p : v * p;
+  }
+}
+
+hipError_t rep_penalty(float* logits, int64_t ld, const int* ids, int maxn, const float* penalty, int B, int V,
+                       hipStream_t stream) {
+  if (B == 0 || maxn == 0) return hipSuccess;
+  hipLaunchKernelGGL(rep_penalty_kernel, dim3(B), dim3(256), 0, stream, logits, ld, ids, maxn, penalty, V);
+  return hipGetLastError();
+}
+
+}  // namespace lumen

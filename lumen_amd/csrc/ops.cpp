@@ -73,7 +73,7 @@ void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tens
           const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& table,
           int64_t table_period, int64_t table_offset, int64_t act, double alpha, at::Tensor out,
           int64_t out_group, int64_t out_group_stride, int64_t out_row_offset, int64_t tile,
-          const c10::optional<at::Tensor>& prelu) {
+          const c10::optional<at::Tensor>& prelu, int64_t glu) {
   check_bf16_rows(a, "a");
   check_bf16_rows(w, "w");
   const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
@@ -81,7 +81,9 @@ void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tens
   TORCH_CHECK(K % 64 == 0, "gemm: K must be a multiple of 64 (pad weights), got ", K);
   TORCH_CHECK(N % 16 == 0, "gemm: N must be a multiple of 16, got ", N);
   check_gpu(out, "out");
-  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) >= N, "gemm: bad out");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) >= (glu ? N / 2 : N), "gemm: bad out");
+  TORCH_CHECK(!glu || (out.scalar_type() == at::kBFloat16 && out_group == 0 && !(residual.has_value() && residual->defined())),
+              "gemm: glu epilogue writes bf16 rows without residual / row remap");
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "gemm: out dtype");
   const int64_t last = M - 1;
   const int64_t need_rows = out_group > 0 ? (last / out_group) * out_group_stride + out_row_offset + last % out_group + 1 : M;
@@ -112,6 +114,8 @@ void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tens
   ep.out_group_stride = out_group_stride;
   ep.out_row_offset = (int)out_row_offset;
   ep.out_f32 = out.scalar_type() == at::kFloat;
+  ep.glu = (int)glu;
+  if (glu) TORCH_CHECK(out.stride(0) % 8 == 0, "gemm: glu out rows must be 16-byte aligned");
   if (prelu.has_value() && prelu->defined()) {
     TORCH_CHECK(prelu->scalar_type() == at::kBFloat16 && prelu->numel() >= N && prelu->is_contiguous(), "gemm: prelu");
     ep.prelu = bf(*prelu);
@@ -409,7 +413,7 @@ void pixel_shuffle_up(const at::Tensor& y, at::Tensor out, int64_t factor) {
 TORCH_LIBRARY(lumen, m) {
   m.def("gemm(Tensor a, Tensor w, Tensor? bias, Tensor? residual, Tensor? table, int table_period, "
         "int table_offset, int act, float alpha, Tensor(o!) out, int out_group, int out_group_stride, "
-        "int out_row_offset, int tile, Tensor? prelu=None) -> ()");
+        "int out_row_offset, int tile, Tensor? prelu=None, int glu=0) -> ()");
   m.def("norm(Tensor x, Tensor? row_idx, Tensor? add, Tensor(r!)? resid_out, Tensor w, Tensor? b, "
         "Tensor(o!) out, float eps, int mode) -> ()");
   m.def("l2norm_(Tensor(a!) x, float eps) -> ()");

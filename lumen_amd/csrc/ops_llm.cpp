@@ -1,0 +1,127 @@
+// torch.ops.lumen.* registration of the decoder-LLM kernels (llm.hip): fused RoPE +
+// paged KV-cache write, paged flash-decoding attention, repetition penalty.
+#include <ATen/ATen.h>
+#include <ATen/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+#include <torch/library.h>
+
+#include "llm.h"
+
+namespace {
+
+#define CHECK_HIP3(expr)                                                                   \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    TORCH_CHECK(_e == hipSuccess, "lumen HIP error: ", hipGetErrorString(_e), " @ ", #expr); \
+  } while (0)
+
+inline hipStream_t cur() { return c10::hip::getCurrentHIPStream().stream(); }
+inline uint16_t* bfp(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+void check_cache(const at::Tensor& kc, const at::Tensor& vc, int64_t Hkv, int64_t D) {
+  TORCH_CHECK(kc.is_cuda() && kc.scalar_type() == at::kBFloat16 && kc.is_contiguous() && kc.dim() == 4,
+              "k_cache: bf16 [NB, Hkv, 64, D]");
+  TORCH_CHECK(vc.is_cuda() && vc.scalar_type() == at::kBFloat16 && vc.is_contiguous() && vc.dim() == 4,
+              "v_cache: bf16 [NB, Hkv, D, 64]");
+  TORCH_CHECK(kc.size(1) == Hkv && kc.size(2) == lumen::KV_BLOCK && kc.size(3) == D, "k_cache shape");
+  TORCH_CHECK(vc.size(0) == kc.size(0) && vc.size(1) == Hkv && vc.size(2) == D && vc.size(3) == lumen::KV_BLOCK,
+              "v_cache shape");
+}
+
+// qkv [T, >= (H + 2 Hkv) D] bf16 (rotated in place); pos int32 [T]; cos_sin f32 [P, D/2, 2];
+// slots int64 [T] (optional): writes rotated k / v into the paged cache.
+void rope_kv(at::Tensor qkv, const at::Tensor& pos, const at::Tensor& cos_sin, const c10::optional<at::Tensor>& slots,
+             at::Tensor k_cache, at::Tensor v_cache, int64_t H, int64_t Hkv, int64_t D) {
+  TORCH_CHECK(qkv.is_cuda() && qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 2 && qkv.stride(1) == 1, "qkv");
+  TORCH_CHECK(qkv.size(1) >= (H + 2 * Hkv) * D, "qkv: too few columns");
+  TORCH_CHECK(D % 2 == 0 && D <= 256, "rope: head dim");
+  const int64_t T = qkv.size(0);
+  TORCH_CHECK(pos.is_cuda() && pos.scalar_type() == at::kInt && pos.numel() == T && pos.is_contiguous(), "pos int32 [T]");
+  TORCH_CHECK(cos_sin.is_cuda() && cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
+              cos_sin.dim() == 3 && cos_sin.size(1) == D / 2 && cos_sin.size(2) == 2, "cos_sin f32 [P, D/2, 2]");
+  lumen::RopeKVArgs a{};
+  a.qkv = bfp(qkv); a.ld = qkv.stride(0);
+  a.pos = pos.data_ptr<int>(); a.cos_sin = cos_sin.data_ptr<float>();
+  if (slots.has_value() && slots->defined()) {
+    TORCH_CHECK(slots->is_cuda() && slots->scalar_type() == at::kLong && slots->numel() == T && slots->is_contiguous(),
+                "slots int64 [T]");
+    check_cache(k_cache, v_cache, Hkv, D);
+    a.slots = slots->data_ptr<int64_t>();
+    a.k_cache = bfp(k_cache); a.v_cache = bfp(v_cache);
+  }
+  a.T = (int)T; a.H = (int)H; a.Hkv = (int)Hkv; a.D = (int)D;
+  const at::DeviceGuard g(qkv.device());
+  CHECK_HIP3(lumen::rope_kv(a, cur()));
+}
+
+// q [B, >= H D] rows (bf16); block_table int32 [B, max_blocks]; ctx_len int32 [B]; out [B, >= H D] rows.
+void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                  const at::Tensor& block_table, const at::Tensor& ctx_len, at::Tensor out, int64_t H, int64_t Hkv,
+                  double scale, int64_t nsplit, int64_t blocks_per_split, const c10::optional<at::Tensor>& part_o,
+                  const c10::optional<at::Tensor>& part_ml) {
+  const int64_t D = k_cache.size(3);
+  check_cache(k_cache, v_cache, Hkv, D);
+  TORCH_CHECK(D == 64 || D == 128, "paged_decode: head dim 64 or 128");
+  TORCH_CHECK(H % Hkv == 0 && H / Hkv <= 16, "paged_decode: at most 16 query heads per kv head");
+  TORCH_CHECK(q.is_cuda() && q.scalar_type() == at::kBFloat16 && q.dim() == 2 && q.stride(1) == 1 && q.size(1) >= H * D &&
+              q.stride(0) % 8 == 0, "paged_decode: q rows");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kBFloat16 && out.dim() == 2 && out.stride(1) == 1 &&
+              out.size(1) >= H * D, "paged_decode: out rows");
+  const int64_t B = q.size(0);
+  TORCH_CHECK(out.size(0) == B, "paged_decode: out batch");
+  TORCH_CHECK(block_table.is_cuda() && block_table.scalar_type() == at::kInt && block_table.dim() == 2 &&
+              block_table.size(0) == B && block_table.stride(1) == 1, "block_table int32 [B, max_blocks]");
+  TORCH_CHECK(ctx_len.is_cuda() && ctx_len.scalar_type() == at::kInt && ctx_len.numel() == B && ctx_len.is_contiguous(),
+              "ctx_len int32 [B]");
+  TORCH_CHECK(nsplit >= 1 && blocks_per_split >= 1 && nsplit * blocks_per_split >= block_table.size(1),
+              "paged_decode: splits must cover the block table");
+  lumen::DecodeArgs a{};
+  a.q = bfp(q); a.q_sb = q.stride(0);
+  a.k_cache = bfp(k_cache); a.v_cache = bfp(v_cache);
+  a.block_table = block_table.data_ptr<int>(); a.bt_stride = (int)block_table.stride(0);
+  a.ctx_len = ctx_len.data_ptr<int>();
+  a.o = bfp(out); a.o_sb = out.stride(0);
+  a.H = (int)H; a.Hkv = (int)Hkv; a.nsplit = (int)nsplit; a.blocks_per_split = (int)blocks_per_split;
+  a.scale_log2 = (float)(scale * 1.4426950408889634);
+  if (nsplit > 1) {
+    TORCH_CHECK(part_o.has_value() && part_ml.has_value(), "paged_decode: split workspace required");
+    TORCH_CHECK(part_o->scalar_type() == at::kFloat && part_o->is_contiguous() && part_o->numel() >= B * H * nsplit * D,
+                "part_o");
+    TORCH_CHECK(part_ml->scalar_type() == at::kFloat && part_ml->is_contiguous() && part_ml->numel() >= B * H * nsplit * 2,
+                "part_ml");
+    a.part_o = part_o->data_ptr<float>(); a.part_ml = part_ml->data_ptr<float>();
+  }
+  if (B == 0) return;
+  const at::DeviceGuard g(q.device());
+  CHECK_HIP3(lumen::paged_decode(a, (int)B, (int)D, cur()));
+}
+
+void rep_penalty_(at::Tensor logits, const at::Tensor& ids, const at::Tensor& penalty) {
+  TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == at::kFloat && logits.dim() == 2 && logits.stride(1) == 1,
+              "rep_penalty: logits f32 [B, V]");
+  const int64_t B = logits.size(0);
+  TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == at::kInt && ids.is_contiguous() && ids.dim() == 2 && ids.size(0) == B,
+              "rep_penalty: ids int32 [B, n]");
+  TORCH_CHECK(penalty.is_cuda() && penalty.scalar_type() == at::kFloat && penalty.numel() == B, "penalty f32 [B]");
+  const at::DeviceGuard g(logits.device());
+  CHECK_HIP3(lumen::rep_penalty(logits.data_ptr<float>(), logits.stride(0), ids.data_ptr<int>(), (int)ids.size(1),
+                                penalty.data_ptr<float>(), (int)B, (int)logits.size(1), cur()));
+}
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(lumen, m) {
+  m.def("rope_kv(Tensor(a!) qkv, Tensor pos, Tensor cos_sin, Tensor? slots, Tensor(k!) k_cache, Tensor(v!) v_cache, "
+        "int H, int Hkv, int D) -> ()");
+  m.def("paged_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_table, Tensor ctx_len, Tensor(o!) out, "
+        "int H, int Hkv, float scale, int nsplit, int blocks_per_split, Tensor(p!)? part_o=None, "
+        "Tensor(m!)? part_ml=None) -> ()");
+  m.def("rep_penalty_(Tensor(a!) logits, Tensor ids, Tensor penalty) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
+  m.impl("rope_kv", &rope_kv);
+  m.impl("paged_decode", &paged_decode);
+  m.impl("rep_penalty_", &rep_penalty_);
+}

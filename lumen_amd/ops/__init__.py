@@ -76,22 +76,26 @@ def linear(
     out_group_stride: int = 0,
     out_row_offset: int = 0,
     tile: int = -1,
+    glu: bool = False,
 ) -> torch.Tensor:
     """y = epi(alpha * x @ w.T): (+bias) -> act -> (+table[m % P + off]) -> (+residual[orow]).
 
     ``x`` is [M, K] (or [..., K]), ``w`` is [N, K].  With ``out_group`` > 0 row m is
     written to ``(m // G) * GS + RO + m % G`` of ``out`` (patch rows into a token
-    buffer).  ``residual`` is indexed by the *output* row.
+    buffer).  ``residual`` is indexed by the *output* row.  ``glu``: the rows of ``w``
+    interleave [gate 8 | up 8] per 16 (see :func:`glu_interleave`) and the output is
+    silu(gate) * up with N/2 columns (SwiGLU fused into the epilogue).
     """
     lead = x.shape[:-1]
     x2 = x.reshape(-1, x.shape[-1])
     M, K = x2.shape
     N = w.shape[0]
     a = act_id(act)
+    NO = N // 2 if glu else N
     if out is None:
         assert out_group == 0, "out_group needs an explicit out tensor"
-        out = torch.empty((M, N), device=x.device, dtype=out_dtype or x.dtype)
-        ret_shape = (*lead, N)
+        out = torch.empty((M, NO), device=x.device, dtype=out_dtype or x.dtype)
+        ret_shape = (*lead, NO)
     else:
         ret_shape = None
     out2 = out if out.dim() == 2 else out.view(-1, out.shape[-1])
@@ -100,11 +104,15 @@ def linear(
             x2 = x2.contiguous()
         res2 = residual.reshape(-1, residual.shape[-1]) if residual is not None else None
         hip_ops().gemm(x2, w, bias, res2, table, int(table_period), int(table_offset), a, float(alpha), out2,
-                       int(out_group), int(out_group_stride), int(out_row_offset), int(tile))
+                       int(out_group), int(out_group_stride), int(out_row_offset), int(tile), None, int(bool(glu)))
     else:
         y = (x2.float() @ w.float().t()) * alpha
         if bias is not None:
-            y = y + bias.float()
+            y = y + bias.float()[:N]
+        if glu:
+            gu = y.view(M, N // 16, 2, 8)
+            out2[:, :NO] = (F.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(M, NO).to(out2.dtype)
+            return out.view(ret_shape) if ret_shape is not None else out
         y = _act_ref(y, a)
         m = torch.arange(M)
         orow = (m // out_group) * out_group_stride + out_row_offset + m % out_group if out_group > 0 else m
@@ -117,6 +125,13 @@ def linear(
     if ret_shape is not None:
         return out.view(ret_shape)
     return out
+
+
+def glu_interleave(w_gate: torch.Tensor, w_up: torch.Tensor) -> torch.Tensor:
+    """[I, K] gate / up projections -> [2I, K] rows grouped [gate 8 | up 8] per 16 (``linear(glu=True)``)."""
+    I, K = w_gate.shape
+    assert I % 8 == 0 and w_up.shape == w_gate.shape
+    return torch.stack([w_gate.reshape(I // 8, 8, K), w_up.reshape(I // 8, 8, K)], 1).reshape(2 * I, K)
 
 
 # --------------------------------------------------------------------------- norms

@@ -1,0 +1,166 @@
+"""Decoder-LLM ops: RoPE tables, fused RoPE + paged KV write, paged decode attention,
+repetition penalty, candidate sampling.
+
+GPU tensors run the HIP kernels of csrc/llm.hip; CPU tensors run fp32 references with
+the same semantics (cache layouts in csrc/llm.h: k [NB, Hkv, 64, D], v [NB, Hkv, D, 64]).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from .._native import hip_ops
+
+KV_BLOCK = 64
+
+
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float = 10000.0, scaling: Optional[dict] = None) -> torch.Tensor:
+    """[max_pos, D/2, 2] fp32 (cos, sin) with HF inv_freq (+ Llama-3 frequency scaling)."""
+    half = head_dim // 2
+    inv = 1.0 / (theta ** (torch.arange(0, half, dtype=torch.float64) * 2 / head_dim))
+    if scaling and scaling.get("rope_type", scaling.get("type")) == "llama3":
+        f = float(scaling.get("factor", 8.0))
+        lo, hi = float(scaling.get("low_freq_factor", 1.0)), float(scaling.get("high_freq_factor", 4.0))
+        old = float(scaling.get("original_max_position_embeddings", 8192))
+        wl = 2 * math.pi / inv
+        smooth = (old / wl - lo) / (hi - lo)
+        scaled = torch.where(wl > old / lo, inv / f, inv)
+        mid = (wl <= old / lo) & (wl >= old / hi)
+        scaled = torch.where(mid, (1 - smooth) * inv / f + smooth * inv, scaled)
+        inv = scaled
+    elif scaling and scaling.get("rope_type", scaling.get("type")) == "linear":
+        inv = inv / float(scaling.get("factor", 1.0))
+    ang = torch.arange(max_pos, dtype=torch.float64)[:, None] * inv[None, :]
+    return torch.stack([torch.cos(ang), torch.sin(ang)], -1).float().contiguous()
+
+
+def _rot_ref(x: torch.Tensor, cs: torch.Tensor) -> torch.Tensor:
+    """x [T, n, D] fp32, cs [T, D/2, 2] -> rotate-half RoPE."""
+    half = x.shape[-1] // 2
+    c, s = cs[..., 0][:, None, :], cs[..., 1][:, None, :]
+    x1, x2 = x[..., :half], x[..., half:]
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], -1)
+
+
+def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor, H: int, Hkv: int, D: int,
+            slots: Optional[torch.Tensor] = None, k_cache: Optional[torch.Tensor] = None,
+            v_cache: Optional[torch.Tensor] = None) -> None:
+    """Rotate q and k heads of qkv [T, (H + 2Hkv) D] in place; with ``slots`` also write k / v
+    of every token into the paged cache (slot = block * 64 + offset, < 0 skipped)."""
+    T = qkv.shape[0]
+    if qkv.is_cuda:
+        hip_ops().rope_kv(qkv, pos.to(torch.int32).contiguous(), cos_sin,
+                          slots.to(torch.long).contiguous() if slots is not None else None,
+                          k_cache if k_cache is not None else qkv, v_cache if v_cache is not None else qkv,
+                          int(H), int(Hkv), int(D))
+        return
+    if T == 0:
+        return
+    cs = cos_sin[pos.long()]
+    nq = (H + Hkv) * D
+    x = qkv[:, :nq].float().view(T, H + Hkv, D)
+    xr = _rot_ref(x, cs).to(qkv.dtype)
+    qkv[:, :nq] = xr.view(T, nq)
+    if slots is not None:
+        v = qkv[:, nq:nq + Hkv * D].view(T, Hkv, D)
+        for t in range(T):
+            sl = int(slots[t])
+            if sl < 0:
+                continue
+            blk, off = sl // KV_BLOCK, sl % KV_BLOCK
+            k_cache[blk, :, off, :] = xr[t, H:].to(k_cache.dtype)
+            v_cache[blk, :, :, off] = v[t].to(v_cache.dtype)
+
+
+def decode_splits(B: int, Hkv: int, max_blocks: int, target_wg: int = 512) -> tuple[int, int]:
+    """(nsplit, blocks_per_split): enough workgroups to fill 256 CUs, >= 4 blocks (one per wave) per split."""
+    want = max(1, -(-target_wg // max(B * Hkv, 1)))
+    nsplit = max(1, min(want, -(-max_blocks // 4)))
+    bps = -(-max_blocks // nsplit)
+    nsplit = -(-max_blocks // bps)
+    return nsplit, bps
+
+
+def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_table: torch.Tensor,
+                 ctx_len: torch.Tensor, H: int, Hkv: int, scale: Optional[float] = None,
+                 out: Optional[torch.Tensor] = None, workspace: Optional[dict] = None) -> torch.Tensor:
+    """Single-token attention of q [B, H*D] (rows may be views) over each sequence's cached
+    context (ctx_len tokens, including the current token)."""
+    B = q.shape[0]
+    D = k_cache.shape[3]
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if out is None:
+        out = torch.empty((B, H * D), device=q.device, dtype=q.dtype)
+    if q.is_cuda:
+        mb = block_table.shape[1]
+        nsplit, bps = decode_splits(B, Hkv, mb)
+        po = pm = None
+        if nsplit > 1:
+            need = B * H * nsplit
+            ws = workspace if workspace is not None else {}
+            po = ws.get("o")
+            if po is None or po.numel() < need * D:
+                po = torch.empty(need * D, device=q.device, dtype=torch.float32)
+                ws["o"] = po
+            pm = ws.get("ml")
+            if pm is None or pm.numel() < need * 2:
+                pm = torch.empty(need * 2, device=q.device, dtype=torch.float32)
+                ws["ml"] = pm
+        hip_ops().paged_decode(q, k_cache, v_cache, block_table, ctx_len, out, int(H), int(Hkv), float(scale),
+                               int(nsplit), int(bps), po, pm)
+        return out
+    G = H // Hkv
+    for b in range(B):
+        L = int(ctx_len[b])
+        nb = -(-L // KV_BLOCK)
+        blocks = block_table[b, :nb].long()
+        k = k_cache[blocks].float().permute(1, 0, 2, 3).reshape(Hkv, nb * KV_BLOCK, D)[:, :L]
+        v = v_cache[blocks].float().permute(1, 0, 3, 2).reshape(Hkv, nb * KV_BLOCK, D)[:, :L]
+        qb = q[b, :H * D].float().view(Hkv, G, D)
+        s = torch.einsum("hgd,htd->hgt", qb, k) * scale
+        p = torch.softmax(s, -1)
+        o = torch.einsum("hgt,htd->hgd", p, v)
+        out[b, :H * D] = o.reshape(H * D).to(out.dtype)
+    return out
+
+
+def rep_penalty_(logits: torch.Tensor, token_ids: Sequence[Sequence[int]], penalty: Sequence[float]) -> torch.Tensor:
+    """logits[b, t] /= p (if > 0) or *= p for every distinct previously seen token t."""
+    B = logits.shape[0]
+    uniq = [sorted(set(int(t) for t in ids)) for ids in token_ids]
+    maxn = max((len(u) for u in uniq), default=0)
+    if maxn == 0:
+        return logits
+    ids = np.full((B, maxn), -1, np.int32)
+    for b, u in enumerate(uniq):
+        ids[b, :len(u)] = u
+    if logits.is_cuda:
+        hip_ops().rep_penalty_(logits, torch.from_numpy(ids).to(logits.device),
+                               torch.tensor(list(penalty), dtype=torch.float32, device=logits.device))
+        return logits
+    for b, u in enumerate(uniq):
+        if not u:
+            continue
+        idx = torch.tensor(u)
+        v = logits[b, idx]
+        logits[b, idx] = torch.where(v > 0, v / penalty[b], v * penalty[b])
+    return logits
+
+
+def sample_from_candidates(vals: np.ndarray, idx: np.ndarray, lse: float, temperature: float, top_p: float,
+                           rng: np.random.Generator) -> int:
+    """Nucleus sampling from the top-k candidates of one row.
+
+    ``vals`` are logits/temperature sorted descending, ``lse`` the log-sum-exp over the
+    full vocabulary of the same scaled logits, so ``exp(vals - lse)`` are exact
+    probabilities.  The nucleus is the smallest prefix with mass >= top_p; when the
+    top-k mass is below top_p the whole candidate set is used (documented truncation)."""
+    p = np.exp(vals.astype(np.float64) - lse)
+    c = np.cumsum(p)
+    n = int(np.searchsorted(c, top_p * c[-1] if c[-1] < top_p else top_p) + 1)
+    n = max(1, min(n, len(p)))
+    q = p[:n] / p[:n].sum()
+    return int(idx[int(rng.choice(n, p=q))])

@@ -1,0 +1,85 @@
+"""Decoder-LLM HIP kernels (SwiGLU epilogue, RoPE + paged KV write, paged decode attention,
+repetition penalty) vs the fp32 PyTorch references."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from lumen_amd import ops
+from lumen_amd.ops import llm
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-6)).item()
+
+
+@pytest.mark.parametrize("M,K,I", [(1, 896, 4864), (37, 512, 1024), (300, 1024, 2816)])
+def test_swiglu_epilogue(M, K, I):
+    g = torch.Generator().manual_seed(M)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    wg = (torch.randn(I, K, generator=g) * K ** -0.5).bfloat16()
+    wu = (torch.randn(I, K, generator=g) * K ** -0.5).bfloat16()
+    w = ops.glu_interleave(wg, wu)
+    ref = ops.linear(x, w, glu=True)
+    got = ops.linear(x.to(DEV), w.to(DEV), glu=True)
+    assert got.shape == (M, I)
+    assert _rel(got, ref) < 1e-2
+
+
+def _cache(NB, Hkv, D, g):
+    k = (torch.randn(NB, Hkv, 64, D, generator=g)).bfloat16()
+    v = (torch.randn(NB, Hkv, D, 64, generator=g)).bfloat16()
+    return k, v
+
+
+@pytest.mark.parametrize("H,Hkv,D", [(14, 2, 64), (32, 8, 128), (4, 4, 64)])
+def test_rope_kv(H, Hkv, D):
+    g = torch.Generator().manual_seed(H)
+    T = 75
+    qkv = torch.randn(T, (H + 2 * Hkv) * D + 16, generator=g).bfloat16()[:, :(H + 2 * Hkv) * D]
+    pos = torch.randint(0, 4000, (T,), generator=g, dtype=torch.int32)
+    cs = llm.rope_cos_sin(4096, D, 1e6)
+    kc, vc = _cache(6, Hkv, D, g)
+    slots = torch.randperm(6 * 64, generator=g)[:T].long()
+    slots[5] = -1
+    q_ref, kc_ref, vc_ref = qkv.clone(), kc.clone(), vc.clone()
+    llm.rope_kv(q_ref, pos, cs, H, Hkv, D, slots, kc_ref, vc_ref)
+    q_g, kc_g, vc_g = qkv.to(DEV), kc.to(DEV), vc.to(DEV)
+    llm.rope_kv(q_g, pos.to(DEV), cs.to(DEV), H, Hkv, D, slots.to(DEV), kc_g, vc_g)
+    assert (q_g.cpu().float() - q_ref.float()).abs().max().item() < 0.05
+    assert (kc_g.cpu().float() - kc_ref.float()).abs().max().item() < 0.05
+    assert torch.equal(vc_g.cpu(), vc_ref)
+
+
+@pytest.mark.parametrize("H,Hkv,D", [(14, 2, 64), (32, 8, 128), (32, 32, 128), (16, 1, 64)])
+@pytest.mark.parametrize("lens", [[1, 64, 65], [700, 3, 2048 + 17], [5000]])
+def test_paged_decode(H, Hkv, D, lens):
+    g = torch.Generator().manual_seed(H * D + len(lens))
+    B = len(lens)
+    maxb = max(-(-L // 64) for L in lens)
+    NB = B * maxb + 3
+    kc, vc = _cache(NB, Hkv, D, g)
+    perm = torch.randperm(NB, generator=g)
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    for b in range(B):
+        bt[b] = perm[b * maxb:(b + 1) * maxb].int()
+    ctx = torch.tensor(lens, dtype=torch.int32)
+    q = torch.randn(B, (H + 2 * Hkv) * D, generator=g).bfloat16()
+    ref = llm.paged_decode(q, kc, vc, bt, ctx, H, Hkv)
+    got = llm.paged_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), ctx.to(DEV), H, Hkv)
+    assert got.shape == (B, H * D)
+    assert _rel(got, ref) < 2e-2
+
+
+def test_rep_penalty():
+    g = torch.Generator().manual_seed(0)
+    lg = torch.randn(3, 1000, generator=g)
+    ids = [[1, 5, 5, 999], [], [0, 2, 3]]
+    ref = llm.rep_penalty_(lg.clone(), ids, [1.3, 1.1, 0.7])
+    got = llm.rep_penalty_(lg.to(DEV), ids, [1.3, 1.1, 0.7]).cpu()
+    assert torch.allclose(got, ref)
