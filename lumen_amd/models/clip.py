@@ -206,6 +206,22 @@ class VisionTower(nn.Module):
         emb = ops.linear(pooled, self.proj_w, out_dtype=torch.float32)
         return ops.l2_normalize_(emb)
 
+    @torch.no_grad()
+    def forward_features(self, patches: torch.Tensor, B: int, layer: int = -2, drop_cls: bool = True) -> torch.Tensor:
+        """Hidden states after block ``layer`` (LLaVA ``mm_vision_select_layer``; -1 = last,
+        -2 = penultimate) -> [B, P(+1), W] bf16 patch features (CLS dropped)."""
+        cfg = self.cfg
+        S, P, W = self.seq, self.num_patches, cfg.width
+        x = torch.empty((B * S, W), device=patches.device, dtype=self.patch_w.dtype)
+        ops.linear(patches, self.patch_w, table=self.pos_emb, table_period=P, table_offset=1, out=x,
+                   out_group=P, out_group_stride=S, out_row_offset=1)
+        ops.cls_fill(x, self.class_emb, self.pos_emb, S)
+        ops.layer_norm(x, self.ln_pre_w, self.ln_pre_b, cfg.ln_eps, out=x)
+        n = len(self.blocks) + layer + 1 if layer < 0 else layer
+        run_blocks(x, self.blocks[:n], B, S, cfg.heads, cfg.act, cfg.ln_eps)
+        x = x.view(B, S, W)
+        return x[:, 1:] if drop_cls else x
+
     def preprocess(self, images, mean, std, filter: str = "pil_bicubic") -> torch.Tensor:
         """uint8 HWC images -> patch rows [B*P, kpad] (squash resize, no crop: the ONNX path)."""
         s = self.cfg.image_size

@@ -1,0 +1,288 @@
+"""Llama / Qwen2 decoder for the VLM, tensor-parallel over RCCL.
+
+Reference: the FastVLM decoder ONNX graph (Qwen2-0.5B) driven by
+packages/lumen-vlm/src/lumen_vlm/backends/onnxrt_backend.py:161-533; the north star
+adds Llama-3-8B (LLaVA-style) at TP=8.  Per layer (every op one gfx950 kernel):
+
+  RMSNorm (fused residual add)  ->  QKV GEMM (+bias, Qwen2)  ->  RoPE + paged-KV write
+  ->  attention (prefill: flash kernel reading the rotated QKV in place, causal;
+      decode: paged flash-decoding)  ->  o_proj GEMM  ->  RMSNorm  ->  gate|up GEMM with
+  the SwiGLU epilogue  ->  down GEMM
+
+Tensor parallelism (Megatron): QKV and gate|up are column-parallel (whole heads /
+whole 8-column GLU groups per rank), o_proj and down are row-parallel followed by
+an all-reduce (RCCL); with TP the residual add is fused into the next RMSNorm
+(``norm(add=partial, resid_out=x)``) instead of the GEMM epilogue.  Embedding and
+lm_head are vocab-parallel (masked lookup + all-reduce; local top-k + all-gather of
+the candidates for sampling).  Weights can be loaded from HF Qwen2/Llama state dicts
+(sharded at load) or random-initialised per rank directly on the device.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import asdict, dataclass, field
+from typing import Optional
+
+import torch
+from torch import nn
+
+from .. import ops
+from ..ops import llm as lops
+
+
+@dataclass
+class LLMConfig:
+    vocab_size: int = 151936
+    hidden_size: int = 896
+    num_layers: int = 24
+    num_heads: int = 14
+    num_kv_heads: int = 2
+    head_dim: int = 64
+    intermediate_size: int = 4864
+    rope_theta: float = 1000000.0
+    rms_eps: float = 1e-6
+    max_position: int = 32768
+    tie_word_embeddings: bool = True
+    qkv_bias: bool = True
+    rope_scaling: Optional[dict] = None
+    bos_token_id: int = 151643
+    eos_token_id: int = 151645
+
+    @staticmethod
+    def from_dict(d: dict) -> "LLMConfig":
+        keys = LLMConfig.__dataclass_fields__.keys()
+        return LLMConfig(**{k: v for k, v in d.items() if k in keys})
+
+    @staticmethod
+    def from_hf(c: dict) -> "LLMConfig":
+        H = c["num_attention_heads"]
+        hd = c.get("head_dim") or c["hidden_size"] // H
+        mt = c.get("model_type", "llama")
+        return LLMConfig(vocab_size=c["vocab_size"], hidden_size=c["hidden_size"], num_layers=c["num_hidden_layers"],
+                         num_heads=H, num_kv_heads=c.get("num_key_value_heads", H), head_dim=hd,
+                         intermediate_size=c["intermediate_size"], rope_theta=c.get("rope_theta", 10000.0),
+                         rms_eps=c.get("rms_norm_eps", 1e-6), max_position=c.get("max_position_embeddings", 4096),
+                         tie_word_embeddings=c.get("tie_word_embeddings", False),
+                         qkv_bias=c.get("attention_bias", mt == "qwen2"), rope_scaling=c.get("rope_scaling"),
+                         bos_token_id=c.get("bos_token_id") or 0,
+                         eos_token_id=(c.get("eos_token_id")[0] if isinstance(c.get("eos_token_id"), list)
+                                       else c.get("eos_token_id") or 0))
+
+    def to_dict(self):
+        return asdict(self)
+
+
+LLM_PRESETS = {
+    "qwen2-0.5b": LLMConfig(),
+    "llama3-8b": LLMConfig(vocab_size=128256, hidden_size=4096, num_layers=32, num_heads=32, num_kv_heads=8,
+                           head_dim=128, intermediate_size=14336, rope_theta=500000.0, rms_eps=1e-5,
+                           max_position=8192, tie_word_embeddings=False, qkv_bias=False, bos_token_id=128000,
+                           eos_token_id=128009),
+    "vicuna-7b": LLMConfig(vocab_size=32000, hidden_size=4096, num_layers=32, num_heads=32, num_kv_heads=32,
+                           head_dim=128, intermediate_size=11008, rope_theta=10000.0, rms_eps=1e-5,
+                           max_position=4096, tie_word_embeddings=False, qkv_bias=False, bos_token_id=1,
+                           eos_token_id=2),
+    "tiny": LLMConfig(vocab_size=512, hidden_size=128, num_layers=2, num_heads=4, num_kv_heads=2, head_dim=32,
+                      intermediate_size=256, max_position=2048, bos_token_id=1, eos_token_id=2),
+}
+
+
+@dataclass
+class TPInfo:
+    rank: int = 0
+    world: int = 1
+    group: object = None
+
+    @property
+    def enabled(self) -> bool:
+        return self.world > 1
+
+
+class DecoderLayer(nn.Module):
+    def __init__(self, cfg: LLMConfig, tp: TPInfo, dtype, device):
+        super().__init__()
+        kw = dict(dtype=dtype, device=device)
+        Hd, D = cfg.hidden_size, cfg.head_dim
+        self.H = cfg.num_heads // tp.world
+        self.Hkv = max(cfg.num_kv_heads // tp.world, 1)
+        self.I = cfg.intermediate_size // tp.world
+        self.ln1 = nn.Parameter(torch.ones(Hd, **kw), requires_grad=False)
+        self.ln2 = nn.Parameter(torch.ones(Hd, **kw), requires_grad=False)
+        self.qkv_w = nn.Parameter(torch.zeros((self.H + 2 * self.Hkv) * D, Hd, **kw), requires_grad=False)
+        self.qkv_b = nn.Parameter(torch.zeros((self.H + 2 * self.Hkv) * D, dtype=torch.float32, device=device),
+                                  requires_grad=False) if cfg.qkv_bias else None
+        self.o_w = nn.Parameter(torch.zeros(Hd, self.H * D, **kw), requires_grad=False)
+        self.gu_w = nn.Parameter(torch.zeros(2 * self.I, Hd, **kw), requires_grad=False)
+        self.down_w = nn.Parameter(torch.zeros(Hd, self.I, **kw), requires_grad=False)
+
+
+class LLM(nn.Module):
+    def __init__(self, cfg: LLMConfig, tp: Optional[TPInfo] = None, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.cfg = cfg
+        self.tp = tp or TPInfo()
+        w = self.tp.world
+        assert cfg.num_heads % w == 0 and (cfg.num_kv_heads % w == 0 or w % cfg.num_kv_heads == 0), "TP heads"
+        assert cfg.intermediate_size % (8 * w) == 0 and cfg.vocab_size % w == 0, "TP shapes"
+        self.Vl = cfg.vocab_size // w
+        self.v0 = self.tp.rank * self.Vl
+        kw = dict(dtype=dtype, device=device)
+        self.embed = nn.Parameter(torch.zeros(self.Vl, cfg.hidden_size, **kw), requires_grad=False)
+        self.layers = nn.ModuleList([DecoderLayer(cfg, self.tp, dtype, device) for _ in range(cfg.num_layers)])
+        self.norm = nn.Parameter(torch.ones(cfg.hidden_size, **kw), requires_grad=False)
+        self.lm_head = None if cfg.tie_word_embeddings else nn.Parameter(torch.zeros(self.Vl, cfg.hidden_size, **kw),
+                                                                         requires_grad=False)
+        self.register_buffer("cos_sin", lops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta,
+                                                          cfg.rope_scaling).to(device), persistent=False)
+        self.H, self.Hkv = self.layers[0].H, self.layers[0].Hkv
+
+    # ------------------------------------------------------------------ weights
+    @torch.no_grad()
+    def random_init(self, seed: int = 0):
+        """Per-rank random shards generated on the model's device (coherent full model)."""
+        dev = self.embed.device
+        g = torch.Generator(device=dev).manual_seed(seed * 1000 + self.tp.rank)
+        Hd = self.cfg.hidden_size
+        L = self.cfg.num_layers
+
+        def rnd(p, std):
+            p.copy_((torch.randn(p.shape, generator=g, device=dev, dtype=torch.float32) * std).to(p.dtype))
+
+        rnd(self.embed, 0.02)
+        if self.lm_head is not None:
+            rnd(self.lm_head, 0.02)
+        for l in self.layers:
+            rnd(l.qkv_w, Hd ** -0.5)
+            rnd(l.o_w, (Hd ** -0.5) / math.sqrt(2 * L))
+            rnd(l.gu_w, Hd ** -0.5)
+            rnd(l.down_w, (l.I * self.tp.world) ** -0.5 / math.sqrt(2 * L))
+            if l.qkv_b is not None:
+                rnd(l.qkv_b, 0.02)
+
+    @torch.no_grad()
+    def load_hf_state_dict(self, sd: dict, prefix: str = "model.") -> None:
+        """HF Qwen2 / Llama weights (``model.layers.N.self_attn.q_proj.weight`` ...), sharded for this rank."""
+        cfg, r, w = self.cfg, self.tp.rank, self.tp.world
+        D = cfg.head_dim
+
+        def get(k):
+            return sd[k].to(torch.float32)
+
+        def rows(t, n, i):   # i-th of n equal row shards
+            s = t.shape[0] // n
+            return t[i * s:(i + 1) * s]
+
+        self.embed.copy_(rows(get(prefix + "embed_tokens.weight"), w, r).to(self.embed.dtype))
+        if self.lm_head is not None:
+            self.lm_head.copy_(rows(get("lm_head.weight"), w, r).to(self.lm_head.dtype))
+        self.norm.copy_(get(prefix + "norm.weight").to(self.norm.dtype))
+        kv_rep = w // cfg.num_kv_heads if w > cfg.num_kv_heads else 1
+        for i, l in enumerate(self.layers):
+            p = f"{prefix}layers.{i}."
+            q = rows(get(p + "self_attn.q_proj.weight"), w, r)
+            kvi = r // kv_rep
+            kvn = max(w // kv_rep, 1)
+            k = rows(get(p + "self_attn.k_proj.weight"), kvn, kvi)
+            v = rows(get(p + "self_attn.v_proj.weight"), kvn, kvi)
+            l.qkv_w.copy_(torch.cat([q, k, v], 0).to(l.qkv_w.dtype))
+            if l.qkv_b is not None:
+                bq = rows(get(p + "self_attn.q_proj.bias"), w, r)
+                bk = rows(get(p + "self_attn.k_proj.bias"), kvn, kvi)
+                bv = rows(get(p + "self_attn.v_proj.bias"), kvn, kvi)
+                l.qkv_b.copy_(torch.cat([bq, bk, bv], 0))
+            o = get(p + "self_attn.o_proj.weight")
+            l.o_w.copy_(o[:, r * l.H * D:(r + 1) * l.H * D].to(l.o_w.dtype))
+            gate = rows(get(p + "mlp.gate_proj.weight"), w, r)
+            up = rows(get(p + "mlp.up_proj.weight"), w, r)
+            l.gu_w.copy_(ops.glu_interleave(gate, up).to(l.gu_w.dtype))
+            dn = get(p + "mlp.down_proj.weight")
+            l.down_w.copy_(dn[:, r * l.I:(r + 1) * l.I].to(l.down_w.dtype))
+            l.ln1.copy_(get(p + "input_layernorm.weight").to(l.ln1.dtype))
+            l.ln2.copy_(get(p + "post_attention_layernorm.weight").to(l.ln2.dtype))
+
+    # ------------------------------------------------------------------ collectives
+    def _all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.tp.enabled:
+            import torch.distributed as dist
+
+            dist.all_reduce(t, group=self.tp.group)
+        return t
+
+    # ------------------------------------------------------------------ pieces
+    def embed_tokens(self, ids: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """ids [T] -> [T, hidden] (vocab-parallel: masked local lookup + all-reduce)."""
+        e = ops.embed(ids.reshape(1, -1), self.embed, id_offset=self.v0,
+                      out=out.view(1, -1, self.cfg.hidden_size) if out is not None else None)
+        e = e.view(-1, self.cfg.hidden_size)
+        return self._all_reduce(e)
+
+    def _layers(self, x: torch.Tensor, pos: torch.Tensor, slots: Optional[torch.Tensor], kv, attn_fn) -> torch.Tensor:
+        """x [T, hidden] residual stream (updated in place); returns x."""
+        cfg = self.cfg
+        D = cfg.head_dim
+        eps = cfg.rms_eps
+        T = x.shape[0]
+        h = torch.empty_like(x)
+        tp = self.tp.enabled
+        pending: Optional[torch.Tensor] = None   # TP: row-parallel partial to add before the next norm
+        for i, l in enumerate(self.layers):
+            if pending is None:
+                ops.rms_norm(x, l.ln1, eps, out=h)
+            else:
+                ops.rms_norm(x, l.ln1, eps, add=self._all_reduce(pending), resid_out=x, out=h)
+            qkv = ops.linear(h, l.qkv_w, l.qkv_b)
+            kc, vc = (kv.k[i], kv.v[i]) if kv is not None else (None, None)
+            lops.rope_kv(qkv, pos, self.cos_sin, l.H, l.Hkv, D, slots, kc, vc)
+            att = attn_fn(qkv, l, kc, vc)                            # [T, H*D]
+            if tp:
+                part = ops.linear(att, l.o_w)
+                ops.rms_norm(x, l.ln2, eps, add=self._all_reduce(part), resid_out=x, out=h)
+            else:
+                ops.linear(att, l.o_w, residual=x, out=x)
+                ops.rms_norm(x, l.ln2, eps, out=h)
+            g = ops.linear(h, l.gu_w, glu=True)
+            if tp:
+                pending = ops.linear(g, l.down_w)
+            else:
+                ops.linear(g, l.down_w, residual=x, out=x)
+            del qkv, att, g
+        if pending is not None:
+            x.add_(self._all_reduce(pending))
+        return x
+
+    def logits(self, x_rows: torch.Tensor) -> torch.Tensor:
+        """final norm + lm_head of rows [B, hidden] -> local-vocab fp32 logits [B, V/tp]."""
+        h = ops.rms_norm(x_rows, self.norm, self.cfg.rms_eps)
+        w = self.lm_head if self.lm_head is not None else self.embed
+        return ops.linear(h, w, out_dtype=torch.float32)
+
+    # ------------------------------------------------------------------ forward passes
+    @torch.no_grad()
+    def prefill(self, x: torch.Tensor, kv=None, slots: Optional[torch.Tensor] = None, start_pos: int = 0
+                ) -> torch.Tensor:
+        """One sequence: input embeddings x [T, hidden] (modified in place) at positions
+        start_pos.., k/v written to ``slots``; returns last-token logits [1, V/tp] fp32."""
+        T = x.shape[0]
+        pos = torch.arange(start_pos, start_pos + T, device=x.device, dtype=torch.int32)
+        D = self.cfg.head_dim
+
+        def attn(qkv, l, kc, vc):
+            q5 = qkv.view(1, T, l.H + 2 * l.Hkv, D)
+            o = ops.attention(q5[:, :, :l.H], q5[:, :, l.H:l.H + l.Hkv], q5[:, :, l.H + l.Hkv:], causal=True)
+            return o.view(T, l.H * D)
+
+        self._layers(x, pos, slots, kv, attn)
+        return self.logits(x[T - 1:T])
+
+    @torch.no_grad()
+    def decode(self, ids: torch.Tensor, pos: torch.Tensor, slots: torch.Tensor, kv, block_table: torch.Tensor,
+               ctx_len: torch.Tensor, workspace: Optional[dict] = None) -> torch.Tensor:
+        """B sequences, one new token each -> logits [B, V/tp] fp32."""
+        x = self.embed_tokens(ids)
+        D = self.cfg.head_dim
+
+        def attn(qkv, l, kc, vc):
+            return lops.paged_decode(qkv, kc, vc, block_table, ctx_len, l.H, l.Hkv, workspace=workspace)
+
+        self._layers(x, pos, slots, kv, attn)
+        return self.logits(x)

@@ -1,0 +1,268 @@
+"""LLaVA-family vision-language model: ViT image encoder -> MLP projector -> decoder LLM.
+
+Reference pipeline (packages/lumen-vlm/src/lumen_vlm/backends/onnxrt_backend.py):
+prompt -> tokens; image -> pad-to-square (black, centred) + bicubic resize -> /255
+-> vision encoder (FastViTHD, 256 tokens) -> projector; token embeddings; the
+vision embeddings replace the ``<image>`` token (:240-296); prefill; decode loop.
+
+Presets:
+* ``fastvlm-0.5b``  — Qwen2-0.5B decoder with a 256-token, 1024-px image encoder.
+  FastViTHD itself (a hybrid conv/attention net) is represented by a ViT with 64-px
+  patches over the same 1024x1024 input producing the same 256 visual tokens —
+  same I/O shapes and token count, not the same layer graph (stand-in, documented).
+* ``llava-llama3-8b`` — north-star config: CLIP ViT-L/14-336 (penultimate layer,
+  576 tokens, CLS dropped) -> 2-layer GELU MLP projector -> Llama-3-8B.
+* ``tiny`` — CPU tests.
+
+MI355X path: one fused pad/resize/normalise/patchify kernel, the ViT on the MFMA
+kernels, projector GEMMs whose second GEMM writes straight into the rows of the
+LLM's prefill embedding buffer that the ``<image>`` token occupies.
+"""
+from __future__ import annotations
+
+from dataclasses import asdict, dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+from torch import nn
+
+from .. import ops
+from .clip import VisionConfig, VisionTower
+from .llm import LLM, LLM_PRESETS, LLMConfig, TPInfo
+
+
+@dataclass
+class VLMConfig:
+    vision: VisionConfig = field(default_factory=lambda: VisionConfig(image_size=1024, patch_size=64, width=768,
+                                                                      layers=12, heads=12, act="gelu"))
+    llm: LLMConfig = field(default_factory=LLMConfig)
+    feature_layer: int = -2
+    image_token_id: int = 151646
+    image_mean: tuple = (0.0, 0.0, 0.0)
+    image_std: tuple = (1.0, 1.0, 1.0)
+    pad_value: float = 0.0          # pad-to-square fill (pixel units)
+    resize_filter: str = "pil_bicubic"
+
+    @property
+    def num_image_tokens(self) -> int:
+        return (self.vision.image_size // self.vision.patch_size) ** 2
+
+    def to_dict(self):
+        return asdict(self)
+
+    @staticmethod
+    def from_dict(d: dict) -> "VLMConfig":
+        v = VisionConfig(**d.get("vision", {}))
+        l = LLMConfig.from_dict(d.get("llm", {}))
+        rest = {k: d[k] for k in ("feature_layer", "image_token_id", "pad_value", "resize_filter") if k in d}
+        for k in ("image_mean", "image_std"):
+            if k in d:
+                rest[k] = tuple(d[k])
+        return VLMConfig(vision=v, llm=l, **rest)
+
+
+VLM_PRESETS = {
+    "fastvlm-0.5b": VLMConfig(),
+    "llava-llama3-8b": VLMConfig(vision=VisionConfig(image_size=336, patch_size=14, width=1024, layers=24, heads=16,
+                                                     act="quick_gelu"),
+                                 llm=LLM_PRESETS["llama3-8b"], image_token_id=128002,
+                                 image_mean=(0.48145466, 0.4578275, 0.40821073),
+                                 image_std=(0.26862954, 0.26130258, 0.27577711), pad_value=116.0),
+    "tiny": VLMConfig(vision=VisionConfig(image_size=32, patch_size=8, width=64, layers=2, heads=2, act="gelu"),
+                      llm=LLM_PRESETS["tiny"], image_token_id=259),
+}
+
+
+class VLM(nn.Module):
+    def __init__(self, cfg: VLMConfig, tp: Optional[TPInfo] = None, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.cfg = cfg
+        kw = dict(dtype=dtype, device=device)
+        self.vision = VisionTower(cfg.vision, 16, dtype, device)
+        Wv, Hd = cfg.vision.width, cfg.llm.hidden_size
+        self.proj1_w = nn.Parameter(torch.zeros(Hd, Wv, **kw), requires_grad=False)
+        self.proj1_b = nn.Parameter(torch.zeros(Hd, dtype=torch.float32, device=device), requires_grad=False)
+        self.proj2_w = nn.Parameter(torch.zeros(Hd, Hd, **kw), requires_grad=False)
+        self.proj2_b = nn.Parameter(torch.zeros(Hd, dtype=torch.float32, device=device), requires_grad=False)
+        self.llm = LLM(cfg.llm, tp, dtype, device)
+
+    @torch.no_grad()
+    def random_init(self, seed: int = 0):
+        """Vision + projector replicated on every rank (same seed); LLM shards per rank."""
+        g = torch.Generator().manual_seed(seed)
+        dev = self.proj1_w.device
+        vis_cpu = VisionTower(self.cfg.vision, 16, torch.float32, "cpu")
+        vis_cpu.random_init(g)
+        self.vision.load_state_dict({k: v.to(self.vision.state_dict()[k].dtype) for k, v in vis_cpu.state_dict().items()})
+        Wv, Hd = self.cfg.vision.width, self.cfg.llm.hidden_size
+        self.proj1_w.copy_((torch.randn(Hd, Wv, generator=g) * Wv ** -0.5).to(self.proj1_w.dtype).to(dev))
+        self.proj2_w.copy_((torch.randn(Hd, Hd, generator=g) * Hd ** -0.5).to(self.proj2_w.dtype).to(dev))
+        self.llm.random_init(seed)
+
+    @property
+    def device(self):
+        return self.proj1_w.device
+
+    # ------------------------------------------------------------------ vision
+    def preprocess(self, images: Sequence[torch.Tensor]) -> torch.Tensor:
+        """uint8 HWC images -> patch rows: pad to a centred square (pad_value), resize, normalise."""
+        v = self.vision
+        s = self.cfg.vision.image_size
+        geoms, off = [], 0
+        for im in images:
+            geoms.append(ops.ImageGeom.pad_square(im.shape[0], im.shape[1], off, s))
+            off += im.numel()
+        return ops.image_prep(list(images), (s, s), mean=self.cfg.image_mean, std=self.cfg.image_std,
+                              filter=self.cfg.resize_filter, layout="patches", patch=self.cfg.vision.patch_size,
+                              kpad=v.kpad, pad=self.cfg.pad_value, geoms=geoms, out_dtype=v.patch_w.dtype,
+                              device=self.device)
+
+    @torch.no_grad()
+    def encode_images(self, images: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """-> projected image embeddings [B * N_img, hidden] (or written into ``out`` rows)."""
+        B = len(images)
+        feats = self.vision.forward_features(self.preprocess(images), B, self.cfg.feature_layer)
+        f = feats.reshape(B * self.cfg.num_image_tokens, -1)
+        if not f.is_contiguous():
+            f = f.contiguous()
+        h = ops.linear(f, self.proj1_w, self.proj1_b, act="gelu")
+        return ops.linear(h, self.proj2_w, self.proj2_b, out=out)
+
+    # ------------------------------------------------------------------ prefill inputs
+    def expand_image_tokens(self, ids: Sequence[int], n_images: int) -> tuple[list[int], list[int]]:
+        """Replace each ``<image>`` id by N_img placeholder positions -> (ids, image row starts)."""
+        N = self.cfg.num_image_tokens
+        out, starts = [], []
+        used = 0
+        for t in ids:
+            if t == self.cfg.image_token_id and used < n_images:
+                starts.append(len(out))
+                out.extend([self.cfg.image_token_id] * N)
+                used += 1
+            else:
+                out.append(int(t))
+        return out, starts
+
+    @torch.no_grad()
+    def build_prefill(self, ids: Sequence[int], images: Sequence[torch.Tensor]) -> torch.Tensor:
+        """Token embeddings with image rows spliced in -> x [T, hidden] on the model device."""
+        full, starts = self.expand_image_tokens(ids, len(images))
+        dev = self.device
+        t = torch.tensor(full, dtype=torch.long, device=dev)
+        x = self.llm.embed_tokens(t)
+        N = self.cfg.num_image_tokens
+        if starts:
+            if all(s == starts[0] + i * N for i, s in enumerate(starts)):
+                self.encode_images(images[:len(starts)], out=x[starts[0]:starts[0] + N * len(starts)])
+            else:
+                emb = self.encode_images(images[:len(starts)])
+                for i, s in enumerate(starts):
+                    x[s:s + N] = emb[i * N:(i + 1) * N]
+        return x
+
+    # ------------------------------------------------------------------ weights
+    def export_state_dict(self) -> dict:
+        """Synthetic-pack layout: ``vision.*`` / ``mm_projector.*`` + HF decoder names."""
+        sd = {f"vision.{k}": v for k, v in self.vision.state_dict().items()}
+        sd["mm_projector.0.weight"], sd["mm_projector.0.bias"] = self.proj1_w, self.proj1_b
+        sd["mm_projector.2.weight"], sd["mm_projector.2.bias"] = self.proj2_w, self.proj2_b
+        l = self.llm
+        assert l.tp.world == 1
+        sd["model.embed_tokens.weight"] = l.embed
+        sd["model.norm.weight"] = l.norm
+        if l.lm_head is not None:
+            sd["lm_head.weight"] = l.lm_head
+        D = l.cfg.head_dim
+        for i, ly in enumerate(l.layers):
+            p = f"model.layers.{i}."
+            q, k, v = torch.split(ly.qkv_w, [ly.H * D, ly.Hkv * D, ly.Hkv * D], 0)
+            sd[p + "self_attn.q_proj.weight"], sd[p + "self_attn.k_proj.weight"], sd[p + "self_attn.v_proj.weight"] = q, k, v
+            if ly.qkv_b is not None:
+                bq, bk, bv = torch.split(ly.qkv_b, [ly.H * D, ly.Hkv * D, ly.Hkv * D], 0)
+                sd[p + "self_attn.q_proj.bias"], sd[p + "self_attn.k_proj.bias"], sd[p + "self_attn.v_proj.bias"] = bq, bk, bv
+            sd[p + "self_attn.o_proj.weight"] = ly.o_w
+            gu = ly.gu_w.view(ly.I // 8, 2, 8, -1)
+            sd[p + "mlp.gate_proj.weight"] = gu[:, 0].reshape(ly.I, -1)
+            sd[p + "mlp.up_proj.weight"] = gu[:, 1].reshape(ly.I, -1)
+            sd[p + "mlp.down_proj.weight"] = ly.down_w
+            sd[p + "input_layernorm.weight"] = ly.ln1
+            sd[p + "post_attention_layernorm.weight"] = ly.ln2
+        return {k: v.detach().contiguous() for k, v in sd.items()}
+
+    @torch.no_grad()
+    def load_pack_state_dict(self, sd: dict) -> None:
+        vis = {k[len("vision."):]: v for k, v in sd.items() if k.startswith("vision.")}
+        own = self.vision.state_dict()
+        self.vision.load_state_dict({k: vis[k].to(own[k].dtype) for k in own})
+        for dst, key in ((self.proj1_w, "mm_projector.0.weight"), (self.proj1_b, "mm_projector.0.bias"),
+                         (self.proj2_w, "mm_projector.2.weight"), (self.proj2_b, "mm_projector.2.bias")):
+            dst.copy_(sd[key].to(dst.dtype))
+        self.llm.load_hf_state_dict(sd)
+
+
+# ============================================================================= synthetic pack
+CHATML_TEMPLATE = ("{% for message in messages %}<|im_start|>{{ message['role'] }}\n{{ message['content'] }}"
+                   "<|im_end|>\n{% endfor %}{% if add_generation_prompt %}<|im_start|>assistant\n{% endif %}")
+
+
+def write_vlm_model(root, name: str, preset: Optional[str] = None, seed: int = 0, weights: Optional[bool] = None):
+    """Synthetic VLM pack: byte-level BPE tokenizer with ChatML specials, chat template,
+    ``lumen_vlm_config.json``, ``model.safetensors`` (small presets) or ``random_init``
+    (large presets are random-initialised on the device at load), ``model_info.json``
+    with the generation / kv-cache / vision metadata the reference backends read."""
+    import copy
+    import json
+    from pathlib import Path
+
+    from ..resources.model_info import ModelInfo
+    from ..resources.synthetic import write_byte_bpe_tokenizer
+
+    root = Path(root)
+    root.mkdir(parents=True, exist_ok=True)
+    n = name.lower()
+    preset = preset or ("tiny" if "tiny" in n else "llava-llama3-8b" if ("llava" in n or "8b" in n) else "fastvlm-0.5b")
+    cfg = copy.deepcopy(VLM_PRESETS[preset])
+    tok = write_byte_bpe_tokenizer(root / "tokenizer.json", bos="<|im_start|>", eos="<|im_end|>",
+                                   extra_special=["<|endoftext|>", "<image>"], add_bos_eos=False)
+    from tokenizers import Tokenizer
+
+    t = Tokenizer.from_file(str(root / "tokenizer.json"))
+    cfg.image_token_id = t.token_to_id("<image>")
+    cfg.llm.eos_token_id = tok["eos_id"]
+    cfg.llm.bos_token_id = tok["bos_id"]
+    (root / "tokenizer_config.json").write_text(json.dumps({"chat_template": CHATML_TEMPLATE,
+                                                            "eos_token": "<|im_end|>", "bos_token": None}, indent=2))
+    (root / "lumen_vlm_config.json").write_text(json.dumps(cfg.to_dict(), indent=2))
+    if weights is None:
+        weights = preset == "tiny"
+    files = ["tokenizer.json", "tokenizer_config.json", "lumen_vlm_config.json"]
+    if weights:
+        m = VLM(cfg, dtype=torch.float32, device="cpu")
+        m.random_init(seed)
+        from safetensors.torch import save_file
+
+        save_file({k: v.to(torch.bfloat16) if v.is_floating_point() and v.dim() > 1 else v
+                   for k, v in m.export_state_dict().items()}, str(root / "model.safetensors"))
+        files.append("model.safetensors")
+    lc = cfg.llm
+    info = {
+        "name": name, "version": "1.0.0", "description": f"synthetic {preset} VLM pack (random init)",
+        "model_type": "vlm", "source": {"format": "custom", "repo_id": f"synthetic/{name}"},
+        "runtimes": {"onnx": {"available": True, "files": files, "devices": ["cuda", "cpu"]},
+                     "torch": {"available": True, "files": files, "devices": ["cuda", "cpu"]}},
+        "extra_metadata": {
+            "synthetic": True, "random_init": not weights, "seed": seed, "lumen_preset": preset,
+            "generation_config": {"bos_token_id": lc.bos_token_id, "eos_token_id": lc.eos_token_id,
+                                  "pad_token_id": tok["eos_id"], "image_token_index": cfg.image_token_id,
+                                  "vocab_size": lc.vocab_size, "max_position_embeddings": lc.max_position},
+            "kv_cache_config": {"num_hidden_layers": lc.num_layers, "num_attention_heads": lc.num_heads,
+                                "num_key_value_heads": lc.num_kv_heads, "hidden_size": lc.hidden_size,
+                                "head_dim": lc.head_dim},
+            "vision_config": {"image_size": cfg.vision.image_size, "patch_size": cfg.vision.patch_size,
+                              "mean": list(cfg.image_mean), "std": list(cfg.image_std)},
+        },
+    }
+    ModelInfo.model_validate(info)
+    (root / "model_info.json").write_text(json.dumps(info, indent=2))
+    return root

@@ -1,0 +1,337 @@
+"""Continuous-batching generation engine for the VLM decoder (paged KV cache, TP-aware).
+
+The reference generates one request at a time on ORT, copying the whole KV cache
+host<->device every token (packages/lumen-vlm/src/lumen_vlm/backends/onnxrt_backend.py:
+298-492).  Here one engine thread owns the device:
+
+* requests are admitted while the native block manager can reserve
+  ``prompt + max_new_tokens`` tokens (no preemption needed at 288 GB/GPU);
+* each admitted request is prefilled (its ``prefill`` callable builds the input
+  embeddings — vision tower + token embeddings — on the engine thread), its first
+  token sampled and streamed immediately (TTFT);
+* all running requests then advance together: one batched decode step per
+  iteration (paged flash-decoding), sampling from on-device top-k candidates;
+* finished sequences release their blocks.
+
+Tensor parallelism: rank 0 runs this loop and broadcasts every step (prefill inputs,
+decode token ids / positions / slots / block tables) to follower ranks running
+:func:`follower_loop`, so every rank issues the same kernels and collectives; only
+rank 0 samples (the candidate merge makes logits identical on all ranks anyway).
+"""
+from __future__ import annotations
+
+import itertools
+import logging
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Any, Callable, Iterator, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..ops import llm as lops
+from .kv_cache import PagedKVCache
+
+log = logging.getLogger("lumen.engine")
+
+
+@dataclass
+class SamplingParams:
+    max_new_tokens: int = 512
+    temperature: float = 0.0
+    top_p: float = 1.0
+    repetition_penalty: float = 1.0
+    stop_token_ids: tuple = ()
+    seed: Optional[int] = None
+
+
+@dataclass
+class GenRequest:
+    rid: int
+    prefill_args: Any                       # opaque, handed to the engine's prefill builder
+    prompt_len: int
+    params: SamplingParams
+    out: "queue.Queue" = field(default_factory=queue.Queue)
+    tokens: list = field(default_factory=list)
+    t_submit: float = 0.0
+    t_first: Optional[float] = None
+    finish_reason: Optional[str] = None
+    ctx: int = 0                            # tokens in the KV cache
+    rng: Any = None
+
+    def stream(self, timeout: Optional[float] = None) -> Iterator[tuple]:
+        """yields ("token", id) ... then ("done", reason) | raises the engine error."""
+        while True:
+            kind, val = self.out.get(timeout=timeout)
+            if kind == "error":
+                raise val
+            yield kind, val
+            if kind == "done":
+                return
+
+
+class Sampler:
+    """Greedy / temperature + nucleus sampling from per-row top-k candidates (vocab-parallel).
+
+    ``spec`` (built on rank 0, broadcast with every TP step) carries everything that
+    changes the local logits shard or the collective shapes: k, per-row 1/T and the
+    repetition-penalty token sets."""
+
+    K_SAMPLE = 64
+
+    def __init__(self, llm):
+        self.llm = llm
+
+    @staticmethod
+    def spec(reqs: Sequence[GenRequest]) -> dict:
+        sample = any(r.params.temperature > 0 for r in reqs)
+        pens = [float(r.params.repetition_penalty) for r in reqs]
+        use_pen = any(abs(p - 1.0) > 1e-6 for p in pens)
+        return {"k": Sampler.K_SAMPLE if sample else 8,
+                "inv": [1.0 / r.params.temperature if r.params.temperature > 0 else 1.0 for r in reqs] if sample else None,
+                "pen": pens if use_pen else None,
+                "pen_ids": [list(r.tokens) for r in reqs] if use_pen else None}
+
+    def candidates(self, logits: torch.Tensor, spec: dict):
+        if spec["pen"] is not None:
+            lops.rep_penalty_(logits, [[t - self.llm.v0 for t in ids] for ids in spec["pen_ids"]], spec["pen"])
+        if spec["inv"] is not None:
+            logits.mul_(torch.tensor(spec["inv"], device=logits.device, dtype=torch.float32)[:, None])
+        k = spec["k"]
+        v, i, lse = ops.row_topk(logits, k, with_lse=True, index_offset=self.llm.v0)
+        tp = self.llm.tp
+        if tp.enabled:
+            import torch.distributed as dist
+
+            vs = [torch.empty_like(v) for _ in range(tp.world)]
+            is_ = [torch.empty_like(i) for _ in range(tp.world)]
+            ls = [torch.empty_like(lse) for _ in range(tp.world)]
+            dist.all_gather(vs, v, group=tp.group)
+            dist.all_gather(is_, i, group=tp.group)
+            dist.all_gather(ls, lse, group=tp.group)
+            v, i = torch.cat(vs, 1), torch.cat(is_, 1)
+            lse = torch.logsumexp(torch.stack(ls, 1), 1)
+            v, order = torch.sort(v, 1, descending=True)
+            i = torch.gather(i, 1, order)
+            v, i = v[:, :k], i[:, :k]
+        return v, i, lse
+
+    def pick(self, cands, reqs: Sequence[GenRequest]) -> list[int]:
+        v, i, lse = (t.cpu().numpy() for t in cands)
+        out = []
+        for b, r in enumerate(reqs):
+            if r.params.temperature > 0:
+                out.append(lops.sample_from_candidates(v[b], i[b], float(lse[b]), r.params.temperature,
+                                                       r.params.top_p, r.rng))
+            else:
+                out.append(int(i[b, 0]))
+        return out
+
+
+class TPSync:
+    """Step broadcast from rank 0 to the follower ranks of a TP group."""
+
+    def __init__(self, group=None, src: int = 0):
+        self.group, self.src = group, src
+
+    def send(self, msg) -> None:
+        import torch.distributed as dist
+
+        obj = [msg]
+        dist.broadcast_object_list(obj, src=self.src, group=self.group)
+
+    def recv(self):
+        import torch.distributed as dist
+
+        obj = [None]
+        dist.broadcast_object_list(obj, src=self.src, group=self.group)
+        return obj[0]
+
+
+class LLMEngine:
+    def __init__(self, llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.Tensor], max_batch: int = 64,
+                 max_prefill_per_step: int = 4, tp_sync: Optional[TPSync] = None, name: str = "vlm"):
+        self.llm = llm
+        self.kv = kv
+        self.build = prefill_builder
+        self.max_batch = max_batch
+        self.max_prefill = max_prefill_per_step
+        self.sync = tp_sync
+        self.sampler = Sampler(llm)
+        self._ids = itertools.count(1)
+        self._waiting: "queue.Queue[GenRequest]" = queue.Queue()
+        self._running: list[GenRequest] = []
+        self._stop = threading.Event()
+        self._ws: dict = {}
+        self.device = llm.embed.device
+        self.stats = {"prefills": 0, "decode_steps": 0, "tokens": 0}
+        self._thread = threading.Thread(target=self._loop, name=f"lumen-{name}-engine", daemon=True)
+        self._thread.start()
+
+    # ------------------------------------------------------------------ public API
+    def submit(self, prefill_args: Any, prompt_len: int, params: SamplingParams) -> GenRequest:
+        if self._stop.is_set():
+            raise RuntimeError("engine stopped")
+        need = prompt_len + params.max_new_tokens
+        if need > self.kv.capacity_tokens:
+            raise ValueError(f"request needs {need} KV tokens, cache holds {self.kv.capacity_tokens}")
+        if prompt_len + params.max_new_tokens > self.llm.cfg.max_position:
+            params.max_new_tokens = max(1, self.llm.cfg.max_position - prompt_len)
+        r = GenRequest(rid=next(self._ids), prefill_args=prefill_args, prompt_len=prompt_len, params=params,
+                       t_submit=time.perf_counter(), rng=np.random.default_rng(params.seed))
+        self._waiting.put(r)
+        return r
+
+    def close(self) -> None:
+        self._stop.set()
+        self._thread.join(timeout=10)
+        if self.sync is not None:
+            try:
+                self.sync.send(("stop",))
+            except Exception:  # pragma: no cover
+                pass
+
+    # ------------------------------------------------------------------ loop
+    def _emit(self, r: GenRequest, tok: int) -> bool:
+        """record token; returns True when the request finished."""
+        p = r.params
+        if tok in p.stop_token_ids:
+            r.finish_reason = "eos_token"
+            return True
+        r.tokens.append(tok)
+        r.out.put(("token", tok))
+        self.stats["tokens"] += 1
+        if len(r.tokens) >= p.max_new_tokens:
+            r.finish_reason = "length"
+            return True
+        return False
+
+    def _finish(self, r: GenRequest) -> None:
+        self.kv.blocks.release(r.rid)
+        r.out.put(("done", r.finish_reason or "stop"))
+
+    def _fail(self, reqs, e: BaseException) -> None:
+        for r in reqs:
+            try:
+                self.kv.blocks.release(r.rid)
+            except Exception:
+                pass
+            r.out.put(("error", e))
+
+    def cancel(self, r: GenRequest) -> None:
+        r.params.max_new_tokens = len(r.tokens)   # finishes at the next step
+
+    def _admit(self) -> list[GenRequest]:
+        adm = []
+        while len(self._running) + len(adm) < self.max_batch and len(adm) < self.max_prefill:
+            try:
+                r = self._waiting.get_nowait()
+            except queue.Empty:
+                break
+            if not self.kv.blocks.reserve(r.rid, r.prompt_len + r.params.max_new_tokens):
+                self._waiting.put(r)   # retry when blocks free up
+                break
+            adm.append(r)
+        return adm
+
+    @torch.no_grad()
+    def _prefill(self, r: GenRequest) -> None:
+        x = self.build(r.prefill_args)
+        T = x.shape[0]
+        r.prompt_len = T
+        slots = self.kv.slots(r.rid, 0, T)
+        spec = Sampler.spec([r])
+        if self.sync is not None:
+            self.sync.send(("prefill", r.prefill_args, slots, spec))
+        logits = self.llm.prefill(x, self.kv, torch.from_numpy(slots).to(self.device))
+        r.ctx = T
+        tok = self.sampler.pick(self.sampler.candidates(logits, spec), [r])[0]
+        r.t_first = time.perf_counter()
+        self.stats["prefills"] += 1
+        if self._emit(r, tok):
+            self._finish(r)
+        else:
+            self._running.append(r)
+
+    @torch.no_grad()
+    def _decode(self) -> None:
+        reqs = self._running
+        B = len(reqs)
+        ids = np.array([r.tokens[-1] for r in reqs], np.int64)
+        pos = np.array([r.ctx for r in reqs], np.int32)
+        slots = np.concatenate([self.kv.slots(r.rid, r.ctx, 1) for r in reqs])
+        bt = self.kv.block_table([r.rid for r in reqs])
+        ctx = pos + 1
+        spec = Sampler.spec(reqs)
+        if self.sync is not None:
+            self.sync.send(("decode", ids, pos, slots, bt, ctx, spec))
+        logits = self._decode_step(ids, pos, slots, bt, ctx)
+        toks = self.sampler.pick(self.sampler.candidates(logits, spec), reqs)
+        self.stats["decode_steps"] += 1
+        still = []
+        for r, t in zip(reqs, toks):
+            r.ctx += 1
+            if self._emit(r, t):
+                self._finish(r)
+            else:
+                still.append(r)
+        self._running = still
+
+    def _decode_step(self, ids, pos, slots, bt, ctx) -> torch.Tensor:
+        d = self.device
+        return self.llm.decode(torch.from_numpy(ids).to(d), torch.from_numpy(pos).to(d),
+                               torch.from_numpy(slots).to(d), self.kv, torch.from_numpy(bt).to(d),
+                               torch.from_numpy(ctx).to(d), workspace=self._ws)
+
+    def _loop(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        while not self._stop.is_set():
+            adm = self._admit()
+            if not adm and not self._running:
+                try:
+                    r = self._waiting.get(timeout=0.05)
+                    self._waiting.put(r)
+                except queue.Empty:
+                    pass
+                continue
+            for r in adm:
+                try:
+                    self._prefill(r)
+                except Exception as e:  # noqa: BLE001 - surfaced to the caller
+                    log.exception("prefill failed")
+                    self._fail([r], e)
+            if self._running:
+                try:
+                    self._decode()
+                except Exception as e:  # noqa: BLE001
+                    log.exception("decode step failed")
+                    self._fail(self._running, e)
+                    self._running = []
+
+
+def follower_loop(llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.Tensor], sync: TPSync) -> None:
+    """Non-zero TP ranks: replay rank 0's steps so every collective is matched."""
+    sampler = Sampler(llm)
+    ws: dict = {}
+    dev = llm.embed.device
+    while True:
+        msg = sync.recv()
+        kind = msg[0]
+        if kind == "stop":
+            return
+        with torch.no_grad():
+            if kind == "prefill":
+                _, args, slots, spec = msg
+                x = prefill_builder(args)
+                logits = llm.prefill(x, kv, torch.from_numpy(slots).to(dev))
+                sampler.candidates(logits, spec)
+            elif kind == "decode":
+                _, ids, pos, slots, bt, ctx, spec = msg
+                logits = llm.decode(torch.from_numpy(ids).to(dev), torch.from_numpy(pos).to(dev),
+                                    torch.from_numpy(slots).to(dev), kv, torch.from_numpy(bt).to(dev),
+                                    torch.from_numpy(ctx).to(dev), workspace=ws)
+                sampler.candidates(logits, spec)

@@ -1,0 +1,456 @@
+"""MI355X VLM backend (L2): chat template, tokenizer, vision + decoder on the engine.
+
+Contract of the reference ``BaseFastVLMBackend`` / ``FastVLMONNXBackend``
+(packages/lumen-vlm/src/lumen_vlm/backends/base.py:63-553, onnxrt_backend.py:55-811):
+``ChatMessage``, ``GenerationConfig`` / ``KVCacheConfig`` / ``VisionConfig`` from
+``model_info.extra_metadata``, ``GenerationRequest`` defaults (max_new_tokens 512,
+temperature 0, top_p 1, repetition_penalty 1), Jinja2 chat template from
+``tokenizer_config.json`` with the ``<|role|>`` fallback, tokenize / detokenize with
+the HF ``tokenizers`` library, stop-sequence truncation, ``GenerationChunk`` /
+``GenerationResult``.
+
+Differences (deliberate): finish reasons follow the TextGenerationV1
+schema (``eos_token`` / ``length`` / ``stop_sequence``; the reference reports
+"length" on EOS and "max_length"/"stop_seq" on the stream path); repetition_penalty
+is applied (accepted but ignored by the reference); when the rendered prompt has no
+``<image>`` token the image is placed before the first user message (the reference
+silently drops the image); streaming yields per-token chunks as they are produced.
+
+Device work runs on :class:`~lumen_amd.runtime.engine.LLMEngine` (continuous
+batching over a paged KV cache) — concurrent requests share decode steps.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Any, Iterable, Iterator, Mapping, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ...models.llm import TPInfo
+from ...models.vlm import VLM, VLM_PRESETS, VLMConfig
+from ...resources.exceptions import ResourceNotFoundError
+from ...runtime.engine import LLMEngine, SamplingParams
+from ...runtime.kv_cache import PagedKVCache
+from ...utils.image import decode_rgb
+from ..common import GenericResources, load_safetensors, pick_device, runtime_name
+
+log = logging.getLogger("lumen.vlm.backend")
+
+DEFAULT_MAX_NEW_TOKENS = 512
+
+
+class BackendError(Exception):
+    pass
+
+
+class BackendNotInitializedError(BackendError):
+    pass
+
+
+class InvalidInputError(BackendError):
+    pass
+
+
+class ModelLoadingError(BackendError):
+    pass
+
+
+class InferenceError(BackendError):
+    pass
+
+
+@dataclass(frozen=True)
+class ChatMessage:
+    role: str
+    content: str
+
+    def to_mapping(self) -> dict:
+        return {"role": self.role, "content": self.content}
+
+
+@dataclass(frozen=True)
+class GenerationConfig:
+    bos_token_id: int
+    eos_token_id: int
+    pad_token_id: int
+    image_token_index: int
+    vocab_size: int
+    max_position_embeddings: Optional[int] = None
+
+    @classmethod
+    def from_dict(cls, d: Mapping) -> "GenerationConfig":
+        req = ["bos_token_id", "eos_token_id", "pad_token_id", "image_token_index", "vocab_size"]
+        miss = [k for k in req if k not in d]
+        if miss:
+            raise ModelLoadingError(f"generation_config missing required keys: {miss}")
+        return cls(*(int(d[k]) for k in req), max_position_embeddings=d.get("max_position_embeddings"))
+
+
+@dataclass(frozen=True)
+class KVCacheConfig:
+    num_hidden_layers: int
+    num_attention_heads: int
+    num_key_value_heads: int
+    hidden_size: int
+    head_dim: int
+
+    @classmethod
+    def from_dict(cls, d: Mapping) -> "KVCacheConfig":
+        req = ["num_hidden_layers", "num_attention_heads", "num_key_value_heads", "hidden_size", "head_dim"]
+        miss = [k for k in req if k not in d]
+        if miss:
+            raise ModelLoadingError(f"kv_cache_config missing keys: {miss}")
+        return cls(*(int(d[k]) for k in req))
+
+
+@dataclass(frozen=True)
+class VisionConfigMeta:
+    image_size: int
+    patch_size: int
+    mean: tuple
+    std: tuple
+
+    @classmethod
+    def from_dict(cls, d: Mapping) -> "VisionConfigMeta":
+        req = ["image_size", "patch_size", "mean", "std"]
+        miss = [k for k in req if k not in d]
+        if miss:
+            raise ModelLoadingError(f"vision_config missing keys: {miss}")
+        for k in ("mean", "std"):
+            if len(d[k]) != 3:
+                raise ModelLoadingError(f"vision_config entries must have 3 values, got {d[k]}")
+        return cls(int(d["image_size"]), int(d["patch_size"]), tuple(float(x) for x in d["mean"]),
+                   tuple(float(x) for x in d["std"]))
+
+
+@dataclass
+class GenerationRequest:
+    messages: Sequence[ChatMessage]
+    image_bytes: bytes
+    add_generation_prompt: bool = True
+    max_new_tokens: int = DEFAULT_MAX_NEW_TOKENS
+    temperature: float = 0.0
+    top_p: float = 1.0
+    repetition_penalty: float = 1.0
+    stop_sequences: Optional[Sequence[str]] = None
+    do_sample: bool = False
+    stream: bool = False
+    extra: dict = field(default_factory=dict)
+
+
+@dataclass
+class GenerationChunk:
+    text: str
+    tokens: list = field(default_factory=list)
+    is_final: bool = False
+    metadata: dict = field(default_factory=dict)
+
+
+@dataclass
+class GenerationResult:
+    text: str
+    tokens: list
+    finish_reason: str
+    metadata: dict = field(default_factory=dict)
+
+
+@dataclass
+class BackendInfo:
+    runtime: str
+    device: Optional[str] = None
+    model_id: Optional[str] = None
+    model_name: Optional[str] = None
+    version: Optional[str] = None
+    precisions: list = field(default_factory=list)
+    max_new_tokens: Optional[int] = None
+    max_context_length: Optional[int] = None
+    vision_image_size: Optional[int] = None
+    vision_patch_size: Optional[int] = None
+    vocab_size: Optional[int] = None
+    extra: dict = field(default_factory=dict)
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k in ("runtime", "device", "model_id", "model_name", "version",
+                                             "max_new_tokens", "max_context_length", "vision_image_size",
+                                             "vision_patch_size", "vocab_size")}
+        d["precisions"] = list(self.precisions)
+        d.update(self.extra)
+        return d
+
+
+def stop_on_sequences(text: str, stop_sequences: Optional[Sequence[str]]) -> tuple[str, str]:
+    """reference base.py:530-541: cut at the first listed stop sequence found."""
+    if not stop_sequences:
+        return text, ""
+    for s in stop_sequences:
+        if not s:
+            continue
+        i = text.find(s)
+        if i != -1:
+            return text[:i], s
+    return text, ""
+
+
+class MI355XVLMBackend:
+    IMAGE_TOKEN = "<image>"
+
+    def __init__(self, resources: GenericResources, device: Optional[str] = None,
+                 max_new_tokens: Optional[int] = None, tp: Optional[TPInfo] = None, kv_blocks: int = 0,
+                 max_batch: int = 64):
+        self.resources = resources
+        self._device_preference = device
+        self._max_new_tokens = max_new_tokens
+        self.tp = tp or TPInfo()
+        self.kv_blocks = kv_blocks
+        self.max_batch = max_batch
+        self._initialized = False
+        self._tokenizer = None
+        tc = resources.configs.get("tokenizer_config.json") or {}
+        t = tc.get("chat_template")
+        self._chat_template = t if isinstance(t, str) and t.strip() else None
+        from jinja2 import Environment, StrictUndefined
+
+        self._jinja = Environment(trim_blocks=True, lstrip_blocks=True, undefined=StrictUndefined)
+        meta = resources.extra
+        self.generation_config = GenerationConfig.from_dict(meta.get("generation_config", {}))
+        self.kv_cache_config = KVCacheConfig.from_dict(meta.get("kv_cache_config", {}))
+        self.vision_config = VisionConfigMeta.from_dict(meta.get("vision_config", {}))
+        self.model: Optional[VLM] = None
+        self.engine: Optional[LLMEngine] = None
+        self.load_time = 0.0
+
+    # ------------------------------------------------------------------ lifecycle
+    @property
+    def is_initialized(self) -> bool:
+        return self._initialized
+
+    @property
+    def device_preference(self):
+        return self._device_preference
+
+    def ensure_initialized(self) -> None:
+        if not self._initialized:
+            raise BackendNotInitializedError("Backend must be initialized before calling inference APIs.")
+
+    def _vlm_config(self) -> VLMConfig:
+        r = self.resources
+        cfgp = r.model_root_path / "lumen_vlm_config.json"
+        if cfgp.exists():
+            return VLMConfig.from_dict(json.loads(cfgp.read_text()))
+        preset = (r.extra.get("lumen_preset") or "").strip()
+        if preset in VLM_PRESETS:
+            return VLM_PRESETS[preset]
+        raise ResourceNotFoundError(f"{r.model_name}: lumen_vlm_config.json missing (MI355X VLM weights are loaded "
+                                    "from model.safetensors; ONNX graph import is not available in this build)")
+
+    def initialize(self) -> None:
+        if self._initialized:
+            return
+        t0 = time.time()
+        self.device = pick_device(self._device_preference)
+        dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        cfg = self._vlm_config()
+        self.cfg = cfg
+        m = VLM(cfg, self.tp, dtype=dtype, device=self.device)
+        wp = self.resources.model_root_path / "model.safetensors"
+        if wp.exists():
+            m.load_pack_state_dict(load_safetensors(wp))
+        elif self.resources.extra.get("random_init"):
+            m.random_init(int(self.resources.extra.get("seed", 0)))
+        else:
+            raise ResourceNotFoundError(f"{self.resources.model_name}: model.safetensors missing")
+        self.model = m.eval()
+        self.tokenizer()
+        lc = cfg.llm
+        self.kv = PagedKVCache(lc.num_layers, self.model.llm.Hkv, lc.head_dim, num_blocks=self.kv_blocks or None,
+                               device=self.device, dtype=dtype)
+        self.engine = LLMEngine(self.model.llm, self.kv, self._build_prefill, max_batch=self.max_batch)
+        self.load_time = time.time() - t0
+        self._initialized = True
+        log.info("VLM %s ready on %s in %.2fs (KV cache %d tokens, %.1f GB)", self.resources.model_name, self.device,
+                 self.load_time, self.kv.capacity_tokens, self.kv.bytes / 1e9)
+
+    def close(self) -> None:
+        if self.engine is not None:
+            self.engine.close()
+        self._initialized = False
+
+    # ------------------------------------------------------------------ prompt / tokens
+    def build_prompt(self, messages: Sequence[ChatMessage], add_generation_prompt: bool = True) -> str:
+        if not messages:
+            raise InvalidInputError("Chat messages cannot be empty.")
+        if self._chat_template:
+            from jinja2 import TemplateError
+
+            try:
+                out = self._jinja.from_string(self._chat_template).render(
+                    messages=[m.to_mapping() for m in messages], add_generation_prompt=add_generation_prompt)
+                if not isinstance(out, str):
+                    raise TemplateError(f"Template rendered non-string value ({type(out)})")
+                return out.strip()
+            except TemplateError as e:
+                log.warning("Chat template rendering failed (%s). Falling back to naive prompt.", e)
+        parts = [f"<|{m.role}|>\n{m.content.strip()}\n" for m in messages]
+        if add_generation_prompt:
+            parts.append("<|assistant|>\n")
+        return "".join(parts)
+
+    def tokenizer(self):
+        if self._tokenizer is None:
+            p = Path(self.resources.model_root_path) / "tokenizer.json"
+            if not p.exists():
+                raise ResourceNotFoundError(f"Tokenizer file not found at {p}. FastVLM backends require tokenizer.json.")
+            from tokenizers import Tokenizer
+
+            try:
+                self._tokenizer = Tokenizer.from_file(str(p))
+            except Exception as e:  # pragma: no cover
+                raise ModelLoadingError(f"Failed to load tokenizer from {p}: {e}") from e
+        return self._tokenizer
+
+    def tokenize(self, text: str, *, add_special_tokens: bool = False) -> list[int]:
+        try:
+            return self.tokenizer().encode(text, add_special_tokens=add_special_tokens).ids
+        except Exception as e:
+            raise InvalidInputError(f"Tokenization failed: {e}") from e
+
+    def detokenize(self, ids: Sequence[int]) -> str:
+        tok = self.tokenizer()
+        V = tok.get_vocab_size(with_added_tokens=True)
+        try:
+            return tok.decode([int(i) for i in ids if 0 <= int(i) < V], skip_special_tokens=True)
+        except Exception as e:
+            raise InvalidInputError(f"Detokenization failed: {e}") from e
+
+    def stop_on_sequences(self, text, stop_sequences):
+        return stop_on_sequences(text, stop_sequences)
+
+    def build_generation_request(self, *, messages: Sequence[ChatMessage], image_bytes: bytes,
+                                 **overrides: Any) -> GenerationRequest:
+        if not image_bytes:
+            raise InvalidInputError("Image payload is empty.")
+        kw = dict(messages=messages, image_bytes=image_bytes,
+                  add_generation_prompt=overrides.pop("add_generation_prompt", True),
+                  max_new_tokens=overrides.pop("max_new_tokens", self._max_new_tokens or DEFAULT_MAX_NEW_TOKENS),
+                  temperature=overrides.pop("temperature", 0.0), top_p=overrides.pop("top_p", 1.0),
+                  repetition_penalty=overrides.pop("repetition_penalty", 1.0),
+                  stop_sequences=overrides.pop("stop_sequences", None), do_sample=overrides.pop("do_sample", False),
+                  stream=overrides.pop("stream", False), extra=overrides.pop("extra", {}))
+        if overrides:
+            raise InvalidInputError(f"Unknown generation overrides: {list(overrides)}")
+        return GenerationRequest(**kw)
+
+    def _with_image_token(self, messages: Sequence[ChatMessage]) -> list[ChatMessage]:
+        if any(self.IMAGE_TOKEN in m.content for m in messages):
+            return list(messages)
+        out, placed = [], False
+        for m in messages:
+            if not placed and m.role == "user":
+                out.append(ChatMessage(m.role, f"{self.IMAGE_TOKEN}\n{m.content}"))
+                placed = True
+            else:
+                out.append(m)
+        if not placed:
+            out.insert(0, ChatMessage("user", self.IMAGE_TOKEN))
+        return out
+
+    # ------------------------------------------------------------------ generation
+    def _build_prefill(self, args) -> torch.Tensor:
+        ids, img = args
+        tens = [torch.from_numpy(img)] if img is not None else []
+        return self.model.build_prefill(ids, tens)
+
+    def _submit(self, req: GenerationRequest):
+        self.ensure_initialized()
+        prompt = self.build_prompt(self._with_image_token(req.messages), req.add_generation_prompt)
+        ids = self.tokenize(prompt)
+        try:
+            img = decode_rgb(req.image_bytes)
+        except ValueError as e:
+            raise InvalidInputError(str(e)) from e
+        full, starts = self.model.expand_image_tokens(ids, 1)
+        gc = self.generation_config
+        stops = {gc.eos_token_id}
+        extra_eos = self.resources.extra.get("stop_token_ids") or []
+        stops.update(int(t) for t in extra_eos)
+        sp = SamplingParams(max_new_tokens=max(1, int(req.max_new_tokens)), temperature=float(req.temperature),
+                            top_p=float(req.top_p), repetition_penalty=float(req.repetition_penalty),
+                            stop_token_ids=tuple(stops), seed=req.extra.get("seed"))
+        r = self.engine.submit((ids, img if starts else None), len(full), sp)
+        return r, len(full)
+
+    def generate(self, request: GenerationRequest):
+        if request.stream:
+            return self._generate_stream(request)
+        r, n_in = self._submit(request)
+        for _ in r.stream():
+            pass
+        text = self.detokenize(r.tokens)
+        cut, stop = stop_on_sequences(text, request.stop_sequences)
+        reason = "stop_sequence" if stop else (r.finish_reason or "stop")
+        return GenerationResult(text=cut, tokens=list(r.tokens), finish_reason=reason,
+                                metadata={"tokens_generated": len(r.tokens), "input_tokens": n_in,
+                                          "ttft_ms": (r.t_first - r.t_submit) * 1000 if r.t_first else None})
+
+    def _generate_stream(self, request: GenerationRequest) -> Iterator[GenerationChunk]:
+        r, n_in = self._submit(request)
+        emitted = ""
+        step = 0
+        for kind, val in r.stream():
+            if kind == "token":
+                text = self.detokenize(r.tokens)
+                cut, stop = stop_on_sequences(text, request.stop_sequences)
+                if stop:
+                    if len(cut) > len(emitted):
+                        yield GenerationChunk(text=cut[len(emitted):], tokens=[val], metadata={"step": step})
+                    self.engine.cancel(r)
+                    for _ in r.stream():
+                        pass
+                    yield GenerationChunk(text="", is_final=True, metadata={"reason": "stop_sequence",
+                                                                           "input_tokens": n_in})
+                    return
+                # hold back text that may be an incomplete UTF-8 sequence
+                if text.endswith("�"):
+                    continue
+                yield GenerationChunk(text=text[len(emitted):], tokens=[val], metadata={"step": step})
+                emitted = text
+                step += 1
+            else:
+                tail = self.detokenize(r.tokens)
+                if len(tail) > len(emitted):
+                    yield GenerationChunk(text=tail[len(emitted):], metadata={"step": step})
+                yield GenerationChunk(text="", is_final=True, metadata={"reason": val, "input_tokens": n_in})
+
+    def get_info(self) -> BackendInfo:
+        gc, vc = self.generation_config, self.vision_config
+        dev = getattr(self, "device", None)
+        return BackendInfo(runtime=runtime_name(dev) if dev is not None else "mi355x-hip",
+                           device=str(dev or self._device_preference), model_id=self.resources.model_info.name,
+                           model_name=self.resources.model_info.name, version=self.resources.model_info.version,
+                           precisions=["bf16"] if dev is None or dev.type == "cuda" else ["fp32"],
+                           max_new_tokens=self._max_new_tokens or DEFAULT_MAX_NEW_TOKENS,
+                           max_context_length=gc.max_position_embeddings, vision_image_size=vc.image_size,
+                           vision_patch_size=vc.patch_size, vocab_size=gc.vocab_size,
+                           extra={"tp_size": str(self.tp.world),
+                                  "kv_cache_tokens": str(self.kv.capacity_tokens) if self._initialized else "0"})
+
+
+def create_backend(settings, resources: GenericResources, runtime: Optional[str] = None) -> MI355XVLMBackend:
+    """Factory (reference backends/factory.py:15-82, onnx only; max_new_tokens fixed 512)."""
+    rt = runtime or resources.runtime
+    if rt not in ("onnx", "torch", "rknn"):
+        raise ValueError(f"unsupported runtime '{rt}'")
+    if rt == "rknn":
+        raise BackendError("RKNN runtime is not available on MI355X builds")
+    from ...resources.config import AmdRuntimeSettings
+
+    amd = AmdRuntimeSettings.from_env()
+    dev = getattr(settings, "device", None) if settings is not None else None
+    return MI355XVLMBackend(resources, device=dev, max_new_tokens=DEFAULT_MAX_NEW_TOKENS, kv_blocks=amd.kv_blocks,
+                            max_batch=min(amd.max_batch, 64))

@@ -1,0 +1,102 @@
+"""VLM decoder / engine / service on the MI355X path vs the fp32 CPU reference."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from lumen_amd.models.llm import LLM, LLM_PRESETS, LLMConfig
+from lumen_amd.runtime.engine import LLMEngine, SamplingParams
+from lumen_amd.runtime.kv_cache import PagedKVCache
+
+pytestmark = pytest.mark.gpu
+
+
+def _cos(a, b):
+    return torch.nn.functional.cosine_similarity(a.float().flatten(), b.float().flatten(), dim=0).item()
+
+
+@pytest.mark.parametrize("preset", ["qwen2-0.5b", "llama-small"])
+def test_decoder_gpu_vs_cpu(preset):
+    if preset == "llama-small":
+        cfg = LLMConfig(vocab_size=32000, hidden_size=1024, num_layers=4, num_heads=8, num_kv_heads=2, head_dim=128,
+                        intermediate_size=2816, rope_theta=500000.0, rms_eps=1e-5, max_position=4096,
+                        tie_word_embeddings=False, qkv_bias=False)
+    else:
+        cfg = LLM_PRESETS[preset]
+    ref = LLM(cfg, dtype=torch.float32, device="cpu")
+    ref.random_init(1)
+    gpu = LLM(cfg, dtype=torch.bfloat16, device="cuda")
+    gpu.load_state_dict({k: v.to(torch.bfloat16) if v.dtype == torch.float32 and "qkv_b" not in k else v
+                         for k, v in ref.state_dict().items()}, strict=False)
+    T = 150
+    ids = torch.randint(0, cfg.vocab_size, (T + 3,), generator=torch.Generator().manual_seed(0))
+    outs = {}
+    for name, m, dev in (("cpu", ref, "cpu"), ("gpu", gpu, "cuda")):
+        kv = PagedKVCache(cfg.num_layers, m.Hkv, cfg.head_dim, num_blocks=16, device=dev,
+                          dtype=torch.float32 if dev == "cpu" else torch.bfloat16)
+        kv.blocks.reserve(1, T + 3)
+        lg = [m.prefill(m.embed_tokens(ids[:T].to(dev)), kv, torch.from_numpy(kv.slots(1, 0, T)).to(dev)).cpu()]
+        bt = torch.from_numpy(kv.block_table([1])).to(dev)
+        for p in range(T, T + 3):
+            lg.append(m.decode(ids[p:p + 1].to(dev), torch.tensor([p], dtype=torch.int32, device=dev),
+                               torch.from_numpy(kv.slots(1, p, 1)).to(dev), kv, bt,
+                               torch.tensor([p + 1], dtype=torch.int32, device=dev)).cpu())
+        outs[name] = lg
+    for a, b in zip(outs["gpu"], outs["cpu"]):
+        assert _cos(a, b) > 0.995
+
+
+def test_engine_gpu_batched():
+    cfg = LLM_PRESETS["qwen2-0.5b"]
+    m = LLM(cfg, device="cuda")
+    m.random_init(2)
+    kv = PagedKVCache(cfg.num_layers, m.Hkv, cfg.head_dim, num_blocks=256, device="cuda")
+    eng = LLMEngine(m, kv, lambda ids: m.embed_tokens(torch.tensor(ids, device="cuda")), max_batch=16)
+    try:
+        prompts = [list(np.random.default_rng(i).integers(0, 150000, 30 + 11 * i)) for i in range(6)]
+        solo = []
+        for p in prompts:
+            r = eng.submit(p, len(p), SamplingParams(max_new_tokens=5))
+            list(r.stream(timeout=120))
+            solo.append(r.tokens)
+        rs = [eng.submit(p, len(p), SamplingParams(max_new_tokens=5)) for p in prompts]
+        agree = 0
+        for r, ref in zip(rs, solo):
+            list(r.stream(timeout=120))
+            assert len(r.tokens) == 5
+            agree += r.tokens[:2] == ref[:2]
+        assert agree >= 5          # bf16 batch-vs-solo rounding may flip a near-tie
+        s = eng.submit(prompts[0], len(prompts[0]), SamplingParams(max_new_tokens=16, temperature=0.8, top_p=0.9,
+                                                                   repetition_penalty=1.2, seed=1))
+        list(s.stream(timeout=120))
+        assert len(s.tokens) == 16
+    finally:
+        eng.close()
+
+
+def test_vlm_service_gpu(tmp_path):
+    from lumen_amd.models.vlm import write_vlm_model
+    from lumen_amd.resources.validator import config_from_dict
+    from lumen_amd.services.vlm import GeneralFastVLMService
+    from lumen_amd.utils.image import encode_jpeg
+
+    write_vlm_model(tmp_path / "models" / "fastvlm-tiny", "fastvlm-tiny")
+    cfg = {"metadata": {"version": "1.0.0", "region": "other", "cache_dir": str(tmp_path)},
+           "deployment": {"mode": "single", "service": "vlm"}, "server": {"port": 50557, "host": "127.0.0.1"},
+           "services": {"vlm": {"enabled": True, "package": "lumen_vlm",
+                                "import_info": {"registry_class": "lumen_vlm.fastvlm.GeneralFastVLMService",
+                                                "add_to_server": "lumen_vlm.proto.ml_service_pb2_grpc.add_InferenceServicer_to_server"},
+                                "backend_settings": {"device": "cuda"},
+                                "models": {"general": {"model": "fastvlm-tiny", "runtime": "onnx"}}}}}
+    s = GeneralFastVLMService.from_config(config_from_dict(cfg).services["vlm"], tmp_path)
+    s.initialize()
+    try:
+        img = encode_jpeg(np.random.default_rng(0).integers(0, 255, (50, 70, 3), dtype=np.uint8))
+        body, _, meta = s.handle("vlm_generate", img, "image/jpeg", {"prompt": "Describe.", "max_new_tokens": "10"})
+        d = json.loads(body)
+        assert d["generated_tokens"] == 10 and float(meta["ttft_ms"]) > 0
+        out = list(s.handle("vlm_generate_stream", img, "image/jpeg", {"prompt": "Hi", "max_new_tokens": "7"}))
+        assert json.loads(out[-1][0])["generated_tokens"] == 7 and out[-1][3]
+    finally:
+        s.close()

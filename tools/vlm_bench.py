@@ -1,0 +1,101 @@
+"""VLM time-to-first-token / decode throughput benchmark (BASELINE metric "VLM p50 TTFT").
+
+TTFT is measured like the reference's generate() up to its first sampled token
+(packages/lumen-vlm/src/lumen_vlm/backends/onnxrt_backend.py:161-214): JPEG decode ->
+pad/resize/normalise -> vision tower -> projector -> token embeddings + image splice
+-> full prefill -> first token, single request, random-init weights of the named
+architecture, synthetic 1024x768 JPEG.  Also reports single-stream decode tokens/s and
+batched decode throughput with concurrent requests on the continuous-batching engine.
+
+usage: python tools/vlm_bench.py --preset fastvlm-0.5b --n 20 --max-new 64 --batch 16
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from lumen_amd._native import load_hip  # noqa: E402
+from lumen_amd.models.vlm import VLM, VLM_PRESETS  # noqa: E402
+from lumen_amd.runtime.engine import LLMEngine, SamplingParams  # noqa: E402
+from lumen_amd.runtime.kv_cache import PagedKVCache  # noqa: E402
+from lumen_amd.utils.image import decode_rgb, encode_jpeg  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--preset", default="fastvlm-0.5b")
+    ap.add_argument("--n", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--max-new", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--prompt-tokens", type=int, default=48)
+    ap.add_argument("--kv-blocks", type=int, default=4096)
+    args = ap.parse_args()
+    load_hip(required=True)
+    dev = torch.device("cuda")
+    cfg = VLM_PRESETS[args.preset]
+    t0 = time.time()
+    m = VLM(cfg, device=dev)
+    m.random_init(0)
+    torch.cuda.synchronize()
+    load_s = time.time() - t0
+    kv = PagedKVCache(cfg.llm.num_layers, m.llm.Hkv, cfg.llm.head_dim, num_blocks=args.kv_blocks, device=dev)
+
+    def build(a):
+        ids, jpeg = a
+        img = torch.from_numpy(decode_rgb(jpeg))
+        return m.build_prefill(ids, [img])
+
+    eng = LLMEngine(m.llm, kv, build, max_batch=max(args.batch, 1))
+    rng = np.random.default_rng(0)
+    jpeg = encode_jpeg(rng.integers(0, 255, (768, 1024, 3), dtype=np.uint8))
+    V = cfg.llm.vocab_size
+    text = [int(t) for t in rng.integers(1000, min(V, 30000), args.prompt_tokens)]
+    ids = text[:8] + [cfg.image_token_id] + text[8:]
+    full, _ = m.expand_image_tokens(ids, 1)
+    eos_none = SamplingParams(max_new_tokens=args.max_new, stop_token_ids=())
+
+    def one(max_new):
+        r = eng.submit((ids, jpeg), len(full), SamplingParams(max_new_tokens=max_new))
+        times = []
+        for kind, _ in r.stream(timeout=600):
+            times.append(time.perf_counter())
+        return r, times
+
+    for _ in range(args.warmup):
+        one(4)
+    ttft, tps = [], []
+    for _ in range(args.n):
+        r, times = one(args.max_new)
+        ttft.append((r.t_first - r.t_submit) * 1000)
+        if len(r.tokens) > 1:
+            tps.append((len(r.tokens) - 1) / (times[len(r.tokens) - 1] - times[0]))
+    # batched decode throughput
+    t1 = time.perf_counter()
+    rs = [eng.submit((ids, jpeg), len(full), SamplingParams(max_new_tokens=args.max_new)) for _ in range(args.batch)]
+    ntok = 0
+    for r in rs:
+        list(r.stream(timeout=900))
+        ntok += len(r.tokens)
+    batch_s = time.perf_counter() - t1
+    eng.close()
+    out = {"metric": "VLM p50 TTFT", "value": float(np.percentile(ttft, 50)), "unit": "ms",
+           "higher_is_better": False, "p90_ttft_ms": float(np.percentile(ttft, 90)),
+           "min_ttft_ms": float(np.min(ttft)), "decode_tok_s_single": float(np.median(tps)) if tps else None,
+           "batch": args.batch, "batch_tok_s": ntok / batch_s, "prompt_tokens": len(full),
+           "image_tokens": cfg.num_image_tokens, "max_new_tokens": args.max_new, "n": args.n,
+           "preset": args.preset, "dtype": "bf16", "data": "synthetic (random-init weights, random 1024x768 JPEG)",
+           "load_s": load_s, "kv_cache_tokens": kv.capacity_tokens}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
