@@ -62,6 +62,14 @@ def create_app(state: Optional[AppState] = None) -> FastAPI:
     def health():
         return {"status": "ok", "version": "0.1.0"}
 
+    @app.get("/metrics")
+    def metrics():
+        from fastapi.responses import Response
+
+        from ..runtime.metrics import exposition
+
+        return Response(exposition(), media_type="text/plain; version=0.0.4")
+
     # ------------------------------------------------------------------ config
     cfg = APIRouter(prefix="/api/v1/config")
 

@@ -135,6 +135,11 @@ def serve(config_path: str, port_override: Optional[int] = None, mode: str = "hu
     port = port_override or config.server.port
     server, bound = build_server(servicer, host, port)
     server.start()
+    from ..runtime.metrics import start_metrics_server
+
+    mport = start_metrics_server()
+    if mport:
+        log.info("Prometheus metrics on :%d/metrics", mport)
     kind = "Hub" if mode == "hub" else "single-service"
     log.info("🚀 Lumen %s service listening on %s:%d", kind, host, bound)
     print(f"Lumen {kind} service listening on {host}:{bound}", flush=True)

@@ -24,6 +24,7 @@ from typing import Any, Callable, Iterable, Optional
 import grpc
 
 from ..proto import ml_service as pb
+from ..runtime.metrics import maybe_fault, observe_request
 
 log = logging.getLogger("lumen.service")
 
@@ -199,24 +200,30 @@ class BaseInferenceService(pb.InferenceServicer):
                         yield self._error(cid, self.UNKNOWN_TASK_CODE, str(e))
                         continue
                     meta = self._request_meta(req, context)
+                    maybe_fault("infer")
                     out = handler(payload, req.payload_mime, meta)
                     if hasattr(out, "__next__"):  # streaming handler: yields (bytes, mime, meta, is_final)
                         for chunk in out:
                             res, mime, extra, final = chunk
                             m = dict(extra or {})
                             m[self.LATENCY_KEY] = str(int((time.perf_counter() - t0) * 1000))
+                            schema = mime.split("schema=")[-1] if (final and "schema=" in mime) else ""
                             yield pb.InferResponse(correlation_id=cid, is_final=final, result=res, result_mime=mime,
-                                                   meta=m)
+                                                   meta=m, result_schema=schema)
+                        observe_request(self.SERVICE_NAME, task, "ok", time.perf_counter() - t0)
                         continue
                     res, mime, extra = out
                     m = dict(extra or {})
                     m[self.LATENCY_KEY] = str(int((time.perf_counter() - t0) * 1000))
                     schema = mime.split("schema=")[-1] if "schema=" in mime else ""
+                    observe_request(self.SERVICE_NAME, task, "ok", time.perf_counter() - t0)
                     yield pb.InferResponse(correlation_id=cid, is_final=True, result=res, result_mime=mime, meta=m,
                                            result_schema=schema)
                 except Exception as e:
                     log.exception("task %s failed", req.task)
-                    yield self._error(cid, pb.ERROR_CODE_INTERNAL, str(e))
+                    code = pb.ERROR_CODE_UNAVAILABLE if _unavailable(e) else pb.ERROR_CODE_INTERNAL
+                    observe_request(self.SERVICE_NAME, req.task, "error", time.perf_counter() - t0)
+                    yield self._error(cid, code, str(e))
         finally:
             buffers.clear()
 
@@ -231,6 +238,13 @@ class BaseInferenceService(pb.InferenceServicer):
 
     def build_capability(self) -> "pb.Capability":  # pragma: no cover - overridden
         return self.registry.build_capability(self.SERVICE_NAME, "unknown", "mi355x", ["bf16"])
+
+
+def _unavailable(e: BaseException) -> bool:
+    """Backend not ready / worker or engine gone -> UNAVAILABLE (client may retry elsewhere)."""
+    name = type(e).__name__
+    return ("NotInitialized" in name or "DeviceUnavailable" in name or "Unavailable" in name
+            or (isinstance(e, RuntimeError) and "engine stopped" in str(e)))
 
 
 def json_bytes(obj: Any) -> bytes:
