@@ -226,6 +226,7 @@ hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream) {
   dim3 grid(a.nsplit, a.Hkv, B), block(256);
   if (D == 64) hipLaunchKernelGGL(paged_decode_kernel<64>, grid, block, 0, stream, a);
   else if (D == 128) hipLaunchKernelGGL(paged_decode_kernel<128>, grid, block, 0, stream, a);
+  else if (D == 32) hipLaunchKernelGGL(paged_decode_kernel<32>, grid, block, 0, stream, a);
   else return hipErrorInvalidValue;
   if (a.nsplit > 1) hipLaunchKernelGGL(decode_combine_kernel, dim3(B * a.H), dim3(128), 0, stream, a, D);
   return hipGetLastError();

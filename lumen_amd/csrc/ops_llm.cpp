@@ -62,7 +62,7 @@ void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
                   const c10::optional<at::Tensor>& part_ml) {
   const int64_t D = k_cache.size(3);
   check_cache(k_cache, v_cache, Hkv, D);
-  TORCH_CHECK(D == 64 || D == 128, "paged_decode: head dim 64 or 128");
+  TORCH_CHECK(D == 32 || D == 64 || D == 128, "paged_decode: head dim 32, 64 or 128");
   TORCH_CHECK(H % Hkv == 0 && H / Hkv <= 16, "paged_decode: at most 16 query heads per kv head");
   TORCH_CHECK(q.is_cuda() && q.scalar_type() == at::kBFloat16 && q.dim() == 2 && q.stride(1) == 1 && q.size(1) >= H * D &&
               q.stride(0) % 8 == 0, "paged_decode: q rows");

@@ -56,7 +56,7 @@ def test_rope_kv(H, Hkv, D):
     assert torch.equal(vc_g.cpu(), vc_ref)
 
 
-@pytest.mark.parametrize("H,Hkv,D", [(14, 2, 64), (32, 8, 128), (32, 32, 128), (16, 1, 64)])
+@pytest.mark.parametrize("H,Hkv,D", [(14, 2, 64), (32, 8, 128), (32, 32, 128), (16, 1, 64), (4, 2, 32)])
 @pytest.mark.parametrize("lens", [[1, 64, 65], [700, 3, 2048 + 17], [5000]])
 def test_paged_decode(H, Hkv, D, lens):
     g = torch.Generator().manual_seed(H * D + len(lens))
