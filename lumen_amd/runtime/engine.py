@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import itertools
 import logging
+import os
 import queue
 import threading
 import time
@@ -151,9 +152,84 @@ class TPSync:
         return obj[0]
 
 
+class DecodeGraphs:
+    """hipGraph-captured decode steps, one graph per padded batch-size bucket.
+
+    A decode step is ~10 kernels per layer (hundreds per token) whose host launch
+    cost dominates small-batch decode; replaying a captured graph issues them in one
+    call.  Inputs are copied into static buffers (ids, positions, cache slots, block
+    table of fixed width, context lengths); padded rows use slot -1 (no cache write)
+    and context 1, and their logits are ignored.
+    """
+
+    BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128)
+
+    def __init__(self, llm, kv: PagedKVCache, max_batch: int, max_blocks: int):
+        self.llm, self.kv = llm, kv
+        self.max_blocks = max_blocks
+        self.buckets = [b for b in self.BUCKETS if b <= max(max_batch, 1)] or [1]
+        if self.buckets[-1] < max_batch:
+            self.buckets.append(max_batch)
+        self.graphs: dict[int, tuple] = {}
+        self.pool = None
+
+    def _bucket(self, B: int) -> int:
+        for b in self.buckets:
+            if b >= B:
+                return b
+        raise ValueError(f"batch {B} exceeds graph buckets {self.buckets}")
+
+    def _capture(self, Bp: int):
+        d = self.llm.embed.device
+        st = {"ids": torch.zeros(Bp, dtype=torch.long, device=d), "pos": torch.zeros(Bp, dtype=torch.int32, device=d),
+              "slots": torch.full((Bp,), -1, dtype=torch.long, device=d),
+              "bt": torch.zeros((Bp, self.max_blocks), dtype=torch.int32, device=d),
+              "ctx": torch.ones(Bp, dtype=torch.int32, device=d)}
+        ws: dict = {}
+
+        def run():
+            return self.llm.decode(st["ids"], st["pos"], st["slots"], self.kv, st["bt"], st["ctx"], workspace=ws)
+
+        s = torch.cuda.Stream(d)
+        s.wait_stream(torch.cuda.current_stream(d))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                run()
+        torch.cuda.current_stream(d).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        if self.pool is None:
+            self.pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(g, pool=self.pool):
+            out = run()
+        self.graphs[Bp] = (g, st, out, ws)
+
+    def run(self, ids, pos, slots, bt, ctx) -> torch.Tensor:
+        B = len(ids)
+        Bp = self._bucket(B)
+        if Bp not in self.graphs:
+            self._capture(Bp)
+        g, st, out, _ = self.graphs[Bp]
+        w = min(bt.shape[1], self.max_blocks)
+        ids_p = np.zeros(Bp, np.int64)
+        ids_p[:B] = ids
+        pos_p = np.zeros(Bp, np.int32)
+        pos_p[:B] = pos
+        sl_p = np.full(Bp, -1, np.int64)
+        sl_p[:B] = slots
+        bt_p = np.zeros((Bp, self.max_blocks), np.int32)
+        bt_p[:B, :w] = bt[:, :w]
+        ctx_p = np.ones(Bp, np.int32)
+        ctx_p[:B] = ctx
+        for k, v in (("ids", ids_p), ("pos", pos_p), ("slots", sl_p), ("bt", bt_p), ("ctx", ctx_p)):
+            st[k].copy_(torch.from_numpy(v), non_blocking=True)
+        g.replay()
+        return out[:B]
+
+
 class LLMEngine:
     def __init__(self, llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.Tensor], max_batch: int = 64,
-                 max_prefill_per_step: int = 4, tp_sync: Optional[TPSync] = None, name: str = "vlm"):
+                 max_prefill_per_step: int = 4, tp_sync: Optional[TPSync] = None, name: str = "vlm",
+                 use_graphs: Optional[bool] = None):
         self.llm = llm
         self.kv = kv
         self.build = prefill_builder
@@ -168,6 +244,11 @@ class LLMEngine:
         self._ws: dict = {}
         self.device = llm.embed.device
         self.stats = {"prefills": 0, "decode_steps": 0, "tokens": 0}
+        if use_graphs is None:
+            use_graphs = os.environ.get("LUMEN_HIP_GRAPHS", "1") == "1"
+        self.graphs: Optional[DecodeGraphs] = None
+        if use_graphs and self.device.type == "cuda" and not llm.tp.enabled:
+            self.graphs = DecodeGraphs(llm, kv, max_batch, -(-llm.cfg.max_position // 64))
         self._thread = threading.Thread(target=self._loop, name=f"lumen-{name}-engine", daemon=True)
         self._thread.start()
 
@@ -282,6 +363,12 @@ class LLMEngine:
 
     def _decode_step(self, ids, pos, slots, bt, ctx) -> torch.Tensor:
         d = self.device
+        if self.graphs is not None and bt.shape[1] <= self.graphs.max_blocks:
+            try:
+                return self.graphs.run(ids, pos, slots, bt, ctx)
+            except Exception as e:  # noqa: BLE001 - capture unsupported: fall back to eager launches
+                log.warning("hipGraph decode disabled: %s", e)
+                self.graphs = None
         return self.llm.decode(torch.from_numpy(ids).to(d), torch.from_numpy(pos).to(d),
                                torch.from_numpy(slots).to(d), self.kv, torch.from_numpy(bt).to(d),
                                torch.from_numpy(ctx).to(d), workspace=self._ws)

@@ -100,3 +100,25 @@ def test_vlm_service_gpu(tmp_path):
         assert json.loads(out[-1][0])["generated_tokens"] == 7 and out[-1][3]
     finally:
         s.close()
+
+
+def test_decode_graphs_match_eager():
+    cfg = LLM_PRESETS["qwen2-0.5b"]
+    m = LLM(cfg, device="cuda")
+    m.random_init(5)
+    kv = PagedKVCache(cfg.num_layers, m.Hkv, cfg.head_dim, num_blocks=64, device="cuda")
+    prompts = [list(np.random.default_rng(i).integers(0, 150000, 40 + 9 * i)) for i in range(3)]
+    outs = {}
+    for graphs in (False, True):
+        eng = LLMEngine(m, kv, lambda ids: m.embed_tokens(torch.tensor(ids, device="cuda")), max_batch=4,
+                        use_graphs=graphs)
+        try:
+            rs = [eng.submit(p, len(p), SamplingParams(max_new_tokens=6)) for p in prompts]
+            for r in rs:
+                list(r.stream(timeout=120))
+            outs[graphs] = [r.tokens for r in rs]
+            if graphs:
+                assert eng.graphs is not None and eng.graphs.graphs, "decode graphs were not captured"
+        finally:
+            eng.close()
+    assert outs[True] == outs[False]

@@ -1,0 +1,123 @@
+"""Face and OCR pipeline throughput on one MI355X (synthetic images, random-init weights).
+
+face: JPEG decode -> letterbox 640 -> SCRFD-10G-shaped detector -> decode/NMS ->
+      ArcFace IResNet-100 (antelopev2 geometry) on a fixed number of faces per image
+      (random weights detect nothing meaningful, so the recogniser batch is fed a
+      fixed F faces/image of 5-point alignments to exercise the full path).
+ocr:  JPEG decode -> DBNet (limit 960) -> DB geometry -> SVTR recogniser on a fixed
+      number of text crops per image.
+
+usage: python tools/face_ocr_bench.py --what face --batch 32 --iters 10
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from lumen_amd._native import load_hip  # noqa: E402
+from lumen_amd.ops import vision  # noqa: E402
+from lumen_amd.utils.image import decode_many, encode_jpeg  # noqa: E402
+
+
+def bench_face(args):
+    from lumen_amd.models.face import IRESNET_PRESETS, SCRFD, SCRFD_PRESETS, IResNet
+    from lumen_amd.services.face.backend import DetParams, FaceSpec, MI355XFaceBackend
+
+    dev = torch.device("cuda")
+    det = SCRFD(SCRFD_PRESETS["10g"])
+    det.random_init(torch.Generator().manual_seed(0))
+    rec = IResNet(IRESNET_PRESETS[args.rec])
+    rec.random_init(torch.Generator().manual_seed(1))
+    be = MI355XFaceBackend.__new__(MI355XFaceBackend)
+    be.det, be.rec, be.spec, be.device, be.dtype = det.to(dev).eval(), rec.to(dev).eval(), FaceSpec(), dev, torch.bfloat16
+    be.template = vision.ARCFACE_DST
+    rng = np.random.default_rng(0)
+    jpegs = [encode_jpeg(rng.integers(0, 255, (720, 1280, 3), dtype=np.uint8)) for _ in range(args.batch)]
+    lms = np.array([[500, 300], [580, 300], [540, 350], [510, 400], [570, 400]], np.float32)
+    minv = np.stack([vision.invert_affine(vision.similarity_transform(lms + 3 * k)) for k in range(args.faces)])
+
+    def step():
+        imgs = decode_many(jpegs)
+        be.detect_images(imgs, [DetParams(0.5, 0.4, 20, 2000)] * len(imgs))
+        idx = [i for i in range(len(imgs)) for _ in range(args.faces)]
+        be.embed_faces(imgs, idx, np.concatenate([minv] * len(imgs)))
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(args.iters):
+        step()
+    dt = (time.perf_counter() - t0) / args.iters
+    return {"metric": "face detect+embed images/s", "value": args.batch / dt, "unit": "img/s",
+            "ms_per_batch": dt * 1000, "batch": args.batch, "faces_per_image": args.faces,
+            "faces_per_s": args.batch * args.faces / dt, "detector": "SCRFD-10G-shaped 640",
+            "recogniser": f"IResNet-{args.rec}", "image": "1280x720 JPEG"}
+
+
+def bench_ocr(args):
+    from lumen_amd.models.ocr import DBNET_PRESETS, REC_PRESETS, DBNet, SVTRRecognizer
+    from lumen_amd.services.ocr.backend import DET_DEFAULTS, REC_DEFAULTS, MI355XOcrBackend, OcrParams
+
+    dev = torch.device("cuda")
+    be = MI355XOcrBackend.__new__(MI355XOcrBackend)
+    det = DBNet(DBNET_PRESETS["mobile"])
+    det.random_init(torch.Generator().manual_seed(0))
+    rec = SVTRRecognizer(REC_PRESETS["mobile"])
+    rec.random_init(torch.Generator().manual_seed(1))
+    be.det, be.rec, be.device, be.dtype = det.to(dev).eval(), rec.to(dev).eval(), dev, torch.bfloat16
+    be.det_config, be.rec_config = dict(DET_DEFAULTS), dict(REC_DEFAULTS)
+    be.rec_h, be.rec_batch, be.bucket = 48, 256, 32
+    be.character_str = ["blank"] + [chr(0x4E00 + i) for i in range(REC_PRESETS["mobile"].num_classes - 1)]
+    rng = np.random.default_rng(0)
+    jpegs = [encode_jpeg(rng.integers(0, 255, (720, 960, 3), dtype=np.uint8)) for _ in range(args.batch)]
+    boxes = []
+    for k in range(args.crops):
+        y = 20 + 25 * k
+        boxes.append(np.array([[30, y], [30 + 200 + 10 * k, y], [30 + 200 + 10 * k, y + 22], [30, y + 22]], np.int32))
+
+    def step():
+        imgs = decode_many(jpegs)
+        be.detect(imgs, [OcrParams()] * len(imgs))
+        crops = [(i, b) for i in range(len(imgs)) for b in boxes]
+        be.recognize(imgs, crops)
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(args.iters):
+        step()
+    dt = (time.perf_counter() - t0) / args.iters
+    return {"metric": "ocr images/s", "value": args.batch / dt, "unit": "img/s", "ms_per_batch": dt * 1000,
+            "batch": args.batch, "crops_per_image": args.crops, "crops_per_s": args.batch * args.crops / dt,
+            "detector": "DBNet-mobile 960", "recogniser": "SVTR-LCNet mobile", "image": "960x720 JPEG"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--what", choices=["face", "ocr"], default="face")
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--faces", type=int, default=4)
+    ap.add_argument("--crops", type=int, default=20)
+    ap.add_argument("--rec", default="r100")
+    a = ap.parse_args()
+    load_hip(required=True)
+    with torch.no_grad():
+        out = bench_face(a) if a.what == "face" else bench_ocr(a)
+    out.update({"dtype": "bf16", "data": "synthetic (random-init weights, random JPEGs)"})
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
