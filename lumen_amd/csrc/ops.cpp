@@ -19,6 +19,9 @@
 namespace lumen {
 hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
                      int64_t ldc, int M, int N, int K, const GemmEpi& ep, int tile, hipStream_t stream);
+hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
+                       int N, int K, const GemmEpi& ep, float* ws, int ksplit, hipStream_t stream);
+int skinny_ksplit(int N, int K);
 hipError_t norm_rows(const uint16_t* x, int64_t x_stride, const int64_t* row_idx, const uint16_t* add,
                      int64_t add_stride, uint16_t* resid_out, int64_t resid_stride, const uint16_t* w,
                      const uint16_t* b, void* out, int64_t out_stride, int out_f32, int rows, int D,
@@ -42,7 +45,8 @@ struct PrepArgs {
 };
 hipError_t image_prep(const PrepArgs& a, int B, int max_ch, int max_dw, hipStream_t stream);
 hipError_t row_topk(const float* scores, int64_t ld, int B, int N, int k, float scale, float* out_v, int* out_i,
-                    float* out_lse, int index_offset, hipStream_t stream);
+                    float* out_lse, int index_offset, float* ws, hipStream_t stream);
+int topk_chunks(int N);
 }  // namespace lumen
 
 namespace {
@@ -121,6 +125,15 @@ void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tens
     ep.prelu = bf(*prelu);
   }
   const at::DeviceGuard guard(a.device());
+  // decode-shaped GEMMs (M <= 32): bandwidth-bound split-K kernel (tile -1 = auto, 9 = force)
+  if ((tile == -1 || tile == 9) && M <= 32 && M > 0) {
+    const int ks = lumen::skinny_ksplit((int)N, (int)K);
+    at::Tensor ws;
+    if (ks > 1) ws = at::zeros({M, N}, a.options().dtype(at::kFloat));
+    LUMEN_CHECK_HIP(lumen::gemm_skinny(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0), (int)M,
+                                       (int)N, (int)K, ep, ks > 1 ? ws.data_ptr<float>() : nullptr, ks, cur_stream()));
+    return;
+  }
   LUMEN_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
                                    (int)M, (int)N, (int)K, ep, (int)tile, cur_stream()));
 }
@@ -271,9 +284,12 @@ void row_topk(const at::Tensor& scores, int64_t k, double scale, at::Tensor out_
     lse = out_lse->data_ptr<float>();
   }
   const at::DeviceGuard guard(scores.device());
+  const int nch = lumen::topk_chunks((int)scores.size(1));
+  at::Tensor ws;
+  if (nch > 1) ws = at::empty({B * nch * (2 * k + 2)}, scores.options());
   LUMEN_CHECK_HIP(lumen::row_topk(scores.data_ptr<float>(), scores.stride(0), (int)B, (int)scores.size(1), (int)k,
                                   (float)scale, out_v.data_ptr<float>(), out_i.data_ptr<int>(), lse, (int)index_offset,
-                                  cur_stream()));
+                                  nch > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
 }
 
 // ---------------------------------------------------------------- convolution / CNN support (NHWC)

@@ -179,11 +179,19 @@ class DecodeGraphs:
                 return b
         raise ValueError(f"batch {B} exceeds graph buckets {self.buckets}")
 
-    def _capture(self, Bp: int):
+    def _width(self, w: int) -> int:
+        """block-table width bucket: the decode kernel's split count follows the width,
+        so short contexts must not pay for the maximum-length table."""
+        for b in (8, 32, 128):
+            if w <= b and b <= self.max_blocks:
+                return b
+        return self.max_blocks
+
+    def _capture(self, Bp: int, W: int):
         d = self.llm.embed.device
         st = {"ids": torch.zeros(Bp, dtype=torch.long, device=d), "pos": torch.zeros(Bp, dtype=torch.int32, device=d),
               "slots": torch.full((Bp,), -1, dtype=torch.long, device=d),
-              "bt": torch.zeros((Bp, self.max_blocks), dtype=torch.int32, device=d),
+              "bt": torch.zeros((Bp, W), dtype=torch.int32, device=d),
               "ctx": torch.ones(Bp, dtype=torch.int32, device=d)}
         ws: dict = {}
 
@@ -201,22 +209,23 @@ class DecodeGraphs:
             self.pool = torch.cuda.graph_pool_handle()
         with torch.cuda.graph(g, pool=self.pool):
             out = run()
-        self.graphs[Bp] = (g, st, out, ws)
+        self.graphs[(Bp, W)] = (g, st, out, ws)
 
     def run(self, ids, pos, slots, bt, ctx) -> torch.Tensor:
         B = len(ids)
         Bp = self._bucket(B)
-        if Bp not in self.graphs:
-            self._capture(Bp)
-        g, st, out, _ = self.graphs[Bp]
-        w = min(bt.shape[1], self.max_blocks)
+        W = self._width(bt.shape[1])
+        if (Bp, W) not in self.graphs:
+            self._capture(Bp, W)
+        g, st, out, _ = self.graphs[(Bp, W)]
+        w = min(bt.shape[1], W)
         ids_p = np.zeros(Bp, np.int64)
         ids_p[:B] = ids
         pos_p = np.zeros(Bp, np.int32)
         pos_p[:B] = pos
         sl_p = np.full(Bp, -1, np.int64)
         sl_p[:B] = slots
-        bt_p = np.zeros((Bp, self.max_blocks), np.int32)
+        bt_p = np.zeros((Bp, W), np.int32)
         bt_p[:B, :w] = bt[:, :w]
         ctx_p = np.ones(Bp, np.int32)
         ctx_p[:B] = ctx

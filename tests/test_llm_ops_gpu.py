@@ -83,3 +83,33 @@ def test_rep_penalty():
     ref = llm.rep_penalty_(lg.clone(), ids, [1.3, 1.1, 0.7])
     got = llm.rep_penalty_(lg.to(DEV), ids, [1.3, 1.1, 0.7]).cpu()
     assert torch.allclose(got, ref)
+
+
+@pytest.mark.parametrize("M", [1, 3, 16, 17, 32])
+@pytest.mark.parametrize("N,K", [(896, 4864), (9728, 896), (4096, 14336), (256, 128)])
+def test_skinny_gemm(M, N, K):
+    g = torch.Generator().manual_seed(M * 7 + N)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
+    b = torch.randn(N, generator=g)
+    r = torch.randn(M, N, generator=g).bfloat16()
+    ref = ops.linear(x, w, b, residual=r)
+    got = ops.linear(x.to(DEV), w.to(DEV), b.to(DEV), residual=r.to(DEV))
+    assert _rel(got, ref) < 1e-2
+    ref32 = ops.linear(x, w, act="silu", out_dtype=torch.float32)
+    got32 = ops.linear(x.to(DEV), w.to(DEV), act="silu", out_dtype=torch.float32)
+    assert got32.dtype == torch.float32 and _rel(got32, ref32) < 1e-2
+    if N % 16 == 0:
+        ref_g = ops.linear(x, w, glu=True)
+        got_g = ops.linear(x.to(DEV), w.to(DEV), glu=True)
+        assert got_g.shape == (M, N // 2) and _rel(got_g, ref_g) < 1e-2
+
+
+@pytest.mark.parametrize("B,N,k", [(1, 151936, 8), (5, 128256, 64), (3, 20000, 16), (2, 1000, 8)])
+def test_row_topk_long_rows(B, N, k):
+    g = torch.Generator().manual_seed(N)
+    s = torch.randn(B, N, generator=g) * 4
+    v, i, lse = ops.row_topk(s, k, scale=0.7, with_lse=True, index_offset=11)
+    vg, ig, lg = ops.row_topk(s.to(DEV), k, scale=0.7, with_lse=True, index_offset=11)
+    assert torch.equal(ig.cpu(), i) and torch.allclose(vg.cpu(), v)
+    assert torch.allclose(lg.cpu(), lse, atol=1e-3)
