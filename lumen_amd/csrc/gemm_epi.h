@@ -107,7 +107,12 @@ __device__ __forceinline__ void epi_store16(float* v, int m, int n, int M, int N
       for (int q = 0; q < 16; ++q) if (n + q < N) v[q] += bf2f(t[q]);
     }
   }
-  if (ep.post_act) apply_act_n<16>(v, ep.post_act);
+  // post-residual activation: ReLU only (ResNet tails).  A second full activation
+  // switch here doubles the epilogue's live state and spills the 256x256 GEMM.
+  if (ep.post_act) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = fmaxf(v[q], 0.f);
+  }
   if (ep.out_f32) {
     float* o = (float*)C + orow * ldc + n;
     if (full) {

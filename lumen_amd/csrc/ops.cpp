@@ -336,6 +336,7 @@ void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Te
     TORCH_CHECK(prelu->scalar_type() == at::kBFloat16 && prelu->numel() == Cout, "conv2d: prelu");
     ep.prelu = bf(*prelu);
   }
+  TORCH_CHECK(post_act == 0 || post_act == 3, "conv2d: post_act supports none / relu");
   ep.post_act = (int)post_act;
   lumen::ConvArgs a{};
   a.x = bf(x); a.w = bf(w); a.out = out.data_ptr(); a.ldx = ldx; a.ldo = ldo;
