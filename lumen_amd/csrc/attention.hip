@@ -74,9 +74,15 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 15, g = lane >> 4;
-  const int b = blockIdx.z, h = blockIdx.y;
+  // XCD-aware tile order: the query blocks of one (batch, head) get consecutive
+  // logical ids on the same XCD, so their K/V reads hit that XCD's L2 instead of
+  // being re-fetched from HBM by up to 8 different dies.
+  const int nqb = gridDim.x;
+  const int lin = xcd_remap(blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z), nqb * gridDim.y * gridDim.z);
+  const int qblk = lin % nqb;
+  const int h = (lin / nqb) % gridDim.y, b = lin / (nqb * gridDim.y);
   const int hk = h / (a.H / a.Hkv);
-  const int q0 = blockIdx.x * 64 + wid * 16;
+  const int q0 = qblk * 64 + wid * 16;
   const int kv_len = a.kv_len ? min(a.kv_len[b], a.Sk) : a.Sk;
   const int causal_off = a.Sk - a.Sq;
 
@@ -123,7 +129,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const int qi = q0 + col;
 
   int kend = kv_len;
-  if (a.causal) kend = min(kend, min(blockIdx.x * 64 + 64, a.Sq) + causal_off);
+  if (a.causal) kend = min(kend, min(qblk * 64 + 64, a.Sq) + causal_off);
   const int nkc = (kend + KC - 1) / KC;
 
   // waves whose 16 queries are all past the end (the ragged last q-block, e.g.
