@@ -417,6 +417,29 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
   tile = tile % 10;
   if (group_m == 0) group_m = 4;
   if (group_m == 1) group_m = 0;
+  // Tail-round split: with one 256x256 workgroup per CU, a tile count just above a
+  // multiple of the 256 CUs (ViT batch 512: M = 512*257 -> 514 row tiles -> 2056
+  // tiles for N = 1024) leaves a nearly empty last round that still costs a full
+  // tile time.  Run the largest row range whose tile count is a multiple of 256 on
+  // the 256x256 kernel and the few remaining rows on 128x128 tiles (4x more, 4x
+  // shorter workgroups) so the tail costs ~1/4 of a round.  Only for plain row maps.
+  if (tile >= 4 && tile <= 6 && ep.out_group == 0 && ep.table == nullptr) {
+    const int tiles_n = (N + 255) / 256;
+    const int tiles_m = (M + 255) / 256;
+    int q = 256;
+    for (int g = tiles_n; g % 2 == 0 && q > 1; g /= 2) q /= 2;      // q = 256 / gcd(256, tiles_n) (power-of-2 part)
+    const int main_m_tiles = tiles_m / q * q;
+    const int tail = tiles_m * tiles_n - main_m_tiles * tiles_n;
+    if (main_m_tiles > 0 && main_m_tiles < tiles_m && tail < 128) {
+      const int M0 = main_m_tiles * 256;
+      hipError_t e = gemm_bf16(A, lda, W, ldw, C, ldc, M0, N, K, ep, tile + 10 * (group_m == 0 ? 1 : group_m), stream);
+      if (e != hipSuccess) return e;
+      GemmEpi e2 = ep;
+      if (e2.residual) e2.residual += (int64_t)M0 * e2.ldr;
+      char* C2 = (char*)C + (int64_t)M0 * ldc * (ep.out_f32 ? 4 : 2);
+      return launch_cfg<128, 128, 2, 2>(A + (int64_t)M0 * lda, lda, W, ldw, C2, ldc, M - M0, N, K, e2, stream);
+    }
+  }
   switch (tile) {
     case 0: return launch_cfg<256, 256, 2, 4>(A, lda, W, ldw, C, ldc, M, N, K, ep, stream);
     case 1: return launch_cfg<128, 128, 2, 2>(A, lda, W, ldw, C, ldc, M, N, K, ep, stream);

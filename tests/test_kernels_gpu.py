@@ -160,3 +160,21 @@ def test_gemm_activations(act):
     ref = ops.linear(x, w, act=act)
     got = ops.linear(x.to(DEV), w.to(DEV), act=act)
     assert _rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [-1, 5])
+def test_gemm_tail_round_split(tile):
+    # 66 row tiles x 4 column tiles: rows [0, 16384) on 256x256, the 300-row tail on 128x128
+    M, N, K = 64 * 256 + 300, 1024, 512
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
+    b = torch.randn(N, generator=g)
+    r = torch.randn(M, N, generator=g).bfloat16()
+    ref = ops.linear(x, w, b, act="gelu", residual=r)
+    got = ops.linear(x.to(DEV), w.to(DEV), b.to(DEV), act="gelu", residual=r.to(DEV), tile=tile)
+    assert _rel(got, ref) < 1e-2
+    assert _rel(got[-300:], ref[-300:]) < 1e-2
+    ref32 = ops.linear(x, w, out_dtype=torch.float32)
+    got32 = ops.linear(x.to(DEV), w.to(DEV), out_dtype=torch.float32, tile=tile)
+    assert _rel(got32[-300:], ref32[-300:]) < 1e-2
