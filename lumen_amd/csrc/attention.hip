@@ -20,6 +20,7 @@
 // key-padded BERT (CN-CLIP), causal GQA decoder prefill (Qwen2 / Llama).
 // Q/K/V are read in place from packed projections via strides, and O is
 // written as [b, s, h, d] so the out-projection GEMM consumes it directly.
+#include <cstdlib>
 #include "common.h"
 
 namespace lumen {
@@ -251,7 +252,191 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+// ----------------------------------------------------------------------------------------------
+// K/V-resident variant for short sequences with many (batch, head) pairs (ViT S = 197 / 257,
+// CLIP text S = 77): one workgroup per (batch, head) DMA-loads the WHOLE K and V (<= 80 KiB,
+// two workgroups per CU) once, then its 4 waves walk 16-query blocks (wave w: blocks w, w+4,
+// ...) over the LDS-resident chunks with no further barriers.  Versus the streaming kernel
+// this reads K/V from HBM once instead of once per 64-query block and removes the per-chunk
+// wait/barrier pairs; the ragged 257th query costs one 16-query block of one wave instead
+// of a whole 64-query workgroup.
+template <int D>
+__global__ void __launch_bounds__(256) attn_res_kernel(AttnArgs a, int nkc) {
+  constexpr int NCH = D / 8;
+  constexpr int KS = D / 32;
+  constexpr int NB = D / 16;
+  constexpr int KC = 64;
+  constexpr int IMG = KC * D * 2;
+  constexpr int RPI = 1024 / (D * 2);
+  constexpr int NI = KC / RPI / 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];   // [nkc][K, V][IMG]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int lin = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+  const int h = lin % a.H, b = lin / a.H;
+  const int hk = h / (a.H / a.Hkv);
+  const int kv_len = a.kv_len ? min(a.kv_len[b], a.Sk) : a.Sk;
+  const int causal_off = a.Sk - a.Sq;
+  const uint16_t* qb = a.q + b * a.q_sb + h * a.q_sh;
+  const uint16_t* kb = a.k + b * a.k_sb + hk * a.k_sh;
+  const uint16_t* vb = a.v + b * a.v_sb + hk * a.v_sh;
+
+  // ---- stage all K/V chunks (clamped rows past Sk keep the images finite)
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  typedef const __attribute__((address_space(1))) void* g_ptr_t;
+  for (int c = 0; c < nkc; ++c) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int r = (wid * NI + i) * RPI + lane / NCH;
+      const int pc = lane % NCH;
+      const int kr = min(c * KC + r, a.Sk - 1);
+      char* dk = smem + c * 2 * IMG + (wid * NI + i) * 1024;
+      __builtin_amdgcn_global_load_lds((g_ptr_t)(kb + (int64_t)kr * a.k_ss + k_phys<D>(r, pc) * 8), (lds_ptr_t)dk, 16,
+                                       0, 0);
+      __builtin_amdgcn_global_load_lds((g_ptr_t)(vb + (int64_t)kr * a.v_ss + v_phys<D>(r, pc) * 8),
+                                       (lds_ptr_t)(dk + IMG), 16, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int nq16 = (a.Sq + 15) / 16;
+  for (int qbk = wid; qbk < nq16; qbk += 4) {
+    const int q0 = qbk * 16;
+    const int qi = q0 + col;
+    bf16x8_t qf[KS];
+    {
+      const int qr = min(qi, a.Sq - 1);
+#pragma unroll
+      for (int t = 0; t < KS; ++t) qf[t] = *(const bf16x8_t*)(qb + (int64_t)qr * a.q_ss + t * 32 + g * 8);
+    }
+    f32x4_t o[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) o[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    float mrow = -INFINITY, lrow = 0.f;
+    const int wave_kend = a.causal ? min(kv_len, min(q0 + 16, a.Sq) + causal_off) : kv_len;
+    const int nc = min(nkc, (wave_kend + KC - 1) / KC);
+    for (int kc = 0; kc < nc; ++kc) {
+      const int k0 = kc * KC;
+      const char* sK = smem + kc * 2 * IMG;
+      const char* sV = sK + IMG;
+      const int nblk = min(4, (wave_kend - k0 + 15) >> 4);
+      f32x4_t sc[4];
+#pragma unroll
+      for (int kb16 = 0; kb16 < 4; ++kb16) {
+        sc[kb16] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        if (kb16 < nblk) {
+          const int kr = kb16 * 16 + col;
+#pragma unroll
+          for (int t = 0; t < KS; ++t) {
+            bf16x8_t kf = *(const bf16x8_t*)(sK + kr * D * 2 + (k_phys<D>(kr, t * 4 + g) << 4));
+            sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[t], sc[kb16], 0, 0, 0);
+          }
+        }
+      }
+      const bool need_mask = (k0 + KC > kv_len) || (a.causal && k0 + KC - 1 > q0 + causal_off);
+      float mx = mrow;
+      if (need_mask) {
+#pragma unroll
+        for (int kb16 = 0; kb16 < 4; ++kb16)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int kj = k0 + kb16 * 16 + g * 4 + r;
+            bool ok = kj < kv_len;
+            if (a.causal) ok = ok && (kj <= qi + causal_off);
+            const float sv = ok ? sc[kb16][r] * a.scale_log2 : -INFINITY;
+            sc[kb16][r] = sv;
+            mx = fmaxf(mx, sv);
+          }
+      } else {
+#pragma unroll
+        for (int kb16 = 0; kb16 < 4; ++kb16)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float sv = sc[kb16][r] * a.scale_log2;
+            sc[kb16][r] = sv;
+            mx = fmaxf(mx, sv);
+          }
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mbase = mx == -INFINITY ? 0.f : mx;
+      const float alpha = exp2f(mrow - mbase);
+      float rs = 0.f;
+#pragma unroll
+      for (int kb16 = 0; kb16 < 4; ++kb16)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(sc[kb16][r] - mbase);
+          sc[kb16][r] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      lrow = lrow * alpha + rs;
+      mrow = mx;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) o[j] *= alpha;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (2 * s >= nblk) break;
+        bf16x8_t pf;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pf[r] = (__bf16)sc[2 * s][r];
+          pf[4 + r] = (__bf16)sc[2 * s + 1][r];
+        }
+        const int q = col >> 2, p = col & 3;
+        const int r0 = s * 32 + 4 * g + q, r1 = r0 + 16;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const int c0 = j * 16 + 4 * p;
+          const char* a0 = sV + r0 * D * 2 + (v_phys<D>(r0, c0 >> 3) << 4) + (c0 & 7) * 2;
+          const char* a1 = sV + r1 * D * 2 + (v_phys<D>(r1, c0 >> 3) << 4) + (c0 & 7) * 2;
+          const s16x4v lo = ds_read_tr16(a0);
+          const s16x4v hi = ds_read_tr16(a1);
+          s16x8_t vv = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, vv), pf, o[j], 0, 0, 0);
+        }
+      }
+    }
+    if (qi < a.Sq) {
+      const float inv = lrow > 0.f ? 1.0f / lrow : 0.f;
+      uint16_t* orow = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qi * a.o_ss;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        uint2 w;
+        w.x = pack2bf(o[j][0] * inv, o[j][1] * inv);
+        w.y = pack2bf(o[j][2] * inv, o[j][3] * inv);
+        *(uint2*)(orow + j * 16 + 4 * g) = w;
+      }
+    }
+  }
+}
+
+template <int D>
+static hipError_t launch_res(const AttnArgs& a, int B, int nkc, hipStream_t stream) {
+  const size_t lds = (size_t)nkc * 2 * 64 * D * 2;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)attn_res_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(attn_res_kernel<D>, dim3(a.H, B), dim3(256), lds, stream, a, nkc);
+  return hipGetLastError();
+}
+
 hipError_t attn_fwd(const AttnArgs& a, int B, int D, hipStream_t stream) {
+  // K/V-resident path when the whole K/V fits in 80 KiB and there are enough (batch, head) pairs
+  const int nkc = (a.Sk + 63) / 64;
+  const bool res_ok = (int64_t)B * a.H >= 1024 && (size_t)nkc * 2 * 64 * D * 2 <= 80 * 1024 && a.Sq <= 1024;
+  if (res_ok && getenv("LUMEN_ATTN_STREAM") == nullptr) {
+    if (D == 64) return launch_res<64>(a, B, nkc, stream);
+    if (D == 128) return launch_res<128>(a, B, nkc, stream);
+    if (D == 32) return launch_res<32>(a, B, nkc, stream);
+  }
   dim3 grid((a.Sq + 63) / 64, a.H, B), block(256);
   if (D == 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, block, 0, stream, a);
   else if (D == 128) hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, block, 0, stream, a);

@@ -404,6 +404,8 @@ static hipError_t launch_glds(const uint16_t* A, int64_t lda, const uint16_t* W,
 hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
                      int64_t ldc, int M, int N, int K, const GemmEpi& ep, int tile,
                      hipStream_t stream) {
+  bool allow_split = true;          // tile codes >= 1000: same config without the tail-round split
+  if (tile >= 1000) { allow_split = false; tile -= 1000; }
   if (tile < 0) {
     const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
     const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
@@ -423,7 +425,7 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
   // tile time.  Run the largest row range whose tile count is a multiple of 256 on
   // the 256x256 kernel and the few remaining rows on 128x128 tiles (4x more, 4x
   // shorter workgroups) so the tail costs ~1/4 of a round.  Only for plain row maps.
-  if (tile >= 4 && tile <= 6 && ep.out_group == 0 && ep.table == nullptr) {
+  if (allow_split && tile >= 4 && tile <= 6 && ep.out_group == 0 && ep.table == nullptr) {
     const int tiles_n = (N + 255) / 256;
     const int tiles_m = (M + 255) / 256;
     int q = 256;

@@ -178,3 +178,18 @@ def test_gemm_tail_round_split(tile):
     ref32 = ops.linear(x, w, out_dtype=torch.float32)
     got32 = ops.linear(x.to(DEV), w.to(DEV), out_dtype=torch.float32, tile=tile)
     assert _rel(got32[-300:], ref32[-300:]) < 1e-2
+
+
+@pytest.mark.parametrize("B,Sq,Sk,H,Hkv,D,causal", [
+    (64, 257, 257, 16, 16, 64, False), (128, 77, 77, 8, 8, 64, True), (40, 100, 100, 32, 8, 128, False),
+    (64, 197, 197, 16, 16, 32, False), (32, 300, 300, 32, 32, 64, True)])
+def test_attention_kv_resident_path(B, Sq, Sk, H, Hkv, D, causal):
+    # B*H >= 1024 and K/V <= 80 KiB -> the K/V-resident kernel
+    g = torch.Generator().manual_seed(Sq + H + D)
+    q = torch.randn(B, Sq, H, D, generator=g).bfloat16()
+    k = torch.randn(B, Sk, Hkv, D, generator=g).bfloat16()
+    v = torch.randn(B, Sk, Hkv, D, generator=g).bfloat16()
+    kl = torch.randint(Sk // 2, Sk + 1, (B,), generator=g, dtype=torch.int32)
+    ref = ops.attention(q, k, v, causal=causal, kv_len=kl)
+    got = ops.attention(q.to(DEV), k.to(DEV), v.to(DEV), causal=causal, kv_len=kl.to(DEV))
+    assert _rel(got, ref) < 2e-2

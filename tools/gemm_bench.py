@@ -20,8 +20,8 @@ for M, N, K in shapes:
     r = {"M": M, "N": N, "K": K}
     variants = [("g1", lambda: ops.linear(x, w, out=out, tile=15)), ("g2", lambda: ops.linear(x, w, out=out, tile=25)),
                 ("g4", lambda: ops.linear(x, w, out=out, tile=45)), ("g8", lambda: ops.linear(x, w, out=out, tile=85)),
-                ("torch", run_t), ("g1b", lambda: ops.linear(x, w, out=out, tile=15)),
-                ("g4b", lambda: ops.linear(x, w, out=out, tile=45)), ("g8b", lambda: ops.linear(x, w, out=out, tile=85)),
+                ("torch", run_t), ("ns4", lambda: ops.linear(x, w, out=out, tile=1045)),
+                ("g4b", lambda: ops.linear(x, w, out=out, tile=45)), ("ns8", lambda: ops.linear(x, w, out=out, tile=1085)),
                 ("g16", lambda: ops.linear(x, w, out=out, tile=165))]
     for name, fn in variants:
         for _ in range(3):
