@@ -158,8 +158,10 @@ class MI355XFaceBackend:
         meta = json.loads(cfgp.read_text())
         dcfg = SCRFDConfig(**{k: tuple(v) if isinstance(v, list) else v for k, v in meta["det"].items()})
         rcfg = IResNetConfig(**{k: tuple(v) if isinstance(v, list) else v for k, v in meta["rec"].items()})
-        ins = (r.extra.get("insightface") or {})
-        d, rc = ins.get("detection", {}), ins.get("recognition", {})
+        from .specs import pack_spec
+
+        spec = pack_spec(r.model_name, r.extra.get("insightface") or {})
+        d, rc = spec["detection"], spec["recognition"]
         self.spec = FaceSpec(det_size=dcfg.input_size, det_mean=float(np.mean(d.get("mean", 127.5))),
                              det_std=float(np.mean(d.get("std", 128.0))), rec_size=rcfg.input_size,
                              rec_mean=float(np.mean(rc.get("mean", 127.5))), rec_std=float(np.mean(rc.get("std", 127.5))),
