@@ -28,6 +28,7 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from lumen_amd.models.clip import CLIPModel, PRESETS  # noqa: E402
+from lumen_amd.parallel import Communicator, destroy, init_distributed  # noqa: E402
 
 METRIC = "CLIP ViT-L/14 images/sec (whole node)"
 
@@ -43,13 +44,10 @@ def main():
     ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    st = init_distributed(tp_size=1, device=torch.device("cuda", local))   # one process per GPU, RCCL
+    world, rank, dev = st.world, st.rank, st.device
+    comm = Communicator(st.dp_group, dev, ipc=False)                      # DP result gather over RCCL
 
     cfg = PRESETS[args.model]
     model = CLIPModel.random(cfg, seed=0, device=dev, with_text=False)
@@ -83,10 +81,7 @@ def main():
         comp.wait_event(copied[i % 2])
         emb = model.encode_image_uint8(dimg[i % 2])
         consumed[i % 2].record(comp)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, emb)
-        else:
-            gathered.copy_(emb)
+        comm.all_gather_into(gathered, emb)
         return emb
 
     for _ in range(args.warmup):
@@ -143,8 +138,7 @@ def main():
             "finite": ok,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    destroy()
 
 
 if __name__ == "__main__":

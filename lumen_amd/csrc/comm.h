@@ -1,0 +1,29 @@
+// IPC one-shot all-reduce (comm.hip) shared with its torch bindings (ops_comm.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace lumen {
+
+constexpr int AR_MAX_RANKS = 8;
+constexpr int AR_MAX_BLOCKS = 64;
+constexpr int64_t AR_CTL_BYTES = 16384;
+constexpr int AR_SPIN_LIMIT = 2000000;   // ~1-4 s of polling before a peer is declared missing
+
+// control block at the start of every rank's buffer
+struct ArCtl {
+  uint32_t flag[2][AR_MAX_BLOCKS][AR_MAX_RANKS];   // flag[parity][block][src rank], written by the peers
+  uint32_t epoch[AR_MAX_BLOCKS];                    // this rank's per-block call counter
+  uint32_t err;                                     // set when a peer never arrived
+};
+static_assert(sizeof(ArCtl) <= AR_CTL_BYTES, "control block too large");
+
+// base[r] = rank r's uncached IPC buffer as mapped in THIS process (base[rank] = own buffer)
+struct ArPeers {
+  char* base[AR_MAX_RANKS];
+};
+
+hipError_t custom_all_reduce(const void* in, void* out, const ArPeers& peers, int rank, int world, int64_t bytes,
+                             int is_bf16, int64_t cap_bytes, hipStream_t stream);
+
+}  // namespace lumen

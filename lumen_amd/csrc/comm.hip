@@ -1,0 +1,130 @@
+// One-shot IPC all-reduce over xGMI for latency-bound tensor-parallel messages
+// (SURVEY §5.8 COMM-2; the reference has no collectives at all).
+//
+// Every rank owns ONE uncached device allocation (hipExtMallocWithFlags
+// hipDeviceMallocUncached) that all peers map through hipIpc handles:
+//
+//   [ control (16 KiB): flag[2][64 blocks][8 ranks] u32 | epoch[64 blocks] u32 | err u32 ]
+//   [ data parity 0 (cap bytes) ][ data parity 1 (cap bytes) ]
+//
+// Call e (per block b, e = epoch[b] + 1, parity p = e & 1):
+//   1. block b copies its slice of the input into its OWN data[p];
+//   2. system-scope release: flag[p][b][rank] = e stored into EVERY peer's control
+//      block (each xGMI link carries one 4-byte write);
+//   3. waits until all peers' flag[p][b][*] >= e in its own (local) control block;
+//   4. reads the same slice of every peer's data[p] (7 links in parallel), sums in
+//      fp32 in fixed rank order (bitwise identical on every rank), writes `out`.
+// Double-buffering by parity makes an end barrier unnecessary: rank r can only
+// rewrite data[p] at call e+2 after every peer passed call e+1's barrier, i.e.
+// finished reading call e.  The epoch lives in device memory (each block bumps
+// its own counter), so the kernel takes no per-call arguments and a captured
+// hipGraph replays it correctly.  Every spin has a bounded budget: a missing
+// peer sets `err` and the kernel drains instead of hanging the GPU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "comm.h"
+
+namespace lumen {
+
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void add_vec(float* acc, const u32x4v v, int is_bf16) {
+  if (is_bf16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[2 * i] += __uint_as_float(v[i] << 16);
+      acc[2 * i + 1] += __uint_as_float(v[i] & 0xffff0000u);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] += __uint_as_float(v[i]);
+  }
+}
+
+__device__ __forceinline__ uint32_t rne_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// BF16 = 1: bf16 elements (8 per 16-byte vector); 0: fp32 (4 per vector).
+template <int BF16>
+__global__ void __launch_bounds__(512) custom_ar_kernel(const u32x4v* __restrict__ in, u32x4v* __restrict__ out,
+                                                        ArPeers peers, int rank, int world, int64_t nvec,
+                                                        int64_t vec_per_block, int64_t cap_bytes) {
+  const int b = blockIdx.x;
+  char* mine = peers.base[rank];
+  ArCtl* ctl = reinterpret_cast<ArCtl*>(mine);
+  __shared__ uint32_t s_epoch;
+  if (threadIdx.x == 0) s_epoch = __hip_atomic_load(&ctl->epoch[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  const uint32_t e = s_epoch;
+  const int p = (int)(e & 1u);
+  const int64_t lo = (int64_t)b * vec_per_block;
+  const int64_t hi = lo + vec_per_block < nvec ? lo + vec_per_block : nvec;
+
+  // 1. stage my slice into my own data[p]
+  u32x4v* my_data = reinterpret_cast<u32x4v*>(mine + AR_CTL_BYTES + (int64_t)p * cap_bytes);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) my_data[i] = in[i];
+  __threadfence_system();
+  __syncthreads();
+
+  // 2. signal every peer (including myself), 3. wait for every peer
+  if (threadIdx.x < (unsigned)world) {
+    ArCtl* pc = reinterpret_cast<ArCtl*>(peers.base[threadIdx.x]);
+    __hip_atomic_store(&pc->flag[p][b][rank], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* f = &ctl->flag[p][b][threadIdx.x];
+    int spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > AR_SPIN_LIMIT) {
+        __hip_atomic_store(&ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+
+  // 4. reduce the slice over all ranks in rank order
+  const int64_t off = AR_CTL_BYTES + (int64_t)p * cap_bytes;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < world; ++r) {
+      const u32x4v v = reinterpret_cast<const u32x4v*>(peers.base[r] + off)[i];
+      add_vec(acc, v, BF16);
+    }
+    u32x4v o;
+    if (BF16) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = rne_bf16(acc[2 * k]) | (rne_bf16(acc[2 * k + 1]) << 16);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = __float_as_uint(acc[k]);
+    }
+    out[i] = o;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&ctl->epoch[b], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+hipError_t custom_all_reduce(const void* in, void* out, const ArPeers& peers, int rank, int world, int64_t bytes,
+                             int is_bf16, int64_t cap_bytes, hipStream_t stream) {
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world) return hipErrorInvalidValue;
+  if (bytes % 16 != 0 || bytes > cap_bytes) return hipErrorInvalidValue;
+  const int64_t nvec = bytes / 16;
+  if (nvec == 0) return hipSuccess;
+  int64_t blocks = (nvec + 511) / 512;
+  if (blocks > AR_MAX_BLOCKS) blocks = AR_MAX_BLOCKS;
+  const int64_t per = (nvec + blocks - 1) / blocks;
+  blocks = (nvec + per - 1) / per;
+  if (is_bf16)
+    hipLaunchKernelGGL(custom_ar_kernel<1>, dim3((unsigned)blocks), dim3(512), 0, stream, (const u32x4v*)in,
+                       (u32x4v*)out, peers, rank, world, nvec, per, cap_bytes);
+  else
+    hipLaunchKernelGGL(custom_ar_kernel<0>, dim3((unsigned)blocks), dim3(512), 0, stream, (const u32x4v*)in,
+                       (u32x4v*)out, peers, rank, world, nvec, per, cap_bytes);
+  return hipGetLastError();
+}
+
+}  // namespace lumen

@@ -135,6 +135,7 @@ class LLM(nn.Module):
         self.register_buffer("cos_sin", lops.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta,
                                                           cfg.rope_scaling).to(device), persistent=False)
         self.H, self.Hkv = self.layers[0].H, self.layers[0].Hkv
+        self.comm = None   # parallel.Communicator for the TP group (IPC one-shot all-reduce + RCCL); None = RCCL
 
     # ------------------------------------------------------------------ weights
     @torch.no_grad()
@@ -203,6 +204,8 @@ class LLM(nn.Module):
     # ------------------------------------------------------------------ collectives
     def _all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp.enabled:
+            if self.comm is not None:
+                return self.comm.all_reduce(t)
             import torch.distributed as dist
 
             dist.all_reduce(t, group=self.tp.group)

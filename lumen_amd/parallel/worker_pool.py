@@ -1,0 +1,307 @@
+"""Multi-process GPU worker pool: image-batch data parallelism for serving.
+
+The reference runs every model in the gRPC server process, batch 1, on one
+device (SURVEY §2.5 DP row).  Here a service with ``LUMEN_DP_SIZE = N`` owns N
+worker processes, one per GPU (each its own HIP context, caching allocator and
+stream — no GIL or allocator contention between GPUs).  The service's dynamic
+batcher hands a merged batch to :meth:`GPUWorkerPool.run`, which splits it into
+contiguous shards, one per live worker, and concatenates the shard results in
+order.  Inputs travel as pickled bytes/arrays over pipes — they are compressed
+images (tens of KB) or token ids, tiny next to the per-GPU compute.
+
+Failure detection: every worker sends a heartbeat each
+``heartbeat_s``; the monitor thread declares a worker lost when its process exits
+or its heartbeat is older than ``dead_after_s``, fails that worker's in-flight
+shards with :class:`WorkerLostError` (the services map it to
+``ERROR_CODE_UNAVAILABLE``) and respawns it.  ``LUMEN_FAULT_KILL_WORKER=w:n``
+makes worker w exit hard after n tasks (fault-injection tests).
+
+Workers are started with the ``spawn`` context (a fresh interpreter started as a
+child process, never an exec of a GPU-initialised process) and pinned to their
+device before the factory builds the model.
+"""
+from __future__ import annotations
+
+import importlib
+import itertools
+import logging
+import multiprocessing as mp
+import os
+import queue
+import threading
+import time
+import traceback
+from concurrent.futures import Future
+from dataclasses import dataclass, field
+from typing import Any, Callable, Optional, Sequence
+
+log = logging.getLogger("lumen.workers")
+
+
+class WorkerLostError(RuntimeError):
+    """A worker process died (or stopped heart-beating) with work in flight."""
+
+
+class WorkerTaskError(RuntimeError):
+    """The worker's batch function raised; carries the remote traceback."""
+
+
+def _resolve(path: str) -> Callable:
+    mod, _, attr = path.partition(":")
+    return getattr(importlib.import_module(mod), attr)
+
+
+def _fault_plan(wid: int) -> Optional[int]:
+    spec = os.environ.get("LUMEN_FAULT_KILL_WORKER", "")
+    if not spec:
+        return None
+    w, _, n = spec.partition(":")
+    return int(n or 0) if int(w) == wid else None
+
+
+def _worker_main(wid: int, device: str, factory: str, kwargs: dict, inq, outq, heartbeat_s: float) -> None:
+    """Child process body: pin device, build the batch fn, serve tasks until None."""
+    try:
+        if device.startswith("cuda"):
+            import torch
+
+            torch.cuda.set_device(torch.device(device))
+        fn = _resolve(factory)(device, **kwargs)
+    except BaseException:  # noqa: BLE001
+        outq.put(("fatal", wid, None, traceback.format_exc()))
+        return
+    outq.put(("ready", wid, None, os.getpid()))
+    kill_after = _fault_plan(wid)
+    done = 0
+    alive = threading.Event()
+
+    def beat():   # heart-beats keep flowing while a long batch runs
+        while not alive.wait(heartbeat_s):
+            outq.put(("hb", wid, None, time.time()))
+
+    threading.Thread(target=beat, name="lumen-worker-hb", daemon=True).start()
+    while True:
+        msg = inq.get()
+        if msg is None:
+            alive.set()
+            break
+        tid, kind, items = msg
+        if kill_after is not None and done >= kill_after:
+            os._exit(17)
+        try:
+            res = fn(kind, items)
+            outq.put(("ok", wid, tid, res))
+        except BaseException:  # noqa: BLE001
+            outq.put(("err", wid, tid, traceback.format_exc()))
+        done += 1
+
+
+@dataclass
+class _Worker:
+    wid: int
+    device: str
+    proc: Any = None
+    inq: Any = None
+    ready: bool = False
+    pid: int = 0
+    last_hb: float = 0.0
+    inflight: dict = field(default_factory=dict)   # tid -> (Future, submit time)
+    restarts: int = 0
+
+
+class GPUWorkerPool:
+    """N worker processes, one per device, running ``factory(device, **kwargs)``'s
+    batch function ``fn(kind, items) -> list``."""
+
+    def __init__(self, factory: str, devices: Sequence[str], kwargs: Optional[dict] = None, heartbeat_s: float = 1.0,
+                 dead_after_s: float = 30.0, respawn: bool = True, start_timeout_s: float = 600.0,
+                 task_timeout_s: Optional[float] = None):
+        self.factory = factory
+        self.kwargs = dict(kwargs or {})
+        self.heartbeat_s = heartbeat_s
+        self.dead_after_s = dead_after_s
+        self.respawn = respawn
+        self.task_timeout_s = task_timeout_s   # a batch running longer => the worker is hung: kill + respawn
+        self._ctx = mp.get_context("spawn")
+        self._outq = self._ctx.Queue()
+        self._lock = threading.Lock()
+        self._tid = itertools.count(1)
+        self._stop = threading.Event()
+        self.workers = [_Worker(wid=i, device=d) for i, d in enumerate(devices)]
+        self.stats = {"tasks": 0, "items": 0, "lost": 0, "restarts": 0}
+        self._fatal: Optional[str] = None
+        for w in self.workers:
+            self._start(w)
+        self._collector = threading.Thread(target=self._collect, name="lumen-pool-collect", daemon=True)
+        self._collector.start()
+        self._monitor = threading.Thread(target=self._watch, name="lumen-pool-monitor", daemon=True)
+        self._monitor.start()
+        self.wait_ready(start_timeout_s)
+
+    # ------------------------------------------------------------------ lifecycle
+    def _start(self, w: _Worker) -> None:
+        w.inq = self._ctx.Queue()
+        w.ready = False
+        w.last_hb = time.time()
+        w.proc = self._ctx.Process(target=_worker_main, name=f"lumen-worker-{w.wid}",
+                                   args=(w.wid, w.device, self.factory, self.kwargs, w.inq, self._outq,
+                                         self.heartbeat_s), daemon=True)
+        w.proc.start()
+
+    def wait_ready(self, timeout: float) -> None:
+        t0 = time.time()
+        while time.time() - t0 < timeout:
+            if self._fatal:
+                self.close()
+                raise RuntimeError(f"worker failed to start:\n{self._fatal}")
+            if all(w.ready for w in self.workers):
+                return
+            time.sleep(0.05)
+        raise TimeoutError("GPU workers did not become ready")
+
+    def close(self) -> None:
+        if self._stop.is_set():
+            return
+        self._stop.set()
+        for w in self.workers:
+            try:
+                w.inq.put(None)
+            except Exception:  # noqa: BLE001
+                pass
+        self._monitor.join(timeout=5)
+        for w in self.workers:
+            proc = w.proc
+            if proc is not None:
+                proc.join(timeout=10)
+                if proc.is_alive():
+                    proc.kill()
+                    proc.join(timeout=5)
+        with self._lock:
+            for w in self.workers:
+                for fut, _ in w.inflight.values():
+                    if not fut.done():
+                        fut.set_exception(WorkerLostError("pool closed"))
+                w.inflight.clear()
+
+    @property
+    def size(self) -> int:
+        return len(self.workers)
+
+    def live(self) -> list[_Worker]:
+        return [w for w in self.workers if w.ready and w.proc is not None and w.proc.is_alive()]
+
+    # ------------------------------------------------------------------ submit
+    def submit(self, kind: str, items: list, worker: Optional[int] = None) -> Future:
+        """One task on one worker (least in-flight unless ``worker`` is given)."""
+        fut: Future = Future()
+        with self._lock:
+            cands = self.live()
+            if not cands:
+                fut.set_exception(WorkerLostError("no live GPU worker"))
+                return fut
+            w = self.workers[worker] if worker is not None else min(cands, key=lambda x: len(x.inflight))
+            tid = next(self._tid)
+            w.inflight[tid] = (fut, time.time())
+            w.inq.put((tid, kind, items))
+            self.stats["tasks"] += 1
+            self.stats["items"] += len(items)
+        return fut
+
+    def run(self, kind: str, items: Sequence, timeout: Optional[float] = None) -> list:
+        """Split ``items`` into one contiguous shard per live worker; ordered results."""
+        items = list(items)
+        if not items:
+            return []
+        n = max(1, min(len(self.live()) or 1, len(items)))
+        per = -(-len(items) // n)
+        futs = [self.submit(kind, items[i:i + per]) for i in range(0, len(items), per)]
+        out: list = []
+        for f in futs:
+            out.extend(f.result(timeout))
+        return out
+
+    # ------------------------------------------------------------------ background threads
+    def _collect(self) -> None:
+        while not self._stop.is_set():
+            try:
+                kind, wid, tid, payload = self._outq.get(timeout=0.2)
+            except queue.Empty:
+                continue
+            except (EOFError, OSError):
+                break
+            w = self.workers[wid]
+            with self._lock:
+                w.last_hb = time.time()
+                if kind == "ready":
+                    w.ready, w.pid = True, int(payload)
+                elif kind == "fatal":
+                    self._fatal = str(payload)
+                elif kind in ("ok", "err"):
+                    fut, _ = w.inflight.pop(tid, (None, 0.0))
+                    if fut is not None and not fut.done():
+                        if kind == "ok":
+                            fut.set_result(payload)
+                        else:
+                            fut.set_exception(WorkerTaskError(str(payload)))
+
+    def _watch(self) -> None:
+        while not self._stop.wait(self.heartbeat_s / 2):
+            now = time.time()
+            for w in self.workers:
+                if w.proc is None or self._stop.is_set():
+                    continue
+                dead = not w.proc.is_alive()
+                stale = w.ready and now - w.last_hb > self.dead_after_s
+                if self.task_timeout_s is not None and w.ready:
+                    with self._lock:
+                        oldest = min((t for _, t in w.inflight.values()), default=now)
+                    stale = stale or now - oldest > self.task_timeout_s
+                if not (dead or stale):
+                    continue
+                with self._lock:
+                    lost = [f for f, _ in w.inflight.values()]
+                    w.inflight.clear()
+                    w.ready = False
+                    self.stats["lost"] += 1
+                for fut in lost:
+                    if not fut.done():
+                        fut.set_exception(WorkerLostError(f"GPU worker {w.wid} ({w.device}) lost"))
+                log.error("GPU worker %d on %s lost (%s)", w.wid, w.device, "exited" if dead else "no heartbeat")
+                if stale and w.proc.is_alive():
+                    w.proc.kill()
+                w.proc.join(timeout=5)
+                if self.respawn and not self._stop.is_set():
+                    w.restarts += 1
+                    self.stats["restarts"] += 1
+                    self._start(w)
+                else:
+                    w.proc = None
+
+
+def default_devices(n: int) -> list[str]:
+    """n device strings: cuda:0..n-1 when GPUs are present, else n CPU workers."""
+    try:
+        import torch
+
+        cnt = torch.cuda.device_count()
+    except Exception:  # noqa: BLE001
+        cnt = 0
+    if cnt:
+        return [f"cuda:{i % cnt}" for i in range(n)]
+    return ["cpu"] * n
+
+
+# ---------------------------------------------------------------------- test/bench factories
+def echo_factory(device: str, scale: float = 1.0):
+    """Worker that returns scale * sum(item) per item (pool plumbing tests)."""
+    import numpy as np
+
+    def fn(kind, items):
+        if kind == "fail":
+            raise ValueError("requested failure")
+        if kind == "sleep":
+            time.sleep(float(items[0]))
+            return [0.0]
+        return [float(np.sum(x)) * scale for x in items]
+
+    return fn

@@ -329,13 +329,21 @@ class LLMEngine:
 
     @torch.no_grad()
     def _prefill(self, r: GenRequest) -> None:
-        x = self.build(r.prefill_args)
-        T = x.shape[0]
-        r.prompt_len = T
-        slots = self.kv.slots(r.rid, 0, T)
         spec = Sampler.spec([r])
         if self.sync is not None:
+            # followers must enter the prefill (its vocab-parallel embedding all-reduce)
+            # together with us: announce it before building the inputs
+            T = r.prompt_len
+            slots = self.kv.slots(r.rid, 0, T)
             self.sync.send(("prefill", r.prefill_args, slots, spec))
+            x = self.build(r.prefill_args)
+            if x.shape[0] != T:
+                raise RuntimeError(f"prefill built {x.shape[0]} rows for a {T}-token prompt")
+        else:
+            x = self.build(r.prefill_args)
+            T = x.shape[0]
+            r.prompt_len = T
+            slots = self.kv.slots(r.rid, 0, T)
         logits = self.llm.prefill(x, self.kv, torch.from_numpy(slots).to(self.device))
         r.ctx = T
         tok = self.sampler.pick(self.sampler.candidates(logits, spec), [r])[0]

@@ -9,7 +9,10 @@ MI355X specifics: image decode on CPU threads, then ONE fused
 resize+normalise+patchify HIP kernel for the whole batch, the bf16 tower on
 MFMA kernels and the L2-normalise epilogue on device; concurrent requests from
 all gRPC streams are merged by a :class:`~lumen_amd.runtime.batcher.DynamicBatcher`
-that owns the device.  The same backend serves runtime ``torch`` and ``onnx``
+that owns the device.  With ``LUMEN_DP_SIZE = N > 1`` the batcher feeds a
+:class:`~lumen_amd.parallel.worker_pool.GPUWorkerPool` instead: N worker
+processes, one per GPU, each holding a replica of the towers, every merged
+batch split into N contiguous shards (image-batch data parallelism).  The same backend serves runtime ``torch`` and ``onnx``
 configs (one native execution path, no multi-backend dispatch); ``device: cpu``
 selects the fp32 PyTorch reference path (BASELINE config #1).
 """
@@ -70,8 +73,10 @@ def pick_device(pref: Optional[str]) -> torch.device:
 
 class MI355XClipBackend:
     def __init__(self, resources: ModelResources, device: Optional[str] = None, batch_size: int = 8,
-                 max_batch: int = 256, max_wait_ms: float = 2.0, precision: Optional[str] = None):
+                 max_batch: int = 256, max_wait_ms: float = 2.0, precision: Optional[str] = None, dp_size: int = 1):
         self.resources = resources
+        self.dp_size = max(1, int(dp_size))
+        self._pool = None
         self.device_pref = device
         self.batch_size = batch_size
         self.max_batch = max_batch
@@ -97,20 +102,37 @@ class MI355XClipBackend:
         cfg.image_mean, cfg.image_std = tuple(mean), tuple(std)
         self.cfg = cfg
         self.context_length = cfg.text.context_length
-        m = CLIPModel(cfg, dtype=dtype, device="cpu")
-        m.load_state_dict_any(load_weights(self.resources.model_root_path))
-        self.model = m.to(self.device)
+        if self.dp_size > 1:
+            from ...parallel.worker_pool import GPUWorkerPool, default_devices
+
+            r = self.resources
+            devs = ["cpu"] * self.dp_size if self.device.type == "cpu" else default_devices(self.dp_size)
+            self._pool = GPUWorkerPool("lumen_amd.services.clip.backend:dp_worker", devs,
+                                       kwargs={"cache_dir": str(r.model_root_path.parent.parent),
+                                               "model": r.model_name, "runtime": r.runtime,
+                                               "dataset": r.dataset})
+            sd = load_weights(r.model_root_path)
+            self._logit_scale = float(sd["logit_scale"]) if "logit_scale" in sd else cfg.logit_scale
+        else:
+            m = CLIPModel(cfg, dtype=dtype, device="cpu")
+            m.load_state_dict_any(load_weights(self.resources.model_root_path))
+            self.model = m.to(self.device)
+            self._logit_scale = self.model.logit_scale
         self._load_tokenizer()
         self._img_batcher = DynamicBatcher(self._encode_images, self.max_batch, self.max_wait_ms, "clip-image")
         self._txt_batcher = DynamicBatcher(self._encode_texts, self.max_batch, self.max_wait_ms, "clip-text")
         self.load_time = time.time() - t0
         self.is_initialized = True
-        log.info("CLIP %s ready on %s in %.2fs", self.resources.model_name, self.device, self.load_time)
+        log.info("CLIP %s ready on %s in %.2fs (dp %d)", self.resources.model_name, self.device, self.load_time,
+                 self.dp_size)
 
     def close(self) -> None:
         for b in (self._img_batcher, self._txt_batcher):
             if b is not None:
                 b.close()
+        if self._pool is not None:
+            self._pool.close()
+            self._pool = None
 
     def _load_tokenizer(self) -> None:
         p = self.resources.tokenizer_path
@@ -134,12 +156,16 @@ class MI355XClipBackend:
         return torch.from_numpy(ids)
 
     def _encode_texts(self, texts: Sequence[str]) -> list:
+        if self._pool is not None:
+            return self._pool.run("text", list(self.tokenize(texts).numpy()))
         with torch.no_grad():
             ids = self.tokenize(texts).to(self.device)
             emb = self.model.encode_text_ids(ids).float().cpu().numpy()
         return list(emb)
 
     def _encode_images(self, payloads: Sequence[bytes]) -> list:
+        if self._pool is not None:
+            return self._pool.run("image", list(payloads))
         imgs = decode_many(payloads)
         with torch.no_grad():
             tens = [torch.from_numpy(i) for i in imgs]
@@ -172,7 +198,7 @@ class MI355XClipBackend:
         return np.stack(out).astype(np.float32) if out else np.zeros((0, self.cfg.embed_dim), np.float32)
 
     def get_temperature(self) -> float:
-        return float(np.exp(self.model.logit_scale)) if self.model is not None else 100.0
+        return float(np.exp(self._logit_scale)) if self.is_initialized else 100.0
 
     def get_info(self) -> BackendInfo:
         r = self.resources
@@ -185,6 +211,37 @@ class MI355XClipBackend:
                            else ("fp32",),
                            extra_metadata={"image_size": str(r.get_image_size()),
                                            "context_length": str(self.context_length)})
+
+
+def dp_worker(device: str, cache_dir: str, model: str, runtime: str, dataset: Optional[str] = None):
+    """GPUWorkerPool factory: one CLIP replica on ``device``; fn(kind, items) -> embeddings.
+
+    kind "image": encoded image bytes (decoded on this worker's CPU threads);
+    kind "text": token-id arrays [ctx]."""
+    from ...resources.config import ModelConfig, Runtime
+    from .resources import ResourceLoader
+
+    res = ResourceLoader.load_model_resources(cache_dir, ModelConfig(model=model, runtime=Runtime(runtime),
+                                                                     dataset=dataset))
+    dev = torch.device(device)
+    cfg = res.clip_config()
+    mean, std = res.get_normalization_stats()
+    cfg.image_mean, cfg.image_std = tuple(mean), tuple(std)
+    m = CLIPModel(cfg, dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32, device="cpu")
+    m.load_state_dict_any(load_weights(res.model_root_path))
+    m = m.to(dev)
+
+    @torch.no_grad()
+    def fn(kind, items):
+        if kind == "image":
+            emb = m.encode_image_uint8([torch.from_numpy(i) for i in decode_many(items)])
+        elif kind == "text":
+            emb = m.encode_text_ids(torch.from_numpy(np.stack(items)).to(dev))
+        else:
+            raise ValueError(f"unknown CLIP task kind {kind!r}")
+        return list(emb.float().cpu().numpy())
+
+    return fn
 
 
 def create_backend(backend_settings, resources: ModelResources, runtime: Optional[str] = None,
@@ -201,4 +258,4 @@ def create_backend(backend_settings, resources: ModelResources, runtime: Optiona
     dev = getattr(backend_settings, "device", None) if backend_settings is not None else None
     bs = getattr(backend_settings, "batch_size", 8) if backend_settings is not None else 8
     return MI355XClipBackend(resources, device=dev, batch_size=bs or 8, max_batch=amd.max_batch,
-                             max_wait_ms=amd.max_wait_ms, precision=precision)
+                             max_wait_ms=amd.max_wait_ms, precision=precision, dp_size=amd.dp_size)

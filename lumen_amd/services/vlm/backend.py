@@ -202,8 +202,10 @@ class MI355XVLMBackend:
 
     def __init__(self, resources: GenericResources, device: Optional[str] = None,
                  max_new_tokens: Optional[int] = None, tp: Optional[TPInfo] = None, kv_blocks: int = 0,
-                 max_batch: int = 64):
+                 max_batch: int = 64, tp_size: int = 1):
         self.resources = resources
+        self.tp_size = max(1, int(tp_size))   # leader: spawn a TP group of this size at initialize()
+        self._tp_group = None
         self._device_preference = device
         self._max_new_tokens = max_new_tokens
         self.tp = tp or TPInfo()
@@ -249,11 +251,14 @@ class MI355XVLMBackend:
         raise ResourceNotFoundError(f"{r.model_name}: lumen_vlm_config.json missing (MI355X VLM weights are loaded "
                                     "from model.safetensors; ONNX graph import is not available in this build)")
 
-    def initialize(self) -> None:
-        if self._initialized:
-            return
-        t0 = time.time()
-        self.device = pick_device(self._device_preference)
+    def _tp_spec(self) -> dict:
+        r = self.resources
+        return {"cache_dir": str(r.model_root_path.parent.parent), "model": r.model_name, "runtime": r.runtime,
+                "precision": r.precision, "kv_blocks": self.kv_blocks, "max_batch": self.max_batch}
+
+    def _build(self) -> None:
+        """Model (this rank's TP shard), tokenizer, paged KV cache, TP communicator."""
+        self.device = pick_device(self._device_preference) if self._tp_group is None else self._tp_group.state.device
         dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
         cfg = self._vlm_config()
         self.cfg = cfg
@@ -266,19 +271,55 @@ class MI355XVLMBackend:
         else:
             raise ResourceNotFoundError(f"{self.resources.model_name}: model.safetensors missing")
         self.model = m.eval()
+        if self.tp.enabled:
+            from ...parallel.comm import Communicator
+
+            self.model.llm.comm = Communicator(self.tp.group, self.device)
         self.tokenizer()
         lc = cfg.llm
         self.kv = PagedKVCache(lc.num_layers, self.model.llm.Hkv, lc.head_dim, num_blocks=self.kv_blocks or None,
                                device=self.device, dtype=dtype)
-        self.engine = LLMEngine(self.model.llm, self.kv, self._build_prefill, max_batch=self.max_batch)
+
+    def initialize(self) -> None:
+        if self._initialized:
+            return
+        t0 = time.time()
+        sync = None
+        if self.tp_size > 1 and not self.tp.enabled:
+            from ...parallel.tp import TPServingGroup
+
+            devs = None
+            if self._device_preference and str(self._device_preference).startswith("cpu"):
+                devs = ["cpu"] * self.tp_size
+            self._tp_group = TPServingGroup(self.tp_size, self._tp_spec(), devices=devs)
+            self.tp = self._tp_group.state.tp_info()
+        if self.tp.enabled:
+            from ...runtime.engine import TPSync
+
+            sync = TPSync(self.tp.group, src=0)
+        self._build()
+        self.engine = LLMEngine(self.model.llm, self.kv, self._build_prefill, max_batch=self.max_batch, tp_sync=sync)
         self.load_time = time.time() - t0
         self._initialized = True
-        log.info("VLM %s ready on %s in %.2fs (KV cache %d tokens, %.1f GB)", self.resources.model_name, self.device,
-                 self.load_time, self.kv.capacity_tokens, self.kv.bytes / 1e9)
+        log.info("VLM %s ready on %s in %.2fs (TP %d, KV cache %d tokens, %.1f GB)", self.resources.model_name,
+                 self.device, self.load_time, self.tp.world, self.kv.capacity_tokens, self.kv.bytes / 1e9)
+
+    def run_follower(self) -> None:
+        """TP ranks > 0: build this rank's shard and replay the leader's steps until it stops."""
+        from ...runtime.engine import TPSync, follower_loop
+
+        self._build()
+        self._initialized = True
+        follower_loop(self.model.llm, self.kv, self._build_prefill, TPSync(self.tp.group, src=0))
+        self._initialized = False
 
     def close(self) -> None:
         if self.engine is not None:
             self.engine.close()
+            self.engine = None
+        if self._tp_group is not None:
+            self._tp_group.close()
+            self._tp_group = None
         self._initialized = False
 
     # ------------------------------------------------------------------ prompt / tokens
@@ -368,6 +409,8 @@ class MI355XVLMBackend:
 
     def _submit(self, req: GenerationRequest):
         self.ensure_initialized()
+        if self._tp_group is not None and self._tp_group.failed:
+            raise BackendError(f"tensor-parallel group unavailable: {self._tp_group.failed}")
         prompt = self.build_prompt(self._with_image_token(req.messages), req.add_generation_prompt)
         ids = self.tokenize(prompt)
         try:
@@ -453,4 +496,4 @@ def create_backend(settings, resources: GenericResources, runtime: Optional[str]
     amd = AmdRuntimeSettings.from_env()
     dev = getattr(settings, "device", None) if settings is not None else None
     return MI355XVLMBackend(resources, device=dev, max_new_tokens=DEFAULT_MAX_NEW_TOKENS, kv_blocks=amd.kv_blocks,
-                            max_batch=min(amd.max_batch, 64))
+                            max_batch=min(amd.max_batch, 64), tp_size=amd.tp_size)

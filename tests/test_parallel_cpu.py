@@ -1,0 +1,220 @@
+"""Parallel runtime on CPU: gloo process groups (world 2 and 4, TP x DP layout),
+Communicator collectives, bucketed all-gather, SPMD data-parallel runner, and the
+multi-process worker pool incl. failure detection / respawn (fault injection)."""
+import multiprocessing as mp
+import os
+import socket
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from lumen_amd.parallel import (BucketedAllGather, Communicator, DataParallelRunner, GPUWorkerPool, WorkerLostError,
+                                WorkerTaskError, shard_range)
+from lumen_amd.parallel.comm import ring_all_reduce_time_model
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_range_covers_everything():
+    for n in (0, 1, 7, 512, 1001):
+        for w in (1, 2, 3, 8):
+            spans = [shard_range(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_cost_model_prefers_one_shot_for_small_messages():
+    small = ring_all_reduce_time_model(8 * 1024, 8)
+    assert small["one_shot_us"] < small["ring_us"] / 5
+
+
+def _dist_worker(rank, world, tp, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from lumen_amd.parallel import destroy, init_distributed
+
+    st = init_distributed(tp_size=tp, device=torch.device("cpu"), timeout_s=60)
+    try:
+        res = {"rank": rank, "tp_rank": st.tp_rank, "dp_rank": st.dp_rank, "tp_ranks": st.tp_ranks,
+               "dp_ranks": st.dp_ranks}
+        # TP all-reduce sums inside the TP group only
+        tpc = Communicator(st.tp_group if tp > 1 else None, ipc=False)
+        x = torch.full((4,), float(rank + 1))
+        tpc.all_reduce(x) if tp > 1 else None
+        res["tp_sum"] = float(x[0])
+        # DP uneven row gather
+        dpc = Communicator(st.dp_group, ipc=False)
+        rows = torch.arange(st.dp_rank + 1, dtype=torch.float32)[:, None].repeat(1, 3) + 10 * st.dp_rank
+        res["gather"] = dpc.all_gather_rows(rows)[:, 0].tolist()
+        # bucketed gather of mixed dtypes/shapes
+        b = BucketedAllGather(dpc, bucket_bytes=64)
+        b.add(torch.full((2, 3), float(st.dp_rank)))
+        b.add(torch.tensor([st.dp_rank, 7], dtype=torch.int64))
+        per = b.flush()
+        res["bucket"] = [[float(p[0][0, 0]), int(p[1][0]), int(p[1][1])] for p in per]
+        # SPMD runner over a global batch of 10 items
+        run = DataParallelRunner(lambda xs: torch.tensor(xs, dtype=torch.float32)[:, None] * 2, dpc)
+        res["dp_run"] = run.run(list(range(10)))[:, 0].tolist()
+        q.put(res)
+    finally:
+        destroy()
+
+
+def _spawn(world, tp):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_dist_worker, args=(r, world, tp, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=180) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+    assert all(p.exitcode == 0 for p in ps)
+    return sorted(out, key=lambda d: d["rank"])
+
+
+def test_dp_world2_gloo():
+    res = _spawn(2, 1)
+    for r in res:
+        assert r["dp_ranks"] == (0, 1)
+        assert r["gather"] == [0.0, 10.0, 11.0]
+        assert r["bucket"] == [[0.0, 0, 7], [1.0, 1, 7]]
+        assert r["dp_run"] == [2.0 * i for i in range(10)]
+
+
+def test_tp2_dp2_layout_world4_gloo():
+    res = _spawn(4, 2)
+    assert [r["tp_ranks"] for r in res] == [(0, 1), (0, 1), (2, 3), (2, 3)]
+    assert [r["dp_ranks"] for r in res] == [(0, 2), (1, 3), (0, 2), (1, 3)]
+    assert [r["tp_sum"] for r in res] == [3.0, 3.0, 7.0, 7.0]
+    assert [r["tp_rank"] for r in res] == [0, 1, 0, 1]
+
+
+def test_worker_pool_runs_and_orders_results():
+    pool = GPUWorkerPool("lumen_amd.parallel.worker_pool:echo_factory", ["cpu", "cpu"], kwargs={"scale": 2.0})
+    try:
+        items = [np.full(3, i, dtype=np.float32) for i in range(9)]
+        assert pool.run("sum", items) == [6.0 * i for i in range(9)]
+        with pytest.raises(WorkerTaskError, match="requested failure"):
+            pool.submit("fail", [1]).result(30)
+        assert pool.run("sum", items[:1]) == [0.0]     # pool still healthy after a task error
+    finally:
+        pool.close()
+
+
+def test_worker_pool_detects_lost_worker_and_respawns(monkeypatch):
+    monkeypatch.setenv("LUMEN_FAULT_KILL_WORKER", "0:1")   # worker 0 dies on its 2nd task
+    pool = GPUWorkerPool("lumen_amd.parallel.worker_pool:echo_factory", ["cpu", "cpu"], heartbeat_s=0.2)
+    try:
+        assert pool.submit("sum", [np.ones(2)], worker=0).result(30) == [2.0]
+        with pytest.raises(WorkerLostError):
+            pool.submit("sum", [np.ones(2)], worker=0).result(30)
+        t0 = time.time()
+        while pool.stats["restarts"] < 1 or len(pool.live()) < 2:
+            assert time.time() - t0 < 120, "worker was not respawned"
+            time.sleep(0.1)
+        assert pool.run("sum", [np.ones(4)] * 4) == [4.0] * 4
+    finally:
+        pool.close()
+
+
+def test_worker_pool_task_timeout_kills_hung_worker():
+    pool = GPUWorkerPool("lumen_amd.parallel.worker_pool:echo_factory", ["cpu"], heartbeat_s=0.2, task_timeout_s=1.0)
+    try:
+        with pytest.raises(WorkerLostError):
+            pool.submit("sleep", [30]).result(60)
+    finally:
+        pool.close()
+
+
+def _vlm_leader(cache, tp, q):
+    import json as _json
+
+    os.environ["LUMEN_TP_SIZE"] = str(tp)
+    from lumen_amd.resources.validator import config_from_dict
+    from lumen_amd.services.vlm import GeneralFastVLMService
+    from lumen_amd.utils.image import encode_jpeg
+
+    cfg = {"metadata": {"version": "1.0.0", "region": "other", "cache_dir": cache},
+           "deployment": {"mode": "single", "service": "vlm"}, "server": {"port": 50557, "host": "127.0.0.1"},
+           "services": {"vlm": {"enabled": True, "package": "lumen_vlm",
+                                "import_info": {"registry_class": "lumen_vlm.fastvlm.GeneralFastVLMService",
+                                                "add_to_server": "lumen_vlm.proto.ml_service_pb2_grpc.add_InferenceServicer_to_server"},
+                                "backend_settings": {"device": "cpu"},
+                                "models": {"general": {"model": "fastvlm-tiny", "runtime": "onnx"}}}}}
+    s = GeneralFastVLMService.from_config(config_from_dict(cfg).services["vlm"], cache)
+    s.initialize()
+    try:
+        img = encode_jpeg(np.random.default_rng(0).integers(0, 255, (40, 60, 3), dtype=np.uint8))
+        outs = []
+        for prompt in ("Describe.", "What is this?"):
+            body, _, _ = s.handle("vlm_generate", img, "image/jpeg", {"prompt": prompt, "max_new_tokens": "9"})
+            outs.append(_json.loads(body)["text"])
+        q.put({"texts": outs, "tp": s.backend.tp.world})
+    finally:
+        s.close()
+
+
+def test_vlm_tensor_parallel_serving_matches_tp1(tmp_path):
+    """The gRPC VLM service with LUMEN_TP_SIZE=2 spawns a follower rank (gloo on CPU) and
+    generates the same greedy text as the single-rank service."""
+    from lumen_amd.models.vlm import write_vlm_model
+
+    write_vlm_model(tmp_path / "models" / "fastvlm-tiny", "fastvlm-tiny")
+    ctx = mp.get_context("spawn")
+    res = {}
+    for tp in (1, 2):
+        q = ctx.Queue()
+        p = ctx.Process(target=_vlm_leader, args=(str(tmp_path), tp, q))
+        p.start()
+        res[tp] = q.get(timeout=240)
+        p.join(60)
+        assert p.exitcode == 0
+    assert res[2]["tp"] == 2 and res[1]["tp"] == 1
+    assert res[2]["texts"] == res[1]["texts"]
+
+
+def test_clip_dp_serving_matches_single_process(tmp_path, monkeypatch):
+    """LUMEN_DP_SIZE=2: the CLIP backend's batches run on 2 worker processes (CPU here,
+    one per GPU on MI355X) and return the same embeddings as the in-process backend."""
+    from lumen_amd.resources.config import ModelConfig, Runtime
+    from lumen_amd.resources.synthetic import write_clip_model
+    from lumen_amd.services.clip.backend import create_backend
+    from lumen_amd.services.clip.resources import ResourceLoader
+    from lumen_amd.utils.image import encode_jpeg
+
+    write_clip_model(tmp_path / "models" / "clip-tiny", "clip-tiny", preset="tiny", dataset="ImageNet_1k", n_labels=8)
+    res = ResourceLoader.load_model_resources(tmp_path, ModelConfig(model="clip-tiny", runtime=Runtime.torch,
+                                                                    dataset="ImageNet_1k"))
+    settings = type("S", (), {"device": "cpu", "batch_size": 4})()
+    imgs = [encode_jpeg(np.random.default_rng(i).integers(0, 255, (40, 30 + i, 3), dtype=np.uint8)) for i in range(5)]
+    texts = ["a cat", "a dog on a sofa", "sunset"]
+    single = create_backend(settings, res, "torch")
+    single.initialize()
+    try:
+        ref_i = single.image_batch_to_vectors(imgs)
+        ref_t = single.text_batch_to_vectors(texts)
+    finally:
+        single.close()
+    monkeypatch.setenv("LUMEN_DP_SIZE", "2")
+    dp = create_backend(settings, res, "torch")
+    dp.initialize()
+    try:
+        assert dp._pool is not None and dp._pool.size == 2
+        np.testing.assert_allclose(dp.image_batch_to_vectors(imgs), ref_i, atol=1e-5)
+        np.testing.assert_allclose(dp.text_batch_to_vectors(texts), ref_t, atol=1e-5)
+        np.testing.assert_allclose(dp.image_to_vector(imgs[2]), ref_i[2], atol=1e-5)
+        assert dp._pool.stats["tasks"] >= 4 and abs(dp.get_temperature() - single.get_temperature()) < 1e-3
+    finally:
+        dp.close()
