@@ -183,12 +183,27 @@ constexpr int G_BUF = 2 * G_OP;
 __device__ __forceinline__ void vm_wait4() { asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
 __device__ __forceinline__ void vm_wait0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+
+// Row-coalesced epilogue of the 256x256 kernels (8 waves, wave (wm, wn) holding
+// acc[qm][qn][i][j] = rows qm*128 + wm*64 + i*16 + [0,16), cols qn*128 + wn*32 + j*16 +
+// [0,16)).  Per 16-row slab the four waves of one wm group scatter their 16 x 64
+// pieces into a shared [16][256] fp32 LDS image, then each wave reads back 4 whole
+// rows, so 16 consecutive lanes cover one 256-column half-row: every store
+// instruction writes 4 rows x 256 contiguous bytes (full 128-B lines).  Writing the
+// per-wave 16 x 64 pieces directly (32-B fragments of 32 different lines per store
+// instruction) capped the C write stream at ~1.7 TB/s and cost ~15 us per tile.
+// Needs 2 x 2 x 16 x 260 x 4 B = 66.5 KiB of free LDS; slabs alternate between two
+// images, one barrier per slab.  (Written inline in each kernel: as a helper taking
+// the accumulator by reference hipcc keeps `acc` in scratch.)
+constexpr int EPI_RS = 260;   // row stride (floats): 4 extra dwords -> conflict-free scatter
+
+
 // MODE 0: 4 phases/K-tile, one half-tile prefetch per phase, counted vmcnt(4) +
 //         raw barrier after phases 0, 1, 3.
 // MODE 1: MODE 0 + s_setprio(1) around each MFMA cluster.
 // MODE 2: whole next tile prefetched at phase 0, one vmcnt(0) + barrier per
 //         K-tile (phases free to interleave LDS reads with MFMAs), setprio.
-template <int MODE>
+template <int MODE, int GLU, int EPI>
 __global__ void __launch_bounds__(512)
 gemm_glds_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                  void* __restrict__ C, int64_t ldc, int M, int N, int K, GemmEpi ep, int group_m) {
@@ -216,6 +231,7 @@ gemm_glds_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     tn = bid % tiles_n;
   }
   const int m0 = tm * 256, n0 = tn * 256;
+  const int64_t t_start = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
 
   // ---- staging geometry: half-tile = 16 wave-instructions of 8 rows x 128 B;
   // wave wid issues groups g = 2*wid + i (i = 0, 1).  Lane l writes LDS row
@@ -267,6 +283,7 @@ gemm_glds_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
   stage(0, 1, 0, 0);
   if (MODE != 2 && nk > 1) vm_wait4(); else vm_wait0();
   __builtin_amdgcn_s_barrier();
+  const int64_t t_pro = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
 
   bf16x8_t fa[4][2], fb[2][2];
   auto load_a = [&](const char* base, int qm) {
@@ -337,11 +354,448 @@ gemm_glds_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     __builtin_amdgcn_s_barrier();
   }
 
-  // ---- epilogue: per (qm, i) slab of 16 rows x 64 cols (2 x 32 col groups)
+  // ---- epilogue (row-coalesced through LDS)
   __syncthreads();
+  const int64_t t_loop = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  const __amdgpu_buffer_rsrc_t crs = c_rsrc(C);   // write-through C stores (host guarantees < 4 GiB of C)
+  if constexpr (EPI == 0 || EPI == 3) {
+    // per-wave 16-row slabs (each wave stores its own 16 x 64 pieces)
+    constexpr int LDSTR = 68;
+    float* es = (float*)smem + wid * 16 * LDSTR;
+    const int rr = lane >> 2, cq = lane & 3;
+    const int ncol = n0 + (cq >> 1) * 128 + wn * 32 + (cq & 1) * 16;
+    Unroll<0, 2>::run([&](const int qm) {
+      Unroll<0, 4>::run([&](const int i) {
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              es[(fq * 4 + r) * LDSTR + qn * 32 + j * 16 + frow] = acc[qm][qn][i][j][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cq * 16 + q * 4);
+          v[q * 4 + 0] = t[0]; v[q * 4 + 1] = t[1]; v[q * 4 + 2] = t[2]; v[q * 4 + 3] = t[3];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        epi_store16_t<EPI == 3>(v, m0 + qm * 128 + wm * 64 + i * 16 + rr, ncol, M, N, C, ldc, ep, crs);
+      });
+    });
+  } else {
+    const int rrow = wn * 4 + (lane >> 4), rl = lane & 15;
+    Unroll<0, 2>::run([&](const int qm) {
+      Unroll<0, 4>::run([&](const int i) {
+        float* R = (float*)smem + (((qm * 4 + i) & 1) * 2 + wm) * 16 * EPI_RS;
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              R[(fq * 4 + r) * EPI_RS + qn * 128 + wn * 32 + j * 16 + frow] = acc[qm][qn][i][j][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const int m = m0 + qm * 128 + wm * 64 + i * 16 + rrow;
+        const float* row = R + rrow * EPI_RS;
+        if constexpr (GLU) {   // SwiGLU needs 16 consecutive (interleaved gate|up) columns per lane
+          float v[16];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x4_t t = *(const f32x4_t*)(row + rl * 16 + q * 4);
+            v[q * 4] = t[0]; v[q * 4 + 1] = t[1]; v[q * 4 + 2] = t[2]; v[q * 4 + 3] = t[3];
+          }
+          epi_store16_t<EPI == 2>(v, m, n0 + rl * 16, M, N, C, ldc, ep, crs);
+        } else {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            float v[8];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const f32x4_t t = *(const f32x4_t*)(row + h * 128 + rl * 8 + q * 4);
+              v[q * 4] = t[0]; v[q * 4 + 1] = t[1]; v[q * 4 + 2] = t[2]; v[q * 4 + 3] = t[3];
+            }
+            epi_store8_t<EPI == 2>(v, m, n0 + h * 128 + rl * 8, M, N, C, ldc, ep, crs);
+          }
+        }
+      });
+    });
+  }
+  if (ep.dbg) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      int64_t* d = ep.dbg + (int64_t)blockIdx.x * 4;
+      d[0] = t_start; d[1] = t_pro; d[2] = t_loop; d[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    }
+  }
+}
+
+// ============================================================================
+// Persistent 256x256x64 LDS-DMA kernel: one workgroup per CU walks its tiles
+// (lin = slot, slot + G, ...) and the staging pipeline never drains between
+// tiles — the last K-step of tile t prefetches K-tile 0 of tile t+1, so the
+// epilogue (LDS-staged, coalesced stores) of t runs while t+1's first operands
+// are already in flight, and its stores drain under t+1's first MFMAs.  With one
+// tile per launch-slot instead (gemm_glds_kernel) every CU issues its whole C tile
+// in the same instant, then waits a full HBM latency for the next tile's first
+// operands: ~15 us per tile at K = 1024, a third of the tile's MFMA time.
+// Same phase schedule / counted vmcnt / raw barriers as gemm_glds_kernel<1>.
+// ============================================================================
+__device__ __forceinline__ void tile_coords(int lin, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
+  if (group_m > 1) {
+    const int span = group_m * tiles_n;
+    const int grp = lin / span, first = grp * group_m;
+    const int gsz = min(tiles_m - first, group_m);
+    const int r = lin % span;
+    tm = first + r % gsz;
+    tn = r / gsz;
+  } else {
+    tm = lin / tiles_n;
+    tn = lin % tiles_n;
+  }
+}
+
+__global__ void __launch_bounds__(512)
+gemm_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
+                    void* __restrict__ C, int64_t ldc, int M, int N, int K, GemmEpi ep, int group_m) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int tiles_n = (N + 255) / 256;
+  const int tiles_m = (M + 255) / 256;
+  const int ntiles = tiles_n * tiles_m;
+  const int G = gridDim.x;
+  int lin = xcd_remap(blockIdx.x, G);   // concurrent tiles of one XCD are consecutive -> share panels in L2
+  if (lin >= ntiles) return;
+
+  // staging geometry (see gemm_glds_kernel): lane writes LDS row g*8 + l/8, physical
+  // chunk l%8, fetching logical chunk (l%8) ^ ((row >> 1) & 7)
+  int srow[2], scol[2], dst_off[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int g = 2 * wid + i;
+    const int r = g * 8 + (lane >> 3);
+    srow[i] = r;
+    scol[i] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+    dst_off[i] = g * 1024;
+  }
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  typedef const __attribute__((address_space(1))) void* g_ptr_t;
+  auto stageA = [&](int h, int buf, int m0_, int koff) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = min(m0_ + h * 128 + srow[i], M - 1);
+      __builtin_amdgcn_global_load_lds((g_ptr_t)(A + (int64_t)row * lda + scol[i] + koff),
+                                       (lds_ptr_t)(smem + buf * G_BUF + h * G_HALF + dst_off[i]), 16, 0, 0);
+    }
+  };
+  auto stageB = [&](int h, int buf, int n0_, int koff) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = min(n0_ + h * 128 + srow[i], N - 1);
+      __builtin_amdgcn_global_load_lds((g_ptr_t)(W + (int64_t)row * ldw + scol[i] + koff),
+                                       (lds_ptr_t)(smem + buf * G_BUF + G_OP + h * G_HALF + dst_off[i]), 16, 0, 0);
+    }
+  };
+
+  const int frow = lane & 15, fq = lane >> 4;
+  const int nk = K / BK;
+  int tm, tn;
+  tile_coords(lin, tiles_m, tiles_n, group_m, tm, tn);
+  int m0 = tm * 256, n0 = tn * 256;
+  // prologue: K-tile 0 of the first tile in phase order A0, B0, B1, A1
+  stageA(0, 0, m0, 0);
+  stageB(0, 0, n0, 0);
+  stageB(1, 0, n0, 0);
+  stageA(1, 0, m0, 0);
+  if (nk > 1 || lin + G < ntiles) vm_wait4(); else vm_wait0();
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8_t fa[4][2], fb[2][2];
+  auto load_a = [&](const char* base, int qm) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        fa[i][s] = *(const bf16x8_t*)(base + qm * G_HALF + swz(wm * 64 + i * 16 + frow, s * 4 + fq));
+  };
+  auto load_b = [&](const char* base, int qn) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        fb[j][s] = *(const bf16x8_t*)(base + G_OP + qn * G_HALF + swz(wn * 32 + j * 16 + frow, s * 4 + fq));
+  };
+
+  int buf = 0;
+  while (true) {
+    const int nlin = lin + G;
+    const bool has_next = nlin < ntiles;
+    int nm0 = 0, nn0 = 0;
+    if (has_next) {
+      int ntm, ntn;
+      tile_coords(nlin, tiles_m, tiles_n, group_m, ntm, ntn);
+      nm0 = ntm * 256;
+      nn0 = ntn * 256;
+    }
+    f32x4_t acc[2][2][4][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool last = kt + 1 == nk;
+      const bool more = !last || has_next;
+      const int pm0 = last ? nm0 : m0, pn0 = last ? nn0 : n0;
+      const int koff = last ? 0 : (kt + 1) * BK;
+      const int nbuf = buf ^ 1;
+      const char* base = smem + buf * G_BUF;
+#define LUMEN_PQUAD(QM, QN)                                                                                    \
+      __builtin_amdgcn_s_setprio(1);                                                                           \
+      Unroll<0, 4>::run([&](const int i) {                                                                    \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                          \
+        _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                          \
+          acc[QM][QN][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[j][s], acc[QM][QN][i][j], 0, 0, 0); \
+      });                                                                                                      \
+      __builtin_amdgcn_s_setprio(0);
+      // phase 0: quadrant (0,0)
+      if (more) stageA(0, nbuf, pm0, koff);
+      load_a(base, 0);
+      load_b(base, 0);
+      LUMEN_PQUAD(0, 0)
+      if (more) vm_wait4(); else vm_wait0();   // B1 landed
+      __builtin_amdgcn_s_barrier();
+      if (more) stageB(0, nbuf, pn0, koff);
+      // phase 1: quadrant (0,1)
+      load_b(base, 1);
+      LUMEN_PQUAD(0, 1)
+      if (more) vm_wait4(); else vm_wait0();   // A1 landed
+      __builtin_amdgcn_s_barrier();
+      if (more) stageB(1, nbuf, pn0, koff);
+      // phase 2: quadrant (1,1)
+      load_a(base, 1);
+      LUMEN_PQUAD(1, 1)
+      // phase 3: quadrant (1,0)
+      if (more) stageA(1, nbuf, pm0, koff);
+      load_b(base, 0);
+      LUMEN_PQUAD(1, 0)
+#undef LUMEN_PQUAD
+      if (more) vm_wait4(); else vm_wait0();   // next A0, B0 landed
+      __builtin_amdgcn_s_barrier();
+      buf = nbuf;
+    }
+
+    // epilogue through the LDS buffer the last K-step consumed (buf ^ 1); the next
+    // tile's first K-tile is landing in `buf` meanwhile.  Every wave finished reading
+    // that buffer before the loop's final barrier.
+    constexpr int LDSTR = 68;
+    float* es = (float*)(smem + (buf ^ 1) * G_BUF) + wid * 16 * LDSTR;
+    const int rr = lane >> 2, cq = lane & 3;
+    const int ncol = n0 + (cq >> 1) * 128 + wn * 32 + (cq & 1) * 16;
+    Unroll<0, 2>::run([&](const int qm) {
+      Unroll<0, 4>::run([&](const int i) {
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              es[(fq * 4 + r) * LDSTR + qn * 32 + j * 16 + frow] = acc[qm][qn][i][j][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cq * 16 + q * 4);
+          v[q * 4 + 0] = t[0]; v[q * 4 + 1] = t[1]; v[q * 4 + 2] = t[2]; v[q * 4 + 3] = t[3];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        epi_store16(v, m0 + qm * 128 + wm * 64 + i * 16 + rr, ncol, M, N, C, ldc, ep);
+      });
+    });
+    if (!has_next) break;
+    // the next tile's phase 0 restages this epilogue buffer: all waves' LDS reads first
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    lin = nlin;
+    m0 = nm0;
+    n0 = nn0;
+  }
+}
+
+// ============================================================================
+// 256x256x64 LDS-DMA kernel on a 10-slot half-tile ring (all 160 KiB of LDS)
+// ============================================================================
+// The K loop is a stream of half-tiles g = 4 kt + h (h: A0, B0, B1, A1), each a
+// 128-row x 128-B image in ring slot g % 10.  Half-tile g is issued at phase g - 5,
+// i.e. 4-5 phases (one phase = one 64x32 accumulator quadrant per wave, 16 MFMAs)
+// before its first read, where the two-buffer kernels above get 2-3: at K = 1024
+// with M in the 10^5 range most A rows come from HBM, and that latency, not MFMA
+// issue, bounds the two-buffer loop.  Phase P: counted vmcnt for the half-tile it
+// reads -> raw barrier -> issue half-tile P + 5 into the slot of P - 5 (last read at
+// phase <= P - 3, behind a barrier) -> ds_read fragments -> 16 MFMAs.  Phase 3 of a
+// K-step re-reads B0 (landed long ago) and needs neither wait nor barrier.
+constexpr int R_SLOTS = 10;
+constexpr int R_DIST = 5;
+constexpr int R_SLOT = 128 * 128;
+
+__device__ __forceinline__ void vm_wait_halves(int rem) {
+  // rem = half-tiles (2 glds each) allowed to remain in flight
+  if (rem >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (rem == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (rem == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__global__ void __launch_bounds__(512)
+gemm_ring_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
+                 void* __restrict__ C, int64_t ldc, int M, int N, int K, GemmEpi ep, int group_m) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int tiles_n = (N + 255) / 256;
+  const int tiles_m = (M + 255) / 256;
+  int tm, tn;
+  tile_coords(xcd_remap(blockIdx.x, tiles_n * tiles_m), tiles_m, tiles_n, group_m, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  int srow[2], scol[2], dst_off[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int g = 2 * wid + i;
+    const int r = g * 8 + (lane >> 3);
+    srow[i] = r;
+    scol[i] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+    dst_off[i] = g * 1024;
+  }
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  typedef const __attribute__((address_space(1))) void* g_ptr_t;
+  // half-tile g: h = g & 3 -> A0, B0, B1, A1
+  auto issue = [&](int g, int slot) {
+    const int h = g & 3;
+    const int koff = (g >> 2) * BK;
+    char* dst = smem + slot * R_SLOT;
+    if (h == 0 || h == 3) {
+      const int base = m0 + (h == 3 ? 128 : 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = min(base + srow[i], M - 1);
+        __builtin_amdgcn_global_load_lds((g_ptr_t)(A + (int64_t)row * lda + scol[i] + koff),
+                                         (lds_ptr_t)(dst + dst_off[i]), 16, 0, 0);
+      }
+    } else {
+      const int base = n0 + (h == 2 ? 128 : 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = min(base + srow[i], N - 1);
+        __builtin_amdgcn_global_load_lds((g_ptr_t)(W + (int64_t)row * ldw + scol[i] + koff),
+                                         (lds_ptr_t)(dst + dst_off[i]), 16, 0, 0);
+      }
+    }
+  };
+
+  const int frow = lane & 15, fq = lane >> 4;
+  const int nk = K / BK;
+  const int nh = 4 * nk;
+  f32x4_t acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  bf16x8_t fa[4][2], fb[2][2];
+  auto load_a = [&](int slot) {
+    const char* base = smem + slot * R_SLOT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fa[i][s] = *(const bf16x8_t*)(base + swz(wm * 64 + i * 16 + frow, s * 4 + fq));
+  };
+  auto load_b = [&](int slot) {
+    const char* base = smem + slot * R_SLOT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fb[j][s] = *(const bf16x8_t*)(base + swz(wn * 32 + j * 16 + frow, s * 4 + fq));
+  };
+
+  // prologue: half-tiles 0 .. R_DIST-1
+  const int npro = nh < R_DIST ? nh : R_DIST;
+#pragma unroll
+  for (int g = 0; g < R_DIST; ++g)
+    if (g < npro) issue(g, g);
+  int last = npro - 1;     // newest half-tile issued
+  int islot = npro % R_SLOTS;   // slot of the next half-tile to issue
+  int s0 = 0;              // slot of A0 of the current K-step
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int P = 4 * kt;
+    const int sA0 = s0, sB0 = s0 + 1 >= R_SLOTS ? s0 + 1 - R_SLOTS : s0 + 1;
+    const int sB1 = sB0 + 1 >= R_SLOTS ? sB0 + 1 - R_SLOTS : sB0 + 1;
+    const int sA1 = sB1 + 1 >= R_SLOTS ? sB1 + 1 - R_SLOTS : sB1 + 1;
+#define LUMEN_RQUAD(QM, QN)                                                                                    \
+    __builtin_amdgcn_s_setprio(1);                                                                             \
+    Unroll<0, 4>::run([&](const int i) {                                                                      \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                            \
+      _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                            \
+        acc[QM][QN][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[j][s], acc[QM][QN][i][j], 0, 0, 0); \
+    });                                                                                                        \
+    __builtin_amdgcn_s_setprio(0);
+#define LUMEN_RISSUE(PP)                                                                                       \
+    if ((PP) + R_DIST < nh) {                                                                                  \
+      issue((PP) + R_DIST, islot);                                                                             \
+      last = (PP) + R_DIST;                                                                                    \
+      islot = islot + 1 == R_SLOTS ? 0 : islot + 1;                                                            \
+    }
+    // phase 0: quadrant (0,0) needs A0 (P) and B0 (P + 1)
+    vm_wait_halves(last - (P + 1));
+    __builtin_amdgcn_s_barrier();
+    LUMEN_RISSUE(P)
+    load_a(sA0);
+    load_b(sB0);
+    LUMEN_RQUAD(0, 0)
+    // phase 1: quadrant (0,1) needs B1 (P + 2)
+    vm_wait_halves(last - (P + 2));
+    __builtin_amdgcn_s_barrier();
+    LUMEN_RISSUE(P + 1)
+    load_b(sB1);
+    LUMEN_RQUAD(0, 1)
+    // phase 2: quadrant (1,1) needs A1 (P + 3)
+    vm_wait_halves(last - (P + 3));
+    __builtin_amdgcn_s_barrier();
+    LUMEN_RISSUE(P + 2)
+    load_a(sA1);
+    LUMEN_RQUAD(1, 1)
+    // phase 3: quadrant (1,0): B0 again (resident), no wait / barrier
+    LUMEN_RISSUE(P + 3)
+    load_b(sB0);
+    LUMEN_RQUAD(1, 0)
+#undef LUMEN_RQUAD
+#undef LUMEN_RISSUE
+    s0 = s0 + 4 >= R_SLOTS ? s0 + 4 - R_SLOTS : s0 + 4;
+  }
+
+  // epilogue through LDS (nothing in flight any more: every issued half-tile was read)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
   constexpr int LDSTR = 68;
   float* es = (float*)smem + wid * 16 * LDSTR;
-  const int rr = lane >> 2, cq = lane & 3;   // 16 rows x 4 col-chunks of 16
+  const int rr = lane >> 2, cq = lane & 3;
   const int ncol = n0 + (cq >> 1) * 128 + wn * 32 + (cq & 1) * 16;
   Unroll<0, 2>::run([&](const int qm) {
     Unroll<0, 4>::run([&](const int i) {
@@ -365,6 +819,20 @@ gemm_glds_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
   });
 }
 
+static hipError_t launch_ring(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
+                              int64_t ldc, int M, int N, int K, const GemmEpi& ep, int group_m, hipStream_t stream) {
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const size_t lds = (size_t)R_SLOTS * R_SLOT;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm_ring_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(gemm_ring_kernel, dim3(tiles), dim3(512), lds, stream, A, lda, W, ldw, C, ldc, M, N, K, ep,
+                     group_m);
+  return hipGetLastError();
+}
+
 template <int BM, int BN, int WM, int WN>
 static hipError_t launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
                              void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep,
@@ -384,23 +852,70 @@ static hipError_t launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, 
   return hipGetLastError();
 }
 
-template <int MODE>
-static hipError_t launch_glds(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
-                              int64_t ldc, int M, int N, int K, const GemmEpi& ep, int group_m, hipStream_t stream) {
+template <int MODE, int EPI>
+static hipError_t launch_glds_e(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
+                                int64_t ldc, int M, int N, int K, const GemmEpi& ep, int group_m, hipStream_t stream) {
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   const size_t lds = 2 * G_BUF;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm_glds_kernel<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)gemm_glds_kernel<MODE, 0, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)gemm_glds_kernel<MODE, 1, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL(gemm_glds_kernel<MODE>, dim3(tiles), dim3(512), lds, stream, A, lda, W, ldw, C, ldc, M, N, K, ep,
+  if (ep.glu)
+    hipLaunchKernelGGL((gemm_glds_kernel<MODE, 1, EPI>), dim3(tiles), dim3(512), lds, stream, A, lda, W, ldw, C, ldc, M,
+                       N, K, ep, group_m);
+  else
+    hipLaunchKernelGGL((gemm_glds_kernel<MODE, 0, EPI>), dim3(tiles), dim3(512), lds, stream, A, lda, W, ldw, C, ldc, M,
+                       N, K, ep, group_m);
+  return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t launch_glds(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
+                              int64_t ldc, int M, int N, int K, const GemmEpi& ep, int group_m, int epi,
+                              hipStream_t stream) {
+  switch (epi) {
+    case 1: return launch_glds_e<MODE, 1>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
+    case 2: return launch_glds_e<MODE, 2>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
+    case 3: return launch_glds_e<MODE, 3>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
+    default: return launch_glds_e<MODE, 0>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
+  }
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+static hipError_t launch_persist(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
+                                 int64_t ldc, int M, int N, int K, const GemmEpi& ep, int group_m,
+                                 hipStream_t stream) {
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const int grid = tiles < num_cus() ? tiles : num_cus();
+  const size_t lds = 2 * G_BUF;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm_persist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(gemm_persist_kernel, dim3(grid), dim3(512), lds, stream, A, lda, W, ldw, C, ldc, M, N, K, ep,
                      group_m);
   return hipGetLastError();
 }
 
-// Host entry: tile choice by problem size.  tile = -1 auto, else forced config id:
-//   0 = 256x256 register-staged, 1 = 128x128, 2 = 64x64, 3 = 32x64, 4 = 256x256 LDS-DMA phased
+// Host entry: tile choice by problem size.  tile = -1 auto, else forced config id
+// (+ 10 * group_m + 100 * epilogue variant + 1000 to disable the tail split):
+//   0 = 256x256 register-staged, 1 = 128x128, 2 = 64x64, 3 = 32x64, 4 = 256x256 LDS-DMA phased,
+//   5 = 4 + setprio, 6 = one wait per K-tile, 7 = persistent 256x256 (cross-tile prefetch),
+//   8 = 256x256 on the 10-slot half-tile ring (deeper prefetch)
 hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
                      int64_t ldc, int M, int N, int K, const GemmEpi& ep, int tile,
                      hipStream_t stream) {
@@ -409,13 +924,18 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
   if (tile < 0) {
     const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
     const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
-    if (t256 >= 512) tile = 5;
+    // measured on MI355X (tools/gemm_bench.py, random bf16, profiles/r1_gemm_epilogue_ab_v1.jsonl):
+    // K <= 512: row-coalesced write-through epilogue (+25-30 %); K 1024-2048: persistent
+    // kernel (+4-8 %); K >= 4096: per-wave epilogue LDS-DMA kernel
+    if (t256 >= 512) tile = K <= 512 ? 245 : (K <= 2048 ? 47 : 5);
     else if (t128 >= 256) tile = 1;
     else if (M <= 64) tile = 3;
     else tile = 2;
   }
-  // tile = config + 10 * group_m (group_m 0 -> default 4 for the 256x256 LDS-DMA kernel)
-  int group_m = tile / 10;
+  // tile = config + 10 * group_m + 100 * epilogue (group_m 0 -> default 4 for the 256x256 LDS-DMA kernel;
+  // epilogue 0 = per-wave slabs, 1 = row-coalesced, 2 = row-coalesced write-through, 3 = per-wave write-through)
+  const int epi = (tile / 100) % 10;
+  int group_m = (tile / 10) % 10;
   tile = tile % 10;
   if (group_m == 0) group_m = 4;
   if (group_m == 1) group_m = 0;
@@ -425,7 +945,7 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
   // tile time.  Run the largest row range whose tile count is a multiple of 256 on
   // the 256x256 kernel and the few remaining rows on 128x128 tiles (4x more, 4x
   // shorter workgroups) so the tail costs ~1/4 of a round.  Only for plain row maps.
-  if (allow_split && tile >= 4 && tile <= 6 && ep.out_group == 0 && ep.table == nullptr) {
+  if (allow_split && tile >= 4 && tile <= 8 && ep.out_group == 0 && ep.table == nullptr) {
     const int tiles_n = (N + 255) / 256;
     const int tiles_m = (M + 255) / 256;
     int q = 256;
@@ -434,7 +954,8 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
     const int tail = tiles_m * tiles_n - main_m_tiles * tiles_n;
     if (main_m_tiles > 0 && main_m_tiles < tiles_m && tail < 128) {
       const int M0 = main_m_tiles * 256;
-      hipError_t e = gemm_bf16(A, lda, W, ldw, C, ldc, M0, N, K, ep, tile + 10 * (group_m == 0 ? 1 : group_m), stream);
+      hipError_t e = gemm_bf16(A, lda, W, ldw, C, ldc, M0, N, K, ep, tile + 10 * (group_m == 0 ? 1 : group_m) + 100 * epi,
+                               stream);
       if (e != hipSuccess) return e;
       GemmEpi e2 = ep;
       if (e2.residual) e2.residual += (int64_t)M0 * e2.ldr;
@@ -442,13 +963,23 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
       return launch_cfg<128, 128, 2, 2>(A + (int64_t)M0 * lda, lda, W, ldw, C2, ldc, M - M0, N, K, e2, stream);
     }
   }
+  if (tile >= 4 && tile <= 6) {
+    // the 256x256 LDS-DMA kernels store C through a 32-bit-offset buffer descriptor
+    const int64_t last_row = ep.out_group > 0 ? (int64_t)((M - 1) / ep.out_group) * ep.out_group_stride +
+                                                    ep.out_row_offset + (M - 1) % ep.out_group
+                                              : (int64_t)M - 1;
+    const int64_t extent = ((last_row + 1) * ldc) * (ep.out_f32 ? 4 : 2);
+    if (extent >= ((int64_t)1 << 32)) tile = 1;
+  }
   switch (tile) {
     case 0: return launch_cfg<256, 256, 2, 4>(A, lda, W, ldw, C, ldc, M, N, K, ep, stream);
     case 1: return launch_cfg<128, 128, 2, 2>(A, lda, W, ldw, C, ldc, M, N, K, ep, stream);
     case 2: return launch_cfg<64, 64, 2, 2>(A, lda, W, ldw, C, ldc, M, N, K, ep, stream);
-    case 4: return launch_glds<0>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
-    case 5: return launch_glds<1>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
-    case 6: return launch_glds<2>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
+    case 4: return launch_glds<0>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, epi, stream);
+    case 5: return launch_glds<1>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, epi, stream);
+    case 6: return launch_glds<2>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, epi, stream);
+    case 7: return launch_persist(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
+    case 8: return launch_ring(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
     default: return launch_cfg<32, 64, 1, 2>(A, lda, W, ldw, C, ldc, M, N, K, ep, stream);
   }
 }

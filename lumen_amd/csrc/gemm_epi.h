@@ -25,7 +25,24 @@ struct GemmEpi {
   int post_act;              // activation applied AFTER the residual add (ResNet: relu(conv + x))
   int glu;                   // SwiGLU: columns interleaved [gate 8 | up 8] per 16; writes silu(g) * u to
                              // column n/2 .. n/2+8 of C (C has N/2 columns)
+  int64_t* dbg;              // profiling only: per-workgroup s_memrealtime stamps (null in production)
 };
+
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+// 16-byte store of C: plain, or write-through (sc1) via a buffer descriptor over C.
+// Write-through matters for the big-tile epilogues: every CU publishing its whole
+// 128 KB C tile at once with plain (write-back) stores drains at ~1.7 TB/s chip-wide
+// (MI355X_MICROARCH publish-large: 64 KB per WG 8.2 us plain vs 3.0 us sc1).
+template <bool WT>
+__device__ __forceinline__ void st16(void* C, __amdgpu_buffer_rsrc_t rs, int64_t byte_off, u32x4_t v) {
+  if constexpr (WT) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, v), rs, (int)byte_off, 0, 16);
+  else *(u32x4_t*)((char*)C + byte_off) = v;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t c_rsrc(void* C) {
+  return __builtin_amdgcn_make_buffer_rsrc(C, (short)0, -1, 0x00020000);
+}
 
 __device__ __forceinline__ int swz(int row, int chunk) {
   // 16-byte chunk index XOR row bits 1..3: a ds_read_b128 lane group that reads
@@ -41,8 +58,9 @@ __device__ __forceinline__ void add8(float* v, const uint16_t* p) {
 }
 
 // Apply the epilogue to 16 consecutive columns [n, n+16) of row m and store.
-__device__ __forceinline__ void epi_store16(float* v, int m, int n, int M, int N, void* __restrict__ C,
-                                            int64_t ldc, const GemmEpi& ep) {
+template <bool WT>
+__device__ __forceinline__ void epi_store16_t(float* v, int m, int n, int M, int N, void* __restrict__ C,
+                                              int64_t ldc, const GemmEpi& ep, __amdgpu_buffer_rsrc_t rs) {
   if (m >= M || n >= N) return;
   const bool full = (n + 16 <= N);
 #pragma unroll
@@ -67,8 +85,7 @@ __device__ __forceinline__ void epi_store16(float* v, int m, int n, int M, int N
     float r[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) r[q] = v[q] * fast_rcp(1.f + __expf(-v[q])) * v[8 + q];
-    uint16_t* o = (uint16_t*)C + (int64_t)m * ldc + (n >> 1);
-    *(u32x4_t*)o = pack8(r);
+    st16<WT>(C, rs, ((int64_t)m * ldc + (n >> 1)) * 2, pack8(r));
     return;
   }
   if (ep.act) apply_act_n<16>(v, ep.act);
@@ -118,7 +135,8 @@ __device__ __forceinline__ void epi_store16(float* v, int m, int n, int M, int N
     if (full) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        *(f32x4_t*)(o + 4 * q) = (f32x4_t){v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+        st16<WT>(C, rs, (orow * ldc + n + 4 * q) * 4,
+                 __builtin_bit_cast(u32x4_t, (f32x4_t){v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]}));
     } else {
 #pragma unroll
       for (int q = 0; q < 16; ++q) if (n + q < N) o[q] = v[q];
@@ -126,13 +144,98 @@ __device__ __forceinline__ void epi_store16(float* v, int m, int n, int M, int N
   } else {
     uint16_t* o = (uint16_t*)C + orow * ldc + n;
     if (full) {
-      *(u32x4_t*)o = pack8(v);
-      *(u32x4_t*)(o + 8) = pack8(v + 8);
+      st16<WT>(C, rs, (orow * ldc + n) * 2, pack8(v));
+      st16<WT>(C, rs, (orow * ldc + n + 8) * 2, pack8(v + 8));
     } else {
 #pragma unroll
       for (int q = 0; q < 16; ++q) if (n + q < N) o[q] = f2bf(v[q]);
     }
   }
+}
+
+// 8-column form (no SwiGLU): [n, n+8) of row m.  Used by the row-coalesced
+// 256x256 epilogue, where 16 consecutive lanes store 256 contiguous bytes.
+template <bool WT>
+__device__ __forceinline__ void epi_store8_t(float* v, int m, int n, int M, int N, void* __restrict__ C, int64_t ldc,
+                                             const GemmEpi& ep, __amdgpu_buffer_rsrc_t rs) {
+  if (m >= M || n >= N) return;
+  const bool full = (n + 8 <= N);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] *= ep.alpha;
+  if (ep.bias) {
+    if (ep.bias_f32) {
+      const float* b = (const float*)ep.bias + n;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] += (full || n + q < N) ? b[q] : 0.f;
+    } else {
+      const uint16_t* b = (const uint16_t*)ep.bias + n;
+      if (full) add8(v, b);
+      else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) if (n + q < N) v[q] += bf2f(b[q]);
+      }
+    }
+  }
+  if (ep.act) apply_act_n<8>(v, ep.act);
+  if (ep.prelu) {
+    float sl[8];
+    if (full) unpack8(*(const u32x4_t*)(ep.prelu + n), sl);
+    else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) sl[q] = (n + q < N) ? bf2f(ep.prelu[n + q]) : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = v[q] > 0.f ? v[q] : v[q] * sl[q];
+  }
+  int64_t orow = m;
+  if (ep.out_group > 0)
+    orow = (int64_t)(m / ep.out_group) * ep.out_group_stride + ep.out_row_offset + (m % ep.out_group);
+  if (ep.table) {
+    const uint16_t* t = ep.table + (int64_t)((m % ep.table_period) + ep.table_offset) * ep.ldt + n;
+    if (full) add8(v, t);
+    else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) if (n + q < N) v[q] += bf2f(t[q]);
+    }
+  }
+  if (ep.residual) {
+    const uint16_t* t = ep.residual + orow * ep.ldr + n;
+    if (full) add8(v, t);
+    else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) if (n + q < N) v[q] += bf2f(t[q]);
+    }
+  }
+  if (ep.post_act) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+  }
+  if (ep.out_f32) {
+    float* o = (float*)C + orow * ldc + n;
+    if (full) {
+      st16<WT>(C, rs, (orow * ldc + n) * 4, __builtin_bit_cast(u32x4_t, (f32x4_t){v[0], v[1], v[2], v[3]}));
+      st16<WT>(C, rs, (orow * ldc + n + 4) * 4, __builtin_bit_cast(u32x4_t, (f32x4_t){v[4], v[5], v[6], v[7]}));
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) if (n + q < N) o[q] = v[q];
+    }
+  } else {
+    uint16_t* o = (uint16_t*)C + orow * ldc + n;
+    if (full) st16<WT>(C, rs, (orow * ldc + n) * 2, pack8(v));
+    else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) if (n + q < N) o[q] = f2bf(v[q]);
+    }
+  }
+}
+
+__device__ __forceinline__ void epi_store16(float* v, int m, int n, int M, int N, void* __restrict__ C, int64_t ldc,
+                                            const GemmEpi& ep) {
+  epi_store16_t<false>(v, m, n, M, N, C, ldc, ep, c_rsrc(C));
+}
+__device__ __forceinline__ void epi_store8(float* v, int m, int n, int M, int N, void* __restrict__ C, int64_t ldc,
+                                           const GemmEpi& ep) {
+  epi_store8_t<false>(v, m, n, M, N, C, ldc, ep, c_rsrc(C));
 }
 
 }  // namespace lumen

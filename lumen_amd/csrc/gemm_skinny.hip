@@ -5,8 +5,10 @@
 //   * a workgroup owns one 16-column N tile and a K range; its 4 waves take
 //     interleaved 32-wide k-steps of that range (split-K inside the workgroup,
 //     reduced through LDS), and grid.y splits K further across workgroups so that
-//     even N = 896 launches ~1000 workgroups (fp32 atomics into a zeroed
-//     workspace, then a finalize pass applies the epilogue);
+//     even N = 896 launches ~1000 workgroups (each K-split writes its fp32 partial
+//     slab, then a finalize pass sums the slabs in split order — deterministic, so
+//     hipGraph replays and eager launches give bitwise-identical logits — and
+//     applies the epilogue);
 //   * both MFMA operands come straight from global memory in fragment layout:
 //     B = W^T (lane: 16 contiguous bytes of weight row n0 + (lane & 15)), A = the
 //     activations (L2-resident, shared by every workgroup), 16 rows per MFMA row
@@ -84,10 +86,11 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const uint16_t* __rest
     for (int r = 0; r < 4; ++r) red[wid][t * 16 + 4 * g + r][col] = acc[t][r];
   __syncthreads();
   if (ws != nullptr) {
+    float* slab = ws + (int64_t)blockIdx.y * M * N;
     for (int idx = tid; idx < MT * 16 * 16; idx += 256) {
       const int m = idx >> 4, c = idx & 15;
       if (m < M && n0 + c < N)
-        atomicAdd(ws + (int64_t)m * N + n0 + c, red[0][m][c] + red[1][m][c] + red[2][m][c] + red[3][m][c]);
+        slab[(int64_t)m * N + n0 + c] = red[0][m][c] + red[1][m][c] + red[2][m][c] + red[3][m][c];
     }
     return;
   }
@@ -102,15 +105,20 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const uint16_t* __rest
   }
 }
 
-__global__ void gemm_skinny_finalize(const float* __restrict__ ws, void* __restrict__ C, int64_t ldc, int M, int N,
-                                     GemmEpi ep) {
+__global__ void gemm_skinny_finalize(const float* __restrict__ ws, int ks, void* __restrict__ C, int64_t ldc, int M,
+                                     int N, GemmEpi ep) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;   // one thread per (m, 16-column group)
   const int groups = (N + 15) / 16;
   if (idx >= M * groups) return;
   const int m = idx / groups, n = (idx - m * groups) * 16;
   float v[16];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) v[c] = n + c < N ? ws[(int64_t)m * N + n + c] : 0.f;
+  for (int c = 0; c < 16; ++c) v[c] = 0.f;
+  for (int s = 0; s < ks; ++s) {     // fixed summation order over the K-split slabs
+    const float* p = ws + ((int64_t)s * M + m) * N + n;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[c] += n + c < N ? p[c] : 0.f;
+  }
   epi_store16(v, m, n, M, N, C, ldc, ep);
 }
 
@@ -141,7 +149,8 @@ hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* W, int64_
     hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, block, 0, stream, A, lda, W, ldw, C, ldc, w, M, N, K, kchunk, ep);
   if (gy > 1) {
     const int total = M * ((N + 15) / 16);
-    hipLaunchKernelGGL(gemm_skinny_finalize, dim3((total + 255) / 256), dim3(256), 0, stream, ws, C, ldc, M, N, ep);
+    hipLaunchKernelGGL(gemm_skinny_finalize, dim3((total + 255) / 256), dim3(256), 0, stream, ws, gy, C, ldc, M, N,
+                       ep);
   }
   return hipGetLastError();
 }

@@ -129,11 +129,26 @@ void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tens
   if ((tile == -1 || tile == 9) && M <= 32 && M > 0) {
     const int ks = lumen::skinny_ksplit((int)N, (int)K);
     at::Tensor ws;
-    if (ks > 1) ws = at::zeros({M, N}, a.options().dtype(at::kFloat));
+    if (ks > 1) ws = at::empty({ks, M, N}, a.options().dtype(at::kFloat));   // per-split slabs, no zero-fill
     LUMEN_CHECK_HIP(lumen::gemm_skinny(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0), (int)M,
                                        (int)N, (int)K, ep, ks > 1 ? ws.data_ptr<float>() : nullptr, ks, cur_stream()));
     return;
   }
+  LUMEN_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
+                                   (int)M, (int)N, (int)K, ep, (int)tile, cur_stream()));
+}
+
+// profiling: plain GEMM with per-workgroup timestamps (start, prologue, K-loop, epilogue) in dbg [wg, 4]
+void gemm_probe(const at::Tensor& a, const at::Tensor& w, at::Tensor out, at::Tensor dbg, int64_t tile) {
+  check_bf16_rows(a, "a");
+  check_bf16_rows(w, "w");
+  TORCH_CHECK(dbg.is_cuda() && dbg.scalar_type() == at::kLong && dbg.is_contiguous(), "gemm_probe: dbg int64");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(dbg.numel() >= ((M + 255) / 256) * ((N + 255) / 256) * 4, "gemm_probe: dbg too small");
+  lumen::GemmEpi ep{};
+  ep.alpha = 1.f;
+  ep.dbg = dbg.data_ptr<int64_t>();
+  const at::DeviceGuard guard(a.device());
   LUMEN_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
                                    (int)M, (int)N, (int)K, ep, (int)tile, cur_stream()));
 }
@@ -434,6 +449,7 @@ TORCH_LIBRARY(lumen, m) {
   m.def("norm(Tensor x, Tensor? row_idx, Tensor? add, Tensor(r!)? resid_out, Tensor w, Tensor? b, "
         "Tensor(o!) out, float eps, int mode) -> ()");
   m.def("l2norm_(Tensor(a!) x, float eps) -> ()");
+  m.def("gemm_probe(Tensor a, Tensor w, Tensor(o!) out, Tensor(d!) dbg, int tile) -> ()");
   m.def("cls_fill(Tensor(a!) x, Tensor cls, Tensor pos, int seq) -> ()");
   m.def("embed_gather(Tensor ids, Tensor table, Tensor? pos, Tensor(o!) out, int seq, int id_offset) -> ()");
   m.def("attention(Tensor q, Tensor k, Tensor v, Tensor(o!) o, Tensor? kv_len, float scale, bool causal) -> ()");
@@ -458,6 +474,7 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("norm", &norm);
   m.impl("l2norm_", &l2norm_);
+  m.impl("gemm_probe", &gemm_probe);
   m.impl("cls_fill", &cls_fill);
   m.impl("embed_gather", &embed_gather);
   m.impl("attention", &attention);

@@ -25,7 +25,7 @@ def test_native_library_loaded():
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 768, 1024), (131, 3072, 1024), (512, 4096, 1024),
                                    (37, 64, 128), (4096, 1024, 4096), (2, 512, 512), (2570, 1024, 640)])
 @pytest.mark.parametrize("act", [None, "gelu", "quick_gelu"])
-@pytest.mark.parametrize("tile", [-1, 4, 5, 6])
+@pytest.mark.parametrize("tile", [-1, 4, 5, 6, 7, 8])
 def test_gemm_vs_fp32(M, N, K, act, tile):
     g = torch.Generator().manual_seed(M + N + K)
     x = torch.randn(M, K, generator=g).bfloat16()
@@ -37,7 +37,7 @@ def test_gemm_vs_fp32(M, N, K, act, tile):
     assert _rel(got, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 def test_gemm_tiles_asymmetric(tile):
     # A = I, asymmetric B: catches a transposed C write
     M = N = K = 256
@@ -162,7 +162,28 @@ def test_gemm_activations(act):
     assert _rel(got, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [-1, 5])
+@pytest.mark.parametrize("M,N,K", [(40 * 256, 2048, 1024), (600 * 256 + 77, 1024, 128), (3000, 768, 256)])
+@pytest.mark.parametrize("tile", [7, 1007, 47, 17, 8, 48, 1008])
+def test_gemm_persistent_multi_tile(M, N, K, tile):
+    """Persistent kernel: several tiles per workgroup (cross-tile prefetch), epilogue with
+    bias + GELU + residual, bf16 and fp32 outputs, with/without the tail split."""
+    g = torch.Generator().manual_seed(M + K)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
+    b = torch.randn(N, generator=g)
+    r = torch.randn(M, N, generator=g).bfloat16()
+    xd, wd = x.to(DEV), w.to(DEV)
+    got = ops.linear(xd, wd, b.to(DEV), act="gelu", residual=r.to(DEV), tile=tile).cpu().float()
+    rows = torch.cat([torch.arange(0, 512), torch.arange(M // 2, M // 2 + 512), torch.arange(M - 700, M)])
+    ref = ops.linear(x[rows], w, b, act="gelu", residual=r[rows])
+    assert _rel(got[rows], ref) < 1e-2
+    got32 = ops.linear(xd, wd, out_dtype=torch.float32, tile=tile).cpu()
+    ref32 = x[rows].float() @ w.float().t()
+    assert _rel(got32[rows], ref32) < 1e-2
+    assert torch.isfinite(got).all()
+
+
+@pytest.mark.parametrize("tile", [-1, 5, 7])
 def test_gemm_tail_round_split(tile):
     # 66 row tiles x 4 column tiles: rows [0, 16384) on 256x256, the 300-row tail on 128x128
     M, N, K = 64 * 256 + 300, 1024, 512

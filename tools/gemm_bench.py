@@ -10,6 +10,10 @@ from lumen_amd import ops
 
 shapes = [(131584, 3072, 1024), (131584, 1024, 1024), (131584, 4096, 1024), (131584, 1024, 4096),
           (8192, 8192, 8192), (4096, 4096, 4096), (39424, 2304, 768)]
+if os.environ.get("GEMM_SHAPES") == "ksweep":
+    shapes = [(65536, 2048, k) for k in (64, 128, 256, 512, 1024, 2048, 4096)]
+if os.environ.get("GEMM_SHAPES") == "probe":
+    shapes = [(8192, 8192, 1024), (8192, 8192, 2048), (32768, 4096, 1024), (131584, 1024, 1024), (16384, 16384, 1024)]
 res = []
 for M, N, K in shapes:
     x = torch.randn(M, K, device="cuda").bfloat16()
@@ -18,11 +22,10 @@ for M, N, K in shapes:
     def run_t():
         torch.matmul(x, w.t(), out=out)
     r = {"M": M, "N": N, "K": K}
-    variants = [("g1", lambda: ops.linear(x, w, out=out, tile=15)), ("g2", lambda: ops.linear(x, w, out=out, tile=25)),
-                ("g4", lambda: ops.linear(x, w, out=out, tile=45)), ("g8", lambda: ops.linear(x, w, out=out, tile=85)),
-                ("torch", run_t), ("ns4", lambda: ops.linear(x, w, out=out, tile=1045)),
-                ("g4b", lambda: ops.linear(x, w, out=out, tile=45)), ("ns8", lambda: ops.linear(x, w, out=out, tile=1085)),
-                ("g16", lambda: ops.linear(x, w, out=out, tile=165))]
+    variants = [("e0", lambda: ops.linear(x, w, out=out, tile=45)), ("torch", run_t),
+                ("e1", lambda: ops.linear(x, w, out=out, tile=145)), ("e2", lambda: ops.linear(x, w, out=out, tile=245)),
+                ("e3", lambda: ops.linear(x, w, out=out, tile=345)), ("p4", lambda: ops.linear(x, w, out=out, tile=47)),
+                ("e0b", lambda: ops.linear(x, w, out=out, tile=45))]
     for name, fn in variants:
         for _ in range(3):
             fn()
@@ -37,8 +40,11 @@ for M, N, K in shapes:
         ms = s.elapsed_time(e) / n
         r[name + "_ms"] = round(ms, 3)
         r[name + "_tflops"] = round(2 * M * N * K / ms / 1e9, 1)
-    ref = (x[:256].float() @ w.float().t())
-    ops.linear(x, w, out=out, tile=4)
-    r["rel_err"] = float(((out[:256].float() - ref).norm() / ref.norm()).item())
+    for tname, t in (("rel_err_e0", 45), ("rel_err_e1", 145), ("rel_err_e2", 245), ("rel_err_e3", 345)):
+        out.zero_()
+        ops.linear(x, w, out=out, tile=t)
+        rows = torch.cat([torch.arange(0, 256), torch.arange(M - 256, M)]).cuda()
+        ref = x[rows].float() @ w.float().t()
+        r[tname] = float(((out[rows].float() - ref).norm() / ref.norm()).item())
     print(json.dumps(r), flush=True)
     res.append(r)

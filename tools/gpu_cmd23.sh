@@ -1,0 +1,7 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+GEMM_SHAPES=ksweep timeout -k 10 300 python tools/gemm_bench.py > gpurun_out/gemm_probe.log 2>&1; echo rc=$?
+grep "^{" gpurun_out/gemm_probe.log
+exit 0
