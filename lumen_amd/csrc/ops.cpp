@@ -19,6 +19,8 @@
 namespace lumen {
 hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
                      int64_t ldc, int M, int N, int K, const GemmEpi& ep, int tile, hipStream_t stream);
+hipError_t gemm_w8(const uint16_t* A, int64_t lda, const uint8_t* W, int64_t ldw, const float* scale, void* C,
+                   int64_t ldc, int M, int N, int K, const GemmEpi& ep, float* ws, int ksplit, hipStream_t stream);
 hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
                        int N, int K, const GemmEpi& ep, float* ws, int ksplit, hipStream_t stream);
 int skinny_ksplit(int N, int K);
@@ -136,6 +138,49 @@ void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tens
   }
   LUMEN_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
                                    (int)M, (int)N, (int)K, ep, (int)tile, cur_stream()));
+}
+
+// ---------------------------------------------------------------- fp8 (e4m3fn) weight GEMM
+// out = epi((a @ w8^T) * scale[n]): bias -> act | SwiGLU -> + residual.  w8 [N, K] float8_e4m3fn.
+void gemm_w8(const at::Tensor& a, const at::Tensor& w8, const at::Tensor& scale, const c10::optional<at::Tensor>& bias,
+             const c10::optional<at::Tensor>& residual, int64_t act, at::Tensor out, int64_t glu) {
+  check_bf16_rows(a, "a");
+  TORCH_CHECK(w8.is_cuda() && w8.scalar_type() == at::kFloat8_e4m3fn && w8.dim() == 2 && w8.stride(1) == 1 &&
+              w8.stride(0) % 16 == 0, "gemm_w8: w8 must be float8_e4m3fn [N, K] with 16-byte aligned rows");
+  const int64_t M = a.size(0), K = a.size(1), N = w8.size(0);
+  TORCH_CHECK(w8.size(1) == K && K % 64 == 0 && N % 16 == 0, "gemm_w8: K % 64 == 0, N % 16 == 0");
+  TORCH_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale.numel() == N && scale.is_contiguous(),
+              "gemm_w8: scale f32 [N]");
+  check_gpu(out, "out");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "gemm_w8: out dtype");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(0) >= M && out.size(1) >= (glu ? N / 2 : N), "gemm_w8: out");
+  TORCH_CHECK(!glu || out.scalar_type() == at::kBFloat16, "gemm_w8: glu writes bf16");
+  lumen::GemmEpi ep{};
+  ep.alpha = 1.f;
+  ep.act = (int)act;
+  ep.glu = (int)glu;
+  ep.out_f32 = out.scalar_type() == at::kFloat;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->numel() >= N && bias->is_contiguous() &&
+                (bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16), "gemm_w8: bias");
+    ep.bias = bias->data_ptr();
+    ep.bias_f32 = bias->scalar_type() == at::kFloat;
+  }
+  if (residual.has_value() && residual->defined()) {
+    check_bf16_rows(*residual, "residual");
+    ep.residual = bf(*residual);
+    ep.ldr = residual->stride(0);
+  }
+  const at::DeviceGuard guard(a.device());
+  int ks = 1;
+  at::Tensor ws;
+  if (M <= 32) {
+    ks = lumen::skinny_ksplit((int)N, (int)K);
+    if (ks > 1) ws = at::empty({ks, M, N}, a.options().dtype(at::kFloat));
+  }
+  LUMEN_CHECK_HIP(lumen::gemm_w8(bf(a), a.stride(0), reinterpret_cast<const uint8_t*>(w8.data_ptr()), w8.stride(0),
+                                 scale.data_ptr<float>(), out.data_ptr(), out.stride(0), (int)M, (int)N, (int)K, ep,
+                                 ks > 1 ? ws.data_ptr<float>() : nullptr, ks, cur_stream()));
 }
 
 // profiling: plain GEMM with per-workgroup timestamps (start, prologue, K-loop, epilogue) in dbg [wg, 4]
@@ -450,6 +495,8 @@ TORCH_LIBRARY(lumen, m) {
         "Tensor(o!) out, float eps, int mode) -> ()");
   m.def("l2norm_(Tensor(a!) x, float eps) -> ()");
   m.def("gemm_probe(Tensor a, Tensor w, Tensor(o!) out, Tensor(d!) dbg, int tile) -> ()");
+  m.def("gemm_w8(Tensor a, Tensor w8, Tensor scale, Tensor? bias, Tensor? residual, int act, Tensor(o!) out, "
+        "int glu) -> ()");
   m.def("cls_fill(Tensor(a!) x, Tensor cls, Tensor pos, int seq) -> ()");
   m.def("embed_gather(Tensor ids, Tensor table, Tensor? pos, Tensor(o!) out, int seq, int id_offset) -> ()");
   m.def("attention(Tensor q, Tensor k, Tensor v, Tensor(o!) o, Tensor? kv_len, float scale, bool causal) -> ()");
@@ -475,6 +522,7 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("norm", &norm);
   m.impl("l2norm_", &l2norm_);
   m.impl("gemm_probe", &gemm_probe);
+  m.impl("gemm_w8", &gemm_w8);
   m.impl("cls_fill", &cls_fill);
   m.impl("embed_gather", &embed_gather);
   m.impl("attention", &attention);

@@ -136,6 +136,7 @@ class LLM(nn.Module):
                                                           cfg.rope_scaling).to(device), persistent=False)
         self.H, self.Hkv = self.layers[0].H, self.layers[0].Hkv
         self.comm = None   # parallel.Communicator for the TP group (IPC one-shot all-reduce + RCCL); None = RCCL
+        self.weight_dtype = "bf16"
 
     # ------------------------------------------------------------------ weights
     @torch.no_grad()
@@ -201,6 +202,29 @@ class LLM(nn.Module):
             l.ln1.copy_(get(p + "input_layernorm.weight").to(l.ln1.dtype))
             l.ln2.copy_(get(p + "post_attention_layernorm.weight").to(l.ln2.dtype))
 
+    @torch.no_grad()
+    def quantize_fp8(self, lm_head: bool = True) -> None:
+        """Weight-only fp8: QKV / o / gate|up / down (and an untied lm_head) become OCP
+        e4m3fn with per-output-row fp32 scales (``<name>_s`` buffers).  Decode GEMMs are
+        HBM-bound on weights, so this halves the bytes per generated token; activations,
+        KV cache and accumulation stay bf16 / fp32."""
+        if self.weight_dtype == "fp8":
+            return
+        for l in self.layers:
+            for name in ("qkv", "o", "gu", "down"):
+                w8, sc = ops.quantize_fp8_rows(getattr(l, name + "_w"))
+                setattr(l, name + "_w", nn.Parameter(w8, requires_grad=False))
+                l.register_buffer(name + "_s", sc, persistent=False)
+        if lm_head and self.lm_head is not None:
+            w8, sc = ops.quantize_fp8_rows(self.lm_head)
+            self.lm_head = nn.Parameter(w8, requires_grad=False)
+            self.register_buffer("lm_head_s", sc, persistent=False)
+        self.weight_dtype = "fp8"
+
+    @staticmethod
+    def _lin(x, l, name, **kw):
+        return ops.linear(x, getattr(l, name + "_w"), w_scale=getattr(l, name + "_s", None), **kw)
+
     # ------------------------------------------------------------------ collectives
     def _all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp.enabled:
@@ -233,21 +257,21 @@ class LLM(nn.Module):
                 ops.rms_norm(x, l.ln1, eps, out=h)
             else:
                 ops.rms_norm(x, l.ln1, eps, add=self._all_reduce(pending), resid_out=x, out=h)
-            qkv = ops.linear(h, l.qkv_w, l.qkv_b)
+            qkv = self._lin(h, l, "qkv", bias=l.qkv_b)
             kc, vc = (kv.k[i], kv.v[i]) if kv is not None else (None, None)
             lops.rope_kv(qkv, pos, self.cos_sin, l.H, l.Hkv, D, slots, kc, vc)
             att = attn_fn(qkv, l, kc, vc)                            # [T, H*D]
             if tp:
-                part = ops.linear(att, l.o_w)
+                part = self._lin(att, l, "o")
                 ops.rms_norm(x, l.ln2, eps, add=self._all_reduce(part), resid_out=x, out=h)
             else:
-                ops.linear(att, l.o_w, residual=x, out=x)
+                self._lin(att, l, "o", residual=x, out=x)
                 ops.rms_norm(x, l.ln2, eps, out=h)
-            g = ops.linear(h, l.gu_w, glu=True)
+            g = self._lin(h, l, "gu", glu=True)
             if tp:
-                pending = ops.linear(g, l.down_w)
+                pending = self._lin(g, l, "down")
             else:
-                ops.linear(g, l.down_w, residual=x, out=x)
+                self._lin(g, l, "down", residual=x, out=x)
             del qkv, att, g
         if pending is not None:
             x.add_(self._all_reduce(pending))
@@ -257,7 +281,7 @@ class LLM(nn.Module):
         """final norm + lm_head of rows [B, hidden] -> local-vocab fp32 logits [B, V/tp]."""
         h = ops.rms_norm(x_rows, self.norm, self.cfg.rms_eps)
         w = self.lm_head if self.lm_head is not None else self.embed
-        return ops.linear(h, w, out_dtype=torch.float32)
+        return ops.linear(h, w, out_dtype=torch.float32, w_scale=getattr(self, "lm_head_s", None))
 
     # ------------------------------------------------------------------ forward passes
     @torch.no_grad()

@@ -77,8 +77,13 @@ def linear(
     out_row_offset: int = 0,
     tile: int = -1,
     glu: bool = False,
+    w_scale: Optional[torch.Tensor] = None,
 ) -> torch.Tensor:
     """y = epi(alpha * x @ w.T): (+bias) -> act -> (+table[m % P + off]) -> (+residual[orow]).
+
+    ``w`` may be an OCP ``torch.float8_e4m3fn`` weight with per-output-row fp32
+    ``w_scale`` [N] (weight-only fp8, :func:`quantize_fp8_rows`): the HIP kernels widen
+    it to bf16 in registers and apply the scale in the fp32 epilogue.
 
     ``x`` is [M, K] (or [..., K]), ``w`` is [N, K].  With ``out_group`` > 0 row m is
     written to ``(m // G) * GS + RO + m % G`` of ``out`` (patch rows into a token
@@ -99,6 +104,16 @@ def linear(
     else:
         ret_shape = None
     out2 = out if out.dim() == 2 else out.view(-1, out.shape[-1])
+    if w.dtype == torch.float8_e4m3fn:
+        assert w_scale is not None, "fp8 weights need w_scale"
+        assert table is None and out_group == 0 and alpha == 1.0, "fp8 GEMM: bias / act / SwiGLU / residual epilogues"
+        if x.is_cuda:
+            if x2.stride(-1) != 1 or x2.stride(0) % 8 != 0:
+                x2 = x2.contiguous()
+            res2 = residual.reshape(-1, residual.shape[-1]) if residual is not None else None
+            hip_ops().gemm_w8(x2, w, w_scale, bias, res2, a, out2, int(bool(glu)))
+            return out.view(ret_shape) if ret_shape is not None else out
+        w = w.float() * w_scale.float()[:, None]
     if x.is_cuda:
         if x2.stride(-1) != 1 or x2.stride(0) % 8 != 0:
             x2 = x2.contiguous()
@@ -125,6 +140,16 @@ def linear(
     if ret_shape is not None:
         return out.view(ret_shape)
     return out
+
+
+FP8_E4M3_MAX = 448.0
+
+
+def quantize_fp8_rows(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """[N, K] weight -> (OCP e4m3fn [N, K], fp32 per-row scale [N]) with w ~= w8 * scale[:, None]."""
+    wf = w.float()
+    s = (wf.abs().amax(dim=1) / FP8_E4M3_MAX).clamp_min(1e-12)
+    return (wf / s[:, None]).clamp(-FP8_E4M3_MAX, FP8_E4M3_MAX).to(torch.float8_e4m3fn), s.contiguous()
 
 
 def glu_interleave(w_gate: torch.Tensor, w_up: torch.Tensor) -> torch.Tensor:

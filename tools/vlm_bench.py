@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--prompt-tokens", type=int, default=48)
     ap.add_argument("--kv-blocks", type=int, default=4096)
+    ap.add_argument("--fp8", action="store_true", help="weight-only OCP e4m3 decoder weights (per-channel scales)")
     args = ap.parse_args()
     load_hip(required=True)
     dev = torch.device("cuda")
@@ -45,6 +46,8 @@ def main():
     t0 = time.time()
     m = VLM(cfg, device=dev)
     m.random_init(0)
+    if args.fp8:
+        m.llm.quantize_fp8()
     torch.cuda.synchronize()
     load_s = time.time() - t0
     kv = PagedKVCache(cfg.llm.num_layers, m.llm.Hkv, cfg.llm.head_dim, num_blocks=args.kv_blocks, device=dev)
@@ -92,7 +95,7 @@ def main():
            "min_ttft_ms": float(np.min(ttft)), "decode_tok_s_single": float(np.median(tps)) if tps else None,
            "batch": args.batch, "batch_tok_s": ntok / batch_s, "prompt_tokens": len(full),
            "image_tokens": cfg.num_image_tokens, "max_new_tokens": args.max_new, "n": args.n,
-           "preset": args.preset, "dtype": "bf16", "data": "synthetic (random-init weights, random 1024x768 JPEG)",
+           "preset": args.preset, "dtype": "bf16" if not args.fp8 else "bf16 activations / fp8-e4m3 decoder weights", "data": "synthetic (random-init weights, random 1024x768 JPEG)",
            "load_s": load_s, "kv_cache_tokens": kv.capacity_tokens}
     print(json.dumps(out))
 
