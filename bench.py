@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--model", default="ViT-L-14")
     ap.add_argument("--src-size", type=int, default=256, help="synthetic decoded image side")
     ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
+    ap.add_argument("--text-steps", type=int, default=None,
+                    help="text-tower steps timed separately for the texts/s side metric (default = --steps; 0 = skip)")
     args = ap.parse_args()
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -50,7 +52,8 @@ def main():
     comm = Communicator(st.dp_group, dev, ipc=False)                      # DP result gather over RCCL
 
     cfg = PRESETS[args.model]
-    model = CLIPModel.random(cfg, seed=0, device=dev, with_text=False)
+    text_steps = args.steps if args.text_steps is None else args.text_steps
+    model = CLIPModel.random(cfg, seed=0, device=dev, with_text=text_steps > 0)
     B = args.batch
     g = torch.Generator().manual_seed(1234 + rank)
     host = torch.randint(0, 256, (B, args.src_size, args.src_size, 3), generator=g, dtype=torch.uint8).pin_memory()
@@ -103,6 +106,26 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     ok = bool(torch.isfinite(gathered).all().item())
+    # side metric (BASELINE config 2 "image + text embed"): text tower on a batch of B
+    # 77-token prompts, timed separately AFTER the headline window (never inside it)
+    text_per_s = None
+    if text_steps > 0:
+        ids = torch.randint(1, cfg.text.vocab_size - 1, (B, cfg.text.context_length), generator=g).to(dev)
+        ids[:, -1] = cfg.text.vocab_size - 1          # EOT = max id (argmax pooling)
+        for _ in range(2):
+            model.encode_text_ids(ids)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(text_steps):
+            temb = model.encode_text_ids(ids)
+        torch.cuda.synchronize()
+        tt = torch.tensor([time.perf_counter() - t1], device=dev, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        text_per_s = world * B * text_steps / float(tt.item())
+        ok = ok and bool(torch.isfinite(temb).all().item())
     if rank == 0:
         ms = dt / args.steps * 1e3
         total = world * B * args.steps / dt
@@ -135,6 +158,9 @@ def main():
                 "includes": "H2D (double-buffered, overlapped) + resize/normalise/patchify + tower + L2 + all-gather",
             },
             "tflops_per_gpu": round(flops_img * total / world / 1e12, 1),
+            "texts_per_s": round(text_per_s, 1) if text_per_s else None,
+            "text_config": {"context_length": cfg.text.context_length, "batch_per_gpu": B,
+                            "timed": "separately, after the image window"} if text_per_s else None,
             "finite": ok,
         }
         print(json.dumps(out), flush=True)

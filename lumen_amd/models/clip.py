@@ -53,6 +53,22 @@ class TextConfig:
 
 
 @dataclass
+class BertConfig:
+    """Chinese-CLIP text tower (BERT / RoBERTa-wwm-ext, post-LN, CLS pooling)."""
+    vocab_size: int = 21128
+    width: int = 768
+    layers: int = 12
+    heads: int = 12
+    intermediate: int = 3072
+    max_position: int = 512
+    type_vocab: int = 2
+    ln_eps: float = 1e-12
+    act: str = "gelu"
+    context_length: int = 52
+    pad_token_id: int = 0
+
+
+@dataclass
 class CLIPConfig:
     embed_dim: int = 768
     vision: VisionConfig = field(default_factory=VisionConfig)
@@ -60,19 +76,27 @@ class CLIPConfig:
     image_mean: tuple = (0.48145466, 0.4578275, 0.40821073)
     image_std: tuple = (0.26862954, 0.26130258, 0.27577711)
     logit_scale: float = math.log(100.0)
+    text_arch: str = "openai"                 # "openai" causal EOT-pooled | "bert" (Chinese-CLIP)
+    bert: Optional[BertConfig] = None
 
     def to_dict(self):
         return asdict(self)
+
+    @property
+    def context_length(self) -> int:
+        return self.bert.context_length if self.text_arch == "bert" else self.text.context_length
 
     @staticmethod
     def from_dict(d: dict) -> "CLIPConfig":
         v = VisionConfig(**d.get("vision", {}))
         t = TextConfig(**d.get("text", {}))
-        rest = {k: d[k] for k in ("embed_dim", "image_mean", "image_std", "logit_scale") if k in d}
+        rest = {k: d[k] for k in ("embed_dim", "image_mean", "image_std", "logit_scale", "text_arch") if k in d}
         if "image_mean" in rest:
             rest["image_mean"] = tuple(rest["image_mean"])
         if "image_std" in rest:
             rest["image_std"] = tuple(rest["image_std"])
+        if d.get("bert"):
+            rest["bert"] = BertConfig(**d["bert"])
         return CLIPConfig(vision=v, text=t, **rest)
 
 
@@ -90,6 +114,21 @@ PRESETS = {
         text=TextConfig(width=512, layers=12, heads=8),
     ),
     "ViT-L-14-336": CLIPConfig(vision=VisionConfig(image_size=336)),
+    # Chinese-CLIP (reference default general CLIP: CN-CLIP_ViT-B-16 / CN-CLIP_ViT-L-14),
+    # RoBERTa-wwm-ext-base-chinese text tower, 52-token context, CLS pooling
+    "CN-ViT-B-16": CLIPConfig(
+        embed_dim=512,
+        vision=VisionConfig(patch_size=16, width=768, layers=12, heads=12),
+        text_arch="bert", bert=BertConfig(),
+    ),
+    "CN-ViT-L-14": CLIPConfig(text_arch="bert", bert=BertConfig()),
+    "cn-tiny": CLIPConfig(
+        embed_dim=64,
+        vision=VisionConfig(image_size=32, patch_size=8, width=64, layers=2, heads=2),
+        text=TextConfig(context_length=16, vocab_size=512, width=64, layers=2, heads=2),
+        text_arch="bert", bert=BertConfig(vocab_size=512, width=64, layers=2, heads=2, intermediate=128,
+                                          max_position=64, context_length=16),
+    ),
     # tiny geometry used by CPU tests and synthetic model directories
     "tiny": CLIPConfig(
         embed_dim=64,
@@ -282,12 +321,97 @@ class TextTower(nn.Module):
         return ops.l2_normalize_(emb)
 
 
+class _BertBlock(nn.Module):
+    def __init__(self, c: BertConfig, dtype, device):
+        super().__init__()
+        kw = dict(dtype=dtype, device=device)
+        W, I = c.width, c.intermediate
+        self.qkv_w = nn.Parameter(torch.empty(3 * W, W, **kw), requires_grad=False)
+        self.qkv_b = nn.Parameter(torch.zeros(3 * W, **kw), requires_grad=False)
+        self.out_w = nn.Parameter(torch.empty(W, W, **kw), requires_grad=False)
+        self.out_b = nn.Parameter(torch.zeros(W, **kw), requires_grad=False)
+        self.ln1_w = nn.Parameter(torch.ones(W, **kw), requires_grad=False)
+        self.ln1_b = nn.Parameter(torch.zeros(W, **kw), requires_grad=False)
+        self.fc1_w = nn.Parameter(torch.empty(I, W, **kw), requires_grad=False)
+        self.fc1_b = nn.Parameter(torch.zeros(I, **kw), requires_grad=False)
+        self.fc2_w = nn.Parameter(torch.empty(W, I, **kw), requires_grad=False)
+        self.fc2_b = nn.Parameter(torch.zeros(W, **kw), requires_grad=False)
+        self.ln2_w = nn.Parameter(torch.ones(W, **kw), requires_grad=False)
+        self.ln2_b = nn.Parameter(torch.zeros(W, **kw), requires_grad=False)
+
+
+class BertTextTower(nn.Module):
+    """Chinese-CLIP text encoder: BERT embeddings (word + position + token-type 0, LN),
+    post-LN blocks, [CLS] hidden state -> text_projection -> L2 normalise.
+
+    Reference: the CN-CLIP ``text.*.onnx`` graphs / ``ChineseCLIPModel`` manual CLS pooling
+    (packages/lumen-clip/src/lumen_clip/backends/torch_backend.py:340-393).  Per block on
+    the GPU: QKV GEMM -> padded attention (per-sequence key length = non-pad tokens) ->
+    out-proj GEMM with the residual fused -> LayerNorm -> fc1 GEMM + GELU -> fc2 GEMM with
+    the residual fused -> LayerNorm.  Token type 0 is folded into the position table."""
+
+    def __init__(self, cfg: BertConfig, embed_dim: int, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.cfg = cfg
+        self.embed_dim = embed_dim
+        kw = dict(dtype=dtype, device=device)
+        W = cfg.width
+        self.token_emb = nn.Parameter(torch.zeros(cfg.vocab_size, W, **kw), requires_grad=False)
+        self.pos_emb = nn.Parameter(torch.zeros(cfg.max_position, W, **kw), requires_grad=False)  # + type[0]
+        self.emb_ln_w = nn.Parameter(torch.ones(W, **kw), requires_grad=False)
+        self.emb_ln_b = nn.Parameter(torch.zeros(W, **kw), requires_grad=False)
+        self.blocks = nn.ModuleList([_BertBlock(cfg, dtype, device) for _ in range(cfg.layers)])
+        self.proj_w = nn.Parameter(torch.zeros(embed_dim, W, **kw), requires_grad=False)
+
+    def random_init(self, gen: torch.Generator):
+        W, I = self.cfg.width, self.cfg.intermediate
+        self.token_emb.data.copy_(torch.randn(self.token_emb.shape, generator=gen) * 0.02)
+        self.pos_emb.data.copy_(torch.randn(self.pos_emb.shape, generator=gen) * 0.02)
+        for b in self.blocks:
+            for p, fan in ((b.qkv_w, W), (b.out_w, W), (b.fc1_w, W), (b.fc2_w, I)):
+                p.data.copy_(torch.randn(p.shape, generator=gen) * fan ** -0.5)
+        self.proj_w.data.copy_(torch.randn(self.embed_dim, W, generator=gen) * W ** -0.5)
+
+    @torch.no_grad()
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        """ids [B, ctx] int64 (right-padded with pad_token_id) -> L2-normalised fp32 [B, E]."""
+        c = self.cfg
+        B, S = ids.shape
+        dev = self.token_emb.device
+        ids = ids.to(dev)
+        W, Hh = c.width, c.heads
+        D = W // Hh
+        kv_len = (ids != c.pad_token_id).sum(dim=1).clamp_min(1).to(torch.int32)
+        x = ops.embed(ids, self.token_emb, self.pos_emb[:S]).view(B * S, W)
+        ops.layer_norm(x, self.emb_ln_w, self.emb_ln_b, c.ln_eps, out=x)
+        o = torch.empty_like(x)
+        for blk in self.blocks:
+            qkv = ops.linear(x, blk.qkv_w, blk.qkv_b)
+            q5 = qkv.view(B, S, 3, Hh, D)
+            ops.attention(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], kv_len=kv_len, out=o.view(B, S, Hh, D))
+            del qkv, q5
+            ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x)          # x + attn
+            ops.layer_norm(x, blk.ln1_w, blk.ln1_b, c.ln_eps, out=x)        # post-LN
+            f = ops.linear(x, blk.fc1_w, blk.fc1_b, act=c.act)
+            ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x)
+            ops.layer_norm(x, blk.ln2_w, blk.ln2_b, c.ln_eps, out=x)
+            del f
+        cls = x.view(B, S, W)[:, 0]
+        emb = ops.linear(cls.contiguous(), self.proj_w, out_dtype=torch.float32)
+        return ops.l2_normalize_(emb)
+
+
 class CLIPModel(nn.Module):
     def __init__(self, cfg: CLIPConfig, dtype=torch.bfloat16, device=None, with_text: bool = True):
         super().__init__()
         self.cfg = cfg
         self.visual = VisionTower(cfg.vision, cfg.embed_dim, dtype, device)
-        self.text = TextTower(cfg.text, cfg.embed_dim, dtype, device) if with_text else None
+        if not with_text:
+            self.text = None
+        elif cfg.text_arch == "bert":
+            self.text = BertTextTower(cfg.bert, cfg.embed_dim, dtype, device)
+        else:
+            self.text = TextTower(cfg.text, cfg.embed_dim, dtype, device)
         self.logit_scale = cfg.logit_scale
 
     @staticmethod
@@ -315,7 +439,10 @@ class CLIPModel(nn.Module):
 
     # ---- weight ingestion
     def load_state_dict_any(self, sd: dict) -> None:
-        """Load OpenCLIP / OpenAI (``visual.*``) or HF ``CLIPModel`` naming."""
+        """Load OpenCLIP / OpenAI (``visual.*``), HF ``CLIPModel`` or HF ``ChineseCLIPModel`` naming."""
+        if self.cfg.text_arch == "bert" and any(k.startswith("text_model.encoder.layer.") for k in sd):
+            _load_bert_text(self.text, sd) if self.text is not None else None
+            sd = {k: v for k, v in sd.items() if not k.startswith("text_model.") and k != "text_projection.weight"}
         if any(k.startswith("vision_model.") for k in sd):
             sd = _hf_to_openclip(sd, self.cfg)
         _load_openclip(self, sd)
@@ -390,6 +517,67 @@ def export_openclip_state_dict(m: CLIPModel) -> dict:
         blocks(t.blocks, "transformer")
         sd["ln_final.weight"], sd["ln_final.bias"] = t.ln_final_w, t.ln_final_b
         sd["text_projection"] = t.proj_w.t()
+    sd["logit_scale"] = torch.tensor(m.logit_scale)
+    return {k: val.detach().contiguous().cpu() for k, val in sd.items()}
+
+
+def _load_bert_text(t: BertTextTower, sd: dict) -> None:
+    """HF ChineseCLIP / BERT text weights (``text_model.*`` + ``text_projection.weight``)."""
+    p = "text_model."
+    _cp(t.token_emb, sd[p + "embeddings.word_embeddings.weight"])
+    pos = sd[p + "embeddings.position_embeddings.weight"].float() + sd[p + "embeddings.token_type_embeddings.weight"][0].float()
+    _cp(t.pos_emb, pos)
+    _cp(t.emb_ln_w, sd[p + "embeddings.LayerNorm.weight"]); _cp(t.emb_ln_b, sd[p + "embeddings.LayerNorm.bias"])
+    for i, b in enumerate(t.blocks):
+        q = f"{p}encoder.layer.{i}."
+        a = q + "attention.self."
+        _cp(b.qkv_w, torch.cat([sd[a + x + ".weight"] for x in ("query", "key", "value")]))
+        _cp(b.qkv_b, torch.cat([sd[a + x + ".bias"] for x in ("query", "key", "value")]))
+        _cp(b.out_w, sd[q + "attention.output.dense.weight"]); _cp(b.out_b, sd[q + "attention.output.dense.bias"])
+        _cp(b.ln1_w, sd[q + "attention.output.LayerNorm.weight"]); _cp(b.ln1_b, sd[q + "attention.output.LayerNorm.bias"])
+        _cp(b.fc1_w, sd[q + "intermediate.dense.weight"]); _cp(b.fc1_b, sd[q + "intermediate.dense.bias"])
+        _cp(b.fc2_w, sd[q + "output.dense.weight"]); _cp(b.fc2_b, sd[q + "output.dense.bias"])
+        _cp(b.ln2_w, sd[q + "output.LayerNorm.weight"]); _cp(b.ln2_b, sd[q + "output.LayerNorm.bias"])
+    _cp(t.proj_w, sd["text_projection.weight"])
+
+
+def export_chinese_clip_state_dict(m: "CLIPModel") -> dict:
+    """HF ``ChineseCLIPModel`` naming (synthetic CN-CLIP model directories)."""
+    sd = {}
+    v = m.visual
+    W, p = v.cfg.width, v.cfg.patch_size
+    vm = "vision_model."
+    sd[vm + "embeddings.patch_embedding.weight"] = v.patch_w[:, : v.kdim].reshape(W, 3, p, p)
+    sd[vm + "embeddings.class_embedding"] = v.class_emb
+    sd[vm + "embeddings.position_embedding.weight"] = v.pos_emb
+    sd[vm + "pre_layrnorm.weight"], sd[vm + "pre_layrnorm.bias"] = v.ln_pre_w, v.ln_pre_b
+    sd[vm + "post_layernorm.weight"], sd[vm + "post_layernorm.bias"] = v.ln_post_w, v.ln_post_b
+    sd["visual_projection.weight"] = v.proj_w
+    for i, b in enumerate(v.blocks):
+        q = f"{vm}encoder.layers.{i}."
+        for x, (w_, b_) in zip("qkv", zip(torch.chunk(b.qkv_w, 3), torch.chunk(b.qkv_b, 3))):
+            sd[q + f"self_attn.{x}_proj.weight"], sd[q + f"self_attn.{x}_proj.bias"] = w_, b_
+        sd[q + "self_attn.out_proj.weight"], sd[q + "self_attn.out_proj.bias"] = b.out_w, b.out_b
+        sd[q + "layer_norm1.weight"], sd[q + "layer_norm1.bias"] = b.ln1_w, b.ln1_b
+        sd[q + "layer_norm2.weight"], sd[q + "layer_norm2.bias"] = b.ln2_w, b.ln2_b
+        sd[q + "mlp.fc1.weight"], sd[q + "mlp.fc1.bias"] = b.fc1_w, b.fc1_b
+        sd[q + "mlp.fc2.weight"], sd[q + "mlp.fc2.bias"] = b.fc2_w, b.fc2_b
+    t = m.text
+    tp = "text_model."
+    sd[tp + "embeddings.word_embeddings.weight"] = t.token_emb
+    sd[tp + "embeddings.position_embeddings.weight"] = t.pos_emb
+    sd[tp + "embeddings.token_type_embeddings.weight"] = torch.zeros(t.cfg.type_vocab, t.cfg.width, dtype=t.pos_emb.dtype)
+    sd[tp + "embeddings.LayerNorm.weight"], sd[tp + "embeddings.LayerNorm.bias"] = t.emb_ln_w, t.emb_ln_b
+    for i, b in enumerate(t.blocks):
+        q = f"{tp}encoder.layer.{i}."
+        for x, (w_, b_) in zip(("query", "key", "value"), zip(torch.chunk(b.qkv_w, 3), torch.chunk(b.qkv_b, 3))):
+            sd[q + f"attention.self.{x}.weight"], sd[q + f"attention.self.{x}.bias"] = w_, b_
+        sd[q + "attention.output.dense.weight"], sd[q + "attention.output.dense.bias"] = b.out_w, b.out_b
+        sd[q + "attention.output.LayerNorm.weight"], sd[q + "attention.output.LayerNorm.bias"] = b.ln1_w, b.ln1_b
+        sd[q + "intermediate.dense.weight"], sd[q + "intermediate.dense.bias"] = b.fc1_w, b.fc1_b
+        sd[q + "output.dense.weight"], sd[q + "output.dense.bias"] = b.fc2_w, b.fc2_b
+        sd[q + "output.LayerNorm.weight"], sd[q + "output.LayerNorm.bias"] = b.ln2_w, b.ln2_b
+    sd["text_projection.weight"] = t.proj_w
     sd["logit_scale"] = torch.tensor(m.logit_scale)
     return {k: val.detach().contiguous().cpu() for k, val in sd.items()}
 

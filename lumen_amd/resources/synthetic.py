@@ -55,6 +55,33 @@ def write_byte_bpe_tokenizer(path: Path, bos: str = "<start_of_text>", eos: str 
     return {"vocab_size": len(vocab), "bos_id": vocab[bos], "eos_id": vocab[eos]}
 
 
+def write_wordpiece_tokenizer(path: Path, vocab_size: int) -> dict:
+    """A BERT-style WordPiece tokenizer.json for CN-CLIP (RoBERTa-wwm-ext-chinese layout):
+    [PAD]=0, [UNK], [CLS], [SEP], [MASK], printable ASCII, then CJK ideographs one per id
+    (BertNormalizer splits CJK characters individually, like the real vocab), filled up
+    to ``vocab_size`` with ``##``-continuations."""
+    from tokenizers import Tokenizer, decoders, models, normalizers, pre_tokenizers, processors
+
+    toks = ["[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]"] + [chr(c) for c in range(33, 127)]
+    cjk = 0x4E00
+    while len(toks) < vocab_size and cjk <= 0x9FFF:
+        toks.append(chr(cjk))
+        cjk += 1
+    i = 0
+    while len(toks) < vocab_size:
+        toks.append("##" + toks[5 + i % 94] + ("" if i < 94 else str(i // 94)))
+        i += 1
+    vocab = {t: j for j, t in enumerate(toks[:vocab_size])}
+    tok = Tokenizer(models.WordPiece(vocab=vocab, unk_token="[UNK]"))
+    tok.normalizer = normalizers.BertNormalizer(clean_text=True, handle_chinese_chars=True, lowercase=True)
+    tok.pre_tokenizer = pre_tokenizers.BertPreTokenizer()
+    tok.post_processor = processors.BertProcessing(("[SEP]", vocab["[SEP]"]), ("[CLS]", vocab["[CLS]"]))
+    tok.decoder = decoders.WordPiece()
+    tok.add_special_tokens(["[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]"])
+    tok.save(str(path))
+    return {"vocab_size": len(vocab), "cls_id": vocab["[CLS]"], "sep_id": vocab["[SEP]"], "pad_id": 0}
+
+
 def _save_safetensors(sd: dict, path: Path) -> None:
     from safetensors.torch import save_file
 
@@ -68,6 +95,8 @@ def _write_info(root: Path, info: dict) -> None:
 
 def clip_preset_for(name: str) -> str:
     n = name.lower()
+    if "cn-clip" in n or "chinese" in n:
+        return "cn-tiny" if "tiny" in n else ("CN-ViT-B-16" if "b-16" in n or "b16" in n else "CN-ViT-L-14")
     if "tiny" in n:
         return "tiny"
     if "b-32" in n or "b32" in n:
@@ -87,6 +116,8 @@ def write_clip_model(root: Path, name: str, preset: Optional[str] = None, datase
     cfg = PRESETS[preset]
     root.mkdir(parents=True, exist_ok=True)
     m = CLIPModel.random(cfg, seed=seed, dtype=torch.float32)
+    if cfg.text_arch == "bert":
+        return _write_cn_clip(root, name, preset, cfg, m, dataset, n_labels, seed)
     _save_safetensors({k: v.to(torch.bfloat16) if v.dim() > 0 else v for k, v in export_openclip_state_dict(m).items()},
                       root / "model.safetensors")
     (root / "lumen_clip_config.json").write_text(json.dumps(cfg.to_dict(), indent=2))
@@ -125,6 +156,54 @@ def write_clip_model(root: Path, name: str, preset: Optional[str] = None, datase
         "datasets": datasets,
         "extra_metadata": {"synthetic": True, "arch": "clip", "preset": preset, "image_size": cfg.vision.image_size,
                            "context_length": cfg.text.context_length},
+    }
+    _write_info(root, info)
+    return root
+
+
+def _write_cn_clip(root: Path, name: str, preset: str, cfg, m, dataset, n_labels: int, seed: int) -> Path:
+    """CN-CLIP in HF ``ChineseCLIPModel`` layout: config.json (model_type chinese_clip),
+    model.safetensors with ``vision_model.* / text_model.*`` names, WordPiece tokenizer.json."""
+    from ..models.clip import export_chinese_clip_state_dict
+
+    sd = export_chinese_clip_state_dict(m)
+    _save_safetensors({k: v.to(torch.bfloat16) for k, v in sd.items()}, root / "model.safetensors")
+    v, b = cfg.vision, cfg.bert
+    hf = {"model_type": "chinese_clip", "projection_dim": cfg.embed_dim, "logit_scale_init_value": 2.6592,
+          "context_length": b.context_length,
+          "text_config": {"model_type": "chinese_clip_text_model", "vocab_size": b.vocab_size, "hidden_size": b.width,
+                          "num_hidden_layers": b.layers, "num_attention_heads": b.heads,
+                          "intermediate_size": b.intermediate, "max_position_embeddings": b.max_position,
+                          "type_vocab_size": b.type_vocab, "layer_norm_eps": b.ln_eps, "pad_token_id": b.pad_token_id,
+                          "hidden_act": "gelu"},
+          "vision_config": {"model_type": "chinese_clip_vision_model", "image_size": v.image_size,
+                            "patch_size": v.patch_size, "hidden_size": v.width, "num_hidden_layers": v.layers,
+                            "num_attention_heads": v.heads, "intermediate_size": int(v.width * v.mlp_ratio),
+                            "hidden_act": v.act, "layer_norm_eps": v.ln_eps},
+          "image_mean": list(cfg.image_mean), "image_std": list(cfg.image_std)}
+    (root / "config.json").write_text(json.dumps(hf, indent=2))
+    write_wordpiece_tokenizer(root / "tokenizer.json", b.vocab_size)
+    files = ["model.safetensors", "config.json", "tokenizer.json"]
+    datasets = None
+    if dataset:
+        rng = np.random.default_rng(seed + 1)
+        (root / "datasets").mkdir(exist_ok=True)
+        emb = rng.standard_normal((n_labels, cfg.embed_dim)).astype(np.float32)
+        emb /= np.linalg.norm(emb, axis=1, keepdims=True)
+        lab_rel, emb_rel = f"datasets/{dataset}_labels.json", f"datasets/{dataset}_embeddings.npy"
+        (root / lab_rel).write_text(json.dumps([f"类别 {i}" for i in range(n_labels)], ensure_ascii=False))
+        np.save(root / emb_rel, emb)
+        datasets = {dataset: {"labels": lab_rel, "embeddings": emb_rel}}
+    info = {
+        "name": name, "version": "1.0.0",
+        "description": f"synthetic random-init {preset} Chinese-CLIP for MI355X tests",
+        "model_type": "clip", "embedding_dim": cfg.embed_dim,
+        "source": {"format": "huggingface", "repo_id": f"synthetic/{name}"},
+        "runtimes": {"torch": {"available": True, "files": files, "devices": ["cuda", "cpu"]},
+                     "onnx": {"available": True, "files": files, "devices": ["cuda", "cpu"]}},
+        "datasets": datasets,
+        "extra_metadata": {"synthetic": True, "arch": "chinese_clip", "preset": preset, "image_size": v.image_size,
+                           "context_length": b.context_length},
     }
     _write_info(root, info)
     return root

@@ -101,7 +101,7 @@ class MI355XClipBackend:
         mean, std = self.resources.get_normalization_stats()
         cfg.image_mean, cfg.image_std = tuple(mean), tuple(std)
         self.cfg = cfg
-        self.context_length = cfg.text.context_length
+        self.context_length = cfg.context_length
         if self.dp_size > 1:
             from ...parallel.worker_pool import GPUWorkerPool, default_devices
 
@@ -142,7 +142,10 @@ class MI355XClipBackend:
 
         tok = Tokenizer.from_file(str(p))
         tok.enable_truncation(max_length=self.context_length)
-        tok.enable_padding(pad_id=0, pad_token="<pad>", length=self.context_length)
+        # OpenAI BPE pads with 0 (EOT-argmax pooling ignores it); CN-CLIP's WordPiece pads with
+        # [PAD]=0 and the BERT tower masks keys past the non-pad length
+        pad = "[PAD]" if self.cfg.text_arch == "bert" else "<pad>"
+        tok.enable_padding(pad_id=0, pad_token=pad, length=self.context_length)
         self.tokenizer = tok
 
     def _ensure(self):

@@ -18,7 +18,7 @@ from typing import Any, Optional
 
 import numpy as np
 
-from ...models.clip import CLIPConfig, TextConfig, VisionConfig
+from ...models.clip import BertConfig, CLIPConfig, TextConfig, VisionConfig
 from ...resources.config import ModelConfig, Runtime
 from ...resources.exceptions import (DatasetNotFoundError, ModelInfoError, ResourceNotFoundError,
                                      RuntimeNotSupportedError)
@@ -102,6 +102,9 @@ class ModelResources:
                             act=vc.act)
             return CLIPConfig(embed_dim=int(c.get("embed_dim", 512)), vision=vc, text=tc, image_mean=tuple(mean),
                               image_std=tuple(std))
+        if "vision_config" in c and (c.get("model_type") == "chinese_clip" or
+                                     c.get("text_config", {}).get("model_type") == "chinese_clip_text_model"):
+            return _chinese_clip_config(c, mean, std)
         if "vision_config" in c:  # HF CLIPConfig
             v, t = c["vision_config"], c.get("text_config", {})
             act = "quick_gelu" if v.get("hidden_act", "quick_gelu") == "quick_gelu" else "gelu"
@@ -118,6 +121,26 @@ class ModelResources:
             return CLIPConfig(embed_dim=int(c.get("projection_dim", 512)), vision=vc, text=tc, image_mean=tuple(mean),
                               image_std=tuple(std))
         raise ModelInfoError(f"cannot infer CLIP architecture from config keys {list(c)}")
+
+
+def _chinese_clip_config(c: dict, mean, std) -> CLIPConfig:
+    """HF ``ChineseCLIPConfig`` (OFA-Sys/chinese-clip-vit-*): ViT vision tower + BERT text tower."""
+    v, t = c["vision_config"], c.get("text_config", {})
+    vw = int(v.get("hidden_size", 768))
+    vc = VisionConfig(image_size=int(v.get("image_size", 224)), patch_size=int(v.get("patch_size", 16)), width=vw,
+                      layers=int(v.get("num_hidden_layers", 12)), heads=int(v.get("num_attention_heads", 12)),
+                      mlp_ratio=float(v.get("intermediate_size", 4 * vw)) / vw,
+                      act="quick_gelu" if v.get("hidden_act", "quick_gelu") == "quick_gelu" else "gelu",
+                      ln_eps=float(v.get("layer_norm_eps", 1e-5)))
+    bc = BertConfig(vocab_size=int(t.get("vocab_size", 21128)), width=int(t.get("hidden_size", 768)),
+                    layers=int(t.get("num_hidden_layers", 12)), heads=int(t.get("num_attention_heads", 12)),
+                    intermediate=int(t.get("intermediate_size", 3072)),
+                    max_position=int(t.get("max_position_embeddings", 512)),
+                    type_vocab=int(t.get("type_vocab_size", 2)), ln_eps=float(t.get("layer_norm_eps", 1e-12)),
+                    context_length=int(c.get("context_length", t.get("context_length", 52))),
+                    pad_token_id=int(t.get("pad_token_id", 0)))
+    return CLIPConfig(embed_dim=int(c.get("projection_dim", 512)), vision=vc, image_mean=tuple(mean),
+                      image_std=tuple(std), text_arch="bert", bert=bc)
 
 
 def _load_json(p: Path) -> dict:

@@ -271,6 +271,9 @@ class MI355XVLMBackend:
         else:
             raise ResourceNotFoundError(f"{self.resources.model_name}: model.safetensors missing")
         self.model = m.eval()
+        if (self.resources.precision or "").lower() in ("fp8", "e4m3", "fp8_e4m3") or \
+                os.environ.get("LUMEN_VLM_FP8", "0") == "1":
+            self.model.llm.quantize_fp8()   # weight-only OCP e4m3 decoder (config precision "fp8")
         if self.tp.enabled:
             from ...parallel.comm import Communicator
 
@@ -476,7 +479,8 @@ class MI355XVLMBackend:
         return BackendInfo(runtime=runtime_name(dev) if dev is not None else "mi355x-hip",
                            device=str(dev or self._device_preference), model_id=self.resources.model_info.name,
                            model_name=self.resources.model_info.name, version=self.resources.model_info.version,
-                           precisions=["bf16"] if dev is None or dev.type == "cuda" else ["fp32"],
+                           precisions=(["bf16", "fp8"] if self.model is not None and self.model.llm.weight_dtype == "fp8"
+                                       else ["bf16"]) if dev is None or dev.type == "cuda" else ["fp32"],
                            max_new_tokens=self._max_new_tokens or DEFAULT_MAX_NEW_TOKENS,
                            max_context_length=gc.max_position_embeddings, vision_image_size=vc.image_size,
                            vision_patch_size=vc.patch_size, vocab_size=gc.vocab_size,

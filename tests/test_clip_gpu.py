@@ -34,3 +34,23 @@ def test_vit_l14_batch_runs():
     # batch invariance: an image's embedding does not depend on its batch mates
     e1 = m.encode_image_uint8(imgs[:1])
     assert (e1[0] * e[0]).sum().item() > 0.999
+
+
+@pytest.mark.parametrize("preset", ["cn-tiny", "CN-ViT-B-16"])
+def test_cn_clip_bert_text_gpu_matches_cpu(preset):
+    """Chinese-CLIP BERT text tower (post-LN, padded key lengths, CLS pooling) on the HIP
+    kernels vs the CPU fp32 path; right-padded rows of different lengths in one batch."""
+    m_cpu = CLIPModel.random(preset, seed=5, dtype=torch.float32)
+    m_gpu = CLIPModel.random(preset, seed=5, dtype=torch.bfloat16, device="cuda")
+    c = m_cpu.cfg.bert
+    ids = torch.randint(5, c.vocab_size, (5, c.context_length), generator=torch.Generator().manual_seed(0))
+    ids[:, 0] = 2
+    for i, n in enumerate([c.context_length, 3, 7, 1, c.context_length // 2]):
+        ids[i, n:] = 0
+    t_ref = m_cpu.encode_text_ids(ids)
+    t = m_gpu.encode_text_ids(ids.cuda()).float().cpu()
+    cos = (t * t_ref).sum(-1)
+    assert cos.min().item() > 0.995, cos
+    # a row's embedding is independent of its batch mates' lengths
+    t1 = m_gpu.encode_text_ids(ids[1:2].cuda()).float().cpu()
+    assert (t1[0] * t[1]).sum().item() > 0.999
