@@ -73,8 +73,20 @@ def _needs(obj: Path, src: Path, deps: list[Path]) -> bool:
 def _run(cmd: list[str]) -> None:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
+        # hipcc can leave a fresh-looking object behind when the device pass fails, which
+        # the mtime check would then take as up to date: remove it
+        if "-o" in cmd:
+            Path(cmd[cmd.index("-o") + 1]).unlink(missing_ok=True)
         sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
         raise RuntimeError(f"compile failed: {cmd[-1] if cmd else ''}")
+
+
+# Per-source extra flags.  attention.hip: MFMA accumulators in VGPRs — the online softmax
+# rescales O and reads S with VALU ops, and with AGPR accumulators hipcc shuttles all of
+# them through v_accvgpr_read/write every 64-key chunk (~40 extra VALU ops per chunk).
+PER_FILE_FLAGS = {
+    "attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
+}
 
 
 def build(verbose: bool = False, jobs: int | None = None) -> dict:
@@ -93,7 +105,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> dict:
         objs.append(o)
         if _needs(o, s, headers):
             lang = ["-x", "hip"] if s.suffix == ".hip" else ["-x", "hip"]
-            todo.append([HIPCC, *flags, *lang, "-c", str(s), "-o", str(o)])
+            todo.append([HIPCC, *flags, *PER_FILE_FLAGS.get(s.name, []), *lang, "-c", str(s), "-o", str(o)])
     with cf.ThreadPoolExecutor(jobs) as ex:
         list(ex.map(_run, todo))
     if todo or not HIP_SO.exists() or any(o.stat().st_mtime > HIP_SO.stat().st_mtime for o in objs):

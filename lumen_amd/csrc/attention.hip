@@ -61,6 +61,61 @@ __device__ __forceinline__ s16x4v ds_read_tr16(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(p));
 }
 
+// ----------------------------------------------------------------------------------------------
+// Online-softmax step on one 64-key chunk of S^T (lane: query col, keys kb16*16 + 4g + r).
+// VALU per score is what bounds D = 64 attention (0.25 MFMA cycles vs ~1 VALU cycle per
+// score), so per score this costs one max (max3-fused) on the RAW score, one FMA folding
+// the softmax scale and the max subtraction, one bare v_exp_f32 (exp2f adds a denormal
+// range fix-up: cmp/cndmask/ldexp) and half a cvt_pk.  The row sum comes from an MFMA
+// against a ones fragment in the PV loop (l4), and O / l4 are only rescaled when some
+// lane's max grew by more than 8 in log2 units (lazy rescale: p <= 256 is exact enough in
+// fp32 accumulators and bf16 P).
+// ----------------------------------------------------------------------------------------------
+template <int NB>
+__device__ __forceinline__ void softmax_chunk(f32x4_t (&sc)[4], f32x4_t (&o)[NB], f32x4_t& l4, float& mrow,
+                                              const AttnArgs& a, bool need_mask, int k0, int g, int qi,
+                                              int kv_len, int causal_off) {
+  float mx = -INFINITY;
+  if (need_mask) {
+#pragma unroll
+    for (int kb16 = 0; kb16 < 4; ++kb16)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kj = k0 + kb16 * 16 + g * 4 + r;
+        bool ok = kj < kv_len;
+        if (a.causal) ok = ok && (kj <= qi + causal_off);
+        const float sv = ok ? sc[kb16][r] : -INFINITY;
+        sc[kb16][r] = sv;
+        mx = fmaxf(mx, sv);
+      }
+  } else {
+#pragma unroll
+    for (int kb16 = 0; kb16 < 4; ++kb16)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sc[kb16][r]);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const float mcand = fmaxf(mrow, mx * a.scale_log2);          // scale > 0 commutes with max
+  if (__any(mcand > mrow + 8.f)) {                              // wave-uniform; first chunk: mrow = -inf
+    const float mb = mcand == -INFINITY ? 0.f : mcand;
+    const float alpha = __builtin_amdgcn_exp2f(mrow - mb);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) o[j] *= alpha;
+    l4 *= alpha;
+    mrow = mcand;
+  }
+  const float nmb = mrow == -INFINITY ? 0.f : -mrow;
+#pragma unroll
+  for (int kb16 = 0; kb16 < 4; ++kb16)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sc[kb16][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kb16][r], a.scale_log2, nmb));
+}
+
+__device__ __forceinline__ bf16x8_t ones_bf16x8() {
+  return __builtin_bit_cast(bf16x8_t, (s16x8_t){0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80});
+}
+
 template <int D>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   constexpr int NCH = D / 8;        // 16-byte chunks per row
@@ -126,7 +181,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   f32x4_t o[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) o[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  float mrow = -INFINITY, lrow = 0.f;   // stats of query q0 + col (replicated over g)
+  float mrow = -INFINITY;               // running max (scaled, log2) of query q0 + col (replicated over g)
+  f32x4_t l4 = (f32x4_t){0.f, 0.f, 0.f, 0.f};   // running row sum (all 4 entries equal)
   const int qi = q0 + col;
 
   int kend = kv_len;
@@ -149,73 +205,29 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     if (!active || k0 >= wave_kend) continue;
     const char* sK = smem + buf * 2 * IMG;
     const char* sV = sK + IMG;
-    // live 16-key blocks of this chunk (wave-uniform): the ragged tail chunk
-    // (257 keys -> 1 live key) only pays for the blocks it needs
-    const int nblk = min(4, (wave_kend - k0 + 15) >> 4);
+    // all 4 key blocks always run (rows past Sk hold clamped, finite copies and are
+    // masked): branch-free chunks keep S/O in fixed VGPRs — skipping the dead blocks of
+    // the ragged tail chunk made hipcc shuffle ~30 v_mov per chunk around the branches
 
     // S^T = K Q^T : 4 key blocks of 16; lane holds keys kb*16 + 4g + r, query col
     f32x4_t sc[4];
 #pragma unroll
     for (int kb16 = 0; kb16 < 4; ++kb16) {
       sc[kb16] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-      if (kb16 < nblk) {
-        const int kr = kb16 * 16 + col;
+      const int kr = kb16 * 16 + col;
 #pragma unroll
-        for (int t = 0; t < KS; ++t) {
-          bf16x8_t kf = *(const bf16x8_t*)(sK + kr * D * 2 + (k_phys<D>(kr, t * 4 + g) << 4));
-          sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[t], sc[kb16], 0, 0, 0);
-        }
+      for (int t = 0; t < KS; ++t) {
+        bf16x8_t kf = *(const bf16x8_t*)(sK + kr * D * 2 + (k_phys<D>(kr, t * 4 + g) << 4));
+        sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[t], sc[kb16], 0, 0, 0);
       }
     }
     // mask (only on chunks that need it) + online softmax (per lane = per query)
     const bool need_mask = (k0 + KC > kv_len) || (a.causal && k0 + KC - 1 > q0 + causal_off);
-    float mx = mrow;
-    if (need_mask) {
-#pragma unroll
-      for (int kb16 = 0; kb16 < 4; ++kb16)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int kj = k0 + kb16 * 16 + g * 4 + r;
-          bool ok = kj < kv_len;
-          if (a.causal) ok = ok && (kj <= qi + causal_off);
-          const float sv = ok ? sc[kb16][r] * a.scale_log2 : -INFINITY;
-          sc[kb16][r] = sv;
-          mx = fmaxf(mx, sv);
-        }
-    } else {
-#pragma unroll
-      for (int kb16 = 0; kb16 < 4; ++kb16)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float sv = sc[kb16][r] * a.scale_log2;
-          sc[kb16][r] = sv;
-          mx = fmaxf(mx, sv);
-        }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mbase = mx == -INFINITY ? 0.f : mx;
-    const float alpha = exp2f(mrow - mbase);
-    float rs = 0.f;
-#pragma unroll
-    for (int kb16 = 0; kb16 < 4; ++kb16)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(sc[kb16][r] - mbase);
-        sc[kb16][r] = p;
-        rs += p;
-      }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    lrow = lrow * alpha + rs;
-    mrow = mx;
-#pragma unroll
-    for (int j = 0; j < NB; ++j) o[j] *= alpha;
+    softmax_chunk<NB>(sc, o, l4, mrow, a, need_mask, k0, g, qi, kv_len, causal_off);
 
     // O^T += V^T P^T over two 32-key steps
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      if (2 * s >= nblk) break;
       bf16x8_t pf;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -235,12 +247,13 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
         s16x8_t vv = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, vv), pf, o[j], 0, 0, 0);
       }
+      l4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones_bf16x8(), pf, l4, 0, 0, 0);   // row sums of P
     }
   }
 
   // ---- normalise and store O[b, q, h, d]: lane holds d = 16j + 4g + r for query col
   if (qi < a.Sq) {
-    const float inv = lrow > 0.f ? 1.0f / lrow : 0.f;
+    const float inv = l4[0] > 0.f ? __builtin_amdgcn_rcpf(l4[0]) : 0.f;
     uint16_t* orow = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qi * a.o_ss;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -282,7 +295,19 @@ __global__ void __launch_bounds__(256) attn_res_kernel(AttnArgs a, int nkc) {
   const uint16_t* qb = a.q + b * a.q_sb + h * a.q_sh;
   const uint16_t* kb = a.k + b * a.k_sb + hk * a.k_sh;
   const uint16_t* vb = a.v + b * a.v_sb + hk * a.v_sh;
+  const __amdgpu_buffer_rsrc_t o_rs = __builtin_amdgcn_make_buffer_rsrc(
+      a.o + b * a.o_sb + h * a.o_sh, (short)0, (int)(((int64_t)(a.Sq - 1) * a.o_ss + D) * 2), 0x00020000);
 
+  const int nq16 = (a.Sq + 15) / 16;
+  // Q fragments are register-prefetched one query block ahead so their HBM latency
+  // hides under the current block's chunks instead of stalling every block start.
+  bf16x8_t qn[KS];
+  auto load_q = [&](int blk) {
+    const int qr = min(blk * 16 + col, a.Sq - 1);
+#pragma unroll
+    for (int t = 0; t < KS; ++t) qn[t] = *(const bf16x8_t*)(qb + (int64_t)qr * a.q_ss + t * 32 + g * 8);
+  };
+  load_q(wid);
   // ---- stage all K/V chunks (clamped rows past Sk keep the images finite)
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   typedef const __attribute__((address_space(1))) void* g_ptr_t;
@@ -302,87 +327,40 @@ __global__ void __launch_bounds__(256) attn_res_kernel(AttnArgs a, int nkc) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  const int nq16 = (a.Sq + 15) / 16;
   for (int qbk = wid; qbk < nq16; qbk += 4) {
     const int q0 = qbk * 16;
     const int qi = q0 + col;
     bf16x8_t qf[KS];
-    {
-      const int qr = min(qi, a.Sq - 1);
 #pragma unroll
-      for (int t = 0; t < KS; ++t) qf[t] = *(const bf16x8_t*)(qb + (int64_t)qr * a.q_ss + t * 32 + g * 8);
-    }
+    for (int t = 0; t < KS; ++t) qf[t] = qn[t];
+    if (qbk + 4 < nq16) load_q(qbk + 4);
     f32x4_t o[NB];
 #pragma unroll
     for (int j = 0; j < NB; ++j) o[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    float mrow = -INFINITY, lrow = 0.f;
+    float mrow = -INFINITY;
+    f32x4_t l4 = (f32x4_t){0.f, 0.f, 0.f, 0.f};
     const int wave_kend = a.causal ? min(kv_len, min(q0 + 16, a.Sq) + causal_off) : kv_len;
     const int nc = min(nkc, (wave_kend + KC - 1) / KC);
     for (int kc = 0; kc < nc; ++kc) {
       const int k0 = kc * KC;
       const char* sK = smem + kc * 2 * IMG;
       const char* sV = sK + IMG;
-      const int nblk = min(4, (wave_kend - k0 + 15) >> 4);
       f32x4_t sc[4];
 #pragma unroll
       for (int kb16 = 0; kb16 < 4; ++kb16) {
         sc[kb16] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-        if (kb16 < nblk) {
-          const int kr = kb16 * 16 + col;
+        const int kr = kb16 * 16 + col;
 #pragma unroll
-          for (int t = 0; t < KS; ++t) {
-            bf16x8_t kf = *(const bf16x8_t*)(sK + kr * D * 2 + (k_phys<D>(kr, t * 4 + g) << 4));
-            sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[t], sc[kb16], 0, 0, 0);
-          }
+        for (int t = 0; t < KS; ++t) {
+          bf16x8_t kf = *(const bf16x8_t*)(sK + kr * D * 2 + (k_phys<D>(kr, t * 4 + g) << 4));
+          sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[t], sc[kb16], 0, 0, 0);
         }
       }
       const bool need_mask = (k0 + KC > kv_len) || (a.causal && k0 + KC - 1 > q0 + causal_off);
-      float mx = mrow;
-      if (need_mask) {
-#pragma unroll
-        for (int kb16 = 0; kb16 < 4; ++kb16)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int kj = k0 + kb16 * 16 + g * 4 + r;
-            bool ok = kj < kv_len;
-            if (a.causal) ok = ok && (kj <= qi + causal_off);
-            const float sv = ok ? sc[kb16][r] * a.scale_log2 : -INFINITY;
-            sc[kb16][r] = sv;
-            mx = fmaxf(mx, sv);
-          }
-      } else {
-#pragma unroll
-        for (int kb16 = 0; kb16 < 4; ++kb16)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float sv = sc[kb16][r] * a.scale_log2;
-            sc[kb16][r] = sv;
-            mx = fmaxf(mx, sv);
-          }
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mbase = mx == -INFINITY ? 0.f : mx;
-      const float alpha = exp2f(mrow - mbase);
-      float rs = 0.f;
-#pragma unroll
-      for (int kb16 = 0; kb16 < 4; ++kb16)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(sc[kb16][r] - mbase);
-          sc[kb16][r] = p;
-          rs += p;
-        }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
-      lrow = lrow * alpha + rs;
-      mrow = mx;
-#pragma unroll
-      for (int j = 0; j < NB; ++j) o[j] *= alpha;
+      softmax_chunk<NB>(sc, o, l4, mrow, a, need_mask, k0, g, qi, kv_len, causal_off);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        if (2 * s >= nblk) break;
-        bf16x8_t pf;
+          bf16x8_t pf;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           pf[r] = (__bf16)sc[2 * s][r];
@@ -400,17 +378,21 @@ __global__ void __launch_bounds__(256) attn_res_kernel(AttnArgs a, int nkc) {
           s16x8_t vv = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, vv), pf, o[j], 0, 0, 0);
         }
+        l4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones_bf16x8(), pf, l4, 0, 0, 0);   // row sums of P
       }
     }
-    if (qi < a.Sq) {
-      const float inv = lrow > 0.f ? 1.0f / lrow : 0.f;
-      uint16_t* orow = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qi * a.o_ss;
+    // Branch-free store through a per-(batch, head) buffer descriptor whose range ends at
+    // the last valid query row: lanes of the ragged last block (qi >= Sq) are dropped by
+    // the range check.  A divergent `if (qi < Sq)` store made hipcc merge its vmcnt
+    // bookkeeping conservatively and wait vmcnt(0) for the prefetched Q at every block.
+    {
+      const float inv = l4[0] > 0.f ? __builtin_amdgcn_rcpf(l4[0]) : 0.f;
+      const int row_off = qi * (int)a.o_ss * 2;
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        uint2 w;
-        w.x = pack2bf(o[j][0] * inv, o[j][1] * inv);
-        w.y = pack2bf(o[j][2] * inv, o[j][3] * inv);
-        *(uint2*)(orow + j * 16 + 4 * g) = w;
+        typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+        const u32x2v w = {pack2bf(o[j][0] * inv, o[j][1] * inv), pack2bf(o[j][2] * inv, o[j][3] * inv)};
+        __builtin_amdgcn_raw_buffer_store_b64(w, o_rs, row_off + (j * 16 + 4 * g) * 2, 0, 0);
       }
     }
   }

@@ -129,13 +129,13 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mbase = mx == -INFINITY ? 0.f : mx;
-    const float alpha = exp2f(mrow - mbase);
+    const float alpha = __builtin_amdgcn_exp2f(mrow - mbase);
     float rs = 0.f;
 #pragma unroll
     for (int kb16 = 0; kb16 < 4; ++kb16)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(sc[kb16][r] - mbase);
+        const float p = __builtin_amdgcn_exp2f(sc[kb16][r] - mbase);
         sc[kb16][r] = p;
         rs += p;
       }
@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
     if (M != -INFINITY) {
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
-        const float e = exp2f(sm_ml[w][0][q] - M);
+        const float e = __builtin_amdgcn_exp2f(sm_ml[w][0][q] - M);
         L += sm_ml[w][1][q] * e;
         O += sm_o[w][d][q] * e;
       }
@@ -213,7 +213,7 @@ __global__ void decode_combine_kernel(DecodeArgs a, int D) {
     float L = 0.f, O = 0.f;
     if (M != -INFINITY) {
       for (int s = 0; s < a.nsplit; ++s) {
-        const float e = exp2f(a.part_ml[(base + s) * 2] - M);
+        const float e = __builtin_amdgcn_exp2f(a.part_ml[(base + s) * 2] - M);
         L += a.part_ml[(base + s) * 2 + 1] * e;
         O += a.part_o[(base + s) * D + d] * e;
       }
