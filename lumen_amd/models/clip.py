@@ -25,6 +25,7 @@ import torch
 from torch import nn
 
 from .. import ops
+from .fastvit import FASTVIT_PRESETS, FastViTConfig, FastViTTower
 
 
 @dataclass
@@ -78,6 +79,8 @@ class CLIPConfig:
     logit_scale: float = math.log(100.0)
     text_arch: str = "openai"                 # "openai" causal EOT-pooled | "bert" (Chinese-CLIP)
     bert: Optional[BertConfig] = None
+    vision_arch: str = "vit"                  # "vit" | "fastvit" (MobileCLIP / MobileCLIP2 MCi towers)
+    fastvit: Optional[FastViTConfig] = None
 
     def to_dict(self):
         return asdict(self)
@@ -90,13 +93,16 @@ class CLIPConfig:
     def from_dict(d: dict) -> "CLIPConfig":
         v = VisionConfig(**d.get("vision", {}))
         t = TextConfig(**d.get("text", {}))
-        rest = {k: d[k] for k in ("embed_dim", "image_mean", "image_std", "logit_scale", "text_arch") if k in d}
+        rest = {k: d[k] for k in ("embed_dim", "image_mean", "image_std", "logit_scale", "text_arch", "vision_arch")
+                if k in d}
         if "image_mean" in rest:
             rest["image_mean"] = tuple(rest["image_mean"])
         if "image_std" in rest:
             rest["image_std"] = tuple(rest["image_std"])
         if d.get("bert"):
             rest["bert"] = BertConfig(**d["bert"])
+        if d.get("fastvit"):
+            rest["fastvit"] = FastViTConfig.from_dict(d["fastvit"])
         return CLIPConfig(vision=v, text=t, **rest)
 
 
@@ -128,6 +134,24 @@ PRESETS = {
         text=TextConfig(context_length=16, vocab_size=512, width=64, layers=2, heads=2),
         text_arch="bert", bert=BertConfig(vocab_size=512, width=64, layers=2, heads=2, intermediate=128,
                                           max_position=64, context_length=16),
+    ),
+    # MobileCLIP2 (reference default general CLIP for region "other"): MCi image towers
+    # (FastViT, reparameterised) + OpenAI-style text transformer; no pixel normalisation
+    "MobileCLIP2-S2": CLIPConfig(
+        embed_dim=512, vision_arch="fastvit", fastvit=FASTVIT_PRESETS["mci2"],
+        vision=VisionConfig(image_size=256), text=TextConfig(width=512, layers=12, heads=8, act="gelu"),
+        image_mean=(0.0, 0.0, 0.0), image_std=(1.0, 1.0, 1.0),
+    ),
+    "MobileCLIP2-S4": CLIPConfig(
+        embed_dim=768, vision_arch="fastvit", fastvit=FASTVIT_PRESETS["mci4"],
+        vision=VisionConfig(image_size=256), text=TextConfig(width=768, layers=12, heads=12, act="gelu"),
+        image_mean=(0.0, 0.0, 0.0), image_std=(1.0, 1.0, 1.0),
+    ),
+    "mobileclip-tiny": CLIPConfig(
+        embed_dim=64, vision_arch="fastvit", fastvit=FASTVIT_PRESETS["tiny"],
+        vision=VisionConfig(image_size=64, patch_size=8, width=64, layers=1, heads=2),
+        text=TextConfig(context_length=16, vocab_size=512, width=64, layers=2, heads=2, act="gelu"),
+        image_mean=(0.0, 0.0, 0.0), image_std=(1.0, 1.0, 1.0),
     ),
     # tiny geometry used by CPU tests and synthetic model directories
     "tiny": CLIPConfig(
@@ -405,7 +429,10 @@ class CLIPModel(nn.Module):
     def __init__(self, cfg: CLIPConfig, dtype=torch.bfloat16, device=None, with_text: bool = True):
         super().__init__()
         self.cfg = cfg
-        self.visual = VisionTower(cfg.vision, cfg.embed_dim, dtype, device)
+        if cfg.vision_arch == "fastvit":
+            self.visual = FastViTTower(cfg.fastvit, cfg.embed_dim, dtype, device)
+        else:
+            self.visual = VisionTower(cfg.vision, cfg.embed_dim, dtype, device)
         if not with_text:
             self.text = None
         elif cfg.text_arch == "bert":
@@ -428,6 +455,9 @@ class CLIPModel(nn.Module):
     # ---- public API (mirrors the reference backend contract: unit-norm fp32 vectors)
     @torch.no_grad()
     def encode_image_uint8(self, images) -> torch.Tensor:
+        if self.cfg.vision_arch == "fastvit":
+            x = self.visual.preprocess(images, self.cfg.image_mean, self.cfg.image_std)
+            return self.visual.forward_embed(x)
         patches = self.visual.preprocess(images, self.cfg.image_mean, self.cfg.image_std)
         B = patches.shape[0] // self.visual.num_patches
         return self.visual.forward_patches(patches, B)
@@ -445,6 +475,8 @@ class CLIPModel(nn.Module):
             sd = {k: v for k, v in sd.items() if not k.startswith("text_model.") and k != "text_projection.weight"}
         if any(k.startswith("vision_model.") for k in sd):
             sd = _hf_to_openclip(sd, self.cfg)
+        if self.cfg.vision_arch == "fastvit":     # open_clip TimmModel: visual.trunk.<timm FastVit names>
+            self.visual.load_timm(sd, prefix="visual.trunk.")
         _load_openclip(self, sd)
 
 
@@ -467,15 +499,16 @@ def _load_blocks(blocks, sd, prefix):
 
 def _load_openclip(m: CLIPModel, sd: dict) -> None:
     v = m.visual
-    conv = sd["visual.conv1.weight"]
-    v.patch_w.data.zero_()
-    v.patch_w.data[:, : v.kdim] = conv.reshape(conv.shape[0], -1).to(v.patch_w.dtype)
-    _cp(v.class_emb, sd["visual.class_embedding"])
-    _cp(v.pos_emb, sd["visual.positional_embedding"])
-    _cp(v.ln_pre_w, sd["visual.ln_pre.weight"]); _cp(v.ln_pre_b, sd["visual.ln_pre.bias"])
-    _load_blocks(v.blocks, sd, "visual.transformer")
-    _cp(v.ln_post_w, sd["visual.ln_post.weight"]); _cp(v.ln_post_b, sd["visual.ln_post.bias"])
-    _cp(v.proj_w, sd["visual.proj"].t())
+    if isinstance(v, VisionTower):
+        conv = sd["visual.conv1.weight"]
+        v.patch_w.data.zero_()
+        v.patch_w.data[:, : v.kdim] = conv.reshape(conv.shape[0], -1).to(v.patch_w.dtype)
+        _cp(v.class_emb, sd["visual.class_embedding"])
+        _cp(v.pos_emb, sd["visual.positional_embedding"])
+        _cp(v.ln_pre_w, sd["visual.ln_pre.weight"]); _cp(v.ln_pre_b, sd["visual.ln_pre.bias"])
+        _load_blocks(v.blocks, sd, "visual.transformer")
+        _cp(v.ln_post_w, sd["visual.ln_post.weight"]); _cp(v.ln_post_b, sd["visual.ln_post.bias"])
+        _cp(v.proj_w, sd["visual.proj"].t())
     if m.text is not None and "token_embedding.weight" in sd:
         t = m.text
         _cp(t.token_emb, sd["token_embedding.weight"])
@@ -491,13 +524,16 @@ def export_openclip_state_dict(m: CLIPModel) -> dict:
     """Inverse of the OpenCLIP loader (used to write synthetic model directories)."""
     sd = {}
     v = m.visual
-    W, p = v.cfg.width, v.cfg.patch_size
-    sd["visual.conv1.weight"] = v.patch_w[:, : v.kdim].reshape(W, 3, p, p)
-    sd["visual.class_embedding"] = v.class_emb
-    sd["visual.positional_embedding"] = v.pos_emb
-    sd["visual.ln_pre.weight"], sd["visual.ln_pre.bias"] = v.ln_pre_w, v.ln_pre_b
-    sd["visual.ln_post.weight"], sd["visual.ln_post.bias"] = v.ln_post_w, v.ln_post_b
-    sd["visual.proj"] = v.proj_w.t()
+    if isinstance(v, FastViTTower):
+        sd.update(v.export_timm(prefix="visual.trunk."))
+    else:
+        W, p = v.cfg.width, v.cfg.patch_size
+        sd["visual.conv1.weight"] = v.patch_w[:, : v.kdim].reshape(W, 3, p, p)
+        sd["visual.class_embedding"] = v.class_emb
+        sd["visual.positional_embedding"] = v.pos_emb
+        sd["visual.ln_pre.weight"], sd["visual.ln_pre.bias"] = v.ln_pre_w, v.ln_pre_b
+        sd["visual.ln_post.weight"], sd["visual.ln_post.bias"] = v.ln_post_w, v.ln_post_b
+        sd["visual.proj"] = v.proj_w.t()
 
     def blocks(bl, prefix):
         for i, b in enumerate(bl):
@@ -509,7 +545,8 @@ def export_openclip_state_dict(m: CLIPModel) -> dict:
             sd[q + "mlp.c_fc.weight"], sd[q + "mlp.c_fc.bias"] = b.fc1_w, b.fc1_b
             sd[q + "mlp.c_proj.weight"], sd[q + "mlp.c_proj.bias"] = b.fc2_w, b.fc2_b
 
-    blocks(v.blocks, "visual.transformer")
+    if isinstance(v, VisionTower):
+        blocks(v.blocks, "visual.transformer")
     if m.text is not None:
         t = m.text
         sd["token_embedding.weight"] = t.token_emb

@@ -6,10 +6,10 @@ prompt -> tokens; image -> pad-to-square (black, centred) + bicubic resize -> /2
 vision embeddings replace the ``<image>`` token (:240-296); prefill; decode loop.
 
 Presets:
-* ``fastvlm-0.5b``  — Qwen2-0.5B decoder with a 256-token, 1024-px image encoder.
-  FastViTHD itself (a hybrid conv/attention net) is represented by a ViT with 64-px
-  patches over the same 1024x1024 input producing the same 256 visual tokens —
-  same I/O shapes and token count, not the same layer graph (stand-in, documented).
+* ``fastvlm-0.5b``  — Qwen2-0.5B decoder with FastViTHD (models/fastvit.py: the
+  reparameterised conv/RepMixer/attention hybrid, 1024 px -> 16 x 16 x 3072 conv_exp map
+  = 256 visual tokens) -> 2-layer GELU projector (3072 -> 896).  ``cfg.vision`` keeps the
+  token geometry (image_size 1024, patch_size = the tower's stride 64).
 * ``llava-llama3-8b`` — north-star config: CLIP ViT-L/14-336 (penultimate layer,
   576 tokens, CLS dropped) -> 2-layer GELU MLP projector -> Llama-3-8B.
 * ``tiny`` — CPU tests.
@@ -29,6 +29,7 @@ from torch import nn
 
 from .. import ops
 from .clip import VisionConfig, VisionTower
+from .fastvit import FASTVIT_PRESETS, FastViTConfig, FastViTTower
 from .llm import LLM, LLM_PRESETS, LLMConfig, TPInfo
 
 
@@ -43,6 +44,12 @@ class VLMConfig:
     image_std: tuple = (1.0, 1.0, 1.0)
     pad_value: float = 0.0          # pad-to-square fill (pixel units)
     resize_filter: str = "pil_bicubic"
+    vision_arch: str = "vit"        # "vit" (LLaVA CLIP towers) | "fastvit" (FastViTHD)
+    fastvit: Optional[FastViTConfig] = None
+
+    @property
+    def vision_width(self) -> int:
+        return self.fastvit.final_features if self.vision_arch == "fastvit" else self.vision.width
 
     @property
     def num_image_tokens(self) -> int:
@@ -55,7 +62,10 @@ class VLMConfig:
     def from_dict(d: dict) -> "VLMConfig":
         v = VisionConfig(**d.get("vision", {}))
         l = LLMConfig.from_dict(d.get("llm", {}))
-        rest = {k: d[k] for k in ("feature_layer", "image_token_id", "pad_value", "resize_filter") if k in d}
+        rest = {k: d[k] for k in ("feature_layer", "image_token_id", "pad_value", "resize_filter", "vision_arch")
+                if k in d}
+        if d.get("fastvit"):
+            rest["fastvit"] = FastViTConfig.from_dict(d["fastvit"])
         for k in ("image_mean", "image_std"):
             if k in d:
                 rest[k] = tuple(d[k])
@@ -63,7 +73,8 @@ class VLMConfig:
 
 
 VLM_PRESETS = {
-    "fastvlm-0.5b": VLMConfig(),
+    "fastvlm-0.5b": VLMConfig(vision=VisionConfig(image_size=1024, patch_size=64, width=3072, layers=0, heads=1),
+                              vision_arch="fastvit", fastvit=FASTVIT_PRESETS["fastvithd"]),
     "llava-llama3-8b": VLMConfig(vision=VisionConfig(image_size=336, patch_size=14, width=1024, layers=24, heads=16,
                                                      act="quick_gelu"),
                                  llm=LLM_PRESETS["llama3-8b"], image_token_id=128002,
@@ -71,6 +82,9 @@ VLM_PRESETS = {
                                  image_std=(0.26862954, 0.26130258, 0.27577711), pad_value=116.0),
     "tiny": VLMConfig(vision=VisionConfig(image_size=32, patch_size=8, width=64, layers=2, heads=2, act="gelu"),
                       llm=LLM_PRESETS["tiny"], image_token_id=259),
+    "tiny-fastvit": VLMConfig(vision=VisionConfig(image_size=64, patch_size=16, width=128, layers=0, heads=1),
+                              vision_arch="fastvit", fastvit=FASTVIT_PRESETS["tiny-ln"], llm=LLM_PRESETS["tiny"],
+                              image_token_id=259),
 }
 
 
@@ -79,8 +93,9 @@ class VLM(nn.Module):
         super().__init__()
         self.cfg = cfg
         kw = dict(dtype=dtype, device=device)
-        self.vision = VisionTower(cfg.vision, 16, dtype, device)
-        Wv, Hd = cfg.vision.width, cfg.llm.hidden_size
+        self.vision = FastViTTower(cfg.fastvit, None, dtype, device) if cfg.vision_arch == "fastvit" \
+            else VisionTower(cfg.vision, 16, dtype, device)
+        Wv, Hd = cfg.vision_width, cfg.llm.hidden_size
         self.proj1_w = nn.Parameter(torch.zeros(Hd, Wv, **kw), requires_grad=False)
         self.proj1_b = nn.Parameter(torch.zeros(Hd, dtype=torch.float32, device=device), requires_grad=False)
         self.proj2_w = nn.Parameter(torch.zeros(Hd, Hd, **kw), requires_grad=False)
@@ -92,10 +107,11 @@ class VLM(nn.Module):
         """Vision + projector replicated on every rank (same seed); LLM shards per rank."""
         g = torch.Generator().manual_seed(seed)
         dev = self.proj1_w.device
-        vis_cpu = VisionTower(self.cfg.vision, 16, torch.float32, "cpu")
+        vis_cpu = FastViTTower(self.cfg.fastvit, None, torch.float32, "cpu") if self.cfg.vision_arch == "fastvit" \
+            else VisionTower(self.cfg.vision, 16, torch.float32, "cpu")
         vis_cpu.random_init(g)
         self.vision.load_state_dict({k: v.to(self.vision.state_dict()[k].dtype) for k, v in vis_cpu.state_dict().items()})
-        Wv, Hd = self.cfg.vision.width, self.cfg.llm.hidden_size
+        Wv, Hd = self.cfg.vision_width, self.cfg.llm.hidden_size
         self.proj1_w.copy_((torch.randn(Hd, Wv, generator=g) * Wv ** -0.5).to(self.proj1_w.dtype).to(dev))
         self.proj2_w.copy_((torch.randn(Hd, Hd, generator=g) * Hd ** -0.5).to(self.proj2_w.dtype).to(dev))
         self.llm.random_init(seed)
@@ -113,6 +129,10 @@ class VLM(nn.Module):
         for im in images:
             geoms.append(ops.ImageGeom.pad_square(im.shape[0], im.shape[1], off, s))
             off += im.numel()
+        if self.cfg.vision_arch == "fastvit":
+            return ops.image_prep(list(images), (s, s), mean=self.cfg.image_mean, std=self.cfg.image_std,
+                                  filter=self.cfg.resize_filter, layout="nhwc8", pad=self.cfg.pad_value, geoms=geoms,
+                                  out_dtype=v.stem0.w.dtype, device=self.device)
         return ops.image_prep(list(images), (s, s), mean=self.cfg.image_mean, std=self.cfg.image_std,
                               filter=self.cfg.resize_filter, layout="patches", patch=self.cfg.vision.patch_size,
                               kpad=v.kpad, pad=self.cfg.pad_value, geoms=geoms, out_dtype=v.patch_w.dtype,
@@ -122,7 +142,10 @@ class VLM(nn.Module):
     def encode_images(self, images: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """-> projected image embeddings [B * N_img, hidden] (or written into ``out`` rows)."""
         B = len(images)
-        feats = self.vision.forward_features(self.preprocess(images), B, self.cfg.feature_layer)
+        if self.cfg.vision_arch == "fastvit":     # conv_exp map [B, 16, 16, 3072]: NHWC rows = image tokens
+            feats = self.vision.forward_features(self.preprocess(images))
+        else:
+            feats = self.vision.forward_features(self.preprocess(images), B, self.cfg.feature_layer)
         f = feats.reshape(B * self.cfg.num_image_tokens, -1)
         if not f.is_contiguous():
             f = f.contiguous()

@@ -95,6 +95,8 @@ def _write_info(root: Path, info: dict) -> None:
 
 def clip_preset_for(name: str) -> str:
     n = name.lower()
+    if "mobileclip" in n:
+        return "mobileclip-tiny" if "tiny" in n else ("MobileCLIP2-S4" if "s4" in n else "MobileCLIP2-S2")
     if "cn-clip" in n or "chinese" in n:
         return "cn-tiny" if "tiny" in n else ("CN-ViT-B-16" if "b-16" in n or "b16" in n else "CN-ViT-L-14")
     if "tiny" in n:
@@ -121,9 +123,16 @@ def write_clip_model(root: Path, name: str, preset: Optional[str] = None, datase
     _save_safetensors({k: v.to(torch.bfloat16) if v.dim() > 0 else v for k, v in export_openclip_state_dict(m).items()},
                       root / "model.safetensors")
     (root / "lumen_clip_config.json").write_text(json.dumps(cfg.to_dict(), indent=2))
+    vcfg = {"image_size": cfg.vision.image_size, "patch_size": cfg.vision.patch_size,
+            "width": cfg.vision.width, "layers": cfg.vision.layers}
+    if cfg.vision_arch == "fastvit":   # open_clip TimmModel tower
+        from ..models.fastvit import FASTVIT_PRESETS
+
+        tname = next((k for k, v in FASTVIT_PRESETS.items() if v == cfg.fastvit), "custom")
+        vcfg = {"timm_model_name": f"fastvit_{tname}", "timm_pool": "avg", "timm_proj": None,
+                "image_size": cfg.fastvit.image_size}
     oc = {"embed_dim": cfg.embed_dim,
-          "vision_cfg": {"image_size": cfg.vision.image_size, "patch_size": cfg.vision.patch_size,
-                         "width": cfg.vision.width, "layers": cfg.vision.layers},
+          "vision_cfg": vcfg,
           "text_cfg": {"context_length": cfg.text.context_length, "vocab_size": cfg.text.vocab_size,
                        "width": cfg.text.width, "heads": cfg.text.heads, "layers": cfg.text.layers},
           "preprocess_cfg": {"mean": list(cfg.image_mean), "std": list(cfg.image_std)}}
@@ -154,7 +163,8 @@ def write_clip_model(root: Path, name: str, preset: Optional[str] = None, datase
         "runtimes": {"torch": {"available": True, "files": files, "devices": ["cuda", "cpu"]},
                      "onnx": {"available": True, "files": files, "devices": ["cuda", "cpu"]}},
         "datasets": datasets,
-        "extra_metadata": {"synthetic": True, "arch": "clip", "preset": preset, "image_size": cfg.vision.image_size,
+        "extra_metadata": {"synthetic": True, "arch": "clip", "preset": preset,
+                           "image_size": cfg.fastvit.image_size if cfg.vision_arch == "fastvit" else cfg.vision.image_size,
                            "context_length": cfg.text.context_length},
     }
     _write_info(root, info)

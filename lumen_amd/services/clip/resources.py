@@ -89,6 +89,8 @@ class ModelResources:
         if "vision" in c and "text" in c:  # lumen_clip_config.json
             return CLIPConfig.from_dict(c)
         mean, std = self.get_normalization_stats()
+        if "vision_cfg" in c and str(c["vision_cfg"].get("timm_model_name", "")).startswith("fastvit_"):
+            return _mobileclip_config(c, mean, std)
         if "vision_cfg" in c:  # OpenCLIP
             v, t = c["vision_cfg"], c.get("text_cfg", {})
             width = int(v.get("width", 768))
@@ -121,6 +123,24 @@ class ModelResources:
             return CLIPConfig(embed_dim=int(c.get("projection_dim", 512)), vision=vc, text=tc, image_mean=tuple(mean),
                               image_std=tuple(std))
         raise ModelInfoError(f"cannot infer CLIP architecture from config keys {list(c)}")
+
+
+def _mobileclip_config(c: dict, mean, std) -> CLIPConfig:
+    """open_clip MobileCLIP / MobileCLIP2 config: timm ``fastvit_mci*`` trunk + text transformer."""
+    import dataclasses
+
+    from ...models.fastvit import FASTVIT_PRESETS
+
+    v, t = c["vision_cfg"], c.get("text_cfg", {})
+    name = v["timm_model_name"][len("fastvit_"):]
+    if name not in FASTVIT_PRESETS:
+        raise ModelInfoError(f"unknown FastViT trunk {v['timm_model_name']}")
+    fv = dataclasses.replace(FASTVIT_PRESETS[name], image_size=int(v.get("image_size", 256)))
+    tw = int(t.get("width", 512))
+    tc = TextConfig(context_length=int(t.get("context_length", 77)), vocab_size=int(t.get("vocab_size", 49408)),
+                    width=tw, layers=int(t.get("layers", 12)), heads=int(t.get("heads", tw // 64)), act="gelu")
+    return CLIPConfig(embed_dim=int(c.get("embed_dim", 512)), vision=VisionConfig(image_size=fv.image_size),
+                      text=tc, image_mean=tuple(mean), image_std=tuple(std), vision_arch="fastvit", fastvit=fv)
 
 
 def _chinese_clip_config(c: dict, mean, std) -> CLIPConfig:

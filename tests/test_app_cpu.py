@@ -129,3 +129,39 @@ def test_server_lifecycle(client, tmp_path):
     assert r["running"] is False
     with client.websocket_connect("/ws/logs") as ws:
         assert ws.receive_json()["type"] == "connected"
+
+
+def test_spa_assets_and_api_coverage(client):
+    """The web UI (static/index.html + app.js + app.css) is served, parses, and every
+    /api/v1 path it calls is a route of the control-plane app (reference UI views:
+    lumen-app/web-ui/src/views/*.tsx, API client lib/api.ts)."""
+    import re
+    import shutil
+    import subprocess
+    from pathlib import Path
+
+    from lumen_amd.app.main import STATIC_DIR
+
+    idx = client.get("/")
+    assert idx.status_code == 200 and 'src="/app.js"' in idx.text
+    for route in ("#/open", "#/session", "#/server", "#/setup/welcome", "#/setup/hardware", "#/setup/config",
+                  "#/setup/install"):
+        assert route in idx.text
+    js = client.get("/app.js")
+    assert js.status_code == 200 and "views[\"/setup/install\"]" in js.text
+    assert client.get("/app.css").status_code == 200
+    if shutil.which("node"):
+        r = subprocess.run(["node", "--check", str(Path(STATIC_DIR) / "app.js")], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+    # every api("...") path used by the UI resolves to a registered route
+    routes = list(client.get("/openapi.json").json()["paths"])
+    pats = [re.compile("^" + re.sub(r"\{[^}]+\}", "[^/]+", p) + "$") for p in routes]
+    used = set(re.findall(r'api\(\s*[`"]([a-z][^`"?$]*)', js.text))
+    assert len(used) >= 15, used
+    for u in used:
+        full = "/api/v1/" + u.split("${")[0].rstrip("/")
+        if "${" in u:   # templated segment: compare with a placeholder id
+            full = "/api/v1/" + re.sub(r"\$\{[^}]+\}", "x", u)
+        assert any(p.match(full) for p in pats), f"UI calls {full}, no such route"
+    for ws in ("/ws/logs", "/ws/install/"):
+        assert ws in js.text
