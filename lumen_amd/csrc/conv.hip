@@ -251,9 +251,106 @@ dw_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, c
   }
 }
 
+// Register-blocked variant (dilation 1, KW in {3, 5, 7}, stride SW in {1, 2}): one thread =
+// 8 channels x PX consecutive output pixels of one row.  Per kernel row it loads the
+// (PX-1)*SW + KW input columns once into registers and slides the KW taps over them, so
+// a 7x7 stride-1 conv issues 10 instead of 28 16-byte loads per 4 outputs and reads each
+// weight row once per 4 outputs (FastViT / MobileCLIP RepMixer, ConvMlp, RepCPE and
+// PatchEmbed convs are 3x3 / 7x7 depthwise).  Channel groups are the fastest thread
+// index, so a wave reads 64 x 16 contiguous bytes of an NHWC row per load.
+template <int KW, int SW, int PX>
+__global__ void __launch_bounds__(256)
+dw_conv_rb_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, const void* __restrict__ bias,
+                  int bias_f32, void* __restrict__ out, int N, int H, int W, int C, int KH, int sh, int ph, int pw,
+                  int Ho, int Wo, int act, int out_f32) {
+  constexpr int SPAN = (PX - 1) * SW + KW;
+  const int CG = C >> 3;
+  const int WB = (Wo + PX - 1) / PX;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)N * Ho * WB * CG;
+  if (gid >= total) return;
+  const int cg = gid % CG;
+  const int64_t r = gid / CG;
+  const int wb = r % WB, ho = (r / WB) % Ho, n = r / ((int64_t)WB * Ho);
+  const int wo0 = wb * PX;
+  const int wi0 = wo0 * SW - pw;
+  float acc[PX][8];
+#pragma unroll
+  for (int p = 0; p < PX; ++p)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[p][i] = 0.f;
+  const uint16_t* xn = x + (int64_t)n * H * W * C + cg * 8;
+  for (int ky = 0; ky < KH; ++ky) {
+    const int hi = ho * sh - ph + ky;
+    if (hi < 0 || hi >= H) continue;
+    const uint16_t* xr = xn + (int64_t)hi * W * C;
+    u32x4_t xv[SPAN];
+#pragma unroll
+    for (int j = 0; j < SPAN; ++j) {
+      const int wi = wi0 + j;
+      xv[j] = (wi >= 0 && wi < W) ? *(const u32x4_t*)(xr + (int64_t)wi * C) : (u32x4_t){0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int kx = 0; kx < KW; ++kx) {
+      float wv[8];
+      unpack8(*(const u32x4_t*)(w + (ky * KW + kx) * C + cg * 8), wv);
+#pragma unroll
+      for (int p = 0; p < PX; ++p) {
+        float xf[8];
+        unpack8(xv[p * SW + kx], xf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[p][i] += xf[i] * wv[i];
+      }
+    }
+  }
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (bias) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      bv[i] = bias_f32 ? ((const float*)bias)[cg * 8 + i] : bf2f(((const uint16_t*)bias)[cg * 8 + i]);
+  }
+#pragma unroll
+  for (int p = 0; p < PX; ++p) {
+    if (wo0 + p >= Wo) break;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[p][i] += bv[i];
+    apply_act_n<8>(acc[p], act);
+    const int64_t pix = ((int64_t)n * Ho + ho) * Wo + wo0 + p;
+    if (out_f32) {
+      float* o = (float*)out + pix * C + cg * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = acc[p][i];
+    } else {
+      *(u32x4_t*)((uint16_t*)out + pix * C + cg * 8) = pack8(acc[p]);
+    }
+  }
+}
+
+template <int KW, int SW>
+static hipError_t launch_dw_rb(const uint16_t* x, const uint16_t* w, const void* bias, int bias_f32, void* out, int N,
+                               int H, int W, int C, int KH, int sh, int ph, int pw, int Ho, int Wo, int act,
+                               int out_f32, hipStream_t stream) {
+  constexpr int PX = 4;
+  const int64_t total = (int64_t)N * Ho * ((Wo + PX - 1) / PX) * (C / 8);
+  hipLaunchKernelGGL((dw_conv_rb_kernel<KW, SW, PX>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, x,
+                     w, bias, bias_f32, out, N, H, W, C, KH, sh, ph, pw, Ho, Wo, act, out_f32);
+  return hipGetLastError();
+}
+
 hipError_t conv2d_depthwise(const uint16_t* x, const uint16_t* w, const void* bias, int bias_f32, void* out, int N,
                             int H, int W, int C, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw,
                             int Ho, int Wo, int act, int out_f32, hipStream_t stream) {
+  if (dh == 1 && dw == 1 && (sw == 1 || sw == 2) && getenv("LUMEN_DW_NAIVE") == nullptr) {
+#define LUMEN_DW_CASE(K)                                                                                       \
+    if (KW == K) return sw == 1 ? launch_dw_rb<K, 1>(x, w, bias, bias_f32, out, N, H, W, C, KH, sh, ph, pw, Ho, Wo, act, \
+                                                     out_f32, stream)                                          \
+                                : launch_dw_rb<K, 2>(x, w, bias, bias_f32, out, N, H, W, C, KH, sh, ph, pw, Ho, Wo, act, \
+                                                     out_f32, stream);
+    LUMEN_DW_CASE(3)
+    LUMEN_DW_CASE(5)
+    LUMEN_DW_CASE(7)
+#undef LUMEN_DW_CASE
+  }
   const int64_t total = (int64_t)N * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(dw_conv_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, x, w, bias,
                      bias_f32, out, N, H, W, C, KH, KW, sh, sw, ph, pw, dh, dw, Ho, Wo, act, out_f32);

@@ -48,7 +48,7 @@ def test_conv2d_into_channel_slice():
     assert big[..., :16].abs().max().item() == 0 and big[..., 32:].abs().max().item() == 0
 
 
-@pytest.mark.parametrize("C,K,s", [(16, 3, 1), (64, 3, 2), (128, 5, 1), (24, 3, 1)])
+@pytest.mark.parametrize("C,K,s", [(16, 3, 1), (64, 3, 2), (128, 5, 1), (24, 3, 1), (96, 7, 1), (80, 7, 2), (32, 5, 2)])
 def test_depthwise(C, K, s):
     x = torch.randn(2, 30, 26, C).bfloat16()
     w = torch.randn(K, K, C).bfloat16() * 0.2
