@@ -458,6 +458,12 @@ __device__ __forceinline__ void tile_coords(int lin, int tiles_m, int tiles_n, i
   }
 }
 
+#ifndef LUMEN_GEMM_RES_PREFETCH
+#define LUMEN_GEMM_RES_PREFETCH 4
+#endif
+// FAST: every tile interior (M, N multiples of 256) with a bf16-bias / act / residual
+// epilogue -> bias + residual prefetched, no bounds checks (chosen on the host).
+template <bool WT, bool FAST>
 __global__ void __launch_bounds__(512)
 gemm_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                     void* __restrict__ C, int64_t ldc, int M, int N, int K, GemmEpi ep, int group_m) {
@@ -600,27 +606,59 @@ gemm_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t*
     // that buffer before the loop's final barrier.
     constexpr int LDSTR = 68;
     float* es = (float*)(smem + (buf ^ 1) * G_BUF) + wid * 16 * LDSTR;
+    const __amdgpu_buffer_rsrc_t crs = c_rsrc(C);
     const int rr = lane >> 2, cq = lane & 3;
     const int ncol = n0 + (cq >> 1) * 128 + wn * 32 + (cq & 1) * 16;
-    Unroll<0, 2>::run([&](const int qm) {
-      Unroll<0, 4>::run([&](const int i) {
+    // interior tiles with plain epilogues: the bias and the residual rows are prefetched
+    // (residual RD slabs ahead) instead of being loaded inside each slab's store
+    constexpr bool fast = FAST;
+    constexpr int RD = LUMEN_GEMM_RES_PREFETCH;
+    u32x4_t bz0 = {0u, 0u, 0u, 0u}, bz1 = {0u, 0u, 0u, 0u};
+    u32x4_t rz[RD][2];
+    auto res_ptr = [&](int s) {
+      return ep.residual + (int64_t)(m0 + (s >> 2) * 128 + wm * 64 + (s & 3) * 16 + rr) * ep.ldr + ncol;
+    };
+    if constexpr (fast) {
+      if (ep.bias) {
+        bz0 = *(const u32x4_t*)((const uint16_t*)ep.bias + ncol);
+        bz1 = *(const u32x4_t*)((const uint16_t*)ep.bias + ncol + 8);
+      }
+      if (ep.residual) {
 #pragma unroll
-        for (int qn = 0; qn < 2; ++qn)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              es[(fq * 4 + r) * LDSTR + qn * 32 + j * 16 + frow] = acc[qm][qn][i][j][r];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        float v[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cq * 16 + q * 4);
-          v[q * 4 + 0] = t[0]; v[q * 4 + 1] = t[1]; v[q * 4 + 2] = t[2]; v[q * 4 + 3] = t[3];
+        for (int s = 0; s < RD; ++s) {
+          rz[s][0] = *(const u32x4_t*)res_ptr(s);
+          rz[s][1] = *(const u32x4_t*)(res_ptr(s) + 8);
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        epi_store16(v, m0 + qm * 128 + wm * 64 + i * 16 + rr, ncol, M, N, C, ldc, ep);
-      });
+      }
+    }
+    Unroll<0, 8>::run([&](const int s) __attribute__((always_inline)) {
+      const int qm = s >> 2, i = s & 3;
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            es[(fq * 4 + r) * LDSTR + qn * 32 + j * 16 + frow] = acc[qm][qn][i][j][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cq * 16 + q * 4);
+        v[q * 4 + 0] = t[0]; v[q * 4 + 1] = t[1]; v[q * 4 + 2] = t[2]; v[q * 4 + 3] = t[3];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int m = m0 + qm * 128 + wm * 64 + i * 16 + rr;
+      if constexpr (fast) {
+        const u32x4_t r0 = rz[s % RD][0], r1 = rz[s % RD][1];
+        if (ep.residual && s + RD < 8) {
+          rz[s % RD][0] = *(const u32x4_t*)res_ptr(s + RD);
+          rz[s % RD][1] = *(const u32x4_t*)(res_ptr(s + RD) + 8);
+        }
+        epi_store16_fast<WT>(v, m, ncol, C, ldc, ep, bz0, bz1, ep.residual != nullptr, r0, r1, crs);
+      } else {
+        epi_store16_t<WT>(v, m, ncol, M, N, C, ldc, ep, crs);
+      }
     });
     if (!has_next) break;
     // the next tile's phase 0 restages this epilogue buffer: all waves' LDS reads first
@@ -895,19 +933,39 @@ static int num_cus() {
   return n;
 }
 
+// wt: write-through (sc1) C stores via a buffer descriptor (C extent < 2 GiB: 32-bit offsets)
+template <bool WT, bool FAST>
+static void launch_persist_t(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc,
+                             int M, int N, int K, const GemmEpi& ep, int group_m, int grid, size_t lds,
+                             hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm_persist_kernel<WT, FAST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemm_persist_kernel<WT, FAST>), dim3(grid), dim3(512), lds, stream, A, lda, W, ldw, C, ldc, M, N,
+                     K, ep, group_m);
+}
+
 static hipError_t launch_persist(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
-                                 int64_t ldc, int M, int N, int K, const GemmEpi& ep, int group_m,
+                                 int64_t ldc, int M, int N, int K, const GemmEpi& ep, int group_m, bool wt,
                                  hipStream_t stream) {
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   const int grid = tiles < num_cus() ? tiles : num_cus();
   const size_t lds = 2 * G_BUF;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm_persist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
+  const int64_t extent = (int64_t)M * ldc * (ep.out_f32 ? 4 : 2);
+  wt = wt && ep.out_group == 0 && extent < ((int64_t)1 << 31);
+  const bool fast = M % 256 == 0 && N % 256 == 0 && ep.out_group == 0 && !ep.glu && !ep.table && !ep.prelu &&
+                    !ep.post_act && !(ep.bias && ep.bias_f32) && extent < ((int64_t)1 << 31) &&
+                    getenv("LUMEN_GEMM_NOFAST") == nullptr;
+  if (fast) {
+    if (wt) launch_persist_t<true, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
+    else launch_persist_t<false, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
+  } else {
+    if (wt) launch_persist_t<true, false>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
+    else launch_persist_t<false, false>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
   }
-  hipLaunchKernelGGL(gemm_persist_kernel, dim3(grid), dim3(512), lds, stream, A, lda, W, ldw, C, ldc, M, N, K, ep,
-                     group_m);
   return hipGetLastError();
 }
 
@@ -978,7 +1036,7 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
     case 4: return launch_glds<0>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, epi, stream);
     case 5: return launch_glds<1>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, epi, stream);
     case 6: return launch_glds<2>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, epi, stream);
-    case 7: return launch_persist(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
+    case 7: return launch_persist(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, epi == 3, stream);
     case 8: return launch_ring(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
     default: return launch_cfg<32, 64, 1, 2>(A, lda, W, ldw, C, ldc, M, N, K, ep, stream);
   }
