@@ -285,17 +285,31 @@ class LLM(nn.Module):
 
     # ------------------------------------------------------------------ forward passes
     @torch.no_grad()
-    def prefill(self, x: torch.Tensor, kv=None, slots: Optional[torch.Tensor] = None, start_pos: int = 0
-                ) -> torch.Tensor:
+    def prefill(self, x: torch.Tensor, kv=None, slots: Optional[torch.Tensor] = None, start_pos: int = 0,
+                prefix_blocks: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One sequence: input embeddings x [T, hidden] (modified in place) at positions
-        start_pos.., k/v written to ``slots``; returns last-token logits [1, V/tp] fp32."""
+        start_pos.., k/v written to ``slots``; returns last-token logits [1, V/tp] fp32.
+
+        Chunked prefill (``start_pos`` > 0): ``prefix_blocks`` (int64, the sequence's KV
+        blocks covering [0, start_pos + T)) — the chunk's queries attend the cached prefix
+        plus themselves (causal, last query aligned with the last key).  K/V of the prefix
+        are gathered from the paged cache (K [blk, Hkv, 64, D]; V stored transposed)."""
         T = x.shape[0]
         pos = torch.arange(start_pos, start_pos + T, device=x.device, dtype=torch.int32)
         D = self.cfg.head_dim
+        S = start_pos + T
 
         def attn(qkv, l, kc, vc):
             q5 = qkv.view(1, T, l.H + 2 * l.Hkv, D)
-            o = ops.attention(q5[:, :, :l.H], q5[:, :, l.H:l.H + l.Hkv], q5[:, :, l.H + l.Hkv:], causal=True)
+            if start_pos > 0:
+                assert prefix_blocks is not None and kc is not None, "chunked prefill needs the KV cache"
+                kb = kc.index_select(0, prefix_blocks)                       # [nb, Hkv, 64, D]
+                vb = vc.index_select(0, prefix_blocks)                       # [nb, Hkv, D, 64]
+                k_all = kb.permute(0, 2, 1, 3).reshape(1, -1, l.Hkv, D)[:, :S]
+                v_all = vb.permute(0, 3, 1, 2).reshape(1, -1, l.Hkv, D)[:, :S].contiguous()
+                o = ops.attention(q5[:, :, :l.H], k_all, v_all, causal=True)
+            else:
+                o = ops.attention(q5[:, :, :l.H], q5[:, :, l.H:l.H + l.Hkv], q5[:, :, l.H + l.Hkv:], causal=True)
             return o.view(T, l.H * D)
 
         self._layers(x, pos, slots, kv, attn)

@@ -9,6 +9,11 @@ host<->device every token (packages/lumen-vlm/src/lumen_vlm/backends/onnxrt_back
 * each admitted request is prefilled (its ``prefill`` callable builds the input
   embeddings — vision tower + token embeddings — on the engine thread), its first
   token sampled and streamed immediately (TTFT);
+* chunked prefill: a prompt longer than ``prefill_chunk`` tokens (env
+  ``LUMEN_PREFILL_CHUNK``, default 2048) is prefilled ``prefill_chunk`` tokens per engine
+  iteration, with a decode step of the running requests between chunks, so a long
+  prompt never stalls the other streams for its whole prefill (each chunk attends the
+  cached prefix: :meth:`LLM.prefill` ``prefix_blocks``);
 * all running requests then advance together: one batched decode step per
   iteration (paged flash-decoding), sampling from on-device top-k candidates;
 * finished sequences release their blocks.
@@ -34,7 +39,7 @@ import torch
 
 from .. import ops
 from ..ops import llm as lops
-from .kv_cache import PagedKVCache
+from .kv_cache import BLOCK, PagedKVCache
 
 log = logging.getLogger("lumen.engine")
 
@@ -62,6 +67,8 @@ class GenRequest:
     finish_reason: Optional[str] = None
     ctx: int = 0                            # tokens in the KV cache
     rng: Any = None
+    x: Any = None                           # prefill input embeddings while the prompt is being chunk-prefilled
+    done: int = 0                           # prompt tokens prefilled so far
 
     def stream(self, timeout: Optional[float] = None) -> Iterator[tuple]:
         """yields ("token", id) ... then ("done", reason) | raises the engine error."""
@@ -238,7 +245,7 @@ class DecodeGraphs:
 class LLMEngine:
     def __init__(self, llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.Tensor], max_batch: int = 64,
                  max_prefill_per_step: int = 4, tp_sync: Optional[TPSync] = None, name: str = "vlm",
-                 use_graphs: Optional[bool] = None):
+                 use_graphs: Optional[bool] = None, prefill_chunk: Optional[int] = None):
         self.llm = llm
         self.kv = kv
         self.build = prefill_builder
@@ -249,10 +256,12 @@ class LLMEngine:
         self._ids = itertools.count(1)
         self._waiting: "queue.Queue[GenRequest]" = queue.Queue()
         self._running: list[GenRequest] = []
+        self._prefilling: list[GenRequest] = []
+        self.prefill_chunk = max(16, int(prefill_chunk or os.environ.get("LUMEN_PREFILL_CHUNK", 2048)))
         self._stop = threading.Event()
         self._ws: dict = {}
         self.device = llm.embed.device
-        self.stats = {"prefills": 0, "decode_steps": 0, "tokens": 0}
+        self.stats = {"prefills": 0, "prefill_chunks": 0, "decode_steps": 0, "tokens": 0}
         if use_graphs is None:
             use_graphs = os.environ.get("LUMEN_HIP_GRAPHS", "1") == "1"
         self.graphs: Optional[DecodeGraphs] = None
@@ -316,7 +325,8 @@ class LLMEngine:
 
     def _admit(self) -> list[GenRequest]:
         adm = []
-        while len(self._running) + len(adm) < self.max_batch and len(adm) < self.max_prefill:
+        while (len(self._running) + len(self._prefilling) + len(adm) < self.max_batch
+               and len(self._prefilling) + len(adm) < self.max_prefill):
             try:
                 r = self._waiting.get_nowait()
             except queue.Empty:
@@ -328,31 +338,63 @@ class LLMEngine:
         return adm
 
     @torch.no_grad()
-    def _prefill(self, r: GenRequest) -> None:
-        spec = Sampler.spec([r])
+    def _prefill_chunk(self, r: GenRequest, budget: int) -> int:
+        """Prefill up to ``budget`` more prompt tokens of ``r``; returns the tokens consumed.
+        On the last chunk the first token is sampled and ``r`` joins the running batch."""
+        if r.x is None:
+            if self.sync is not None:
+                # followers must enter the build (its vocab-parallel embedding all-reduce)
+                # together with us: announce it before building the inputs
+                self.sync.send(("pbuild", r.rid, r.prefill_args))
+                x = self.build(r.prefill_args)
+                if x.shape[0] != r.prompt_len:
+                    raise RuntimeError(f"prefill built {x.shape[0]} rows for a {r.prompt_len}-token prompt")
+            else:
+                x = self.build(r.prefill_args)
+                r.prompt_len = x.shape[0]
+            r.x, r.done = x, 0
+        T = r.prompt_len
+        s = r.done
+        e = min(T, s + max(1, budget))
+        last = e == T
+        slots = self.kv.slots(r.rid, s, e - s)
+        tab = np.asarray(self.kv.blocks.table(r.rid), np.int64)[: -(-e // BLOCK)] if s > 0 else None
+        spec = Sampler.spec([r]) if last else None
         if self.sync is not None:
-            # followers must enter the prefill (its vocab-parallel embedding all-reduce)
-            # together with us: announce it before building the inputs
-            T = r.prompt_len
-            slots = self.kv.slots(r.rid, 0, T)
-            self.sync.send(("prefill", r.prefill_args, slots, spec))
-            x = self.build(r.prefill_args)
-            if x.shape[0] != T:
-                raise RuntimeError(f"prefill built {x.shape[0]} rows for a {T}-token prompt")
-        else:
-            x = self.build(r.prefill_args)
-            T = x.shape[0]
-            r.prompt_len = T
-            slots = self.kv.slots(r.rid, 0, T)
-        logits = self.llm.prefill(x, self.kv, torch.from_numpy(slots).to(self.device))
+            self.sync.send(("pchunk", r.rid, s, e, slots, tab, spec, last))
+        logits = self.llm.prefill(r.x[s:e], self.kv, torch.from_numpy(slots).to(self.device), start_pos=s,
+                                  prefix_blocks=torch.from_numpy(tab).to(self.device) if tab is not None else None)
+        r.done = e
+        self.stats["prefill_chunks"] += 1
+        if not last:
+            return e - s
+        r.x = None
         r.ctx = T
         tok = self.sampler.pick(self.sampler.candidates(logits, spec), [r])[0]
         r.t_first = time.perf_counter()
         self.stats["prefills"] += 1
+        self._prefilling.remove(r)
         if self._emit(r, tok):
             self._finish(r)
         else:
             self._running.append(r)
+        return e - s
+
+    def _prefill_round(self) -> None:
+        """One engine iteration's prefill work: up to ``prefill_chunk`` prompt tokens,
+        oldest request first."""
+        budget = self.prefill_chunk
+        for r in list(self._prefilling):
+            if budget <= 0:
+                break
+            try:
+                budget -= self._prefill_chunk(r, budget)
+            except Exception as e:  # noqa: BLE001 - surfaced to the caller
+                log.exception("prefill failed")
+                if r in self._prefilling:
+                    self._prefilling.remove(r)
+                r.x = None
+                self._fail([r], e)
 
     @torch.no_grad()
     def _decode(self) -> None:
@@ -394,20 +436,16 @@ class LLMEngine:
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
         while not self._stop.is_set():
-            adm = self._admit()
-            if not adm and not self._running:
+            self._prefilling.extend(self._admit())
+            if not self._prefilling and not self._running:
                 try:
                     r = self._waiting.get(timeout=0.05)
                     self._waiting.put(r)
                 except queue.Empty:
                     pass
                 continue
-            for r in adm:
-                try:
-                    self._prefill(r)
-                except Exception as e:  # noqa: BLE001 - surfaced to the caller
-                    log.exception("prefill failed")
-                    self._fail([r], e)
+            if self._prefilling:
+                self._prefill_round()
             if self._running:
                 try:
                     self._decode()
@@ -421,6 +459,7 @@ def follower_loop(llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.
     """Non-zero TP ranks: replay rank 0's steps so every collective is matched."""
     sampler = Sampler(llm)
     ws: dict = {}
+    xs: dict = {}                            # rid -> prefill embeddings of prompts being chunk-prefilled
     dev = llm.embed.device
     while True:
         msg = sync.recv()
@@ -428,11 +467,16 @@ def follower_loop(llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.
         if kind == "stop":
             return
         with torch.no_grad():
-            if kind == "prefill":
-                _, args, slots, spec = msg
-                x = prefill_builder(args)
-                logits = llm.prefill(x, kv, torch.from_numpy(slots).to(dev))
-                sampler.candidates(logits, spec)
+            if kind == "pbuild":
+                _, rid, args = msg
+                xs[rid] = prefill_builder(args)
+            elif kind == "pchunk":
+                _, rid, s, e, slots, tab, spec, last = msg
+                x = xs[rid] if not last else xs.pop(rid)
+                logits = llm.prefill(x[s:e], kv, torch.from_numpy(slots).to(dev), start_pos=s,
+                                     prefix_blocks=torch.from_numpy(tab).to(dev) if tab is not None else None)
+                if last:
+                    sampler.candidates(logits, spec)
             elif kind == "decode":
                 _, ids, pos, slots, bt, ctx, spec = msg
                 logits = llm.decode(torch.from_numpy(ids).to(dev), torch.from_numpy(pos).to(dev),

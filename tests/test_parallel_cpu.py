@@ -142,6 +142,8 @@ def _vlm_leader(cache, tp, q):
     import json as _json
 
     os.environ["LUMEN_TP_SIZE"] = str(tp)
+    if tp > 1:   # also exercise chunked prefill across ranks (prompts here are ~50 tokens)
+        os.environ["LUMEN_PREFILL_CHUNK"] = "16"
     from lumen_amd.resources.validator import config_from_dict
     from lumen_amd.services.vlm import GeneralFastVLMService
     from lumen_amd.utils.image import encode_jpeg
@@ -161,7 +163,7 @@ def _vlm_leader(cache, tp, q):
         for prompt in ("Describe.", "What is this?"):
             body, _, _ = s.handle("vlm_generate", img, "image/jpeg", {"prompt": prompt, "max_new_tokens": "9"})
             outs.append(_json.loads(body)["text"])
-        q.put({"texts": outs, "tp": s.backend.tp.world})
+        q.put({"texts": outs, "tp": s.backend.tp.world, "chunks": s.backend.engine.stats["prefill_chunks"]})
     finally:
         s.close()
 
@@ -182,6 +184,7 @@ def test_vlm_tensor_parallel_serving_matches_tp1(tmp_path):
         p.join(60)
         assert p.exitcode == 0
     assert res[2]["tp"] == 2 and res[1]["tp"] == 1
+    assert res[2]["chunks"] > res[1]["chunks"]          # TP=2 run prefilled in 16-token chunks
     assert res[2]["texts"] == res[1]["texts"]
 
 

@@ -211,3 +211,27 @@ def test_vlm_service_stream(vlm_service):
     assert "processing_time_ms" in out[-1].meta
     cap = vlm_service.build_capability()
     assert cap.service_name == "vlm-fast" and {t.name for t in cap.tasks} == {"vlm_generate", "vlm_generate_stream"}
+
+
+def test_chunked_prefill_matches_single_shot():
+    """Prompts longer than the prefill chunk (64 tokens here, crossing KV block
+    boundaries) are prefilled chunk by chunk, interleaved with other streams' decode
+    steps, and generate exactly the tokens of a single-shot prefill."""
+    cfg = LLM_PRESETS["tiny"]
+    m = LLM(cfg, dtype=torch.float32, device="cpu")
+    m.random_init(5)
+    prompts = [list(np.random.default_rng(10 + i).integers(0, cfg.vocab_size, n)) for i, n in enumerate((150, 30, 200))]
+    outs = {}
+    for chunk in (4096, 64):
+        kv = PagedKVCache(cfg.num_layers, m.Hkv, cfg.head_dim, num_blocks=64, dtype=torch.float32)
+        eng = LLMEngine(m, kv, lambda ids: m.embed_tokens(torch.tensor(ids)), max_batch=8, prefill_chunk=chunk)
+        try:
+            rs = [eng.submit(p, len(p), SamplingParams(max_new_tokens=10)) for p in prompts]
+            for r in rs:
+                list(r.stream(timeout=120))
+            outs[chunk] = [r.tokens for r in rs]
+            if chunk == 64:
+                assert eng.stats["prefill_chunks"] >= 3 + 1 + 4
+        finally:
+            eng.close()
+    assert outs[64] == outs[4096]

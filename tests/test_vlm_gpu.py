@@ -122,3 +122,36 @@ def test_decode_graphs_match_eager():
         finally:
             eng.close()
     assert outs[True] == outs[False]
+
+
+def test_chunked_prefill_gpu_matches_single_shot():
+    """Chunked prefill on the HIP kernels (prefix K/V gathered from the paged cache, causal
+    attention aligned to the last key) reproduces the single-shot prefill's logits and
+    K/V cache, and the engine streams with 128-token chunks."""
+    cfg = LLM_PRESETS["qwen2-0.5b"]
+    m = LLM(cfg, device="cuda")
+    m.random_init(4)
+    ids = torch.tensor(np.random.default_rng(20).integers(0, 150000, 700), device="cuda")
+    res = {}
+    for chunk in (700, 128):
+        kv = PagedKVCache(cfg.num_layers, m.Hkv, cfg.head_dim, num_blocks=32, device="cuda")
+        assert kv.blocks.reserve(1, 700)
+        x = m.embed_tokens(ids)
+        tab = torch.from_numpy(np.asarray(kv.blocks.table(1), np.int64)).cuda()
+        for s in range(0, 700, chunk):
+            e = min(700, s + chunk)
+            slots = torch.from_numpy(kv.slots(1, s, e - s)).cuda()
+            logits = m.prefill(x[s:e], kv, slots, start_pos=s, prefix_blocks=tab[: -(-e // 64)] if s else None)
+        res[chunk] = (logits.float(), kv.k[5][tab].float())
+    assert _cos(res[128][0], res[700][0]) > 0.999
+    assert _cos(res[128][1], res[700][1]) > 0.999
+    kv = PagedKVCache(cfg.num_layers, m.Hkv, cfg.head_dim, num_blocks=64, device="cuda")
+    eng = LLMEngine(m, kv, lambda t: m.embed_tokens(torch.tensor(t, device="cuda")), max_batch=8, prefill_chunk=128)
+    try:
+        rs = [eng.submit(list(ids.cpu().numpy()[:n]), n, SamplingParams(max_new_tokens=6)) for n in (700, 90, 333)]
+        for r in rs:
+            list(r.stream(timeout=120))
+            assert len(r.tokens) == 6
+        assert eng.stats["prefill_chunks"] >= 6 + 1 + 3
+    finally:
+        eng.close()
