@@ -31,3 +31,24 @@ def test_example_validates_and_resolves(path):
         mod, cls = target.rsplit(".", 1)
         assert hasattr(importlib.import_module(mod), cls)
         assert sc.models
+
+
+@pytest.mark.parametrize("ctype", ["minimal", "light_weight", "basic", "brave"])
+@pytest.mark.parametrize("region", ["cn", "other"])
+def test_generated_configs_import_strings_resolve(ctype, region):
+    """Counterpart of the reference's tests/test_package_init_contract.py: every
+    registry_class / add_to_server string the control plane writes into a generated
+    config imports (via the hub loader) to a real MI355X object, for every preset."""
+    from lumen_amd.app import presets as P
+    from lumen_amd.hub.loader import ServiceLoader
+    from lumen_amd.resources.config import Region
+
+    for name in P.detection_order():
+        c = P.Config("~/.lumen", P.PRESETS[name].create_config(), Region(region), "lumen-ai", 50051)
+        lc = getattr(c, ctype)()
+        for svc in lc.services.values():
+            cls = ServiceLoader.get_class(svc.import_info.registry_class)
+            assert hasattr(cls, "from_config"), svc.import_info.registry_class
+            assert callable(ServiceLoader.get_class(svc.import_info.add_to_server))
+            for m in svc.models.values():
+                assert m.model
