@@ -461,9 +461,11 @@ __device__ __forceinline__ void tile_coords(int lin, int tiles_m, int tiles_n, i
 #ifndef LUMEN_GEMM_RES_PREFETCH
 #define LUMEN_GEMM_RES_PREFETCH 4
 #endif
-// FAST: every tile interior (M, N multiples of 256) with a bf16-bias / act / residual
-// epilogue -> bias + residual prefetched, no bounds checks (chosen on the host).
-template <bool WT, bool FAST>
+// FK > 0 (FAST): every tile interior (M, N multiples of 256), bf16 output, optional bf16
+// bias (FK-1 bit 0) / activation / residual (FK-1 bit 1) -> bias + residual prefetched, no
+// bounds checks, and every VMEM count static so hipcc's own waits are exact (chosen on the
+// host).  FK = 0: the generic bounds-checked epilogue.
+template <bool WT, int FK>
 __global__ void __launch_bounds__(512)
 gemm_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                     void* __restrict__ C, int64_t ldc, int M, int N, int K, GemmEpi ep, int group_m) {
@@ -539,6 +541,7 @@ gemm_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t*
   };
 
   int buf = 0;
+  bool after_epi = false;
   while (true) {
     const int nlin = lin + G;
     const bool has_next = nlin < ntiles;
@@ -565,6 +568,11 @@ gemm_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t*
       const int pm0 = last ? nm0 : m0, pn0 = last ? nn0 : n0;
       const int koff = last ? 0 : (kt + 1) * BK;
       const int nbuf = buf ^ 1;
+      // First K-step after an epilogue: the epilogue's C stores (>= 16 VMEM ops per wave on
+      // the FAST path) are younger than the B1 / A1 loads waited for below, so vmcnt(4)
+      // would also wait for most of those stores to be acknowledged; vmcnt(20) waits for
+      // exactly the loads (stores and loads share the in-order vmcnt counter).
+      const bool relax = FK > 0 && after_epi && kt == 0 && more;
       const char* base = smem + buf * G_BUF;
 #define LUMEN_PQUAD(QM, QN)                                                                                    \
       __builtin_amdgcn_s_setprio(1);                                                                           \
@@ -579,13 +587,15 @@ gemm_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t*
       load_a(base, 0);
       load_b(base, 0);
       LUMEN_PQUAD(0, 0)
-      if (more) vm_wait4(); else vm_wait0();   // B1 landed
+      if (relax) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+      else if (more) vm_wait4(); else vm_wait0();   // B1 landed
       __builtin_amdgcn_s_barrier();
       if (more) stageB(0, nbuf, pn0, koff);
       // phase 1: quadrant (0,1)
       load_b(base, 1);
       LUMEN_PQUAD(0, 1)
-      if (more) vm_wait4(); else vm_wait0();   // A1 landed
+      if (relax) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+      else if (more) vm_wait4(); else vm_wait0();   // A1 landed
       __builtin_amdgcn_s_barrier();
       if (more) stageB(1, nbuf, pn0, koff);
       // phase 2: quadrant (1,1)
@@ -611,7 +621,8 @@ gemm_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t*
     const int ncol = n0 + (cq >> 1) * 128 + wn * 32 + (cq & 1) * 16;
     // interior tiles with plain epilogues: the bias and the residual rows are prefetched
     // (residual RD slabs ahead) instead of being loaded inside each slab's store
-    constexpr bool fast = FAST;
+    constexpr bool fast = FK > 0;
+    constexpr bool FB = fast && ((FK - 1) & 1), FR = fast && ((FK - 1) & 2);
     constexpr int RD = LUMEN_GEMM_RES_PREFETCH;
     u32x4_t bz0 = {0u, 0u, 0u, 0u}, bz1 = {0u, 0u, 0u, 0u};
     u32x4_t rz[RD][2];
@@ -619,11 +630,11 @@ gemm_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t*
       return ep.residual + (int64_t)(m0 + (s >> 2) * 128 + wm * 64 + (s & 3) * 16 + rr) * ep.ldr + ncol;
     };
     if constexpr (fast) {
-      if (ep.bias) {
+      if constexpr (FB) {
         bz0 = *(const u32x4_t*)((const uint16_t*)ep.bias + ncol);
         bz1 = *(const u32x4_t*)((const uint16_t*)ep.bias + ncol + 8);
       }
-      if (ep.residual) {
+      if constexpr (FR) {
 #pragma unroll
         for (int s = 0; s < RD; ++s) {
           rz[s][0] = *(const u32x4_t*)res_ptr(s);
@@ -651,16 +662,19 @@ gemm_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t*
       const int m = m0 + qm * 128 + wm * 64 + i * 16 + rr;
       if constexpr (fast) {
         const u32x4_t r0 = rz[s % RD][0], r1 = rz[s % RD][1];
-        if (ep.residual && s + RD < 8) {
-          rz[s % RD][0] = *(const u32x4_t*)res_ptr(s + RD);
-          rz[s % RD][1] = *(const u32x4_t*)(res_ptr(s + RD) + 8);
+        if constexpr (FR) {
+          if (s + RD < 8) {
+            rz[s % RD][0] = *(const u32x4_t*)res_ptr(s + RD);
+            rz[s % RD][1] = *(const u32x4_t*)(res_ptr(s + RD) + 8);
+          }
         }
-        epi_store16_fast<WT>(v, m, ncol, C, ldc, ep, bz0, bz1, ep.residual != nullptr, r0, r1, crs);
+        epi_store16_fast<WT, FR>(v, m, ncol, C, ldc, ep, bz0, bz1, r0, r1, crs);
       } else {
         epi_store16_t<WT>(v, m, ncol, M, N, C, ldc, ep, crs);
       }
     });
     if (!has_next) break;
+    after_epi = true;
     // the next tile's phase 0 restages this epilogue buffer: all waves' LDS reads first
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -934,18 +948,30 @@ static int num_cus() {
 }
 
 // wt: write-through (sc1) C stores via a buffer descriptor (C extent < 2 GiB: 32-bit offsets)
-template <bool WT, bool FAST>
+template <bool WT, int FK>
 static void launch_persist_t(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc,
                              int M, int N, int K, const GemmEpi& ep, int group_m, int grid, size_t lds,
                              hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm_persist_kernel<WT, FAST>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)lds);
+    hipFuncSetAttribute((const void*)gemm_persist_kernel<WT, FK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm_persist_kernel<WT, FAST>), dim3(grid), dim3(512), lds, stream, A, lda, W, ldw, C, ldc, M, N,
+  hipLaunchKernelGGL((gemm_persist_kernel<WT, FK>), dim3(grid), dim3(512), lds, stream, A, lda, W, ldw, C, ldc, M, N,
                      K, ep, group_m);
+}
+
+template <bool WT>
+static void launch_persist_fk(int fk, const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
+                              int64_t ldc, int M, int N, int K, const GemmEpi& ep, int group_m, int grid, size_t lds,
+                              hipStream_t stream) {
+  switch (fk) {
+    case 1: return launch_persist_t<WT, 1>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
+    case 2: return launch_persist_t<WT, 2>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
+    case 3: return launch_persist_t<WT, 3>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
+    case 4: return launch_persist_t<WT, 4>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
+    default: return launch_persist_t<WT, 0>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
+  }
 }
 
 static hipError_t launch_persist(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
@@ -957,15 +983,11 @@ static hipError_t launch_persist(const uint16_t* A, int64_t lda, const uint16_t*
   const int64_t extent = (int64_t)M * ldc * (ep.out_f32 ? 4 : 2);
   wt = wt && ep.out_group == 0 && extent < ((int64_t)1 << 31);
   const bool fast = M % 256 == 0 && N % 256 == 0 && ep.out_group == 0 && !ep.glu && !ep.table && !ep.prelu &&
-                    !ep.post_act && !(ep.bias && ep.bias_f32) && extent < ((int64_t)1 << 31) &&
+                    !ep.post_act && !ep.out_f32 && !(ep.bias && ep.bias_f32) && extent < ((int64_t)1 << 31) &&
                     getenv("LUMEN_GEMM_NOFAST") == nullptr;
-  if (fast) {
-    if (wt) launch_persist_t<true, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
-    else launch_persist_t<false, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
-  } else {
-    if (wt) launch_persist_t<true, false>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
-    else launch_persist_t<false, false>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
-  }
+  const int fk = fast ? 1 + (ep.bias ? 1 : 0) + (ep.residual ? 2 : 0) : 0;
+  if (wt) launch_persist_fk<true>(fk, A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
+  else launch_persist_fk<false>(fk, A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
   return hipGetLastError();
 }
 
