@@ -1,0 +1,31 @@
+"""ONNX graph executor on the MI355X kernels (NHWC conv / depthwise / pooling / resize /
+fused BN-activation-residual) vs its fp32 CPU reference path."""
+import pytest
+import torch
+
+from lumen_amd.runtime.onnx_graph import OnnxGraph
+from lumen_amd.utils import onnx_lite as ox
+
+from test_onnx_cpu import detnet_graph, resnet_graph
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float().cpu() - b.float()).norm() / b.float().norm()).item()
+
+
+@pytest.mark.parametrize("build", [resnet_graph, detnet_graph])
+def test_onnx_executor_gpu_matches_cpu(build):
+    g, _ = build()
+    data = ox.write_model(g)
+    x = torch.randn(2, 3, 32, 32)
+    ref = OnnxGraph(data).run({"x": x})
+    gpu = OnnxGraph(data, device="cuda")
+    assert any(k == "conv" and s["mode"] in ("dense", "dw") for k, s in gpu.plan)
+    got = gpu.run({"x": x.cuda()})
+    for a, b in zip(got, ref):
+        if b.is_floating_point():
+            assert _rel(a, b) < 3e-2, _rel(a, b)
+        else:
+            assert a.cpu().tolist() == b.tolist()
