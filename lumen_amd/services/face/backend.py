@@ -149,26 +149,35 @@ class MI355XFaceBackend:
         self.device = pick_device(self.device_pref)
         r = self.resources
         cfgp = r.model_root_path / "lumen_face_config.json"
-        if not cfgp.exists():
-            raise ResourceNotFoundError(
-                f"{r.model_name}: lumen_face_config.json missing — MI355X face weights are loaded from "
-                "detection/recognition.safetensors (ONNX initializer import is not available in this build)")
-        import json
-
-        meta = json.loads(cfgp.read_text())
-        dcfg = SCRFDConfig(**{k: tuple(v) if isinstance(v, list) else v for k, v in meta["det"].items()})
-        rcfg = IResNetConfig(**{k: tuple(v) if isinstance(v, list) else v for k, v in meta["rec"].items()})
         from .specs import pack_spec
 
         spec = pack_spec(r.model_name, r.extra.get("insightface") or {})
         d, rc = spec["detection"], spec["recognition"]
-        self.spec = FaceSpec(det_size=dcfg.input_size, det_mean=float(np.mean(d.get("mean", 127.5))),
-                             det_std=float(np.mean(d.get("std", 128.0))), rec_size=rcfg.input_size,
+        if cfgp.exists():
+            import json
+
+            meta = json.loads(cfgp.read_text())
+            dcfg = SCRFDConfig(**{k: tuple(v) if isinstance(v, list) else v for k, v in meta["det"].items()})
+            rcfg = IResNetConfig(**{k: tuple(v) if isinstance(v, list) else v for k, v in meta["rec"].items()})
+            det, rec = SCRFD(dcfg), IResNet(rcfg)
+            det.load_state_dict(load_safetensors(r.get_model_file("detection.safetensors")))
+            rec.load_state_dict(load_safetensors(r.get_model_file("recognition.safetensors")))
+            det_size, rec_size = dcfg.input_size, rcfg.input_size
+        else:
+            # the reference's InsightFace ONNX pack, run by the MI355X graph executor
+            from .onnx_pack import OnnxArcFace, OnnxSCRFD, find_onnx_pair
+
+            dpath, rpath = find_onnx_pair(r.model_root_path)
+            if dpath is None or rpath is None:
+                raise ResourceNotFoundError(
+                    f"{r.model_name}: neither lumen_face_config.json (+ safetensors) nor a detection/recognition "
+                    f"ONNX pair found in {r.model_root_path}")
+            det, rec = OnnxSCRFD(dpath, self.device, d), OnnxArcFace(rpath, self.device, rc)
+            det_size, rec_size = det.cfg.input_size, rec.cfg.input_size
+        self.spec = FaceSpec(det_size=det_size, det_mean=float(np.mean(d.get("mean", 127.5))),
+                             det_std=float(np.mean(d.get("std", 128.0))), rec_size=rec_size,
                              rec_mean=float(np.mean(rc.get("mean", 127.5))), rec_std=float(np.mean(rc.get("std", 127.5))),
                              rec_color=rc.get("color_order", "rgb"), align_landmarks=rc.get("align_landmarks", True))
-        det, rec = SCRFD(dcfg), IResNet(rcfg)
-        det.load_state_dict(load_safetensors(r.get_model_file("detection.safetensors")))
-        rec.load_state_dict(load_safetensors(r.get_model_file("recognition.safetensors")))
         self.det, self.rec = det.to(self.device).eval(), rec.to(self.device).eval()
         self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
         self._det_batcher = DynamicBatcher(self._detect_batch, self.max_batch, self.max_wait_ms, "face-det")
