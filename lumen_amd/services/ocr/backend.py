@@ -181,20 +181,27 @@ class MI355XOcrBackend:
             chars.append(" ")
         self.character_str = ["blank"] + chars
         cfgp = r.model_root_path / "lumen_ocr_config.json"
-        if not cfgp.exists():
-            raise ResourceNotFoundError(f"{r.model_name}: lumen_ocr_config.json missing (MI355X OCR weights are "
-                                        "loaded from detection/recognition.safetensors)")
-        meta = json.loads(cfgp.read_text())
-        dcfg = DBNetConfig(**{k: _tup(v) for k, v in meta["det"].items()})
-        rcfg = RecConfig(**{k: _tup(v) for k, v in meta["rec"].items()})
         self.device = pick_device(self.device_pref)
         self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
-        det, rec = DBNet(dcfg), SVTRRecognizer(rcfg)
-        try:
-            det.load_state_dict(load_safetensors(r.get_model_file("detection.safetensors")))
-            rec.load_state_dict(load_safetensors(r.get_model_file("recognition.safetensors")))
-        except Exception as e:
-            raise ModelLoadingError(f"Initialization failed: {e}") from e
+        if cfgp.exists():
+            meta = json.loads(cfgp.read_text())
+            dcfg = DBNetConfig(**{k: _tup(v) for k, v in meta["det"].items()})
+            rcfg = RecConfig(**{k: _tup(v) for k, v in meta["rec"].items()})
+            det, rec = DBNet(dcfg), SVTRRecognizer(rcfg)
+            try:
+                det.load_state_dict(load_safetensors(r.get_model_file("detection.safetensors")))
+                rec.load_state_dict(load_safetensors(r.get_model_file("recognition.safetensors")))
+            except Exception as e:
+                raise ModelLoadingError(f"Initialization failed: {e}") from e
+        else:
+            # the reference's PP-OCR ONNX pack, run by the MI355X graph executor
+            from .onnx_pack import OnnxCTCRecognizer, OnnxDBNet, find_onnx_pair
+
+            dpath, rpath = find_onnx_pair(r.model_root_path)
+            if dpath is None or rpath is None:
+                raise ResourceNotFoundError(f"{r.model_name}: neither lumen_ocr_config.json (+ safetensors) nor a "
+                                            f"detection/recognition ONNX pair found in {r.model_root_path}")
+            det, rec = OnnxDBNet(dpath, self.device), OnnxCTCRecognizer(rpath, self.device)
         self.det, self.rec = det.to(self.device).eval(), rec.to(self.device).eval()
         self.rec_h = int(self.rec_config["image_shape"][1])
         self._batcher = DynamicBatcher(self._predict_batch, self.max_batch, self.max_wait_ms, "ocr")
