@@ -341,7 +341,11 @@ __global__ void __launch_bounds__(256) attn_res_kernel(AttnArgs a, int nkc) {
     f32x4_t l4 = (f32x4_t){0.f, 0.f, 0.f, 0.f};
     const int wave_kend = a.causal ? min(kv_len, min(q0 + 16, a.Sq) + causal_off) : kv_len;
     const int nc = min(nkc, (wave_kend + KC - 1) / KC);
-    for (int kc = 0; kc < nc; ++kc) {
+    // a ragged last chunk with <= 16 live keys (ViT S = 257: 1 key; CLIP text S = 77: 13)
+    // runs a 16-key tail step below: 7 MFMAs and 4 scores per lane instead of 18 and 16
+    const bool tail1 = nc > 0 && wave_kend - (nc - 1) * KC <= 16;
+    const int nfull = tail1 ? nc - 1 : nc;
+    for (int kc = 0; kc < nfull; ++kc) {
       const int k0 = kc * KC;
       const char* sK = smem + kc * 2 * IMG;
       const char* sV = sK + IMG;
@@ -380,6 +384,57 @@ __global__ void __launch_bounds__(256) attn_res_kernel(AttnArgs a, int nkc) {
         }
         l4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones_bf16x8(), pf, l4, 0, 0, 0);   // row sums of P
       }
+    }
+    if (tail1) {
+      const int k0 = nfull * KC;
+      const char* sK = smem + nfull * 2 * IMG;
+      const char* sV = sK + IMG;
+      f32x4_t s0 = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < KS; ++t) {
+        bf16x8_t kf = *(const bf16x8_t*)(sK + col * D * 2 + (k_phys<D>(col, t * 4 + g) << 4));
+        s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[t], s0, 0, 0, 0);
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kj = k0 + g * 4 + r;
+        bool ok = kj < kv_len;
+        if (a.causal) ok = ok && (kj <= qi + causal_off);
+        s0[r] = ok ? s0[r] : -INFINITY;
+        mx = fmaxf(mx, s0[r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mcand = fmaxf(mrow, mx * a.scale_log2);
+      if (__any(mcand > mrow + 8.f)) {
+        const float mb = mcand == -INFINITY ? 0.f : mcand;
+        const float alpha = __builtin_amdgcn_exp2f(mrow - mb);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) o[j] *= alpha;
+        l4 *= alpha;
+        mrow = mcand;
+      }
+      const float nmb = mrow == -INFINITY ? 0.f : -mrow;
+      bf16x8_t pf;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pf[r] = (__bf16)__builtin_amdgcn_exp2f(__builtin_fmaf(s0[r], a.scale_log2, nmb));
+        pf[4 + r] = (__bf16)0.f;                  // keys 16..31 of the chunk: past the tail
+      }
+      const int q = col >> 2, p = col & 3;
+      const int r0 = 4 * g + q, r1 = r0 + 16;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int c0 = j * 16 + 4 * p;
+        const char* a0 = sV + r0 * D * 2 + (v_phys<D>(r0, c0 >> 3) << 4) + (c0 & 7) * 2;
+        const char* a1 = sV + r1 * D * 2 + (v_phys<D>(r1, c0 >> 3) << 4) + (c0 & 7) * 2;
+        const s16x4v lo = ds_read_tr16(a0);
+        const s16x4v hi = ds_read_tr16(a1);
+        s16x8_t vv = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, vv), pf, o[j], 0, 0, 0);
+      }
+      l4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones_bf16x8(), pf, l4, 0, 0, 0);
     }
     // Branch-free store through a per-(batch, head) buffer descriptor whose range ends at
     // the last valid query row: lanes of the ragged last block (qi >= Sq) are dropped by
