@@ -18,6 +18,7 @@ OpenAI-style towers (torch_backend.py:340-393).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field, asdict
 from typing import Optional
 
@@ -194,6 +195,23 @@ class _Block(nn.Module):
             p.data.copy_(torch.randn(p.shape, generator=gen) * s)
 
 
+# Residual adds of the out-proj / fc2 GEMMs move into the following LayerNorm (add + LN +
+# residual-stream write in one pass) and those two GEMMs become plain bias GEMMs on
+# hipBLASLt, which measured faster than the fused-residual MFMA kernel on exactly these
+# shapes (ViT-L/14 b512: out-proj 0.26 vs 0.36 ms, fc2 K=4096 0.80 vs 1.05 ms; see
+# profiles/r1_gemm_epilogue_fast_v1.jsonl).  qkv (bias) and fc1 (bias + GELU/QuickGELU)
+# stay on the hand-written kernel, which matches or beats hipBLASLt there.
+_BLAS_RESID = os.environ.get("LUMEN_BLAS_RESID", "1") != "0"
+_BLAS_RESID_MIN_ROWS = int(os.environ.get("LUMEN_BLAS_RESID_MIN_ROWS", "8192"))
+
+
+def _bias_gemm(a: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: torch.Tensor) -> None:
+    if b is not None:
+        torch.addmm(b, a, w.t(), out=out)
+    else:
+        torch.mm(a, w.t(), out=out)
+
+
 def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float,
                causal: bool = False, kv_len: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Run pre-LN blocks over the flat residual stream x [B*S, W] (updated in place)."""
@@ -201,17 +219,30 @@ def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, ep
     D = W // heads
     h = torch.empty_like(x)
     o = torch.empty_like(x)
-    for blk in blocks:
-        ops.layer_norm(x, blk.ln1_w, blk.ln1_b, eps, out=h)
+    blocks = list(blocks)
+    fuse = _BLAS_RESID and x.is_cuda and T >= _BLAS_RESID_MIN_ROWS
+    y = torch.empty_like(x) if fuse else None
+    for i, blk in enumerate(blocks):
+        if i == 0 or not fuse:
+            ops.layer_norm(x, blk.ln1_w, blk.ln1_b, eps, out=h)
         qkv = ops.linear(h, blk.qkv_w, blk.qkv_b)
         q5 = qkv.view(B, S, 3, heads, D)
         ops.attention(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], causal=causal, kv_len=kv_len,
                       out=o.view(B, S, heads, D))
         del qkv, q5
-        ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x)
-        ops.layer_norm(x, blk.ln2_w, blk.ln2_b, eps, out=h)
+        if fuse:
+            _bias_gemm(o, blk.out_w, blk.out_b, y)
+            ops.layer_norm(y, blk.ln2_w, blk.ln2_b, eps, add=x, resid_out=x, out=h)
+        else:
+            ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x)
+            ops.layer_norm(x, blk.ln2_w, blk.ln2_b, eps, out=h)
         f = ops.linear(h, blk.fc1_w, blk.fc1_b, act=act)
-        ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x)
+        if fuse and i + 1 < len(blocks):
+            nb = blocks[i + 1]
+            _bias_gemm(f, blk.fc2_w, blk.fc2_b, y)
+            ops.layer_norm(y, nb.ln1_w, nb.ln1_b, eps, add=x, resid_out=x, out=h)
+        else:
+            ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x)
         del f
     return x
 

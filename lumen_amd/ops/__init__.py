@@ -194,8 +194,10 @@ def _norm(x, w, b, eps, mode, row_idx=None, add=None, resid_out=None, out=None, 
     return out
 
 
-def layer_norm(x, w, b=None, eps=1e-5, row_idx=None, out=None, out_dtype=None):
-    out = _norm(x, w, b, eps, 0, row_idx=row_idx, out=out, out_dtype=out_dtype)
+def layer_norm(x, w, b=None, eps=1e-5, row_idx=None, out=None, out_dtype=None, add=None, resid_out=None):
+    """LayerNorm(x [+ add]); when ``resid_out`` is given the pre-norm sum is stored there
+    (the residual-stream update of a pre-LN block fused into the next norm)."""
+    out = _norm(x, w, b, eps, 0, row_idx=row_idx, add=add, resid_out=resid_out, out=out, out_dtype=out_dtype)
     if row_idx is None and out.shape != x.shape and out.numel() == x.numel():
         return out.view(x.shape)
     return out
