@@ -269,4 +269,45 @@ __device__ __forceinline__ void epi_store8(float* v, int m, int n, int M, int N,
   epi_store8_t<false>(v, m, n, M, N, C, ldc, ep, c_rsrc(C));
 }
 
+// Sum of the K-split fp32 slabs ws[s][M][N] for s = 0..ks-1 (fixed order: deterministic) at
+// row m, columns n..n+15.  The finalize passes of the skinny decode GEMMs run with only
+// M * N / 16 threads (256 for N = 4096), so a serial per-slab loop pays one dependent HBM
+// latency per split (~10 us at ks = 4, measured); here the loads of 4 slabs are issued
+// before any is consumed (one round trip per 4 slabs), as 16-B loads when N % 4 == 0.
+__device__ __forceinline__ void splitk_sum16(const float* __restrict__ ws, int ks, int m, int n, int M, int N,
+                                             float* v) {
+#pragma unroll
+  for (int c = 0; c < 16; ++c) v[c] = 0.f;
+  const int64_t slab = (int64_t)M * N;
+  const float* p0 = ws + (int64_t)m * N + n;
+  if ((N & 3) == 0 && n + 16 <= N) {
+    int s = 0;
+    for (; s + 4 <= ks; s += 4) {
+      f32x4_t x[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[u][q] = *(const f32x4_t*)(p0 + (s + u) * slab + 4 * q);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[4 * q + e] += x[u][q][e];
+    }
+    for (; s < ks; ++s) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4_t x = *(const f32x4_t*)(p0 + s * slab + 4 * q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * q + e] += x[e];
+      }
+    }
+  } else {
+    for (int s = 0; s < ks; ++s)
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] += n + c < N ? p0[s * slab + c] : 0.f;
+  }
+}
+
 }  // namespace lumen

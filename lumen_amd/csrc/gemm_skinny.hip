@@ -112,13 +112,7 @@ __global__ void gemm_skinny_finalize(const float* __restrict__ ws, int ks, void*
   if (idx >= M * groups) return;
   const int m = idx / groups, n = (idx - m * groups) * 16;
   float v[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) v[c] = 0.f;
-  for (int s = 0; s < ks; ++s) {     // fixed summation order over the K-split slabs
-    const float* p = ws + ((int64_t)s * M + m) * N + n;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) v[c] += n + c < N ? p[c] : 0.f;
-  }
+  splitk_sum16(ws, ks, m, n, M, N, v);   // fixed summation order over the K-split slabs
   epi_store16(v, m, n, M, N, C, ldc, ep);
 }
 
@@ -149,7 +143,7 @@ hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* W, int64_
     hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, block, 0, stream, A, lda, W, ldw, C, ldc, w, M, N, K, kchunk, ep);
   if (gy > 1) {
     const int total = M * ((N + 15) / 16);
-    hipLaunchKernelGGL(gemm_skinny_finalize, dim3((total + 255) / 256), dim3(256), 0, stream, ws, gy, C, ldc, M, N,
+    hipLaunchKernelGGL(gemm_skinny_finalize, dim3((total + 63) / 64), dim3(64), 0, stream, ws, gy, C, ldc, M, N,
                        ep);
   }
   return hipGetLastError();

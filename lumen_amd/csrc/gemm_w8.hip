@@ -145,13 +145,7 @@ __global__ void gemm_w8_finalize(const float* __restrict__ ws, int ks, const flo
   if (idx >= M * groups) return;
   const int m = idx / groups, n = (idx - m * groups) * 16;
   float v[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) v[c] = 0.f;
-  for (int s = 0; s < ks; ++s) {
-    const float* p = ws + ((int64_t)s * M + m) * N + n;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) v[c] += n + c < N ? p[c] : 0.f;
-  }
+  splitk_sum16(ws, ks, m, n, M, N, v);
 #pragma unroll
   for (int c = 0; c < 16; ++c) v[c] *= n + c < N ? scale[n + c] : 0.f;
   epi_store16(v, m, n, M, N, C, ldc, ep);
@@ -316,7 +310,7 @@ hipError_t gemm_w8(const uint16_t* A, int64_t lda, const uint8_t* W, int64_t ldw
                          kchunk, ep);
     if (gy > 1) {
       const int total = M * ((N + 15) / 16);
-      hipLaunchKernelGGL(gemm_w8_finalize, dim3((total + 255) / 256), dim3(256), 0, stream, ws, gy, scale, C, ldc, M,
+      hipLaunchKernelGGL(gemm_w8_finalize, dim3((total + 63) / 64), dim3(64), 0, stream, ws, gy, scale, C, ldc, M,
                          N, ep);
     }
     return hipGetLastError();

@@ -63,7 +63,7 @@ def test_gemm_row_scatter_table_f32out():
     assert f.dtype == torch.float32 and _rel(f, x.float() @ w.float().t()) < 1e-2
 
 
-@pytest.mark.parametrize("rows,D", [(1, 64), (257, 1024), (1000, 768), (33, 4096), (7, 896), (5, 3584)])
+@pytest.mark.parametrize("rows,D", [(1, 64), (257, 1024), (1000, 768), (33, 4096), (7, 896), (5, 3584), (64, 8192), (65, 2048)])
 def test_layernorm_rmsnorm(rows, D):
     x = torch.randn(rows, D).bfloat16() * 3
     w = torch.randn(D).bfloat16()
@@ -75,6 +75,24 @@ def test_layernorm_rmsnorm(rows, D):
     ref = ops.rms_norm(x, w, add=add, resid_out=ro_ref)
     got = ops.rms_norm(x.to(DEV), w.to(DEV), add=add.to(DEV), resid_out=ro)
     assert _rel(got, ref) < 1e-2 and _rel(ro, ro_ref) < 1e-2
+
+
+@pytest.mark.parametrize("rows,D", [(1, 4096), (16, 896), (300, 1024)])
+def test_norm_add_inplace_residual(rows, D):
+    """Decode-style fused residual update: resid_out aliases the add operand (block-per-row
+    kernel for few rows, wave-per-row kernel for many), LayerNorm and RMSNorm."""
+    g = torch.Generator().manual_seed(rows)
+    y = torch.randn(rows, D, generator=g).bfloat16()
+    r = torch.randn(rows, D, generator=g).bfloat16() * 4
+    w, b = torch.randn(D, generator=g).bfloat16(), torch.randn(D, generator=g).bfloat16()
+    r_ref = r.clone()
+    ref = ops.layer_norm(y, w, b, add=r_ref, resid_out=r_ref)
+    r_d = r.to(DEV)
+    got = ops.layer_norm(y.to(DEV), w.to(DEV), b.to(DEV), add=r_d, resid_out=r_d)
+    assert _rel(got, ref) < 1e-2 and _rel(r_d, r_ref) < 1e-2
+    ref = ops.rms_norm(y, w, add=r_ref, resid_out=r_ref)
+    got = ops.rms_norm(y.to(DEV), w.to(DEV), add=r_d, resid_out=r_d)
+    assert _rel(got, ref) < 1e-2 and _rel(r_d, r_ref) < 1e-2
 
 
 def test_layernorm_row_gather_and_l2():
