@@ -269,45 +269,52 @@ __device__ __forceinline__ void epi_store8(float* v, int m, int n, int M, int N,
   epi_store8_t<false>(v, m, n, M, N, C, ldc, ep, c_rsrc(C));
 }
 
-// Sum of the K-split fp32 slabs ws[s][M][N] for s = 0..ks-1 (fixed order: deterministic) at
-// row m, columns n..n+15.  The finalize passes of the skinny decode GEMMs run with only
-// M * N / 16 threads (256 for N = 4096), so a serial per-slab loop pays one dependent HBM
-// latency per split (~10 us at ks = 4, measured); here the loads of 4 slabs are issued
-// before any is consumed (one round trip per 4 slabs), as 16-B loads when N % 4 == 0.
-__device__ __forceinline__ void splitk_sum16(const float* __restrict__ ws, int ks, int m, int n, int M, int N,
-                                             float* v) {
-#pragma unroll
-  for (int c = 0; c < 16; ++c) v[c] = 0.f;
+// In-launch split-K reduction of the skinny decode GEMMs (the counter form of the
+// write-through hand-off, cdna_hip_programming.md §6 G16 / MI355X_MICROARCH.md: per-XCD
+// L2s are not coherent, and a __threadfence() per block costs ~4x the whole GEMM).
+// Called by every thread once `red` ([4 waves][rows][17] LDS partials) is complete:
+//   1. the workgroup's summed partial tile goes to its fp32 slab with agent-scope
+//      (sc1, write-through) stores, drained by every wave before the barrier;
+//   2. lane 0 draws a ticket from the tile's counter (relaxed agent fetch_add); the
+//      workgroup that draws nsplit-1 arrived last, resets the counter (buffer is
+//      all-zero between kernels) and tells its waves through red's padding column;
+//   3. the last arriver reads every slab with sc1 loads and sums them in split order
+//      (deterministic, independent of arrival order) into red[1][m][c].
+// No release/acquire fences: sc1 stores leave L2 before the ticket, sc1 loads bypass L1.
+template <int ROWS>
+__device__ __forceinline__ bool splitk_reduce_last(float (&red)[4][ROWS][17], float* ws, uint32_t* cnt, int M, int N,
+                                                   int n0) {
+  const int tid = threadIdx.x;
   const int64_t slab = (int64_t)M * N;
-  const float* p0 = ws + (int64_t)m * N + n;
-  if ((N & 3) == 0 && n + 16 <= N) {
-    int s = 0;
-    for (; s + 4 <= ks; s += 4) {
-      f32x4_t x[4][4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) x[u][q] = *(const f32x4_t*)(p0 + (s + u) * slab + 4 * q);
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[4 * q + e] += x[u][q][e];
-    }
-    for (; s < ks; ++s) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4_t x = *(const f32x4_t*)(p0 + s * slab + 4 * q);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[4 * q + e] += x[e];
-      }
-    }
-  } else {
-    for (int s = 0; s < ks; ++s)
-#pragma unroll
-      for (int c = 0; c < 16; ++c) v[c] += n + c < N ? p0[s * slab + c] : 0.f;
+  float* mine = ws + (int64_t)blockIdx.y * slab;
+  for (int idx = tid; idx < ROWS * 16; idx += blockDim.x) {
+    const int m = idx >> 4, c = idx & 15;
+    if (m < M && n0 + c < N)
+      __hip_atomic_store(mine + (int64_t)m * N + n0 + c, red[0][m][c] + red[1][m][c] + red[2][m][c] + red[3][m][c],
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = prev == gridDim.y - 1;
+    if (last) __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    red[0][0][16] = last ? 1.f : 0.f;
+  }
+  __syncthreads();
+  if (red[0][0][16] == 0.f) return false;
+  for (int idx = tid; idx < ROWS * 16; idx += blockDim.x) {
+    const int m = idx >> 4, c = idx & 15;
+    float v = 0.f;
+    if (m < M && n0 + c < N) {
+      const float* p = ws + (int64_t)m * N + n0 + c;
+      for (int s = 0; s < (int)gridDim.y; ++s)
+        v += __hip_atomic_load(p + s * slab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    red[1][m][c] = v;
+  }
+  __syncthreads();
+  return true;
 }
 
 }  // namespace lumen

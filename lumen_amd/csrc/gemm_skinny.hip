@@ -6,9 +6,10 @@
 //     interleaved 32-wide k-steps of that range (split-K inside the workgroup,
 //     reduced through LDS), and grid.y splits K further across workgroups so that
 //     even N = 896 launches ~1000 workgroups (each K-split writes its fp32 partial
-//     slab, then a finalize pass sums the slabs in split order — deterministic, so
-//     hipGraph replays and eager launches give bitwise-identical logits — and
-//     applies the epilogue);
+//     slab; the last split of a tile to arrive — per-tile atomic counter — sums the
+//     slabs in split order — deterministic, so hipGraph replays and eager launches
+//     give bitwise-identical logits — and applies the epilogue, with no second
+//     kernel launch);
 //   * both MFMA operands come straight from global memory in fragment layout:
 //     B = W^T (lane: 16 contiguous bytes of weight row n0 + (lane & 15)), A = the
 //     activations (L2-resident, shared by every workgroup), 16 rows per MFMA row
@@ -26,7 +27,8 @@ template <int MT>
 __global__ void __launch_bounds__(256) gemm_skinny_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                           const uint16_t* __restrict__ W, int64_t ldw,
                                                           void* __restrict__ C, int64_t ldc, float* __restrict__ ws,
-                                                          int M, int N, int K, int kchunk, GemmEpi ep) {
+                                                          uint32_t* __restrict__ cnt, int M, int N, int K, int kchunk,
+                                                          GemmEpi ep) {
   __shared__ float red[4][MT * 16][17];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -85,12 +87,13 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const uint16_t* __rest
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wid][t * 16 + 4 * g + r][col] = acc[t][r];
   __syncthreads();
-  if (ws != nullptr) {
-    float* slab = ws + (int64_t)blockIdx.y * M * N;
-    for (int idx = tid; idx < MT * 16 * 16; idx += 256) {
-      const int m = idx >> 4, c = idx & 15;
-      if (m < M && n0 + c < N)
-        slab[(int64_t)m * N + n0 + c] = red[0][m][c] + red[1][m][c] + red[2][m][c] + red[3][m][c];
+  if (ws != nullptr) {   // K split over grid.y: the last split to arrive reduces + runs the epilogue
+    if (!splitk_reduce_last(red, ws, cnt, M, N, n0)) return;
+    if (tid < M) {
+      float v[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] = red[1][tid][c];
+      epi_store16(v, tid, n0, M, N, C, ldc, ep);
     }
     return;
   }
@@ -105,17 +108,6 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const uint16_t* __rest
   }
 }
 
-__global__ void gemm_skinny_finalize(const float* __restrict__ ws, int ks, void* __restrict__ C, int64_t ldc, int M,
-                                     int N, GemmEpi ep) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;   // one thread per (m, 16-column group)
-  const int groups = (N + 15) / 16;
-  if (idx >= M * groups) return;
-  const int m = idx / groups, n = (idx - m * groups) * 16;
-  float v[16];
-  splitk_sum16(ws, ks, m, n, M, N, v);   // fixed summation order over the K-split slabs
-  epi_store16(v, m, n, M, N, C, ldc, ep);
-}
-
 // workgroups across K so that the grid reaches ~target workgroups; each keeps >= 512 of K
 int skinny_ksplit(int N, int K) {
   const int ntiles = (N + 15) / 16;
@@ -128,7 +120,7 @@ int skinny_ksplit(int N, int K) {
 }
 
 hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
-                       int N, int K, const GemmEpi& ep, float* ws, int ksplit, hipStream_t stream) {
+                       int N, int K, const GemmEpi& ep, float* ws, uint32_t* cnt, int ksplit, hipStream_t stream) {
   if (M <= 0 || M > 32 || K % 32 != 0) return hipErrorInvalidValue;
   // K chunk per workgroup: a multiple of 32 * 4 waves
   int kchunk = (K + ksplit - 1) / ksplit;
@@ -137,15 +129,13 @@ hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* W, int64_
   dim3 grid((N + 15) / 16, gy), block(256);
   float* w = gy > 1 ? ws : nullptr;
   if (gy > 1 && ws == nullptr) return hipErrorInvalidValue;
+  if (gy > 1 && cnt == nullptr) return hipErrorInvalidValue;
   if (M <= 16)
-    hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, block, 0, stream, A, lda, W, ldw, C, ldc, w, M, N, K, kchunk, ep);
-  else
-    hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, block, 0, stream, A, lda, W, ldw, C, ldc, w, M, N, K, kchunk, ep);
-  if (gy > 1) {
-    const int total = M * ((N + 15) / 16);
-    hipLaunchKernelGGL(gemm_skinny_finalize, dim3((total + 63) / 64), dim3(64), 0, stream, ws, gy, C, ldc, M, N,
+    hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, block, 0, stream, A, lda, W, ldw, C, ldc, w, cnt, M, N, K, kchunk,
                        ep);
-  }
+  else
+    hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, block, 0, stream, A, lda, W, ldw, C, ldc, w, cnt, M, N, K, kchunk,
+                       ep);
   return hipGetLastError();
 }
 

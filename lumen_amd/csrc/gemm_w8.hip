@@ -48,7 +48,7 @@ template <int MT>
 __global__ void __launch_bounds__(256) gemm_skinny_w8_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                              const uint8_t* __restrict__ W, int64_t ldw,
                                                              const float* __restrict__ scale, void* __restrict__ C,
-                                                             int64_t ldc, float* __restrict__ ws, int M, int N, int K,
+                                                             int64_t ldc, float* __restrict__ ws, uint32_t* __restrict__ cnt, int M, int N, int K,
                                                              int kchunk, GemmEpi ep) {
   __shared__ float red[4][MT * 16][17];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -117,12 +117,15 @@ __global__ void __launch_bounds__(256) gemm_skinny_w8_kernel(const uint16_t* __r
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wid][t * 16 + 4 * g + r][col] = acc[t][r];
   __syncthreads();
-  if (ws != nullptr) {
-    float* slab = ws + (int64_t)blockIdx.y * M * N;
-    for (int idx = tid; idx < MT * 16 * 16; idx += 256) {
-      const int m = idx >> 4, c = idx & 15;
-      if (m < M && n0 + c < N)
-        slab[(int64_t)m * N + n0 + c] = red[0][m][c] + red[1][m][c] + red[2][m][c] + red[3][m][c];
+  if (ws != nullptr) {   // K split over grid.y: the last split to arrive reduces + runs the epilogue
+    if (!splitk_reduce_last(red, ws, cnt, M, N, n0)) return;
+    if (tid < M) {
+      float v[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] = red[1][tid][c];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] *= n0 + c < N ? scale[n0 + c] : 0.f;
+      epi_store16(v, tid, n0, M, N, C, ldc, ep);
     }
     return;
   }
@@ -136,19 +139,6 @@ __global__ void __launch_bounds__(256) gemm_skinny_w8_kernel(const uint16_t* __r
       epi_store16(v, m, n0, M, N, C, ldc, ep);
     }
   }
-}
-
-__global__ void gemm_w8_finalize(const float* __restrict__ ws, int ks, const float* __restrict__ scale,
-                                 void* __restrict__ C, int64_t ldc, int M, int N, GemmEpi ep) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  const int groups = (N + 15) / 16;
-  if (idx >= M * groups) return;
-  const int m = idx / groups, n = (idx - m * groups) * 16;
-  float v[16];
-  splitk_sum16(ws, ks, m, n, M, N, v);
-#pragma unroll
-  for (int c = 0; c < 16; ++c) v[c] *= n + c < N ? scale[n + c] : 0.f;
-  epi_store16(v, m, n, M, N, C, ldc, ep);
 }
 
 // ============================================================================ prefill
@@ -293,26 +283,22 @@ static hipError_t launch_w8(const uint16_t* A, int64_t lda, const uint8_t* W, in
 int skinny_ksplit(int N, int K);
 
 hipError_t gemm_w8(const uint16_t* A, int64_t lda, const uint8_t* W, int64_t ldw, const float* scale, void* C,
-                   int64_t ldc, int M, int N, int K, const GemmEpi& ep, float* ws, int ksplit, hipStream_t stream) {
+                   int64_t ldc, int M, int N, int K, const GemmEpi& ep, float* ws, uint32_t* cnt, int ksplit,
+                   hipStream_t stream) {
   if (K % 64 != 0 || M <= 0) return hipErrorInvalidValue;
   if (M <= 32) {
     int kchunk = (K + ksplit - 1) / ksplit;
     kchunk = (kchunk + 255) / 256 * 256;   // whole 64-wide blocks for each of the 4 waves
     const int gy = (K + kchunk - 1) / kchunk;
-    if (gy > 1 && ws == nullptr) return hipErrorInvalidValue;
+    if (gy > 1 && (ws == nullptr || cnt == nullptr)) return hipErrorInvalidValue;
     dim3 grid((N + 15) / 16, gy), block(256);
     float* w = gy > 1 ? ws : nullptr;
     if (M <= 16)
-      hipLaunchKernelGGL(gemm_skinny_w8_kernel<1>, grid, block, 0, stream, A, lda, W, ldw, scale, C, ldc, w, M, N, K,
-                         kchunk, ep);
+      hipLaunchKernelGGL(gemm_skinny_w8_kernel<1>, grid, block, 0, stream, A, lda, W, ldw, scale, C, ldc, w, cnt, M,
+                         N, K, kchunk, ep);
     else
-      hipLaunchKernelGGL(gemm_skinny_w8_kernel<2>, grid, block, 0, stream, A, lda, W, ldw, scale, C, ldc, w, M, N, K,
-                         kchunk, ep);
-    if (gy > 1) {
-      const int total = M * ((N + 15) / 16);
-      hipLaunchKernelGGL(gemm_w8_finalize, dim3((total + 63) / 64), dim3(64), 0, stream, ws, gy, scale, C, ldc, M,
-                         N, ep);
-    }
+      hipLaunchKernelGGL(gemm_skinny_w8_kernel<2>, grid, block, 0, stream, A, lda, W, ldw, scale, C, ldc, w, cnt, M,
+                         N, K, kchunk, ep);
     return hipGetLastError();
   }
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);

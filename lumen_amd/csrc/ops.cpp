@@ -12,6 +12,9 @@
 #include <hip/hip_runtime.h>
 
 #include <vector>
+#include <mutex>
+#include <unordered_map>
+#include <algorithm>
 
 #include "gemm_epi.h"
 #include "conv.h"
@@ -20,9 +23,10 @@ namespace lumen {
 hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
                      int64_t ldc, int M, int N, int K, const GemmEpi& ep, int tile, hipStream_t stream);
 hipError_t gemm_w8(const uint16_t* A, int64_t lda, const uint8_t* W, int64_t ldw, const float* scale, void* C,
-                   int64_t ldc, int M, int N, int K, const GemmEpi& ep, float* ws, int ksplit, hipStream_t stream);
+                   int64_t ldc, int M, int N, int K, const GemmEpi& ep, float* ws, uint32_t* cnt, int ksplit,
+                   hipStream_t stream);
 hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
-                       int N, int K, const GemmEpi& ep, float* ws, int ksplit, hipStream_t stream);
+                       int N, int K, const GemmEpi& ep, float* ws, uint32_t* cnt, int ksplit, hipStream_t stream);
 int skinny_ksplit(int N, int K);
 hipError_t norm_rows(const uint16_t* x, int64_t x_stride, const int64_t* row_idx, const uint16_t* add,
                      int64_t add_stride, uint16_t* resid_out, int64_t resid_stride, const uint16_t* w,
@@ -60,6 +64,24 @@ namespace {
   } while (0)
 
 inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+// Split-K arrival counters of the skinny (decode) GEMMs, one per 16-column tile.  The
+// last K-split workgroup of a tile to arrive reduces the slabs and resets its counter
+// to 0, so the buffer is all-zero between kernels.  Kept per (device, stream): split-K
+// GEMMs on different streams may run concurrently and must not share tiles.  A buffer
+// first requested inside a stream capture comes from the graph's pool and its zero-fill
+// is captured too (harmless on replay: the counters are zero between kernels anyway).
+uint32_t* splitk_counters(const at::Tensor& like, int64_t tiles) {
+  static std::mutex mu;
+  static std::unordered_map<uint64_t, at::Tensor> bufs;
+  const auto st = c10::hip::getCurrentHIPStream();
+  const uint64_t key = ((uint64_t)(uint8_t)like.device().index() << 56) ^ (uint64_t)st.id();
+  std::lock_guard<std::mutex> g(mu);
+  at::Tensor& t = bufs[key];
+  if (!t.defined() || t.numel() < tiles)
+    t = at::zeros({std::max<int64_t>(tiles, 16384)}, like.options().dtype(at::kInt));
+  return reinterpret_cast<uint32_t*>(t.data_ptr());
+}
 inline const uint16_t* bf(const at::Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
 inline uint16_t* bfm(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
 
@@ -132,8 +154,10 @@ void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tens
     const int ks = lumen::skinny_ksplit((int)N, (int)K);
     at::Tensor ws;
     if (ks > 1) ws = at::empty({ks, M, N}, a.options().dtype(at::kFloat));   // per-split slabs, no zero-fill
+    uint32_t* cnt = ks > 1 ? splitk_counters(a, (N + 15) / 16) : nullptr;
     LUMEN_CHECK_HIP(lumen::gemm_skinny(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0), (int)M,
-                                       (int)N, (int)K, ep, ks > 1 ? ws.data_ptr<float>() : nullptr, ks, cur_stream()));
+                                       (int)N, (int)K, ep, ks > 1 ? ws.data_ptr<float>() : nullptr, cnt, ks,
+                                       cur_stream()));
     return;
   }
   LUMEN_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
@@ -174,13 +198,17 @@ void gemm_w8(const at::Tensor& a, const at::Tensor& w8, const at::Tensor& scale,
   const at::DeviceGuard guard(a.device());
   int ks = 1;
   at::Tensor ws;
+  uint32_t* cnt = nullptr;
   if (M <= 32) {
     ks = lumen::skinny_ksplit((int)N, (int)K);
-    if (ks > 1) ws = at::empty({ks, M, N}, a.options().dtype(at::kFloat));
+    if (ks > 1) {
+      ws = at::empty({ks, M, N}, a.options().dtype(at::kFloat));
+      cnt = splitk_counters(a, (N + 15) / 16);
+    }
   }
   LUMEN_CHECK_HIP(lumen::gemm_w8(bf(a), a.stride(0), reinterpret_cast<const uint8_t*>(w8.data_ptr()), w8.stride(0),
                                  scale.data_ptr<float>(), out.data_ptr(), out.stride(0), (int)M, (int)N, (int)K, ep,
-                                 ks > 1 ? ws.data_ptr<float>() : nullptr, ks, cur_stream()));
+                                 ks > 1 ? ws.data_ptr<float>() : nullptr, cnt, ks, cur_stream()));
 }
 
 // profiling: plain GEMM with per-workgroup timestamps (start, prologue, K-loop, epilogue) in dbg [wg, 4]
