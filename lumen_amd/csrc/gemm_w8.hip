@@ -16,6 +16,8 @@
 //  * gemm_w8_kernel (M > 32, prefill): register-staged 2-stage tile; the W tile is
 //    loaded as 8 fp8 per chunk and widened to bf16 on its way into the swizzled LDS
 //    image, after which the MFMA loop is the bf16 one.
+#include <cstdlib>
+
 #include "common.h"
 #include "gemm_epi.h"
 
@@ -42,9 +44,9 @@ __device__ __forceinline__ void fp8x16_to_bf16(const u32x4_t w, bf16x8_t& f0, bf
 }
 
 // ============================================================================ decode
-constexpr int W8_UNROLL = 4;
-
-template <int MT>
+// UNR: 64-wide k blocks loaded per wave before any MFMA issues; NT: weights streamed with
+// non-temporal loads (read once per token; keep L2 for the activations / KV)
+template <int MT, int W8_UNROLL, bool NT>
 __global__ void __launch_bounds__(256) gemm_skinny_w8_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                              const uint8_t* __restrict__ W, int64_t ldw,
                                                              const float* __restrict__ scale, void* __restrict__ C,
@@ -98,7 +100,7 @@ __global__ void __launch_bounds__(256) gemm_skinny_w8_kernel(const uint16_t* __r
 #pragma unroll
     for (int u = 0; u < W8_UNROLL; ++u) {
       const int k = k_begin + (s + 4 * u) * 64;
-      wf[u] = *(const u32x4_t*)(wr + k);
+      wf[u] = NT ? __builtin_nontemporal_load((const u32x4_t*)(wr + k)) : *(const u32x4_t*)(wr + k);
       load_a(k, af[u]);
     }
 #pragma unroll
@@ -106,7 +108,7 @@ __global__ void __launch_bounds__(256) gemm_skinny_w8_kernel(const uint16_t* __r
   }
   for (; s < nblk; s += 4) {
     const int k = k_begin + s * 64;
-    const u32x4_t wf = *(const u32x4_t*)(wr + k);
+    const u32x4_t wf = NT ? __builtin_nontemporal_load((const u32x4_t*)(wr + k)) : *(const u32x4_t*)(wr + k);
     u32x4_t af[MT][2];
     load_a(k, af);
     mma_block(wf, af);
@@ -293,12 +295,25 @@ hipError_t gemm_w8(const uint16_t* A, int64_t lda, const uint8_t* W, int64_t ldw
     if (gy > 1 && (ws == nullptr || cnt == nullptr)) return hipErrorInvalidValue;
     dim3 grid((N + 15) / 16, gy), block(256);
     float* w = gy > 1 ? ws : nullptr;
-    if (M <= 16)
-      hipLaunchKernelGGL(gemm_skinny_w8_kernel<1>, grid, block, 0, stream, A, lda, W, ldw, scale, C, ldc, w, cnt, M,
-                         N, K, kchunk, ep);
-    else
-      hipLaunchKernelGGL(gemm_skinny_w8_kernel<2>, grid, block, 0, stream, A, lda, W, ldw, scale, C, ldc, w, cnt, M,
-                         N, K, kchunk, ep);
+    // LUMEN_W8_SKINNY: bit 0 = non-temporal weight loads, bit 1 = 8 k blocks per wave in flight
+    static const int variant = [] {
+      const char* e = getenv("LUMEN_W8_SKINNY");
+      return e ? atoi(e) & 3 : 0;
+    }();
+#define W8_LAUNCH(MT_, U_, NT_)                                                                                   \
+  hipLaunchKernelGGL((gemm_skinny_w8_kernel<MT_, U_, NT_>), grid, block, 0, stream, A, lda, W, ldw, scale, C, ldc, w, \
+                     cnt, M, N, K, kchunk, ep)
+    if (M <= 16) {
+      switch (variant) {
+        case 1: W8_LAUNCH(1, 4, true); break;
+        case 2: W8_LAUNCH(1, 8, false); break;
+        case 3: W8_LAUNCH(1, 8, true); break;
+        default: W8_LAUNCH(1, 4, false);
+      }
+    } else {
+      W8_LAUNCH(2, 4, false);
+    }
+#undef W8_LAUNCH
     return hipGetLastError();
   }
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
