@@ -20,6 +20,7 @@ the candidates for sampling).  Weights can be loaded from HF Qwen2/Llama state d
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import asdict, dataclass, field
 from typing import Optional
 
@@ -28,6 +29,25 @@ from torch import nn
 
 from .. import ops
 from ..ops import llm as lops
+
+# Prefill-shaped projections (>= _PREFILL_BLAS_MIN_ROWS tokens) without a fused SwiGLU go
+# through hipBLASLt: at M = 624 on Llama-3-8B it measured 1.7-1.9x the hand-written MFMA
+# kernels on qkv / o / down (profiles/r1_prefill_gemm_bench_v1.json: 37 / 31 / 88 us vs
+# 69 / 56 / 151 us for the fp8-weight kernel), while decode (M <= 32) stays on the skinny
+# split-K kernels.  With fp8 weights the layer also keeps a bf16 image of the DEQUANTISED
+# fp8 weight for this path (same numerics as the fp8 kernel; +14 GB for Llama-3-8B, cheap
+# against 288 GB of HBM per GPU).  gate|up: hipBLASLt GEMM + one HBM-bound SwiGLU pass
+# (ops.llm.swiglu_rows) instead of the fused-SwiGLU MFMA kernel (132 + ~10 vs 196 us).
+_PREFILL_BLAS = os.environ.get("LUMEN_LLM_PREFILL_BLAS", "1") != "0"
+_PREFILL_BLAS_MIN_ROWS = int(os.environ.get("LUMEN_LLM_PREFILL_BLAS_MIN_ROWS", "128"))
+_PREFILL_BLAS_NAMES = ("qkv", "o", "gu", "down")
+# the unfused gate|up (+ SwiGLU pass) only pays on wide layers: on Qwen2-0.5B (K = 896) it
+# cost FastVLM 1.6 ms of TTFT, on Llama-3-8B (K = 4096) it saved 0.9 ms
+_PREFILL_BLAS_GLU_MIN_K = int(os.environ.get("LUMEN_LLM_PREFILL_BLAS_GLU_MIN_K", "2048"))
+
+
+def _prefill_blas_ok(name: str, K: int) -> bool:
+    return _PREFILL_BLAS and name in _PREFILL_BLAS_NAMES and (name != "gu" or K >= _PREFILL_BLAS_GLU_MIN_K)
 
 
 @dataclass
@@ -215,6 +235,8 @@ class LLM(nn.Module):
                 w8, sc = ops.quantize_fp8_rows(getattr(l, name + "_w"))
                 setattr(l, name + "_w", nn.Parameter(w8, requires_grad=False))
                 l.register_buffer(name + "_s", sc, persistent=False)
+                if w8.is_cuda and _prefill_blas_ok(name, w8.shape[1]):
+                    l.register_buffer(name + "_wb", (w8.float() * sc[:, None]).to(torch.bfloat16), persistent=False)
         if lm_head and self.lm_head is not None:
             w8, sc = ops.quantize_fp8_rows(self.lm_head)
             self.lm_head = nn.Parameter(w8, requires_grad=False)
@@ -222,8 +244,25 @@ class LLM(nn.Module):
         self.weight_dtype = "fp8"
 
     @staticmethod
-    def _lin(x, l, name, **kw):
-        return ops.linear(x, getattr(l, name + "_w"), w_scale=getattr(l, name + "_s", None), **kw)
+    def _lin(x, l, name, bias=None, residual=None, out=None, glu=False):
+        w = getattr(l, name + "_w")
+        if x.is_cuda and x.shape[0] >= _PREFILL_BLAS_MIN_ROWS and _prefill_blas_ok(name, x.shape[-1]):
+            wb = getattr(l, name + "_wb", None)
+            if wb is None and w.dtype == torch.bfloat16:
+                wb = w
+            if wb is not None and x.dtype == torch.bfloat16:
+                if glu:
+                    assert bias is None and residual is None
+                    return lops.swiglu_rows(torch.mm(x, wb.t()), out=out)
+                if residual is not None:                      # out += x @ W^T (in place on the residual stream)
+                    assert out is None or out.data_ptr() == residual.data_ptr()
+                    return residual.addmm_(x, wb.t())
+                if bias is not None:
+                    b = bias.to(x.dtype)
+                    return torch.addmm(b, x, wb.t(), out=out) if out is not None else torch.addmm(b, x, wb.t())
+                return torch.mm(x, wb.t(), out=out) if out is not None else torch.mm(x, wb.t())
+        return ops.linear(x, w, bias=bias, residual=residual, out=out, glu=glu,
+                          w_scale=getattr(l, name + "_s", None))
 
     # ------------------------------------------------------------------ collectives
     def _all_reduce(self, t: torch.Tensor) -> torch.Tensor:
