@@ -21,17 +21,22 @@
 namespace lumen {
 
 // ------------------------------------------------------------------------------ RoPE + KV write
-__global__ void __launch_bounds__(256) rope_kv_kernel(RopeKVArgs a) {
+// grid (T, nrot_blocks + v_blocks): one (token, 256-element chunk) per workgroup and ONE
+// rotation pair / V element per thread, so a decode step (T = 1..16) spreads over 14+
+// workgroups per token instead of looping 10x inside one (each pass of that loop paid a
+// dependent global round trip: 8 us per layer per token, measured)
+__global__ void __launch_bounds__(256) rope_kv_kernel(RopeKVArgs a, int nrot_blocks) {
   const int t = blockIdx.x;
   const int half = a.D >> 1;
-  const int p = a.pos[t];
-  const float2* cs = reinterpret_cast<const float2*>(a.cos_sin) + (int64_t)p * half;
   uint16_t* row = a.qkv + (int64_t)t * a.ld;
   const int64_t slot = a.slots ? a.slots[t] : -1;
   const int64_t blk = slot >= 0 ? (slot >> 6) : 0;
   const int off = (int)(slot & 63);
-  const int nrot = (a.H + a.Hkv) * half;
-  for (int idx = threadIdx.x; idx < nrot; idx += blockDim.x) {
+  if ((int)blockIdx.y < nrot_blocks) {
+    const int idx = blockIdx.y * 256 + threadIdx.x;
+    if (idx >= (a.H + a.Hkv) * half) return;
+    const int p = a.pos[t];
+    const float2* cs = reinterpret_cast<const float2*>(a.cos_sin) + (int64_t)p * half;
     const int hh = idx / half, i = idx - hh * half;
     uint16_t* hp = row + hh * a.D;
     const float x1 = bf2f(hp[i]), x2 = bf2f(hp[i + half]);
@@ -45,19 +50,21 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(RopeKVArgs a) {
       kr[i] = b1;
       kr[i + half] = b2;
     }
+    return;
   }
-  if (slot >= 0) {
-    const uint16_t* vr = row + (a.H + a.Hkv) * a.D;
-    for (int idx = threadIdx.x; idx < a.Hkv * a.D; idx += blockDim.x) {
-      const int kh = idx / a.D, d = idx - kh * a.D;
-      a.v_cache[((blk * a.Hkv + kh) * a.D + d) * KV_BLOCK + off] = vr[idx];
-    }
-  }
+  if (slot < 0) return;
+  const int idx = (blockIdx.y - nrot_blocks) * 256 + threadIdx.x;
+  if (idx >= a.Hkv * a.D) return;
+  const uint16_t* vr = row + (a.H + a.Hkv) * a.D;
+  const int kh = idx / a.D, d = idx - kh * a.D;
+  a.v_cache[((blk * a.Hkv + kh) * a.D + d) * KV_BLOCK + off] = vr[idx];
 }
 
 hipError_t rope_kv(const RopeKVArgs& a, hipStream_t stream) {
   if (a.T == 0) return hipSuccess;
-  hipLaunchKernelGGL(rope_kv_kernel, dim3(a.T), dim3(256), 0, stream, a);
+  const int nrot_blocks = ((a.H + a.Hkv) * (a.D / 2) + 255) / 256;
+  const int v_blocks = a.slots ? (a.Hkv * a.D + 255) / 256 : 0;
+  hipLaunchKernelGGL(rope_kv_kernel, dim3(a.T, nrot_blocks + v_blocks), dim3(256), 0, stream, a, nrot_blocks);
   return hipGetLastError();
 }
 
