@@ -16,6 +16,8 @@
 //     tile, rows >= M zero;
 //   * 4 k-steps are loaded before any MFMA issues (64 B of W in flight per lane).
 // The epilogue is the shared GemmEpi (bias / act / residual / SwiGLU / f32 out).
+#include <cstdlib>
+
 #include "common.h"
 #include "gemm_epi.h"
 
@@ -111,7 +113,11 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const uint16_t* __rest
 // workgroups across K so that the grid reaches ~target workgroups; each keeps >= 512 of K
 int skinny_ksplit(int N, int K) {
   const int ntiles = (N + 15) / 16;
-  const int target = 1024;
+  static const int target = [] {   // LUMEN_SKINNY_TARGET_WG: workgroups the K split aims for
+    const char* e = getenv("LUMEN_SKINNY_TARGET_WG");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 256;   // swept 256..2048 on the Llama-3-8B decode shapes: 256 fastest (profiles/r1_ksplit_sweep_v1.jsonl)
+  }();
   int ks = (target + ntiles - 1) / ntiles;
   const int kmax = K / 512 > 1 ? K / 512 : 1;
   ks = ks < kmax ? ks : kmax;
