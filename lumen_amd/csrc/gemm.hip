@@ -31,7 +31,6 @@
 
 namespace lumen {
 
-constexpr int BK = 64;  // K elements per tile = 128-byte LDS rows
 
 // ============================================================================
 // Generic register-staged kernel
@@ -176,12 +175,6 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda,
 // for quadrants qm, qn in {0,1}: quadrant (qm, qn) reads only A-half qm and
 // B-half qn, so half-tiles can be streamed and retired independently.
 // LDS: [buf 2][op 2 (A,B)][half 2][128 rows][128 B] = 128 KiB.
-constexpr int G_HALF = 128 * 128;       // bytes per half-tile image
-constexpr int G_OP = 2 * G_HALF;
-constexpr int G_BUF = 2 * G_OP;
-
-__device__ __forceinline__ void vm_wait4() { asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
-__device__ __forceinline__ void vm_wait0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 
 // Row-coalesced epilogue of the 256x256 kernels (8 waves, wave (wm, wn) holding
@@ -444,23 +437,7 @@ gemm_glds_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
 // operands: ~15 us per tile at K = 1024, a third of the tile's MFMA time.
 // Same phase schedule / counted vmcnt / raw barriers as gemm_glds_kernel<1>.
 // ============================================================================
-__device__ __forceinline__ void tile_coords(int lin, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
-  if (group_m > 1) {
-    const int span = group_m * tiles_n;
-    const int grp = lin / span, first = grp * group_m;
-    const int gsz = min(tiles_m - first, group_m);
-    const int r = lin % span;
-    tm = first + r % gsz;
-    tn = r / gsz;
-  } else {
-    tm = lin / tiles_n;
-    tn = lin % tiles_n;
-  }
-}
 
-#ifndef LUMEN_GEMM_RES_PREFETCH
-#define LUMEN_GEMM_RES_PREFETCH 4
-#endif
 // FK > 0 (FAST): every tile interior (M, N multiples of 256), bf16 output, optional bf16
 // bias (FK-1 bit 0) / activation / residual (FK-1 bit 1) -> bias + residual prefetched, no
 // bounds checks, and every VMEM count static so hipcc's own waits are exact (chosen on the
@@ -995,7 +972,8 @@ static hipError_t launch_persist(const uint16_t* A, int64_t lda, const uint16_t*
 // (+ 10 * group_m + 100 * epilogue variant + 1000 to disable the tail split):
 //   0 = 256x256 register-staged, 1 = 128x128, 2 = 64x64, 3 = 32x64, 4 = 256x256 LDS-DMA phased,
 //   5 = 4 + setprio, 6 = one wait per K-tile, 7 = persistent 256x256 (cross-tile prefetch),
-//   8 = 256x256 on the 10-slot half-tile ring (deeper prefetch)
+//   8 = 256x256 on the 10-slot half-tile ring (deeper prefetch), 9 = 256x256 ping-pong (epilogue digit:
+//   bit 0 write-through C, bit 1 static priority for the lagging wave group)
 hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
                      int64_t ldc, int M, int N, int K, const GemmEpi& ep, int tile,
                      hipStream_t stream) {
@@ -1007,7 +985,9 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
     // measured on MI355X (tools/gemm_bench.py, random bf16, profiles/r1_gemm_epilogue_ab_v1.jsonl):
     // K <= 512: row-coalesced write-through epilogue (+25-30 %); K 1024-2048: persistent
     // kernel (+4-8 %); K >= 4096: per-wave epilogue LDS-DMA kernel
-    if (t256 >= 512) tile = K <= 512 ? 245 : (K <= 2048 ? 47 : 5);
+    // r2: the ping-pong kernel (gemm_pp.hip, two phases per K-tile, static priority for the
+    // lagging wave group) beats all of these at K >= 1024 (profiles/r2_gemm_pp_v2.jsonl)
+    if (t256 >= 512) tile = K <= 512 ? 245 : 609;
     else if (t128 >= 256) tile = 1;
     else if (M <= 64) tile = 3;
     else tile = 2;
@@ -1025,7 +1005,7 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
   // tile time.  Run the largest row range whose tile count is a multiple of 256 on
   // the 256x256 kernel and the few remaining rows on 128x128 tiles (4x more, 4x
   // shorter workgroups) so the tail costs ~1/4 of a round.  Only for plain row maps.
-  if (allow_split && tile >= 4 && tile <= 8 && ep.out_group == 0 && ep.table == nullptr) {
+  if (allow_split && tile >= 4 && tile <= 9 && ep.out_group == 0 && ep.table == nullptr) {
     const int tiles_n = (N + 255) / 256;
     const int tiles_m = (M + 255) / 256;
     int q = 256;
@@ -1043,7 +1023,7 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
       return launch_cfg<128, 128, 2, 2>(A + (int64_t)M0 * lda, lda, W, ldw, C2, ldc, M - M0, N, K, e2, stream);
     }
   }
-  if (tile >= 4 && tile <= 6) {
+  if ((tile >= 4 && tile <= 6) || tile == 9) {
     // the 256x256 LDS-DMA kernels store C through a 32-bit-offset buffer descriptor
     const int64_t last_row = ep.out_group > 0 ? (int64_t)((M - 1) / ep.out_group) * ep.out_group_stride +
                                                     ep.out_row_offset + (M - 1) % ep.out_group
@@ -1060,6 +1040,7 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
     case 6: return launch_glds<2>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, epi, stream);
     case 7: return launch_persist(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, epi == 3, stream);
     case 8: return launch_ring(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
+    case 9: return gemm_pp(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, epi, stream);
     default: return launch_cfg<32, 64, 1, 2>(A, lda, W, ldw, C, ldc, M, N, K, ep, stream);
   }
 }

@@ -30,6 +30,40 @@ struct GemmEpi {
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
+// ---- shared geometry of the 256x256x64 LDS-DMA kernels (gemm.hip, gemm_pp.hip)
+constexpr int BK = 64;                  // K elements per tile = 128-byte LDS rows
+constexpr int G_HALF = 128 * 128;       // bytes per half-tile image (128 rows x 128 B)
+constexpr int G_OP = 2 * G_HALF;
+constexpr int G_BUF = 2 * G_OP;
+
+#ifndef LUMEN_GEMM_RES_PREFETCH
+#define LUMEN_GEMM_RES_PREFETCH 4
+#endif
+
+__device__ __forceinline__ void vm_wait4() { asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
+__device__ __forceinline__ void vm_wait0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// linear tile id -> (row tile, column tile); group_m > 1 walks group_m row panels per column
+__device__ __forceinline__ void tile_coords(int lin, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
+  if (group_m > 1) {
+    const int span = group_m * tiles_n;
+    const int grp = lin / span, first = grp * group_m;
+    const int gsz = min(tiles_m - first, group_m);
+    const int r = lin % span;
+    tm = first + r % gsz;
+    tn = r / gsz;
+  } else {
+    tm = lin / tiles_n;
+    tn = lin % tiles_n;
+  }
+}
+
+// ping-pong 256x256 GEMM (gemm_pp.hip); variant bit 0: write-through C, bit 1: static
+// priority for the lagging wave group, bit 2: two phases per K-tile (32 MFMAs per phase)
+hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
+                   int N, int K, const GemmEpi& ep, int group_m, int variant, hipStream_t stream);
+
+
 // 16-byte store of C: plain, or write-through (sc1) via a buffer descriptor over C.
 // Write-through matters for the big-tile epilogues: every CU publishing its whole
 // 128 KB C tile at once with plain (write-back) stores drains at ~1.7 TB/s chip-wide

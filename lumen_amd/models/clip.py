@@ -195,21 +195,17 @@ class _Block(nn.Module):
             p.data.copy_(torch.randn(p.shape, generator=gen) * s)
 
 
-# Residual adds of the out-proj / fc2 GEMMs move into the following LayerNorm (add + LN +
-# residual-stream write in one pass) and those two GEMMs become plain bias GEMMs on
-# hipBLASLt, which measured faster than the fused-residual MFMA kernel on exactly these
-# shapes (ViT-L/14 b512: out-proj 0.26 vs 0.36 ms, fc2 K=4096 0.80 vs 1.05 ms; see
-# profiles/r1_gemm_epilogue_fast_v1.jsonl).  qkv (bias) and fc1 (bias + GELU/QuickGELU)
-# stay on the hand-written kernel, which matches or beats hipBLASLt there.
-_BLAS_RESID = os.environ.get("LUMEN_BLAS_RESID", "1") != "0"
+# Two ways to add the out-proj / fc2 residual: in the GEMM epilogue (default; the ping-pong
+# MFMA GEMM adds the prefetched residual rows before its single bf16 rounding), or as a plain
+# bias GEMM followed by an add + LayerNorm + residual-stream-write pass (LUMEN_BLAS_RESID=1).
+# Both run only hand-written kernels; ViT-L/14 b512 measured 5951 vs 5837 img/s
+# (profiles/r2_bench_resid_paths_v1.txt).
+_BLAS_RESID = os.environ.get("LUMEN_BLAS_RESID", "0") != "0"
 _BLAS_RESID_MIN_ROWS = int(os.environ.get("LUMEN_BLAS_RESID_MIN_ROWS", "8192"))
 
 
 def _bias_gemm(a: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: torch.Tensor) -> None:
-    if b is not None:
-        torch.addmm(b, a, w.t(), out=out)
-    else:
-        torch.mm(a, w.t(), out=out)
+    ops.linear(a, w, b, out=out)
 
 
 def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float,

@@ -105,6 +105,32 @@ def _signed64(x: int) -> int:
     return x - (1 << 64) if x >= 1 << 63 else x
 
 
+def _read_external(base_dir: Path, name: str, external: dict) -> bytes:
+    """Read an external-data initializer, confined to the model directory.
+
+    A downloaded pack is untrusted: an absolute ``location`` or one with ``..`` that
+    resolves outside ``base_dir`` is refused (it could pull any host file into a
+    weight tensor), and offset/length are checked against the file size before
+    reading (no unbounded reads of devices such as /dev/zero)."""
+    loc = external.get("location", "")
+    if not loc or Path(loc).is_absolute():
+        raise ValueError(f"tensor {name}: external data location {loc!r} must be a relative path")
+    root = base_dir.resolve()
+    p = (root / loc).resolve()
+    if root != p and root not in p.parents:
+        raise ValueError(f"tensor {name}: external data {loc!r} escapes the model directory")
+    if not p.is_file():
+        raise ValueError(f"tensor {name}: external data file {loc!r} not found")
+    size = p.stat().st_size
+    off = int(external.get("offset", 0))
+    ln = int(external["length"]) if external.get("length") else size - off
+    if off < 0 or ln < 0 or off + ln > size:
+        raise ValueError(f"tensor {name}: external data range [{off}, {off + ln}) outside {loc!r} ({size} B)")
+    with open(p, "rb") as fh:
+        fh.seek(off)
+        return fh.read(ln)
+
+
 def _parse_tensor(b: memoryview, base_dir: Optional[Path]) -> Tensor:
     dims, dtype, name, raw = [], 1, "", None
     floats, int32s, int64s, doubles = [], [], [], []
@@ -141,12 +167,7 @@ def _parse_tensor(b: memoryview, base_dir: Optional[Path]) -> Tensor:
     if location == 1:                          # external data
         if base_dir is None:
             raise ValueError(f"tensor {name}: external data without a model path")
-        p = base_dir / external["location"]
-        off = int(external.get("offset", 0))
-        ln = external.get("length")
-        with open(p, "rb") as fh:
-            fh.seek(off)
-            raw = fh.read(int(ln) if ln else -1)
+        raw = _read_external(Path(base_dir), name, external)
     if dtype == BF16:
         u16 = np.frombuffer(raw, "<u2") if raw is not None else np.asarray(int32s, np.uint16)
         arr = (u16.astype(np.uint32) << 16).view(np.float32)

@@ -1,0 +1,64 @@
+# GPU-box task runner (run through gpurun): bash tools/gpu.sh TASK [TASK ...]
+#
+# Every GPU step runs under its own time limit; the first step that faults, aborts or
+# times out ends the script (no retries).  Outputs land in gpurun_out/.
+#
+#   tests          pytest -m gpu (one process, 120 s per test)
+#   smoke          __graft_entry__.smoke()
+#   bench          headline bench.py (defaults)
+#   prof_bench     rocprofv3 kernel stats of the headline bench (3 steps)
+#   gemm           tools/gemm_bench_tiles.py on the ViT-L/14 shapes ($GEMM_TILES, $GEMM_EPI)
+#   vlm8b / vlm05  tools/vlm_bench.py Llama-3-8B fp8 / FastVLM-0.5B
+#   prof_vlm8b     rocprofv3 kernel stats of the 8B fp8 decode bench
+#   face_ocr       tools/face_ocr_bench.py face + ocr
+#   prof_face / prof_ocr   rocprofv3 kernel stats of the face / OCR bench
+#   pmc_gemm       PMC counters (MFMA, LDS conflicts, busy) of one ViT-L/14 GEMM shape
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+
+step() {   # step NAME SECONDS CMD...  (stdout+stderr -> gpurun_out/NAME.log)
+  local name=$1 secs=$2
+  shift 2
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc"
+  tail -3 "gpurun_out/$name.log"
+  case $rc in 0) ;; *) exit $rc ;; esac
+}
+
+for task in "$@"; do
+  case $task in
+    tests) step tests 1500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 400 python bench.py ;;
+    prof_bench)
+      step prof_bench 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o run -- \
+        python3 bench.py --steps 3 --warmup 1 --text-steps 3 ;;
+    gemm)
+      step gemm 500 python -u tools/gemm_bench_tiles.py --tiles="${GEMM_TILES:--1}" --epi "${GEMM_EPI:-plain}" \
+        --shapes "${GEMM_SHAPES:-vit}" ;;
+    vlm8b) step vlm8b 600 python tools/vlm_bench.py --preset llava-llama3-8b --fp8 ;;
+    vlm05) step vlm05 400 python tools/vlm_bench.py --preset fastvlm-0.5b ;;
+    prof_vlm8b)
+      step prof_vlm8b 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_vlm8b -o run -- \
+        python3 tools/vlm_bench.py --preset llava-llama3-8b --n 3 --warmup 1 --max-new 32 --batch 16 --fp8 ;;
+    face_ocr)
+      step face 400 python tools/face_ocr_bench.py --what face
+      step ocr 400 python tools/face_ocr_bench.py --what ocr ;;
+    prof_face)
+      step prof_face 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_face -o run -- \
+        python3 tools/face_ocr_bench.py --what face --iters 3 ;;
+    prof_ocr)
+      step prof_ocr 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ocr -o run -- \
+        python3 tools/face_ocr_bench.py --what ocr --iters 3 ;;
+    pmc_gemm)
+      step pmc_gemm 120 timeout -s KILL 100 rocprofv3 --kernel-trace \
+        --pmc SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+        -d gpurun_out/pmc_gemm -o run -- python3 tools/gemm_bench_tiles.py --tiles=609 --rounds 1 --iters 2 \
+        --shapes "${GEMM_SHAPES:-131584x3072x1024}" ;;
+    *) echo "unknown task $task"; exit 2 ;;
+  esac
+done
+exit 0
