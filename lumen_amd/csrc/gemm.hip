@@ -972,8 +972,9 @@ static hipError_t launch_persist(const uint16_t* A, int64_t lda, const uint16_t*
 // (+ 10 * group_m + 100 * epilogue variant + 1000 to disable the tail split):
 //   0 = 256x256 register-staged, 1 = 128x128, 2 = 64x64, 3 = 32x64, 4 = 256x256 LDS-DMA phased,
 //   5 = 4 + setprio, 6 = one wait per K-tile, 7 = persistent 256x256 (cross-tile prefetch),
-//   8 = 256x256 on the 10-slot half-tile ring (deeper prefetch), 9 = 256x256 ping-pong (epilogue digit:
-//   bit 0 write-through C, bit 1 static priority for the lagging wave group)
+//   8 = 256x256 on the 10-slot half-tile ring (deeper prefetch), 9 = 256x256 ping-pong (gemm_pp.hip;
+//   hundreds digit = variant: bit 0 persistent, bit 1 static priority for the lagging group, bit 2 two
+//   phases per K-tile)
 hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
                      int64_t ldc, int M, int N, int K, const GemmEpi& ep, int tile,
                      hipStream_t stream) {
@@ -987,7 +988,9 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
     // kernel (+4-8 %); K >= 4096: per-wave epilogue LDS-DMA kernel
     // r2: the ping-pong kernel (gemm_pp.hip, two phases per K-tile, static priority for the
     // lagging wave group) beats all of these at K >= 1024 (profiles/r2_gemm_pp_v2.jsonl)
-    if (t256 >= 512) tile = K <= 512 ? 245 : 609;
+    // residual epilogues at K <= 2048 run the persistent form (next tile's operands stream in
+    // during the residual-reading epilogue: +2-7 %, profiles/r2_gemm_pps_phase_v1.txt)
+    if (t256 >= 512) tile = K <= 512 ? 245 : (ep.residual && K <= 2048 && M % 256 == 0 && N % 256 == 0 ? 709 : 609);
     else if (t128 >= 256) tile = 1;
     else if (M <= 64) tile = 3;
     else tile = 2;

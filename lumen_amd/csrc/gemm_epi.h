@@ -58,8 +58,8 @@ __device__ __forceinline__ void tile_coords(int lin, int tiles_m, int tiles_n, i
   }
 }
 
-// ping-pong 256x256 GEMM (gemm_pp.hip); variant bit 0: write-through C, bit 1: static
-// priority for the lagging wave group, bit 2: two phases per K-tile (32 MFMAs per phase)
+// ping-pong 256x256 GEMM (gemm_pp.hip); variant bit 0: persistent (interior tiles), bit 1:
+// static priority for the lagging wave group, bit 2: two phases per K-tile (32 MFMAs per phase)
 hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
                    int N, int K, const GemmEpi& ep, int group_m, int variant, hipStream_t stream);
 

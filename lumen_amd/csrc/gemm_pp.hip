@@ -320,10 +320,399 @@ static void launch_pp_fk(const uint16_t* A, int64_t lda, const uint16_t* W, int6
   }
 }
 
+// ============================================================================
+// Persistent form of the 2-phase ping-pong kernel (interior tiles: M, N multiples of 256,
+// K / 64 >= 2).  One workgroup per CU walks tiles lin, lin + G, ... as ONE continuous
+// stream of K-tiles ("units"): the LDS-DMA staging of units u + 1 / u + 2 runs across tile
+// boundaries, so the next tile's first operands land while an epilogue runs.
+//
+// Epilogue desynchronisation: with every CU on the same tile schedule, all 256 epilogues
+// store their 128 KiB C tiles in the same few microseconds (32 MiB per round: an HBM write
+// burst with every matrix core idle, ~9 us per tile at K = 1024).  Workgroup slot j (of 32
+// per XCD) therefore starts PHI_j = j * nk / 32 K-tiles into its first tile: it runs
+// K-tiles [PHI, nk) of tile 0, saves that partial accumulator to a private fp32 workspace
+// (fragment order: one coalesced 1 KiB store per register quad), runs tiles 1 .. R-1,
+// and finishes tile 0 with K-tiles [0, PHI) starting from the reloaded partial.  Every
+// workgroup still executes R * nk K-tiles (no imbalance, no inter-workgroup hand-off), but
+// the tile boundaries — and the C write bursts — are spread over the whole tile period.
+//
+// The epilogue stages 16 x 32 fp32 pieces in its own 18 KiB LDS region beside the 128 KiB
+// pipeline.  Its VMEM ops (E per wave, static on the FAST path; 32 for a partial save) sit
+// between staging loads in the in-order vmcnt queue, so the two waits after an epilogue
+// count them in (a count may only under-state the ops issued after the awaited one).
+// ============================================================================
+template <int N>
+__device__ __forceinline__ void vm_wait_i() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+constexpr int PPS_STR = 36;                       // epilogue staging row stride (floats)
+constexpr int PPS_WAVE = 16 * PPS_STR * 4;        // bytes per wave
+constexpr int PPS_LDS = 2 * G_BUF + 8 * PPS_WAVE;
+constexpr int PPS_PART = 8 * 128 * 64 * 4;        // partial accumulator bytes per workgroup
+
+template <int FK, int PRIO>
+__global__ void __launch_bounds__(512)
+gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
+                void* __restrict__ C, int64_t ldc, int M, int N, int K, GemmEpi ep, int group_m,
+                float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int tiles_n = N / 256;
+  const int tiles_m = M / 256;
+  const int ntiles = tiles_n * tiles_m;
+  const int G = gridDim.x;
+  const int lin0 = xcd_remap(blockIdx.x, G);
+  if (lin0 >= ntiles) return;
+  const int nk = K / BK;
+  const int R = (ntiles - lin0 + G - 1) / G;          // tiles of this workgroup
+  // phase offset of the first tile (0: plain tile order).  Keyed by the first tile's row panel:
+  // the workgroups that share an A panel (same row tile, other column tiles) keep the same
+  // schedule and keep reading it from one L2 together; 8 phase classes spread the C bursts.
+  int phi = 0;
+  if (part != nullptr && R >= 2 && nk >= 8) {
+    int tm0, tn0;
+    tile_coords(lin0, tiles_m, tiles_n, group_m, tm0, tn0);
+    phi = ((tm0 & 7) * nk) / 8;
+    if (phi < 3) phi = 0;
+    if (phi > nk - 3) phi = nk - 3;
+  }
+
+
+  int off[4][2];   // per-lane element offsets inside a tile: h 0 = A0, 1 = B0, 2 = B1, 3 = A1
+  int dst[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int g = 2 * wid + i;
+    const int r = g * 8 + (lane >> 3);
+    const int c = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+    dst[i] = g * 1024;
+    off[0][i] = r * (int)lda + c;
+    off[3][i] = (128 + r) * (int)lda + c;
+    off[1][i] = r * (int)ldw + c;
+    off[2][i] = (128 + r) * (int)ldw + c;
+  }
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  typedef const __attribute__((address_space(1))) void* g_ptr_t;
+  // Segments: phi > 0: s = 0 is tile 0 K-tiles [phi, nk), s = 1 .. R-1 tiles 1 .. R-1, s = R
+  // tile 0 K-tiles [0, phi); phi = 0: segment s = tile s.  Every segment has >= 2 K-tiles, so
+  // K-tile u + 2 is at most one segment ahead.
+  const int S = R + (phi > 0 ? 1 : 0);
+  auto seg_info = [&](int s_, int& m0, int& n0, int& kb, int& ke) {
+    const int r = (phi > 0 && s_ == S - 1) ? 0 : s_;
+    int tm, tn;
+    tile_coords(lin0 + r * G, tiles_m, tiles_n, group_m, tm, tn);
+    m0 = tm * 256;
+    n0 = tn * 256;
+    kb = (phi > 0 && s_ == 0) ? phi : 0;
+    ke = (phi > 0 && s_ == S - 1) ? phi : nk;
+  };
+  auto issue = [&](const int h, int buf, int m0, int n0, int kt) {
+    const int hoff = (h == 1 || h == 2 ? G_OP : 0) + (h >= 2 ? G_HALF : 0);
+    const uint16_t* base = (h == 0 || h == 3) ? A + (int64_t)m0 * lda : W + (int64_t)n0 * ldw;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((g_ptr_t)(base + off[h][i] + kt * BK),
+                                       (lds_ptr_t)(smem + buf * G_BUF + hoff + dst[i]), 16, 0, 0);
+  };
+
+  const int frow = lane & 15, fq = lane >> 4;
+  bf16x8_t fa[4][2], fb[2][2][2];
+  auto load_a = [&](const char* base, int qm) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        fa[i][s] = *(const bf16x8_t*)(base + qm * G_HALF + swz(wm * 64 + i * 16 + frow, s * 4 + fq));
+  };
+  auto load_b = [&](const char* base, int qn) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        fb[qn][j][s] = *(const bf16x8_t*)(base + G_OP + qn * G_HALF + swz(wn * 32 + j * 16 + frow, s * 4 + fq));
+  };
+
+  constexpr bool fast = FK > 0;
+  constexpr bool FB = fast && ((FK - 1) & 1), FR = fast && ((FK - 1) & 2);
+  constexpr int E = fast ? 16 + (FB ? 2 : 0) + (FR ? 16 : 0) : 0;   // VMEM ops of one epilogue (0: unknown)
+  constexpr int EP = 32;                                             // VMEM ops of a partial save
+
+  int m0, n0, kb, ke;
+  seg_info(0, m0, n0, kb, ke);
+  // prologue: K-tile kb whole, then A0, B0, B1 of K-tile kb + 1 (every segment has >= 2)
+  issue(0, 0, m0, n0, kb);
+  issue(1, 0, m0, n0, kb);
+  issue(2, 0, m0, n0, kb);
+  issue(3, 0, m0, n0, kb);
+  issue(0, 1, m0, n0, kb + 1);
+  issue(1, 1, m0, n0, kb + 1);
+  issue(2, 1, m0, n0, kb + 1);
+  vm_wait_i<8>();
+  pp_barrier();
+  if (wm == 1) pp_barrier();   // the stagger
+  if constexpr (PRIO == 1) { if (wm == 1) __builtin_amdgcn_s_setprio(1); }
+
+  float* es = (float*)(smem + 2 * G_BUF + wid * PPS_WAVE);
+  // this wave's partial-accumulator slot (32 KiB, fragment order) through a buffer descriptor:
+  // scalar base + lane offset, no per-fragment 64-bit addresses held in VGPRs
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc(part ? part + ((int64_t)blockIdx.x * 8 + wid) * (128 * 64) : (float*)C, (short)0,
+                                        32768, 0x00020000);
+  const __amdgpu_buffer_rsrc_t crs = c_rsrc(C);
+  int T = 0;       // global K-tile counter (LDS buffer parity)
+  int after = 0;   // 0: none, 1: a C epilogue, 2: a partial save since the previous staging
+  for (int sg = 0; sg < S; ++sg) {
+    const bool has_next = sg + 1 < S;
+    int nm0 = m0, nn0 = n0, nkb = 0, nke = 0;
+    if (has_next) seg_info(sg + 1, nm0, nn0, nkb, nke);
+    f32x4_t acc[2][2][4][2];
+    if (phi > 0 && sg == S - 1) {
+      // final segment: tile 0 resumes from its saved partial accumulator
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bq = 0; bq < 2; ++bq)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[a][bq][i][j] = __builtin_bit_cast(
+                  f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(prs, lane * 16, (((a * 2 + bq) * 4 + i) * 2 + j) * 1024, 0));
+      // consume the loads here: otherwise hipcc's wait for them lands after the merge, as a
+      // vmcnt(0) in front of every K-tile's first MFMA (draining the LDS-DMA pipeline)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bq = 0; bq < 2; ++bq)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[a][bq][i][j]));
+    } else {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bq = 0; bq < 2; ++bq)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[a][bq][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    }
+
+#define LUMEN_PPS_CLUSTER(QM, QN)                                                                               \
+    Unroll<0, 4>::run([&](const int i) {                                                                      \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                            \
+      _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                            \
+        acc[QM][QN][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[QN][j][s], acc[QM][QN][i][j], 0, 0, 0); \
+    });
+    for (int kt = kb; kt < ke; ++kt) {
+      const int b = T & 1;
+      const char* base = smem + b * G_BUF;
+      // K-tile T + 1 / T + 2 (possibly in the next segment)
+      const bool c1 = kt + 1 < ke, c2 = kt + 2 < ke;
+      const bool e1 = c1 || has_next, e2 = c2 || has_next;
+      const int k1 = c1 ? kt + 1 : nkb;
+      const int k2 = c2 ? kt + 2 : nkb + (kt + 2 - ke);
+      const int af = kt == kb ? after : 0;
+      // phase 0: rows qm = 0 <- A0, B0, B1; stage A1(T+1); retire A1(T)
+      load_a(base, 0);
+      load_b(base, 0);
+      load_b(base, 1);
+      if (e1) {
+        issue(3, b ^ 1, c1 ? m0 : nm0, c1 ? n0 : nn0, k1);
+        if (af == 0) vm_wait_i<8>(); else if (af == 1) vm_wait_i<8 + E>(); else vm_wait_i<8 + EP>();
+      } else {
+        vm_wait_i<0>();
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      pp_barrier();
+      if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
+      LUMEN_PPS_CLUSTER(0, 0)
+      LUMEN_PPS_CLUSTER(0, 1)
+      if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+      // phase 1: rows qm = 1 <- A1; stage A0, B0, B1 of T+2; retire A0, B0, B1 of T+1
+      load_a(base, 1);
+      if (e2) {
+        const int am = c2 ? m0 : nm0, an = c2 ? n0 : nn0;
+        issue(0, b, am, an, k2);
+        issue(1, b, am, an, k2);
+        issue(2, b, am, an, k2);
+        if (af == 0) vm_wait_i<8>(); else if (af == 1) vm_wait_i<8 + E>(); else vm_wait_i<8 + EP>();
+      } else if (e1) {
+        if (af == 0) vm_wait_i<2>(); else if (af == 1) vm_wait_i<2 + E>(); else vm_wait_i<2 + EP>();
+      } else {
+        vm_wait_i<0>();
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      pp_barrier();
+      if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
+      LUMEN_PPS_CLUSTER(1, 0)
+      LUMEN_PPS_CLUSTER(1, 1)
+      if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+      ++T;
+    }
+#undef LUMEN_PPS_CLUSTER
+
+    if (phi > 0 && sg == 0) {
+      // end of the first (shifted) segment: park the partial accumulator
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bq = 0; bq < 2; ++bq)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, acc[a][bq][i][j]), prs, lane * 16,
+                                                     (((a * 2 + bq) * 4 + i) * 2 + j) * 1024, 0);
+      after = 2;
+    } else {
+      // ---- C epilogue: 16 passes (qm, i, qn) of 16 rows x 32 columns through this wave's
+      // staging region; lane (rr, cq) stores 8 columns (16 B) of one row.
+      const int rr = lane >> 2, cq = lane & 3;
+      constexpr int RD = LUMEN_GEMM_RES_PREFETCH;
+      u32x4_t bq[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+      u32x4_t rz[RD];
+      auto col_of = [&](int qn) { return n0 + qn * 128 + wn * 32 + cq * 8; };
+      auto row_of = [&](int p) { return m0 + (p >> 3) * 128 + wm * 64 + ((p >> 1) & 3) * 16 + rr; };
+      if constexpr (FB) {
+        bq[0] = *(const u32x4_t*)((const uint16_t*)ep.bias + col_of(0));
+        bq[1] = *(const u32x4_t*)((const uint16_t*)ep.bias + col_of(1));
+      }
+      if constexpr (FR) {
+#pragma unroll
+        for (int p = 0; p < RD; ++p) rz[p] = *(const u32x4_t*)(ep.residual + (int64_t)row_of(p) * ep.ldr + col_of(p & 1));
+      }
+      Unroll<0, 16>::run([&](const int p) __attribute__((always_inline)) {
+        const int qm = p >> 3, i = (p >> 1) & 3, qn = p & 1;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int rq = 0; rq < 4; ++rq) es[(fq * 4 + rq) * PPS_STR + j * 16 + frow] = acc[qm][qn][i][j][rq];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        float v[8];
+        {
+          const f32x4_t t0 = *(const f32x4_t*)(es + rr * PPS_STR + cq * 8);
+          const f32x4_t t1 = *(const f32x4_t*)(es + rr * PPS_STR + cq * 8 + 4);
+          v[0] = t0[0]; v[1] = t0[1]; v[2] = t0[2]; v[3] = t0[3];
+          v[4] = t1[0]; v[5] = t1[1]; v[6] = t1[2]; v[7] = t1[3];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int m = row_of(p), n = col_of(qn);
+        if constexpr (fast) {
+          float f[8];
+          unpack8(bq[qn], f);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = v[q] * ep.alpha + f[q];
+          if (ep.act) apply_act_n<8>(v, ep.act);
+          if constexpr (FR) {
+            unpack8(rz[p % RD], f);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] += f[q];
+            if (p + RD < 16) rz[p % RD] = *(const u32x4_t*)(ep.residual + (int64_t)row_of(p + RD) * ep.ldr + col_of((p + RD) & 1));
+          }
+          st16<false>(C, crs, ((int64_t)m * ldc + n) * 2, pack8(v));
+        } else {
+          epi_store8_t<false>(v, m, n, M, N, C, ldc, ep, crs);
+        }
+      });
+      after = 1;
+    }
+    m0 = nm0;
+    n0 = nn0;
+    kb = nkb;
+    ke = nke;
+  }
+  if constexpr (PRIO == 1) { if (wm == 1) __builtin_amdgcn_s_setprio(0); }
+  if (wm == 0) pp_barrier();
+}
+
+static int pp_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+// per-device partial-accumulator workspace of the phase-shifted persistent kernel
+// (PPS_PART bytes per workgroup); allocated once, outside any stream capture
+static float* pps_workspace(int grid, hipStream_t stream) {
+  static float* ws[64] = {nullptr};
+  static int cap[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (cap[dev] >= grid) return ws[dev];
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  // measured slower than the plain tile order on the ViT-L/14 shapes (profiles/r2_gemm_pps_phase_v1.txt:
+  // workgroups of one row-panel class drift apart and lose the shared L2 panel reads): opt-in
+  const char* ph = getenv("LUMEN_GEMM_PHASE");
+  if (ph == nullptr || ph[0] == '0') return nullptr;
+  void* p = nullptr;
+  if (hipMalloc(&p, (size_t)grid * PPS_PART) != hipSuccess) return nullptr;
+  if (ws[dev]) (void)hipFree(ws[dev]);
+  ws[dev] = (float*)p;
+  cap[dev] = grid;
+  return ws[dev];
+}
+
+template <int FK, int PRIO>
+static void launch_pps_t(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
+                         int N, int K, const GemmEpi& ep, int group_m, hipStream_t stream) {
+  const int tiles = (M / 256) * (N / 256);
+  const int grid = tiles < pp_num_cus() ? tiles : pp_num_cus();
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm_pps_kernel<FK, PRIO>, hipFuncAttributeMaxDynamicSharedMemorySize, PPS_LDS);
+    attr_set = true;
+  }
+  float* part = pps_workspace(grid, stream);
+  hipLaunchKernelGGL((gemm_pps_kernel<FK, PRIO>), dim3(grid), dim3(512), PPS_LDS, stream, A, lda, W, ldw, C, ldc, M,
+                     N, K, ep, group_m, part);
+}
+
 hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
                    int N, int K, const GemmEpi& ep, int group_m, int variant, hipStream_t stream) {
+  if (variant & 1) {
+    // persistent form: interior tiles only, 32-bit in-tile offsets, >= 2 K-tiles
+    const bool ok = M % 256 == 0 && N % 256 == 0 && K / BK >= 2 && 255 * lda + K < (1LL << 31) &&
+                    255 * ldw + K < (1LL << 31) && ep.out_group == 0 && !ep.glu && !ep.out_f32;
+    if (ok) {
+      const int64_t extent = (int64_t)M * ldc * 2;
+      const bool fast = !ep.table && !ep.prelu && !ep.post_act && !(ep.bias && ep.bias_f32) &&
+                        extent < ((int64_t)1 << 31);
+      const int fk = fast ? 1 + (ep.bias ? 1 : 0) + (ep.residual ? 2 : 0) : 0;
+      const bool prio1 = (variant & 2) != 0;
+#define LUMEN_PPS_CASE(FKV)                                                                                     \
+      case FKV:                                                                                                 \
+        if (prio1) launch_pps_t<FKV, 1>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);                  \
+        else launch_pps_t<FKV, 0>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);                        \
+        break;
+      switch (fk) {
+        LUMEN_PPS_CASE(1)
+        LUMEN_PPS_CASE(2)
+        LUMEN_PPS_CASE(3)
+        LUMEN_PPS_CASE(4)
+        default:
+        LUMEN_PPS_CASE(0)
+      }
+#undef LUMEN_PPS_CASE
+      return hipGetLastError();
+    }
+    variant |= 4;   // two-phase non-persistent form otherwise
+  }
   const int64_t extent = (int64_t)M * ldc * (ep.out_f32 ? 4 : 2);
-  const bool wt = (variant & 1) && ep.out_group == 0 && extent < ((int64_t)1 << 31);
+  const bool wt = false;
   const bool fast = M % 256 == 0 && N % 256 == 0 && ep.out_group == 0 && !ep.glu && !ep.table && !ep.prelu &&
                     !ep.post_act && !ep.out_f32 && !(ep.bias && ep.bias_f32) && extent < ((int64_t)1 << 31);
   const int fk = fast ? 1 + (ep.bias ? 1 : 0) + (ep.residual ? 2 : 0) : 0;

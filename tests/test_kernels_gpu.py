@@ -25,7 +25,7 @@ def test_native_library_loaded():
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 768, 1024), (131, 3072, 1024), (512, 4096, 1024),
                                    (37, 64, 128), (4096, 1024, 4096), (2, 512, 512), (2570, 1024, 640)])
 @pytest.mark.parametrize("act", [None, "gelu", "quick_gelu"])
-@pytest.mark.parametrize("tile", [-1, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("tile", [-1, 4, 5, 6, 7, 8, 9, 209, 609, 709, 109])
 def test_gemm_vs_fp32(M, N, K, act, tile):
     g = torch.Generator().manual_seed(M + N + K)
     x = torch.randn(M, K, generator=g).bfloat16()
@@ -37,7 +37,7 @@ def test_gemm_vs_fp32(M, N, K, act, tile):
     assert _rel(got, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 609, 709])
 def test_gemm_tiles_asymmetric(tile):
     # A = I, asymmetric B: catches a transposed C write
     M = N = K = 256
@@ -181,7 +181,7 @@ def test_gemm_activations(act):
 
 
 @pytest.mark.parametrize("M,N,K", [(40 * 256, 2048, 1024), (600 * 256 + 77, 1024, 128), (3000, 768, 256)])
-@pytest.mark.parametrize("tile", [7, 1007, 47, 17, 8, 48, 1008])
+@pytest.mark.parametrize("tile", [7, 1007, 47, 17, 8, 48, 1008, 609, 709, 1709, 109])
 def test_gemm_persistent_multi_tile(M, N, K, tile):
     """Persistent kernel: several tiles per workgroup (cross-tile prefetch), epilogue with
     bias + GELU + residual, bf16 and fp32 outputs, with/without the tail split."""
@@ -201,7 +201,33 @@ def test_gemm_persistent_multi_tile(M, N, K, tile):
     assert torch.isfinite(got).all()
 
 
-@pytest.mark.parametrize("tile", [-1, 5, 7])
+@pytest.mark.parametrize("M,N,K", [(40 * 256, 2048, 192), (24 * 256, 3072, 128), (600 * 256, 1024, 1024),
+                                   (300 * 256, 768, 64 * 7)])
+@pytest.mark.parametrize("tile", [709, 1709, 609])
+@pytest.mark.parametrize("act", [None, "quick_gelu"])
+def test_gemm_pingpong_fast_epilogue(M, N, K, tile, act):
+    """Ping-pong kernels on interior tiles (bf16 bias -> FAST epilogue), several tiles per
+    workgroup for the persistent form, odd and minimal K-tile counts (nk = 2, 3, 7): the
+    cross-tile LDS-DMA stream and the vmcnt counts after each epilogue."""
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
+    b = torch.randn(N, generator=g).bfloat16()
+    r = torch.randn(M, N, generator=g).bfloat16()
+    xd, wd, bd, rd = x.to(DEV), w.to(DEV), b.to(DEV), r.to(DEV)
+    rows = torch.cat([torch.arange(0, 700), torch.randint(0, M, (1500,), generator=g), torch.arange(M - 700, M)])
+    for kw in ({}, {"bias": b}, {"bias": b, "residual": r}):
+        kd = {k: v.to(DEV) for k, v in kw.items()}
+        got = ops.linear(xd, wd, act=act, tile=tile, **kd).cpu().float()
+        kr = dict(kw)
+        if "residual" in kr:
+            kr["residual"] = r[rows]
+        ref = ops.linear(x[rows], w, act=act, **kr)
+        assert _rel(got[rows], ref) < 1e-2, kw.keys()
+        assert torch.isfinite(got).all()
+
+
+@pytest.mark.parametrize("tile", [-1, 5, 7, 709])
 def test_gemm_tail_round_split(tile):
     # 66 row tiles x 4 column tiles: rows [0, 16384) on 256x256, the 300-row tail on 128x128
     M, N, K = 64 * 256 + 300, 1024, 512
