@@ -33,6 +33,45 @@ from lumen_amd.parallel import Communicator, destroy, init_distributed  # noqa: 
 METRIC = "CLIP ViT-L/14 images/sec (whole node)"
 
 
+def _decode_window(model, B, side, dev, world, steps, g):
+    """End-to-end side metric: B JPEG files per step decoded on the CPU decode pool into a
+    pinned staging buffer (while the previous batch runs on the GPU), H2D, tower."""
+    from lumen_amd.utils.image import decode_many, encode_jpeg
+
+    rng = torch.randint(0, 256, (16, side, side, 3), generator=g, dtype=torch.uint8).numpy()
+    jpegs = [encode_jpeg(rng[i % 16]) for i in range(B)]
+    pinned = [torch.empty((B, side, side, 3), dtype=torch.uint8).pin_memory() for _ in range(2)]
+    dbuf = torch.empty((B, side, side, 3), dtype=torch.uint8, device=dev)
+    done = [None, None]
+
+    def run(i):
+        arrs = decode_many(jpegs)          # overlaps the previous batch's tower on the GPU
+        if done[i % 2] is not None:
+            done[i % 2].synchronize()      # its H2D from this staging buffer has finished
+        hb = pinned[i % 2]
+        for k, a in enumerate(arrs):
+            hb[k].copy_(torch.from_numpy(a))
+        dbuf.copy_(hb, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        done[i % 2] = ev
+        return model.encode_image_uint8(dbuf)
+
+    run(0)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        run(i)
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    return {"images_per_s": round(world * B * steps / float(el.item()), 2), "steps": steps,
+            "jpeg": f"{side}x{side} q90", "decode": "CPU thread pool (Pillow/libjpeg-turbo), draft off"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -44,6 +83,12 @@ def main():
     ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
     ap.add_argument("--text-steps", type=int, default=None,
                     help="text-tower steps timed separately for the texts/s side metric (default = --steps; 0 = skip)")
+    ap.add_argument("--seconds", type=float, default=0.0,
+                    help="after the K-step window, run a steady-state window of at least this many seconds "
+                         "(BASELINE.md asks >= 30 s) and report it as a side metric")
+    ap.add_argument("--include-decode", action="store_true",
+                    help="side metric: end-to-end images/s with JPEG decode (CPU thread pool, libjpeg-turbo) "
+                         "+ pinned staging + H2D + tower, timed after the headline window")
     args = ap.parse_args()
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -106,6 +151,28 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     ok = bool(torch.isfinite(gathered).all().item())
+    steady = None
+    if args.seconds > 0:
+        # steady-state window: whole steps until >= --seconds of wall clock (BASELINE.md rule)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        n_ss, t_ss0 = 0, time.perf_counter()
+        while True:
+            for _ in range(5):
+                step()
+            n_ss += 5
+            torch.cuda.synchronize()
+            if time.perf_counter() - t_ss0 >= args.seconds:
+                break
+        el = torch.tensor([time.perf_counter() - t_ss0], device=dev, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        steady = {"seconds": round(float(el.item()), 2), "steps": n_ss,
+                  "images_per_s": round(world * B * n_ss / float(el.item()), 2)}
+    e2e = None
+    if args.include_decode:
+        e2e = _decode_window(model, B, args.src_size, dev, world, max(3, min(args.steps, 10)), g)
     # side metric (BASELINE config 2 "image + text embed"): text tower on a batch of B
     # 77-token prompts, timed separately AFTER the headline window (never inside it)
     text_per_s = None
@@ -161,6 +228,8 @@ def main():
             "texts_per_s": round(text_per_s, 1) if text_per_s else None,
             "text_config": {"context_length": cfg.text.context_length, "batch_per_gpu": B,
                             "timed": "separately, after the image window"} if text_per_s else None,
+            "steady_state": steady,
+            "e2e_with_jpeg_decode": e2e,
             "finite": ok,
         }
         print(json.dumps(out), flush=True)

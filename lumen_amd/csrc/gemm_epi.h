@@ -26,6 +26,8 @@ struct GemmEpi {
   int glu;                   // SwiGLU: columns interleaved [gate 8 | up 8] per 16; writes silu(g) * u to
                              // column n/2 .. n/2+8 of C (C has N/2 columns)
   int64_t* dbg;              // profiling only: per-workgroup s_memrealtime stamps (null in production)
+  int64_t split_koff;        // split-K launches (gridDim.y = splits): A, W advance by y * split_koff
+  int64_t split_cstride;     // elements; C (fp32 slabs) advances by y * split_cstride
 };
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
@@ -62,6 +64,11 @@ __device__ __forceinline__ void tile_coords(int lin, int tiles_m, int tiles_n, i
 // static priority for the lagging wave group, bit 2: two phases per K-tile (32 MFMAs per phase)
 hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
                    int N, int K, const GemmEpi& ep, int group_m, int variant, hipStream_t stream);
+// split-K form for a few row tiles (the tail rows of a round-split GEMM): fp32 slabs from one
+// ping-pong launch over (tile, split), then one reduce + epilogue pass.  hipErrorNotSupported
+// when the epilogue / shape / workspace does not allow it (caller falls back).
+hipError_t gemm_tail_splitk(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc,
+                            int M, int N, int K, const GemmEpi& ep, hipStream_t stream);
 
 
 // 16-byte store of C: plain, or write-through (sc1) via a buffer descriptor over C.

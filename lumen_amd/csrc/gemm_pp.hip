@@ -58,6 +58,11 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   int tm, tn;
   tile_coords(xcd_remap(blockIdx.x, tiles_n * tiles_m), tiles_m, tiles_n, group_m, tm, tn);
   const int m0 = tm * 256, n0 = tn * 256;
+  if (ep.split_koff) {   // split-K: this workgroup's K slice and fp32 slab
+    A += blockIdx.y * ep.split_koff;
+    W += blockIdx.y * ep.split_koff;
+    C = (float*)C + blockIdx.y * ep.split_cstride;
+  }
 
   // half-tile h: 0 = A0, 1 = B0, 2 = B1, 3 = A1.  Lane writes LDS row g*8 + l/8, physical
   // chunk l%8, fetching logical chunk (l%8) ^ ((row >> 1) & 7).
@@ -292,8 +297,8 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
 
 template <bool WT, int FK, int PRIO, int NPH>
 static void launch_pp_t(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
-                        int N, int K, const GemmEpi& ep, int group_m, hipStream_t stream) {
-  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+                        int N, int K, const GemmEpi& ep, int group_m, hipStream_t stream, int splits = 1) {
+  const dim3 tiles(((M + 255) / 256) * ((N + 255) / 256), splits);
   const size_t lds = 2 * G_BUF;
   static bool attr_set = false;
   if (!attr_set) {
@@ -724,6 +729,75 @@ hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ld
     case 4: launch_pp_fk<4>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, stream); break;
     default: launch_pp_fk<0>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, stream); break;
   }
+  return hipGetLastError();
+}
+
+
+// ============================================================================
+// Split-K tail: out = epi( sum_s slab[s] ), 8 columns per thread, fp32 throughout
+// ============================================================================
+__global__ void __launch_bounds__(256)
+splitk_reduce_epi_kernel(const float* __restrict__ slabs, int S, int M, int N, void* __restrict__ C, int64_t ldc,
+                         GemmEpi ep) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int nc = N / 8;
+  if (idx >= (int64_t)M * nc) return;
+  const int m = (int)(idx / nc), n = (int)(idx % nc) * 8;
+  const int64_t slab = (int64_t)M * N;
+  float v[8];
+  {
+    const f32x4_t a = *(const f32x4_t*)(slabs + (int64_t)m * N + n);
+    const f32x4_t b = *(const f32x4_t*)(slabs + (int64_t)m * N + n + 4);
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+  }
+  for (int s = 1; s < S; ++s) {   // split order: deterministic
+    const f32x4_t a = *(const f32x4_t*)(slabs + s * slab + (int64_t)m * N + n);
+    const f32x4_t b = *(const f32x4_t*)(slabs + s * slab + (int64_t)m * N + n + 4);
+    v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3]; v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
+  }
+  GemmEpi e = ep;
+  e.alpha = 1.f;   // applied by the slab GEMM
+  epi_store8_t<false>(v, m, n, M, N, C, ldc, e, c_rsrc(C));
+}
+
+static float* tail_workspace(size_t bytes, hipStream_t stream) {
+  static float* ws[64] = {nullptr};
+  static size_t cap[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (cap[dev] >= bytes) return ws[dev];
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  void* p = nullptr;
+  const size_t want = bytes < ((size_t)64 << 20) ? ((size_t)64 << 20) : bytes;
+  if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+  if (ws[dev]) (void)hipFree(ws[dev]);
+  ws[dev] = (float*)p;
+  cap[dev] = want;
+  return ws[dev];
+}
+
+hipError_t gemm_tail_splitk(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc,
+                            int M, int N, int K, const GemmEpi& ep, hipStream_t stream) {
+  if (ep.glu || ep.out_group || ep.table || ep.split_koff || N % 8 != 0 || K % BK != 0 || M <= 0)
+    return hipErrorNotSupported;
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const int nk = K / BK;
+  // splits: power of two, >= 2 K-tiles each, <= 128 workgroups in all (slab traffic vs parallelism)
+  int S = 1;
+  while (S * 2 * tiles <= pp_num_cus() / 2 && nk % (S * 2) == 0 && nk / (S * 2) >= 2) S *= 2;
+  if (S == 1) return hipErrorNotSupported;
+  float* slabs = tail_workspace((size_t)S * M * N * sizeof(float), stream);
+  if (slabs == nullptr) return hipErrorNotSupported;
+  GemmEpi e{};
+  e.alpha = ep.alpha;
+  e.out_f32 = 1;
+  e.split_koff = (int64_t)(nk / S) * BK;
+  e.split_cstride = (int64_t)M * N;
+  launch_pp_t<false, 0, 1, 2>(A, lda, W, ldw, slabs, N, M, N, K / S, e, 4, stream, S);
+  const int64_t work = (int64_t)M * (N / 8);
+  hipLaunchKernelGGL(splitk_reduce_epi_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, stream, slabs, S, M,
+                     N, C, ldc, ep);
   return hipGetLastError();
 }
 

@@ -1,0 +1,33 @@
+"""Kernel statistics from a rocprofv3 SQLite (rocpd) database, as the CSV the older
+``--stats`` output used: Name, Calls, TotalDurationNs, AverageNs, Percentage.
+
+  python tools/rocpd_stats.py gpurun_out/prof_bench/run_results.db [out.csv] [--top N]
+"""
+import csv
+import sqlite3
+import sys
+
+
+def stats(db):
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, count(*), sum(end - start) from kernels group by name order by 3 desc").fetchall()
+    tot = sum(r[2] for r in rows) or 1
+    return [(n, k, t, t / k, 100.0 * t / tot) for n, k, t in rows]
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    top = int(sys.argv[sys.argv.index("--top") + 1]) if "--top" in sys.argv else 15
+    rows = stats(args[0])
+    if len(args) > 1:
+        with open(args[1], "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage"])
+            for r in rows:
+                w.writerow([r[0], r[1], r[2], round(r[3], 1), round(r[4], 3)])
+    for n, k, t, a, p in rows[:top]:
+        print(f"{p:6.2f}%  {k:6d}  {a / 1e3:9.2f} us  {n[:110]}")
+
+
+if __name__ == "__main__":
+    main()
