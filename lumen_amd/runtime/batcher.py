@@ -17,6 +17,8 @@ import time
 from concurrent.futures import Future
 from typing import Any, Callable, Optional, Sequence
 
+from .metrics import StageTimer, batch_size, current_timer, use_timer
+
 log = logging.getLogger("lumen.batcher")
 
 
@@ -38,15 +40,25 @@ class DynamicBatcher:
         if self._stop.is_set():
             raise RuntimeError(f"{self.name} is closed")
         fut: Future = Future()
+        fut.lumen_t_submit = time.perf_counter()
         self._q.put((item, fut))
         return fut
 
+    @staticmethod
+    def _collect(fut: Future, timeout: Optional[float]) -> Any:
+        out = fut.result(timeout)
+        t = current_timer()
+        stats = getattr(fut, "lumen_stats", None)
+        if t is not None and stats:
+            t.merge(stats)
+        return out
+
     def __call__(self, item: Any, timeout: Optional[float] = None) -> Any:
-        return self.submit(item).result(timeout)
+        return self._collect(self.submit(item), timeout)
 
     def map(self, items: Sequence[Any], timeout: Optional[float] = None) -> list:
         futs = [self.submit(x) for x in items]
-        return [f.result(timeout) for f in futs]
+        return [self._collect(f, timeout) for f in futs]
 
     def _loop(self) -> None:
         while not self._stop.is_set():
@@ -63,11 +75,21 @@ class DynamicBatcher:
                 except queue.Empty:
                     break
             items = [b[0] for b in batch]
+            t_start = time.perf_counter()
+            timer = StageTimer(self.name)
             try:
-                outs = self.fn(items)
+                with use_timer(timer):
+                    outs = self.fn(items)
+                stats = dict(timer.finish())
+                h = batch_size()
+                if h is not None:
+                    h.labels(self.name).observe(len(items))
                 if len(outs) != len(items):
                     raise RuntimeError(f"{self.name}: batch fn returned {len(outs)} results for {len(items)} items")
                 for (_, fut), out in zip(batch, outs):
+                    # per request: the batch's stage times, its queue wait and the batch size
+                    fut.lumen_stats = dict(stats, queue=(t_start - getattr(fut, "lumen_t_submit", t_start)) * 1000)
+                    fut.lumen_batch = len(items)
                     if isinstance(out, BaseException):
                         fut.set_exception(out)
                     else:

@@ -63,7 +63,9 @@ class GenRequest:
     out: "queue.Queue" = field(default_factory=queue.Queue)
     tokens: list = field(default_factory=list)
     t_submit: float = 0.0
+    t_admit: Optional[float] = None         # prefill started (left the admission queue)
     t_first: Optional[float] = None
+    t_done: Optional[float] = None
     finish_reason: Optional[str] = None
     ctx: int = 0                            # tokens in the KV cache
     rng: Any = None
@@ -310,6 +312,7 @@ class LLMEngine:
 
     def _finish(self, r: GenRequest) -> None:
         self.kv.blocks.release(r.rid)
+        r.t_done = time.perf_counter()
         r.out.put(("done", r.finish_reason or "stop"))
 
     def _fail(self, reqs, e: BaseException) -> None:
@@ -342,6 +345,8 @@ class LLMEngine:
         """Prefill up to ``budget`` more prompt tokens of ``r``; returns the tokens consumed.
         On the last chunk the first token is sampled and ``r`` joins the running batch."""
         if r.x is None:
+            if r.t_admit is None:
+                r.t_admit = time.perf_counter()
             if self.sync is not None:
                 # followers must enter the build (its vocab-parallel embedding all-reduce)
                 # together with us: announce it before building the inputs

@@ -17,6 +17,7 @@ probability (sites: ``infer``, ``batch``, ``engine``).
 from __future__ import annotations
 
 import contextlib
+import contextvars
 import os
 import random
 import threading
@@ -135,8 +136,45 @@ class StageTimer:
             self._events.clear()
         return self.ms
 
+    def merge(self, ms: dict, prefix: str = "") -> None:
+        """Add stage times measured elsewhere (a dynamic batcher's batch) to this timer."""
+        for k, v in (ms or {}).items():
+            key = prefix + k
+            self.ms[key] = self.ms.get(key, 0.0) + float(v)
+
     def meta(self, prefix: str = "t_") -> dict[str, str]:
         return {f"{prefix}{k}_ms": f"{v:.3f}" for k, v in self.finish().items()}
+
+
+# The request's timer travels in a context variable: the service installs one per request
+# (:func:`use_timer`), the pipelines mark stages with :func:`stage` without plumbing a timer
+# argument through every layer, and a dynamic batcher's worker thread runs each batch under
+# its own timer whose stage times are merged back into every request of the batch.
+_CURRENT: "contextvars.ContextVar[Optional[StageTimer]]" = contextvars.ContextVar("lumen_stage_timer", default=None)
+
+
+def current_timer() -> Optional[StageTimer]:
+    return _CURRENT.get()
+
+
+@contextlib.contextmanager
+def use_timer(t: Optional[StageTimer]):
+    tok = _CURRENT.set(t)
+    try:
+        yield t
+    finally:
+        _CURRENT.reset(tok)
+
+
+@contextlib.contextmanager
+def stage(name: str):
+    """Time a pipeline stage on the current request/batch timer (no-op without one)."""
+    t = _CURRENT.get()
+    if t is None:
+        yield
+        return
+    with t.stage(name):
+        yield
 
 
 _nvtx_mod = None

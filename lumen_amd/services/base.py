@@ -24,7 +24,7 @@ from typing import Any, Callable, Iterable, Optional
 import grpc
 
 from ..proto import ml_service as pb
-from ..runtime.metrics import maybe_fault, observe_request
+from ..runtime.metrics import StageTimer, maybe_fault, observe_request, use_timer
 
 log = logging.getLogger("lumen.service")
 
@@ -201,11 +201,19 @@ class BaseInferenceService(pb.InferenceServicer):
                         continue
                     meta = self._request_meta(req, context)
                     maybe_fault("infer")
-                    out = handler(payload, req.payload_mime, meta)
+                    timer = StageTimer(self.SERVICE_NAME)
+                    with use_timer(timer):
+                        out = handler(payload, req.payload_mime, meta)
                     if hasattr(out, "__next__"):  # streaming handler: yields (bytes, mime, meta, is_final)
-                        for chunk in out:
+                        while True:
+                            with use_timer(timer):   # the generator body runs on each next()
+                                chunk = next(out, None)
+                            if chunk is None:
+                                break
                             res, mime, extra, final = chunk
                             m = dict(extra or {})
+                            if final:
+                                m.update(timer.meta())
                             m[self.LATENCY_KEY] = str(int((time.perf_counter() - t0) * 1000))
                             schema = mime.split("schema=")[-1] if (final and "schema=" in mime) else ""
                             yield pb.InferResponse(correlation_id=cid, is_final=final, result=res, result_mime=mime,
@@ -214,6 +222,7 @@ class BaseInferenceService(pb.InferenceServicer):
                         continue
                     res, mime, extra = out
                     m = dict(extra or {})
+                    m.update(timer.meta())   # per-stage times: t_<stage>_ms (decode, forward, queue, ...)
                     m[self.LATENCY_KEY] = str(int((time.perf_counter() - t0) * 1000))
                     schema = mime.split("schema=")[-1] if "schema=" in mime else ""
                     observe_request(self.SERVICE_NAME, task, "ok", time.perf_counter() - t0)

@@ -29,6 +29,7 @@ import torch
 
 from ...models.clip import CLIPModel
 from ...runtime.batcher import DynamicBatcher
+from ...runtime.metrics import stage
 from ...utils.image import decode_many
 from .resources import ModelResources, load_weights
 
@@ -159,18 +160,22 @@ class MI355XClipBackend:
         return torch.from_numpy(ids)
 
     def _encode_texts(self, texts: Sequence[str]) -> list:
+        with stage("tokenize"):
+            ids = self.tokenize(texts)
         if self._pool is not None:
-            return self._pool.run("text", list(self.tokenize(texts).numpy()))
-        with torch.no_grad():
-            ids = self.tokenize(texts).to(self.device)
-            emb = self.model.encode_text_ids(ids).float().cpu().numpy()
+            with stage("dp_forward"):
+                return self._pool.run("text", list(ids.numpy()))
+        with torch.no_grad(), stage("forward"):      # H2D + text tower + D2H (synchronising)
+            emb = self.model.encode_text_ids(ids.to(self.device)).float().cpu().numpy()
         return list(emb)
 
     def _encode_images(self, payloads: Sequence[bytes]) -> list:
         if self._pool is not None:
-            return self._pool.run("image", list(payloads))
-        imgs = decode_many(payloads)
-        with torch.no_grad():
+            with stage("dp_forward"):
+                return self._pool.run("image", list(payloads))
+        with stage("decode"):
+            imgs = decode_many(payloads)
+        with torch.no_grad(), stage("forward"):      # H2D + resize/normalise + tower + D2H
             tens = [torch.from_numpy(i) for i in imgs]
             emb = self.model.encode_image_uint8(tens).float().cpu().numpy()
         return list(emb)

@@ -43,6 +43,7 @@ from ...models.face import IRESNET_PRESETS, SCRFD_PRESETS, IResNet, IResNetConfi
 from ...ops import vision
 from ...resources.exceptions import ResourceNotFoundError
 from ...runtime.batcher import DynamicBatcher
+from ...runtime.metrics import stage
 from ...utils.image import decode_rgb
 from ..common import BackendInfo, GenericResources, load_safetensors, pick_device, runtime_name
 
@@ -212,10 +213,20 @@ class MI355XFaceBackend:
         tens = [torch.from_numpy(np.ascontiguousarray(im)) for im in images]
         if self.device.type == "cuda":
             tens = [t.pin_memory() for t in tens] if len(tens) > 1 else tens
-        x = ops.image_prep(tens, (S, S), mean=(self.spec.det_mean,) * 3, std=(self.spec.det_std,) * 3, scale=1.0,
-                           filter="cv2_linear", layout="nhwc8", pad=0.0, geoms=geoms, out_dtype=self.dtype,
-                           device=self.device)
-        heads = self.det(x)
+        with stage("det_preprocess"):
+            x = ops.image_prep(tens, (S, S), mean=(self.spec.det_mean,) * 3, std=(self.spec.det_std,) * 3, scale=1.0,
+                               filter="cv2_linear", layout="nhwc8", pad=0.0, geoms=geoms, out_dtype=self.dtype,
+                               device=self.device)
+        with stage("det_forward"):
+            heads = self.det(x)
+        return self._det_post(images, params, heads, scales)
+
+    def _det_post(self, images, params, heads, scales) -> list[list[FaceDetection]]:
+        N = len(images)
+        with stage("det_decode_nms"):      # decode + NMS kernels, the D2H of kept rows synchronises
+            return self._det_post_inner(images, params, heads, scales, N)
+
+    def _det_post_inner(self, images, params, heads, scales, N) -> list[list[FaceDetection]]:
         img_scale = torch.tensor(scales, dtype=torch.float32, device=self.device)
         img_hw = torch.tensor([[im.shape[0], im.shape[1]] for im in images], dtype=torch.float32, device=self.device)
         A = self.det.cfg.anchors
@@ -261,12 +272,14 @@ class MI355XFaceBackend:
         if len(img_index) == 0:
             return np.zeros((0, self.rec.cfg.embedding), np.float32)
         R = self.spec.rec_size
-        x = vision.warp_batch(images, img_index, minv, (R, R), cpad=8, scale=1.0 / self.spec.rec_std,
-                              mean=self.spec.rec_mean / self.spec.rec_std, std=1.0,
-                              swap_rb=self.spec.rec_color.lower() == "bgr", device=self.device)
-        if x.dtype != self.dtype:
-            x = x.to(self.dtype)
-        return self.rec(x).float().cpu().numpy()
+        with stage("align_warp"):
+            x = vision.warp_batch(images, img_index, minv, (R, R), cpad=8, scale=1.0 / self.spec.rec_std,
+                                  mean=self.spec.rec_mean / self.spec.rec_std, std=1.0,
+                                  swap_rb=self.spec.rec_color.lower() == "bgr", device=self.device)
+            if x.dtype != self.dtype:
+                x = x.to(self.dtype)
+        with stage("rec_forward"):
+            return self.rec(x).float().cpu().numpy()
 
     def _detect_batch(self, items):
         imgs = [it[0] for it in items]
@@ -291,7 +304,8 @@ class MI355XFaceBackend:
         if not image_bytes:
             raise InvalidInputError("image_bytes cannot be empty")
         try:
-            return decode_rgb(image_bytes)
+            with stage("decode"):
+                return decode_rgb(image_bytes)
         except ValueError as e:
             raise InvalidInputError(f"Failed to decode image bytes: {e}") from e
 

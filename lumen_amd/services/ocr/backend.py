@@ -42,6 +42,7 @@ from ...models.ocr import DBNet, DBNetConfig, RecConfig, SVTRRecognizer
 from ...ops import vision
 from ...resources.exceptions import ResourceNotFoundError
 from ...runtime.batcher import DynamicBatcher
+from ...runtime.metrics import stage
 from ...utils.image import decode_rgb
 from ..common import BackendInfo, GenericResources, load_safetensors, pick_device, runtime_name
 
@@ -232,17 +233,27 @@ class MI355XOcrBackend:
                 geoms.append(ops.ImageGeom.resize(h, w, off, rh, rw))
                 off += images[i].size
                 tens.append(torch.from_numpy(np.ascontiguousarray(images[i])))
-            x = ops.image_prep(tens, (rh, rw), mean=dc["mean"], std=dc["std"], scale=float(dc["scale"]),
-                               filter="cv2_linear", layout="nhwc8", swap_rb=True, geoms=geoms, out_dtype=self.dtype,
-                               device=self.device)
-            prob = self.det(x).float().cpu().numpy()
-            for j, i in enumerate(idx):
-                h, w = images[i].shape[:2]
-                p = params[i]
-                boxes, _ = vision.db_boxes(prob[j], thresh=p.det_thresh, box_thresh=p.box_thresh,
-                                           unclip_ratio=p.unclip_ratio, scale_xy=(w / rw, h / rh), src_wh=(w, h))
-                out[i] = sorted_boxes(list(boxes))
+            with stage("det_preprocess"):
+                x = ops.image_prep(tens, (rh, rw), mean=dc["mean"], std=dc["std"], scale=float(dc["scale"]),
+                                   filter="cv2_linear", layout="nhwc8", swap_rb=True, geoms=geoms,
+                                   out_dtype=self.dtype, device=self.device)
+            with stage("det_forward"):
+                prob = self.det(x)
+            with stage("db_post"):
+                out_g = self._db_post(prob, [images[i].shape[:2] for i in idx], [params[i] for i in idx], rh, rw)
+            for i, bx in zip(idx, out_g):
+                out[i] = bx
         return out
+
+    def _db_post(self, prob: torch.Tensor, hw, params, rh: int, rw: int) -> list:
+        """DB post-processing of a [n, rh, rw] probability batch -> boxes in reading order."""
+        pm = prob.float().cpu().numpy()
+        res = []
+        for j, ((h, w), p) in enumerate(zip(hw, params)):
+            boxes, _ = vision.db_boxes(pm[j], thresh=p.det_thresh, box_thresh=p.box_thresh,
+                                       unclip_ratio=p.unclip_ratio, scale_xy=(w / rw, h / rh), src_wh=(w, h))
+            res.append(sorted_boxes(list(boxes)))
+        return res
 
     # ------------------------------------------------------------------ recognition
     @torch.no_grad()
@@ -264,15 +275,18 @@ class MI355XOcrBackend:
             widths = [maps[k][1] for k in chunk]
             Wb = max(self.bucket, -(-max(widths) // self.bucket) * self.bucket)
             minv = np.stack([maps[k][0] for k in chunk])
-            x = vision.warp_batch(images, [crops[k][0] for k in chunk], minv, (H, Wb), out_w=widths, cpad=8,
-                                  scale=scale / std, mean=mean / std, std=1.0, swap_rb=True, cubic=True,
-                                  replicate=True, device=self.device)
-            if x.dtype != self.dtype:
-                x = x.to(self.dtype)
-            logits = self.rec(x, valid_w=widths)
+            with stage("crop_warp"):
+                x = vision.warp_batch(images, [crops[k][0] for k in chunk], minv, (H, Wb), out_w=widths, cpad=8,
+                                      scale=scale / std, mean=mean / std, std=1.0, swap_rb=True, cubic=True,
+                                      replicate=True, device=self.device)
+                if x.dtype != self.dtype:
+                    x = x.to(self.dtype)
+            with stage("rec_forward"):
+                logits = self.rec(x, valid_w=widths)
             ts = self.rec.time_stride
-            ids, conf = vision.ctc_greedy(logits, blank=0, from_logits=True,
-                                          tlen=[-(-w // ts) for w in widths])
+            with stage("ctc"):
+                ids, conf = vision.ctc_greedy(logits, blank=0, from_logits=True,
+                                              tlen=[-(-w // ts) for w in widths])
             for k, seq, c in zip(chunk, ids, conf):
                 res[k] = ("".join(self.character_str[i] for i in seq if 0 < i < len(self.character_str)), float(c))
         return res
@@ -301,7 +315,8 @@ class MI355XOcrBackend:
         if not image_bytes:
             raise InvalidInputError("Failed to decode image bytes")
         try:
-            img = decode_rgb(image_bytes)
+            with stage("decode"):
+                img = decode_rgb(image_bytes)
         except ValueError as e:
             raise InvalidInputError(f"Failed to decode image bytes: {e}") from e
         p = OcrParams(det_thresh=float(det_threshold), rec_thresh=float(rec_threshold),

@@ -37,6 +37,7 @@ from ...models.vlm import VLM, VLM_PRESETS, VLMConfig
 from ...resources.exceptions import ResourceNotFoundError
 from ...runtime.engine import LLMEngine, SamplingParams
 from ...runtime.kv_cache import PagedKVCache
+from ...runtime.metrics import current_timer, stage
 from ...utils.image import decode_rgb
 from ..common import GenericResources, load_safetensors, pick_device, runtime_name
 
@@ -195,6 +196,17 @@ def stop_on_sequences(text: str, stop_sequences: Optional[Sequence[str]]) -> tup
         if i != -1:
             return text[:i], s
     return text, ""
+
+
+def _engine_stages(r) -> None:
+    """Engine-side stage times of a finished request onto the request's timer: admission
+    queue, prefill (incl. vision tower) to first token, and the decode phase."""
+    t = current_timer()
+    if t is None or r.t_first is None:
+        return
+    adm = r.t_admit or r.t_submit
+    t.merge({"queue": (adm - r.t_submit) * 1000, "prefill": (r.t_first - adm) * 1000,
+             "decode_tokens": ((r.t_done or r.t_first) - r.t_first) * 1000})
 
 
 class MI355XVLMBackend:
@@ -414,10 +426,12 @@ class MI355XVLMBackend:
         self.ensure_initialized()
         if self._tp_group is not None and self._tp_group.failed:
             raise BackendError(f"tensor-parallel group unavailable: {self._tp_group.failed}")
-        prompt = self.build_prompt(self._with_image_token(req.messages), req.add_generation_prompt)
-        ids = self.tokenize(prompt)
+        with stage("tokenize"):
+            prompt = self.build_prompt(self._with_image_token(req.messages), req.add_generation_prompt)
+            ids = self.tokenize(prompt)
         try:
-            img = decode_rgb(req.image_bytes)
+            with stage("decode"):
+                img = decode_rgb(req.image_bytes)
         except ValueError as e:
             raise InvalidInputError(str(e)) from e
         full, starts = self.model.expand_image_tokens(ids, 1)
@@ -437,6 +451,7 @@ class MI355XVLMBackend:
         r, n_in = self._submit(request)
         for _ in r.stream():
             pass
+        _engine_stages(r)
         text = self.detokenize(r.tokens)
         cut, stop = stop_on_sequences(text, request.stop_sequences)
         reason = "stop_sequence" if stop else (r.finish_reason or "stop")
@@ -458,6 +473,7 @@ class MI355XVLMBackend:
                     self.engine.cancel(r)
                     for _ in r.stream():
                         pass
+                    _engine_stages(r)
                     yield GenerationChunk(text="", is_final=True, metadata={"reason": "stop_sequence",
                                                                            "input_tokens": n_in})
                     return
@@ -471,6 +487,7 @@ class MI355XVLMBackend:
                 tail = self.detokenize(r.tokens)
                 if len(tail) > len(emitted):
                     yield GenerationChunk(text=tail[len(emitted):], metadata={"step": step})
+                _engine_stages(r)
                 yield GenerationChunk(text="", is_final=True, metadata={"reason": val, "input_tokens": n_in})
 
     def get_info(self) -> BackendInfo:

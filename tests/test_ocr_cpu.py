@@ -107,6 +107,8 @@ def test_ocr_service(ocr):
                        None))[0]
     assert not r.HasField("error"), r.error
     assert r.result_schema == "ocr_v1" and "duration_ms" in r.meta
+    for k in ("t_decode_ms", "t_det_forward_ms", "t_db_post_ms", "t_rec_forward_ms", "t_ctc_ms", "t_queue_ms"):
+        assert float(r.meta[k]) >= 0.0, (k, dict(r.meta))
     d = json.loads(r.result)
     assert d["model_id"] == "ppocr-tiny_onnx" and d["count"] == len(d["items"]) >= 1
     for it in d["items"]:

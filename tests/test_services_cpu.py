@@ -80,6 +80,9 @@ def test_image_and_text_embed(hub):
     assert d["dim"] == 64 and len(d["vector"]) == 64 and d["model_id"] == "clip-tiny_torch"
     assert abs(np.linalg.norm(d["vector"]) - 1) < 1e-4
     assert "lat_ms" in r.meta and r.meta["dim"] == "64"
+    # per-stage timings (StageTimer through the dynamic batcher): decode, forward, queue wait
+    for k in ("t_decode_ms", "t_forward_ms", "t_queue_ms"):
+        assert k in r.meta and float(r.meta[k]) >= 0.0, (k, dict(r.meta))
     t = json.loads(_one(stub, "clip_text_embed", b"a cat", "text/plain").result)
     assert t["model_id"] == "clip-tiny:clip-tiny_torch"
 

@@ -209,6 +209,8 @@ def test_vlm_service_stream(vlm_service):
     d = json.loads(out[-1].result)
     assert d["generated_tokens"] == 6 and out[-1].meta["streaming_chunks"] == str(len(out) - 1)
     assert "processing_time_ms" in out[-1].meta
+    for k in ("t_tokenize_ms", "t_decode_ms", "t_prefill_ms", "t_decode_tokens_ms"):
+        assert float(out[-1].meta[k]) >= 0.0, (k, dict(out[-1].meta))
     cap = vlm_service.build_capability()
     assert cap.service_name == "vlm-fast" and {t.name for t in cap.tasks} == {"vlm_generate", "vlm_generate_stream"}
 
