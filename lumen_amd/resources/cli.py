@@ -33,6 +33,15 @@ def cmd_download(a) -> int:
 
 
 def cmd_validate(a) -> int:
+    if not getattr(a, "strict", True):
+        from .validator import ConfigValidator
+
+        ok, errs = ConfigValidator().validate_file(a.config, strict=False)
+        if not ok:
+            print("invalid configuration (schema):\n  - " + "\n  - ".join(errs))
+            return 1
+        print(f"valid configuration (schema only): {a.config}")
+        return 0
     try:
         cfg = load_and_validate_config(a.config)
     except (ConfigError, Exception) as e:  # noqa: BLE001
@@ -44,6 +53,22 @@ def cmd_validate(a) -> int:
 
 
 def cmd_validate_model_info(a) -> int:
+    if not getattr(a, "strict", True):
+        import json as _json
+
+        from .model_info import model_info_schema_errors
+
+        p = Path(a.model_info)
+        p = p / "model_info.json" if p.is_dir() else p
+        try:
+            errs = model_info_schema_errors(_json.loads(p.read_text(encoding="utf-8")))
+        except (OSError, ValueError) as e:
+            errs = [str(e)]
+        if errs:
+            print("invalid model_info (schema):\n  - " + "\n  - ".join(errs))
+            return 1
+        print(f"valid model_info (schema only): {p}")
+        return 0
     try:
         info = load_and_validate_model_info(a.model_info)
     except (ModelInfoError, Exception) as e:  # noqa: BLE001

@@ -75,6 +75,13 @@ class ModelInfo(BaseModel):
     metadata: Optional[Metadata] = None
 
 
+def model_info_schema_errors(data: Any) -> list[str]:
+    """Draft-7 schema check of a parsed manifest (``validate-model-info --schema-only``)."""
+    from .jsonschema_lite import SchemaValidator
+
+    return SchemaValidator.from_file(Path(__file__).resolve().parent / "schemas" / "model_info-schema.json").errors(data)
+
+
 def load_and_validate_model_info(path: Union[str, Path]) -> ModelInfo:
     p = Path(path)
     if p.is_dir():

@@ -1,10 +1,12 @@
-"""Config validation: strict (pydantic) and schema-only (structural) modes.
+"""Config validation: strict (JSON schema + pydantic) and schema-only (JSON schema) modes.
 
 Mirrors packages/lumen-resources/src/lumen_resources/lumen_config_validator.py:19-270
-(``load_and_validate_config``, ``ConfigValidator.validate_and_load``, ``--schema-only``)
-including the cross-field rules of config-schema.yaml: mdns.service_name required when
-mDNS is enabled, rknn_device required for runtime=rknn, deployment.service must name a
-configured service (single), every hub service must exist.
+(``load_and_validate_config``, ``ConfigValidator.validate_and_load``, ``--schema-only``).
+The Draft-7 schema ``schemas/config-schema.json`` (checked by :mod:`jsonschema_lite`)
+carries the conditional rules of the reference's config-schema.yaml — ``oneOf`` single |
+hub deployment, mdns.service_name required when mDNS is enabled, rknn_device required
+for runtime=rknn — and :func:`semantic_errors` the cross-references a schema cannot
+express (deployment.service / every hub service must be configured).
 """
 from __future__ import annotations
 
@@ -16,6 +18,40 @@ import yaml
 
 from .config import LumenConfig
 from .exceptions import ConfigError
+from .jsonschema_lite import SchemaValidator
+
+SCHEMA_DIR = Path(__file__).resolve().parent / "schemas"
+_CONFIG_SCHEMA: "SchemaValidator | None" = None
+
+
+def config_schema() -> SchemaValidator:
+    global _CONFIG_SCHEMA
+    if _CONFIG_SCHEMA is None:
+        _CONFIG_SCHEMA = SchemaValidator.from_file(SCHEMA_DIR / "config-schema.json")
+    return _CONFIG_SCHEMA
+
+
+def schema_errors(data: dict) -> list[str]:
+    """JSON-schema validation only (``--schema-only``; like the reference, cross-references
+    between nodes are checked in strict mode only — a reference example config names a
+    service key that does not exist and still passes its schema)."""
+    return config_schema().errors(data)
+
+
+def semantic_errors(data: dict) -> list[str]:
+    """Rules that need more than one node of the document."""
+    errs: list[str] = []
+    dep = data.get("deployment") if isinstance(data, dict) else None
+    services = data.get("services") if isinstance(data, dict) else None
+    if not isinstance(dep, dict) or not isinstance(services, dict):
+        return errs
+    if dep.get("mode") == "single" and isinstance(dep.get("service"), str) and dep["service"] not in services:
+        errs.append(f"deployment.service '{dep['service']}' is not defined under services")
+    if dep.get("mode") == "hub":
+        for s in dep.get("services") or []:
+            if isinstance(s, str) and s not in services:
+                errs.append(f"hub service '{s}' is not defined under services")
+    return errs
 
 
 def _load_yaml(path: Union[str, Path]) -> dict:
@@ -89,11 +125,14 @@ def structural_errors(data: dict) -> list[str]:
 
 class ConfigValidator:
     def validate_file(self, path, strict: bool = True) -> tuple[bool, list[str]]:
+        """strict: JSON schema + hand rules + pydantic; schema-only: JSON schema + cross-refs."""
         try:
             data = _load_yaml(path)
         except ConfigError as e:
             return False, [str(e)]
-        errs = structural_errors(data)
+        errs = schema_errors(data)
+        if strict and not errs:
+            errs = structural_errors(data)
         if strict and not errs:
             try:
                 LumenConfig.model_validate(data)
@@ -103,7 +142,7 @@ class ConfigValidator:
 
     def validate_and_load(self, path) -> LumenConfig:
         data = _load_yaml(path)
-        errs = structural_errors(data)
+        errs = schema_errors(data) or structural_errors(data)
         if errs:
             raise ConfigError("configuration invalid:\n  - " + "\n  - ".join(errs))
         try:
@@ -118,7 +157,7 @@ def load_and_validate_config(path: Union[str, Path]) -> LumenConfig:
 
 
 def config_from_dict(data: dict[str, Any]) -> LumenConfig:
-    errs = structural_errors(data)
+    errs = schema_errors(data) or structural_errors(data)
     if errs:
         raise ConfigError("configuration invalid:\n  - " + "\n  - ".join(errs))
     return LumenConfig.model_validate(data)
