@@ -133,6 +133,10 @@ class InstallSetupRequest(BaseModel):
     cache_dir: str = "~/.lumen"
     environment_name: str = "lumen_env"
     force_reinstall: bool = False
+    # where Lumen runs: "current" = this interpreter (no env created), "venv" = an isolated
+    # venv over the host's ROCm PyTorch, "micromamba" = a conda env from envs/rocm.yaml
+    env_kind: Literal["current", "venv", "micromamba"] = "current"
+    wheel: Optional[str] = None        # explicit lumen_amd wheel / source dir
 
 
 class InstallStep(BaseModel):

@@ -70,19 +70,23 @@ def test_hardware(client):
 def test_install_tasks(client, tmp_path, monkeypatch):
     monkeypatch.setattr(InstallOrchestrator, "_do_build_native",
                         lambda self, t, i: self._step(t, i, "skipped", "prebuilt"))
+    monkeypatch.setattr(InstallOrchestrator, "_do_verify_installation",
+                        lambda self, t, i: self._step(t, i, "completed", "verified (stub)"))
     st = client.get("/api/v1/install/status", params={"cache_dir": str(tmp_path)}).json()
     assert "missing_components" in st and "drivers" in st
     cp = client.get("/api/v1/install/check-path", params={"path": str(tmp_path)}).json()
     assert cp["recommended_action"] in ("configure_new", "repair", "start_existing")
     r = client.post("/api/v1/install/setup", json={"preset": "cpu", "cache_dir": str(tmp_path / "c")}).json()
     tid = r["task_id"]
-    for _ in range(100):
+    for _ in range(600):
         t = client.get(f"/api/v1/install/tasks/{tid}").json()
         if t["status"] in ("completed", "failed"):
             break
         time.sleep(0.05)
     assert t["status"] == "completed", t
-    assert [s["status"] for s in t["steps"]] == ["completed", "completed", "skipped", "completed"]
+    assert [s["step_id"] for s in t["steps"]] == ["check_python", "build_native", "verify_installation",
+                                                  "prepare_cache"]
+    assert [s["status"] for s in t["steps"]] == ["completed", "skipped", "completed", "completed"]
     assert (tmp_path / "c" / "models").is_dir()
     assert client.get("/api/v1/install/tasks").json()["total"] == 1
     logs = client.get(f"/api/v1/install/tasks/{tid}/logs", params={"tail": 10}).json()
