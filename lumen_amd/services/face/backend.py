@@ -23,9 +23,17 @@ thread per model).
 
 Deliberate fixes of reference quirks: alignment uses the landmarks in
 the coordinate frame of the image they were detected in (the reference applies
-original-image landmarks to the bbox crop), and the canonical insightface 112x112
-ArcFace template (the reference's template is the 96-wide one without the +8 px x
-offset, onnxrt_backend.py:1388-1397) — ``LUMEN_FACE_REFERENCE_TEMPLATE=1`` restores it.
+original-image landmarks to the bbox crop, face_model.py:429-470 + onnxrt_backend.py:
+1327-1332), and the canonical insightface 112x112 ArcFace template (the reference's
+template is the 96-wide one without the +8 px x offset, onnxrt_backend.py:1388-1397).
+
+Embedding compatibility (``LUMEN_FACE_ALIGN=reference``, or ``extra.face_align:
+reference`` in model_info): reproduces the reference geometry exactly so vectors match
+embeddings a reference deployment already stored — the face is cut out at its integer,
+image-clipped bbox, the similarity transform is estimated from the ORIGINAL-image
+landmarks onto the 96-wide template and applied to the CROP (border 0 at the crop's
+edge), or the crop is resized to 112 when there are no landmarks; an empty crop yields a
+zero vector.  ``LUMEN_FACE_REFERENCE_TEMPLATE=1`` switches the template only.
 """
 from __future__ import annotations
 
@@ -139,8 +147,12 @@ class MI355XFaceBackend:
         self.load_time = 0.0
         self._det_batcher: Optional[DynamicBatcher] = None
         self._emb_batcher: Optional[DynamicBatcher] = None
-        self.template = REFERENCE_TEMPLATE if os.environ.get("LUMEN_FACE_REFERENCE_TEMPLATE") == "1" \
-            else vision.ARCFACE_DST
+        self.align_mode = (os.environ.get("LUMEN_FACE_ALIGN") or
+                           str((resources.extra or {}).get("face_align", "standard"))).lower()
+        if self.align_mode not in ("standard", "reference"):
+            raise ValueError(f"face_align must be 'standard' or 'reference', got {self.align_mode!r}")
+        self.template = REFERENCE_TEMPLATE if (os.environ.get("LUMEN_FACE_REFERENCE_TEMPLATE") == "1" or
+                                               self.align_mode == "reference") else vision.ARCFACE_DST
 
     # ------------------------------------------------------------------ lifecycle
     def initialize(self) -> None:
@@ -267,15 +279,37 @@ class MI355XFaceBackend:
         return crop_minv(bbox, out)
 
     @torch.no_grad()
-    def embed_faces(self, images: Sequence[np.ndarray], img_index: Sequence[int], minv: np.ndarray) -> np.ndarray:
+    def warp_faces(self, images: Sequence[np.ndarray], img_index: Sequence[int], minv: np.ndarray,
+                   replicate: Optional[Sequence[bool]] = None) -> torch.Tensor:
+        """Batched alignment warp -> recogniser input [F, R, R, 8].  ``replicate`` (per face)
+        selects the edge-replicating border of a cv2.resize instead of the constant 0 of a
+        cv2.warpAffine; faces of the two kinds are warped by one launch each."""
+        R = self.spec.rec_size
+        kw = dict(cpad=8, scale=1.0 / self.spec.rec_std, mean=self.spec.rec_mean / self.spec.rec_std, std=1.0,
+                  swap_rb=self.spec.rec_color.lower() == "bgr", device=self.device)
+        if replicate is None or not any(replicate):
+            return vision.warp_batch(images, img_index, minv, (R, R), **kw)
+        rep = np.asarray(replicate, bool)
+        parts, order = [], []
+        for flag in (False, True):
+            sel = np.nonzero(rep == flag)[0]
+            if len(sel):
+                parts.append(vision.warp_batch(images, [img_index[k] for k in sel], minv[sel], (R, R),
+                                               replicate=flag, **kw))
+                order.extend(sel.tolist())
+        x = torch.cat(parts) if len(parts) > 1 else parts[0]
+        inv = torch.empty(len(order), dtype=torch.long)
+        inv[torch.tensor(order)] = torch.arange(len(order))
+        return x.index_select(0, inv.to(x.device))
+
+    @torch.no_grad()
+    def embed_faces(self, images: Sequence[np.ndarray], img_index: Sequence[int], minv: np.ndarray,
+                    replicate: Optional[Sequence[bool]] = None) -> np.ndarray:
         """Warp + embed F faces -> [F, D] fp32 (L2-normalised)."""
         if len(img_index) == 0:
             return np.zeros((0, self.rec.cfg.embedding), np.float32)
-        R = self.spec.rec_size
         with stage("align_warp"):
-            x = vision.warp_batch(images, img_index, minv, (R, R), cpad=8, scale=1.0 / self.spec.rec_std,
-                                  mean=self.spec.rec_mean / self.spec.rec_std, std=1.0,
-                                  swap_rb=self.spec.rec_color.lower() == "bgr", device=self.device)
+            x = self.warp_faces(images, img_index, minv, replicate)
             if x.dtype != self.dtype:
                 x = x.to(self.dtype)
         with stage("rec_forward"):
@@ -285,8 +319,43 @@ class MI355XFaceBackend:
         imgs = [it[0] for it in items]
         return self.detect_images(imgs, [it[1] for it in items])
 
+    def _reference_crop(self, img: np.ndarray, landmarks, bbox):
+        """Reference geometry: (source image, dst->src map) of one face, or None for an
+        empty crop (the reference then returns a zero vector)."""
+        src = img
+        if bbox is not None:
+            h, w = img.shape[:2]
+            x1, y1, x2, y2 = (int(v) for v in bbox)
+            x1, x2 = max(0, min(x1, w)), max(0, min(x2, w))
+            y1, y2 = max(0, min(y1, h)), max(0, min(y2, h))
+            if x2 <= x1 or y2 <= y1:
+                return None
+            src = np.ascontiguousarray(img[y1:y2, x1:x2])
+        out = self.spec.rec_size
+        if landmarks is not None and len(landmarks) == 5 and self.spec.align_landmarks:
+            # original-image landmarks, transform applied to the crop (reference behaviour);
+            # cv2.warpAffine: border 0
+            M = vision.similarity_transform(np.asarray(landmarks, np.float32), REFERENCE_TEMPLATE * (out / 112.0))
+            return src, vision.invert_affine(M), False
+        # cv2.resize of the crop (half-pixel centres, edge-replicating)
+        return src, crop_minv((0, 0, src.shape[1], src.shape[0]), out), True
+
     def _embed_batch(self, items):
         # items: (image, landmarks, bbox); identical image objects are uploaded once
+        if self.align_mode == "reference":
+            srcs, minvs, reps, slot = [], [], [], []
+            for img, lm, bb in items:
+                r = self._reference_crop(img, lm, bb)
+                if r is None:
+                    slot.append(-1)
+                    continue
+                slot.append(len(srcs))
+                srcs.append(r[0])
+                minvs.append(r[1])
+                reps.append(r[2])
+            emb = self.embed_faces(srcs, list(range(len(srcs))), np.stack(minvs), reps) if srcs else None
+            dim = self.rec.cfg.embedding
+            return [emb[k] if k >= 0 else np.zeros(dim, np.float32) for k in slot]
         uniq: dict = {}
         images, index, minvs = [], [], []
         for img, lm, bb in items:
