@@ -66,7 +66,17 @@ def _worker_main(wid: int, device: str, factory: str, kwargs: dict, inq, outq, h
             import torch
 
             torch.cuda.set_device(torch.device(device))
-        fn = _resolve(factory)(device, **kwargs)
+        fac = _resolve(factory)
+        kw = dict(kwargs)
+        pool_world = int(kw.pop("_pool_world", 1))
+        import inspect
+
+        params = inspect.signature(fac).parameters
+        if "rank" in params and "rank" not in kw:      # sharded workers (e.g. a label-bank shard)
+            kw["rank"] = wid
+        if "world" in params and "world" not in kw:
+            kw["world"] = pool_world
+        fn = fac(device, **kw)
     except BaseException:  # noqa: BLE001
         outq.put(("fatal", wid, None, traceback.format_exc()))
         return
@@ -143,8 +153,10 @@ class GPUWorkerPool:
         w.inq = self._ctx.Queue()
         w.ready = False
         w.last_hb = time.time()
+        kwargs = dict(self.kwargs)
+        kwargs.setdefault("_pool_world", len(self.workers))
         w.proc = self._ctx.Process(target=_worker_main, name=f"lumen-worker-{w.wid}",
-                                   args=(w.wid, w.device, self.factory, self.kwargs, w.inq, self._outq,
+                                   args=(w.wid, w.device, self.factory, kwargs, w.inq, self._outq,
                                          self.heartbeat_s), daemon=True)
         w.proc.start()
 
@@ -206,6 +218,12 @@ class GPUWorkerPool:
             self.stats["tasks"] += 1
             self.stats["items"] += len(items)
         return fut
+
+    def broadcast(self, kind: str, items: list, timeout: Optional[float] = None) -> list:
+        """The same task on EVERY worker (in worker order) — sharded state such as a
+        label-bank shard per GPU; fails if a worker is not live (its shard is missing)."""
+        futs = [self.submit(kind, list(items), worker=w.wid) for w in self.workers]
+        return [f.result(timeout) for f in futs]
 
     def run(self, kind: str, items: Sequence, timeout: Optional[float] = None) -> list:
         """Split ``items`` into one contiguous shard per live worker; ordered results."""

@@ -89,6 +89,7 @@ class MI355XClipBackend:
         self.load_time = 0.0
         self._img_batcher: Optional[DynamicBatcher] = None
         self._txt_batcher: Optional[DynamicBatcher] = None
+        self.shard_bank = False        # BioCLIP: each DP worker holds a slice of the label bank
         self.is_initialized = False
 
     # ------------------------------------------------------------------ lifecycle
@@ -111,7 +112,7 @@ class MI355XClipBackend:
             self._pool = GPUWorkerPool("lumen_amd.services.clip.backend:dp_worker", devs,
                                        kwargs={"cache_dir": str(r.model_root_path.parent.parent),
                                                "model": r.model_name, "runtime": r.runtime,
-                                               "dataset": r.dataset})
+                                               "dataset": r.dataset, "shard_bank": self.shard_bank})
             sd = load_weights(r.model_root_path)
             self._logit_scale = float(sd["logit_scale"]) if "logit_scale" in sd else cfg.logit_scale
         else:
@@ -221,11 +222,14 @@ class MI355XClipBackend:
                                            "context_length": str(self.context_length)})
 
 
-def dp_worker(device: str, cache_dir: str, model: str, runtime: str, dataset: Optional[str] = None):
+def dp_worker(device: str, cache_dir: str, model: str, runtime: str, dataset: Optional[str] = None,
+              shard_bank: bool = False, rank: int = 0, world: int = 1):
     """GPUWorkerPool factory: one CLIP replica on ``device``; fn(kind, items) -> embeddings.
 
     kind "image": encoded image bytes (decoded on this worker's CPU threads);
-    kind "text": token-id arrays [ctx]."""
+    kind "text": token-id arrays [ctx];
+    kind "bank_topk" (``shard_bank``): items = [(queries [B, D], k, scale, softmax)] -> this
+    worker's label-bank shard candidates (rows rank/world of the memory-mapped bank .npy)."""
     from ...resources.config import ModelConfig, Runtime
     from .resources import ResourceLoader
 
@@ -238,9 +242,19 @@ def dp_worker(device: str, cache_dir: str, model: str, runtime: str, dataset: Op
     m = CLIPModel(cfg, dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32, device="cpu")
     m.load_state_dict_any(load_weights(res.model_root_path))
     m = m.to(dev)
+    bank = None
+    if shard_bank and res.label_embeddings is not None:
+        from ...runtime.label_bank import LabelBank, orient_bank
+
+        emb = orient_bank(res.label_embeddings, len(res.labels) if res.labels is not None else 0, cfg.embed_dim)
+        bank = LabelBank(emb, dev, shard=(rank, world))
 
     @torch.no_grad()
     def fn(kind, items):
+        if kind == "bank_topk":
+            if bank is None:
+                raise RuntimeError("this worker holds no label-bank shard")
+            return [bank.topk_local(q, k, scale, sm) for q, k, scale, sm in items]
         if kind == "image":
             emb = m.encode_image_uint8([torch.from_numpy(i) for i in decode_many(items)])
         elif kind == "text":

@@ -21,7 +21,7 @@ from typing import Any, Optional
 
 import numpy as np
 
-from ...runtime.label_bank import LabelBank
+from ...runtime.label_bank import LabelBank, PoolShardedBank, orient_bank
 from ..base import RuntimeModelInfo
 from .backend import MI355XClipBackend
 
@@ -139,18 +139,29 @@ class BioCLIPModelManager:
     def initialize(self) -> None:
         if self.is_initialized:
             return
+        # with DP workers and a stored bank (TreeOfLife, 10^5-10^6 x 768), every GPU worker
+        # holds 1/world of it (K13): queries are broadcast, candidates merged here
+        shard = self.labels and self.resources.label_embeddings is not None and self.backend.dp_size > 1
+        self.backend.shard_bank = bool(shard)
         self.backend.initialize()
         if self.labels:
-            emb = self.resources.label_embeddings
-            if emb is None:
-                emb = self.backend.text_batch_to_vectors([f"a photo of {n}" for n in self.labels])
-            emb = np.asarray(emb, dtype=np.float32)
             dim = self.backend.cfg.embed_dim
-            if emb.shape[0] != len(self.labels) and emb.shape[1] == len(self.labels) and emb.shape[0] == dim:
-                log.warning("BioCLIP bank stored (D, N); transposing")
-                emb = emb.T
-            self.text_embeddings = emb
-            self.bank = LabelBank(emb, self.backend.device)
+            if shard and self.backend._pool is not None:
+                emb = orient_bank(self.resources.label_embeddings, len(self.labels), dim)
+                self.text_embeddings = emb                  # memory-mapped; never loaded whole here
+                self.bank = PoolShardedBank(self.backend._pool, emb.shape[0])
+                log.info("BioCLIP bank %d x %d sharded over %d DP workers", emb.shape[0], emb.shape[1],
+                         self.backend._pool.size)
+            else:
+                emb = self.resources.label_embeddings
+                if emb is None:
+                    emb = self.backend.text_batch_to_vectors([f"a photo of {n}" for n in self.labels])
+                emb = np.asarray(emb, dtype=np.float32)
+                if emb.shape[0] != len(self.labels) and emb.shape[1] == len(self.labels) and emb.shape[0] == dim:
+                    log.warning("BioCLIP bank stored (D, N); transposing")
+                emb = orient_bank(emb, len(self.labels), dim)
+                self.text_embeddings = emb
+                self.bank = LabelBank(emb, self.backend.device)
         self.is_initialized = True
 
     def _ensure(self):
