@@ -1,0 +1,362 @@
+// FP8 x FP8 GEMM on the gfx950 block-scaled matrix cores (W8A8, per-token x per-channel).
+//
+//   C[M, N] = epi( (A8[M, K] . W8[N, K]^T) * sa[m] * sw[n] )
+//
+// A8 / W8 are OCP e4m3fn (gfx950's fp8 encoding, not the MI300 fnuz one); sa is the
+// per-token activation scale written by the quantising producer (rms_norm_quant_fp8 /
+// quant_rows_fp8 below), sw the per-output-channel weight scale of quantize_fp8_rows.
+// The MFMA is v_mfma_scale_f32_16x16x128_f8f6f4 with unit E8M0 block scales (127): 128
+// k-values per instruction at twice the bf16 per-clock rate (MI355X_MICROARCH.md, "FP8
+// ~5 PF dense: block-scaled ... 2x BF16 per clock").  The fp32 scales are applied once
+// in the epilogue, then the shared GEMM epilogue (fp32 bias, SwiGLU, residual) runs.
+//
+// This replaces the decoder's prefill projections (reference FastVLM decoder.onnx
+// MatMuls, packages/lumen-vlm/src/lumen_vlm/backends/onnxrt_backend.py:420-492) and
+// makes the former bf16 image of the dequantised weights + hipBLASLt path unnecessary.
+//
+// Tile: 128 x 128 x 128 B per K-step, 4 waves (2 x 2), each wave 64 x 64 = 4 x 4 MFMAs.
+// Prefill M is a few hundred tokens, so 128-row tiles keep ~5 x N/128 workgroups in
+// flight (240 for Llama-3-8B qkv at 624 tokens) where 256 x 256 tiles would leave most
+// of the 256 CUs idle.  Operands stream with LDS-DMA (global_load_lds, 16 B per lane)
+// into NSTAGE 32 KiB stages; one counted `s_waitcnt vmcnt` + raw s_barrier per K-step
+// keeps NSTAGE-2 stages in flight across the barrier.  LDS rows are 128 B with the
+// 16-byte chunk XOR swizzle of gemm_epi.h::swz applied on the per-lane *source*
+// address.  Each MFMA lane reads two 16-byte chunks of its row: lane group g = lane/16
+// takes logical chunks g and g+4 (k = 16g..16g+15 and 64+16g..64+16g+15).  The same
+// k permutation is used for A and W, so the dot products are unchanged, and with it
+// every ds_read_b128 lane group hits 64 distinct banks (chunks 2g, 2g+1 would be 2-way).
+#include <cstdlib>
+
+#include "common.h"
+#include "gemm_epi.h"
+
+namespace lumen {
+
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+
+constexpr float FP8_MAX = 448.f;
+
+template <int N>
+__device__ __forceinline__ void f8_vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int NSTAGE, int WN>
+__global__ void __launch_bounds__(128 * WN)
+gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restrict__ sa, const uint8_t* __restrict__ W,
+               int64_t ldw, const float* __restrict__ sw, void* __restrict__ C, int64_t ldc, int M, int N, int K,
+               GemmEpi ep) {
+  constexpr int NW = 2 * WN;             // waves: 2 (M) x WN (N)
+  constexpr int TN = 128 / WN;           // wave tile 64 x TN
+  constexpr int NR = TN / 16;
+  constexpr int PER = 16 / NW;           // glds instructions per wave per operand per stage
+  constexpr int STAGE = 2 * 128 * 128;   // bytes: A image then W image
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_m = (M + 127) / 128, tiles_n = (N + 127) / 128;
+  // XCD-aware: consecutive logical tiles share a W column panel (row tiles fastest), and
+  // xcd_remap hands each XCD a contiguous run of them -> each W panel is read from HBM once
+  const int lin = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = lin % tiles_m, tn = lin / tiles_m;
+  const int m0 = tm * 128, n0 = tn * 128;
+
+  // staging: wave wid, instruction i covers rows (PER*wid + i)*8 + lane/8 of both images
+  const uint8_t* src_a[PER];
+  const uint8_t* src_w[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int r = (PER * wid + i) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    src_a[i] = A + (int64_t)min(m0 + r, M - 1) * lda + c * 16;
+    src_w[i] = W + (int64_t)min(n0 + r, N - 1) * ldw + c * 16;
+  }
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  typedef const __attribute__((address_space(1))) void* g_ptr_t;
+  auto stage = [&](int s, int64_t koff) {
+    char* base = smem + s * STAGE + wid * PER * 1024;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      __builtin_amdgcn_global_load_lds((g_ptr_t)(src_a[i] + koff), (lds_ptr_t)(base + i * 1024), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      __builtin_amdgcn_global_load_lds((g_ptr_t)(src_w[i] + koff), (lds_ptr_t)(base + 128 * 128 + i * 1024), 16, 0,
+                                       0);
+  };
+
+  f32x4_t acc[4][NR];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / 128;
+  const int frow = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < nk) stage(s, (int64_t)s * 128);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt landed for this wave (NSTAGE-2 younger stages may stay in flight) ...
+    if (kt + NSTAGE - 2 < nk) f8_vm_wait<2 * PER * (NSTAGE - 2)>();
+    else f8_vm_wait<0>();
+    // ... and for every wave; every wave is also done reading stage kt-1's buffer
+    __builtin_amdgcn_s_barrier();
+    if (kt + NSTAGE - 1 < nk) stage((kt + NSTAGE - 1) % NSTAGE, (int64_t)(kt + NSTAGE - 1) * 128);
+    const char* sA = smem + (kt % NSTAGE) * STAGE;
+    const char* sW = sA + 128 * 128;
+    i32x8_t fa[4], fb[NR];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int r = wn * TN + j * 16 + frow;
+      const u32x4_t lo = *(const u32x4_t*)(sW + swz(r, g));
+      const u32x4_t hi = *(const u32x4_t*)(sW + swz(r, g + 4));
+      fb[j] = (i32x8_t){(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wm * 64 + i * 16 + frow;
+      const u32x4_t lo = *(const u32x4_t*)(sA + swz(r, g));
+      const u32x4_t hi = *(const u32x4_t*)(sA + swz(r, g + 4));
+      fa[i] = (i32x8_t){(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[i], fb[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+  }
+  __syncthreads();
+
+  // epilogue: per-wave 16-row slabs through LDS; lane -> (row, 16 columns)
+  constexpr int LDSTR = TN + 4;
+  constexpr int LPR = TN / 16;           // lanes per row
+  constexpr int RPP = 64 / LPR;          // rows per pass
+  constexpr int NPASS = RPP >= 16 ? 1 : 16 / RPP;
+  float* es = (float*)smem + wid * 16 * LDSTR;
+  const int cc = (lane % LPR) * 16;
+  const int n = n0 + wn * TN + cc;
+  float cs[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) cs[q] = n + q < N ? sw[n + q] : 0.f;
+  const __amdgpu_buffer_rsrc_t crs = c_rsrc(C);
+  Unroll<0, 4>::run([&](const int i) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) es[(g * 4 + r) * LDSTR + j * 16 + frow] = acc[i][j][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const int rr = p * RPP + lane / LPR;
+      if (rr >= 16) continue;
+      const int m = m0 + wm * 64 + i * 16 + rr;
+      const float rs = m < M ? sa[m] : 0.f;
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cc + q * 4);
+        v[q * 4 + 0] = t[0] * rs * cs[q * 4 + 0];
+        v[q * 4 + 1] = t[1] * rs * cs[q * 4 + 1];
+        v[q * 4 + 2] = t[2] * rs * cs[q * 4 + 2];
+        v[q * 4 + 3] = t[3] * rs * cs[q * 4 + 3];
+      }
+      epi_store16_t<false>(v, m, n, M, N, C, ldc, ep, crs);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  });
+}
+
+template <int NS, int WN>
+static hipError_t launch_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
+                            const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep,
+                            hipStream_t stream) {
+  const size_t lds = (size_t)NS * 2 * 128 * 128;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm_f8_kernel<NS, WN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN>), dim3(tiles), dim3(128 * WN), lds, stream, A, lda, sa, W, ldw, sw, C,
+                     ldc, M, N, K, ep);
+  return hipGetLastError();
+}
+
+hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw, const float* sw,
+                   void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, hipStream_t stream) {
+  if (K % 128 != 0 || N % 16 != 0 || M <= 0 || lda % 16 != 0 || ldw % 16 != 0) return hipErrorInvalidValue;
+  // Measured at M = 624 on the Llama-3-8B projections (profiles/r2_f8_gemm_variants_v1.txt):
+  // grids of more than one wave of workgroups (gate|up: 1120 tiles) run best at 2 stages x
+  // 4 waves (64 KiB LDS -> 2 workgroups per CU overlap each other's barriers); grids that
+  // fit in one wave (qkv / o / down: 160-240 tiles) at 3 stages x 8 waves (2 waves / SIMD).
+  // LUMEN_F8_VARIANT forces one (A/B): 1 = 4 st x 4 w, 2 = 2 st x 4 w, 3 = 3 st x 8 w,
+  // 4 = 4 st x 8 w, 5 = 2 st x 8 w.
+  static const int variant = [] {
+    const char* e = getenv("LUMEN_F8_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  int v = variant;
+  if (v == 0) {
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (cus <= 0) cus = 256;
+    }
+    v = tiles > cus ? 2 : 3;
+  }
+  switch (v) {
+    case 1: return launch_f8<4, 2>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    case 2: return launch_f8<2, 2>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    case 4: return launch_f8<4, 4>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    case 5: return launch_f8<2, 4>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    default: return launch_f8<3, 4>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+  }
+}
+
+// ============================================================================ quantisers
+// Per-token dynamic quantisation: scale[m] = max|y[m, :]| / 448, out = e4m3(y / scale).
+// One 256-thread workgroup per row; rows are re-read (L2-resident) instead of being held
+// in registers so one kernel covers every hidden / intermediate width.
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  v = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  return v;
+}
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  v = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return v;
+}
+
+// 8 floats (already divided by the scale) -> 8 e4m3 bytes
+__device__ __forceinline__ uint2 to_fp8x8(const float* f) {
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+  return make_uint2((unsigned)lo, (unsigned)hi);
+}
+
+__global__ void __launch_bounds__(256) quant_rows_fp8_kernel(const uint16_t* __restrict__ x, int64_t ldx,
+                                                             uint8_t* __restrict__ out, int64_t ldo,
+                                                             float* __restrict__ scale, int K) {
+  __shared__ float red[4];
+  const int64_t m = blockIdx.x;
+  const uint16_t* xr = x + m * ldx;
+  float amax = 0.f;
+  for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
+    float f[8];
+    unpack8(*(const u32x4_t*)(xr + k), f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) amax = fmaxf(amax, fabsf(f[q]));
+  }
+  amax = block_max(amax, red);
+  const float s = fmaxf(amax, 1e-12f) / FP8_MAX;
+  const float inv = 1.f / s;
+  if (threadIdx.x == 0) scale[m] = s;
+  for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
+    float f[8];
+    unpack8(*(const u32x4_t*)(xr + k), f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) f[q] = fminf(fmaxf(f[q] * inv, -FP8_MAX), FP8_MAX);
+    *(uint2*)(out + m * ldo + k) = to_fp8x8(f);
+  }
+}
+
+// RMSNorm (optionally after x += add, written back to resid_out) fused with the
+// per-token fp8 quantisation of its output: the qkv / gate|up GEMM inputs of the decoder.
+// Same numerics as norm_rows_kernel mode 1 (fp32 sum, y = x * rstd * gamma, no
+// intermediate rounding).  The row stays in registers (K <= 16384: 8 chunks of 8 per thread).
+__global__ void __launch_bounds__(256) rms_norm_quant_fp8_kernel(const uint16_t* __restrict__ x, int64_t ldx,
+                                                                 const uint16_t* __restrict__ add, int64_t ldadd,
+                                                                 uint16_t* __restrict__ resid_out, int64_t ldr,
+                                                                 const uint16_t* __restrict__ gamma, float eps,
+                                                                 uint8_t* __restrict__ out, int64_t ldo,
+                                                                 float* __restrict__ scale, int K) {
+  __shared__ float red[4];
+  const int64_t m = blockIdx.x;
+  float v[8][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int k = (threadIdx.x + c * 256) * 8;
+    if (k < K) {
+      unpack8(*(const u32x4_t*)(x + m * ldx + k), v[c]);
+      if (add) {
+        float a[8];
+        unpack8(*(const u32x4_t*)(add + m * ldadd + k), a);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[c][q] += a[q];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ss += v[c][q] * v[c][q];
+    }
+  }
+  if (resid_out) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int k = (threadIdx.x + c * 256) * 8;
+      if (k < K) *(u32x4_t*)(resid_out + m * ldr + k) = pack8(v[c]);
+    }
+  }
+  const float rstd = rsqrtf(block_sum(ss, red) / (float)K + eps);
+  float amax = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int k = (threadIdx.x + c * 256) * 8;
+    if (k < K) {
+      float gm[8];
+      unpack8(*(const u32x4_t*)(gamma + k), gm);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        v[c][q] = v[c][q] * rstd * gm[q];
+        amax = fmaxf(amax, fabsf(v[c][q]));
+      }
+    }
+  }
+  amax = block_max(amax, red);
+  const float s = fmaxf(amax, 1e-12f) / FP8_MAX;
+  const float inv = 1.f / s;
+  if (threadIdx.x == 0) scale[m] = s;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int k = (threadIdx.x + c * 256) * 8;
+    if (k < K) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[c][q] = fminf(fmaxf(v[c][q] * inv, -FP8_MAX), FP8_MAX);
+      *(uint2*)(out + m * ldo + k) = to_fp8x8(v[c]);
+    }
+  }
+}
+
+hipError_t quant_rows_fp8(const uint16_t* x, int64_t ldx, uint8_t* out, int64_t ldo, float* scale, int M, int K,
+                          hipStream_t stream) {
+  if (K % 8 != 0 || M <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(quant_rows_fp8_kernel, dim3(M), dim3(256), 0, stream, x, ldx, out, ldo, scale, K);
+  return hipGetLastError();
+}
+
+hipError_t rms_norm_quant_fp8(const uint16_t* x, int64_t ldx, const uint16_t* add, int64_t ldadd, uint16_t* resid_out,
+                              int64_t ldr, const uint16_t* gamma, float eps, uint8_t* out, int64_t ldo, float* scale,
+                              int M, int K, hipStream_t stream) {
+  if (K % 8 != 0 || K > 16384 || M <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rms_norm_quant_fp8_kernel, dim3(M), dim3(256), 0, stream, x, ldx, add, ldadd, resid_out, ldr,
+                     gamma, eps, out, ldo, scale, K);
+  return hipGetLastError();
+}
+
+}  // namespace lumen

@@ -25,6 +25,13 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
 hipError_t gemm_w8(const uint16_t* A, int64_t lda, const uint8_t* W, int64_t ldw, const float* scale, void* C,
                    int64_t ldc, int M, int N, int K, const GemmEpi& ep, float* ws, uint32_t* cnt, int ksplit,
                    hipStream_t stream);
+hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw, const float* sw,
+                   void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, hipStream_t stream);
+hipError_t quant_rows_fp8(const uint16_t* x, int64_t ldx, uint8_t* out, int64_t ldo, float* scale, int M, int K,
+                          hipStream_t stream);
+hipError_t rms_norm_quant_fp8(const uint16_t* x, int64_t ldx, const uint16_t* add, int64_t ldadd, uint16_t* resid_out,
+                              int64_t ldr, const uint16_t* gamma, float eps, uint8_t* out, int64_t ldo, float* scale,
+                              int M, int K, hipStream_t stream);
 hipError_t gemm_skinny(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
                        int N, int K, const GemmEpi& ep, float* ws, uint32_t* cnt, int ksplit, hipStream_t stream);
 int skinny_ksplit(int N, int K);
@@ -209,6 +216,101 @@ void gemm_w8(const at::Tensor& a, const at::Tensor& w8, const at::Tensor& scale,
   LUMEN_CHECK_HIP(lumen::gemm_w8(bf(a), a.stride(0), reinterpret_cast<const uint8_t*>(w8.data_ptr()), w8.stride(0),
                                  scale.data_ptr<float>(), out.data_ptr(), out.stride(0), (int)M, (int)N, (int)K, ep,
                                  ks > 1 ? ws.data_ptr<float>() : nullptr, cnt, ks, cur_stream()));
+}
+
+// ---------------------------------------------------------------- fp8 x fp8 (W8A8) GEMM
+// out = epi((a8 @ w8^T) * sa[m] * sw[n]): fp32 bias | SwiGLU -> + residual; a8 [M, K] and
+// w8 [N, K] float8_e4m3fn, sa [M] / sw [N] fp32 (per-token / per-channel scales).
+static void check_f8_rows(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat8_e4m3fn && t.dim() == 2 && t.stride(1) == 1 &&
+              t.stride(0) % 16 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name,
+              ": float8_e4m3fn [rows, K] with 16-byte aligned rows");
+}
+void gemm_f8(const at::Tensor& a8, const at::Tensor& sa, const at::Tensor& w8, const at::Tensor& sw,
+             const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& residual, at::Tensor out,
+             int64_t glu) {
+  check_f8_rows(a8, "gemm_f8: a8");
+  check_f8_rows(w8, "gemm_f8: w8");
+  const int64_t M = a8.size(0), K = a8.size(1), N = w8.size(0);
+  TORCH_CHECK(w8.size(1) == K && K % 128 == 0 && N % 16 == 0, "gemm_f8: K % 128 == 0, N % 16 == 0");
+  TORCH_CHECK(sa.is_cuda() && sa.scalar_type() == at::kFloat && sa.numel() >= M && sa.is_contiguous(),
+              "gemm_f8: sa f32 [M]");
+  TORCH_CHECK(sw.is_cuda() && sw.scalar_type() == at::kFloat && sw.numel() == N && sw.is_contiguous(),
+              "gemm_f8: sw f32 [N]");
+  check_gpu(out, "out");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "gemm_f8: out dtype");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(0) >= M && out.size(1) >= (glu ? N / 2 : N),
+              "gemm_f8: out");
+  TORCH_CHECK(!glu || out.scalar_type() == at::kBFloat16, "gemm_f8: glu writes bf16");
+  lumen::GemmEpi ep{};
+  ep.alpha = 1.f;
+  ep.glu = (int)glu;
+  ep.out_f32 = out.scalar_type() == at::kFloat;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->numel() >= N && bias->is_contiguous() &&
+                (bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16), "gemm_f8: bias");
+    ep.bias = bias->data_ptr();
+    ep.bias_f32 = bias->scalar_type() == at::kFloat;
+  }
+  if (residual.has_value() && residual->defined()) {
+    check_bf16_rows(*residual, "residual");
+    ep.residual = bf(*residual);
+    ep.ldr = residual->stride(0);
+  }
+  const at::DeviceGuard guard(a8.device());
+  LUMEN_CHECK_HIP(lumen::gemm_f8(reinterpret_cast<const uint8_t*>(a8.data_ptr()), a8.stride(0), sa.data_ptr<float>(),
+                                 reinterpret_cast<const uint8_t*>(w8.data_ptr()), w8.stride(0), sw.data_ptr<float>(),
+                                 out.data_ptr(), out.stride(0), (int)M, (int)N, (int)K, ep, cur_stream()));
+}
+
+// per-token fp8 quantisation of bf16 rows: out8 [M, K] e4m3fn, scale [M] = amax / 448
+void quant_rows_fp8(const at::Tensor& x, at::Tensor out8, at::Tensor scale) {
+  check_bf16_rows(x, "x");
+  check_f8_rows(out8, "quant_rows_fp8: out8");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(out8.size(0) >= M && out8.size(1) == K && K % 8 == 0, "quant_rows_fp8: shapes");
+  TORCH_CHECK(x.stride(0) % 8 == 0, "quant_rows_fp8: x rows must be 16-byte aligned");
+  TORCH_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale.numel() >= M && scale.is_contiguous(),
+              "quant_rows_fp8: scale f32 [M]");
+  const at::DeviceGuard guard(x.device());
+  LUMEN_CHECK_HIP(lumen::quant_rows_fp8(bf(x), x.stride(0), reinterpret_cast<uint8_t*>(out8.data_ptr()), out8.stride(0),
+                                        scale.data_ptr<float>(), (int)M, (int)K, cur_stream()));
+}
+
+// RMSNorm(x [+ add] -> resid_out) fused with per-token fp8 quantisation of the normed rows
+void rms_norm_quant_fp8(const at::Tensor& x, const c10::optional<at::Tensor>& add,
+                        const c10::optional<at::Tensor>& resid_out, const at::Tensor& gamma, double eps, at::Tensor out8,
+                        at::Tensor scale) {
+  check_bf16_rows(x, "x");
+  check_f8_rows(out8, "rms_norm_quant_fp8: out8");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(K % 8 == 0 && K <= 16384 && x.stride(0) % 8 == 0, "rms_norm_quant_fp8: K % 8 == 0, K <= 16384");
+  TORCH_CHECK(out8.size(0) >= M && out8.size(1) == K, "rms_norm_quant_fp8: out8 shape");
+  TORCH_CHECK(gamma.is_cuda() && gamma.scalar_type() == at::kBFloat16 && gamma.numel() == K && gamma.is_contiguous(),
+              "rms_norm_quant_fp8: gamma bf16 [K]");
+  TORCH_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale.numel() >= M && scale.is_contiguous(),
+              "rms_norm_quant_fp8: scale f32 [M]");
+  const uint16_t* ap = nullptr;
+  int64_t lda = 0;
+  if (add.has_value() && add->defined()) {
+    check_bf16_rows(*add, "add");
+    TORCH_CHECK(add->size(0) >= M && add->size(1) == K && add->stride(0) % 8 == 0, "rms_norm_quant_fp8: add");
+    ap = bf(*add);
+    lda = add->stride(0);
+  }
+  uint16_t* rp = nullptr;
+  int64_t ldr = 0;
+  if (resid_out.has_value() && resid_out->defined()) {
+    check_bf16_rows(*resid_out, "resid_out");
+    TORCH_CHECK(resid_out->size(0) >= M && resid_out->size(1) == K && resid_out->stride(0) % 8 == 0,
+                "rms_norm_quant_fp8: resid_out");
+    rp = const_cast<uint16_t*>(bf(*resid_out));
+    ldr = resid_out->stride(0);
+  }
+  const at::DeviceGuard guard(x.device());
+  LUMEN_CHECK_HIP(lumen::rms_norm_quant_fp8(bf(x), x.stride(0), ap, lda, rp, ldr, bf(gamma), (float)eps,
+                                            reinterpret_cast<uint8_t*>(out8.data_ptr()), out8.stride(0),
+                                            scale.data_ptr<float>(), (int)M, (int)K, cur_stream()));
 }
 
 // profiling: plain GEMM with per-workgroup timestamps (start, prologue, K-loop, epilogue) in dbg [wg, 4]
@@ -525,6 +627,11 @@ TORCH_LIBRARY(lumen, m) {
   m.def("gemm_probe(Tensor a, Tensor w, Tensor(o!) out, Tensor(d!) dbg, int tile) -> ()");
   m.def("gemm_w8(Tensor a, Tensor w8, Tensor scale, Tensor? bias, Tensor? residual, int act, Tensor(o!) out, "
         "int glu) -> ()");
+  m.def("gemm_f8(Tensor a8, Tensor sa, Tensor w8, Tensor sw, Tensor? bias, Tensor? residual, Tensor(o!) out, "
+        "int glu) -> ()");
+  m.def("quant_rows_fp8(Tensor x, Tensor(o!) out8, Tensor(s!) scale) -> ()");
+  m.def("rms_norm_quant_fp8(Tensor x, Tensor? add, Tensor(r!)? resid_out, Tensor gamma, float eps, Tensor(o!) out8, "
+        "Tensor(s!) scale) -> ()");
   m.def("cls_fill(Tensor(a!) x, Tensor cls, Tensor pos, int seq) -> ()");
   m.def("embed_gather(Tensor ids, Tensor table, Tensor? pos, Tensor(o!) out, int seq, int id_offset) -> ()");
   m.def("attention(Tensor q, Tensor k, Tensor v, Tensor(o!) o, Tensor? kv_len, float scale, bool causal) -> ()");
@@ -551,6 +658,9 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("l2norm_", &l2norm_);
   m.impl("gemm_probe", &gemm_probe);
   m.impl("gemm_w8", &gemm_w8);
+  m.impl("gemm_f8", &gemm_f8);
+  m.impl("quant_rows_fp8", &quant_rows_fp8);
+  m.impl("rms_norm_quant_fp8", &rms_norm_quant_fp8);
   m.impl("cls_fill", &cls_fill);
   m.impl("embed_gather", &embed_gather);
   m.impl("attention", &attention);

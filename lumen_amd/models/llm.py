@@ -30,20 +30,22 @@ from torch import nn
 from .. import ops
 from ..ops import llm as lops
 
-# Prefill-shaped projections (>= _PREFILL_BLAS_MIN_ROWS tokens) without a fused SwiGLU go
-# through hipBLASLt: at M = 624 on Llama-3-8B it measured 1.7-1.9x the hand-written MFMA
-# kernels on qkv / o / down (profiles/r1_prefill_gemm_bench_v1.json: 37 / 31 / 88 us vs
-# 69 / 56 / 151 us for the fp8-weight kernel), while decode (M <= 32) stays on the skinny
-# split-K kernels.  With fp8 weights the layer also keeps a bf16 image of the DEQUANTISED
-# fp8 weight for this path (same numerics as the fp8 kernel; +14 GB for Llama-3-8B, cheap
-# against 288 GB of HBM per GPU).  gate|up: hipBLASLt GEMM + one HBM-bound SwiGLU pass
-# (ops.llm.swiglu_rows) instead of the fused-SwiGLU MFMA kernel (132 + ~10 vs 196 us).
+# Prefill-shaped projections (>= _PREFILL_BLAS_MIN_ROWS tokens) of a bf16-weight model
+# without a fused SwiGLU or bias go through hipBLASLt (plain library GEMMs; at M = 624 on
+# Llama-3-8B bf16 they measured 1.7-1.9x the hand-written bf16 MFMA kernels,
+# profiles/r1_prefill_gemm_bench_v1.json).  A bias keeps the hand kernel so it is added in
+# fp32 in the epilogue (HF Qwen2 q/k biases are large).  fp8 models never take this path:
+# their prefill runs W8A8 on the fp8 matrix cores (ops.linear_f8, csrc/gemm_f8.hip) with
+# per-token activation scales produced by the fused RMSNorm+quant kernel, so no bf16 image
+# of the weights is kept (profiles/r2_f8_gemm_bench_v1.jsonl).
 _PREFILL_BLAS = os.environ.get("LUMEN_LLM_PREFILL_BLAS", "1") != "0"
 _PREFILL_BLAS_MIN_ROWS = int(os.environ.get("LUMEN_LLM_PREFILL_BLAS_MIN_ROWS", "128"))
 _PREFILL_BLAS_NAMES = ("qkv", "o", "gu", "down")
 # the unfused gate|up (+ SwiGLU pass) only pays on wide layers: on Qwen2-0.5B (K = 896) it
 # cost FastVLM 1.6 ms of TTFT, on Llama-3-8B (K = 4096) it saved 0.9 ms
 _PREFILL_BLAS_GLU_MIN_K = int(os.environ.get("LUMEN_LLM_PREFILL_BLAS_GLU_MIN_K", "2048"))
+# W8A8 prefill from this many tokens up (decode batches stay on the weight-only skinny kernels)
+_F8_MIN_ROWS = int(os.environ.get("LUMEN_LLM_F8_MIN_ROWS", "33"))
 
 
 def _prefill_blas_ok(name: str, K: int) -> bool:
@@ -224,10 +226,11 @@ class LLM(nn.Module):
 
     @torch.no_grad()
     def quantize_fp8(self, lm_head: bool = True) -> None:
-        """Weight-only fp8: QKV / o / gate|up / down (and an untied lm_head) become OCP
-        e4m3fn with per-output-row fp32 scales (``<name>_s`` buffers).  Decode GEMMs are
-        HBM-bound on weights, so this halves the bytes per generated token; activations,
-        KV cache and accumulation stay bf16 / fp32."""
+        """fp8 decoder: QKV / o / gate|up / down (and an untied lm_head) become OCP e4m3fn
+        with per-output-row fp32 scales (``<name>_s`` buffers).  Decode GEMMs (<= 32 rows)
+        are HBM-bound on weights and stream the fp8 weights into bf16 MFMAs (half the bytes
+        per token); prefill quantises the activations per token and runs fp8 x fp8 on the
+        block-scaled matrix cores (:meth:`_f8_ok`).  Accumulation and epilogues are fp32."""
         if self.weight_dtype == "fp8":
             return
         for l in self.layers:
@@ -235,8 +238,6 @@ class LLM(nn.Module):
                 w8, sc = ops.quantize_fp8_rows(getattr(l, name + "_w"))
                 setattr(l, name + "_w", nn.Parameter(w8, requires_grad=False))
                 l.register_buffer(name + "_s", sc, persistent=False)
-                if w8.is_cuda and _prefill_blas_ok(name, w8.shape[1]):
-                    l.register_buffer(name + "_wb", (w8.float() * sc[:, None]).to(torch.bfloat16), persistent=False)
         if lm_head and self.lm_head is not None:
             w8, sc = ops.quantize_fp8_rows(self.lm_head)
             self.lm_head = nn.Parameter(w8, requires_grad=False)
@@ -246,23 +247,29 @@ class LLM(nn.Module):
     @staticmethod
     def _lin(x, l, name, bias=None, residual=None, out=None, glu=False):
         w = getattr(l, name + "_w")
-        if x.is_cuda and x.shape[0] >= _PREFILL_BLAS_MIN_ROWS and _prefill_blas_ok(name, x.shape[-1]):
-            wb = getattr(l, name + "_wb", None)
-            if wb is None and w.dtype == torch.bfloat16:
-                wb = w
-            if wb is not None and x.dtype == torch.bfloat16:
-                if glu:
-                    assert bias is None and residual is None
-                    return lops.swiglu_rows(torch.mm(x, wb.t()), out=out)
-                if residual is not None:                      # out += x @ W^T (in place on the residual stream)
-                    assert out is None or out.data_ptr() == residual.data_ptr()
-                    return residual.addmm_(x, wb.t())
-                if bias is not None:
-                    b = bias.to(x.dtype)
-                    return torch.addmm(b, x, wb.t(), out=out) if out is not None else torch.addmm(b, x, wb.t())
-                return torch.mm(x, wb.t(), out=out) if out is not None else torch.mm(x, wb.t())
+        if (x.is_cuda and w.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and bias is None
+                and x.shape[0] >= _PREFILL_BLAS_MIN_ROWS and _prefill_blas_ok(name, x.shape[-1])):
+            if glu:
+                assert residual is None
+                return lops.swiglu_rows(torch.mm(x, w.t()), out=out)
+            if residual is not None:                      # out += x @ W^T (in place on the residual stream)
+                assert out is None or out.data_ptr() == residual.data_ptr()
+                return residual.addmm_(x, w.t())
+            return torch.mm(x, w.t(), out=out) if out is not None else torch.mm(x, w.t())
         return ops.linear(x, w, bias=bias, residual=residual, out=out, glu=glu,
                           w_scale=getattr(l, name + "_s", None))
+
+    def _f8_ok(self, T: int) -> bool:
+        """W8A8 prefill: fp8 weights, enough rows, every projection K a multiple of 128."""
+        if self.weight_dtype != "fp8" or T < _F8_MIN_ROWS:
+            return False
+        l = self.layers[0]
+        return all(getattr(l, n + "_w").shape[1] % 128 == 0 for n in ("qkv", "o", "gu", "down"))
+
+    @staticmethod
+    def _lin8(x8, xs, l, name, bias=None, residual=None, out=None, glu=False):
+        return ops.linear_f8(x8, xs, getattr(l, name + "_w"), getattr(l, name + "_s"), bias=bias, residual=residual,
+                             out=out, glu=glu)
 
     # ------------------------------------------------------------------ collectives
     def _all_reduce(self, t: torch.Tensor) -> torch.Tensor:
@@ -284,6 +291,8 @@ class LLM(nn.Module):
 
     def _layers(self, x: torch.Tensor, pos: torch.Tensor, slots: Optional[torch.Tensor], kv, attn_fn) -> torch.Tensor:
         """x [T, hidden] residual stream (updated in place); returns x."""
+        if self._f8_ok(x.shape[0]):
+            return self._layers_f8(x, pos, slots, kv, attn_fn)
         cfg = self.cfg
         D = cfg.head_dim
         eps = cfg.rms_eps
@@ -312,6 +321,42 @@ class LLM(nn.Module):
             else:
                 self._lin(g, l, "down", residual=x, out=x)
             del qkv, att, g
+        if pending is not None:
+            x.add_(self._all_reduce(pending))
+        return x
+
+    def _layers_f8(self, x, pos, slots, kv, attn_fn):
+        """W8A8 layer stack: every projection input is quantised per token by the kernel that
+        produces it (RMSNorm+quant for qkv / gate|up, a row-quant pass for o / down) and the
+        GEMMs run fp8 x fp8 (csrc/gemm_f8.hip).  Same TP structure as :meth:`_layers`."""
+        cfg = self.cfg
+        D, eps, T = cfg.head_dim, cfg.rms_eps, x.shape[0]
+        dev = x.device
+        h8 = torch.empty((T, x.shape[1]), device=dev, dtype=torch.float8_e4m3fn)
+        hs = torch.empty((T,), device=dev, dtype=torch.float32)
+        tp = self.tp.enabled
+        pending: Optional[torch.Tensor] = None
+        for i, l in enumerate(self.layers):
+            add = self._all_reduce(pending) if pending is not None else None
+            ops.rms_norm_quant_fp8(x, l.ln1, eps, add=add, resid_out=x if add is not None else None, out=h8, scale=hs)
+            qkv = self._lin8(h8, hs, l, "qkv", bias=l.qkv_b)
+            kc, vc = (kv.k[i], kv.v[i]) if kv is not None else (None, None)
+            lops.rope_kv(qkv, pos, self.cos_sin, l.H, l.Hkv, D, slots, kc, vc)
+            att = attn_fn(qkv, l, kc, vc)                            # [T, H*D] bf16
+            a8, as_ = ops.quant_rows_fp8(att)
+            if tp:
+                part = self._lin8(a8, as_, l, "o")
+                ops.rms_norm_quant_fp8(x, l.ln2, eps, add=self._all_reduce(part), resid_out=x, out=h8, scale=hs)
+            else:
+                self._lin8(a8, as_, l, "o", residual=x, out=x)
+                ops.rms_norm_quant_fp8(x, l.ln2, eps, out=h8, scale=hs)
+            g = self._lin8(h8, hs, l, "gu", glu=True)
+            g8, gs = ops.quant_rows_fp8(g)
+            if tp:
+                pending = self._lin8(g8, gs, l, "down")
+            else:
+                self._lin8(g8, gs, l, "down", residual=x, out=x)
+            del qkv, att, a8, g, g8
         if pending is not None:
             x.add_(self._all_reduce(pending))
         return x

@@ -152,6 +152,73 @@ def quantize_fp8_rows(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     return (wf / s[:, None]).clamp(-FP8_E4M3_MAX, FP8_E4M3_MAX).to(torch.float8_e4m3fn), s.contiguous()
 
 
+def quant_rows_fp8(x: torch.Tensor, out: Optional[torch.Tensor] = None,
+                   scale: Optional[torch.Tensor] = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """Per-token dynamic fp8: bf16 rows [M, K] -> (e4m3fn [M, K], fp32 scale [M]) with
+    x ~= x8 * scale[:, None] (scale = max|x_m| / 448)."""
+    M, K = x.shape
+    if out is None:
+        out = torch.empty((M, K), device=x.device, dtype=torch.float8_e4m3fn)
+    if scale is None:
+        scale = torch.empty((M,), device=x.device, dtype=torch.float32)
+    if x.is_cuda:
+        hip_ops().quant_rows_fp8(x, out, scale)
+    else:
+        xf = x.float()
+        s = (xf.abs().amax(dim=1) / FP8_E4M3_MAX).clamp_min(1e-12 / FP8_E4M3_MAX)
+        out[:M].copy_((xf / s[:, None]).clamp(-FP8_E4M3_MAX, FP8_E4M3_MAX).to(torch.float8_e4m3fn))
+        scale[:M].copy_(s)
+    return out, scale
+
+
+def rms_norm_quant_fp8(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-6, add: Optional[torch.Tensor] = None,
+                       resid_out: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+                       scale: Optional[torch.Tensor] = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """RMSNorm(x [+ add], stored to ``resid_out``) quantised per token to fp8 in the same
+    kernel: the input of an fp8 x fp8 projection (:func:`linear_f8`)."""
+    M, K = x.shape
+    if out is None:
+        out = torch.empty((M, K), device=x.device, dtype=torch.float8_e4m3fn)
+    if scale is None:
+        scale = torch.empty((M,), device=x.device, dtype=torch.float32)
+    if x.is_cuda:
+        hip_ops().rms_norm_quant_fp8(x, add, resid_out, w, float(eps), out, scale)
+        return out, scale
+    xf = x.float() + (add.float() if add is not None else 0.0)
+    if resid_out is not None:
+        resid_out.copy_(xf.to(resid_out.dtype))
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    return quant_rows_fp8(y, out, scale)
+
+
+def linear_f8(x8: torch.Tensor, x_scale: torch.Tensor, w8: torch.Tensor, w_scale: torch.Tensor,
+              bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
+              out: Optional[torch.Tensor] = None, glu: bool = False,
+              out_dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """W8A8 projection on the gfx950 fp8 matrix cores (csrc/gemm_f8.hip):
+    y = epi((x8 @ w8^T) * x_scale[m] * w_scale[n]) with fp32 bias, SwiGLU (``glu``, see
+    :func:`glu_interleave`) or + residual.  x8 / w8 are e4m3fn, K % 128 == 0."""
+    M, K = x8.shape
+    N = w8.shape[0]
+    NO = N // 2 if glu else N
+    if out is None:
+        out = torch.empty((M, NO), device=x8.device, dtype=out_dtype)
+    if x8.is_cuda:
+        hip_ops().gemm_f8(x8, x_scale, w8, w_scale, bias, residual, out, int(bool(glu)))
+        return out
+    y = (x8.float() @ w8.float().t()) * x_scale.float()[:M, None] * w_scale.float()[None, :]
+    if bias is not None:
+        y = y + bias.float()[:N]
+    if glu:
+        gu = y.view(M, N // 16, 2, 8)
+        out[:, :NO] = (F.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(M, NO).to(out.dtype)
+        return out
+    if residual is not None:
+        y = y + residual.float()[:M, :N]
+    out[:M, :N] = y.to(out.dtype)
+    return out
+
+
 def glu_interleave(w_gate: torch.Tensor, w_up: torch.Tensor) -> torch.Tensor:
     """[I, K] gate / up projections -> [2I, K] rows grouped [gate 8 | up 8] per 16 (``linear(glu=True)``)."""
     I, K = w_gate.shape

@@ -38,3 +38,20 @@ def test_llm_fp8_close_to_bf16_weights():
     got = m.prefill(m.embed_tokens(ids))
     cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0).item()
     assert cos > 0.98, cos       # e4m3 per-channel weights on a random-init model
+
+
+def test_llm_w8a8_prefill_close_to_bf16_weights():
+    """>= 33 prompt tokens: the fp8 model's prefill quantises activations per token (W8A8,
+    RMSNorm+quant / row-quant producers); still close to the unquantised model."""
+    from lumen_amd.models import llm as llm_mod
+
+    cfg = LLM_PRESETS["tiny"]
+    m = LLM(cfg, dtype=torch.float32, device="cpu")
+    m.random_init(4)
+    ids = torch.randint(0, cfg.vocab_size, (64,), generator=torch.Generator().manual_seed(5))
+    ref = m.prefill(m.embed_tokens(ids))
+    m.quantize_fp8()
+    assert m._f8_ok(64) and not m._f8_ok(llm_mod._F8_MIN_ROWS - 1)
+    got = m.prefill(m.embed_tokens(ids))
+    cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0).item()
+    assert cos > 0.97, cos

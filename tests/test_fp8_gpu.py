@@ -57,3 +57,80 @@ def test_llm_fp8_matches_cpu_reference():
     got = gpu.prefill(gpu.embed_tokens(ids.to(DEV)))
     cos = torch.nn.functional.cosine_similarity(got.float().cpu().flatten(), ref.flatten(), dim=0).item()
     assert cos > 0.99, cos
+
+
+# ----------------------------------------------------------------------------- W8A8 (fp8 x fp8 MFMA)
+def _f8_operands(M, N, K, seed):
+    g = torch.Generator().manual_seed(seed)
+    x8, xs = ops.quant_rows_fp8(torch.randn(M, K, generator=g).bfloat16())
+    w8, ws = ops.quantize_fp8_rows(torch.randn(N, K, generator=g) * K ** -0.5)
+    return g, x8, xs, w8, ws
+
+
+def test_gemm_f8_exact_small_integers():
+    """Asymmetric integer operands (exact in e4m3 and in fp32 accumulation): catches any
+    row/column swap or k-permutation mismatch between the A and W fragments."""
+    M, N, K = 160, 144, 256
+    a = (torch.arange(M)[:, None] * 3 + torch.arange(K)[None, :] * 5) % 7 - 3
+    w = (torch.arange(N)[:, None] * 2 + torch.arange(K)[None, :] * 11) % 5 - 2
+    a8, w8 = a.float().to(torch.float8_e4m3fn), w.float().to(torch.float8_e4m3fn)
+    sa = torch.ones(M)
+    sw = torch.arange(1, N + 1).float() / 16
+    ref = (a.float() @ w.float().t()) * sw
+    got = ops.linear_f8(a8.to(DEV), sa.to(DEV), w8.to(DEV), sw.to(DEV), out_dtype=torch.float32)
+    torch.testing.assert_close(got.cpu(), ref, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 128, 128), (33, 896, 896), (129, 4864, 896), (624, 6144, 4096),
+                                   (624, 4096, 14336), (700, 1024, 640)])
+def test_gemm_f8_vs_fp32_reference(M, N, K):
+    g, x8, xs, w8, ws = _f8_operands(M, N, K, M + N)
+    b = torch.randn(N, generator=g)
+    r = torch.randn(M, N, generator=g).bfloat16()
+    ref = (x8.float() @ w8.float().t()) * xs[:, None] * ws[None, :] + b + r.float()
+    got = ops.linear_f8(x8.to(DEV), xs.to(DEV), w8.to(DEV), ws.to(DEV), bias=b.to(DEV), residual=r.to(DEV))
+    assert _rel(got, ref) < 8e-3                     # bf16 output rounding only
+    ref32 = (x8.float() @ w8.float().t()) * xs[:, None] * ws[None, :]
+    got32 = ops.linear_f8(x8.to(DEV), xs.to(DEV), w8.to(DEV), ws.to(DEV), out_dtype=torch.float32)
+    assert _rel(got32, ref32) < 1e-4                 # fp32 accumulation order
+
+
+@pytest.mark.parametrize("M", [7, 300])
+def test_gemm_f8_swiglu(M):
+    K, I = 1024, 2816
+    g = torch.Generator().manual_seed(M)
+    x8, xs = ops.quant_rows_fp8(torch.randn(M, K, generator=g).bfloat16())
+    w8, ws = ops.quantize_fp8_rows(ops.glu_interleave(torch.randn(I, K, generator=g) * K ** -0.5,
+                                                      torch.randn(I, K, generator=g) * K ** -0.5))
+    ref = ops.linear_f8(x8, xs, w8, ws, glu=True)
+    got = ops.linear_f8(x8.to(DEV), xs.to(DEV), w8.to(DEV), ws.to(DEV), glu=True)
+    assert got.shape == (M, I) and _rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,K", [(1, 896), (37, 4096), (624, 14336)])
+def test_quant_rows_fp8_matches_torch(M, K):
+    x = (torch.randn(M, K) * torch.logspace(-2, 2, M)[:, None]).bfloat16()
+    ref8, refs = ops.quant_rows_fp8(x)
+    got8, gots = ops.quant_rows_fp8(x.to(DEV))
+    torch.testing.assert_close(gots.cpu(), refs, rtol=1e-6, atol=0)
+    # e4m3 bytes: round-to-nearest-even on both sides; allow a handful of 1-ulp ties
+    diff = (got8.cpu().view(torch.uint8).int() - ref8.view(torch.uint8).int()).abs()
+    assert diff.max() <= 1 and (diff > 0).float().mean() < 1e-3
+
+
+@pytest.mark.parametrize("M,K,add", [(5, 896, False), (624, 4096, True)])
+def test_rms_norm_quant_fp8(M, K, add):
+    g = torch.Generator().manual_seed(K)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    a = torch.randn(M, K, generator=g).bfloat16() if add else None
+    w = (1 + 0.1 * torch.randn(K, generator=g)).bfloat16()
+    ref_res = torch.empty_like(x) if add else None
+    ref8, refs = ops.rms_norm_quant_fp8(x, w, 1e-5, add=a, resid_out=ref_res)
+    xd = x.to(DEV)
+    got8, gots = ops.rms_norm_quant_fp8(xd, w.to(DEV), 1e-5, add=a.to(DEV) if add else None,
+                                        resid_out=xd if add else None)
+    torch.testing.assert_close(gots.cpu(), refs, rtol=1e-4, atol=0)
+    deq = got8.cpu().float() * gots.cpu()[:, None]
+    assert _rel(deq, ref8.float() * refs[:, None]) < 2e-2
+    if add:
+        torch.testing.assert_close(xd.cpu(), ref_res, rtol=0, atol=0)

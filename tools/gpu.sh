@@ -12,6 +12,7 @@
 #   prof_vlm8b     rocprofv3 kernel stats of the 8B fp8 decode bench
 #   face_ocr       tools/face_ocr_bench.py face + ocr
 #   prof_face / prof_ocr   rocprofv3 kernel stats of the face / OCR bench
+#   f8             fp8 tests (tests/test_fp8_gpu.py) + tools/f8_gemm_bench.py ($F8_SHAPES, $F8_M)
 #   pmc_gemm       PMC counters (MFMA, LDS conflicts, busy) of one ViT-L/14 GEMM shape
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -39,6 +40,9 @@ for task in "$@"; do
     gemm)
       step gemm 500 python -u tools/gemm_bench_tiles.py --tiles="${GEMM_TILES:--1}" --epi "${GEMM_EPI:-plain}" \
         --shapes "${GEMM_SHAPES:-vit}" ;;
+    f8)
+      step f8_tests 300 python -u -m pytest tests/test_fp8_gpu.py -x -q --timeout 120 --timeout-method thread
+      step f8_bench 300 python -u tools/f8_gemm_bench.py --M "${F8_M:-624}" --shapes "${F8_SHAPES:-llama8b}" ;;
     vlm8b) step vlm8b 600 python tools/vlm_bench.py --preset llava-llama3-8b --fp8 ;;
     vlm05) step vlm05 400 python tools/vlm_bench.py --preset fastvlm-0.5b ;;
     prof_vlm8b)
