@@ -46,15 +46,24 @@ class AppService:
 
     @classmethod
     def from_app_config(cls, config: LumenConfig, initialize: bool = True) -> "AppService":
+        """Each enabled service is built and initialised under its GPU set
+        (runtime/placement.py: disjoint GPUs per service, DP workers per GPU)."""
+        from ..runtime import placement
+
         services, names = [], []
-        for name, svc_cfg in config.enabled_services().items():
+        enabled = config.enabled_services()
+        plan = placement.plan_from_env(list(enabled))
+        for name, svc_cfg in enabled.items():
             cls_ = ServiceLoader.get_class(svc_cfg.import_info.registry_class)
-            svc = cls_.from_config(svc_cfg, config.cache_path())
-            if initialize and hasattr(svc, "initialize"):
-                svc.initialize()
+            with placement.use(plan.get(name)):
+                svc = cls_.from_config(svc_cfg, config.cache_path())
+                if initialize and hasattr(svc, "initialize"):
+                    svc.initialize()
             services.append(svc)
             names.append(name)
-        return cls(services, names)
+        app = cls(services, names)
+        app.placement = plan
+        return app
 
     def close(self):
         for s in self.services:

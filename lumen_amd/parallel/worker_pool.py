@@ -4,10 +4,16 @@ The reference runs every model in the gRPC server process, batch 1, on one
 device (SURVEY §2.5 DP row).  Here a service with ``LUMEN_DP_SIZE = N`` owns N
 worker processes, one per GPU (each its own HIP context, caching allocator and
 stream — no GIL or allocator contention between GPUs).  The service's dynamic
-batcher hands a merged batch to :meth:`GPUWorkerPool.run`, which splits it into
-contiguous shards, one per live worker, and concatenates the shard results in
-order.  Inputs travel as pickled bytes/arrays over pipes — they are compressed
-images (tens of KB) or token ids, tiny next to the per-GPU compute.
+batcher runs several dispatcher threads (``concurrency``), each handing a whole merged
+batch to :meth:`GPUWorkerPool.submit` (least in-flight worker), so every GPU has up to
+two batches queued: host decode / transfer of the next batch overlaps the current one.
+:meth:`GPUWorkerPool.run` (split one batch into per-worker shards) stays for SPMD-style
+callers.  Inputs travel pickled over pipes — compressed images (tens of KB) or token
+ids.  Results that are a list of equally shaped numpy rows (embeddings) come back
+through a per-worker shared-memory ring (``shm_slots`` x ``shm_slot_bytes``, created
+by the pool, attached by the worker): the worker writes the stacked array into the next
+slot once the pool has released it (a semaphore per worker), the pool copies it out and
+releases the slot — no pickling of the payload.
 
 Failure detection: every worker sends a heartbeat each
 ``heartbeat_s``; the monitor thread declares a worker lost when its process exits
@@ -46,6 +52,9 @@ class WorkerTaskError(RuntimeError):
     """The worker's batch function raised; carries the remote traceback."""
 
 
+_SHM_MIN_BYTES = 64 * 1024      # smaller results are cheaper to pickle
+
+
 def _resolve(path: str) -> Callable:
     mod, _, attr = path.partition(":")
     return getattr(importlib.import_module(mod), attr)
@@ -59,8 +68,47 @@ def _fault_plan(wid: int) -> Optional[int]:
     return int(n or 0) if int(w) == wid else None
 
 
-def _worker_main(wid: int, device: str, factory: str, kwargs: dict, inq, outq, heartbeat_s: float) -> None:
+def _as_rows(res):
+    """A result that is a list of equally shaped numpy arrays -> one stacked array, else None."""
+    try:
+        import numpy as np
+    except ImportError:  # pragma: no cover
+        return None
+    if not isinstance(res, list) or not res or not all(isinstance(r, np.ndarray) for r in res):
+        return None
+    r0 = res[0]
+    if r0.dtype.hasobject or any(r.shape != r0.shape or r.dtype != r0.dtype for r in res):
+        return None
+    return np.stack(res)
+
+
+class _ShmRing:
+    """Worker side of the result ring: slot k of ``nslots`` at offset k * slot_bytes."""
+
+    def __init__(self, name: str, nslots: int, slot_bytes: int, free_sem):
+        from multiprocessing import shared_memory
+
+        self.shm = shared_memory.SharedMemory(name=name)
+        self.nslots, self.slot_bytes, self.free = nslots, slot_bytes, free_sem
+        self.next = 0
+
+    def put(self, arr):
+        import numpy as np
+
+        if arr.nbytes > self.slot_bytes:
+            return None
+        self.free.acquire()
+        slot = self.next
+        self.next = (self.next + 1) % self.nslots
+        dst = np.ndarray(arr.shape, arr.dtype, buffer=self.shm.buf, offset=slot * self.slot_bytes)
+        dst[...] = arr
+        return slot, arr.shape, arr.dtype.str
+
+
+def _worker_main(wid: int, device: str, factory: str, kwargs: dict, inq, outq, heartbeat_s: float,
+                 shm: Optional[tuple] = None) -> None:
     """Child process body: pin device, build the batch fn, serve tasks until None."""
+    ring = None
     try:
         if device.startswith("cuda"):
             import torch
@@ -77,6 +125,8 @@ def _worker_main(wid: int, device: str, factory: str, kwargs: dict, inq, outq, h
         if "world" in params and "world" not in kw:
             kw["world"] = pool_world
         fn = fac(device, **kw)
+        if shm is not None:
+            ring = _ShmRing(*shm)
     except BaseException:  # noqa: BLE001
         outq.put(("fatal", wid, None, traceback.format_exc()))
         return
@@ -100,7 +150,12 @@ def _worker_main(wid: int, device: str, factory: str, kwargs: dict, inq, outq, h
             os._exit(17)
         try:
             res = fn(kind, items)
-            outq.put(("ok", wid, tid, res))
+            arr = _as_rows(res) if ring is not None else None
+            desc = ring.put(arr) if arr is not None and arr.nbytes >= _SHM_MIN_BYTES else None
+            if desc is not None:
+                outq.put(("okshm", wid, tid, desc))
+            else:
+                outq.put(("ok", wid, tid, res))
         except BaseException:  # noqa: BLE001
             outq.put(("err", wid, tid, traceback.format_exc()))
         done += 1
@@ -117,6 +172,8 @@ class _Worker:
     last_hb: float = 0.0
     inflight: dict = field(default_factory=dict)   # tid -> (Future, submit time)
     restarts: int = 0
+    shm: Any = None          # SharedMemory of the result ring (owned by the pool)
+    shm_free: Any = None     # semaphore: free slots of the ring
 
 
 class GPUWorkerPool:
@@ -125,8 +182,10 @@ class GPUWorkerPool:
 
     def __init__(self, factory: str, devices: Sequence[str], kwargs: Optional[dict] = None, heartbeat_s: float = 1.0,
                  dead_after_s: float = 30.0, respawn: bool = True, start_timeout_s: float = 600.0,
-                 task_timeout_s: Optional[float] = None):
+                 task_timeout_s: Optional[float] = None, shm_slots: int = 4, shm_slot_bytes: int = 8 << 20):
         self.factory = factory
+        self.shm_slots = int(shm_slots)
+        self.shm_slot_bytes = int(shm_slot_bytes)
         self.kwargs = dict(kwargs or {})
         self.heartbeat_s = heartbeat_s
         self.dead_after_s = dead_after_s
@@ -138,7 +197,7 @@ class GPUWorkerPool:
         self._tid = itertools.count(1)
         self._stop = threading.Event()
         self.workers = [_Worker(wid=i, device=d) for i, d in enumerate(devices)]
-        self.stats = {"tasks": 0, "items": 0, "lost": 0, "restarts": 0}
+        self.stats = {"tasks": 0, "items": 0, "lost": 0, "restarts": 0, "shm_results": 0}
         self._fatal: Optional[str] = None
         for w in self.workers:
             self._start(w)
@@ -155,10 +214,32 @@ class GPUWorkerPool:
         w.last_hb = time.time()
         kwargs = dict(self.kwargs)
         kwargs.setdefault("_pool_world", len(self.workers))
+        self._free_shm(w)
+        shm = None
+        if self.shm_slots > 0:
+            from multiprocessing import shared_memory
+
+            try:
+                w.shm = shared_memory.SharedMemory(create=True, size=self.shm_slots * self.shm_slot_bytes)
+                w.shm_free = self._ctx.Semaphore(self.shm_slots)
+                shm = (w.shm.name, self.shm_slots, self.shm_slot_bytes, w.shm_free)
+            except OSError as e:   # no /dev/shm space: results travel pickled
+                log.warning("worker %d: no shared-memory ring (%s)", w.wid, e)
+                w.shm = w.shm_free = None
         w.proc = self._ctx.Process(target=_worker_main, name=f"lumen-worker-{w.wid}",
                                    args=(w.wid, w.device, self.factory, kwargs, w.inq, self._outq,
-                                         self.heartbeat_s), daemon=True)
+                                         self.heartbeat_s, shm), daemon=True)
         w.proc.start()
+
+    @staticmethod
+    def _free_shm(w: _Worker) -> None:
+        if w.shm is not None:
+            try:
+                w.shm.close()
+                w.shm.unlink()
+            except Exception:  # noqa: BLE001
+                pass
+            w.shm = w.shm_free = None
 
     def wait_ready(self, timeout: float) -> None:
         t0 = time.time()
@@ -194,6 +275,9 @@ class GPUWorkerPool:
                     if not fut.done():
                         fut.set_exception(WorkerLostError("pool closed"))
                 w.inflight.clear()
+        self._collector.join(timeout=2)
+        for w in self.workers:
+            self._free_shm(w)
 
     @property
     def size(self) -> int:
@@ -254,13 +338,27 @@ class GPUWorkerPool:
                     w.ready, w.pid = True, int(payload)
                 elif kind == "fatal":
                     self._fatal = str(payload)
-                elif kind in ("ok", "err"):
+                elif kind == "okshm":
+                    payload = self._read_shm(w, payload)
+                    self.stats["shm_results"] += 1
+                    kind = "ok"
+                if kind in ("ok", "err"):
                     fut, _ = w.inflight.pop(tid, (None, 0.0))
                     if fut is not None and not fut.done():
                         if kind == "ok":
                             fut.set_result(payload)
                         else:
                             fut.set_exception(WorkerTaskError(str(payload)))
+
+    def _read_shm(self, w: _Worker, desc) -> list:
+        """Copy a result out of worker w's ring slot and release the slot (messages of one
+        worker arrive in order, so slots are consumed in the order the worker filled them)."""
+        import numpy as np
+
+        slot, shape, dt = desc
+        arr = np.ndarray(shape, np.dtype(dt), buffer=w.shm.buf, offset=slot * self.shm_slot_bytes).copy()
+        w.shm_free.release()
+        return list(arr)
 
     def _watch(self) -> None:
         while not self._stop.wait(self.heartbeat_s / 2):

@@ -6,7 +6,9 @@ requests from all gRPC streams are queued and a single worker thread — the
 only thread that launches work on that model's HIP stream — drains up to
 ``max_batch`` items or waits at most ``max_wait_ms`` after the first item, then
 runs one batched call.  Results are delivered through futures, so callers stay
-synchronous.
+synchronous.  ``concurrency`` > 1 runs that many dispatcher threads on the same
+queue, for batch functions that hand work to a multi-GPU worker pool (several
+batches in flight, one per dispatcher).
 """
 from __future__ import annotations
 
@@ -24,17 +26,20 @@ log = logging.getLogger("lumen.batcher")
 
 class DynamicBatcher:
     def __init__(self, fn: Callable[[Sequence[Any]], Sequence[Any]], max_batch: int = 64, max_wait_ms: float = 2.0,
-                 name: str = "batcher"):
+                 name: str = "batcher", concurrency: int = 1):
         self.fn = fn
         self.max_batch = max(1, int(max_batch))
         self.max_wait = max_wait_ms / 1000.0
         self.name = name
         self._q: "queue.Queue[tuple[Any, Future]]" = queue.Queue()
         self._stop = threading.Event()
-        self._thread = threading.Thread(target=self._loop, name=f"lumen-{name}", daemon=True)
-        self._thread.start()
         self.batches = 0
         self.items = 0
+        self._count_lock = threading.Lock()
+        self._threads = [threading.Thread(target=self._loop, name=f"lumen-{name}-{i}", daemon=True)
+                         for i in range(max(1, int(concurrency)))]
+        for t in self._threads:
+            t.start()
 
     def submit(self, item: Any) -> Future:
         if self._stop.is_set():
@@ -99,12 +104,14 @@ class DynamicBatcher:
                 for _, fut in batch:
                     if not fut.done():
                         fut.set_exception(e)
-            self.batches += 1
-            self.items += len(items)
+            with self._count_lock:
+                self.batches += 1
+                self.items += len(items)
 
     def close(self) -> None:
         self._stop.set()
-        self._thread.join(timeout=2.0)
+        for t in self._threads:
+            t.join(timeout=2.0)
         while True:
             try:
                 _, fut = self._q.get_nowait()

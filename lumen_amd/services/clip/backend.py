@@ -74,9 +74,11 @@ def pick_device(pref: Optional[str]) -> torch.device:
 
 class MI355XClipBackend:
     def __init__(self, resources: ModelResources, device: Optional[str] = None, batch_size: int = 8,
-                 max_batch: int = 256, max_wait_ms: float = 2.0, precision: Optional[str] = None, dp_size: int = 1):
+                 max_batch: int = 256, max_wait_ms: float = 2.0, precision: Optional[str] = None, dp_size: int = 1,
+                 dp_devices: Optional[Sequence[str]] = None):
         self.resources = resources
-        self.dp_size = max(1, int(dp_size))
+        self.dp_devices = list(dp_devices or [])
+        self.dp_size = max(1, len(self.dp_devices) or int(dp_size))
         self._pool = None
         self.device_pref = device
         self.batch_size = batch_size
@@ -108,7 +110,8 @@ class MI355XClipBackend:
             from ...parallel.worker_pool import GPUWorkerPool, default_devices
 
             r = self.resources
-            devs = ["cpu"] * self.dp_size if self.device.type == "cpu" else default_devices(self.dp_size)
+            devs = self.dp_devices or (["cpu"] * self.dp_size if self.device.type == "cpu"
+                                       else default_devices(self.dp_size))
             self._pool = GPUWorkerPool("lumen_amd.services.clip.backend:dp_worker", devs,
                                        kwargs={"cache_dir": str(r.model_root_path.parent.parent),
                                                "model": r.model_name, "runtime": r.runtime,
@@ -121,8 +124,10 @@ class MI355XClipBackend:
             self.model = m.to(self.device)
             self._logit_scale = self.model.logit_scale
         self._load_tokenizer()
-        self._img_batcher = DynamicBatcher(self._encode_images, self.max_batch, self.max_wait_ms, "clip-image")
-        self._txt_batcher = DynamicBatcher(self._encode_texts, self.max_batch, self.max_wait_ms, "clip-text")
+        # with DP workers: 2 dispatchers per GPU, each batch goes whole to the least-loaded worker
+        conc = 2 * self.dp_size if self._pool is not None else 1
+        self._img_batcher = DynamicBatcher(self._encode_images, self.max_batch, self.max_wait_ms, "clip-image", conc)
+        self._txt_batcher = DynamicBatcher(self._encode_texts, self.max_batch, self.max_wait_ms, "clip-text", conc)
         self.load_time = time.time() - t0
         self.is_initialized = True
         log.info("CLIP %s ready on %s in %.2fs (dp %d)", self.resources.model_name, self.device, self.load_time,
@@ -165,7 +170,7 @@ class MI355XClipBackend:
             ids = self.tokenize(texts)
         if self._pool is not None:
             with stage("dp_forward"):
-                return self._pool.run("text", list(ids.numpy()))
+                return self._pool.submit("text", list(ids.numpy())).result()
         with torch.no_grad(), stage("forward"):      # H2D + text tower + D2H (synchronising)
             emb = self.model.encode_text_ids(ids.to(self.device)).float().cpu().numpy()
         return list(emb)
@@ -173,7 +178,7 @@ class MI355XClipBackend:
     def _encode_images(self, payloads: Sequence[bytes]) -> list:
         if self._pool is not None:
             with stage("dp_forward"):
-                return self._pool.run("image", list(payloads))
+                return self._pool.submit("image", list(payloads)).result()
         with stage("decode"):
             imgs = decode_many(payloads)
         with torch.no_grad(), stage("forward"):      # H2D + resize/normalise + tower + D2H
@@ -190,6 +195,13 @@ class MI355XClipBackend:
 
     def image_batch_to_vectors(self, images: Sequence[bytes]) -> np.ndarray:
         self._ensure()
+        if self._pool is not None:       # every chunk in flight at once, spread over the GPUs
+            n = self._pool.size
+            per = min(self.max_batch, max(1, -(-len(images) // n)))
+            with stage("dp_forward"):
+                futs = [self._pool.submit("image", list(images[i:i + per])) for i in range(0, len(images), per)]
+                out = [e for f in futs for e in f.result()]
+            return np.stack(out).astype(np.float32)
         out = []
         for i in range(0, len(images), self.max_batch):
             out.extend(self._encode_images(images[i:i + self.max_batch]))
@@ -276,8 +288,11 @@ def create_backend(backend_settings, resources: ModelResources, runtime: Optiona
         raise ImportError("RKNN runtime is not available on MI355X builds")
     from ...resources.config import AmdRuntimeSettings
 
+    from ...runtime import placement
+
     amd = AmdRuntimeSettings.from_env()
     dev = getattr(backend_settings, "device", None) if backend_settings is not None else None
+    dev, dp_devs = placement.resolve(dev, placement.dp_size_env())
     bs = getattr(backend_settings, "batch_size", 8) if backend_settings is not None else 8
     return MI355XClipBackend(resources, device=dev, batch_size=bs or 8, max_batch=amd.max_batch,
-                             max_wait_ms=amd.max_wait_ms, precision=precision, dp_size=amd.dp_size)
+                             max_wait_ms=amd.max_wait_ms, precision=precision, dp_devices=dp_devs)

@@ -34,6 +34,15 @@ image-clipped bbox, the similarity transform is estimated from the ORIGINAL-imag
 landmarks onto the 96-wide template and applied to the CROP (border 0 at the crop's
 edge), or the crop is resized to 112 when there are no landmarks; an empty crop yields a
 zero vector.  ``LUMEN_FACE_REFERENCE_TEMPLATE=1`` switches the template only.
+
+Data parallelism (BASELINE config 3; reference hot loop face_service.py:516-574 is
+sequential per face): with more than one device (the hub's placement or
+``LUMEN_DP_SIZE``) the backend owns a :class:`GPUWorkerPool`, one worker process per
+GPU, each with its own detector + recogniser (:func:`dp_worker`).  Requests are batched
+here and every batch goes whole to the least-loaded worker (two batches in flight per
+GPU); the worker decodes the JPEGs on its own CPU threads and runs decode -> detect ->
+align -> embed for the whole batch, so nothing but compressed bytes and (bbox,
+landmarks, embedding) rows cross the process boundary.
 """
 from __future__ import annotations
 
@@ -134,8 +143,11 @@ def crop_minv(bbox, out: int) -> np.ndarray:
 
 class MI355XFaceBackend:
     def __init__(self, resources: GenericResources, device: Optional[str] = None, max_batch: int = 64,
-                 max_wait_ms: float = 2.0, max_faces_batch: int = 512):
+                 max_wait_ms: float = 2.0, max_faces_batch: int = 512, dp_devices: Optional[Sequence[str]] = None):
         self.resources = resources
+        self.dp_devices = list(dp_devices or [])
+        self._pool = None
+        self._dp: dict = {}
         self.device_pref = device
         self.max_batch = max_batch
         self.max_wait_ms = max_wait_ms
@@ -160,6 +172,13 @@ class MI355XFaceBackend:
             return
         t0 = time.time()
         self.device = pick_device(self.device_pref)
+        if len(self.dp_devices) > 1:
+            self._init_pool()
+            self.load_time = time.time() - t0
+            self.is_initialized = True
+            log.info("face pack %s ready on %d DP workers %s in %.2fs", self.resources.model_name,
+                     len(self.dp_devices), self.dp_devices, self.load_time)
+            return
         r = self.resources
         cfgp = r.model_root_path / "lumen_face_config.json"
         from .specs import pack_spec
@@ -199,10 +218,33 @@ class MI355XFaceBackend:
         self.is_initialized = True
         log.info("face pack %s ready on %s in %.2fs", r.model_name, self.device, self.load_time)
 
+    def _init_pool(self) -> None:
+        from ...parallel.worker_pool import GPUWorkerPool
+
+        self._pool = GPUWorkerPool("lumen_amd.services.face.backend:dp_worker", self.dp_devices,
+                                   kwargs={"resources": self.resources, "max_batch": self.max_batch})
+        info = self._pool.submit("info", [None]).result()[0]
+        self.spec = info["spec"]
+        self._emb_dim = info["embedding_dim"]
+        self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        conc = 2 * self._pool.size
+        for kind, cap in (("detect", self.max_batch), ("det_emb", self.max_batch), ("embed", self.max_faces_batch)):
+            self._dp[kind] = DynamicBatcher(self._pool_fn(kind), cap, self.max_wait_ms, f"face-dp-{kind}", conc)
+
+    def _pool_fn(self, kind: str):
+        def fn(items):
+            with stage("dp_forward"):
+                return self._pool.submit(kind, list(items)).result()
+        return fn
+
     def close(self) -> None:
-        for b in (self._det_batcher, self._emb_batcher):
+        for b in (self._det_batcher, self._emb_batcher, *self._dp.values()):
             if b is not None:
                 b.close()
+        self._dp = {}
+        if self._pool is not None:
+            self._pool.close()
+            self._pool = None
 
     def _ensure(self):
         if not self.is_initialized:
@@ -382,27 +424,62 @@ class MI355XFaceBackend:
                        nms_threshold: float = 0.4, face_size_min: int = 50, face_size_max: int = 1000
                        ) -> list[FaceDetection]:
         self._ensure()
+        params = DetParams(detection_confidence_threshold, nms_threshold, face_size_min, face_size_max)
+        if self._pool is not None:
+            if not image_bytes:
+                raise InvalidInputError("image_bytes cannot be empty")
+            return self._dp["detect"]((bytes(image_bytes), params))
         img = self.decode(image_bytes)
-        return self.detect_decoded(img, DetParams(detection_confidence_threshold, nms_threshold, face_size_min,
-                                                  face_size_max))
+        return self.detect_decoded(img, params)
 
     def detect_decoded(self, img: np.ndarray, params: DetParams) -> list[FaceDetection]:
         self._ensure()
+        if self._pool is not None:
+            return self._dp["detect"]((img, params))
         return self._det_batcher((img, params))
+
+    def detect_and_embed(self, image_bytes: bytes, params: DetParams, max_faces: int = -1
+                         ) -> list[tuple[FaceDetection, np.ndarray]]:
+        """Detect + embed every face of one image (decoded once; one recogniser batch).
+        A failed embedding yields zero vectors like the reference (face_model.py:357-364)."""
+        self._ensure()
+        if self._pool is not None:
+            if not image_bytes:
+                raise InvalidInputError("image_bytes cannot be empty")
+            return self._dp["det_emb"]((bytes(image_bytes), params, int(max_faces)))
+        img = self.decode(image_bytes)
+        faces = self.detect_decoded(img, params)
+        if 0 < max_faces < len(faces):
+            faces = faces[:max_faces]
+        if not faces:
+            return []
+        try:
+            embs = self.embed_detections(img, faces)
+        except Exception as e:  # noqa: BLE001
+            log.warning("face embedding failed: %s", e)
+            embs = [np.zeros((self.get_info().embedding_dim or 512,), np.float32) for _ in faces]
+        return list(zip(faces, embs))
 
     def face_to_embedding(self, face_image: Optional[bytes] = None, cropped_face_array: Optional[np.ndarray] = None,
                           landmarks: Optional[list] = None) -> np.ndarray:
         self._ensure()
         if face_image is None and cropped_face_array is None:
             raise InvalidInputError("Either face_image or cropped_face_array must be provided")
+        if self._pool is not None and face_image is not None:
+            return self._dp["embed"]((bytes(face_image), landmarks, None))
         img = self.decode(face_image) if face_image is not None else \
             np.ascontiguousarray(np.clip(cropped_face_array, 0, 255).astype(np.uint8))
+        if self._pool is not None:
+            return self._dp["embed"]((img, landmarks, None))
         return self._emb_batcher((img, landmarks, None))
 
     def embed_detections(self, img: np.ndarray, faces: Sequence[FaceDetection]) -> list[np.ndarray]:
         """Embed detected faces of one decoded image (aligned from the full image)."""
         self._ensure()
-        return self._emb_batcher.map([(img, f.landmarks, f.bbox) for f in faces])
+        items = [(img, f.landmarks, f.bbox) for f in faces]
+        if self._pool is not None:
+            return self._dp["embed"].map(items)
+        return self._emb_batcher.map(items)
 
     def get_runtime_info(self) -> BackendInfo:
         return self.get_info()
@@ -411,12 +488,14 @@ class MI355XFaceBackend:
         r = self.resources
         dev = getattr(self, "device", None)
         cuda = dev is not None and dev.type == "cuda"
-        emb = self.rec.cfg.embedding if self.rec is not None else (r.get_embedding_dim() or 512)
+        emb = self.rec.cfg.embedding if self.rec is not None else \
+            (getattr(self, "_emb_dim", None) or r.get_embedding_dim() or 512)
         return BackendInfo(runtime=runtime_name(dev) if dev is not None else "mi355x-hip", device=str(dev or self.device_pref),
                            model_id=r.model_id, model_name=r.model_name, version=r.model_info.version,
                            precisions=("bf16",) if cuda or dev is None else ("fp32",), embedding_dim=emb,
                            extra={"det_size": str(self.spec.det_size), "rec_size": str(self.spec.rec_size),
-                                  "detector": "scrfd", "max_batch": str(self.max_batch)})
+                                  "detector": "scrfd", "max_batch": str(self.max_batch),
+                                  "dp_workers": str(len(self.dp_devices) if self._pool is not None else 1)})
 
 
 def create_backend(settings, resources: GenericResources, runtime: Optional[str] = None) -> MI355XFaceBackend:
@@ -428,6 +507,75 @@ def create_backend(settings, resources: GenericResources, runtime: Optional[str]
         raise DeviceUnavailableError("RKNN runtime is not available on MI355X builds")
     from ...resources.config import AmdRuntimeSettings
 
+    from ...runtime import placement
+
     amd = AmdRuntimeSettings.from_env()
     dev = getattr(settings, "device", None) if settings is not None else None
-    return MI355XFaceBackend(resources, device=dev, max_batch=min(amd.max_batch, 64), max_wait_ms=amd.max_wait_ms)
+    dev, dp_devs = placement.resolve(dev, placement.dp_size_env())
+    return MI355XFaceBackend(resources, device=dev, max_batch=min(amd.max_batch, 64), max_wait_ms=amd.max_wait_ms,
+                             dp_devices=dp_devs)
+
+
+def dp_worker(device: str, resources: GenericResources, max_batch: int = 64):
+    """GPUWorkerPool factory: one detector + recogniser on ``device``; fn(kind, items):
+
+    "detect":  [(jpeg bytes | RGB array, DetParams)] -> [list[FaceDetection]]
+    "det_emb": [(jpeg bytes, DetParams, max_faces)] -> [list[(FaceDetection, embedding)]]
+               (every face of the batch aligned + embedded as ONE recogniser batch)
+    "embed":   [(jpeg bytes | RGB array, landmarks | None, bbox | None)] -> [embedding]
+    "info":    -> [{"spec": FaceSpec, "embedding_dim": int}]
+    A payload that fails to decode yields an InvalidInputError for that request only."""
+    b = MI355XFaceBackend(resources, device=device, max_batch=max_batch)
+    b.initialize()
+
+    def load(x):
+        if isinstance(x, np.ndarray):
+            return x
+        try:
+            return b.decode(x)
+        except InvalidInputError as e:
+            return e
+
+    @torch.no_grad()
+    def fn(kind, items):
+        if kind == "info":
+            return [{"spec": b.spec, "embedding_dim": int(b.rec.cfg.embedding)}]
+        imgs = [load(it[0]) for it in items]
+        ok = [k for k, im in enumerate(imgs) if not isinstance(im, BaseException)]
+        out: list = [imgs[k] for k in range(len(items))]          # decode errors stay in place
+        if kind == "embed":
+            if ok:
+                embs = b._embed_batch([(imgs[k], items[k][1], items[k][2]) for k in ok])
+                for k, e in zip(ok, embs):
+                    out[k] = e
+            return out
+        dets = b.detect_images([imgs[k] for k in ok], [items[k][1] for k in ok]) if ok else []
+        if kind == "detect":
+            for k, d in zip(ok, dets):
+                out[k] = d
+            return out
+        if kind != "det_emb":
+            raise ValueError(f"unknown face task kind {kind!r}")
+        flat, owner = [], []
+        for k, d in zip(ok, dets):
+            mf = items[k][2]
+            d = d[:mf] if 0 < mf < len(d) else d
+            out[k] = d
+            for f in d:
+                flat.append((imgs[k], f.landmarks, f.bbox))
+                owner.append(k)
+        embs: list = []
+        if flat:
+            try:
+                embs = b._embed_batch(flat)
+            except Exception as e:  # noqa: BLE001  (reference: zero vectors on failure)
+                log.warning("face embedding failed: %s", e)
+                embs = [np.zeros((b.rec.cfg.embedding,), np.float32) for _ in flat]
+        per: dict = {k: [] for k in ok}
+        for k, e in zip(owner, embs):
+            per[k].append(e)
+        for k in ok:
+            out[k] = list(zip(out[k], per[k]))
+        return out
+
+    return fn

@@ -57,20 +57,8 @@ class FaceModelManager:
     def detect_and_extract(self, image_bytes: bytes, detection_confidence_threshold: float = 0.7,
                            nms_threshold: float = 0.4, face_size_min: int = 50, face_size_max: int = 1000,
                            max_faces: int = -1) -> list[tuple[FaceDetection, np.ndarray]]:
-        img = self.backend.decode(image_bytes)
-        faces = self.backend.detect_decoded(img, DetParams(detection_confidence_threshold, nms_threshold,
-                                                           face_size_min, face_size_max))
-        if 0 < max_faces < len(faces):
-            faces = faces[:max_faces]
-        if not faces:
-            return []
-        try:
-            embs = self.backend.embed_detections(img, faces)
-        except Exception as e:  # reference: zero vector on failure
-            log.warning("face embedding failed: %s", e)
-            dim = self.get_info().embedding_dim or 512
-            embs = [np.zeros((dim,), np.float32) for _ in faces]
-        return list(zip(faces, embs))
+        return self.backend.detect_and_embed(image_bytes, DetParams(detection_confidence_threshold, nms_threshold,
+                                                                    face_size_min, face_size_max), max_faces)
 
     # ---------------------------------------------------------------- comparisons
     @staticmethod

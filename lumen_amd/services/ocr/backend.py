@@ -147,8 +147,11 @@ def crop_map(box: np.ndarray, rec_h: int) -> tuple[np.ndarray, int]:
 
 class MI355XOcrBackend:
     def __init__(self, resources: GenericResources, device: Optional[str] = None, max_batch: int = 16,
-                 max_wait_ms: float = 2.0, rec_batch: int = 256, bucket: int = 32):
+                 max_wait_ms: float = 2.0, rec_batch: int = 256, bucket: int = 32,
+                 dp_devices: Optional[Sequence[str]] = None):
         self.resources = resources
+        self.dp_devices = list(dp_devices or [])
+        self._pool = None
         self.device_pref = device
         self.max_batch = max_batch
         self.max_wait_ms = max_wait_ms
@@ -184,6 +187,25 @@ class MI355XOcrBackend:
         cfgp = r.model_root_path / "lumen_ocr_config.json"
         self.device = pick_device(self.device_pref)
         self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        if len(self.dp_devices) > 1:
+            # one DBNet + SVTR per GPU worker (dp_worker); batches go whole to the least-loaded
+            # worker, 2 in flight per GPU, JPEG decode on the workers
+            from ...parallel.worker_pool import GPUWorkerPool
+
+            self._pool = GPUWorkerPool("lumen_amd.services.ocr.backend:dp_worker", self.dp_devices,
+                                       kwargs={"resources": r, "max_batch": self.max_batch})
+            pool = self._pool
+
+            def fn(items):
+                with stage("dp_forward"):
+                    return pool.submit("ocr", list(items)).result()
+
+            self._batcher = DynamicBatcher(fn, self.max_batch, self.max_wait_ms, "ocr-dp", 2 * pool.size)
+            self.load_time = time.time() - t0
+            self.is_initialized = True
+            log.info("OCR %s ready on %d DP workers %s in %.2fs", r.model_name, pool.size, self.dp_devices,
+                     self.load_time)
+            return
         if cfgp.exists():
             meta = json.loads(cfgp.read_text())
             dcfg = DBNetConfig(**{k: _tup(v) for k, v in meta["det"].items()})
@@ -214,6 +236,9 @@ class MI355XOcrBackend:
     def close(self) -> None:
         if self._batcher is not None:
             self._batcher.close()
+        if self._pool is not None:
+            self._pool.close()
+            self._pool = None
 
     # ------------------------------------------------------------------ detection
     @torch.no_grad()
@@ -314,16 +339,18 @@ class MI355XOcrBackend:
         self._ensure()
         if not image_bytes:
             raise InvalidInputError("Failed to decode image bytes")
-        try:
-            with stage("decode"):
-                img = decode_rgb(image_bytes)
-        except ValueError as e:
-            raise InvalidInputError(f"Failed to decode image bytes: {e}") from e
+        img = None
+        if self._pool is None:
+            try:
+                with stage("decode"):
+                    img = decode_rgb(image_bytes)
+            except ValueError as e:
+                raise InvalidInputError(f"Failed to decode image bytes: {e}") from e
         p = OcrParams(det_thresh=float(det_threshold), rec_thresh=float(rec_threshold),
                       box_thresh=float(kwargs.get("box_thresh", self.det_config["box_thresh"])),
                       unclip_ratio=float(kwargs.get("unclip_ratio", self.det_config["unclip_ratio"])),
                       use_angle_cls=bool(use_angle_cls))
-        return self._batcher((img, p))
+        return self._batcher((img if img is not None else bytes(image_bytes), p))
 
     def get_info(self) -> BackendInfo:
         r = self.resources
@@ -352,6 +379,40 @@ def create_backend(settings, resources: GenericResources, runtime: Optional[str]
         raise BackendError("RKNN runtime is not available on MI355X builds")
     from ...resources.config import AmdRuntimeSettings
 
+    from ...runtime import placement
+
     amd = AmdRuntimeSettings.from_env()
     dev = getattr(settings, "device", None) if settings is not None else None
-    return MI355XOcrBackend(resources, device=dev, max_batch=min(amd.max_batch, 16), max_wait_ms=amd.max_wait_ms)
+    dev, dp_devs = placement.resolve(dev, placement.dp_size_env())
+    return MI355XOcrBackend(resources, device=dev, max_batch=min(amd.max_batch, 16), max_wait_ms=amd.max_wait_ms,
+                            dp_devices=dp_devs)
+
+
+def dp_worker(device: str, resources: GenericResources, max_batch: int = 16):
+    """GPUWorkerPool factory: DBNet + SVTR on ``device``; fn("ocr", [(jpeg bytes, OcrParams)])
+    -> per image list of OcrResult (decode failures -> InvalidInputError for that image)."""
+    b = MI355XOcrBackend(resources, device=device, max_batch=max_batch)
+    b.initialize()
+
+    def fn(kind, items):
+        if kind != "ocr":
+            raise ValueError(f"unknown OCR task kind {kind!r}")
+        out: list = [None] * len(items)
+        ok = []
+        for k, (payload, _) in enumerate(items):
+            if isinstance(payload, np.ndarray):
+                out[k] = payload
+                ok.append(k)
+                continue
+            try:
+                out[k] = decode_rgb(payload)
+                ok.append(k)
+            except ValueError as e:
+                out[k] = InvalidInputError(f"Failed to decode image bytes: {e}")
+        if ok:
+            res = b._predict_batch([(out[k], items[k][1]) for k in ok])
+            for k, r in zip(ok, res):
+                out[k] = r
+        return out
+
+    return fn

@@ -1,0 +1,203 @@
+"""Multi-GPU serving topology on CPU workers: face / OCR data-parallel worker pools give the
+same results as the single-process backends (reference hot loops: face_service.py:516-574,
+ocr onnxrt_backend.py:150-632), the shared-memory result ring, concurrent dispatchers, and
+the hub's per-service GPU placement plan."""
+import json
+import threading
+
+import numpy as np
+import pytest
+
+from lumen_amd.parallel.worker_pool import GPUWorkerPool
+from lumen_amd.runtime import placement
+from lumen_amd.runtime.batcher import DynamicBatcher
+from lumen_amd.utils.image import encode_jpeg, encode_png
+
+
+# ----------------------------------------------------------------------------- placement
+def test_placement_plan_auto_and_spec():
+    p = placement.plan(["clip", "face", "ocr", "vlm"], 8)
+    assert sorted(i for v in p.values() for i in v) == list(range(8))           # disjoint, all used
+    assert all(len(v) >= 1 for v in p.values()) and len(p["clip"]) >= len(p["ocr"])
+    assert placement.plan(["clip", "face"], 1) == {"clip": [0], "face": [0]}     # shared
+    assert placement.plan(["clip"], 0) == {"clip": []}
+    p = placement.plan(["clip", "face", "ocr"], 8, "face=4,5;clip=0-3")
+    assert p["face"] == [4, 5] and p["clip"] == [0, 1, 2, 3] and p["ocr"] == [6, 7]
+    with pytest.raises(ValueError):
+        placement.plan(["clip"], 4, "clip=5")
+    with pytest.raises(ValueError):
+        placement.parse_spec("clip")
+
+
+def test_placement_resolve(monkeypatch):
+    monkeypatch.delenv("LUMEN_DP_SIZE", raising=False)
+    assert placement.resolve(None) == (None, [])
+    assert placement.resolve("cpu", 2) == ("cpu", ["cpu", "cpu"])
+    with placement.use([4, 5, 6]):
+        assert placement.current() == (4, 5, 6)
+        assert placement.resolve(None) == ("cuda:4", ["cuda:4", "cuda:5", "cuda:6"])
+        assert placement.resolve(None, 1) == ("cuda:4", [])
+        assert placement.resolve("cuda:7") == ("cuda:7", [])       # explicit device wins
+    assert placement.current() is None
+
+
+# ----------------------------------------------------------------------------- pool transport
+def _rows_factory(device, dim=4096):
+    def fn(kind, items):
+        if kind == "small":
+            return [np.full(3, float(x), np.float32) for x in items]
+        return [np.full(dim, float(x), np.float32) for x in items]
+    return fn
+
+
+def test_shm_result_ring_round_trip():
+    pool = GPUWorkerPool("tests.test_dp_serving_cpu:_rows_factory", ["cpu"], shm_slots=2, shm_slot_bytes=1 << 20)
+    try:
+        futs = [pool.submit("rows", list(range(i, i + 16))) for i in range(0, 160, 16)]   # > slots in flight
+        for i, f in zip(range(0, 160, 16), futs):
+            r = f.result(60)
+            assert len(r) == 16 and all(r[k][0] == i + k and r[k].shape == (4096,) for k in range(16))
+        assert pool.stats["shm_results"] == 10
+        small = pool.submit("small", [1, 2]).result(60)                                    # below threshold
+        assert [float(x[0]) for x in small] == [1.0, 2.0] and pool.stats["shm_results"] == 10
+    finally:
+        pool.close()
+
+
+def test_batcher_concurrency_keeps_batches_in_flight():
+    active, peak, lock = [0], [0], threading.Lock()
+    gate = threading.Event()
+
+    def fn(items):
+        with lock:
+            active[0] += 1
+            peak[0] = max(peak[0], active[0])
+        gate.wait(5)
+        with lock:
+            active[0] -= 1
+        return [x * 2 for x in items]
+
+    b = DynamicBatcher(fn, max_batch=2, max_wait_ms=1, name="t", concurrency=3)
+    try:
+        futs = [b.submit(i) for i in range(6)]
+        threading.Timer(0.5, gate.set).start()
+        assert [f.result(10) for f in futs] == [2 * i for i in range(6)]
+        assert peak[0] >= 2
+    finally:
+        b.close()
+
+
+# ----------------------------------------------------------------------------- face DP
+def _face_svc(cache, monkeypatch, dp):
+    from lumen_amd.resources.validator import config_from_dict
+    from lumen_amd.services.face import GeneralFaceService
+    from tests.test_face_service_cpu import _svc_cfg
+
+    if dp > 1:
+        monkeypatch.setenv("LUMEN_DP_SIZE", str(dp))
+    else:
+        monkeypatch.delenv("LUMEN_DP_SIZE", raising=False)
+    cfg = config_from_dict(_svc_cfg(cache))
+    svc = GeneralFaceService.from_config(cfg.services["face"], cache)
+    svc.initialize()
+    return svc
+
+
+def _cos(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
+
+
+LOW = {"detection_confidence_threshold": "0.0", "face_size_min": "0", "nms_threshold": "0.3", "max_faces": "4"}
+
+
+def test_face_dp2_matches_single_process(tmp_path, monkeypatch):
+    from lumen_amd.models.face import write_face_model
+
+    write_face_model(tmp_path / "models" / "buffalo_tiny", "buffalo_tiny")
+    imgs = [encode_jpeg(np.random.default_rng(s).integers(0, 255, (96, 128 + 8 * s, 3), dtype=np.uint8))
+            for s in range(4)]
+    crop = encode_jpeg(np.random.default_rng(9).integers(0, 255, (112, 112, 3), dtype=np.uint8))
+
+    def run(svc):
+        out = [json.loads(svc.handle("face_detect_and_embed", im, "image/jpeg", LOW)[0]) for im in imgs]
+        out.append(json.loads(svc.handle("face_detect", imgs[0], "image/jpeg", LOW)[0]))
+        out.append(json.loads(svc.handle("face_embed", crop, "image/jpeg", {})[0]))
+        return out
+
+    single = _face_svc(tmp_path, monkeypatch, 1)
+    try:
+        ref = run(single)
+    finally:
+        single.close()
+    dp = _face_svc(tmp_path, monkeypatch, 2)
+    try:
+        assert dp.backend._pool is not None and dp.backend._pool.size == 2
+        # concurrent requests from several threads: batches spread over both workers
+        got: list = [None] * 8
+        ths = [threading.Thread(target=lambda k=k: got.__setitem__(k, run(dp))) for k in range(8)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(120)
+        assert dp.backend.get_info().extra["dp_workers"] == "2"
+        with pytest.raises(Exception):
+            dp.handle("face_detect", b"not a jpeg", "image/jpeg", LOW)
+    finally:
+        dp.close()
+    for g in got:
+        assert g is not None and len(g) == len(ref)
+        for a, b in zip(g, ref):
+            if "faces" in a:
+                assert a["count"] == b["count"] > 0
+                for fa, fb in zip(a["faces"], b["faces"]):
+                    np.testing.assert_allclose(fa["bbox"], fb["bbox"], atol=1e-4)
+                    if fa.get("embedding") is not None:      # fp32 CPU convs batch differently: cosine, not bits
+                        assert _cos(fa["embedding"], fb["embedding"]) > 0.99999
+            else:
+                assert _cos(a["vector"], b["vector"]) > 0.99999
+
+
+# ----------------------------------------------------------------------------- OCR DP
+def test_ocr_dp2_matches_single_process(tmp_path, monkeypatch):
+    from lumen_amd.models.ocr import write_ocr_model
+    from lumen_amd.resources.validator import config_from_dict
+    from lumen_amd.services.ocr.service import GeneralOcrService
+    from tests.test_ocr_cpu import _cfg, _rgb
+
+    write_ocr_model(tmp_path / "models" / "ppocr-tiny", "ppocr-tiny")
+    meta = {"detection_threshold": "0.0", "ocr.box_thresh": "0.0", "recognition_threshold": "0.0"}
+    imgs = [encode_png(_rgb(70, 150, s)) for s in range(3)]
+
+    def build(dp):
+        if dp > 1:
+            monkeypatch.setenv("LUMEN_DP_SIZE", str(dp))
+        else:
+            monkeypatch.delenv("LUMEN_DP_SIZE", raising=False)
+        cfg = config_from_dict(_cfg(tmp_path))
+        svc = GeneralOcrService.from_config(cfg.services["ocr"], tmp_path)
+        svc.initialize()
+        return svc
+
+    single = build(1)
+    try:
+        ref = [json.loads(single.handle("ocr", im, "image/png", meta)[0]) for im in imgs]
+    finally:
+        single.close()
+    dp = build(2)
+    try:
+        assert dp.manager.backend._pool is not None and dp.manager.backend._pool.size == 2
+        got: list = [None] * len(imgs)
+        ths = [threading.Thread(target=lambda k=k: got.__setitem__(
+            k, json.loads(dp.handle("ocr", imgs[k], "image/png", meta)[0]))) for k in range(len(imgs))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(120)
+    finally:
+        dp.close()
+    for a, b in zip(got, ref):
+        assert a["count"] == b["count"] >= 1
+        for ia, ib in zip(a["items"], b["items"]):
+            assert ia["box"] == ib["box"] and ia["text"] == ib["text"]
+            assert abs(ia["confidence"] - ib["confidence"]) < 1e-5
