@@ -975,9 +975,15 @@ static hipError_t launch_persist(const uint16_t* A, int64_t lda, const uint16_t*
 //   8 = 256x256 on the 10-slot half-tile ring (deeper prefetch), 9 = 256x256 ping-pong (gemm_pp.hip;
 //   hundreds digit = variant: bit 0 persistent, bit 1 static priority for the lagging group, bit 2 two
 //   phases per K-tile)
+hipError_t gemm_lds128_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc,
+                            int M, int N, int K, const GemmEpi& ep, int variant, hipStream_t stream);
+
+// tile codes 20000 + v: the 128x128 LDS-DMA pipeline of gemm_f8.hip on bf16 operands
+// (v = 0 auto, 1..5 stage / wave variants)
 hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C,
                      int64_t ldc, int M, int N, int K, const GemmEpi& ep, int tile,
                      hipStream_t stream) {
+  if (tile >= 20000) return gemm_lds128_bf16(A, lda, W, ldw, C, ldc, M, N, K, ep, tile - 20000, stream);
   bool allow_split = true;          // tile codes >= 1000: same config without the tail-round split
   if (tile >= 1000) { allow_split = false; tile -= 1000; }
   if (tile < 0) {
@@ -990,10 +996,17 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
     // lagging wave group) beats all of these at K >= 1024 (profiles/r2_gemm_pp_v2.jsonl)
     // residual epilogues at K <= 2048 run the persistent form (next tile's operands stream in
     // during the residual-reading epilogue: +2-7 %, profiles/r2_gemm_pps_phase_v1.txt)
+    // r2 mid-size shapes (a few hundred to a few thousand rows, profiles/r2_gemm_mid_lds128_v1.jsonl): the
+    // 128x128 LDS-DMA pipeline (gemm_f8.hip, bf16 form) beats the register-staged 128x128 / 64x64 tiles
+    // once there are ~150+ 128x128 tiles; fewer tiles (e.g. 577 x 1024 x 4096) stay on 64x64
+    const bool lds_ok = K % 64 == 0 && N % 16 == 0 && lda % 8 == 0 && ldw % 8 == 0 &&
+                        ((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0;
     if (t256 >= 512) tile = K <= 512 ? 245 : (ep.residual && K <= 2048 && M % 256 == 0 && N % 256 == 0 ? 709 : 609);
-    else if (t128 >= 256) tile = 1;
+    else if (t128 >= 256) tile = lds_ok ? 20000 : 1;
     else if (M <= 64) tile = 3;
+    else if (t128 >= 144 && lds_ok) tile = 20005;
     else tile = 2;
+    if (tile >= 20000) return gemm_lds128_bf16(A, lda, W, ldw, C, ldc, M, N, K, ep, tile - 20000, stream);
   }
   // tile = config + 10 * group_m + 100 * epilogue (group_m 0 -> default 4 for the 256x256 LDS-DMA kernel;
   // epilogue 0 = per-wave slabs, 1 = row-coalesced, 2 = row-coalesced write-through, 3 = per-wave write-through)

@@ -322,17 +322,20 @@ __device__ __forceinline__ void epi_store8(float* v, int m, int n, int M, int N,
 //   3. the last arriver reads every slab with sc1 loads and sums them in split order
 //      (deterministic, independent of arrival order) into red[1][m][c].
 // No release/acquire fences: sc1 stores leave L2 before the ticket, sc1 loads bypass L1.
-template <int ROWS>
-__device__ __forceinline__ bool splitk_reduce_last(float (&red)[4][ROWS][17], float* ws, uint32_t* cnt, int M, int N,
+template <int NWV, int ROWS>
+__device__ __forceinline__ bool splitk_reduce_last(float (&red)[NWV][ROWS][17], float* ws, uint32_t* cnt, int M, int N,
                                                    int n0) {
   const int tid = threadIdx.x;
   const int64_t slab = (int64_t)M * N;
   float* mine = ws + (int64_t)blockIdx.y * slab;
   for (int idx = tid; idx < ROWS * 16; idx += blockDim.x) {
     const int m = idx >> 4, c = idx & 15;
-    if (m < M && n0 + c < N)
-      __hip_atomic_store(mine + (int64_t)m * N + n0 + c, red[0][m][c] + red[1][m][c] + red[2][m][c] + red[3][m][c],
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (m < M && n0 + c < N) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) v += red[w][m][c];
+      __hip_atomic_store(mine + (int64_t)m * N + n0 + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();

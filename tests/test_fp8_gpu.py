@@ -113,7 +113,7 @@ def test_quant_rows_fp8_matches_torch(M, K):
     ref8, refs = ops.quant_rows_fp8(x)
     got8, gots = ops.quant_rows_fp8(x.to(DEV))
     torch.testing.assert_close(gots.cpu(), refs, rtol=1e-6, atol=0)
-    # e4m3 bytes: round-to-nearest-even on both sides; allow a handful of 1-ulp ties
+    # e4m3 bytes: round-to-nearest-even on both sides; a few 1-ulp differences
     diff = (got8.cpu().view(torch.uint8).int() - ref8.view(torch.uint8).int()).abs()
     assert diff.max() <= 1 and (diff > 0).float().mean() < 1e-3
 

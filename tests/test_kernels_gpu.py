@@ -25,7 +25,7 @@ def test_native_library_loaded():
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 768, 1024), (131, 3072, 1024), (512, 4096, 1024),
                                    (37, 64, 128), (4096, 1024, 4096), (2, 512, 512), (2570, 1024, 640)])
 @pytest.mark.parametrize("act", [None, "gelu", "quick_gelu"])
-@pytest.mark.parametrize("tile", [-1, 4, 5, 6, 7, 8, 9, 209, 609, 709, 109])
+@pytest.mark.parametrize("tile", [-1, 4, 5, 6, 7, 8, 9, 209, 609, 709, 109, 20000, 20002, 20003])
 def test_gemm_vs_fp32(M, N, K, act, tile):
     g = torch.Generator().manual_seed(M + N + K)
     x = torch.randn(M, K, generator=g).bfloat16()
@@ -37,7 +37,7 @@ def test_gemm_vs_fp32(M, N, K, act, tile):
     assert _rel(got, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 609, 709])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 609, 709, 20002, 20003])
 def test_gemm_tiles_asymmetric(tile):
     # A = I, asymmetric B: catches a transposed C write
     M = N = K = 256

@@ -179,7 +179,7 @@ def test_swiglu_rows(M, N):
 
 
 def test_llm_prefill_blas_matches_kernel_path():
-    """Prefill projections through hipBLASLt (+ SwiGLU pass) vs the all-MFMA path of the same fp8 model."""
+    """bf16 weights: prefill projections through hipBLASLt (+ SwiGLU pass) vs the all-MFMA path."""
     from lumen_amd.models import llm as llm_mod
     cfg = llm_mod.LLM_PRESETS["qwen2-0.5b"]
     old, old_k = llm_mod._PREFILL_BLAS, llm_mod._PREFILL_BLAS_GLU_MIN_K
@@ -187,8 +187,6 @@ def test_llm_prefill_blas_matches_kernel_path():
         llm_mod._PREFILL_BLAS_GLU_MIN_K = 0            # also route gate|up (+ swiglu_rows) at this width
         m = llm_mod.LLM(cfg, device=torch.device(DEV))
         m.random_init(0)
-        m.quantize_fp8()
-        assert hasattr(m.layers[0], "gu_wb") and hasattr(m.layers[0], "down_wb")
         x0 = (torch.randn(300, cfg.hidden_size, generator=torch.Generator().manual_seed(3)) * 0.5).bfloat16().to(DEV)
         a = m.prefill(x0.clone())
         llm_mod._PREFILL_BLAS = False
@@ -197,3 +195,44 @@ def test_llm_prefill_blas_matches_kernel_path():
         llm_mod._PREFILL_BLAS, llm_mod._PREFILL_BLAS_GLU_MIN_K = old, old_k
     assert torch.isfinite(a).all()
     assert _rel(a, b) < 2e-2
+
+
+def test_llm_fp8_w8a8_prefill_vs_weight_only():
+    """fp8 model: W8A8 prefill (fp8 x fp8 MFMA, per-token scales) vs the weight-only fp8 path
+    (bf16 activations) of the same weights; no bf16 weight image is kept."""
+    from lumen_amd.models import llm as llm_mod
+    cfg = llm_mod.LLM_PRESETS["qwen2-0.5b"]
+    m = llm_mod.LLM(cfg, device=torch.device(DEV))
+    m.random_init(0)
+    m.quantize_fp8()
+    assert not any(n.endswith("_wb") for n, _ in m.named_buffers())
+    x0 = (torch.randn(300, cfg.hidden_size, generator=torch.Generator().manual_seed(3)) * 0.5).bfloat16().to(DEV)
+    assert m._f8_ok(300)
+    a = m.prefill(x0.clone())
+    old = llm_mod._F8_MIN_ROWS
+    try:
+        llm_mod._F8_MIN_ROWS = 1 << 30
+        b = m.prefill(x0.clone())
+    finally:
+        llm_mod._F8_MIN_ROWS = old
+    cos = torch.nn.functional.cosine_similarity(a.float().flatten(), b.float().flatten(), dim=0).item()
+    assert torch.isfinite(a).all() and cos > 0.99, cos
+
+
+def test_llm_prefill_large_bias_fp32():
+    """HF-scale q/k biases (Qwen2 has |b| of several units): the prefill adds them in fp32 in the
+    GEMM epilogue (no bf16 rounding of the bias), matching the fp32 CPU model."""
+    from lumen_amd.models import llm as llm_mod
+    cfg = llm_mod.LLM_PRESETS["tiny"]
+    cpu = llm_mod.LLM(cfg, dtype=torch.float32, device="cpu")
+    cpu.random_init(5)
+    with torch.no_grad():
+        for l in cpu.layers:
+            l.qkv_b.copy_(torch.randn(l.qkv_b.shape, generator=torch.Generator().manual_seed(7)) * 8.0)
+    gpu = llm_mod.LLM(cfg, device=torch.device(DEV))
+    gpu.load_state_dict({k: v.to(gpu.state_dict()[k].dtype) for k, v in cpu.state_dict().items()}, strict=False)
+    ids = torch.randint(0, cfg.vocab_size, (200,), generator=torch.Generator().manual_seed(1))
+    ref = cpu.prefill(cpu.embed_tokens(ids))
+    got = gpu.prefill(gpu.embed_tokens(ids.to(DEV)))
+    cos = torch.nn.functional.cosine_similarity(got.float().cpu().flatten(), ref.flatten(), dim=0).item()
+    assert cos > 0.995, cos

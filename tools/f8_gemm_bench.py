@@ -21,12 +21,23 @@ SHAPES = {
 }
 
 
-def _time(fn, iters):
+def _time(fn, iters, graph=False):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
+    if graph:       # decode-shaped launches replay from a hipGraph in serving: time them that way
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(iters):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        s.record()
+        g.replay()
+        e.record()
+    else:
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
     e.synchronize()
     return s.elapsed_time(e) / iters * 1e3   # us
 
@@ -55,6 +66,15 @@ def main():
         x8, xs = ops.quant_rows_fp8(x)
         out = torch.empty(M, N // 2 if glu else N, device=dev, dtype=torch.bfloat16)
         outf = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        if M <= 32:     # decode: the weight-only fp8 skinny kernel (bf16 activations), graph-replayed
+            f = lambda: ops.linear(x, w8, w_scale=ws, out=out, glu=glu)  # noqa: E731
+            f()
+            torch.cuda.synchronize()
+            us = statistics.median(_time(f, a.iters, graph=True) for _ in range(a.rounds))
+            nbytes = N * K + M * K * 2
+            print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "w8_skinny_us": round(us, 2),
+                              "GBs": round(nbytes / us / 1e3, 1)}), flush=True)
+            continue
         cands = {
             "f8f8": lambda: ops.linear_f8(x8, xs, w8, ws, out=out, glu=glu),
             "f8f8+quant": lambda: ops.linear_f8(*ops.quant_rows_fp8(x), w8, ws, out=out, glu=glu),
