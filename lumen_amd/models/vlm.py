@@ -72,6 +72,16 @@ class VLMConfig:
         return VLMConfig(vision=v, llm=l, **rest)
 
 
+def vlm_config_from_hf(c: dict) -> VLMConfig:
+    """FastVLM (``llava_qwen2`` with the FastViTHD / MobileCLIP-L tower) HF ``config.json`` ->
+    VLMConfig, for reference ONNX packs that ship no lumen config."""
+    fv = FASTVIT_PRESETS["fastvithd"]
+    size = int(c.get("image_size") or (c.get("vision_config") or {}).get("image_size") or 1024)
+    return VLMConfig(vision=VisionConfig(image_size=size, patch_size=64, width=fv.final_features, layers=0, heads=1),
+                     llm=LLMConfig.from_hf(c.get("text_config") or c), vision_arch="fastvit", fastvit=fv,
+                     image_token_id=int(c.get("image_token_index", 151646)))
+
+
 VLM_PRESETS = {
     "fastvlm-0.5b": VLMConfig(vision=VisionConfig(image_size=1024, patch_size=64, width=3072, layers=0, heads=1),
                               vision_arch="fastvit", fastvit=FASTVIT_PRESETS["fastvithd"]),

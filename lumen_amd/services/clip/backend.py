@@ -116,11 +116,11 @@ class MI355XClipBackend:
                                        kwargs={"cache_dir": str(r.model_root_path.parent.parent),
                                                "model": r.model_name, "runtime": r.runtime,
                                                "dataset": r.dataset, "shard_bank": self.shard_bank})
-            sd = load_weights(r.model_root_path)
+            sd = load_weights(r.model_root_path, self.precision)
             self._logit_scale = float(sd["logit_scale"]) if "logit_scale" in sd else cfg.logit_scale
         else:
             m = CLIPModel(cfg, dtype=dtype, device="cpu")
-            m.load_state_dict_any(load_weights(self.resources.model_root_path))
+            m.load_state_dict_any(load_weights(self.resources.model_root_path, self.precision))
             self.model = m.to(self.device)
             self._logit_scale = self.model.logit_scale
         self._load_tokenizer()

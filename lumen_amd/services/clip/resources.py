@@ -221,8 +221,11 @@ class ResourceLoader:
         return labels, emb
 
 
-def load_weights(root: Path) -> dict:
-    """Model weights with loaders that execute nothing from the file."""
+def load_weights(root: Path, precision: Optional[str] = None) -> dict:
+    """Model weights with loaders that execute nothing from the file: safetensors / torch
+    ``weights_only`` checkpoints, else the reference's ONNX pack (``onnx/vision[.<prec>].onnx``
+    + ``onnx/text[.<prec>].onnx``) whose initializers are mapped back to the exported
+    model's parameter names (utils/onnx_import.py) -- the graphs themselves never run."""
     import torch
 
     for name in ("model.safetensors", "open_clip_model.safetensors"):
@@ -234,4 +237,12 @@ def load_weights(root: Path) -> dict:
         if (root / name).exists():
             sd = torch.load(str(root / name), map_location="cpu", weights_only=True)
             return sd.get("state_dict", sd) if isinstance(sd, dict) else sd
-    raise ResourceNotFoundError(f"no weights (*.safetensors / *.bin) in {root}")
+    from ...utils import onnx_import
+
+    odir = root / "onnx"
+    vis = onnx_import.pick_file(odir, "vision", precision) if odir.is_dir() else None
+    if vis is not None:
+        txt = onnx_import.pick_file(odir, "text", precision)
+        log.info("CLIP weights from ONNX pack: %s + %s", vis.name, txt.name if txt else "-")
+        return onnx_import.clip_state_dict(vis, txt)
+    raise ResourceNotFoundError(f"no weights (*.safetensors / *.bin / onnx/vision*.onnx) in {root}")

@@ -260,8 +260,12 @@ class MI355XVLMBackend:
         preset = (r.extra.get("lumen_preset") or "").strip()
         if preset in VLM_PRESETS:
             return VLM_PRESETS[preset]
-        raise ResourceNotFoundError(f"{r.model_name}: lumen_vlm_config.json missing (MI355X VLM weights are loaded "
-                                    "from model.safetensors; ONNX graph import is not available in this build)")
+        hfp = r.model_root_path / "config.json"
+        if hfp.exists():
+            from ...models.vlm import vlm_config_from_hf
+
+            return vlm_config_from_hf(json.loads(hfp.read_text()))
+        raise ResourceNotFoundError(f"{r.model_name}: no lumen_vlm_config.json, preset or HF config.json")
 
     def _tp_spec(self) -> dict:
         r = self.resources
@@ -276,12 +280,20 @@ class MI355XVLMBackend:
         self.cfg = cfg
         m = VLM(cfg, self.tp, dtype=dtype, device=self.device)
         wp = self.resources.model_root_path / "model.safetensors"
+        from ...utils import onnx_import
+
+        pack = onnx_import.find_vlm_pack(self.resources.model_root_path, self.resources.precision)
         if wp.exists():
             m.load_pack_state_dict(load_safetensors(wp))
+        elif pack is not None:
+            # the reference's FastVLM ONNX pack: initializers mapped onto the native FastViTHD +
+            # projector + decoder (the graphs are not executed)
+            log.info("VLM weights from ONNX pack %s", [p.name for p in pack])
+            onnx_import.load_vlm(m, *pack)
         elif self.resources.extra.get("random_init"):
             m.random_init(int(self.resources.extra.get("seed", 0)))
         else:
-            raise ResourceNotFoundError(f"{self.resources.model_name}: model.safetensors missing")
+            raise ResourceNotFoundError(f"{self.resources.model_name}: model.safetensors / onnx pack missing")
         self.model = m.eval()
         if (self.resources.precision or "").lower() in ("fp8", "e4m3", "fp8_e4m3") or \
                 os.environ.get("LUMEN_VLM_FP8", "0") == "1":
