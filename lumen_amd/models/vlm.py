@@ -178,20 +178,45 @@ class VLM(nn.Module):
         return out, starts
 
     @torch.no_grad()
-    def build_prefill(self, ids: Sequence[int], images: Sequence[torch.Tensor]) -> torch.Tensor:
-        """Token embeddings with image rows spliced in -> x [T, hidden] on the model device."""
-        full, starts = self.expand_image_tokens(ids, len(images))
+    def build_prefill(self, ids: Sequence[int], images: Sequence[torch.Tensor],
+                      n_images: Optional[int] = None) -> torch.Tensor:
+        """Token embeddings with image rows spliced in -> x [T, hidden] on the model device.
+
+        Tensor parallel: every rank embeds the text (vocab-parallel lookup + all-reduce), but
+        only TP rank 0 holds the images (``n_images`` tells the others how many) and runs the
+        vision tower + projector; the [N_img, hidden] features are broadcast to the group
+        (one RCCL broadcast instead of N-1 redundant JPEG decodes and vision towers)."""
+        n = len(images) if n_images is None else int(n_images)
+        full, starts = self.expand_image_tokens(ids, n)
         dev = self.device
         t = torch.tensor(full, dtype=torch.long, device=dev)
         x = self.llm.embed_tokens(t)
         N = self.cfg.num_image_tokens
-        if starts:
-            if all(s == starts[0] + i * N for i, s in enumerate(starts)):
-                self.encode_images(images[:len(starts)], out=x[starts[0]:starts[0] + N * len(starts)])
-            else:
-                emb = self.encode_images(images[:len(starts)])
+        if not starts:
+            return x
+        tp = self.llm.tp
+        contiguous = all(s == starts[0] + i * N for i, s in enumerate(starts))
+        if tp.enabled:
+            import torch.distributed as dist
+
+            buf = x[starts[0]:starts[0] + N * len(starts)] if contiguous else \
+                torch.empty((N * len(starts), x.shape[1]), device=dev, dtype=x.dtype)
+            if tp.rank == 0:
+                self.encode_images(images[:len(starts)], out=buf)
+            staged = buf.cpu() if dist.get_backend(tp.group) == "gloo" and buf.is_cuda else buf
+            dist.broadcast(staged, src=dist.get_global_rank(tp.group, 0), group=tp.group)
+            if staged is not buf:
+                buf.copy_(staged)
+            if not contiguous:
                 for i, s in enumerate(starts):
-                    x[s:s + N] = emb[i * N:(i + 1) * N]
+                    x[s:s + N] = buf[i * N:(i + 1) * N]
+            return x
+        if contiguous:
+            self.encode_images(images[:len(starts)], out=x[starts[0]:starts[0] + N * len(starts)])
+        else:
+            emb = self.encode_images(images[:len(starts)])
+            for i, s in enumerate(starts):
+                x[s:s + N] = emb[i * N:(i + 1) * N]
         return x
 
     # ------------------------------------------------------------------ weights

@@ -61,6 +61,11 @@ def env_world() -> tuple[int, int, int]:
 
 
 def _pick_backend(device: torch.device) -> str:
+    """RCCL on GPUs, gloo on CPU; ``LUMEN_DIST_BACKEND`` overrides (e.g. gloo for several ranks
+    sharing one GPU in tests: RCCL refuses two ranks on the same device)."""
+    env = os.environ.get("LUMEN_DIST_BACKEND")
+    if env:
+        return env
     return "nccl" if device.type == "cuda" else "gloo"
 
 

@@ -116,6 +116,8 @@ class Sampler:
         if tp.enabled:
             import torch.distributed as dist
 
+            if v.is_cuda and dist.get_backend(tp.group) == "gloo":    # gloo gathers host tensors only
+                v, i, lse = v.cpu(), i.cpu(), lse.cpu()
             vs = [torch.empty_like(v) for _ in range(tp.world)]
             is_ = [torch.empty_like(i) for _ in range(tp.world)]
             ls = [torch.empty_like(lse) for _ in range(tp.world)]
@@ -142,23 +144,78 @@ class Sampler:
 
 
 class TPSync:
-    """Step broadcast from rank 0 to the follower ranks of a TP group."""
+    """Step broadcast from rank 0 to the follower ranks of a TP group.
 
-    def __init__(self, group=None, src: int = 0):
+    Every step starts with a fixed 8 x int32 header broadcast.  Decode steps (the per-token
+    critical path) then send ONE int32 payload of fixed layout -- ids, positions, cache
+    slots, context lengths, block table -- instead of a pickled object (two broadcasts +
+    pickling on both sides); the header carries the op, batch, table width, top-k and the
+    graph flag.  Prefill / control messages and decode steps whose sampling needs per-row
+    state (temperatures, repetition-penalty token sets) fall back to an object broadcast.
+    The payload lives on the device the group's backend moves (GPU for RCCL, host for gloo).
+    """
+
+    OBJ, DECODE = 1, 2
+
+    def __init__(self, group=None, src: int = 0, device: Optional[torch.device] = None):
+        import torch.distributed as dist
+
         self.group, self.src = group, src
+        if device is None:
+            be = dist.get_backend(group) if dist.is_initialized() else "gloo"
+            device = torch.device("cuda", torch.cuda.current_device()) if be == "nccl" else torch.device("cpu")
+        self.device = device
+        self.hdr = torch.zeros(8, dtype=torch.int32, device=device)
+        self.stats = {"tensor_steps": 0, "object_steps": 0}
+
+    def _bcast(self, t: torch.Tensor) -> None:
+        import torch.distributed as dist
+
+        dist.broadcast(t, src=self.src, group=self.group)
 
     def send(self, msg) -> None:
         import torch.distributed as dist
 
+        self.hdr.fill_(0)
+        self.hdr[0] = self.OBJ
+        self._bcast(self.hdr)
         obj = [msg]
         dist.broadcast_object_list(obj, src=self.src, group=self.group)
+        self.stats["object_steps"] += 1
+
+    def send_decode(self, ids, pos, slots, bt, ctx, spec, graph: bool) -> None:
+        if spec["inv"] is not None or spec["pen"] is not None:
+            self.send(("decode", ids, pos, slots, bt, ctx, spec, graph))
+            return
+        B, W = len(ids), bt.shape[1]
+        h = torch.tensor([self.DECODE, B, W, spec["k"], int(graph), 0, 0, 0], dtype=torch.int32)
+        self.hdr.copy_(h)
+        self._bcast(self.hdr)
+        pay = np.concatenate([np.asarray(ids, np.int64).astype(np.int32), np.asarray(pos, np.int32),
+                              np.asarray(slots, np.int64).astype(np.int32), np.asarray(ctx, np.int32),
+                              np.asarray(bt, np.int32).reshape(-1)])
+        self._bcast(torch.from_numpy(pay).to(self.device))
+        self.stats["tensor_steps"] += 1
 
     def recv(self):
         import torch.distributed as dist
 
-        obj = [None]
-        dist.broadcast_object_list(obj, src=self.src, group=self.group)
-        return obj[0]
+        self._bcast(self.hdr)
+        h = self.hdr.cpu().tolist()
+        if h[0] == self.OBJ:
+            obj = [None]
+            dist.broadcast_object_list(obj, src=self.src, group=self.group)
+            return obj[0]
+        B, W, k, graph = h[1], h[2], h[3], bool(h[4])
+        pay = torch.empty(4 * B + B * W, dtype=torch.int32, device=self.device)
+        self._bcast(pay)
+        p = pay.cpu().numpy()
+        ids = p[:B].astype(np.int64)
+        pos = p[B:2 * B].copy()
+        slots = p[2 * B:3 * B].astype(np.int64)
+        ctx = p[3 * B:4 * B].copy()
+        bt = p[4 * B:].reshape(B, W).copy()
+        return ("decode", ids, pos, slots, bt, ctx, {"k": k, "inv": None, "pen": None, "pen_ids": None}, graph)
 
 
 class DecodeGraphs:
@@ -247,7 +304,10 @@ class DecodeGraphs:
 class LLMEngine:
     def __init__(self, llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.Tensor], max_batch: int = 64,
                  max_prefill_per_step: int = 4, tp_sync: Optional[TPSync] = None, name: str = "vlm",
-                 use_graphs: Optional[bool] = None, prefill_chunk: Optional[int] = None):
+                 use_graphs: Optional[bool] = None, prefill_chunk: Optional[int] = None,
+                 follower_args: Optional[Callable[[Any], Any]] = None):
+        """``follower_args``: what the TP followers receive instead of the prefill arguments
+        (the VLM strips the image: only rank 0 decodes it and runs the vision tower)."""
         self.llm = llm
         self.kv = kv
         self.build = prefill_builder
@@ -267,8 +327,13 @@ class LLMEngine:
         if use_graphs is None:
             use_graphs = os.environ.get("LUMEN_HIP_GRAPHS", "1") == "1"
         self.graphs: Optional[DecodeGraphs] = None
-        if use_graphs and self.device.type == "cuda" and not llm.tp.enabled:
+        # under TP every rank captures / replays the same decode graphs in lockstep (the leader's
+        # step descriptor says when); the in-graph all-reduces are the IPC one-shot kernel or RCCL
+        if use_graphs and llm.tp.enabled:
+            use_graphs = os.environ.get("LUMEN_TP_GRAPHS", "1") == "1"
+        if use_graphs and self.device.type == "cuda":
             self.graphs = DecodeGraphs(llm, kv, max_batch, -(-llm.cfg.max_position // 64))
+        self.follower_args = follower_args
         self._thread = threading.Thread(target=self._loop, name=f"lumen-{name}-engine", daemon=True)
         self._thread.start()
 
@@ -350,7 +415,8 @@ class LLMEngine:
             if self.sync is not None:
                 # followers must enter the build (its vocab-parallel embedding all-reduce)
                 # together with us: announce it before building the inputs
-                self.sync.send(("pbuild", r.rid, r.prefill_args))
+                fa = self.follower_args(r.prefill_args) if self.follower_args is not None else r.prefill_args
+                self.sync.send(("pbuild", r.rid, fa))
                 x = self.build(r.prefill_args)
                 if x.shape[0] != r.prompt_len:
                     raise RuntimeError(f"prefill built {x.shape[0]} rows for a {r.prompt_len}-token prompt")
@@ -411,9 +477,10 @@ class LLMEngine:
         bt = self.kv.block_table([r.rid for r in reqs])
         ctx = pos + 1
         spec = Sampler.spec(reqs)
+        graph = self.graphs is not None and bt.shape[1] <= self.graphs.max_blocks
         if self.sync is not None:
-            self.sync.send(("decode", ids, pos, slots, bt, ctx, spec))
-        logits = self._decode_step(ids, pos, slots, bt, ctx)
+            self.sync.send_decode(ids, pos, slots, bt, ctx, spec, graph)
+        logits = self._decode_step(ids, pos, slots, bt, ctx, graph)
         toks = self.sampler.pick(self.sampler.candidates(logits, spec), reqs)
         self.stats["decode_steps"] += 1
         still = []
@@ -425,12 +492,14 @@ class LLMEngine:
                 still.append(r)
         self._running = still
 
-    def _decode_step(self, ids, pos, slots, bt, ctx) -> torch.Tensor:
+    def _decode_step(self, ids, pos, slots, bt, ctx, graph: bool = True) -> torch.Tensor:
         d = self.device
-        if self.graphs is not None and bt.shape[1] <= self.graphs.max_blocks:
+        if graph and self.graphs is not None and bt.shape[1] <= self.graphs.max_blocks:
             try:
                 return self.graphs.run(ids, pos, slots, bt, ctx)
             except Exception as e:  # noqa: BLE001 - capture unsupported: fall back to eager launches
+                if self.sync is not None:
+                    raise            # TP ranks must not diverge: surface instead of falling back
                 log.warning("hipGraph decode disabled: %s", e)
                 self.graphs = None
         return self.llm.decode(torch.from_numpy(ids).to(d), torch.from_numpy(pos).to(d),
@@ -460,12 +529,17 @@ class LLMEngine:
                     self._running = []
 
 
-def follower_loop(llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.Tensor], sync: TPSync) -> None:
+def follower_loop(llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.Tensor], sync: TPSync,
+                  max_batch: int = 64) -> None:
     """Non-zero TP ranks: replay rank 0's steps so every collective is matched."""
     sampler = Sampler(llm)
     ws: dict = {}
     xs: dict = {}                            # rid -> prefill embeddings of prompts being chunk-prefilled
     dev = llm.embed.device
+    graphs = None
+    if dev.type == "cuda" and os.environ.get("LUMEN_HIP_GRAPHS", "1") == "1" and \
+            os.environ.get("LUMEN_TP_GRAPHS", "1") == "1":
+        graphs = DecodeGraphs(llm, kv, max_batch, -(-llm.cfg.max_position // 64))   # the leader's buckets
     while True:
         msg = sync.recv()
         kind = msg[0]
@@ -483,8 +557,11 @@ def follower_loop(llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.
                 if last:
                     sampler.candidates(logits, spec)
             elif kind == "decode":
-                _, ids, pos, slots, bt, ctx, spec = msg
-                logits = llm.decode(torch.from_numpy(ids).to(dev), torch.from_numpy(pos).to(dev),
-                                    torch.from_numpy(slots).to(dev), kv, torch.from_numpy(bt).to(dev),
-                                    torch.from_numpy(ctx).to(dev), workspace=ws)
+                _, ids, pos, slots, bt, ctx, spec, graph = msg
+                if graph and graphs is not None:
+                    logits = graphs.run(ids, pos, slots, bt, ctx)
+                else:
+                    logits = llm.decode(torch.from_numpy(ids).to(dev), torch.from_numpy(pos).to(dev),
+                                        torch.from_numpy(slots).to(dev), kv, torch.from_numpy(bt).to(dev),
+                                        torch.from_numpy(ctx).to(dev), workspace=ws)
                 sampler.candidates(logits, spec)

@@ -325,7 +325,8 @@ class MI355XVLMBackend:
 
             sync = TPSync(self.tp.group, src=0)
         self._build()
-        self.engine = LLMEngine(self.model.llm, self.kv, self._build_prefill, max_batch=self.max_batch, tp_sync=sync)
+        self.engine = LLMEngine(self.model.llm, self.kv, self._build_prefill, max_batch=self.max_batch, tp_sync=sync,
+                                follower_args=self._follower_args)
         self.load_time = time.time() - t0
         self._initialized = True
         log.info("VLM %s ready on %s in %.2fs (TP %d, KV cache %d tokens, %.1f GB)", self.resources.model_name,
@@ -337,7 +338,8 @@ class MI355XVLMBackend:
 
         self._build()
         self._initialized = True
-        follower_loop(self.model.llm, self.kv, self._build_prefill, TPSync(self.tp.group, src=0))
+        follower_loop(self.model.llm, self.kv, self._build_prefill, TPSync(self.tp.group, src=0),
+                      max_batch=self.max_batch)
         self._initialized = False
 
     def close(self) -> None:
@@ -430,9 +432,16 @@ class MI355XVLMBackend:
 
     # ------------------------------------------------------------------ generation
     def _build_prefill(self, args) -> torch.Tensor:
-        ids, img = args
+        ids, img = args[0], args[1]
+        if len(args) > 2:                    # TP follower: no image here, rank 0 broadcasts its features
+            return self.model.build_prefill(ids, [], n_images=args[2])
         tens = [torch.from_numpy(img)] if img is not None else []
         return self.model.build_prefill(ids, tens)
+
+    @staticmethod
+    def _follower_args(args):
+        ids, img = args[0], args[1]
+        return (ids, None, 1 if img is not None else 0)
 
     def jpeg_draft_size(self):
         """JPEG DCT-domain downscaled decode (libjpeg scale 1/2, 1/4, 1/8) down to no less than the

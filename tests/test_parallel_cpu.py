@@ -163,7 +163,9 @@ def _vlm_leader(cache, tp, q):
         for prompt in ("Describe.", "What is this?"):
             body, _, _ = s.handle("vlm_generate", img, "image/jpeg", {"prompt": prompt, "max_new_tokens": "9"})
             outs.append(_json.loads(body)["text"])
-        q.put({"texts": outs, "tp": s.backend.tp.world, "chunks": s.backend.engine.stats["prefill_chunks"]})
+        sync = s.backend.engine.sync
+        q.put({"texts": outs, "tp": s.backend.tp.world, "chunks": s.backend.engine.stats["prefill_chunks"],
+               "sync": dict(sync.stats) if sync is not None else None})
     finally:
         s.close()
 
@@ -186,6 +188,8 @@ def test_vlm_tensor_parallel_serving_matches_tp1(tmp_path):
     assert res[2]["tp"] == 2 and res[1]["tp"] == 1
     assert res[2]["chunks"] > res[1]["chunks"]          # TP=2 run prefilled in 16-token chunks
     assert res[2]["texts"] == res[1]["texts"]
+    # greedy decode steps travel as fixed int32 descriptors, prefill/control as objects
+    assert res[2]["sync"]["tensor_steps"] >= 8 and res[2]["sync"]["object_steps"] >= 2
 
 
 def test_clip_dp_serving_matches_single_process(tmp_path, monkeypatch):

@@ -1,0 +1,65 @@
+"""Tensor-parallel VLM decode on MI355X: TP=2 (two ranks sharing the box's one GPU, gloo for the
+host-side step broadcast / candidate gather, the IPC one-shot all-reduce inside the decode
+graphs) with hipGraph-captured decode steps generates the same greedy text as TP=1.  Decode
+steps travel as fixed int32 descriptors; only rank 0 decodes the image and runs the vision
+tower (its features are broadcast).  CPU twin: test_parallel_cpu.py::test_vlm_tensor_parallel_*."""
+import multiprocessing as mp
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _leader(cache, tp, q):
+    import json as _json
+
+    os.environ["LUMEN_TP_SIZE"] = str(tp)
+    os.environ["LUMEN_DIST_BACKEND"] = "gloo"          # RCCL refuses two ranks on one device
+    from lumen_amd.resources.validator import config_from_dict
+    from lumen_amd.services.vlm import GeneralFastVLMService
+    from lumen_amd.utils.image import encode_jpeg
+    import numpy as np
+
+    cfg = {"metadata": {"version": "1.0.0", "region": "other", "cache_dir": cache},
+           "deployment": {"mode": "single", "service": "vlm"}, "server": {"port": 50558, "host": "127.0.0.1"},
+           "services": {"vlm": {"enabled": True, "package": "lumen_vlm",
+                                "import_info": {"registry_class": "lumen_vlm.fastvlm.GeneralFastVLMService",
+                                                "add_to_server": "lumen_vlm.proto.ml_service_pb2_grpc.add_InferenceServicer_to_server"},
+                                "backend_settings": {"device": "cuda"},
+                                "models": {"general": {"model": "fastvlm-tiny", "runtime": "onnx"}}}}}
+    s = GeneralFastVLMService.from_config(config_from_dict(cfg).services["vlm"], cache)
+    s.initialize()
+    try:
+        img = encode_jpeg(np.random.default_rng(0).integers(0, 255, (40, 60, 3), dtype=np.uint8))
+        outs = []
+        for prompt in ("Describe.", "What is this?"):
+            body, _, _ = s.handle("vlm_generate", img, "image/jpeg", {"prompt": prompt, "max_new_tokens": "12"})
+            outs.append(_json.loads(body)["text"])
+        eng = s.backend.engine
+        q.put({"texts": outs, "tp": s.backend.tp.world, "graphs": eng.graphs is not None and len(eng.graphs.graphs) > 0,
+               "sync": dict(eng.sync.stats) if eng.sync is not None else None})
+    except BaseException as e:  # noqa: BLE001
+        q.put({"error": repr(e)})
+    finally:
+        s.close()
+
+
+def test_vlm_tp2_graphs_match_tp1(tmp_path):
+    from lumen_amd.models.vlm import write_vlm_model
+
+    write_vlm_model(tmp_path / "models" / "fastvlm-tiny", "fastvlm-tiny")
+    ctx = mp.get_context("spawn")
+    res = {}
+    for tp in (1, 2):
+        q = ctx.Queue()
+        p = ctx.Process(target=_leader, args=(str(tmp_path), tp, q))
+        p.start()
+        res[tp] = q.get(timeout=110)
+        p.join(30)
+        assert "error" not in res[tp], res[tp]
+        assert p.exitcode == 0
+    assert res[2]["tp"] == 2 and res[1]["tp"] == 1
+    assert res[1]["graphs"] and res[2]["graphs"]                     # decode replayed from hipGraphs on both
+    assert res[2]["sync"]["tensor_steps"] >= 10
+    assert res[2]["texts"] == res[1]["texts"]
