@@ -206,6 +206,65 @@ int lumen_db_boxes(const float* prob, int H, int W, float thresh, float box_thre
   return out;
 }
 
+// ---- split form for the GPU labelling path (csrc/db_post.hip) ----------------------------
+// pts: int32 [K, 3] boundary pixels (component root, x, y) grouped by root in ascending
+// root order (== the raster order of the components' first pixels, as above).  For the
+// first max_candidates components: hull -> min-area rect; rects below min_size dropped.
+// Writes quads [n, 8] (the rect's corners, for the GPU box score), rects [n, 5]
+// (cx, cy, w, h, angle) and the component root; returns n.
+int lumen_db_candidates(const int* pts, int K, int max_candidates, int min_size, float* quads, float* rects,
+                        int* roots, int max_out) {
+  int out = 0, comps = 0;
+  for (int i = 0; i < K && out < max_out;) {
+    int j = i;
+    while (j < K && pts[3 * j] == pts[3 * i]) ++j;
+    if (comps++ >= max_candidates) break;
+    if (j - i >= 3) {
+      std::vector<P> v;
+      v.reserve(j - i);
+      for (int t = i; t < j; ++t) v.push_back(P{(double)pts[3 * t + 1], (double)pts[3 * t + 2]});
+      const Rect r = min_area_rect(hull(v));
+      if (std::min(r.w, r.h) >= min_size) {
+        P q[4];
+        rect_corners(r, q);
+        for (int k = 0; k < 4; ++k) { quads[out * 8 + 2 * k] = (float)q[k].x; quads[out * 8 + 2 * k + 1] = (float)q[k].y; }
+        const double rv[5] = {r.cx, r.cy, r.w, r.h, r.ang};
+        for (int k = 0; k < 5; ++k) rects[out * 5 + k] = (float)rv[k];
+        roots[out] = pts[3 * i];
+        ++out;
+      }
+    }
+    i = j;
+  }
+  return out;
+}
+
+// score filter, unclip, size filter, TL-clockwise order, rescale + clip (lumen_db_boxes steps 3b-5)
+int lumen_db_finalize(const float* rects, const float* scores, int m, float box_thresh, float unclip_ratio,
+                      int min_size, float scale_x, float scale_y, int src_w, int src_h, float* boxes,
+                      float* out_scores, int max_boxes) {
+  int out = 0;
+  for (int i = 0; i < m && out < max_boxes; ++i) {
+    if (scores[i] < box_thresh) continue;
+    Rect r{rects[i * 5], rects[i * 5 + 1], rects[i * 5 + 2], rects[i * 5 + 3], rects[i * 5 + 4]};
+    const double area = r.w * r.h, perim = 2 * (r.w + r.h);
+    const double d = perim > 0 ? area * unclip_ratio / perim : 0;
+    r.w += 2 * d;
+    r.h += 2 * d;
+    if (std::min(r.w, r.h) < min_size + 2) continue;
+    P q[4];
+    rect_corners(r, q);
+    order_box(q);
+    for (int k = 0; k < 4; ++k) {
+      boxes[out * 8 + 2 * k] = (float)std::min(std::max(std::round(q[k].x * scale_x), 0.0), (double)src_w);
+      boxes[out * 8 + 2 * k + 1] = (float)std::min(std::max(std::round(q[k].y * scale_y), 0.0), (double)src_h);
+    }
+    out_scores[out] = scores[i];
+    ++out;
+  }
+  return out;
+}
+
 // Umeyama similarity transform (no reflection) mapping src[n,2] -> dst[n,2];
 // writes the 2x3 forward matrix M (row major).  Used for 5-point face alignment
 // (reference: cv2.estimateAffinePartial2D, face onnxrt_backend.py:1382-1417).

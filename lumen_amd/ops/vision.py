@@ -274,6 +274,76 @@ def ctc_greedy(probs: torch.Tensor, blank: int = 0, from_logits: bool = False,
     return seqs, confs
 
 
+# --------------------------------------------------------------------------- DB post-processing (GPU + host)
+def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw: int, max_candidates: int = 1000,
+                 min_size: int = 3, max_boxes: int = 1000, cap: Optional[int] = None) -> list:
+    """Batched DB post-processing of a device probability batch [n, rh, rw]: GPU threshold +
+    connected components + boundary extraction (db_post.hip), host hull / min-area rect on
+    the boundary pixels, GPU box score, host unclip / order / rescale.  ``params[j]`` has
+    ``det_thresh`` / ``box_thresh`` / ``unclip_ratio``; ``hw[j]`` is the source (h, w).
+    Returns per image (boxes [k, 4, 2] int32, scores [k]) -- the same boxes as :func:`db_boxes`."""
+    lib = load_host()
+    if lib is None:
+        raise RuntimeError("lumen host library (_lumen_host.so) not built")
+    n = prob.shape[0]
+    prob = prob.contiguous()
+    if prob.dtype not in (torch.bfloat16, torch.float32):
+        prob = prob.float()
+    dev = prob.device
+    thr = torch.tensor([float(p.det_thresh) for p in params], dtype=torch.float32, device=dev)
+    cap = cap or max(1 << 16, n * rh * rw // 4)
+    lab = torch.empty(n * rh * rw, dtype=torch.int32, device=dev)
+    pts = torch.empty((cap, 3), dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    hip_ops().db_components(prob, thr, lab, pts, cnt)
+    K = int(cnt.item())
+    if K > cap:                                      # pathological maps: retry with room for every pixel
+        return db_boxes_gpu(prob, params, hw, rh, rw, max_candidates, min_size, max_boxes, cap=n * rh * rw)
+    P = pts[:K].cpu().numpy()
+    P = P[np.argsort(P[:, 0], kind="stable")]
+    HW = rh * rw
+    ip = ctypes.POINTER(ctypes.c_int)
+    fp = ctypes.POINTER(ctypes.c_float)
+    per_img = []
+    all_q, all_r, all_i = [], [], []
+    starts = np.searchsorted(P[:, 0], np.arange(n + 1) * HW) if K else np.zeros(n + 1, np.int64)
+    for j in range(n):
+        seg = np.ascontiguousarray(P[starts[j]:starts[j + 1]])
+        mx = max_candidates
+        q = np.zeros((mx, 8), np.float32)
+        r = np.zeros((mx, 5), np.float32)
+        roots = np.zeros((mx,), np.int32)
+        m = lib.lumen_db_candidates(seg.ctypes.data_as(ip), ctypes.c_int(len(seg)), ctypes.c_int(max_candidates),
+                                    ctypes.c_int(min_size), q.ctypes.data_as(fp), r.ctypes.data_as(fp),
+                                    roots.ctypes.data_as(ip), ctypes.c_int(mx)) if len(seg) else 0
+        all_q.append(q[:m])
+        all_r.append(r[:m])
+        all_i.append(np.full(m, j, np.int32))
+        per_img.append(m)
+    Q = np.concatenate(all_q) if all_q else np.zeros((0, 8), np.float32)
+    scores = np.zeros((len(Q),), np.float32)
+    if len(Q):
+        sc = torch.empty(len(Q), dtype=torch.float32, device=dev)
+        hip_ops().db_quad_score(prob, torch.from_numpy(Q).to(dev), torch.from_numpy(np.concatenate(all_i)).to(dev), sc)
+        scores = sc.cpu().numpy()
+    out, o = [], 0
+    for j in range(n):
+        m = per_img[j]
+        h, w = hw[j]
+        boxes = np.zeros((max_boxes, 8), np.float32)
+        bs = np.zeros((max_boxes,), np.float32)
+        R = np.ascontiguousarray(all_r[j])
+        S = np.ascontiguousarray(scores[o:o + m])
+        k = lib.lumen_db_finalize(R.ctypes.data_as(fp), S.ctypes.data_as(fp), ctypes.c_int(m),
+                                  ctypes.c_float(params[j].box_thresh), ctypes.c_float(params[j].unclip_ratio),
+                                  ctypes.c_int(min_size), ctypes.c_float(w / rw), ctypes.c_float(h / rh),
+                                  ctypes.c_int(w), ctypes.c_int(h), boxes.ctypes.data_as(fp), bs.ctypes.data_as(fp),
+                                  ctypes.c_int(max_boxes)) if m else 0
+        out.append((boxes[:k].reshape(k, 4, 2).astype(np.int32), bs[:k]))
+        o += m
+    return out
+
+
 # --------------------------------------------------------------------------- DB post-processing (host C++)
 def db_boxes(prob: np.ndarray, thresh: float = 0.3, box_thresh: float = 0.6, unclip_ratio: float = 1.5,
              max_candidates: int = 1000, min_size: int = 3, scale_xy=(1.0, 1.0), src_wh=(0, 0),

@@ -28,6 +28,7 @@ softmax is fused into the CTC arg-max kernel.
 from __future__ import annotations
 
 import json
+import os
 import logging
 import math
 import time
@@ -271,7 +272,11 @@ class MI355XOcrBackend:
         return out
 
     def _db_post(self, prob: torch.Tensor, hw, params, rh: int, rw: int) -> list:
-        """DB post-processing of a [n, rh, rw] probability batch -> boxes in reading order."""
+        """DB post-processing of a [n, rh, rw] probability batch -> boxes in reading order.
+        On the GPU: threshold + connected components + boundary extraction + box scores run on
+        the device (ops.vision.db_boxes_gpu), only boundary pixels and scores come back."""
+        if prob.is_cuda and os.environ.get("LUMEN_OCR_GPU_DB", "1") != "0":
+            return [sorted_boxes(list(b)) for b, _ in vision.db_boxes_gpu(prob, params, hw, rh, rw)]
         pm = prob.float().cpu().numpy()
         res = []
         for j, ((h, w), p) in enumerate(zip(hw, params)):

@@ -87,3 +87,31 @@ def test_ctc_greedy():
     ids, cf = vision.ctc_greedy(logits.to(DEV), from_logits=True, tlen=tl)
     assert ids == ids_r
     np.testing.assert_allclose(cf, cf_r, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_db_boxes_gpu_matches_host(dtype):
+    """GPU threshold + connected components + boundary + box score (db_post.hip) give the same
+    boxes as the host path on a batch of maps with per-image thresholds."""
+    from tests.test_db_post_cpu import _blob_map
+    from lumen_amd.ops import vision as _v
+
+    maps = [_blob_map(s, 96, 160) for s in range(4)]
+    maps[3][:] = 0.0                                          # an empty map in the batch
+    P = type("P", (), {})
+    params = []
+    for j in range(4):
+        p = P()
+        p.det_thresh, p.box_thresh, p.unclip_ratio = 0.3 + 0.05 * j, 0.5, 1.5
+        params.append(p)
+    hw = [(192, 320)] * 4
+    prob = torch.from_numpy(np.stack(maps)).to(dtype)
+    got = _v.db_boxes_gpu(prob.to("cuda"), params, hw, 96, 160)
+    for j in range(4):
+        ref_b, ref_s = _v.db_boxes(prob[j].float().numpy(), thresh=params[j].det_thresh, box_thresh=0.5,
+                                   unclip_ratio=1.5, scale_xy=(2.0, 2.0), src_wh=(320, 192))
+        b, s = got[j]
+        assert len(b) == len(ref_b)
+        np.testing.assert_array_equal(b, ref_b)
+        np.testing.assert_allclose(s, ref_s, rtol=1e-4)
+    assert len(got[3][0]) == 0 and len(got[0][0]) > 0

@@ -1,7 +1,10 @@
 """Kernel statistics from a rocprofv3 SQLite (rocpd) database, as the CSV the older
 ``--stats`` output used: Name, Calls, TotalDurationNs, AverageNs, Percentage.
 
-  python tools/rocpd_stats.py gpurun_out/prof_bench/run_results.db [out.csv] [--top N]
+  python tools/rocpd_stats.py gpurun_out/prof_bench/run_results.db [out.csv] [--top N] [--ar-share]
+
+``--ar-share`` also prints the all-reduce share of GPU kernel time (IPC one-shot ``custom_ar``
+kernels + RCCL collectives) — BASELINE row 5's "all-reduce share of decode step time".
 """
 import csv
 import sqlite3
@@ -27,6 +30,16 @@ def main():
                 w.writerow([r[0], r[1], r[2], round(r[3], 1), round(r[4], 3)])
     for n, k, t, a, p in rows[:top]:
         print(f"{p:6.2f}%  {k:6d}  {a / 1e3:9.2f} us  {n[:110]}")
+    if "--ar-share" in sys.argv:
+        keys = ("custom_ar", "allreduce", "AllReduce", "ncclDevKernel", "rccl")
+        ar = [r for r in rows if any(k in r[0] for k in keys)]
+        tot = sum(r[2] for r in rows) or 1
+        import json
+
+        print(json.dumps({"all_reduce_share_of_kernel_time": sum(r[2] for r in ar) / tot,
+                          "all_reduce_calls": sum(r[1] for r in ar),
+                          "all_reduce_avg_us": (sum(r[2] for r in ar) / max(sum(r[1] for r in ar), 1)) / 1e3,
+                          "kernels": [r[0][:80] for r in ar]}))
 
 
 if __name__ == "__main__":
