@@ -14,6 +14,8 @@
 //
 // Replaces the Conv / BatchNormalization / Relu / PRelu / Add ONNX nodes of the
 // reference's detection.*.onnx / recognition.*.onnx graphs.
+#include <cstdlib>
+
 #include "conv.h"
 #include "gemm_epi.h"
 
@@ -193,8 +195,20 @@ static hipError_t launch_conv(const ConvArgs& a, const GemmEpi& ep, hipStream_t 
   return hipGetLastError();
 }
 
+bool conv_lds_ok(const ConvArgs& a);
+hipError_t conv2d_lds(const ConvArgs& a, const GemmEpi& ep, int variant, hipStream_t stream);
+
+// tile: -1 auto, 0..2 register-staged configs, 10 + v the LDS-DMA pipeline (conv_lds.hip, v = variant)
 hipError_t conv2d_igemm(const ConvArgs& a, const GemmEpi& ep, int tile, hipStream_t stream) {
   const int64_t M = (int64_t)a.N * a.Ho * a.Wo;
+  if (tile >= 10) return conv2d_lds(a, ep, tile - 10, stream);
+  // Cin % 64 == 0 layers (IResNet, SCRFD / DBNet trunks): the LDS-DMA pipeline
+  // (profiles/r2_conv_lds_v1.txt); LUMEN_CONV_LDS=0 keeps the register-staged kernels
+  static const bool lds_on = [] {
+    const char* e = getenv("LUMEN_CONV_LDS");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (tile < 0 && lds_on && conv_lds_ok(a)) return conv2d_lds(a, ep, 0, stream);
   if (tile < 0) {
     const int64_t t128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
     if (a.Cout >= 128 && t128 >= 256) tile = 0;

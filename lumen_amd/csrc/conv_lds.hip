@@ -1,0 +1,199 @@
+// Implicit-GEMM convolution on the 128 x BN LDS-DMA pipeline of gemm_f8.hip (bf16 form):
+// NSTAGE K-stages of global_load_lds (16 B per lane, XOR swizzle on the source address),
+// one counted vmcnt + raw barrier per K-step, 2 x WN waves with 64 x (BN/WN) wave tiles of
+// v_mfma_f32_16x16x32_bf16.  For Cin % 64 == 0 one 64-wide K-step is 64 channels of ONE
+// filter tap, so every LDS row of the A stage is a single contiguous 128-byte run of an
+// NHWC input pixel -- the gather is pure address arithmetic on the DMA source (taps that
+// fall into the zero padding read a zeroed 128-byte page).  Replaces the register-staged
+// 2-stage conv_igemm_kernel on the IResNet / SCRFD / DBNet layers with Cin >= 64
+// (r1: 55 us per call, 1.3 % of peak on face).
+//
+// GEMM view (conv.hip): M = N*Ho*Wo, N = Cout, K = KH*KW*Cin, A[m][k] = x[n, ho*sh-ph+ky*dh,
+// wo*sw-pw+kx*dw, ci], B = w [Cout, KH, KW, Cin]; C = NHWC output (pixel stride ldo) through
+// the shared GemmEpi epilogue (folded-BN bias, activation, PReLU, residual, post-ReLU).
+#include <cstdlib>
+
+#include "common.h"
+#include "conv.h"
+#include "gemm_epi.h"
+
+namespace lumen {
+
+__device__ __attribute__((aligned(256))) uint16_t g_conv_zero_page[128];   // 256 zero bytes
+
+template <int NSTAGE, int WN, int BN>
+__global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi ep) {
+  constexpr int NW = 2 * WN;
+  constexpr int TN = BN / WN;
+  constexpr int NR = TN / 16;
+  constexpr int PERA = 16 / NW;             // A: 128 rows = 16 x 8-row DMA units
+  constexpr int PERB = BN / 8 / NW;          // B: BN rows
+  static_assert(PERA >= 1 && PERB >= 1 && NR >= 1, "tiling");
+  constexpr int ASZ = 128 * 128, STAGE = ASZ + BN * 128;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int M = a.N * a.Ho * a.Wo, N = a.Cout, K = a.KH * a.KW * a.Cin;
+  const int tiles_m = (M + 127) / 128, tiles_n = (N + BN - 1) / BN;
+  const int lin = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = lin % tiles_m, tn = lin / tiles_m;
+  const int m0 = tm * 128, n0 = tn * BN;
+
+  // A rows of this lane: output pixel -> image base + top-left input coordinate
+  const uint16_t* xb[PERA];
+  int hb[PERA], wb[PERA], ca[PERA];
+#pragma unroll
+  for (int i = 0; i < PERA; ++i) {
+    const int r = (PERA * wid + i) * 8 + (lane >> 3);
+    ca[i] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;                 // channel offset of this lane's 16 B
+    const int m = min(m0 + r, M - 1);
+    const int img = m / (a.Ho * a.Wo), rem = m % (a.Ho * a.Wo);
+    xb[i] = a.x + (int64_t)img * a.H * a.W * a.ldx;
+    hb[i] = (rem / a.Wo) * a.sh - a.ph;
+    wb[i] = (rem % a.Wo) * a.sw - a.pw;
+  }
+  const uint16_t* wsrc[PERB];
+#pragma unroll
+  for (int i = 0; i < PERB; ++i) {
+    const int r = (PERB * wid + i) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    wsrc[i] = a.w + (int64_t)min(n0 + r, N - 1) * K + c * 8;
+  }
+  const int cblk = a.Cin / 64;
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  typedef const __attribute__((address_space(1))) void* g_ptr_t;
+  auto stage = [&](int s, int kt) {
+    const int tap = kt / cblk, c0 = (kt - tap * cblk) * 64;
+    const int ky = tap / a.KW, kx = tap - ky * a.KW;
+    char* baseA = smem + s * STAGE + wid * PERA * 1024;
+#pragma unroll
+    for (int i = 0; i < PERA; ++i) {
+      const int ih = hb[i] + ky * a.dh, iw = wb[i] + kx * a.dw;
+      const bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      const uint16_t* src = ok ? xb[i] + ((int64_t)ih * a.W + iw) * a.ldx + c0 + ca[i] : g_conv_zero_page;
+      __builtin_amdgcn_global_load_lds((g_ptr_t)src, (lds_ptr_t)(baseA + i * 1024), 16, 0, 0);
+    }
+    char* baseB = smem + s * STAGE + ASZ + wid * PERB * 1024;
+    const int64_t koff = (int64_t)kt * 64;
+#pragma unroll
+    for (int i = 0; i < PERB; ++i)
+      __builtin_amdgcn_global_load_lds((g_ptr_t)(wsrc[i] + koff), (lds_ptr_t)(baseB + i * 1024), 16, 0, 0);
+  };
+
+  f32x4_t acc[4][NR];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / 64;
+  const int frow = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < nk) stage(s, s);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + NSTAGE - 2 < nk) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((PERA + PERB) * (NSTAGE - 2)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kt + NSTAGE - 1 < nk) stage((kt + NSTAGE - 1) % NSTAGE, kt + NSTAGE - 1);
+    const char* sA = smem + (kt % NSTAGE) * STAGE;
+    const char* sW = sA + ASZ;
+    u32x4_t fa[4][2], fb[NR][2];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int r = wn * TN + j * 16 + frow;
+      fb[j][0] = *(const u32x4_t*)(sW + swz(r, g));
+      fb[j][1] = *(const u32x4_t*)(sW + swz(r, g + 4));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wm * 64 + i * 16 + frow;
+      fa[i][0] = *(const u32x4_t*)(sA + swz(r, g));
+      fa[i][1] = *(const u32x4_t*)(sA + swz(r, g + 4));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[i][0]),
+                                                            __builtin_bit_cast(bf16x8_t, fb[j][0]), acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[i][1]),
+                                                            __builtin_bit_cast(bf16x8_t, fb[j][1]), acc[i][j], 0, 0, 0);
+      }
+  }
+  __syncthreads();
+
+  constexpr int LDSTR = TN + 4;
+  constexpr int LPR = TN / 16;
+  constexpr int RPP = 64 / LPR;
+  constexpr int NPASS = RPP >= 16 ? 1 : 16 / RPP;
+  float* es = (float*)smem + wid * 16 * LDSTR;
+  const int cc = (lane % LPR) * 16;
+  const int n = n0 + wn * TN + cc;
+  const __amdgpu_buffer_rsrc_t crs = c_rsrc(a.out);
+  Unroll<0, 4>::run([&](const int i) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) es[(g * 4 + r) * LDSTR + j * 16 + frow] = acc[i][j][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const int rr = p * RPP + lane / LPR;
+      if (rr >= 16) continue;
+      const int m = m0 + wm * 64 + i * 16 + rr;
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cc + q * 4);
+        v[q * 4 + 0] = t[0]; v[q * 4 + 1] = t[1]; v[q * 4 + 2] = t[2]; v[q * 4 + 3] = t[3];
+      }
+      epi_store16_t<false>(v, m, n, M, N, a.out, a.ldo, ep, crs);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  });
+}
+
+template <int NS, int WN, int BN>
+static hipError_t launch_conv_lds(const ConvArgs& a, const GemmEpi& ep, hipStream_t stream) {
+  const size_t lds = (size_t)NS * (128 + BN) * 128;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_lds_kernel<NS, WN, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)lds);
+    attr = true;
+  }
+  const int M = a.N * a.Ho * a.Wo;
+  const int tiles = ((M + 127) / 128) * ((a.Cout + BN - 1) / BN);
+  hipLaunchKernelGGL((conv_lds_kernel<NS, WN, BN>), dim3(tiles), dim3(128 * WN), lds, stream, a, ep);
+  return hipGetLastError();
+}
+
+bool conv_lds_ok(const ConvArgs& a) {
+  return a.Cin % 64 == 0 && a.Cout % 16 == 0 && a.ldx % 8 == 0 && a.ldo % 8 == 0 &&
+         ((uintptr_t)a.x & 15) == 0 && ((uintptr_t)a.w & 15) == 0 && (int64_t)a.N * a.Ho * a.Wo < (1LL << 31);
+}
+
+// variant: 0 auto; 1 = 128x128 3 stages 8 waves, 2 = 128x128 2 stages 4 waves, 3 = 128x64 3 stages 4 waves,
+// 4 = 128x64 2 stages 4 waves (two workgroups per CU)
+hipError_t conv2d_lds(const ConvArgs& a, const GemmEpi& ep, int variant, hipStream_t stream) {
+  if (!conv_lds_ok(a)) return hipErrorInvalidValue;
+  if (variant == 0) {
+    const int64_t M = (int64_t)a.N * a.Ho * a.Wo;
+    const int64_t t128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
+    if (a.Cout >= 128) variant = t128 > 256 ? 2 : 1;
+    else variant = 4;
+  }
+  switch (variant) {
+    case 1: return launch_conv_lds<3, 4, 128>(a, ep, stream);
+    case 2: return launch_conv_lds<2, 2, 128>(a, ep, stream);
+    case 3: return launch_conv_lds<3, 2, 64>(a, ep, stream);
+    default: return launch_conv_lds<2, 2, 64>(a, ep, stream);
+  }
+}
+
+}  // namespace lumen

@@ -12,8 +12,10 @@
 //                 index -- the raster-order first pixel, i.e. the same component order
 //                 as the host two-pass labelling (max_candidates cuts identically)
 //   db_flatten    lab[p] = root(p)
+//   db_bbox       pixel-centre bounding box per component (boundary pixels, atomics)
 //   db_boundary   (root, x, y) of every pixel with a 4-neighbour outside its component
-//                 (or on the map border), appended with one atomic per wave
+//                 (or on the map border) of components that can pass min_size, appended
+//                 with one atomic per wave
 //   db_quad_score mean probability inside each candidate rectangle (one workgroup each)
 //
 // Only the boundary list (a few % of the pixels) and the per-box scores cross PCIe; the
@@ -44,12 +46,16 @@ __global__ void db_label_kernel(const T* __restrict__ prob, const float* __restr
 __device__ __forceinline__ int db_ld(const int* lab, int i) {
   return __hip_atomic_load(lab + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ int db_find(const int* lab, int i) {
+__device__ __forceinline__ int db_find(int* lab, int i) {
+  const int start = i;
   int p = db_ld(lab, i);
   while (p != i) {
     i = p;
     p = db_ld(lab, i);
   }
+  // path compression: the start pixel points straight at its (current) root.  atomicMin keeps
+  // the invariant lab[x] <= x monotone under concurrent relinks (a root only ever decreases).
+  if (i != start) atomicMin(lab + start, i);
   return i;
 }
 
@@ -70,18 +76,25 @@ __device__ __forceinline__ void db_union(int* lab, int a, int b) {
   }
 }
 
+// Each foreground pixel merges with its earlier 8-neighbours, skipping the ones another
+// merge already connects: with N foreground, NW and NE are N's own W / E neighbours (linked
+// by N's merges); with W foreground, NW is W's N neighbour.  Halves the atomics on text
+// blobs (and on the fully-foreground maps of untrained weights).
 __global__ void db_merge_kernel(int* __restrict__ lab, int H, int W, int64_t total) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total || lab[i] < 0) return;
   const int HW = H * W;
   const int p = (int)(i % HW), x = p % W, y = p / W;
-  const int dx[4] = {-1, -1, 0, 1}, dy[4] = {0, -1, -1, -1};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int xx = x + dx[k], yy = y + dy[k];
-    if (xx < 0 || yy < 0 || xx >= W) continue;
-    const int64_t j = i + (int64_t)dy[k] * W + dx[k];
-    if (lab[j] >= 0) db_union(lab, (int)i, (int)j);
+  const bool w = x > 0 && lab[i - 1] >= 0;
+  const bool n = y > 0 && lab[i - W] >= 0;
+  const bool nw = x > 0 && y > 0 && lab[i - W - 1] >= 0;
+  const bool ne = x < W - 1 && y > 0 && lab[i - W + 1] >= 0;
+  if (w) db_union(lab, (int)i, (int)(i - 1));
+  if (n) {
+    db_union(lab, (int)i, (int)(i - W));
+  } else {
+    if (nw && !w) db_union(lab, (int)i, (int)(i - W - 1));
+    if (ne) db_union(lab, (int)i, (int)(i - W + 1));
   }
 }
 
@@ -91,23 +104,83 @@ __global__ void db_flatten_kernel(int* __restrict__ lab, int64_t total) {
   lab[i] = db_find(lab, (int)i);
 }
 
-__global__ void db_boundary_kernel(const int* __restrict__ lab, int H, int W, int64_t total, int* __restrict__ out,
-                                   int* __restrict__ count, int cap) {
+__device__ __forceinline__ bool db_is_boundary(const int* lab, int64_t i, int x, int y, int H, int W) {
+  return x == 0 || y == 0 || x == W - 1 || y == H - 1 || lab[i - 1] < 0 || lab[i + 1] < 0 || lab[i - W] < 0 ||
+         lab[i + W] < 0;
+}
+
+// pass 1: pixel-centre bounding box of every component from its boundary pixels
+// (bb[4 * root] = xmin, xmax, ymin, ymax; initialised to (W, -1, H, -1) by db_bbox_init)
+__global__ void db_bbox_init_kernel(int* __restrict__ bb, int H, int W, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  bb[4 * i] = W; bb[4 * i + 1] = -1; bb[4 * i + 2] = H; bb[4 * i + 3] = -1;
+}
+
+// 1024-thread workgroups: lanes in the component of the workgroup's first pixel (an untrained
+// map's giant blob: millions of boundary pixels, ONE root) reduce through LDS atomics first and
+// the workgroup issues 4 global atomics; other pixels go through runs of consecutive lanes
+// (head: xmin / ymin / ymax, tail: xmax).
+__global__ void __launch_bounds__(1024) db_bbox_kernel(const int* __restrict__ lab, int* __restrict__ bb, int H, int W,
+                                                       int64_t total) {
+  __shared__ int sb[4];
+  const int64_t base = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t i = min(base + threadIdx.x, total - 1);   // whole waves stay active
+  const int L = lab[base];                                 // the workgroup's first pixel's component
+  if (threadIdx.x == 0) { sb[0] = W; sb[1] = -1; sb[2] = H; sb[3] = -1; }
+  __syncthreads();
+  const int l = lab[i];
+  const int p = (int)(i % ((int64_t)H * W)), x = p % W, y = p / W;
+  const bool act = l >= 0 && db_is_boundary(lab, i, x, y, H, W);
+  const bool dom = act && l == L;
+  if (dom) {
+    atomicMin(sb, x); atomicMax(sb + 1, x);
+    atomicMin(sb + 2, y); atomicMax(sb + 3, y);
+  }
+  const int lane = threadIdx.x & 63;
+  const bool oth = act && !dom;
+  const int lp = __shfl_up(l, 1, 64), ap = __shfl_up((int)oth, 1, 64), yp = __shfl_up(y, 1, 64);
+  const int ln = __shfl_down(l, 1, 64), an = __shfl_down((int)oth, 1, 64), yn = __shfl_down(y, 1, 64);
+  if (oth) {
+    int* b = bb + 4 * (int64_t)l;
+    if (!(lane > 0 && ap && lp == l && yp == y)) {
+      atomicMin(b, x);
+      atomicMin(b + 2, y);
+      atomicMax(b + 3, y);
+    }
+    if (!(lane < 63 && an && ln == l && yn == y)) atomicMax(b + 1, x);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && L >= 0 && sb[1] >= 0) {
+    int* b = bb + 4 * (int64_t)L;
+    atomicMin(b, sb[0]); atomicMax(b + 1, sb[1]);
+    atomicMin(b + 2, sb[2]); atomicMax(b + 3, sb[3]);
+  }
+}
+
+// pass 2: (root, x, y) of the boundary pixels of components that can still make a box: a
+// component whose pixel-centre bbox is below min_size on BOTH sides has a min-area rect of area
+// < min_size^2, hence a short side < min_size, and the host would drop it -- on untrained or
+// noisy maps those are millions of pixels of 1-10 pixel specks that need not cross PCIe.
+// One atomic per wave: ballot the emitting lanes, the first reserves, each lane takes its rank.
+__global__ void db_boundary_kernel(const int* __restrict__ lab, const int* __restrict__ bb, int H, int W,
+                                   int64_t total, int min_size, int* __restrict__ out, int* __restrict__ count,
+                                   int cap) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool emit = false;
   int x = 0, y = 0, l = -1;
   if (i < total) {
     l = lab[i];
     if (l >= 0) {
-      const int HW = H * W;
-      const int p = (int)(i % HW);
+      const int p = (int)(i % ((int64_t)H * W));
       x = p % W;
       y = p / W;
-      emit = x == 0 || y == 0 || x == W - 1 || y == H - 1 || lab[i - 1] < 0 || lab[i + 1] < 0 || lab[i - W] < 0 ||
-             lab[i + W] < 0;
+      if (db_is_boundary(lab, i, x, y, H, W)) {
+        const int* b = bb + 4 * (int64_t)l;
+        emit = (b[1] - b[0]) >= min_size || (b[3] - b[2]) >= min_size;
+      }
     }
   }
-  // one atomic per wave: ballot the emitting lanes, lane 0 reserves, each lane takes its rank
   const uint64_t m = __ballot(emit);
   if (m == 0) return;
   const int lane = threadIdx.x & 63;
@@ -124,12 +197,13 @@ __global__ void db_boundary_kernel(const int* __restrict__ lab, int H, int W, in
   }
 }
 
-// quads [m, 8] (x0,y0 .. x3,y3 in map pixels), img[m] -> score[m] = mean prob of the pixel
-// centres inside the quad (host in_quad test, box_score_fast)
+// quads [m, 8] (x0,y0 .. x3,y3 in map pixels), img[m]: acc[q] += (sum of prob, count) of the
+// pixel centres inside the quad (host in_quad test, box_score_fast).  gridDim.y workgroups
+// share one quad's bounding box (a full-map blob is ~1M pixels), partials added atomically.
 template <typename T>
 __global__ void __launch_bounds__(256) db_quad_score_kernel(const T* __restrict__ prob, int H, int W,
                                                             const float* __restrict__ quads,
-                                                            const int* __restrict__ img, float* __restrict__ score) {
+                                                            const int* __restrict__ img, float* __restrict__ acc) {
   __shared__ float rs[4], rc[4];
   const int q = blockIdx.x;
   float px[4], py[4];
@@ -150,13 +224,14 @@ __global__ void __launch_bounds__(256) db_quad_score_kernel(const T* __restrict_
   const T* pm = prob + (int64_t)img[q] * H * W;
   float s = 0.f, c = 0.f;
   if (bw > 0 && bh > 0) {
-    for (int t = threadIdx.x; t < bw * bh; t += blockDim.x) {
+    const int npix = bw * bh;
+    const int step = blockDim.x * gridDim.y;
+    for (int t = blockIdx.y * blockDim.x + threadIdx.x; t < npix; t += step) {
       const float xx = (float)(x0 + t % bw), yy = (float)(y0 + t / bw);
       bool pos = false, neg = false;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int k1 = (k + 1) & 3;
-        // same orientation test as the host path (double there; the corners are pixel-scale floats)
         const float cr = (px[k1] - px[k]) * (yy - py[k]) - (py[k1] - py[k]) * (xx - px[k]);
         pos |= cr > 0.f;
         neg |= cr < 0.f;
@@ -173,15 +248,21 @@ __global__ void __launch_bounds__(256) db_quad_score_kernel(const T* __restrict_
   if ((threadIdx.x & 63) == 0) { rs[wid] = s; rc[wid] = c; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float S = rs[0] + rs[1] + rs[2] + rs[3], C = rc[0] + rc[1] + rc[2] + rc[3];
-    score[q] = C > 0.f ? S / C : 0.f;
+    atomicAdd(acc + 2 * q, rs[0] + rs[1] + rs[2] + rs[3]);
+    atomicAdd(acc + 2 * q + 1, rc[0] + rc[1] + rc[2] + rc[3]);
   }
+}
+
+__global__ void db_score_div_kernel(const float* __restrict__ acc, float* __restrict__ score, int m) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < m) score[q] = acc[2 * q + 1] > 0.f ? acc[2 * q] / acc[2 * q + 1] : 0.f;
 }
 
 // prob: [n, H, W] (bf16 if is_bf16 else f32); thresh [n] f32; lab: int32 workspace [n*H*W];
 // out: int32 [cap, 3]; count: int32 [1] (zeroed here).
+// lab: int32 workspace [5 * n*H*W] (labels + per-root bounding boxes)
 hipError_t db_components(const void* prob, int is_bf16, const float* thresh, int n, int H, int W, int* lab,
-                         int* out, int* count, int cap, hipStream_t stream) {
+                         int* out, int* count, int cap, int min_size, hipStream_t stream) {
   const int64_t total = (int64_t)n * H * W;
   if (total <= 0 || total >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
   const int blocks = (int)((total + 255) / 256);
@@ -194,19 +275,28 @@ hipError_t db_components(const void* prob, int is_bf16, const float* thresh, int
                        H * W, total);
   hipLaunchKernelGGL(db_merge_kernel, dim3(blocks), dim3(256), 0, stream, lab, H, W, total);
   hipLaunchKernelGGL(db_flatten_kernel, dim3(blocks), dim3(256), 0, stream, lab, total);
-  hipLaunchKernelGGL(db_boundary_kernel, dim3(blocks), dim3(256), 0, stream, lab, H, W, total, out, count, cap);
+  int* bb = lab + total;
+  hipLaunchKernelGGL(db_bbox_init_kernel, dim3(blocks), dim3(256), 0, stream, bb, H, W, total);
+  hipLaunchKernelGGL(db_bbox_kernel, dim3((int)((total + 1023) / 1024)), dim3(1024), 0, stream, lab, bb, H, W, total);
+  hipLaunchKernelGGL(db_boundary_kernel, dim3(blocks), dim3(256), 0, stream, lab, bb, H, W, total, min_size, out,
+                     count, cap);
   return hipGetLastError();
 }
 
+// score: f32 [3 * m] -- [0, m) the scores, [m, 3m) the (sum, count) accumulators
 hipError_t db_quad_score(const void* prob, int is_bf16, int H, int W, const float* quads, const int* img, float* score,
                          int m, hipStream_t stream) {
   if (m <= 0) return hipSuccess;
+  float* acc = score + m;
+  (void)hipMemsetAsync(acc, 0, sizeof(float) * 2 * m, stream);
+  const int split = 8;           // 8 workgroups per quad: big blobs spread, small ones finish at once
   if (is_bf16)
-    hipLaunchKernelGGL(db_quad_score_kernel<uint16_t>, dim3(m), dim3(256), 0, stream, (const uint16_t*)prob, H, W,
-                       quads, img, score);
+    hipLaunchKernelGGL(db_quad_score_kernel<uint16_t>, dim3(m, split), dim3(256), 0, stream, (const uint16_t*)prob, H,
+                       W, quads, img, acc);
   else
-    hipLaunchKernelGGL(db_quad_score_kernel<float>, dim3(m), dim3(256), 0, stream, (const float*)prob, H, W, quads,
-                       img, score);
+    hipLaunchKernelGGL(db_quad_score_kernel<float>, dim3(m, split), dim3(256), 0, stream, (const float*)prob, H, W,
+                       quads, img, acc);
+  hipLaunchKernelGGL(db_score_div_kernel, dim3((m + 255) / 256), dim3(256), 0, stream, acc, score, m);
   return hipGetLastError();
 }
 

@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <climits>
 #include <numeric>
 #include <vector>
 
@@ -220,9 +221,23 @@ int lumen_db_candidates(const int* pts, int K, int max_candidates, int min_size,
     while (j < K && pts[3 * j] == pts[3 * i]) ++j;
     if (comps++ >= max_candidates) break;
     if (j - i >= 3) {
+      // the hull of a pixel set is the hull of each row's leftmost / rightmost pixel: reduce a
+      // large component's boundary (an untrained map's blob: ~10^5 pixels) to <= 2 per row in O(n)
+      int ymin = pts[3 * i + 2], ymax = ymin;
+      for (int t = i; t < j; ++t) { ymin = std::min(ymin, pts[3 * t + 2]); ymax = std::max(ymax, pts[3 * t + 2]); }
+      std::vector<int> lo(ymax - ymin + 1, INT32_MAX), hi(ymax - ymin + 1, INT32_MIN);
+      for (int t = i; t < j; ++t) {
+        const int yy = pts[3 * t + 2] - ymin, xx = pts[3 * t + 1];
+        lo[yy] = std::min(lo[yy], xx);
+        hi[yy] = std::max(hi[yy], xx);
+      }
       std::vector<P> v;
-      v.reserve(j - i);
-      for (int t = i; t < j; ++t) v.push_back(P{(double)pts[3 * t + 1], (double)pts[3 * t + 2]});
+      v.reserve(2 * lo.size());
+      for (size_t yy = 0; yy < lo.size(); ++yy) {
+        if (lo[yy] == INT32_MAX) continue;
+        v.push_back(P{(double)lo[yy], (double)(yy + ymin)});
+        if (hi[yy] != lo[yy]) v.push_back(P{(double)hi[yy], (double)(yy + ymin)});
+      }
       const Rect r = min_area_rect(hull(v));
       if (std::min(r.w, r.h) >= min_size) {
         P q[4];

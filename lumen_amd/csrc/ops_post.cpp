@@ -11,7 +11,7 @@
 
 namespace lumen {
 hipError_t db_components(const void* prob, int is_bf16, const float* thresh, int n, int H, int W, int* lab,
-                         int* out, int* count, int cap, hipStream_t stream);
+                         int* out, int* count, int cap, int min_size, hipStream_t stream);
 hipError_t db_quad_score(const void* prob, int is_bf16, int H, int W, const float* quads, const int* img, float* score,
                          int m, hipStream_t stream);
 }  // namespace lumen
@@ -103,21 +103,22 @@ void ctc_greedy(const at::Tensor& probs, int64_t blank, at::Tensor out_ids, at::
 
 // DB post-processing on the GPU (db_post.hip): prob [n, H, W] bf16/f32, thresh f32 [n];
 // lab int32 [n*H*W] workspace; out int32 [cap, 3] (root, x, y); count int32 [1]
-void db_components(const at::Tensor& prob, const at::Tensor& thresh, at::Tensor lab, at::Tensor out, at::Tensor count) {
+void db_components(const at::Tensor& prob, const at::Tensor& thresh, at::Tensor lab, at::Tensor out, at::Tensor count,
+                   int64_t min_size) {
   TORCH_CHECK(prob.is_cuda() && prob.is_contiguous() && prob.dim() == 3 &&
               (prob.scalar_type() == at::kBFloat16 || prob.scalar_type() == at::kFloat), "db_components: prob");
   f32c(thresh, "thresh");
   const int64_t n = prob.size(0), H = prob.size(1), W = prob.size(2);
   TORCH_CHECK(thresh.numel() == n, "db_components: thresh [n]");
-  TORCH_CHECK(lab.is_cuda() && lab.scalar_type() == at::kInt && lab.numel() >= n * H * W && lab.is_contiguous(),
-              "db_components: lab workspace int32 [n*H*W]");
+  TORCH_CHECK(lab.is_cuda() && lab.scalar_type() == at::kInt && lab.numel() >= 5 * n * H * W && lab.is_contiguous(),
+              "db_components: lab workspace int32 [5*n*H*W]");
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kInt && out.dim() == 2 && out.size(1) == 3 &&
               out.is_contiguous(), "db_components: out int32 [cap, 3]");
   TORCH_CHECK(count.is_cuda() && count.scalar_type() == at::kInt && count.numel() >= 1, "db_components: count");
   const at::DeviceGuard g(prob.device());
   CHECK_HIP2(lumen::db_components(prob.data_ptr(), prob.scalar_type() == at::kBFloat16, thresh.data_ptr<float>(),
                                   (int)n, (int)H, (int)W, lab.data_ptr<int>(), out.data_ptr<int>(),
-                                  count.data_ptr<int>(), (int)out.size(0), stream()));
+                                  count.data_ptr<int>(), (int)out.size(0), (int)min_size, stream()));
 }
 
 void db_quad_score(const at::Tensor& prob, const at::Tensor& quads, const at::Tensor& img, at::Tensor score) {
@@ -126,7 +127,8 @@ void db_quad_score(const at::Tensor& prob, const at::Tensor& quads, const at::Te
   f32c(quads, "quads");
   f32c(score, "score");
   const int64_t m = quads.size(0);
-  TORCH_CHECK(quads.dim() == 2 && quads.size(1) == 8 && score.numel() >= m, "db_quad_score: quads [m, 8]");
+  TORCH_CHECK(quads.dim() == 2 && quads.size(1) == 8 && score.numel() >= 3 * m,
+              "db_quad_score: quads [m, 8], score f32 [3m] (scores + accumulators)");
   TORCH_CHECK(img.is_cuda() && img.scalar_type() == at::kInt && img.numel() == m && img.is_contiguous(),
               "db_quad_score: img int32 [m]");
   const at::DeviceGuard g(prob.device());
@@ -138,7 +140,8 @@ void db_quad_score(const at::Tensor& prob, const at::Tensor& quads, const at::Te
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(lumen, m) {
-  m.def("db_components(Tensor prob, Tensor thresh, Tensor(l!) lab, Tensor(o!) out, Tensor(c!) count) -> ()");
+  m.def("db_components(Tensor prob, Tensor thresh, Tensor(l!) lab, Tensor(o!) out, Tensor(c!) count, "
+        "int min_size) -> ()");
   m.def("db_quad_score(Tensor prob, Tensor quads, Tensor img, Tensor(s!) score) -> ()");
   m.def("det_decode(Tensor scores, Tensor bbox, Tensor? kps, Tensor? priors, int H, int W, int A, int stride, "
         "float thresh, Tensor img_scale, Tensor img_hw, float min_size, float max_size, float var0, float var1, "

@@ -477,8 +477,12 @@ def image_prep(
     geoms: Optional[Sequence[ImageGeom]] = None,
     out_dtype: torch.dtype = torch.float32,
     device=None,
+    src: Optional[torch.Tensor] = None,
 ) -> torch.Tensor:
     """Resize/pad/normalise a batch of uint8 HWC RGB images into one tensor.
+
+    ``src``: the images already on the device as one flat uint8 tensor (PinnedUploader);
+    ``geoms`` then carry the offsets into it and ``images`` only provide the shapes.
 
     ``images`` is a list of [H, W, 3] uint8 tensors (ragged sizes allowed) or a
     [B, H, W, 3] uint8 tensor.  Output value = ((px * scale) - mean) / std with the
@@ -512,8 +516,9 @@ def image_prep(
     else:
         out = torch.empty((B, OH, OW, 3), device=device, dtype=out_dtype)
     if torch.device(device).type == "cuda":
-        src = flat_src if flat_src is not None else torch.cat([im.reshape(-1) for im in imgs])
-        src = src.to(device, non_blocking=True)
+        if src is None:
+            src = flat_src if flat_src is not None else torch.cat([im.reshape(-1) for im in imgs])
+            src = src.to(device, non_blocking=True)
         g = torch.tensor([gg.row() for gg in geoms], dtype=torch.long).to(device, non_blocking=True)
         max_ch = max(gg.ch for gg in geoms)
         max_dw = max(gg.dw for gg in geoms)

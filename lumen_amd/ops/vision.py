@@ -178,7 +178,7 @@ def invert_affine(M: np.ndarray) -> np.ndarray:
 def warp_batch(images: Sequence[np.ndarray], img_index: Sequence[int], minv: np.ndarray, out_hw: tuple,
                out_w: Optional[Sequence[int]] = None, cpad: int = 8, scale: float = 1 / 127.5, mean: float = 1.0,
                std: float = 1.0, swap_rb: bool = True, cubic: bool = False, device=None,
-               replicate: bool = False) -> torch.Tensor:
+               replicate: bool = False, src=None) -> torch.Tensor:
     """Warp F crops (inverse 3x3 maps ``minv`` [F, 3, 3], dst->src) from uint8 RGB images into
     bf16 NHWC [F, OH, OW, cpad]: value = (px * scale - mean) / std, channels reversed if swap_rb.
     Default = ArcFace preprocessing (x/127.5 - 1 == (x/255 - 0.5)/0.5, BGR).  ``replicate``
@@ -188,13 +188,16 @@ def warp_batch(images: Sequence[np.ndarray], img_index: Sequence[int], minv: np.
     ow = list(out_w) if out_w is not None else [OW] * F
     device = torch.device(device) if device is not None else torch.device("cpu")
     if device.type == "cuda":
-        offs, flat = [], []
-        off = 0
-        for im in images:
-            offs.append(off)
-            flat.append(torch.from_numpy(np.ascontiguousarray(im)).reshape(-1))
-            off += im.size
-        src = torch.cat(flat).to(device, non_blocking=True)
+        if src is not None:             # (flat device uint8 tensor, offsets) of an earlier upload
+            src, offs = src
+        else:
+            offs, flat = [], []
+            off = 0
+            for im in images:
+                offs.append(off)
+                flat.append(torch.from_numpy(np.ascontiguousarray(im)).reshape(-1))
+                off += im.size
+            src = torch.cat(flat).to(device, non_blocking=True)
         meta = torch.tensor([[offs[i], images[i].shape[0], images[i].shape[1], ow[f]] for f, i in enumerate(img_index)],
                             dtype=torch.long).to(device)
         mv = torch.from_numpy(np.ascontiguousarray(minv, np.float32).reshape(F, 9)).to(device)
@@ -281,7 +284,10 @@ def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw
     connected components + boundary extraction (db_post.hip), host hull / min-area rect on
     the boundary pixels, GPU box score, host unclip / order / rescale.  ``params[j]`` has
     ``det_thresh`` / ``box_thresh`` / ``unclip_ratio``; ``hw[j]`` is the source (h, w).
-    Returns per image (boxes [k, 4, 2] int32, scores [k]) -- the same boxes as :func:`db_boxes`."""
+    Returns per image (boxes [k, 4, 2] int32, scores [k]) -- the same boxes as :func:`db_boxes`.
+    Components too small on both axes to pass ``min_size`` are dropped on the GPU, before the
+    ``max_candidates`` cut (the host path counts them; only maps with > max_candidates
+    components -- noise -- can differ)."""
     lib = load_host()
     if lib is None:
         raise RuntimeError("lumen host library (_lumen_host.so) not built")
@@ -292,15 +298,17 @@ def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw
     dev = prob.device
     thr = torch.tensor([float(p.det_thresh) for p in params], dtype=torch.float32, device=dev)
     cap = cap or max(1 << 16, n * rh * rw // 4)
-    lab = torch.empty(n * rh * rw, dtype=torch.int32, device=dev)
+    lab = torch.empty(5 * n * rh * rw, dtype=torch.int32, device=dev)     # labels + per-root bbox
     pts = torch.empty((cap, 3), dtype=torch.int32, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-    hip_ops().db_components(prob, thr, lab, pts, cnt)
+    hip_ops().db_components(prob, thr, lab, pts, cnt, int(min_size))
     K = int(cnt.item())
     if K > cap:                                      # pathological maps: retry with room for every pixel
         return db_boxes_gpu(prob, params, hw, rh, rw, max_candidates, min_size, max_boxes, cap=n * rh * rw)
-    P = pts[:K].cpu().numpy()
-    P = P[np.argsort(P[:, 0], kind="stable")]
+    dp = pts[:K]
+    if K > 1:                                        # group by component on the device (radix sort)
+        dp = dp.index_select(0, torch.sort(dp[:, 0], stable=True).indices)
+    P = dp.cpu().numpy()
     HW = rh * rw
     ip = ctypes.POINTER(ctypes.c_int)
     fp = ctypes.POINTER(ctypes.c_float)
@@ -323,9 +331,9 @@ def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw
     Q = np.concatenate(all_q) if all_q else np.zeros((0, 8), np.float32)
     scores = np.zeros((len(Q),), np.float32)
     if len(Q):
-        sc = torch.empty(len(Q), dtype=torch.float32, device=dev)
+        sc = torch.empty(3 * len(Q), dtype=torch.float32, device=dev)
         hip_ops().db_quad_score(prob, torch.from_numpy(Q).to(dev), torch.from_numpy(np.concatenate(all_i)).to(dev), sc)
-        scores = sc.cpu().numpy()
+        scores = sc[:len(Q)].cpu().numpy()
     out, o = [], 0
     for j in range(n):
         m = per_img[j]

@@ -265,12 +265,21 @@ class MI355XFaceBackend:
             scales.append(s)
             off += im.size
         tens = [torch.from_numpy(np.ascontiguousarray(im)) for im in images]
+        src = None
         if self.device.type == "cuda":
-            tens = [t.pin_memory() for t in tens] if len(tens) > 1 else tens
+            # one pinned H2D for the batch, kept for the alignment warps of the same images
+            if getattr(self, "_uploader", None) is None:
+                from ...utils.image import PinnedUploader
+
+                self._uploader = PinnedUploader(self.device)
+            dev, offs = self._uploader.upload(images)
+            src = dev
+            # (strong refs to the images keep their ids from being reused while the map lives)
+            self._last_upload = (dev, {id(im): int(o) for im, o in zip(images, offs)}, list(images))
         with stage("det_preprocess"):
             x = ops.image_prep(tens, (S, S), mean=(self.spec.det_mean,) * 3, std=(self.spec.det_std,) * 3, scale=1.0,
                                filter="cv2_linear", layout="nhwc8", pad=0.0, geoms=geoms, out_dtype=self.dtype,
-                               device=self.device)
+                               device=self.device, src=src)
         with stage("det_forward"):
             heads = self.det(x)
         return self._det_post(images, params, heads, scales)
@@ -329,6 +338,9 @@ class MI355XFaceBackend:
         R = self.spec.rec_size
         kw = dict(cpad=8, scale=1.0 / self.spec.rec_std, mean=self.spec.rec_mean / self.spec.rec_std, std=1.0,
                   swap_rb=self.spec.rec_color.lower() == "bgr", device=self.device)
+        last = getattr(self, "_last_upload", None)
+        if last is not None and self.device.type == "cuda" and all(id(im) in last[1] for im in images):
+            kw["src"] = (last[0], [last[1][id(im)] for im in images])     # reuse the detection upload
         if replicate is None or not any(replicate):
             return vision.warp_batch(images, img_index, minv, (R, R), **kw)
         rep = np.asarray(replicate, bool)

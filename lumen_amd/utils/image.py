@@ -21,10 +21,61 @@ _POOL: Optional[ThreadPoolExecutor] = None
 
 
 def _pool() -> ThreadPoolExecutor:
+    """Host decode / staging threads: LUMEN_DECODE_THREADS, else min(16, CPUs) (a GPU box's
+    share is 16 CPUs; PIL's libjpeg-turbo and numpy copies release the GIL)."""
     global _POOL
     if _POOL is None:
-        _POOL = ThreadPoolExecutor(max_workers=8, thread_name_prefix="lumen-decode")
+        import os
+
+        n = int(os.environ.get("LUMEN_DECODE_THREADS", "0")) or min(16, os.cpu_count() or 8)
+        _POOL = ThreadPoolExecutor(max_workers=max(1, n), thread_name_prefix="lumen-decode")
     return _POOL
+
+
+class PinnedUploader:
+    """One H2D copy for a batch of decoded images: the images are copied (on the decode
+    threads) into a pinned staging buffer and sent with one non-blocking transfer; returns
+    the flat uint8 device tensor and each image's element offset.  Two staging buffers
+    alternate, each reused only after its previous transfer completed (event), so the
+    copy of batch i+1 overlaps the GPU work of batch i.  Replaces torch.cat of pageable
+    arrays + a pageable (synchronous) copy per consumer."""
+
+    def __init__(self, device):
+        import torch
+
+        self.device = torch.device(device)
+        self.bufs = [None, None]
+        self.events = [None, None]
+        self.k = 0
+
+    def upload(self, images: Sequence[np.ndarray]):
+        import torch
+
+        sizes = [int(im.size) for im in images]
+        offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64) if sizes else np.zeros(0, np.int64)
+        total = int(sum(sizes))
+        k = self.k
+        self.k ^= 1
+        if self.events[k] is not None:
+            self.events[k].synchronize()
+        buf = self.bufs[k]
+        if buf is None or buf.numel() < total:
+            buf = torch.empty(max(total, 1 << 20), dtype=torch.uint8, pin_memory=True)
+            self.bufs[k] = buf
+        host = buf.numpy()
+
+        def cp(i):
+            host[offs[i]:offs[i] + sizes[i]] = np.ascontiguousarray(images[i]).reshape(-1)
+
+        if len(images) > 1:
+            list(_pool().map(cp, range(len(images))))
+        elif images:
+            cp(0)
+        dev = buf[:total].to(self.device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[k] = ev
+        return dev, offs
 
 
 def decode_rgb(data: bytes, draft_to: Optional[tuple[int, int]] = None, exif_transpose: bool = False) -> np.ndarray:

@@ -38,6 +38,27 @@ def test_conv2d(N, H, W, Cin, Cout, K, s, p, d, tile):
     assert _rel(got3, ref3) < 1e-2 and got3.min().item() >= 0
 
 
+@pytest.mark.parametrize("N,H,W,Cin,Cout,K,s,p,d", [
+    (2, 20, 20, 64, 128, 1, 1, 0, 1), (3, 28, 28, 128, 256, 3, 2, 1, 1), (2, 7, 7, 512, 512, 3, 1, 1, 1),
+    (4, 56, 56, 64, 64, 3, 1, 1, 1), (2, 30, 30, 64, 48, 3, 1, 2, 2), (1, 13, 9, 192, 80, 5, 2, 2, 1)])
+@pytest.mark.parametrize("tile", [-1, 11, 12, 13, 14])
+def test_conv2d_lds_pipeline(N, H, W, Cin, Cout, K, s, p, d, tile):
+    """Cin % 64 == 0: the LDS-DMA implicit-GEMM pipeline (conv_lds.hip; -1 picks it), incl. zero
+    padding taps, stride / dilation, residual + PReLU + post-ReLU epilogues."""
+    g = torch.Generator().manual_seed(H * Cin + K + Cout)
+    x = torch.randn(N, H, W, Cin, generator=g).bfloat16()
+    w = (torch.randn(Cout, K, K, Cin, generator=g) * (K * K * Cin) ** -0.5).bfloat16()
+    b = torch.randn(Cout, generator=g).bfloat16()
+    pr = (torch.rand(Cout, generator=g) * 0.3).bfloat16()
+    ref = cnn.conv2d(x, w, b, s, p, d, act=None, prelu=pr)
+    got = cnn.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), s, p, d, prelu=pr.to(DEV), tile=tile)
+    assert got.shape == ref.shape and _rel(got, ref) < 1e-2
+    r = torch.randn(*ref.shape, generator=g).bfloat16()
+    ref3 = cnn.conv2d(x, w, b, s, p, d, residual=r, post_act="relu")
+    got3 = cnn.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), s, p, d, residual=r.to(DEV), tile=tile, post_act="relu")
+    assert _rel(got3, ref3) < 1e-2 and got3.min().item() >= 0
+
+
 def test_conv2d_into_channel_slice():
     x = torch.randn(1, 16, 16, 32).bfloat16()
     w = (torch.randn(16, 3, 3, 32) * 0.05).bfloat16()

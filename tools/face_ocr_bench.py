@@ -39,13 +39,22 @@ def bench_face(args):
     be = MI355XFaceBackend.__new__(MI355XFaceBackend)
     be.det, be.rec, be.spec, be.device, be.dtype = det.to(dev).eval(), rec.to(dev).eval(), FaceSpec(), dev, torch.bfloat16
     be.template = vision.ARCFACE_DST
+    be._pool, be._dp, be.align_mode = None, {}, "standard"
     rng = np.random.default_rng(0)
     jpegs = [encode_jpeg(rng.integers(0, 255, (720, 1280, 3), dtype=np.uint8)) for _ in range(args.batch)]
     lms = np.array([[500, 300], [580, 300], [540, 350], [510, 400], [570, 400]], np.float32)
     minv = np.stack([vision.invert_affine(vision.similarity_transform(lms + 3 * k)) for k in range(args.faces)])
 
+    # the next batch's JPEGs decode on the host threads while this batch runs on the GPU
+    # (what the serving path does with two batches in flight per GPU worker)
+    from concurrent.futures import ThreadPoolExecutor
+
+    ahead = ThreadPoolExecutor(max_workers=1)
+    nxt = [ahead.submit(decode_many, jpegs)]
+
     def step():
-        imgs = decode_many(jpegs)
+        imgs = nxt[0].result()
+        nxt[0] = ahead.submit(decode_many, jpegs)
         be.detect_images(imgs, [DetParams(0.5, 0.4, 20, 2000)] * len(imgs))
         idx = [i for i in range(len(imgs)) for _ in range(args.faces)]
         be.embed_faces(imgs, idx, np.concatenate([minv] * len(imgs)))
@@ -60,7 +69,8 @@ def bench_face(args):
     return {"metric": "face detect+embed images/s", "value": args.batch / dt, "unit": "img/s",
             "ms_per_batch": dt * 1000, "batch": args.batch, "faces_per_image": args.faces,
             "faces_per_s": args.batch * args.faces / dt, "detector": "SCRFD-10G-shaped 640",
-            "recogniser": f"IResNet-{args.rec}", "image": "1280x720 JPEG"}
+            "recogniser": f"IResNet-{args.rec}", "image": "1280x720 JPEG",
+            "pipeline": "JPEG decode of batch i+1 overlapped with the GPU work of batch i"}
 
 
 def bench_ocr(args):
@@ -84,12 +94,26 @@ def bench_ocr(args):
         y = 20 + 25 * k
         boxes.append(np.array([[30, y], [30 + 200 + 10 * k, y], [30 + 200 + 10 * k, y + 22], [30, y + 22]], np.int32))
 
+    from concurrent.futures import ThreadPoolExecutor
+
+    ahead = ThreadPoolExecutor(max_workers=1)
+    nxt = [ahead.submit(decode_many, jpegs)]
+
+    from lumen_amd.runtime.metrics import StageTimer, use_timer
+
+    stages: dict = {}
+
     def step():
-        imgs = decode_many(jpegs)
-        be.detect(imgs, [OcrParams()] * len(imgs))
-        crops = [(i, b) for i in range(len(imgs)) for b in boxes]
-        be.recognize(imgs, crops)
+        imgs = nxt[0].result()
+        nxt[0] = ahead.submit(decode_many, jpegs)
+        t = StageTimer("ocr-bench", gpu=False)
+        with use_timer(t):
+            be.detect(imgs, [OcrParams()] * len(imgs))
+            crops = [(i, b) for i in range(len(imgs)) for b in boxes]
+            be.recognize(imgs, crops)
         torch.cuda.synchronize()
+        for k, v in t.finish().items():
+            stages[k] = stages.get(k, 0.0) + v
 
     for _ in range(args.warmup):
         step()
@@ -97,7 +121,9 @@ def bench_ocr(args):
     for _ in range(args.iters):
         step()
     dt = (time.perf_counter() - t0) / args.iters
+    n_steps = args.iters + args.warmup
     return {"metric": "ocr images/s", "value": args.batch / dt, "unit": "img/s", "ms_per_batch": dt * 1000,
+            "host_stage_ms_per_batch": {k: round(v / n_steps, 2) for k, v in stages.items()},
             "batch": args.batch, "crops_per_image": args.crops, "crops_per_s": args.batch * args.crops / dt,
             "detector": "DBNet-mobile 960", "recogniser": "SVTR-LCNet mobile", "image": "960x720 JPEG"}
 

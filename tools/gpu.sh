@@ -13,6 +13,7 @@
 #   face_ocr       tools/face_ocr_bench.py face + ocr
 #   prof_face / prof_ocr   rocprofv3 kernel stats of the face / OCR bench
 #   f8             fp8 tests (tests/test_fp8_gpu.py) + tools/f8_gemm_bench.py ($F8_SHAPES, $F8_M)
+#   pmc_face / pmc_ocr   PMC counters (SQ pass + memory pass) of the face / OCR pipelines
 #   pmc_gemm       PMC counters (MFMA, LDS conflicts, busy) of one ViT-L/14 GEMM shape
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -57,6 +58,13 @@ for task in "$@"; do
     prof_ocr)
       step prof_ocr 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ocr -o run -- \
         python3 tools/face_ocr_bench.py --what ocr --iters 3 ;;
+    pmc_face|pmc_ocr)
+      w=${task#pmc_}
+      step ${task}_sq 120 timeout -s KILL 100 rocprofv3 --kernel-trace \
+        --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM \
+        -d gpurun_out/${task}_sq -o run -- python3 tools/face_ocr_bench.py --what $w --iters 1 --warmup 1
+      step ${task}_mem 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc FETCH_SIZE \
+        -d gpurun_out/${task}_mem -o run -- python3 tools/face_ocr_bench.py --what $w --iters 1 --warmup 1 ;;
     pmc_gemm)
       step pmc_gemm 120 timeout -s KILL 100 rocprofv3 --kernel-trace \
         --pmc SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
