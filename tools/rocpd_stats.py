@@ -3,6 +3,8 @@
 
   python tools/rocpd_stats.py gpurun_out/prof_bench/run_results.db [out.csv] [--top N] [--ar-share]
 
+``--pmc`` prints per-kernel sums of the collected PMC counters (pmc_events view) instead, with
+derived MFMA / LDS-conflict / VALU ratios; ``--kernels a,b`` filters by name substring.
 ``--ar-share`` also prints the all-reduce share of GPU kernel time (IPC one-shot ``custom_ar``
 kernels + RCCL collectives) — BASELINE row 5's "all-reduce share of decode step time".
 """
@@ -18,8 +20,41 @@ def stats(db):
     return [(n, k, t, t / k, 100.0 * t / tot) for n, k, t in rows]
 
 
+def _flag_values():
+    return [sys.argv[i + 1] for i, a in enumerate(sys.argv[:-1]) if a in ("--top", "--kernels")]
+
+
+def pmc(db, kernels=None):
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, counter_name, sum(counter_value), count(distinct dispatch_id) from pmc_events "
+                     "group by name, counter_name").fetchall()
+    out: dict = {}
+    for n, cn, v, k in rows:
+        if kernels and not any(x in n for x in kernels):
+            continue
+        d = out.setdefault(n, {"dispatches": k})
+        d[cn] = v
+    for d in out.values():
+        if d.get("SQ_INSTS_LDS"):
+            d["lds_bank_conflict_cycles_per_lds_inst"] = d.get("SQ_LDS_BANK_CONFLICT", 0) / d["SQ_INSTS_LDS"]
+        tot = sum(d.get(k, 0) for k in ("SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_INSTS_LDS", "SQ_INSTS_VMEM"))
+        if tot:
+            d["mfma_inst_fraction"] = d.get("SQ_INSTS_MFMA", 0) / tot
+        if d.get("SQ_WAVE_CYCLES"):
+            d["wait_inst_fraction"] = d.get("SQ_WAIT_INST_ANY", 0) / d["SQ_WAVE_CYCLES"]
+    return out
+
+
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    if "--pmc" in sys.argv:
+        import json
+
+        ks = sys.argv[sys.argv.index("--kernels") + 1].split(",") if "--kernels" in sys.argv else None
+        for n, d in sorted(pmc(args[0], ks).items()):
+            print(json.dumps({"kernel": n[:120], **{k: (round(v, 4) if isinstance(v, float) else v)
+                                                   for k, v in d.items()}}))
+        return
     top = int(sys.argv[sys.argv.index("--top") + 1]) if "--top" in sys.argv else 15
     rows = stats(args[0])
     if len(args) > 1:
