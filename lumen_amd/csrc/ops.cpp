@@ -504,9 +504,13 @@ void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Te
   const int64_t Cout = w.size(0), KH = w.size(1), KW = w.size(2);
   TORCH_CHECK(w.size(3) == Cin && Cin % 8 == 0, "conv2d: Cin mismatch or not a multiple of 8");
   TORCH_CHECK(Cout % 16 == 0, "conv2d: Cout must be a multiple of 16");
-  TORCH_CHECK(stride.size() == 2 && padding.size() == 2 && dilation.size() == 2, "conv2d: 2-D params");
-  const int64_t Ho = (H + 2 * padding[0] - dilation[0] * (KH - 1) - 1) / stride[0] + 1;
-  const int64_t Wo = (W + 2 * padding[1] - dilation[1] * (KW - 1) - 1) / stride[1] + 1;
+  TORCH_CHECK(stride.size() == 2 && (padding.size() == 2 || padding.size() == 4) && dilation.size() == 2,
+              "conv2d: 2-D params (padding [ph, pw] or ONNX-style [top, left, bottom, right])");
+  // asymmetric padding: the kernels pad top / left explicitly; bottom / right follow from Ho / Wo
+  // (taps past the input edge read zeros either way)
+  const int64_t pb = padding.size() == 4 ? padding[2] : padding[0], pr = padding.size() == 4 ? padding[3] : padding[1];
+  const int64_t Ho = (H + padding[0] + pb - dilation[0] * (KH - 1) - 1) / stride[0] + 1;
+  const int64_t Wo = (W + padding[1] + pr - dilation[1] * (KW - 1) - 1) / stride[1] + 1;
   const int64_t ldo = pixel_stride(out, "out");
   TORCH_CHECK(out.size(0) == N && out.size(1) == Ho && out.size(2) == Wo && out.size(3) == Cout, "conv2d: out shape");
   lumen::GemmEpi ep{};

@@ -19,9 +19,23 @@ def _pair(v):
     return (v, v) if isinstance(v, int) else tuple(v)
 
 
+def _pads4(padding) -> tuple:
+    """int | (ph, pw) | ONNX (top, left, bottom, right) -> (top, left, bottom, right)."""
+    if isinstance(padding, (tuple, list)) and len(padding) == 4:
+        return tuple(int(v) for v in padding)
+    p = _pair(padding)
+    return (p[0], p[1], p[0], p[1])
+
+
+def _pad_arg(padding) -> list:
+    q = _pads4(padding)
+    return [q[0], q[1]] if (q[0], q[1]) == (q[2], q[3]) else list(q)
+
+
 def conv_out_hw(H, W, KH, KW, stride, padding, dilation):
-    s, p, d = _pair(stride), _pair(padding), _pair(dilation)
-    return ((H + 2 * p[0] - d[0] * (KH - 1) - 1) // s[0] + 1, (W + 2 * p[1] - d[1] * (KW - 1) - 1) // s[1] + 1)
+    s, d = _pair(stride), _pair(dilation)
+    pt, pl, pb, pr = _pads4(padding)
+    return ((H + pt + pb - d[0] * (KH - 1) - 1) // s[0] + 1, (W + pl + pr - d[1] * (KW - 1) - 1) // s[1] + 1)
 
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride=1, padding=0, dilation=1,
@@ -35,11 +49,12 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         out = torch.empty((N, Ho, Wo, Cout), device=x.device, dtype=out_dtype or x.dtype)
     a = act_id(act)
     if x.is_cuda:
-        hip_ops().conv2d(x, w, bias, residual, prelu, a, list(_pair(stride)), list(_pair(padding)),
+        hip_ops().conv2d(x, w, bias, residual, prelu, a, list(_pair(stride)), _pad_arg(padding),
                          list(_pair(dilation)), out, int(tile), act_id(post_act))
         return out
-    y = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, _pair(stride), _pair(padding),
-                 _pair(dilation)).permute(0, 2, 3, 1)
+    pt, pl, pb, pr = _pads4(padding)
+    y = F.conv2d(F.pad(x.float().permute(0, 3, 1, 2), (pl, pr, pt, pb)), w.float().permute(0, 3, 1, 2), None,
+                 _pair(stride), 0, _pair(dilation)).permute(0, 2, 3, 1)
     if bias is not None:
         y = y + bias.float()
     y = _act_ref(y, a)
@@ -61,11 +76,14 @@ def conv2d_dw(x, w, bias=None, stride=1, padding=0, dilation=1, act=None, out=No
         out = torch.empty((N, Ho, Wo, C), device=x.device, dtype=x.dtype)
     a = act_id(act)
     if x.is_cuda:
-        hip_ops().conv2d_dw(x.contiguous(), w.contiguous(), bias, a, list(_pair(stride)), list(_pair(padding)),
+        pt, pl = _pads4(padding)[:2]            # bottom / right follow from the out size
+        hip_ops().conv2d_dw(x.contiguous(), w.contiguous(), bias, a, list(_pair(stride)), [pt, pl],
                             list(_pair(dilation)), out)
         return out
     wt = w.float().permute(2, 0, 1).unsqueeze(1)  # [C, 1, KH, KW]
-    y = F.conv2d(x.float().permute(0, 3, 1, 2), wt, None, _pair(stride), _pair(padding), _pair(dilation), groups=C)
+    pt, pl, pb, pr = _pads4(padding)
+    y = F.conv2d(F.pad(x.float().permute(0, 3, 1, 2), (pl, pr, pt, pb)), wt, None, _pair(stride), 0, _pair(dilation),
+                 groups=C)
     y = y.permute(0, 2, 3, 1)
     if bias is not None:
         y = y + bias.float()

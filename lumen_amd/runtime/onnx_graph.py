@@ -12,11 +12,16 @@ onnxrt_backend.py, packages/lumen-ocr/src/lumen_ocr/backends/onnxrt_backend.py).
   depthwise ``[KH, KW, C]`` layouts, channel counts padded to the kernels' multiples.
 
 At run time 4-D activations stay NHWC on the GPU (channels padded to a multiple of 8/16
-and sliced back only when an NCHW-semantic op needs them): Conv (dense / depthwise /
-grouped), pooling, GlobalAveragePool, nearest Resize x2 (+ fused Add), Concat on channels
-and standalone activations run on HIP kernels; shape / reshape / transpose / softmax /
-elementwise-broadcast nodes run as torch ops in NCHW semantics.  On the CPU every node runs
-the fp32 NCHW reference (the numerics oracle for the GPU path in the tests).
+and sliced back only when an NCHW-semantic op needs them).  On the GPU every compute node is
+a HIP kernel: Conv (dense incl. asymmetric padding, depthwise, grouped = one dense launch per
+group on channel slices), ConvTranspose with kernel == stride (1x1 GEMM + pixel shuffle, BN /
+activation folded), pooling, GlobalAveragePool, nearest / bilinear Resize, Concat on channels,
+LayerNormalization (and the ReduceMean-Sub-Pow-ReduceMean-Add-Sqrt-Div-Mul-Add subgraph
+exporters emit for it), Softmax, activation x activation MatMul (strided batched GEMM),
+elementwise unary / broadcast binary ops (csrc/onnx_ops.hip).  Shape arithmetic (Shape,
+integer Gather / Concat / Mul, Reshape targets) stays on the host; Reshape / Transpose /
+Slice are views or copies.  Unsupported ops are reported when the graph is LOADED.  On the
+CPU every node runs the fp32 NCHW reference (the numerics oracle for the GPU path).
 """
 from __future__ import annotations
 
@@ -34,6 +39,18 @@ from ..ops import cnn
 from ..utils import onnx_lite as ox
 
 _ACTS = {"Relu": "relu", "Sigmoid": "sigmoid", "HardSwish": "hardswish", "LeakyRelu": "leaky"}
+
+SUPPORTED_OPS = frozenset({
+    "Conv", "ConvTranspose", "BatchNormalization", "Relu", "Sigmoid", "Tanh", "Exp", "Log", "Sqrt", "Neg", "Abs",
+    "Reciprocal", "Floor", "Ceil", "Erf", "LeakyRelu", "HardSigmoid", "HardSwish", "PRelu", "Clip", "Add", "Sub", "Mul",
+    "Div", "Pow", "Max", "Min", "Equal", "Greater", "Less", "MaxPool", "AveragePool", "GlobalAveragePool",
+    "GlobalMaxPool", "Resize", "Upsample", "Concat", "Flatten", "Reshape", "Transpose", "Squeeze", "Unsqueeze",
+    "Shape", "Gather", "Slice", "Cast", "Softmax", "Gemm", "MatMul", "Constant", "ReduceMean", "ArgMax",
+    "Identity", "Dropout", "LayerNormalization"})
+_UNARY = {"Relu": 0, "Sigmoid": 1, "Tanh": 2, "Exp": 3, "Log": 4, "Sqrt": 5, "Neg": 6, "Abs": 7, "Reciprocal": 8,
+          "HardSwish": 9, "HardSigmoid": 10, "LeakyRelu": 11, "Clip": 12, "Floor": 13, "Ceil": 14, "Erf": 15}
+_BINARY = {"Add": 0, "Sub": 1, "Mul": 2, "Div": 3, "Pow": 4, "Max": 5, "Min": 6}
+_RESIZE_MODES = {"half_pixel": 0, "align_corners": 1, "asymmetric": 2, "pytorch_half_pixel": 3}
 
 
 def _pad_to(c: int, m: int) -> int:
@@ -61,11 +78,15 @@ class OnnxGraph:
         self.device = torch.device(device)
         self.gpu = self.device.type == "cuda"
         self.dtype = dtype or (torch.bfloat16 if self.gpu else torch.float32)
+        bad = sorted({n.op_type for n in g.nodes} - SUPPORTED_OPS)
+        if bad:     # fail at load time, not on the first request
+            raise NotImplementedError(f"ONNX ops not supported by the MI355X graph executor: {', '.join(bad)}")
         self.init = {k: torch.from_numpy(np.array(v)) for k, v in g.initializers.items()}
         self.consumers: dict[str, list] = {}
         for n in g.nodes:
             for x in n.inputs:
                 self.consumers.setdefault(x, []).append(n)
+        self._dev_init: dict = {}
         self.plan = self._plan(g)
 
     # ------------------------------------------------------------------ planning
@@ -83,9 +104,105 @@ class OnnxGraph:
             if n.op_type == "Conv" and n.inputs[1] in self.init:
                 step = self._plan_conv(n, skip)
                 plan.append(step)
+            elif n.op_type == "ConvTranspose" and self.gpu and self._convt_ok(n):
+                plan.append(self._plan_convt(n, skip))
+            elif n.op_type == "ReduceMean" and self.gpu and (ln := self._match_layernorm(n)) is not None:
+                skip.update(ln.pop("nodes"))
+                plan.append(("ln", ln))
             else:
                 plan.append(("node", n))
         return plan
+
+    # ---- ConvTranspose with kernel == stride (DBNet heads): 1x1 GEMM to f*f*Cout + pixel shuffle
+    def _convt_ok(self, n) -> bool:
+        a = n.attrs
+        if n.inputs[1] not in self.init or int(a.get("group", 1)) != 1:
+            return False
+        w = self.init[n.inputs[1]]
+        k = tuple(a.get("kernel_shape", w.shape[2:]))
+        s = tuple(a.get("strides", [1, 1]))
+        return (w.dim() == 4 and k[0] == k[1] == s[0] == s[1] and not any(a.get("pads", [0, 0, 0, 0]))
+                and not any(a.get("output_padding", [0, 0])) and tuple(a.get("dilations", [1, 1])) == (1, 1))
+
+    def _plan_convt(self, n, skip):
+        w = self.init[n.inputs[1]].float()                       # [Cin, Cout, f, f]
+        cin, cout, f, _ = w.shape
+        b = self.init[n.inputs[2]].float() if len(n.inputs) > 2 and n.inputs[2] else torch.zeros(cout)
+        out = n.outputs[0]
+        bn = self._single_consumer(out, "BatchNormalization")
+        if bn is not None and all(x in self.init for x in bn.inputs[1:5]):
+            sc, bi, mu, var = (self.init[x].float() for x in bn.inputs[1:5])
+            s = sc / torch.sqrt(var + float(bn.attrs.get("epsilon", 1e-5)))
+            w = w * s.view(1, -1, 1, 1)
+            b = (b - mu) * s + bi
+            skip.add(id(bn))
+            out = bn.outputs[0]
+        act = None
+        nxt = self.consumers.get(out, [])
+        if len(nxt) == 1 and out not in self.model.graph.outputs and nxt[0].op_type in ("Relu", "Sigmoid"):
+            act = _ACTS[nxt[0].op_type]
+            skip.add(id(nxt[0]))
+            out = nxt[0].outputs[0]
+        cin_p, cout_p = _pad_to(cin, 8), _pad_to(cout, 8)
+        while (f * f * cout_p) % 16:
+            cout_p += 8
+        w1 = torch.zeros(f, f, cout_p, cin_p)                     # rows (dy, dx, co) = pixel-shuffle order
+        w1[:, :, :cout, :cin] = w.permute(2, 3, 1, 0)
+        b1 = torch.zeros(f, f, cout_p)
+        b1[:, :, :cout] = b
+        st = {"x": n.inputs[0], "out": out, "f": f, "cin_p": cin_p, "cout": cout, "cout_p": cout_p, "act": act,
+              "gw": w1.reshape(f * f * cout_p, 1, 1, cin_p).to(self.device, self.dtype).contiguous(),
+              "gb": b1.reshape(-1).to(self.device).contiguous()}
+        return ("convt", st)
+
+    # ---- LayerNorm subgraph: m = ReduceMean(x); d = Sub(x, m); v = ReduceMean(Pow(d, 2));
+    #      y = Div(d, Sqrt(Add(v, eps))) [* gamma] [+ beta], all over the last axis
+    def _match_layernorm(self, rm):
+        def one(name, op):
+            c = self.consumers.get(name, [])
+            return c[0] if len(c) == 1 and c[0].op_type == op else None
+
+        def const(name):
+            return float(self.init[name].reshape(-1)[0]) if name in self.init and self.init[name].numel() == 1 else None
+
+        if rm.attrs.get("axes") not in ([-1],) or not rm.attrs.get("keepdims", 1):
+            return None
+        x = rm.inputs[0]
+        subs = [c for c in self.consumers.get(rm.outputs[0], []) if c.op_type == "Sub" and c.inputs[0] == x]
+        if len(subs) != 1:
+            return None
+        sub = subs[0]
+        d = sub.outputs[0]
+        dc = self.consumers.get(d, [])
+        pw = next((c for c in dc if c.op_type == "Pow"), None)
+        dv = next((c for c in dc if c.op_type == "Div" and c.inputs[0] == d), None)
+        if pw is None or dv is None or len(dc) != 2 or const(pw.inputs[1]) != 2.0:
+            return None
+        rm2 = one(pw.outputs[0], "ReduceMean")
+        if rm2 is None or rm2.attrs.get("axes") not in ([-1],):
+            return None
+        ad = one(rm2.outputs[0], "Add")
+        if ad is None:
+            return None
+        eps = const(ad.inputs[1] if ad.inputs[0] == rm2.outputs[0] else ad.inputs[0])
+        sq = one(ad.outputs[0], "Sqrt")
+        if eps is None or sq is None or dv.inputs[1] != sq.outputs[0]:
+            return None
+        nodes = [rm, sub, pw, rm2, ad, sq, dv]
+        out, gamma, beta = dv.outputs[0], None, None
+        mul = one(out, "Mul")
+        if mul is not None:
+            g = mul.inputs[1] if mul.inputs[0] == out else mul.inputs[0]
+            if g in self.init:
+                gamma, out = g, mul.outputs[0]
+                nodes.append(mul)
+                add = one(out, "Add")
+                if add is not None:
+                    bb = add.inputs[1] if add.inputs[0] == out else add.inputs[0]
+                    if bb in self.init:
+                        beta, out = bb, add.outputs[0]
+                        nodes.append(add)
+        return {"x": x, "out": out, "eps": eps, "gamma": gamma, "beta": beta, "nodes": {id(q) for q in nodes}}
 
     def _plan_conv(self, n: ox.Node, skip: set):
         w = self.init[n.inputs[1]].float()
@@ -166,8 +283,17 @@ class OnnxGraph:
             s["gb"] = bb.to(dev).contiguous()
             s["mode"] = "dw"
             s["mult"] = mult
+        elif cin % G == 0 and (cin // G) % 8 == 0 and (cout // G) % 16 == 0:
+            # grouped: one dense conv per group over channel slices (ipg % 8: 16-byte slice starts)
+            ipg, opg = cin // G, cout // G
+            s["gws"] = [w[gi * opg:(gi + 1) * opg].permute(0, 2, 3, 1).to(dev, dt).contiguous() for gi in range(G)]
+            s["gb"] = s["b"].to(dev).contiguous()
+            if s["prelu"] is not None:
+                pr = s["prelu"] if s["prelu"].numel() > 1 else s["prelu"].expand(cout)
+                s["gprelu"] = pr.to(dev, dt).contiguous()
+            s.update(mode="grouped", ipg=ipg, opg=opg, kh=kh, kw=kw)
         else:
-            s["mode"] = "ref"     # general grouped conv: NCHW torch on the device
+            s["mode"] = "ref"     # grouped conv with unaligned group widths: NCHW torch on the device
 
     # ------------------------------------------------------------------ execution
     @torch.no_grad()
@@ -178,6 +304,10 @@ class OnnxGraph:
         for kind, step in self.plan:
             if kind == "conv":
                 vals[step["out"]] = self._conv(step, vals)
+            elif kind == "convt":
+                vals[step["out"]] = self._convt(step, vals)
+            elif kind == "ln":
+                vals[step["out"]] = self._layernorm(vals, step["x"], step["gamma"], step["beta"], step["eps"])
             else:
                 for name, v in zip(step.outputs, self._node(step, vals)):
                     vals[name] = v
@@ -191,8 +321,28 @@ class OnnxGraph:
         if name in vals:
             return vals[name]
         if name in self.init:
-            return _V(self.init[name].to(self.device))
+            t = self.init[name]
+            if not t.is_floating_point():       # shape / index data: host-side
+                return _V(t)
+            if name not in self._dev_init:
+                self._dev_init[name] = t.to(self.device)
+            return _V(self._dev_init[name])
         raise KeyError(f"onnx value {name} not computed")
+
+    def _convt(self, s: dict, vals) -> _V:
+        x = self._nhwc(self._get(vals, s["x"]), s["cin_p"])
+        y = cnn.conv2d(x, s["gw"], s["gb"], 1, 0, 1, act=s["act"])
+        return _V(cnn.pixel_shuffle_up(y, s["cout_p"], s["f"]), True, s["cout"])
+
+    def _layernorm(self, vals, x_name, gamma, beta, eps) -> _V:
+        v = self._get(vals, x_name)
+        x = v.nchw() if v.nhwc else v.t
+        D = x.shape[-1]
+        g = self._get(vals, gamma).t.to(self.dtype) if gamma else torch.ones(D, device=self.device, dtype=self.dtype)
+        b = self._get(vals, beta).t.to(self.dtype) if beta else torch.zeros(D, device=self.device, dtype=self.dtype)
+        x2 = x.reshape(-1, D).to(self.dtype).contiguous()
+        y = ops.layer_norm(x2, g.reshape(-1).contiguous(), b.reshape(-1).contiguous(), eps)
+        return _V(y.reshape(x.shape))
 
     def _nhwc(self, v: _V, cp: int) -> torch.Tensor:
         """value as a contiguous NHWC tensor with ``cp`` (padded) channels, compute dtype."""
@@ -227,41 +377,83 @@ class OnnxGraph:
                 y = y + self._get(vals, s["res"]).nchw().to(y.dtype)
             return _V(y.to(self.dtype) if self.gpu else y)
         pt, pl, pb, pr = s["pads"]
-        if (pt, pl) != (pb, pr):
-            raise NotImplementedError("asymmetric conv padding on the GPU path")
+        pads = (pt, pl, pb, pr)                  # asymmetric: the kernels pad top / left, Ho / Wo do the rest
         act = s["act"]
+        relu6 = act == "relu6"
         if s["mode"] == "dense":
             cin_p = s["gw"].shape[-1]
             xt = self._nhwc(x, cin_p)
             res = None
             if s["res"] is not None:
                 res = self._nhwc(self._get(vals, s["res"]), s["gw"].shape[0])
-            y = cnn.conv2d(xt, s["gw"], s["gb"], s["stride"], (pt, pl), s["dil"],
-                           act=None if act == "relu6" else act, residual=res, prelu=s.get("gprelu"))
-            if act == "relu6":
-                y.clamp_(0, 6)
+            y = cnn.conv2d(xt, s["gw"], s["gb"], s["stride"], pads, s["dil"], act=None if relu6 else act,
+                           residual=res, prelu=s.get("gprelu"))
+            if relu6:
+                y = self._unary(y, 12, 0.0, 6.0)
+            return _V(y, True, s["cout"])
+        if s["mode"] == "grouped":               # one dense launch per group on channel slices
+            G, ipg, opg = s["groups"], s["ipg"], s["opg"]
+            xt = self._nhwc(x, s["cin"])
+            N, H, W, _ = xt.shape
+            Ho, Wo = cnn.conv_out_hw(H, W, s["kh"], s["kw"], s["stride"], pads, s["dil"])
+            y = torch.empty((N, Ho, Wo, s["cout"]), device=self.device, dtype=self.dtype)
+            res = self._nhwc(self._get(vals, s["res"]), s["cout"]) if s["res"] is not None else None
+            for gi in range(G):
+                cs, os_ = slice(gi * ipg, (gi + 1) * ipg), slice(gi * opg, (gi + 1) * opg)
+                cnn.conv2d(xt[..., cs], s["gws"][gi], s["gb"][os_], s["stride"], pads, s["dil"],
+                           act=None if relu6 else act, residual=res[..., os_] if res is not None else None,
+                           prelu=s["gprelu"][os_] if s.get("gprelu") is not None else None, out=y[..., os_])
+            if relu6:
+                y = self._unary(y, 12, 0.0, 6.0)
             return _V(y, True, s["cout"])
         # depthwise (channel multiplier m): duplicate input channels, one dw pass
-        xt = self._nhwc(x, _pad_to(s["cin"], 8))[..., : s["cin"]]
-        if s["mult"] > 1:
-            xt = xt.repeat_interleave(s["mult"], dim=-1)
         cp = s["gw"].shape[-1]
-        if xt.shape[-1] != cp:
-            xt = F.pad(xt, (0, cp - xt.shape[-1]))
-        xt = xt.contiguous()
-        y = cnn.conv2d_dw(xt, s["gw"], s["gb"], s["stride"], (pt, pl), s["dil"],
-                          act=None if act == "relu6" else act)
-        if act == "relu6":
-            y.clamp_(0, 6)
-        if s["prelu"] is not None:
+        if s["mult"] > 1:
+            xt = self._nhwc(x, _pad_to(s["cin"], 8))[..., : s["cin"]].repeat_interleave(s["mult"], dim=-1)
+            if xt.shape[-1] != cp:
+                xt = F.pad(xt, (0, cp - xt.shape[-1]))
+            xt = xt.contiguous()
+        else:
+            xt = self._nhwc(x, cp)
+        N, H, W, _ = xt.shape
+        Ho, Wo = cnn.conv_out_hw(H, W, s["gw"].shape[0], s["gw"].shape[1], s["stride"], pads, s["dil"])
+        y = torch.empty((N, Ho, Wo, cp), device=self.device, dtype=self.dtype)
+        y = cnn.conv2d_dw(xt, s["gw"], s["gb"], s["stride"], pads, s["dil"], act=None if relu6 else act, out=y)
+        if relu6:
+            y = self._unary(y, 12, 0.0, 6.0)
+        if s["prelu"] is not None:          # per-channel PReLU = max(x,0) + a*min(x,0) via the binary kernel
             p = s["prelu"].to(self.device, torch.float32)
-            p = p if p.numel() > 1 else p.expand(s["cout"])
-            yf = y[..., : s["cout"]].float()
-            y[..., : s["cout"]] = torch.where(yf > 0, yf, yf * p).to(y.dtype)
+            p = (p if p.numel() > 1 else p.expand(s["cout"])).contiguous()
+            pp = torch.zeros(cp, device=self.device)
+            pp[: s["cout"]] = p
+            neg = self._binary(y, torch.zeros((), device=self.device), 6)        # min(x, 0)
+            pos = self._binary(y, torch.zeros((), device=self.device), 5)        # max(x, 0)
+            y = self._binary(pos, self._binary(neg, pp, 2, f32=True), 0)
         if s["res"] is not None:
             r = self._nhwc(self._get(vals, s["res"]), cp)
-            y = (y.float() + r.float()).to(y.dtype)
+            y = self._binary(y, r, 0)
         return _V(y, True, s["cout"])
+
+    # ---- elementwise HIP kernels (csrc/onnx_ops.hip)
+    def _unary(self, x: torch.Tensor, op: int, p0: float = 0.0, p1: float = 0.0) -> torch.Tensor:
+        x = x.contiguous()
+        out = torch.empty(x.shape, device=self.device, dtype=self.dtype)
+        ops.hip_ops().ew_unary(x, out, int(op), float(p0), float(p1))
+        return out
+
+    def _binary(self, a: torch.Tensor, b: torch.Tensor, op: int, f32: bool = False) -> torch.Tensor:
+        shape = torch.broadcast_shapes(a.shape, b.shape)
+        if not a.is_floating_point():
+            a = a.float()
+        if not b.is_floating_point():
+            b = b.float()
+        if a.dtype not in (torch.float32, torch.bfloat16):
+            a = a.float()
+        if b.dtype not in (torch.float32, torch.bfloat16):
+            b = b.float()
+        out = torch.empty(shape, device=self.device, dtype=torch.float32 if f32 else self.dtype)
+        ops.hip_ops().ew_binary(a.to(self.device), b.to(self.device), out, int(op))
+        return out
 
     # ------------------------------------------------------------------ generic nodes
     def _node(self, n: ox.Node, vals) -> list[_V]:
@@ -269,6 +461,8 @@ class OnnxGraph:
         ins = [self._get(vals, x) if x else None for x in n.inputs]
         if self.gpu:
             fast = self._node_nhwc(n, ins)
+            if fast is None:
+                fast = self._node_gpu(n, ins)
             if fast is not None:
                 return fast
         t = [i.nchw() if i is not None else None for i in ins]
@@ -368,8 +562,8 @@ class OnnxGraph:
             for ax in sorted(int(q) for q in axes):
                 x = x.unsqueeze(ax if ax >= 0 else x.dim() + 1 + ax)
             return out(x)
-        if op == "Shape":
-            return out(torch.tensor(list(t[0].shape), dtype=torch.int64, device=self.device))
+        if op == "Shape":        # host-side: shape arithmetic never launches device kernels
+            return out(torch.tensor(list(t[0].shape), dtype=torch.int64))
         if op == "Gather":
             ax = int(a.get("axis", 0))
             idx = t[1].long()
@@ -396,13 +590,98 @@ class OnnxGraph:
         if op in ("Gemm", "MatMul"):
             return out(self._matmul(n, t))
         if op == "Constant":
-            return out(torch.as_tensor(np.array(a["value"])).to(self.device))
+            c = torch.as_tensor(np.array(a["value"]))
+            return out(c.to(self.device) if c.is_floating_point() else c)
         if op == "ReduceMean":
             axes = a.get("axes", None)
             return out(t[0].mean(dim=tuple(axes), keepdim=bool(a.get("keepdims", 1))) if axes else t[0].mean())
+        if op == "LayerNormalization":
+            ax = int(a.get("axis", -1)) % t[0].dim()
+            shape = t[0].shape[ax:]
+            w = t[1] if len(t) > 1 and t[1] is not None else None
+            b = t[2] if len(t) > 2 and t[2] is not None else None
+            return out(F.layer_norm(t[0], shape, w.reshape(shape) if w is not None else None,
+                                    b.reshape(shape) if b is not None else None, float(a.get("epsilon", 1e-5))))
+        if op == "Erf":
+            return out(torch.erf(t[0]))
         if op == "ArgMax":
             return out(t[0].argmax(dim=int(a.get("axis", 0)), keepdim=bool(a.get("keepdims", 1))))
         raise NotImplementedError(f"ONNX op {op} is not supported by the MI355X graph executor")
+
+    def _node_gpu(self, n: ox.Node, ins) -> Optional[list]:
+        """HIP kernels for the NCHW-semantic compute nodes; None -> the generic path (host-side
+        shape arithmetic, views / copies)."""
+        op, a = n.op_type, n.attrs
+        t = [i.nchw() if i is not None else None for i in ins]
+        fp = [x is not None and x.is_floating_point() for x in t]
+        if op in _UNARY and t and fp[0]:
+            p0, p1 = 0.0, 0.0
+            if op == "HardSigmoid":
+                p0, p1 = float(a.get("alpha", 0.2)), float(a.get("beta", 0.5))
+            elif op == "LeakyRelu":
+                p0 = float(a.get("alpha", 0.01))
+            elif op == "Clip":
+                lo = float(t[1]) if len(t) > 1 and t[1] is not None else a.get("min", None)
+                hi = float(t[2]) if len(t) > 2 and t[2] is not None else a.get("max", None)
+                p0 = float(lo) if lo is not None else -math.inf
+                p1 = float(hi) if hi is not None else math.inf
+            return [_V(self._unary(t[0], _UNARY[op], p0, p1))]
+        if op in _BINARY and len(t) == 2 and (fp[0] or fp[1]):
+            return [_V(self._binary(t[0], t[1], _BINARY[op]))]
+        if op == "PRelu" and fp[0]:
+            sl = t[1]
+            if sl.dim() == 1 and t[0].dim() == 4:
+                sl = sl.view(1, -1, 1, 1)
+            z = torch.zeros((), device=self.device)
+            return [_V(self._binary(self._binary(t[0], z, 5), self._binary(self._binary(t[0], z, 6), sl, 2), 0))]
+        if op == "BatchNormalization" and fp[0]:
+            sc, bi, mu, var = (x.float() for x in t[1:5])
+            scale = sc / torch.sqrt(var + float(a.get("epsilon", 1e-5)))
+            shift = bi - mu * scale
+            if t[0].dim() == 4:
+                scale, shift = scale.view(1, -1, 1, 1), shift.view(1, -1, 1, 1)
+            return [_V(self._binary(self._binary(t[0], scale, 2, f32=True), shift, 0))]
+        if op == "Softmax" and fp[0]:
+            x = t[0]
+            ax = int(a.get("axis", -1)) % x.dim()
+            xm = x.movedim(ax, -1).contiguous()
+            y = torch.empty(xm.shape, device=self.device, dtype=self.dtype)
+            ops.hip_ops().softmax_rows(xm, y)
+            return [_V(y.movedim(-1, ax))]
+        if op == "LayerNormalization" and fp[0] and int(a.get("axis", -1)) in (-1, t[0].dim() - 1):
+            return [self._layernorm({n.inputs[0]: ins[0]}, n.inputs[0], n.inputs[1] if len(n.inputs) > 1 else None,
+                                    n.inputs[2] if len(n.inputs) > 2 else None, float(a.get("epsilon", 1e-5)))]
+        if op == "MatMul" and fp[0] and fp[1] and not (n.inputs[1] in self.init and t[1].dim() == 2):
+            x, w = t[0], t[1]
+            if x.dim() >= 2 and w.dim() >= 2:
+                lead = torch.broadcast_shapes(x.shape[:-2], w.shape[:-2])
+                M, K, N = x.shape[-2], x.shape[-1], w.shape[-1]
+                xb = x.expand(*lead, M, K).reshape(-1, M, K)
+                wb = w.expand(*lead, K, N).reshape(-1, K, N)
+                y = torch.empty((xb.shape[0], M, N), device=self.device, dtype=torch.float32)
+                ops.hip_ops().bmm(xb, wb, y)
+                return [_V(y.reshape(*lead, M, N).to(self.dtype))]
+        if op in ("Resize", "Upsample") and fp[0] and t[0].dim() == 4 and a.get("mode", "nearest") == "linear":
+            x = ins[0]
+            cp = _pad_to(x.c if x.nhwc else t[0].shape[1], 8)
+            xt = self._nhwc(x, cp)
+            N, H, W, _ = xt.shape
+            scales = sizes = None
+            if op == "Upsample":
+                scales = t[1].tolist()
+            else:
+                if len(t) > 2 and t[2] is not None and t[2].numel():
+                    scales = t[2].tolist()
+                if len(t) > 3 and t[3] is not None and t[3].numel():
+                    sizes = [int(q) for q in t[3].tolist()]
+            Ho, Wo = (sizes[2], sizes[3]) if sizes else (int(H * scales[2]), int(W * scales[3]))
+            mode = _RESIZE_MODES.get(a.get("coordinate_transformation_mode", "half_pixel"))
+            if mode is None:
+                return None
+            y = torch.empty((N, Ho, Wo, cp), device=self.device, dtype=self.dtype)
+            ops.hip_ops().resize_bilinear_nhwc(xt.contiguous(), y, int(mode))
+            return [_V(y, True, x.c if x.nhwc else t[0].shape[1])]
+        return None
 
     def _resize(self, n, t):
         a = n.attrs

@@ -150,3 +150,83 @@ def test_unsupported_op_is_loud():
     g = ox.Graph([ox.Node("NonMaxSuppression", ["x"], ["y"])], {}, ["x"], ["y"])
     with pytest.raises(NotImplementedError):
         OnnxGraph(ox.write_model(g)).run({"x": torch.zeros(1)})
+
+
+def test_unsupported_op_fails_at_load():
+    g = ox.Graph([ox.Node("Relu", ["x"], ["r"]), ox.Node("NonMaxSuppression", ["r"], ["y"]),
+                  ox.Node("Einsum", ["r"], ["z"])], {}, ["x"], ["y", "z"])
+    with pytest.raises(NotImplementedError, match="Einsum, NonMaxSuppression"):
+        OnnxGraph(ox.write_model(g))
+
+
+def ocrnet_graph():
+    """PP-OCR-style coverage of the executor's remaining node kinds: asymmetric conv padding,
+    grouped conv, ConvTranspose (k == s) + BN + ReLU, bilinear Resize, a decomposed LayerNorm
+    subgraph, LayerNormalization, attention (MatMul of activations + Softmax), broadcast
+    binary ops, unary ops, PRelu, Clip."""
+    N = ox.Node
+    init = {"w0": _w(32, 3, 3, 3), "b0": _w(32), "wg": _w(32, 16, 3, 3), "bg": _w(32),
+            "wt": _w(32, 16, 2, 2), "bt": _w(16), "wq": _w(16, 16), "wk": _w(16, 16), "wv": _w(16, 16),
+            "g1": (1 + 0.1 * R.standard_normal(16)).astype(np.float32), "be1": _w(16),
+            "g2": (1 + 0.1 * R.standard_normal(16)).astype(np.float32), "be2": _w(16),
+            "two": np.array(2.0, np.float32), "eps": np.array(1e-5, np.float32),
+            "sc": np.array(0.25, np.float32), "sz": np.array([1, 16, 20, 28], np.int64),
+            "roi": np.zeros(0, np.float32), "noscale": np.zeros(0, np.float32),
+            "shp3": np.array([0, 16, -1], np.int64), "pr": np.full(16, 0.2, np.float32),
+            "lo": np.array(-1.0, np.float32), "hi": np.array(2.0, np.float32)}
+    nodes = [N("Conv", ["x", "w0", "b0"], ["c0"], attrs={"kernel_shape": [3, 3], "pads": [0, 0, 1, 1],
+                                                          "strides": [2, 2]}),
+             N("Relu", ["c0"], ["r0"]),
+             N("Conv", ["r0", "wg", "bg"], ["cg"], attrs={"kernel_shape": [3, 3], "pads": [1, 1, 1, 1], "group": 2}),
+             N("ConvTranspose", ["cg", "wt", "bt"], ["ct"], attrs={"kernel_shape": [2, 2], "strides": [2, 2]}),
+             N("BatchNormalization", ["ct"] + _bn(init, "bnt", 16), ["btn"]),
+             N("Relu", ["btn"], ["rt"]),
+             N("Resize", ["rt", "roi", "noscale", "sz"], ["rs"], attrs={"mode": "linear",
+                                                                       "coordinate_transformation_mode": "half_pixel"}),
+             N("Reshape", ["rs", "shp3"], ["seq0"]),                  # [1, 16, 560]
+             N("Transpose", ["seq0"], ["seq"], attrs={"perm": [0, 2, 1]}),   # [1, 560, 16]
+             # decomposed LayerNorm
+             N("ReduceMean", ["seq"], ["m"], attrs={"axes": [-1], "keepdims": 1}),
+             N("Sub", ["seq", "m"], ["d"]),
+             N("Pow", ["d", "two"], ["d2"]),
+             N("ReduceMean", ["d2"], ["v"], attrs={"axes": [-1], "keepdims": 1}),
+             N("Add", ["v", "eps"], ["ve"]),
+             N("Sqrt", ["ve"], ["sd"]),
+             N("Div", ["d", "sd"], ["nn"]),
+             N("Mul", ["nn", "g1"], ["ng"]),
+             N("Add", ["ng", "be1"], ["ln1"]),
+             # attention
+             N("MatMul", ["ln1", "wq"], ["q"]), N("MatMul", ["ln1", "wk"], ["k"]), N("MatMul", ["ln1", "wv"], ["vv"]),
+             N("Transpose", ["k"], ["kt"], attrs={"perm": [0, 2, 1]}),
+             N("MatMul", ["q", "kt"], ["qk"]),
+             N("Mul", ["qk", "sc"], ["qks"]),
+             N("Softmax", ["qks"], ["att"], attrs={"axis": -1}),
+             N("MatMul", ["att", "vv"], ["ctx"]),
+             N("Add", ["ctx", "ln1"], ["res"]),
+             N("LayerNormalization", ["res", "g2", "be2"], ["ln2"], attrs={"axis": -1, "epsilon": 1e-5}),
+             N("PRelu", ["ln2", "pr"], ["p"]),
+             N("Clip", ["p", "lo", "hi"], ["cl"]),
+             N("Tanh", ["cl"], ["th"]),
+             N("HardSigmoid", ["th"], ["y"], attrs={"alpha": 0.2, "beta": 0.5})]
+    return ox.Graph(nodes, init, ["x"], ["y", "ct"]), init
+
+
+def test_ocrnet_graph_matches_torch():
+    g, i = ocrnet_graph()
+    x = torch.randn(1, 3, 20, 28)
+    y, ct = OnnxGraph(ox.write_model(g)).run({"x": x})
+    t = {k: torch.from_numpy(v) for k, v in i.items()}
+    c0 = F.relu(F.conv2d(F.pad(x, (0, 1, 0, 1)), t["w0"], t["b0"], stride=2))
+    cg = F.conv2d(c0, t["wg"], t["bg"], padding=1, groups=2)
+    ct_ref = F.conv_transpose2d(cg, t["wt"], t["bt"], stride=2)
+    torch.testing.assert_close(ct, ct_ref, rtol=1e-4, atol=1e-4)
+    bt = F.relu(F.batch_norm(ct_ref, t["bnt_m"], t["bnt_v"], t["bnt_s"], t["bnt_b"], False, 0.0, 1e-5))
+    rs = F.interpolate(bt, size=(20, 28), mode="bilinear", align_corners=False)
+    seq = rs.reshape(1, 16, -1).transpose(1, 2)
+    ln1 = F.layer_norm(seq, (16,), t["g1"], t["be1"], 1e-5)
+    q, k, v = ln1 @ t["wq"], ln1 @ t["wk"], ln1 @ t["wv"]
+    ctx = torch.softmax(q @ k.transpose(1, 2) * 0.25, -1) @ v
+    ln2 = F.layer_norm(ctx + ln1, (16,), t["g2"], t["be2"], 1e-5)
+    p = torch.where(ln2 > 0, ln2, ln2 * 0.2)
+    ref = torch.clamp(torch.tanh(torch.clamp(p, -1, 2)) * 0.2 + 0.5, 0, 1)
+    torch.testing.assert_close(y, ref, rtol=1e-4, atol=1e-4)
