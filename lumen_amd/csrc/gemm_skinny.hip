@@ -4,8 +4,9 @@
 // the kernel is shaped for bandwidth, not reuse:
 //   * a workgroup owns one 16-column N tile and a K range; its 4 waves take
 //     interleaved 32-wide k-steps of that range (split-K inside the workgroup,
-//     reduced through LDS), and grid.y splits K further across workgroups so that
-//     even N = 896 launches ~1000 workgroups (each K-split writes its fp32 partial
+//     reduced through LDS), and grid.y splits K across workgroups only when the N
+//     tiles alone leave CUs idle (skinny_ksplit: N >= 4096 runs unsplit, narrow N such
+//     as 896 splits up to ~1024 workgroups; each K-split writes its fp32 partial
 //     slab; the last split of a tile to arrive — per-tile atomic counter — sums the
 //     slabs in split order — deterministic, so hipGraph replays and eager launches
 //     give bitwise-identical logits — and applies the epilogue, with no second
@@ -110,14 +111,23 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const uint16_t* __rest
   }
 }
 
-// workgroups across K so that the grid reaches ~target workgroups; each keeps >= 512 of K
+// K split per shape: when the 16-column N tiles already cover every CU (ntiles >= 256,
+// all four Llama-3-8B decode GEMMs) the split only adds slab traffic and is skipped;
+// narrower N (FastVLM-0.5B: 896 / 1152 wide) splits K until the grid reaches ~target
+// workgroups, each keeping >= 512 of K.  LUMEN_SKINNY_TARGET_WG overrides the target.
 int skinny_ksplit(int N, int K) {
   const int ntiles = (N + 15) / 16;
-  static const int target = [] {   // LUMEN_SKINNY_TARGET_WG: workgroups the K split aims for
+  static const int target = [] {
     const char* e = getenv("LUMEN_SKINNY_TARGET_WG");
     const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 256;   // swept 256..2048 on the Llama-3-8B decode shapes: 256 fastest (profiles/r1_ksplit_sweep_v1.jsonl)
+    return v > 0 ? v : 1024;
   }();
+  static const int full = [] {   // tile count that already fills the chip without a split
+    const char* e = getenv("LUMEN_SKINNY_FULL_TILES");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 256;
+  }();
+  if (ntiles >= full) return 1;
   int ks = (target + ntiles - 1) / ntiles;
   const int kmax = K / 512 > 1 ? K / 512 : 1;
   ks = ks < kmax ? ks : kmax;

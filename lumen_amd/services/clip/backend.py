@@ -31,21 +31,44 @@ from ...models.clip import CLIPModel
 from ...runtime.batcher import DynamicBatcher
 from ...runtime.metrics import stage
 from ...utils.image import decode_many
+from ...resources.exceptions import ResourceError
 from .resources import ModelResources, load_weights
 
 log = logging.getLogger("lumen.clip.backend")
 
 
+# exception hierarchy of the reference (packages/lumen-clip/src/lumen_clip/backends/backend_exceptions.py:7-59)
 class BackendError(Exception):
-    pass
+    """Base class for all backend errors."""
 
 
 class BackendNotInitializedError(BackendError):
-    pass
+    """Backend used before initialize()."""
 
 
 class InvalidInputError(BackendError):
-    pass
+    """Input data invalid or malformed."""
+
+
+class InferenceError(BackendError):
+    """A forward pass failed (HIP launch error, OOM, ...)."""
+
+
+class ModelLoadingError(BackendError):
+    """Weights / tokenizer / config could not be loaded."""
+
+
+class DeviceUnavailableError(BackendError):
+    """The requested device does not exist on this host."""
+
+
+class BackendDependencyError(BackendError):
+    """A runtime kind whose optional dependencies are not part of this build."""
+
+    def __init__(self, runtime: str) -> None:
+        super().__init__(f"Backend '{runtime}' is not available in the MI355X build "
+                         f"(supported runtimes: onnx, torch — both served by the native HIP engine)")
+        self.runtime = runtime
 
 
 @dataclass
@@ -67,7 +90,10 @@ def pick_device(pref: Optional[str]) -> torch.device:
         return torch.device("cpu")
     if torch.cuda.is_available():
         if pref and pref.startswith("cuda"):
-            return torch.device(pref)
+            d = torch.device(pref)
+            if d.index is not None and d.index >= torch.cuda.device_count():
+                raise DeviceUnavailableError(f"{pref} requested but only {torch.cuda.device_count()} GPU(s) visible")
+            return d
         return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1))
     return torch.device("cpu")
 
@@ -119,8 +145,12 @@ class MI355XClipBackend:
             sd = load_weights(r.model_root_path, self.precision)
             self._logit_scale = float(sd["logit_scale"]) if "logit_scale" in sd else cfg.logit_scale
         else:
-            m = CLIPModel(cfg, dtype=dtype, device="cpu")
-            m.load_state_dict_any(load_weights(self.resources.model_root_path, self.precision))
+            try:
+                m = CLIPModel(cfg, dtype=dtype, device="cpu")
+                m.load_state_dict_any(load_weights(self.resources.model_root_path, self.precision))
+            except (OSError, KeyError, ValueError, RuntimeError, ResourceError) as e:
+                raise ModelLoadingError(f"loading {self.resources.model_name} from "
+                                        f"{self.resources.model_root_path}: {e}") from e
             self.model = m.to(self.device)
             self._logit_scale = self.model.logit_scale
         self._load_tokenizer()
@@ -144,7 +174,7 @@ class MI355XClipBackend:
     def _load_tokenizer(self) -> None:
         p = self.resources.tokenizer_path
         if p is None:
-            raise BackendError(f"tokenizer.json missing in {self.resources.model_root_path}")
+            raise ModelLoadingError(f"tokenizer.json missing in {self.resources.model_root_path}")
         from tokenizers import Tokenizer
 
         tok = Tokenizer.from_file(str(p))
@@ -285,7 +315,7 @@ def create_backend(backend_settings, resources: ModelResources, runtime: Optiona
     if rt not in ("onnx", "torch", "rknn"):
         raise ValueError(f"unsupported runtime '{rt}' (expected onnx|torch|rknn)")
     if rt == "rknn":
-        raise ImportError("RKNN runtime is not available on MI355X builds")
+        raise BackendDependencyError("rknn")
     from ...resources.config import AmdRuntimeSettings
 
     from ...runtime import placement

@@ -157,3 +157,30 @@ def test_concurrent_streams_batched(hub):
     assert len(out) == 8
     b = svc.backend._img_batcher
     assert b.items >= 8
+
+
+def test_clip_backend_exception_hierarchy(tmp_path):
+    """Reference backends/backend_exceptions.py:7-59: every error derives from BackendError;
+    rknn -> BackendDependencyError, missing weights -> ModelLoadingError."""
+    import pytest
+
+    from lumen_amd.resources.config import ModelConfig, Runtime
+    from lumen_amd.resources.synthetic import write_clip_model
+    from lumen_amd.services.clip import backend as cb
+    from lumen_amd.services.clip.resources import ResourceLoader
+
+    for cls in (cb.BackendNotInitializedError, cb.InvalidInputError, cb.InferenceError, cb.ModelLoadingError,
+                cb.DeviceUnavailableError, cb.BackendDependencyError):
+        assert issubclass(cls, cb.BackendError)
+    write_clip_model(tmp_path / "models" / "clip-tiny", "clip-tiny", preset="tiny")
+    res = ResourceLoader.load_model_resources(tmp_path, ModelConfig(model="clip-tiny", runtime=Runtime.torch))
+    settings = type("S", (), {"device": "cpu", "batch_size": 4})()
+    with pytest.raises(cb.BackendDependencyError):
+        cb.create_backend(settings, res, "rknn")
+    b = cb.create_backend(settings, res, "torch")
+    with pytest.raises(cb.BackendNotInitializedError):
+        b._ensure()
+    for f in (tmp_path / "models" / "clip-tiny").rglob("*.safetensors"):
+        f.unlink()
+    with pytest.raises(cb.ModelLoadingError):
+        b.initialize()

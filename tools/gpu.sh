@@ -9,7 +9,7 @@
 #   prof_bench     rocprofv3 kernel stats of the headline bench (3 steps)
 #   gemm           tools/gemm_bench_tiles.py on the ViT-L/14 shapes ($GEMM_TILES, $GEMM_EPI)
 #   vlm8b / vlm05  tools/vlm_bench.py Llama-3-8B fp8 / FastVLM-0.5B
-#   prof_vlm8b     rocprofv3 kernel stats of the 8B fp8 decode bench
+#   prof_vlm8b     rocprofv3 kernel stats of the 8B fp8 decode bench (batch 16; prof_vlm8b_b1: single stream)
 #   face_ocr       tools/face_ocr_bench.py face + ocr
 #   prof_face / prof_ocr   rocprofv3 kernel stats of the face / OCR bench
 #   f8             fp8 tests (tests/test_fp8_gpu.py) + tools/f8_gemm_bench.py ($F8_SHAPES, $F8_M)
@@ -49,6 +49,9 @@ for task in "$@"; do
     prof_vlm8b)
       step prof_vlm8b 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_vlm8b -o run -- \
         python3 tools/vlm_bench.py --preset llava-llama3-8b --n 3 --warmup 1 --max-new 32 --batch 16 --fp8 ;;
+    prof_vlm8b_b1)
+      step prof_vlm8b_b1 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_vlm8b_b1 -o run -- \
+        python3 tools/vlm_bench.py --preset llava-llama3-8b --n 3 --warmup 1 --max-new 64 --batch 1 --fp8 ;;
     face_ocr)
       step face 400 python tools/face_ocr_bench.py --what face
       step ocr 400 python tools/face_ocr_bench.py --what ocr ;;
