@@ -204,13 +204,10 @@ _BLAS_RESID = os.environ.get("LUMEN_BLAS_RESID", "0") != "0"
 _BLAS_RESID_MIN_ROWS = int(os.environ.get("LUMEN_BLAS_RESID_MIN_ROWS", "8192"))
 
 
-def _bias_gemm(a: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: torch.Tensor) -> None:
-    ops.linear(a, w, b, out=out)
-
-
-def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float,
-               causal: bool = False, kv_len: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Run pre-LN blocks over the flat residual stream x [B*S, W] (updated in place)."""
+def _block_steps(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float,
+                 causal: bool = False, kv_len: Optional[torch.Tensor] = None, tile: int = -1):
+    """Pre-LN blocks over the flat residual stream x [B*S, W] (updated in place), one
+    ``yield`` per block so several micro-batches can be issued layer-interleaved."""
     T, W = x.shape
     D = W // heads
     h = torch.empty_like(x)
@@ -221,25 +218,80 @@ def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, ep
     for i, blk in enumerate(blocks):
         if i == 0 or not fuse:
             ops.layer_norm(x, blk.ln1_w, blk.ln1_b, eps, out=h)
-        qkv = ops.linear(h, blk.qkv_w, blk.qkv_b)
+        qkv = ops.linear(h, blk.qkv_w, blk.qkv_b, tile=tile)
         q5 = qkv.view(B, S, 3, heads, D)
         ops.attention(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], causal=causal, kv_len=kv_len,
                       out=o.view(B, S, heads, D))
         del qkv, q5
         if fuse:
-            _bias_gemm(o, blk.out_w, blk.out_b, y)
+            ops.linear(o, blk.out_w, blk.out_b, out=y, tile=tile)
             ops.layer_norm(y, blk.ln2_w, blk.ln2_b, eps, add=x, resid_out=x, out=h)
         else:
-            ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x)
+            ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x, tile=tile)
             ops.layer_norm(x, blk.ln2_w, blk.ln2_b, eps, out=h)
-        f = ops.linear(h, blk.fc1_w, blk.fc1_b, act=act)
+        f = ops.linear(h, blk.fc1_w, blk.fc1_b, act=act, tile=tile)
         if fuse and i + 1 < len(blocks):
             nb = blocks[i + 1]
-            _bias_gemm(f, blk.fc2_w, blk.fc2_b, y)
+            ops.linear(f, blk.fc2_w, blk.fc2_b, out=y, tile=tile)
             ops.layer_norm(y, nb.ln1_w, nb.ln1_b, eps, add=x, resid_out=x, out=h)
         else:
-            ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x)
+            ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x, tile=tile)
         del f
+        yield i
+
+
+def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float,
+               causal: bool = False, kv_len: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Run pre-LN blocks over the flat residual stream x [B*S, W] (updated in place)."""
+    for _ in _block_steps(x, blocks, B, S, heads, act, eps, causal, kv_len):
+        pass
+    return x
+
+
+# Micro-batched tower (large image batches on the GPU): the batch is cut into LUMEN_VIT_MICRO
+# row ranges, each issued on its own HIP stream, layer-interleaved.  A 256x256-tile GEMM over
+# M = B*257 rows ends on a nearly empty round of tiles (ViT-L/14 b512: 514 row tiles); with two
+# streams the other micro-batch's kernels fill those CUs, so the GEMMs run without the split-K
+# tail pass (tile code 1609: ping-pong 256x256, non-persistent, no tail split) and attention /
+# LayerNorm of one half overlap GEMM tails of the other.
+_VIT_MICRO = int(os.environ.get("LUMEN_VIT_MICRO", "2"))
+_VIT_MICRO_MIN_ROWS = 65536          # per micro-batch: every GEMM stays >= 512 tiles of 256x256
+_MICRO_STREAMS: dict = {}
+
+
+def _micro_streams(dev: torch.device, n: int):
+    key = (dev.index, n)
+    if key not in _MICRO_STREAMS:
+        _MICRO_STREAMS[key] = [torch.cuda.Stream(device=dev) for _ in range(n)]
+    return _MICRO_STREAMS[key]
+
+
+def run_blocks_micro(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float) -> torch.Tensor:
+    """run_blocks over micro-batches on separate streams (falls back to run_blocks when the
+    batch is too small to split or x is on the CPU)."""
+    n = _VIT_MICRO
+    if not x.is_cuda or n <= 1 or B < n or (B // n) * S < _VIT_MICRO_MIN_ROWS:
+        return run_blocks(x, blocks, B, S, heads, act, eps)
+    cur = torch.cuda.current_stream(x.device)
+    streams = _micro_streams(x.device, n)
+    bounds = [B * i // n for i in range(n + 1)]
+    gens = []
+    for i, st in enumerate(streams):
+        st.wait_stream(cur)
+        b0, b1 = bounds[i], bounds[i + 1]
+        with torch.cuda.stream(st):
+            gens.append(_block_steps(x[b0 * S:b1 * S], blocks, b1 - b0, S, heads, act, eps, tile=1609))
+    live = list(zip(gens, streams))
+    while live:
+        nxt = []
+        for g, st in live:
+            with torch.cuda.stream(st):
+                if next(g, None) is not None:
+                    nxt.append((g, st))
+        live = nxt
+    for st in streams:
+        cur.wait_stream(st)
+    x.record_stream(streams[0])
     return x
 
 
@@ -290,7 +342,7 @@ class VisionTower(nn.Module):
                    out_group=P, out_group_stride=S, out_row_offset=1)
         ops.cls_fill(x, self.class_emb, self.pos_emb, S)
         ops.layer_norm(x, self.ln_pre_w, self.ln_pre_b, cfg.ln_eps, out=x)
-        run_blocks(x, self.blocks, B, S, cfg.heads, cfg.act, cfg.ln_eps)
+        run_blocks_micro(x, self.blocks, B, S, cfg.heads, cfg.act, cfg.ln_eps)
         cls_rows = torch.arange(B, device=dev, dtype=torch.long) * S
         pooled = ops.layer_norm(x, self.ln_post_w, self.ln_post_b, cfg.ln_eps, row_idx=cls_rows)
         emb = ops.linear(pooled, self.proj_w, out_dtype=torch.float32)

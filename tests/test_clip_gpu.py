@@ -75,3 +75,23 @@ def test_blas_residual_ln_fusion_matches(monkeypatch):
     for a, b, r in ((e0, e1, e_ref), (t0, t1, t_ref)):
         assert (a * b).sum(-1).min().item() > 0.999
         assert (b * r).sum(-1).min().item() > 0.995
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_vit_micro_batch_streams_match(monkeypatch, n):
+    """Micro-batched image tower (row ranges on separate HIP streams, layer-interleaved,
+    GEMMs without the tail split) vs the single-stream tower and the CPU fp32 reference."""
+    import lumen_amd.models.clip as clip_mod
+
+    m_cpu = CLIPModel.random("ViT-B-32", seed=5, dtype=torch.float32)
+    m_gpu = CLIPModel.random("ViT-B-32", seed=5, dtype=torch.bfloat16, device="cuda")
+    imgs = torch.randint(0, 256, (37, 224, 224, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(3))
+    e_ref = m_cpu.encode_image_uint8(imgs[:8])
+    monkeypatch.setattr(clip_mod, "_VIT_MICRO", 1)
+    e1 = m_gpu.encode_image_uint8(imgs.cuda()).cpu()
+    monkeypatch.setattr(clip_mod, "_VIT_MICRO", n)
+    monkeypatch.setattr(clip_mod, "_VIT_MICRO_MIN_ROWS", 0)
+    e2 = m_gpu.encode_image_uint8(imgs.cuda()).cpu()
+    torch.cuda.synchronize()
+    assert (e1 * e2).sum(-1).min().item() > 0.9995
+    assert (e2[:8] * e_ref).sum(-1).min().item() > 0.995
