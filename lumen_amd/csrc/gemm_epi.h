@@ -28,7 +28,44 @@ struct GemmEpi {
   int64_t* dbg;              // profiling only: per-workgroup s_memrealtime stamps (null in production)
   int64_t split_koff;        // split-K launches (gridDim.y = splits): A, W advance by y * split_koff
   int64_t split_cstride;     // elements; C (fp32 slabs) advances by y * split_cstride
+  // ---- decode (skinny) GEMMs only: RMSNorm folded into the projection.  gamma is folded
+  // into W at load time (LLM.fold_norms), so rms_norm(x) . W'^T = rstd(x) * (x . W'^T): the
+  // kernel runs on the raw residual-stream rows and scales row m of the accumulator by
+  // rstd[m] before the bias.  rstd comes from ssq_in -- per (row, 16-column tile) sums of
+  // squares of the stored bf16 rows that the producing GEMM's epilogue wrote to its
+  // ssq_out, [M][ssq_tiles], summed in a fixed order -- or, when null, from A itself.
+  int norm;
+  float norm_eps;
+  const float* ssq_in;
+  float* ssq_out;
+  int ssq_tiles;
 };
+
+// rstd of the M (<= 32) A rows of a norm-folded decode GEMM into LDS (wave w: rows w, w + NWV, ...);
+// the caller's next __syncthreads publishes it.  K = row length (the normalised width).
+template <int NWV>
+__device__ __forceinline__ void skinny_rstd(const uint16_t* __restrict__ A, int64_t lda, int M, int K,
+                                            const GemmEpi& ep, float* rstd) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int m = wid; m < M; m += NWV) {
+    float s = 0.f;
+    if (ep.ssq_in) {
+      const float* p = ep.ssq_in + (int64_t)m * ep.ssq_tiles;
+      for (int j = lane; j < ep.ssq_tiles; j += 64) s += p[j];
+    } else {
+      const uint16_t* r = A + (int64_t)m * lda;
+#pragma unroll 4
+      for (int c = lane * 8; c < K; c += 512) {
+        float f[8];
+        unpack8(*(const u32x4_t*)(r + c), f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += f[i] * f[i];
+      }
+    }
+    s = wave_sum(s);
+    if (lane == 0) rstd[m] = rsqrtf(s / (float)K + ep.norm_eps);
+  }
+}
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
@@ -308,6 +345,25 @@ __device__ __forceinline__ void epi_store16(float* v, int m, int n, int M, int N
 __device__ __forceinline__ void epi_store8(float* v, int m, int n, int M, int N, void* __restrict__ C, int64_t ldc,
                                            const GemmEpi& ep) {
   epi_store8_t<false>(v, m, n, M, N, C, ldc, ep, c_rsrc(C));
+}
+// decode GEMM epilogue: optional rstd row scale (norm folding, before the bias), the shared
+// epilogue, then the producer's per-tile sum of squares of the stored bf16 values (ssq_out)
+__device__ __forceinline__ void epi_store16_dec(float* v, float rs, int m, int n, int M, int N,
+                                                void* __restrict__ C, int64_t ldc, const GemmEpi& ep) {
+  if (ep.norm) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] *= rs;
+  }
+  epi_store16(v, m, n, M, N, C, ldc, ep);
+  if (ep.ssq_out && m < M && n < N) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float f = bf2f(f2bf(v[q]));
+      s += n + q < N ? f * f : 0.f;
+    }
+    ep.ssq_out[(int64_t)m * ep.ssq_tiles + (n >> 4)] = s;
+  }
 }
 
 // In-launch split-K reduction of the skinny decode GEMMs (the counter form of the

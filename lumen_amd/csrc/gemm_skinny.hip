@@ -33,6 +33,7 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const uint16_t* __rest
                                                           uint32_t* __restrict__ cnt, int M, int N, int K, int kchunk,
                                                           GemmEpi ep) {
   __shared__ float red[4][MT * 16][17];
+  __shared__ float rstd_s[MT * 16];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 15, g = lane >> 4;
@@ -89,6 +90,7 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const uint16_t* __rest
   for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wid][t * 16 + 4 * g + r][col] = acc[t][r];
+  if (ep.norm) skinny_rstd<4>(A, lda, M, K, ep, rstd_s);
   __syncthreads();
   if (ws != nullptr) {   // K split over grid.y: the last split to arrive reduces + runs the epilogue
     if (!splitk_reduce_last(red, ws, cnt, M, N, n0)) return;
@@ -96,7 +98,7 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const uint16_t* __rest
       float v[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) v[c] = red[1][tid][c];
-      epi_store16(v, tid, n0, M, N, C, ldc, ep);
+      epi_store16_dec(v, rstd_s[tid], tid, n0, M, N, C, ldc, ep);
     }
     return;
   }
@@ -106,7 +108,7 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const uint16_t* __rest
       float v[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) v[c] = red[0][m][c] + red[1][m][c] + red[2][m][c] + red[3][m][c];
-      epi_store16(v, m, n0, M, N, C, ldc, ep);
+      epi_store16_dec(v, rstd_s[m], m, n0, M, N, C, ldc, ep);
     }
   }
 }

@@ -56,6 +56,7 @@ __global__ void __launch_bounds__(64 * NWV) gemm_skinny_w8_kernel(const uint16_t
                                                              int64_t ldc, float* __restrict__ ws, uint32_t* __restrict__ cnt, int M, int N, int K,
                                                              int kchunk, GemmEpi ep) {
   __shared__ float red[NWV][MT * 16][17];
+  __shared__ float rstd_s[MT * 16];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 15, g = lane >> 4;
@@ -121,6 +122,7 @@ __global__ void __launch_bounds__(64 * NWV) gemm_skinny_w8_kernel(const uint16_t
   for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wid][t * 16 + 4 * g + r][col] = acc[t][r];
+  if (ep.norm) skinny_rstd<NWV>(A, lda, M, K, ep, rstd_s);
   __syncthreads();
   if (ws != nullptr) {   // K split over grid.y: the last split to arrive reduces + runs the epilogue
     if (!splitk_reduce_last(red, ws, cnt, M, N, n0)) return;
@@ -130,7 +132,7 @@ __global__ void __launch_bounds__(64 * NWV) gemm_skinny_w8_kernel(const uint16_t
       for (int c = 0; c < 16; ++c) v[c] = red[1][tid][c];
 #pragma unroll
       for (int c = 0; c < 16; ++c) v[c] *= n0 + c < N ? scale[n0 + c] : 0.f;
-      epi_store16(v, tid, n0, M, N, C, ldc, ep);
+      epi_store16_dec(v, rstd_s[tid], tid, n0, M, N, C, ldc, ep);
     }
     return;
   }
@@ -145,7 +147,7 @@ __global__ void __launch_bounds__(64 * NWV) gemm_skinny_w8_kernel(const uint16_t
         for (int w = 0; w < NWV; ++w) t += red[w][m][c];
         v[c] = t * (n0 + c < N ? scale[n0 + c] : 0.f);
       }
-      epi_store16(v, m, n0, M, N, C, ldc, ep);
+      epi_store16_dec(v, rstd_s[m], m, n0, M, N, C, ldc, ep);
     }
   }
 }

@@ -218,6 +218,78 @@ void gemm_w8(const at::Tensor& a, const at::Tensor& w8, const at::Tensor& scale,
                                  ks > 1 ? ws.data_ptr<float>() : nullptr, cnt, ks, cur_stream()));
 }
 
+// ---------------------------------------------------------------- decode GEMM (norm folding)
+// out = epi(rstd(a) * (a @ w^T) [* scale]) for M <= 32 rows on the skinny decode kernels.
+// norm = 1: rows are scaled by rstd = rsqrt(mean(a^2) + eps) before the bias (RMSNorm with
+// its gamma folded into w, see LLM.fold_norms), rstd from ssq_in [M, tiles] (sums of squares
+// the producing GEMM wrote) or from a itself.  ssq_out [M, N/16]: this GEMM's epilogue writes
+// the per-16-column sums of squares of its stored bf16 rows (the residual stream), for the
+// next norm-folded GEMM.  w bf16 [N, K], or float8_e4m3fn with fp32 per-row scale.
+void gemm_dec(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tensor>& scale,
+              const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& residual, at::Tensor out,
+              int64_t glu, int64_t norm, double eps, const c10::optional<at::Tensor>& ssq_in,
+              const c10::optional<at::Tensor>& ssq_out) {
+  check_bf16_rows(a, "a");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(M > 0 && M <= 32, "gemm_dec: decode rows only (1..32)");
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K && w.stride(1) == 1 && N % 16 == 0, "gemm_dec: w [N, K], N % 16 == 0");
+  check_gpu(out, "out");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(0) >= M && out.size(1) >= (glu ? N / 2 : N),
+              "gemm_dec: out");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || (out.scalar_type() == at::kFloat && !glu), "gemm_dec: out dtype");
+  lumen::GemmEpi ep{};
+  ep.alpha = 1.f;
+  ep.glu = (int)glu;
+  ep.out_f32 = out.scalar_type() == at::kFloat;
+  ep.norm = (int)norm;
+  ep.norm_eps = (float)eps;
+  if (norm && ssq_in.has_value() && ssq_in->defined()) {
+    TORCH_CHECK(ssq_in->is_cuda() && ssq_in->scalar_type() == at::kFloat && ssq_in->dim() == 2 &&
+                ssq_in->size(0) >= M && ssq_in->is_contiguous(), "gemm_dec: ssq_in f32 [>= M, tiles]");
+    TORCH_CHECK(ssq_in->size(1) * 16 == K, "gemm_dec: ssq_in tiles * 16 must equal K");
+    ep.ssq_in = ssq_in->data_ptr<float>();
+    ep.ssq_tiles = (int)ssq_in->size(1);
+  }
+  if (ssq_out.has_value() && ssq_out->defined()) {
+    TORCH_CHECK(!norm || !ep.ssq_in, "gemm_dec: ssq_in and ssq_out share the tile count field");
+    TORCH_CHECK(!glu && out.scalar_type() == at::kBFloat16, "gemm_dec: ssq_out needs a bf16 non-GLU output");
+    TORCH_CHECK(ssq_out->is_cuda() && ssq_out->scalar_type() == at::kFloat && ssq_out->dim() == 2 &&
+                ssq_out->size(0) >= M && ssq_out->size(1) * 16 == N && ssq_out->is_contiguous(),
+                "gemm_dec: ssq_out f32 [>= M, N / 16]");
+    ep.ssq_out = ssq_out->data_ptr<float>();
+    ep.ssq_tiles = (int)ssq_out->size(1);
+  }
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->numel() >= N && bias->is_contiguous() &&
+                (bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16), "gemm_dec: bias");
+    ep.bias = bias->data_ptr();
+    ep.bias_f32 = bias->scalar_type() == at::kFloat;
+  }
+  if (residual.has_value() && residual->defined()) {
+    check_bf16_rows(*residual, "residual");
+    ep.residual = bf(*residual);
+    ep.ldr = residual->stride(0);
+  }
+  const at::DeviceGuard guard(a.device());
+  const int ks = lumen::skinny_ksplit((int)N, (int)K);
+  at::Tensor ws;
+  if (ks > 1) ws = at::empty({ks, M, N}, a.options().dtype(at::kFloat));
+  uint32_t* cnt = ks > 1 ? splitk_counters(a, (N + 15) / 16) : nullptr;
+  float* wsp = ks > 1 ? ws.data_ptr<float>() : nullptr;
+  if (w.scalar_type() == at::kFloat8_e4m3fn) {
+    TORCH_CHECK(scale.has_value() && scale->defined() && scale->scalar_type() == at::kFloat && scale->numel() == N,
+                "gemm_dec: fp8 weights need scale f32 [N]");
+    TORCH_CHECK(K % 64 == 0 && w.stride(0) % 16 == 0, "gemm_dec: fp8 K % 64");
+    LUMEN_CHECK_HIP(lumen::gemm_w8(bf(a), a.stride(0), reinterpret_cast<const uint8_t*>(w.data_ptr()), w.stride(0),
+                                   scale->data_ptr<float>(), out.data_ptr(), out.stride(0), (int)M, (int)N, (int)K, ep,
+                                   wsp, cnt, ks, cur_stream()));
+  } else {
+    TORCH_CHECK(w.scalar_type() == at::kBFloat16 && K % 32 == 0, "gemm_dec: bf16 weights, K % 32");
+    LUMEN_CHECK_HIP(lumen::gemm_skinny(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0), (int)M,
+                                       (int)N, (int)K, ep, wsp, cnt, ks, cur_stream()));
+  }
+}
+
 // ---------------------------------------------------------------- fp8 x fp8 (W8A8) GEMM
 // out = epi((a8 @ w8^T) * sa[m] * sw[n]): fp32 bias | SwiGLU -> + residual; a8 [M, K] and
 // w8 [N, K] float8_e4m3fn, sa [M] / sw [N] fp32 (per-token / per-channel scales).
@@ -631,6 +703,8 @@ TORCH_LIBRARY(lumen, m) {
   m.def("gemm_probe(Tensor a, Tensor w, Tensor(o!) out, Tensor(d!) dbg, int tile) -> ()");
   m.def("gemm_w8(Tensor a, Tensor w8, Tensor scale, Tensor? bias, Tensor? residual, int act, Tensor(o!) out, "
         "int glu) -> ()");
+  m.def("gemm_dec(Tensor a, Tensor w, Tensor? scale, Tensor? bias, Tensor? residual, Tensor(o!) out, int glu, "
+        "int norm, float eps, Tensor? ssq_in, Tensor(s!)? ssq_out) -> ()");
   m.def("gemm_f8(Tensor a8, Tensor sa, Tensor w8, Tensor sw, Tensor? bias, Tensor? residual, Tensor(o!) out, "
         "int glu) -> ()");
   m.def("quant_rows_fp8(Tensor x, Tensor(o!) out8, Tensor(s!) scale) -> ()");
@@ -663,6 +737,7 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("gemm_probe", &gemm_probe);
   m.impl("gemm_w8", &gemm_w8);
   m.impl("gemm_f8", &gemm_f8);
+  m.impl("gemm_dec", &gemm_dec);
   m.impl("quant_rows_fp8", &quant_rows_fp8);
   m.impl("rms_norm_quant_fp8", &rms_norm_quant_fp8);
   m.impl("cls_fill", &cls_fill);

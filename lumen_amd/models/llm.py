@@ -46,6 +46,9 @@ _PREFILL_BLAS_NAMES = ("qkv", "o", "gu", "down")
 _PREFILL_BLAS_GLU_MIN_K = int(os.environ.get("LUMEN_LLM_PREFILL_BLAS_GLU_MIN_K", "2048"))
 # W8A8 prefill from this many tokens up (decode batches stay on the weight-only skinny kernels)
 _F8_MIN_ROWS = int(os.environ.get("LUMEN_LLM_F8_MIN_ROWS", "33"))
+# GPU: RMSNorm gammas folded into qkv / gate|up / lm_head (LLM.fold_norms); decode norms become
+# rstd row scales in the skinny GEMM epilogues (ops.linear_dec)
+_FUSED_DECODE_NORM = os.environ.get("LUMEN_LLM_FUSED_NORM", "1") != "0"
 
 
 def _prefill_blas_ok(name: str, K: int) -> bool:
@@ -159,6 +162,8 @@ class LLM(nn.Module):
         self.H, self.Hkv = self.layers[0].H, self.layers[0].Hkv
         self.comm = None   # parallel.Communicator for the TP group (IPC one-shot all-reduce + RCCL); None = RCCL
         self.weight_dtype = "bf16"
+        self.norm_folded = False     # RMSNorm gammas folded into the consuming projections (fold_norms)
+        self._ssq = None             # decode: per-(row, 16-column tile) sums of squares of the residual stream
 
     # ------------------------------------------------------------------ weights
     @torch.no_grad()
@@ -172,6 +177,7 @@ class LLM(nn.Module):
         def rnd(p, std):
             p.copy_((torch.randn(p.shape, generator=g, device=dev, dtype=torch.float32) * std).to(p.dtype))
 
+        self.norm_folded = False
         rnd(self.embed, 0.02)
         if self.lm_head is not None:
             rnd(self.lm_head, 0.02)
@@ -196,6 +202,7 @@ class LLM(nn.Module):
             s = t.shape[0] // n
             return t[i * s:(i + 1) * s]
 
+        self.norm_folded = False
         self.embed.copy_(rows(get(prefix + "embed_tokens.weight"), w, r).to(self.embed.dtype))
         if self.lm_head is not None:
             self.lm_head.copy_(rows(get("lm_head.weight"), w, r).to(self.lm_head.dtype))
@@ -223,6 +230,51 @@ class LLM(nn.Module):
             l.down_w.copy_(dn[:, r * l.I:(r + 1) * l.I].to(l.down_w.dtype))
             l.ln1.copy_(get(p + "input_layernorm.weight").to(l.ln1.dtype))
             l.ln2.copy_(get(p + "post_attention_layernorm.weight").to(l.ln2.dtype))
+
+    @torch.no_grad()
+    def fold_norms(self) -> None:
+        """Fold every RMSNorm gamma into the projection that consumes it -- W' = W * gamma[k]
+        for qkv (ln1), gate|up (ln2) and an untied lm_head (final norm) -- and set the gammas
+        to 1.  rms_norm(x, g) . W^T = rstd(x) * (x . W'^T), so the decode GEMMs run on the raw
+        residual stream and apply rstd in their epilogue (ops.linear_dec): no norm launch and
+        no normalised copy of x per token.  fp8 weights are dequantised, folded and
+        requantised per row.  Weight loads reset the flag."""
+        if self.norm_folded:
+            return
+
+        def fold(obj, wname, gamma):
+            w = getattr(obj, wname)
+            sc = getattr(obj, wname[:-2] + "_s" if wname.endswith("_w") else wname + "_s", None)
+            g = gamma.float()[None, :]
+            for r0 in range(0, w.shape[0], 8192):            # bounded fp32 temporaries
+                blk = w[r0:r0 + 8192].float()
+                if w.dtype == torch.float8_e4m3fn:
+                    blk = blk * sc[r0:r0 + 8192].float()[:, None] * g
+                    w8, s8 = ops.quantize_fp8_rows(blk)
+                    w[r0:r0 + 8192].copy_(w8)
+                    sc[r0:r0 + 8192].copy_(s8)
+                else:
+                    w[r0:r0 + 8192].copy_((blk * g).to(w.dtype))
+
+        for l in self.layers:
+            fold(l, "qkv_w", l.ln1)
+            l.ln1.fill_(1)
+            fold(l, "gu_w", l.ln2)
+            l.ln2.fill_(1)
+        if self.lm_head is not None:
+            fold(self, "lm_head", self.norm)
+            self.norm.fill_(1)
+        self.norm_folded = True
+
+    def _ssq_buf(self, dev) -> torch.Tensor:
+        if self._ssq is None or self._ssq.device != dev:
+            self._ssq = torch.zeros((32, self.cfg.hidden_size // 16), device=dev, dtype=torch.float32)
+        return self._ssq
+
+    def _maybe_fold(self, x: torch.Tensor) -> None:
+        if x.is_cuda and _FUSED_DECODE_NORM and not self.norm_folded:
+            self.fold_norms()
+            self._ssq_buf(x.device)
 
     @torch.no_grad()
     def quantize_fp8(self, lm_head: bool = True) -> None:
@@ -299,6 +351,11 @@ class LLM(nn.Module):
         T = x.shape[0]
         h = torch.empty_like(x)
         tp = self.tp.enabled
+        # decode rows with folded norms: every RMSNorm is an rstd row scale in the epilogue of the
+        # skinny GEMM that consumes it, fed by the sums of squares the producing GEMM's epilogue
+        # wrote (TP keeps the norm kernel: it also adds the all-reduced row-parallel partial)
+        if x.is_cuda and T <= 32 and not tp and self.norm_folded:
+            return self._layers_dec(x, pos, slots, kv, attn_fn)
         pending: Optional[torch.Tensor] = None   # TP: row-parallel partial to add before the next norm
         for i, l in enumerate(self.layers):
             if pending is None:
@@ -323,6 +380,25 @@ class LLM(nn.Module):
             del qkv, att, g
         if pending is not None:
             x.add_(self._all_reduce(pending))
+        return x
+
+    def _layers_dec(self, x, pos, slots, kv, attn_fn):
+        """Decode layer stack (<= 32 rows, norms folded): 4 GEMM launches per layer and no norm
+        kernel -- o / down write the residual stream plus its per-tile sums of squares
+        (``ssq``), qkv / gate|up scale their rows by the rstd those give (ops.linear_dec)."""
+        D, eps = self.cfg.head_dim, self.cfg.rms_eps
+        ssq = self._ssq_buf(x.device)
+        for i, l in enumerate(self.layers):
+            # layer 0 reads the embeddings (no producer GEMM): rstd from x itself
+            qkv = ops.linear_dec(x, l.qkv_w, getattr(l, "qkv_s", None), bias=l.qkv_b, norm_eps=eps,
+                                 ssq_in=ssq if i > 0 else None)
+            kc, vc = (kv.k[i], kv.v[i]) if kv is not None else (None, None)
+            lops.rope_kv(qkv, pos, self.cos_sin, l.H, l.Hkv, D, slots, kc, vc)
+            att = attn_fn(qkv, l, kc, vc)
+            ops.linear_dec(att, l.o_w, getattr(l, "o_s", None), residual=x, out=x, ssq_out=ssq)
+            g = ops.linear_dec(x, l.gu_w, getattr(l, "gu_s", None), glu=True, norm_eps=eps, ssq_in=ssq)
+            ops.linear_dec(g, l.down_w, getattr(l, "down_s", None), residual=x, out=x, ssq_out=ssq)
+            del qkv, att, g
         return x
 
     def _layers_f8(self, x, pos, slots, kv, attn_fn):
@@ -361,11 +437,16 @@ class LLM(nn.Module):
             x.add_(self._all_reduce(pending))
         return x
 
-    def logits(self, x_rows: torch.Tensor) -> torch.Tensor:
-        """final norm + lm_head of rows [B, hidden] -> local-vocab fp32 logits [B, V/tp]."""
-        h = ops.rms_norm(x_rows, self.norm, self.cfg.rms_eps)
+    def logits(self, x_rows: torch.Tensor, ssq: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """final norm + lm_head of rows [B, hidden] -> local-vocab fp32 logits [B, V/tp].
+        With folded norms (untied head, <= 32 rows) the norm is the lm_head GEMM's rstd row
+        scale; ``ssq``: the last down projection's sums of squares of these rows (decode)."""
         w = self.lm_head if self.lm_head is not None else self.embed
-        return ops.linear(h, w, out_dtype=torch.float32, w_scale=getattr(self, "lm_head_s", None))
+        ws = getattr(self, "lm_head_s", None)
+        if self.norm_folded and self.lm_head is not None and x_rows.is_cuda and x_rows.shape[0] <= 32:
+            return ops.linear_dec(x_rows, w, ws, norm_eps=self.cfg.rms_eps, ssq_in=ssq, out_dtype=torch.float32)
+        h = ops.rms_norm(x_rows, self.norm, self.cfg.rms_eps)
+        return ops.linear(h, w, out_dtype=torch.float32, w_scale=ws)
 
     # ------------------------------------------------------------------ forward passes
     @torch.no_grad()
@@ -378,6 +459,7 @@ class LLM(nn.Module):
         blocks covering [0, start_pos + T)) — the chunk's queries attend the cached prefix
         plus themselves (causal, last query aligned with the last key).  K/V of the prefix
         are gathered from the paged cache (K [blk, Hkv, 64, D]; V stored transposed)."""
+        self._maybe_fold(x)
         T = x.shape[0]
         pos = torch.arange(start_pos, start_pos + T, device=x.device, dtype=torch.int32)
         D = self.cfg.head_dim
@@ -404,10 +486,11 @@ class LLM(nn.Module):
                ctx_len: torch.Tensor, workspace: Optional[dict] = None) -> torch.Tensor:
         """B sequences, one new token each -> logits [B, V/tp] fp32."""
         x = self.embed_tokens(ids)
-        D = self.cfg.head_dim
+        self._maybe_fold(x)
 
         def attn(qkv, l, kc, vc):
             return lops.paged_decode(qkv, kc, vc, block_table, ctx_len, l.H, l.Hkv, workspace=workspace)
 
         self._layers(x, pos, slots, kv, attn)
-        return self.logits(x)
+        dec = self.norm_folded and x.is_cuda and x.shape[0] <= 32 and not self.tp.enabled
+        return self.logits(x, ssq=self._ssq if dec else None)

@@ -191,6 +191,37 @@ def rms_norm_quant_fp8(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-6, add:
     return quant_rows_fp8(y, out, scale)
 
 
+def linear_dec(x: torch.Tensor, w: torch.Tensor, w_scale: Optional[torch.Tensor] = None,
+               bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
+               out: Optional[torch.Tensor] = None, glu: bool = False, norm_eps: Optional[float] = None,
+               ssq_in: Optional[torch.Tensor] = None, ssq_out: Optional[torch.Tensor] = None,
+               out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """Decode projection (M <= 32 rows) on the skinny kernels with RMSNorm folding:
+
+    * ``norm_eps`` set: y = rstd(x) * (x @ w^T) (+bias ...), i.e. ``linear(rms_norm(x), w)``
+      for a ``w`` whose norm gamma is already folded in (``LLM.fold_norms``).  rstd comes
+      from ``ssq_in`` ([>= M, K / 16] per-tile sums of squares written by the GEMM that
+      produced x) or is computed from x.
+    * ``ssq_out`` ([>= M, N / 16] fp32): this GEMM (bf16 residual-stream output) writes the
+      per-16-column sums of squares of its stored rows for the next norm-folded GEMM.
+
+    CPU (and M > 32): plain ``rms_norm`` (unit gamma) + :func:`linear`; ``ssq_*`` unused."""
+    M, K = x.shape
+    N = w.shape[0]
+    NO = N // 2 if glu else N
+    if out is None:
+        out = torch.empty((M, NO), device=x.device, dtype=out_dtype or x.dtype)
+    if x.is_cuda and 0 < M <= 32:
+        if x.stride(-1) != 1 or x.stride(0) % 8 != 0:
+            x = x.contiguous()
+        hip_ops().gemm_dec(x, w, w_scale, bias, residual, out, int(bool(glu)), int(norm_eps is not None),
+                           float(norm_eps or 0.0), ssq_in if norm_eps is not None else None, ssq_out)
+        return out
+    if norm_eps is not None:
+        x = rms_norm(x, torch.ones(K, dtype=x.dtype, device=x.device), norm_eps)
+    return linear(x, w, bias=bias, residual=residual, out=out, glu=glu, w_scale=w_scale)
+
+
 def linear_f8(x8: torch.Tensor, x_scale: torch.Tensor, w8: torch.Tensor, w_scale: torch.Tensor,
               bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
               out: Optional[torch.Tensor] = None, glu: bool = False,

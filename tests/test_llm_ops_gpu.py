@@ -237,3 +237,51 @@ def test_llm_prefill_large_bias_fp32():
     got = gpu.prefill(gpu.embed_tokens(ids.to(DEV)))
     cos = torch.nn.functional.cosine_similarity(got.float().cpu().flatten(), ref.flatten(), dim=0).item()
     assert cos > 0.995, cos
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("M,N,K,glu", [(1, 6144, 4096, False), (5, 896 + 256, 896, False), (16, 2048, 4096, True),
+                                       (32, 1024, 4096, False), (3, 128256 // 8, 4096, False)])
+def test_linear_dec_norm_folding_matches_cpu(fp8, M, N, K, glu):
+    """Decode GEMM with the RMSNorm folded (gamma in W, rstd as an epilogue row scale) vs
+    rms_norm -> linear in fp32 on the CPU: rstd computed from x, and rstd from the sums of
+    squares a producing residual GEMM wrote (ssq_out -> ssq_in); split-K shapes included."""
+    g = torch.Generator().manual_seed(M * 7 + N)
+    x0 = (torch.randn(M, K, generator=g) * 3).bfloat16()
+    gamma = (1 + 0.3 * torch.randn(K, generator=g)).bfloat16()
+    wf = torch.randn(N, K, generator=g) * K ** -0.5
+    b = None if glu else torch.randn(N, generator=g) * 0.1
+    wfold = wf * gamma.float()[None, :]
+    if fp8:
+        w, s = ops.quantize_fp8_rows(wf)
+        wd, sd = ops.quantize_fp8_rows(wfold)
+    else:
+        w, s = wf.bfloat16(), None
+        wd, sd = wfold.bfloat16(), None
+    # producer: x = x0 + a @ Wp^T (residual GEMM) writing the per-tile sums of squares
+    a = torch.randn(M, 512, generator=g).bfloat16()
+    wp = (torch.randn(K, 512, generator=g) * 512 ** -0.5).bfloat16()
+    x_ref = ops.linear(a.float(), wp.float(), residual=x0.float()).bfloat16()
+    ssq = torch.zeros(32, K // 16, device=DEV)
+    x = x0.to(DEV).clone()
+    ops.linear_dec(a.to(DEV), wp.to(DEV), residual=x, out=x, ssq_out=ssq)
+    assert _rel(x, x_ref) < 1e-2
+    xr = x.cpu()
+    ref_ssq = (xr.float() ** 2).view(M, K // 16, 16).sum(-1)
+    torch.testing.assert_close(ssq[:M].cpu(), ref_ssq, rtol=1e-4, atol=1e-3)
+    one = torch.ones(K)
+    # same (folded, quantised) weights: the kernel's norm folding itself
+    ref = ops.linear(ops.rms_norm(xr.float(), one, 1e-5), wd, bias=b, glu=glu, w_scale=sd)
+    # unfolded fp32 model (bf16: folding costs one extra weight rounding; fp8: requantisation noise)
+    ref_unfold = ops.linear(ops.rms_norm(xr.float(), gamma.float(), 1e-5), w, bias=b, glu=glu, w_scale=s)
+    sdev = None if sd is None else sd.to(DEV)
+    for sq in (None, ssq):
+        got = ops.linear_dec(x, wd.to(DEV), sdev, bias=None if b is None else b.to(DEV), glu=glu, norm_eps=1e-5,
+                             ssq_in=sq)
+        assert got.shape == ref.shape
+        assert _rel(got, ref) < 1e-2
+        assert _rel(got, ref_unfold) < (6e-2 if fp8 else 1.5e-2)
+    if not glu:
+        got32 = ops.linear_dec(x, wd.to(DEV), sdev, norm_eps=1e-5, ssq_in=ssq, out_dtype=torch.float32)
+        ref32 = ops.linear(ops.rms_norm(xr.float(), one, 1e-5), wd, w_scale=sd)
+        assert got32.dtype == torch.float32 and _rel(got32, ref32) < 1e-2
