@@ -1005,6 +1005,9 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
     else if (t128 >= 256) tile = lds_ok ? 20000 : 1;
     else if (M <= 64) tile = 3;
     else if (t128 >= 144 && lds_ok) tile = 20005;
+    // fewer 128x128 tiles (VLM vision tower at 577 tokens: 40-120): the same pipeline with K split
+    // over gridDim.y + one reduce/epilogue pass (gemm_f8.hip f8_pick_splits) instead of 64x64 tiles
+    else if (lds_ok && M >= 128 && K >= 4096 && getenv("LUMEN_GEMM_NO_LDS128_SPLIT") == nullptr) tile = 20000;
     else tile = 2;
     if (tile >= 20000) return gemm_lds128_bf16(A, lda, W, ldw, C, ldc, M, N, K, ep, tile - 20000, stream);
   }

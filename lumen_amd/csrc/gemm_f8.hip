@@ -26,6 +26,9 @@
 // k permutation is used for A and W, so the dot products are unchanged, and with it
 // every ds_read_b128 lane group hits 64 distinct banks (chunks 2g, 2g+1 would be 2-way).
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "common.h"
 #include "gemm_epi.h"
@@ -64,6 +67,11 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int tiles_m = (M + 127) / 128, tiles_n = (N + 127) / 128;
+  if (ep.split_koff) {   // split-K (gridDim.y = splits): this workgroup's K slice -> its fp32 slab
+    A += blockIdx.y * ep.split_koff * ES;
+    W += blockIdx.y * ep.split_koff * ES;
+    C = (float*)C + blockIdx.y * ep.split_cstride;
+  }
   // XCD-aware: consecutive logical tiles share a W column panel (row tiles fastest), and
   // xcd_remap hands each XCD a contiguous run of them -> each W panel is read from HBM once
   const int lin = xcd_remap(blockIdx.x, tiles_m * tiles_n);
@@ -189,7 +197,7 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
 template <int NS, int WN, bool F8 = true>
 static hipError_t launch_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
                             const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep,
-                            hipStream_t stream) {
+                            hipStream_t stream, int splits = 1) {
   const size_t lds = (size_t)NS * 2 * 128 * 128;
   static bool attr = false;
   if (!attr) {
@@ -198,8 +206,117 @@ static hipError_t launch_f8(const uint8_t* A, int64_t lda, const float* sa, cons
     attr = true;
   }
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8>), dim3(tiles), dim3(128 * WN), lds, stream, A, lda, sa, W, ldw, sw,
-                     C, ldc, M, N, K, ep);
+  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8>), dim3(tiles, splits), dim3(128 * WN), lds, stream, A, lda, sa, W,
+                     ldw, sw, C, ldc, M, N, K, ep);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- split-K
+// Mid-size GEMMs whose 128x128 tile count leaves CUs idle (LLaVA vision tower at 577 tokens:
+// 40-160 tiles; 8B prefill o / down at 624 tokens: 160) split K over gridDim.y: each split
+// writes scaled fp32 partials to its slab, one reduce pass sums the slabs in split order
+// (deterministic) and runs the real epilogue (bias / act / SwiGLU / residual, 16 columns per
+// thread).  Slabs live in a per-(device, stream) workspace; never during graph capture.
+__global__ void __launch_bounds__(256)
+splitk_reduce16_kernel(const float* __restrict__ slabs, int S, int M, int N, void* __restrict__ C, int64_t ldc,
+                       GemmEpi ep) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int nc = N / 16;
+  if (idx >= (int64_t)M * nc) return;
+  const int m = (int)(idx / nc), n = (int)(idx % nc) * 16;
+  const int64_t slab = (int64_t)M * N;
+  float v[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = 0.f;
+  for (int s = 0; s < S; ++s) {   // split order: deterministic
+    const float* p = slabs + s * slab + (int64_t)m * N + n;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4_t a = *(const f32x4_t*)(p + 4 * q);
+      v[4 * q] += a[0]; v[4 * q + 1] += a[1]; v[4 * q + 2] += a[2]; v[4 * q + 3] += a[3];
+    }
+  }
+  GemmEpi e = ep;
+  e.alpha = 1.f;   // scales were applied by the slab GEMM
+  epi_store16_t<false>(v, m, n, M, N, C, ldc, e, c_rsrc(C));
+}
+
+static float* split_workspace(size_t bytes, hipStream_t stream) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> cache;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& slot = cache[{dev, stream}];
+  if (slot.second >= bytes) return slot.first;
+  if (slot.first) {   // the stream's earlier users of the old buffer must be done before it goes
+    (void)hipStreamSynchronize(stream);
+    (void)hipFree(slot.first);
+  }
+  void* p = nullptr;
+  const size_t want = bytes < ((size_t)32 << 20) ? ((size_t)32 << 20) : bytes;
+  if (hipMalloc(&p, want) != hipSuccess) {
+    slot = {nullptr, 0};
+    return nullptr;
+  }
+  slot = {(float*)p, want};
+  return slot.first;
+}
+
+static int f8_num_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+// K splits for a 128x128-tile GEMM: LUMEN_F8_SPLIT forces S (1 = off); auto splits only grids
+// of at most half the CUs, to ~1-2 workgroups per CU, keeping >= 4 k tiles (128 B) per split
+static int f8_pick_splits(int tiles, int nk, const GemmEpi& ep) {
+  static const int force = [] {
+    const char* e = getenv("LUMEN_F8_SPLIT");
+    return e ? atoi(e) : 0;
+  }();
+  if (ep.out_group || ep.table || ep.split_koff || ep.prelu || ep.post_act) return 1;
+  const int cus = f8_num_cus();
+  int S = 1;
+  if (force > 0) {
+    S = force;
+  } else if (2 * tiles <= cus && nk >= 32) {
+    // deep K only: the fp32 slab round trip costs more than the idle CUs on K <= 1024 shapes
+    // (577 x 3072 x 1024: 14.2 -> 28.2 us split; 577 x 1024 x 4096: 35.8 -> 25.8 us;
+    // 624 x 4096 x 14336 fp8: 61.9 -> 57.4 us at S = 2; profiles/r2_splitk_mid_v1.txt)
+    for (int c : {2, 3, 4, 6, 8})
+      if (tiles * c <= 2 * cus && nk % c == 0 && nk / c >= 8) S = c;
+  }
+  while (S > 1 && (nk % S != 0 || nk / S < 2)) --S;
+  return S;
+}
+
+template <int NS, int WN, bool F8>
+static hipError_t launch_f8_split(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
+                                  const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep,
+                                  int S, hipStream_t stream) {
+  constexpr int ES = F8 ? 1 : 2;
+  float* slabs = split_workspace((size_t)S * M * N * sizeof(float), stream);
+  if (slabs == nullptr) return launch_f8<NS, WN, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+  GemmEpi e{};
+  e.alpha = 1.f;
+  e.out_f32 = 1;
+  e.split_koff = (int64_t)(K / S);
+  e.split_cstride = (int64_t)M * N;
+  (void)ES;
+  hipError_t err = launch_f8<NS, WN, F8>(A, lda, sa, W, ldw, sw, slabs, N, M, N, K / S, e, stream, S);
+  if (err != hipSuccess) return err;
+  const int64_t work = (int64_t)M * (N / 16);
+  hipLaunchKernelGGL(splitk_reduce16_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, stream, slabs, S, M,
+                     N, C, ldc, ep);
   return hipGetLastError();
 }
 
@@ -209,15 +326,15 @@ hipError_t gemm_lds128_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
   if (K % 64 != 0 || N % 16 != 0 || M <= 0 || lda % 8 != 0 || ldw % 8 != 0) return hipErrorInvalidValue;
   const uint8_t* a = (const uint8_t*)A;
   const uint8_t* w = (const uint8_t*)W;
-  if (variant == 0) {
-    static int cus = 0;
-    if (cus == 0) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (cus <= 0) cus = 256;
+  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  const int S = f8_pick_splits(tiles, K / 64, ep);
+  if (variant == 0) variant = tiles * S > f8_num_cus() ? 2 : 3;
+  if (S > 1) {
+    switch (variant) {
+      case 2: return launch_f8_split<2, 2, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, S, stream);
+      case 5: return launch_f8_split<2, 4, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, S, stream);
+      default: return launch_f8_split<3, 4, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, S, stream);
     }
-    variant = ((M + 127) / 128) * ((N + 127) / 128) > cus ? 2 : 3;
   }
   switch (variant) {
     case 1: return launch_f8<4, 2, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, stream);
@@ -242,16 +359,15 @@ hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t
     return e ? atoi(e) : 0;
   }();
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  const int S = f8_pick_splits(tiles, K / 128, ep);
   int v = variant;
-  if (v == 0) {
-    static int cus = 0;
-    if (cus == 0) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (cus <= 0) cus = 256;
+  if (v == 0) v = tiles * S > f8_num_cus() ? 2 : 3;
+  if (S > 1) {
+    switch (v) {
+      case 2: return launch_f8_split<2, 2, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
+      case 5: return launch_f8_split<2, 4, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
+      default: return launch_f8_split<3, 4, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
     }
-    v = tiles > cus ? 2 : 3;
   }
   switch (v) {
     case 1: return launch_f8<4, 2>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);

@@ -134,3 +134,38 @@ def test_rms_norm_quant_fp8(M, K, add):
     assert _rel(deq, ref8.float() * refs[:, None]) < 2e-2
     if add:
         torch.testing.assert_close(xd.cpu(), ref_res, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("M,N,K,glu", [(624, 1024, 4096, False), (300, 2048, 1024, True), (130, 640, 2048, False)])
+def test_gemm_f8_splitk_vs_fp32_reference(M, N, K, glu):
+    """Grids of <= 128 128x128 tiles split K over gridDim.y (fp32 slabs + ordered reduce with the
+    real epilogue): bias + residual, SwiGLU, and repeat launches are bitwise identical."""
+    g, x8, xs, w8, ws = _f8_operands(M, N, K, M + N + 1)
+    if glu:
+        ref = ops.linear_f8(x8, xs, w8, ws, glu=True)
+        got = ops.linear_f8(x8.to(DEV), xs.to(DEV), w8.to(DEV), ws.to(DEV), glu=True)
+        assert got.shape == (M, N // 2) and _rel(got, ref) < 1e-2
+        return
+    b = torch.randn(N, generator=g)
+    r = torch.randn(M, N, generator=g).bfloat16()
+    ref = (x8.float() @ w8.float().t()) * xs[:, None] * ws[None, :] + b + r.float()
+    args = (x8.to(DEV), xs.to(DEV), w8.to(DEV), ws.to(DEV))
+    got = ops.linear_f8(*args, bias=b.to(DEV), residual=r.to(DEV))
+    assert _rel(got, ref) < 8e-3
+    again = ops.linear_f8(*args, bias=b.to(DEV), residual=r.to(DEV))
+    assert torch.equal(got, again)
+
+
+@pytest.mark.parametrize("M,N,K,act", [(577, 1024, 4096, None), (577, 3072, 1024, None), (577, 4096, 1024, "quick_gelu"),
+                                       (300, 1024, 1024, None)])
+def test_gemm_bf16_lds128_splitk_vs_fp32(M, N, K, act):
+    """Mid-size bf16 GEMMs (the LLaVA vision tower at 577 tokens) on the 128x128 LDS-DMA
+    pipeline with K split across workgroups, vs the fp32 CPU reference (bias / act / residual)."""
+    g = torch.Generator().manual_seed(M * 3 + N)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
+    b = torch.randn(N, generator=g).bfloat16()
+    r = torch.randn(M, N, generator=g).bfloat16()
+    ref = ops.linear(x.float(), w.float(), b.float(), act=act, residual=r.float())
+    got = ops.linear(x.to(DEV), w.to(DEV), b.to(DEV), act=act, residual=r.to(DEV))
+    assert _rel(got, ref) < 1e-2

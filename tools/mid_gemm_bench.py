@@ -1,0 +1,59 @@
+"""Mid-size bf16 GEMMs (LLaVA vision tower: ViT-L/14-336 at 577 tokens) through ops.linear with
+the auto tile choice.  Run once with LUMEN_GEMM_NO_LDS128_SPLIT=1 (64x64 register-staged tiles
+for < 144 128x128 tiles) and once without (128x128 LDS-DMA pipeline + K split) to compare.
+
+    python tools/mid_gemm_bench.py [--M 577]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from lumen_amd import ops  # noqa: E402
+from lumen_amd._native import load_hip  # noqa: E402
+
+SHAPES = [("qkv", 3072, 1024, None, False), ("out", 1024, 1024, None, True), ("fc1", 4096, 1024, "quick_gelu", False),
+          ("fc2", 1024, 4096, None, True)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, default=577)
+    ap.add_argument("--iters", type=int, default=50)
+    a = ap.parse_args()
+    load_hip(required=True)
+    dev = "cuda"
+    tot = 0.0
+    res = {"M": a.M, "split": os.environ.get("LUMEN_GEMM_NO_LDS128_SPLIT") is None}
+    for name, N, K, act, resid in SHAPES:
+        x = torch.randn(a.M, K, device=dev).bfloat16()
+        w = (torch.randn(N, K, device=dev) * K ** -0.5).bfloat16()
+        b = torch.randn(N, device=dev).bfloat16()
+        r = torch.randn(a.M, N, device=dev).bfloat16() if resid else None
+        out = torch.empty(a.M, N, device=dev, dtype=torch.bfloat16)
+        f = lambda: ops.linear(x, w, b, act=act, residual=r, out=out)  # noqa: E731
+        f()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(5):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(a.iters):
+                f()
+            e.record()
+            e.synchronize()
+            ts.append(s.elapsed_time(e) / a.iters * 1e3)
+        us = statistics.median(ts)
+        tot += us
+        res[f"{name}_us"] = round(us, 2)
+        res[f"{name}_tf"] = round(2 * a.M * N * K / us / 1e6, 1)
+    res["layer_us"] = round(tot, 2)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
