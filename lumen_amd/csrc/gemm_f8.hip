@@ -244,13 +244,15 @@ splitk_reduce16_kernel(const float* __restrict__ slabs, int S, int M, int N, voi
 static float* split_workspace(size_t bytes, hipStream_t stream) {
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> cache;
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> lk(mu);
   auto& slot = cache[{dev, stream}];
+  // a graph captured on a stream bakes in the buffer an eager warm-up on that stream allocated
+  // (callers keep such streams private to the graph); nothing is allocated during capture
   if (slot.second >= bytes) return slot.first;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
   if (slot.first) {   // the stream's earlier users of the old buffer must be done before it goes
     (void)hipStreamSynchronize(stream);
     (void)hipFree(slot.first);
