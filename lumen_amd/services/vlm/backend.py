@@ -279,25 +279,41 @@ class MI355XVLMBackend:
         cfg = self._vlm_config()
         self.cfg = cfg
         m = VLM(cfg, self.tp, dtype=dtype, device=self.device)
-        wp = self.resources.model_root_path / "model.safetensors"
+        root = self.resources.model_root_path
+        wp = root / "model.safetensors"
+        from ...runtime import shard_cache
         from ...utils import onnx_import
 
-        pack = onnx_import.find_vlm_pack(self.resources.model_root_path, self.resources.precision)
-        if wp.exists():
-            m.load_pack_state_dict(load_safetensors(wp))
-        elif pack is not None:
-            # the reference's FastVLM ONNX pack: initializers mapped onto the native FastViTHD +
-            # projector + decoder (the graphs are not executed)
-            log.info("VLM weights from ONNX pack %s", [p.name for p in pack])
-            onnx_import.load_vlm(m, *pack)
-        elif self.resources.extra.get("random_init"):
-            m.random_init(int(self.resources.extra.get("seed", 0)))
+        fp8 = (self.resources.precision or "").lower() in ("fp8", "e4m3", "fp8_e4m3") or \
+            os.environ.get("LUMEN_VLM_FP8", "0") == "1"
+        # pre-sharded cache: TP ranks / fp8 builds reload their own (sharded, quantised) tensors
+        cached = None
+        if shard_cache.enabled() and (self.tp.enabled or fp8) and self.device.type == "cuda" and \
+                not self.resources.extra.get("random_init"):
+            cached = (shard_cache.shard_path(root, self.tp.world, self.tp.rank, "fp8" if fp8 else "bf16"),
+                      shard_cache.source_fingerprint(root), cfg.to_dict())
+        if cached is not None and shard_cache.valid(*cached):
+            extra = shard_cache.load(m, cached[0], self.device)
+            m.llm.weight_dtype = extra.get("weight_dtype", m.llm.weight_dtype)
+            log.info("VLM rank %d/%d weights from shard cache %s", self.tp.rank, self.tp.world, cached[0])
         else:
-            raise ResourceNotFoundError(f"{self.resources.model_name}: model.safetensors / onnx pack missing")
+            pack = onnx_import.find_vlm_pack(root, self.resources.precision)
+            if wp.exists():
+                m.load_pack_state_dict(load_safetensors(wp))
+            elif pack is not None:
+                # the reference's FastVLM ONNX pack: initializers mapped onto the native FastViTHD +
+                # projector + decoder (the graphs are not executed)
+                log.info("VLM weights from ONNX pack %s", [p.name for p in pack])
+                onnx_import.load_vlm(m, *pack)
+            elif self.resources.extra.get("random_init"):
+                m.random_init(int(self.resources.extra.get("seed", 0)))
+            else:
+                raise ResourceNotFoundError(f"{self.resources.model_name}: model.safetensors / onnx pack missing")
+            if fp8:
+                m.llm.quantize_fp8()   # weight-only OCP e4m3 decoder (config precision "fp8")
+            if cached is not None:
+                shard_cache.save(m, cached[0], cached[1], cached[2], {"weight_dtype": m.llm.weight_dtype})
         self.model = m.eval()
-        if (self.resources.precision or "").lower() in ("fp8", "e4m3", "fp8_e4m3") or \
-                os.environ.get("LUMEN_VLM_FP8", "0") == "1":
-            self.model.llm.quantize_fp8()   # weight-only OCP e4m3 decoder (config precision "fp8")
         if self.tp.enabled:
             from ...parallel.comm import Communicator
 
