@@ -214,12 +214,15 @@ __global__ void decode_combine_kernel(DecodeArgs a, int D) {
   const int bh = blockIdx.x;
   const int b = bh / a.H, h = bh - b * a.H;
   const int64_t base = (int64_t)bh * a.nsplit;
+  // only splits that cover context blocks (the table is sized for the batch bucket's longest sequence)
+  const int nblk = (a.ctx_len[b] + KV_BLOCK - 1) / KV_BLOCK;
+  const int ns = max(1, min(a.nsplit, (nblk + a.blocks_per_split - 1) / a.blocks_per_split));
   float M = -INFINITY;
-  for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, a.part_ml[(base + s) * 2]);
+  for (int s = 0; s < ns; ++s) M = fmaxf(M, a.part_ml[(base + s) * 2]);
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
     float L = 0.f, O = 0.f;
     if (M != -INFINITY) {
-      for (int s = 0; s < a.nsplit; ++s) {
+      for (int s = 0; s < ns; ++s) {
         const float e = __builtin_amdgcn_exp2f(a.part_ml[(base + s) * 2] - M);
         L += a.part_ml[(base + s) * 2 + 1] * e;
         O += a.part_o[(base + s) * D + d] * e;

@@ -71,9 +71,26 @@ def test_paged_decode(H, Hkv, D, lens):
     ctx = torch.tensor(lens, dtype=torch.int32)
     q = torch.randn(B, (H + 2 * Hkv) * D, generator=g).bfloat16()
     ref = llm.paged_decode(q, kc, vc, bt, ctx, H, Hkv)
-    got = llm.paged_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), ctx.to(DEV), H, Hkv)
+    args = (q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), ctx.to(DEV), H, Hkv)
+    got = llm.paged_decode(*args)
     assert got.shape == (B, H * D)
     assert _rel(got, ref) < 2e-2
+    # split partials are merged in-launch by the last arriving split (self-resetting counters):
+    # repeat launches and a graph replay give the same bits
+    for _ in range(3):
+        assert torch.equal(llm.paged_decode(*args), got)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        llm.paged_decode(*args)
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        cap = llm.paged_decode(*args)
+    for _ in range(3):
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(cap, got)
 
 
 def test_rep_penalty():
