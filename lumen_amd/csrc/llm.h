@@ -41,6 +41,14 @@ struct DecodeArgs {
   float* part_ml;         // [B, H, nsplit, 2]
   int H, Hkv, nsplit, blocks_per_split;
   float scale_log2;
+  // fused RoPE + cache write (decode, D = 64 / 128): q comes unrotated from the QKV projection
+  // and is rotated in registers; the split owning the sequence's last block rotates the current
+  // token's k and writes k / v to slots[b] before its attention loop reads that block
+  const int* pos;         // [B] positions (null = q / cache already prepared by rope_kv)
+  const float* cos_sin;   // [max_pos, D/2, 2]
+  const int64_t* slots;   // [B]
+  uint16_t* k_cache_w;    // writable views of the caches
+  uint16_t* v_cache_w;
 };
 hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream);
 

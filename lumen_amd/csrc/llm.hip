@@ -91,12 +91,59 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
   {
     const bool qv = col < G;
     const uint16_t* qp = a.q + (int64_t)b * a.q_sb + (int64_t)(hk * G + (qv ? col : 0)) * D;
+    u32x4_t w[KS];
 #pragma unroll
     for (int t = 0; t < KS; ++t) {
-      u32x4_t w = *(const u32x4_t*)(qp + t * 32 + g * 8);
-      if (!qv) w = (u32x4_t){0u, 0u, 0u, 0u};
-      qf[t] = __builtin_bit_cast(bf16x8_t, w);
+      w[t] = *(const u32x4_t*)(qp + t * 32 + g * 8);
+      if (!qv) w[t] = (u32x4_t){0u, 0u, 0u, 0u};
     }
+    if constexpr (KS >= 2) {
+      if (a.pos) {   // fused RoPE (rotate-half): element e pairs with e + D/2, i.e. chunk t with t + KS/2
+        const float2* cs = reinterpret_cast<const float2*>(a.cos_sin) + (int64_t)a.pos[b] * (D / 2);
+#pragma unroll
+        for (int t = 0; t < KS / 2; ++t) {
+          float x1[8], x2[8];
+          unpack8(w[t], x1);
+          unpack8(w[t + KS / 2], x2);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float2 c = cs[t * 32 + g * 8 + j];
+            const float y1 = x1[j] * c.x - x2[j] * c.y, y2 = x2[j] * c.x + x1[j] * c.y;
+            x1[j] = y1;
+            x2[j] = y2;
+          }
+          w[t] = pack8(x1);
+          w[t + KS / 2] = pack8(x2);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < KS; ++t) qf[t] = __builtin_bit_cast(bf16x8_t, w[t]);
+  }
+  // fused cache write of the current token (position ctx - 1): only the split owning the last
+  // block reads it, so that workgroup rotates k, writes k / v for kv head hk and then reads
+  // the block back like any other (stores drained + barrier before the loop)
+  if (a.pos && blk0 <= nblk - 1 && nblk - 1 < blk1) {
+    const int64_t slot = a.slots[b];
+    if (slot >= 0) {
+      const int64_t cblk = slot >> 6;
+      const int coff = (int)(slot & 63);
+      const uint16_t* kv = a.q + (int64_t)b * a.q_sb + (int64_t)(a.H + hk) * D;   // unrotated k head
+      const int half = D / 2;
+      if (tid < half) {
+        const float2 c = reinterpret_cast<const float2*>(a.cos_sin)[(int64_t)a.pos[b] * half + tid];
+        const float x1 = bf2f(kv[tid]), x2 = bf2f(kv[tid + half]);
+        uint16_t* kr = a.k_cache_w + ((cblk * a.Hkv + hk) * KV_BLOCK + coff) * D;
+        kr[tid] = f2bf(x1 * c.x - x2 * c.y);
+        kr[tid + half] = f2bf(x2 * c.x + x1 * c.y);
+      } else if (tid < half + D) {
+        const int d = tid - half;
+        const uint16_t* vr = a.q + (int64_t)b * a.q_sb + (int64_t)(a.H + a.Hkv + hk) * D;
+        a.v_cache_w[((cblk * a.Hkv + hk) * D + d) * KV_BLOCK + coff] = vr[d];
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
   f32x4_t o[NB];
 #pragma unroll

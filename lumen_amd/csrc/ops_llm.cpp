@@ -59,7 +59,8 @@ void rope_kv(at::Tensor qkv, const at::Tensor& pos, const at::Tensor& cos_sin, c
 void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                   const at::Tensor& block_table, const at::Tensor& ctx_len, at::Tensor out, int64_t H, int64_t Hkv,
                   double scale, int64_t nsplit, int64_t blocks_per_split, const c10::optional<at::Tensor>& part_o,
-                  const c10::optional<at::Tensor>& part_ml) {
+                  const c10::optional<at::Tensor>& part_ml, const c10::optional<at::Tensor>& pos,
+                  const c10::optional<at::Tensor>& cos_sin, const c10::optional<at::Tensor>& slots) {
   const int64_t D = k_cache.size(3);
   check_cache(k_cache, v_cache, Hkv, D);
   TORCH_CHECK(D == 32 || D == 64 || D == 128, "paged_decode: head dim 32, 64 or 128");
@@ -91,6 +92,21 @@ void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
     TORCH_CHECK(part_ml->scalar_type() == at::kFloat && part_ml->is_contiguous() && part_ml->numel() >= B * H * nsplit * 2,
                 "part_ml");
     a.part_o = part_o->data_ptr<float>(); a.part_ml = part_ml->data_ptr<float>();
+  }
+  if (pos.has_value() && pos->defined()) {   // fused RoPE + current-token cache write
+    TORCH_CHECK(D == 64 || D == 128, "paged_decode: fused rope needs head dim 64 or 128");
+    TORCH_CHECK(q.size(1) >= (H + 2 * Hkv) * D, "paged_decode: fused rope needs the packed qkv rows");
+    TORCH_CHECK(pos->is_cuda() && pos->scalar_type() == at::kInt && pos->numel() == B && pos->is_contiguous(),
+                "pos int32 [B]");
+    TORCH_CHECK(cos_sin.has_value() && cos_sin->is_cuda() && cos_sin->scalar_type() == at::kFloat &&
+                cos_sin->is_contiguous() && cos_sin->size(-1) == 2 && cos_sin->size(-2) * 2 == D, "cos_sin f32 [P, D/2, 2]");
+    TORCH_CHECK(slots.has_value() && slots->is_cuda() && slots->scalar_type() == at::kLong && slots->numel() == B &&
+                slots->is_contiguous(), "slots int64 [B]");
+    a.pos = pos->data_ptr<int>();
+    a.cos_sin = cos_sin->data_ptr<float>();
+    a.slots = slots->data_ptr<int64_t>();
+    a.k_cache_w = reinterpret_cast<uint16_t*>(k_cache.data_ptr());
+    a.v_cache_w = reinterpret_cast<uint16_t*>(v_cache.data_ptr());
   }
   if (B == 0) return;
   const at::DeviceGuard g(q.device());
@@ -126,9 +142,9 @@ void swiglu_rows(const at::Tensor& y, at::Tensor out) {
 TORCH_LIBRARY_FRAGMENT(lumen, m) {
   m.def("rope_kv(Tensor(a!) qkv, Tensor pos, Tensor cos_sin, Tensor? slots, Tensor(k!) k_cache, Tensor(v!) v_cache, "
         "int H, int Hkv, int D) -> ()");
-  m.def("paged_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_table, Tensor ctx_len, Tensor(o!) out, "
-        "int H, int Hkv, float scale, int nsplit, int blocks_per_split, Tensor(p!)? part_o=None, "
-        "Tensor(m!)? part_ml=None) -> ()");
+  m.def("paged_decode(Tensor q, Tensor(k!) k_cache, Tensor(v!) v_cache, Tensor block_table, Tensor ctx_len, "
+        "Tensor(o!) out, int H, int Hkv, float scale, int nsplit, int blocks_per_split, Tensor(p!)? part_o=None, "
+        "Tensor(m!)? part_ml=None, Tensor? pos=None, Tensor? cos_sin=None, Tensor? slots=None) -> ()");
   m.def("rep_penalty_(Tensor(a!) logits, Tensor ids, Tensor penalty) -> ()");
   m.def("swiglu_rows(Tensor y, Tensor(o!) out) -> ()");
 }

@@ -49,6 +49,8 @@ _F8_MIN_ROWS = int(os.environ.get("LUMEN_LLM_F8_MIN_ROWS", "33"))
 # GPU: RMSNorm gammas folded into qkv / gate|up / lm_head (LLM.fold_norms); decode norms become
 # rstd row scales in the skinny GEMM epilogues (ops.linear_dec)
 _FUSED_DECODE_NORM = os.environ.get("LUMEN_LLM_FUSED_NORM", "1") != "0"
+# decode: RoPE + current-token KV-cache write inside the paged attention kernel (no rope_kv launch)
+_FUSED_DECODE_ROPE = os.environ.get("LUMEN_LLM_FUSED_ROPE", "1") != "0"
 
 
 def _prefill_blas_ok(name: str, K: int) -> bool:
@@ -364,7 +366,8 @@ class LLM(nn.Module):
                 ops.rms_norm(x, l.ln1, eps, add=self._all_reduce(pending), resid_out=x, out=h)
             qkv = self._lin(h, l, "qkv", bias=l.qkv_b)
             kc, vc = (kv.k[i], kv.v[i]) if kv is not None else (None, None)
-            lops.rope_kv(qkv, pos, self.cos_sin, l.H, l.Hkv, D, slots, kc, vc)
+            if not getattr(attn_fn, "fuses_rope", False):
+                lops.rope_kv(qkv, pos, self.cos_sin, l.H, l.Hkv, D, slots, kc, vc)
             att = attn_fn(qkv, l, kc, vc)                            # [T, H*D]
             if tp:
                 part = self._lin(att, l, "o")
@@ -393,7 +396,8 @@ class LLM(nn.Module):
             qkv = ops.linear_dec(x, l.qkv_w, getattr(l, "qkv_s", None), bias=l.qkv_b, norm_eps=eps,
                                  ssq_in=ssq if i > 0 else None)
             kc, vc = (kv.k[i], kv.v[i]) if kv is not None else (None, None)
-            lops.rope_kv(qkv, pos, self.cos_sin, l.H, l.Hkv, D, slots, kc, vc)
+            if not getattr(attn_fn, "fuses_rope", False):      # decode attention rotates + caches itself
+                lops.rope_kv(qkv, pos, self.cos_sin, l.H, l.Hkv, D, slots, kc, vc)
             att = attn_fn(qkv, l, kc, vc)
             ops.linear_dec(att, l.o_w, getattr(l, "o_s", None), residual=x, out=x, ssq_out=ssq)
             g = ops.linear_dec(x, l.gu_w, getattr(l, "gu_s", None), glu=True, norm_eps=eps, ssq_in=ssq)
@@ -488,9 +492,14 @@ class LLM(nn.Module):
         x = self.embed_tokens(ids)
         self._maybe_fold(x)
 
-        def attn(qkv, l, kc, vc):
-            return lops.paged_decode(qkv, kc, vc, block_table, ctx_len, l.H, l.Hkv, workspace=workspace)
+        fuse = _FUSED_DECODE_ROPE and x.is_cuda and self.cfg.head_dim in (64, 128) and \
+            self.norm_folded and x.shape[0] <= 32 and not self.tp.enabled and kv is not None
 
+        def attn(qkv, l, kc, vc):
+            return lops.paged_decode(qkv, kc, vc, block_table, ctx_len, l.H, l.Hkv, workspace=workspace,
+                                     rope=(pos, self.cos_sin, slots) if fuse else None)
+
+        attn.fuses_rope = fuse     # read by _layers_dec: no separate rope_kv launch
         self._layers(x, pos, slots, kv, attn)
         dec = self.norm_folded and x.is_cuda and x.shape[0] <= 32 and not self.tp.enabled
         return self.logits(x, ssq=self._ssq if dec else None)

@@ -86,11 +86,22 @@ def decode_splits(B: int, Hkv: int, max_blocks: int, target_wg: int = 512) -> tu
 
 def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_table: torch.Tensor,
                  ctx_len: torch.Tensor, H: int, Hkv: int, scale: Optional[float] = None,
-                 out: Optional[torch.Tensor] = None, workspace: Optional[dict] = None) -> torch.Tensor:
+                 out: Optional[torch.Tensor] = None, workspace: Optional[dict] = None,
+                 rope: Optional[tuple] = None) -> torch.Tensor:
     """Single-token attention of q [B, H*D] (rows may be views) over each sequence's cached
-    context (ctx_len tokens, including the current token)."""
+    context (ctx_len tokens, including the current token).
+
+    ``rope = (pos [B] int32, cos_sin, slots [B] int64)``: q is the *unrotated* packed QKV row
+    and the kernel applies RoPE to q in registers and writes the current token's rotated k and
+    its v to ``slots`` itself (what :func:`rope_kv` would do; one launch per layer fewer).
+    Head dims 64 / 128 on the GPU."""
     B = q.shape[0]
     D = k_cache.shape[3]
+    if rope is not None and not (q.is_cuda and D in (64, 128)):
+        pos, cos_sin, slots = rope
+        q = q.clone()
+        rope_kv(q, pos, cos_sin, H, Hkv, D, slots, k_cache, v_cache)
+        rope = None
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     if out is None:
         out = torch.empty((B, H * D), device=q.device, dtype=q.dtype)
@@ -109,8 +120,10 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
             if pm is None or pm.numel() < need * 2:
                 pm = torch.empty(need * 2, device=q.device, dtype=torch.float32)
                 ws["ml"] = pm
+        rp = (None, None, None) if rope is None else \
+            (rope[0].to(torch.int32).contiguous(), rope[1], rope[2].to(torch.long).contiguous())
         hip_ops().paged_decode(q, k_cache, v_cache, block_table, ctx_len, out, int(H), int(Hkv), float(scale),
-                               int(nsplit), int(bps), po, pm)
+                               int(nsplit), int(bps), po, pm, *rp)
         return out
     G = H // Hkv
     for b in range(B):

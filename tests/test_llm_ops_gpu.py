@@ -302,3 +302,33 @@ def test_linear_dec_norm_folding_matches_cpu(fp8, M, N, K, glu):
         got32 = ops.linear_dec(x, wd.to(DEV), sdev, norm_eps=1e-5, ssq_in=ssq, out_dtype=torch.float32)
         ref32 = ops.linear(ops.rms_norm(xr.float(), one, 1e-5), wd, w_scale=sd)
         assert got32.dtype == torch.float32 and _rel(got32, ref32) < 1e-2
+
+
+@pytest.mark.parametrize("H,Hkv,D", [(32, 8, 128), (14, 2, 64)])
+@pytest.mark.parametrize("lens", [[1, 64, 65], [700, 3, 2048 + 17]])
+def test_paged_decode_fused_rope_matches_rope_kv(H, Hkv, D, lens):
+    """Decode attention with RoPE + current-token cache write fused in (q unrotated) == rope_kv
+    then paged_decode: same output bits and the same K / V cache contents."""
+    g = torch.Generator().manual_seed(H + D + len(lens))
+    B = len(lens)
+    maxb = max(-(-L // 64) for L in lens)
+    NB = B * maxb + 3
+    kc, vc = _cache(NB, Hkv, D, g)
+    perm = torch.randperm(NB, generator=g)
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    for b in range(B):
+        bt[b] = perm[b * maxb:(b + 1) * maxb].int()
+    ctx = torch.tensor(lens, dtype=torch.int32)
+    pos = ctx - 1
+    slots = torch.tensor([int(bt[b, (L - 1) // 64]) * 64 + (L - 1) % 64 for b, L in enumerate(lens)], dtype=torch.long)
+    cs = llm.rope_cos_sin(4096, D, 500000.0)
+    qkv = torch.randn(B, (H + 2 * Hkv) * D, generator=g).bfloat16()
+    q1, k1, v1 = qkv.to(DEV), kc.to(DEV), vc.to(DEV)
+    llm.rope_kv(q1, pos.to(DEV), cs.to(DEV), H, Hkv, D, slots.to(DEV), k1, v1)
+    ref = llm.paged_decode(q1, k1, v1, bt.to(DEV), ctx.to(DEV), H, Hkv)
+    q2, k2, v2 = qkv.to(DEV), kc.to(DEV), vc.to(DEV)
+    got = llm.paged_decode(q2, k2, v2, bt.to(DEV), ctx.to(DEV), H, Hkv,
+                           rope=(pos.to(DEV), cs.to(DEV), slots.to(DEV)))
+    assert torch.equal(k2, k1) and torch.equal(v2, v1)
+    assert torch.equal(got, ref)
+    assert torch.equal(q2, qkv.to(DEV))            # the QKV rows are not rotated in place
