@@ -152,6 +152,83 @@ __global__ void __launch_bounds__(64 * NWV) gemm_skinny_w8_kernel(const uint16_t
   }
 }
 
+// Two 16-column tiles per workgroup (unsplit K, M <= 16): the A fragments of each k block feed
+// both tiles' MFMAs and every wave keeps twice the weight bytes in flight.  For the widest decode
+// GEMMs (Llama-3-8B gate|up: 1792 tiles, lm_head) this halves the workgroup count, so the grid
+// fits in one round of resident workgroups instead of 1.2+ (6 per CU at 70 VGPRs).
+template <int W8_UNROLL, int NWV = 4>
+__global__ void __launch_bounds__(64 * NWV) gemm_skinny_w8x2_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                               const uint8_t* __restrict__ W, int64_t ldw,
+                                                               const float* __restrict__ scale, void* __restrict__ C,
+                                                               int64_t ldc, int M, int N, int K, GemmEpi ep) {
+  __shared__ float red[NWV][16][33];
+  __shared__ float rstd_s[16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 32;
+  const uint8_t* wr0 = W + (int64_t)min(n0 + col, N - 1) * ldw + g * 16;
+  const uint8_t* wr1 = W + (int64_t)min(n0 + 16 + col, N - 1) * ldw + g * 16;
+  const bool av = col < M;
+  const uint16_t* ar = A + (int64_t)(av ? col : 0) * lda + g * 16;
+  f32x4_t acc0 = (f32x4_t){0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+
+  auto mma2 = [&](const u32x4_t w8, const u32x4_t a0, const u32x4_t a1, f32x4_t& acc) {
+    bf16x8_t f0, f1;
+    fp8x16_to_bf16(w8, f0, f1);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a0), f0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a1), f1, acc, 0, 0, 0);
+  };
+  const int nblk = K / 64;
+  int s = wid;
+  for (; s + NWV * (W8_UNROLL - 1) < nblk; s += NWV * W8_UNROLL) {
+    u32x4_t w0[W8_UNROLL], w1[W8_UNROLL], a0[W8_UNROLL], a1[W8_UNROLL];
+#pragma unroll
+    for (int u = 0; u < W8_UNROLL; ++u) {
+      const int k = (s + NWV * u) * 64;
+      w0[u] = *(const u32x4_t*)(wr0 + k);
+      w1[u] = *(const u32x4_t*)(wr1 + k);
+      a0[u] = av ? *(const u32x4_t*)(ar + k) : (u32x4_t){0u, 0u, 0u, 0u};
+      a1[u] = av ? *(const u32x4_t*)(ar + k + 8) : (u32x4_t){0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < W8_UNROLL; ++u) {
+      mma2(w0[u], a0[u], a1[u], acc0);
+      mma2(w1[u], a0[u], a1[u], acc1);
+    }
+  }
+  for (; s < nblk; s += NWV) {
+    const int k = s * 64;
+    const u32x4_t w0 = *(const u32x4_t*)(wr0 + k), w1 = *(const u32x4_t*)(wr1 + k);
+    const u32x4_t a0 = av ? *(const u32x4_t*)(ar + k) : (u32x4_t){0u, 0u, 0u, 0u};
+    const u32x4_t a1 = av ? *(const u32x4_t*)(ar + k + 8) : (u32x4_t){0u, 0u, 0u, 0u};
+    mma2(w0, a0, a1, acc0);
+    mma2(w1, a0, a1, acc1);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    red[wid][4 * g + r][col] = acc0[r];
+    red[wid][4 * g + r][16 + col] = acc1[r];
+  }
+  if (ep.norm) skinny_rstd<NWV>(A, lda, M, K, ep, rstd_s);
+  __syncthreads();
+  if (tid < 2 * 16) {   // thread: (row m, tile tl)
+    const int m = tid & 15, tl = tid >> 4;
+    const int n = n0 + tl * 16;
+    if (m < M && n < N) {
+      float v[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) t += red[w][m][tl * 16 + c];
+        v[c] = t * (n + c < N ? scale[n + c] : 0.f);
+      }
+      epi_store16_dec(v, rstd_s[m], m, n, M, N, C, ldc, ep);
+    }
+  }
+}
+
 // ============================================================================ prefill
 template <int BM, int BN, int WM, int WN>
 __global__ void __launch_bounds__(WM* WN * 64)
@@ -327,6 +404,26 @@ hipError_t gemm_w8(const uint16_t* A, int64_t lda, const uint8_t* W, int64_t ldw
     default: W8_LAUNCH(1, U_, NT_, 4);          \
   }
     (void)block;
+    // two tiles per workgroup for wide unsplit GEMMs (LUMEN_W8_NTL=1|2 forces; auto: > 6 tiles per CU)
+    static const int ntl_env = [] {
+      const char* e = getenv("LUMEN_W8_NTL");
+      return e ? atoi(e) : 0;
+    }();
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (cus <= 0) cus = 256;
+    }
+    const int ntiles = (N + 15) / 16;
+    const bool x2 = M <= 16 && gy == 1 && variant == 0 && nwv == 4 &&
+                    (ntl_env == 2 || (ntl_env == 0 && ntiles > 6 * cus));
+    if (x2) {
+      hipLaunchKernelGGL((gemm_skinny_w8x2_kernel<4, 4>), dim3((N + 31) / 32), dim3(256), 0, stream, A, lda, W, ldw,
+                         scale, C, ldc, M, N, K, ep);
+      return hipGetLastError();
+    }
     if (M <= 16) {
       switch (variant) {
         case 1: W8_NW(4, true); break;

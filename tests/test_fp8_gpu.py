@@ -17,7 +17,8 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 896, 896), (4, 4864, 896), (16, 896, 4864), (30, 1024, 14336),
-                                   (100, 1024, 4096), (624, 4096, 4096), (700, 2048, 640)])
+                                   (100, 1024, 4096), (624, 4096, 4096), (700, 2048, 640),
+                                   (1, 28672, 4096), (13, 26640, 1024)])   # two tiles per workgroup
 def test_gemm_w8_vs_dequantized(M, N, K):
     g = torch.Generator().manual_seed(M + N)
     x = torch.randn(M, K, generator=g).bfloat16()
@@ -169,3 +170,16 @@ def test_gemm_bf16_lds128_splitk_vs_fp32(M, N, K, act):
     ref = ops.linear(x.float(), w.float(), b.float(), act=act, residual=r.float())
     got = ops.linear(x.to(DEV), w.to(DEV), b.to(DEV), act=act, residual=r.to(DEV))
     assert _rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 16])
+def test_gemm_w8_two_tile_glu_norm(M):
+    """Two-tile-per-workgroup decode kernel (wide N) through linear_dec: SwiGLU + folded RMSNorm."""
+    K, I = 1024, 14336
+    g = torch.Generator().manual_seed(M + 5)
+    x = (torch.randn(M, K, generator=g) * 2).bfloat16()
+    w8, ws = ops.quantize_fp8_rows(ops.glu_interleave(torch.randn(I, K, generator=g) * K ** -0.5,
+                                                      torch.randn(I, K, generator=g) * K ** -0.5))
+    ref = ops.linear(ops.rms_norm(x.float(), torch.ones(K), 1e-5), w8, glu=True, w_scale=ws)
+    got = ops.linear_dec(x.to(DEV), w8.to(DEV), ws.to(DEV), glu=True, norm_eps=1e-5)
+    assert got.shape == (M, I) and _rel(got, ref) < 1e-2
