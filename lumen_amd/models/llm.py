@@ -30,20 +30,11 @@ from torch import nn
 from .. import ops
 from ..ops import llm as lops
 
-# Prefill-shaped projections (>= _PREFILL_BLAS_MIN_ROWS tokens) of a bf16-weight model
-# without a fused SwiGLU or bias go through hipBLASLt (plain library GEMMs; at M = 624 on
-# Llama-3-8B bf16 they measured 1.7-1.9x the hand-written bf16 MFMA kernels,
-# profiles/r1_prefill_gemm_bench_v1.json).  A bias keeps the hand kernel so it is added in
-# fp32 in the epilogue (HF Qwen2 q/k biases are large).  fp8 models never take this path:
-# their prefill runs W8A8 on the fp8 matrix cores (ops.linear_f8, csrc/gemm_f8.hip) with
-# per-token activation scales produced by the fused RMSNorm+quant kernel, so no bf16 image
-# of the weights is kept (profiles/r2_f8_gemm_bench_v1.jsonl).
-_PREFILL_BLAS = os.environ.get("LUMEN_LLM_PREFILL_BLAS", "1") != "0"
-_PREFILL_BLAS_MIN_ROWS = int(os.environ.get("LUMEN_LLM_PREFILL_BLAS_MIN_ROWS", "128"))
-_PREFILL_BLAS_NAMES = ("qkv", "o", "gu", "down")
-# the unfused gate|up (+ SwiGLU pass) only pays on wide layers: on Qwen2-0.5B (K = 896) it
-# cost FastVLM 1.6 ms of TTFT, on Llama-3-8B (K = 4096) it saved 0.9 ms
-_PREFILL_BLAS_GLU_MIN_K = int(os.environ.get("LUMEN_LLM_PREFILL_BLAS_GLU_MIN_K", "2048"))
+# Every projection runs on the hand-written kernels: bf16 prefill on the MFMA GEMMs (128x128
+# LDS-DMA pipeline at a few hundred tokens), fp8 prefill W8A8 on the fp8 matrix cores
+# (ops.linear_f8, csrc/gemm_f8.hip, per-token scales from the fused RMSNorm+quant kernel),
+# decode on the skinny split-K kernels.  The r1 hipBLASLt prefill path is gone: FastVLM-0.5B
+# TTFT measured 12.25-12.72 ms without it vs 12.60-12.76 ms with it (same box, r2).
 # W8A8 prefill from this many tokens up (decode batches stay on the weight-only skinny kernels)
 _F8_MIN_ROWS = int(os.environ.get("LUMEN_LLM_F8_MIN_ROWS", "33"))
 # GPU: RMSNorm gammas folded into qkv / gate|up / lm_head (LLM.fold_norms); decode norms become
@@ -51,10 +42,6 @@ _F8_MIN_ROWS = int(os.environ.get("LUMEN_LLM_F8_MIN_ROWS", "33"))
 _FUSED_DECODE_NORM = os.environ.get("LUMEN_LLM_FUSED_NORM", "1") != "0"
 # decode: RoPE + current-token KV-cache write inside the paged attention kernel (no rope_kv launch)
 _FUSED_DECODE_ROPE = os.environ.get("LUMEN_LLM_FUSED_ROPE", "1") != "0"
-
-
-def _prefill_blas_ok(name: str, K: int) -> bool:
-    return _PREFILL_BLAS and name in _PREFILL_BLAS_NAMES and (name != "gu" or K >= _PREFILL_BLAS_GLU_MIN_K)
 
 
 @dataclass
@@ -301,15 +288,6 @@ class LLM(nn.Module):
     @staticmethod
     def _lin(x, l, name, bias=None, residual=None, out=None, glu=False):
         w = getattr(l, name + "_w")
-        if (x.is_cuda and w.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and bias is None
-                and x.shape[0] >= _PREFILL_BLAS_MIN_ROWS and _prefill_blas_ok(name, x.shape[-1])):
-            if glu:
-                assert residual is None
-                return lops.swiglu_rows(torch.mm(x, w.t()), out=out)
-            if residual is not None:                      # out += x @ W^T (in place on the residual stream)
-                assert out is None or out.data_ptr() == residual.data_ptr()
-                return residual.addmm_(x, w.t())
-            return torch.mm(x, w.t(), out=out) if out is not None else torch.mm(x, w.t())
         return ops.linear(x, w, bias=bias, residual=residual, out=out, glu=glu,
                           w_scale=getattr(l, name + "_s", None))
 

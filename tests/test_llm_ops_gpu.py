@@ -196,25 +196,6 @@ def test_swiglu_rows(M, N):
     assert _rel(got, ref) < 1e-2
 
 
-def test_llm_prefill_blas_matches_kernel_path():
-    """bf16 weights: prefill projections through hipBLASLt (+ SwiGLU pass) vs the all-MFMA path."""
-    from lumen_amd.models import llm as llm_mod
-    cfg = llm_mod.LLM_PRESETS["qwen2-0.5b"]
-    old, old_k = llm_mod._PREFILL_BLAS, llm_mod._PREFILL_BLAS_GLU_MIN_K
-    try:
-        llm_mod._PREFILL_BLAS_GLU_MIN_K = 0            # also route gate|up (+ swiglu_rows) at this width
-        m = llm_mod.LLM(cfg, device=torch.device(DEV))
-        m.random_init(0)
-        x0 = (torch.randn(300, cfg.hidden_size, generator=torch.Generator().manual_seed(3)) * 0.5).bfloat16().to(DEV)
-        a = m.prefill(x0.clone())
-        llm_mod._PREFILL_BLAS = False
-        b = m.prefill(x0.clone())
-    finally:
-        llm_mod._PREFILL_BLAS, llm_mod._PREFILL_BLAS_GLU_MIN_K = old, old_k
-    assert torch.isfinite(a).all()
-    assert _rel(a, b) < 2e-2
-
-
 def test_llm_fp8_w8a8_prefill_vs_weight_only():
     """fp8 model: W8A8 prefill (fp8 x fp8 MFMA, per-token scales) vs the weight-only fp8 path
     (bf16 activations) of the same weights; no bf16 weight image is kept."""
