@@ -205,7 +205,8 @@ _BLAS_RESID_MIN_ROWS = int(os.environ.get("LUMEN_BLAS_RESID_MIN_ROWS", "8192"))
 
 
 def _block_steps(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float,
-                 causal: bool = False, kv_len: Optional[torch.Tensor] = None, tile: int = -1):
+                 causal: bool = False, kv_len: Optional[torch.Tensor] = None, tile: int = -1,
+                 res_tile: Optional[int] = None):
     """Pre-LN blocks over the flat residual stream x [B*S, W] (updated in place), one
     ``yield`` per block so several micro-batches can be issued layer-interleaved."""
     T, W = x.shape
@@ -227,7 +228,7 @@ def _block_steps(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, 
             ops.linear(o, blk.out_w, blk.out_b, out=y, tile=tile)
             ops.layer_norm(y, blk.ln2_w, blk.ln2_b, eps, add=x, resid_out=x, out=h)
         else:
-            ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x, tile=tile)
+            ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x, tile=tile if res_tile is None else res_tile)
             ops.layer_norm(x, blk.ln2_w, blk.ln2_b, eps, out=h)
         f = ops.linear(h, blk.fc1_w, blk.fc1_b, act=act, tile=tile)
         if fuse and i + 1 < len(blocks):
@@ -235,7 +236,7 @@ def _block_steps(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, 
             ops.linear(f, blk.fc2_w, blk.fc2_b, out=y, tile=tile)
             ops.layer_norm(y, nb.ln1_w, nb.ln1_b, eps, add=x, resid_out=x, out=h)
         else:
-            ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x, tile=tile)
+            ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x, tile=tile if res_tile is None else res_tile)
         del f
         yield i
 
@@ -255,6 +256,8 @@ def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, ep
 # tail pass (tile code 1609: ping-pong 256x256, non-persistent, no tail split) and attention /
 # LayerNorm of one half overlap GEMM tails of the other.
 _VIT_MICRO = int(os.environ.get("LUMEN_VIT_MICRO", "2"))
+_VIT_MICRO_TILE = int(os.environ.get("LUMEN_VIT_MICRO_TILE", "1609"))
+_VIT_MICRO_RES_TILE = int(os.environ.get("LUMEN_VIT_MICRO_RES_TILE", "1609"))   # out-proj / fc2 (+ residual)
 _VIT_MICRO_MIN_ROWS = 65536          # per micro-batch: every GEMM stays >= 512 tiles of 256x256
 _MICRO_STREAMS: dict = {}
 
@@ -280,7 +283,8 @@ def run_blocks_micro(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: s
         st.wait_stream(cur)
         b0, b1 = bounds[i], bounds[i + 1]
         with torch.cuda.stream(st):
-            gens.append(_block_steps(x[b0 * S:b1 * S], blocks, b1 - b0, S, heads, act, eps, tile=1609))
+            gens.append(_block_steps(x[b0 * S:b1 * S], blocks, b1 - b0, S, heads, act, eps, tile=_VIT_MICRO_TILE,
+                                     res_tile=_VIT_MICRO_RES_TILE))
     live = list(zip(gens, streams))
     while live:
         nxt = []
