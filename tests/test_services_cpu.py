@@ -184,3 +184,38 @@ def test_clip_backend_exception_hierarchy(tmp_path):
         f.unlink()
     with pytest.raises(cb.ModelLoadingError):
         b.initialize()
+
+
+def test_mdns_advertisement_optional_and_registered(monkeypatch):
+    """setup_mdns: without zeroconf it degrades to a logged no-op; with a zeroconf module it
+    registers _lumen._tcp.local. with the configured name, port and TXT properties."""
+    import sys
+    import types
+
+    from lumen_amd.hub import server as hs
+
+    cfg = types.SimpleNamespace(service_name="lumen-test", enabled=True)
+    monkeypatch.setitem(sys.modules, "zeroconf", None)          # import fails
+    assert hs.setup_mdns(50051, cfg) == (None, None)
+
+    seen = {}
+
+    class FakeInfo:
+        def __init__(self, **kw):
+            seen["info"] = kw
+
+    class FakeZC:
+        def register_service(self, info):
+            seen["registered"] = info
+
+    fake = types.ModuleType("zeroconf")
+    fake.ServiceInfo, fake.Zeroconf = FakeInfo, FakeZC
+    monkeypatch.setitem(sys.modules, "zeroconf", fake)
+    monkeypatch.setenv("ADVERTISE_IP", "10.1.2.3")
+    monkeypatch.setenv("SERVICE_UUID", "u-1")
+    zc, info = hs.setup_mdns(50077, cfg)
+    assert isinstance(zc, FakeZC) and seen["registered"] is info
+    kw = seen["info"]
+    assert kw["type_"] == "_lumen._tcp.local." and kw["name"] == "lumen-test._lumen._tcp.local."
+    assert kw["port"] == 50077 and kw["addresses"] == [bytes([10, 1, 2, 3])]
+    assert kw["properties"]["uuid"] == "u-1" and kw["properties"]["status"] == "ready"
