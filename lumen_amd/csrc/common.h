@@ -64,6 +64,24 @@ __device__ __forceinline__ u32x4_t pack8(const float* f) {
   return v;
 }
 
+// ---- OCP e4m3fn (fp8) <-> bf16 / f32 ---------------------------------------
+// fp8 bytes 0,1 (lo) or 2,3 (hi) of a dword -> 2 bf16 packed in a dword
+__device__ __forceinline__ uint32_t fp8x2_lo(uint32_t w) {
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w, 1.0f, false));
+}
+__device__ __forceinline__ uint32_t fp8x2_hi(uint32_t w) {
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w, 1.0f, true));
+}
+// 8 fp8 (two dwords) -> 8 bf16 (16 bytes)
+__device__ __forceinline__ u32x4_t fp8x8_to_bf16(uint32_t w0, uint32_t w1) {
+  return (u32x4_t){fp8x2_lo(w0), fp8x2_hi(w0), fp8x2_lo(w1), fp8x2_hi(w1)};
+}
+// one float -> one e4m3fn byte (saturated to +-448, round to nearest even)
+__device__ __forceinline__ uint8_t f2fp8(float v) {
+  v = fminf(fmaxf(v, -448.f), 448.f);
+  return (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false) & 0xff);
+}
+
 // ---- wave reductions (64 lanes) -----------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -26,18 +26,6 @@ namespace lumen {
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
-// fp8 bytes 0,1 (lo) or 2,3 (hi) of a dword -> 2 bf16 packed in a dword
-__device__ __forceinline__ uint32_t fp8x2_lo(uint32_t w) {
-  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w, 1.0f, false));
-}
-__device__ __forceinline__ uint32_t fp8x2_hi(uint32_t w) {
-  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w, 1.0f, true));
-}
-// 8 fp8 (two dwords) -> 8 bf16 (16 bytes)
-__device__ __forceinline__ u32x4_t fp8x8_to_bf16(uint32_t w0, uint32_t w1) {
-  return (u32x4_t){fp8x2_lo(w0), fp8x2_hi(w0), fp8x2_lo(w1), fp8x2_hi(w1)};
-}
-
 __device__ __forceinline__ void fp8x16_to_bf16(const u32x4_t w, bf16x8_t& f0, bf16x8_t& f1) {
   f0 = __builtin_bit_cast(bf16x8_t, fp8x8_to_bf16(w[0], w[1]));
   f1 = __builtin_bit_cast(bf16x8_t, fp8x8_to_bf16(w[2], w[3]));

@@ -5,6 +5,8 @@
 //                                      reads 16-byte pieces of K rows directly from HBM
 //   v_cache [num_blocks, Hkv, D, 64]   transposed (d-major): the O^T = V^T P^T A-operand
 //                                      needs 8 consecutive tokens of one d -> one 16-byte load
+// Either bf16 or OCP e4m3fn (LUMEN_KV_DTYPE=fp8: half the bytes per token; 8-byte loads widened
+// to bf16 fragments in registers, unit scale, values saturated to +-448 on write).
 // so the decode kernel streams both straight from global memory into MFMA
 // fragments with no LDS staging and no transposing reads.
 #pragma once
@@ -24,6 +26,7 @@ struct RopeKVArgs {
   uint16_t* k_cache;
   uint16_t* v_cache;
   int T, H, Hkv, D;
+  int kv_fp8;             // caches hold OCP e4m3fn bytes (unit scale, saturated) instead of bf16
 };
 hipError_t rope_kv(const RopeKVArgs& a, hipStream_t stream);
 
@@ -49,6 +52,7 @@ struct DecodeArgs {
   const int64_t* slots;   // [B]
   uint16_t* k_cache_w;    // writable views of the caches
   uint16_t* v_cache_w;
+  int kv_fp8;             // caches hold e4m3fn bytes: widened to bf16 on load (cvt_scalef32_pk_bf16_fp8)
 };
 hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream);
 

@@ -46,9 +46,16 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(RopeKVArgs a, int nrot_blo
     hp[i] = b1;
     hp[i + half] = b2;
     if (hh >= a.H && slot >= 0) {
-      uint16_t* kr = a.k_cache + ((blk * a.Hkv + (hh - a.H)) * KV_BLOCK + off) * a.D;
-      kr[i] = b1;
-      kr[i + half] = b2;
+      const int64_t ko = ((blk * a.Hkv + (hh - a.H)) * KV_BLOCK + off) * a.D;
+      if (a.kv_fp8) {
+        uint8_t* kr = reinterpret_cast<uint8_t*>(a.k_cache) + ko;
+        kr[i] = f2fp8(bf2f(b1));
+        kr[i + half] = f2fp8(bf2f(b2));
+      } else {
+        uint16_t* kr = a.k_cache + ko;
+        kr[i] = b1;
+        kr[i + half] = b2;
+      }
     }
     return;
   }
@@ -57,7 +64,9 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(RopeKVArgs a, int nrot_blo
   if (idx >= a.Hkv * a.D) return;
   const uint16_t* vr = row + (a.H + a.Hkv) * a.D;
   const int kh = idx / a.D, d = idx - kh * a.D;
-  a.v_cache[((blk * a.Hkv + kh) * a.D + d) * KV_BLOCK + off] = vr[idx];
+  const int64_t vo = ((blk * a.Hkv + kh) * a.D + d) * KV_BLOCK + off;
+  if (a.kv_fp8) reinterpret_cast<uint8_t*>(a.v_cache)[vo] = f2fp8(bf2f(vr[idx]));
+  else a.v_cache[vo] = vr[idx];
 }
 
 hipError_t rope_kv(const RopeKVArgs& a, hipStream_t stream) {
@@ -69,7 +78,7 @@ hipError_t rope_kv(const RopeKVArgs& a, hipStream_t stream) {
 }
 
 // ------------------------------------------------------------------------------ paged decode attention
-template <int D>
+template <int D, bool F8KV>
 __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
   constexpr int KS = D / 32;   // k-steps of S^T over the head dim
   constexpr int NB = D / 16;   // 16-wide d blocks of O^T
@@ -133,13 +142,22 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
       if (tid < half) {
         const float2 c = reinterpret_cast<const float2*>(a.cos_sin)[(int64_t)a.pos[b] * half + tid];
         const float x1 = bf2f(kv[tid]), x2 = bf2f(kv[tid + half]);
-        uint16_t* kr = a.k_cache_w + ((cblk * a.Hkv + hk) * KV_BLOCK + coff) * D;
-        kr[tid] = f2bf(x1 * c.x - x2 * c.y);
-        kr[tid + half] = f2bf(x2 * c.x + x1 * c.y);
+        const uint16_t y1 = f2bf(x1 * c.x - x2 * c.y), y2 = f2bf(x2 * c.x + x1 * c.y);
+        const int64_t ko = ((cblk * a.Hkv + hk) * KV_BLOCK + coff) * D;
+        if constexpr (F8KV) {
+          uint8_t* kr = reinterpret_cast<uint8_t*>(a.k_cache_w) + ko;
+          kr[tid] = f2fp8(bf2f(y1));
+          kr[tid + half] = f2fp8(bf2f(y2));
+        } else {
+          a.k_cache_w[ko + tid] = y1;
+          a.k_cache_w[ko + tid + half] = y2;
+        }
       } else if (tid < half + D) {
         const int d = tid - half;
         const uint16_t* vr = a.q + (int64_t)b * a.q_sb + (int64_t)(a.H + a.Hkv + hk) * D;
-        a.v_cache_w[((cblk * a.Hkv + hk) * D + d) * KV_BLOCK + coff] = vr[d];
+        const int64_t vo = ((cblk * a.Hkv + hk) * D + d) * KV_BLOCK + coff;
+        if constexpr (F8KV) reinterpret_cast<uint8_t*>(a.v_cache_w)[vo] = f2fp8(bf2f(vr[d]));
+        else a.v_cache_w[vo] = vr[d];
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -152,8 +170,11 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
 
   for (int bi = blk0 + wid; bi < blk1; bi += 4) {
     const int phys = a.block_table[(int64_t)b * a.bt_stride + bi];
-    const uint16_t* kb = a.k_cache + ((int64_t)phys * a.Hkv + hk) * KV_BLOCK * D;
-    const uint16_t* vb = a.v_cache + ((int64_t)phys * a.Hkv + hk) * D * KV_BLOCK;
+    const int64_t kvo = ((int64_t)phys * a.Hkv + hk) * KV_BLOCK * D;   // elements (= bytes for fp8)
+    const uint16_t* kb = a.k_cache + kvo;
+    const uint16_t* vb = a.v_cache + kvo;
+    const uint8_t* kb8 = reinterpret_cast<const uint8_t*>(a.k_cache) + kvo;
+    const uint8_t* vb8 = reinterpret_cast<const uint8_t*>(a.v_cache) + kvo;
     const int valid = min(KV_BLOCK, ctx - bi * KV_BLOCK);
 
     // S^T tiles: tile kb16 = (s = kb16 >> 1, hf = kb16 & 1); MFMA row i <-> token
@@ -162,10 +183,19 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
 #pragma unroll
     for (int kb16 = 0; kb16 < 4; ++kb16) {
       const int tok = 32 * (kb16 >> 1) + 8 * (col >> 2) + 4 * (kb16 & 1) + (col & 3);
-      const uint16_t* kr = kb + (int64_t)tok * D + g * 8;
       bf16x8_t kf[KS];
+      if constexpr (F8KV) {
+        const uint8_t* kr = kb8 + (int64_t)tok * D + g * 8;
 #pragma unroll
-      for (int t = 0; t < KS; ++t) kf[t] = *(const bf16x8_t*)(kr + t * 32);
+        for (int t = 0; t < KS; ++t) {
+          const uint2 w = *(const uint2*)(kr + t * 32);
+          kf[t] = __builtin_bit_cast(bf16x8_t, fp8x8_to_bf16(w.x, w.y));
+        }
+      } else {
+        const uint16_t* kr = kb + (int64_t)tok * D + g * 8;
+#pragma unroll
+        for (int t = 0; t < KS; ++t) kf[t] = *(const bf16x8_t*)(kr + t * 32);
+      }
       sc[kb16] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < KS; ++t) sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t], qf[t], sc[kb16], 0, 0, 0);
@@ -210,10 +240,16 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
         pf[r] = (__bf16)sc[2 * s][r];
         pf[4 + r] = (__bf16)sc[2 * s + 1][r];
       }
-      const uint16_t* vr = vb + (int64_t)col * KV_BLOCK + 32 * s + 8 * g;
+      const int64_t vro = (int64_t)col * KV_BLOCK + 32 * s + 8 * g;
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        const bf16x8_t vf = *(const bf16x8_t*)(vr + (int64_t)j * 16 * KV_BLOCK);
+        bf16x8_t vf;
+        if constexpr (F8KV) {
+          const uint2 w = *(const uint2*)(vb8 + vro + (int64_t)j * 16 * KV_BLOCK);
+          vf = __builtin_bit_cast(bf16x8_t, fp8x8_to_bf16(w.x, w.y));
+        } else {
+          vf = *(const bf16x8_t*)(vb + vro + (int64_t)j * 16 * KV_BLOCK);
+        }
         o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[j], 0, 0, 0);
       }
     }
@@ -281,10 +317,16 @@ __global__ void decode_combine_kernel(DecodeArgs a, int D) {
 
 hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream) {
   dim3 grid(a.nsplit, a.Hkv, B), block(256);
-  if (D == 64) hipLaunchKernelGGL(paged_decode_kernel<64>, grid, block, 0, stream, a);
-  else if (D == 128) hipLaunchKernelGGL(paged_decode_kernel<128>, grid, block, 0, stream, a);
-  else if (D == 32) hipLaunchKernelGGL(paged_decode_kernel<32>, grid, block, 0, stream, a);
+#define PD_LAUNCH(D_)                                                                           \
+  do {                                                                                          \
+    if (a.kv_fp8) hipLaunchKernelGGL((paged_decode_kernel<D_, true>), grid, block, 0, stream, a);  \
+    else hipLaunchKernelGGL((paged_decode_kernel<D_, false>), grid, block, 0, stream, a);          \
+  } while (0)
+  if (D == 64) PD_LAUNCH(64);
+  else if (D == 128) PD_LAUNCH(128);
+  else if (D == 32) PD_LAUNCH(32);
   else return hipErrorInvalidValue;
+#undef PD_LAUNCH
   if (a.nsplit > 1) hipLaunchKernelGGL(decode_combine_kernel, dim3(B * a.H), dim3(128), 0, stream, a, D);
   return hipGetLastError();
 }

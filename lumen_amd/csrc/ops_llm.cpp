@@ -19,14 +19,17 @@ namespace {
 inline hipStream_t cur() { return c10::hip::getCurrentHIPStream().stream(); }
 inline uint16_t* bfp(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
 
-void check_cache(const at::Tensor& kc, const at::Tensor& vc, int64_t Hkv, int64_t D) {
-  TORCH_CHECK(kc.is_cuda() && kc.scalar_type() == at::kBFloat16 && kc.is_contiguous() && kc.dim() == 4,
-              "k_cache: bf16 [NB, Hkv, 64, D]");
-  TORCH_CHECK(vc.is_cuda() && vc.scalar_type() == at::kBFloat16 && vc.is_contiguous() && vc.dim() == 4,
-              "v_cache: bf16 [NB, Hkv, D, 64]");
+// bf16 or float8_e4m3fn caches (both the same dtype); returns 1 for fp8
+int check_cache(const at::Tensor& kc, const at::Tensor& vc, int64_t Hkv, int64_t D) {
+  const bool f8 = kc.scalar_type() == at::kFloat8_e4m3fn;
+  TORCH_CHECK(kc.is_cuda() && (kc.scalar_type() == at::kBFloat16 || f8) && kc.is_contiguous() && kc.dim() == 4,
+              "k_cache: bf16 / float8_e4m3fn [NB, Hkv, 64, D]");
+  TORCH_CHECK(vc.is_cuda() && vc.scalar_type() == kc.scalar_type() && vc.is_contiguous() && vc.dim() == 4,
+              "v_cache: same dtype as k_cache, [NB, Hkv, D, 64]");
   TORCH_CHECK(kc.size(1) == Hkv && kc.size(2) == lumen::KV_BLOCK && kc.size(3) == D, "k_cache shape");
   TORCH_CHECK(vc.size(0) == kc.size(0) && vc.size(1) == Hkv && vc.size(2) == D && vc.size(3) == lumen::KV_BLOCK,
               "v_cache shape");
+  return f8 ? 1 : 0;
 }
 
 // qkv [T, >= (H + 2 Hkv) D] bf16 (rotated in place); pos int32 [T]; cos_sin f32 [P, D/2, 2];
@@ -46,9 +49,9 @@ void rope_kv(at::Tensor qkv, const at::Tensor& pos, const at::Tensor& cos_sin, c
   if (slots.has_value() && slots->defined()) {
     TORCH_CHECK(slots->is_cuda() && slots->scalar_type() == at::kLong && slots->numel() == T && slots->is_contiguous(),
                 "slots int64 [T]");
-    check_cache(k_cache, v_cache, Hkv, D);
+    a.kv_fp8 = check_cache(k_cache, v_cache, Hkv, D);
     a.slots = slots->data_ptr<int64_t>();
-    a.k_cache = bfp(k_cache); a.v_cache = bfp(v_cache);
+    a.k_cache = reinterpret_cast<uint16_t*>(k_cache.data_ptr()); a.v_cache = reinterpret_cast<uint16_t*>(v_cache.data_ptr());
   }
   a.T = (int)T; a.H = (int)H; a.Hkv = (int)Hkv; a.D = (int)D;
   const at::DeviceGuard g(qkv.device());
@@ -62,7 +65,7 @@ void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
                   const c10::optional<at::Tensor>& part_ml, const c10::optional<at::Tensor>& pos,
                   const c10::optional<at::Tensor>& cos_sin, const c10::optional<at::Tensor>& slots) {
   const int64_t D = k_cache.size(3);
-  check_cache(k_cache, v_cache, Hkv, D);
+  const int kv_fp8 = check_cache(k_cache, v_cache, Hkv, D);
   TORCH_CHECK(D == 32 || D == 64 || D == 128, "paged_decode: head dim 32, 64 or 128");
   TORCH_CHECK(H % Hkv == 0 && H / Hkv <= 16, "paged_decode: at most 16 query heads per kv head");
   TORCH_CHECK(q.is_cuda() && q.scalar_type() == at::kBFloat16 && q.dim() == 2 && q.stride(1) == 1 && q.size(1) >= H * D &&
@@ -79,7 +82,9 @@ void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
               "paged_decode: splits must cover the block table");
   lumen::DecodeArgs a{};
   a.q = bfp(q); a.q_sb = q.stride(0);
-  a.k_cache = bfp(k_cache); a.v_cache = bfp(v_cache);
+  a.k_cache = reinterpret_cast<const uint16_t*>(k_cache.data_ptr());
+  a.v_cache = reinterpret_cast<const uint16_t*>(v_cache.data_ptr());
+  a.kv_fp8 = kv_fp8;
   a.block_table = block_table.data_ptr<int>(); a.bt_stride = (int)block_table.stride(0);
   a.ctx_len = ctx_len.data_ptr<int>();
   a.o = bfp(out); a.o_sb = out.stride(0);

@@ -453,6 +453,8 @@ class LLM(nn.Module):
                 assert prefix_blocks is not None and kc is not None, "chunked prefill needs the KV cache"
                 kb = kc.index_select(0, prefix_blocks)                       # [nb, Hkv, 64, D]
                 vb = vc.index_select(0, prefix_blocks)                       # [nb, Hkv, D, 64]
+                if kb.dtype != qkv.dtype:                                     # fp8 cache -> bf16
+                    kb, vb = kb.to(qkv.dtype), vb.to(qkv.dtype)
                 k_all = kb.permute(0, 2, 1, 3).reshape(1, -1, l.Hkv, D)[:, :S]
                 v_all = vb.permute(0, 3, 1, 2).reshape(1, -1, l.Hkv, D)[:, :S].contiguous()
                 o = ops.attention(q5[:, :, :l.H], k_all, v_all, causal=True)

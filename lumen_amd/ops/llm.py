@@ -71,8 +71,11 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor, H: int,
             if sl < 0:
                 continue
             blk, off = sl // KV_BLOCK, sl % KV_BLOCK
-            k_cache[blk, :, off, :] = xr[t, H:].to(k_cache.dtype)
-            v_cache[blk, :, :, off] = v[t].to(v_cache.dtype)
+            kt, vt = xr[t, H:].float(), v[t].float()
+            if k_cache.dtype == torch.float8_e4m3fn:      # the GPU writers saturate to +-448
+                kt, vt = kt.clamp(-448, 448), vt.clamp(-448, 448)
+            k_cache[blk, :, off, :] = kt.to(k_cache.dtype)
+            v_cache[blk, :, :, off] = vt.to(v_cache.dtype)
 
 
 def decode_splits(B: int, Hkv: int, max_blocks: int, target_wg: int = 512) -> tuple[int, int]:

@@ -9,6 +9,7 @@ TP-shard leaves room for ~10^6 cached tokens per GPU.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Sequence
 
 import numpy as np
@@ -72,6 +73,17 @@ class BlockManager:
 
     def release(self, seq: int) -> None:
         self.lib.lumen_kv_release(self.h, seq)
+
+
+def kv_dtype_from_env(default=torch.bfloat16):
+    """LUMEN_KV_DTYPE=fp8 -> OCP e4m3fn paged cache (half the HBM per token; decode attention
+    widens it to bf16 in registers), bf16 (default) otherwise."""
+    v = os.environ.get("LUMEN_KV_DTYPE", "").strip().lower()
+    if v in ("fp8", "e4m3", "float8_e4m3fn"):
+        return torch.float8_e4m3fn
+    if v in ("bf16", "bfloat16"):
+        return torch.bfloat16
+    return default
 
 
 class PagedKVCache:

@@ -320,8 +320,11 @@ class MI355XVLMBackend:
             self.model.llm.comm = Communicator(self.tp.group, self.device)
         self.tokenizer()
         lc = cfg.llm
+        from ...runtime.kv_cache import kv_dtype_from_env
+
+        kv_dtype = kv_dtype_from_env(dtype) if self.device.type == "cuda" else dtype   # LUMEN_KV_DTYPE=fp8
         self.kv = PagedKVCache(lc.num_layers, self.model.llm.Hkv, lc.head_dim, num_blocks=self.kv_blocks or None,
-                               device=self.device, dtype=dtype)
+                               device=self.device, dtype=kv_dtype)
 
     def initialize(self) -> None:
         if self._initialized:

@@ -313,3 +313,39 @@ def test_paged_decode_fused_rope_matches_rope_kv(H, Hkv, D, lens):
     assert torch.equal(k2, k1) and torch.equal(v2, v1)
     assert torch.equal(got, ref)
     assert torch.equal(q2, qkv.to(DEV))            # the QKV rows are not rotated in place
+
+
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("H,Hkv,D", [(32, 8, 128), (14, 2, 64)])
+def test_fp8_kv_cache_matches_cpu(H, Hkv, D, fused):
+    """OCP e4m3 paged KV cache: the GPU writers (rope_kv / the fused decode path) store the same
+    bytes as the CPU reference cast (saturated), and decode attention over the fp8 cache matches
+    the CPU reference over the same cache."""
+    g = torch.Generator().manual_seed(D + H)
+    lens = [1, 200, 1000]
+    B = len(lens)
+    maxb = max(-(-L // 64) for L in lens)
+    NB = B * maxb + 2
+    kc = (torch.randn(NB, Hkv, 64, D, generator=g) * 2).to(torch.float8_e4m3fn)
+    vc = (torch.randn(NB, Hkv, D, 64, generator=g) * 2).to(torch.float8_e4m3fn)
+    perm = torch.randperm(NB, generator=g)
+    bt = torch.stack([perm[b * maxb:(b + 1) * maxb] for b in range(B)]).int()
+    ctx = torch.tensor(lens, dtype=torch.int32)
+    pos = ctx - 1
+    slots = torch.tensor([int(bt[b, (L - 1) // 64]) * 64 + (L - 1) % 64 for b, L in enumerate(lens)], dtype=torch.long)
+    cs = llm.rope_cos_sin(4096, D, 1e6)
+    qkv = (torch.randn(B, (H + 2 * Hkv) * D, generator=g) * 3).bfloat16()
+    q_ref, k_ref, v_ref = qkv.clone(), kc.clone(), vc.clone()
+    llm.rope_kv(q_ref, pos, cs, H, Hkv, D, slots, k_ref, v_ref)
+    ref = llm.paged_decode(q_ref, k_ref, v_ref, bt, ctx, H, Hkv)
+    kg, vg = kc.to(DEV), vc.to(DEV)
+    if fused:
+        got = llm.paged_decode(qkv.to(DEV), kg, vg, bt.to(DEV), ctx.to(DEV), H, Hkv,
+                               rope=(pos.to(DEV), cs.to(DEV), slots.to(DEV)))
+    else:
+        qg = qkv.to(DEV)
+        llm.rope_kv(qg, pos.to(DEV), cs.to(DEV), H, Hkv, D, slots.to(DEV), kg, vg)
+        got = llm.paged_decode(qg, kg, vg, bt.to(DEV), ctx.to(DEV), H, Hkv)
+    assert torch.equal(kg.cpu().view(torch.uint8), k_ref.view(torch.uint8))
+    assert torch.equal(vg.cpu().view(torch.uint8), v_ref.view(torch.uint8))
+    assert _rel(got, ref) < 2e-2

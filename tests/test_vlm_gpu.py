@@ -155,3 +155,38 @@ def test_chunked_prefill_gpu_matches_single_shot():
         assert eng.stats["prefill_chunks"] >= 6 + 1 + 3
     finally:
         eng.close()
+
+
+def test_engine_fp8_kv_cache_serves():
+    """The engine on an OCP e4m3 paged KV cache (eager and hipGraph decode give the same tokens;
+    first-step logits close to the bf16-cache run: per-element fp8 rounding of K / V only)."""
+    cfg = LLM_PRESETS["qwen2-0.5b"]
+    m = LLM(cfg, device="cuda")
+    m.random_init(6)
+    prompts = [list(np.random.default_rng(10 + i).integers(0, 150000, 70 + 30 * i)) for i in range(2)]
+    toks = {}
+    for dt, graphs in ((torch.float8_e4m3fn, False), (torch.float8_e4m3fn, True)):
+        kv = PagedKVCache(cfg.num_layers, m.Hkv, cfg.head_dim, num_blocks=32, device="cuda", dtype=dt)
+        eng = LLMEngine(m, kv, lambda ids: m.embed_tokens(torch.tensor(ids, device="cuda")), max_batch=4,
+                        use_graphs=graphs)
+        try:
+            rs = [eng.submit(p, len(p), SamplingParams(max_new_tokens=5)) for p in prompts]
+            for r in rs:
+                list(r.stream(timeout=120))
+            toks[graphs] = [r.tokens for r in rs]
+        finally:
+            eng.close()
+    assert toks[True] == toks[False] and all(len(t) == 5 for t in toks[True])
+    # one decode step on the two cache dtypes from the same prefill
+    logits = []
+    p = prompts[1]
+    for dt in (torch.bfloat16, torch.float8_e4m3fn):
+        kv = PagedKVCache(cfg.num_layers, m.Hkv, cfg.head_dim, num_blocks=8, device="cuda", dtype=dt)
+        T = len(p)
+        slots = torch.arange(T + 1, device="cuda", dtype=torch.long)
+        m.prefill(m.embed_tokens(torch.tensor(p, device="cuda")), kv, slots[:T])
+        bt = torch.arange(8, device="cuda", dtype=torch.int32).view(1, 8)
+        lg = m.decode(torch.tensor([5], device="cuda"), torch.tensor([T], device="cuda", dtype=torch.int32),
+                      slots[T:T + 1], kv, bt, torch.tensor([T + 1], device="cuda", dtype=torch.int32))
+        logits.append(lg.float().cpu())
+    assert _cos(logits[0], logits[1]) > 0.99

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--kv-blocks", type=int, default=4096)
     ap.add_argument("--full-decode", action="store_true", help="decode the JPEG at full resolution")
     ap.add_argument("--fp8", action="store_true", help="weight-only OCP e4m3 decoder weights (per-channel scales)")
+    ap.add_argument("--kv-fp8", action="store_true", help="OCP e4m3 paged KV cache (unit scale)")
     args = ap.parse_args()
     load_hip(required=True)
     dev = torch.device("cuda")
@@ -51,7 +52,8 @@ def main():
         m.llm.quantize_fp8()
     torch.cuda.synchronize()
     load_s = time.time() - t0
-    kv = PagedKVCache(cfg.llm.num_layers, m.llm.Hkv, cfg.llm.head_dim, num_blocks=args.kv_blocks, device=dev)
+    kv = PagedKVCache(cfg.llm.num_layers, m.llm.Hkv, cfg.llm.head_dim, num_blocks=args.kv_blocks, device=dev,
+                      dtype=torch.float8_e4m3fn if args.kv_fp8 else torch.bfloat16)
 
     dec_ms = []
     # JPEG decoded with libjpeg DCT scaling down to >= the vision input (as the VLM service does,
@@ -109,7 +111,7 @@ def main():
            "decode_tok_s_single": float(np.median(tps)) if tps else None,
            "batch": args.batch, "batch_tok_s": ntok / batch_s, "prompt_tokens": len(full),
            "image_tokens": cfg.num_image_tokens, "max_new_tokens": args.max_new, "n": args.n,
-           "preset": args.preset, "dtype": "bf16" if not args.fp8 else "fp8-e4m3 decoder (W8A8 prefill, fp8-weight decode), bf16 vision", "data": "synthetic (random-init weights, random 1024x768 JPEG)",
+           "preset": args.preset, "kv_cache": "fp8-e4m3" if args.kv_fp8 else "bf16", "dtype": "bf16" if not args.fp8 else "fp8-e4m3 decoder (W8A8 prefill, fp8-weight decode), bf16 vision", "data": "synthetic (random-init weights, random 1024x768 JPEG)",
            "load_s": load_s, "kv_cache_tokens": kv.capacity_tokens,
            "jpeg_decode": "full resolution" if args.full_decode else f"DCT-scaled to >= {cfg.vision.image_size}px"}
     print(json.dumps(out))
