@@ -273,15 +273,19 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 // this reads K/V from HBM once instead of once per 64-query block and removes the per-chunk
 // wait/barrier pairs; the ragged 257th query costs one 16-query block of one wave instead
 // of a whole 64-query workgroup.
-template <int D>
-__global__ void __launch_bounds__(256) attn_res_kernel(AttnArgs a, int nkc) {
+// NW waves per workgroup (4 or 8): with two K/V-resident workgroups per CU, 8 waves give 4 per
+// SIMD to hide the LDS / MFMA latencies of the query-block walk (ViT S = 257: 17 blocks -> at most
+// 3 per wave instead of 5).
+template <int D, int NW>
+__global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc) {
   constexpr int NCH = D / 8;
   constexpr int KS = D / 32;
   constexpr int NB = D / 16;
   constexpr int KC = 64;
   constexpr int IMG = KC * D * 2;
   constexpr int RPI = 1024 / (D * 2);
-  constexpr int NI = KC / RPI / 4;
+  constexpr int NI = KC / RPI / NW;
+  static_assert(NI >= 1, "K/V staging: at least one 1 KiB DMA piece per wave per chunk");
   extern __shared__ __attribute__((aligned(16))) char smem[];   // [nkc][K, V][IMG]
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -327,13 +331,13 @@ __global__ void __launch_bounds__(256) attn_res_kernel(AttnArgs a, int nkc) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int qbk = wid; qbk < nq16; qbk += 4) {
+  for (int qbk = wid; qbk < nq16; qbk += NW) {
     const int q0 = qbk * 16;
     const int qi = q0 + col;
     bf16x8_t qf[KS];
 #pragma unroll
     for (int t = 0; t < KS; ++t) qf[t] = qn[t];
-    if (qbk + 4 < nq16) load_q(qbk + 4);
+    if (qbk + NW < nq16) load_q(qbk + NW);
     f32x4_t o[NB];
 #pragma unroll
     for (int j = 0; j < NB; ++j) o[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
@@ -453,16 +457,32 @@ __global__ void __launch_bounds__(256) attn_res_kernel(AttnArgs a, int nkc) {
   }
 }
 
-template <int D>
-static hipError_t launch_res(const AttnArgs& a, int B, int nkc, hipStream_t stream) {
+template <int D, int NW>
+static hipError_t launch_res_nw(const AttnArgs& a, int B, int nkc, hipStream_t stream) {
   const size_t lds = (size_t)nkc * 2 * 64 * D * 2;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)attn_res_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    hipFuncSetAttribute((const void*)attn_res_kernel<D, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL(attn_res_kernel<D>, dim3(a.H, B), dim3(256), lds, stream, a, nkc);
+  hipLaunchKernelGGL((attn_res_kernel<D, NW>), dim3(a.H, B), dim3(64 * NW), lds, stream, a, nkc);
   return hipGetLastError();
+}
+
+template <int D>
+static hipError_t launch_res(const AttnArgs& a, int B, int nkc, hipStream_t stream) {
+  // LUMEN_ATTN_RES_WAVES forces 4 or 8 waves per workgroup; auto: 8 once there are >= 10 query
+  // blocks to share (ViT-L/14 S = 257: 0.416 -> 0.357 ms at b512, profiles/r2_attn_res_waves_v1.txt),
+  // 4 for short sequences (CLIP text S = 77 has 5 blocks: extra waves would idle)
+  static const int nw_env = [] {
+    const char* e = getenv("LUMEN_ATTN_RES_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  const int nw = nw_env == 4 || nw_env == 8 ? nw_env : ((a.Sq + 15) / 16 >= 10 ? 8 : 4);
+  if constexpr (D >= 64) {
+    if (nw == 8) return launch_res_nw<D, 8>(a, B, nkc, stream);
+  }
+  return launch_res_nw<D, 4>(a, B, nkc, stream);
 }
 
 hipError_t attn_fwd(const AttnArgs& a, int B, int D, hipStream_t stream) {
