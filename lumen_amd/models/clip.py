@@ -256,8 +256,13 @@ def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, ep
 # tail pass (tile code 1609: ping-pong 256x256, non-persistent, no tail split) and attention /
 # LayerNorm of one half overlap GEMM tails of the other.
 _VIT_MICRO = int(os.environ.get("LUMEN_VIT_MICRO", "2"))
-_VIT_MICRO_TILE = int(os.environ.get("LUMEN_VIT_MICRO_TILE", "1609"))
-_VIT_MICRO_RES_TILE = int(os.environ.get("LUMEN_VIT_MICRO_RES_TILE", "1609"))   # out-proj / fc2 (+ residual)
+# ping-pong 256x256, 2 phases per K-tile + priority, group_m = 2, no tail split (1629 vs 1609 / 1689:
+# 6209-6222 vs 6203-6204 / 6129-6130 img/s, profiles/r2_vit_micro_streams_v1.txt)
+_VIT_MICRO_TILE = int(os.environ.get("LUMEN_VIT_MICRO_TILE", "1629"))
+_VIT_MICRO_RES_TILE = int(os.environ.get("LUMEN_VIT_MICRO_RES_TILE", "1629"))   # out-proj / fc2 (+ residual)
+# text tower (B x 77 rows): micro-batched with the auto tile choice once it has this many rows per
+# half (b512 x 77: 50.4-50.6k -> 56.2-56.4k texts/s, profiles/r2_vit_micro_streams_v1.txt)
+_TEXT_MICRO_MIN_ROWS = int(os.environ.get("LUMEN_TEXT_MICRO_MIN_ROWS", "16384"))
 _VIT_MICRO_MIN_ROWS = 65536          # per micro-batch: every GEMM stays >= 512 tiles of 256x256
 _MICRO_STREAMS: dict = {}
 
@@ -269,12 +274,17 @@ def _micro_streams(dev: torch.device, n: int):
     return _MICRO_STREAMS[key]
 
 
-def run_blocks_micro(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float) -> torch.Tensor:
+def run_blocks_micro(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float,
+                     causal: bool = False, min_rows: Optional[int] = None, tile: Optional[int] = None,
+                     res_tile: Optional[int] = None) -> torch.Tensor:
     """run_blocks over micro-batches on separate streams (falls back to run_blocks when the
     batch is too small to split or x is on the CPU)."""
     n = _VIT_MICRO
-    if not x.is_cuda or n <= 1 or B < n or (B // n) * S < _VIT_MICRO_MIN_ROWS:
-        return run_blocks(x, blocks, B, S, heads, act, eps)
+    min_rows = _VIT_MICRO_MIN_ROWS if min_rows is None else min_rows
+    if not x.is_cuda or n <= 1 or B < n or (B // n) * S < min_rows:
+        return run_blocks(x, blocks, B, S, heads, act, eps, causal=causal)
+    tile = _VIT_MICRO_TILE if tile is None else tile
+    res_tile = _VIT_MICRO_RES_TILE if res_tile is None else res_tile
     cur = torch.cuda.current_stream(x.device)
     streams = _micro_streams(x.device, n)
     bounds = [B * i // n for i in range(n + 1)]
@@ -283,8 +293,8 @@ def run_blocks_micro(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: s
         st.wait_stream(cur)
         b0, b1 = bounds[i], bounds[i + 1]
         with torch.cuda.stream(st):
-            gens.append(_block_steps(x[b0 * S:b1 * S], blocks, b1 - b0, S, heads, act, eps, tile=_VIT_MICRO_TILE,
-                                     res_tile=_VIT_MICRO_RES_TILE))
+            gens.append(_block_steps(x[b0 * S:b1 * S], blocks, b1 - b0, S, heads, act, eps, causal=causal,
+                                     tile=tile, res_tile=res_tile))
     live = list(zip(gens, streams))
     while live:
         nxt = []
@@ -293,9 +303,8 @@ def run_blocks_micro(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: s
                 if next(g, None) is not None:
                     nxt.append((g, st))
         live = nxt
-    for st in streams:
+    for st in streams:             # join: x (allocated on cur) is only freed after this point on cur
         cur.wait_stream(st)
-    x.record_stream(streams[0])
     return x
 
 
@@ -417,7 +426,8 @@ class TextTower(nn.Module):
         dev = self.token_emb.device
         ids = ids.to(dev)
         x = ops.embed(ids, self.token_emb, self.pos_emb[:S]).view(B * S, cfg.width)
-        run_blocks(x, self.blocks, B, S, cfg.heads, cfg.act, cfg.ln_eps, causal=True)
+        run_blocks_micro(x, self.blocks, B, S, cfg.heads, cfg.act, cfg.ln_eps, causal=True,
+                         min_rows=_TEXT_MICRO_MIN_ROWS, tile=-1, res_tile=-1)
         if cfg.eot_token_id is None:
             eot = ids.argmax(dim=-1)
         else:

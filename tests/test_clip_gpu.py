@@ -95,3 +95,20 @@ def test_vit_micro_batch_streams_match(monkeypatch, n):
     torch.cuda.synchronize()
     assert (e1 * e2).sum(-1).min().item() > 0.9995
     assert (e2[:8] * e_ref).sum(-1).min().item() > 0.995
+
+
+def test_text_micro_batch_streams_match(monkeypatch):
+    """Text tower (causal) micro-batched over 2 streams == single stream, and vs the CPU reference."""
+    import lumen_amd.models.clip as clip_mod
+
+    m_cpu = CLIPModel.random("ViT-B-32", seed=6, dtype=torch.float32)
+    m_gpu = CLIPModel.random("ViT-B-32", seed=6, dtype=torch.bfloat16, device="cuda")
+    ids = torch.randint(1, 4000, (41, 77), generator=torch.Generator().manual_seed(4))
+    ids[:, 20] = m_cpu.cfg.text.vocab_size - 1
+    t_ref = m_cpu.encode_text_ids(ids[:6])
+    monkeypatch.setattr(clip_mod, "_TEXT_MICRO_MIN_ROWS", 1 << 30)
+    t1 = m_gpu.encode_text_ids(ids.cuda()).cpu()
+    monkeypatch.setattr(clip_mod, "_TEXT_MICRO_MIN_ROWS", 0)
+    t2 = m_gpu.encode_text_ids(ids.cuda()).cpu()
+    assert (t1 * t2).sum(-1).min().item() > 0.9995
+    assert (t2[:6] * t_ref).sum(-1).min().item() > 0.995
