@@ -261,7 +261,10 @@ class LLM(nn.Module):
         return self._ssq
 
     def _maybe_fold(self, x: torch.Tensor) -> None:
-        if x.is_cuda and _FUSED_DECODE_NORM and not self.norm_folded:
+        # never inside a graph capture: the in-place weight rewrite would be replayed every step
+        # (the engine warms up eagerly before capturing, so the fold has happened by then)
+        if x.is_cuda and _FUSED_DECODE_NORM and not self.norm_folded and \
+                not torch.cuda.is_current_stream_capturing():
             self.fold_norms()
             self._ssq_buf(x.device)
 
