@@ -22,8 +22,9 @@ from __future__ import annotations
 import math
 import os
 from dataclasses import asdict, dataclass, field
-from typing import Optional
+from typing import Optional, Sequence
 
+import numpy as np
 import torch
 from torch import nn
 
@@ -467,6 +468,34 @@ class LLM(nn.Module):
 
         self._layers(x, pos, slots, kv, attn)
         return self.logits(x[T - 1:T])
+
+    @torch.no_grad()
+    def prefill_packed(self, x: torch.Tensor, kv, slots: torch.Tensor, lens: Sequence[int]) -> torch.Tensor:
+        """Several whole prompts in one pass: x [sum(lens), hidden] = the sequences' input rows
+        back to back (modified in place), k/v written to ``slots``; returns each sequence's
+        last-token logits [len(lens), V/tp].  The projections see all rows at once (the W8A8 /
+        MFMA GEMMs run at M = sum of the prompts instead of one prompt's few hundred rows);
+        attention runs per sequence (causal, its own rows only)."""
+        self._maybe_fold(x)
+        N = x.shape[0]
+        dev = x.device
+        assert sum(lens) == N and len(lens) >= 1
+        pos = torch.cat([torch.arange(T, dtype=torch.int32) for T in lens]).to(dev)
+        bounds = np.cumsum([0] + list(lens)).tolist()
+        D = self.cfg.head_dim
+
+        def attn(qkv, l, kc, vc):
+            q5 = qkv.view(1, N, l.H + 2 * l.Hkv, D)
+            o = torch.empty((N, l.H * D), device=dev, dtype=qkv.dtype)
+            o5 = o.view(1, N, l.H, D)
+            for s0, s1 in zip(bounds[:-1], bounds[1:]):
+                ops.attention(q5[:, s0:s1, :l.H], q5[:, s0:s1, l.H:l.H + l.Hkv], q5[:, s0:s1, l.H + l.Hkv:],
+                              causal=True, out=o5[:, s0:s1])
+            return o
+
+        self._layers(x, pos, slots, kv, attn)
+        last = torch.tensor([b - 1 for b in bounds[1:]], device=dev, dtype=torch.long)
+        return self.logits(x.index_select(0, last))
 
     @torch.no_grad()
     def decode(self, ids: torch.Tensor, pos: torch.Tensor, slots: torch.Tensor, kv, block_table: torch.Tensor,
