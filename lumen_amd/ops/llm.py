@@ -7,6 +7,7 @@ the same semantics (cache layouts in csrc/llm.h: k [NB, Hkv, 64, D], v [NB, Hkv,
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Sequence
 
 import numpy as np
@@ -78,8 +79,12 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor, H: int,
             v_cache[blk, :, :, off] = vt.to(v_cache.dtype)
 
 
-def decode_splits(B: int, Hkv: int, max_blocks: int, target_wg: int = 512) -> tuple[int, int]:
+_DECODE_TARGET_WG = int(os.environ.get("LUMEN_DECODE_TARGET_WG", "512"))
+
+
+def decode_splits(B: int, Hkv: int, max_blocks: int, target_wg: Optional[int] = None) -> tuple[int, int]:
     """(nsplit, blocks_per_split): enough workgroups to fill 256 CUs, >= 4 blocks (one per wave) per split."""
+    target_wg = _DECODE_TARGET_WG if target_wg is None else target_wg
     want = max(1, -(-target_wg // max(B * Hkv, 1)))
     nsplit = max(1, min(want, -(-max_blocks // 4)))
     bps = -(-max_blocks // nsplit)
