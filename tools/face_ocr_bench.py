@@ -27,6 +27,26 @@ from lumen_amd.ops import vision  # noqa: E402
 from lumen_amd.utils.image import decode_many, encode_jpeg  # noqa: E402
 
 
+def synth_image(rng, h, w, kind):
+    """uint8 [h, w, 3]: 'noise' = uniform random pixels (incompressible: a ~0.8 MB q90 JPEG at 1280x720,
+    the worst case for the host entropy decoder); 'photo' = smooth low-frequency colour fields +
+    edges + mild sensor noise (~130 KB at 1280x720, like a camera photo)."""
+    if kind == "noise":
+        return rng.integers(0, 255, (h, w, 3), dtype=np.uint8)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    img = np.zeros((h, w, 3), np.float32)
+    for c in range(3):
+        for _ in range(6):
+            fy, fx = rng.uniform(0.5, 6, 2) / np.array([h, w])
+            ph = rng.uniform(0, 2 * np.pi, 2)
+            img[..., c] += rng.uniform(10, 40) * np.sin(2 * np.pi * fy * yy + ph[0]) * np.cos(2 * np.pi * fx * xx + ph[1])
+    for _ in range(12):      # flat-coloured rectangles: edges
+        y0, x0 = rng.integers(0, h - 40), rng.integers(0, w - 40)
+        img[y0:y0 + rng.integers(20, h // 3), x0:x0 + rng.integers(20, w // 3)] += rng.uniform(-60, 60, 3)
+    img += 128 + rng.normal(0, 3, img.shape)
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
 def bench_face(args):
     from lumen_amd.models.face import IRESNET_PRESETS, SCRFD, SCRFD_PRESETS, IResNet
     from lumen_amd.services.face.backend import DetParams, FaceSpec, MI355XFaceBackend
@@ -41,7 +61,7 @@ def bench_face(args):
     be.template = vision.ARCFACE_DST
     be._pool, be._dp, be.align_mode = None, {}, "standard"
     rng = np.random.default_rng(0)
-    jpegs = [encode_jpeg(rng.integers(0, 255, (720, 1280, 3), dtype=np.uint8)) for _ in range(args.batch)]
+    jpegs = [encode_jpeg(synth_image(rng, 720, 1280, args.image_kind)) for _ in range(args.batch)]
     lms = np.array([[500, 300], [580, 300], [540, 350], [510, 400], [570, 400]], np.float32)
     minv = np.stack([vision.invert_affine(vision.similarity_transform(lms + 3 * k)) for k in range(args.faces)])
 
@@ -73,6 +93,7 @@ def bench_face(args):
             "faces_per_s": args.batch * args.faces / dt, "detector": "SCRFD-10G-shaped 640",
             "recogniser": f"IResNet-{args.rec}", "image": "1280x720 JPEG",
             "jpeg_decode": "excluded (decoded once up front)" if args.predecoded else "included",
+            "image_kind": args.image_kind, "jpeg_kb": round(sum(len(j) for j in jpegs) / len(jpegs) / 1024, 1),
             "pipeline": "JPEG decode of batch i+1 overlapped with the GPU work of batch i"}
 
 
@@ -91,7 +112,7 @@ def bench_ocr(args):
     be.rec_h, be.rec_batch, be.bucket = 48, 256, 32
     be.character_str = ["blank"] + [chr(0x4E00 + i) for i in range(REC_PRESETS["mobile"].num_classes - 1)]
     rng = np.random.default_rng(0)
-    jpegs = [encode_jpeg(rng.integers(0, 255, (720, 960, 3), dtype=np.uint8)) for _ in range(args.batch)]
+    jpegs = [encode_jpeg(synth_image(rng, 720, 960, args.image_kind)) for _ in range(args.batch)]
     boxes = []
     for k in range(args.crops):
         y = 20 + 25 * k
@@ -131,6 +152,7 @@ def bench_ocr(args):
             "host_stage_ms_per_batch": {k: round(v / n_steps, 2) for k, v in stages.items()},
             "batch": args.batch, "crops_per_image": args.crops, "crops_per_s": args.batch * args.crops / dt,
             "jpeg_decode": "excluded (decoded once up front)" if args.predecoded else "included",
+            "image_kind": args.image_kind, "jpeg_kb": round(sum(len(j) for j in jpegs) / len(jpegs) / 1024, 1),
             "detector": "DBNet-mobile 960", "recogniser": "SVTR-LCNet mobile", "image": "960x720 JPEG"}
 
 
@@ -143,6 +165,8 @@ def main():
     ap.add_argument("--faces", type=int, default=4)
     ap.add_argument("--crops", type=int, default=20)
     ap.add_argument("--rec", default="r100")
+    ap.add_argument("--image-kind", choices=["noise", "photo"], default="noise",
+                    help="synthetic JPEG content: uniform noise (worst-case host decode) or photo-like")
     ap.add_argument("--predecoded", action="store_true",
                     help="decode the JPEGs once up front (GPU pipeline throughput without host JPEG decode)")
     a = ap.parse_args()
