@@ -217,3 +217,38 @@ def test_prefill_packed_gpu_matches_single(fp8):
     for i in range(len(lens)):
         assert _cos(got[i], ref[i]) > 0.999
     assert _cos(kvs[0].k[3].float().cpu(), kvs[1].k[3].float().cpu()) > 0.999
+
+
+def test_vlm_backend_fp8_shard_cache(tmp_path, monkeypatch):
+    """precision fp8 on the GPU: the first build writes this rank's quantised shard
+    (.lumen_shards/tp1_r0_fp8.safetensors), the second build loads it (no requantisation) and
+    generates the same greedy tokens."""
+    from lumen_amd.models.vlm import write_vlm_model
+    from lumen_amd.resources.config import ModelConfig, Runtime
+    from lumen_amd.services.common import load_model_resources
+    from lumen_amd.services.vlm.backend import ChatMessage, GenerationRequest, create_backend
+
+    write_vlm_model(tmp_path / "models" / "fastvlm-tiny", "fastvlm-tiny")
+    res = load_model_resources(tmp_path, ModelConfig(model="fastvlm-tiny", runtime=Runtime.onnx, precision="fp8"))
+    settings = type("S", (), {"device": "cuda"})()
+    shard = tmp_path / "models" / "fastvlm-tiny" / ".lumen_shards" / "tp1_r0_fp8.safetensors"
+    outs = []
+    for i in range(2):
+        b = create_backend(settings, res, "onnx")
+        b.initialize()
+        try:
+            assert shard.is_file()
+            assert b.model.llm.weight_dtype == "fp8"
+            if i == 0:
+                mtime = shard.stat().st_mtime_ns
+            else:
+                assert shard.stat().st_mtime_ns == mtime          # loaded, not rewritten
+            from lumen_amd.utils.image import encode_jpeg
+
+            jpg = encode_jpeg(np.random.default_rng(0).integers(0, 255, (40, 60, 3), dtype=np.uint8))
+            req = GenerationRequest(messages=[ChatMessage(role="user", content="hello there")], image_bytes=jpg,
+                                    max_new_tokens=8, temperature=0.0)
+            outs.append(b.generate(req).text)
+        finally:
+            b.close()
+    assert outs[0] == outs[1]
