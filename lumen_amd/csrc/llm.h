@@ -56,7 +56,6 @@ struct DecodeArgs {
 };
 hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream);
 
-hipError_t swiglu_rows(const uint16_t* y, int64_t ldy, uint16_t* out, int64_t ldo, int M, int N, hipStream_t stream);
 hipError_t rep_penalty(float* logits, int64_t ld, const int* ids, int maxn, const float* penalty, int B, int V,
                        hipStream_t stream);
 

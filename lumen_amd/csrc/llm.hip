@@ -351,36 +351,4 @@ hipError_t rep_penalty(float* logits, int64_t ld, const int* ids, int maxn, cons
   return hipGetLastError();
 }
 
-// SwiGLU of a materialised gate|up projection (prefill rows through hipBLASLt): y [M, N]
-// bf16 with columns interleaved [gate 8 | up 8] per 16 (glu_interleave) -> out [M, N/2],
-// out[m, 8j + q] = silu(y[m, 16j + q]) * y[m, 16j + 8 + q].  One thread per 16-column
-// group: two 16-B loads, one 16-B store (HBM-bound, ~6 TB/s at prefill sizes).
-__global__ void swiglu_rows_kernel(const uint16_t* __restrict__ y, int64_t ldy, uint16_t* __restrict__ out,
-                                   int64_t ldo, int M, int G) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)M * G) return;
-  const int m = (int)(idx / G), j = (int)(idx - (int64_t)m * G);
-  const u32x4_t* src = (const u32x4_t*)(y + (int64_t)m * ldy + 16 * j);
-  const u32x4_t gv = src[0], uv = src[1];
-  u32x4_t r;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float g0 = __uint_as_float(gv[q] << 16), g1 = __uint_as_float(gv[q] & 0xffff0000u);
-    const float u0 = __uint_as_float(uv[q] << 16), u1 = __uint_as_float(uv[q] & 0xffff0000u);
-    const float o0 = g0 / (1.f + __expf(-g0)) * u0, o1 = g1 / (1.f + __expf(-g1)) * u1;
-    r[q] = (uint32_t)f2bf(o0) | ((uint32_t)f2bf(o1) << 16);
-  }
-  *(u32x4_t*)(out + (int64_t)m * ldo + 8 * j) = r;
-}
-
-hipError_t swiglu_rows(const uint16_t* y, int64_t ldy, uint16_t* out, int64_t ldo, int M, int N, hipStream_t stream) {
-  if (N % 16 != 0 || ldy % 8 != 0 || ldo % 8 != 0) return hipErrorInvalidValue;
-  const int G = N / 16;
-  const int64_t total = (int64_t)M * G;
-  if (total == 0) return hipSuccess;
-  hipLaunchKernelGGL(swiglu_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, y, ldy, out, ldo,
-                     M, G);
-  return hipGetLastError();
-}
-
 }  // namespace lumen

@@ -130,18 +130,6 @@ void rep_penalty_(at::Tensor logits, const at::Tensor& ids, const at::Tensor& pe
                                 penalty.data_ptr<float>(), (int)B, (int)logits.size(1), cur()));
 }
 
-void swiglu_rows(const at::Tensor& y, at::Tensor out) {
-  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.dim() == 2 && y.stride(1) == 1 &&
-              y.size(1) % 16 == 0 && y.stride(0) % 8 == 0, "swiglu_rows: y bf16 [M, N], N % 16 == 0, 16-B rows");
-  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kBFloat16 && out.dim() == 2 && out.stride(1) == 1 &&
-              out.size(0) == y.size(0) && out.size(1) == y.size(1) / 2 && out.stride(0) % 8 == 0,
-              "swiglu_rows: out bf16 [M, N/2], 16-B rows");
-  const at::DeviceGuard g(y.device());
-  CHECK_HIP3(lumen::swiglu_rows(reinterpret_cast<const uint16_t*>(y.data_ptr()), y.stride(0),
-                                reinterpret_cast<uint16_t*>(out.data_ptr()), out.stride(0), (int)y.size(0),
-                                (int)y.size(1), cur()));
-}
-
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(lumen, m) {
@@ -151,12 +139,10 @@ TORCH_LIBRARY_FRAGMENT(lumen, m) {
         "Tensor(o!) out, int H, int Hkv, float scale, int nsplit, int blocks_per_split, Tensor(p!)? part_o=None, "
         "Tensor(m!)? part_ml=None, Tensor? pos=None, Tensor? cos_sin=None, Tensor? slots=None) -> ()");
   m.def("rep_penalty_(Tensor(a!) logits, Tensor ids, Tensor penalty) -> ()");
-  m.def("swiglu_rows(Tensor y, Tensor(o!) out) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("rope_kv", &rope_kv);
   m.impl("paged_decode", &paged_decode);
   m.impl("rep_penalty_", &rep_penalty_);
-  m.impl("swiglu_rows", &swiglu_rows);
 }

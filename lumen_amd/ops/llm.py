@@ -185,18 +185,3 @@ def sample_from_candidates(vals: np.ndarray, idx: np.ndarray, lse: float, temper
     n = max(1, min(n, len(p)))
     q = p[:n] / p[:n].sum()
     return int(idx[int(rng.choice(n, p=q))])
-
-
-def swiglu_rows(y: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """SwiGLU of a materialised gate|up projection: y [M, N] with columns interleaved
-    [gate 8 | up 8] per 16 (:func:`lumen_amd.ops.glu_interleave`) -> silu(gate) * up
-    [M, N/2] — the same result the GEMM's fused ``glu`` epilogue writes."""
-    M, N = y.shape
-    if out is None:
-        out = torch.empty((M, N // 2), device=y.device, dtype=y.dtype)
-    if y.is_cuda:
-        hip_ops().swiglu_rows(y, out)
-        return out
-    g = y.float().view(M, N // 16, 2, 8)
-    out.copy_((torch.nn.functional.silu(g[:, :, 0]) * g[:, :, 1]).reshape(M, N // 2))
-    return out

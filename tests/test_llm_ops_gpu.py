@@ -186,16 +186,6 @@ def test_skinny_splitk_inkernel_reduction(fp8):
             assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("M,N", [(1, 32), (624, 28672), (130, 9728)])
-def test_swiglu_rows(M, N):
-    g = torch.Generator().manual_seed(M + N)
-    y = (torch.randn(M, N, generator=g) * 3).bfloat16()
-    ref = llm.swiglu_rows(y.float()).float()
-    got = llm.swiglu_rows(y.to(DEV)).float().cpu()
-    assert got.shape == (M, N // 2)
-    assert _rel(got, ref) < 1e-2
-
-
 def test_llm_fp8_w8a8_prefill_vs_weight_only():
     """fp8 model: W8A8 prefill (fp8 x fp8 MFMA, per-token scales) vs the weight-only fp8 path
     (bf16 activations) of the same weights; no bf16 weight image is kept."""
