@@ -1,7 +1,7 @@
 """SPMD image-batch data parallelism (one process per GPU, RCCL all-gather).
 
-Used by ``bench.py`` and by batch jobs launched with torchrun (label-bank
-precompute, offline embedding of a photo library): every rank encodes its
+Used by batch jobs launched with torchrun (``tools/build_label_bank.py``: the
+BioCLIP / CLIP label-bank precompute): every rank encodes its
 contiguous shard of the global batch on its own GPU, then one RCCL
 ``all_gather_into_tensor`` over xGMI assembles the [global_batch, D] result on
 every rank.  For online serving behind one gRPC endpoint the equivalent is

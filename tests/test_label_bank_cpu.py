@@ -5,6 +5,7 @@ BioCLIP under LUMEN_DP_SIZE=2 classifies through per-worker bank shards."""
 import multiprocessing as mp
 import os
 import socket
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -140,3 +141,66 @@ def test_bioclip_dp2_sharded_bank_matches_single(tmp_path, monkeypatch):
             np.testing.assert_allclose([g[1] for g in got], [x[1] for x in r], atol=1e-5)
     finally:
         dp.backend.close()
+
+
+def _bank_worker(rank, world, port, argv, q):
+    import os
+    import sys
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import build_label_bank
+
+    from lumen_amd.parallel import destroy
+
+    sys.argv = ["build_label_bank.py"] + argv
+    try:
+        q.put((rank, build_label_bank.main()))
+    finally:
+        destroy()
+
+
+def test_label_bank_tool_data_parallel_matches_single(tmp_path):
+    """tools/build_label_bank.py under 2 gloo ranks (parallel.DataParallelRunner shards the
+    labels and all-gathers the rows) writes the same bank as the single-process run."""
+    import json
+    import socket
+    import sys
+
+    import torch.multiprocessing as mp
+
+    from lumen_amd.resources.synthetic import write_clip_model
+
+    write_clip_model(tmp_path / "models" / "clip-tiny", "clip-tiny", preset="tiny")
+    labels = [f"label number {i}" for i in range(23)]
+    (tmp_path / "labels.json").write_text(json.dumps(labels))
+    argv = ["--cache", str(tmp_path), "--model", "clip-tiny", "--dataset", "Bank", "--labels",
+            str(tmp_path / "labels.json"), "--device", "cpu", "--batch", "4"]
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
+    import build_label_bank
+
+    old = sys.argv
+    sys.argv = ["build_label_bank.py"] + argv
+    try:
+        assert build_label_bank.main() == 0
+    finally:
+        sys.argv = old
+    emb_path = tmp_path / "models" / "clip-tiny" / "datasets" / "Bank_embeddings.npy"
+    single = np.load(emb_path)
+    emb_path.unlink()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_bank_worker, args=(r, 2, port, argv, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    rets = [q.get(timeout=240) for _ in range(2)]
+    for p in ps:
+        p.join(timeout=60)
+    assert sorted(rets) == [(0, 0), (1, 0)]
+    dp = np.load(emb_path)
+    assert dp.shape == single.shape == (23, single.shape[1])
+    np.testing.assert_allclose(dp, single, atol=1e-5)

@@ -11,8 +11,13 @@ Prompts follow the managers: CLIP "a photo of a {label}", BioCLIP "a photo of {n
 with name = common name or "Genus species".  The text tower runs in batches of 512 on
 the MI355X kernels (or the CPU reference with --device cpu).
 
+Multi-GPU: launched with torchrun (one process per GPU), every rank encodes its contiguous
+shard of the labels on its own GPU and parallel.DataParallelRunner all-gathers the rows over
+RCCL (gloo on the CPU); rank 0 writes the bank.
+
 usage: python tools/build_label_bank.py --cache ~/.lumen --model bioclip-2 --dataset TreeOfLife-10M \
            --labels names.json [--bio] [--device cuda]
+       torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/build_label_bank.py ...
 """
 from __future__ import annotations
 
@@ -60,15 +65,44 @@ def main() -> int:
         device = a.device
         batch_size = a.batch
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    st = None
+    if world > 1:
+        import torch
+
+        from lumen_amd.parallel.state import init_distributed
+
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        gpu = (a.device or "cuda").startswith("cuda") and torch.cuda.is_available()
+        st = init_distributed(tp_size=1, device=torch.device("cuda", local) if gpu else torch.device("cpu"))
+        _S.device = f"cuda:{local}" if gpu else "cpu"
+
     be = create_backend(_S(), res, a.runtime)
     be.initialize()
     prompts = [f"a photo of {bio_name(l)}" if a.bio else f"a photo of a {l}" for l in labels]
-    embs = []
-    for i in range(0, len(prompts), a.batch):
-        embs.append(be.text_batch_to_vectors(prompts[i:i + a.batch]))
-        print(f"\r{min(i + a.batch, len(prompts))}/{len(prompts)}", end="", flush=True)
-    print()
-    emb = np.concatenate(embs).astype(np.float32)
+
+    def encode(items):
+        embs = []
+        for i in range(0, len(items), a.batch):
+            embs.append(np.asarray(be.text_batch_to_vectors(items[i:i + a.batch]), np.float32))
+            print(f"\r{min(i + a.batch, len(items))}/{len(items)}", end="", flush=True)
+        print()
+        return np.concatenate(embs) if embs else np.zeros((0, be.cfg.embed_dim), np.float32)
+
+    if st is None:
+        emb = encode(prompts)
+    else:
+        import torch
+
+        from lumen_amd.parallel import Communicator, DataParallelRunner
+
+        comm = Communicator(st.dp_group, st.device, ipc=False)
+        run = DataParallelRunner(lambda items: torch.from_numpy(encode(list(items))).to(st.device), comm)
+        emb = run.run(prompts).cpu().numpy()
+        if st.rank != 0:
+            be.close()
+            return 0
+    emb = emb.astype(np.float32)
     emb /= np.maximum(np.linalg.norm(emb, axis=1, keepdims=True), 1e-12)
     root = Path(res.model_root_path)
     (root / "datasets").mkdir(exist_ok=True)
