@@ -49,7 +49,9 @@ __device__ __forceinline__ void f8_vm_wait() {
 // the mid-size bf16 GEMMs (a few hundred to a few thousand rows: VLM vision tower at 577
 // tokens, bf16 decoder prefill) whose 256x256 tile counts cannot fill the chip.
 // lda / ldw are in ELEMENTS of the operand type, K in elements; sa / sw may be null (1.0).
-template <int NSTAGE, int WN, bool F8>
+// BN: tile width (128, or 64 for grids whose 128x128 tiles leave CUs idle -- twice the tiles,
+// 72 KiB of LDS at 3 stages so two workgroups share a CU).
+template <int NSTAGE, int WN, bool F8, int BN = 128>
 __global__ void __launch_bounds__(128 * WN)
 gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restrict__ sa, const uint8_t* __restrict__ W,
                int64_t ldw, const float* __restrict__ sw, void* __restrict__ C, int64_t ldc, int M, int N, int K,
@@ -58,15 +60,17 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
   lda *= ES;
   ldw *= ES;
   constexpr int NW = 2 * WN;             // waves: 2 (M) x WN (N)
-  constexpr int TN = 128 / WN;           // wave tile 64 x TN
+  constexpr int TN = BN / WN;            // wave tile 64 x TN
   constexpr int NR = TN / 16;
-  constexpr int PER = 16 / NW;           // glds instructions per wave per operand per stage
-  constexpr int STAGE = 2 * 128 * 128;   // bytes: A image then W image
+  constexpr int PER = 16 / NW;           // glds instructions per wave for the A image per stage
+  constexpr int PERW = (BN / 8) / NW;    // ... and for the W image
+  static_assert(NR >= 1 && PERW >= 1, "tile / wave split");
+  constexpr int STAGE = 128 * 128 + BN * 128;   // bytes: A image then W image
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
-  const int tiles_m = (M + 127) / 128, tiles_n = (N + 127) / 128;
+  const int tiles_m = (M + 127) / 128, tiles_n = (N + BN - 1) / BN;
   if (ep.split_koff) {   // split-K (gridDim.y = splits): this workgroup's K slice -> its fp32 slab
     A += blockIdx.y * ep.split_koff * ES;
     W += blockIdx.y * ep.split_koff * ES;
@@ -76,29 +80,36 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
   // xcd_remap hands each XCD a contiguous run of them -> each W panel is read from HBM once
   const int lin = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   const int tm = lin % tiles_m, tn = lin / tiles_m;
-  const int m0 = tm * 128, n0 = tn * 128;
+  const int m0 = tm * 128, n0 = tn * BN;
 
-  // staging: wave wid, instruction i covers rows (PER*wid + i)*8 + lane/8 of both images
+  // staging: wave wid, instruction i covers rows (PER*wid + i)*8 + lane/8 of the A image and
+  // rows (PERW*wid + i)*8 + lane/8 of the W image
   const uint8_t* src_a[PER];
-  const uint8_t* src_w[PER];
+  const uint8_t* src_w[PERW];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int r = (PER * wid + i) * 8 + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
     src_a[i] = A + (int64_t)min(m0 + r, M - 1) * lda + c * 16;
+  }
+#pragma unroll
+  for (int i = 0; i < PERW; ++i) {
+    const int r = (PERW * wid + i) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
     src_w[i] = W + (int64_t)min(n0 + r, N - 1) * ldw + c * 16;
   }
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   typedef const __attribute__((address_space(1))) void* g_ptr_t;
   auto stage = [&](int s, int64_t koff) {
-    char* base = smem + s * STAGE + wid * PER * 1024;
+    char* base = smem + s * STAGE;
 #pragma unroll
     for (int i = 0; i < PER; ++i)
-      __builtin_amdgcn_global_load_lds((g_ptr_t)(src_a[i] + koff), (lds_ptr_t)(base + i * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((g_ptr_t)(src_a[i] + koff), (lds_ptr_t)(base + (wid * PER + i) * 1024), 16,
+                                       0, 0);
 #pragma unroll
-    for (int i = 0; i < PER; ++i)
-      __builtin_amdgcn_global_load_lds((g_ptr_t)(src_w[i] + koff), (lds_ptr_t)(base + 128 * 128 + i * 1024), 16, 0,
-                                       0);
+    for (int i = 0; i < PERW; ++i)
+      __builtin_amdgcn_global_load_lds((g_ptr_t)(src_w[i] + koff),
+                                       (lds_ptr_t)(base + 128 * 128 + (wid * PERW + i) * 1024), 16, 0, 0);
   };
 
   f32x4_t acc[4][NR];
@@ -115,7 +126,7 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
 
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt landed for this wave (NSTAGE-2 younger stages may stay in flight) ...
-    if (kt + NSTAGE - 2 < nk) f8_vm_wait<2 * PER * (NSTAGE - 2)>();
+    if (kt + NSTAGE - 2 < nk) f8_vm_wait<(PER + PERW) * (NSTAGE - 2)>();
     else f8_vm_wait<0>();
     // ... and for every wave; every wave is also done reading stage kt-1's buffer
     __builtin_amdgcn_s_barrier();
@@ -194,19 +205,19 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
   });
 }
 
-template <int NS, int WN, bool F8 = true>
+template <int NS, int WN, bool F8 = true, int BN = 128>
 static hipError_t launch_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
                             const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep,
                             hipStream_t stream, int splits = 1) {
-  const size_t lds = (size_t)NS * 2 * 128 * 128;
+  const size_t lds = (size_t)NS * (128 * 128 + BN * 128);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm_f8_kernel<NS, WN, F8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipFuncSetAttribute((const void*)gemm_f8_kernel<NS, WN, F8, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)lds);
     attr = true;
   }
-  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8>), dim3(tiles, splits), dim3(128 * WN), lds, stream, A, lda, sa, W,
+  const int tiles = ((M + 127) / 128) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8, BN>), dim3(tiles, splits), dim3(128 * WN), lds, stream, A, lda, sa, W,
                      ldw, sw, C, ldc, M, N, K, ep);
   return hipGetLastError();
 }
@@ -362,6 +373,16 @@ hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t
   }();
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
   const int S = f8_pick_splits(tiles, K / 128, ep);
+  // LUMEN_F8_BN=64: 128x64 tiles (twice the workgroups, two per CU) for grids whose 128x128 tiles
+  // leave CUs idle.  Opt-in: faster in isolation on the Llama-3-8B prefill shapes (o 23.9 -> 21.8,
+  // down 62.9 -> 58.3 us, weights L2/MALL-warm) but the full 624-token prefill, streaming 7.5 GB of
+  // weights, ran 9.23-9.35 ms with 128x128 vs 9.87-9.90 ms with it (profiles/r2_f8_bn64_v1.txt)
+  static const int bn_env = [] {
+    const char* e = getenv("LUMEN_F8_BN");
+    return e ? atoi(e) : 0;
+  }();
+  const bool bn64 = S == 1 && variant == 0 && N % 64 == 0 && bn_env == 64;
+  if (bn64) return launch_f8<3, 2, true, 64>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
   int v = variant;
   if (v == 0) v = tiles * S > f8_num_cus() ? 2 : 3;
   if (S > 1) {
