@@ -116,15 +116,20 @@ __device__ __forceinline__ bf16x8_t ones_bf16x8() {
   return __builtin_bit_cast(bf16x8_t, (s16x8_t){0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80});
 }
 
-template <int D>
-__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
+// NW waves per workgroup, 16 queries each (a 16*NW-query block): NW = 2 doubles the workgroup
+// count of the few-(batch, head) prefills (one LLaVA image: 16 heads x 10 blocks; 8B prefill:
+// 32 heads x 10) at the price of staging each K/V chunk for half as many queries.
+template <int D, int NW = 4>
+__global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
   constexpr int NCH = D / 8;        // 16-byte chunks per row
   constexpr int KS = D / 32;        // MFMA k-steps over head dim (S^T)
   constexpr int NB = D / 16;        // 16-wide d blocks (O^T)
   constexpr int KC = 64;            // keys per chunk
   constexpr int IMG = KC * D * 2;   // bytes per K (or V) chunk image
   constexpr int RPI = 1024 / (D * 2);  // rows per 1 KiB DMA wave-instruction
-  constexpr int NI = KC / RPI / 4;  // DMA instructions per wave per image
+  constexpr int NI = KC / RPI / NW; // DMA instructions per wave per image
+  constexpr int QB = 16 * NW;       // queries per workgroup
+  static_assert(NI >= 1, "K/V staging");
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * IMG];  // [buf][K,V]
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -138,7 +143,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const int qblk = lin % nqb;
   const int h = (lin / nqb) % gridDim.y, b = lin / (nqb * gridDim.y);
   const int hk = h / (a.H / a.Hkv);
-  const int q0 = qblk * 64 + wid * 16;
+  const int q0 = qblk * QB + wid * 16;
   const int kv_len = a.kv_len ? min(a.kv_len[b], a.Sk) : a.Sk;
   const int causal_off = a.Sk - a.Sq;
 
@@ -186,7 +191,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const int qi = q0 + col;
 
   int kend = kv_len;
-  if (a.causal) kend = min(kend, min(qblk * 64 + 64, a.Sq) + causal_off);
+  if (a.causal) kend = min(kend, min(qblk * QB + QB, a.Sq) + causal_off);
   const int nkc = (kend + KC - 1) / KC;
 
   // waves whose 16 queries are all past the end (the ragged last q-block, e.g.
@@ -494,10 +499,25 @@ hipError_t attn_fwd(const AttnArgs& a, int B, int D, hipStream_t stream) {
     if (D == 128) return launch_res<128>(a, B, nkc, stream);
     if (D == 32) return launch_res<32>(a, B, nkc, stream);
   }
+  // LUMEN_ATTN_FWD_WAVES=2: 32-query blocks (twice the workgroups for few-(batch, head) prefills);
+  // default 4 (64-query blocks)
+  static const int nw_env = [] {
+    const char* e = getenv("LUMEN_ATTN_FWD_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  const int nw = nw_env == 2 ? 2 : 4;
+  if (nw == 2) {
+    dim3 grid((a.Sq + 31) / 32, a.H, B), block(128);
+    if (D == 64) hipLaunchKernelGGL((attn_fwd_kernel<64, 2>), grid, block, 0, stream, a);
+    else if (D == 128) hipLaunchKernelGGL((attn_fwd_kernel<128, 2>), grid, block, 0, stream, a);
+    else if (D == 32) hipLaunchKernelGGL((attn_fwd_kernel<32, 2>), grid, block, 0, stream, a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   dim3 grid((a.Sq + 63) / 64, a.H, B), block(256);
-  if (D == 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, block, 0, stream, a);
-  else if (D == 128) hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, block, 0, stream, a);
-  else if (D == 32) hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, block, 0, stream, a);
+  if (D == 64) hipLaunchKernelGGL((attn_fwd_kernel<64, 4>), grid, block, 0, stream, a);
+  else if (D == 128) hipLaunchKernelGGL((attn_fwd_kernel<128, 4>), grid, block, 0, stream, a);
+  else if (D == 32) hipLaunchKernelGGL((attn_fwd_kernel<32, 4>), grid, block, 0, stream, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
