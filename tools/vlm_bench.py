@@ -27,6 +27,7 @@ from lumen_amd.models.vlm import VLM, VLM_PRESETS  # noqa: E402
 from lumen_amd.runtime.engine import LLMEngine, SamplingParams  # noqa: E402
 from lumen_amd.runtime.kv_cache import PagedKVCache  # noqa: E402
 from lumen_amd.utils.image import decode_rgb, encode_jpeg  # noqa: E402
+from tools.face_ocr_bench import synth_image  # noqa: E402
 
 
 def main():
@@ -41,6 +42,8 @@ def main():
     ap.add_argument("--full-decode", action="store_true", help="decode the JPEG at full resolution")
     ap.add_argument("--fp8", action="store_true", help="weight-only OCP e4m3 decoder weights (per-channel scales)")
     ap.add_argument("--kv-fp8", action="store_true", help="OCP e4m3 paged KV cache (unit scale)")
+    ap.add_argument("--image-kind", choices=["noise", "photo"], default="noise",
+                    help="synthetic JPEG content: uniform noise (worst-case host decode) or photo-like")
     args = ap.parse_args()
     load_hip(required=True)
     dev = torch.device("cuda")
@@ -75,7 +78,7 @@ def main():
 
     eng = LLMEngine(m.llm, kv, build, max_batch=max(args.batch, 1))
     rng = np.random.default_rng(0)
-    jpeg = encode_jpeg(rng.integers(0, 255, (768, 1024, 3), dtype=np.uint8))
+    jpeg = encode_jpeg(synth_image(rng, 768, 1024, args.image_kind))
     V = cfg.llm.vocab_size
     text = [int(t) for t in rng.integers(1000, min(V, 30000), args.prompt_tokens)]
     ids = text[:8] + [cfg.image_token_id] + text[8:]
@@ -124,7 +127,7 @@ def main():
            "decode_tok_s_single": float(np.median(tps)) if tps else None,
            "batch": args.batch, "batch_tok_s": ntok / batch_s, "prompt_tokens": len(full),
            "image_tokens": cfg.num_image_tokens, "max_new_tokens": args.max_new, "n": args.n,
-           "preset": args.preset, "kv_cache": "fp8-e4m3" if args.kv_fp8 else "bf16", "dtype": "bf16" if not args.fp8 else "fp8-e4m3 decoder (W8A8 prefill, fp8-weight decode), bf16 vision", "data": "synthetic (random-init weights, random 1024x768 JPEG)",
+           "preset": args.preset, "kv_cache": "fp8-e4m3" if args.kv_fp8 else "bf16", "dtype": "bf16" if not args.fp8 else "fp8-e4m3 decoder (W8A8 prefill, fp8-weight decode), bf16 vision", "data": f"synthetic (random-init weights, {args.image_kind} 1024x768 JPEG, {len(jpeg) // 1024} KiB)",
            "load_s": load_s, "kv_cache_tokens": kv.capacity_tokens,
            "jpeg_decode": "full resolution" if args.full_decode else f"DCT-scaled to >= {cfg.vision.image_size}px"}
     print(json.dumps(out))
