@@ -7,8 +7,10 @@ image tower (bf16, random-init weights of the real architecture: 24 layers,
 width 1024, 16 heads, patch 14, 224x224) -> fp32 L2-normalised 768-d
 embeddings -> RCCL all-gather of every rank's embeddings (the DP result
 gather).  Weak scaling: the per-GPU batch is fixed, so the global batch grows
-with N.  JPEG decode is not in the timed region (reported separately by
-``--include-decode`` runs, off by default).
+with N.  JPEG decode is not in the headline timed region.  After it, two side windows
+run by default: a >= 30 s steady-state window of the same step (``--seconds``,
+``steady_state``) and an end-to-end window with JPEG decode on the CPU pool
+(``--include-decode``, ``e2e_with_jpeg_decode``); then the text tower (``texts_per_s``).
 
 Launch: ``python bench.py --gpus 1`` or
 ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``.
@@ -83,12 +85,13 @@ def main():
     ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
     ap.add_argument("--text-steps", type=int, default=None,
                     help="text-tower steps timed separately for the texts/s side metric (default = --steps; 0 = skip)")
-    ap.add_argument("--seconds", type=float, default=0.0,
+    ap.add_argument("--seconds", type=float, default=30.0,
                     help="after the K-step window, run a steady-state window of at least this many seconds "
-                         "(BASELINE.md asks >= 30 s) and report it as a side metric")
-    ap.add_argument("--include-decode", action="store_true",
+                         "(BASELINE.md asks >= 30 s) and report it as a side metric (0 = skip)")
+    ap.add_argument("--include-decode", action=argparse.BooleanOptionalAction, default=True,
                     help="side metric: end-to-end images/s with JPEG decode (CPU thread pool, libjpeg-turbo) "
-                         "+ pinned staging + H2D + tower, timed after the headline window")
+                         "+ pinned staging + H2D + tower, timed after the headline window (--no-include-decode "
+                         "skips it)")
     args = ap.parse_args()
 
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -24,7 +24,7 @@ class CoreInstaller:
                  region: str = "other"):
         self.cache_dir = Path(cache_dir).expanduser()
         self.env_kind = env_kind
-        self.mamba = MicromambaInstaller(self.cache_dir)
+        self.mamba = MicromambaInstaller(self.cache_dir, region=region)
         self.env: Optional[PythonEnvManager] = None
         if env_kind != "current":
             self.env = PythonEnvManager(self.cache_dir, EnvSpec(env_name, env_kind))

@@ -1,18 +1,20 @@
 """micromamba locate / install / check (reference utils/installation/micromamba_installer.py).
 
 Search order: ``$MAMBA_EXE``, ``<cache_dir>/bin/micromamba``, ``micromamba`` on PATH.
-Install downloads the static binary for this platform from the mirror list (official
-micro.mamba.pm API, then the GitHub release through CN-friendly proxies) into
-``<cache_dir>/bin`` and verifies it with ``micromamba --version``.
+Install downloads the static binary for this platform from the mamba-org GitHub release
+(region ``cn`` also tries the gh-proxy.org mirror, as the reference does), verifies it against
+the SHA-256 digest the release publishes next to it (``micromamba-<plat>.sha256``, fetched
+from the same host) BEFORE it is made executable, then checks ``micromamba --version``.  A
+binary whose digest is missing or differs is deleted and never run.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import platform
 import shutil
 import stat
 import subprocess
-import tarfile
 import tempfile
 import threading
 import urllib.request
@@ -23,11 +25,32 @@ from typing import Callable, Optional
 
 from ._proc import Cancelled
 
-MIRRORS = (
-    "https://micro.mamba.pm/api/micromamba/{plat}/latest",
-    "https://github.com/mamba-org/micromamba-releases/releases/latest/download/micromamba-{plat}",
-    "https://gh-proxy.com/https://github.com/mamba-org/micromamba-releases/releases/latest/download/micromamba-{plat}",
-)
+RELEASE = "https://github.com/mamba-org/micromamba-releases/releases/latest/download/micromamba-{plat}"
+CN_PROXY = "https://gh-proxy.org/"          # reference micromamba_installer.py: region == cn only
+
+
+def mirrors_for(region: str = "other") -> tuple:
+    return (RELEASE, CN_PROXY + RELEASE) if region == "cn" else (RELEASE,)
+
+
+MIRRORS = mirrors_for("other")
+
+
+def sha256_file(path) -> str:
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def parse_sha256(text: str) -> Optional[str]:
+    """The first 64-hex-digit token of a ``.sha256`` sidecar (``<digest>  <name>`` or bare)."""
+    for tok in text.replace("*", " ").split():
+        t = tok.strip().lower()
+        if len(t) == 64 and all(c in "0123456789abcdef" for c in t):
+            return t
+    return None
 
 
 class MicromambaStatus(Enum):
@@ -55,10 +78,12 @@ def platform_tag() -> str:
 
 
 class MicromambaInstaller:
-    def __init__(self, cache_dir, mirrors=MIRRORS, timeout: float = 60.0):
+    def __init__(self, cache_dir, mirrors=None, timeout: float = 60.0, region: str = "other",
+                 sha256: Optional[str] = None):
         self.cache_dir = Path(os.path.expanduser(str(cache_dir)))
-        self.mirrors = tuple(mirrors)
+        self.mirrors = tuple(mirrors) if mirrors is not None else mirrors_for(region)
         self.timeout = timeout
+        self.sha256 = sha256.lower() if sha256 else None   # pinned digest (else the release sidecar)
 
     @property
     def local_path(self) -> Path:
@@ -112,18 +137,19 @@ class MicromambaInstaller:
         return MicromambaResult(MicromambaStatus.NOT_INSTALLED, message="; ".join(errors) or "no mirrors")
 
     def _fetch(self, url: str) -> None:
+        """Download to a temp file, verify its SHA-256, then move it into place + chmod."""
         with tempfile.TemporaryDirectory() as td:
             tmp = Path(td) / "dl"
             with urllib.request.urlopen(url, timeout=self.timeout) as resp, open(tmp, "wb") as f:
                 shutil.copyfileobj(resp, f)
-            if tarfile.is_tarfile(tmp):   # micro.mamba.pm serves a .tar.bz2 with bin/micromamba
-                with tarfile.open(tmp) as tf:
-                    member = next((mm for mm in tf.getmembers() if mm.name.endswith("bin/micromamba")), None)
-                    if member is None or not member.isfile():
-                        raise RuntimeError("archive without bin/micromamba")
-                    src = tf.extractfile(member)
-                    with open(self.local_path, "wb") as out:
-                        shutil.copyfileobj(src, out)
-            else:
-                shutil.copyfile(tmp, self.local_path)
+            want = self.sha256
+            if want is None:
+                with urllib.request.urlopen(url + ".sha256", timeout=self.timeout) as resp:
+                    want = parse_sha256(resp.read(4096).decode("utf-8", "replace"))
+            if want is None:
+                raise RuntimeError("no published SHA-256 for the micromamba binary; refusing to install it")
+            got = sha256_file(tmp)
+            if got != want:
+                raise RuntimeError(f"micromamba SHA-256 mismatch: got {got}, expected {want}")
+            shutil.copyfile(tmp, self.local_path)
         self.local_path.chmod(self.local_path.stat().st_mode | stat.S_IXUSR | stat.S_IXGRP | stat.S_IXOTH)

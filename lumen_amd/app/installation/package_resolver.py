@@ -6,10 +6,13 @@ Resolution order:
 2. a wheel already in ``<cache_dir>/wheels``;
 3. this source tree (``pip install <repo root>`` — the gfx950 libraries are built in-tree
    by the native build step, so the tree installs as-is);
-4. the latest GitHub release asset (``LUMEN_RELEASE_REPO``), through the mirror list.
+4. the latest GitHub release asset (``LUMEN_RELEASE_REPO``); region ``cn`` also tries the
+   gh-proxy.org mirror.  A downloaded wheel must match the SHA-256 the release publishes
+   (the asset's ``digest`` field, or a ``<wheel>.sha256`` asset) or it is deleted.
 """
 from __future__ import annotations
 
+import hashlib
 import json
 import os
 import urllib.request
@@ -18,7 +21,7 @@ from pathlib import Path
 from typing import Optional
 
 GITHUB_API = "https://api.github.com/repos/{repo}/releases/latest"
-DOWNLOAD_MIRRORS = ("{url}", "https://gh-proxy.com/{url}", "https://ghfast.top/{url}")
+DOWNLOAD_MIRRORS = ("{url}", "https://gh-proxy.org/{url}")     # the proxy only for region == cn
 PYPI_MIRRORS = {"cn": "https://mirrors.aliyun.com/pypi/simple/", "other": None}
 # preset -> pip extras of the lumen_amd package (reference: cpu/cuda/apple/openvino/rknn/torch)
 PRESET_EXTRAS = {"amd_mi355x": ["rocm"], "cpu": ["cpu"]}
@@ -30,6 +33,7 @@ class PackageSource:
     location: str                   # path or URL
     version: Optional[str] = None
     extras: list = field(default_factory=list)
+    sha256: Optional[str] = None    # published digest of a release asset
 
     def pip_target(self) -> str:
         ex = f"[{','.join(self.extras)}]" if self.extras else ""
@@ -72,10 +76,25 @@ class LumenPackageResolver:
         req = urllib.request.Request(GITHUB_API.format(repo=self.repo), headers={"Accept": "application/vnd.github+json"})
         with urllib.request.urlopen(req, timeout=self.timeout) as r:
             rel = json.load(r)
-        for a in rel.get("assets", []):
-            if a.get("name", "").startswith("lumen_amd-") and a["name"].endswith(".whl"):
-                return PackageSource("release", a["browser_download_url"], rel.get("tag_name"), extras)
+        assets = rel.get("assets", [])
+        for a in assets:
+            name = a.get("name", "")
+            if name.startswith("lumen_amd-") and name.endswith(".whl"):
+                return PackageSource("release", a["browser_download_url"], rel.get("tag_name"), extras,
+                                     sha256=self._asset_digest(a, assets))
         raise RuntimeError(f"release {rel.get('tag_name')} of {self.repo} has no lumen_amd wheel")
+
+    def _asset_digest(self, asset: dict, assets: list) -> Optional[str]:
+        d = asset.get("digest") or ""
+        if d.startswith("sha256:"):
+            return d.split(":", 1)[1].lower()
+        side = next((a for a in assets if a.get("name") == asset.get("name", "") + ".sha256"), None)
+        if side is None:
+            return None
+        from .micromamba import parse_sha256
+
+        with urllib.request.urlopen(side["browser_download_url"], timeout=self.timeout) as r:
+            return parse_sha256(r.read(4096).decode("utf-8", "replace"))
 
     def download(self, src: PackageSource) -> PackageSource:
         """Fetch a release asset into <cache>/wheels (mirror list)."""
@@ -85,10 +104,18 @@ class LumenPackageResolver:
         dst.parent.mkdir(parents=True, exist_ok=True)
         errs = []
         mirrors = DOWNLOAD_MIRRORS if self.region == "cn" else DOWNLOAD_MIRRORS[:1]
+        if not src.sha256:
+            raise RuntimeError(f"{src.location}: the release publishes no SHA-256 digest; refusing to install it")
         for m in mirrors:
             try:
+                h = hashlib.sha256()
                 with urllib.request.urlopen(m.format(url=src.location), timeout=self.timeout) as r, open(dst, "wb") as f:
-                    f.write(r.read())
+                    for chunk in iter(lambda: r.read(1 << 20), b""):
+                        h.update(chunk)
+                        f.write(chunk)
+                if h.hexdigest() != src.sha256:
+                    dst.unlink(missing_ok=True)
+                    raise RuntimeError(f"SHA-256 mismatch: got {h.hexdigest()}, expected {src.sha256}")
                 return PackageSource("wheel", str(dst), src.version, src.extras)
             except Exception as e:  # noqa: BLE001
                 errs.append(str(e))

@@ -32,6 +32,7 @@
 
 #include "common.h"
 #include "gemm_epi.h"
+#include "workspace.h"
 
 namespace lumen {
 
@@ -253,29 +254,7 @@ splitk_reduce16_kernel(const float* __restrict__ slabs, int S, int M, int N, voi
 }
 
 static float* split_workspace(size_t bytes, hipStream_t stream) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> cache;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  auto& slot = cache[{dev, stream}];
-  // a graph captured on a stream bakes in the buffer an eager warm-up on that stream allocated
-  // (callers keep such streams private to the graph); nothing is allocated during capture
-  if (slot.second >= bytes) return slot.first;
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
-  if (slot.first) {   // the stream's earlier users of the old buffer must be done before it goes
-    (void)hipStreamSynchronize(stream);
-    (void)hipFree(slot.first);
-  }
-  void* p = nullptr;
-  const size_t want = bytes < ((size_t)32 << 20) ? ((size_t)32 << 20) : bytes;
-  if (hipMalloc(&p, want) != hipSuccess) {
-    slot = {nullptr, 0};
-    return nullptr;
-  }
-  slot = {(float*)p, want};
-  return slot.first;
+  return (float*)stream_workspace(bytes, stream, WS_F8_SPLIT, (size_t)32 << 20);
 }
 
 static int f8_num_cus() {

@@ -25,6 +25,7 @@
 // packages/lumen-clip/src/lumen_clip/backends/onnxrt_backend.py:466-495 runs the CLIP tower
 // through them).
 #include "gemm_epi.h"
+#include "workspace.h"
 
 namespace lumen {
 
@@ -652,23 +653,11 @@ static int pp_num_cus() {
 // per-device partial-accumulator workspace of the phase-shifted persistent kernel
 // (PPS_PART bytes per workgroup); allocated once, outside any stream capture
 static float* pps_workspace(int grid, hipStream_t stream) {
-  static float* ws[64] = {nullptr};
-  static int cap[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (cap[dev] >= grid) return ws[dev];
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
   // measured slower than the plain tile order on the ViT-L/14 shapes (profiles/r2_gemm_pps_phase_v1.txt:
   // workgroups of one row-panel class drift apart and lose the shared L2 panel reads): opt-in
   const char* ph = getenv("LUMEN_GEMM_PHASE");
   if (ph == nullptr || ph[0] == '0') return nullptr;
-  void* p = nullptr;
-  if (hipMalloc(&p, (size_t)grid * PPS_PART) != hipSuccess) return nullptr;
-  if (ws[dev]) (void)hipFree(ws[dev]);
-  ws[dev] = (float*)p;
-  cap[dev] = grid;
-  return ws[dev];
+  return (float*)stream_workspace((size_t)grid * PPS_PART, stream, WS_PP_PERSIST, 0);
 }
 
 template <int FK, int PRIO>
@@ -761,20 +750,7 @@ splitk_reduce_epi_kernel(const float* __restrict__ slabs, int S, int M, int N, v
 }
 
 static float* tail_workspace(size_t bytes, hipStream_t stream) {
-  static float* ws[64] = {nullptr};
-  static size_t cap[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (cap[dev] >= bytes) return ws[dev];
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
-  void* p = nullptr;
-  const size_t want = bytes < ((size_t)64 << 20) ? ((size_t)64 << 20) : bytes;
-  if (hipMalloc(&p, want) != hipSuccess) return nullptr;
-  if (ws[dev]) (void)hipFree(ws[dev]);
-  ws[dev] = (float*)p;
-  cap[dev] = want;
-  return ws[dev];
+  return (float*)stream_workspace(bytes, stream, WS_PP_TAIL, (size_t)64 << 20);
 }
 
 hipError_t gemm_tail_splitk(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc,

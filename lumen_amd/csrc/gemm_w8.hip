@@ -217,6 +217,263 @@ __global__ void __launch_bounds__(64 * NWV) gemm_skinny_w8x2_kernel(const uint16
   }
 }
 
+// t + <8 bf16 of x, 8 bf16 of y> on v_dot2c_f32_bf16.  The pairs are taken by shuffling a
+// bf16x8 view: bit-casting a u32 vector ELEMENT to bf16x2 miscompiles on ROCm 7.2 (every
+// element reads lane 0's dword).
+__device__ __forceinline__ float dot8_bf16(const u32x4_t x, const u32x4_t y, float t) {
+  const bf16x8_t xv = __builtin_bit_cast(bf16x8_t, x), yv = __builtin_bit_cast(bf16x8_t, y);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bf16x2_t p = {xv[2 * j], xv[2 * j + 1]}, q = {yv[2 * j], yv[2 * j + 1]};
+    t = __builtin_amdgcn_fdot2_f32_bf16(p, q, t, false);
+  }
+  return t;
+}
+
+// ============================================================================ decode, M <= 4
+// Row-streaming GEMV.  Every wave streams whole weight rows: one wave instruction reads 1 KiB
+// contiguous of ONE row (lane l: bytes [16 l, 16 l + 16) of a 1024-wide k step).  The k steps
+// run as a two-slot register pipeline of U-step chunks (chunk c + 1 is issued before chunk c is
+// consumed: up to 2 * U * R * 16 B in flight per lane); each 16 fp8 widen to 8 bf16 pairs
+// (v_cvt_scalef32_pk_bf16_fp8) and meet the bf16 activations (L1/L2-resident) in
+// v_dot2c_f32_bf16; every (row, m) partial is reduced over the 64 lanes once at the end.
+// A workgroup = 4 waves x 4 rows = 16 consecutive output columns, so the decode epilogue
+// works on whole 16-column tiles (SwiGLU [gate 8 | up 8] pairing, ssq tiles).  Everything the
+// epilogue reads -- the folded-norm sums of squares, the per-channel scales, bias and residual
+// -- is loaded BEFORE the weight stream, so the tail after the last weight byte is only the
+// reductions and the store (vmcnt retires in issue order: a load issued after the stream
+// would wait behind it).  No MFMA: at M <= 4 the dot products use ~20-40 % of the VALU issue
+// budget while HBM streams.
+template <int MR, int U>
+__global__ void __launch_bounds__(256) gemv_w8_rows_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                           const uint8_t* __restrict__ W, int64_t ldw,
+                                                           const float* __restrict__ scale, void* __restrict__ C,
+                                                           int64_t ldc, int M, int N, int K, GemmEpi ep) {
+  constexpr int R = 4;
+  constexpr int SSQ_MAX = 16;   // ssq tiles per lane: K <= 16 * 64 * 16 = 16384
+  __shared__ float red[16][MR];
+  __shared__ float sc_s[16];
+  __shared__ float rstd_s[MR];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n0 = blockIdx.x * 16;
+
+  // ---- epilogue operands first (see header); straight-line loads at clamped addresses, so no
+  // exec-masked branch makes the compiler drain vmcnt before the weight stream is issued
+  const float scv = scale[min(n0 + (lane & 15), N - 1)];
+  constexpr int SSQ4 = 4;   // float4 ssq loads per lane and row: K <= 4 * 4 * 64 * 16 = 16384
+  const bool rs_pre = MR <= 2 && ep.norm && ep.ssq_in != nullptr && K <= SSQ4 * 4 * 64 * 16;
+  f32x4_t ssq_v[MR <= 2 ? MR : 1][SSQ4];
+  if (rs_pre) {   // wave-uniform
+    const int n4 = ep.ssq_tiles >> 2;
+#pragma unroll
+    for (int m = 0; m < (MR <= 2 ? MR : 1); ++m) {
+      const f32x4_t* p = (const f32x4_t*)(ep.ssq_in + (int64_t)min(m, M - 1) * ep.ssq_tiles);
+#pragma unroll
+      for (int j = 0; j < SSQ4; ++j) ssq_v[m][j] = p[min(lane + j * 64, n4 - 1)];
+    }
+  }
+  const int prow = min(lane, M - 1);
+  const bool full16 = n0 + 16 <= N;
+  const bool pre_bias = ep.bias && !ep.bias_f32 && full16;
+  const bool pre_res = ep.residual && full16;
+  u32x4_t pre_b[2] = {(u32x4_t){0u, 0u, 0u, 0u}, (u32x4_t){0u, 0u, 0u, 0u}};
+  u32x4_t pre_r[2] = {(u32x4_t){0u, 0u, 0u, 0u}, (u32x4_t){0u, 0u, 0u, 0u}};
+  if (pre_bias) {
+    pre_b[0] = *(const u32x4_t*)((const uint16_t*)ep.bias + n0);
+    pre_b[1] = *(const u32x4_t*)((const uint16_t*)ep.bias + n0 + 8);
+  }
+  if (pre_res) {
+    pre_r[0] = *(const u32x4_t*)(ep.residual + (int64_t)prow * ep.ldr + n0);
+    pre_r[1] = *(const u32x4_t*)(ep.residual + (int64_t)prow * ep.ldr + n0 + 8);
+  }
+
+  // ---- weight stream
+  const int r0 = n0 + wid * R;
+  const uint8_t* wp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) wp[r] = W + (int64_t)min(r0 + r, N - 1) * ldw + lane * 16;
+  const uint16_t* ap[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) ap[m] = A + (int64_t)(m < M ? m : 0) * lda + lane * 16;
+  float acc[R][MR];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int m = 0; m < MR; ++m) acc[r][m] = 0.f;
+
+  u32x4_t wb[2][U][R];
+  u32x4_t ab[2][U][MR][2];
+  auto issue = [&](const int slot, const int st0) {   // U full 1024-wide steps
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t ko = (int64_t)(st0 + u) << 10;
+#pragma unroll
+      for (int r = 0; r < R; ++r) wb[slot][u][r] = *(const u32x4_t*)(wp[r] + ko);
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        ab[slot][u][m][0] = *(const u32x4_t*)(ap[m] + ko);
+        ab[slot][u][m][1] = *(const u32x4_t*)(ap[m] + ko + 8);
+      }
+    }
+  };
+  auto consume = [&](const int slot, const int nu) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < nu) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const u32x4_t b0 = fp8x8_to_bf16(wb[slot][u][r][0], wb[slot][u][r][1]);
+          const u32x4_t b1 = fp8x8_to_bf16(wb[slot][u][r][2], wb[slot][u][r][3]);
+#pragma unroll
+          for (int m = 0; m < MR; ++m)
+            acc[r][m] = dot8_bf16(b1, ab[slot][u][m][1], dot8_bf16(b0, ab[slot][u][m][0], acc[r][m]));
+        }
+      }
+    }
+  };
+  // Straight-line steady state (a conditional issue inside the loop makes the waitcnt pass
+  // merge both paths and drain everything), and a sched_barrier after every issue: the machine
+  // scheduler otherwise sinks part of chunk c's loads below chunk c + 1's.
+  const int nfull = K >> 10;
+  const int nch = nfull / U;
+  if (nch > 0) {
+    issue(0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    int c = 0;
+    for (; c + 2 < nch; c += 2) {
+      issue(1, (c + 1) * U);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(0, U);
+      __builtin_amdgcn_sched_barrier(0);
+      issue(0, (c + 2) * U);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(1, U);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (c + 1 < nch) {
+      issue(1, (c + 1) * U);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(0, U);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(1, U);
+    } else {
+      consume(0, U);
+    }
+  }
+  // remainder: full steps past the last chunk, then the partial step (K % 1024; Qwen2: 896,
+  // 4864), whose lanes past K load a clamped in-row address and zero their activations
+  for (int st = nch * U; st < nfull; ++st) {
+    const int64_t ko = (int64_t)st << 10;
+#pragma unroll
+    for (int r = 0; r < R; ++r) wb[0][0][r] = *(const u32x4_t*)(wp[r] + ko);
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      ab[0][0][m][0] = *(const u32x4_t*)(ap[m] + ko);
+      ab[0][0][m][1] = *(const u32x4_t*)(ap[m] + ko + 8);
+    }
+    consume(0, 1);
+  }
+  if ((K & 1023) != 0) {
+    const int k = (nfull << 10) + lane * 16;
+    const bool ok = k < K;
+    const int64_t ko = ok ? k - lane * 16 : K - 16 - lane * 16;
+#pragma unroll
+    for (int r = 0; r < R; ++r) wb[0][0][r] = *(const u32x4_t*)(wp[r] + ko);
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      const u32x4_t a0 = *(const u32x4_t*)(ap[m] + ko), a1 = *(const u32x4_t*)(ap[m] + ko + 8);
+      ab[0][0][m][0] = ok ? a0 : (u32x4_t){0u, 0u, 0u, 0u};
+      ab[0][0][m][1] = ok ? a1 : (u32x4_t){0u, 0u, 0u, 0u};
+    }
+    consume(0, 1);
+  }
+
+  // ---- reductions + epilogue
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      const float v = wave_sum(acc[r][m]);
+      if (lane == 0) red[wid * R + r][m] = v;
+    }
+  if (tid < 16) sc_s[tid] = scv;
+  if (ep.norm) {
+    if (rs_pre) {
+      if (wid == 0) {
+        const int n4 = ep.ssq_tiles >> 2;
+#pragma unroll
+        for (int m = 0; m < (MR <= 2 ? MR : 1); ++m) {
+          float t = 0.f;
+#pragma unroll
+          for (int j = 0; j < SSQ4; ++j)
+            if (lane + j * 64 < n4) t += (ssq_v[m][j][0] + ssq_v[m][j][1]) + (ssq_v[m][j][2] + ssq_v[m][j][3]);
+          t = wave_sum(t);
+          if (lane == 0 && m < M) rstd_s[m] = rsqrtf(t / (float)K + ep.norm_eps);
+        }
+      }
+    } else {
+      skinny_rstd<4>(A, lda, M, K, ep, rstd_s);
+    }
+  }
+  __syncthreads();
+  if (tid < M) {
+    float v[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[c] = red[c][tid] * sc_s[c];
+    if (ep.norm) {
+      const float rs = rstd_s[tid];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] *= rs;
+    }
+    const bool fast = full16 && !ep.bias_f32 && !ep.act && !ep.out_f32 && ep.out_group == 0 && !ep.table &&
+                      !ep.prelu && !ep.post_act && ep.alpha == 1.f;
+    if (fast) {   // bias / residual from the prologue registers (lane tid < M loaded row tid)
+      if (pre_bias) {
+        float f[8];
+        unpack8(pre_b[0], f);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] += f[q];
+        unpack8(pre_b[1], f);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[8 + q] += f[q];
+      }
+      if (ep.glu) {
+        float g[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) g[q] = v[q] * fast_rcp(1.f + __expf(-v[q])) * v[8 + q];
+        *(u32x4_t*)((uint16_t*)C + (int64_t)tid * ldc + (n0 >> 1)) = pack8(g);
+        return;
+      }
+      if (pre_res) {
+        float f[8];
+        unpack8(pre_r[0], f);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] += f[q];
+        unpack8(pre_r[1], f);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[8 + q] += f[q];
+      }
+      const u32x4_t o0 = pack8(v), o1 = pack8(v + 8);
+      uint16_t* o = (uint16_t*)C + (int64_t)tid * ldc + n0;
+      *(u32x4_t*)o = o0;
+      *(u32x4_t*)(o + 8) = o1;
+      if (ep.ssq_out) {
+        float f[16], t = 0.f;
+        unpack8(o0, f);
+        unpack8(o1, f + 8);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) t += f[q] * f[q];
+        ep.ssq_out[(int64_t)tid * ep.ssq_tiles + (n0 >> 4)] = t;
+      }
+    } else {
+      GemmEpi e2 = ep;
+      e2.norm = 0;   // rstd applied above
+      epi_store16_dec(v, 1.f, tid, n0, M, N, C, ldc, e2);
+    }
+  }
+}
+
 // ============================================================================ prefill
 template <int BM, int BN, int WM, int WN>
 __global__ void __launch_bounds__(WM* WN * 64)
@@ -362,6 +619,23 @@ hipError_t gemm_w8(const uint16_t* A, int64_t lda, const uint8_t* W, int64_t ldw
                    int64_t ldc, int M, int N, int K, const GemmEpi& ep, float* ws, uint32_t* cnt, int ksplit,
                    hipStream_t stream) {
   if (K % 64 != 0 || M <= 0) return hipErrorInvalidValue;
+  static const int dec_v = [] {
+    const char* e = getenv("LUMEN_W8_DEC");
+    return e ? atoi(e) : 1;
+  }();
+  if (M <= 4 && dec_v > 0) {
+    const dim3 grid((N + 15) / 16);
+#define ROWS_LAUNCH(MR_, U_)                                                                                      \
+  hipLaunchKernelGGL((gemv_w8_rows_kernel<MR_, U_>), grid, dim3(256), 0, stream, A, lda, W, ldw, scale, C, ldc, M, \
+                     N, K, ep)
+    if (dec_v == 2) {
+      if (M == 1) ROWS_LAUNCH(1, 4); else if (M == 2) ROWS_LAUNCH(2, 4); else ROWS_LAUNCH(4, 2);
+    } else {
+      if (M == 1) ROWS_LAUNCH(1, 2); else if (M == 2) ROWS_LAUNCH(2, 2); else ROWS_LAUNCH(4, 1);
+    }
+#undef ROWS_LAUNCH
+    return hipGetLastError();
+  }
   if (M <= 32) {
     // LUMEN_W8_SKINNY: bit 0 = non-temporal weight loads, bit 1 = 8 k blocks per wave in flight;
     // LUMEN_W8_SKINNY_NW: waves per workgroup (4, 8 or 16) for M <= 16; 4 measured fastest

@@ -53,6 +53,7 @@ struct DecodeArgs {
   uint16_t* k_cache_w;    // writable views of the caches
   uint16_t* v_cache_w;
   int kv_fp8;             // caches hold e4m3fn bytes: widened to bf16 on load (cvt_scalef32_pk_bf16_fp8)
+  uint32_t* split_cnt;    // [B, Hkv] zeroed tickets of the in-launch split combine (nsplit > 1; nsplit <= 32)
 };
 hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream);
 

@@ -8,7 +8,8 @@
 //    (split, kv-head, sequence); the G = H / Hkv query heads sharing a kv head
 //    are the 16 MFMA columns, each wave walks its own 64-token blocks with an
 //    online softmax, the 4 wave states are merged through LDS and — when the
-//    context is split across workgroups — a combine kernel merges the splits.
+//    context is split across workgroups — the last split to finish merges them
+//    (in-launch, ticket counter; no combine kernel).
 //    Both MFMA operands come straight from HBM: S^T = K Q^T reads K rows in a
 //    permuted token order chosen so that each lane's 8 P values are 8
 //    consecutive tokens, which the transposed V cache serves with one 16-byte
@@ -78,12 +79,23 @@ hipError_t rope_kv(const RopeKVArgs& a, hipStream_t stream) {
 }
 
 // ------------------------------------------------------------------------------ paged decode attention
+// One workgroup per (split, kv head, sequence); each wave takes the split's 64-token blocks
+// wid, wid + 4, ...  Per block the wave issues ALL of its K and V fragment loads before any
+// math (one HBM round trip per block instead of K -> softmax -> V), then S^T = K Q^T, the
+// online softmax and O^T += V^T P^T.  The 4 wave states merge through LDS.  A context split
+// over several workgroups is combined IN the launch: every split publishes its (m, l, o)
+// partials with write-through (sc1) stores, draws a ticket from the (sequence, kv head)
+// counter, and the last to arrive merges all splits (sc1 loads) and writes the output --
+// no combine launch (MI355X_MICROARCH.md hand-off rules: sc1 stores drained before the
+// ticket, sc1 loads, no fences; the last arriver re-zeroes the counter for the next launch).
 template <int D, bool F8KV>
 __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
   constexpr int KS = D / 32;   // k-steps of S^T over the head dim
   constexpr int NB = D / 16;   // 16-wide d blocks of O^T
   __shared__ float sm_ml[4][2][16];
   __shared__ float sm_o[4][D][17];
+  __shared__ float sm_c[2][16][32];   // combine: (m, l) of up to 32 splits per query head
+  __shared__ int sm_last;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -94,6 +106,8 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
   const int nblk = (ctx + KV_BLOCK - 1) / KV_BLOCK;
   const int blk0 = split * a.blocks_per_split;
   const int blk1 = min(blk0 + a.blocks_per_split, nblk);
+  const int ns = max(1, (nblk + a.blocks_per_split - 1) / a.blocks_per_split);   // splits holding blocks
+  if (split >= ns) return;
 
   // Q^T fragment (B operand): column = query head hk*G + col (zero beyond G)
   bf16x8_t qf[KS];
@@ -177,28 +191,43 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
     const uint8_t* vb8 = reinterpret_cast<const uint8_t*>(a.v_cache) + kvo;
     const int valid = min(KV_BLOCK, ctx - bi * KV_BLOCK);
 
+    // ---- every K and V fragment of the block in flight at once
     // S^T tiles: tile kb16 = (s = kb16 >> 1, hf = kb16 & 1); MFMA row i <-> token
     // 32s + 8(i >> 2) + 4hf + (i & 3), so C row 4g + r holds token 32s + 8g + 4hf + r.
-    f32x4_t sc[4];
+    bf16x8_t kf[4][KS];
+    bf16x8_t vf[2][NB];
+    const int64_t vro = (int64_t)col * KV_BLOCK + 8 * g;
 #pragma unroll
     for (int kb16 = 0; kb16 < 4; ++kb16) {
       const int tok = 32 * (kb16 >> 1) + 8 * (col >> 2) + 4 * (kb16 & 1) + (col & 3);
-      bf16x8_t kf[KS];
-      if constexpr (F8KV) {
-        const uint8_t* kr = kb8 + (int64_t)tok * D + g * 8;
 #pragma unroll
-        for (int t = 0; t < KS; ++t) {
-          const uint2 w = *(const uint2*)(kr + t * 32);
-          kf[t] = __builtin_bit_cast(bf16x8_t, fp8x8_to_bf16(w.x, w.y));
+      for (int t = 0; t < KS; ++t) {
+        if constexpr (F8KV) {
+          const uint2 w = *(const uint2*)(kb8 + (int64_t)tok * D + g * 8 + t * 32);
+          kf[kb16][t] = __builtin_bit_cast(bf16x8_t, fp8x8_to_bf16(w.x, w.y));
+        } else {
+          kf[kb16][t] = *(const bf16x8_t*)(kb + (int64_t)tok * D + g * 8 + t * 32);
         }
-      } else {
-        const uint16_t* kr = kb + (int64_t)tok * D + g * 8;
-#pragma unroll
-        for (int t = 0; t < KS; ++t) kf[t] = *(const bf16x8_t*)(kr + t * 32);
       }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        if constexpr (F8KV) {
+          const uint2 w = *(const uint2*)(vb8 + vro + 32 * s + (int64_t)j * 16 * KV_BLOCK);
+          vf[s][j] = __builtin_bit_cast(bf16x8_t, fp8x8_to_bf16(w.x, w.y));
+        } else {
+          vf[s][j] = *(const bf16x8_t*)(vb + vro + 32 * s + (int64_t)j * 16 * KV_BLOCK);
+        }
+      }
+
+    f32x4_t sc[4];
+#pragma unroll
+    for (int kb16 = 0; kb16 < 4; ++kb16) {
       sc[kb16] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int t = 0; t < KS; ++t) sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t], qf[t], sc[kb16], 0, 0, 0);
+      for (int t = 0; t < KS; ++t) sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kb16][t], qf[t], sc[kb16], 0, 0, 0);
     }
     float mx = mrow;
 #pragma unroll
@@ -230,28 +259,29 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) o[j] *= alpha;
 
+    // a partial block: V columns past the context may hold any finite stale value (p = 0 there),
+    // but zero them anyway so that a never-written slot cannot inject a NaN through 0 * NaN
+    if (valid < KV_BLOCK) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (32 * s + 8 * g + e >= valid) {
+#pragma unroll
+            for (int j = 0; j < NB; ++j) vf[s][j][e] = (__bf16)0.f;
+          }
+    }
     // O^T += V^T P^T over two 32-token steps; lane's P k-slots 8g + j = tokens 32s + 8g + j
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      if (32 * s >= valid) break;
       bf16x8_t pf;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         pf[r] = (__bf16)sc[2 * s][r];
         pf[4 + r] = (__bf16)sc[2 * s + 1][r];
       }
-      const int64_t vro = (int64_t)col * KV_BLOCK + 32 * s + 8 * g;
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        bf16x8_t vf;
-        if constexpr (F8KV) {
-          const uint2 w = *(const uint2*)(vb8 + vro + (int64_t)j * 16 * KV_BLOCK);
-          vf = __builtin_bit_cast(bf16x8_t, fp8x8_to_bf16(w.x, w.y));
-        } else {
-          vf = *(const bf16x8_t*)(vb + vro + (int64_t)j * 16 * KV_BLOCK);
-        }
-        o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[j], 0, 0, 0);
-      }
+      for (int j = 0; j < NB; ++j) o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[s][j], pf, o[j], 0, 0, 0);
     }
   }
 
@@ -280,35 +310,63 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
       }
     }
     const int h = hk * G + q;
-    if (a.nsplit == 1) {
+    if (ns == 1) {
       a.o[(int64_t)b * a.o_sb + (int64_t)h * D + d] = f2bf(L > 0.f ? O / L : 0.f);
     } else {
       const int64_t pi = ((int64_t)b * a.H + h) * a.nsplit + split;
-      a.part_o[pi * D + d] = O;
+      __hip_atomic_store(a.part_o + pi * D + d, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (d == 0) {
-        a.part_ml[pi * 2] = M;
-        a.part_ml[pi * 2 + 1] = L;
+        __hip_atomic_store(a.part_ml + pi * 2, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.part_ml + pi * 2 + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
-}
+  if (ns == 1) return;
 
-__global__ void decode_combine_kernel(DecodeArgs a, int D) {
-  const int bh = blockIdx.x;
-  const int b = bh / a.H, h = bh - b * a.H;
-  const int64_t base = (int64_t)bh * a.nsplit;
-  // only splits that cover context blocks (the table is sized for the batch bucket's longest sequence)
-  const int nblk = (a.ctx_len[b] + KV_BLOCK - 1) / KV_BLOCK;
-  const int ns = max(1, min(a.nsplit, (nblk + a.blocks_per_split - 1) / a.blocks_per_split));
-  float M = -INFINITY;
-  for (int s = 0; s < ns; ++s) M = fmaxf(M, a.part_ml[(base + s) * 2]);
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+  // ---- in-launch combine: the last split of (b, hk) to arrive merges all ns splits
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t* c = a.split_cnt + (int64_t)b * a.Hkv + hk;
+    const uint32_t prev = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = prev == (uint32_t)ns - 1;
+    if (last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sm_last = last ? 1 : 0;
+  }
+  __syncthreads();
+  if (!sm_last) return;
+  for (int i = tid; i < G * ns; i += 256) {
+    const int q = i / ns, sp = i - q * ns;
+    const int64_t pi = ((int64_t)b * a.H + hk * G + q) * a.nsplit + sp;
+    sm_c[0][q][sp] = __hip_atomic_load(a.part_ml + pi * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sm_c[1][q][sp] = __hip_atomic_load(a.part_ml + pi * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  for (int idx = tid; idx < G * D; idx += 256) {
+    const int q = idx / D, d = idx - q * D;
+    const int h = hk * G + q;
+    const int64_t pi0 = ((int64_t)b * a.H + h) * a.nsplit;
+    float M = -INFINITY;
+    for (int sp = 0; sp < ns; ++sp) M = fmaxf(M, sm_c[0][q][sp]);
     float L = 0.f, O = 0.f;
     if (M != -INFINITY) {
-      for (int s = 0; s < ns; ++s) {
-        const float e = __builtin_amdgcn_exp2f(a.part_ml[(base + s) * 2] - M);
-        L += a.part_ml[(base + s) * 2 + 1] * e;
-        O += a.part_o[(base + s) * D + d] * e;
+      // 8 splits' partial loads in flight per round trip (a dependent load per split made the
+      // merge a chain of ns L2 round trips); accumulation in split order: deterministic
+      for (int s0 = 0; s0 < ns; s0 += 8) {
+        float pv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int sp = min(s0 + j, ns - 1);
+          pv[j] = __hip_atomic_load(a.part_o + (pi0 + sp) * D + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (s0 + j < ns) {
+            const float e = __builtin_amdgcn_exp2f(sm_c[0][q][s0 + j] - M);
+            L += sm_c[1][q][s0 + j] * e;
+            O += pv[j] * e;
+          }
+        }
       }
     }
     a.o[(int64_t)b * a.o_sb + (int64_t)h * D + d] = f2bf(L > 0.f ? O / L : 0.f);
@@ -316,6 +374,7 @@ __global__ void decode_combine_kernel(DecodeArgs a, int D) {
 }
 
 hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream) {
+  if (a.nsplit > 32 || (a.nsplit > 1 && a.split_cnt == nullptr)) return hipErrorInvalidValue;
   dim3 grid(a.nsplit, a.Hkv, B), block(256);
 #define PD_LAUNCH(D_)                                                                           \
   do {                                                                                          \
@@ -327,7 +386,6 @@ hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream) {
   else if (D == 32) PD_LAUNCH(32);
   else return hipErrorInvalidValue;
 #undef PD_LAUNCH
-  if (a.nsplit > 1) hipLaunchKernelGGL(decode_combine_kernel, dim3(B * a.H), dim3(128), 0, stream, a, D);
   return hipGetLastError();
 }
 

@@ -62,17 +62,9 @@ hipError_t row_topk(const float* scores, int64_t ld, int B, int N, int k, float 
 int topk_chunks(int N);
 }  // namespace lumen
 
-namespace {
-
-#define LUMEN_CHECK_HIP(expr)                                                          \
-  do {                                                                                 \
-    hipError_t _e = (expr);                                                            \
-    TORCH_CHECK(_e == hipSuccess, "lumen HIP error: ", hipGetErrorString(_e), " @ ", #expr); \
-  } while (0)
-
-inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
-
-// Split-K arrival counters of the skinny (decode) GEMMs, one per 16-column tile.  The
+namespace lumen {
+// Split-K arrival counters of the skinny (decode) GEMMs (one per 16-column tile) and of the
+// decode attention's in-launch split combine (one per sequence x kv head).  The
 // last K-split workgroup of a tile to arrive reduces the slabs and resets its counter
 // to 0, so the buffer is all-zero between kernels.  Kept per (device, stream): split-K
 // GEMMs on different streams may run concurrently and must not share tiles.  A buffer
@@ -89,6 +81,19 @@ uint32_t* splitk_counters(const at::Tensor& like, int64_t tiles) {
     t = at::zeros({std::max<int64_t>(tiles, 16384)}, like.options().dtype(at::kInt));
   return reinterpret_cast<uint32_t*>(t.data_ptr());
 }
+}  // namespace lumen
+
+namespace {
+
+#define LUMEN_CHECK_HIP(expr)                                                          \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    TORCH_CHECK(_e == hipSuccess, "lumen HIP error: ", hipGetErrorString(_e), " @ ", #expr); \
+  } while (0)
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+using lumen::splitk_counters;
 inline const uint16_t* bf(const at::Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
 inline uint16_t* bfm(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
 

@@ -8,6 +8,10 @@
 
 #include "llm.h"
 
+namespace lumen {
+uint32_t* splitk_counters(const at::Tensor& like, int64_t tiles);   // ops.cpp
+}
+
 namespace {
 
 #define CHECK_HIP3(expr)                                                                   \
@@ -97,6 +101,8 @@ void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
     TORCH_CHECK(part_ml->scalar_type() == at::kFloat && part_ml->is_contiguous() && part_ml->numel() >= B * H * nsplit * 2,
                 "part_ml");
     a.part_o = part_o->data_ptr<float>(); a.part_ml = part_ml->data_ptr<float>();
+    TORCH_CHECK(nsplit <= 32, "paged_decode: at most 32 context splits");
+    a.split_cnt = lumen::splitk_counters(q, B * Hkv);
   }
   if (pos.has_value() && pos->defined()) {   // fused RoPE + current-token cache write
     TORCH_CHECK(D == 64 || D == 128, "paged_decode: fused rope needs head dim 64 or 128");

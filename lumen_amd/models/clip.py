@@ -377,12 +377,13 @@ class VisionTower(nn.Module):
         x = x.view(B, S, W)
         return x[:, 1:] if drop_cls else x
 
-    def preprocess(self, images, mean, std, filter: str = "pil_bicubic") -> torch.Tensor:
-        """uint8 HWC images -> patch rows [B*P, kpad] (squash resize, no crop: the ONNX path)."""
+    def preprocess(self, images, mean, std, filter: str = "pil_bicubic", center_crop: bool = False) -> torch.Tensor:
+        """uint8 HWC images -> patch rows [B*P, kpad]: squash resize (the reference's ONNX
+        runtime) or shortest-side resize + centre crop (its torch / open_clip runtime)."""
         s = self.cfg.image_size
         return ops.image_prep(images, (s, s), mean=mean, std=std, filter=filter, layout="patches",
                               patch=self.cfg.patch_size, kpad=self.kpad, out_dtype=self.patch_w.dtype,
-                              device=self.patch_w.device)
+                              device=self.patch_w.device, center_crop=center_crop)
 
     def preprocess_nchw_to_patches(self, pix: torch.Tensor) -> torch.Tensor:
         """Already-normalised NCHW float pixels -> patch rows (used for parity tests)."""
@@ -522,6 +523,7 @@ class CLIPModel(nn.Module):
     def __init__(self, cfg: CLIPConfig, dtype=torch.bfloat16, device=None, with_text: bool = True):
         super().__init__()
         self.cfg = cfg
+        self.center_crop = False   # preprocessor: see encode_image_uint8
         if cfg.vision_arch == "fastvit":
             self.visual = FastViTTower(cfg.fastvit, cfg.embed_dim, dtype, device)
         else:
@@ -548,10 +550,14 @@ class CLIPModel(nn.Module):
     # ---- public API (mirrors the reference backend contract: unit-norm fp32 vectors)
     @torch.no_grad()
     def encode_image_uint8(self, images) -> torch.Tensor:
+        """uint8 HWC images -> unit fp32 embeddings.  ``self.center_crop`` picks the
+        preprocessor: False = squash resize (reference ONNX runtime, onnxrt_backend.py:410-431),
+        True = shortest side + centre crop (reference torch runtime, torch_backend.py:201-204)."""
+        crop = self.center_crop
         if self.cfg.vision_arch == "fastvit":
-            x = self.visual.preprocess(images, self.cfg.image_mean, self.cfg.image_std)
+            x = self.visual.preprocess(images, self.cfg.image_mean, self.cfg.image_std, center_crop=crop)
             return self.visual.forward_embed(x)
-        patches = self.visual.preprocess(images, self.cfg.image_mean, self.cfg.image_std)
+        patches = self.visual.preprocess(images, self.cfg.image_mean, self.cfg.image_std, center_crop=crop)
         B = patches.shape[0] // self.visual.num_patches
         return self.visual.forward_patches(patches, B)
 

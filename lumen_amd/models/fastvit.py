@@ -361,10 +361,10 @@ class FastViTTower(nn.Module):
         emb = self.head(pooled, out_dtype=torch.float32)
         return ops.l2_normalize_(emb.contiguous())
 
-    def preprocess(self, images, mean, std, filter: str = "pil_bicubic") -> torch.Tensor:
+    def preprocess(self, images, mean, std, filter: str = "pil_bicubic", center_crop: bool = False) -> torch.Tensor:
         s = self.cfg.image_size
         return ops.image_prep(images, (s, s), mean=mean, std=std, filter=filter, layout="nhwc8",
-                              out_dtype=self.stem0.w.dtype, device=self.stem0.w.device)
+                              out_dtype=self.stem0.w.dtype, device=self.stem0.w.device, center_crop=center_crop)
 
     # ---------------------------------------------------------------- weights
     def load_timm(self, sd: dict, prefix: str = "") -> None:

@@ -10,6 +10,7 @@ Every op has exactly two implementations:
 """
 from __future__ import annotations
 
+import functools
 import math
 from typing import Optional, Sequence
 
@@ -442,17 +443,31 @@ class ImageGeom:
         return ImageGeom(ih, iw, off, iw, ih, 0, 0, 0, 0, rw, rh)
 
     @staticmethod
+    def center_crop(ih, iw, off, size):
+        """open_clip / torchvision ``Resize(size)`` (shortest side -> size, long side
+        ``int(size * long / short)``) then ``CenterCrop(size)`` (offsets ``int(round(d / 2))``):
+        the resized image is placed at a negative destination offset, so the output window
+        is its centre (reference torch runtime, lumen-clip torch_backend.py:201-204,568-576)."""
+        if iw <= ih:
+            nw, nh = size, int(size * ih / iw)
+        else:
+            nh, nw = size, int(size * iw / ih)
+        top, left = int(round((nh - size) / 2.0)), int(round((nw - size) / 2.0))
+        return ImageGeom(ih, iw, off, iw, ih, 0, 0, -left, -top, nw, nh)
+
+    @staticmethod
     def pad_square(ih, iw, off, out):
         """Centre on a black max(h, w) square, then resize the square to out x out."""
         s = max(ih, iw)
         return ImageGeom(ih, iw, off, s, s, (s - iw) // 2, (s - ih) // 2, 0, 0, out, out)
 
 
-def _ref_resample_axis(img: torch.Tensor, out_len: int, axis: int, filt: int) -> torch.Tensor:
-    """1-D resample of float image [H, W, 3] along axis (0=H, 1=W) matching the kernel."""
-    in_len = img.shape[axis]
+@functools.lru_cache(maxsize=256)
+def _resample_matrix(in_len: int, out_len: int, filt: int) -> torch.Tensor:
+    """[out_len, in_len] fp32 weights of the kernel's 1-D resample (normalised windows;
+    cv2 filters replicate the border by clamping the tap index)."""
     scale = in_len / out_len
-    res = []
+    m = torch.zeros((out_len, in_len), dtype=torch.float32)
     for i in range(out_len):
         if filt >= 2:
             center = (i + 0.5) * scale - 0.5
@@ -469,13 +484,18 @@ def _ref_resample_axis(img: torch.Tensor, out_len: int, axis: int, filt: int) ->
             x1 = min(int(center + sup + 0.5), in_len)
             xs = list(range(x0, x1))
             ws = [_filt((x - center + 0.5) / ss, filt) for x in xs]
-        wt = torch.tensor(ws, dtype=torch.float32)
-        wt = wt / wt.sum() if float(wt.sum()) != 0 else wt * 0
-        sl = img.index_select(axis, torch.tensor(xs))
-        shape = [1, 1, 1]
-        shape[axis] = len(xs)
-        res.append((sl * wt.view(shape)).sum(axis, keepdim=True))
-    out = torch.cat(res, axis)
+        tot = sum(ws)
+        for x, w in zip(xs, ws):
+            m[i, x] += w / tot if tot != 0 else 0.0
+    return m
+
+
+def _ref_resample_axis(img: torch.Tensor, out_len: int, axis: int, filt: int) -> torch.Tensor:
+    """1-D resample of float image [H, W, 3] along axis (0=H, 1=W) matching the kernel
+    (one matmul with the cached weight matrix; PIL filters round to uint8 after each pass,
+    cv2 filters after the vertical one)."""
+    w = _resample_matrix(img.shape[axis], out_len, filt)
+    out = torch.einsum("oi,iwc->owc", w, img) if axis == 0 else torch.einsum("oi,hic->hoc", w, img)
     if filt < 2 or axis == 0:
         out = out.round().clamp(0, 255)
     return out
@@ -509,8 +529,12 @@ def image_prep(
     out_dtype: torch.dtype = torch.float32,
     device=None,
     src: Optional[torch.Tensor] = None,
+    center_crop: bool = False,
 ) -> torch.Tensor:
     """Resize/pad/normalise a batch of uint8 HWC RGB images into one tensor.
+
+    ``center_crop``: shortest side -> OH then the centre OH x OW window (open_clip's
+    transform, :meth:`ImageGeom.center_crop`) instead of squashing to (OH, OW).
 
     ``src``: the images already on the device as one flat uint8 tensor (PinnedUploader);
     ``geoms`` then carry the offsets into it and ``images`` only provide the shapes.
@@ -532,7 +556,11 @@ def image_prep(
         off = 0
         geoms = []
         for im in imgs:
-            geoms.append(ImageGeom.resize(im.shape[0], im.shape[1], off, OH, OW))
+            if center_crop:
+                assert OH == OW, "center_crop needs a square output"
+                geoms.append(ImageGeom.center_crop(im.shape[0], im.shape[1], off, OH))
+            else:
+                geoms.append(ImageGeom.resize(im.shape[0], im.shape[1], off, OH, OW))
             off += im.numel()
     lay = LAYOUTS[layout]
     filt = FILTERS[filter]
@@ -566,7 +594,9 @@ def image_prep(
         t = _ref_resample_axis(canvas, gg.dw, 1, filt)
         t = _ref_resample_axis(t, gg.dh, 0, filt)
         full = torch.full((OH, OW, 3), float(pad))
-        full[gg.dy:gg.dy + gg.dh, gg.dx:gg.dx + gg.dw] = t
+        y0, x0 = max(gg.dy, 0), max(gg.dx, 0)                      # crop geometries: dx, dy < 0
+        y1, x1 = min(gg.dy + gg.dh, OH), min(gg.dx + gg.dw, OW)
+        full[y0:y1, x0:x1] = t[y0 - gg.dy:y1 - gg.dy, x0 - gg.dx:x1 - gg.dx]
         if swap_rb:
             full = full.flip(-1)
         v = (full * scale - torch.tensor(mean, dtype=torch.float32)) / torch.tensor(std, dtype=torch.float32)

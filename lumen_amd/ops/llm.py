@@ -79,14 +79,16 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor, H: int,
             v_cache[blk, :, :, off] = vt.to(v_cache.dtype)
 
 
-_DECODE_TARGET_WG = int(os.environ.get("LUMEN_DECODE_TARGET_WG", "512"))
+_DECODE_TARGET_WG = 512
+_DECODE_MAX_SPLITS = 32        # the in-launch split combine merges at most 32 splits per kv head
 
 
 def decode_splits(B: int, Hkv: int, max_blocks: int, target_wg: Optional[int] = None) -> tuple[int, int]:
-    """(nsplit, blocks_per_split): enough workgroups to fill 256 CUs, >= 4 blocks (one per wave) per split."""
+    """(nsplit, blocks_per_split): enough workgroups to fill 256 CUs, >= 4 blocks (one per wave) per
+    split, at most 32 splits (longer contexts give each wave several blocks)."""
     target_wg = _DECODE_TARGET_WG if target_wg is None else target_wg
     want = max(1, -(-target_wg // max(B * Hkv, 1)))
-    nsplit = max(1, min(want, -(-max_blocks // 4)))
+    nsplit = max(1, min(want, -(-max_blocks // 4), _DECODE_MAX_SPLITS))
     bps = -(-max_blocks // nsplit)
     nsplit = -(-max_blocks // bps)
     return nsplit, bps

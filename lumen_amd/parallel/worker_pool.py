@@ -8,12 +8,19 @@ batcher runs several dispatcher threads (``concurrency``), each handing a whole 
 batch to :meth:`GPUWorkerPool.submit` (least in-flight worker), so every GPU has up to
 two batches queued: host decode / transfer of the next batch overlaps the current one.
 :meth:`GPUWorkerPool.run` (split one batch into per-worker shards) stays for SPMD-style
-callers.  Inputs travel pickled over pipes — compressed images (tens of KB) or token
-ids.  Results that are a list of equally shaped numpy rows (embeddings) come back
-through a per-worker shared-memory ring (``shm_slots`` x ``shm_slot_bytes``, created
-by the pool, attached by the worker): the worker writes the stacked array into the next
-slot once the pool has released it (a semaphore per worker), the pool copies it out and
-releases the slot — no pickling of the payload.
+callers.  Payloads move through per-worker shared-memory rings created by the pool
+(``shm_slots`` x ``shm_slot_bytes`` each way), never pickled through the pipe:
+
+* inputs that are a list of ``bytes`` (compressed images): the pool packs the batch into
+  the next free input slot (a semaphore counts free slots, the worker releases a slot once
+  it has copied the batch out) and sends only the offsets;
+* results that are a list of equally shaped numpy rows (embeddings): the worker writes the
+  stacked array into the next free result slot, the pool copies it out and releases it.
+
+Anything else (token ids, small results, a batch larger than a slot) travels pickled.
+Each spawn of a worker gets a new generation number and fresh rings; ring descriptors
+carry the generation, so a message a dead worker left queued is dropped instead of
+reading (or releasing a slot of) a ring that no longer exists.
 
 Failure detection: every worker sends a heartbeat each
 ``heartbeat_s``; the monitor thread declares a worker lost when its process exits
@@ -83,13 +90,13 @@ def _as_rows(res):
 
 
 class _ShmRing:
-    """Worker side of the result ring: slot k of ``nslots`` at offset k * slot_bytes."""
+    """Worker side of a ring: slot k of ``nslots`` at offset k * slot_bytes."""
 
-    def __init__(self, name: str, nslots: int, slot_bytes: int, free_sem):
+    def __init__(self, name: str, nslots: int, slot_bytes: int, free_sem, gen: int):
         from multiprocessing import shared_memory
 
         self.shm = shared_memory.SharedMemory(name=name)
-        self.nslots, self.slot_bytes, self.free = nslots, slot_bytes, free_sem
+        self.nslots, self.slot_bytes, self.free, self.gen = nslots, slot_bytes, free_sem, gen
         self.next = 0
 
     def put(self, arr):
@@ -102,13 +109,36 @@ class _ShmRing:
         self.next = (self.next + 1) % self.nslots
         dst = np.ndarray(arr.shape, arr.dtype, buffer=self.shm.buf, offset=slot * self.slot_bytes)
         dst[...] = arr
-        return slot, arr.shape, arr.dtype.str
+        return self.gen, slot, arr.shape, arr.dtype.str
+
+    def take(self, desc) -> list:
+        """Input ring: copy the batch of ``bytes`` items out of its slot, then free the slot."""
+        _gen, slot, ends = desc
+        base = slot * self.slot_bytes
+        buf = self.shm.buf
+        out, a = [], 0
+        for b in ends:
+            out.append(bytes(buf[base + a:base + b]))
+            a = b
+        self.free.release()
+        return out
+
+
+def _as_blobs(items) -> Optional[list]:
+    """Cumulative end offsets when ``items`` is a non-empty list of bytes-like objects."""
+    if not isinstance(items, list) or not items or not all(isinstance(x, (bytes, bytearray, memoryview)) for x in items):
+        return None
+    ends, t = [], 0
+    for x in items:
+        t += len(x)
+        ends.append(t)
+    return ends
 
 
 def _worker_main(wid: int, device: str, factory: str, kwargs: dict, inq, outq, heartbeat_s: float,
-                 shm: Optional[tuple] = None) -> None:
+                 shm: Optional[tuple] = None, shm_in: Optional[tuple] = None) -> None:
     """Child process body: pin device, build the batch fn, serve tasks until None."""
-    ring = None
+    ring = in_ring = None
     try:
         if device.startswith("cuda"):
             import torch
@@ -127,6 +157,8 @@ def _worker_main(wid: int, device: str, factory: str, kwargs: dict, inq, outq, h
         fn = fac(device, **kw)
         if shm is not None:
             ring = _ShmRing(*shm)
+        if shm_in is not None:
+            in_ring = _ShmRing(*shm_in)
     except BaseException:  # noqa: BLE001
         outq.put(("fatal", wid, None, traceback.format_exc()))
         return
@@ -145,10 +177,12 @@ def _worker_main(wid: int, device: str, factory: str, kwargs: dict, inq, outq, h
         if msg is None:
             alive.set()
             break
-        tid, kind, items = msg
+        tid, kind, items, in_desc = msg
         if kill_after is not None and done >= kill_after:
             os._exit(17)
         try:
+            if in_desc is not None:
+                items = in_ring.take(in_desc)
             res = fn(kind, items)
             arr = _as_rows(res) if ring is not None else None
             desc = ring.put(arr) if arr is not None and arr.nbytes >= _SHM_MIN_BYTES else None
@@ -173,7 +207,12 @@ class _Worker:
     inflight: dict = field(default_factory=dict)   # tid -> (Future, submit time)
     restarts: int = 0
     shm: Any = None          # SharedMemory of the result ring (owned by the pool)
-    shm_free: Any = None     # semaphore: free slots of the ring
+    shm_free: Any = None     # semaphore: free slots of the result ring
+    shm_in: Any = None       # SharedMemory of the input ring (owned by the pool)
+    shm_in_free: Any = None  # semaphore: free slots of the input ring
+    in_next: int = 0         # next input slot the pool fills
+    in_lock: Any = field(default_factory=threading.Lock)   # orders slot fill + enqueue per worker
+    gen: int = 0             # spawn generation (tags ring descriptors)
 
 
 class GPUWorkerPool:
@@ -197,7 +236,9 @@ class GPUWorkerPool:
         self._tid = itertools.count(1)
         self._stop = threading.Event()
         self.workers = [_Worker(wid=i, device=d) for i, d in enumerate(devices)]
-        self.stats = {"tasks": 0, "items": 0, "lost": 0, "restarts": 0, "shm_results": 0}
+        self.stats = {"tasks": 0, "items": 0, "lost": 0, "restarts": 0, "shm_results": 0, "shm_inputs": 0,
+                      "stale_dropped": 0}
+        self._gen = itertools.count(1)
         self._fatal: Optional[str] = None
         for w in self.workers:
             self._start(w)
@@ -209,37 +250,46 @@ class GPUWorkerPool:
 
     # ------------------------------------------------------------------ lifecycle
     def _start(self, w: _Worker) -> None:
+        """(Re)spawn worker w with fresh rings; the caller holds ``self._lock`` on a restart."""
         w.inq = self._ctx.Queue()
         w.ready = False
         w.last_hb = time.time()
+        w.gen = next(self._gen)
+        w.in_next = 0
         kwargs = dict(self.kwargs)
         kwargs.setdefault("_pool_world", len(self.workers))
         self._free_shm(w)
-        shm = None
+        shm = shm_in = None
         if self.shm_slots > 0:
             from multiprocessing import shared_memory
 
             try:
                 w.shm = shared_memory.SharedMemory(create=True, size=self.shm_slots * self.shm_slot_bytes)
                 w.shm_free = self._ctx.Semaphore(self.shm_slots)
-                shm = (w.shm.name, self.shm_slots, self.shm_slot_bytes, w.shm_free)
-            except OSError as e:   # no /dev/shm space: results travel pickled
-                log.warning("worker %d: no shared-memory ring (%s)", w.wid, e)
-                w.shm = w.shm_free = None
+                shm = (w.shm.name, self.shm_slots, self.shm_slot_bytes, w.shm_free, w.gen)
+                w.shm_in = shared_memory.SharedMemory(create=True, size=self.shm_slots * self.shm_slot_bytes)
+                w.shm_in_free = self._ctx.Semaphore(self.shm_slots)
+                shm_in = (w.shm_in.name, self.shm_slots, self.shm_slot_bytes, w.shm_in_free, w.gen)
+            except OSError as e:   # no /dev/shm space: payloads travel pickled
+                log.warning("worker %d: no shared-memory rings (%s)", w.wid, e)
+                self._free_shm(w)
+                shm = shm_in = None
         w.proc = self._ctx.Process(target=_worker_main, name=f"lumen-worker-{w.wid}",
                                    args=(w.wid, w.device, self.factory, kwargs, w.inq, self._outq,
-                                         self.heartbeat_s, shm), daemon=True)
+                                         self.heartbeat_s, shm, shm_in), daemon=True)
         w.proc.start()
 
     @staticmethod
     def _free_shm(w: _Worker) -> None:
-        if w.shm is not None:
-            try:
-                w.shm.close()
-                w.shm.unlink()
-            except Exception:  # noqa: BLE001
-                pass
-            w.shm = w.shm_free = None
+        for name in ("shm", "shm_in"):
+            seg = getattr(w, name)
+            if seg is not None:
+                try:
+                    seg.close()
+                    seg.unlink()
+                except Exception:  # noqa: BLE001
+                    pass
+        w.shm = w.shm_free = w.shm_in = w.shm_in_free = None
 
     def wait_ready(self, timeout: float) -> None:
         t0 = time.time()
@@ -298,9 +348,31 @@ class GPUWorkerPool:
             w = self.workers[worker] if worker is not None else min(cands, key=lambda x: len(x.inflight))
             tid = next(self._tid)
             w.inflight[tid] = (fut, time.time())
-            w.inq.put((tid, kind, items))
             self.stats["tasks"] += 1
             self.stats["items"] += len(items)
+            gen, seg, free, inq = w.gen, w.shm_in, w.shm_in_free, w.inq
+        ends = _as_blobs(items) if seg is not None else None
+        if ends is None or ends[-1] > self.shm_slot_bytes:
+            inq.put((tid, kind, items, None))
+            return fut
+        # input ring: wait for a free slot OUTSIDE the pool lock (back-pressure on this caller
+        # only); the per-worker lock keeps slot order == queue order, which the worker relies on
+        with w.in_lock:
+            while not free.acquire(timeout=0.5):
+                if self._stop.is_set() or w.gen != gen:   # worker respawned: its ring is gone
+                    return fut                            # (the future was failed by the monitor)
+            if w.gen != gen:
+                return fut
+            slot = w.in_next
+            w.in_next = (slot + 1) % self.shm_slots
+            base, a = slot * self.shm_slot_bytes, 0
+            buf = seg.buf
+            for x, b in zip(items, ends):
+                buf[base + a:base + b] = x
+                a = b
+            inq.put((tid, kind, None, (gen, slot, ends)))
+        with self._lock:
+            self.stats["shm_inputs"] += 1
         return fut
 
     def broadcast(self, kind: str, items: list, timeout: Optional[float] = None) -> list:
@@ -331,31 +403,40 @@ class GPUWorkerPool:
                 continue
             except (EOFError, OSError):
                 break
-            w = self.workers[wid]
-            with self._lock:
-                w.last_hb = time.time()
-                if kind == "ready":
-                    w.ready, w.pid = True, int(payload)
-                elif kind == "fatal":
-                    self._fatal = str(payload)
-                elif kind == "okshm":
-                    payload = self._read_shm(w, payload)
-                    self.stats["shm_results"] += 1
-                    kind = "ok"
-                if kind in ("ok", "err"):
-                    fut, _ = w.inflight.pop(tid, (None, 0.0))
-                    if fut is not None and not fut.done():
-                        if kind == "ok":
-                            fut.set_result(payload)
-                        else:
-                            fut.set_exception(WorkerTaskError(str(payload)))
+            try:
+                self._handle(kind, wid, tid, payload)
+            except Exception:  # noqa: BLE001 -- one bad message must not kill the collector
+                log.exception("worker pool: dropping message %r from worker %s", kind, wid)
+
+    def _handle(self, kind, wid, tid, payload) -> None:
+        w = self.workers[wid]
+        with self._lock:
+            w.last_hb = time.time()
+            if kind == "ready":
+                w.ready, w.pid = True, int(payload)
+            elif kind == "fatal":
+                self._fatal = str(payload)
+            elif kind == "okshm":
+                if payload[0] != w.gen or w.shm is None:   # from a previous spawn: ring is gone
+                    self.stats["stale_dropped"] += 1
+                    return
+                payload = self._read_shm(w, payload)
+                self.stats["shm_results"] += 1
+                kind = "ok"
+            if kind in ("ok", "err"):
+                fut, _ = w.inflight.pop(tid, (None, 0.0))
+                if fut is not None and not fut.done():
+                    if kind == "ok":
+                        fut.set_result(payload)
+                    else:
+                        fut.set_exception(WorkerTaskError(str(payload)))
 
     def _read_shm(self, w: _Worker, desc) -> list:
         """Copy a result out of worker w's ring slot and release the slot (messages of one
         worker arrive in order, so slots are consumed in the order the worker filled them)."""
         import numpy as np
 
-        slot, shape, dt = desc
+        _gen, slot, shape, dt = desc
         arr = np.ndarray(shape, np.dtype(dt), buffer=w.shm.buf, offset=slot * self.shm_slot_bytes).copy()
         w.shm_free.release()
         return list(arr)
@@ -387,9 +468,10 @@ class GPUWorkerPool:
                     w.proc.kill()
                 w.proc.join(timeout=5)
                 if self.respawn and not self._stop.is_set():
-                    w.restarts += 1
-                    self.stats["restarts"] += 1
-                    self._start(w)
+                    with self._lock:   # the collector reads w.shm / w.gen under this lock
+                        w.restarts += 1
+                        self.stats["restarts"] += 1
+                        self._start(w)
                 else:
                     w.proc = None
 

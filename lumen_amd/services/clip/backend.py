@@ -151,6 +151,7 @@ class MI355XClipBackend:
             except (OSError, KeyError, ValueError, RuntimeError, ResourceError) as e:
                 raise ModelLoadingError(f"loading {self.resources.model_name} from "
                                         f"{self.resources.model_root_path}: {e}") from e
+            m.center_crop = torch_runtime_crop(self.resources.runtime)
             self.model = m.to(self.device)
             self._logit_scale = self.model.logit_scale
         self._load_tokenizer()
@@ -264,6 +265,12 @@ class MI355XClipBackend:
                                            "context_length": str(self.context_length)})
 
 
+def torch_runtime_crop(runtime) -> bool:
+    """The reference's two CLIP preprocessors: its torch runtime (open_clip / HF processors)
+    resizes the shortest side and centre-crops; its ONNX runtime squashes to the model size."""
+    return str(getattr(runtime, "value", runtime)).lower() == "torch"
+
+
 def dp_worker(device: str, cache_dir: str, model: str, runtime: str, dataset: Optional[str] = None,
               shard_bank: bool = False, rank: int = 0, world: int = 1):
     """GPUWorkerPool factory: one CLIP replica on ``device``; fn(kind, items) -> embeddings.
@@ -283,6 +290,7 @@ def dp_worker(device: str, cache_dir: str, model: str, runtime: str, dataset: Op
     cfg.image_mean, cfg.image_std = tuple(mean), tuple(std)
     m = CLIPModel(cfg, dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32, device="cpu")
     m.load_state_dict_any(load_weights(res.model_root_path))
+    m.center_crop = torch_runtime_crop(runtime)
     m = m.to(dev)
     bank = None
     if shard_bank and res.label_embeddings is not None:

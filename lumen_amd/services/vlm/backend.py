@@ -290,7 +290,10 @@ class MI355XVLMBackend:
         cached = None
         if shard_cache.enabled() and (self.tp.enabled or fp8) and self.device.type == "cuda" and \
                 not self.resources.extra.get("random_init"):
-            cached = (shard_cache.shard_path(root, self.tp.world, self.tp.rank, "fp8" if fp8 else "bf16"),
+            # key: the compute dtype AND the configured precision -- two non-fp8 precisions pick
+            # different ONNX pack files from the same directory (find_vlm_pack)
+            prec = (self.resources.precision or "default").lower().replace("/", "_")
+            cached = (shard_cache.shard_path(root, self.tp.world, self.tp.rank, f"{'fp8' if fp8 else 'bf16'}-{prec}"),
                       shard_cache.source_fingerprint(root), cfg.to_dict())
         if cached is not None and shard_cache.valid(*cached):
             extra = shard_cache.load(m, cached[0], self.device)

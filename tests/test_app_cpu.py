@@ -1,4 +1,5 @@
 """Control plane (FastAPI TestClient): every SURVEY §A.1 endpoint path and response shape."""
+import os
 import time
 
 import pytest
@@ -169,3 +170,78 @@ def test_spa_assets_and_api_coverage(client):
         assert any(p.match(full) for p in pats), f"UI calls {full}, no such route"
     for ws in ("/ws/logs", "/ws/install/"):
         assert ws in js.text
+
+
+# ----------------------------------------------------------------------------- download integrity
+class _Resp:
+    def __init__(self, data: bytes):
+        import io
+
+        self._b = io.BytesIO(data)
+
+    def read(self, n=-1):
+        return self._b.read(n)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _fake_urlopen(table):
+    def urlopen(url, timeout=None):
+        url = getattr(url, "full_url", url)
+        if url not in table:
+            raise OSError(f"404 {url}")
+        return _Resp(table[url])
+    return urlopen
+
+
+def test_micromamba_mirrors_and_checksum(tmp_path, monkeypatch):
+    import hashlib
+
+    from lumen_amd.app.installation import micromamba as mm
+
+    assert all("proxy" not in m for m in mm.mirrors_for("other"))
+    assert any(m.startswith("https://gh-proxy.org/") for m in mm.mirrors_for("cn"))
+    payload = b"#!/bin/sh\necho 2.0.0\n"
+    url = mm.RELEASE.format(plat=mm.platform_tag())
+    digest = hashlib.sha256(payload).hexdigest()
+    inst = mm.MicromambaInstaller(tmp_path)
+    # wrong published digest: the binary is never put in place
+    monkeypatch.setattr(mm.urllib.request, "urlopen", _fake_urlopen({url: payload, url + ".sha256": b"0" * 64}))
+    with pytest.raises(RuntimeError, match="mismatch"):
+        inst._fetch(url)
+    assert not inst.local_path.exists()
+    # no sidecar: refused
+    monkeypatch.setattr(mm.urllib.request, "urlopen", _fake_urlopen({url: payload}))
+    with pytest.raises(OSError):
+        inst._fetch(url)
+    assert not inst.local_path.exists()
+    # matching digest: installed and executable
+    monkeypatch.setattr(mm.urllib.request, "urlopen",
+                        _fake_urlopen({url: payload, url + ".sha256": f"{digest}  micromamba".encode()}))
+    inst.local_path.parent.mkdir(parents=True, exist_ok=True)
+    inst._fetch(url)
+    assert inst.local_path.read_bytes() == payload and os.access(inst.local_path, os.X_OK)
+
+
+def test_release_wheel_download_requires_matching_digest(tmp_path, monkeypatch):
+    import hashlib
+
+    from lumen_amd.app.installation import package_resolver as pr
+
+    data = b"PK\x03\x04 not really a wheel"
+    url = "https://github.com/o/r/releases/download/v1/lumen_amd-1.0-py3-none-any.whl"
+    res = pr.LumenPackageResolver(tmp_path, region="other")
+    monkeypatch.setattr(pr.urllib.request, "urlopen", _fake_urlopen({url: data}))
+    with pytest.raises(RuntimeError, match="no SHA-256"):
+        res.download(pr.PackageSource("release", url, "v1"))
+    with pytest.raises(RuntimeError, match="mismatch"):
+        res.download(pr.PackageSource("release", url, "v1", sha256="ab" * 32))
+    assert not (tmp_path / "wheels" / url.rsplit("/", 1)[-1]).exists()
+    got = res.download(pr.PackageSource("release", url, "v1", sha256=hashlib.sha256(data).hexdigest()))
+    assert got.kind == "wheel" and open(got.location, "rb").read() == data
+    # the asset digest field of the GitHub API is picked up
+    assert res._asset_digest({"name": "x.whl", "digest": "sha256:" + "cd" * 32}, []) == "cd" * 32

@@ -44,6 +44,8 @@ def test_placement_resolve(monkeypatch):
 # ----------------------------------------------------------------------------- pool transport
 def _rows_factory(device, dim=4096):
     def fn(kind, items):
+        if kind == "blobs":      # inputs through the shared-memory input ring
+            return [np.full(dim, float(len(b) + b[0]), np.float32) for b in items]
         if kind == "small":
             return [np.full(3, float(x), np.float32) for x in items]
         return [np.full(dim, float(x), np.float32) for x in items]
@@ -201,3 +203,34 @@ def test_ocr_dp2_matches_single_process(tmp_path, monkeypatch):
         for ia, ib in zip(a["items"], b["items"]):
             assert ia["box"] == ib["box"] and ia["text"] == ib["text"]
             assert abs(ia["confidence"] - ib["confidence"]) < 1e-5
+
+
+def test_shm_input_ring_round_trip_and_fallback():
+    pool = GPUWorkerPool("tests.test_dp_serving_cpu:_rows_factory", ["cpu"], shm_slots=2, shm_slot_bytes=1 << 16)
+    try:
+        batches = [[bytes([i % 251]) * (100 + 37 * k) for k in range(8)] for i in range(12)]   # > slots in flight
+        futs = [pool.submit("blobs", b) for b in batches]
+        for b, f in zip(batches, futs):
+            r = f.result(60)
+            assert [float(x[0]) for x in r] == [float(len(x) + x[0]) for x in b]
+        assert pool.stats["shm_inputs"] == 12
+        big = [bytes([7]) * 40000, bytes([9]) * 40000]               # > one slot: pickled
+        assert [float(x[0]) for x in pool.submit("blobs", big).result(60)] == [40007.0, 40009.0]
+        assert pool.stats["shm_inputs"] == 12
+    finally:
+        pool.close()
+
+
+def test_stale_ring_descriptor_is_dropped():
+    """A result descriptor from a previous spawn of the worker (its ring is gone) is dropped
+    without touching the new ring's semaphore, and the collector keeps running."""
+    pool = GPUWorkerPool("tests.test_dp_serving_cpu:_rows_factory", ["cpu"], shm_slots=2, shm_slot_bytes=1 << 20)
+    try:
+        w = pool.workers[0]
+        pool._handle("okshm", 0, 12345, (w.gen - 1, 0, (4, 4096), "<f4"))
+        assert pool.stats["stale_dropped"] == 1
+        pool._outq.put(("okshm", 0, 999, "garbage"))                  # malformed: logged, not fatal
+        r = pool.submit("rows", list(range(16))).result(60)
+        assert len(r) == 16 and r[3][0] == 3.0
+    finally:
+        pool.close()

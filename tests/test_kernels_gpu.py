@@ -258,3 +258,19 @@ def test_attention_kv_resident_path(B, Sq, Sk, H, Hkv, D, causal):
     ref = ops.attention(q, k, v, causal=causal, kv_len=kl)
     got = ops.attention(q.to(DEV), k.to(DEV), v.to(DEV), causal=causal, kv_len=kl.to(DEV))
     assert _rel(got, ref) < 2e-2
+
+
+def test_image_prep_center_crop_matches_reference():
+    """centre-crop geometry (negative destination offsets) on the HIP prep kernels vs the CPU
+    reference, patch-row layout as the CLIP towers consume it."""
+    g = torch.Generator().manual_seed(3)
+    imgs = [torch.randint(0, 256, (90, 61, 3), generator=g, dtype=torch.uint8),
+            torch.randint(0, 256, (40, 120, 3), generator=g, dtype=torch.uint8)]
+    kw = dict(mean=(0.48, 0.45, 0.40), std=(0.26, 0.26, 0.27), center_crop=True)
+    ref = ops.image_prep(imgs, (32, 32), **kw)
+    got = ops.image_prep([i.to(DEV) for i in imgs], (32, 32), **kw)
+    assert (got.cpu() - ref).abs().max().item() <= 1.01 / (255 * 0.26)
+    refp = ops.image_prep(imgs, (32, 32), layout="patches", patch=8, kpad=256, out_dtype=torch.bfloat16, **kw)
+    gotp = ops.image_prep([i.to(DEV) for i in imgs], (32, 32), layout="patches", patch=8, kpad=256,
+                          out_dtype=torch.bfloat16, **kw)
+    assert (gotp.float().cpu() - refp.float()).abs().max().item() <= 0.05

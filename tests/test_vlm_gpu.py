@@ -221,7 +221,8 @@ def test_prefill_packed_gpu_matches_single(fp8):
 
 def test_vlm_backend_fp8_shard_cache(tmp_path, monkeypatch):
     """precision fp8 on the GPU: the first build writes this rank's quantised shard
-    (.lumen_shards/tp1_r0_fp8.safetensors), the second build loads it (no requantisation) and
+    (.lumen_shards/tp1_r0_fp8-fp8.safetensors: compute dtype + configured precision), the second
+    build loads it (no requantisation) and
     generates the same greedy tokens."""
     from lumen_amd.models.vlm import write_vlm_model
     from lumen_amd.resources.config import ModelConfig, Runtime
@@ -231,7 +232,7 @@ def test_vlm_backend_fp8_shard_cache(tmp_path, monkeypatch):
     write_vlm_model(tmp_path / "models" / "fastvlm-tiny", "fastvlm-tiny")
     res = load_model_resources(tmp_path, ModelConfig(model="fastvlm-tiny", runtime=Runtime.onnx, precision="fp8"))
     settings = type("S", (), {"device": "cuda"})()
-    shard = tmp_path / "models" / "fastvlm-tiny" / ".lumen_shards" / "tp1_r0_fp8.safetensors"
+    shard = tmp_path / "models" / "fastvlm-tiny" / ".lumen_shards" / "tp1_r0_fp8-fp8.safetensors"
     outs = []
     for i in range(2):
         b = create_backend(settings, res, "onnx")

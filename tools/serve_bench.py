@@ -1,0 +1,186 @@
+"""Serving-path benchmark: the real gRPC hub, end to end.
+
+Starts a hub in this process on 127.0.0.1:<free port> with ONE service (synthetic,
+random-init model of the named architecture written into a temp cache by the downloader),
+then drives it with C concurrent gRPC clients.  Each client thread owns a channel and sends
+requests back to back, one ``Infer`` stream per request carrying one JPEG (the reference's
+client pattern: ``src/lumen/server.py:232-235`` serves them on a 10-thread pool, batch 1).
+Everything the service does is inside the measured latency: gRPC transport, chunk
+reassembly, JPEG decode, the dynamic batcher (``LUMEN_MAX_BATCH`` / ``LUMEN_MAX_WAIT_MS``),
+the DP worker pool and its shared-memory rings (``--dp``), the GPU kernels and the JSON
+response.  Reports images/s over the timed window and per-request p50 / p99 latency.
+
+    # BASELINE config 1: CPU ViT-B/32 single-image latency through the service
+    python tools/serve_bench.py --service clip --model CLIP-ViT-B-32 --device cpu --clients 1 --seconds 20
+    # CLIP ViT-L/14 serving on one GPU, 64 concurrent clients
+    python tools/serve_bench.py --service clip --model CLIP-ViT-L-14 --device cuda --clients 64
+    # face detect + embed (SCRFD-10G + IResNet-100) through the service
+    python tools/serve_bench.py --service face --model antelopev2 --device cuda --clients 32
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import threading
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+TASKS = {"clip": "clip_image_embed", "face": "face_detect_and_embed", "ocr": "ocr"}
+REGISTRY = {"clip": ("lumen_clip", "lumen_clip.general_clip.GeneralCLIPService"),
+            "face": ("lumen_face", "lumen_face.general_face.GeneralFaceService"),
+            "ocr": ("lumen_ocr", "lumen_ocr.general_ocr.GeneralOcrService")}
+
+
+def _config(service: str, model: str, device: str, batch: int, cache: str, runtime: str):
+    from lumen_amd.resources.config import LumenConfig
+
+    pkg, reg = REGISTRY[service]
+    mc = {"model": model, "runtime": runtime}
+    if service == "clip":
+        mc["dataset"] = "ImageNet_1k"
+    d = {"metadata": {"version": "1.0.0", "region": "other", "cache_dir": cache},
+         "deployment": {"mode": "hub", "services": [service]},
+         "server": {"port": 50051, "host": "127.0.0.1"},
+         "services": {service: {"enabled": True, "package": pkg,
+                                "import_info": {"registry_class": reg,
+                                                "add_to_server": f"{pkg}.proto.ml_service_pb2_grpc."
+                                                                 "add_InferenceServicer_to_server"},
+                                "backend_settings": {"device": device, "batch_size": batch},
+                                "models": {"general": mc}}}}
+    return LumenConfig.model_validate(d)
+
+
+def _images(n: int, side: int, kind: str, seed: int = 0) -> list[bytes]:
+    from lumen_amd.utils.image import encode_jpeg
+
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        if kind == "noise":
+            a = rng.integers(0, 256, (side, side * 4 // 3, 3), dtype=np.uint8)
+        else:   # photo-like: smooth gradients + a few blobs (compresses like a real photo)
+            h, w = side, side * 4 // 3
+            y, x = np.mgrid[0:h, 0:w].astype(np.float32)
+            a = np.stack([(x / w * 255 + i * 7) % 256, (y / h * 255 + i * 13) % 256,
+                          ((x + y) / (h + w) * 255) % 256], -1)
+            for _ in range(6):
+                cy, cx, r = rng.integers(0, h), rng.integers(0, w), rng.integers(h // 16, h // 4)
+                m = (y - cy) ** 2 + (x - cx) ** 2 < r * r
+                a[m] = rng.integers(0, 256, 3)
+            a = a.astype(np.uint8)
+        out.append(encode_jpeg(a))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--service", choices=sorted(TASKS), default="clip")
+    ap.add_argument("--model", default="CLIP-ViT-L-14")
+    ap.add_argument("--runtime", default="torch")
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--dp", type=int, default=1, help="DP worker processes (LUMEN_DP_SIZE); 1 = in-process")
+    ap.add_argument("--batch", type=int, default=128, help="backend_settings.batch_size (dynamic batcher cap)")
+    ap.add_argument("--max-wait-ms", type=float, default=None, help="LUMEN_MAX_WAIT_MS")
+    ap.add_argument("--clients", type=int, default=32)
+    ap.add_argument("--seconds", type=float, default=20.0, help="timed window after the warm-up")
+    ap.add_argument("--warmup", type=float, default=5.0)
+    ap.add_argument("--image-side", type=int, default=384, help="JPEG height (width = 4/3 height)")
+    ap.add_argument("--image-kind", choices=["photo", "noise"], default="photo")
+    ap.add_argument("--server-threads", type=int, default=None)
+    args = ap.parse_args()
+
+    os.environ["LUMEN_SYNTHETIC"] = "1"
+    if args.dp > 1:
+        os.environ["LUMEN_DP_SIZE"] = str(args.dp)
+    if args.max_wait_ms is not None:
+        os.environ["LUMEN_MAX_WAIT_MS"] = str(args.max_wait_ms)
+    os.environ.setdefault("LUMEN_MAX_BATCH", str(args.batch))
+
+    import grpc
+
+    from lumen_amd.hub.router import HubRouter
+    from lumen_amd.hub.server import AppService, build_server
+    from lumen_amd.proto import ml_service as pb
+    from lumen_amd.resources.downloader import Downloader
+
+    cache = tempfile.mkdtemp(prefix="lumen_serve_bench_")
+    cfg = _config(args.service, args.model, args.device, args.batch, cache, args.runtime)
+    t0 = time.perf_counter()
+    res = Downloader(cfg).download_all()
+    assert all(r.success for r in res.values()), {k: r.error for k, r in res.items()}
+    app = AppService.from_app_config(cfg)
+    threads = args.server_threads or max(16, args.clients + 4)
+    server, port = build_server(HubRouter(app.services), "127.0.0.1", 0, max_workers=threads)
+    server.start()
+    load_s = time.perf_counter() - t0
+    task = TASKS[args.service]
+    imgs = _images(16, args.image_side, args.image_kind)
+    lat: list[float] = []
+    errors = [0]
+    lock = threading.Lock()
+    phase = {"timed": False, "stop": False}
+    counts = {"n": 0}
+
+    def client(ci: int):
+        ch = grpc.insecure_channel(f"127.0.0.1:{port}", options=[("grpc.max_send_message_length", 64 << 20),
+                                                                ("grpc.max_receive_message_length", 64 << 20)])
+        stub = pb.InferenceStub(ch)
+        k = ci
+        try:
+            while not phase["stop"]:
+                img = imgs[k % len(imgs)]
+                k += 1
+                t = time.perf_counter()
+                rs = list(stub.Infer(iter([pb.InferRequest(correlation_id=f"{ci}-{k}", task=task, payload=img,
+                                                           payload_mime="image/jpeg")]), timeout=300))
+                dt = time.perf_counter() - t
+                ok = len(rs) == 1 and not rs[0].HasField("error")
+                with lock:
+                    if not ok:
+                        errors[0] += 1
+                    elif phase["timed"]:
+                        lat.append(dt)
+                        counts["n"] += 1
+        finally:
+            ch.close()
+
+    ths = [threading.Thread(target=client, args=(i,), daemon=True) for i in range(args.clients)]
+    for t in ths:
+        t.start()
+    time.sleep(args.warmup)
+    with lock:
+        phase["timed"] = True
+        t_start = time.perf_counter()
+    time.sleep(args.seconds)
+    with lock:
+        phase["timed"] = False
+        n = counts["n"]
+        el = time.perf_counter() - t_start
+    phase["stop"] = True
+    for t in ths:
+        t.join(timeout=120)
+    server.stop(0)
+    app.close()
+    la = np.asarray(lat) * 1e3 if lat else np.zeros(1)
+    out = {"metric": f"serving {task} images/s", "value": round(n / el, 2), "unit": "images/s",
+           "p50_ms": round(float(np.percentile(la, 50)), 2), "p99_ms": round(float(np.percentile(la, 99)), 2),
+           "mean_ms": round(float(la.mean()), 2), "requests": n, "seconds": round(el, 2), "errors": errors[0],
+           "clients": args.clients, "service": args.service, "model": args.model, "device": args.device,
+           "dp_workers": args.dp, "batch_cap": args.batch, "max_wait_ms": os.environ.get("LUMEN_MAX_WAIT_MS"),
+           "image": f"{args.image_kind} JPEG {args.image_side * 4 // 3}x{args.image_side}, "
+                    f"{int(np.mean([len(b) for b in imgs]) / 1024)} KiB mean",
+           "load_s": round(load_s, 1),
+           "data": "synthetic (random-init weights of the named architecture, generated JPEGs)",
+           "path": "gRPC Infer stream -> hub router -> service -> dynamic batcher -> "
+                   + ("GPU worker pool (shm rings)" if args.dp > 1 else "in-process backend")}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
