@@ -41,6 +41,15 @@ struct GemmEpi {
   int ssq_tiles;
 };
 
+// Launch plan of an fp8-weight decode GEMM (gemm_w8.hip): column tiles per wave, K splits and
+// the K chunk per split.  The host sizes the split-K slabs / counters from the same plan.
+struct W8DecPlan {
+  int tpw;
+  int ks;
+  int kchunk;
+};
+W8DecPlan w8_dec_plan(int M, int N, int K);
+
 // rstd of the M (<= 32) A rows of a norm-folded decode GEMM into LDS (wave w: rows w, w + NWV, ...);
 // the caller's next __syncthreads publishes it.  K = row length (the normalised width).
 template <int NWV>

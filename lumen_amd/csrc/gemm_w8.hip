@@ -31,18 +31,19 @@ __device__ __forceinline__ void fp8x16_to_bf16(const u32x4_t w, bf16x8_t& f0, bf
   f1 = __builtin_bit_cast(bf16x8_t, fp8x8_to_bf16(w[2], w[3]));
 }
 
-// ============================================================================ decode
-// UNR: 64-wide k blocks loaded per wave before any MFMA issues; NT: weights streamed with
-// non-temporal loads (read once per token; keep L2 for the activations / KV).  NWV waves
-// per workgroup split the workgroup's K range: a decode GEMM is a chain of HBM round trips
-// per wave (k blocks / UNR of them), so more waves per 16-column tile = fewer round trips
-// (measured r2: 4 waves stay best, profiles/r2_w8_skinny_waves_v1.txt).
-template <int MT, int W8_UNROLL, bool NT, int NWV = 4>
-__global__ void __launch_bounds__(64 * NWV) gemm_skinny_w8_kernel(const uint16_t* __restrict__ A, int64_t lda,
+// ============================================================================ decode, 16 < M <= 32
+// Two 16-row MFMA tiles per wave (MT = 2); the K range of a 16-column tile is split over the
+// 4 waves (64-wide k blocks interleaved, 4 in flight per wave) and, for narrow N, over grid.y
+// with the in-launch split-K reduction.  The MFMA k order inside a 64-wide block is permuted
+// identically for A and W (lane group g owns k in [16g, 16g + 16)), so one 16-byte W load
+// feeds two MFMAs.
+template <int MT>
+__global__ void __launch_bounds__(256) gemm_skinny_w8_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                              const uint8_t* __restrict__ W, int64_t ldw,
                                                              const float* __restrict__ scale, void* __restrict__ C,
-                                                             int64_t ldc, float* __restrict__ ws, uint32_t* __restrict__ cnt, int M, int N, int K,
-                                                             int kchunk, GemmEpi ep) {
+                                                             int64_t ldc, float* __restrict__ ws, uint32_t* __restrict__ cnt,
+                                                             int M, int N, int K, int kchunk, GemmEpi ep) {
+  constexpr int NWV = 4, UNR = 4;
   __shared__ float red[NWV][MT * 16][17];
   __shared__ float rstd_s[MT * 16];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -51,8 +52,7 @@ __global__ void __launch_bounds__(64 * NWV) gemm_skinny_w8_kernel(const uint16_t
   const int n0 = blockIdx.x * 16;
   const int k_begin = blockIdx.y * kchunk;
   const int k_end = min(K, k_begin + kchunk);
-  const int nrow = min(n0 + col, N - 1);
-  const uint8_t* wr = W + (int64_t)nrow * ldw + g * 16;
+  const uint8_t* wr = W + (int64_t)min(n0 + col, N - 1) * ldw + g * 16;
   const uint16_t* ar[MT];
   bool av[MT];
 #pragma unroll
@@ -82,25 +82,23 @@ __global__ void __launch_bounds__(64 * NWV) gemm_skinny_w8_kernel(const uint16_t
       if (!av[t]) a[t][0] = a[t][1] = (u32x4_t){0u, 0u, 0u, 0u};
     }
   };
-
-  // 64-wide k blocks: wave wid takes blocks wid, wid + NWV, ... (W8_UNROLL at a time)
   const int nblk = (k_end - k_begin) / 64;
   int s = wid;
-  for (; s + NWV * (W8_UNROLL - 1) < nblk; s += NWV * W8_UNROLL) {
-    u32x4_t wf[W8_UNROLL];
-    u32x4_t af[W8_UNROLL][MT][2];
+  for (; s + NWV * (UNR - 1) < nblk; s += NWV * UNR) {
+    u32x4_t wf[UNR];
+    u32x4_t af[UNR][MT][2];
 #pragma unroll
-    for (int u = 0; u < W8_UNROLL; ++u) {
+    for (int u = 0; u < UNR; ++u) {
       const int k = k_begin + (s + NWV * u) * 64;
-      wf[u] = NT ? __builtin_nontemporal_load((const u32x4_t*)(wr + k)) : *(const u32x4_t*)(wr + k);
+      wf[u] = *(const u32x4_t*)(wr + k);
       load_a(k, af[u]);
     }
 #pragma unroll
-    for (int u = 0; u < W8_UNROLL; ++u) mma_block(wf[u], af[u]);
+    for (int u = 0; u < UNR; ++u) mma_block(wf[u], af[u]);
   }
   for (; s < nblk; s += NWV) {
     const int k = k_begin + s * 64;
-    const u32x4_t wf = NT ? __builtin_nontemporal_load((const u32x4_t*)(wr + k)) : *(const u32x4_t*)(wr + k);
+    const u32x4_t wf = *(const u32x4_t*)(wr + k);
     u32x4_t af[MT][2];
     load_a(k, af);
     mma_block(wf, af);
@@ -117,103 +115,204 @@ __global__ void __launch_bounds__(64 * NWV) gemm_skinny_w8_kernel(const uint16_t
     if (tid < M) {
       float v[16];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) v[c] = red[1][tid][c];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) v[c] *= n0 + c < N ? scale[n0 + c] : 0.f;
+      for (int c = 0; c < 16; ++c) v[c] = red[1][tid][c] * (n0 + c < N ? scale[n0 + c] : 0.f);
       epi_store16_dec(v, rstd_s[tid], tid, n0, M, N, C, ldc, ep);
     }
     return;
   }
-  if (tid < MT * 16) {
-    const int m = tid;
-    if (m < M) {
-      float v[16];
+  if (tid < M) {
+    float v[16];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        float t = 0.f;
+    for (int c = 0; c < 16; ++c) {
+      float t = 0.f;
 #pragma unroll
-        for (int w = 0; w < NWV; ++w) t += red[w][m][c];
-        v[c] = t * (n0 + c < N ? scale[n0 + c] : 0.f);
-      }
-      epi_store16_dec(v, rstd_s[m], m, n0, M, N, C, ldc, ep);
+      for (int w = 0; w < NWV; ++w) t += red[w][tid][c];
+      v[c] = t * (n0 + c < N ? scale[n0 + c] : 0.f);
     }
+    epi_store16_dec(v, rstd_s[tid], tid, n0, M, N, C, ldc, ep);
   }
 }
 
-// Two 16-column tiles per workgroup (unsplit K, M <= 16): the A fragments of each k block feed
-// both tiles' MFMAs and every wave keeps twice the weight bytes in flight.  For the widest decode
-// GEMMs (Llama-3-8B gate|up: 1792 tiles, lm_head) this halves the workgroup count, so the grid
-// fits in one round of resident workgroups instead of 1.2+ (6 per CU at 70 VGPRs).
-template <int W8_UNROLL, int NWV = 4>
-__global__ void __launch_bounds__(64 * NWV) gemm_skinny_w8x2_kernel(const uint16_t* __restrict__ A, int64_t lda,
-                                                               const uint8_t* __restrict__ W, int64_t ldw,
-                                                               const float* __restrict__ scale, void* __restrict__ C,
-                                                               int64_t ldc, int M, int N, int K, GemmEpi ep) {
-  __shared__ float red[NWV][16][33];
+// ============================================================================ decode, 4 < M <= 16
+// Batched decode GEMV on MFMA: a workgroup owns a stripe of 16 * TPW output columns and a K
+// range (grid.y splits K for narrow N); its 4 waves interleave 64-wide k blocks.  Per k block a
+// wave loads the A fragment (16 rows x 32 B per lane group) ONCE and TPW weight fragments, and
+// issues 2 * TPW MFMAs: the activations cost 1 / (2 TPW) of the weight bytes in load traffic
+// (the one-tile kernel paid 2x the weight bytes in L2 reads of A).  k blocks run as a two-slot
+// register pipeline of U-block chunks.  Norm sums of squares and the column scales are loaded
+// before the weight stream (vmcnt retires in issue order).
+template <int TPW, int U>
+__global__ void __launch_bounds__(256) gemv_w8_mfma_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                           const uint8_t* __restrict__ W, int64_t ldw,
+                                                           const float* __restrict__ scale, void* __restrict__ C,
+                                                           int64_t ldc, float* __restrict__ ws, uint32_t* __restrict__ cnt,
+                                                           int M, int N, int K, int kchunk, GemmEpi ep) {
+  constexpr int COLS = 16 * TPW;
+  __shared__ float red[4][16][COLS + 1];
+  __shared__ float sc_s[COLS];
   __shared__ float rstd_s[16];
+  __shared__ int last_s;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * 32;
-  const uint8_t* wr0 = W + (int64_t)min(n0 + col, N - 1) * ldw + g * 16;
-  const uint8_t* wr1 = W + (int64_t)min(n0 + 16 + col, N - 1) * ldw + g * 16;
-  const bool av = col < M;
-  const uint16_t* ar = A + (int64_t)(av ? col : 0) * lda + g * 16;
-  f32x4_t acc0 = (f32x4_t){0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  const int n0 = blockIdx.x * COLS;
+  const int k_begin = blockIdx.y * kchunk;
+  const int k_end = min(K, k_begin + kchunk);
 
-  auto mma2 = [&](const u32x4_t w8, const u32x4_t a0, const u32x4_t a1, f32x4_t& acc) {
-    bf16x8_t f0, f1;
-    fp8x16_to_bf16(w8, f0, f1);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a0), f0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a1), f1, acc, 0, 0, 0);
+  // ---- epilogue operands first
+  const float scv = scale[min(n0 + (tid % COLS), N - 1)];
+  const bool rs_pre = ep.norm && ep.ssq_in != nullptr && ep.ssq_tiles <= 16 * 16;   // K <= 4096
+  f32x4_t ssq_v[4];
+  if (rs_pre) {   // thread (row tid / 16, part tid % 16): float4 s part, part + 16, ...
+    const f32x4_t* p = (const f32x4_t*)(ep.ssq_in + (int64_t)min(tid >> 4, M - 1) * ep.ssq_tiles);
+    const int n4 = ep.ssq_tiles >> 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ssq_v[j] = p[min((tid & 15) + 16 * j, n4 - 1)];
+  }
+
+  const uint8_t* wr[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) wr[t] = W + (int64_t)min(n0 + t * 16 + col, N - 1) * ldw + g * 16;
+  const bool arow = col < M;
+  const uint16_t* ar = A + (int64_t)(arow ? col : 0) * lda + g * 16;
+  f32x4_t acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  u32x4_t wb[2][U][TPW];
+  u32x4_t ab[2][U][2];
+  const int nblk = (k_end - k_begin) >> 6;
+  const int mine = wid < nblk ? (nblk - wid + 3) >> 2 : 0;   // this wave's k blocks: wid, wid + 4, ...
+  auto issue = [&](const int slot, const int j0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = k_begin + (int64_t)(wid + 4 * (j0 + u)) * 64;
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) wb[slot][u][t] = *(const u32x4_t*)(wr[t] + k);
+      ab[slot][u][0] = *(const u32x4_t*)(ar + k);
+      ab[slot][u][1] = *(const u32x4_t*)(ar + k + 8);
+    }
   };
-  const int nblk = K / 64;
-  int s = wid;
-  for (; s + NWV * (W8_UNROLL - 1) < nblk; s += NWV * W8_UNROLL) {
-    u32x4_t w0[W8_UNROLL], w1[W8_UNROLL], a0[W8_UNROLL], a1[W8_UNROLL];
+  auto consume = [&](const int slot, const int nu) {
 #pragma unroll
-    for (int u = 0; u < W8_UNROLL; ++u) {
-      const int k = (s + NWV * u) * 64;
-      w0[u] = *(const u32x4_t*)(wr0 + k);
-      w1[u] = *(const u32x4_t*)(wr1 + k);
-      a0[u] = av ? *(const u32x4_t*)(ar + k) : (u32x4_t){0u, 0u, 0u, 0u};
-      a1[u] = av ? *(const u32x4_t*)(ar + k + 8) : (u32x4_t){0u, 0u, 0u, 0u};
-    }
+    for (int u = 0; u < U; ++u) {
+      if (u < nu) {
+        const u32x4_t a0 = arow ? ab[slot][u][0] : (u32x4_t){0u, 0u, 0u, 0u};
+        const u32x4_t a1 = arow ? ab[slot][u][1] : (u32x4_t){0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int u = 0; u < W8_UNROLL; ++u) {
-      mma2(w0[u], a0[u], a1[u], acc0);
-      mma2(w1[u], a0[u], a1[u], acc1);
-    }
-  }
-  for (; s < nblk; s += NWV) {
-    const int k = s * 64;
-    const u32x4_t w0 = *(const u32x4_t*)(wr0 + k), w1 = *(const u32x4_t*)(wr1 + k);
-    const u32x4_t a0 = av ? *(const u32x4_t*)(ar + k) : (u32x4_t){0u, 0u, 0u, 0u};
-    const u32x4_t a1 = av ? *(const u32x4_t*)(ar + k + 8) : (u32x4_t){0u, 0u, 0u, 0u};
-    mma2(w0, a0, a1, acc0);
-    mma2(w1, a0, a1, acc1);
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    red[wid][4 * g + r][col] = acc0[r];
-    red[wid][4 * g + r][16 + col] = acc1[r];
-  }
-  if (ep.norm) skinny_rstd<NWV>(A, lda, M, K, ep, rstd_s);
-  __syncthreads();
-  if (tid < 2 * 16) {   // thread: (row m, tile tl)
-    const int m = tid & 15, tl = tid >> 4;
-    const int n = n0 + tl * 16;
-    if (m < M && n < N) {
-      float v[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        float t = 0.f;
-#pragma unroll
-        for (int w = 0; w < NWV; ++w) t += red[w][m][tl * 16 + c];
-        v[c] = t * (n + c < N ? scale[n + c] : 0.f);
+        for (int t = 0; t < TPW; ++t) {
+          bf16x8_t f0, f1;
+          fp8x16_to_bf16(wb[slot][u][t], f0, f1);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a0), f0, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a1), f1, acc[t], 0, 0, 0);
+        }
       }
-      epi_store16_dec(v, rstd_s[m], m, n, M, N, C, ldc, ep);
     }
+  };
+  const int nch = mine / U;
+  if (nch > 0) {
+    issue(0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    int c = 0;
+    for (; c + 2 < nch; c += 2) {
+      issue(1, (c + 1) * U);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(0, U);
+      __builtin_amdgcn_sched_barrier(0);
+      issue(0, (c + 2) * U);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(1, U);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (c + 1 < nch) {
+      issue(1, (c + 1) * U);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(0, U);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(1, U);
+    } else {
+      consume(0, U);
+    }
+  }
+  for (int j = nch * U; j < mine; ++j) {   // remainder blocks, one at a time
+    const int64_t k = k_begin + (int64_t)(wid + 4 * j) * 64;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) wb[0][0][t] = *(const u32x4_t*)(wr[t] + k);
+    ab[0][0][0] = *(const u32x4_t*)(ar + k);
+    ab[0][0][1] = *(const u32x4_t*)(ar + k + 8);
+    consume(0, 1);
+  }
+
+  // ---- wave partials -> LDS (C fragment: row 4g + r, column t * 16 + col)
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wid][4 * g + r][t * 16 + col] = acc[t][r];
+  if (tid < COLS) sc_s[tid] = scv;
+  if (ep.norm) {
+    if (rs_pre) {
+      const int n4 = ep.ssq_tiles >> 2;
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if ((tid & 15) + 16 * j < n4) t += (ssq_v[j][0] + ssq_v[j][1]) + (ssq_v[j][2] + ssq_v[j][3]);
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o, 64);
+      if ((tid & 15) == 0 && (tid >> 4) < 16) rstd_s[tid >> 4] = rsqrtf(t / (float)K + ep.norm_eps);
+    } else {
+      skinny_rstd<4>(A, lda, M, K, ep, rstd_s);
+    }
+  }
+  __syncthreads();
+  // wave sum, kept in red[0] (thread-owned elements only: no race)
+  for (int i = tid; i < 16 * COLS; i += 256) {
+    const int m = i / COLS, c = i - m * COLS;
+    red[0][m][c] = (red[0][m][c] + red[1][m][c]) + (red[2][m][c] + red[3][m][c]);
+  }
+  if (ws != nullptr) {
+    // ---- in-launch split-K: write-through partial slab, ticket, the last split sums in order
+    const int64_t slab = (int64_t)M * N;
+    for (int i = tid; i < M * COLS; i += 256) {
+      const int m = i / COLS, c = i - m * COLS;
+      if (n0 + c < N)
+        __hip_atomic_store(ws + blockIdx.y * slab + (int64_t)m * N + n0 + c, red[0][m][c], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t prev = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = prev == gridDim.y - 1;
+      if (last) __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_s = last ? 1 : 0;
+    }
+    __syncthreads();
+    if (!last_s) return;
+    const int S = gridDim.y;
+    for (int i = tid; i < M * COLS; i += 256) {
+      const int m = i / COLS, c = i - m * COLS;
+      const float* p = ws + (int64_t)m * N + min(n0 + c, N - 1);
+      float v = 0.f;
+      for (int s0 = 0; s0 < S; s0 += 8) {   // 8 slab loads in flight; summed in split order
+        float pv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          pv[j] = __hip_atomic_load(p + min(s0 + j, S - 1) * slab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v += s0 + j < S ? pv[j] : 0.f;
+      }
+      red[1][m][c] = v;
+    }
+    __syncthreads();
+  }
+  const int src = ws != nullptr ? 1 : 0;
+  __syncthreads();
+  if (tid < M * TPW) {   // thread: (row m, 16-column tile t)
+    const int m = tid / TPW, t = tid - m * TPW;
+    float v[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[c] = red[src][m][t * 16 + c] * sc_s[t * 16 + c];
+    epi_store16_dec(v, rstd_s[m], m, n0 + t * 16, M, N, C, ldc, ep);
   }
 }
 
@@ -615,89 +714,72 @@ static hipError_t launch_w8(const uint16_t* A, int64_t lda, const uint8_t* W, in
 
 int skinny_ksplit(int N, int K);
 
+// Decode plan for fp8 weights, 4 < M <= 32 (M <= 4 runs the unsplit row-streaming GEMV):
+// M <= 16: column stripes of 64 / 32 / 16 (N divisibility), K split so that stripes x splits
+// reach ~512 workgroups (2 per CU), every split >= 4 k blocks (one per wave);
+// 16 < M <= 32: 16-column tiles, the skinny split heuristic.
+W8DecPlan w8_dec_plan(int M, int N, int K) {
+  W8DecPlan p{};
+  p.tpw = 1;
+  p.ks = 1;
+  p.kchunk = K;
+  if (M <= 4) return p;
+  int ks = 1;
+  if (M <= 16) {
+    p.tpw = N % 64 == 0 ? 4 : (N % 32 == 0 ? 2 : 1);
+    const int stripes = (N + 16 * p.tpw - 1) / (16 * p.tpw);
+    ks = (512 + stripes - 1) / stripes;
+    const int kmax = K / 256 > 1 ? K / 256 : 1;
+    ks = ks < kmax ? ks : kmax;
+    int kchunk = (K + ks - 1) / ks;
+    kchunk = (kchunk + 63) / 64 * 64;
+    p.kchunk = kchunk;
+    p.ks = (K + kchunk - 1) / kchunk;
+  } else {
+    ks = skinny_ksplit(N, K);
+    int kchunk = (K + ks - 1) / ks;
+    kchunk = (kchunk + 255) / 256 * 256;   // whole 64-wide blocks for every wave
+    p.kchunk = kchunk;
+    p.ks = (K + kchunk - 1) / kchunk;
+  }
+  if (p.ks == 1) p.kchunk = K;
+  return p;
+}
+
 hipError_t gemm_w8(const uint16_t* A, int64_t lda, const uint8_t* W, int64_t ldw, const float* scale, void* C,
                    int64_t ldc, int M, int N, int K, const GemmEpi& ep, float* ws, uint32_t* cnt, int ksplit,
                    hipStream_t stream) {
   if (K % 64 != 0 || M <= 0) return hipErrorInvalidValue;
-  static const int dec_v = [] {
-    const char* e = getenv("LUMEN_W8_DEC");
-    return e ? atoi(e) : 1;
-  }();
-  if (M <= 4 && dec_v > 0) {
+  if (M <= 4) {   // row-streaming GEMV
     const dim3 grid((N + 15) / 16);
 #define ROWS_LAUNCH(MR_, U_)                                                                                      \
   hipLaunchKernelGGL((gemv_w8_rows_kernel<MR_, U_>), grid, dim3(256), 0, stream, A, lda, W, ldw, scale, C, ldc, M, \
                      N, K, ep)
-    if (dec_v == 2) {
-      if (M == 1) ROWS_LAUNCH(1, 4); else if (M == 2) ROWS_LAUNCH(2, 4); else ROWS_LAUNCH(4, 2);
-    } else {
-      if (M == 1) ROWS_LAUNCH(1, 2); else if (M == 2) ROWS_LAUNCH(2, 2); else ROWS_LAUNCH(4, 1);
-    }
+    if (M == 1) ROWS_LAUNCH(1, 2);
+    else if (M == 2) ROWS_LAUNCH(2, 2);
+    else ROWS_LAUNCH(4, 1);
 #undef ROWS_LAUNCH
     return hipGetLastError();
   }
   if (M <= 32) {
-    // LUMEN_W8_SKINNY: bit 0 = non-temporal weight loads, bit 1 = 8 k blocks per wave in flight;
-    // LUMEN_W8_SKINNY_NW: waves per workgroup (4, 8 or 16) for M <= 16; 4 measured fastest
-    // (graph-replayed, Llama-3-8B shapes: 8 waves +5-10 %, 16 waves 3-8x slower; r2_w8_skinny_waves_v1.txt)
-    static const int variant = [] {
-      const char* e = getenv("LUMEN_W8_SKINNY");
-      return e ? atoi(e) & 3 : 0;
-    }();
-    static const int nw_env = [] {
-      const char* e = getenv("LUMEN_W8_SKINNY_NW");
-      const int v = e ? atoi(e) : 4;
-      return v == 8 || v == 16 ? v : 4;
-    }();
-    const int nwv = M <= 16 ? nw_env : 4;
-    int kchunk = (K + ksplit - 1) / ksplit;
-    kchunk = (kchunk + 64 * nwv - 1) / (64 * nwv) * (64 * nwv);   // whole 64-wide blocks for every wave
-    const int gy = (K + kchunk - 1) / kchunk;
+    const W8DecPlan pl = w8_dec_plan(M, N, K);
+    if (pl.ks > 1 && pl.ks != ksplit) return hipErrorInvalidValue;   // host sized ws / counters for its plan
+    const int gy = pl.ks;
     if (gy > 1 && (ws == nullptr || cnt == nullptr)) return hipErrorInvalidValue;
-    dim3 grid((N + 15) / 16, gy), block(64 * nwv);
     float* w = gy > 1 ? ws : nullptr;
-#define W8_LAUNCH(MT_, U_, NT_, NW_)                                                                            \
-  hipLaunchKernelGGL((gemm_skinny_w8_kernel<MT_, U_, NT_, NW_>), grid, dim3(64 * NW_), 0, stream, A, lda, W, ldw,  \
-                     scale, C, ldc, w, cnt, M, N, K, kchunk, ep)
-#define W8_NW(U_, NT_)                          \
-  switch (nwv) {                                \
-    case 8: W8_LAUNCH(1, U_, NT_, 8); break;    \
-    case 16: W8_LAUNCH(1, U_, NT_, 16); break;  \
-    default: W8_LAUNCH(1, U_, NT_, 4);          \
-  }
-    (void)block;
-    // two tiles per workgroup for wide unsplit GEMMs (LUMEN_W8_NTL=1|2 forces; auto: > 6 tiles per CU)
-    static const int ntl_env = [] {
-      const char* e = getenv("LUMEN_W8_NTL");
-      return e ? atoi(e) : 0;
-    }();
-    static int cus = 0;
-    if (cus == 0) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (cus <= 0) cus = 256;
-    }
-    const int ntiles = (N + 15) / 16;
-    const bool x2 = M <= 16 && gy == 1 && variant == 0 && nwv == 4 &&
-                    (ntl_env == 2 || (ntl_env == 0 && ntiles > 6 * cus));
-    if (x2) {
-      hipLaunchKernelGGL((gemm_skinny_w8x2_kernel<4, 4>), dim3((N + 31) / 32), dim3(256), 0, stream, A, lda, W, ldw,
-                         scale, C, ldc, M, N, K, ep);
-      return hipGetLastError();
-    }
     if (M <= 16) {
-      switch (variant) {
-        case 1: W8_NW(4, true); break;
-        case 2: W8_NW(8, false); break;
-        case 3: W8_NW(8, true); break;
-        default: W8_NW(4, false);
-      }
+      const dim3 grid((N + 16 * pl.tpw - 1) / (16 * pl.tpw), gy);
+#define MFMA_LAUNCH(T_)                                                                                          \
+  hipLaunchKernelGGL((gemv_w8_mfma_kernel<T_, 2>), grid, dim3(256), 0, stream, A, lda, W, ldw, scale, C, ldc, w, cnt, \
+                     M, N, K, pl.kchunk, ep)
+      if (pl.tpw == 4) MFMA_LAUNCH(4);
+      else if (pl.tpw == 2) MFMA_LAUNCH(2);
+      else MFMA_LAUNCH(1);
+#undef MFMA_LAUNCH
     } else {
-      W8_LAUNCH(2, 4, false, 4);
+      hipLaunchKernelGGL((gemm_skinny_w8_kernel<2>), dim3((N + 15) / 16, gy), dim3(256), 0, stream, A, lda, W, ldw,
+                         scale, C, ldc, w, cnt, M, N, K, pl.kchunk, ep);
     }
-#undef W8_NW
-#undef W8_LAUNCH
     return hipGetLastError();
   }
   const int64_t t128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);

@@ -79,21 +79,60 @@ hipError_t rope_kv(const RopeKVArgs& a, hipStream_t stream) {
 }
 
 // ------------------------------------------------------------------------------ paged decode attention
-// One workgroup per (split, kv head, sequence); each wave takes the split's 64-token blocks
-// wid, wid + 4, ...  Per block the wave issues ALL of its K and V fragment loads before any
-// math (one HBM round trip per block instead of K -> softmax -> V), then S^T = K Q^T, the
-// online softmax and O^T += V^T P^T.  The 4 wave states merge through LDS.  A context split
-// over several workgroups is combined IN the launch: every split publishes its (m, l, o)
-// partials with write-through (sc1) stores, draws a ticket from the (sequence, kv head)
-// counter, and the last to arrive merges all splits (sc1 loads) and writes the output --
-// no combine launch (MI355X_MICROARCH.md hand-off rules: sc1 stores drained before the
-// ticket, sc1 loads, no fences; the last arriver re-zeroes the counter for the next launch).
+// One workgroup of NW = 4 waves per (split, kv head, sequence); wave w takes the split's 64-token
+// blocks w, w + 4, ... (up to 32 splits of 4 blocks -- 8k tokens -- one block per wave, so a
+// context of <= 256 tokens is ONE workgroup per kv head; longer contexts loop with an online
+// softmax).  The latency chain per wave is: block-table entry -> every K and V fragment of the
+// block in flight at once -> S^T = K Q^T, online softmax, O^T += V^T P^T; the 8 wave states
+// merge through LDS.  Fused RoPE mode (decode): q and the current token's k are rotated in
+// registers, and the current token enters the wave that owns its block straight from registers
+// (its score q . k_cur as a lane-group dot product, its v into the V fragment) -- the cache
+// write of that token is fire-and-forget (the next step reads it), so no workgroup waits for a
+// store round trip.  A context split over several workgroups is
+// combined IN the launch: every split publishes its (m, l, o) partials with write-through (sc1)
+// stores, draws a ticket from the (sequence, kv head) counter, and the last to arrive merges
+// all splits (sc1 loads, 8 in flight) -- no combine launch, no fences (MI355X_MICROARCH.md
+// hand-off rules); the last arriver re-zeroes the counter for the next launch.
+constexpr int PD_NW = 4;   // 1 wave per SIMD: the 512-VGPR budget holds a whole block's K and V fragments
+
+template <int D>
+__device__ __forceinline__ void rope_chunks(u32x4_t (&w)[D / 32], const float2* cs, int g) {
+  constexpr int KS = D / 32;
+#pragma unroll
+  for (int t = 0; t < KS / 2; ++t) {   // element e pairs with e + D/2: chunk t with t + KS/2
+    float x1[8], x2[8];
+    unpack8(w[t], x1);
+    unpack8(w[t + KS / 2], x2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float2 c = cs[t * 32 + g * 8 + j];
+      const float y1 = x1[j] * c.x - x2[j] * c.y, y2 = x2[j] * c.x + x1[j] * c.y;
+      x1[j] = y1;
+      x2[j] = y2;
+    }
+    w[t] = pack8(x1);
+    w[t + KS / 2] = pack8(x2);
+  }
+}
+
+// bf16 values as the cache stores them (fp8 cache: rounded through e4m3fn)
+template <bool F8KV>
+__device__ __forceinline__ __bf16 as_cached(__bf16 v) {
+  if constexpr (F8KV) {
+    const uint32_t b = f2fp8((float)v);
+    return __builtin_bit_cast(bf16x8_t, fp8x8_to_bf16(b, 0u))[0];
+  } else {
+    return v;
+  }
+}
+
 template <int D, bool F8KV>
-__global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
+__global__ void __launch_bounds__(64 * PD_NW) paged_decode_kernel(DecodeArgs a) {
+  constexpr int NW = PD_NW;
   constexpr int KS = D / 32;   // k-steps of S^T over the head dim
   constexpr int NB = D / 16;   // 16-wide d blocks of O^T
-  __shared__ float sm_ml[4][2][16];
-  __shared__ float sm_o[4][D][17];
+  __shared__ float sm_ml[NW][2][16];
+  __shared__ float sm_o[NW][D][17];
   __shared__ float sm_c[2][16][32];   // combine: (m, l) of up to 32 splits per query head
   __shared__ int sm_last;
 
@@ -108,82 +147,59 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
   const int blk1 = min(blk0 + a.blocks_per_split, nblk);
   const int ns = max(1, (nblk + a.blocks_per_split - 1) / a.blocks_per_split);   // splits holding blocks
   if (split >= ns) return;
+  // this wave's blocks: blk0 + wid, + NW, ... (one block per wave up to 512 tokens per split)
+  int phys = blk0 + wid < blk1 ? a.block_table[(int64_t)b * a.bt_stride + blk0 + wid] : 0;   // first load of the chain
 
-  // Q^T fragment (B operand): column = query head hk*G + col (zero beyond G)
+  // Q^T fragment (B operand): column = query head hk*G + col (zero beyond G).  Loaded here, rotated
+  // (fused RoPE) only after the first block's K / V loads are in flight: its VALU then overlaps
+  // that round trip instead of delaying the issue.
   bf16x8_t qf[KS];
+  const bool fused = a.pos != nullptr;
+  const float2* cs = fused ? reinterpret_cast<const float2*>(a.cos_sin) + (int64_t)a.pos[b] * (D / 2) : nullptr;
+  const bool qv = col < G;
+  u32x4_t qraw[KS];
   {
-    const bool qv = col < G;
     const uint16_t* qp = a.q + (int64_t)b * a.q_sb + (int64_t)(hk * G + (qv ? col : 0)) * D;
-    u32x4_t w[KS];
 #pragma unroll
-    for (int t = 0; t < KS; ++t) {
-      w[t] = *(const u32x4_t*)(qp + t * 32 + g * 8);
-      if (!qv) w[t] = (u32x4_t){0u, 0u, 0u, 0u};
-    }
+    for (int t = 0; t < KS; ++t) qraw[t] = *(const u32x4_t*)(qp + t * 32 + g * 8);
+  }
+  bool q_ready = false;
+  auto prep_q = [&]() {
+#pragma unroll
+    for (int t = 0; t < KS; ++t)
+      if (!qv) qraw[t] = (u32x4_t){0u, 0u, 0u, 0u};
     if constexpr (KS >= 2) {
-      if (a.pos) {   // fused RoPE (rotate-half): element e pairs with e + D/2, i.e. chunk t with t + KS/2
-        const float2* cs = reinterpret_cast<const float2*>(a.cos_sin) + (int64_t)a.pos[b] * (D / 2);
-#pragma unroll
-        for (int t = 0; t < KS / 2; ++t) {
-          float x1[8], x2[8];
-          unpack8(w[t], x1);
-          unpack8(w[t + KS / 2], x2);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float2 c = cs[t * 32 + g * 8 + j];
-            const float y1 = x1[j] * c.x - x2[j] * c.y, y2 = x2[j] * c.x + x1[j] * c.y;
-            x1[j] = y1;
-            x2[j] = y2;
-          }
-          w[t] = pack8(x1);
-          w[t + KS / 2] = pack8(x2);
-        }
-      }
+      if (fused) rope_chunks<D>(qraw, cs, g);
     }
 #pragma unroll
-    for (int t = 0; t < KS; ++t) qf[t] = __builtin_bit_cast(bf16x8_t, w[t]);
+    for (int t = 0; t < KS; ++t) qf[t] = __builtin_bit_cast(bf16x8_t, qraw[t]);
+    q_ready = true;
+  };
+  // current token (position ctx - 1) in fused mode: the wave owning its block takes it from
+  // registers; the owning split's workgroup also writes it to the cache AFTER its attention
+  // (fire-and-forget: only the next decode step reads it)
+  const int cur = ctx - 1;
+  const bool owns_cur = fused && blk0 <= cur / KV_BLOCK && cur / KV_BLOCK < blk1;
+  // the current token's k (rotated) and v as this lane's fragments need them, loaded BEFORE the
+  // K / V stream (vmcnt retires in issue order; a load issued after it would wait behind it)
+  u32x4_t kcur[KS];
+  uint16_t vcur[NB];
+  if (owns_cur) {
+    const uint16_t* kp = a.q + (int64_t)b * a.q_sb + (int64_t)(a.H + hk) * D;
+    const uint16_t* vp = a.q + (int64_t)b * a.q_sb + (int64_t)(a.H + a.Hkv + hk) * D;
+#pragma unroll
+    for (int t = 0; t < KS; ++t) kcur[t] = *(const u32x4_t*)(kp + t * 32 + g * 8);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) vcur[j] = vp[j * 16 + col];
   }
-  // fused cache write of the current token (position ctx - 1): only the split owning the last
-  // block reads it, so that workgroup rotates k, writes k / v for kv head hk and then reads
-  // the block back like any other (stores drained + barrier before the loop)
-  if (a.pos && blk0 <= nblk - 1 && nblk - 1 < blk1) {
-    const int64_t slot = a.slots[b];
-    if (slot >= 0) {
-      const int64_t cblk = slot >> 6;
-      const int coff = (int)(slot & 63);
-      const uint16_t* kv = a.q + (int64_t)b * a.q_sb + (int64_t)(a.H + hk) * D;   // unrotated k head
-      const int half = D / 2;
-      if (tid < half) {
-        const float2 c = reinterpret_cast<const float2*>(a.cos_sin)[(int64_t)a.pos[b] * half + tid];
-        const float x1 = bf2f(kv[tid]), x2 = bf2f(kv[tid + half]);
-        const uint16_t y1 = f2bf(x1 * c.x - x2 * c.y), y2 = f2bf(x2 * c.x + x1 * c.y);
-        const int64_t ko = ((cblk * a.Hkv + hk) * KV_BLOCK + coff) * D;
-        if constexpr (F8KV) {
-          uint8_t* kr = reinterpret_cast<uint8_t*>(a.k_cache_w) + ko;
-          kr[tid] = f2fp8(bf2f(y1));
-          kr[tid + half] = f2fp8(bf2f(y2));
-        } else {
-          a.k_cache_w[ko + tid] = y1;
-          a.k_cache_w[ko + tid + half] = y2;
-        }
-      } else if (tid < half + D) {
-        const int d = tid - half;
-        const uint16_t* vr = a.q + (int64_t)b * a.q_sb + (int64_t)(a.H + a.Hkv + hk) * D;
-        const int64_t vo = ((cblk * a.Hkv + hk) * D + d) * KV_BLOCK + coff;
-        if constexpr (F8KV) reinterpret_cast<uint8_t*>(a.v_cache_w)[vo] = f2fp8(bf2f(vr[d]));
-        else a.v_cache_w[vo] = vr[d];
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
+
   f32x4_t o[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) o[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   float mrow = -INFINITY, lrow = 0.f;
 
-  for (int bi = blk0 + wid; bi < blk1; bi += 4) {
-    const int phys = a.block_table[(int64_t)b * a.bt_stride + bi];
+  for (int bi = blk0 + wid; bi < blk1; bi += NW) {
+    if (bi != blk0 + wid) phys = a.block_table[(int64_t)b * a.bt_stride + bi];
     const int64_t kvo = ((int64_t)phys * a.Hkv + hk) * KV_BLOCK * D;   // elements (= bytes for fp8)
     const uint16_t* kb = a.k_cache + kvo;
     const uint16_t* vb = a.v_cache + kvo;
@@ -221,13 +237,49 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
           vf[s][j] = *(const bf16x8_t*)(vb + vro + 32 * s + (int64_t)j * 16 * KV_BLOCK);
         }
       }
+    // the current token's v from registers (the cache store above may not have landed)
+    const bool cur_here = owns_cur && bi == cur / KV_BLOCK;
+    const int coff = cur - bi * KV_BLOCK;
+    if (cur_here) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int e = coff - 32 * s - 8 * g;   // lane-dependent: a select per element, no branch
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const __bf16 v = as_cached<F8KV>(__builtin_bit_cast(__bf16, vcur[j]));
+#pragma unroll
+          for (int ee = 0; ee < 8; ++ee) vf[s][j][ee] = ee == e ? v : vf[s][j][ee];
+        }
+      }
+    }
 
+    if (!q_ready) prep_q();
     f32x4_t sc[4];
 #pragma unroll
     for (int kb16 = 0; kb16 < 4; ++kb16) {
       sc[kb16] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < KS; ++t) sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kb16][t], qf[t], sc[kb16], 0, 0, 0);
+    }
+    if (cur_here) {   // the current token's score q . k_cur from registers (rotated, rounded as cached)
+      u32x4_t kw[KS];
+#pragma unroll
+      for (int t = 0; t < KS; ++t) kw[t] = kcur[t];
+      if constexpr (KS >= 2) rope_chunks<D>(kw, cs, g);
+      float dot = 0.f;
+#pragma unroll
+      for (int t = 0; t < KS; ++t) {
+        const bf16x8_t kv8 = __builtin_bit_cast(bf16x8_t, kw[t]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dot += (float)as_cached<F8KV>(kv8[e]) * (float)qf[t][e];
+      }
+      dot += __shfl_xor(dot, 16, 64);   // sum over the 4 lane groups (d ranges) of query col
+      dot += __shfl_xor(dot, 32, 64);
+#pragma unroll
+      for (int kb16 = 0; kb16 < 4; ++kb16)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (32 * (kb16 >> 1) + 8 * g + 4 * (kb16 & 1) + r == coff) sc[kb16][r] = dot;
     }
     float mx = mrow;
 #pragma unroll
@@ -242,7 +294,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mbase = mx == -INFINITY ? 0.f : mx;
-    const float alpha = __builtin_amdgcn_exp2f(mrow - mbase);
+    const float alpha = __builtin_amdgcn_exp2f(mrow - mbase);   // online softmax over a wave's blocks
     float rs = 0.f;
 #pragma unroll
     for (int kb16 = 0; kb16 < 4; ++kb16)
@@ -285,7 +337,37 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
     }
   }
 
-  // ---- merge the 4 wave states through LDS
+  if (owns_cur) {   // the current token's k (rotated) / v into the cache for the next step
+    const int64_t slot = a.slots[b];
+    if (slot >= 0) {
+      const int64_t cblk = slot >> 6;
+      const int coff = (int)(slot & 63);
+      const uint16_t* kv = a.q + (int64_t)b * a.q_sb + (int64_t)(a.H + hk) * D;   // unrotated k head
+      const int half = D / 2;
+      if (tid < half) {
+        const float2 c = reinterpret_cast<const float2*>(a.cos_sin)[(int64_t)a.pos[b] * half + tid];
+        const float x1 = bf2f(kv[tid]), x2 = bf2f(kv[tid + half]);
+        const uint16_t y1 = f2bf(x1 * c.x - x2 * c.y), y2 = f2bf(x2 * c.x + x1 * c.y);
+        const int64_t ko = ((cblk * a.Hkv + hk) * KV_BLOCK + coff) * D;
+        if constexpr (F8KV) {
+          uint8_t* kr = reinterpret_cast<uint8_t*>(a.k_cache_w) + ko;
+          kr[tid] = f2fp8(bf2f(y1));
+          kr[tid + half] = f2fp8(bf2f(y2));
+        } else {
+          a.k_cache_w[ko + tid] = y1;
+          a.k_cache_w[ko + tid + half] = y2;
+        }
+      } else if (tid < half + D) {
+        const int d = tid - half;
+        const uint16_t* vr = a.q + (int64_t)b * a.q_sb + (int64_t)(a.H + a.Hkv + hk) * D;
+        const int64_t vo = ((cblk * a.Hkv + hk) * D + d) * KV_BLOCK + coff;
+        if constexpr (F8KV) reinterpret_cast<uint8_t*>(a.v_cache_w)[vo] = f2fp8(bf2f(vr[d]));
+        else a.v_cache_w[vo] = vr[d];
+      }
+    }
+  }
+
+  // ---- merge the NW wave states through LDS
   if (g == 0) {
     sm_ml[wid][0][col] = mrow;
     sm_ml[wid][1][col] = lrow;
@@ -295,15 +377,15 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) sm_o[wid][j * 16 + 4 * g + r][col] = o[j][r];
   __syncthreads();
-  for (int idx = tid; idx < G * D; idx += 256) {
+  for (int idx = tid; idx < G * D; idx += 64 * NW) {
     const int q = idx / D, d = idx - q * D;
     float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm_ml[w][0][q]);
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, sm_ml[w][0][q]);
     float L = 0.f, O = 0.f;
     if (M != -INFINITY) {
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < NW; ++w) {
         const float e = __builtin_amdgcn_exp2f(sm_ml[w][0][q] - M);
         L += sm_ml[w][1][q] * e;
         O += sm_o[w][d][q] * e;
@@ -335,14 +417,14 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
   }
   __syncthreads();
   if (!sm_last) return;
-  for (int i = tid; i < G * ns; i += 256) {
+  for (int i = tid; i < G * ns; i += 64 * NW) {
     const int q = i / ns, sp = i - q * ns;
     const int64_t pi = ((int64_t)b * a.H + hk * G + q) * a.nsplit + sp;
     sm_c[0][q][sp] = __hip_atomic_load(a.part_ml + pi * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sm_c[1][q][sp] = __hip_atomic_load(a.part_ml + pi * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  for (int idx = tid; idx < G * D; idx += 256) {
+  for (int idx = tid; idx < G * D; idx += 64 * NW) {
     const int q = idx / D, d = idx - q * D;
     const int h = hk * G + q;
     const int64_t pi0 = ((int64_t)b * a.H + h) * a.nsplit;
@@ -350,8 +432,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
     for (int sp = 0; sp < ns; ++sp) M = fmaxf(M, sm_c[0][q][sp]);
     float L = 0.f, O = 0.f;
     if (M != -INFINITY) {
-      // 8 splits' partial loads in flight per round trip (a dependent load per split made the
-      // merge a chain of ns L2 round trips); accumulation in split order: deterministic
+      // 8 splits' partial loads in flight per round trip; accumulation in split order: deterministic
       for (int s0 = 0; s0 < ns; s0 += 8) {
         float pv[8];
 #pragma unroll
@@ -374,8 +455,9 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeArgs a) {
 }
 
 hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream) {
-  if (a.nsplit > 32 || (a.nsplit > 1 && a.split_cnt == nullptr)) return hipErrorInvalidValue;
-  dim3 grid(a.nsplit, a.Hkv, B), block(256);
+  if (a.nsplit > 32 || (a.nsplit > 1 && a.split_cnt == nullptr))
+    return hipErrorInvalidValue;
+  dim3 grid(a.nsplit, a.Hkv, B), block(64 * PD_NW);
 #define PD_LAUNCH(D_)                                                                           \
   do {                                                                                          \
     if (a.kv_fp8) hipLaunchKernelGGL((paged_decode_kernel<D_, true>), grid, block, 0, stream, a);  \

@@ -212,7 +212,7 @@ void gemm_w8(const at::Tensor& a, const at::Tensor& w8, const at::Tensor& scale,
   at::Tensor ws;
   uint32_t* cnt = nullptr;
   if (M <= 32) {
-    ks = lumen::skinny_ksplit((int)N, (int)K);
+    ks = lumen::w8_dec_plan((int)M, (int)N, (int)K).ks;
     if (ks > 1) {
       ws = at::empty({ks, M, N}, a.options().dtype(at::kFloat));
       cnt = splitk_counters(a, (N + 15) / 16);
@@ -276,7 +276,8 @@ void gemm_dec(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::
     ep.ldr = residual->stride(0);
   }
   const at::DeviceGuard guard(a.device());
-  const int ks = lumen::skinny_ksplit((int)N, (int)K);
+  const bool is_f8 = w.scalar_type() == at::kFloat8_e4m3fn;
+  const int ks = is_f8 ? lumen::w8_dec_plan((int)M, (int)N, (int)K).ks : lumen::skinny_ksplit((int)N, (int)K);
   at::Tensor ws;
   if (ks > 1) ws = at::empty({ks, M, N}, a.options().dtype(at::kFloat));
   uint32_t* cnt = ks > 1 ? splitk_counters(a, (N + 15) / 16) : nullptr;

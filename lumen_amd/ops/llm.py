@@ -79,19 +79,18 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor, H: int,
             v_cache[blk, :, :, off] = vt.to(v_cache.dtype)
 
 
-_DECODE_TARGET_WG = 512
+_DECODE_WAVES = 4             # waves (= 64-token blocks) per paged-decode workgroup (csrc/llm.hip PD_NW)
 _DECODE_MAX_SPLITS = 32        # the in-launch split combine merges at most 32 splits per kv head
 
 
 def decode_splits(B: int, Hkv: int, max_blocks: int, target_wg: Optional[int] = None) -> tuple[int, int]:
-    """(nsplit, blocks_per_split): enough workgroups to fill 256 CUs, >= 4 blocks (one per wave) per
-    split, at most 32 splits (longer contexts give each wave several blocks)."""
-    target_wg = _DECODE_TARGET_WG if target_wg is None else target_wg
-    want = max(1, -(-target_wg // max(B * Hkv, 1)))
-    nsplit = max(1, min(want, -(-max_blocks // 4), _DECODE_MAX_SPLITS))
+    """(nsplit, blocks_per_split) of the paged decode kernel: a split is one workgroup of 4 waves,
+    one 64-token block per wave, so a context of <= 256 tokens is one workgroup per kv head with
+    no cross-workgroup combine; longer contexts use up to 32 splits merged in-launch, and past
+    8k tokens the waves loop over several blocks."""
+    nsplit = max(1, min(-(-max_blocks // _DECODE_WAVES), _DECODE_MAX_SPLITS))
     bps = -(-max_blocks // nsplit)
-    nsplit = -(-max_blocks // bps)
-    return nsplit, bps
+    return -(-max_blocks // bps), bps
 
 
 def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_table: torch.Tensor,

@@ -22,9 +22,17 @@ elementwise unary / broadcast binary ops (csrc/onnx_ops.hip).  Shape arithmetic 
 integer Gather / Concat / Mul, Reshape targets) stays on the host; Reshape / Transpose /
 Slice are views or copies.  Unsupported ops are reported when the graph is LOADED.  On the
 CPU every node runs the fp32 NCHW reference (the numerics oracle for the GPU path).
+
+Compute nodes that no HIP path covers run on a torch fp32 tier on the GPU (a conv whose
+weight is computed, a ConvTranspose with kernel != stride, AveragePool, GlobalMaxPool, a
+ReduceMean outside the LayerNorm pattern, unusual Resize modes, ...).  They are never silent:
+the load-time scan logs every node that can only take that tier (``fallback_nodes``;
+``strict=True`` refuses such a graph), and every execution on it is counted per op type in
+``fallback_counts`` with a warning the first time a node takes it.
 """
 from __future__ import annotations
 
+import logging
 import math
 from dataclasses import dataclass
 from pathlib import Path
@@ -37,6 +45,8 @@ import torch.nn.functional as F
 from .. import ops
 from ..ops import cnn
 from ..utils import onnx_lite as ox
+
+log = logging.getLogger("lumen.onnx")
 
 _ACTS = {"Relu": "relu", "Sigmoid": "sigmoid", "HardSwish": "hardswish", "LeakyRelu": "leaky"}
 
@@ -51,6 +61,11 @@ _UNARY = {"Relu": 0, "Sigmoid": 1, "Tanh": 2, "Exp": 3, "Log": 4, "Sqrt": 5, "Ne
           "HardSwish": 9, "HardSigmoid": 10, "LeakyRelu": 11, "Clip": 12, "Floor": 13, "Ceil": 14, "Erf": 15}
 _BINARY = {"Add": 0, "Sub": 1, "Mul": 2, "Div": 3, "Pow": 4, "Max": 5, "Min": 6}
 _RESIZE_MODES = {"half_pixel": 0, "align_corners": 1, "asymmetric": 2, "pytorch_half_pixel": 3}
+# ops whose generic path is data movement / host shape arithmetic (not a compute fallback)
+_DATA_OPS = frozenset({"Flatten", "Reshape", "Transpose", "Squeeze", "Unsqueeze", "Shape", "Gather", "Slice", "Cast",
+                       "Constant", "Identity", "Dropout", "Concat", "ArgMax"})
+# planned "node" steps of these ops have no HIP path on the GPU (known at load time)
+_TORCH_ONLY = frozenset({"Conv", "ConvTranspose", "AveragePool", "GlobalMaxPool", "ReduceMean"})
 
 
 def _pad_to(c: int, m: int) -> int:
@@ -72,7 +87,7 @@ class _V:
 
 class OnnxGraph:
     def __init__(self, src: Union[str, Path, bytes, ox.Model], device: Union[str, torch.device] = "cpu",
-                 dtype: Optional[torch.dtype] = None):
+                 dtype: Optional[torch.dtype] = None, strict: bool = False):
         self.model = src if isinstance(src, ox.Model) else ox.load_model(src)
         g = self.model.graph
         self.device = torch.device(device)
@@ -88,6 +103,45 @@ class OnnxGraph:
                 self.consumers.setdefault(x, []).append(n)
         self._dev_init: dict = {}
         self.plan = self._plan(g)
+        self.fallback_counts: dict[str, int] = {}
+        self._fallback_seen: set = set()
+        self.fallback_nodes = self._scan_fallbacks() if self.gpu else []
+        if self.fallback_nodes:
+            ops_ = sorted({op for op, _ in self.fallback_nodes})
+            msg = (f"ONNX graph: {len(self.fallback_nodes)} compute node(s) have no HIP path and run on the "
+                   f"torch fp32 tier on {self.device}: {', '.join(ops_)} "
+                   f"({', '.join(nm for _, nm in self.fallback_nodes[:8])}{' ...' if len(self.fallback_nodes) > 8 else ''})")
+            if strict:
+                raise NotImplementedError(msg)
+            log.warning(msg)
+
+    def _scan_fallbacks(self) -> list[tuple[str, str]]:
+        """(op, node name) of the planned generic steps that can only take the torch tier."""
+        out = []
+        for kind, step in self.plan:
+            if kind == "conv" and step.get("mode") == "ref":
+                out.append(("Conv", step.get("name", step["out"])))
+            elif kind == "node":
+                op, a = step.op_type, step.attrs
+                bad = op in _TORCH_ONLY
+                if op == "MaxPool":
+                    p = a.get("pads", [0, 0, 0, 0])
+                    bad = p[:2] != p[2:] or bool(a.get("ceil_mode", 0))
+                if op in ("Resize", "Upsample"):
+                    mode = a.get("mode", "nearest")
+                    bad = mode not in ("nearest", "linear") or (
+                        mode == "linear" and a.get("coordinate_transformation_mode", "half_pixel") not in _RESIZE_MODES)
+                if bad:
+                    out.append((op, step.name or (step.outputs[0] if step.outputs else op)))
+        return out
+
+    def _note_fallback(self, n) -> None:
+        self.fallback_counts[n.op_type] = self.fallback_counts.get(n.op_type, 0) + 1
+        key = id(n)
+        if key not in self._fallback_seen:
+            self._fallback_seen.add(key)
+            log.warning("ONNX node %s (%s) ran on the torch fp32 tier on %s (no HIP path for its inputs)",
+                        n.name or n.outputs[0], n.op_type, self.device)
 
     # ------------------------------------------------------------------ planning
     def _single_consumer(self, name: str, op: str):
@@ -356,6 +410,8 @@ class OnnxGraph:
 
     def _conv(self, s: dict, vals) -> _V:
         x = self._get(vals, s["x"])
+        if self.gpu and s.get("mode") == "ref":
+            self.fallback_counts["Conv"] = self.fallback_counts.get("Conv", 0) + 1
         if not self.gpu or s.get("mode") == "ref":
             xt = x.nchw().float() if self.gpu else x.nchw()
             pt, pl, pb, pr = s["pads"][0], s["pads"][1], s["pads"][2], s["pads"][3]
@@ -468,6 +524,8 @@ class OnnxGraph:
         t = [i.nchw() if i is not None else None for i in ins]
         if self.gpu:
             t = [x.float() if x is not None and x.is_floating_point() else x for x in t]
+            if op not in _DATA_OPS and any(x is not None and x.is_floating_point() for x in t):
+                self._note_fallback(n)
 
         def out(*ys):
             return [_V(y.to(self.dtype) if self.gpu and y.is_floating_point() else y) for y in ys]

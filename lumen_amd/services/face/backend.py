@@ -493,6 +493,39 @@ class MI355XFaceBackend:
             return self._dp["embed"].map(items)
         return self._emb_batcher.map(items)
 
+    def embed_batch_detections(self, images: Sequence[np.ndarray], dets: Sequence[Sequence[FaceDetection]],
+                               max_faces: Sequence[int]) -> list[list[tuple[FaceDetection, np.ndarray]]]:
+        """Every face of a batch of decoded images (detections capped at max_faces[i] when > 0)
+        aligned + embedded as ONE recogniser batch -> per image [(FaceDetection, embedding)].
+        A failed embedding yields zero vectors like the reference (face_model.py:357-364)."""
+        kept, flat, owner = [], [], []
+        for k, (img, d) in enumerate(zip(images, dets)):
+            mf = int(max_faces[k])
+            d = list(d[:mf]) if 0 < mf < len(d) else list(d)
+            kept.append(d)
+            for f in d:
+                flat.append((img, f.landmarks, f.bbox))
+                owner.append(k)
+        embs: list = []
+        if flat:
+            try:
+                embs = self._embed_batch(flat)
+            except Exception as e:  # noqa: BLE001
+                log.warning("face embedding failed: %s", e)
+                embs = [np.zeros((self.rec.cfg.embedding,), np.float32) for _ in flat]
+        per: list = [[] for _ in images]
+        for k, e in zip(owner, embs):
+            per[k].append(e)
+        return [list(zip(kept[k], per[k])) for k in range(len(images))]
+
+    def detect_and_embed_images(self, images: Sequence[np.ndarray], params: Sequence[DetParams],
+                                max_faces: int = -1) -> list[list[tuple[FaceDetection, np.ndarray]]]:
+        """Batched detect + embed of decoded images on THIS process's device (one detector batch,
+        one recogniser batch): the per-rank body of the SPMD data-parallel path
+        (services/face/spmd.py) and of the DP worker's "det_emb" task."""
+        dets = self.detect_images(images, params)
+        return self.embed_batch_detections(images, dets, [max_faces] * len(images))
+
     def get_runtime_info(self) -> BackendInfo:
         return self.get_info()
 
@@ -568,26 +601,9 @@ def dp_worker(device: str, resources: GenericResources, max_batch: int = 64):
             return out
         if kind != "det_emb":
             raise ValueError(f"unknown face task kind {kind!r}")
-        flat, owner = [], []
-        for k, d in zip(ok, dets):
-            mf = items[k][2]
-            d = d[:mf] if 0 < mf < len(d) else d
-            out[k] = d
-            for f in d:
-                flat.append((imgs[k], f.landmarks, f.bbox))
-                owner.append(k)
-        embs: list = []
-        if flat:
-            try:
-                embs = b._embed_batch(flat)
-            except Exception as e:  # noqa: BLE001  (reference: zero vectors on failure)
-                log.warning("face embedding failed: %s", e)
-                embs = [np.zeros((b.rec.cfg.embedding,), np.float32) for _ in flat]
-        per: dict = {k: [] for k in ok}
-        for k, e in zip(owner, embs):
-            per[k].append(e)
-        for k in ok:
-            out[k] = list(zip(out[k], per[k]))
+        res = b.embed_batch_detections([imgs[k] for k in ok], dets, [items[k][2] for k in ok])
+        for k, r in zip(ok, res):
+            out[k] = r
         return out
 
     return fn

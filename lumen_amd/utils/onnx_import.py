@@ -22,6 +22,16 @@ names are recovered, in order of reliability, from:
    ``visual.proj`` / ``text_projection``).
 ``Gemm`` weights honour ``transB``; fp16 graphs are widened to fp32 (the models cast to
 their compute dtype on load).
+
+Quantised packs (the reference selects ``vision.{precision}.onnx`` for precision ``int8`` /
+``q4fp16``, packages/lumen-clip/src/lumen_clip/backends/onnxrt_backend.py:245-289) are
+dequantised first (:func:`dequantize_model`): ``DequantizeLinear`` of an initializer (QDQ,
+per-tensor or per-axis), ``MatMulInteger`` with an int8 / uint8 weight and its
+``<w>_scale`` / ``<w>_zero_point`` initializers (dynamic quantisation), and ``MatMulNBits``
+(com.microsoft, 4-bit blockwise, fp16 / fp32 scales, optional packed zero points) become
+plain float ``MatMul`` operands under the original weight name, so the name recovery above
+applies unchanged.  The native models then run the dequantised weights in their own compute
+dtype (bf16 / fp8 on the GPU) -- the int8 / 4-bit ONNX runtime kernels are not emulated.
 """
 from __future__ import annotations
 
@@ -59,9 +69,116 @@ def _scope_to_param(node_name: str, suffix: str = "weight") -> Optional[str]:
     return ".".join(out) + "." + suffix
 
 
+# ---------------------------------------------------------------------------- quantised packs
+def _strip(name: str, suffixes: Sequence[str]) -> str:
+    for suf in suffixes:
+        if name.endswith(suf):
+            return name[: -len(suf)]
+    return name
+
+
+def dequantize_linear(q: np.ndarray, scale: np.ndarray, zp: Optional[np.ndarray], axis: int = 1) -> np.ndarray:
+    """ONNX DequantizeLinear: (q - zero_point) * scale, per tensor or along ``axis``."""
+    x = q.astype(np.float32)
+    sc = np.asarray(scale, np.float32)
+    z = np.zeros_like(sc) if zp is None else np.asarray(zp).astype(np.float32)
+    if sc.ndim == 1 and sc.size > 1:
+        shape = [1] * x.ndim
+        shape[axis % x.ndim] = sc.size
+        sc, z = sc.reshape(shape), z.reshape(shape)
+    return (x - z) * sc
+
+
+def dequantize_nbits(b: np.ndarray, scales: np.ndarray, zero_points: Optional[np.ndarray], K: int, N: int,
+                     bits: int = 4, block_size: int = 32) -> np.ndarray:
+    """com.microsoft MatMulNBits weight -> float [N, K] (the nn.Linear layout).  ``b``: uint8
+    [N, n_blocks, block_size * bits / 8], values packed low nibble first; ``scales`` [N * n_blocks];
+    ``zero_points``: uint8 packed like b (or float, one per block), default 2^(bits-1)."""
+    if bits != 4:
+        raise ValueError(f"MatMulNBits with {bits} bits is not supported (4-bit packs only)")
+    nb = -(-K // block_size)
+    raw = np.asarray(b, np.uint8).reshape(N, nb, block_size // 2)
+    q = np.empty((N, nb, block_size), np.float32)
+    q[..., 0::2] = raw & 0x0F
+    q[..., 1::2] = raw >> 4
+    sc = np.asarray(scales).astype(np.float32).reshape(N, nb)
+    if zero_points is None:
+        zp = np.full((N, nb), 8.0, np.float32)
+    elif np.asarray(zero_points).dtype == np.uint8:
+        zr = np.asarray(zero_points, np.uint8).reshape(N, -1)
+        zz = np.empty((N, zr.shape[1] * 2), np.float32)
+        zz[:, 0::2] = zr & 0x0F
+        zz[:, 1::2] = zr >> 4
+        zp = zz[:, :nb]
+    else:
+        zp = np.asarray(zero_points).astype(np.float32).reshape(N, nb)
+    w = (q - zp[..., None]) * sc[..., None]
+    return w.reshape(N, nb * block_size)[:, :K]
+
+
+def dequantize_model(m: onnx_lite.Model) -> onnx_lite.Model:
+    """Replace quantised weight patterns by float initializers + plain MatMul (see module doc)."""
+    g = m.graph
+    inits = dict(g.initializers)
+    rename: dict[str, str] = {}
+    nodes: list = []
+    spent: set = set()          # quantised tensors folded into a float initializer
+    for n in g.nodes:
+        op = n.op_type
+        if op == "DequantizeLinear" and n.inputs and n.inputs[0] in inits:
+            q = inits[n.inputs[0]]
+            sc = inits[n.inputs[1]]
+            zp = inits.get(n.inputs[2]) if len(n.inputs) > 2 and n.inputs[2] else None
+            base = _strip(n.inputs[0], ("_quantized", "_q", "_int8"))
+            name = base if base != n.inputs[0] else n.outputs[0]
+            inits[name] = dequantize_linear(q, sc, zp, int(n.attrs.get("axis", 1)))
+            rename[n.outputs[0]] = name
+            spent.update(x for x in n.inputs if x)
+            continue
+        if op == "MatMulInteger" and len(n.inputs) > 1 and n.inputs[1] in inits:
+            wq = n.inputs[1]
+            base = _strip(wq, ("_quantized", "_q", "_int8"))
+            sc = inits.get(base + "_scale")
+            if sc is None:
+                raise ValueError(f"MatMulInteger {n.name or n.outputs[0]}: no {base}_scale initializer")
+            zp = inits.get(n.inputs[3]) if len(n.inputs) > 3 and n.inputs[3] else inits.get(base + "_zero_point")
+            inits[base] = dequantize_linear(inits[wq], sc, zp, 1)      # B [K, N]: per-column scales
+            spent.update({wq, base + "_scale", base + "_zero_point"} | ({n.inputs[3]} if len(n.inputs) > 3 else set()))
+            nodes.append(onnx_lite.Node("MatMul", [n.inputs[0], base], list(n.outputs), name=n.name))
+            continue
+        if op == "MatMulNBits" and len(n.inputs) > 2 and n.inputs[1] in inits:
+            a = n.attrs
+            K, N = int(a["K"]), int(a["N"])
+            zp = inits.get(n.inputs[3]) if len(n.inputs) > 3 and n.inputs[3] else None
+            w = dequantize_nbits(inits[n.inputs[1]], inits[n.inputs[2]], zp, K, N, int(a.get("bits", 4)),
+                                 int(a.get("block_size", 32)))
+            base = _strip(n.inputs[1], ("_Q4", "_Q8", "_q4", "_quantized"))
+            inits[base] = w.T                                            # MatMul B operand [K, N]
+            spent.update(x for x in n.inputs[1:4] if x)
+            out = n.outputs[0]
+            if len(n.inputs) > 5 and n.inputs[5]:                        # fused bias input
+                nodes.append(onnx_lite.Node("MatMul", [n.inputs[0], base], [out + "__mm"], name=n.name))
+                nodes.append(onnx_lite.Node("Add", [n.inputs[5], out + "__mm"], [out], name=n.name + "_bias"))
+            else:
+                nodes.append(onnx_lite.Node("MatMul", [n.inputs[0], base], [out], name=n.name))
+            continue
+        nodes.append(n)
+    if not spent:
+        return m
+    for n in nodes:
+        n.inputs = [rename.get(x, x) for x in n.inputs]
+    used = {x for n in nodes for x in n.inputs}
+    keep = {k: v for k, v in inits.items() if k in used or k not in spent}
+    g2 = onnx_lite.Graph(nodes=nodes, initializers=keep, inputs=list(g.inputs),
+                         outputs=[rename.get(x, x) for x in g.outputs], name=g.name)
+    return onnx_lite.Model(graph=g2, opset=m.opset, ir_version=m.ir_version)
+
+
 def recover_state_dict(src: Union[str, Path, bytes, onnx_lite.Model]) -> tuple[dict, list]:
-    """(name -> np.float32 array in PyTorch layout, [unresolved (node, array)]) of one graph."""
+    """(name -> np.float32 array in PyTorch layout, [unresolved (node, array)]) of one graph
+    (quantised weights are dequantised first, :func:`dequantize_model`)."""
     m = src if isinstance(src, onnx_lite.Model) else onnx_lite.load_model(src)
+    m = dequantize_model(m)
     g = m.graph
     inits = g.initializers
     consumers: dict[str, list] = {}
@@ -84,7 +201,7 @@ def recover_state_dict(src: Union[str, Path, bytes, onnx_lite.Model]) -> tuple[d
             if node.op_type == "MatMul" and idx == 1 and np.ndim(arr) == 2:
                 w = f32(arr).T
                 pname = None
-                for nxt, _ in consumers.get(node.outputs[0], []):
+                for nxt, _ in _downstream(consumers, node.outputs[0]):
                     if nxt.op_type == "Add":
                         other = [x for x in nxt.inputs if x != node.outputs[0]]
                         if other and other[0] in inits and not _is_generated(other[0]):
@@ -123,6 +240,23 @@ def recover_state_dict(src: Union[str, Path, bytes, onnx_lite.Model]) -> tuple[d
         if not placed:
             out.setdefault(name, f32(arr))
     return out, unresolved
+
+
+def _downstream(consumers: dict, name: str, hops: int = 3) -> list:
+    """Consumers of ``name``, looking through the Cast / Mul of a dequantised product
+    (MatMulInteger -> Cast -> Mul(scales) -> Add(bias))."""
+    out, frontier = [], [name]
+    for _ in range(hops):
+        nxt = []
+        for v in frontier:
+            for node, i in consumers.get(v, []):
+                out.append((node, i))
+                if node.op_type in ("Cast", "Mul"):
+                    nxt.append(node.outputs[0])
+        frontier = nxt
+        if not frontier:
+            break
+    return out
 
 
 def pick_file(root: Path, component: str, precision: Optional[str] = None) -> Optional[Path]:

@@ -234,3 +234,81 @@ def test_stale_ring_descriptor_is_dropped():
         assert len(r) == 16 and r[3][0] == 3.0
     finally:
         pool.close()
+
+
+# ----------------------------------------------------------------------------- SPMD face DP (RCCL path, gloo here)
+def _face_backend_cpu(cache):
+    from lumen_amd.resources.config import ModelConfig, Runtime
+    from lumen_amd.services.common import load_model_resources
+    from lumen_amd.services.face.backend import MI355XFaceBackend
+
+    res = load_model_resources(cache, ModelConfig(model="buffalo_tiny", runtime=Runtime.onnx))
+    be = MI355XFaceBackend(res, device="cpu")
+    be.initialize()
+    return be
+
+
+def _spmd_images():
+    from lumen_amd.utils.image import decode_rgb
+
+    return [decode_rgb(encode_jpeg(np.random.default_rng(s).integers(0, 255, (96, 120 + 8 * s, 3), dtype=np.uint8)))
+            for s in range(5)]
+
+
+def _spmd_face_rank(rank, world, port, cache, q):
+    import os
+
+    import torch
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from lumen_amd.parallel import Communicator, destroy, init_distributed
+    from lumen_amd.services.face.backend import DetParams
+    from lumen_amd.services.face.spmd import SPMDFaceRunner
+
+    st = init_distributed(tp_size=1, device=torch.device("cpu"), timeout_s=120)
+    try:
+        be = _face_backend_cpu(cache)
+        imgs = _spmd_images()
+        run = SPMDFaceRunner(be, Communicator(st.dp_group, ipc=False), torch.device("cpu"))
+        out = run.run(imgs, [DetParams(0.0, 0.3, 0, 10000)] * len(imgs), max_faces=4)
+        q.put((rank, [[(f.bbox, f.confidence, f.landmarks, e.tolist()) for f, e in faces] for faces in out]))
+        be.close()
+    finally:
+        destroy()
+
+
+def test_spmd_face_world2_matches_single_process(tmp_path):
+    """Each of 2 gloo ranks detects + embeds its shard of 5 images; one all-gather of the packed
+    (bbox, confidence, landmarks, embedding) rows gives every rank the single-process result."""
+    import multiprocessing as mp
+
+    from lumen_amd.models.face import write_face_model
+    from lumen_amd.services.face.backend import DetParams
+    from tests.test_parallel_cpu import _port
+
+    write_face_model(tmp_path / "models" / "buffalo_tiny", "buffalo_tiny")
+    be = _face_backend_cpu(tmp_path)
+    imgs = _spmd_images()
+    ref = be.detect_and_embed_images(imgs, [DetParams(0.0, 0.3, 0, 10000)] * len(imgs), max_faces=4)
+    be.close()
+    assert sum(len(f) for f in ref) > 0
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_spmd_face_rank, args=(r, 2, port, tmp_path, qq)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(qq.get(timeout=300) for _ in range(2))
+    for p in ps:
+        p.join(60)
+    assert all(p.exitcode == 0 for p in ps)
+    for rank in (0, 1):
+        got = res[rank]
+        assert [len(f) for f in got] == [len(f) for f in ref]
+        for gf, rf in zip(got, ref):
+            for (bb, conf, lm, emb), (f, e) in zip(gf, rf):
+                np.testing.assert_allclose(bb, f.bbox, atol=1e-3)
+                assert abs(conf - f.confidence) < 1e-5
+                np.testing.assert_allclose(np.asarray(lm).ravel(), np.asarray(f.landmarks).ravel(), atol=1e-3)
+                assert _cos(emb, e) > 0.99999

@@ -279,7 +279,9 @@ def test_linear_dec_norm_folding_matches_cpu(fp8, M, N, K, glu):
 @pytest.mark.parametrize("lens", [[1, 64, 65], [700, 3, 2048 + 17]])
 def test_paged_decode_fused_rope_matches_rope_kv(H, Hkv, D, lens):
     """Decode attention with RoPE + current-token cache write fused in (q unrotated) == rope_kv
-    then paged_decode: same output bits and the same K / V cache contents."""
+    then paged_decode: the same K / V cache contents, and the same attention output up to the
+    summation order of the current token's score (the fused kernel takes q . k_cur from
+    registers as a lane-group dot product instead of reading the token back through MFMA)."""
     g = torch.Generator().manual_seed(H + D + len(lens))
     B = len(lens)
     maxb = max(-(-L // 64) for L in lens)
@@ -300,8 +302,10 @@ def test_paged_decode_fused_rope_matches_rope_kv(H, Hkv, D, lens):
     q2, k2, v2 = qkv.to(DEV), kc.to(DEV), vc.to(DEV)
     got = llm.paged_decode(q2, k2, v2, bt.to(DEV), ctx.to(DEV), H, Hkv,
                            rope=(pos.to(DEV), cs.to(DEV), slots.to(DEV)))
+    torch.cuda.synchronize()
     assert torch.equal(k2, k1) and torch.equal(v2, v1)
-    assert torch.equal(got, ref)
+    assert _rel(got, ref) < 2e-3
+    assert (got.float() - ref.float()).abs().max().item() < 2e-2
     assert torch.equal(q2, qkv.to(DEV))            # the QKV rows are not rotated in place
 
 

@@ -48,3 +48,28 @@ def test_ocrnet_graph_gpu_all_hip():
     got = gpu.run({"x": x.cuda()})
     for a, b in zip(got, ref):
         assert _rel(a, b) < 3e-2, _rel(a, b)
+
+
+def test_torch_tier_nodes_are_reported_at_load_and_counted():
+    """A compute node with no HIP path (AveragePool) is listed when the graph is loaded, counted
+    when it runs on the torch tier, and refused with strict=True; the HIP-covered graphs report
+    nothing."""
+    import numpy as np
+
+    N = ox.Node
+    g = ox.Graph(nodes=[N("Conv", ["x", "w"], ["c"], attrs={"kernel_shape": [3, 3], "pads": [1, 1, 1, 1]}),
+                        N("AveragePool", ["c"], ["y"], attrs={"kernel_shape": [2, 2], "strides": [2, 2]})],
+                 initializers={"w": (np.random.default_rng(0).standard_normal((16, 8, 3, 3)) * 0.1).astype(np.float32)},
+                 inputs=["x"], outputs=["y"])
+    data = ox.write_model(g)
+    gpu = OnnxGraph(data, device="cuda")
+    assert [op for op, _ in gpu.fallback_nodes] == ["AveragePool"]
+    x = torch.randn(1, 8, 16, 16)
+    got = gpu.run({"x": x.cuda()})[0]
+    ref = OnnxGraph(data).run({"x": x})[0]
+    assert _rel(got, ref) < 3e-2
+    assert gpu.fallback_counts == {"AveragePool": 1}
+    with pytest.raises(NotImplementedError, match="AveragePool"):
+        OnnxGraph(data, device="cuda", strict=True)
+    g2, _ = resnet_graph()
+    assert OnnxGraph(ox.write_model(g2), device="cuda").fallback_nodes == []

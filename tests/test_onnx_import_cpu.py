@@ -162,3 +162,103 @@ def test_vlm_service_serves_onnx_pack(tmp_path):
     (src / "model_info.json").write_text(json.dumps(info))
     got = run()
     assert got == ref
+
+
+# ----------------------------------------------------------------------------- quantised CLIP packs
+def _quantize_pack(src_path, dst_path, mode):
+    """Re-encode every generated MatMul weight of an exported graph the way ONNX Runtime's
+    quantisers do: "qdq" (DequantizeLinear of an int8 per-channel initializer), "dynamic"
+    (MatMulInteger + <w>_scale / <w>_zero_point, uint8 asymmetric per tensor), "q4"
+    (com.microsoft MatMulNBits, 4-bit blocks of 32, fp16 scales, no zero points)."""
+    from lumen_amd.utils import onnx_lite as ox
+
+    m = ox.load_model(src_path)
+    g = m.graph
+    inits = dict(g.initializers)
+    nodes = []
+    for n in g.nodes:
+        if n.op_type != "MatMul" or n.inputs[1] not in inits or not n.inputs[1].startswith("onnx::"):
+            nodes.append(n)
+            continue
+        wname = n.inputs[1]
+        B = np.asarray(inits.pop(wname), np.float32)          # [K, N]
+        K, N = B.shape
+        if mode == "qdq":
+            sc = np.abs(B).max(0) / 127 + 1e-12                # per output column (axis 1)
+            inits[wname + "_quantized"] = np.clip(np.round(B / sc), -127, 127).astype(np.int8)
+            inits[wname + "_scale"] = sc.astype(np.float32)
+            inits[wname + "_zero_point"] = np.zeros(N, np.int8)
+            dq = wname + "_DequantizeLinear_Output"
+            nodes.append(ox.Node("DequantizeLinear", [wname + "_quantized", wname + "_scale", wname + "_zero_point"],
+                                 [dq], name=n.name + "_dq", attrs={"axis": 1}))
+            nodes.append(ox.Node("MatMul", [n.inputs[0], dq], list(n.outputs), name=n.name))
+        elif mode == "dynamic":
+            lo, hi = min(B.min(), 0.0), max(B.max(), 0.0)
+            sc = (hi - lo) / 255 + 1e-12
+            zp = np.uint8(np.clip(np.round(-lo / sc), 0, 255))
+            inits[wname + "_quantized"] = np.clip(np.round(B / sc) + zp, 0, 255).astype(np.uint8)
+            inits[wname + "_scale"] = np.array(sc, np.float32)
+            inits[wname + "_zero_point"] = np.array(zp, np.uint8)
+            o = n.outputs[0]
+            nodes += [ox.Node("DynamicQuantizeLinear", [n.inputs[0]], [o + "_xq", o + "_xs", o + "_xz"]),
+                      ox.Node("MatMulInteger", [o + "_xq", wname + "_quantized", o + "_xz", wname + "_zero_point"],
+                              [o + "_i32"], name=n.name + "_quant"),
+                      ox.Node("Cast", [o + "_i32"], [o + "_f"], attrs={"to": 1}),
+                      ox.Node("Mul", [o + "_xs", wname + "_scale"], [o + "_s"]),
+                      ox.Node("Mul", [o + "_f", o + "_s"], [o])]
+        else:
+            bs = 32
+            Wt = B.T                                            # [N, K]
+            nb = -(-K // bs)
+            Wp = np.zeros((N, nb * bs), np.float32)
+            Wp[:, :K] = Wt
+            blk = Wp.reshape(N, nb, bs)
+            sc = np.abs(blk).max(-1) / 7 + 1e-12
+            q = (np.clip(np.round(blk / sc[..., None]), -8, 7) + 8).astype(np.uint8)
+            packed = (q[..., 0::2] | (q[..., 1::2] << 4)).astype(np.uint8)
+            inits[wname + "_Q4"] = packed
+            inits[wname + "_scales"] = sc.astype(np.float16).reshape(-1)
+            nodes.append(ox.Node("MatMulNBits", [n.inputs[0], wname + "_Q4", wname + "_scales"], list(n.outputs),
+                                 name=n.name, domain="com.microsoft",
+                                 attrs={"K": K, "N": N, "bits": 4, "block_size": bs}))
+    g2 = ox.Graph(nodes=nodes, initializers=inits, inputs=g.inputs, outputs=g.outputs, name=g.name)
+    dst_path.write_bytes(ox.write_model(g2, opset=17))
+
+
+@pytest.mark.parametrize("mode,prec,tol", [("qdq", "int8", 0.995), ("dynamic", "int8", 0.99), ("q4", "q4fp16", 0.97)])
+def test_quantized_clip_pack_imports(tmp_path, mode, prec, tol):
+    """vision/text.{int8,q4fp16}.onnx (QDQ, MatMulInteger dynamic, MatMulNBits 4-bit) load onto the
+    native CLIP model: dequantised weights under their recovered names, embeddings close to the
+    fp32 pack (quantisation error only)."""
+    from lumen_amd.resources.config import ModelConfig, Runtime
+    from lumen_amd.resources.synthetic import write_clip_model
+    from lumen_amd.services.clip.backend import create_backend
+    from lumen_amd.services.clip.resources import ResourceLoader
+    from lumen_amd.utils.image import encode_jpeg
+
+    src = tmp_path / "models" / "clip-tiny"
+    write_clip_model(src, "clip-tiny", preset="tiny", dataset=None)
+    imgs = [encode_jpeg(np.random.default_rng(i).integers(0, 255, (40, 40, 3), dtype=np.uint8)) for i in range(3)]
+
+    def embed(precision=None):
+        settings = type("S", (), {"device": "cpu", "batch_size": 4})()
+        res = ResourceLoader.load_model_resources(tmp_path, ModelConfig(model="clip-tiny", runtime=Runtime.onnx,
+                                                                        precision=precision))
+        b = create_backend(settings, res, "onnx", precision)
+        b.initialize()
+        try:
+            return b.image_batch_to_vectors(imgs), b.text_batch_to_vectors(["a cat", "two dogs"])
+        finally:
+            b.close()
+
+    _write_clip_onnx(src)
+    (src / "model.safetensors").unlink()
+    ref_i, ref_t = embed()
+    for comp in ("vision", "text"):
+        _quantize_pack(src / "onnx" / f"{comp}.onnx", src / "onnx" / f"{comp}.{prec}.onnx", mode)
+    sd, unresolved = onnx_import.recover_state_dict(src / "onnx" / f"vision.{prec}.onnx")
+    assert not any(k.endswith(("_quantized", "_Q4", "_scales")) for k in sd)
+    got_i, got_t = embed(prec)
+    for a, b in ((got_i, ref_i), (got_t, ref_t)):
+        cos = [float(np.dot(x, y) / np.linalg.norm(x) / np.linalg.norm(y)) for x, y in zip(a, b)]
+        assert min(cos) > tol, cos

@@ -115,3 +115,76 @@ def test_db_boxes_gpu_matches_host(dtype):
         np.testing.assert_array_equal(b, ref_b)
         np.testing.assert_allclose(s, ref_s, rtol=1e-4)
     assert len(got[3][0]) == 0 and len(got[0][0]) > 0
+
+
+def _cc_reference(binmaps, min_size):
+    """CPU emulation of db_components: 8-connected components (scipy), root = the raster-first
+    (smallest global) pixel index, boundary pixels (a 4-neighbour outside or the map border) of
+    components whose pixel-centre bbox spans >= min_size on some axis -> set of (root, x, y)."""
+    from scipy import ndimage
+
+    out = set()
+    n, H, W = binmaps.shape
+    for j in range(n):
+        lab, k = ndimage.label(binmaps[j], structure=np.ones((3, 3), bool))
+        if k == 0:
+            continue
+        ys, xs = np.nonzero(lab)
+        ids = lab[ys, xs]
+        gidx = j * H * W + ys * W + xs
+        root = np.full(k + 1, np.iinfo(np.int64).max)
+        np.minimum.at(root, ids, gidx)
+        pad = np.pad(binmaps[j], 1)
+        inner = pad[1:-1, 2:] & pad[1:-1, :-2] & pad[2:, 1:-1] & pad[:-2, 1:-1]
+        bnd = binmaps[j] & ~inner
+        bnd[0, :] |= binmaps[j][0, :]
+        bnd[-1, :] |= binmaps[j][-1, :]
+        bnd[:, 0] |= binmaps[j][:, 0]
+        bnd[:, -1] |= binmaps[j][:, -1]
+        x0, x1 = np.full(k + 1, W), np.full(k + 1, -1)
+        y0, y1 = np.full(k + 1, H), np.full(k + 1, -1)
+        np.minimum.at(x0, ids, xs)
+        np.maximum.at(x1, ids, xs)
+        np.minimum.at(y0, ids, ys)
+        np.maximum.at(y1, ids, ys)
+        keep = ((x1 - x0) >= min_size) | ((y1 - y0) >= min_size)
+        by, bx = np.nonzero(bnd)
+        bid = lab[by, bx]
+        for y, x, c in zip(by, bx, bid):
+            if keep[c]:
+                out.add((int(root[c]), int(x), int(y)))
+    return out
+
+
+@pytest.mark.parametrize("kind", ["text", "noise"])
+def test_db_components_exact_vs_cpu(kind):
+    """Tile-local LDS labelling + cross-tile border merge + flatten/bbox + boundary (db_post.hip)
+    vs an exact CPU emulation: the same (root, x, y) boundary set, on text-like rectangle maps
+    (components crossing 32-px tile borders, diagonal-only contacts) and on noise maps."""
+    rng = np.random.default_rng(7)
+    n, H, W = 3, 150, 203                                    # partial tiles on both axes
+    maps = np.zeros((n, H, W), np.float32)
+    if kind == "text":
+        for j in range(n):
+            for _ in range(25):
+                y, x = rng.integers(0, H - 12), rng.integers(0, W - 60)
+                maps[j, y:y + rng.integers(3, 12), x:x + rng.integers(5, 60)] = rng.uniform(0.5, 1.0)
+            maps[j, 31, 31] = maps[j, 32, 32] = 0.9          # diagonal contact across a tile corner
+            maps[j, 63, 95] = maps[j, 64, 94] = 0.9          # anti-diagonal across a corner
+    else:
+        maps[:] = rng.uniform(0, 1, (n, H, W))
+    thr = torch.tensor([0.3, 0.45, 0.6], dtype=torch.float32)
+    prob = torch.from_numpy(maps)
+    lab = torch.empty(5 * n * H * W, dtype=torch.int32, device=DEV)
+    cap = n * H * W
+    pts = torch.empty((cap, 3), dtype=torch.int32, device=DEV)
+    cnt = torch.zeros(1, dtype=torch.int32, device=DEV)
+    from lumen_amd._native import hip_ops
+
+    for min_size in (0, 3):
+        hip_ops().db_components(prob.to(DEV), thr.to(DEV), lab, pts, cnt, min_size)
+        K = int(cnt.item())
+        got = {tuple(r) for r in pts[:K].cpu().numpy().tolist()}
+        assert len(got) == K
+        ref = _cc_reference(maps > thr.numpy()[:, None, None], min_size)
+        assert got == ref

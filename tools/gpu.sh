@@ -8,6 +8,9 @@
 #   bench          headline bench.py (defaults)
 #   prof_bench     rocprofv3 kernel stats of the headline bench (3 steps)
 #   gemm           tools/gemm_bench_tiles.py on the ViT-L/14 shapes ($GEMM_TILES, $GEMM_EPI)
+#   llm_tests      fp8 / LLM-op / VLM GPU tests only
+#   post_tests     post-processing / image kernels / OCR GPU tests only
+#   w8bench        tools/w8_decode_bench.py: HBM-cold decode GEMMs ($W8_M rows, default 1,16)
 #   vlm8b / vlm05  tools/vlm_bench.py Llama-3-8B fp8 / FastVLM-0.5B
 #   prof_vlm8b     rocprofv3 kernel stats of the 8B fp8 decode bench (batch 16; prof_vlm8b_b1: single stream)
 #   face_ocr       tools/face_ocr_bench.py face + ocr
@@ -44,6 +47,13 @@ for task in "$@"; do
     f8)
       step f8_tests 300 python -u -m pytest tests/test_fp8_gpu.py -x -q --timeout 120 --timeout-method thread
       step f8_bench 300 python -u tools/f8_gemm_bench.py --M "${F8_M:-624}" --shapes "${F8_SHAPES:-llama8b}" ;;
+    llm_tests)
+      step llm_tests 400 python -u -m pytest tests/test_fp8_gpu.py tests/test_llm_ops_gpu.py tests/test_vlm_gpu.py \
+        -x -q --timeout 120 --timeout-method thread ;;
+    w8bench) step w8bench 300 python -u tools/w8_decode_bench.py --m "${W8_M:-1,16}" ;;
+    post_tests)
+      step post_tests 300 python -u -m pytest tests/test_postproc_gpu.py tests/test_kernels_gpu.py tests/test_ocr_gpu.py \
+        -x -q --timeout 120 --timeout-method thread ;;
     vlm8b) step vlm8b 600 python tools/vlm_bench.py --preset llava-llama3-8b --fp8 ;;
     vlm05) step vlm05 400 python tools/vlm_bench.py --preset fastvlm-0.5b ;;
     prof_vlm8b)
