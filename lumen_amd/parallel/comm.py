@@ -28,6 +28,14 @@ import torch
 log = logging.getLogger("lumen.comm")
 
 DEFAULT_IPC_MAX_BYTES = int(os.environ.get("LUMEN_IPC_AR_MAX_BYTES", str(512 * 1024)))
+# without RCCL (gloo groups: several TP ranks sharing one GPU in tests) every message the IPC
+# kernel cannot take is staged through the host; cover prefill-sized all-reduces there too
+GLOO_IPC_MAX_BYTES = 32 << 20
+
+
+class TPGroupUnavailable(RuntimeError):
+    """A tensor-parallel peer stopped answering (the IPC all-reduce gave up waiting for it):
+    the group's results are invalid and the service reports UNAVAILABLE."""
 
 
 def _group_ranks(group) -> tuple[int, int]:
@@ -120,6 +128,8 @@ class Communicator:
             ipc = os.environ.get("LUMEN_IPC_ALLREDUCE", "1") == "1"
             ipc = ipc and self.world > 1 and device is not None and device.type == "cuda"
         if ipc and self.world > 1:
+            if self.enabled and dist.get_backend(group) != "nccl":
+                ipc_max_bytes = max(ipc_max_bytes, GLOO_IPC_MAX_BYTES)
             try:
                 self.custom = CustomAllReduce(group, device, ipc_max_bytes)
             except Exception as e:  # noqa: BLE001 - fall back to RCCL, loudly
@@ -188,6 +198,12 @@ class Communicator:
             import torch.distributed as dist
 
             dist.barrier(group=self.group)
+
+    def check(self) -> None:
+        """Raise :class:`TPGroupUnavailable` if an IPC all-reduce gave up on a peer (synchronises:
+        call it at points that already wait for the device, e.g. after a step's token D2H)."""
+        if self.custom is not None and self.custom.error():
+            raise TPGroupUnavailable("tensor-parallel peer not responding (IPC all-reduce timed out)")
 
     def close(self) -> None:
         if self.custom is not None:

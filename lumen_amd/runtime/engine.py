@@ -114,21 +114,21 @@ class Sampler:
         v, i, lse = ops.row_topk(logits, k, with_lse=True, index_offset=self.llm.v0)
         tp = self.llm.tp
         if tp.enabled:
+            # ONE all-gather of the packed (values, indices, lse) rows -- vocab ids < 2^24 are exact
+            # in fp32 -- and the merge (global top-k, lse of the shard lse's) on the device
             import torch.distributed as dist
 
-            if v.is_cuda and dist.get_backend(tp.group) == "gloo":    # gloo gathers host tensors only
-                v, i, lse = v.cpu(), i.cpu(), lse.cpu()
-            vs = [torch.empty_like(v) for _ in range(tp.world)]
-            is_ = [torch.empty_like(i) for _ in range(tp.world)]
-            ls = [torch.empty_like(lse) for _ in range(tp.world)]
-            dist.all_gather(vs, v, group=tp.group)
-            dist.all_gather(is_, i, group=tp.group)
-            dist.all_gather(ls, lse, group=tp.group)
-            v, i = torch.cat(vs, 1), torch.cat(is_, 1)
-            lse = torch.logsumexp(torch.stack(ls, 1), 1)
-            v, order = torch.sort(v, 1, descending=True)
-            i = torch.gather(i, 1, order)
-            v, i = v[:, :k], i[:, :k]
+            B = v.shape[0]
+            packed = torch.cat([v, i.to(torch.float32), lse.view(B, 1)], 1).contiguous()
+            if packed.is_cuda and dist.get_backend(tp.group) == "gloo":    # gloo gathers host tensors only
+                packed = packed.cpu()
+            parts = [torch.empty_like(packed) for _ in range(tp.world)]
+            dist.all_gather(parts, packed, group=tp.group)
+            allp = torch.stack(parts, 1)                                   # [B, world, 2k + 1]
+            vals, ids = allp[..., :k].reshape(B, -1), allp[..., k:2 * k].reshape(B, -1)
+            lse = torch.logsumexp(allp[..., 2 * k], 1)
+            v, order = torch.topk(vals, k, dim=1)
+            i = torch.gather(ids, 1, order).to(torch.int32)
         return v, i, lse
 
     def pick(self, cands, reqs: Sequence[GenRequest]) -> list[int]:
@@ -146,18 +146,20 @@ class Sampler:
 class TPSync:
     """Step broadcast from rank 0 to the follower ranks of a TP group.
 
-    Every step starts with a fixed 8 x int32 header broadcast.  Decode steps (the per-token
-    critical path) then send ONE int32 payload of fixed layout -- ids, positions, cache
-    slots, context lengths, block table -- instead of a pickled object (two broadcasts +
-    pickling on both sides); the header carries the op, batch, table width, top-k and the
-    graph flag.  Prefill / control messages and decode steps whose sampling needs per-row
-    state (temperatures, repetition-penalty token sets) fall back to an object broadcast.
-    The payload lives on the device the group's backend moves (GPU for RCCL, host for gloo).
+    Every step is ONE broadcast of a fixed-capacity int32 buffer: an 8-int header (op, batch,
+    table width, top-k, graph flag) followed, for decode steps, by the step descriptor -- ids,
+    positions, cache slots, context lengths, block table -- so a follower pays one collective
+    and one small D2H per token (the header decides which graph to replay; nothing is pickled).
+    Prefill / control messages and decode steps whose sampling needs per-row state
+    (temperatures, repetition-penalty token sets) add an object broadcast after the header.
+    The buffer lives on the device the group's backend moves (GPU for RCCL, host for gloo).
+    ``capacity`` (ints after the header) must hold 4 * batch + batch * table width of the
+    largest decode step: :func:`tp_sync_capacity`.
     """
 
     OBJ, DECODE = 1, 2
 
-    def __init__(self, group=None, src: int = 0, device: Optional[torch.device] = None):
+    def __init__(self, group=None, src: int = 0, device: Optional[torch.device] = None, capacity: int = 1 << 15):
         import torch.distributed as dist
 
         self.group, self.src = group, src
@@ -165,7 +167,8 @@ class TPSync:
             be = dist.get_backend(group) if dist.is_initialized() else "gloo"
             device = torch.device("cuda", torch.cuda.current_device()) if be == "nccl" else torch.device("cpu")
         self.device = device
-        self.hdr = torch.zeros(8, dtype=torch.int32, device=device)
+        self.capacity = int(capacity)
+        self.buf = torch.zeros(8 + self.capacity, dtype=torch.int32, device=device)
         self.stats = {"tensor_steps": 0, "object_steps": 0}
 
     def _bcast(self, t: torch.Tensor) -> None:
@@ -176,46 +179,50 @@ class TPSync:
     def send(self, msg) -> None:
         import torch.distributed as dist
 
-        self.hdr.fill_(0)
-        self.hdr[0] = self.OBJ
-        self._bcast(self.hdr)
+        self.buf[:8].fill_(0)
+        self.buf[0] = self.OBJ
+        self._bcast(self.buf)
         obj = [msg]
         dist.broadcast_object_list(obj, src=self.src, group=self.group)
         self.stats["object_steps"] += 1
 
     def send_decode(self, ids, pos, slots, bt, ctx, spec, graph: bool) -> None:
-        if spec["inv"] is not None or spec["pen"] is not None:
+        B, W = len(ids), bt.shape[1]
+        if spec["inv"] is not None or spec["pen"] is not None or 4 * B + B * W > self.capacity:
             self.send(("decode", ids, pos, slots, bt, ctx, spec, graph))
             return
-        B, W = len(ids), bt.shape[1]
-        h = torch.tensor([self.DECODE, B, W, spec["k"], int(graph), 0, 0, 0], dtype=torch.int32)
-        self.hdr.copy_(h)
-        self._bcast(self.hdr)
-        pay = np.concatenate([np.asarray(ids, np.int64).astype(np.int32), np.asarray(pos, np.int32),
-                              np.asarray(slots, np.int64).astype(np.int32), np.asarray(ctx, np.int32),
-                              np.asarray(bt, np.int32).reshape(-1)])
-        self._bcast(torch.from_numpy(pay).to(self.device))
+        msg = np.zeros(8 + 4 * B + B * W, np.int32)
+        msg[:8] = [self.DECODE, B, W, spec["k"], int(graph), 0, 0, 0]
+        msg[8:] = np.concatenate([np.asarray(ids, np.int64).astype(np.int32), np.asarray(pos, np.int32),
+                                  np.asarray(slots, np.int64).astype(np.int32), np.asarray(ctx, np.int32),
+                                  np.asarray(bt, np.int32).reshape(-1)])
+        self.buf[:len(msg)].copy_(torch.from_numpy(msg), non_blocking=self.device.type == "cuda")
+        self._bcast(self.buf)
         self.stats["tensor_steps"] += 1
 
     def recv(self):
         import torch.distributed as dist
 
-        self._bcast(self.hdr)
-        h = self.hdr.cpu().tolist()
+        self._bcast(self.buf)
+        p = self.buf.cpu().numpy()
+        h = p[:8].tolist()
         if h[0] == self.OBJ:
             obj = [None]
             dist.broadcast_object_list(obj, src=self.src, group=self.group)
             return obj[0]
         B, W, k, graph = h[1], h[2], h[3], bool(h[4])
-        pay = torch.empty(4 * B + B * W, dtype=torch.int32, device=self.device)
-        self._bcast(pay)
-        p = pay.cpu().numpy()
+        p = p[8:8 + 4 * B + B * W]
         ids = p[:B].astype(np.int64)
         pos = p[B:2 * B].copy()
         slots = p[2 * B:3 * B].astype(np.int64)
         ctx = p[3 * B:4 * B].copy()
         bt = p[4 * B:].reshape(B, W).copy()
         return ("decode", ids, pos, slots, bt, ctx, {"k": k, "inv": None, "pen": None, "pen_ids": None}, graph)
+
+
+def tp_sync_capacity(max_batch: int, max_position: int) -> int:
+    """Descriptor ints of the largest decode step: 4 per row + the block table (64-token blocks)."""
+    return max_batch * (4 + -(-max_position // 64))
 
 
 class DecodeGraphs:
@@ -531,6 +538,9 @@ class LLMEngine:
         logits = self._decode_step(ids, pos, slots, bt, ctx, graph)
         toks = self.sampler.pick(self.sampler.candidates(logits, spec), reqs)
         self.stats["decode_steps"] += 1
+        comm = getattr(self.llm, "comm", None)
+        if comm is not None and self.stats["decode_steps"] % 16 == 0:
+            comm.check()    # the tokens' D2H already waited for the step: the flag read costs a copy only
         still = []
         for r, t in zip(reqs, toks):
             r.ctx += 1

@@ -342,11 +342,12 @@ class MI355XVLMBackend:
                 devs = ["cpu"] * self.tp_size
             self._tp_group = TPServingGroup(self.tp_size, self._tp_spec(), devices=devs)
             self.tp = self._tp_group.state.tp_info()
-        if self.tp.enabled:
-            from ...runtime.engine import TPSync
-
-            sync = TPSync(self.tp.group, src=0)
         self._build()
+        if self.tp.enabled:
+            from ...runtime.engine import TPSync, tp_sync_capacity
+
+            sync = TPSync(self.tp.group, src=0,
+                          capacity=tp_sync_capacity(self.max_batch, self.model.llm.cfg.max_position))
         self.engine = LLMEngine(self.model.llm, self.kv, self._build_prefill, max_batch=self.max_batch, tp_sync=sync,
                                 follower_args=self._follower_args)
         self.load_time = time.time() - t0
@@ -356,12 +357,12 @@ class MI355XVLMBackend:
 
     def run_follower(self) -> None:
         """TP ranks > 0: build this rank's shard and replay the leader's steps until it stops."""
-        from ...runtime.engine import TPSync, follower_loop
+        from ...runtime.engine import TPSync, follower_loop, tp_sync_capacity
 
         self._build()
         self._initialized = True
-        follower_loop(self.model.llm, self.kv, self._build_prefill, TPSync(self.tp.group, src=0),
-                      max_batch=self.max_batch)
+        sync = TPSync(self.tp.group, src=0, capacity=tp_sync_capacity(self.max_batch, self.model.llm.cfg.max_position))
+        follower_loop(self.model.llm, self.kv, self._build_prefill, sync, max_batch=self.max_batch)
         self._initialized = False
 
     def close(self) -> None:

@@ -10,6 +10,7 @@
 #   gemm           tools/gemm_bench_tiles.py on the ViT-L/14 shapes ($GEMM_TILES, $GEMM_EPI)
 #   llm_tests      fp8 / LLM-op / VLM GPU tests only
 #   post_tests     post-processing / image kernels / OCR GPU tests only
+#   tp             TP=2 (two ranks sharing the GPU) tests + tools/tp_decode_bench.py (8B fp8)
 #   w8bench        tools/w8_decode_bench.py: HBM-cold decode GEMMs ($W8_M rows, default 1,16)
 #   vlm8b / vlm05  tools/vlm_bench.py Llama-3-8B fp8 / FastVLM-0.5B
 #   prof_vlm8b     rocprofv3 kernel stats of the 8B fp8 decode bench (batch 16; prof_vlm8b_b1: single stream)
@@ -55,6 +56,10 @@ for task in "$@"; do
       step post_tests 300 python -u -m pytest tests/test_postproc_gpu.py tests/test_kernels_gpu.py tests/test_ocr_gpu.py \
         -x -q --timeout 120 --timeout-method thread ;;
     vlm8b) step vlm8b 600 python tools/vlm_bench.py --preset llava-llama3-8b --fp8 ;;
+    tp)
+      step tp_tests 300 python -u -m pytest tests/test_tp_gpu.py tests/test_comm_gpu.py -x -q --timeout 200 \
+        --timeout-method thread
+      step tp2_bench 500 python -u tools/tp_decode_bench.py --preset llava-llama3-8b --tp 2 --fp8 --share-gpu ;;
     vlm05) step vlm05 400 python tools/vlm_bench.py --preset fastvlm-0.5b ;;
     prof_vlm8b)
       step prof_vlm8b 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_vlm8b -o run -- \
