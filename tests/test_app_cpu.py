@@ -154,14 +154,17 @@ def test_spa_assets_and_api_coverage(client):
         assert route in idx.text
     js = client.get("/app.js")
     assert js.status_code == 200 and "views[\"/setup/install\"]" in js.text
+    core = client.get("/lumen.js")
+    assert core.status_code == 200
     assert client.get("/app.css").status_code == 200
     if shutil.which("node"):
-        r = subprocess.run(["node", "--check", str(Path(STATIC_DIR) / "app.js")], capture_output=True, text=True)
-        assert r.returncode == 0, r.stderr
-    # every api("...") path used by the UI resolves to a registered route
+        for f in ("app.js", "lumen.js"):
+            r = subprocess.run(["node", "--check", str(Path(STATIC_DIR) / f)], capture_output=True, text=True)
+            assert r.returncode == 0, r.stderr
+    # every call("...") path of the UI's API client resolves to a registered route
     routes = list(client.get("/openapi.json").json()["paths"])
     pats = [re.compile("^" + re.sub(r"\{[^}]+\}", "[^/]+", p) + "$") for p in routes]
-    used = set(re.findall(r'api\(\s*[`"]([a-z][^`"?$]*)', js.text))
+    used = set(re.findall(r'call\(\s*[`"]([a-z][^`"?]*)', core.text))
     assert len(used) >= 15, used
     for u in used:
         full = "/api/v1/" + u.split("${")[0].rstrip("/")
