@@ -476,14 +476,10 @@ static hipError_t launch_res_nw(const AttnArgs& a, int B, int nkc, hipStream_t s
 
 template <int D>
 static hipError_t launch_res(const AttnArgs& a, int B, int nkc, hipStream_t stream) {
-  // LUMEN_ATTN_RES_WAVES forces 4 or 8 waves per workgroup; auto: 8 once there are >= 10 query
-  // blocks to share (ViT-L/14 S = 257: 0.416 -> 0.357 ms at b512, profiles/r2_attn_res_waves_v1.txt),
-  // 4 for short sequences (CLIP text S = 77 has 5 blocks: extra waves would idle)
-  static const int nw_env = [] {
-    const char* e = getenv("LUMEN_ATTN_RES_WAVES");
-    return e ? atoi(e) : 0;
-  }();
-  const int nw = nw_env == 4 || nw_env == 8 ? nw_env : ((a.Sq + 15) / 16 >= 10 ? 8 : 4);
+  // 8 waves per workgroup once there are >= 10 query blocks to share (ViT-L/14 S = 257:
+  // 0.416 -> 0.357 ms at b512, profiles/r2_attn_res_waves_v1.txt), 4 for short sequences
+  // (CLIP text S = 77 has 5 blocks: extra waves would idle)
+  const int nw = (a.Sq + 15) / 16 >= 10 ? 8 : 4;
   if constexpr (D >= 64) {
     if (nw == 8) return launch_res_nw<D, 8>(a, B, nkc, stream);
   }
@@ -494,26 +490,13 @@ hipError_t attn_fwd(const AttnArgs& a, int B, int D, hipStream_t stream) {
   // K/V-resident path when the whole K/V fits in 80 KiB and there are enough (batch, head) pairs
   const int nkc = (a.Sk + 63) / 64;
   const bool res_ok = (int64_t)B * a.H >= 1024 && (size_t)nkc * 2 * 64 * D * 2 <= 80 * 1024 && a.Sq <= 1024;
-  if (res_ok && getenv("LUMEN_ATTN_STREAM") == nullptr) {
+  if (res_ok) {
     if (D == 64) return launch_res<64>(a, B, nkc, stream);
     if (D == 128) return launch_res<128>(a, B, nkc, stream);
     if (D == 32) return launch_res<32>(a, B, nkc, stream);
   }
-  // LUMEN_ATTN_FWD_WAVES=2: 32-query blocks (twice the workgroups for few-(batch, head) prefills);
-  // default 4 (64-query blocks)
-  static const int nw_env = [] {
-    const char* e = getenv("LUMEN_ATTN_FWD_WAVES");
-    return e ? atoi(e) : 0;
-  }();
-  const int nw = nw_env == 2 ? 2 : 4;
-  if (nw == 2) {
-    dim3 grid((a.Sq + 31) / 32, a.H, B), block(128);
-    if (D == 64) hipLaunchKernelGGL((attn_fwd_kernel<64, 2>), grid, block, 0, stream, a);
-    else if (D == 128) hipLaunchKernelGGL((attn_fwd_kernel<128, 2>), grid, block, 0, stream, a);
-    else if (D == 32) hipLaunchKernelGGL((attn_fwd_kernel<32, 2>), grid, block, 0, stream, a);
-    else return hipErrorInvalidValue;
-    return hipGetLastError();
-  }
+  // streaming path: 64-query blocks, 4 waves (32-query / 2-wave blocks measured slower on the
+  // few-(batch, head) prefills they were meant for, r2)
   dim3 grid((a.Sq + 63) / 64, a.H, B), block(256);
   if (D == 64) hipLaunchKernelGGL((attn_fwd_kernel<64, 4>), grid, block, 0, stream, a);
   else if (D == 128) hipLaunchKernelGGL((attn_fwd_kernel<128, 4>), grid, block, 0, stream, a);

@@ -203,12 +203,8 @@ hipError_t conv2d_igemm(const ConvArgs& a, const GemmEpi& ep, int tile, hipStrea
   const int64_t M = (int64_t)a.N * a.Ho * a.Wo;
   if (tile >= 10) return conv2d_lds(a, ep, tile - 10, stream);
   // Cin % 64 == 0 layers (IResNet, SCRFD / DBNet trunks): the LDS-DMA pipeline
-  // (profiles/r2_conv_lds_v1.txt); LUMEN_CONV_LDS=0 keeps the register-staged kernels
-  static const bool lds_on = [] {
-    const char* e = getenv("LUMEN_CONV_LDS");
-    return e == nullptr || e[0] != '0';
-  }();
-  if (tile < 0 && lds_on && conv_lds_ok(a)) return conv2d_lds(a, ep, 0, stream);
+  // (profiles/r2_conv_lds_v1.txt); other shapes use the register-staged kernels
+  if (tile < 0 && conv_lds_ok(a)) return conv2d_lds(a, ep, 0, stream);
   if (tile < 0) {
     const int64_t t128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
     if (a.Cout >= 128 && t128 >= 256) tile = 0;
@@ -354,7 +350,7 @@ static hipError_t launch_dw_rb(const uint16_t* x, const uint16_t* w, const void*
 hipError_t conv2d_depthwise(const uint16_t* x, const uint16_t* w, const void* bias, int bias_f32, void* out, int N,
                             int H, int W, int C, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw,
                             int Ho, int Wo, int act, int out_f32, hipStream_t stream) {
-  if (dh == 1 && dw == 1 && (sw == 1 || sw == 2) && getenv("LUMEN_DW_NAIVE") == nullptr) {
+  if (dh == 1 && dw == 1 && (sw == 1 || sw == 2)) {
 #define LUMEN_DW_CASE(K)                                                                                       \
     if (KW == K) return sw == 1 ? launch_dw_rb<K, 1>(x, w, bias, bias_f32, out, N, H, W, C, KH, sh, ph, pw, Ho, Wo, act, \
                                                      out_f32, stream)                                          \

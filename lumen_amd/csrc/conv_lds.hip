@@ -4,7 +4,7 @@
 // v_mfma_f32_16x16x32_bf16.  For Cin % 64 == 0 one 64-wide K-step is 64 channels of ONE
 // filter tap, so every LDS row of the A stage is a single contiguous 128-byte run of an
 // NHWC input pixel -- the gather is pure address arithmetic on the DMA source (taps that
-// fall into the zero padding read a zeroed 128-byte page).  Replaces the register-staged
+// fall into the zero padding read past the end of the buffer descriptor: zeros).  Replaces the register-staged
 // 2-stage conv_igemm_kernel on the IResNet / SCRFD / DBNet layers with Cin >= 64
 // (r1: 55 us per call, 1.3 % of peak on face).
 //
@@ -18,8 +18,6 @@
 #include "gemm_epi.h"
 
 namespace lumen {
-
-__device__ __attribute__((aligned(256))) uint16_t g_conv_zero_page[128];   // 256 zero bytes
 
 template <int NSTAGE, int WN, int BN>
 __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi ep) {
@@ -40,45 +38,69 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
   const int tm = lin % tiles_m, tn = lin / tiles_m;
   const int m0 = tm * 128, n0 = tn * BN;
 
-  // A rows of this lane: output pixel -> image base + top-left input coordinate
-  const uint16_t* xb[PERA];
-  int hb[PERA], wb[PERA], ca[PERA];
+  // Operands through buffer descriptors, so the per-K-step source address is one 32-bit add:
+  //   A row (output pixel) -> byte offset of its top-left input tap + this lane's 16 channels,
+  //   plus a wave-uniform tap offset; a tap in the zero padding gets an offset past the end of
+  //   the buffer, which the range check turns into 16 zero bytes in LDS.
+  //   B row -> byte offset of this lane's 16 B in filter row n; the K step goes in soffset.
+  // Tap validity is a per-row bit mask built once (bit t: tap t inside the image), so the
+  // K loop does no division and no bounds arithmetic: r2 measured 5.6 VALU per MFMA on this
+  // kernel from exactly that per-step index math (profiles/r2_face_pmc_sq_v1.jsonl).
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, (short)0, (int)((int64_t)a.N * a.H * a.W * a.ldx * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, (int)((int64_t)N * K * 2), 0x00020000);
+  int rofs[PERA];
+  uint64_t tmask[PERA];
 #pragma unroll
   for (int i = 0; i < PERA; ++i) {
     const int r = (PERA * wid + i) * 8 + (lane >> 3);
-    ca[i] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;                 // channel offset of this lane's 16 B
+    const int ca = ((lane & 7) ^ ((r >> 1) & 7)) * 8;             // channel offset of this lane's 16 B
     const int m = min(m0 + r, M - 1);
     const int img = m / (a.Ho * a.Wo), rem = m % (a.Ho * a.Wo);
-    xb[i] = a.x + (int64_t)img * a.H * a.W * a.ldx;
-    hb[i] = (rem / a.Wo) * a.sh - a.ph;
-    wb[i] = (rem % a.Wo) * a.sw - a.pw;
+    const int hb = (rem / a.Wo) * a.sh - a.ph, wb = (rem % a.Wo) * a.sw - a.pw;
+    rofs[i] = (((img * a.H + hb) * a.W + wb) * a.ldx + ca) * 2;   // wraps for padding rows: never used then
+    uint64_t msk = 0;
+    for (int ky = 0, t = 0; ky < a.KH; ++ky)
+      for (int kx = 0; kx < a.KW; ++kx, ++t) {
+        const int ih = hb + ky * a.dh, iw = wb + kx * a.dw;
+        if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W) msk |= 1ull << t;
+      }
+    tmask[i] = msk;
   }
-  const uint16_t* wsrc[PERB];
+  int wofs[PERB];
 #pragma unroll
   for (int i = 0; i < PERB; ++i) {
     const int r = (PERB * wid + i) * 8 + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
-    wsrc[i] = a.w + (int64_t)min(n0 + r, N - 1) * K + c * 8;
+    wofs[i] = (min(n0 + r, N - 1) * K + c * 8) * 2;
   }
-  const int cblk = a.Cin / 64;
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  typedef const __attribute__((address_space(1))) void* g_ptr_t;
+  // wave-uniform walk over (tap, 64-channel block): advanced once per stage() call, in K order
+  int ky = 0, kx = 0, c0 = 0, tofs = 0;
+  uint64_t tbit = 1;
+  const int row_step = a.dh * a.W * a.ldx * 2, col_step = a.dw * a.ldx * 2;
   auto stage = [&](int s, int kt) {
-    const int tap = kt / cblk, c0 = (kt - tap * cblk) * 64;
-    const int ky = tap / a.KW, kx = tap - ky * a.KW;
     char* baseA = smem + s * STAGE + wid * PERA * 1024;
 #pragma unroll
     for (int i = 0; i < PERA; ++i) {
-      const int ih = hb[i] + ky * a.dh, iw = wb[i] + kx * a.dw;
-      const bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-      const uint16_t* src = ok ? xb[i] + ((int64_t)ih * a.W + iw) * a.ldx + c0 + ca[i] : g_conv_zero_page;
-      __builtin_amdgcn_global_load_lds((g_ptr_t)src, (lds_ptr_t)(baseA + i * 1024), 16, 0, 0);
+      const int off = (tmask[i] & tbit) ? rofs[i] + tofs : (int)0x80000000;
+      buf_load_lds16(xr, baseA + i * 1024, off, 0);
     }
     char* baseB = smem + s * STAGE + ASZ + wid * PERB * 1024;
-    const int64_t koff = (int64_t)kt * 64;
 #pragma unroll
     for (int i = 0; i < PERB; ++i)
-      __builtin_amdgcn_global_load_lds((g_ptr_t)(wsrc[i] + koff), (lds_ptr_t)(baseB + i * 1024), 16, 0, 0);
+      buf_load_lds16(wr, baseB + i * 1024, wofs[i], kt * 128);
+    c0 += 64;
+    tofs += 128;
+    if (c0 == a.Cin) {
+      c0 = 0;
+      tbit <<= 1;
+      if (++kx == a.KW) {
+        kx = 0;
+        ++ky;
+      }
+      tofs = ky * row_step + kx * col_step;
+    }
   };
 
   f32x4_t acc[4][NR];
@@ -174,8 +196,12 @@ static hipError_t launch_conv_lds(const ConvArgs& a, const GemmEpi& ep, hipStrea
 }
 
 bool conv_lds_ok(const ConvArgs& a) {
+  // 32-bit buffer offsets: input and filter below 2 GiB (the padding sentinel 0x80000000 lies
+  // past both); <= 64 filter taps (the per-row validity mask)
   return a.Cin % 64 == 0 && a.Cout % 16 == 0 && a.ldx % 8 == 0 && a.ldo % 8 == 0 &&
-         ((uintptr_t)a.x & 15) == 0 && ((uintptr_t)a.w & 15) == 0 && (int64_t)a.N * a.Ho * a.Wo < (1LL << 31);
+         ((uintptr_t)a.x & 15) == 0 && ((uintptr_t)a.w & 15) == 0 && (int64_t)a.N * a.Ho * a.Wo < (1LL << 31) &&
+         (int64_t)a.N * a.H * a.W * a.ldx * 2 < (1LL << 31) && (int64_t)a.Cout * a.KH * a.KW * a.Cin * 2 < (1LL << 31) &&
+         a.KH * a.KW <= 64;
 }
 
 // variant: 0 auto; 1 = 128x128 3 stages 8 waves, 2 = 128x128 2 stages 4 waves, 3 = 128x64 3 stages 4 waves,

@@ -960,8 +960,7 @@ static hipError_t launch_persist(const uint16_t* A, int64_t lda, const uint16_t*
   const int64_t extent = (int64_t)M * ldc * (ep.out_f32 ? 4 : 2);
   wt = wt && ep.out_group == 0 && extent < ((int64_t)1 << 31);
   const bool fast = M % 256 == 0 && N % 256 == 0 && ep.out_group == 0 && !ep.glu && !ep.table && !ep.prelu &&
-                    !ep.post_act && !ep.out_f32 && !(ep.bias && ep.bias_f32) && extent < ((int64_t)1 << 31) &&
-                    getenv("LUMEN_GEMM_NOFAST") == nullptr;
+                    !ep.post_act && !ep.out_f32 && !(ep.bias && ep.bias_f32) && extent < ((int64_t)1 << 31);
   const int fk = fast ? 1 + (ep.bias ? 1 : 0) + (ep.residual ? 2 : 0) : 0;
   if (wt) launch_persist_fk<true>(fk, A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
   else launch_persist_fk<false>(fk, A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
@@ -1007,7 +1006,7 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
     else if (t128 >= 144 && lds_ok) tile = 20005;
     // fewer 128x128 tiles (VLM vision tower at 577 tokens: 40-120): the same pipeline with K split
     // over gridDim.y + one reduce/epilogue pass (gemm_f8.hip f8_pick_splits) instead of 64x64 tiles
-    else if (lds_ok && M >= 128 && K >= 4096 && getenv("LUMEN_GEMM_NO_LDS128_SPLIT") == nullptr) tile = 20000;
+    else if (lds_ok && M >= 128 && K >= 4096) tile = 20000;
     else tile = 2;
     if (tile >= 20000) return gemm_lds128_bf16(A, lda, W, ldw, C, ldc, M, N, K, ep, tile - 20000, stream);
   }
@@ -1041,8 +1040,7 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
       char* C2 = (char*)C + (int64_t)M0 * ldc * (ep.out_f32 ? 4 : 2);
       // tail rows: split-K ping-pong + reduce/epilogue pass (r2: the 128x128 register-staged
       // tail took 9.5 % of the ViT-L/14 step for 0.4 % of its FLOPs)
-      if (getenv("LUMEN_GEMM_TAIL128") == nullptr &&
-          gemm_tail_splitk(A + (int64_t)M0 * lda, lda, W, ldw, C2, ldc, M - M0, N, K, e2, stream) == hipSuccess)
+      if (gemm_tail_splitk(A + (int64_t)M0 * lda, lda, W, ldw, C2, ldc, M - M0, N, K, e2, stream) == hipSuccess)
         return hipSuccess;
       (void)hipGetLastError();
       return launch_cfg<128, 128, 2, 2>(A + (int64_t)M0 * lda, lda, W, ldw, C2, ldc, M - M0, N, K, e2, stream);

@@ -127,6 +127,13 @@ __device__ __forceinline__ void st16(void* C, __amdgpu_buffer_rsrc_t rs, int64_t
   else *(u32x4_t*)((char*)C + byte_off) = v;
 }
 
+// 16-byte LDS-DMA through a buffer descriptor (buffer_load_dwordx4 ... offen lds): per-lane 32-bit
+// byte offset, wave-uniform soffset; an offset past num_records lands as zeros.  A non-template
+// wrapper: called directly from a kernel template the builtin suppresses the host-side stub.
+__device__ __forceinline__ void buf_load_lds16(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t c_rsrc(void* C) {
   return __builtin_amdgcn_make_buffer_rsrc(C, (short)0, -1, 0x00020000);
 }

@@ -268,19 +268,13 @@ static int f8_num_cus() {
   return cus;
 }
 
-// K splits for a 128x128-tile GEMM: LUMEN_F8_SPLIT forces S (1 = off); auto splits only grids
-// of at most half the CUs, to ~1-2 workgroups per CU, keeping >= 4 k tiles (128 B) per split
+// K splits for a 128x128-tile GEMM: only grids of at most half the CUs split, to ~1-2
+// workgroups per CU, keeping >= 4 k tiles (128 B) per split
 static int f8_pick_splits(int tiles, int nk, const GemmEpi& ep) {
-  static const int force = [] {
-    const char* e = getenv("LUMEN_F8_SPLIT");
-    return e ? atoi(e) : 0;
-  }();
   if (ep.out_group || ep.table || ep.split_koff || ep.prelu || ep.post_act) return 1;
   const int cus = f8_num_cus();
   int S = 1;
-  if (force > 0) {
-    S = force;
-  } else if (2 * tiles <= cus && nk >= 32) {
+  if (2 * tiles <= cus && nk >= 32) {
     // deep K only: the fp32 slab round trip costs more than the idle CUs on K <= 1024 shapes
     // (577 x 3072 x 1024: 14.2 -> 28.2 us split; 577 x 1024 x 4096: 35.8 -> 25.8 us;
     // 624 x 4096 x 14336 fp8: 61.9 -> 57.4 us at S = 2; profiles/r2_splitk_mid_v1.txt)
@@ -329,9 +323,7 @@ hipError_t gemm_lds128_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
     }
   }
   switch (variant) {
-    case 1: return launch_f8<4, 2, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, stream);
     case 2: return launch_f8<2, 2, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, stream);
-    case 4: return launch_f8<4, 4, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, stream);
     case 5: return launch_f8<2, 4, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, stream);
     default: return launch_f8<3, 4, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, stream);
   }
@@ -344,40 +336,17 @@ hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t
   // grids of more than one wave of workgroups (gate|up: 1120 tiles) run best at 2 stages x
   // 4 waves (64 KiB LDS -> 2 workgroups per CU overlap each other's barriers); grids that
   // fit in one wave (qkv / o / down: 160-240 tiles) at 3 stages x 8 waves (2 waves / SIMD).
-  // LUMEN_F8_VARIANT forces one (A/B): 1 = 4 st x 4 w, 2 = 2 st x 4 w, 3 = 3 st x 8 w,
-  // 4 = 4 st x 8 w, 5 = 2 st x 8 w.
-  static const int variant = [] {
-    const char* e = getenv("LUMEN_F8_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
+  // (128x64 tiles were faster in isolation but slower over the whole weight-streaming prefill,
+  // 9.87 vs 9.23-9.35 ms, profiles/r2_f8_bn64_v1.txt, and were removed.)
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
   const int S = f8_pick_splits(tiles, K / 128, ep);
-  // LUMEN_F8_BN=64: 128x64 tiles (twice the workgroups, two per CU) for grids whose 128x128 tiles
-  // leave CUs idle.  Opt-in: faster in isolation on the Llama-3-8B prefill shapes (o 23.9 -> 21.8,
-  // down 62.9 -> 58.3 us, weights L2/MALL-warm) but the full 624-token prefill, streaming 7.5 GB of
-  // weights, ran 9.23-9.35 ms with 128x128 vs 9.87-9.90 ms with it (profiles/r2_f8_bn64_v1.txt)
-  static const int bn_env = [] {
-    const char* e = getenv("LUMEN_F8_BN");
-    return e ? atoi(e) : 0;
-  }();
-  const bool bn64 = S == 1 && variant == 0 && N % 64 == 0 && bn_env == 64;
-  if (bn64) return launch_f8<3, 2, true, 64>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
-  int v = variant;
-  if (v == 0) v = tiles * S > f8_num_cus() ? 2 : 3;
+  const bool multi_wave = tiles * S > f8_num_cus();
   if (S > 1) {
-    switch (v) {
-      case 2: return launch_f8_split<2, 2, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
-      case 5: return launch_f8_split<2, 4, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
-      default: return launch_f8_split<3, 4, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
-    }
+    if (multi_wave) return launch_f8_split<2, 2, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
+    return launch_f8_split<3, 4, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
   }
-  switch (v) {
-    case 1: return launch_f8<4, 2>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
-    case 2: return launch_f8<2, 2>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
-    case 4: return launch_f8<4, 4>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
-    case 5: return launch_f8<2, 4>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
-    default: return launch_f8<3, 4>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
-  }
+  if (multi_wave) return launch_f8<2, 2>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+  return launch_f8<3, 4>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
 }
 
 // ============================================================================ quantisers

@@ -332,20 +332,15 @@ static void launch_pp_fk(const uint16_t* A, int64_t lda, const uint16_t* W, int6
 // stream of K-tiles ("units"): the LDS-DMA staging of units u + 1 / u + 2 runs across tile
 // boundaries, so the next tile's first operands land while an epilogue runs.
 //
-// Epilogue desynchronisation: with every CU on the same tile schedule, all 256 epilogues
-// store their 128 KiB C tiles in the same few microseconds (32 MiB per round: an HBM write
-// burst with every matrix core idle, ~9 us per tile at K = 1024).  Workgroup slot j (of 32
-// per XCD) therefore starts PHI_j = j * nk / 32 K-tiles into its first tile: it runs
-// K-tiles [PHI, nk) of tile 0, saves that partial accumulator to a private fp32 workspace
-// (fragment order: one coalesced 1 KiB store per register quad), runs tiles 1 .. R-1,
-// and finishes tile 0 with K-tiles [0, PHI) starting from the reloaded partial.  Every
-// workgroup still executes R * nk K-tiles (no imbalance, no inter-workgroup hand-off), but
-// the tile boundaries — and the C write bursts — are spread over the whole tile period.
+// (A phase-shifted variant -- each workgroup starting part-way into its first tile so the
+// 256 C-write bursts spread over the tile period -- measured slower on the ViT-L/14 shapes:
+// workgroups sharing a row panel drifted apart and lost the shared L2 panel reads,
+// profiles/r2_gemm_pps_phase_v1.txt.  It was removed.)
 //
 // The epilogue stages 16 x 32 fp32 pieces in its own 18 KiB LDS region beside the 128 KiB
-// pipeline.  Its VMEM ops (E per wave, static on the FAST path; 32 for a partial save) sit
-// between staging loads in the in-order vmcnt queue, so the two waits after an epilogue
-// count them in (a count may only under-state the ops issued after the awaited one).
+// pipeline.  Its VMEM ops (E per wave, static on the FAST path) sit between staging loads in
+// the in-order vmcnt queue, so the two waits after an epilogue count them in (a count may
+// only under-state the ops issued after the awaited one).
 // ============================================================================
 template <int N>
 __device__ __forceinline__ void vm_wait_i() {
@@ -355,13 +350,11 @@ __device__ __forceinline__ void vm_wait_i() {
 constexpr int PPS_STR = 36;                       // epilogue staging row stride (floats)
 constexpr int PPS_WAVE = 16 * PPS_STR * 4;        // bytes per wave
 constexpr int PPS_LDS = 2 * G_BUF + 8 * PPS_WAVE;
-constexpr int PPS_PART = 8 * 128 * 64 * 4;        // partial accumulator bytes per workgroup
 
 template <int FK, int PRIO>
 __global__ void __launch_bounds__(512)
 gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
-                void* __restrict__ C, int64_t ldc, int M, int N, int K, GemmEpi ep, int group_m,
-                float* __restrict__ part) {
+                void* __restrict__ C, int64_t ldc, int M, int N, int K, GemmEpi ep, int group_m) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -375,18 +368,6 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
   if (lin0 >= ntiles) return;
   const int nk = K / BK;
   const int R = (ntiles - lin0 + G - 1) / G;          // tiles of this workgroup
-  // phase offset of the first tile (0: plain tile order).  Keyed by the first tile's row panel:
-  // the workgroups that share an A panel (same row tile, other column tiles) keep the same
-  // schedule and keep reading it from one L2 together; 8 phase classes spread the C bursts.
-  int phi = 0;
-  if (part != nullptr && R >= 2 && nk >= 8) {
-    int tm0, tn0;
-    tile_coords(lin0, tiles_m, tiles_n, group_m, tm0, tn0);
-    phi = ((tm0 & 7) * nk) / 8;
-    if (phi < 3) phi = 0;
-    if (phi > nk - 3) phi = nk - 3;
-  }
-
 
   int off[4][2];   // per-lane element offsets inside a tile: h 0 = A0, 1 = B0, 2 = B1, 3 = A1
   int dst[2];
@@ -403,18 +384,16 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
   }
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   typedef const __attribute__((address_space(1))) void* g_ptr_t;
-  // Segments: phi > 0: s = 0 is tile 0 K-tiles [phi, nk), s = 1 .. R-1 tiles 1 .. R-1, s = R
-  // tile 0 K-tiles [0, phi); phi = 0: segment s = tile s.  Every segment has >= 2 K-tiles, so
-  // K-tile u + 2 is at most one segment ahead.
-  const int S = R + (phi > 0 ? 1 : 0);
+  // Segment s = tile s of this workgroup, K-tiles [kb, ke) = [0, nk).  Every segment has >= 2
+  // K-tiles, so K-tile u + 2 is at most one segment ahead.
+  const int S = R;
   auto seg_info = [&](int s_, int& m0, int& n0, int& kb, int& ke) {
-    const int r = (phi > 0 && s_ == S - 1) ? 0 : s_;
     int tm, tn;
-    tile_coords(lin0 + r * G, tiles_m, tiles_n, group_m, tm, tn);
+    tile_coords(lin0 + s_ * G, tiles_m, tiles_n, group_m, tm, tn);
     m0 = tm * 256;
     n0 = tn * 256;
-    kb = (phi > 0 && s_ == 0) ? phi : 0;
-    ke = (phi > 0 && s_ == S - 1) ? phi : nk;
+    kb = 0;
+    ke = nk;
   };
   auto issue = [&](const int h, int buf, int m0, int n0, int kt) {
     const int hoff = (h == 1 || h == 2 ? G_OP : 0) + (h >= 2 ? G_HALF : 0);
@@ -445,7 +424,6 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
   constexpr bool fast = FK > 0;
   constexpr bool FB = fast && ((FK - 1) & 1), FR = fast && ((FK - 1) & 2);
   constexpr int E = fast ? 16 + (FB ? 2 : 0) + (FR ? 16 : 0) : 0;   // VMEM ops of one epilogue (0: unknown)
-  constexpr int EP = 32;                                             // VMEM ops of a partial save
 
   int m0, n0, kb, ke;
   seg_info(0, m0, n0, kb, ke);
@@ -463,51 +441,22 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
   if constexpr (PRIO == 1) { if (wm == 1) __builtin_amdgcn_s_setprio(1); }
 
   float* es = (float*)(smem + 2 * G_BUF + wid * PPS_WAVE);
-  // this wave's partial-accumulator slot (32 KiB, fragment order) through a buffer descriptor:
-  // scalar base + lane offset, no per-fragment 64-bit addresses held in VGPRs
-  const __amdgpu_buffer_rsrc_t prs =
-      __builtin_amdgcn_make_buffer_rsrc(part ? part + ((int64_t)blockIdx.x * 8 + wid) * (128 * 64) : (float*)C, (short)0,
-                                        32768, 0x00020000);
   const __amdgpu_buffer_rsrc_t crs = c_rsrc(C);
   int T = 0;       // global K-tile counter (LDS buffer parity)
-  int after = 0;   // 0: none, 1: a C epilogue, 2: a partial save since the previous staging
+  int after = 0;   // 0: none, 1: a C epilogue since the previous staging
   for (int sg = 0; sg < S; ++sg) {
     const bool has_next = sg + 1 < S;
     int nm0 = m0, nn0 = n0, nkb = 0, nke = 0;
     if (has_next) seg_info(sg + 1, nm0, nn0, nkb, nke);
     f32x4_t acc[2][2][4][2];
-    if (phi > 0 && sg == S - 1) {
-      // final segment: tile 0 resumes from its saved partial accumulator
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int bq = 0; bq < 2; ++bq)
+      for (int bq = 0; bq < 2; ++bq)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
-              acc[a][bq][i][j] = __builtin_bit_cast(
-                  f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(prs, lane * 16, (((a * 2 + bq) * 4 + i) * 2 + j) * 1024, 0));
-      // consume the loads here: otherwise hipcc's wait for them lands after the merge, as a
-      // vmcnt(0) in front of every K-tile's first MFMA (draining the LDS-DMA pipeline)
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int bq = 0; bq < 2; ++bq)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[a][bq][i][j]));
-    } else {
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int bq = 0; bq < 2; ++bq)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) acc[a][bq][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    }
+          for (int j = 0; j < 2; ++j) acc[a][bq][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
 #define LUMEN_PPS_CLUSTER(QM, QN)                                                                               \
     Unroll<0, 4>::run([&](const int i) {                                                                      \
@@ -530,7 +479,7 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
       load_b(base, 1);
       if (e1) {
         issue(3, b ^ 1, c1 ? m0 : nm0, c1 ? n0 : nn0, k1);
-        if (af == 0) vm_wait_i<8>(); else if (af == 1) vm_wait_i<8 + E>(); else vm_wait_i<8 + EP>();
+        if (af == 0) vm_wait_i<8>(); else vm_wait_i<8 + E>();
       } else {
         vm_wait_i<0>();
       }
@@ -548,9 +497,9 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
         issue(0, b, am, an, k2);
         issue(1, b, am, an, k2);
         issue(2, b, am, an, k2);
-        if (af == 0) vm_wait_i<8>(); else if (af == 1) vm_wait_i<8 + E>(); else vm_wait_i<8 + EP>();
+        if (af == 0) vm_wait_i<8>(); else vm_wait_i<8 + E>();
       } else if (e1) {
-        if (af == 0) vm_wait_i<2>(); else if (af == 1) vm_wait_i<2 + E>(); else vm_wait_i<2 + EP>();
+        if (af == 0) vm_wait_i<2>(); else vm_wait_i<2 + E>();
       } else {
         vm_wait_i<0>();
       }
@@ -565,20 +514,7 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
     }
 #undef LUMEN_PPS_CLUSTER
 
-    if (phi > 0 && sg == 0) {
-      // end of the first (shifted) segment: park the partial accumulator
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int bq = 0; bq < 2; ++bq)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, acc[a][bq][i][j]), prs, lane * 16,
-                                                     (((a * 2 + bq) * 4 + i) * 2 + j) * 1024, 0);
-      after = 2;
-    } else {
+    {
       // ---- C epilogue: 16 passes (qm, i, qn) of 16 rows x 32 columns through this wave's
       // staging region; lane (rr, cq) stores 8 columns (16 B) of one row.
       const int rr = lane >> 2, cq = lane & 3;
@@ -650,16 +586,6 @@ static int pp_num_cus() {
   return n;
 }
 
-// per-device partial-accumulator workspace of the phase-shifted persistent kernel
-// (PPS_PART bytes per workgroup); allocated once, outside any stream capture
-static float* pps_workspace(int grid, hipStream_t stream) {
-  // measured slower than the plain tile order on the ViT-L/14 shapes (profiles/r2_gemm_pps_phase_v1.txt:
-  // workgroups of one row-panel class drift apart and lose the shared L2 panel reads): opt-in
-  const char* ph = getenv("LUMEN_GEMM_PHASE");
-  if (ph == nullptr || ph[0] == '0') return nullptr;
-  return (float*)stream_workspace((size_t)grid * PPS_PART, stream, WS_PP_PERSIST, 0);
-}
-
 template <int FK, int PRIO>
 static void launch_pps_t(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
                          int N, int K, const GemmEpi& ep, int group_m, hipStream_t stream) {
@@ -670,9 +596,8 @@ static void launch_pps_t(const uint16_t* A, int64_t lda, const uint16_t* W, int6
     hipFuncSetAttribute((const void*)gemm_pps_kernel<FK, PRIO>, hipFuncAttributeMaxDynamicSharedMemorySize, PPS_LDS);
     attr_set = true;
   }
-  float* part = pps_workspace(grid, stream);
   hipLaunchKernelGGL((gemm_pps_kernel<FK, PRIO>), dim3(grid), dim3(512), PPS_LDS, stream, A, lda, W, ldw, C, ldc, M,
-                     N, K, ep, group_m, part);
+                     N, K, ep, group_m);
 }
 
 hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,

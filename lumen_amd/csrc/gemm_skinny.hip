@@ -116,19 +116,11 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const uint16_t* __rest
 // K split per shape: when the 16-column N tiles already cover every CU (ntiles >= 256,
 // all four Llama-3-8B decode GEMMs) the split only adds slab traffic and is skipped;
 // narrower N (FastVLM-0.5B: 896 / 1152 wide) splits K until the grid reaches ~target
-// workgroups, each keeping >= 512 of K.  LUMEN_SKINNY_TARGET_WG overrides the target.
+// workgroups, each keeping >= 512 of K.
 int skinny_ksplit(int N, int K) {
   const int ntiles = (N + 15) / 16;
-  static const int target = [] {
-    const char* e = getenv("LUMEN_SKINNY_TARGET_WG");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 1024;
-  }();
-  static const int full = [] {   // tile count that already fills the chip without a split
-    const char* e = getenv("LUMEN_SKINNY_FULL_TILES");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 256;
-  }();
+  constexpr int target = 1024;
+  constexpr int full = 256;   // tile count that already fills the chip without a split
   if (ntiles >= full) return 1;
   int ks = (target + ntiles - 1) / ntiles;
   const int kmax = K / 512 > 1 ? K / 512 : 1;

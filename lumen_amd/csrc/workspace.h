@@ -17,7 +17,7 @@
 
 namespace lumen {
 
-enum WorkspaceTag : int { WS_F8_SPLIT = 0, WS_PP_TAIL = 1, WS_PP_PERSIST = 2 };
+enum WorkspaceTag : int { WS_F8_SPLIT = 0, WS_PP_TAIL = 1 };
 
 inline void* stream_workspace(size_t bytes, hipStream_t stream, int tag, size_t min_bytes) {
   struct Slot {

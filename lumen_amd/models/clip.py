@@ -195,15 +195,6 @@ class _Block(nn.Module):
             p.data.copy_(torch.randn(p.shape, generator=gen) * s)
 
 
-# Two ways to add the out-proj / fc2 residual: in the GEMM epilogue (default; the ping-pong
-# MFMA GEMM adds the prefetched residual rows before its single bf16 rounding), or as a plain
-# bias GEMM followed by an add + LayerNorm + residual-stream-write pass (LUMEN_BLAS_RESID=1).
-# Both run only hand-written kernels; ViT-L/14 b512 measured 5951 vs 5837 img/s
-# (profiles/r2_bench_resid_paths_v1.txt).
-_BLAS_RESID = os.environ.get("LUMEN_BLAS_RESID", "0") != "0"
-_BLAS_RESID_MIN_ROWS = int(os.environ.get("LUMEN_BLAS_RESID_MIN_ROWS", "8192"))
-
-
 def _block_steps(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float,
                  causal: bool = False, kv_len: Optional[torch.Tensor] = None, tile: int = -1,
                  res_tile: Optional[int] = None):
@@ -213,30 +204,20 @@ def _block_steps(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, 
     D = W // heads
     h = torch.empty_like(x)
     o = torch.empty_like(x)
-    blocks = list(blocks)
-    fuse = _BLAS_RESID and x.is_cuda and T >= _BLAS_RESID_MIN_ROWS
-    y = torch.empty_like(x) if fuse else None
+    # the out-proj / fc2 residual is added in the GEMM epilogue (the MFMA GEMM adds the prefetched
+    # residual rows before its single bf16 rounding); a separate add + LayerNorm pass measured
+    # 5837 vs 5951 img/s on ViT-L/14 b512 (profiles/r2_bench_resid_paths_v1.txt)
     for i, blk in enumerate(blocks):
-        if i == 0 or not fuse:
-            ops.layer_norm(x, blk.ln1_w, blk.ln1_b, eps, out=h)
+        ops.layer_norm(x, blk.ln1_w, blk.ln1_b, eps, out=h)
         qkv = ops.linear(h, blk.qkv_w, blk.qkv_b, tile=tile)
         q5 = qkv.view(B, S, 3, heads, D)
         ops.attention(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], causal=causal, kv_len=kv_len,
                       out=o.view(B, S, heads, D))
         del qkv, q5
-        if fuse:
-            ops.linear(o, blk.out_w, blk.out_b, out=y, tile=tile)
-            ops.layer_norm(y, blk.ln2_w, blk.ln2_b, eps, add=x, resid_out=x, out=h)
-        else:
-            ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x, tile=tile if res_tile is None else res_tile)
-            ops.layer_norm(x, blk.ln2_w, blk.ln2_b, eps, out=h)
+        ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x, tile=tile if res_tile is None else res_tile)
+        ops.layer_norm(x, blk.ln2_w, blk.ln2_b, eps, out=h)
         f = ops.linear(h, blk.fc1_w, blk.fc1_b, act=act, tile=tile)
-        if fuse and i + 1 < len(blocks):
-            nb = blocks[i + 1]
-            ops.linear(f, blk.fc2_w, blk.fc2_b, out=y, tile=tile)
-            ops.layer_norm(y, nb.ln1_w, nb.ln1_b, eps, add=x, resid_out=x, out=h)
-        else:
-            ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x, tile=tile if res_tile is None else res_tile)
+        ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x, tile=tile if res_tile is None else res_tile)
         del f
         yield i
 
@@ -258,11 +239,10 @@ def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, ep
 _VIT_MICRO = int(os.environ.get("LUMEN_VIT_MICRO", "2"))
 # ping-pong 256x256, 2 phases per K-tile + priority, group_m = 2, no tail split (1629 vs 1609 / 1689:
 # 6209-6222 vs 6203-6204 / 6129-6130 img/s, profiles/r2_vit_micro_streams_v1.txt)
-_VIT_MICRO_TILE = int(os.environ.get("LUMEN_VIT_MICRO_TILE", "1629"))
-_VIT_MICRO_RES_TILE = int(os.environ.get("LUMEN_VIT_MICRO_RES_TILE", "1629"))   # out-proj / fc2 (+ residual)
+_VIT_MICRO_TILE = 1629
 # text tower (B x 77 rows): micro-batched with the auto tile choice once it has this many rows per
 # half (b512 x 77: 50.4-50.6k -> 56.2-56.4k texts/s, profiles/r2_vit_micro_streams_v1.txt)
-_TEXT_MICRO_MIN_ROWS = int(os.environ.get("LUMEN_TEXT_MICRO_MIN_ROWS", "16384"))
+_TEXT_MICRO_MIN_ROWS = 16384
 _VIT_MICRO_MIN_ROWS = 65536          # per micro-batch: every GEMM stays >= 512 tiles of 256x256
 _MICRO_STREAMS: dict = {}
 
@@ -284,7 +264,7 @@ def run_blocks_micro(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: s
     if not x.is_cuda or n <= 1 or B < n or (B // n) * S < min_rows:
         return run_blocks(x, blocks, B, S, heads, act, eps, causal=causal)
     tile = _VIT_MICRO_TILE if tile is None else tile
-    res_tile = _VIT_MICRO_RES_TILE if res_tile is None else res_tile
+    res_tile = _VIT_MICRO_TILE if res_tile is None else res_tile
     cur = torch.cuda.current_stream(x.device)
     streams = _micro_streams(x.device, n)
     bounds = [B * i // n for i in range(n + 1)]

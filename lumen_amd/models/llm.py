@@ -20,7 +20,6 @@ the candidates for sampling).  Weights can be loaded from HF Qwen2/Llama state d
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import asdict, dataclass, field
 from typing import Optional, Sequence
 
@@ -37,12 +36,12 @@ from ..ops import llm as lops
 # decode on the skinny split-K kernels.  The r1 hipBLASLt prefill path is gone: FastVLM-0.5B
 # TTFT measured 12.25-12.72 ms without it vs 12.60-12.76 ms with it (same box, r2).
 # W8A8 prefill from this many tokens up (decode batches stay on the weight-only skinny kernels)
-_F8_MIN_ROWS = int(os.environ.get("LUMEN_LLM_F8_MIN_ROWS", "33"))
+_F8_MIN_ROWS = 33
 # GPU: RMSNorm gammas folded into qkv / gate|up / lm_head (LLM.fold_norms); decode norms become
 # rstd row scales in the skinny GEMM epilogues (ops.linear_dec)
-_FUSED_DECODE_NORM = os.environ.get("LUMEN_LLM_FUSED_NORM", "1") != "0"
+_FUSED_DECODE_NORM = True
 # decode: RoPE + current-token KV-cache write inside the paged attention kernel (no rope_kv launch)
-_FUSED_DECODE_ROPE = os.environ.get("LUMEN_LLM_FUSED_ROPE", "1") != "0"
+_FUSED_DECODE_ROPE = True
 
 
 @dataclass
@@ -468,34 +467,6 @@ class LLM(nn.Module):
 
         self._layers(x, pos, slots, kv, attn)
         return self.logits(x[T - 1:T])
-
-    @torch.no_grad()
-    def prefill_packed(self, x: torch.Tensor, kv, slots: torch.Tensor, lens: Sequence[int]) -> torch.Tensor:
-        """Several whole prompts in one pass: x [sum(lens), hidden] = the sequences' input rows
-        back to back (modified in place), k/v written to ``slots``; returns each sequence's
-        last-token logits [len(lens), V/tp].  The projections see all rows at once (the W8A8 /
-        MFMA GEMMs run at M = sum of the prompts instead of one prompt's few hundred rows);
-        attention runs per sequence (causal, its own rows only)."""
-        self._maybe_fold(x)
-        N = x.shape[0]
-        dev = x.device
-        assert sum(lens) == N and len(lens) >= 1
-        pos = torch.cat([torch.arange(T, dtype=torch.int32) for T in lens]).to(dev)
-        bounds = np.cumsum([0] + list(lens)).tolist()
-        D = self.cfg.head_dim
-
-        def attn(qkv, l, kc, vc):
-            q5 = qkv.view(1, N, l.H + 2 * l.Hkv, D)
-            o = torch.empty((N, l.H * D), device=dev, dtype=qkv.dtype)
-            o5 = o.view(1, N, l.H, D)
-            for s0, s1 in zip(bounds[:-1], bounds[1:]):
-                ops.attention(q5[:, s0:s1, :l.H], q5[:, s0:s1, l.H:l.H + l.Hkv], q5[:, s0:s1, l.H + l.Hkv:],
-                              causal=True, out=o5[:, s0:s1])
-            return o
-
-        self._layers(x, pos, slots, kv, attn)
-        last = torch.tensor([b - 1 for b in bounds[1:]], device=dev, dtype=torch.long)
-        return self.logits(x.index_select(0, last))
 
     @torch.no_grad()
     def decode(self, ids: torch.Tensor, pos: torch.Tensor, slots: torch.Tensor, kv, block_table: torch.Tensor,

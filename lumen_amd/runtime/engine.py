@@ -327,9 +327,6 @@ class LLMEngine:
         self._running: list[GenRequest] = []
         self._prefilling: list[GenRequest] = []
         self.prefill_chunk = max(16, int(prefill_chunk or os.environ.get("LUMEN_PREFILL_CHUNK", 2048)))
-        # packed multi-prompt prefill is opt-in (LUMEN_PREFILL_PACK=1): measured neutral for
-        # Llama-3-8B fp8 and slower for FastVLM-0.5B batch-16 (profiles/r2_prefill_pack_v1.txt)
-        self.pack_prefill = os.environ.get("LUMEN_PREFILL_PACK", "0") == "1"
         self._stop = threading.Event()
         self._ws: dict = {}
         self.device = llm.embed.device
@@ -461,55 +458,12 @@ class LLMEngine:
             self._running.append(r)
         return e - s
 
-    @torch.no_grad()
-    def _prefill_packed(self, reqs: list) -> None:
-        """Whole prompts of several fresh requests in one forward (LLM.prefill_packed): the
-        projections run at M = the summed prompt lengths.  Each request then samples its first
-        token and joins the running batch exactly as after a single-request prefill."""
-        xs = []
-        for r in reqs:
-            if r.t_admit is None:
-                r.t_admit = time.perf_counter()
-            x = self.build(r.prefill_args)
-            r.prompt_len = x.shape[0]
-            xs.append(x)
-        lens = [x.shape[0] for x in xs]
-        slots = np.concatenate([self.kv.slots(r.rid, 0, T) for r, T in zip(reqs, lens)])
-        logits = self.llm.prefill_packed(torch.cat(xs), self.kv, torch.from_numpy(slots).to(self.device), lens)
-        toks = self.sampler.pick(self.sampler.candidates(logits, Sampler.spec(reqs)), reqs)
-        now = time.perf_counter()
-        for r, T, tok in zip(reqs, lens, toks):
-            r.x, r.done, r.ctx, r.t_first = None, T, T, now
-            self.stats["prefill_chunks"] += 1
-            self.stats["prefills"] += 1
-            self._prefilling.remove(r)
-            if self._emit(r, tok):
-                self._finish(r)
-            else:
-                self._running.append(r)
-
     def _prefill_round(self) -> None:
         """One engine iteration's prefill work: up to ``prefill_chunk`` prompt tokens,
-        oldest request first.  Without TP, fresh requests whose whole prompts fit the budget
-        together can be prefilled in one packed pass (LUMEN_PREFILL_PACK=1)."""
+        oldest request first.  (Packing several prompts into one forward measured neutral for
+        Llama-3-8B fp8 and slower for FastVLM-0.5B batch 16, profiles/r2_prefill_pack_v1.txt,
+        so chunks run per request.)"""
         budget = self.prefill_chunk
-        if self.sync is None and self.pack_prefill:
-            group, tot = [], 0
-            for r in self._prefilling:
-                if r.x is None and tot + r.prompt_len <= budget:
-                    group.append(r)
-                    tot += r.prompt_len
-            if len(group) >= 2:
-                try:
-                    self._prefill_packed(group)
-                except Exception as e:  # noqa: BLE001 - surfaced to the callers
-                    log.exception("packed prefill failed")
-                    for r in group:
-                        if r in self._prefilling:
-                            self._prefilling.remove(r)
-                        r.x = None
-                    self._fail(group, e)
-                budget -= tot
         for r in list(self._prefilling):
             if budget <= 0:
                 break

@@ -2,9 +2,7 @@
 installer.py, utils/env_checker.py, utils/installation/*, utils/package_resolver.py):
 step planning, cancellation with cache cleanup, micromamba install from a mirror, venv
 environments, package resolution and the in-environment verifier."""
-import io
 import os
-import tarfile
 import threading
 import time
 from pathlib import Path
@@ -76,23 +74,18 @@ def test_clear_cache_refuses_unsafe(tmp_path):
     assert clear_cache_dir(tmp_path) is None and list(tmp_path.iterdir()) == []
 
 
-def _fake_micromamba_tar() -> bytes:
-    script = b"#!/bin/sh\necho 2.0.5\n"
-    buf = io.BytesIO()
-    with tarfile.open(fileobj=buf, mode="w:bz2") as tf:
-        ti = tarfile.TarInfo("bin/micromamba")
-        ti.size = len(script)
-        ti.mode = 0o755
-        tf.addfile(ti, io.BytesIO(script))
-    return buf.getvalue()
-
-
 def test_micromamba_install_from_mirror(tmp_path, monkeypatch):
+    """The release asset is the bare executable; the installer tries mirrors in order and only
+    installs a download whose SHA-256 matches the ``.sha256`` sidecar next to it."""
+    import hashlib
+
     monkeypatch.delenv("MAMBA_EXE", raising=False)
     monkeypatch.setenv("PATH", "/usr/bin:/bin")
-    arch = tmp_path / "mm.tar.bz2"
-    arch.write_bytes(_fake_micromamba_tar())
-    inst = MicromambaInstaller(tmp_path / "cache", mirrors=("file:///nonexistent/{plat}", f"file://{arch}"))
+    exe = tmp_path / "micromamba-linux-64"
+    exe.write_bytes(b"#!/bin/sh\necho 2.0.5\n")
+    (tmp_path / "micromamba-linux-64.sha256").write_text(
+        f"{hashlib.sha256(exe.read_bytes()).hexdigest()}  micromamba-linux-64\n")
+    inst = MicromambaInstaller(tmp_path / "cache", mirrors=("file:///nonexistent/{plat}", f"file://{exe}"))
     assert inst.check().status == MicromambaStatus.NOT_INSTALLED
     logs = []
     r = inst.install(logs.append)

@@ -237,32 +237,3 @@ def test_chunked_prefill_matches_single_shot():
         finally:
             eng.close()
     assert outs[64] == outs[4096]
-
-
-@pytest.mark.parametrize("kind", ["qwen2", "llama"])
-def test_prefill_packed_matches_single(kind):
-    """Several prompts in one packed prefill == each prompt prefilled alone: last-token logits
-    and the K/V written to each sequence's cache slots."""
-    cfg = _cfgs()[kind]
-    m = LLM(cfg, dtype=torch.float32, device="cpu")
-    m.random_init(3)
-    g = torch.Generator().manual_seed(2)
-    lens = [37, 70, 5]
-    prompts = [torch.randint(0, cfg.vocab_size, (T,), generator=g) for T in lens]
-    kv1 = PagedKVCache(cfg.num_layers, m.Hkv, cfg.head_dim, num_blocks=16, dtype=torch.float32)
-    kv2 = PagedKVCache(cfg.num_layers, m.Hkv, cfg.head_dim, num_blocks=16, dtype=torch.float32)
-    ref, slots_all = [], []
-    for i, (p, T) in enumerate(zip(prompts, lens)):
-        for kv in (kv1, kv2):
-            kv.blocks.reserve(i + 1, T + 4)
-        sl = kv1.slots(i + 1, 0, T)
-        slots_all.append(sl)
-        ref.append(m.prefill(m.embed_tokens(p), kv1, torch.from_numpy(sl))[0])
-    x = torch.cat([m.embed_tokens(p) for p in prompts])
-    got = m.prefill_packed(x, kv2, torch.from_numpy(np.concatenate(slots_all)), lens)
-    assert got.shape[0] == len(lens)
-    for i in range(len(lens)):
-        assert torch.allclose(got[i], ref[i], atol=1e-4), (i, (got[i] - ref[i]).abs().max())
-    for layer in range(cfg.num_layers):
-        assert torch.allclose(kv1.k[layer], kv2.k[layer], atol=1e-5)
-        assert torch.allclose(kv1.v[layer], kv2.v[layer], atol=1e-5)

@@ -192,33 +192,6 @@ def test_engine_fp8_kv_cache_serves():
     assert _cos(logits[0], logits[1]) > 0.99
 
 
-@pytest.mark.parametrize("fp8", [False, True])
-def test_prefill_packed_gpu_matches_single(fp8):
-    """Packed multi-prompt prefill on the HIP kernels (W8A8 / MFMA GEMMs at the summed M,
-    per-sequence attention) vs one prefill per prompt: logits and cached K."""
-    cfg = LLM_PRESETS["qwen2-0.5b"]
-    m = LLM(cfg, device="cuda")
-    m.random_init(8)
-    if fp8:
-        m.quantize_fp8()
-    g = np.random.default_rng(3)
-    lens = [300, 129, 77]
-    prompts = [torch.tensor(g.integers(0, 150000, T), device="cuda") for T in lens]
-    kvs = [PagedKVCache(cfg.num_layers, m.Hkv, cfg.head_dim, num_blocks=32, device="cuda") for _ in range(2)]
-    ref, slots = [], []
-    for i, (p, T) in enumerate(zip(prompts, lens)):
-        for kv in kvs:
-            kv.blocks.reserve(i + 1, T + 4)
-        sl = kvs[0].slots(i + 1, 0, T)
-        slots.append(sl)
-        ref.append(m.prefill(m.embed_tokens(p), kvs[0], torch.from_numpy(sl).cuda())[0].float().cpu())
-    x = torch.cat([m.embed_tokens(p) for p in prompts])
-    got = m.prefill_packed(x, kvs[1], torch.from_numpy(np.concatenate(slots)).cuda(), lens).float().cpu()
-    for i in range(len(lens)):
-        assert _cos(got[i], ref[i]) > 0.999
-    assert _cos(kvs[0].k[3].float().cpu(), kvs[1].k[3].float().cpu()) > 0.999
-
-
 def test_vlm_backend_fp8_shard_cache(tmp_path, monkeypatch):
     """precision fp8 on the GPU: the first build writes this rank's quantised shard
     (.lumen_shards/tp1_r0_fp8-fp8.safetensors: compute dtype + configured precision), the second

@@ -9,6 +9,7 @@
 #   prof_bench     rocprofv3 kernel stats of the headline bench (3 steps)
 #   gemm           tools/gemm_bench_tiles.py on the ViT-L/14 shapes ($GEMM_TILES, $GEMM_EPI)
 #   llm_tests      fp8 / LLM-op / VLM GPU tests only
+#   cnn_tests      conv / face / OCR / FastViT GPU tests only
 #   post_tests     post-processing / image kernels / OCR GPU tests only
 #   tp             TP=2 (two ranks sharing the GPU) tests + tools/tp_decode_bench.py (8B fp8)
 #   w8bench        tools/w8_decode_bench.py: HBM-cold decode GEMMs ($W8_M rows, default 1,16)
@@ -52,6 +53,9 @@ for task in "$@"; do
       step llm_tests 400 python -u -m pytest tests/test_fp8_gpu.py tests/test_llm_ops_gpu.py tests/test_vlm_gpu.py \
         -x -q --timeout 120 --timeout-method thread ;;
     w8bench) step w8bench 300 python -u tools/w8_decode_bench.py --m "${W8_M:-1,16}" ;;
+    cnn_tests)
+      step cnn_tests 400 python -u -m pytest tests/test_cnn_gpu.py tests/test_face_gpu.py tests/test_face_onnx_gpu.py \
+        tests/test_ocr_gpu.py tests/test_fastvit_gpu.py -x -q --timeout 120 --timeout-method thread ;;
     post_tests)
       step post_tests 300 python -u -m pytest tests/test_postproc_gpu.py tests/test_kernels_gpu.py tests/test_ocr_gpu.py \
         -x -q --timeout 120 --timeout-method thread ;;

@@ -1,6 +1,6 @@
 """Mid-size bf16 GEMMs (LLaVA vision tower: ViT-L/14-336 at 577 tokens) through ops.linear with
-the auto tile choice.  Run once with LUMEN_GEMM_NO_LDS128_SPLIT=1 (64x64 register-staged tiles
-for < 144 128x128 tiles) and once without (128x128 LDS-DMA pipeline + K split) to compare.
+the auto tile choice (128x128 LDS-DMA pipeline, K split for the small grids), next to the same
+product through torch (hipBLASLt, bias/activation/residual as separate ops) as the library baseline.
 
     python tools/mid_gemm_bench.py [--M 577]
 """
@@ -28,14 +28,9 @@ def main():
     load_hip(required=True)
     dev = "cuda"
     tot = 0.0
-    res = {"M": a.M, "split": os.environ.get("LUMEN_GEMM_NO_LDS128_SPLIT") is None}
-    for name, N, K, act, resid in SHAPES:
-        x = torch.randn(a.M, K, device=dev).bfloat16()
-        w = (torch.randn(N, K, device=dev) * K ** -0.5).bfloat16()
-        b = torch.randn(N, device=dev).bfloat16()
-        r = torch.randn(a.M, N, device=dev).bfloat16() if resid else None
-        out = torch.empty(a.M, N, device=dev, dtype=torch.bfloat16)
-        f = lambda: ops.linear(x, w, b, act=act, residual=r, out=out)  # noqa: E731
+    res = {"M": a.M}
+
+    def med_us(f):
         f()
         torch.cuda.synchronize()
         ts = []
@@ -47,7 +42,24 @@ def main():
             e.record()
             e.synchronize()
             ts.append(s.elapsed_time(e) / a.iters * 1e3)
-        us = statistics.median(ts)
+        return statistics.median(ts)
+
+    for name, N, K, act, resid in SHAPES:
+        x = torch.randn(a.M, K, device=dev).bfloat16()
+        w = (torch.randn(N, K, device=dev) * K ** -0.5).bfloat16()
+        b = torch.randn(N, device=dev).bfloat16()
+        r = torch.randn(a.M, N, device=dev).bfloat16() if resid else None
+        out = torch.empty(a.M, N, device=dev, dtype=torch.bfloat16)
+        f = lambda: ops.linear(x, w, b, act=act, residual=r, out=out)  # noqa: E731
+
+        def lib():
+            y = torch.nn.functional.linear(x, w, b)
+            if act:
+                y = y * torch.sigmoid(1.702 * y)
+            return y + r if resid else y
+
+        us = med_us(f)
+        res[f"{name}_torch_us"] = round(med_us(lib), 2)
         tot += us
         res[f"{name}_us"] = round(us, 2)
         res[f"{name}_tf"] = round(2 * a.M * N * K / us / 1e6, 1)

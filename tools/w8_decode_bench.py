@@ -33,7 +33,7 @@ def main():
     args = ap.parse_args()
     load_hip(required=True)
     dev = torch.device("cuda")
-    out = {"variant": os.environ.get("LUMEN_W8_DEC", "default")}
+    out = {}
     for name in args.shapes.split(","):
         N, K, kind = SHAPES[name]
         copies = max(2, (1 << 30) // (N * K))
