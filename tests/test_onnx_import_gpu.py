@@ -26,6 +26,7 @@ def test_clip_onnx_pack_gpu_matches_safetensors(tmp_path):
         b.initialize()
         try:
             assert b.device.type == "cuda"
+            b.model.center_crop = False   # same preprocessor on both runtimes (torch's crop is tested apart)
             return b.image_batch_to_vectors(imgs), b.text_batch_to_vectors(["a cat", "two dogs", "x"])
         finally:
             b.close()

@@ -37,7 +37,7 @@ step() {   # step NAME SECONDS CMD...  (stdout+stderr -> gpurun_out/NAME.log)
 
 for task in "$@"; do
   case $task in
-    tests) step tests 1500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    tests) step tests 900 python -u -m pytest tests -m gpu --maxfail=15 -q --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 400 python bench.py ;;
     prof_bench)
