@@ -961,7 +961,7 @@ static hipError_t launch_persist(const uint16_t* A, int64_t lda, const uint16_t*
   wt = wt && ep.out_group == 0 && extent < ((int64_t)1 << 31);
   const bool fast = M % 256 == 0 && N % 256 == 0 && ep.out_group == 0 && !ep.glu && !ep.table && !ep.prelu &&
                     !ep.post_act && !ep.out_f32 && !(ep.bias && ep.bias_f32) && extent < ((int64_t)1 << 31);
-  const int fk = fast ? 1 + (ep.bias ? 1 : 0) + (ep.residual ? 2 : 0) : 0;
+  const int fk = fast && !ep.row_aff ? 1 + (ep.bias ? 1 : 0) + (ep.residual ? 2 : 0) : 0;
   if (wt) launch_persist_fk<true>(fk, A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
   else launch_persist_fk<false>(fk, A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, grid, lds, stream);
   return hipGetLastError();

@@ -39,6 +39,14 @@ struct GemmEpi {
   const float* ssq_in;
   float* ssq_out;
   int ssq_tiles;
+  // ---- LayerNorm folded into the projection (pre-LN transformer blocks, ops.linear_lnf):
+  //   LN(x) . W^T + b = rstd * (x . W'^T) - rstd * mean * colsum(W') + (b + W . beta),
+  //   W' = W * gamma (prepared once on the host), so the GEMM runs on the raw residual
+  //   stream and no normalised copy of x is written.  row_aff [M][2] = (rstd, -mean * rstd)
+  //   per A row (ln_row_stats), col_aff [2][N] fp32 = (colsum(W'), b + W . beta).  Applied
+  //   first, in place of alpha and bias (the host passes neither).
+  const float* row_aff;
+  const float* col_aff;
 };
 
 // Launch plan of an fp8-weight decode GEMM (gemm_w8.hip): column tiles per wave, K splits and
@@ -157,6 +165,12 @@ __device__ __forceinline__ void epi_store16_t(float* v, int m, int n, int M, int
                                               int64_t ldc, const GemmEpi& ep, __amdgpu_buffer_rsrc_t rs) {
   if (m >= M || n >= N) return;
   const bool full = (n + 16 <= N);
+  if (ep.row_aff) {
+    const float rs = ep.row_aff[2 * (int64_t)m], ro = ep.row_aff[2 * (int64_t)m + 1];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      v[q] = (full || n + q < N) ? v[q] * rs + ro * ep.col_aff[n + q] + ep.col_aff[N + n + q] : 0.f;
+  }
 #pragma unroll
   for (int q = 0; q < 16; ++q) v[q] *= ep.alpha;
   if (ep.bias) {
@@ -254,6 +268,12 @@ __device__ __forceinline__ void epi_store8_t(float* v, int m, int n, int M, int 
                                              const GemmEpi& ep, __amdgpu_buffer_rsrc_t rs) {
   if (m >= M || n >= N) return;
   const bool full = (n + 8 <= N);
+  if (ep.row_aff) {
+    const float rs = ep.row_aff[2 * (int64_t)m], ro = ep.row_aff[2 * (int64_t)m + 1];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      v[q] = (full || n + q < N) ? v[q] * rs + ro * ep.col_aff[n + q] + ep.col_aff[N + n + q] : 0.f;
+  }
 #pragma unroll
   for (int q = 0; q < 8; ++q) v[q] *= ep.alpha;
   if (ep.bias) {
@@ -352,6 +372,19 @@ __device__ __forceinline__ void epi_store16_fast(float* v, int64_t m, int n, voi
   }
   st16<WT>(C, rs, (m * ldc + n) * 2, pack8(v));          // bf16 output only (host-checked)
   st16<WT>(C, rs, (m * ldc + n + 8) * 2, pack8(v + 8));
+}
+
+// LN-folded fast path (FK = 5 of the ping-pong kernels): v[q] = v[q] * rs + ro * cs[q] + cb[q], then the
+// activation, bf16 store of n_cols (8 or 16) columns.  cs / cb: the lane's columns of col_aff, prefetched.
+template <bool WT, int NC>
+__device__ __forceinline__ void epi_store_lnf(float* v, int64_t m, int n, void* __restrict__ C, int64_t ldc,
+                                              const GemmEpi& ep, float rs, float ro, const float* cs, const float* cb,
+                                              __amdgpu_buffer_rsrc_t r) {
+#pragma unroll
+  for (int q = 0; q < NC; ++q) v[q] = v[q] * rs + (ro * cs[q] + cb[q]);
+  if (ep.act) apply_act_n<NC>(v, ep.act);
+#pragma unroll
+  for (int h = 0; h < NC / 8; ++h) st16<WT>(C, r, (m * ldc + n + 8 * h) * 2, pack8(v + 8 * h));
 }
 
 __device__ __forceinline__ void epi_store16(float* v, int m, int n, int M, int N, void* __restrict__ C, int64_t ldc,

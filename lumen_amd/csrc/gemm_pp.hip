@@ -245,11 +245,31 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   const __amdgpu_buffer_rsrc_t crs = c_rsrc(C);
   const int rr = lane >> 2, cq = lane & 3;
   const int ncol = n0 + (cq >> 1) * 128 + wn * 32 + (cq & 1) * 16;
-  constexpr bool fast = FK > 0;
+  constexpr bool FL = FK == 5;   // LN-folded row / column affine (GemmEpi::row_aff), no residual
+  constexpr bool fast = FK > 0 && !FL;
   constexpr bool FB = fast && ((FK - 1) & 1), FR = fast && ((FK - 1) & 2);
   constexpr int RD = LUMEN_GEMM_RES_PREFETCH;
   u32x4_t bz0 = {0u, 0u, 0u, 0u}, bz1 = {0u, 0u, 0u, 0u};
   u32x4_t rz[RD][2];
+  float lcs[FL ? 16 : 1], lcb[FL ? 16 : 1], lrs[FL ? 8 : 1], lro[FL ? 8 : 1];
+  if constexpr (FL) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4_t a = *(const f32x4_t*)(ep.col_aff + ncol + 4 * q);
+      const f32x4_t b = *(const f32x4_t*)(ep.col_aff + N + ncol + 4 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        lcs[4 * q + e] = a[e];
+        lcb[4 * q + e] = b[e];
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int64_t m = m0 + (s >> 2) * 128 + wm * 64 + (s & 3) * 16 + rr;
+      lrs[s] = ep.row_aff[2 * m];
+      lro[s] = ep.row_aff[2 * m + 1];
+    }
+  }
   auto res_ptr = [&](int s) {
     return ep.residual + (int64_t)(m0 + (s >> 2) * 128 + wm * 64 + (s & 3) * 16 + rr) * ep.ldr + ncol;
   };
@@ -281,7 +301,9 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int m = m0 + qm * 128 + wm * 64 + i * 16 + rr;
-    if constexpr (fast) {
+    if constexpr (FL) {
+      epi_store_lnf<WT, 16>(v, m, ncol, C, ldc, ep, lrs[s], lro[s], lcs, lcb, crs);
+    } else if constexpr (fast) {
       const u32x4_t r0 = rz[s % RD][0], r1 = rz[s % RD][1];
       if constexpr (FR) {
         if (s + RD < 8) {
@@ -421,9 +443,12 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
         fb[qn][j][s] = *(const bf16x8_t*)(base + G_OP + qn * G_HALF + swz(wn * 32 + j * 16 + frow, s * 4 + fq));
   };
 
-  constexpr bool fast = FK > 0;
+  constexpr bool FL = FK == 5;   // LN-folded row / column affine, no residual
+  constexpr bool fast = FK > 0 && !FL;
   constexpr bool FB = fast && ((FK - 1) & 1), FR = fast && ((FK - 1) & 2);
-  constexpr int E = fast ? 16 + (FB ? 2 : 0) + (FR ? 16 : 0) : 0;   // VMEM ops of one epilogue (0: unknown)
+  // VMEM ops of one epilogue (0: unknown): 16 stores (+ bias / residual loads; LN-folded: 8 column
+  // vectors + 16 row scalars)
+  constexpr int E = FL ? 16 + 8 + 16 : fast ? 16 + (FB ? 2 : 0) + (FR ? 16 : 0) : 0;
 
   int m0, n0, kb, ke;
   seg_info(0, m0, n0, kb, ke);
@@ -531,6 +556,27 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
 #pragma unroll
         for (int p = 0; p < RD; ++p) rz[p] = *(const u32x4_t*)(ep.residual + (int64_t)row_of(p) * ep.ldr + col_of(p & 1));
       }
+      float lcs[FL ? 16 : 1], lcb[FL ? 16 : 1], lrs[FL ? 8 : 1], lro[FL ? 8 : 1];
+      if constexpr (FL) {
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const f32x4_t a = *(const f32x4_t*)(ep.col_aff + col_of(qn) + 4 * h);
+            const f32x4_t b = *(const f32x4_t*)(ep.col_aff + N + col_of(qn) + 4 * h);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              lcs[qn * 8 + 4 * h + e] = a[e];
+              lcb[qn * 8 + 4 * h + e] = b[e];
+            }
+          }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int64_t m = row_of(2 * r);
+          lrs[r] = ep.row_aff[2 * m];
+          lro[r] = ep.row_aff[2 * m + 1];
+        }
+      }
       Unroll<0, 16>::run([&](const int p) __attribute__((always_inline)) {
         const int qm = p >> 3, i = (p >> 1) & 3, qn = p & 1;
 #pragma unroll
@@ -547,7 +593,9 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const int m = row_of(p), n = col_of(qn);
-        if constexpr (fast) {
+        if constexpr (FL) {
+          epi_store_lnf<false, 8>(v, m, n, C, ldc, ep, lrs[p >> 1], lro[p >> 1], lcs + qn * 8, lcb + qn * 8, crs);
+        } else if constexpr (fast) {
           float f[8];
           unpack8(bq[qn], f);
 #pragma unroll
@@ -610,7 +658,8 @@ hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ld
       const int64_t extent = (int64_t)M * ldc * 2;
       const bool fast = !ep.table && !ep.prelu && !ep.post_act && !(ep.bias && ep.bias_f32) &&
                         extent < ((int64_t)1 << 31);
-      const int fk = fast ? 1 + (ep.bias ? 1 : 0) + (ep.residual ? 2 : 0) : 0;
+      const bool lnf = ep.row_aff && !ep.bias && !ep.residual && ep.alpha == 1.f && fast;
+      const int fk = lnf ? 5 : fast && !ep.row_aff ? 1 + (ep.bias ? 1 : 0) + (ep.residual ? 2 : 0) : 0;
       const bool prio1 = (variant & 2) != 0;
 #define LUMEN_PPS_CASE(FKV)                                                                                     \
       case FKV:                                                                                                 \
@@ -622,6 +671,7 @@ hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ld
         LUMEN_PPS_CASE(2)
         LUMEN_PPS_CASE(3)
         LUMEN_PPS_CASE(4)
+        LUMEN_PPS_CASE(5)
         default:
         LUMEN_PPS_CASE(0)
       }
@@ -634,13 +684,15 @@ hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ld
   const bool wt = false;
   const bool fast = M % 256 == 0 && N % 256 == 0 && ep.out_group == 0 && !ep.glu && !ep.table && !ep.prelu &&
                     !ep.post_act && !ep.out_f32 && !(ep.bias && ep.bias_f32) && extent < ((int64_t)1 << 31);
-  const int fk = fast ? 1 + (ep.bias ? 1 : 0) + (ep.residual ? 2 : 0) : 0;
+  const bool lnf = ep.row_aff && !ep.bias && !ep.residual && ep.alpha == 1.f && fast;
+  const int fk = lnf ? 5 : fast && !ep.row_aff ? 1 + (ep.bias ? 1 : 0) + (ep.residual ? 2 : 0) : 0;
   const bool prio1 = (variant & 2) != 0, two = (variant & 4) != 0;
   switch (fk) {
     case 1: launch_pp_fk<1>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, stream); break;
     case 2: launch_pp_fk<2>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, stream); break;
     case 3: launch_pp_fk<3>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, stream); break;
     case 4: launch_pp_fk<4>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, stream); break;
+    case 5: launch_pp_fk<5>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, stream); break;
     default: launch_pp_fk<0>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, stream); break;
   }
   return hipGetLastError();

@@ -219,6 +219,59 @@ hipError_t norm_rows(const uint16_t* x, int64_t x_stride, const int64_t* row_idx
 }
 
 // Row L2 normalisation of fp32 rows in place (embedding epilogue).
+// LayerNorm statistics only, for a projection with the norm folded in (GemmEpi::row_aff):
+// out[row] = (rstd, -mean * rstd).  Same fp32 two-pass arithmetic as norm_rows_kernel mode 0, but
+// 8 bytes per row are written instead of the normalised row.  One wave per row, D <= 64 * 8 * CPL.
+template <int CPL>
+__global__ void __launch_bounds__(256)
+ln_row_stats_kernel(const uint16_t* __restrict__ x, int64_t x_stride, float* __restrict__ out, int rows, int D,
+                    float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const uint16_t* xr = x + (int64_t)row * x_stride;
+  const int nch = D >> 3;
+  float v[CPL][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      unpack8(*(const u32x4_t*)(xr + ch * 8), v[c]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[c][i] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[c][i];
+  }
+  const float mean = wave_sum(s) / (float)D;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    if (lane + c * 64 < nch) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[c][i] - mean;
+        ss += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / (float)D + eps);
+  if (lane == 0) *(float2*)(out + 2 * (int64_t)row) = make_float2(rstd, -mean * rstd);
+}
+
+hipError_t ln_row_stats(const uint16_t* x, int64_t x_stride, float* out, int rows, int D, float eps,
+                        hipStream_t stream) {
+  if (D % 8 != 0 || D > 64 * 8 * 8 || rows <= 0) return hipErrorInvalidValue;
+  const dim3 grid((rows + 3) / 4);
+  if (D <= 512) hipLaunchKernelGGL(ln_row_stats_kernel<1>, grid, dim3(256), 0, stream, x, x_stride, out, rows, D, eps);
+  else if (D <= 1024) hipLaunchKernelGGL(ln_row_stats_kernel<2>, grid, dim3(256), 0, stream, x, x_stride, out, rows, D, eps);
+  else if (D <= 2048) hipLaunchKernelGGL(ln_row_stats_kernel<4>, grid, dim3(256), 0, stream, x, x_stride, out, rows, D, eps);
+  else hipLaunchKernelGGL(ln_row_stats_kernel<8>, grid, dim3(256), 0, stream, x, x_stride, out, rows, D, eps);
+  return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(256) l2norm_f32_kernel(float* __restrict__ x, int rows, int D, float eps) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);

@@ -40,6 +40,8 @@ hipError_t norm_rows(const uint16_t* x, int64_t x_stride, const int64_t* row_idx
                      const uint16_t* b, void* out, int64_t out_stride, int out_f32, int rows, int D,
                      float eps, int mode, hipStream_t stream);
 hipError_t l2norm_f32(float* x, int rows, int D, float eps, hipStream_t stream);
+hipError_t ln_row_stats(const uint16_t* x, int64_t x_stride, float* out, int rows, int D, float eps,
+                        hipStream_t stream);
 hipError_t cls_fill(uint16_t* x, int64_t seq_stride, const uint16_t* cls, const uint16_t* pos, int B, int D,
                     hipStream_t stream);
 hipError_t embed_gather(const int64_t* ids, const uint16_t* table, const uint16_t* pos, int S, uint16_t* out,
@@ -174,6 +176,40 @@ void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tens
   }
   LUMEN_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
                                    (int)M, (int)N, (int)K, ep, (int)tile, cur_stream()));
+}
+
+// LayerNorm folded into the projection: out = act(rstd * (a . w'^T) - mean * rstd * colsum(w') + bias')
+// with w' = w * gamma; col_aff [2, N] fp32 = (colsum(w'), bias'), row_aff [M, 2] fp32 = (rstd, -mean * rstd)
+// from ln_row_stats over the same rows of a.  Never the skinny path (it has its own folded-norm form).
+void gemm_lnf(const at::Tensor& a, const at::Tensor& w, const at::Tensor& col_aff, const at::Tensor& row_aff,
+              int64_t act, at::Tensor out, int64_t tile) {
+  check_bf16_rows(a, "a");
+  check_bf16_rows(w, "w");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && K % 64 == 0 && N % 16 == 0, "gemm_lnf: shapes");
+  TORCH_CHECK(col_aff.is_cuda() && col_aff.scalar_type() == at::kFloat && col_aff.is_contiguous() &&
+                  col_aff.numel() == 2 * N, "gemm_lnf: col_aff must be fp32 [2, N]");
+  TORCH_CHECK(row_aff.is_cuda() && row_aff.scalar_type() == at::kFloat && row_aff.is_contiguous() &&
+                  row_aff.numel() >= 2 * M, "gemm_lnf: row_aff must be fp32 [M, 2]");
+  check_bf16_rows(out, "out");
+  TORCH_CHECK(out.size(0) >= M && out.size(1) >= N, "gemm_lnf: out");
+  lumen::GemmEpi ep{};
+  ep.alpha = 1.f;
+  ep.act = (int)act;
+  ep.row_aff = row_aff.data_ptr<float>();
+  ep.col_aff = col_aff.data_ptr<float>();
+  const at::DeviceGuard guard(a.device());
+  LUMEN_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
+                                   (int)M, (int)N, (int)K, ep, (int)tile, cur_stream()));
+}
+
+void ln_row_stats(const at::Tensor& x, at::Tensor out, double eps) {
+  check_bf16_rows(x, "x");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() >= 2 * x.size(0),
+              "ln_row_stats: out must be fp32 [rows, 2]");
+  const at::DeviceGuard guard(x.device());
+  LUMEN_CHECK_HIP(lumen::ln_row_stats(bf(x), x.stride(0), out.data_ptr<float>(), (int)x.size(0), (int)x.size(1),
+                                      (float)eps, cur_stream()));
 }
 
 // ---------------------------------------------------------------- fp8 (e4m3fn) weight GEMM
@@ -706,6 +742,8 @@ TORCH_LIBRARY(lumen, m) {
   m.def("norm(Tensor x, Tensor? row_idx, Tensor? add, Tensor(r!)? resid_out, Tensor w, Tensor? b, "
         "Tensor(o!) out, float eps, int mode) -> ()");
   m.def("l2norm_(Tensor(a!) x, float eps) -> ()");
+  m.def("gemm_lnf(Tensor a, Tensor w, Tensor col_aff, Tensor row_aff, int act, Tensor(o!) out, int tile) -> ()");
+  m.def("ln_row_stats(Tensor x, Tensor(o!) out, float eps) -> ()");
   m.def("gemm_probe(Tensor a, Tensor w, Tensor(o!) out, Tensor(d!) dbg, int tile) -> ()");
   m.def("gemm_w8(Tensor a, Tensor w8, Tensor scale, Tensor? bias, Tensor? residual, int act, Tensor(o!) out, "
         "int glu) -> ()");
@@ -740,6 +778,8 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("norm", &norm);
   m.impl("l2norm_", &l2norm_);
+  m.impl("gemm_lnf", &gemm_lnf);
+  m.impl("ln_row_stats", &ln_row_stats);
   m.impl("gemm_probe", &gemm_probe);
   m.impl("gemm_w8", &gemm_w8);
   m.impl("gemm_f8", &gemm_f8);

@@ -186,6 +186,20 @@ class _Block(nn.Module):
         self.fc2_w = nn.Parameter(torch.empty(width, mlp, **kw), requires_grad=False)
         self.fc2_b = nn.Parameter(torch.zeros(width, **kw), requires_grad=False)
 
+    def lnf(self):
+        """GPU form with both LayerNorms folded into the projections that consume them
+        (ops.ln_fold_weights): (qkv w', qkv col_aff, fc1 w', fc1 col_aff).  Rebuilt whenever a
+        parameter it derives from is rewritten (weight loads bump the tensors' versions)."""
+        src = (self.ln1_w, self.ln1_b, self.qkv_w, self.qkv_b, self.ln2_w, self.ln2_b, self.fc1_w, self.fc1_b)
+        key = tuple((p.data_ptr(), p._version) for p in src)
+        if getattr(self, "_lnf_key", None) != key:
+            with torch.no_grad():
+                qw, qa = ops.ln_fold_weights(self.qkv_w, self.qkv_b, self.ln1_w, self.ln1_b)
+                fw, fa = ops.ln_fold_weights(self.fc1_w, self.fc1_b, self.ln2_w, self.ln2_b)
+            self._lnf_cache = (qw, qa, fw, fa)
+            self._lnf_key = key
+        return self._lnf_cache
+
     def random_init(self, gen: torch.Generator, layers: int):
         w = self.qkv_w.shape[1]
         attn_std = w ** -0.5
@@ -202,21 +216,36 @@ def _block_steps(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, 
     ``yield`` per block so several micro-batches can be issued layer-interleaved."""
     T, W = x.shape
     D = W // heads
-    h = torch.empty_like(x)
     o = torch.empty_like(x)
+    # GPU: both LayerNorms are folded into qkv / fc1 (ops.linear_lnf): a row-statistics pass writes
+    # 8 bytes per row instead of a normalised copy of x, and the GEMMs read the residual stream
+    fold = x.is_cuda and _LN_FOLD
+    if fold:
+        st = torch.empty((T, 2), device=x.device, dtype=torch.float32)
+    else:
+        h = torch.empty_like(x)
     # the out-proj / fc2 residual is added in the GEMM epilogue (the MFMA GEMM adds the prefetched
     # residual rows before its single bf16 rounding); a separate add + LayerNorm pass measured
     # 5837 vs 5951 img/s on ViT-L/14 b512 (profiles/r2_bench_resid_paths_v1.txt)
     for i, blk in enumerate(blocks):
-        ops.layer_norm(x, blk.ln1_w, blk.ln1_b, eps, out=h)
-        qkv = ops.linear(h, blk.qkv_w, blk.qkv_b, tile=tile)
+        if fold:
+            qw, qa, fw, fa = blk.lnf()
+            ops.ln_row_stats(x, eps, out=st)
+            qkv = ops.linear_lnf(x, qw, qa, st, tile=tile)
+        else:
+            ops.layer_norm(x, blk.ln1_w, blk.ln1_b, eps, out=h)
+            qkv = ops.linear(h, blk.qkv_w, blk.qkv_b, tile=tile)
         q5 = qkv.view(B, S, 3, heads, D)
         ops.attention(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], causal=causal, kv_len=kv_len,
                       out=o.view(B, S, heads, D))
         del qkv, q5
         ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x, tile=tile if res_tile is None else res_tile)
-        ops.layer_norm(x, blk.ln2_w, blk.ln2_b, eps, out=h)
-        f = ops.linear(h, blk.fc1_w, blk.fc1_b, act=act, tile=tile)
+        if fold:
+            ops.ln_row_stats(x, eps, out=st)
+            f = ops.linear_lnf(x, fw, fa, st, act=act, tile=tile)
+        else:
+            ops.layer_norm(x, blk.ln2_w, blk.ln2_b, eps, out=h)
+            f = ops.linear(h, blk.fc1_w, blk.fc1_b, act=act, tile=tile)
         ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x, tile=tile if res_tile is None else res_tile)
         del f
         yield i
@@ -237,6 +266,7 @@ def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, ep
 # tail pass (tile code 1609: ping-pong 256x256, non-persistent, no tail split) and attention /
 # LayerNorm of one half overlap GEMM tails of the other.
 _VIT_MICRO = int(os.environ.get("LUMEN_VIT_MICRO", "2"))
+_LN_FOLD = True   # GPU blocks: LayerNorms folded into qkv / fc1 (see _block_steps)
 # ping-pong 256x256, 2 phases per K-tile + priority, group_m = 2, no tail split (1629 vs 1609 / 1689:
 # 6209-6222 vs 6203-6204 / 6129-6130 img/s, profiles/r2_vit_micro_streams_v1.txt)
 _VIT_MICRO_TILE = 1629

@@ -302,6 +302,55 @@ def layer_norm(x, w, b=None, eps=1e-5, row_idx=None, out=None, out_dtype=None, a
     return out
 
 
+def ln_row_stats(x: torch.Tensor, eps: float = 1e-5, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """LayerNorm statistics of the rows of x [R, D]: fp32 [R, 2] = (rstd, -mean * rstd), the
+    row half of a LayerNorm folded into the next projection (:func:`linear_lnf`)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    if out is None:
+        out = torch.empty((x2.shape[0], 2), device=x.device, dtype=torch.float32)
+    if x.is_cuda:
+        if x2.stride(-1) != 1 or x2.stride(0) % 8 != 0:
+            x2 = x2.contiguous()
+        hip_ops().ln_row_stats(x2, out, float(eps))
+        return out
+    xf = x2.float()
+    mean = xf.mean(-1)
+    rstd = torch.rsqrt(((xf - mean[:, None]) ** 2).mean(-1) + eps)
+    out[:, 0] = rstd
+    out[:, 1] = -mean * rstd
+    return out
+
+
+def ln_fold_weights(w: torch.Tensor, bias: Optional[torch.Tensor], gamma: torch.Tensor,
+                    beta: Optional[torch.Tensor]) -> tuple[torch.Tensor, torch.Tensor]:
+    """Fold LayerNorm(gamma, beta) into the projection (w [N, K], bias [N]) that consumes it:
+    returns w' = w * gamma (w's dtype) and col_aff fp32 [2, N] = (colsum(w'), bias + w . beta),
+    colsum taken over the rounded w' the GEMM multiplies with."""
+    wf = (w.float() * gamma.float()[None, :]).to(w.dtype)
+    cs = wf.float().sum(1)
+    cb = bias.float().clone() if bias is not None else torch.zeros(w.shape[0], device=w.device)
+    if beta is not None:
+        cb += w.float() @ beta.float()
+    return wf, torch.stack([cs, cb]).contiguous()
+
+
+def linear_lnf(x: torch.Tensor, wf: torch.Tensor, col_aff: torch.Tensor, row_aff: torch.Tensor, act=None,
+               out: Optional[torch.Tensor] = None, tile: int = -1) -> torch.Tensor:
+    """act(LayerNorm(x) . w^T + b) with the norm folded in (:func:`ln_fold_weights`,
+    :func:`ln_row_stats`): act(rstd * (x . w'^T) - mean * rstd * colsum(w') + b') over the raw rows
+    of x [M, K] (bf16 on the GPU), so no normalised copy of x is written."""
+    M, N = x.shape[0], wf.shape[0]
+    if out is None:
+        out = torch.empty((M, N), device=x.device, dtype=x.dtype)
+    a = act_id(act)
+    if x.is_cuda:
+        hip_ops().gemm_lnf(x, wf, col_aff, row_aff, a, out, int(tile))
+        return out
+    y = (x.float() @ wf.float().t()) * row_aff[:M, :1] + row_aff[:M, 1:] * col_aff[0] + col_aff[1]
+    out.copy_(_act_ref(y, a).to(out.dtype))
+    return out
+
+
 def rms_norm(x, w, eps=1e-6, add=None, resid_out=None, out=None, out_dtype=None):
     """RMSNorm(x [+ add]); when ``resid_out`` is given the pre-norm sum is stored there."""
     o = _norm(x, w, None, eps, 1, add=add, resid_out=resid_out, out=out, out_dtype=out_dtype)

@@ -274,3 +274,30 @@ def test_image_prep_center_crop_matches_reference():
     gotp = ops.image_prep([i.to(DEV) for i in imgs], (32, 32), layout="patches", patch=8, kpad=256,
                           out_dtype=torch.bfloat16, **kw)
     assert (gotp.float().cpu() - refp.float()).abs().max().item() <= 0.05
+
+
+@pytest.mark.parametrize("M,N,K,tile", [(24 * 256, 3072, 1024, 1629), (24 * 256, 4096, 1024, 609),
+                                        (16 * 256, 1024, 1024, 709), (24 * 256 + 77, 3072, 1024, -1),
+                                        (577, 3072, 1024, -1), (577, 4096, 1024, -1), (40, 768, 768, -1),
+                                        (512 * 77, 2304, 768, -1), (300 * 256 + 300, 1024, 512, 609)])
+@pytest.mark.parametrize("act", [None, "quick_gelu"])
+def test_gemm_layernorm_folded(M, N, K, tile, act):
+    """LayerNorm folded into the projection (ln_row_stats + gemm_lnf): ping-pong FAST form (interior
+    tiles), persistent form, generic / tail-split / 128x128 / small-M epilogues, against the fp32
+    LayerNorm + Linear reference."""
+    g = torch.Generator().manual_seed(M + N)
+    x = (torch.randn(M, K, generator=g) * 2 + 0.5).bfloat16()
+    gam, bet = torch.rand(K, generator=g) + 0.5, torch.randn(K, generator=g) * 0.1
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
+    b = torch.randn(N, generator=g).bfloat16()
+    rows = torch.cat([torch.arange(0, min(M, 600)), torch.randint(0, M, (800,), generator=g),
+                      torch.arange(max(0, M - 600), M)])
+    ref = ops.linear(ops.layer_norm(x[rows].float(), gam, bet, 1e-5), w.float(), b.float(), act=act)
+    wf, ca = ops.ln_fold_weights(w.to(DEV), b.to(DEV), gam.to(DEV).bfloat16(), bet.to(DEV).bfloat16())
+    xd = x.to(DEV)
+    st = ops.ln_row_stats(xd, 1e-5)
+    st_ref = ops.ln_row_stats(x[rows], 1e-5)
+    assert torch.allclose(st.cpu()[rows], st_ref, rtol=1e-4, atol=1e-5)
+    got = ops.linear_lnf(xd, wf, ca, st, act=act, tile=tile).cpu().float()
+    assert _rel(got[rows], ref) < 1e-2
+    assert torch.isfinite(got).all()

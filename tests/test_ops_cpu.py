@@ -189,3 +189,17 @@ def test_center_crop_matches_open_clip_transform(hw):
                          center_crop=True)[0]
     assert got.shape == (S, S, 3)
     assert np.abs(got.numpy() - ref).max() <= 1.0                # PIL 8-bit coefficients: 1 LSB
+
+
+def test_layernorm_folded_into_linear_matches_unfused():
+    """ln_row_stats + linear_lnf (LayerNorm folded into the projection, the GPU block form)
+    equals layer_norm followed by linear, on rows with a large common offset."""
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn(37, 96, generator=g) * 3 + 5).bfloat16()
+    gam, bet = torch.rand(96, generator=g) + 0.5, torch.randn(96, generator=g)
+    w, b = torch.randn(48, 96, generator=g) * 0.1, torch.randn(48, generator=g)
+    ref = ops.linear(ops.layer_norm(x.float(), gam, bet, 1e-5), w, b, act="gelu")
+    wf, ca = ops.ln_fold_weights(w, b, gam, bet)
+    st = ops.ln_row_stats(x, 1e-5)
+    got = ops.linear_lnf(x.float(), wf, ca, st, act="gelu", out=torch.empty(37, 48))
+    assert torch.allclose(got, ref, atol=1e-4, rtol=1e-4)

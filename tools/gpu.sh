@@ -19,6 +19,7 @@
 #   prof_face / prof_ocr   rocprofv3 kernel stats of the face / OCR bench
 #   f8             fp8 tests (tests/test_fp8_gpu.py) + tools/f8_gemm_bench.py ($F8_SHAPES, $F8_M)
 #   pmc_face / pmc_ocr   PMC counters (SQ pass + memory pass) of the face / OCR pipelines
+#   serve          tools/serve_bench.py: gRPC hub end to end (CLIP ViT-L/14 64 clients, face 32 clients)
 #   pmc_gemm       PMC counters (MFMA, LDS conflicts, busy) of one ViT-L/14 GEMM shape
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -92,6 +93,11 @@ for task in "$@"; do
         --pmc SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
         -d gpurun_out/pmc_gemm -o run -- python3 tools/gemm_bench_tiles.py --tiles=609 --rounds 1 --iters 2 \
         --shapes "${GEMM_SHAPES:-131584x3072x1024}" ;;
+    serve)
+      step serve_clip 300 python -u tools/serve_bench.py --service clip --model CLIP-ViT-L-14 --device cuda --clients 64 \
+        --seconds 20
+      step serve_face 300 python -u tools/serve_bench.py --service face --model antelopev2 --device cuda --clients 32 \
+        --seconds 20 ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
 done
