@@ -54,6 +54,12 @@ struct DecodeArgs {
   uint16_t* v_cache_w;
   int kv_fp8;             // caches hold e4m3fn bytes: widened to bf16 on load (cvt_scalef32_pk_bf16_fp8)
   uint32_t* split_cnt;    // [B, Hkv] zeroed tickets of the in-launch split combine (nsplit > 1; nsplit <= 32)
+  // Weight prefetch into the Infinity Cache: workgroups beyond the attention grid (grid.z >= B)
+  // read these bytes with default-policy loads and drop them, so the GEMV that runs next (the
+  // o projection) streams its weights from the 256 MiB MALL instead of HBM while the attention
+  // itself occupies only a few dozen CUs.  null / 0 = none.
+  const uint8_t* pf[2];
+  int64_t pf_bytes[2];
 };
 hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream);
 

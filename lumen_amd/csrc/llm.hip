@@ -93,7 +93,36 @@ hipError_t rope_kv(const RopeKVArgs& a, hipStream_t stream) {
 // stores, draws a ticket from the (sequence, kv head) counter, and the last to arrive merges
 // all splits (sc1 loads, 8 in flight) -- no combine launch, no fences (MI355X_MICROARCH.md
 // hand-off rules); the last arriver re-zeroes the counter for the next launch.
-constexpr int PD_NW = 4;   // 1 wave per SIMD: the 512-VGPR budget holds a whole block's K and V fragments
+// 4 waves = 1 per SIMD: the 512-VGPR budget holds a whole block's K and V fragments.  The launch
+// fixes the number of splits (grid.x); blocks per split = max(a.blocks_per_split, ceil(blocks /
+// grid.x)) is derived from each sequence's own ctx_len on the device, so a graph captured for the
+// longest context spreads every shorter one over all its splits as well.  (One-wave workgroups with
+// one block each measured 2x slower: their single-wave split combine is latency-serial,
+// profiles/r3_decode_attn_splits_v1.txt.)
+constexpr int PD_NW = 4;
+
+// Prefetch workgroups (blockIdx.z >= B): stream a.pf[] once through the memory-side cache.
+__device__ __forceinline__ void pd_prefetch(const DecodeArgs& a, int wg, int nwg) {
+  uint32_t x = 0;
+#pragma unroll 1
+  for (int r = 0; r < 2; ++r) {
+    if (a.pf[r] == nullptr || a.pf_bytes[r] <= 0) continue;
+    const int64_t n16 = a.pf_bytes[r] >> 4;                     // whole 16-byte chunks
+    const int64_t per = (n16 + nwg - 1) / nwg;
+    const int64_t c0 = (int64_t)wg * per, c1 = min(n16, c0 + per);
+    const u32x4_t* p = reinterpret_cast<const u32x4_t*>(a.pf[r]);
+    int64_t c = c0 + threadIdx.x;
+    for (; c + 7 * (int64_t)blockDim.x < c1; c += 8 * (int64_t)blockDim.x) {   // 8 loads in flight per lane
+      u32x4_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[c + u * (int64_t)blockDim.x];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x ^= v[u][0] ^ v[u][3];
+    }
+    for (; c < c1; c += blockDim.x) x ^= p[c][0];
+  }
+  if (x == 0x9e3779b9u && a.pf_bytes[0] < 0) a.o[threadIdx.x] = 0;   // never true: keeps the loads
+}
 
 template <int D>
 __device__ __forceinline__ void rope_chunks(u32x4_t (&w)[D / 32], const float2* cs, int g) {
@@ -127,8 +156,13 @@ __device__ __forceinline__ __bf16 as_cached(__bf16 v) {
 }
 
 template <int D, bool F8KV>
-__global__ void __launch_bounds__(64 * PD_NW) paged_decode_kernel(DecodeArgs a) {
+__global__ void __launch_bounds__(64 * PD_NW) paged_decode_kernel(DecodeArgs a, int B) {
   constexpr int NW = PD_NW;
+  if ((int)blockIdx.z >= B) {   // MALL prefetch workgroups
+    pd_prefetch(a, ((blockIdx.z - B) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x,
+                (gridDim.z - B) * gridDim.y * gridDim.x);
+    return;
+  }
   constexpr int KS = D / 32;   // k-steps of S^T over the head dim
   constexpr int NB = D / 16;   // 16-wide d blocks of O^T
   __shared__ float sm_ml[NW][2][16];
@@ -143,9 +177,10 @@ __global__ void __launch_bounds__(64 * PD_NW) paged_decode_kernel(DecodeArgs a) 
   const int G = a.H / a.Hkv;
   const int ctx = a.ctx_len[b];
   const int nblk = (ctx + KV_BLOCK - 1) / KV_BLOCK;
-  const int blk0 = split * a.blocks_per_split;
-  const int blk1 = min(blk0 + a.blocks_per_split, nblk);
-  const int ns = max(1, (nblk + a.blocks_per_split - 1) / a.blocks_per_split);   // splits holding blocks
+  const int bps = max(a.blocks_per_split, (nblk + (int)gridDim.x - 1) / (int)gridDim.x);
+  const int blk0 = split * bps;
+  const int blk1 = min(blk0 + bps, nblk);
+  const int ns = max(1, (nblk + bps - 1) / bps);   // splits holding blocks
   if (split >= ns) return;
   // this wave's blocks: blk0 + wid, + NW, ... (one block per wave up to 512 tokens per split)
   int phys = blk0 + wid < blk1 ? a.block_table[(int64_t)b * a.bt_stride + blk0 + wid] : 0;   // first load of the chain
@@ -344,25 +379,27 @@ __global__ void __launch_bounds__(64 * PD_NW) paged_decode_kernel(DecodeArgs a) 
       const int coff = (int)(slot & 63);
       const uint16_t* kv = a.q + (int64_t)b * a.q_sb + (int64_t)(a.H + hk) * D;   // unrotated k head
       const int half = D / 2;
-      if (tid < half) {
-        const float2 c = reinterpret_cast<const float2*>(a.cos_sin)[(int64_t)a.pos[b] * half + tid];
-        const float x1 = bf2f(kv[tid]), x2 = bf2f(kv[tid + half]);
+      for (int i = tid; i < half + D; i += 64 * NW) {   // k rotation pairs, then v elements
+      if (i < half) {
+        const float2 c = reinterpret_cast<const float2*>(a.cos_sin)[(int64_t)a.pos[b] * half + i];
+        const float x1 = bf2f(kv[i]), x2 = bf2f(kv[i + half]);
         const uint16_t y1 = f2bf(x1 * c.x - x2 * c.y), y2 = f2bf(x2 * c.x + x1 * c.y);
         const int64_t ko = ((cblk * a.Hkv + hk) * KV_BLOCK + coff) * D;
         if constexpr (F8KV) {
           uint8_t* kr = reinterpret_cast<uint8_t*>(a.k_cache_w) + ko;
-          kr[tid] = f2fp8(bf2f(y1));
-          kr[tid + half] = f2fp8(bf2f(y2));
+          kr[i] = f2fp8(bf2f(y1));
+          kr[i + half] = f2fp8(bf2f(y2));
         } else {
-          a.k_cache_w[ko + tid] = y1;
-          a.k_cache_w[ko + tid + half] = y2;
+          a.k_cache_w[ko + i] = y1;
+          a.k_cache_w[ko + i + half] = y2;
         }
-      } else if (tid < half + D) {
-        const int d = tid - half;
+      } else {
+        const int d = i - half;
         const uint16_t* vr = a.q + (int64_t)b * a.q_sb + (int64_t)(a.H + a.Hkv + hk) * D;
         const int64_t vo = ((cblk * a.Hkv + hk) * D + d) * KV_BLOCK + coff;
         if constexpr (F8KV) reinterpret_cast<uint8_t*>(a.v_cache_w)[vo] = f2fp8(bf2f(vr[d]));
         else a.v_cache_w[vo] = vr[d];
+      }
       }
     }
   }
@@ -455,13 +492,16 @@ __global__ void __launch_bounds__(64 * PD_NW) paged_decode_kernel(DecodeArgs a) 
 }
 
 hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream) {
-  if (a.nsplit > 32 || (a.nsplit > 1 && a.split_cnt == nullptr))
-    return hipErrorInvalidValue;
-  dim3 grid(a.nsplit, a.Hkv, B), block(64 * PD_NW);
-#define PD_LAUNCH(D_)                                                                           \
-  do {                                                                                          \
-    if (a.kv_fp8) hipLaunchKernelGGL((paged_decode_kernel<D_, true>), grid, block, 0, stream, a);  \
-    else hipLaunchKernelGGL((paged_decode_kernel<D_, false>), grid, block, 0, stream, a);          \
+  if (a.nsplit > 32 || (a.nsplit > 1 && a.split_cnt == nullptr)) return hipErrorInvalidValue;
+  // prefetch slices: enough z-slices of (nsplit x Hkv) workgroups for >= 192 prefetching CUs
+  const bool pf = (a.pf[0] != nullptr && a.pf_bytes[0] > 0) || (a.pf[1] != nullptr && a.pf_bytes[1] > 0);
+  const int per_z = a.nsplit * a.Hkv;
+  const int pfz = pf ? (192 + per_z - 1) / per_z : 0;
+  dim3 grid(a.nsplit, a.Hkv, B + pfz), block(64 * PD_NW);
+#define PD_LAUNCH(D_)                                                                               \
+  do {                                                                                              \
+    if (a.kv_fp8) hipLaunchKernelGGL((paged_decode_kernel<D_, true>), grid, block, 0, stream, a, B);  \
+    else hipLaunchKernelGGL((paged_decode_kernel<D_, false>), grid, block, 0, stream, a, B);          \
   } while (0)
   if (D == 64) PD_LAUNCH(64);
   else if (D == 128) PD_LAUNCH(128);

@@ -67,7 +67,8 @@ void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
                   const at::Tensor& block_table, const at::Tensor& ctx_len, at::Tensor out, int64_t H, int64_t Hkv,
                   double scale, int64_t nsplit, int64_t blocks_per_split, const c10::optional<at::Tensor>& part_o,
                   const c10::optional<at::Tensor>& part_ml, const c10::optional<at::Tensor>& pos,
-                  const c10::optional<at::Tensor>& cos_sin, const c10::optional<at::Tensor>& slots) {
+                  const c10::optional<at::Tensor>& cos_sin, const c10::optional<at::Tensor>& slots,
+                  const c10::optional<at::Tensor>& pf0, const c10::optional<at::Tensor>& pf1) {
   const int64_t D = k_cache.size(3);
   const int kv_fp8 = check_cache(k_cache, v_cache, Hkv, D);
   TORCH_CHECK(D == 32 || D == 64 || D == 128, "paged_decode: head dim 32, 64 or 128");
@@ -82,8 +83,9 @@ void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
               block_table.size(0) == B && block_table.stride(1) == 1, "block_table int32 [B, max_blocks]");
   TORCH_CHECK(ctx_len.is_cuda() && ctx_len.scalar_type() == at::kInt && ctx_len.numel() == B && ctx_len.is_contiguous(),
               "ctx_len int32 [B]");
-  TORCH_CHECK(nsplit >= 1 && blocks_per_split >= 1 && nsplit * blocks_per_split >= block_table.size(1),
-              "paged_decode: splits must cover the block table");
+  // the kernel widens the splits to cover each sequence's own context (blocks per split =
+  // max(blocks_per_split, ceil(blocks / nsplit))), so any split count covers the table
+  TORCH_CHECK(nsplit >= 1 && blocks_per_split >= 1, "paged_decode: nsplit / blocks_per_split");
   lumen::DecodeArgs a{};
   a.q = bfp(q); a.q_sb = q.stride(0);
   a.k_cache = reinterpret_cast<const uint16_t*>(k_cache.data_ptr());
@@ -119,6 +121,15 @@ void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
     a.k_cache_w = reinterpret_cast<uint16_t*>(k_cache.data_ptr());
     a.v_cache_w = reinterpret_cast<uint16_t*>(v_cache.data_ptr());
   }
+  const c10::optional<at::Tensor>* pfs[2] = {&pf0, &pf1};
+  for (int r = 0; r < 2; ++r) {
+    const auto& t = *pfs[r];
+    if (t.has_value() && t->defined()) {
+      TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->device() == q.device(), "paged_decode: prefetch tensor");
+      a.pf[r] = reinterpret_cast<const uint8_t*>(t->data_ptr());
+      a.pf_bytes[r] = t->numel() * t->element_size();
+    }
+  }
   if (B == 0) return;
   const at::DeviceGuard g(q.device());
   CHECK_HIP3(lumen::paged_decode(a, (int)B, (int)D, cur()));
@@ -143,7 +154,8 @@ TORCH_LIBRARY_FRAGMENT(lumen, m) {
         "int H, int Hkv, int D) -> ()");
   m.def("paged_decode(Tensor q, Tensor(k!) k_cache, Tensor(v!) v_cache, Tensor block_table, Tensor ctx_len, "
         "Tensor(o!) out, int H, int Hkv, float scale, int nsplit, int blocks_per_split, Tensor(p!)? part_o=None, "
-        "Tensor(m!)? part_ml=None, Tensor? pos=None, Tensor? cos_sin=None, Tensor? slots=None) -> ()");
+        "Tensor(m!)? part_ml=None, Tensor? pos=None, Tensor? cos_sin=None, Tensor? slots=None, Tensor? pf0=None, "
+        "Tensor? pf1=None) -> ()");
   m.def("rep_penalty_(Tensor(a!) logits, Tensor ids, Tensor penalty) -> ()");
 }
 

@@ -12,7 +12,8 @@
 namespace lumen {
 hipError_t db_components(const void* prob, int is_bf16, const float* thresh, int n, int H, int W, int* lab,
                          int* out, int* count, int cap, int min_size, hipStream_t stream);
-hipError_t db_quad_score(const void* prob, int is_bf16, int H, int W, const float* quads, const int* img, float* score,
+hipError_t db_quad_score(const void* prob, int is_bf16, int n, int H, int W, const float* quads, const int* img, float* score,
+                         double* pre,
                          int m, hipStream_t stream);
 }  // namespace lumen
 
@@ -101,6 +102,42 @@ void ctc_greedy(const at::Tensor& probs, int64_t blank, at::Tensor out_ids, at::
                                out_conf.data_ptr<float>(), stream()));
 }
 
+// Recogniser classifier + CTC greedy decode without stored logits: h [B*T, K] bf16 rows, w [N, K]
+// bf16, bias f32 [N] (optional), C real classes (<= N) -> out_ids [B, T] (-1 padded), out_len [B],
+// out_conf [B]; top1_idx / top1_conf [B*T] receive the per-step arg-max and its probability.
+void cls_ctc(const at::Tensor& h, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t C, int64_t B,
+             int64_t T, int64_t blank, const c10::optional<at::Tensor>& tlen, at::Tensor top1_idx, at::Tensor top1_conf,
+             at::Tensor out_ids, at::Tensor out_len, at::Tensor out_conf) {
+  TORCH_CHECK(h.is_cuda() && h.scalar_type() == at::kBFloat16 && h.dim() == 2 && h.stride(1) == 1 &&
+                  h.stride(0) % 8 == 0, "cls_ctc: h bf16 rows");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.size(1) == h.size(1),
+              "cls_ctc: w bf16 [N, K]");
+  const int64_t M = h.size(0), K = h.size(1), N = w.size(0);
+  TORCH_CHECK(K == 64 || K == 128 || K == 256, "cls_ctc: K must be 64, 128 or 256");
+  TORCH_CHECK(M == B * T && C >= 1 && C <= N, "cls_ctc: shapes");
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() >= N, "cls_ctc: bias f32 [N]");
+    bp = bias->data_ptr<float>();
+  }
+  TORCH_CHECK(top1_idx.scalar_type() == at::kInt && top1_idx.numel() == M && top1_idx.is_contiguous(), "top1_idx");
+  TORCH_CHECK(top1_conf.scalar_type() == at::kFloat && top1_conf.numel() == M && top1_conf.is_contiguous(), "top1_conf");
+  TORCH_CHECK(out_ids.scalar_type() == at::kInt && out_ids.numel() == M && out_ids.is_contiguous(), "ids");
+  TORCH_CHECK(out_len.scalar_type() == at::kInt && out_len.numel() == B, "len");
+  TORCH_CHECK(out_conf.scalar_type() == at::kFloat && out_conf.numel() == B, "conf");
+  const int* tl = nullptr;
+  if (tlen.has_value() && tlen->defined()) {
+    TORCH_CHECK(tlen->is_cuda() && tlen->scalar_type() == at::kInt && tlen->numel() == B && tlen->is_contiguous(), "tlen");
+    tl = tlen->data_ptr<int>();
+  }
+  const at::DeviceGuard g(h.device());
+  CHECK_HIP2(lumen::cls_argmax(reinterpret_cast<const uint16_t*>(h.data_ptr()), h.stride(0),
+                               reinterpret_cast<const uint16_t*>(w.data_ptr()), bp, (int)M, (int)N, (int)K, (int)C,
+                               top1_idx.data_ptr<int>(), top1_conf.data_ptr<float>(), stream()));
+  CHECK_HIP2(lumen::ctc_collapse(top1_idx.data_ptr<int>(), top1_conf.data_ptr<float>(), (int)B, (int)T, (int)blank, tl,
+                                 out_ids.data_ptr<int>(), out_len.data_ptr<int>(), out_conf.data_ptr<float>(), stream()));
+}
+
 // DB post-processing on the GPU (db_post.hip): prob [n, H, W] bf16/f32, thresh f32 [n];
 // lab int32 [n*H*W] workspace; out int32 [cap, 3] (root, x, y); count int32 [1]
 void db_components(const at::Tensor& prob, const at::Tensor& thresh, at::Tensor lab, at::Tensor out, at::Tensor count,
@@ -132,9 +169,11 @@ void db_quad_score(const at::Tensor& prob, const at::Tensor& quads, const at::Te
   TORCH_CHECK(img.is_cuda() && img.scalar_type() == at::kInt && img.numel() == m && img.is_contiguous(),
               "db_quad_score: img int32 [m]");
   const at::DeviceGuard g(prob.device());
-  CHECK_HIP2(lumen::db_quad_score(prob.data_ptr(), prob.scalar_type() == at::kBFloat16, (int)prob.size(1),
-                                  (int)prob.size(2), quads.data_ptr<float>(), img.data_ptr<int>(),
-                                  score.data_ptr<float>(), (int)m, stream()));
+  // fp64 row prefix sums of every map (the O(rows) span sums of the score kernel)
+  auto pre = at::empty({prob.size(0) * prob.size(1) * (prob.size(2) + 1)}, prob.options().dtype(at::kDouble));
+  CHECK_HIP2(lumen::db_quad_score(prob.data_ptr(), prob.scalar_type() == at::kBFloat16, (int)prob.size(0),
+                                  (int)prob.size(1), (int)prob.size(2), quads.data_ptr<float>(), img.data_ptr<int>(),
+                                  score.data_ptr<float>(), pre.data_ptr<double>(), (int)m, stream()));
 }
 
 }  // namespace
@@ -149,6 +188,8 @@ TORCH_LIBRARY_FRAGMENT(lumen, m) {
   m.def("nms(Tensor cand, Tensor count, float iou_thr, Tensor(k!) keep, Tensor(n!) keep_n) -> ()");
   m.def("warp_batch(Tensor src, Tensor meta, Tensor minv, Tensor(o!) out, float scale, float mean, float std, "
         "bool swap_rb, bool cubic, bool replicate=False) -> ()");
+  m.def("cls_ctc(Tensor h, Tensor w, Tensor? bias, int C, int B, int T, int blank, Tensor? tlen, Tensor(a!) top1_idx, "
+        "Tensor(b!) top1_conf, Tensor(i!) out_ids, Tensor(l!) out_len, Tensor(c!) out_conf) -> ()");
   m.def("ctc_greedy(Tensor probs, int blank, Tensor(i!) out_ids, Tensor(l!) out_len, Tensor(c!) out_conf, "
         "bool from_logits=False, Tensor? tlen=None) -> ()");
 }
@@ -158,6 +199,7 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("nms", &nms);
   m.impl("warp_batch", &warp_batch);
   m.impl("ctc_greedy", &ctc_greedy);
+  m.impl("cls_ctc", &cls_ctc);
   m.impl("db_components", &db_components);
   m.impl("db_quad_score", &db_quad_score);
 }

@@ -43,6 +43,10 @@ struct WarpArgs {
   int replicate;         // border: 0 constant 0, 1 replicate (cv2 BORDER_REPLICATE)
 };
 hipError_t warp_batch(const WarpArgs& a, hipStream_t stream);
+hipError_t cls_argmax(const uint16_t* h, int64_t ldh, const uint16_t* w, const float* bias, int M, int N, int K, int C,
+                      int* idx_out, float* conf_out, hipStream_t stream);
+hipError_t ctc_collapse(const int* idx, const float* conf, int B, int T, int blank, const int* tlen, int* out_ids,
+                        int* out_len, float* out_conf, hipStream_t stream);
 hipError_t ctc_greedy(const float* probs, int B, int T, int C, int blank, int from_logits, const int* tlen,
                       int* tmp_idx, float* tmp_conf, int* out_ids, int* out_len, float* out_conf, hipStream_t stream);
 

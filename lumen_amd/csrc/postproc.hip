@@ -292,6 +292,158 @@ __global__ void ctc_collapse_kernel(const int* __restrict__ idx, const float* __
   out_conf[b] = n > 0 ? s / n : 0.f;
 }
 
+// Recogniser classifier fused with the CTC arg-max (O-8): logits = h . W^T + bias are never
+// stored.  For the PP-OCR recogniser (6625 classes, ~25k time steps per batch) the fp32 logits
+// are ~650 MB; here each workgroup keeps 128 rows of h in registers (4 waves x 2 MFMA row
+// fragments), streams W (L2-resident, [N, K] bf16) through a double-buffered, XOR-swizzled LDS
+// tile of 64 classes, and folds every tile into per-row online (max, arg-max, sum of exp)
+// states; one 16-lane reduction at the end gives idx[row] and conf[row] = 1 / sum (the softmax
+// probability of the arg-max, what ctc_argmax_kernel computes from stored logits).  Ties keep the
+// smaller class index.  K in {64, 128, 256}; classes >= C (padding) never win.
+template <int K>
+__global__ void __launch_bounds__(256) cls_argmax_kernel(const uint16_t* __restrict__ h, int64_t ldh,
+                                                         const uint16_t* __restrict__ w, const float* __restrict__ bias,
+                                                         int M, int N, int C, int* __restrict__ idx_out,
+                                                         float* __restrict__ conf_out) {
+  constexpr int KS = K / 32;          // MFMA k-steps
+  constexpr int CPR = K / 8;          // 16-byte chunks per W row
+  constexpr int TILE = 64 * K * 2;    // bytes of one 64-class W tile
+  constexpr int LPT = TILE / (256 * 16);   // 16-byte loads per thread per tile
+  __shared__ __attribute__((aligned(16))) char sw[2][TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int frow = lane & 15, g = lane >> 4;
+  const int row0 = blockIdx.x * 128 + wid * 32;
+  // A fragments of the wave's 2 x 16 rows, whole K, kept in registers
+  bf16x8_t fa[2][KS];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = min(row0 + i * 16 + frow, M - 1);
+#pragma unroll
+    for (int t = 0; t < KS; ++t) fa[i][t] = *(const bf16x8_t*)(h + (int64_t)r * ldh + t * 32 + g * 8);
+  }
+  const int ntile = (N + 63) / 64;
+  auto load_tile = [&](int nt, u32x4_t (&v)[LPT]) {
+#pragma unroll
+    for (int q = 0; q < LPT; ++q) {
+      const int c = tid + q * 256;                 // 16-byte chunk of the tile
+      const int r = c / CPR, ch = c % CPR;
+      const int n = min(nt * 64 + r, N - 1);
+      v[q] = *(const u32x4_t*)(w + (int64_t)n * K + ch * 8);
+    }
+  };
+  auto store_tile = [&](int buf, const u32x4_t (&v)[LPT]) {
+#pragma unroll
+    for (int q = 0; q < LPT; ++q) {
+      const int c = tid + q * 256;
+      const int r = c / CPR, ch = c % CPR;
+      *(u32x4_t*)(sw[buf] + r * (K * 2) + ((ch ^ (r % CPR)) << 4)) = v[q];
+    }
+  };
+  const float L2E = 1.4426950408889634f;
+  float m[2][4], s[2][4];
+  int bi[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      m[i][r] = -INFINITY;
+      s[i][r] = 0.f;
+      bi[i][r] = 0;
+    }
+  u32x4_t stage[LPT];
+  load_tile(0, stage);
+  store_tile(0, stage);
+  __syncthreads();
+  for (int nt = 0; nt < ntile; ++nt) {
+    const int buf = nt & 1;
+    if (nt + 1 < ntile) load_tile(nt + 1, stage);   // lands while this tile computes
+    f32x4_t acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = j * 16 + frow, ch = t * 4 + g;
+        const bf16x8_t fb = *(const bf16x8_t*)(sw[buf] + r * (K * 2) + ((ch ^ (r % CPR)) << 4));
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][t], fb, acc[i][j], 0, 0, 0);
+      }
+    }
+    // fold the tile: lane column n = nt*64 + 16j + frow, rows 16i + 4g + r (increasing n per lane)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = nt * 64 + j * 16 + frow;
+      const bool ok = n < C;
+      const float b = (ok && bias) ? bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = ok ? (acc[i][j][r] + b) * L2E : -INFINITY;
+          if (v > m[i][r]) {
+            s[i][r] = (m[i][r] == -INFINITY ? 0.f : s[i][r] * __builtin_amdgcn_exp2f(m[i][r] - v)) + 1.f;
+            m[i][r] = v;
+            bi[i][r] = n;
+          } else if (ok) {
+            s[i][r] += __builtin_amdgcn_exp2f(v - m[i][r]);
+          }
+        }
+    }
+    if (nt + 1 < ntile) {
+      __syncthreads();                 // every wave is done reading buf ^ 1 (tile nt - 1)
+      store_tile(buf ^ 1, stage);
+      __syncthreads();
+    }
+  }
+  // reduce the 16 lanes (frow) that share each row
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float bm = m[i][r], bs = s[i][r];
+      int bx = bi[i][r];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float om = __shfl_xor(bm, o, 64), os = __shfl_xor(bs, o, 64);
+        const int ox = __shfl_xor(bx, o, 64);
+        const float mm = fmaxf(bm, om);
+        const float ns = (bm == -INFINITY ? 0.f : bs * __builtin_amdgcn_exp2f(bm - mm)) +
+                         (om == -INFINITY ? 0.f : os * __builtin_amdgcn_exp2f(om - mm));
+        if (om > bm || (om == bm && ox < bx)) bx = ox;
+        bm = mm;
+        bs = ns;
+      }
+      const int row = row0 + i * 16 + 4 * g + r;
+      if (frow == 0 && row < M) {
+        idx_out[row] = bx;
+        conf_out[row] = bs > 0.f ? 1.f / bs : 0.f;
+      }
+    }
+}
+
+hipError_t cls_argmax(const uint16_t* h, int64_t ldh, const uint16_t* w, const float* bias, int M, int N, int K, int C,
+                      int* idx_out, float* conf_out, hipStream_t stream) {
+  if (M <= 0) return hipSuccess;
+  const dim3 grid((M + 127) / 128);
+  switch (K) {
+    case 64: hipLaunchKernelGGL(cls_argmax_kernel<64>, grid, dim3(256), 0, stream, h, ldh, w, bias, M, N, C, idx_out, conf_out); break;
+    case 128: hipLaunchKernelGGL(cls_argmax_kernel<128>, grid, dim3(256), 0, stream, h, ldh, w, bias, M, N, C, idx_out, conf_out); break;
+    case 256: hipLaunchKernelGGL(cls_argmax_kernel<256>, grid, dim3(256), 0, stream, h, ldh, w, bias, M, N, C, idx_out, conf_out); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t ctc_collapse(const int* idx, const float* conf, int B, int T, int blank, const int* tlen, int* out_ids,
+                        int* out_len, float* out_conf, hipStream_t stream) {
+  hipLaunchKernelGGL(ctc_collapse_kernel, dim3((B + 63) / 64), dim3(64), 0, stream, idx, conf, B, T, blank, tlen,
+                     out_ids, out_len, out_conf);
+  return hipGetLastError();
+}
+
 hipError_t ctc_greedy(const float* probs, int B, int T, int C, int blank, int from_logits, const int* tlen,
                       int* tmp_idx, float* tmp_conf, int* out_ids, int* out_len, float* out_conf, hipStream_t stream) {
   const int rows = B * T;

@@ -32,6 +32,7 @@ from torch import nn
 from .. import ops
 from ..ops import cnn
 from .clip import _Block, run_blocks
+from ..ops import vision
 from .layers import ConvBN, DWConvBN, Linear
 
 
@@ -243,6 +244,32 @@ class SVTRRecognizer(nn.Module):
     def forward(self, x: torch.Tensor, valid_w: Optional[Sequence[int]] = None) -> torch.Tensor:
         """x NHWC8 [B, 48, W, 8] -> class logits fp32 [B, T, Cpad] (T = W / time_stride; columns
         >= num_classes carry -1e9).  ``valid_w`` masks width padding in the attention."""
+        hn, B, T = self.features(x, valid_w)
+        logits = ops.linear(hn, self.cls.w, self.cls.b, out_dtype=torch.float32)
+        return logits.view(B, T, -1)
+
+    @torch.no_grad()
+    def ctc_decode(self, x: torch.Tensor, valid_w: Optional[Sequence[int]] = None, blank: int = 0):
+        """x -> greedy CTC (ids per crop, mean confidence per crop).  On the GPU the classifier is
+        fused with the per-step arg-max (csrc/postproc.hip cls_argmax_kernel): the [B, T, classes]
+        logits (~650 MB fp32 for a PP-OCR batch) are never written."""
+        hn, B, T = self.features(x, valid_w)
+        return self.ctc_from_features(hn, B, T, valid_w, blank)
+
+    @torch.no_grad()
+    def ctc_from_features(self, hn: torch.Tensor, B: int, T: int, valid_w: Optional[Sequence[int]] = None,
+                          blank: int = 0):
+        """classifier + greedy CTC of :meth:`features` output (fused on the GPU, see ctc_decode)."""
+        ts = self.time_stride
+        tlen = None if valid_w is None else [-(-int(w) // ts) for w in valid_w]
+        if hn.is_cuda and self.cls.cin_p in (64, 128, 256) and hn.shape[1] == self.cls.cin_p:
+            return vision.cls_ctc_greedy(hn, self.cls.w, self.cls.b, self.cfg.num_classes, B, T, blank=blank,
+                                         tlen=tlen)
+        logits = ops.linear(hn, self.cls.w, self.cls.b, out_dtype=torch.float32).view(B, T, -1)
+        return vision.ctc_greedy(logits, blank=blank, from_logits=True, tlen=tlen)
+
+    def features(self, x: torch.Tensor, valid_w: Optional[Sequence[int]] = None):
+        """x -> final-LayerNorm sequence features [B*T, dim] bf16 (the classifier input), B, T."""
         h = self.stem(x)
         for b in self.blocks:
             h = b(h)
@@ -258,9 +285,7 @@ class SVTRRecognizer(nn.Module):
             kv = torch.tensor([max(1, min(T, -(-int(w) // ts))) for w in valid_w], dtype=torch.int32,
                               device=x.device)
         run_blocks(seq, self.tblocks, B, T, self.cfg.heads, "gelu", 1e-6, kv_len=kv)
-        hn = ops.layer_norm(seq, self.ln_w, self.ln_b, 1e-6)
-        logits = ops.linear(hn, self.cls.w, self.cls.b, out_dtype=torch.float32)
-        return logits.view(B, T, -1)
+        return ops.layer_norm(seq, self.ln_w, self.ln_b, 1e-6), B, T
 
 
 # ============================================================================= synthetic pack

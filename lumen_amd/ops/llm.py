@@ -83,12 +83,25 @@ _DECODE_WAVES = 4             # waves (= 64-token blocks) per paged-decode workg
 _DECODE_MAX_SPLITS = 32        # the in-launch split combine merges at most 32 splits per kv head
 
 
+_DECODE_FEW = 4                # <= this many sequences: one-wave workgroups, one block per split
+
+
 def decode_splits(B: int, Hkv: int, max_blocks: int, target_wg: Optional[int] = None) -> tuple[int, int]:
-    """(nsplit, blocks_per_split) of the paged decode kernel: a split is one workgroup of 4 waves,
-    one 64-token block per wave, so a context of <= 256 tokens is one workgroup per kv head with
-    no cross-workgroup combine; longer contexts use up to 32 splits merged in-launch, and past
-    8k tokens the waves loop over several blocks."""
+    """(nsplit, min blocks_per_split) of the paged decode kernel.
+
+    A split is one workgroup of 4 waves, one 64-token block per wave.  Batched decode (B > 4):
+    splits of >= 4 blocks, so a context of <= 256 tokens is one workgroup per kv head with no
+    cross-workgroup combine; longer contexts use up to 32 splits merged in-launch, and past 8k
+    tokens the waves loop over several blocks.  A few sequences (B <= 4): the same launch with
+    no minimum, so each sequence's blocks spread over all launched splits.  The kernel sizes the
+    splits from each sequence's ctx_len on the device (blocks per split = max(min,
+    ceil(blocks / nsplit)))."""
     nsplit = max(1, min(-(-max_blocks // _DECODE_WAVES), _DECODE_MAX_SPLITS))
+    if B <= _DECODE_FEW:
+        # one block per wave, but the context spread over every launched split: 650 tokens on an
+        # 8-split launch run as 6 splits x 2 blocks, 9.8 us vs 10.7 us as 3 x 4 and 20.4 us as 32
+        # one-wave splits, whose single-wave combine is latency-serial (r3_decode_attn_splits_v1.txt)
+        return nsplit, 1
     bps = -(-max_blocks // nsplit)
     return -(-max_blocks // bps), bps
 
@@ -96,13 +109,16 @@ def decode_splits(B: int, Hkv: int, max_blocks: int, target_wg: Optional[int] = 
 def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_table: torch.Tensor,
                  ctx_len: torch.Tensor, H: int, Hkv: int, scale: Optional[float] = None,
                  out: Optional[torch.Tensor] = None, workspace: Optional[dict] = None,
-                 rope: Optional[tuple] = None) -> torch.Tensor:
+                 rope: Optional[tuple] = None, prefetch: Sequence[torch.Tensor] = (),
+                 splits: Optional[tuple] = None) -> torch.Tensor:
     """Single-token attention of q [B, H*D] (rows may be views) over each sequence's cached
     context (ctx_len tokens, including the current token).
 
     ``rope = (pos [B] int32, cos_sin, slots [B] int64)``: q is the *unrotated* packed QKV row
     and the kernel applies RoPE to q in registers and writes the current token's rotated k and
     its v to ``slots`` itself (what :func:`rope_kv` would do; one launch per layer fewer).
+    ``prefetch``: up to two tensors (the next GEMMs' weights) that extra workgroups of the same
+    launch read once into the Infinity Cache while the attention occupies only a few CUs.
     Head dims 64 / 128 on the GPU."""
     B = q.shape[0]
     D = k_cache.shape[3]
@@ -116,7 +132,7 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
         out = torch.empty((B, H * D), device=q.device, dtype=q.dtype)
     if q.is_cuda:
         mb = block_table.shape[1]
-        nsplit, bps = decode_splits(B, Hkv, mb)
+        nsplit, bps = splits if splits is not None else decode_splits(B, Hkv, mb)   # splits: benchmarks
         po = pm = None
         if nsplit > 1:
             need = B * H * nsplit
@@ -131,8 +147,9 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
                 ws["ml"] = pm
         rp = (None, None, None) if rope is None else \
             (rope[0].to(torch.int32).contiguous(), rope[1], rope[2].to(torch.long).contiguous())
+        pf = list(prefetch)[:2] + [None, None]
         hip_ops().paged_decode(q, k_cache, v_cache, block_table, ctx_len, out, int(H), int(Hkv), float(scale),
-                               int(nsplit), int(bps), po, pm, *rp)
+                               int(nsplit), int(bps), po, pm, *rp, pf[0], pf[1])
         return out
     G = H // Hkv
     for b in range(B):

@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from .._native import hip_ops, load_host
+from ..runtime.metrics import stage
 
 # ArcFace 5-point template for 112x112 crops (insightface canonical coordinates)
 ARCFACE_DST = np.array([[38.2946, 51.6963], [73.5318, 51.5014], [56.0252, 71.7366], [41.5493, 92.3655],
@@ -277,6 +278,26 @@ def ctc_greedy(probs: torch.Tensor, blank: int = 0, from_logits: bool = False,
     return seqs, confs
 
 
+def cls_ctc_greedy(h: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], num_classes: int, B: int, T: int,
+                   blank: int = 0, tlen: Optional[Sequence[int]] = None):
+    """Classifier + greedy CTC with the logits never stored (GPU): h [B*T, K] bf16 features,
+    w [N, K] bf16 classifier, bias f32 [N]; classes >= num_classes are ignored.  Same result as
+    ``ctc_greedy(h @ w.T + bias, from_logits=True)``."""
+    dev = h.device
+    M = B * T
+    i1 = torch.empty(M, dtype=torch.int32, device=dev)
+    c1 = torch.empty(M, dtype=torch.float32, device=dev)
+    ids = torch.empty((B, T), dtype=torch.int32, device=dev)
+    ln = torch.empty((B,), dtype=torch.int32, device=dev)
+    cf = torch.empty((B,), dtype=torch.float32, device=dev)
+    tl = torch.tensor(list(tlen), dtype=torch.int32).to(dev) if tlen is not None else None
+    b = bias.float().contiguous() if bias is not None else None
+    hip_ops().cls_ctc(h.contiguous(), w.contiguous(), b, int(num_classes), int(B), int(T), int(blank), tl, i1, c1,
+                      ids, ln, cf)
+    ids, ln, cf = ids.cpu(), ln.cpu(), cf.cpu()
+    return [ids[k, : int(ln[k])].tolist() for k in range(B)], cf.tolist()
+
+
 # --------------------------------------------------------------------------- DB post-processing (GPU + host)
 def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw: int, max_candidates: int = 1000,
                  min_size: int = 3, max_boxes: int = 1000, cap: Optional[int] = None) -> list:
@@ -301,20 +322,24 @@ def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw
     lab = torch.empty(5 * n * rh * rw, dtype=torch.int32, device=dev)     # labels + per-root bbox
     pts = torch.empty((cap, 3), dtype=torch.int32, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-    hip_ops().db_components(prob, thr, lab, pts, cnt, int(min_size))
-    K = int(cnt.item())
+    with stage("db_gpu"):
+        hip_ops().db_components(prob, thr, lab, pts, cnt, int(min_size))
+        K = int(cnt.item())
     if K > cap:                                      # pathological maps: retry with room for every pixel
         return db_boxes_gpu(prob, params, hw, rh, rw, max_candidates, min_size, max_boxes, cap=n * rh * rw)
-    dp = pts[:K]
-    if K > 1:                                        # group by component on the device (radix sort)
-        dp = dp.index_select(0, torch.sort(dp[:, 0], stable=True).indices)
-    P = dp.cpu().numpy()
+    with stage("db_points"):
+        dp = pts[:K]
+        if K > 1:                                    # group by component on the device (radix sort)
+            dp = dp.index_select(0, torch.sort(dp[:, 0], stable=True).indices)
+        P = dp.cpu().numpy()
     HW = rh * rw
     ip = ctypes.POINTER(ctypes.c_int)
     fp = ctypes.POINTER(ctypes.c_float)
     per_img = []
     all_q, all_r, all_i = [], [], []
     starts = np.searchsorted(P[:, 0], np.arange(n + 1) * HW) if K else np.zeros(n + 1, np.int64)
+    t_cand = stage("db_cand")
+    t_cand.__enter__()
     for j in range(n):
         seg = np.ascontiguousarray(P[starts[j]:starts[j + 1]])
         mx = max_candidates
@@ -328,12 +353,15 @@ def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw
         all_r.append(r[:m])
         all_i.append(np.full(m, j, np.int32))
         per_img.append(m)
+    t_cand.__exit__(None, None, None)
     Q = np.concatenate(all_q) if all_q else np.zeros((0, 8), np.float32)
     scores = np.zeros((len(Q),), np.float32)
     if len(Q):
-        sc = torch.empty(3 * len(Q), dtype=torch.float32, device=dev)
-        hip_ops().db_quad_score(prob, torch.from_numpy(Q).to(dev), torch.from_numpy(np.concatenate(all_i)).to(dev), sc)
-        scores = sc[:len(Q)].cpu().numpy()
+        with stage("db_score"):
+            sc = torch.empty(3 * len(Q), dtype=torch.float32, device=dev)
+            hip_ops().db_quad_score(prob, torch.from_numpy(Q).to(dev), torch.from_numpy(np.concatenate(all_i)).to(dev),
+                                    sc)
+            scores = sc[:len(Q)].cpu().numpy()
     out, o = [], 0
     for j in range(n):
         m = per_img[j]

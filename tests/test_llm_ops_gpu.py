@@ -57,7 +57,7 @@ def test_rope_kv(H, Hkv, D):
 
 
 @pytest.mark.parametrize("H,Hkv,D", [(14, 2, 64), (32, 8, 128), (32, 32, 128), (16, 1, 64), (4, 2, 32)])
-@pytest.mark.parametrize("lens", [[1, 64, 65], [700, 3, 2048 + 17], [5000]])
+@pytest.mark.parametrize("lens", [[1, 64, 65], [700, 3, 2048 + 17], [5000], [70, 700, 3, 1, 2048 + 17, 64]])
 def test_paged_decode(H, Hkv, D, lens):
     g = torch.Generator().manual_seed(H * D + len(lens))
     B = len(lens)
@@ -79,6 +79,9 @@ def test_paged_decode(H, Hkv, D, lens):
     # repeat launches and a graph replay give the same bits
     for _ in range(3):
         assert torch.equal(llm.paged_decode(*args), got)
+    # weight prefetch workgroups in the same launch (read-only side stream of two tensors) change nothing
+    pf = (torch.randn(3 << 20, device=DEV).bfloat16(), torch.empty(12345, device=DEV, dtype=torch.uint8))
+    assert torch.equal(llm.paged_decode(*args, prefetch=pf), got)
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):

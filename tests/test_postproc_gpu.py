@@ -119,8 +119,8 @@ def test_db_boxes_gpu_matches_host(dtype):
 
 def _cc_reference(binmaps, min_size):
     """CPU emulation of db_components: 8-connected components (scipy), root = the raster-first
-    (smallest global) pixel index, boundary pixels (a 4-neighbour outside or the map border) of
-    components whose pixel-centre bbox spans >= min_size on some axis -> set of (root, x, y)."""
+    (smallest global) pixel index; for components whose pixel-centre bbox spans >= min_size on
+    some axis, the leftmost and rightmost pixel of each of their rows -> set of (root, x, y)."""
     from scipy import ndimage
 
     out = set()
@@ -150,16 +150,21 @@ def _cc_reference(binmaps, min_size):
         keep = ((x1 - x0) >= min_size) | ((y1 - y0) >= min_size)
         by, bx = np.nonzero(bnd)
         bid = lab[by, bx]
+        ext = {}
         for y, x, c in zip(by, bx, bid):
             if keep[c]:
-                out.add((int(root[c]), int(x), int(y)))
+                lo, hi = ext.get((c, y), (x, x))
+                ext[(c, y)] = (min(lo, x), max(hi, x))
+        for (c, y), (lo, hi) in ext.items():
+            out.add((int(root[c]), int(lo), int(y)))
+            out.add((int(root[c]), int(hi), int(y)))
     return out
 
 
 @pytest.mark.parametrize("kind", ["text", "noise"])
 def test_db_components_exact_vs_cpu(kind):
-    """Tile-local LDS labelling + cross-tile border merge + flatten/bbox + boundary (db_post.hip)
-    vs an exact CPU emulation: the same (root, x, y) boundary set, on text-like rectangle maps
+    """Tile-local LDS labelling + cross-tile border merge + flatten/bbox + per-row extremes
+    (db_post.hip) vs an exact CPU emulation: the same (root, x, y) set, on text-like rectangle maps
     (components crossing 32-px tile borders, diagonal-only contacts) and on noise maps."""
     rng = np.random.default_rng(7)
     n, H, W = 3, 150, 203                                    # partial tiles on both axes
@@ -188,3 +193,74 @@ def test_db_components_exact_vs_cpu(kind):
         assert len(got) == K
         ref = _cc_reference(maps > thr.numpy()[:, None, None], min_size)
         assert got == ref
+
+
+@pytest.mark.parametrize("K,N,C", [(128, 6640, 6625), (64, 112, 97), (256, 1024, 1000)])
+def test_cls_ctc_fused_matches_logits_path(K, N, C):
+    """Classifier fused with the CTC arg-max (no stored logits) vs the fp32 logits + host CTC
+    reference: same ids per crop (random features, padded classes carry -1e9 bias), close mean
+    confidences, width-padded time steps honoured."""
+    from lumen_amd.ops import vision
+
+    g = torch.Generator().manual_seed(K + N)
+    B, T = 37, 41
+    h = torch.randn(B * T, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * 0.3).bfloat16()
+    b = torch.randn(N, generator=g) * 0.5
+    b[C:] = -1e9
+    # a few repeated / blank steps so the collapse is exercised
+    h[5:9] = h[4]
+    tlen = [int(t) for t in torch.randint(1, T + 1, (B,), generator=g)]
+    logits = (h.float() @ w.float().t() + b).view(B, T, N)
+    ref_ids, ref_conf = vision.ctc_greedy(logits, blank=0, from_logits=True, tlen=tlen)
+    ids, conf = vision.cls_ctc_greedy(h.to(DEV), w.to(DEV), b.to(DEV), C, B, T, blank=0, tlen=tlen)
+    same = sum(a == r for a, r in zip(ids, ref_ids))
+    assert same >= B - 1, (same, B)     # a near-tie between two classes may flip one crop
+    ok = [k for k in range(B) if ids[k] == ref_ids[k]]
+    assert np.allclose(np.asarray(conf)[ok], np.asarray(ref_conf)[ok], atol=2e-3)
+
+
+def test_db_quad_score_spans_match_pixel_scan():
+    """Box score by row spans over fp64 row prefix sums (O(rows) per quad) vs a per-pixel scan of
+    each quad's bounding box with the same centre-inside test: rotated, huge (full-map), tiny,
+    partly outside and degenerate quads."""
+    g = np.random.default_rng(3)
+    n, H, W = 3, 200, 300
+    prob = g.random((n, H, W), dtype=np.float32)
+    quads = []
+    for _ in range(60):
+        cx, cy = g.uniform(-20, W + 20), g.uniform(-20, H + 20)
+        w, h, a = g.uniform(1, 400), g.uniform(1, 120), g.uniform(0, np.pi)
+        c, s = np.cos(a), np.sin(a)
+        pts = [(cx + c * dx - s * dy, cy + s * dx + c * dy) for dx, dy in
+               ((-w / 2, -h / 2), (w / 2, -h / 2), (w / 2, h / 2), (-w / 2, h / 2))]
+        quads.append(np.array(pts, np.float32).reshape(8))
+    quads.append(np.array([0, 0, W - 1, 0, W - 1, H - 1, 0, H - 1], np.float32))      # full map
+    quads.append(np.array([5, 5, 50, 50, 50, 50, 5, 5], np.float32))                  # degenerate (a line)
+    Q = np.stack(quads)
+    img = np.arange(len(Q), dtype=np.int32) % n
+
+    def ref(q, j):
+        px, py = q[0::2], q[1::2]
+        x0, x1 = max(0, int(np.floor(px.min()))), min(W - 1, int(np.ceil(px.max())))
+        y0, y1 = max(0, int(np.floor(py.min()))), min(H - 1, int(np.ceil(py.max())))
+        if x1 < x0 or y1 < y0:
+            return 0.0
+        ys, xs = np.mgrid[y0:y1 + 1, x0:x1 + 1].astype(np.float32)
+        pos = np.zeros_like(xs, bool)
+        neg = np.zeros_like(xs, bool)
+        for k in range(4):
+            k1 = (k + 1) % 4
+            cr = (px[k1] - px[k]) * (ys - py[k]) - (py[k1] - py[k]) * (xs - px[k])
+            pos |= cr > 0
+            neg |= cr < 0
+        m = ~(pos & neg)
+        return float(prob[j, y0:y1 + 1, x0:x1 + 1][m].astype(np.float64).mean()) if m.any() else 0.0
+
+    sc = torch.empty(3 * len(Q), dtype=torch.float32, device=DEV)
+    from lumen_amd._native import hip_ops
+    hip_ops().db_quad_score(torch.from_numpy(prob).to(DEV), torch.from_numpy(Q).to(DEV), torch.from_numpy(img).to(DEV),
+                            sc)
+    got = sc[:len(Q)].cpu().numpy()
+    want = np.array([ref(Q[i], img[i]) for i in range(len(Q))])
+    np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-5)

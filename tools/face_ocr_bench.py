@@ -171,11 +171,12 @@ def bench_ocr(args):
 
     for _ in range(args.warmup):
         step()
+    stages.clear()                      # stage times of the timed steps only
     t0 = time.perf_counter()
     for _ in range(args.iters):
         step()
     dt = (time.perf_counter() - t0) / args.iters
-    n_steps = args.iters + args.warmup
+    n_steps = args.iters
     return {"metric": "ocr images/s", "value": args.batch / dt, "unit": "img/s", "ms_per_batch": dt * 1000,
             "host_stage_ms_per_batch": {k: round(v / n_steps, 2) for k, v in stages.items()},
             "batch": args.batch, "crops_per_image": args.crops, "crops_per_s": args.batch * args.crops / dt,

@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, default=577)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--tiles", default="-1", help="comma list of forced tile codes (ops.linear tile=)")
     a = ap.parse_args()
     load_hip(required=True)
     dev = "cuda"
@@ -50,7 +51,11 @@ def main():
         b = torch.randn(N, device=dev).bfloat16()
         r = torch.randn(a.M, N, device=dev).bfloat16() if resid else None
         out = torch.empty(a.M, N, device=dev, dtype=torch.bfloat16)
-        f = lambda: ops.linear(x, w, b, act=act, residual=r, out=out)  # noqa: E731
+        for t in [int(v) for v in a.tiles.split(",")][1:]:
+            g = lambda: ops.linear(x, w, b, act=act, residual=r, out=out, tile=t)  # noqa: E731
+            res[f"{name}_t{t}_us"] = round(med_us(g), 2)
+        t0 = int(a.tiles.split(",")[0])
+        f = lambda: ops.linear(x, w, b, act=act, residual=r, out=out, tile=t0)  # noqa: E731
 
         def lib():
             y = torch.nn.functional.linear(x, w, b)

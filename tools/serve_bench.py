@@ -126,6 +126,7 @@ def main():
     lock = threading.Lock()
     phase = {"timed": False, "stop": False}
     counts = {"n": 0}
+    smeta: dict = {}
 
     def client(ci: int):
         ch = grpc.insecure_channel(f"127.0.0.1:{port}", options=[("grpc.max_send_message_length", 64 << 20),
@@ -147,6 +148,12 @@ def main():
                     elif phase["timed"]:
                         lat.append(dt)
                         counts["n"] += 1
+                        for key, v in rs[0].meta.items():      # server-side stage times of this request
+                            if key.startswith("t_") or key in ("duration_ms", "batch_size"):
+                                try:
+                                    smeta.setdefault(key, []).append(float(v))
+                                except ValueError:
+                                    pass
         finally:
             ch.close()
 
@@ -176,6 +183,7 @@ def main():
            "image": f"{args.image_kind} JPEG {args.image_side * 4 // 3}x{args.image_side}, "
                     f"{int(np.mean([len(b) for b in imgs]) / 1024)} KiB mean",
            "load_s": round(load_s, 1),
+           "server_stage_ms_p50": {k: round(float(np.median(v)), 2) for k, v in sorted(smeta.items())},
            "data": "synthetic (random-init weights of the named architecture, generated JPEGs)",
            "path": "gRPC Infer stream -> hub router -> service -> dynamic batcher -> "
                    + ("GPU worker pool (shm rings)" if args.dp > 1 else "in-process backend")}
