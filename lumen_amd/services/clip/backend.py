@@ -30,7 +30,7 @@ import torch
 from ...models.clip import CLIPModel
 from ...runtime.batcher import DynamicBatcher
 from ...runtime.metrics import stage
-from ...utils.image import decode_many
+from ...utils.image import decode_many, decode_rgb
 from ...resources.exceptions import ResourceError
 from .resources import ModelResources, load_weights
 
@@ -155,8 +155,9 @@ class MI355XClipBackend:
             self.model = m.to(self.device)
             self._logit_scale = self.model.logit_scale
         self._load_tokenizer()
-        # with DP workers: 2 dispatchers per GPU, each batch goes whole to the least-loaded worker
-        conc = 2 * self.dp_size if self._pool is not None else 1
+        # with DP workers: 2 dispatchers per GPU, each batch goes whole to the least-loaded worker; one
+        # GPU in-process: 2 dispatchers, so one batch's stacking / H2D / D2H overlaps the other's tower
+        conc = 2 * self.dp_size if self._pool is not None else (2 if self.device.type == "cuda" else 1)
         self._img_batcher = DynamicBatcher(self._encode_images, self.max_batch, self.max_wait_ms, "clip-image", conc)
         self._txt_batcher = DynamicBatcher(self._encode_texts, self.max_batch, self.max_wait_ms, "clip-text", conc)
         self.load_time = time.time() - t0
@@ -210,8 +211,12 @@ class MI355XClipBackend:
         if self._pool is not None:
             with stage("dp_forward"):
                 return self._pool.submit("image", list(payloads)).result()
-        with stage("decode"):
-            imgs = decode_many(payloads)
+        raw = [i for i, p in enumerate(payloads) if not isinstance(p, np.ndarray)]
+        imgs = list(payloads)
+        if raw:                                       # batch API: decode here (single requests arrive decoded)
+            with stage("decode"):
+                for i, a in zip(raw, decode_many([payloads[i] for i in raw])):
+                    imgs[i] = a
         with torch.no_grad(), stage("forward"):      # H2D + resize/normalise + tower + D2H
             tens = [torch.from_numpy(i) for i in imgs]
             emb = self.model.encode_image_uint8(tens).float().cpu().numpy()
@@ -222,7 +227,16 @@ class MI355XClipBackend:
         self._ensure()
         if not image_bytes:
             raise InvalidInputError("empty image payload")
-        return self._img_batcher(image_bytes)
+        if self._pool is not None:                    # DP workers decode in their own processes
+            return self._img_batcher(image_bytes)
+        # decoded on the caller's (gRPC) thread: Pillow releases the GIL, so concurrent requests decode
+        # in parallel and the batch's critical path is only the GPU work; a bad payload fails alone
+        with stage("decode"):
+            try:
+                img = decode_rgb(image_bytes)
+            except ValueError as e:
+                raise InvalidInputError(str(e)) from e
+        return self._img_batcher(img)
 
     def image_batch_to_vectors(self, images: Sequence[bytes]) -> np.ndarray:
         self._ensure()

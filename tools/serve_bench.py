@@ -78,6 +78,54 @@ def _images(n: int, side: int, kind: str, seed: int = 0) -> list[bytes]:
     return out
 
 
+def _client_proc(plan_q, res_q, task: str, imgs: list, nthreads: int, pid: int) -> None:
+    """One client process: ``nthreads`` threads, each with its own channel, sending one-image
+    ``Infer`` streams back to back; requests that start and finish inside [t_on, t_off] count."""
+    import grpc
+
+    from lumen_amd.proto import ml_service as pb
+
+    port, t_on, t_off = plan_q.get()
+    lock = threading.Lock()
+    acc = {"lat": [], "errors": 0, "n": 0, "meta": {}}
+
+    def run(ci: int):
+        ch = grpc.insecure_channel(f"127.0.0.1:{port}", options=[("grpc.max_send_message_length", 64 << 20),
+                                                                ("grpc.max_receive_message_length", 64 << 20)])
+        stub = pb.InferenceStub(ch)
+        k = ci
+        try:
+            while time.time() < t_off:
+                img = imgs[k % len(imgs)]
+                k += 1
+                t_w, t = time.time(), time.perf_counter()
+                rs = list(stub.Infer(iter([pb.InferRequest(correlation_id=f"{pid}-{ci}-{k}", task=task, payload=img,
+                                                           payload_mime="image/jpeg")]), timeout=300))
+                dt = time.perf_counter() - t
+                ok = len(rs) == 1 and not rs[0].HasField("error")
+                with lock:
+                    if not ok:
+                        acc["errors"] += 1
+                    elif t_w >= t_on and t_w + dt <= t_off:
+                        acc["lat"].append(dt)
+                        acc["n"] += 1
+                        for key, v in rs[0].meta.items():      # server-side stage times of this request
+                            if key.startswith("t_") or key in ("duration_ms", "batch_size"):
+                                try:
+                                    acc["meta"].setdefault(key, []).append(float(v))
+                                except ValueError:
+                                    pass
+        finally:
+            ch.close()
+
+    ths = [threading.Thread(target=run, args=(i,), daemon=True) for i in range(nthreads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    res_q.put(acc)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--service", choices=sorted(TASKS), default="clip")
@@ -93,6 +141,7 @@ def main():
     ap.add_argument("--image-side", type=int, default=384, help="JPEG height (width = 4/3 height)")
     ap.add_argument("--image-kind", choices=["photo", "noise"], default="photo")
     ap.add_argument("--server-threads", type=int, default=None)
+    ap.add_argument("--client-procs", type=int, default=4, help="client processes (threads spread over them)")
     args = ap.parse_args()
 
     os.environ["LUMEN_SYNTHETIC"] = "1"
@@ -109,6 +158,21 @@ def main():
     from lumen_amd.proto import ml_service as pb
     from lumen_amd.resources.downloader import Downloader
 
+    # client processes first, before this process touches the GPU (they only speak gRPC): remote-like
+    # clients that do not share the server's GIL
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    nproc = max(1, min(args.client_procs, args.clients))
+    plan_q, res_q = ctx.Queue(), ctx.Queue()
+    task = TASKS[args.service]
+    imgs = _images(16, args.image_side, args.image_kind)
+    procs = [ctx.Process(target=_client_proc, args=(plan_q, res_q, task, imgs, args.clients * (i + 1) // nproc -
+                                                    args.clients * i // nproc, i), daemon=True)
+             for i in range(nproc)]
+    for pr in procs:
+        pr.start()
+
     cache = tempfile.mkdtemp(prefix="lumen_serve_bench_")
     cfg = _config(args.service, args.model, args.device, args.batch, cache, args.runtime)
     t0 = time.perf_counter()
@@ -119,65 +183,28 @@ def main():
     server, port = build_server(HubRouter(app.services), "127.0.0.1", 0, max_workers=threads)
     server.start()
     load_s = time.perf_counter() - t0
-    task = TASKS[args.service]
-    imgs = _images(16, args.image_side, args.image_kind)
-    lat: list[float] = []
-    errors = [0]
-    lock = threading.Lock()
-    phase = {"timed": False, "stop": False}
-    counts = {"n": 0}
-    smeta: dict = {}
-
-    def client(ci: int):
-        ch = grpc.insecure_channel(f"127.0.0.1:{port}", options=[("grpc.max_send_message_length", 64 << 20),
-                                                                ("grpc.max_receive_message_length", 64 << 20)])
-        stub = pb.InferenceStub(ch)
-        k = ci
-        try:
-            while not phase["stop"]:
-                img = imgs[k % len(imgs)]
-                k += 1
-                t = time.perf_counter()
-                rs = list(stub.Infer(iter([pb.InferRequest(correlation_id=f"{ci}-{k}", task=task, payload=img,
-                                                           payload_mime="image/jpeg")]), timeout=300))
-                dt = time.perf_counter() - t
-                ok = len(rs) == 1 and not rs[0].HasField("error")
-                with lock:
-                    if not ok:
-                        errors[0] += 1
-                    elif phase["timed"]:
-                        lat.append(dt)
-                        counts["n"] += 1
-                        for key, v in rs[0].meta.items():      # server-side stage times of this request
-                            if key.startswith("t_") or key in ("duration_ms", "batch_size"):
-                                try:
-                                    smeta.setdefault(key, []).append(float(v))
-                                except ValueError:
-                                    pass
-        finally:
-            ch.close()
-
-    ths = [threading.Thread(target=client, args=(i,), daemon=True) for i in range(args.clients)]
-    for t in ths:
-        t.start()
-    time.sleep(args.warmup)
-    with lock:
-        phase["timed"] = True
-        t_start = time.perf_counter()
-    time.sleep(args.seconds)
-    with lock:
-        phase["timed"] = False
-        n = counts["n"]
-        el = time.perf_counter() - t_start
-    phase["stop"] = True
-    for t in ths:
-        t.join(timeout=120)
+    t_on = time.time() + args.warmup
+    t_off = t_on + args.seconds
+    for _ in procs:
+        plan_q.put((port, t_on, t_off))
+    lat, errors, n, smeta = [], 0, 0, {}
+    for _ in procs:
+        r = res_q.get(timeout=args.warmup + args.seconds + 600)
+        lat += r["lat"]
+        errors += r["errors"]
+        n += r["n"]
+        for k, v in r["meta"].items():
+            smeta.setdefault(k, []).extend(v)
+    for pr in procs:
+        pr.join(timeout=60)
+    el = args.seconds
     server.stop(0)
     app.close()
     la = np.asarray(lat) * 1e3 if lat else np.zeros(1)
     out = {"metric": f"serving {task} images/s", "value": round(n / el, 2), "unit": "images/s",
+           "client_processes": nproc,
            "p50_ms": round(float(np.percentile(la, 50)), 2), "p99_ms": round(float(np.percentile(la, 99)), 2),
-           "mean_ms": round(float(la.mean()), 2), "requests": n, "seconds": round(el, 2), "errors": errors[0],
+           "mean_ms": round(float(la.mean()), 2), "requests": n, "seconds": round(el, 2), "errors": errors,
            "clients": args.clients, "service": args.service, "model": args.model, "device": args.device,
            "dp_workers": args.dp, "batch_cap": args.batch, "max_wait_ms": os.environ.get("LUMEN_MAX_WAIT_MS"),
            "image": f"{args.image_kind} JPEG {args.image_side * 4 // 3}x{args.image_side}, "
