@@ -112,10 +112,12 @@ def setup_mdns(port: int, mdns_cfg) -> tuple:
     return zc, info
 
 
-def build_server(servicer, host: str, port: int, max_workers: int = 16):
-    server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers),
-                         options=[("grpc.max_receive_message_length", 64 * 1024 * 1024),
-                                  ("grpc.max_send_message_length", 64 * 1024 * 1024)])
+def build_server(servicer, host: str, port: int, max_workers: int = 16, reuse_port: bool = False):
+    opts = [("grpc.max_receive_message_length", 64 * 1024 * 1024),
+            ("grpc.max_send_message_length", 64 * 1024 * 1024)]
+    if reuse_port:   # several replica processes accept on one port; the kernel spreads the connections
+        opts.append(("grpc.so_reuseport", 1))
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers), options=opts)
     if isinstance(servicer, HubRouter):
         servicer.attach_to_server(server)
     else:
@@ -126,13 +128,47 @@ def build_server(servicer, host: str, port: int, max_workers: int = 16):
     return server, bound
 
 
+def _replica_main(config_path: str, port: int, mode: str, stop_event, ready_q, idx: int) -> None:
+    """A replica process of :func:`serve` (spawned before any GPU use): same config, same port."""
+    setup_logging(os.environ.get("LUMEN_LOG_LEVEL", "INFO"))
+    serve(config_path, port, mode=mode, stop_event=stop_event, procs=1, replica=idx, ready_q=ready_q)
+
+
+def start_replicas(config_path: str, port: int, n: int, mode: str = "hub", ready_q=None):
+    """Spawn ``n`` replica server processes of ``config_path`` on ``port`` (SO_REUSEPORT).  Python
+    gRPC serving is bound by one interpreter's lock (~0.7k one-image streams/s per process on the
+    CLIP path, r3_serve_clip_256c_dp2_v1.log); replicas multiply that, each with its own models and
+    batchers on the GPU(s).  Must run before this process initialises the GPU.  Returns
+    (processes, stop event)."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    stop = ctx.Event()
+    procs = [ctx.Process(target=_replica_main, args=(config_path, port, mode, stop, ready_q, i + 1), daemon=False)
+             for i in range(n)]
+    for p in procs:
+        p.start()
+    return procs, stop
+
+
 def serve(config_path: str, port_override: Optional[int] = None, mode: str = "hub",
-          stop_event: Optional[threading.Event] = None) -> None:
+          stop_event: Optional[threading.Event] = None, procs: Optional[int] = None, replica: int = 0,
+          ready_q=None) -> None:
+    """Run the server.  ``procs`` > 1 (or LUMEN_HUB_PROCS): this process plus procs - 1 spawned
+    replicas accept on the same port (SO_REUSEPORT; a fixed port is required)."""
     config = load_and_validate_config(config_path)
     if config.deployment.mode != mode:
         log.error("this server runs deployment.mode=%s; config has %s", mode, config.deployment.mode)
         raise SystemExit(1)
-    handle_download_results(Downloader(config).download_all())
+    nproc = int(procs if procs is not None else os.environ.get("LUMEN_HUB_PROCS", "1"))
+    if replica == 0:
+        handle_download_results(Downloader(config).download_all())
+    reps, rep_stop = [], None
+    if nproc > 1 and replica == 0:
+        port0 = port_override or config.server.port
+        if not port0:
+            raise SystemExit("LUMEN_HUB_PROCS > 1 needs a fixed server.port")
+        reps, rep_stop = start_replicas(config_path, port0, nproc - 1, mode)
     app = AppService.from_app_config(config)
     if mode == "single":
         target = config.deployment.service
@@ -142,11 +178,14 @@ def serve(config_path: str, port_override: Optional[int] = None, mode: str = "hu
         servicer = HubRouter(app.services)
     host = config.server.host or "0.0.0.0"
     port = port_override or config.server.port
-    server, bound = build_server(servicer, host, port)
+    multi = nproc > 1 or replica > 0
+    server, bound = build_server(servicer, host, port, reuse_port=multi)
     server.start()
+    if ready_q is not None:
+        ready_q.put((replica, bound))
     from ..runtime.metrics import start_metrics_server
 
-    mport = start_metrics_server()
+    mport = start_metrics_server() if replica == 0 else None
     if mport:
         log.info("Prometheus metrics on :%d/metrics", mport)
     kind = "Hub" if mode == "hub" else "single-service"
@@ -160,7 +199,7 @@ def serve(config_path: str, port_override: Optional[int] = None, mode: str = "hu
             log.warning("  %s: capability probe failed: %s", name, e)
     zc = info = None
     mdns = config.server.mdns
-    if mdns is not None and mdns.enabled:
+    if mdns is not None and mdns.enabled and replica == 0:
         zc, info = setup_mdns(bound, mdns)
     done = stop_event or threading.Event()
 
@@ -171,7 +210,13 @@ def serve(config_path: str, port_override: Optional[int] = None, mode: str = "hu
     if threading.current_thread() is threading.main_thread():
         signal.signal(signal.SIGINT, _stop)
         signal.signal(signal.SIGTERM, _stop)
-    done.wait()
+    while not done.wait(0.5):
+        if replica > 0 and os.getppid() == 1:     # parent gone: do not outlive it
+            break
+    if rep_stop is not None:
+        rep_stop.set()
+        for p in reps:
+            p.join(timeout=30)
     if zc is not None:
         try:
             zc.unregister_service(info)
@@ -187,11 +232,13 @@ def main(argv=None, mode: str = "hub", prog: str = "lumen") -> int:
     ap.add_argument("--config", required=True, help="path to lumen-config.yaml")
     ap.add_argument("--port", type=int, default=None)
     ap.add_argument("--log-level", default="INFO", choices=["DEBUG", "INFO", "WARNING", "ERROR"])
+    ap.add_argument("--procs", type=int, default=None,
+                    help="server replica processes on the one port (default LUMEN_HUB_PROCS or 1)")
     ap.add_argument("--version", action="version", version=f"%(prog)s {__version__}")
     args = ap.parse_args(argv)
     setup_logging(args.log_level)
     try:
-        serve(args.config, args.port, mode=mode)
+        serve(args.config, args.port, mode=mode, procs=args.procs)
     except SystemExit as e:
         return int(e.code or 0)
     return 0

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import json
 import logging
+import os
 import threading
 import time
 from dataclasses import dataclass, field
@@ -177,6 +178,13 @@ class BaseInferenceService(pb.InferenceServicer):
         return handler(payload, mime, meta)
 
     # ---- gRPC methods
+    # > 0: requests of ONE stream are handled concurrently, up to this many in flight (responses in
+    # request order), so a client streaming many images feeds the dynamic batcher whole batches
+    # instead of one request per round trip.  Services whose handlers stream (VLM) keep 0.
+    PIPELINE = 0
+    _pipe_pool = None
+    _pipe_lock = threading.Lock()
+
     def Infer(self, request_iterator: Iterable, context):
         if not self.is_initialized:
             try:
@@ -184,6 +192,9 @@ class BaseInferenceService(pb.InferenceServicer):
             except Exception as e:  # surface as FAILED_PRECONDITION like the reference
                 log.exception("initialize failed")
                 context.abort(grpc.StatusCode.FAILED_PRECONDITION, f"Model not initialized: {e}")
+        if self.PIPELINE > 1:
+            yield from self._infer_pipelined(request_iterator, context)
+            return
         buffers: dict[str, bytearray] = {}
         try:
             for req in request_iterator:
@@ -235,6 +246,101 @@ class BaseInferenceService(pb.InferenceServicer):
                     yield self._error(cid, code, str(e))
         finally:
             buffers.clear()
+
+    def _one(self, req, cid: str, payload: bytes, context) -> list:
+        """One assembled request -> its response messages (pipelined path; non-streaming handlers)."""
+        t0 = time.perf_counter()
+        try:
+            task = req.task or self.DEFAULT_TASK or ""
+            try:
+                handler = self.registry.get_handler(task)
+            except ValueError as e:
+                return [self._error(cid, self.UNKNOWN_TASK_CODE, str(e))]
+            meta = self._request_meta(req, context)
+            maybe_fault("infer")
+            timer = StageTimer(self.SERVICE_NAME)
+            with use_timer(timer):
+                out = handler(payload, req.payload_mime, meta)
+                if hasattr(out, "__next__"):      # a streaming handler: run it out here, in order
+                    chunks = list(out)
+            msgs = []
+            if hasattr(out, "__next__"):
+                for res, mime, extra, final in chunks:
+                    m = dict(extra or {})
+                    if final:
+                        m.update(timer.meta())
+                    m[self.LATENCY_KEY] = str(int((time.perf_counter() - t0) * 1000))
+                    schema = mime.split("schema=")[-1] if (final and "schema=" in mime) else ""
+                    msgs.append(pb.InferResponse(correlation_id=cid, is_final=final, result=res, result_mime=mime,
+                                                 meta=m, result_schema=schema))
+            else:
+                res, mime, extra = out
+                m = dict(extra or {})
+                m.update(timer.meta())
+                m[self.LATENCY_KEY] = str(int((time.perf_counter() - t0) * 1000))
+                schema = mime.split("schema=")[-1] if "schema=" in mime else ""
+                msgs.append(pb.InferResponse(correlation_id=cid, is_final=True, result=res, result_mime=mime, meta=m,
+                                             result_schema=schema))
+            observe_request(self.SERVICE_NAME, task, "ok", time.perf_counter() - t0)
+            return msgs
+        except Exception as e:
+            log.exception("task %s failed", req.task)
+            code = pb.ERROR_CODE_UNAVAILABLE if _unavailable(e) else pb.ERROR_CODE_INTERNAL
+            observe_request(self.SERVICE_NAME, req.task, "error", time.perf_counter() - t0)
+            return [self._error(cid, code, str(e))]
+
+    def _infer_pipelined(self, request_iterator: Iterable, context):
+        import queue as _queue
+        from concurrent.futures import ThreadPoolExecutor
+
+        with BaseInferenceService._pipe_lock:
+            if BaseInferenceService._pipe_pool is None:
+                BaseInferenceService._pipe_pool = ThreadPoolExecutor(max_workers=int(
+                    os.environ.get("LUMEN_PIPELINE_THREADS", "256")), thread_name_prefix="lumen-pipe")
+        pool = BaseInferenceService._pipe_pool
+        q: "_queue.Queue" = _queue.Queue()
+        slots = threading.Semaphore(self.PIPELINE)
+        stop = threading.Event()
+
+        def reader():
+            buffers: dict[str, bytearray] = {}
+            try:
+                for req in request_iterator:
+                    cid = req.correlation_id or f"cid-{now_ms()}"
+                    try:
+                        payload, ready = self._assemble(cid, req, buffers)
+                    except Exception as e:
+                        q.put(("msg", [self._error(cid, pb.ERROR_CODE_INVALID_ARGUMENT, str(e))]))
+                        continue
+                    if not ready:
+                        continue
+                    while not slots.acquire(timeout=0.5):
+                        if stop.is_set():
+                            return
+                    q.put(("fut", pool.submit(self._one, req, cid, payload, context)))
+            except Exception as e:  # the stream itself failed (client cancelled, ...)
+                q.put(("err", e))
+            finally:
+                buffers.clear()
+                q.put(("end", None))
+
+        threading.Thread(target=reader, name="lumen-pipe-reader", daemon=True).start()
+        try:
+            while True:
+                kind, item = q.get()
+                if kind == "end":
+                    break
+                if kind == "err":
+                    raise item
+                if kind == "fut":
+                    msgs = item.result()
+                    slots.release()
+                else:
+                    msgs = item
+                for m in msgs:
+                    yield m
+        finally:
+            stop.set()
 
     def GetCapabilities(self, request, context):
         return self.build_capability()

@@ -56,6 +56,7 @@ def _labels(pairs, model_id: str) -> bytes:
 
 class GeneralCLIPService(BaseInferenceService):
     SERVICE_NAME = "lumen_clip"
+    PIPELINE = 64   # one stream's requests batch together (services/base.py Infer)
     LATENCY_KEY = "lat_ms"
 
     def __init__(self, backend, resources):
@@ -122,6 +123,7 @@ class GeneralCLIPService(BaseInferenceService):
 
 class BioCLIPService(BaseInferenceService):
     SERVICE_NAME = "lumen_bioclip"
+    PIPELINE = 64   # one stream's requests batch together (services/base.py Infer)
     LATENCY_KEY = "lat_ms"
 
     def __init__(self, backend, resources):
@@ -188,6 +190,7 @@ class SmartCLIPService(BaseInferenceService):
     """General CLIP + BioCLIP behind one service (both use the CLIP model's runtime)."""
 
     SERVICE_NAME = "lumen_smartclip"
+    PIPELINE = 64   # one stream's requests batch together (services/base.py Infer)
     LATENCY_KEY = "lat_ms"
 
     def __init__(self, clip_backend, clip_resources, bio_backend, bio_resources):

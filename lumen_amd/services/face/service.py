@@ -57,6 +57,7 @@ def _face(f, embedding=None) -> rs.Face:
 
 class GeneralFaceService(BaseInferenceService):
     SERVICE_NAME = "face-general"
+    PIPELINE = 64   # one stream's requests batch together (services/base.py Infer)
     LATENCY_KEY = "processing_time_ms"
     UNKNOWN_TASK_CODE = pb.ERROR_CODE_INTERNAL
 

@@ -81,6 +81,7 @@ def _f(v, default: float) -> float:
 
 class GeneralOcrService(BaseInferenceService):
     SERVICE_NAME = "ocr"
+    PIPELINE = 64   # one stream's requests batch together (services/base.py Infer)
     LATENCY_KEY = "duration_ms"
     UNKNOWN_TASK_CODE = pb.ERROR_CODE_INTERNAL
     DEFAULT_TASK = "ocr"

@@ -78,7 +78,7 @@ def _images(n: int, side: int, kind: str, seed: int = 0) -> list[bytes]:
     return out
 
 
-def _client_proc(plan_q, res_q, task: str, imgs: list, nthreads: int, pid: int) -> None:
+def _client_proc(plan_q, res_q, task: str, imgs: list, nthreads: int, pid: int, per_stream: int = 1) -> None:
     """One client process: ``nthreads`` threads, each with its own channel, sending one-image
     ``Infer`` streams back to back; requests that start and finish inside [t_on, t_off] count."""
     import grpc
@@ -96,19 +96,21 @@ def _client_proc(plan_q, res_q, task: str, imgs: list, nthreads: int, pid: int) 
         k = ci
         try:
             while time.time() < t_off:
-                img = imgs[k % len(imgs)]
-                k += 1
+                reqs = []
+                for _ in range(per_stream):
+                    reqs.append(pb.InferRequest(correlation_id=f"{pid}-{ci}-{k}", task=task,
+                                                payload=imgs[k % len(imgs)], payload_mime="image/jpeg"))
+                    k += 1
                 t_w, t = time.time(), time.perf_counter()
-                rs = list(stub.Infer(iter([pb.InferRequest(correlation_id=f"{pid}-{ci}-{k}", task=task, payload=img,
-                                                           payload_mime="image/jpeg")]), timeout=300))
+                rs = list(stub.Infer(iter(reqs), timeout=300))
                 dt = time.perf_counter() - t
-                ok = len(rs) == 1 and not rs[0].HasField("error")
+                ok = len(rs) == per_stream and not any(r.HasField("error") for r in rs)
                 with lock:
                     if not ok:
                         acc["errors"] += 1
                     elif t_w >= t_on and t_w + dt <= t_off:
                         acc["lat"].append(dt)
-                        acc["n"] += 1
+                        acc["n"] += per_stream
                         for key, v in rs[0].meta.items():      # server-side stage times of this request
                             if key.startswith("t_") or key in ("duration_ms", "batch_size"):
                                 try:
@@ -142,6 +144,10 @@ def main():
     ap.add_argument("--image-kind", choices=["photo", "noise"], default="photo")
     ap.add_argument("--server-threads", type=int, default=None)
     ap.add_argument("--client-procs", type=int, default=4, help="client processes (threads spread over them)")
+    ap.add_argument("--procs", type=int, default=1, help="hub replica processes on one port (LUMEN_HUB_PROCS)")
+    ap.add_argument("--per-stream", type=int, default=1,
+                    help="images per Infer stream (the service handles a stream's requests concurrently); "
+                         "latency is then per stream")
     args = ap.parse_args()
 
     os.environ["LUMEN_SYNTHETIC"] = "1"
@@ -168,7 +174,7 @@ def main():
     task = TASKS[args.service]
     imgs = _images(16, args.image_side, args.image_kind)
     procs = [ctx.Process(target=_client_proc, args=(plan_q, res_q, task, imgs, args.clients * (i + 1) // nproc -
-                                                    args.clients * i // nproc, i), daemon=True)
+                                                    args.clients * i // nproc, i, args.per_stream), daemon=True)
              for i in range(nproc)]
     for pr in procs:
         pr.start()
@@ -178,10 +184,32 @@ def main():
     t0 = time.perf_counter()
     res = Downloader(cfg).download_all()
     assert all(r.success for r in res.values()), {k: r.error for k, r in res.items()}
-    app = AppService.from_app_config(cfg)
-    threads = args.server_threads or max(16, args.clients + 4)
-    server, port = build_server(HubRouter(app.services), "127.0.0.1", 0, max_workers=threads)
-    server.start()
+    reps, rep_stop = [], None
+    if args.procs > 1:
+        # hub replica processes on one port (hub/server.py start_replicas, SO_REUSEPORT); this process
+        # only drives the clients
+        import socket
+
+        from lumen_amd.hub.server import start_replicas
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cfg_path = os.path.join(cache, "lumen-config.json")
+        d = cfg.model_dump(mode="json", exclude_none=True)
+        d["server"]["port"] = port
+        with open(cfg_path, "w") as f:
+            json.dump(d, f)
+        ready = ctx.Queue()
+        reps, rep_stop = start_replicas(cfg_path, port, args.procs, ready_q=ready)
+        for _ in reps:
+            ready.get(timeout=600)
+        app = server = None
+    else:
+        app = AppService.from_app_config(cfg)
+        threads = args.server_threads or max(16, args.clients + 4)
+        server, port = build_server(HubRouter(app.services), "127.0.0.1", 0, max_workers=threads)
+        server.start()
     load_s = time.perf_counter() - t0
     t_on = time.time() + args.warmup
     t_off = t_on + args.seconds
@@ -198,15 +226,20 @@ def main():
     for pr in procs:
         pr.join(timeout=60)
     el = args.seconds
-    server.stop(0)
-    app.close()
+    if server is not None:
+        server.stop(0)
+        app.close()
+    if rep_stop is not None:
+        rep_stop.set()
+        for pr in reps:
+            pr.join(timeout=60)
     la = np.asarray(lat) * 1e3 if lat else np.zeros(1)
     out = {"metric": f"serving {task} images/s", "value": round(n / el, 2), "unit": "images/s",
            "client_processes": nproc,
            "p50_ms": round(float(np.percentile(la, 50)), 2), "p99_ms": round(float(np.percentile(la, 99)), 2),
            "mean_ms": round(float(la.mean()), 2), "requests": n, "seconds": round(el, 2), "errors": errors,
            "clients": args.clients, "service": args.service, "model": args.model, "device": args.device,
-           "dp_workers": args.dp, "batch_cap": args.batch, "max_wait_ms": os.environ.get("LUMEN_MAX_WAIT_MS"),
+           "dp_workers": args.dp, "hub_processes": args.procs, "images_per_stream": args.per_stream, "batch_cap": args.batch, "max_wait_ms": os.environ.get("LUMEN_MAX_WAIT_MS"),
            "image": f"{args.image_kind} JPEG {args.image_side * 4 // 3}x{args.image_side}, "
                     f"{int(np.mean([len(b) for b in imgs]) / 1024)} KiB mean",
            "load_s": round(load_s, 1),
