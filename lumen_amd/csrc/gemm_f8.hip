@@ -274,7 +274,10 @@ static int f8_pick_splits(int tiles, int nk, const GemmEpi& ep) {
   if (ep.out_group || ep.table || ep.split_koff || ep.prelu || ep.post_act) return 1;
   const int cus = f8_num_cus();
   int S = 1;
-  if (2 * tiles <= cus && nk >= 32) {
+  // (r3, warm, M = 624: a grid of <= one workgroup per CU with very deep K splits 2-way too --
+  // 624 x 4096 x 14336: 62.3 -> 59.4 us; K = 4096 shapes lose at S = 2: 23.8 -> 31.7 us,
+  // profiles/r3_f8_splits_v1.txt)
+  if ((2 * tiles <= cus && nk >= 32) || (tiles <= cus && nk >= 96)) {
     // deep K only: the fp32 slab round trip costs more than the idle CUs on K <= 1024 shapes
     // (577 x 3072 x 1024: 14.2 -> 28.2 us split; 577 x 1024 x 4096: 35.8 -> 25.8 us;
     // 624 x 4096 x 14336 fp8: 61.9 -> 57.4 us at S = 2; profiles/r2_splitk_mid_v1.txt)
@@ -330,7 +333,7 @@ hipError_t gemm_lds128_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
 }
 
 hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw, const float* sw,
-                   void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, hipStream_t stream) {
+                   void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, hipStream_t stream, int splits) {
   if (K % 128 != 0 || N % 16 != 0 || M <= 0 || lda % 16 != 0 || ldw % 16 != 0) return hipErrorInvalidValue;
   // Measured at M = 624 on the Llama-3-8B projections (profiles/r2_f8_gemm_variants_v1.txt):
   // grids of more than one wave of workgroups (gate|up: 1120 tiles) run best at 2 stages x
@@ -339,7 +342,11 @@ hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t
   // (128x64 tiles were faster in isolation but slower over the whole weight-streaming prefill,
   // 9.87 vs 9.23-9.35 ms, profiles/r2_f8_bn64_v1.txt, and were removed.)
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  const int S = f8_pick_splits(tiles, K / 128, ep);
+  int S = f8_pick_splits(tiles, K / 128, ep);
+  if (splits > 0 && !(ep.out_group || ep.table || ep.split_koff || ep.prelu || ep.post_act)) {   // forced (benchmarks)
+    S = splits;
+    while (S > 1 && ((K / 128) % S != 0 || (K / 128) / S < 2)) --S;
+  }
   const bool multi_wave = tiles * S > f8_num_cus();
   if (S > 1) {
     if (multi_wave) return launch_f8_split<2, 2, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);

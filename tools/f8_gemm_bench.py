@@ -77,6 +77,9 @@ def main():
             continue
         cands = {
             "f8f8": lambda: ops.linear_f8(x8, xs, w8, ws, out=out, glu=glu),
+            "f8f8_s1": lambda: ops.linear_f8(x8, xs, w8, ws, out=out, glu=glu, splits=1),
+            "f8f8_s2": lambda: ops.linear_f8(x8, xs, w8, ws, out=out, glu=glu, splits=2),
+            "f8f8_s4": lambda: ops.linear_f8(x8, xs, w8, ws, out=out, glu=glu, splits=4),
             "f8f8+quant": lambda: ops.linear_f8(*ops.quant_rows_fp8(x), w8, ws, out=out, glu=glu),
             "w8_bf16mfma": lambda: ops.linear(x, w8, w_scale=ws, out=out, glu=glu),
             "blas_bf16": lambda: torch.mm(x, wb.t(), out=outf),
