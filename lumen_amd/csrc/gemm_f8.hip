@@ -274,10 +274,10 @@ static int f8_pick_splits(int tiles, int nk, const GemmEpi& ep) {
   if (ep.out_group || ep.table || ep.split_koff || ep.prelu || ep.post_act) return 1;
   const int cus = f8_num_cus();
   int S = 1;
-  // (r3, warm, M = 624: a grid of <= one workgroup per CU with very deep K splits 2-way too --
-  // 624 x 4096 x 14336: 62.3 -> 59.4 us; K = 4096 shapes lose at S = 2: 23.8 -> 31.7 us,
-  // profiles/r3_f8_splits_v1.txt)
-  if ((2 * tiles <= cus && nk >= 32) || (tiles <= cus && nk >= 96)) {
+  // (r3, warm caches, M = 624: 2-way split of the 160-tile down projection 62.3 -> 59.4 us, K = 4096
+  // shapes lose at S = 2: 23.8 -> 31.7 us, profiles/r3_f8_splits_v1.txt; in the cold-weight prefill
+  // the down split did not show a TTFT gain, so the single-wave grid stays unsplit)
+  if (2 * tiles <= cus && nk >= 32) {
     // deep K only: the fp32 slab round trip costs more than the idle CUs on K <= 1024 shapes
     // (577 x 3072 x 1024: 14.2 -> 28.2 us split; 577 x 1024 x 4096: 35.8 -> 25.8 us;
     // 624 x 4096 x 14336 fp8: 61.9 -> 57.4 us at S = 2; profiles/r2_splitk_mid_v1.txt)
