@@ -26,6 +26,15 @@ namespace lumen {
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
+// row-streaming decode weights (M <= 4): read once per launch by one CU -> non-temporal
+// (LUMEN_W8_NT, default on: 8B fp8 single-stream decode 428 -> 452 tok/s).  The batched kernels
+// (M > 4) keep the default policy: nt measured 5 % slower there (r3_w8_nt_ab_v1.txt).
+template <bool NT>
+__device__ __forceinline__ u32x4_t wload(const uint8_t* p) {
+  if constexpr (NT) return ld_nt16(p);
+  else return *(const u32x4_t*)p;
+}
+
 __device__ __forceinline__ void fp8x16_to_bf16(const u32x4_t w, bf16x8_t& f0, bf16x8_t& f1) {
   f0 = __builtin_bit_cast(bf16x8_t, fp8x8_to_bf16(w[0], w[1]));
   f1 = __builtin_bit_cast(bf16x8_t, fp8x8_to_bf16(w[2], w[3]));
@@ -343,7 +352,7 @@ __device__ __forceinline__ float dot8_bf16(const u32x4_t x, const u32x4_t y, flo
 // reductions and the store (vmcnt retires in issue order: a load issued after the stream
 // would wait behind it).  No MFMA: at M <= 4 the dot products use ~20-40 % of the VALU issue
 // budget while HBM streams.
-template <int MR, int U>
+template <int MR, int U, bool NT>
 __global__ void __launch_bounds__(256) gemv_w8_rows_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                            const uint8_t* __restrict__ W, int64_t ldw,
                                                            const float* __restrict__ scale, void* __restrict__ C,
@@ -408,7 +417,7 @@ __global__ void __launch_bounds__(256) gemv_w8_rows_kernel(const uint16_t* __res
     for (int u = 0; u < U; ++u) {
       const int64_t ko = (int64_t)(st0 + u) << 10;
 #pragma unroll
-      for (int r = 0; r < R; ++r) wb[slot][u][r] = *(const u32x4_t*)(wp[r] + ko);
+      for (int r = 0; r < R; ++r) wb[slot][u][r] = wload<NT>(wp[r] + ko);
 #pragma unroll
       for (int m = 0; m < MR; ++m) {
         ab[slot][u][m][0] = *(const u32x4_t*)(ap[m] + ko);
@@ -465,7 +474,7 @@ __global__ void __launch_bounds__(256) gemv_w8_rows_kernel(const uint16_t* __res
   for (int st = nch * U; st < nfull; ++st) {
     const int64_t ko = (int64_t)st << 10;
 #pragma unroll
-    for (int r = 0; r < R; ++r) wb[0][0][r] = *(const u32x4_t*)(wp[r] + ko);
+    for (int r = 0; r < R; ++r) wb[0][0][r] = wload<NT>(wp[r] + ko);
 #pragma unroll
     for (int m = 0; m < MR; ++m) {
       ab[0][0][m][0] = *(const u32x4_t*)(ap[m] + ko);
@@ -478,7 +487,7 @@ __global__ void __launch_bounds__(256) gemv_w8_rows_kernel(const uint16_t* __res
     const bool ok = k < K;
     const int64_t ko = ok ? k - lane * 16 : K - 16 - lane * 16;
 #pragma unroll
-    for (int r = 0; r < R; ++r) wb[0][0][r] = *(const u32x4_t*)(wp[r] + ko);
+    for (int r = 0; r < R; ++r) wb[0][0][r] = wload<NT>(wp[r] + ko);
 #pragma unroll
     for (int m = 0; m < MR; ++m) {
       const u32x4_t a0 = *(const u32x4_t*)(ap[m] + ko), a1 = *(const u32x4_t*)(ap[m] + ko + 8);
@@ -750,11 +759,19 @@ hipError_t gemm_w8(const uint16_t* A, int64_t lda, const uint8_t* W, int64_t ldw
                    int64_t ldc, int M, int N, int K, const GemmEpi& ep, float* ws, uint32_t* cnt, int ksplit,
                    hipStream_t stream) {
   if (K % 64 != 0 || M <= 0) return hipErrorInvalidValue;
+  static const bool nt = [] {
+    const char* e = std::getenv("LUMEN_W8_NT");
+    return e == nullptr || e[0] != '0';
+  }();
   if (M <= 4) {   // row-streaming GEMV
     const dim3 grid((N + 15) / 16);
 #define ROWS_LAUNCH(MR_, U_)                                                                                      \
-  hipLaunchKernelGGL((gemv_w8_rows_kernel<MR_, U_>), grid, dim3(256), 0, stream, A, lda, W, ldw, scale, C, ldc, M, \
-                     N, K, ep)
+  do {                                                                                                         \
+    if (nt) hipLaunchKernelGGL((gemv_w8_rows_kernel<MR_, U_, true>), grid, dim3(256), 0, stream, A, lda, W, ldw,  \
+                               scale, C, ldc, M, N, K, ep);                                                     \
+    else hipLaunchKernelGGL((gemv_w8_rows_kernel<MR_, U_, false>), grid, dim3(256), 0, stream, A, lda, W, ldw,    \
+                            scale, C, ldc, M, N, K, ep);                                                        \
+  } while (0)
     if (M == 1) ROWS_LAUNCH(1, 2);
     else if (M == 2) ROWS_LAUNCH(2, 2);
     else ROWS_LAUNCH(4, 1);
