@@ -38,15 +38,14 @@ row_topk_kernel(const float* __restrict__ scores, int64_t ld, int N, int k, floa
 #pragma unroll
   for (int i = 0; i < K; ++i) { v[i] = -INFINITY; id[i] = -1; }
   float m = -INFINITY, l = 0.f;
-  for (int j = j0 + threadIdx.x; j < j1; j += 256) {
-    const float x = s[j];
+  auto take = [&](const float x, const int j) {
     if (!in_ml) {
       const float xs = x * scale;
       if (xs > m) { l = l * __expf(m - xs) + 1.f; m = xs; }
       else l += __expf(xs - m);
     }
     if (x > v[K - 1]) {
-      v[K - 1] = x; id[K - 1] = ix ? ix[j] : j;
+      v[K - 1] = x; id[K - 1] = j;
 #pragma unroll
       for (int i = K - 1; i > 0; --i) {
         if (v[i] > v[i - 1]) {
@@ -55,6 +54,22 @@ row_topk_kernel(const float* __restrict__ scores, int64_t ld, int N, int k, floa
         }
       }
     }
+  };
+  // 8 loads in flight per thread before any is consumed: a strided scalar loop paid one
+  // dependent memory round trip per element (16 per thread on a 4096-column chunk)
+  constexpr int LU = 8;
+  for (int j = j0 + threadIdx.x; j < j1; j += 256 * LU) {
+    float xv[LU];
+    int iv[LU];
+#pragma unroll
+    for (int u = 0; u < LU; ++u) {
+      const int jj = min(j + u * 256, j1 - 1);
+      xv[u] = s[jj];
+      iv[u] = ix ? ix[jj] : jj;
+    }
+#pragma unroll
+    for (int u = 0; u < LU; ++u)
+      if (j + u * 256 < j1) take(xv[u], iv[u]);
   }
   __shared__ float red_v[4];
   __shared__ int red_i[4];
@@ -63,13 +78,29 @@ row_topk_kernel(const float* __restrict__ scores, int64_t ld, int N, int k, floa
   const int64_t obase = ((int64_t)row * nblk + part) * k;
   // block log-sum-exp (or the merge of phase-1 partials)
   if (in_ml) {
-    if (threadIdx.x == 0 && out_lse) {
+    if (out_lse) {   // merge the phase-1 (max, sum-exp) partials: one per thread, then a block reduction
       const float* pm = in_ml + (int64_t)row * nparts * 2;
-      float M = -INFINITY;
-      for (int p = 0; p < nparts; ++p) M = fmaxf(M, pm[2 * p]);
-      float L = 0.f;
-      for (int p = 0; p < nparts; ++p) L += pm[2 * p] == -INFINITY ? 0.f : pm[2 * p + 1] * __expf(pm[2 * p] - M);
-      out_lse[row] = M + logf(L);
+      float pmx = -INFINITY, pl = 0.f;
+      for (int p = threadIdx.x; p < nparts; p += 256) {
+        const float qm = pm[2 * p], ql = pm[2 * p + 1];
+        if (qm == -INFINITY) continue;
+        if (qm > pmx) { pl = pl * __expf(pmx - qm) + ql; pmx = qm; }
+        else pl += ql * __expf(qm - pmx);
+      }
+      float mm = pmx;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mm = fmaxf(mm, __shfl_xor(mm, o, 64));
+      float ll = pmx == -INFINITY ? 0.f : pl * __expf(pmx - mm);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) ll += __shfl_xor(ll, o, 64);
+      if (lane == 0) { red_m[w] = mm; red_l[w] = ll; }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const float M = fmaxf(fmaxf(red_m[0], red_m[1]), fmaxf(red_m[2], red_m[3]));
+        float L = 0.f;
+        for (int i = 0; i < 4; ++i) L += red_m[i] == -INFINITY ? 0.f : red_l[i] * __expf(red_m[i] - M);
+        out_lse[row] = M + logf(L);
+      }
     }
   } else {
     float mm = m;

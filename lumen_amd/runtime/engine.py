@@ -43,6 +43,9 @@ from .kv_cache import BLOCK, PagedKVCache
 
 log = logging.getLogger("lumen.engine")
 
+# look-ahead greedy decode on the graph path (LUMEN_DECODE_LOOKAHEAD=0: one synchronous step at a time)
+_LOOKAHEAD = os.environ.get("LUMEN_DECODE_LOOKAHEAD", "1") != "0"
+
 
 @dataclass
 class SamplingParams:
@@ -226,16 +229,24 @@ def tp_sync_capacity(max_batch: int, max_position: int) -> int:
 
 
 class DecodeGraphs:
-    """hipGraph-captured decode steps, one graph per padded batch-size bucket.
+    """hipGraph-captured decode steps, one graph per (padded batch-size, table-width) bucket.
 
-    A decode step is ~10 kernels per layer (hundreds per token) whose host launch
-    cost dominates small-batch decode; replaying a captured graph issues them in one
-    call.  Inputs are copied into static buffers (ids, positions, cache slots, block
-    table of fixed width, context lengths); padded rows use slot -1 (no cache write)
-    and context 1, and their logits are ignored.
+    A decode step is ~5 kernels per layer (hundreds per token) whose host launch cost
+    dominates small-batch decode; replaying a captured graph issues them in one call.
+    Inputs live in ONE device buffer per graph (positions, context lengths, block table of
+    fixed width, cache slots) filled by ONE H2D copy from a pinned staging buffer; padded
+    rows use slot -1 (no cache write) and context 1, and their logits are ignored.
+
+    Without TP the graph also holds the greedy sampler: the row top-8 candidates + row lse go
+    to one packed result buffer (one D2H per step) and the arg-max token is written straight
+    into the batch bucket's token-id buffer, which every graph of that bucket embeds from --
+    so the NEXT step can be launched before the host has read this one
+    (:meth:`launch` with ``ids=None``; LLMEngine's look-ahead decode).  Staging and result
+    buffers are double-buffered and fenced by the event of the launch that last used them.
     """
 
     BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128)
+    K_GREEDY = 8
 
     def __init__(self, llm, kv: PagedKVCache, max_batch: int, max_blocks: int):
         self.llm, self.kv = llm, kv
@@ -243,8 +254,10 @@ class DecodeGraphs:
         self.buckets = [b for b in self.BUCKETS if b <= max(max_batch, 1)] or [1]
         if self.buckets[-1] < max_batch:
             self.buckets.append(max_batch)
-        self.graphs: dict[int, tuple] = {}
+        self.graphs: dict[tuple, dict] = {}
+        self.ids: dict[int, torch.Tensor] = {}       # batch bucket -> device token ids (shared by its graphs)
         self.pool = None
+        self.in_graph_sampler = not llm.tp.enabled
 
     def _bucket(self, B: int) -> int:
         for b in self.buckets:
@@ -260,16 +273,49 @@ class DecodeGraphs:
                 return b
         return self.max_blocks
 
-    def _capture(self, Bp: int, W: int):
+    @staticmethod
+    def _layout(Bp: int, W: int) -> dict:
+        """byte offsets of (slots i64, pos i32, ctx i32, bt i32) in the step buffer"""
+        o_pos = 8 * Bp
+        o_ctx = o_pos + 4 * Bp
+        o_bt = o_ctx + 4 * Bp
+        return {"slots": (0, Bp), "pos": (o_pos, Bp), "ctx": (o_ctx, Bp), "bt": (o_bt, Bp * W),
+                "bytes": -(-(o_bt + 4 * Bp * W) // 16) * 16}
+
+    def _capture(self, Bp: int, W: int) -> dict:
         d = self.llm.embed.device
-        st = {"ids": torch.zeros(Bp, dtype=torch.long, device=d), "pos": torch.zeros(Bp, dtype=torch.int32, device=d),
-              "slots": torch.full((Bp,), -1, dtype=torch.long, device=d),
-              "bt": torch.zeros((Bp, W), dtype=torch.int32, device=d),
-              "ctx": torch.ones(Bp, dtype=torch.int32, device=d)}
+        lay = self._layout(Bp, W)
+        dbuf = torch.zeros(lay["bytes"], dtype=torch.uint8, device=d)
+
+        def views(buf):
+            o, n = lay["slots"]
+            v = {"slots": buf[o:o + 8 * n].view(torch.int64)}
+            for k in ("pos", "ctx"):
+                o, n = lay[k]
+                v[k] = buf[o:o + 4 * n].view(torch.int32)
+            o, n = lay["bt"]
+            v["bt"] = buf[o:o + 4 * n].view(torch.int32).view(Bp, W)
+            return v
+
+        st = views(dbuf)
+        st["slots"].fill_(-1)
+        st["ctx"].fill_(1)
+        if Bp not in self.ids:
+            self.ids[Bp] = torch.zeros(Bp, dtype=torch.long, device=d)
+        ids = self.ids[Bp]
+        k = self.K_GREEDY
+        res = torch.zeros(2 * Bp * k + Bp, dtype=torch.float32, device=d) if self.in_graph_sampler else None
         ws: dict = {}
 
         def run():
-            return self.llm.decode(st["ids"], st["pos"], st["slots"], self.kv, st["bt"], st["ctx"], workspace=ws)
+            logits = self.llm.decode(ids, st["pos"], st["slots"], self.kv, st["bt"], st["ctx"], workspace=ws)
+            if res is not None:
+                v = res[:Bp * k].view(Bp, k)
+                i = res[Bp * k:2 * Bp * k].view(torch.int32).view(Bp, k)
+                hip = ops.hip_ops()
+                hip.row_topk(logits, k, 1.0, v, i, res[2 * Bp * k:], int(self.llm.v0))
+                ids.copy_(i[:, 0])                                   # greedy next token, on the device
+            return logits
 
         s = torch.cuda.Stream(d)
         s.wait_stream(torch.cuda.current_stream(d))
@@ -280,32 +326,73 @@ class DecodeGraphs:
         g = torch.cuda.CUDAGraph()
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
-        with torch.cuda.graph(g, pool=self.pool):
+        # captured on the warm-up stream: the split-K tickets / workspaces the kernels key by stream
+        # already exist (a first request inside the capture would record its zero-fill into every replay)
+        with torch.cuda.graph(g, pool=self.pool, stream=s):
             out = run()
-        self.graphs[(Bp, W)] = (g, st, out, ws)
+        pin = lambda t: torch.empty(t.shape, dtype=t.dtype).pin_memory()  # noqa: E731
+        ent = {"g": g, "st": st, "dbuf": dbuf, "out": out, "ws": ws, "res": res, "lay": lay, "Bp": Bp, "W": W,
+               "h_step": [pin(dbuf) for _ in range(2)], "h_ids": [pin(ids) for _ in range(2)],
+               "h_res": [pin(res) for _ in range(2)] if res is not None else None,
+               "ev": [None, None], "par": 0}
+        ent["h_views"] = [views(h) for h in ent["h_step"]]
+        self.graphs[(Bp, W)] = ent
+        return ent
+
+    def _entry(self, B: int, width: int) -> dict:
+        key = (self._bucket(B), self._width(width))
+        return self.graphs[key] if key in self.graphs else self._capture(*key)
+
+    def launch(self, ids, pos, slots, bt, ctx) -> dict:
+        """Stage + replay one step (host arrays; ``ids=None``: the token ids the previous
+        replay of this batch bucket wrote on the device).  Returns a handle for
+        :meth:`tokens` / :meth:`logits`."""
+        B = len(pos)
+        e = self._entry(B, bt.shape[1])
+        Bp, W = e["Bp"], e["W"]
+        par = e["par"]
+        e["par"] ^= 1
+        if e["ev"][par] is not None:
+            e["ev"][par].synchronize()        # the copies that last used these pinned buffers are done
+        hv = e["h_views"][par]
+        w = min(bt.shape[1], W)
+        sl, po, cx, tb = (hv[k].numpy() for k in ("slots", "pos", "ctx", "bt"))
+        sl[:] = -1
+        sl[:B] = slots
+        po[:] = 0
+        po[:B] = pos
+        cx[:] = 1
+        cx[:B] = ctx
+        tb[:] = 0
+        tb[:B, :w] = bt[:, :w]
+        e["dbuf"].copy_(e["h_step"][par], non_blocking=True)
+        if ids is not None:
+            hi = e["h_ids"][par].numpy()
+            hi[:] = 0
+            hi[:B] = ids
+            self.ids[Bp].copy_(e["h_ids"][par], non_blocking=True)
+        e["g"].replay()
+        if e["res"] is not None:
+            e["h_res"][par].copy_(e["res"], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        e["ev"][par] = ev
+        return {"e": e, "par": par, "B": B, "ev": ev}
+
+    def tokens(self, h: dict):
+        """(values [B, 8], ids [B, 8], lse [B]) numpy of a launched step (waits for it)."""
+        e, B = h["e"], h["B"]
+        h["ev"].synchronize()
+        r = e["h_res"][h["par"]]
+        Bp, k = e["Bp"], self.K_GREEDY
+        v = r[:Bp * k].view(Bp, k)[:B].numpy()
+        i = r[Bp * k:2 * Bp * k].view(torch.int32).view(Bp, k)[:B].numpy()
+        return v, i, r[2 * Bp * k:2 * Bp * k + B].numpy()
 
     def run(self, ids, pos, slots, bt, ctx) -> torch.Tensor:
-        B = len(ids)
-        Bp = self._bucket(B)
-        W = self._width(bt.shape[1])
-        if (Bp, W) not in self.graphs:
-            self._capture(Bp, W)
-        g, st, out, _ = self.graphs[(Bp, W)]
-        w = min(bt.shape[1], W)
-        ids_p = np.zeros(Bp, np.int64)
-        ids_p[:B] = ids
-        pos_p = np.zeros(Bp, np.int32)
-        pos_p[:B] = pos
-        sl_p = np.full(Bp, -1, np.int64)
-        sl_p[:B] = slots
-        bt_p = np.zeros((Bp, W), np.int32)
-        bt_p[:B, :w] = bt[:, :w]
-        ctx_p = np.ones(Bp, np.int32)
-        ctx_p[:B] = ctx
-        for k, v in (("ids", ids_p), ("pos", pos_p), ("slots", sl_p), ("bt", bt_p), ("ctx", ctx_p)):
-            st[k].copy_(torch.from_numpy(v), non_blocking=True)
-        g.replay()
-        return out[:B]
+        """Replay one step and return its logits [B, V/tp] (device, valid until the next replay)."""
+        h = self.launch(ids, pos, slots, bt, ctx)
+        return h["e"]["out"][:h["B"]]
 
 
 class LLMEngine:
@@ -329,6 +416,7 @@ class LLMEngine:
         self.prefill_chunk = max(16, int(prefill_chunk or os.environ.get("LUMEN_PREFILL_CHUNK", 2048)))
         self._stop = threading.Event()
         self._ws: dict = {}
+        self._pending: Optional[tuple] = None     # (request ids, handle) of a look-ahead decode step in flight
         self.device = llm.embed.device
         self.stats = {"prefills": 0, "prefill_chunks": 0, "decode_steps": 0, "tokens": 0}
         if use_graphs is None:
@@ -476,16 +564,85 @@ class LLMEngine:
                 r.x = None
                 self._fail([r], e)
 
+    def _greedy_graph_ok(self, reqs, spec) -> bool:
+        """the in-graph greedy sampler serves this step: single rank, graphs on, every request
+        greedy without repetition penalty, batch and table within the graph buckets"""
+        g = self.graphs
+        return (g is not None and g.in_graph_sampler and self.sync is None and _LOOKAHEAD
+                and spec["inv"] is None and spec["pen"] is None and spec["k"] <= g.K_GREEDY
+                and len(reqs) <= g.buckets[-1])
+
+    def _graph_ready(self, reqs) -> bool:
+        """the step's graph exists or captures now (a capture failure disables graphs)"""
+        w = max(len(self.kv.blocks.table(r.rid)) for r in reqs)
+        if w > self.graphs.max_blocks:
+            return False
+        try:
+            self.graphs._entry(len(reqs), w)
+            return True
+        except Exception as e:  # noqa: BLE001 - capture unsupported: eager launches from now on
+            log.warning("hipGraph decode disabled: %s", e)
+            self.graphs = None
+            return False
+
+    def _step_inputs(self, reqs, ahead: int):
+        """positions / slots / block table / context lengths of the step that feeds position
+        r.ctx + ahead of every request"""
+        pos = np.array([r.ctx + ahead for r in reqs], np.int32)
+        slots = np.concatenate([self.kv.slots(r.rid, r.ctx + ahead, 1) for r in reqs])
+        bt = self.kv.block_table([r.rid for r in reqs])
+        return pos, slots, bt, pos + 1
+
+    def _can_look_ahead(self, reqs) -> bool:
+        """every request surely runs one more step after this one (no length finish, its reserved
+        blocks cover the next position) and nothing waits to join the batch"""
+        if self._prefilling or not self._waiting.empty():
+            return False
+        for r in reqs:
+            if len(r.tokens) + 1 >= r.params.max_new_tokens:
+                return False
+            if len(self.kv.blocks.table(r.rid)) * BLOCK <= r.ctx + 1:
+                return False
+        return True
+
     @torch.no_grad()
     def _decode(self) -> None:
         reqs = self._running
         B = len(reqs)
+        spec = Sampler.spec(reqs)
+        if self._greedy_graph_ok(reqs, spec) and self._graph_ready(reqs):
+            # look-ahead decode: the step after this one is launched (token ids taken from this
+            # step's in-graph arg-max) BEFORE this step's tokens are read, so the host work of
+            # reading, streaming and scheduling overlaps the GPU instead of idling it between steps
+            rids = [r.rid for r in reqs]
+            pend, self._pending = self._pending, None
+            if pend is not None and pend[0] == rids:
+                h = pend[1]
+            else:
+                ids = np.array([r.tokens[-1] for r in reqs], np.int64)
+                h = self.graphs.launch(ids, *self._step_inputs(reqs, 0))
+            nxt = self.graphs.launch(None, *self._step_inputs(reqs, 1)) if self._can_look_ahead(reqs) else None
+            _v, i, _lse = self.graphs.tokens(h)
+            toks = [int(i[b, 0]) for b in range(B)]
+            self.stats["decode_steps"] += 1
+            still = []
+            for r, t in zip(reqs, toks):
+                r.ctx += 1
+                if self._emit(r, t):
+                    self._finish(r)
+                else:
+                    still.append(r)
+            self._running = still
+            if nxt is not None and len(still) == B:
+                self._pending = (rids, nxt)
+                self.stats["lookahead_steps"] = self.stats.get("lookahead_steps", 0) + 1
+            return
+        self._pending = None
         ids = np.array([r.tokens[-1] for r in reqs], np.int64)
         pos = np.array([r.ctx for r in reqs], np.int32)
         slots = np.concatenate([self.kv.slots(r.rid, r.ctx, 1) for r in reqs])
         bt = self.kv.block_table([r.rid for r in reqs])
         ctx = pos + 1
-        spec = Sampler.spec(reqs)
         graph = self.graphs is not None and bt.shape[1] <= self.graphs.max_blocks
         if self.sync is not None:
             self.sync.send_decode(ids, pos, slots, bt, ctx, spec, graph)
@@ -539,6 +696,7 @@ class LLMEngine:
                     log.exception("decode step failed")
                     self._fail(self._running, e)
                     self._running = []
+                    self._pending = None
 
 
 def follower_loop(llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.Tensor], sync: TPSync,

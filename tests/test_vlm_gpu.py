@@ -113,12 +113,14 @@ def test_decode_graphs_match_eager():
         eng = LLMEngine(m, kv, lambda ids: m.embed_tokens(torch.tensor(ids, device="cuda")), max_batch=4,
                         use_graphs=graphs)
         try:
-            rs = [eng.submit(p, len(p), SamplingParams(max_new_tokens=6)) for p in prompts]
+            # different lengths: requests leave the batch at different steps (look-ahead discards)
+            rs = [eng.submit(p, len(p), SamplingParams(max_new_tokens=6 + 5 * i)) for i, p in enumerate(prompts)]
             for r in rs:
                 list(r.stream(timeout=120))
             outs[graphs] = [r.tokens for r in rs]
             if graphs:
                 assert eng.graphs is not None and eng.graphs.graphs, "decode graphs were not captured"
+                assert eng.stats.get("lookahead_steps", 0) > 0, "look-ahead decode never engaged"
         finally:
             eng.close()
     assert outs[True] == outs[False]

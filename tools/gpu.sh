@@ -13,7 +13,7 @@
 #   post_tests     post-processing / image kernels / OCR GPU tests only
 #   tp             TP=2 (two ranks sharing the GPU) tests + tools/tp_decode_bench.py (8B fp8)
 #   w8bench        tools/w8_decode_bench.py: HBM-cold decode GEMMs ($W8_M rows, default 1,16)
-#   vlm8b / vlm05  tools/vlm_bench.py Llama-3-8B fp8 / FastVLM-0.5B
+#   vlm8b / vlm05  tools/vlm_bench.py Llama-3-8B fp8 / FastVLM-0.5B (vlm8b_quick: 30 requests)
 #   prof_vlm8b     rocprofv3 kernel stats of the 8B fp8 decode bench (batch 16; prof_vlm8b_b1: single stream)
 #   face_ocr       tools/face_ocr_bench.py face + ocr
 #   prof_face / prof_ocr   rocprofv3 kernel stats of the face / OCR bench
@@ -61,6 +61,7 @@ for task in "$@"; do
       step post_tests 300 python -u -m pytest tests/test_postproc_gpu.py tests/test_kernels_gpu.py tests/test_ocr_gpu.py \
         -x -q --timeout 120 --timeout-method thread ;;
     vlm8b) step vlm8b 600 python tools/vlm_bench.py --preset llava-llama3-8b --fp8 ;;
+    vlm8b_quick) step vlm8b_quick 400 python tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 ;;
     tp)
       step tp_tests 300 python -u -m pytest tests/test_tp_gpu.py tests/test_comm_gpu.py -x -q --timeout 200 \
         --timeout-method thread
