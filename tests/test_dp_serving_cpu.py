@@ -312,3 +312,98 @@ def test_spmd_face_world2_matches_single_process(tmp_path):
                 assert abs(conf - f.confidence) < 1e-5
                 np.testing.assert_allclose(np.asarray(lm).ravel(), np.asarray(f.landmarks).ravel(), atol=1e-3)
                 assert _cos(emb, e) > 0.99999
+
+
+# ----------------------------------------------------------------------------- SPMD OCR DP (RCCL path, gloo here)
+def _ocr_backend_cpu(cache):
+    from lumen_amd.resources.config import ModelConfig, Runtime
+    from lumen_amd.services.common import load_model_resources
+    from lumen_amd.services.ocr.backend import MI355XOcrBackend
+
+    res = load_model_resources(cache, ModelConfig(model="ppocr-tiny", runtime=Runtime.onnx))
+    be = MI355XOcrBackend(res, device="cpu")
+    be.initialize()
+    return be
+
+
+def _ocr_images():
+    from tests.test_ocr_cpu import _rgb
+
+    return [_rgb(70, 150 + 10 * s, s) for s in range(5)]
+
+
+_OCR_P = dict(det_thresh=0.0, rec_thresh=0.0, box_thresh=0.0)
+
+
+def _spmd_ocr_rank(rank, world, port, cache, q):
+    import os
+
+    import torch
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from lumen_amd.parallel import Communicator, destroy, init_distributed
+    from lumen_amd.services.ocr.backend import OcrParams
+    from lumen_amd.services.ocr.spmd import SPMDOcrRunner
+
+    st = init_distributed(tp_size=1, device=torch.device("cpu"), timeout_s=120)
+    try:
+        be = _ocr_backend_cpu(cache)
+        imgs = _ocr_images()
+        run = SPMDOcrRunner(be, Communicator(st.dp_group, ipc=False), torch.device("cpu"))
+        out = run.run(imgs, [OcrParams(**_OCR_P)] * len(imgs))
+        q.put((rank, [[(r.box, r.text, r.confidence) for r in lines] for lines in out]))
+        be.close()
+    finally:
+        destroy()
+
+
+def test_spmd_ocr_pack_roundtrip():
+    """Packed OCR rows (box, confidence, code points) survive pack -> unpack exactly, including
+    non-ASCII text and images without lines."""
+    from lumen_amd.services.ocr.backend import OcrResult
+    from lumen_amd.services.ocr.spmd import pack_lines, unpack_lines
+
+    res = [[OcrResult(box=[(1, 2), (30, 2), (30, 9), (1, 9)], text="ab中文", confidence=0.75)], [],
+           [OcrResult(box=[(0, 0), (5, 0), (5, 5), (0, 5)], text="", confidence=0.5),
+            OcrResult(box=[(7, 8), (9, 8), (9, 12), (7, 12)], text="\U0001F600x", confidence=1.0)]]
+    rows, counts = pack_lines(res, 4, 2, 4)
+    back = unpack_lines(rows.numpy(), counts.numpy())
+    assert back[3] == [] and [[(r.box, r.text, r.confidence) for r in ls] for ls in back[:3]] == \
+        [[(r.box, r.text, r.confidence) for r in ls] for ls in res]
+
+
+def test_spmd_ocr_world2_matches_single_process(tmp_path):
+    """Each of 2 gloo ranks runs detect + recognise on its shard of 5 images; one all-gather of
+    the packed (box, confidence, code point) rows gives every rank the single-process result."""
+    import multiprocessing as mp
+
+    from lumen_amd.models.ocr import write_ocr_model
+    from lumen_amd.services.ocr.backend import OcrParams
+    from tests.test_parallel_cpu import _port
+
+    write_ocr_model(tmp_path / "models" / "ppocr-tiny", "ppocr-tiny")
+    be = _ocr_backend_cpu(tmp_path)
+    imgs = _ocr_images()
+    ref = be._predict_batch([(im, OcrParams(**_OCR_P)) for im in imgs])
+    be.close()
+    assert sum(len(ls) for ls in ref) > 0
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_spmd_ocr_rank, args=(r, 2, port, tmp_path, qq)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(qq.get(timeout=300) for _ in range(2))
+    for p in ps:
+        p.join(60)
+    assert all(p.exitcode == 0 for p in ps)
+    want = [[(r.box, r.text, r.confidence) for r in ls] for ls in ref]
+    for rank in (0, 1):
+        got = res[rank]
+        assert [len(ls) for ls in got] == [len(ls) for ls in want]
+        for gl, wl in zip(got, want):
+            for (gb, gt, gc), (wb, wt, wc) in zip(gl, wl):
+                assert list(map(tuple, gb)) == list(map(tuple, wb)), (gb, wb)
+                assert gt == wt, (gt, wt)
+                assert abs(gc - wc) < 1e-4, (gc, wc)   # fp32 recogniser over a different batch
