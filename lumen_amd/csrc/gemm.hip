@@ -1002,7 +1002,10 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
                         ((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0;
     if (t256 >= 512) tile = K <= 512 ? 245 : (ep.residual && K <= 2048 && M % 256 == 0 && N % 256 == 0 ? 709 : 609);
     else if (t128 >= 256) tile = lds_ok ? 20000 : 1;
-    else if (M <= 64) tile = 3;
+    // few rows over a deep K (the IResNet embedding FC at 64 faces: 64 x 512 x 25088 took 268 us as
+    // 16 register-staged 32x64 tiles): the LDS-DMA pipeline with K split over gridDim.y streams W once
+    else if (M <= 64 && !(lds_ok && K >= 4096)) tile = 3;
+    else if (M <= 64) tile = 20000;
     else if (t128 >= 144 && lds_ok) tile = 20005;
     // fewer 128x128 tiles (VLM vision tower at 577 tokens: 40-120): the same pipeline with K split
     // over gridDim.y + one reduce/epilogue pass (gemm_f8.hip f8_pick_splits) instead of 64x64 tiles

@@ -183,3 +183,16 @@ def test_gemm_w8_two_tile_glu_norm(M):
     ref = ops.linear(ops.rms_norm(x.float(), torch.ones(K), 1e-5), w8, glu=True, w_scale=ws)
     got = ops.linear_dec(x.to(DEV), w8.to(DEV), ws.to(DEV), glu=True, norm_eps=1e-5)
     assert got.shape == (M, I) and _rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 512, 25088), (37, 512, 25088), (8, 256, 4096)])
+def test_gemm_bf16_few_rows_deep_k_vs_fp32(M, N, K):
+    """Few rows over a deep K (the IResNet embedding FC, fp32 output + bias) on the split-K
+    LDS-DMA pipeline, vs the fp32 CPU reference."""
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
+    b = torch.randn(N, generator=g)
+    ref = ops.linear(x.float(), w.float(), b)
+    got = ops.linear(x.to(DEV), w.to(DEV), b.to(DEV), out_dtype=torch.float32)
+    assert got.dtype == torch.float32 and _rel(got, ref) < 1e-2
