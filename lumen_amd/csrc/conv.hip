@@ -202,7 +202,7 @@ hipError_t conv2d_lds(const ConvArgs& a, const GemmEpi& ep, int variant, hipStre
 hipError_t conv2d_igemm(const ConvArgs& a, const GemmEpi& ep, int tile, hipStream_t stream) {
   const int64_t M = (int64_t)a.N * a.Ho * a.Wo;
   if (tile >= 10) return conv2d_lds(a, ep, tile - 10, stream);
-  // Cin % 64 == 0 layers (IResNet, SCRFD / DBNet trunks) and Cin 8 / 16 / 32 stems: the LDS-DMA pipeline
+  // Cin % 64 == 0 layers (IResNet, SCRFD / DBNet trunks): the LDS-DMA pipeline
   // (profiles/r2_conv_lds_v1.txt); other shapes use the register-staged kernels
   if (tile < 0 && conv_lds_ok(a)) return conv2d_lds(a, ep, 0, stream);
   if (tile < 0) {

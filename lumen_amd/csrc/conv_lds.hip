@@ -19,11 +19,9 @@
 
 namespace lumen {
 
-// SC > 0: small-channel layers (stems: Cin 8 / 16 / 32 after channel padding), SC = Cin / 8 16-byte
-// chunks per tap: one 64-wide K-step spans 8 / SC taps, so the tap (and its validity bit) is per
-// lane rather than wave-uniform; K = KH*KW*Cin need not be a multiple of 64 (the taps past KH*KW
-// are masked to zero on the A side, which zeroes whatever the B side reads there).
-template <int NSTAGE, int WN, int BN, int SC>
+// PRE: the epilogue adds the per-position table (ep.table_pre: a folded pre-conv ChannelAffine's
+// border bias) before act / PReLU; a separate instantiation, so the plain form is unchanged.
+template <int NSTAGE, int WN, int BN, bool PRE>
 __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi ep) {
   constexpr int NW = 2 * WN;
   constexpr int TN = BN / WN;
@@ -56,13 +54,10 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
       __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, (int)((int64_t)N * K * 2), 0x00020000);
   int rofs[PERA];
   uint64_t tmask[PERA];
-  int ctap[PERA];                                                   // SC > 0: tap of this lane's chunk in a K-step
 #pragma unroll
   for (int i = 0; i < PERA; ++i) {
     const int r = (PERA * wid + i) * 8 + (lane >> 3);
-    const int cl = (lane & 7) ^ ((r >> 1) & 7);                     // 16-byte chunk of the K-step this lane loads
-    const int ca = SC > 0 ? (cl % (SC > 0 ? SC : 1)) * 8 : cl * 8;  // channel offset of this lane's 16 B
-    ctap[i] = SC > 0 ? cl / (SC > 0 ? SC : 1) : 0;
+    const int ca = ((lane & 7) ^ ((r >> 1) & 7)) * 8;             // channel offset of this lane's 16 B
     const int m = min(m0 + r, M - 1);
     const int img = m / (a.Ho * a.Wo), rem = m % (a.Ho * a.Wo);
     const int hb = (rem / a.Wo) * a.sh - a.ph, wb = (rem % a.Wo) * a.sw - a.pw;
@@ -88,27 +83,15 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
   const int row_step = a.dh * a.W * a.ldx * 2, col_step = a.dw * a.ldx * 2;
   auto stage = [&](int s, int kt) {
     char* baseA = smem + s * STAGE + wid * PERA * 1024;
-    if constexpr (SC > 0) {
 #pragma unroll
-      for (int i = 0; i < PERA; ++i) {
-        const int t = kt * (8 / SC) + ctap[i];
-        const bool ok = t < 64 && ((tmask[i] >> t) & 1ull);
-        const int ty = t / a.KW, tx = t - ty * a.KW;
-        const int off = ok ? rofs[i] + ty * row_step + tx * col_step : (int)0x80000000;
-        buf_load_lds16(xr, baseA + i * 1024, off, 0);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < PERA; ++i) {
-        const int off = (tmask[i] & tbit) ? rofs[i] + tofs : (int)0x80000000;
-        buf_load_lds16(xr, baseA + i * 1024, off, 0);
-      }
+    for (int i = 0; i < PERA; ++i) {
+      const int off = (tmask[i] & tbit) ? rofs[i] + tofs : (int)0x80000000;
+      buf_load_lds16(xr, baseA + i * 1024, off, 0);
     }
     char* baseB = smem + s * STAGE + ASZ + wid * PERB * 1024;
 #pragma unroll
     for (int i = 0; i < PERB; ++i)
       buf_load_lds16(wr, baseB + i * 1024, wofs[i], kt * 128);
-    if constexpr (SC > 0) return;
     c0 += 64;
     tofs += 128;
     if (c0 == a.Cin) {
@@ -128,7 +111,7 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
 #pragma unroll
     for (int j = 0; j < NR; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = SC > 0 ? (K + 63) / 64 : K / 64;
+  const int nk = K / 64;
   const int frow = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
@@ -193,32 +176,37 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
         const f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cc + q * 4);
         v[q * 4 + 0] = t[0]; v[q * 4 + 1] = t[1]; v[q * 4 + 2] = t[2]; v[q * 4 + 3] = t[3];
       }
-      if (ep.table_pre) epi_store16_t<false, true>(v, m, n, M, N, a.out, a.ldo, ep, crs);
-      else epi_store16_t<false>(v, m, n, M, N, a.out, a.ldo, ep, crs);
+      epi_store16_t<false, PRE>(v, m, n, M, N, a.out, a.ldo, ep, crs);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   });
 }
 
-template <int NS, int WN, int BN, int SC = 0>
-static hipError_t launch_conv_lds(const ConvArgs& a, const GemmEpi& ep, hipStream_t stream) {
+template <int NS, int WN, int BN, bool PRE>
+static hipError_t launch_conv_lds_t(const ConvArgs& a, const GemmEpi& ep, hipStream_t stream) {
   const size_t lds = (size_t)NS * (128 + BN) * 128;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_lds_kernel<NS, WN, BN, SC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipFuncSetAttribute((const void*)conv_lds_kernel<NS, WN, BN, PRE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)lds);
     attr = true;
   }
   const int M = a.N * a.Ho * a.Wo;
   const int tiles = ((M + 127) / 128) * ((a.Cout + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_lds_kernel<NS, WN, BN, SC>), dim3(tiles), dim3(128 * WN), lds, stream, a, ep);
+  hipLaunchKernelGGL((conv_lds_kernel<NS, WN, BN, PRE>), dim3(tiles), dim3(128 * WN), lds, stream, a, ep);
   return hipGetLastError();
+}
+
+template <int NS, int WN, int BN>
+static hipError_t launch_conv_lds(const ConvArgs& a, const GemmEpi& ep, hipStream_t stream) {
+  return ep.table_pre ? launch_conv_lds_t<NS, WN, BN, true>(a, ep, stream)
+                      : launch_conv_lds_t<NS, WN, BN, false>(a, ep, stream);
 }
 
 bool conv_lds_ok(const ConvArgs& a) {
   // 32-bit buffer offsets: input and filter below 2 GiB (the padding sentinel 0x80000000 lies
   // past both); <= 64 filter taps (the per-row validity mask)
-  return (a.Cin % 64 == 0 || a.Cin == 8 || a.Cin == 16 || a.Cin == 32) && a.Cout % 16 == 0 && a.ldx % 8 == 0 && a.ldo % 8 == 0 &&
+  return a.Cin % 64 == 0 && a.Cout % 16 == 0 && a.ldx % 8 == 0 && a.ldo % 8 == 0 &&
          ((uintptr_t)a.x & 15) == 0 && ((uintptr_t)a.w & 15) == 0 && (int64_t)a.N * a.Ho * a.Wo < (1LL << 31) &&
          (int64_t)a.N * a.H * a.W * a.ldx * 2 < (1LL << 31) && (int64_t)a.Cout * a.KH * a.KW * a.Cin * 2 < (1LL << 31) &&
          a.KH * a.KW <= 64;
@@ -228,13 +216,6 @@ bool conv_lds_ok(const ConvArgs& a) {
 // 4 = 128x64 2 stages 4 waves (two workgroups per CU)
 hipError_t conv2d_lds(const ConvArgs& a, const GemmEpi& ep, int variant, hipStream_t stream) {
   if (!conv_lds_ok(a)) return hipErrorInvalidValue;
-  if (a.Cin < 64) {   // stems: 128 x 64 tiles, 2 stages, 4 waves (two workgroups per CU)
-    switch (a.Cin) {
-      case 8: return launch_conv_lds<2, 2, 64, 1>(a, ep, stream);
-      case 16: return launch_conv_lds<2, 2, 64, 2>(a, ep, stream);
-      default: return launch_conv_lds<2, 2, 64, 4>(a, ep, stream);
-    }
-  }
   if (variant == 0) {
     const int64_t M = (int64_t)a.N * a.Ho * a.Wo;
     const int64_t t128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);

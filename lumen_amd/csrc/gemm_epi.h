@@ -195,7 +195,18 @@ __device__ __forceinline__ void epi_store16_t(float* v, int m, int n, int M, int
     }
   }
   if constexpr (PRE) {
-    const uint16_t* t = ep.table + (int64_t)((m % ep.table_period) + ep.table_offset) * ep.ldt + n;
+    // table_pre == 2: 3x3 / stride 1 / pad 1 border classes -- row (3 * ycls + xcls) of a [9, ldt]
+    // table, ycls / xcls = 0 first, 1 interior, 2 last row / column (table_period = Ho * Wo,
+    // table_offset = Wo); else a periodic per-position table
+    int64_t trow;
+    if (ep.table_pre == 2) {
+      const int p = m % ep.table_period, wo_n = ep.table_offset, ho_n = ep.table_period / wo_n;
+      const int ho = p / wo_n, wo = p - ho * wo_n;
+      trow = 3 * (ho == 0 ? 0 : (ho == ho_n - 1 ? 2 : 1)) + (wo == 0 ? 0 : (wo == wo_n - 1 ? 2 : 1));
+    } else {
+      trow = (m % ep.table_period) + ep.table_offset;
+    }
+    const uint16_t* t = ep.table + trow * ep.ldt + n;
     if (full) {
       add8(v, t);
       add8(v + 8, t + 8);

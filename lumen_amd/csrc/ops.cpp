@@ -647,14 +647,21 @@ void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Te
   }
   TORCH_CHECK(post_act == 0 || post_act == 3, "conv2d: post_act supports none / relu");
   ep.post_act = (int)post_act;
-  if (pos_bias.has_value() && pos_bias->defined()) {   // per-output-position bias [Ho * Wo, Cout], before act
+  if (pos_bias.has_value() && pos_bias->defined()) {   // per-output-position bias, before act
+    // [Ho * Wo, Cout]: one row per output position; [9, Cout] (3x3 / stride 1 / pad 1): one row per
+    // border class (first / interior / last row x column)
     TORCH_CHECK(pos_bias->scalar_type() == at::kBFloat16 && pos_bias->is_contiguous() && pos_bias->dim() == 2 &&
-                pos_bias->size(0) == Ho * Wo && pos_bias->size(1) == Cout, "conv2d: pos_bias bf16 [Ho * Wo, Cout]");
+                pos_bias->size(1) == Cout, "conv2d: pos_bias bf16 [Ho * Wo | 9, Cout]");
+    const bool cls = pos_bias->size(0) == 9 && Ho * Wo != 9;
+    TORCH_CHECK(cls || pos_bias->size(0) == Ho * Wo, "conv2d: pos_bias rows");
+    TORCH_CHECK(!cls || (KH == 3 && KW == 3 && stride[0] == 1 && stride[1] == 1 && padding[0] == 1 && padding[1] == 1 &&
+                         dilation[0] == 1 && dilation[1] == 1 && Ho >= 2 && Wo >= 2),
+                "conv2d: border-class pos_bias needs a 3x3 / stride 1 / pad 1 conv");
     ep.table = bf(*pos_bias);
     ep.ldt = Cout;
     ep.table_period = (int)(Ho * Wo);
-    ep.table_offset = 0;
-    ep.table_pre = 1;
+    ep.table_offset = cls ? (int)Wo : 0;
+    ep.table_pre = cls ? 2 : 1;
   }
   lumen::ConvArgs a{};
   a.x = bf(x); a.w = bf(w); a.out = out.data_ptr(); a.ldx = ldx; a.ldo = ldo;

@@ -78,8 +78,21 @@ class IBasicBlock(nn.Module):
         self._pre = (ws.to(self.conv1.w.dtype).contiguous(), b.contiguous(), tap, {})
 
     def _border(self, H: int, W: int) -> torch.Tensor:
-        """[H * W, Cout_p] bf16: minus the shift terms of the taps that fall into the padding."""
+        """Minus the shift terms of the taps that fall into the padding: [9, Cout_p] bf16, one row per
+        border class (3x3 / pad 1: the kernel derives the class from the output position), or
+        [H * W, Cout_p] per position for other geometries."""
         ws, b, tap, tabs = self._pre
+        if (H, W) not in tabs and self.conv1.k == 3 and self.conv1.pad == 1 and H >= 2 and W >= 2 and H * W != 9:
+            full = torch.zeros(9, tap.shape[0], device=tap.device)
+            for yc, ys in ((0, [0]), (1, []), (2, [2])):
+                for xc, xs in ((0, [0]), (1, []), (2, [2])):
+                    miss = torch.zeros(3, 3, device=tap.device)
+                    for ky in ys:
+                        miss[ky, :] = 1
+                    for kx in xs:
+                        miss[:, kx] = 1
+                    full[3 * yc + xc] = -(tap * miss).sum((1, 2))
+            tabs[(H, W)] = full.bfloat16().contiguous()
         if (H, W) not in tabs:
             k, p = self.conv1.k, self.conv1.pad
             oy = torch.arange(H, device=tap.device)[:, None] - p + torch.arange(k, device=tap.device)[None, :]
@@ -92,7 +105,7 @@ class IBasicBlock(nn.Module):
 
     def forward(self, x):
         sc = self.down(x) if self.down is not None else x
-        if x.is_cuda and _FOLD_BN1:
+        if x.is_cuda and _FOLD_BN1 and self.conv1.cin_p % 64 == 0:   # the LDS-DMA conv path serves pos_bias
             if self._pre is None:
                 self._fold_bn1()
             ws, b, _, _ = self._pre
