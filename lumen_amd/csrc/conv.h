@@ -16,7 +16,6 @@ struct ConvArgs {
 };
 
 hipError_t conv2d_igemm(const ConvArgs& a, const GemmEpi& ep, int tile, hipStream_t stream);
-bool conv_lds_ok(const ConvArgs& a);   // conv_lds.hip: the LDS-DMA pipeline serves this layer
 hipError_t conv2d_depthwise(const uint16_t* x, const uint16_t* w, const void* bias, int bias_f32, void* out,
                             int N, int H, int W, int C, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw,
                             int Ho, int Wo, int act, int out_f32, hipStream_t stream);

@@ -19,9 +19,7 @@
 
 namespace lumen {
 
-// PRE: the epilogue adds the per-position table (ep.table_pre: a folded pre-conv ChannelAffine's
-// border bias) before act / PReLU; a separate instantiation, so the plain form is unchanged.
-template <int NSTAGE, int WN, int BN, bool PRE>
+template <int NSTAGE, int WN, int BN>
 __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi ep) {
   constexpr int NW = 2 * WN;
   constexpr int TN = BN / WN;
@@ -176,31 +174,25 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
         const f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cc + q * 4);
         v[q * 4 + 0] = t[0]; v[q * 4 + 1] = t[1]; v[q * 4 + 2] = t[2]; v[q * 4 + 3] = t[3];
       }
-      epi_store16_t<false, PRE>(v, m, n, M, N, a.out, a.ldo, ep, crs);
+      epi_store16_t<false>(v, m, n, M, N, a.out, a.ldo, ep, crs);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   });
 }
 
-template <int NS, int WN, int BN, bool PRE>
-static hipError_t launch_conv_lds_t(const ConvArgs& a, const GemmEpi& ep, hipStream_t stream) {
+template <int NS, int WN, int BN>
+static hipError_t launch_conv_lds(const ConvArgs& a, const GemmEpi& ep, hipStream_t stream) {
   const size_t lds = (size_t)NS * (128 + BN) * 128;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_lds_kernel<NS, WN, BN, PRE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipFuncSetAttribute((const void*)conv_lds_kernel<NS, WN, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)lds);
     attr = true;
   }
   const int M = a.N * a.Ho * a.Wo;
   const int tiles = ((M + 127) / 128) * ((a.Cout + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_lds_kernel<NS, WN, BN, PRE>), dim3(tiles), dim3(128 * WN), lds, stream, a, ep);
+  hipLaunchKernelGGL((conv_lds_kernel<NS, WN, BN>), dim3(tiles), dim3(128 * WN), lds, stream, a, ep);
   return hipGetLastError();
-}
-
-template <int NS, int WN, int BN>
-static hipError_t launch_conv_lds(const ConvArgs& a, const GemmEpi& ep, hipStream_t stream) {
-  return ep.table_pre ? launch_conv_lds_t<NS, WN, BN, true>(a, ep, stream)
-                      : launch_conv_lds_t<NS, WN, BN, false>(a, ep, stream);
 }
 
 bool conv_lds_ok(const ConvArgs& a) {

@@ -47,9 +47,6 @@ struct GemmEpi {
   //   first, in place of alpha and bias (the host passes neither).
   const float* row_aff;
   const float* col_aff;
-  // table_pre: the periodic table is added with the bias, BEFORE act / PReLU (a per-position bias:
-  // a ChannelAffine folded into the following zero-padded conv leaves border-pixel corrections)
-  int table_pre;
 };
 
 // Launch plan of an fp8-weight decode GEMM (gemm_w8.hip): column tiles per wave, K splits and
@@ -163,9 +160,7 @@ __device__ __forceinline__ void add8(float* v, const uint16_t* p) {
 }
 
 // Apply the epilogue to 16 consecutive columns [n, n+16) of row m and store.
-// PRE: the periodic table joins the bias before act / PReLU (ep.table_pre; instantiated only by the
-// kernels that serve it, so the GEMM kernels' register budget is unchanged).
-template <bool WT, bool PRE = false>
+template <bool WT>
 __device__ __forceinline__ void epi_store16_t(float* v, int m, int n, int M, int N, void* __restrict__ C,
                                               int64_t ldc, const GemmEpi& ep, __amdgpu_buffer_rsrc_t rs) {
   if (m >= M || n >= N) return;
@@ -194,27 +189,6 @@ __device__ __forceinline__ void epi_store16_t(float* v, int m, int n, int M, int
       }
     }
   }
-  if constexpr (PRE) {
-    // table_pre == 2: 3x3 / stride 1 / pad 1 border classes -- row (3 * ycls + xcls) of a [9, ldt]
-    // table, ycls / xcls = 0 first, 1 interior, 2 last row / column (table_period = Ho * Wo,
-    // table_offset = Wo); else a periodic per-position table
-    int64_t trow;
-    if (ep.table_pre == 2) {
-      const int p = m % ep.table_period, wo_n = ep.table_offset, ho_n = ep.table_period / wo_n;
-      const int ho = p / wo_n, wo = p - ho * wo_n;
-      trow = 3 * (ho == 0 ? 0 : (ho == ho_n - 1 ? 2 : 1)) + (wo == 0 ? 0 : (wo == wo_n - 1 ? 2 : 1));
-    } else {
-      trow = (m % ep.table_period) + ep.table_offset;
-    }
-    const uint16_t* t = ep.table + trow * ep.ldt + n;
-    if (full) {
-      add8(v, t);
-      add8(v + 8, t + 8);
-    } else {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) if (n + q < N) v[q] += bf2f(t[q]);
-    }
-  }
   if (ep.glu) {
     float r[8];
 #pragma unroll
@@ -238,7 +212,7 @@ __device__ __forceinline__ void epi_store16_t(float* v, int m, int n, int M, int
   int64_t orow = m;
   if (ep.out_group > 0)
     orow = (int64_t)(m / ep.out_group) * ep.out_group_stride + ep.out_row_offset + (m % ep.out_group);
-  if (!PRE && ep.table) {
+  if (ep.table) {
     const uint16_t* t = ep.table + (int64_t)((m % ep.table_period) + ep.table_offset) * ep.ldt + n;
     if (full) {
       add8(v, t);

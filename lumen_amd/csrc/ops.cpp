@@ -610,7 +610,7 @@ static int64_t pixel_stride(const at::Tensor& t, const char* name) {
 void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
             const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& prelu, int64_t act,
             std::vector<int64_t> stride, std::vector<int64_t> padding, std::vector<int64_t> dilation, at::Tensor out,
-            int64_t tile, int64_t post_act, const c10::optional<at::Tensor>& pos_bias) {
+            int64_t tile, int64_t post_act) {
   check_gpu(x, "x");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv2d: bf16");
   const int64_t ldx = pixel_stride(x, "x");
@@ -647,28 +647,11 @@ void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Te
   }
   TORCH_CHECK(post_act == 0 || post_act == 3, "conv2d: post_act supports none / relu");
   ep.post_act = (int)post_act;
-  if (pos_bias.has_value() && pos_bias->defined()) {   // per-output-position bias, before act
-    // [Ho * Wo, Cout]: one row per output position; [9, Cout] (3x3 / stride 1 / pad 1): one row per
-    // border class (first / interior / last row x column)
-    TORCH_CHECK(pos_bias->scalar_type() == at::kBFloat16 && pos_bias->is_contiguous() && pos_bias->dim() == 2 &&
-                pos_bias->size(1) == Cout, "conv2d: pos_bias bf16 [Ho * Wo | 9, Cout]");
-    const bool cls = pos_bias->size(0) == 9 && Ho * Wo != 9;
-    TORCH_CHECK(cls || pos_bias->size(0) == Ho * Wo, "conv2d: pos_bias rows");
-    TORCH_CHECK(!cls || (KH == 3 && KW == 3 && stride[0] == 1 && stride[1] == 1 && padding[0] == 1 && padding[1] == 1 &&
-                         dilation[0] == 1 && dilation[1] == 1 && Ho >= 2 && Wo >= 2),
-                "conv2d: border-class pos_bias needs a 3x3 / stride 1 / pad 1 conv");
-    ep.table = bf(*pos_bias);
-    ep.ldt = Cout;
-    ep.table_period = (int)(Ho * Wo);
-    ep.table_offset = cls ? (int)Wo : 0;
-    ep.table_pre = cls ? 2 : 1;
-  }
   lumen::ConvArgs a{};
   a.x = bf(x); a.w = bf(w); a.out = out.data_ptr(); a.ldx = ldx; a.ldo = ldo;
   a.N = (int)N; a.H = (int)H; a.W = (int)W; a.Cin = (int)Cin; a.Cout = (int)Cout; a.KH = (int)KH; a.KW = (int)KW;
   a.sh = (int)stride[0]; a.sw = (int)stride[1]; a.ph = (int)padding[0]; a.pw = (int)padding[1];
   a.dh = (int)dilation[0]; a.dw = (int)dilation[1]; a.Ho = (int)Ho; a.Wo = (int)Wo;
-  TORCH_CHECK(!ep.table_pre || (lumen::conv_lds_ok(a) && tile < 0), "conv2d: pos_bias needs the LDS-DMA conv path");
   const at::DeviceGuard guard(x.device());
   LUMEN_CHECK_HIP(lumen::conv2d_igemm(a, ep, (int)tile, cur_stream()));
 }
@@ -781,7 +764,7 @@ TORCH_LIBRARY(lumen, m) {
   m.def("row_topk(Tensor scores, int k, float scale, Tensor(v!) out_v, Tensor(i!) out_i, Tensor(l!)? out_lse, "
         "int index_offset) -> ()");
   m.def("conv2d(Tensor x, Tensor w, Tensor? bias, Tensor? residual, Tensor? prelu, int act, int[] stride, "
-        "int[] padding, int[] dilation, Tensor(o!) out, int tile, int post_act=0, Tensor? pos_bias=None) -> ()");
+        "int[] padding, int[] dilation, Tensor(o!) out, int tile, int post_act=0) -> ()");
   m.def("conv2d_dw(Tensor x, Tensor w, Tensor? bias, int act, int[] stride, int[] padding, int[] dilation, "
         "Tensor(o!) out) -> ()");
   m.def("channel_affine(Tensor x, Tensor scale, Tensor shift, Tensor(o!) out, int act, Tensor? prelu) -> ()");

@@ -34,9 +34,6 @@ from ..ops import cnn
 from .layers import ChannelAffine, ConvBN, Linear, fold_bn
 
 
-# GPU IResNet blocks: the pre-conv BatchNorm folded into conv1 (weights, bias, border pos_bias)
-_FOLD_BN1 = True
-
 # =============================================================================== recogniser
 @dataclass
 class IResNetConfig:
@@ -59,59 +56,9 @@ class IBasicBlock(nn.Module):
         self.conv1 = ConvBN(cin, cout, 3, 1, prelu=True)          # conv1 + bn2 + prelu
         self.conv2 = ConvBN(cout, cout, 3, stride)                 # conv2 + bn3 (+ shortcut)
         self.down = ConvBN(cin, cout, 1, stride, pad=0) if (stride != 1 or cin != cout) else None
-        self._pre = None     # GPU: bn1 folded into conv1 (see _fold_bn1)
-
-    @torch.no_grad()
-    def _fold_bn1(self):
-        """conv1(s * x + t) with zero padding in the affine's output space =
-        conv1_{w * s}(x) + sum over the taps inside the image of w . t: the interior sum of the
-        shift term joins the bias, and border pixels (taps in the padding) get a per-position
-        correction (``pos_bias``, added before the PReLU).  Removes one full read + write pass
-        (the channel_affine kernel) per block."""
-        s, t = self.bn1.scale.float(), self.bn1.shift.float()
-        w = self.conv1.w.float()                                   # [Cout_p, 3, 3, Cin_p]
-        c = s.numel()
-        ws = w.clone()
-        ws[..., :c] *= s
-        tap = (w[..., :c] * t).sum(-1)                             # [Cout_p, 3, 3] shift term per tap
-        b = self.conv1.b.float() + tap.sum((1, 2))
-        self._pre = (ws.to(self.conv1.w.dtype).contiguous(), b.contiguous(), tap, {})
-
-    def _border(self, H: int, W: int) -> torch.Tensor:
-        """Minus the shift terms of the taps that fall into the padding: [9, Cout_p] bf16, one row per
-        border class (3x3 / pad 1: the kernel derives the class from the output position), or
-        [H * W, Cout_p] per position for other geometries."""
-        ws, b, tap, tabs = self._pre
-        if (H, W) not in tabs and self.conv1.k == 3 and self.conv1.pad == 1 and H >= 2 and W >= 2 and H * W != 9:
-            full = torch.zeros(9, tap.shape[0], device=tap.device)
-            for yc, ys in ((0, [0]), (1, []), (2, [2])):
-                for xc, xs in ((0, [0]), (1, []), (2, [2])):
-                    miss = torch.zeros(3, 3, device=tap.device)
-                    for ky in ys:
-                        miss[ky, :] = 1
-                    for kx in xs:
-                        miss[:, kx] = 1
-                    full[3 * yc + xc] = -(tap * miss).sum((1, 2))
-            tabs[(H, W)] = full.bfloat16().contiguous()
-        if (H, W) not in tabs:
-            k, p = self.conv1.k, self.conv1.pad
-            oy = torch.arange(H, device=tap.device)[:, None] - p + torch.arange(k, device=tap.device)[None, :]
-            ox = torch.arange(W, device=tap.device)[:, None] - p + torch.arange(k, device=tap.device)[None, :]
-            out_y = ((oy < 0) | (oy >= H)).float()                 # [H, k]
-            out_x = ((ox < 0) | (ox >= W)).float()                 # [W, k]
-            miss = 1.0 - (1.0 - out_y)[:, None, :, None] * (1.0 - out_x)[None, :, None, :]   # [H, W, k, k]
-            tabs[(H, W)] = (-torch.einsum("hwyx,cyx->hwc", miss, tap)).reshape(H * W, -1).bfloat16().contiguous()
-        return tabs[(H, W)]
 
     def forward(self, x):
         sc = self.down(x) if self.down is not None else x
-        if x.is_cuda and _FOLD_BN1 and self.conv1.cin_p % 64 == 0:   # the LDS-DMA conv path serves pos_bias
-            if self._pre is None:
-                self._fold_bn1()
-            ws, b, _, _ = self._pre
-            h = cnn.conv2d(x, ws, b, 1, self.conv1.pad, 1, prelu=self.conv1.prelu,
-                           pos_bias=self._border(x.shape[1], x.shape[2]))
-            return self.conv2(h, residual=sc)
         h = self.bn1(x)
         h = self.conv1(h)
         return self.conv2(h, residual=sc)
@@ -143,7 +90,6 @@ class IResNet(nn.Module):
         # keep the residual stream well scaled at random init
         for b in self.blocks:
             b.conv2.w.data.mul_(0.2)
-            b._pre = None
 
     @torch.no_grad()
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -182,8 +128,6 @@ class IResNet(nn.Module):
         if feat["running_mean"] is not None:
             w, b = fold_bn(w, b, feat)
         self.fc.load_torch(w, b)
-        for blk in self.blocks:
-            blk._pre = None
 
 
 # =============================================================================== detector

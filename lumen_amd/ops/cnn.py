@@ -40,12 +40,8 @@ def conv_out_hw(H, W, KH, KW, stride, padding, dilation):
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride=1, padding=0, dilation=1,
            act=None, residual: Optional[torch.Tensor] = None, prelu: Optional[torch.Tensor] = None,
-           out: Optional[torch.Tensor] = None, out_dtype=None, tile: int = -1, post_act=None,
-           pos_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out = post_act(prelu(act(conv(x, w) + bias + pos_bias)) + residual)   (NHWC; w [Cout, KH, KW, Cin];
-    ``pos_bias`` bf16 [Ho * Wo, Cout]: a per-output-position bias, e.g. the border corrections of a
-    channel affine folded into this zero-padded conv; [9, Cout] for a 3x3 / stride 1 / pad 1 conv: one
-    row per border class 3 * ycls + xcls, ycls / xcls = 0 first, 1 interior, 2 last row / column)."""
+           out: Optional[torch.Tensor] = None, out_dtype=None, tile: int = -1, post_act=None) -> torch.Tensor:
+    """out = post_act(prelu(act(conv(x, w) + bias)) + residual)   (NHWC; w [Cout, KH, KW, Cin])."""
     N, H, W, Cin = x.shape
     Cout, KH, KW, _ = w.shape
     Ho, Wo = conv_out_hw(H, W, KH, KW, stride, padding, dilation)
@@ -54,23 +50,13 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     a = act_id(act)
     if x.is_cuda:
         hip_ops().conv2d(x, w, bias, residual, prelu, a, list(_pair(stride)), _pad_arg(padding),
-                         list(_pair(dilation)), out, int(tile), act_id(post_act), pos_bias)
+                         list(_pair(dilation)), out, int(tile), act_id(post_act))
         return out
     pt, pl, pb, pr = _pads4(padding)
     y = F.conv2d(F.pad(x.float().permute(0, 3, 1, 2), (pl, pr, pt, pb)), w.float().permute(0, 3, 1, 2), None,
                  _pair(stride), 0, _pair(dilation)).permute(0, 2, 3, 1)
     if bias is not None:
         y = y + bias.float()
-    if pos_bias is not None:
-        if pos_bias.shape[0] == 9 and Ho * Wo != 9:        # 3x3 / s1 / p1 border classes
-            yc = torch.ones(Ho, dtype=torch.long)
-            yc[0], yc[-1] = 0, 2
-            xc = torch.ones(Wo, dtype=torch.long)
-            xc[0], xc[-1] = 0, 2
-            pb = pos_bias.float()[(3 * yc[:, None] + xc[None, :]).reshape(-1)]
-        else:
-            pb = pos_bias.float()
-        y = y + pb.view(1, Ho, Wo, Cout)
     y = _act_ref(y, a)
     if prelu is not None:
         y = torch.where(y > 0, y, y * prelu.float())

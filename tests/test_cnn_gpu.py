@@ -96,22 +96,3 @@ def test_pool_affine_upsample_scale_shuffle():
     assert _rel(cnn.channel_scale_(b, s.to(DEV)), cnn.channel_scale_(a, s)) < 1e-2
     y = torch.randn(2, 5, 6, 4 * 16).bfloat16()
     assert torch.equal(cnn.pixel_shuffle_up(y.to(DEV), 16, 2).cpu(), cnn.pixel_shuffle_up(y, 16, 2))
-
-
-@pytest.mark.parametrize("H,cin,cout,stride", [(14, 64, 64, 1), (28, 64, 128, 2), (7, 256, 512, 2)])
-def test_iresnet_block_bn1_fold_matches_unfolded(H, cin, cout, stride):
-    """IBasicBlock on the GPU with the pre-conv BatchNorm folded into conv1 (scaled weights, shift
-    sum in the bias, per-position border corrections before the PReLU) == bn1 -> conv1 -> conv2 on
-    the fp32 CPU path."""
-    from lumen_amd.models.face import IBasicBlock
-
-    g = torch.Generator().manual_seed(H + cin + cout)
-    blk = IBasicBlock(cin, cout, stride)
-    for m in (blk.bn1, blk.conv1, blk.conv2) + ((blk.down,) if blk.down is not None else ()):
-        m.random_init(g)
-    blk.bn1.shift.data.mul_(20.0)                  # large shift: the border terms matter
-    x = torch.randn(2, H, H, cin, generator=g).bfloat16()
-    ref = blk(x)
-    got = blk.to(DEV)(x.to(DEV))
-    assert blk._pre is not None and got.shape == ref.shape
-    assert _rel(got, ref) < 1e-2

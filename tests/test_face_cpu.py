@@ -98,24 +98,3 @@ def test_scrfd_heads_and_pack(tmp_path):
     root = write_face_model(tmp_path / "buffalo_tiny", "buffalo_tiny")
     info = json.loads((root / "model_info.json").read_text())
     assert info["model_type"] == "face" and (root / "detection.safetensors").exists()
-
-
-def test_iresnet_bn1_fold_math_cpu():
-    """The GPU block's bn1 -> conv1 fold (scaled weights, interior shift sum in the bias, border
-    pos_bias before the PReLU), evaluated with the fp32 CPU conv reference, equals bn1 then conv1."""
-    import torch
-
-    from lumen_amd.models.face import IBasicBlock
-    from lumen_amd.ops import cnn
-
-    g = torch.Generator().manual_seed(3)
-    blk = IBasicBlock(16, 32, 2)
-    for m in (blk.bn1, blk.conv1):
-        m.random_init(g)
-    blk.bn1.shift.data.mul_(20.0)
-    x = torch.randn(2, 9, 11, 16, generator=g).bfloat16()
-    ref = blk.conv1(blk.bn1(x)).float()
-    blk._fold_bn1()
-    ws, b, _, _ = blk._pre
-    got = cnn.conv2d(x, ws, b, 1, blk.conv1.pad, 1, prelu=blk.conv1.prelu, pos_bias=blk._border(9, 11)).float()
-    assert ((got - ref).norm() / ref.norm()).item() < 2e-2
