@@ -1040,6 +1040,10 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
       if (e != hipSuccess) return e;
       GemmEpi e2 = ep;
       if (e2.residual) e2.residual += (int64_t)M0 * e2.ldr;
+      // every per-A-row epilogue operand follows the row shift (LN-folded row stats, RMS sums)
+      if (e2.row_aff) e2.row_aff += 2 * (int64_t)M0;
+      if (e2.ssq_in) e2.ssq_in += (int64_t)M0 * e2.ssq_tiles;
+      if (e2.ssq_out) e2.ssq_out += (int64_t)M0 * e2.ssq_tiles;
       char* C2 = (char*)C + (int64_t)M0 * ldc * (ep.out_f32 ? 4 : 2);
       // tail rows: split-K ping-pong + reduce/epilogue pass (r2: the 128x128 register-staged
       // tail took 9.5 % of the ViT-L/14 step for 0.4 % of its FLOPs)

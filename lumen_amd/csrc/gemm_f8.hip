@@ -288,25 +288,64 @@ static int f8_pick_splits(int tiles, int nk, const GemmEpi& ep) {
   return S;
 }
 
-template <int NS, int WN, bool F8>
+template <int NS, int WN, bool F8, int BN = 128>
 static hipError_t launch_f8_split(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
                                   const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep,
                                   int S, hipStream_t stream) {
   constexpr int ES = F8 ? 1 : 2;
   float* slabs = split_workspace((size_t)S * M * N * sizeof(float), stream);
-  if (slabs == nullptr) return launch_f8<NS, WN, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+  if (slabs == nullptr) return launch_f8<NS, WN, F8, BN>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
   GemmEpi e{};
   e.alpha = 1.f;
   e.out_f32 = 1;
   e.split_koff = (int64_t)(K / S);
   e.split_cstride = (int64_t)M * N;
   (void)ES;
-  hipError_t err = launch_f8<NS, WN, F8>(A, lda, sa, W, ldw, sw, slabs, N, M, N, K / S, e, stream, S);
+  hipError_t err = launch_f8<NS, WN, F8, BN>(A, lda, sa, W, ldw, sw, slabs, N, M, N, K / S, e, stream, S);
   if (err != hipSuccess) return err;
   const int64_t work = (int64_t)M * (N / 16);
   hipLaunchKernelGGL(splitk_reduce16_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, stream, slabs, S, M,
                      N, C, ldc, ep);
   return hipGetLastError();
+}
+
+// Pipeline shapes (NSTAGE x waves x tile width), selected by a variant code:
+//   1 = <2 stages, 4 waves, 128>   2 = <3, 8, 128>   3 = <4, 8, 128>   4 = <4, 4, 128>
+//   5 = <2, 8, 128>                6 = <3, 8, 256>   7 = <2, 8, 256>   8 = <5, 8, 128>
+// 128 x 256 tiles halve the A/W staging bytes per MFMA of 128 x 128 ones; deeper rings keep
+// more bytes in flight per CU for the cold-weight (HBM-latency-bound) regime of a layer stack.
+// r4 also measured, and removed: a blocked weight layout (each K-step's W slice contiguous: no
+// change, so not TLB-bound) and a software-pipelined loop (fragments of step k + 1 read during the
+// MFMAs of step k: no change); every shape runs ~0.53 us per 128-byte K-step + ~7 us per launch
+// (profiles/r4_cold_gemm_blocked_sp_v1.txt, r4_f8_gemm_time_vs_k_v1.txt).
+static int variant_bn(int v) { return v == 6 || v == 7 ? 256 : 128; }
+
+template <bool F8>
+static hipError_t launch_variant(int v, const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
+                                 const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, int S,
+                                 hipStream_t stream) {
+  if (S > 1) {
+    switch (v) {
+      case 1: return launch_f8_split<2, 2, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
+      case 3: return launch_f8_split<4, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
+      case 4: return launch_f8_split<4, 2, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
+      case 5: return launch_f8_split<2, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
+      case 6: return launch_f8_split<3, 4, F8, 256>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
+      case 7: return launch_f8_split<2, 4, F8, 256>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
+      case 8: return launch_f8_split<5, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
+      default: return launch_f8_split<3, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
+    }
+  }
+  switch (v) {
+    case 1: return launch_f8<2, 2, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    case 3: return launch_f8<4, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    case 4: return launch_f8<4, 2, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    case 5: return launch_f8<2, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    case 6: return launch_f8<3, 4, F8, 256>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    case 7: return launch_f8<2, 4, F8, 256>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    case 8: return launch_f8<5, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    default: return launch_f8<3, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+  }
 }
 
 // bf16 operands on the same 128x128 LDS-DMA pipeline (K % 64 == 0, 16-byte aligned rows)
@@ -315,25 +354,19 @@ hipError_t gemm_lds128_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
   if (K % 64 != 0 || N % 16 != 0 || M <= 0 || lda % 8 != 0 || ldw % 8 != 0) return hipErrorInvalidValue;
   const uint8_t* a = (const uint8_t*)A;
   const uint8_t* w = (const uint8_t*)W;
-  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  const int S = f8_pick_splits(tiles, K / 64, ep);
-  if (variant == 0) variant = tiles * S > f8_num_cus() ? 2 : 3;
-  if (S > 1) {
-    switch (variant) {
-      case 2: return launch_f8_split<2, 2, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, S, stream);
-      case 5: return launch_f8_split<2, 4, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, S, stream);
-      default: return launch_f8_split<3, 4, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, S, stream);
-    }
-  }
-  switch (variant) {
-    case 2: return launch_f8<2, 2, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, stream);
-    case 5: return launch_f8<2, 4, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, stream);
-    default: return launch_f8<3, 4, false>(a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, stream);
-  }
+  // variant (bf16 tile codes 2000v): 0 = auto; 2 / 3 / 5 keep their r2 meaning (<2,2> / <3,4> / <2,4>);
+  // 10 + v selects launch_variant's code v (deeper rings, 128 x 256 tiles)
+  int code = variant >= 10 ? variant - 10 : variant == 2 ? 1 : variant == 5 ? 5 : variant == 0 ? 0 : 2;
+  const int bn = variant_bn(code);
+  const int tiles = ((M + 127) / 128) * ((N + bn - 1) / bn);
+  int S = f8_pick_splits(tiles, K / 64, ep);
+  if (code == 0) code = tiles * S > f8_num_cus() ? 1 : 2;
+  return launch_variant<false>(code, a, lda, nullptr, w, ldw, nullptr, C, ldc, M, N, K, ep, S, stream);
 }
 
 hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw, const float* sw,
-                   void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, hipStream_t stream, int splits) {
+                   void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, hipStream_t stream, int splits,
+                   int variant) {
   if (K % 128 != 0 || N % 16 != 0 || M <= 0 || lda % 16 != 0 || ldw % 16 != 0) return hipErrorInvalidValue;
   // Measured at M = 624 on the Llama-3-8B projections (profiles/r2_f8_gemm_variants_v1.txt):
   // grids of more than one wave of workgroups (gate|up: 1120 tiles) run best at 2 stages x
@@ -341,19 +374,16 @@ hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t
   // fit in one wave (qkv / o / down: 160-240 tiles) at 3 stages x 8 waves (2 waves / SIMD).
   // (128x64 tiles were faster in isolation but slower over the whole weight-streaming prefill,
   // 9.87 vs 9.23-9.35 ms, profiles/r2_f8_bn64_v1.txt, and were removed.)
-  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  const int bn = variant > 0 ? variant_bn(variant) : 128;
+  const int tiles = ((M + 127) / 128) * ((N + bn - 1) / bn);
   int S = f8_pick_splits(tiles, K / 128, ep);
   if (splits > 0 && !(ep.out_group || ep.table || ep.split_koff || ep.prelu || ep.post_act)) {   // forced (benchmarks)
     S = splits;
     while (S > 1 && ((K / 128) % S != 0 || (K / 128) / S < 2)) --S;
   }
   const bool multi_wave = tiles * S > f8_num_cus();
-  if (S > 1) {
-    if (multi_wave) return launch_f8_split<2, 2, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
-    return launch_f8_split<3, 4, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
-  }
-  if (multi_wave) return launch_f8<2, 2>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
-  return launch_f8<3, 4>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+  if (variant > 0) return launch_variant<true>(variant, A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
+  return launch_variant<true>(multi_wave ? 1 : 2, A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
 }
 
 // ============================================================================ quantisers

@@ -26,7 +26,8 @@ hipError_t gemm_w8(const uint16_t* A, int64_t lda, const uint8_t* W, int64_t ldw
                    int64_t ldc, int M, int N, int K, const GemmEpi& ep, float* ws, uint32_t* cnt, int ksplit,
                    hipStream_t stream);
 hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw, const float* sw,
-                   void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, hipStream_t stream, int splits = -1);
+                   void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, hipStream_t stream, int splits = -1,
+                   int variant = 0);
 hipError_t quant_rows_fp8(const uint16_t* x, int64_t ldx, uint8_t* out, int64_t ldo, float* scale, int M, int K,
                           hipStream_t stream);
 hipError_t rms_norm_quant_fp8(const uint16_t* x, int64_t ldx, const uint16_t* add, int64_t ldadd, uint16_t* resid_out,
@@ -342,11 +343,12 @@ static void check_f8_rows(const at::Tensor& t, const char* name) {
 }
 void gemm_f8(const at::Tensor& a8, const at::Tensor& sa, const at::Tensor& w8, const at::Tensor& sw,
              const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& residual, at::Tensor out,
-             int64_t glu, int64_t splits) {
+             int64_t glu, int64_t splits, int64_t variant) {
   check_f8_rows(a8, "gemm_f8: a8");
   check_f8_rows(w8, "gemm_f8: w8");
   const int64_t M = a8.size(0), K = a8.size(1), N = w8.size(0);
   TORCH_CHECK(w8.size(1) == K && K % 128 == 0 && N % 16 == 0, "gemm_f8: K % 128 == 0, N % 16 == 0");
+  TORCH_CHECK(variant >= 0 && variant <= 8, "gemm_f8: variant 0..8");
   TORCH_CHECK(sa.is_cuda() && sa.scalar_type() == at::kFloat && sa.numel() >= M && sa.is_contiguous(),
               "gemm_f8: sa f32 [M]");
   TORCH_CHECK(sw.is_cuda() && sw.scalar_type() == at::kFloat && sw.numel() == N && sw.is_contiguous(),
@@ -375,7 +377,7 @@ void gemm_f8(const at::Tensor& a8, const at::Tensor& sa, const at::Tensor& w8, c
   LUMEN_CHECK_HIP(lumen::gemm_f8(reinterpret_cast<const uint8_t*>(a8.data_ptr()), a8.stride(0), sa.data_ptr<float>(),
                                  reinterpret_cast<const uint8_t*>(w8.data_ptr()), w8.stride(0), sw.data_ptr<float>(),
                                  out.data_ptr(), out.stride(0), (int)M, (int)N, (int)K, ep, cur_stream(),
-                                 (int)splits));
+                                 (int)splits, (int)variant));
 }
 
 // per-token fp8 quantisation of bf16 rows: out8 [M, K] e4m3fn, scale [M] = amax / 448
@@ -751,7 +753,7 @@ TORCH_LIBRARY(lumen, m) {
   m.def("gemm_dec(Tensor a, Tensor w, Tensor? scale, Tensor? bias, Tensor? residual, Tensor(o!) out, int glu, "
         "int norm, float eps, Tensor? ssq_in, Tensor(s!)? ssq_out) -> ()");
   m.def("gemm_f8(Tensor a8, Tensor sa, Tensor w8, Tensor sw, Tensor? bias, Tensor? residual, Tensor(o!) out, "
-        "int glu, int splits=-1) -> ()");
+        "int glu, int splits=-1, int variant=0) -> ()");
   m.def("quant_rows_fp8(Tensor x, Tensor(o!) out8, Tensor(s!) scale) -> ()");
   m.def("rms_norm_quant_fp8(Tensor x, Tensor? add, Tensor(r!)? resid_out, Tensor gamma, float eps, Tensor(o!) out8, "
         "Tensor(s!) scale) -> ()");

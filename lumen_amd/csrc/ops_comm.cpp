@@ -85,9 +85,24 @@ void custom_all_reduce(const at::Tensor& inp, at::Tensor out, at::IntArrayRef ba
                                       c10::hip::getCurrentHIPStream().stream()));
 }
 
+// A HIP stream owned by the caller for the life of the process (never from PyTorch's
+// round-robin pool): graph captures key their split-K counters / workspaces by the capture
+// stream, so that stream must never be handed to another thread's eager work.
+int64_t private_stream(int64_t device) {
+  int prev = 0;
+  CHECK_HIPC(hipGetDevice(&prev));
+  CHECK_HIPC(hipSetDevice((int)device));
+  hipStream_t s = nullptr;
+  const hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  (void)hipSetDevice(prev);
+  CHECK_HIPC(e);
+  return reinterpret_cast<int64_t>(s);
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(lumen, m) {
+  m.def("private_stream(int device) -> int", &private_stream);
   m.def("ar_alloc(int cap) -> int", &ar_alloc);
   m.def("ar_free(int ptr) -> ()", &ar_free);
   m.def("ar_handle(int ptr) -> Tensor", &ar_handle);

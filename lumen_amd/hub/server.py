@@ -128,10 +128,25 @@ def build_server(servicer, host: str, port: int, max_workers: int = 16, reuse_po
     return server, bound
 
 
-def _replica_main(config_path: str, port: int, mode: str, stop_event, ready_q, idx: int) -> None:
-    """A replica process of :func:`serve` (spawned before any GPU use): same config, same port."""
+def _replica_main(config_path: str, port: int, mode: str, stop_event, ready_q, idx: int, parent_pid: int) -> None:
+    """A replica process of :func:`serve` (spawned before any GPU use): same config, same port.
+    ``stop_event`` is the parent's shared stop; ``parent_pid`` the pid to outlive-check against
+    (a plain ``getppid() == 1`` test misfires when the parent itself is PID 1 in a container)."""
     setup_logging(os.environ.get("LUMEN_LOG_LEVEL", "INFO"))
-    serve(config_path, port, mode=mode, stop_event=stop_event, procs=1, replica=idx, ready_q=ready_q)
+    serve(config_path, port, mode=mode, stop_event=stop_event, procs=1, replica=idx, ready_q=ready_q,
+          parent_pid=parent_pid)
+
+
+def _pid_alive(pid: int) -> bool:
+    if os.getppid() != pid:        # re-parented: the original parent exited
+        return False
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:       # pragma: no cover - exists, other owner
+        return True
+    return True
 
 
 def start_replicas(config_path: str, port: int, n: int, mode: str = "hub", ready_q=None):
@@ -144,7 +159,8 @@ def start_replicas(config_path: str, port: int, n: int, mode: str = "hub", ready
 
     ctx = mp.get_context("spawn")
     stop = ctx.Event()
-    procs = [ctx.Process(target=_replica_main, args=(config_path, port, mode, stop, ready_q, i + 1), daemon=False)
+    procs = [ctx.Process(target=_replica_main, args=(config_path, port, mode, stop, ready_q, i + 1, os.getpid()),
+                         daemon=False)
              for i in range(n)]
     for p in procs:
         p.start()
@@ -153,7 +169,7 @@ def start_replicas(config_path: str, port: int, n: int, mode: str = "hub", ready
 
 def serve(config_path: str, port_override: Optional[int] = None, mode: str = "hub",
           stop_event: Optional[threading.Event] = None, procs: Optional[int] = None, replica: int = 0,
-          ready_q=None) -> None:
+          ready_q=None, parent_pid: Optional[int] = None) -> None:
     """Run the server.  ``procs`` > 1 (or LUMEN_HUB_PROCS): this process plus procs - 1 spawned
     replicas accept on the same port (SO_REUSEPORT; a fixed port is required)."""
     config = load_and_validate_config(config_path)
@@ -201,7 +217,10 @@ def serve(config_path: str, port_override: Optional[int] = None, mode: str = "hu
     mdns = config.server.mdns
     if mdns is not None and mdns.enabled and replica == 0:
         zc, info = setup_mdns(bound, mdns)
-    done = stop_event or threading.Event()
+    # a replica's own signals stop only that replica (a local event); the parent's shared event
+    # (stop_event) stops them all
+    done = threading.Event() if replica > 0 or stop_event is None else stop_event
+    shared = stop_event if replica > 0 else None
 
     def _stop(signum, frame):
         log.info("signal %s: shutting down", signum)
@@ -211,7 +230,9 @@ def serve(config_path: str, port_override: Optional[int] = None, mode: str = "hu
         signal.signal(signal.SIGINT, _stop)
         signal.signal(signal.SIGTERM, _stop)
     while not done.wait(0.5):
-        if replica > 0 and os.getppid() == 1:     # parent gone: do not outlive it
+        if shared is not None and shared.is_set():
+            break
+        if replica > 0 and parent_pid is not None and not _pid_alive(parent_pid):   # parent gone
             break
     if rep_stop is not None:
         rep_stop.set()

@@ -19,7 +19,6 @@ the candidates for sampling).  Weights can be loaded from HF Qwen2/Llama state d
 """
 from __future__ import annotations
 
-import os
 
 import math
 from dataclasses import asdict, dataclass, field
@@ -44,11 +43,6 @@ _F8_MIN_ROWS = 33
 _FUSED_DECODE_NORM = True
 # decode: RoPE + current-token KV-cache write inside the paged attention kernel (no rope_kv launch)
 _FUSED_DECODE_ROPE = True
-# decode: extra workgroups of the attention launch read the o projection's weights (1) and also
-# the next layer's qkv weights (2) into the Infinity Cache while the attention runs (0 = off).
-# Off: the o projection gains ~2 us but the attention loses 2.5-3 us to the competing HBM stream
-# (8B fp8 single stream 373.6 / 373.5 / 362.3 tok/s at 0 / 1 / 2, r3_decode_prefetch_v1.txt)
-_DECODE_PREFETCH = int(os.environ.get("LUMEN_DECODE_PREFETCH", "0"))
 
 
 @dataclass
@@ -485,20 +479,9 @@ class LLM(nn.Module):
         fuse = _FUSED_DECODE_ROPE and x.is_cuda and self.cfg.head_dim in (64, 128) and \
             self.norm_folded and x.shape[0] <= 32 and not self.tp.enabled and kv is not None
 
-        layers = self.layers
-        nxt = {id(l): layers[i + 1] if i + 1 < len(layers) else None for i, l in enumerate(layers)}
-
         def attn(qkv, l, kc, vc):
-            # the attention occupies a few dozen CUs: the rest pull the o projection's weights (and,
-            # with LUMEN_DECODE_PREFETCH=2, the next layer's qkv) into the Infinity Cache meanwhile
-            pf = ()
-            if _DECODE_PREFETCH and x.is_cuda:
-                pf = (l.o_w,)
-                n = nxt[id(l)]
-                if _DECODE_PREFETCH >= 2 and n is not None:
-                    pf = (l.o_w, n.qkv_w)
             return lops.paged_decode(qkv, kc, vc, block_table, ctx_len, l.H, l.Hkv, workspace=workspace,
-                                     rope=(pos, self.cos_sin, slots) if fuse else None, prefetch=pf)
+                                     rope=(pos, self.cos_sin, slots) if fuse else None)
 
         attn.fuses_rope = fuse     # read by _layers_dec: no separate rope_kv launch
         self._layers(x, pos, slots, kv, attn)

@@ -226,7 +226,7 @@ def linear_dec(x: torch.Tensor, w: torch.Tensor, w_scale: Optional[torch.Tensor]
 def linear_f8(x8: torch.Tensor, x_scale: torch.Tensor, w8: torch.Tensor, w_scale: torch.Tensor,
               bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
               out: Optional[torch.Tensor] = None, glu: bool = False,
-              out_dtype: torch.dtype = torch.bfloat16, splits: int = -1) -> torch.Tensor:
+              out_dtype: torch.dtype = torch.bfloat16, splits: int = -1, variant: int = 0) -> torch.Tensor:
     """W8A8 projection on the gfx950 fp8 matrix cores (csrc/gemm_f8.hip):
     y = epi((x8 @ w8^T) * x_scale[m] * w_scale[n]) with fp32 bias, SwiGLU (``glu``, see
     :func:`glu_interleave`) or + residual.  x8 / w8 are e4m3fn, K % 128 == 0."""
@@ -236,7 +236,7 @@ def linear_f8(x8: torch.Tensor, x_scale: torch.Tensor, w8: torch.Tensor, w_scale
     if out is None:
         out = torch.empty((M, NO), device=x8.device, dtype=out_dtype)
     if x8.is_cuda:
-        hip_ops().gemm_f8(x8, x_scale, w8, w_scale, bias, residual, out, int(bool(glu)), int(splits))
+        hip_ops().gemm_f8(x8, x_scale, w8, w_scale, bias, residual, out, int(bool(glu)), int(splits), int(variant))
         return out
     y = (x8.float() @ w8.float().t()) * x_scale.float()[:M, None] * w_scale.float()[None, :]
     if bias is not None:

@@ -286,6 +286,9 @@ class GPUWorkerPool:
             if seg is not None:
                 try:
                     seg.close()
+                except Exception:  # noqa: BLE001 - e.g. BufferError with views alive; still unlink
+                    pass
+                try:
                     seg.unlink()
                 except Exception:  # noqa: BLE001
                     pass
@@ -327,7 +330,8 @@ class GPUWorkerPool:
                 w.inflight.clear()
         self._collector.join(timeout=2)
         for w in self.workers:
-            self._free_shm(w)
+            with w.in_lock:
+                self._free_shm(w)
 
     @property
     def size(self) -> int:
@@ -468,7 +472,11 @@ class GPUWorkerPool:
                     w.proc.kill()
                 w.proc.join(timeout=5)
                 if self.respawn and not self._stop.is_set():
-                    with self._lock:   # the collector reads w.shm / w.gen under this lock
+                    with self._lock:
+                        w.gen = 0      # a submit waiting for an input slot sees the ring retired
+                    # the input ring is replaced under its fill lock (no submit mid-copy into it),
+                    # and the collector reads w.shm / w.gen under the pool lock
+                    with w.in_lock, self._lock:
                         w.restarts += 1
                         self.stats["restarts"] += 1
                         self._start(w)

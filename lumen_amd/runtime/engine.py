@@ -258,6 +258,7 @@ class DecodeGraphs:
         self.ids: dict[int, torch.Tensor] = {}       # batch bucket -> device token ids (shared by its graphs)
         self.pool = None
         self.in_graph_sampler = not llm.tp.enabled
+        self._stream = None     # the capture stream, private to this instance (see _capture_stream)
 
     def _bucket(self, B: int) -> int:
         for b in self.buckets:
@@ -281,6 +282,20 @@ class DecodeGraphs:
         o_bt = o_ctx + 4 * Bp
         return {"slots": (0, Bp), "pos": (o_pos, Bp), "ctx": (o_ctx, Bp), "bt": (o_bt, Bp * W),
                 "bytes": -(-(o_bt + 4 * Bp * W) // 16) * 16}
+
+    def _capture_stream(self, d: torch.device) -> torch.cuda.Stream:
+        """One stream per engine that nothing else ever uses.  The split-K tickets and
+        workspaces the kernels key by stream are baked into the graphs captured on it; a
+        stream from PyTorch's recycled pool could later be handed to another thread's eager
+        split-K work while a graph replays, and the two would share counters."""
+        if self._stream is None:
+            try:
+                ptr = int(ops.hip_ops().private_stream(d.index if d.index is not None else
+                                                       torch.cuda.current_device()))
+                self._stream = torch.cuda.ExternalStream(ptr, device=d)
+            except (AttributeError, RuntimeError):   # extension without the op (CPU-only builds)
+                self._stream = torch.cuda.Stream(d)
+        return self._stream
 
     def _capture(self, Bp: int, W: int) -> dict:
         d = self.llm.embed.device
@@ -317,7 +332,7 @@ class DecodeGraphs:
                 ids.copy_(i[:, 0])                                   # greedy next token, on the device
             return logits
 
-        s = torch.cuda.Stream(d)
+        s = self._capture_stream(d)
         s.wait_stream(torch.cuda.current_stream(d))
         with torch.cuda.stream(s):
             for _ in range(2):

@@ -157,6 +157,36 @@ def test_gemm_f8_splitk_vs_fp32_reference(M, N, K, glu):
     assert torch.equal(got, again)
 
 
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("M,N,K,splits", [(624, 6144, 4096, 1), (624, 4096, 4096, 2), (300, 1536, 1024, 1),
+                                          (97, 768, 2048, 4), (130, 1040, 1024, 1)])
+def test_gemm_f8_pipeline_variants(M, N, K, splits, variant):
+    """Every fp8 pipeline shape (ring depth, waves, 128- / 256-wide tiles), with and without K
+    splits, against the fp32 reference (bias + residual epilogue)."""
+    g, x8, xs, w8, ws = _f8_operands(M, N, K, M + N + variant)
+    b = torch.randn(N, generator=g)
+    r = torch.randn(M, N, generator=g).bfloat16()
+    ref = (x8.float() @ w8.float().t()) * xs[:, None] * ws[None, :] + b + r.float()
+    wd = w8.to(DEV)
+    got = ops.linear_f8(x8.to(DEV), xs.to(DEV), wd, ws.to(DEV), bias=b.to(DEV), residual=r.to(DEV),
+                        splits=splits, variant=variant)
+    assert _rel(got, ref) < 8e-3
+
+
+@pytest.mark.parametrize("tile", [20011, 20012, 20013, 20014, 20015, 20016, 20017, 20018])
+@pytest.mark.parametrize("M,N,K,act", [(577, 3072, 1024, None), (577, 1024, 4096, None), (200, 512, 640, "quick_gelu")])
+def test_gemm_bf16_pipeline_variants(M, N, K, act, tile):
+    """bf16 operands on every LDS-DMA pipeline shape (tile codes 20010 + launch_variant code)."""
+    g = torch.Generator().manual_seed(M + N + tile)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
+    b = torch.randn(N, generator=g).bfloat16()
+    r = torch.randn(M, N, generator=g).bfloat16()
+    ref = ops.linear(x.float(), w.float(), b.float(), act=act, residual=r.float())
+    got = ops.linear(x.to(DEV), w.to(DEV), b.to(DEV), act=act, residual=r.to(DEV), tile=tile)
+    assert _rel(got, ref) < 1e-2
+
+
 @pytest.mark.parametrize("M,N,K,act", [(577, 1024, 4096, None), (577, 3072, 1024, None), (577, 4096, 1024, "quick_gelu"),
                                        (300, 1024, 1024, None)])
 def test_gemm_bf16_lds128_splitk_vs_fp32(M, N, K, act):

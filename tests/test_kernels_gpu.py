@@ -279,7 +279,8 @@ def test_image_prep_center_crop_matches_reference():
 @pytest.mark.parametrize("M,N,K,tile", [(24 * 256, 3072, 1024, 1629), (24 * 256, 4096, 1024, 609),
                                         (16 * 256, 1024, 1024, 709), (24 * 256 + 77, 3072, 1024, -1),
                                         (577, 3072, 1024, -1), (577, 4096, 1024, -1), (40, 768, 768, -1),
-                                        (512 * 77, 2304, 768, -1), (300 * 256 + 300, 1024, 512, 609)])
+                                        (512 * 77, 2304, 768, -1), (300 * 256 + 300, 1024, 512, 609),
+                                        (257 * 256, 3072, 1024, -1)])
 @pytest.mark.parametrize("act", [None, "quick_gelu"])
 def test_gemm_layernorm_folded(M, N, K, tile, act):
     """LayerNorm folded into the projection (ln_row_stats + gemm_lnf): ping-pong FAST form (interior

@@ -14,6 +14,7 @@
 #   tp             TP=2 (two ranks sharing the GPU) tests + tools/tp_decode_bench.py (8B fp8)
 #   w8bench        tools/w8_decode_bench.py: HBM-cold decode GEMMs ($W8_M rows, default 1,16)
 #   vlm8b / vlm05  tools/vlm_bench.py Llama-3-8B fp8 / FastVLM-0.5B (vlm8b_quick: 30 requests)
+#   prof_ttft      rocprofv3 kernel trace of 3 single-request TTFTs (8B fp8, 2 new tokens)
 #   prof_vlm8b     rocprofv3 kernel stats of the 8B fp8 decode bench (batch 16; prof_vlm8b_b1: single stream)
 #   face_ocr       tools/face_ocr_bench.py face + ocr
 #   prof_face / prof_ocr   rocprofv3 kernel stats of the face / OCR bench
@@ -73,6 +74,9 @@ for task in "$@"; do
     prof_vlm8b_b1)
       step prof_vlm8b_b1 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_vlm8b_b1 -o run -- \
         python3 tools/vlm_bench.py --preset llava-llama3-8b --n 3 --warmup 1 --max-new 64 --batch 1 --fp8 ;;
+    prof_ttft)
+      step prof_ttft 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ttft -o run -- \
+        python3 tools/vlm_bench.py --preset llava-llama3-8b --n 3 --warmup 2 --max-new 2 --batch 0 --fp8 ;;
     face_ocr)
       step face 400 python tools/face_ocr_bench.py --what face
       step ocr 400 python tools/face_ocr_bench.py --what ocr ;;

@@ -111,6 +111,13 @@ def main():
     # (16 concurrent clients: each decodes its JPEG in its own thread, then submits)
     from concurrent.futures import ThreadPoolExecutor
 
+    if args.batch <= 0:       # TTFT / single-stream only (profiling runs)
+        eng.close()
+        print(json.dumps({"metric": "VLM p50 TTFT", "value": float(np.percentile(ttft, 50)), "unit": "ms",
+                          "admit_to_first_token": float(np.median(admit_first_ms)),
+                          "jpeg_decode": float(np.median(dec_ms[:args.n])),
+                          "decode_tok_s_single": float(np.median(tps)) if tps else None, "n": args.n}))
+        return
     t1 = time.perf_counter()
     with ThreadPoolExecutor(max_workers=max(args.batch, 1)) as ex:
         rs = list(ex.map(lambda _: eng.submit((ids, decode(jpeg)), len(full),
