@@ -25,6 +25,7 @@
 // takes logical chunks g and g+4 (k = 16g..16g+15 and 64+16g..64+16g+15).  The same
 // k permutation is used for A and W, so the dot products are unchanged, and with it
 // every ds_read_b128 lane group hits 64 distinct banks (chunks 2g, 2g+1 would be 2-way).
+#include <algorithm>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -52,11 +53,26 @@ __device__ __forceinline__ void f8_vm_wait() {
 // lda / ldw are in ELEMENTS of the operand type, K in elements; sa / sw may be null (1.0).
 // BN: tile width (128, or 64 for grids whose 128x128 tiles leave CUs idle -- twice the tiles,
 // 72 KiB of LDS at 3 stages so two workgroups share a CU).
-template <int NSTAGE, int WN, bool F8, int BN = 128>
+// Stream-K form (SK): the grid is one workgroup per CU and the (tile, K-step) iteration space
+// is cut into equal contiguous ranges, one per workgroup, so a mid-size GEMM whose 128x128 tiles
+// cannot fill 256 CUs (LLaVA vision tower at 577 tokens: 40-160 tiles; 8B W8A8 prefill at 624
+// tokens: 160-240 tiles) still keeps every CU streaming.  A tile whose K range spans several
+// workgroups is combined in the launch: each contributor stores its fp32 accumulators
+// write-through (sc1) to a slab, drains, and draws a ticket; the last arriver acquires, adds the
+// other slabs to its registers and runs the normal epilogue (cdna_hip_programming.md Guideline 16,
+// split-K seam).  Nobody waits on another workgroup, so residency is never assumed.
+struct SkArgs {
+  int ipw;          // (tile, K-step) iterations per workgroup
+  int maxc;         // slab slots per tile (max contributors)
+  float* ws;        // [tiles][maxc][128 * BN] fp32 slabs
+  uint32_t* cnt;    // [tiles] arrival tickets (zero between launches: the last arriver resets)
+};
+
+template <int NSTAGE, int WN, bool F8, int BN = 128, bool SK = false>
 __global__ void __launch_bounds__(128 * WN)
 gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restrict__ sa, const uint8_t* __restrict__ W,
                int64_t ldw, const float* __restrict__ sw, void* __restrict__ C, int64_t ldc, int M, int N, int K,
-               GemmEpi ep) {
+               GemmEpi ep, SkArgs sk) {
   constexpr int ES = F8 ? 1 : 2;         // bytes per element
   lda *= ES;
   ldw *= ES;
@@ -72,138 +88,200 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int tiles_m = (M + 127) / 128, tiles_n = (N + BN - 1) / BN;
-  if (ep.split_koff) {   // split-K (gridDim.y = splits): this workgroup's K slice -> its fp32 slab
+  if (!SK && ep.split_koff) {   // split-K (gridDim.y = splits): this workgroup's K slice -> its fp32 slab
     A += blockIdx.y * ep.split_koff * ES;
     W += blockIdx.y * ep.split_koff * ES;
     C = (float*)C + blockIdx.y * ep.split_cstride;
   }
-  // XCD-aware: consecutive logical tiles share a W column panel (row tiles fastest), and
-  // xcd_remap hands each XCD a contiguous run of them -> each W panel is read from HBM once
-  const int lin = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = lin % tiles_m, tn = lin / tiles_m;
-  const int m0 = tm * 128, n0 = tn * BN;
-
-  // staging: wave wid, instruction i covers rows (PER*wid + i)*8 + lane/8 of the A image and
-  // rows (PERW*wid + i)*8 + lane/8 of the W image
-  const uint8_t* src_a[PER];
-  const uint8_t* src_w[PERW];
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int r = (PER * wid + i) * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    src_a[i] = A + (int64_t)min(m0 + r, M - 1) * lda + c * 16;
-  }
-#pragma unroll
-  for (int i = 0; i < PERW; ++i) {
-    const int r = (PERW * wid + i) * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    src_w[i] = W + (int64_t)min(n0 + r, N - 1) * ldw + c * 16;
-  }
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  typedef const __attribute__((address_space(1))) void* g_ptr_t;
-  auto stage = [&](int s, int64_t koff) {
-    char* base = smem + s * STAGE;
-#pragma unroll
-    for (int i = 0; i < PER; ++i)
-      __builtin_amdgcn_global_load_lds((g_ptr_t)(src_a[i] + koff), (lds_ptr_t)(base + (wid * PER + i) * 1024), 16,
-                                       0, 0);
-#pragma unroll
-    for (int i = 0; i < PERW; ++i)
-      __builtin_amdgcn_global_load_lds((g_ptr_t)(src_w[i] + koff),
-                                       (lds_ptr_t)(base + 128 * 128 + (wid * PERW + i) * 1024), 16, 0, 0);
-  };
-
-  f32x4_t acc[4][NR];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-
   const int nk = K * ES / 128;
   const int frow = lane & 15, g = lane >> 4;
-#pragma unroll
-  for (int s = 0; s < NSTAGE - 1; ++s)
-    if (s < nk) stage(s, (int64_t)s * 128);
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  typedef const __attribute__((address_space(1))) void* g_ptr_t;
+  f32x4_t acc[4][NR];
 
-  for (int kt = 0; kt < nk; ++kt) {
-    // stage kt landed for this wave (NSTAGE-2 younger stages may stay in flight) ...
-    if (kt + NSTAGE - 2 < nk) f8_vm_wait<(PER + PERW) * (NSTAGE - 2)>();
-    else f8_vm_wait<0>();
-    // ... and for every wave; every wave is also done reading stage kt-1's buffer
-    __builtin_amdgcn_s_barrier();
-    if (kt + NSTAGE - 1 < nk) stage((kt + NSTAGE - 1) % NSTAGE, (int64_t)(kt + NSTAGE - 1) * 128);
-    const char* sA = smem + (kt % NSTAGE) * STAGE;
-    const char* sW = sA + 128 * 128;
-    u32x4_t fa[4][2], fb[NR][2];
+  // ---- K-steps [k0, k1) of tile (tm, tn) into acc (zeroed first)
+  auto mainloop = [&](const int m0, const int n0, const int k0, const int k1) {
+    // staging: wave wid, instruction i covers rows (PER*wid + i)*8 + lane/8 of the A image and
+    // rows (PERW*wid + i)*8 + lane/8 of the W image
+    const uint8_t* src_a[PER];
+    const uint8_t* src_w[PERW];
 #pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const int r = wn * TN + j * 16 + frow;
-      fb[j][0] = *(const u32x4_t*)(sW + swz(r, g));
-      fb[j][1] = *(const u32x4_t*)(sW + swz(r, g + 4));
+    for (int i = 0; i < PER; ++i) {
+      const int r = (PER * wid + i) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      src_a[i] = A + (int64_t)min(m0 + r, M - 1) * lda + c * 16;
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = wm * 64 + i * 16 + frow;
-      fa[i][0] = *(const u32x4_t*)(sA + swz(r, g));
-      fa[i][1] = *(const u32x4_t*)(sA + swz(r, g + 4));
+    for (int i = 0; i < PERW; ++i) {
+      const int r = (PERW * wid + i) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      src_w[i] = W + (int64_t)min(n0 + r, N - 1) * ldw + c * 16;
     }
+    auto stage = [&](int s, int64_t koff) {
+      char* base = smem + s * STAGE;
+#pragma unroll
+      for (int i = 0; i < PER; ++i)
+        __builtin_amdgcn_global_load_lds((g_ptr_t)(src_a[i] + koff), (lds_ptr_t)(base + (wid * PER + i) * 1024), 16,
+                                         0, 0);
+#pragma unroll
+      for (int i = 0; i < PERW; ++i)
+        __builtin_amdgcn_global_load_lds((g_ptr_t)(src_w[i] + koff),
+                                         (lds_ptr_t)(base + 128 * 128 + (wid * PERW + i) * 1024), 16, 0, 0);
+    };
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
+      for (int j = 0; j < NR; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const int n = k1 - k0;
+#pragma unroll
+    for (int s = 0; s < NSTAGE - 1; ++s)
+      if (s < n) stage(s, (int64_t)(k0 + s) * 128);
+
+    for (int kt = 0; kt < n; ++kt) {
+      // stage kt landed for this wave (NSTAGE-2 younger stages may stay in flight) ...
+      if (kt + NSTAGE - 2 < n) f8_vm_wait<(PER + PERW) * (NSTAGE - 2)>();
+      else f8_vm_wait<0>();
+      // ... and for every wave; every wave is also done reading stage kt-1's buffer
+      __builtin_amdgcn_s_barrier();
+      if (kt + NSTAGE - 1 < n) stage((kt + NSTAGE - 1) % NSTAGE, (int64_t)(k0 + kt + NSTAGE - 1) * 128);
+      const char* sA = smem + (kt % NSTAGE) * STAGE;
+      const char* sW = sA + 128 * 128;
+      u32x4_t fa[4][2], fb[NR][2];
+#pragma unroll
       for (int j = 0; j < NR; ++j) {
-        if constexpr (F8) {
-          const i32x8_t a8 = (i32x8_t){(int)fa[i][0][0], (int)fa[i][0][1], (int)fa[i][0][2], (int)fa[i][0][3],
-                                       (int)fa[i][1][0], (int)fa[i][1][1], (int)fa[i][1][2], (int)fa[i][1][3]};
-          const i32x8_t b8 = (i32x8_t){(int)fb[j][0][0], (int)fb[j][0][1], (int)fb[j][0][2], (int)fb[j][0][3],
-                                       (int)fb[j][1][0], (int)fb[j][1][1], (int)fb[j][1][2], (int)fb[j][1][3]};
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, acc[i][j], 0, 0, 0, 127, 0, 127);
-        } else {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[i][0]),
-                                                              __builtin_bit_cast(bf16x8_t, fb[j][0]), acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[i][1]),
-                                                              __builtin_bit_cast(bf16x8_t, fb[j][1]), acc[i][j], 0, 0, 0);
+        const int r = wn * TN + j * 16 + frow;
+        fb[j][0] = *(const u32x4_t*)(sW + swz(r, g));
+        fb[j][1] = *(const u32x4_t*)(sW + swz(r, g + 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 64 + i * 16 + frow;
+        fa[i][0] = *(const u32x4_t*)(sA + swz(r, g));
+        fa[i][1] = *(const u32x4_t*)(sA + swz(r, g + 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+          if constexpr (F8) {
+            const i32x8_t a8 = (i32x8_t){(int)fa[i][0][0], (int)fa[i][0][1], (int)fa[i][0][2], (int)fa[i][0][3],
+                                         (int)fa[i][1][0], (int)fa[i][1][1], (int)fa[i][1][2], (int)fa[i][1][3]};
+            const i32x8_t b8 = (i32x8_t){(int)fb[j][0][0], (int)fb[j][0][1], (int)fb[j][0][2], (int)fb[j][0][3],
+                                         (int)fb[j][1][0], (int)fb[j][1][1], (int)fb[j][1][2], (int)fb[j][1][3]};
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, acc[i][j], 0, 0, 0, 127, 0, 127);
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[i][0]),
+                                                                __builtin_bit_cast(bf16x8_t, fb[j][0]), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[i][1]),
+                                                                __builtin_bit_cast(bf16x8_t, fb[j][1]), acc[i][j], 0, 0, 0);
+          }
+        }
+    }
+    __syncthreads();   // every wave done with the stage buffers (the epilogue reuses them)
+  };
+
+  // ---- epilogue: per-wave 16-row slabs through LDS; lane -> (row, 16 columns)
+  auto epilogue = [&](const int m0, const int n0) {
+    constexpr int LDSTR = TN + 4;
+    constexpr int LPR = TN / 16;           // lanes per row
+    constexpr int RPP = 64 / LPR;          // rows per pass
+    constexpr int NPASS = RPP >= 16 ? 1 : 16 / RPP;
+    float* es = (float*)smem + wid * 16 * LDSTR;
+    const int cc = (lane % LPR) * 16;
+    const int n = n0 + wn * TN + cc;
+    float cs[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) cs[q] = n + q < N ? (sw ? sw[n + q] : 1.f) : 0.f;
+    const __amdgpu_buffer_rsrc_t crs = c_rsrc(C);
+    Unroll<0, 4>::run([&](const int i) {
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) es[(g * 4 + r) * LDSTR + j * 16 + frow] = acc[i][j][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int p = 0; p < NPASS; ++p) {
+        const int rr = p * RPP + lane / LPR;
+        if (rr >= 16) continue;
+        const int m = m0 + wm * 64 + i * 16 + rr;
+        const float rs = m < M ? (sa ? sa[m] : 1.f) : 0.f;
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cc + q * 4);
+          v[q * 4 + 0] = t[0] * rs * cs[q * 4 + 0];
+          v[q * 4 + 1] = t[1] * rs * cs[q * 4 + 1];
+          v[q * 4 + 2] = t[2] * rs * cs[q * 4 + 2];
+          v[q * 4 + 3] = t[3] * rs * cs[q * 4 + 3];
+        }
+        epi_store16_t<false>(v, m, n, M, N, C, ldc, ep, crs);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    });
+  };
+
+  if constexpr (!SK) {
+    // XCD-aware: consecutive logical tiles share a W column panel (row tiles fastest), and
+    // xcd_remap hands each XCD a contiguous run of them -> each W panel is read from HBM once
+    const int lin = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    const int tm = lin % tiles_m, tn = lin / tiles_m;
+    mainloop(tm * 128, tn * BN, 0, nk);
+    epilogue(tm * 128, tn * BN);
+  } else {
+    // logical workgroup l (consecutive l on one XCD) takes iterations [l * ipw, (l + 1) * ipw)
+    const int l = xcd_remap(blockIdx.x, gridDim.x);
+    const int total = tiles_m * tiles_n * nk;
+    int it = l * sk.ipw;
+    const int end = min(total, it + sk.ipw);
+    __shared__ int last_flag;
+    while (it < end) {
+      const int t = it / nk, k0 = it % nk, k1 = min(nk, k0 + (end - it));
+      const int tm = t % tiles_m, tn = t / tiles_m;
+      mainloop(tm * 128, tn * BN, k0, k1);
+      it += k1 - k0;
+      if (k0 != 0 || k1 != nk) {
+        const int first = (t * nk) / sk.ipw, lastw = ((t + 1) * nk - 1) / sk.ipw;
+        const int nc = lastw - first + 1;
+        float* slabs = sk.ws + (int64_t)t * sk.maxc * (128 * BN);
+        // accumulator-register layout: wave, fragment (i, j), lane -> 16 contiguous bytes
+        const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+            slabs + (int64_t)(l - first) * (128 * BN), (short)0, 128 * BN * 4, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, acc[i][j]), srs,
+                                                   (((wid * 4 + i) * NR + j) * 64 + lane) * 16, 0, 16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
+        __syncthreads();
+        if (tid == 0) {
+          const uint32_t prev = __hip_atomic_fetch_add(sk.cnt + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const bool last = prev == (uint32_t)(nc - 1);
+          if (last) {
+            __hip_atomic_store(sk.cnt + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          last_flag = last ? 1 : 0;
+        }
+        __syncthreads();
+        if (!last_flag) continue;
+        for (int c = 0; c < nc; ++c) {
+          if (c == l - first) continue;
+          const float* src = slabs + (int64_t)c * (128 * BN);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NR; ++j) {
+              const f32x4_t v = *(const f32x4_t*)(src + (((wid * 4 + i) * NR + j) * 64 + lane) * 4);
+              acc[i][j] += v;
+            }
         }
       }
-  }
-  __syncthreads();
-
-  // epilogue: per-wave 16-row slabs through LDS; lane -> (row, 16 columns)
-  constexpr int LDSTR = TN + 4;
-  constexpr int LPR = TN / 16;           // lanes per row
-  constexpr int RPP = 64 / LPR;          // rows per pass
-  constexpr int NPASS = RPP >= 16 ? 1 : 16 / RPP;
-  float* es = (float*)smem + wid * 16 * LDSTR;
-  const int cc = (lane % LPR) * 16;
-  const int n = n0 + wn * TN + cc;
-  float cs[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) cs[q] = n + q < N ? (sw ? sw[n + q] : 1.f) : 0.f;
-  const __amdgpu_buffer_rsrc_t crs = c_rsrc(C);
-  Unroll<0, 4>::run([&](const int i) {
-#pragma unroll
-    for (int j = 0; j < NR; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) es[(g * 4 + r) * LDSTR + j * 16 + frow] = acc[i][j][r];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int p = 0; p < NPASS; ++p) {
-      const int rr = p * RPP + lane / LPR;
-      if (rr >= 16) continue;
-      const int m = m0 + wm * 64 + i * 16 + rr;
-      const float rs = m < M ? (sa ? sa[m] : 1.f) : 0.f;
-      float v[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cc + q * 4);
-        v[q * 4 + 0] = t[0] * rs * cs[q * 4 + 0];
-        v[q * 4 + 1] = t[1] * rs * cs[q * 4 + 1];
-        v[q * 4 + 2] = t[2] * rs * cs[q * 4 + 2];
-        v[q * 4 + 3] = t[3] * rs * cs[q * 4 + 3];
-      }
-      epi_store16_t<false>(v, m, n, M, N, C, ldc, ep, crs);
+      epilogue(tm * 128, tn * BN);
+      __syncthreads();   // the epilogue's LDS slabs are free before the next tile's staging
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  });
+  }
 }
 
 template <int NS, int WN, bool F8 = true, int BN = 128>
@@ -219,7 +297,42 @@ static hipError_t launch_f8(const uint8_t* A, int64_t lda, const float* sa, cons
   }
   const int tiles = ((M + 127) / 128) * ((N + BN - 1) / BN);
   hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8, BN>), dim3(tiles, splits), dim3(128 * WN), lds, stream, A, lda, sa, W,
-                     ldw, sw, C, ldc, M, N, K, ep);
+                     ldw, sw, C, ldc, M, N, K, ep, SkArgs{});
+  return hipGetLastError();
+}
+
+// Stream-K launch (see SkArgs): grid = min(CUs, iterations), slabs / tickets in the stream's
+// workspace.  Returns hipErrorNotReady when no workspace is available (graph capture of a first
+// call): the caller falls back to the tiled launch.
+static uint32_t* sk_counters(size_t n, hipStream_t stream);
+static float* sk_slabs(size_t bytes, hipStream_t stream);
+static int f8_num_cus();
+
+template <int NS, int WN, bool F8 = true, int BN = 128>
+static hipError_t launch_f8_sk(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
+                               const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep,
+                               hipStream_t stream) {
+  constexpr int ES = F8 ? 1 : 2;
+  const int tiles = ((M + 127) / 128) * ((N + BN - 1) / BN);
+  const int nk = K * ES / 128;
+  const int total = tiles * nk;
+  const int grid = std::min(f8_num_cus(), total);
+  SkArgs sk{};
+  sk.ipw = (total + grid - 1) / grid;
+  sk.maxc = (nk + sk.ipw - 1) / sk.ipw + 1;
+  sk.ws = sk_slabs((size_t)tiles * sk.maxc * 128 * BN * sizeof(float), stream);
+  sk.cnt = sk_counters((size_t)tiles, stream);
+  if (sk.ws == nullptr || sk.cnt == nullptr) return hipErrorNotReady;
+  const size_t lds = (size_t)NS * (128 * 128 + BN * 128);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm_f8_kernel<NS, WN, F8, BN, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)lds);
+    attr = true;
+  }
+  const int used = (total + sk.ipw - 1) / sk.ipw;   // workgroups with work
+  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8, BN, true>), dim3(used), dim3(128 * WN), lds, stream, A, lda, sa, W, ldw,
+                     sw, C, ldc, M, N, K, ep, sk);
   return hipGetLastError();
 }
 
@@ -255,6 +368,14 @@ splitk_reduce16_kernel(const float* __restrict__ slabs, int S, int M, int N, voi
 
 static float* split_workspace(size_t bytes, hipStream_t stream) {
   return (float*)stream_workspace(bytes, stream, WS_F8_SPLIT, (size_t)32 << 20);
+}
+
+static float* sk_slabs(size_t bytes, hipStream_t stream) {
+  return (float*)stream_workspace(bytes, stream, WS_SK_SLAB, (size_t)16 << 20);
+}
+
+static uint32_t* sk_counters(size_t n, hipStream_t stream) {
+  return (uint32_t*)stream_workspace(n * sizeof(uint32_t), stream, WS_SK_CNT, 65536, true);
 }
 
 static int f8_num_cus() {
@@ -318,12 +439,21 @@ static hipError_t launch_f8_split(const uint8_t* A, int64_t lda, const float* sa
 // change, so not TLB-bound) and a software-pipelined loop (fragments of step k + 1 read during the
 // MFMAs of step k: no change); every shape runs ~0.53 us per 128-byte K-step + ~7 us per launch
 // (profiles/r4_cold_gemm_blocked_sp_v1.txt, r4_f8_gemm_time_vs_k_v1.txt).
+//   9 = stream-K <3, 8, 128>   10 = stream-K <4, 4, 128>   11 = stream-K <4, 8, 128>
 static int variant_bn(int v) { return v == 6 || v == 7 ? 256 : 128; }
 
 template <bool F8>
 static hipError_t launch_variant(int v, const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
                                  const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, int S,
                                  hipStream_t stream) {
+  if (v >= 9 && v <= 11 && ep.split_koff == 0) {
+    hipError_t e = v == 9 ? launch_f8_sk<3, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream)
+                 : v == 10 ? launch_f8_sk<4, 2, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream)
+                           : launch_f8_sk<4, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    if (e != hipErrorNotReady) return e;
+    v = 2;      // no workspace (first call inside a graph capture): the tiled pipeline
+    S = 1;
+  }
   if (S > 1) {
     switch (v) {
       case 1: return launch_f8_split<2, 2, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);

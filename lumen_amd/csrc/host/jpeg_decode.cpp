@@ -1,0 +1,623 @@
+// Parallel baseline-JPEG entropy decoder (host runtime, C ABI for ctypes).
+//
+// Replaces the single-threaded libjpeg-turbo decode (via Pillow) that the reference runs per
+// request (packages/lumen-vlm/src/lumen_vlm/backends/onnxrt_backend.py:661-665,
+// packages/lumen-clip/src/lumen_clip/backends/onnxrt_backend.py:478).  On a high-entropy photo
+// most of libjpeg's time is the Huffman decode (a 687 KiB noise JPEG: 80 % of its decode time
+// even at 1/8 DCT scale), which is sequential by construction.  Here it is split over the
+// cores; the dequantise + IDCT + chroma upsampling + colour conversion run on the GPU
+// (csrc/jpeg.hip) from the coefficient planes this file produces.
+//
+// Without restart markers the bitstream has no known symbol boundaries, so every chunk of
+// the (unstuffed) entropy-coded segment is first decoded SPECULATIVELY from its first bit,
+// guessing "start of an MCU", recording every block boundary (bit position, block phase
+// inside the MCU) it passes.  Huffman codes self-synchronise: an exact decode entering the
+// chunk (from the previous chunk's exact end) soon lands on one of those recorded
+// boundaries, and from there the speculative blocks are the true ones.  The sequential
+// fix-up pass therefore only re-decodes the few blocks before that meeting point; a chunk
+// that never synchronises is simply decoded exactly (correct, just serial).  With restart
+// markers (DRI) the restart intervals are decoded independently.
+//
+// Coefficients land de-zigzagged, not dequantised, in per-component planes
+// [blocks_h][blocks_w][64] int16 (padded to whole MCUs), DC already integrated.
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace {
+
+const int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+                         41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+                         30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+constexpr int kFast = 10;   // lookahead bits of the fast tables
+
+struct Huff {
+  uint16_t fast[1 << kFast];   // (length << 8) | symbol for codes of <= kFast bits, 0 = slow path
+  // AC only: code AND its extra bits within the lookahead -> the coefficient in one step:
+  // (value << 16) | (run << 12) | (total length << 4) | 1, 0 = not in the lookahead
+  int32_t fast_ac[1 << kFast];
+  int32_t maxcode[18];
+  int32_t valptr[17];
+  int32_t mincode[17];
+  uint8_t vals[256];
+  bool present = false;
+};
+
+struct Comp {
+  int id, h, v, tq, td, ta;
+  int bw, bh;   // blocks per row / column (whole MCUs)
+};
+
+struct Jpeg {
+  int width = 0, height = 0, ncomp = 0, hmax = 1, vmax = 1, restart = 0;
+  int mcux = 0, mcuy = 0;
+  bool progressive = false, supported = true;
+  Comp comp[4];
+  uint16_t qt[4][64];   // natural order
+  Huff dc[4], ac[4];
+  int scan_ncomp = 0, scan_comp[4];
+  size_t ecs_begin = 0, ecs_end = 0;   // entropy-coded segment in the input
+};
+
+void build_huff(Huff& h, const uint8_t* counts, const uint8_t* vals, int nvals) {
+  memset(h.fast, 0, sizeof(h.fast));
+  memcpy(h.vals, vals, nvals);
+  int code = 0, k = 0;
+  for (int l = 1; l <= 16; ++l) {
+    h.valptr[l] = k;
+    h.mincode[l] = code;
+    code += counts[l - 1];
+    k += counts[l - 1];
+    h.maxcode[l] = counts[l - 1] ? code - 1 : -1;
+    code <<= 1;
+  }
+  h.maxcode[17] = 0x7fffffff;
+  // fast tables
+  memset(h.fast_ac, 0, sizeof(h.fast_ac));
+  code = 0;
+  k = 0;
+  for (int l = 1; l <= kFast; ++l) {
+    for (int i = 0; i < counts[l - 1]; ++i, ++k, ++code) {
+      const int shift = kFast - l;
+      const int rs = vals[k], run = rs >> 4, sz = rs & 15;
+      for (int j = 0; j < (1 << shift); ++j) {
+        const int idx = (code << shift) | j;
+        h.fast[idx] = (uint16_t)((l << 8) | rs);
+        if (sz != 0 && l + sz <= kFast) {
+          const int extra = (j >> (shift - sz)) & ((1 << sz) - 1);
+          const int v = extra < (1 << (sz - 1)) ? extra - (1 << sz) + 1 : extra;
+          h.fast_ac[idx] = (int32_t)((uint32_t)(v & 0xFFFF) << 16) | (run << 12) | ((l + sz) << 4) | 1;
+        }
+      }
+    }
+    code <<= 1;
+  }
+  h.present = true;
+}
+
+inline int read16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
+
+// 0 ok, 1 unsupported, -1 malformed
+int parse(const uint8_t* d, size_t n, Jpeg& J) {
+  if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) return -1;
+  size_t i = 2;
+  bool sof = false;
+  while (i + 4 <= n) {
+    if (d[i] != 0xFF) return -1;
+    int m = d[i + 1];
+    if (m == 0xFF) { ++i; continue; }
+    if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) { i += 2; continue; }
+    const int L = read16(d + i + 2);
+    if (i + 2 + (size_t)L > n || L < 2) return -1;
+    const uint8_t* s = d + i + 4;
+    const int sl = L - 2;
+    if (m == 0xC0 || m == 0xC1) {          // baseline / extended sequential Huffman
+      if (sl < 6) return -1;
+      if (s[0] != 8) return 1;             // 12-bit
+      J.height = read16(s + 1);
+      J.width = read16(s + 3);
+      J.ncomp = s[5];
+      if (J.ncomp != 1 && J.ncomp != 3) return 1;
+      if (sl < 6 + 3 * J.ncomp || J.width <= 0 || J.height <= 0) return -1;
+      for (int c = 0; c < J.ncomp; ++c) {
+        J.comp[c].id = s[6 + 3 * c];
+        J.comp[c].h = s[7 + 3 * c] >> 4;
+        J.comp[c].v = s[7 + 3 * c] & 15;
+        J.comp[c].tq = s[8 + 3 * c] & 3;
+        if (J.comp[c].h < 1 || J.comp[c].h > 2 || J.comp[c].v < 1 || J.comp[c].v > 2) return 1;
+        J.hmax = std::max(J.hmax, J.comp[c].h);
+        J.vmax = std::max(J.vmax, J.comp[c].v);
+      }
+      sof = true;
+    } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+      return 1;                            // progressive / lossless / arithmetic
+    } else if (m == 0xC4) {                // DHT
+      int o = 0;
+      while (o + 17 <= sl) {
+        const int tc = s[o] >> 4, th = s[o] & 15;
+        if (th > 3 || tc > 1) return -1;
+        int tot = 0;
+        for (int l = 0; l < 16; ++l) tot += s[o + 1 + l];
+        if (tot > 256 || o + 17 + tot > sl) return -1;
+        build_huff(tc == 0 ? J.dc[th] : J.ac[th], s + o + 1, s + o + 17, tot);
+        o += 17 + tot;
+      }
+    } else if (m == 0xDB) {                // DQT
+      int o = 0;
+      while (o < sl) {
+        const int pq = s[o] >> 4, tq = s[o] & 15;
+        if (tq > 3) return -1;
+        if (pq == 0) {
+          if (o + 65 > sl) return -1;
+          for (int k = 0; k < 64; ++k) J.qt[tq][kZigzag[k]] = s[o + 1 + k];
+          o += 65;
+        } else {
+          if (o + 129 > sl) return -1;
+          for (int k = 0; k < 64; ++k) J.qt[tq][kZigzag[k]] = (uint16_t)read16(s + o + 1 + 2 * k);
+          o += 129;
+        }
+      }
+    } else if (m == 0xDD) {                // DRI
+      if (sl < 2) return -1;
+      J.restart = read16(s);
+    } else if (m == 0xDA) {                // SOS: the one scan of a sequential image
+      if (!sof) return -1;
+      J.scan_ncomp = s[0];
+      if (J.scan_ncomp != J.ncomp) return 1;   // multi-scan sequential files: not handled here
+      for (int k = 0; k < J.scan_ncomp; ++k) {
+        const int cid = s[1 + 2 * k];
+        int ci = -1;
+        for (int c = 0; c < J.ncomp; ++c)
+          if (J.comp[c].id == cid) ci = c;
+        if (ci < 0) return -1;
+        J.scan_comp[k] = ci;
+        J.comp[ci].td = s[2 + 2 * k] >> 4;
+        J.comp[ci].ta = s[2 + 2 * k] & 15;
+        if (J.comp[ci].td > 3 || J.comp[ci].ta > 3 || !J.dc[J.comp[ci].td].present || !J.ac[J.comp[ci].ta].present)
+          return -1;
+      }
+      J.ecs_begin = i + 2 + L;
+      // the segment runs to the first marker that is not a stuffed 0xFF00 or an RSTn
+      size_t e = J.ecs_begin;
+      while (e + 1 < n) {
+        if (d[e] == 0xFF && d[e + 1] != 0x00 && !(d[e + 1] >= 0xD0 && d[e + 1] <= 0xD7)) break;
+        ++e;
+      }
+      J.ecs_end = e;
+      break;
+    }
+    i += 2 + L;
+  }
+  if (!sof || J.ecs_end <= J.ecs_begin) return -1;
+  if (J.ncomp == 1) {   // a single-component scan is not interleaved: 8x8 MCUs
+    J.comp[0].h = J.comp[0].v = J.hmax = J.vmax = 1;
+  }
+  J.mcux = (J.width + 8 * J.hmax - 1) / (8 * J.hmax);
+  J.mcuy = (J.height + 8 * J.vmax - 1) / (8 * J.vmax);
+  for (int c = 0; c < J.ncomp; ++c) {
+    J.comp[c].bw = J.mcux * J.comp[c].h;
+    J.comp[c].bh = J.mcuy * J.comp[c].v;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------- bitstream
+struct Stream {
+  std::vector<uint8_t> bytes;      // unstuffed, + kPad zero bytes (one block's worst-case read)
+  std::vector<size_t> seg_bits;    // restart-interval starts (bit offsets), seg_bits[0] = 0
+  size_t nbits = 0;
+};
+
+constexpr size_t kPad = 512;
+
+void unstuff(const uint8_t* d, size_t b, size_t e, Stream& S) {
+  S.bytes.resize(e - b + kPad);
+  uint8_t* out = S.bytes.data();
+  size_t o = 0;
+  S.seg_bits.push_back(0);
+  size_t i = b;
+  while (i < e) {
+    const uint8_t* ff = static_cast<const uint8_t*>(memchr(d + i, 0xFF, e - i));
+    const size_t run = ff ? (size_t)(ff - (d + i)) : e - i;
+    memcpy(out + o, d + i, run);
+    o += run;
+    i += run;
+    if (i >= e) break;
+    // d[i] == 0xFF
+    if (i + 1 < e && d[i + 1] == 0x00) {
+      out[o++] = 0xFF;
+      i += 2;
+    } else if (i + 1 < e && d[i + 1] >= 0xD0 && d[i + 1] <= 0xD7) {
+      S.seg_bits.push_back(o * 8);
+      i += 2;
+    } else {
+      out[o++] = 0xFF;
+      ++i;
+    }
+  }
+  S.nbits = o * 8;
+  S.bytes.resize(o + kPad);
+  memset(S.bytes.data() + o, 0, kPad);
+}
+
+inline uint64_t peek64(const uint8_t* p, size_t pos) {
+  uint64_t w;
+  memcpy(&w, p + (pos >> 3), 8);
+  w = __builtin_bswap64(w);
+  return w << (pos & 7);
+}
+
+inline int decode_slow(const Huff& h, uint64_t w, size_t& pos) {
+  for (int l = kFast + 1; l <= 16; ++l) {
+    const int code = (int)(w >> (64 - l));
+    if (code <= h.maxcode[l]) {
+      pos += l;
+      return h.vals[h.valptr[l] + code - h.mincode[l]];
+    }
+  }
+  return -1;
+}
+
+inline int decode_sym(const Huff& h, const uint8_t* p, size_t& pos) {
+  const uint64_t w = peek64(p, pos);
+  const uint16_t f = h.fast[w >> (64 - kFast)];
+  if (f) {
+    pos += f >> 8;
+    return f & 0xFF;
+  }
+  return decode_slow(h, w, pos);
+}
+
+inline int extend(uint32_t v, int s) { return v < (1u << (s - 1)) ? (int)v - (1 << s) + 1 : (int)v; }
+
+inline uint32_t getbits(const uint8_t* p, size_t& pos, int s) {
+  const uint32_t v = (uint32_t)(peek64(p, pos) >> (64 - s));
+  pos += s;
+  return v;
+}
+
+// one block (DC diff in out[0]); false on an invalid code or a coefficient run past 63
+inline bool decode_block(const uint8_t* p, size_t& pos, const Huff& dc, const Huff& ac, int16_t* out) {
+  memset(out, 0, 64 * sizeof(int16_t));
+  int s = decode_sym(dc, p, pos);
+  if (s < 0 || s > 11) return false;
+  out[0] = (int16_t)(s ? extend(getbits(p, pos, s), s) : 0);
+  for (int k = 1; k < 64;) {
+    const uint64_t w = peek64(p, pos);
+    const int32_t fa = ac.fast_ac[w >> (64 - kFast)];
+    if (fa) {   // code + extra bits in the lookahead
+      k += (fa >> 12) & 15;
+      if (k > 63) return false;
+      out[kZigzag[k]] = (int16_t)(fa >> 16);
+      pos += (fa >> 4) & 31;
+      ++k;
+      continue;
+    }
+    const uint16_t f = ac.fast[w >> (64 - kFast)];
+    int rs;
+    if (f) {
+      pos += f >> 8;
+      rs = f & 0xFF;
+    } else {
+      rs = decode_slow(ac, w, pos);
+    }
+    if (rs < 0) return false;
+    const int r = rs >> 4, sz = rs & 15;
+    if (sz == 0) {
+      if (r != 15) break;   // EOB
+      k += 16;
+      continue;
+    }
+    k += r;
+    if (k > 63) return false;
+    out[kZigzag[k]] = (int16_t)extend(getbits(p, pos, sz), sz);
+    ++k;
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------- thread pool
+class Pool {
+ public:
+  explicit Pool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] { run(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return (int)th_.size(); }
+  // f(i) for i in [0, n), the calling thread helping; returns when all are done.  Concurrent
+  // callers (several request threads) take turns.
+  void parallel_for(int n, const std::function<void(int)>& f) {
+    std::lock_guard<std::mutex> turn(run_mu_);
+    std::atomic<int> next{0}, done{0};
+    auto work = [&] {
+      for (int i; (i = next.fetch_add(1)) < n;) {
+        f(i);
+        done.fetch_add(1);
+      }
+    };
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = work;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    while (done.load() < n) std::this_thread::yield();
+    std::lock_guard<std::mutex> g(mu_);
+    job_ = nullptr;
+  }
+
+ private:
+  void run() {
+    uint64_t seen = 0;
+    for (;;) {
+      std::function<void()> job;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || (gen_ != seen && job_); });
+        if (stop_) return;
+        seen = gen_;
+        job = job_;
+      }
+      job();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex run_mu_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::function<void()> job_;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+std::mutex g_pool_mu;
+Pool* g_pool = nullptr;
+
+// created once, with the first caller's thread count (never resized: a resize would tear
+// down threads another request may be using)
+Pool& pool(int want) {
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  if (g_pool == nullptr) g_pool = new Pool(std::max(0, want - 1));
+  return *g_pool;
+}
+
+// ---------------------------------------------------------------------------- decode
+struct Layout {
+  int bpm = 1;                 // blocks per MCU
+  int pcomp[10], ph[10], pv[10];
+  size_t plane_off[4];         // element offset of each component plane in the coefficient buffer
+};
+
+Layout make_layout(const Jpeg& J) {
+  Layout L;
+  int k = 0;
+  for (int s = 0; s < J.scan_ncomp; ++s) {
+    const int c = J.scan_comp[s];
+    for (int v = 0; v < J.comp[c].v; ++v)
+      for (int h = 0; h < J.comp[c].h; ++h) {
+        L.pcomp[k] = c;
+        L.ph[k] = h;
+        L.pv[k] = v;
+        ++k;
+      }
+  }
+  L.bpm = k;
+  size_t off = 0;
+  for (int c = 0; c < J.ncomp; ++c) {
+    L.plane_off[c] = off;
+    off += (size_t)J.comp[c].bw * J.comp[c].bh * 64;
+  }
+  return L;
+}
+
+// decode-order block index -> its coefficient block in the planes
+inline int16_t* block_ptr(const Jpeg& J, const Layout& L, int16_t* coefs, int64_t b) {
+  const int64_t mcu = b / L.bpm;
+  const int ph = (int)(b % L.bpm);
+  const int c = L.pcomp[ph];
+  const int my = (int)(mcu / J.mcux), mx = (int)(mcu % J.mcux);
+  const int row = my * J.comp[c].v + L.pv[ph], col = mx * J.comp[c].h + L.ph[ph];
+  return coefs + L.plane_off[c] + ((size_t)row * J.comp[c].bw + col) * 64;
+}
+
+struct Boundary {
+  size_t pos;
+  int phase;
+  int nb;   // blocks decoded (into the chunk's buffer) before this boundary
+};
+
+struct Chunk {
+  size_t start, end;
+  std::vector<int16_t> blk;      // speculative blocks, 64 each
+  std::vector<Boundary> marks;   // block boundaries passed
+  Boundary fin{};                // first boundary at / after `end` (or where decoding stopped)
+  // fix-up results
+  std::vector<int16_t> pre;      // exact blocks decoded before the meeting point
+  int take_from = 0, take_to = 0;   // speculative blocks [take_from, take_to) are exact
+  int count = 0;                 // exact blocks this chunk contributes
+};
+
+void speculate(const Jpeg& J, const Layout& L, const uint8_t* p, Chunk& C, int64_t max_blocks) {
+  size_t pos = C.start;
+  int phase = 0;
+  int16_t tmp[64];
+  C.blk.reserve(((C.end - C.start) / 16 + 16) * 64);
+  while (pos < C.end) {
+    C.marks.push_back({pos, phase, (int)(C.blk.size() / 64)});
+    if ((int64_t)(C.blk.size() / 64) >= max_blocks) break;
+    const Comp& cp = J.comp[L.pcomp[phase]];
+    const size_t p0 = pos;
+    if (!decode_block(p, pos, J.dc[cp.td], J.ac[cp.ta], tmp)) {
+      pos = p0 + 1;   // garbage: slide one bit, guess an MCU start again
+      phase = 0;
+      continue;
+    }
+    C.blk.insert(C.blk.end(), tmp, tmp + 64);
+    phase = phase + 1 == L.bpm ? 0 : phase + 1;
+  }
+  C.fin = {pos, phase, (int)(C.blk.size() / 64)};
+}
+
+}  // namespace
+
+extern "C" {
+
+// info: [w, h, ncomp, hmax, vmax, restart, mcux, mcuy, (h, v, bw, bh, tq) x ncomp]
+// returns 0 ok, 1 unsupported (progressive / arithmetic / 12-bit / CMYK / multi-scan), -1 malformed
+int lumen_jpeg_info(const uint8_t* data, uint64_t len, int* info) {
+  Jpeg J;
+  const int r = parse(data, (size_t)len, J);
+  if (r != 0) return r;
+  info[0] = J.width; info[1] = J.height; info[2] = J.ncomp; info[3] = J.hmax; info[4] = J.vmax;
+  info[5] = J.restart; info[6] = J.mcux; info[7] = J.mcuy;
+  for (int c = 0; c < J.ncomp; ++c) {
+    info[8 + 5 * c] = J.comp[c].h; info[9 + 5 * c] = J.comp[c].v; info[10 + 5 * c] = J.comp[c].bw;
+    info[11 + 5 * c] = J.comp[c].bh; info[12 + 5 * c] = J.comp[c].tq;
+  }
+  return 0;
+}
+
+// Entropy-decode into coefs (sum over components of bw * bh * 64 int16, zero-filled by the caller
+// is not required) and the components' quantisation tables qt [ncomp][64] (natural order).
+// nthreads <= 1: sequential.  stats (nullable) [chunks, resynced, serial_blocks, total_blocks].
+// Returns 0 ok, 1 unsupported, -1 malformed / truncated.
+int lumen_jpeg_decode_coefs(const uint8_t* data, uint64_t len, int nthreads, int16_t* coefs, uint16_t* qt,
+                            int64_t* stats) {
+  Jpeg J;
+  const int r = parse(data, (size_t)len, J);
+  if (r != 0) return r;
+  const Layout L = make_layout(J);
+  for (int c = 0; c < J.ncomp; ++c) memcpy(qt + 64 * c, J.qt[J.comp[c].tq], 64 * sizeof(uint16_t));
+  Stream S;
+  unstuff(data, J.ecs_begin, J.ecs_end, S);
+  const uint8_t* p = S.bytes.data();
+  const int64_t total = (int64_t)J.mcux * J.mcuy * L.bpm;
+  int64_t st[4] = {0, 0, 0, total};
+  std::vector<int16_t> dcdiff;   // decode order DC differences are integrated at the end
+
+  if (J.restart > 0 && S.seg_bits.size() > 1) {
+    // restart intervals: independent segments, DC predictors reset at each
+    const int nseg = (int)S.seg_bits.size();
+    const int64_t per = (int64_t)J.restart * L.bpm;
+    std::atomic<int> bad{0};
+    auto seg = [&](int s) {
+      size_t pos = S.seg_bits[s];
+      int64_t b0 = (int64_t)s * per, b1 = std::min(total, b0 + per);
+      int pred[4] = {0, 0, 0, 0};
+      for (int64_t b = b0; b < b1; ++b) {
+        const int ph = (int)(b % L.bpm);
+        const Comp& cp = J.comp[L.pcomp[ph]];
+        int16_t* out = block_ptr(J, L, coefs, b);
+        if (pos > S.nbits || !decode_block(p, pos, J.dc[cp.td], J.ac[cp.ta], out)) { bad.store(1); return; }
+        pred[L.pcomp[ph]] += out[0];
+        out[0] = (int16_t)pred[L.pcomp[ph]];
+      }
+    };
+    if (nthreads > 1) pool(nthreads).parallel_for(nseg, seg);
+    else for (int s = 0; s < nseg; ++s) seg(s);
+    st[0] = nseg;
+    if (stats) memcpy(stats, st, sizeof(st));
+    return bad.load() ? -1 : 0;
+  }
+
+  // no restart markers: speculative chunks + sequential fix-up + parallel placement
+  const size_t nbits = S.nbits;
+  int nch = nthreads > 1 ? std::min<int64_t>(4 * nthreads, (int64_t)(nbits / 4096) + 1) : 1;
+  nch = std::max(nch, 1);
+  std::vector<Chunk> ch(nch);
+  for (int i = 0; i < nch; ++i) {
+    ch[i].start = nbits * i / nch;
+    ch[i].end = nbits * (i + 1) / nch;
+  }
+  auto spec = [&](int i) { speculate(J, L, p, ch[i], total); };
+  if (nch > 1) pool(nthreads).parallel_for(nch, spec);
+  else spec(0);
+  // chunk 0 started at the true start: exact as it stands
+  ch[0].take_from = 0;
+  ch[0].take_to = ch[0].fin.nb;
+  ch[0].count = ch[0].fin.nb;
+  size_t pos = ch[0].fin.pos;
+  int phase = ch[0].fin.phase;
+  int64_t done = ch[0].count;
+  int16_t tmp[64];
+  for (int i = 1; i < nch && done < total; ++i) {
+    Chunk& C = ch[i];
+    size_t m = 0;   // first mark at / after pos
+    while (m < C.marks.size() && C.marks[m].pos < pos) ++m;
+    bool synced = false;
+    for (;;) {
+      while (m < C.marks.size() && C.marks[m].pos < pos) ++m;
+      if (m < C.marks.size() && C.marks[m].pos == pos && C.marks[m].phase == phase) { synced = true; break; }
+      if (pos >= C.end || done >= total) break;
+      const Comp& cp = J.comp[L.pcomp[phase]];
+      if (!decode_block(p, pos, J.dc[cp.td], J.ac[cp.ta], tmp)) return -1;   // the exact decode failed
+      C.pre.insert(C.pre.end(), tmp, tmp + 64);
+      ++done;
+      phase = phase + 1 == L.bpm ? 0 : phase + 1;
+      ++st[2];
+    }
+    if (synced) {
+      ++st[1];
+      C.take_from = C.marks[m].nb;
+      C.take_to = C.fin.nb;
+      const int64_t room = total - done;
+      if (C.take_to - C.take_from > room) C.take_to = C.take_from + (int)room;
+      done += C.take_to - C.take_from;
+      pos = C.fin.pos;
+      phase = C.fin.phase;
+    }
+    C.count = (int)(C.pre.size() / 64) + (C.take_to - C.take_from);
+  }
+  // blocks past the last chunk (should not happen: the last chunk ends at the stream's end)
+  std::vector<int16_t> tail;
+  while (done < total) {
+    if (pos >= nbits) return -1;
+    const Comp& cp = J.comp[L.pcomp[phase]];
+    if (!decode_block(p, pos, J.dc[cp.td], J.ac[cp.ta], tmp)) return -1;
+    tail.insert(tail.end(), tmp, tmp + 64);
+    ++done;
+    phase = phase + 1 == L.bpm ? 0 : phase + 1;
+    ++st[2];
+  }
+  // placement (parallel), then the DC integration in decode order (sequential, cheap)
+  std::vector<int64_t> base(nch + 1, 0);
+  for (int i = 0; i < nch; ++i) base[i + 1] = base[i] + ch[i].count;
+  const int64_t tail0 = base[nch];
+  auto place = [&](int i) {
+    const Chunk& C = ch[i];
+    int64_t b = base[i];
+    const int npre = (int)(C.pre.size() / 64);
+    for (int k = 0; k < npre; ++k, ++b) memcpy(block_ptr(J, L, coefs, b), &C.pre[64 * k], 128);
+    for (int k = C.take_from; k < C.take_to; ++k, ++b) memcpy(block_ptr(J, L, coefs, b), &C.blk[64 * (size_t)k], 128);
+  };
+  if (nch > 1) pool(nthreads).parallel_for(nch, place);
+  else place(0);
+  for (size_t k = 0; k < tail.size() / 64; ++k) memcpy(block_ptr(J, L, coefs, tail0 + (int64_t)k), &tail[64 * k], 128);
+  int pred[4] = {0, 0, 0, 0};
+  for (int64_t b = 0; b < total; ++b) {
+    const int c = L.pcomp[b % L.bpm];
+    int16_t* out = block_ptr(J, L, coefs, b);
+    pred[c] += out[0];
+    out[0] = (int16_t)pred[c];
+  }
+  st[0] = nch;
+  if (stats) memcpy(stats, st, sizeof(st));
+  return 0;
+}
+
+}  // extern "C"

@@ -15,6 +15,13 @@ hipError_t db_components(const void* prob, int is_bf16, const float* thresh, int
 hipError_t db_quad_score(const void* prob, int is_bf16, int n, int H, int W, const float* quads, const int* img, float* score,
                          double* pre,
                          int m, hipStream_t stream);
+struct JpegPlanes {
+  const int16_t* coef; const uint16_t* qt; uint8_t* samp;
+  int64_t coef_off[3], samp_off[3];
+  int bw[3], bh[3], h[3], v[3];
+  int ncomp, hmax, vmax, width, height;
+};
+hipError_t jpeg_reconstruct(const JpegPlanes& P, uint8_t* out, hipStream_t stream);
 }  // namespace lumen
 
 namespace {
@@ -176,9 +183,48 @@ void db_quad_score(const at::Tensor& prob, const at::Tensor& quads, const at::Te
                                   score.data_ptr<float>(), pre.data_ptr<double>(), (int)m, stream()));
 }
 
+// JPEG pixels from entropy-decoded coefficient planes (host/jpeg_decode.cpp): coef int16 (all
+// planes), qt uint16 [ncomp, 64], meta [ncomp, hmax, vmax, width, height, (h, v, bw, bh) x ncomp],
+// samp uint8 scratch (sum of bw * bh * 64), out uint8 [height, width, 3].
+void jpeg_reconstruct(const at::Tensor& coef, const at::Tensor& qt, at::IntArrayRef meta, at::Tensor samp,
+                      at::Tensor out) {
+  TORCH_CHECK(coef.is_cuda() && coef.scalar_type() == at::kShort && coef.is_contiguous(), "jpeg: coef int16");
+  TORCH_CHECK(qt.is_cuda() && qt.scalar_type() == at::kShort && qt.is_contiguous(), "jpeg: qt int16 (uint16 bits)");
+  TORCH_CHECK(samp.is_cuda() && samp.scalar_type() == at::kByte && samp.is_contiguous(), "jpeg: samp uint8");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kByte && out.is_contiguous(), "jpeg: out uint8");
+  TORCH_CHECK(meta.size() >= 5, "jpeg: meta");
+  lumen::JpegPlanes P{};
+  P.ncomp = (int)meta[0];
+  P.hmax = (int)meta[1];
+  P.vmax = (int)meta[2];
+  P.width = (int)meta[3];
+  P.height = (int)meta[4];
+  TORCH_CHECK((P.ncomp == 1 || P.ncomp == 3) && (int64_t)meta.size() == 5 + 4 * P.ncomp, "jpeg: meta size");
+  TORCH_CHECK(out.numel() == (int64_t)P.width * P.height * 3, "jpeg: out must be [height, width, 3]");
+  int64_t co = 0;
+  for (int c = 0; c < P.ncomp; ++c) {
+    P.h[c] = (int)meta[5 + 4 * c];
+    P.v[c] = (int)meta[6 + 4 * c];
+    P.bw[c] = (int)meta[7 + 4 * c];
+    P.bh[c] = (int)meta[8 + 4 * c];
+    TORCH_CHECK(P.bw[c] * 8 >= (P.width * P.h[c] + P.hmax - 1) / P.hmax &&
+                P.bh[c] * 8 >= (P.height * P.v[c] + P.vmax - 1) / P.vmax, "jpeg: plane smaller than the image");
+    P.coef_off[c] = co;
+    P.samp_off[c] = co;
+    co += (int64_t)P.bw[c] * P.bh[c] * 64;
+  }
+  TORCH_CHECK(coef.numel() >= co && samp.numel() >= co && qt.numel() >= 64 * P.ncomp, "jpeg: buffer sizes");
+  P.coef = coef.data_ptr<int16_t>();
+  P.qt = reinterpret_cast<const uint16_t*>(qt.data_ptr<int16_t>());
+  P.samp = samp.data_ptr<uint8_t>();
+  const at::DeviceGuard g(coef.device());
+  CHECK_HIP2(lumen::jpeg_reconstruct(P, out.data_ptr<uint8_t>(), stream()));
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(lumen, m) {
+  m.def("jpeg_reconstruct(Tensor coef, Tensor qt, int[] meta, Tensor(s!) samp, Tensor(o!) out) -> ()");
   m.def("db_components(Tensor prob, Tensor thresh, Tensor(l!) lab, Tensor(o!) out, Tensor(c!) count, "
         "int min_size) -> ()");
   m.def("db_quad_score(Tensor prob, Tensor quads, Tensor img, Tensor(s!) score) -> ()");
@@ -195,6 +241,7 @@ TORCH_LIBRARY_FRAGMENT(lumen, m) {
 }
 
 TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
+  m.impl("jpeg_reconstruct", &jpeg_reconstruct);
   m.impl("det_decode", &det_decode);
   m.impl("nms", &nms);
   m.impl("warp_batch", &warp_batch);

@@ -17,9 +17,10 @@
 
 namespace lumen {
 
-enum WorkspaceTag : int { WS_F8_SPLIT = 0, WS_PP_TAIL = 1 };
+enum WorkspaceTag : int { WS_F8_SPLIT = 0, WS_PP_TAIL = 1, WS_SK_SLAB = 2, WS_SK_CNT = 3 };
 
-inline void* stream_workspace(size_t bytes, hipStream_t stream, int tag, size_t min_bytes) {
+// zero: a fresh allocation is zero-filled on the stream (arrival counters)
+inline void* stream_workspace(size_t bytes, hipStream_t stream, int tag, size_t min_bytes, bool zero = false) {
   struct Slot {
     void* p = nullptr;
     size_t cap = 0;
@@ -52,6 +53,10 @@ inline void* stream_workspace(size_t bytes, hipStream_t stream, int tag, size_t 
   void* p = nullptr;
   const size_t want = bytes < min_bytes ? min_bytes : bytes;
   if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+  if (zero && hipMemsetAsync(p, 0, want, stream) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
   s.p = p;
   s.cap = want;
   return p;

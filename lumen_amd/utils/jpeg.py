@@ -1,0 +1,213 @@
+"""Device-side JPEG decode (K1): parallel host entropy decode + GPU pixel reconstruction.
+
+The reference decodes every image with Pillow on one CPU thread
+(packages/lumen-vlm/src/lumen_vlm/backends/onnxrt_backend.py:661-665,
+packages/lumen-clip/src/lumen_clip/backends/onnxrt_backend.py:478,
+packages/lumen-face/src/lumen_face/backends/onnxrt_backend.py:716-723).  Here a baseline JPEG is
+
+1. entropy-decoded by ``csrc/host/jpeg_decode.cpp`` over a pool of host threads (speculative
+   chunks re-synchronised on block boundaries; restart intervals in parallel when present) into
+   int16 coefficient planes, then
+2. uploaded (one pinned H2D) and turned into pixels on the GPU by ``csrc/jpeg.hip``
+   (dequantise, 8x8 IDCT, libjpeg "fancy" chroma upsampling, libjpeg's YCbCr -> RGB).
+
+:func:`decode_to_device` returns a uint8 [H, W, 3] tensor on the device, ready for
+``ops.image_prep``.  Anything else -- PNG / WebP, progressive or arithmetic JPEGs, CMYK --
+falls back to Pillow (:func:`lumen_amd.utils.image.decode_rgb`) plus an upload.
+:func:`reconstruct_reference` is the NumPy form of step 2 (CPU path and test oracle).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from .._native import load_host
+
+_lock = threading.Lock()
+_typed = False
+
+
+def _lib():
+    global _typed
+    lib = load_host()
+    if lib is None or not hasattr(lib, "lumen_jpeg_decode_coefs"):
+        return None
+    if not _typed:
+        with _lock:
+            lib.lumen_jpeg_info.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int)]
+            lib.lumen_jpeg_info.restype = ctypes.c_int
+            lib.lumen_jpeg_decode_coefs.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
+                                                    ctypes.c_void_p, ctypes.c_void_p]
+            lib.lumen_jpeg_decode_coefs.restype = ctypes.c_int
+            _typed = True
+    return lib
+
+
+def default_threads() -> int:
+    env = os.environ.get("LUMEN_JPEG_THREADS")
+    if env:
+        return max(1, int(env))
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+@dataclass
+class JpegInfo:
+    width: int
+    height: int
+    ncomp: int
+    hmax: int
+    vmax: int
+    restart: int
+    comps: list          # [(h, v, bw, bh, tq)]
+
+    @property
+    def coef_count(self) -> int:
+        return sum(bw * bh * 64 for _, _, bw, bh, _ in self.comps)
+
+    def meta(self) -> list[int]:
+        m = [self.ncomp, self.hmax, self.vmax, self.width, self.height]
+        for h, v, bw, bh, _ in self.comps:
+            m += [h, v, bw, bh]
+        return m
+
+
+def info(data: bytes) -> Optional[JpegInfo]:
+    """Header of a baseline JPEG this decoder handles, else None."""
+    lib = _lib()
+    if lib is None or len(data) < 4 or data[:2] != b"\xff\xd8":
+        return None
+    out = (ctypes.c_int * 32)()
+    if lib.lumen_jpeg_info(data, len(data), out) != 0:
+        return None
+    nc = out[2]
+    comps = [tuple(out[8 + 5 * c + k] for k in range(5)) for c in range(nc)]
+    return JpegInfo(out[0], out[1], nc, out[3], out[4], out[5], comps)
+
+
+def decode_coefs(data: bytes, threads: Optional[int] = None, jinfo: Optional[JpegInfo] = None,
+                 out: Optional[np.ndarray] = None):
+    """-> (coefficients int16 [coef_count], quant tables uint16 [ncomp, 64], JpegInfo, stats) or None."""
+    lib = _lib()
+    ji = jinfo or info(data)
+    if lib is None or ji is None:
+        return None
+    coef = out if out is not None else np.empty(ji.coef_count, np.int16)
+    qt = np.empty((ji.ncomp, 64), np.uint16)
+    st = np.zeros(4, np.int64)
+    r = lib.lumen_jpeg_decode_coefs(data, len(data), int(threads or default_threads()), coef.ctypes.data,
+                                    qt.ctypes.data, st.ctypes.data)
+    if r != 0:
+        return None
+    return coef, qt, ji, {"chunks": int(st[0]), "resynced": int(st[1]), "serial_blocks": int(st[2]),
+                          "blocks": int(st[3])}
+
+
+# ------------------------------------------------------------------ NumPy reference of csrc/jpeg.hip
+def _idct_matrix() -> np.ndarray:
+    k = np.zeros((8, 8), np.float64)
+    for u in range(8):
+        cu = np.sqrt(0.5) if u == 0 else 1.0
+        for x in range(8):
+            k[u, x] = cu / 2 * np.cos((2 * x + 1) * u * np.pi / 16)
+    return k
+
+
+def _fancy(pl: np.ndarray, dw: int, dh: int, W: int, H: int, sx: int, sy: int) -> np.ndarray:
+    """libjpeg fancy upsampling of a chroma plane (valid region dh x dw) to H x W."""
+    p = pl[:dh, :dw].astype(np.int32)
+    if sx == 1 and sy == 1:
+        return p[:H, :W]
+    X = np.arange(W)
+    c = X // sx
+    if sy == 2:
+        Y = np.arange(H)
+        r = Y // 2
+        rf = np.where(Y & 1, np.minimum(r + 1, dh - 1), np.maximum(r - 1, 0))
+        cs = 3 * p[r] + p[rf]                                   # [H, dw]
+        left = cs[:, np.maximum(c - 1, 0)]
+        right = cs[:, np.minimum(c + 1, dw - 1)]
+        mid = cs[:, c]
+        return np.where(X & 1, (3 * mid + right + 7) >> 4, (3 * mid + left + 8) >> 4)
+    cs = p[:H]
+    left, right, mid = cs[:, np.maximum(c - 1, 0)], cs[:, np.minimum(c + 1, dw - 1)], cs[:, c]
+    return np.where(X & 1, (3 * mid + right + 2) >> 2, (3 * mid + left + 1) >> 2)
+
+
+def reconstruct_reference(coef: np.ndarray, qt: np.ndarray, ji: JpegInfo) -> np.ndarray:
+    """The GPU kernel's arithmetic in NumPy: coefficient planes -> uint8 [H, W, 3]."""
+    K = _idct_matrix()
+    planes, off = [], 0
+    for c, (h, v, bw, bh, _) in enumerate(ji.comps):
+        n = bw * bh * 64
+        blk = coef[off:off + n].reshape(bh, bw, 8, 8).astype(np.float64) * qt[c].reshape(8, 8)
+        off += n
+        pix = np.einsum("vy,ux,abvu->abyx", K, K, blk)           # [bh, bw, y, x]
+        pix = np.clip(np.rint(pix + 128.0), 0, 255).astype(np.int32)
+        planes.append(pix.transpose(0, 2, 1, 3).reshape(bh * 8, bw * 8))
+    W, H = ji.width, ji.height
+    y = planes[0][:H, :W]
+    if ji.ncomp == 1:
+        return np.repeat(y[..., None], 3, -1).astype(np.uint8)
+    ch = []
+    for c in (1, 2):
+        h, v = ji.comps[c][0], ji.comps[c][1]
+        dw, dh = (W * h + ji.hmax - 1) // ji.hmax, (H * v + ji.vmax - 1) // ji.vmax
+        ch.append(_fancy(planes[c], dw, dh, W, H, ji.hmax // h, ji.vmax // v) - 128)
+    cb, cr = ch
+    r = y + ((91881 * cr + 32768) >> 16)
+    g = y + ((-22554 * cb - 46802 * cr + 32768) >> 16)
+    b = y + ((116130 * cb + 32768) >> 16)
+    return np.clip(np.stack([r, g, b], -1), 0, 255).astype(np.uint8)
+
+
+# ------------------------------------------------------------------ device decode
+class _Staging(threading.local):
+    buf = None
+    ev = None       # the H2D copy that last read buf
+
+
+_staging = _Staging()
+
+
+def decode_to_device(data: bytes, device, threads: Optional[int] = None, stats: Optional[dict] = None):
+    """JPEG bytes -> uint8 [H, W, 3] tensor on ``device``.  Baseline JPEGs take the parallel
+    entropy decoder + GPU reconstruction; everything else (and CPU devices) decodes with
+    Pillow.  Raises ValueError on undecodable input, like decode_rgb."""
+    import torch
+
+    from .image import decode_rgb
+
+    dev = torch.device(device)
+    ji = info(data) if dev.type == "cuda" else None
+    if ji is not None:
+        # coefficients straight into a pinned, per-thread staging buffer -> one async H2D
+        n = ji.coef_count
+        if _staging.ev is not None:
+            _staging.ev.synchronize()      # this thread's previous upload has read the buffer
+        st = _staging.buf
+        if st is None or st.numel() < n:
+            st = torch.empty(max(n, 1 << 20), dtype=torch.int16).pin_memory()
+            _staging.buf = st
+        host = st[:n].numpy()
+        res = decode_coefs(data, threads, ji, out=host)
+        if res is not None:
+            coef, qt, ji, s = res
+            if stats is not None:
+                stats.update(s)
+            from ..ops import hip_ops
+
+            cd = st[:n].to(dev, non_blocking=True)
+            qd = torch.from_numpy(qt.view(np.int16)).to(dev, non_blocking=True)
+            samp = torch.empty(n, dtype=torch.uint8, device=dev)
+            out = torch.empty((ji.height, ji.width, 3), dtype=torch.uint8, device=dev)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            _staging.ev = ev
+            hip_ops().jpeg_reconstruct(cd, qd, ji.meta(), samp, out)
+            return out
+    return torch.from_numpy(decode_rgb(data)).to(dev)
