@@ -47,7 +47,10 @@ class AppService:
     @classmethod
     def from_app_config(cls, config: LumenConfig, initialize: bool = True) -> "AppService":
         """Each enabled service is built and initialised under its GPU set
-        (runtime/placement.py: disjoint GPUs per service, DP workers per GPU)."""
+        (runtime/placement.py: disjoint GPUs per service, DP workers per GPU).  In a serving front
+        end (parallel/engine.py) a service whose engines are attached finds them through
+        ``remote_scope`` and loads no model here."""
+        from ..parallel.engine import remote_scope
         from ..runtime import placement
 
         services, names = [], []
@@ -55,7 +58,7 @@ class AppService:
         plan = placement.plan_from_env(list(enabled))
         for name, svc_cfg in enabled.items():
             cls_ = ServiceLoader.get_class(svc_cfg.import_info.registry_class)
-            with placement.use(plan.get(name)):
+            with placement.use(plan.get(name)), remote_scope(name):
                 svc = cls_.from_config(svc_cfg, config.cache_path())
                 if initialize and hasattr(svc, "initialize"):
                     svc.initialize()
@@ -137,6 +140,93 @@ def _replica_main(config_path: str, port: int, mode: str, stop_event, ready_q, i
           parent_pid=parent_pid)
 
 
+def _frontend_main(config_path: str, port: int, mode: str, stop_event, ready_q, idx: int, parent_pid: int,
+                   specs: dict) -> None:
+    """A serving front-end process (spawned before any GPU use): the services of the config with
+    their GPU work forwarded to the engine processes, gRPC on the shared port (SO_REUSEPORT)."""
+    setup_logging(os.environ.get("LUMEN_LOG_LEVEL", "INFO"))
+    from ..parallel.engine import attach_frontend
+
+    attach_frontend(specs)
+    serve(config_path, port, mode=mode, stop_event=stop_event, procs=1, replica=idx, ready_q=ready_q,
+          parent_pid=parent_pid, frontends=0)
+
+
+def engine_devices() -> list[str]:
+    """One engine per visible GPU (LUMEN_ENGINE_DEVICES=cuda:0,cuda:1,... to choose), else one CPU engine."""
+    env = os.environ.get("LUMEN_ENGINE_DEVICES")
+    if env:
+        return [d.strip() for d in env.split(",") if d.strip()]
+    try:
+        import torch
+
+        n = torch.cuda.device_count()   # counts without initialising the GPU in this process
+    except Exception:  # noqa: BLE001
+        n = 0
+    return [f"cuda:{i}" for i in range(n)] or ["cpu"]
+
+
+def serve_frontends(config_path: str, port: int, frontends: int, mode: str = "hub",
+                    stop_event: Optional[threading.Event] = None, ready_q=None, devices=None) -> bool:
+    """Engine/front-end topology: one GPU engine process per device holding the models, and
+    ``frontends`` gRPC front-end processes sharing ``port``.  Returns False (nothing started) when
+    a service of the config cannot run on engines -- the caller then serves in-process."""
+    import multiprocessing as mp
+
+    from ..parallel.engine import EngineSet
+
+    config = load_and_validate_config(config_path)
+    handle_download_results(Downloader(config).download_all())
+    specs = {}
+    for name, svc_cfg in config.enabled_services().items():
+        cls_ = ServiceLoader.get_class(svc_cfg.import_info.registry_class)
+        svc = cls_.from_config(svc_cfg, config.cache_path())   # not initialised: no model, no GPU
+        spec = svc.engine_spec() if hasattr(svc, "engine_spec") else None
+        try:
+            svc.close()
+        except Exception:  # noqa: BLE001
+            pass
+        if spec is None:
+            log.warning("service %s cannot run on GPU engines: serving in-process instead", name)
+            return False
+        specs[name] = spec
+    devs = list(devices or engine_devices())
+    log.info("starting %d GPU engine(s) on %s for %s", len(devs), devs, list(specs))
+    engines = EngineSet(specs, devs)
+    ctx = mp.get_context("spawn")
+    stop = ctx.Event()
+    rq = ready_q if ready_q is not None else ctx.Queue()
+    procs = [ctx.Process(target=_frontend_main, args=(config_path, port, mode, stop, rq, i + 1, os.getpid(),
+                                                      engines.frontend_specs()), daemon=False)
+             for i in range(frontends)]
+    for p in procs:
+        p.start()
+    if ready_q is None:
+        for _ in procs:
+            rq.get(timeout=900)
+    log.info("Lumen front ends: %d process(es) on :%d over %d engine(s)", frontends, port, len(devs))
+    print(f"Lumen Hub service listening on {config.server.host or '0.0.0.0'}:{port} "
+          f"({frontends} front ends, {len(devs)} engines)", flush=True)
+    done = stop_event or threading.Event()
+
+    def _stop(signum, frame):
+        log.info("signal %s: shutting down", signum)
+        done.set()
+
+    if threading.current_thread() is threading.main_thread() and stop_event is None:
+        signal.signal(signal.SIGINT, _stop)
+        signal.signal(signal.SIGTERM, _stop)
+    while not done.wait(0.5):
+        pass
+    stop.set()
+    for p in procs:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    engines.close()
+    return True
+
+
 def _pid_alive(pid: int) -> bool:
     if os.getppid() != pid:        # re-parented: the original parent exited
         return False
@@ -169,13 +259,22 @@ def start_replicas(config_path: str, port: int, n: int, mode: str = "hub", ready
 
 def serve(config_path: str, port_override: Optional[int] = None, mode: str = "hub",
           stop_event: Optional[threading.Event] = None, procs: Optional[int] = None, replica: int = 0,
-          ready_q=None, parent_pid: Optional[int] = None) -> None:
-    """Run the server.  ``procs`` > 1 (or LUMEN_HUB_PROCS): this process plus procs - 1 spawned
-    replicas accept on the same port (SO_REUSEPORT; a fixed port is required)."""
+          ready_q=None, parent_pid: Optional[int] = None, frontends: Optional[int] = None) -> None:
+    """Run the server.  ``frontends`` > 0 (or LUMEN_FRONTENDS): GPU engine processes + that many
+    front-end processes on one port (:func:`serve_frontends`).  ``procs`` > 1 (or LUMEN_HUB_PROCS):
+    this process plus procs - 1 spawned full replicas accept on the same port (SO_REUSEPORT; a
+    fixed port is required)."""
     config = load_and_validate_config(config_path)
     if config.deployment.mode != mode:
         log.error("this server runs deployment.mode=%s; config has %s", mode, config.deployment.mode)
         raise SystemExit(1)
+    nfront = int(frontends if frontends is not None else os.environ.get("LUMEN_FRONTENDS", "0"))
+    if nfront > 0 and replica == 0:
+        port0 = port_override or config.server.port
+        if not port0:
+            raise SystemExit("front-end processes need a fixed server.port")
+        if serve_frontends(config_path, port0, nfront, mode, stop_event=stop_event):
+            return
     nproc = int(procs if procs is not None else os.environ.get("LUMEN_HUB_PROCS", "1"))
     if replica == 0:
         handle_download_results(Downloader(config).download_all())
@@ -255,11 +354,14 @@ def main(argv=None, mode: str = "hub", prog: str = "lumen") -> int:
     ap.add_argument("--log-level", default="INFO", choices=["DEBUG", "INFO", "WARNING", "ERROR"])
     ap.add_argument("--procs", type=int, default=None,
                     help="server replica processes on the one port (default LUMEN_HUB_PROCS or 1)")
+    ap.add_argument("--frontends", type=int, default=None,
+                    help="front-end processes over one GPU engine per device (default LUMEN_FRONTENDS or 0: "
+                         "in-process serving)")
     ap.add_argument("--version", action="version", version=f"%(prog)s {__version__}")
     args = ap.parse_args(argv)
     setup_logging(args.log_level)
     try:
-        serve(args.config, args.port, mode=mode, procs=args.procs)
+        serve(args.config, args.port, mode=mode, procs=args.procs, frontends=args.frontends)
     except SystemExit as e:
         return int(e.code or 0)
     return 0

@@ -1,0 +1,324 @@
+"""One GPU engine process per device, fed by many serving front-end processes.
+
+The reference serves everything from one process on a 10-thread gRPC pool, batch 1
+(``src/lumen/server.py:232-235``).  Round 3 scaled serving by running N full hub replicas per
+GPU (N copies of every model, N independent batchers).  Here the serving stack splits in two:
+
+* **front ends** (K processes, ``hub.server.serve(frontends=K)``): gRPC accept, chunk reassembly,
+  JPEG decode, tokenisation and the service logic -- the Python-bound work that one
+  interpreter lock would serialise -- each running the normal service classes whose backends
+  see a :class:`RemotePool` where a GPU worker pool would be;
+* **engines** (one process per GPU, :func:`engine_main`): the models, and a batch loop per
+  service that pops whatever requests ALL front ends have queued on that service's
+  :class:`~lumen_amd.parallel.shm_channel.ShmChannel` (futex wait, then a short linger), runs
+  them as one device batch through the service's GPU-worker factory (the same
+  ``fn(kind, items)`` the DP worker pool runs) and completes each request slot.
+
+A request slot carries one front-end batch (pickled item list; images arrive decoded), so a
+front end pays one channel round trip per batch while the engine merges batches of every
+front end.  Engines heart-beat into the channel; the :class:`EngineSet` supervisor respawns a
+dead engine, whose restart fails the requests it had taken (front ends see
+:class:`~lumen_amd.parallel.worker_pool.WorkerLostError` -> gRPC UNAVAILABLE) while queued ones
+wait for the new engine.
+"""
+from __future__ import annotations
+
+import importlib
+import inspect
+import logging
+import multiprocessing as mp
+import os
+import pickle
+import threading
+import time
+import traceback
+from concurrent.futures import Future, ThreadPoolExecutor
+from contextlib import contextmanager
+from typing import Optional, Sequence
+
+from .shm_channel import ChannelError, ChannelGroup, ChannelSpec, EngineUnavailable, ShmChannel
+from .worker_pool import WorkerLostError, WorkerTaskError
+
+log = logging.getLogger("lumen.engine")
+
+KINDS = ("call",)          # every request is one pickled (kind, items) batch
+
+
+def _resolve(path: str):
+    mod, _, attr = path.partition(":")
+    return getattr(importlib.import_module(mod), attr)
+
+
+# ============================================================================ front-end side
+class RemotePool:
+    """Stand-in for :class:`~lumen_amd.parallel.worker_pool.GPUWorkerPool` inside a front-end
+    process: ``submit(kind, items)`` ships the batch to the least-loaded engine of the service."""
+
+    def __init__(self, group: ChannelGroup, info: Optional[dict] = None, timeout_s: float = 300.0,
+                 max_inflight: int = 64):
+        self.group = group
+        self.info = info or {}
+        self.timeout_s = timeout_s
+        self._ex = ThreadPoolExecutor(max_workers=max_inflight, thread_name_prefix="lumen-remote")
+        self.stats = {"tasks": 0, "items": 0, "split": 0}
+
+    @property
+    def size(self) -> int:
+        return len(self.group.channels)
+
+    def _call(self, kind: str, items: list) -> list:
+        blob = pickle.dumps((kind, items), protocol=pickle.HIGHEST_PROTOCOL)
+        ch = self.group.pick()
+        if len(blob) > ch.slot_bytes and len(items) > 1:      # split a batch larger than a slot
+            self.stats["split"] += 1
+            h = len(items) // 2
+            return self._call(kind, items[:h]) + self._call(kind, items[h:])
+        try:
+            res = ch.call("call", blob, timeout=self.timeout_s)
+        except EngineUnavailable as e:
+            raise WorkerLostError(str(e)) from e
+        except ChannelError as e:
+            msg = str(e)
+            if msg.startswith("engine restarted"):
+                raise WorkerLostError(msg) from e
+            raise WorkerTaskError(msg) from e
+        out = pickle.loads(res)
+        if isinstance(out, BaseException):
+            raise out
+        return out
+
+    def submit(self, kind: str, items: list, worker: Optional[int] = None) -> Future:
+        self.stats["tasks"] += 1
+        self.stats["items"] += len(items)
+        return self._ex.submit(self._call, kind, list(items))
+
+    def run(self, kind: str, items: Sequence, timeout: Optional[float] = None) -> list:
+        return self.submit(kind, list(items)).result(timeout)
+
+    def broadcast(self, kind: str, items: list, timeout: Optional[float] = None) -> list:
+        futs = []
+        for ch in self.group.channels:
+            g = ChannelGroup([ch])
+            futs.append(self._ex.submit(RemotePool(g, self.info, self.timeout_s, 1)._call, kind, list(items)))
+        return [f.result(timeout) for f in futs]
+
+    def close(self) -> None:
+        self._ex.shutdown(wait=False)
+
+
+_REMOTE: dict = {}
+_scope = threading.local()
+
+
+def install_remote(service: str, pool: RemotePool) -> None:
+    _REMOTE[service] = pool
+
+
+@contextmanager
+def remote_scope(service: Optional[str]):
+    """While building service ``service`` in a front end, backends find its RemotePool."""
+    prev = getattr(_scope, "name", None)
+    _scope.name = service
+    try:
+        yield
+    finally:
+        _scope.name = prev
+
+
+def current_remote() -> Optional[RemotePool]:
+    name = getattr(_scope, "name", None)
+    return _REMOTE.get(name) if name is not None else None
+
+
+# ============================================================================ engine side
+def _serve_channel(ch: ShmChannel, fn, stop: threading.Event, max_items: int, linger_us: int,
+                   stats: dict) -> None:
+    """Batch loop over one channel: pop queued front-end batches, merge by kind, run, complete."""
+    while not stop.is_set():
+        slots = ch.pop_batch(ch.nslots, wait_ms=100, linger_us=linger_us)
+        if not slots:
+            continue
+        groups: dict = {}
+        for s in slots:
+            try:
+                _kind, blob, _meta = ch.request(s)
+                kind, items = pickle.loads(bytes(blob))
+                if kind == "__stats__":        # engine counters (tests, tools/serve_bench.py)
+                    ch.complete(s, pickle.dumps([dict(stats)]))
+                    continue
+                groups.setdefault(kind, []).append((s, items))
+            except Exception as e:  # noqa: BLE001 - a bad request fails alone
+                ch.complete(s, error=f"bad request: {e}")
+        for kind, reqs in groups.items():
+            fronts = len({ch.tag(s) >> 32 for s, _ in reqs})
+            stats["max_frontends_per_batch"] = max(stats.get("max_frontends_per_batch", 0), fronts)
+            if fronts > 1:
+                stats["shared_batches"] = stats.get("shared_batches", 0) + 1
+            flat = [it for _, items in reqs for it in items]
+            try:
+                res: list = []
+                for i in range(0, len(flat), max_items):
+                    res.extend(fn(kind, flat[i:i + max_items]))
+                if len(res) != len(flat):
+                    raise RuntimeError(f"engine fn returned {len(res)} results for {len(flat)} items")
+            except Exception:  # noqa: BLE001 - the whole merged batch failed
+                msg = traceback.format_exc()
+                for s, _ in reqs:
+                    ch.complete(s, error=msg[-4000:])
+                continue
+            k = 0
+            for s, items in reqs:
+                part = res[k:k + len(items)]
+                k += len(items)
+                try:
+                    ch.complete(s, pickle.dumps(part, protocol=pickle.HIGHEST_PROTOCOL))
+                except Exception as e:  # noqa: BLE001 - e.g. a result larger than the slot
+                    ch.complete(s, error=f"result: {e}")
+            stats["batches"] = stats.get("batches", 0) + 1
+            stats["items"] = stats.get("items", 0) + len(flat)
+            stats["slots"] = stats.get("slots", 0) + len(reqs)
+
+
+def engine_main(services: dict, device: str, ready_q, stop_ev, max_items: int = 256, linger_us: int = 1500,
+                threads_per_service: int = 2) -> None:
+    """Engine process body.  ``services``: name -> (ChannelSpec, factory path, kwargs).  Pins the
+    device, builds every service's batch function, then serves each channel with
+    ``threads_per_service`` batch loops (one batch's host work overlaps the other's GPU work)."""
+    try:
+        if device.startswith("cuda"):
+            import torch
+
+            torch.cuda.set_device(torch.device(device))
+        chans, fns = {}, {}
+        for name, (spec, factory, kwargs) in services.items():
+            ch = ShmChannel.attach(spec)
+            fac = _resolve(factory)
+            kw = dict(kwargs)
+            params = inspect.signature(fac).parameters
+            if "rank" in params and "rank" not in kw:
+                kw["rank"] = 0
+            if "world" in params and "world" not in kw:
+                kw["world"] = 1
+            fns[name] = fac(device, **kw)
+            chans[name] = ch
+        for ch in chans.values():
+            failed = ch.engine_start()
+            if failed:
+                log.warning("engine on %s: failed %d request(s) left running by a previous engine", device, failed)
+            ch.register_host()
+    except BaseException:  # noqa: BLE001
+        ready_q.put(("fatal", device, traceback.format_exc()))
+        return
+    stop = threading.Event()
+    stats: dict = {}
+    ths = []
+    for name, ch in chans.items():
+        for i in range(threads_per_service):
+            t = threading.Thread(target=_serve_channel, args=(ch, fns[name], stop, max_items, linger_us, stats),
+                                 name=f"lumen-engine-{name}-{i}", daemon=True)
+            t.start()
+            ths.append(t)
+    ready_q.put(("ready", device, os.getpid()))
+    # stop_ev: a shared byte, polled (an mp.Event's set() blocks on a waiter that died in its wait)
+    while not stop_ev.value:
+        for ch in chans.values():
+            ch.heartbeat()
+        time.sleep(0.25)
+    stop.set()
+    for t in ths:
+        t.join(timeout=5)
+
+
+class EngineSet:
+    """Launcher side: one channel per (service, engine), one engine process per device,
+    supervision (a dead engine is respawned on the same channels)."""
+
+    def __init__(self, services: dict, devices: Sequence[str], nslots: int = 64, slot_bytes: int = 32 << 20,
+                 result_bytes: int = 4 << 20, start_timeout_s: float = 900.0, respawn: bool = True,
+                 threads_per_service: int = 2, linger_us: int = 1500, max_items: int = 256):
+        """``services``: name -> (factory path, kwargs)."""
+        self.services = dict(services)
+        self.loop_args = (max_items, linger_us, threads_per_service)
+        self.devices = list(devices)
+        self.respawn = respawn
+        self._ctx = mp.get_context("spawn")
+        self._ready = self._ctx.Queue()
+        self._stop = self._ctx.Value("b", 0, lock=False)
+        self.channels: dict = {name: [ShmChannel.create(f"{name}-{i}", KINDS, nslots, slot_bytes, result_bytes)
+                                      for i in range(len(self.devices))] for name in self.services}
+        self.procs: list = [None] * len(self.devices)
+        self.restarts = 0
+        for i in range(len(self.devices)):
+            self._spawn(i)
+        self._wait_ready(len(self.devices), start_timeout_s)
+        self._mon_stop = threading.Event()
+        self._mon = threading.Thread(target=self._monitor, name="lumen-engine-monitor", daemon=True)
+        self._mon.start()
+
+    def _spawn(self, i: int) -> None:
+        svc = {name: (self.channels[name][i].spec(), fac, kw) for name, (fac, kw) in self.services.items()}
+        p = self._ctx.Process(target=engine_main, args=(svc, self.devices[i], self._ready, self._stop, *self.loop_args),
+                              name=f"lumen-engine-{i}", daemon=False)
+        p.start()
+        self.procs[i] = p
+
+    def _wait_ready(self, n: int, timeout: float) -> None:
+        t0 = time.time()
+        got = 0
+        while got < n:
+            left = timeout - (time.time() - t0)
+            if left <= 0:
+                raise TimeoutError("GPU engines did not become ready")
+            kind, dev, payload = self._ready.get(timeout=left)
+            if kind == "fatal":
+                self.close()
+                raise RuntimeError(f"engine on {dev} failed to start:\n{payload}")
+            got += 1
+
+    def _monitor(self) -> None:
+        while not self._mon_stop.wait(1.0):
+            for i, p in enumerate(self.procs):
+                if p is not None and not p.is_alive() and self.respawn and not self._stop.value:
+                    log.error("engine %d on %s exited (%s): respawning", i, self.devices[i], p.exitcode)
+                    self.restarts += 1
+                    self._spawn(i)
+                    try:
+                        self._wait_ready(1, 900.0)
+                    except Exception:  # noqa: BLE001
+                        log.exception("engine %d respawn failed", i)
+
+    def frontend_specs(self) -> dict:
+        """name -> [ChannelSpec per engine] for ONE front-end process (fresh fd handles)."""
+        return {name: [c.spec() for c in chans] for name, chans in self.channels.items()}
+
+    def close(self) -> None:
+        self._stop.value = 1
+        if getattr(self, "_mon_stop", None) is not None:
+            self._mon_stop.set()
+        for p in self.procs:
+            if p is not None:
+                p.join(timeout=15)
+                if p.is_alive():
+                    p.kill()
+                    p.join(timeout=5)
+        for chans in self.channels.values():
+            for c in chans:
+                c.close()
+
+
+def attach_frontend(specs: dict, dead_after_s: float = 30.0) -> None:
+    """In a front-end process: map every service's channels and install its RemotePool."""
+    for name, sl in specs.items():
+        chans = [ShmChannel.attach(s) for s in sl]
+        install_remote(name, RemotePool(ChannelGroup(chans, dead_after_s)))
+
+
+def engine_factory_of(service_cls, svc_cfg, cache_dir) -> Optional[tuple]:
+    """(factory path, kwargs) when the service class can run on engines, else None."""
+    f = getattr(service_cls, "engine_spec", None)
+    return f(svc_cfg, cache_dir) if f is not None else None
+
+
+# a ChannelSpec must be importable where pickled objects are rebuilt
+__all__ = ["RemotePool", "EngineSet", "engine_main", "attach_frontend", "install_remote", "remote_scope",
+           "current_remote", "engine_factory_of", "ChannelSpec"]

@@ -120,7 +120,6 @@ class ShmChannel:
         self._pay = [int(self.lib.lumen_ch_payload_off(self.base, i)) for i in range(self.nslots)]
         self._res = [int(self.lib.lumen_ch_result_off(self.base, i)) for i in range(self.nslots)]
         self._seq = itertools.count(1)
-        self._out = (ctypes.c_int * max(self.nslots, 1))()
         self._registered = None
 
     # ------------------------------------------------------------------ lifecycle
@@ -271,8 +270,15 @@ class ShmChannel:
         self.lib.lumen_ch_heartbeat(self.base, os.getpid())
 
     def pop_batch(self, max_n: int, wait_ms: int = 100, linger_us: int = 0) -> list[int]:
-        n = self.lib.lumen_ch_pop_batch(self.base, self._out, min(max_n, self.nslots), int(wait_ms), int(linger_us))
-        return [self._out[i] for i in range(n)]
+        """Engine: up to max_n RUNNING slots (thread-safe: several batch loops may pop)."""
+        k = min(max_n, self.nslots)
+        out = (ctypes.c_int * k)()
+        n = self.lib.lumen_ch_pop_batch(self.base, out, k, int(wait_ms), int(linger_us))
+        return [out[i] for i in range(n)]
+
+    def tag(self, slot: int) -> int:
+        """Submitter tag of a slot: (front-end pid << 32) | sequence."""
+        return int(self._desc[slot].tag)
 
     def request(self, slot: int):
         """(kind, payload view, meta dict) of a RUNNING slot (the view is valid until complete())."""

@@ -153,6 +153,11 @@ class BaseInferenceService(pb.InferenceServicer):
     def close(self) -> None:
         pass
 
+    def engine_spec(self):
+        """(factory path, kwargs) of this service's GPU side for the engine / front-end serving
+        topology (parallel/engine.py), or None when the service runs in-process only."""
+        return None
+
     # ---- helpers
     @staticmethod
     def _assemble(cid: str, req, buffers: dict) -> tuple[bytes, bool]:

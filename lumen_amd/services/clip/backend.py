@@ -132,7 +132,17 @@ class MI355XClipBackend:
         cfg.image_mean, cfg.image_std = tuple(mean), tuple(std)
         self.cfg = cfg
         self.context_length = cfg.context_length
-        if self.dp_size > 1:
+        from ...parallel.engine import current_remote
+
+        remote = current_remote()
+        if remote is not None:
+            # serving front end (parallel/engine.py): the towers live in the GPU engine processes;
+            # this process decodes, tokenises and ships batches there
+            self._pool = remote
+            self.device = torch.device("cpu")
+            info = remote.submit("info", [None]).result()[0]
+            self._logit_scale = float(info["logit_scale"])
+        elif self.dp_size > 1:
             from ...parallel.worker_pool import GPUWorkerPool, default_devices
 
             r = self.resources
@@ -157,7 +167,8 @@ class MI355XClipBackend:
         self._load_tokenizer()
         # with DP workers: 2 dispatchers per GPU, each batch goes whole to the least-loaded worker; one
         # GPU in-process: 2 dispatchers, so one batch's stacking / H2D / D2H overlaps the other's tower
-        conc = 2 * self.dp_size if self._pool is not None else (2 if self.device.type == "cuda" else 1)
+        conc = (2 * self._pool.size if self._pool is not None and remote is not None else
+                2 * self.dp_size if self._pool is not None else (2 if self.device.type == "cuda" else 1))
         self._img_batcher = DynamicBatcher(self._encode_images, self.max_batch, self.max_wait_ms, "clip-image", conc)
         self._txt_batcher = DynamicBatcher(self._encode_texts, self.max_batch, self.max_wait_ms, "clip-text", conc)
         self.load_time = time.time() - t0
@@ -190,6 +201,13 @@ class MI355XClipBackend:
     def _ensure(self):
         if not self.is_initialized:
             raise BackendNotInitializedError("backend not initialized")
+
+    @property
+    def remote(self) -> bool:
+        """True in a serving front end: batches go to the GPU engine processes (decoded here)."""
+        from ...parallel.engine import RemotePool
+
+        return isinstance(self._pool, RemotePool)
 
     # ------------------------------------------------------------------ batched workers
     def tokenize(self, texts: Sequence[str]) -> torch.Tensor:
@@ -227,7 +245,7 @@ class MI355XClipBackend:
         self._ensure()
         if not image_bytes:
             raise InvalidInputError("empty image payload")
-        if self._pool is not None:                    # DP workers decode in their own processes
+        if self._pool is not None and not self.remote:  # DP workers decode in their own processes
             return self._img_batcher(image_bytes)
         # decoded on the caller's (gRPC) thread: Pillow releases the GIL, so concurrent requests decode
         # in parallel and the batch's critical path is only the GPU work; a bad payload fails alone
@@ -319,8 +337,16 @@ def dp_worker(device: str, cache_dir: str, model: str, runtime: str, dataset: Op
             if bank is None:
                 raise RuntimeError("this worker holds no label-bank shard")
             return [bank.topk_local(q, k, scale, sm) for q, k, scale, sm in items]
+        if kind == "info":
+            return [{"logit_scale": float(m.logit_scale), "embed_dim": int(cfg.embed_dim)}]
         if kind == "image":
-            emb = m.encode_image_uint8([torch.from_numpy(i) for i in decode_many(items)])
+            # encoded images (DP workers decode here) or uint8 HWC arrays (decoded by a serving front end)
+            raw = [k for k, it in enumerate(items) if not isinstance(it, np.ndarray)]
+            imgs = list(items)
+            if raw:
+                for k, a in zip(raw, decode_many([items[k] for k in raw])):
+                    imgs[k] = a
+            emb = m.encode_image_uint8([torch.from_numpy(np.ascontiguousarray(i)) for i in imgs])
         elif kind == "text":
             emb = m.encode_text_ids(torch.from_numpy(np.stack(items)).to(dev))
         else:
@@ -328,6 +354,14 @@ def dp_worker(device: str, cache_dir: str, model: str, runtime: str, dataset: Op
         return list(emb.float().cpu().numpy())
 
     return fn
+
+
+def engine_spec(resources: ModelResources) -> tuple:
+    """(factory path, kwargs) of the GPU engine side of this backend (parallel/engine.py)."""
+    r = resources
+    return ("lumen_amd.services.clip.backend:dp_worker",
+            {"cache_dir": str(r.model_root_path.parent.parent), "model": r.model_name, "runtime": r.runtime,
+             "dataset": r.dataset, "shard_bank": False})
 
 
 def create_backend(backend_settings, resources: ModelResources, runtime: Optional[str] = None,

@@ -89,6 +89,11 @@ class GeneralCLIPService(BaseInferenceService):
     def _initialize(self):
         self.model.initialize()
 
+    def engine_spec(self):
+        from .backend import engine_spec
+
+        return engine_spec(self.resources)
+
     # ---- handlers
     def _handle_embed(self, payload: bytes, mime: str, meta: dict):
         text = payload.decode("utf-8")

@@ -171,6 +171,18 @@ class MI355XFaceBackend:
         if self.is_initialized:
             return
         t0 = time.time()
+        from ...parallel.engine import current_remote
+
+        remote = current_remote()
+        if remote is not None:
+            # serving front end (parallel/engine.py): SCRFD + IResNet live in the GPU engine
+            # processes; this process decodes the JPEGs and ships batches there
+            self.device = torch.device("cpu")
+            self._init_pool(remote)
+            self.load_time = time.time() - t0
+            self.is_initialized = True
+            log.info("face pack %s served by %d GPU engine(s)", self.resources.model_name, remote.size)
+            return
         self.device = pick_device(self.device_pref)
         if len(self.dp_devices) > 1:
             self._init_pool()
@@ -218,11 +230,11 @@ class MI355XFaceBackend:
         self.is_initialized = True
         log.info("face pack %s ready on %s in %.2fs", r.model_name, self.device, self.load_time)
 
-    def _init_pool(self) -> None:
+    def _init_pool(self, pool=None) -> None:
         from ...parallel.worker_pool import GPUWorkerPool
 
-        self._pool = GPUWorkerPool("lumen_amd.services.face.backend:dp_worker", self.dp_devices,
-                                   kwargs={"resources": self.resources, "max_batch": self.max_batch})
+        self._pool = pool or GPUWorkerPool("lumen_amd.services.face.backend:dp_worker", self.dp_devices,
+                                           kwargs={"resources": self.resources, "max_batch": self.max_batch})
         info = self._pool.submit("info", [None]).result()[0]
         self.spec = info["spec"]
         self._emb_dim = info["embedding_dim"]
@@ -423,6 +435,13 @@ class MI355XFaceBackend:
         return list(emb)
 
     # ------------------------------------------------------------------ public API (reference contract)
+    def _payload(self, image_bytes: bytes):
+        """What a worker batch item carries: a serving front end decodes here (its own core),
+        a DP worker pool gets the JPEG and decodes in the worker."""
+        from ...parallel.engine import RemotePool
+
+        return self.decode(image_bytes) if isinstance(self._pool, RemotePool) else bytes(image_bytes)
+
     def decode(self, image_bytes: bytes) -> np.ndarray:
         if not image_bytes:
             raise InvalidInputError("image_bytes cannot be empty")
@@ -440,7 +459,7 @@ class MI355XFaceBackend:
         if self._pool is not None:
             if not image_bytes:
                 raise InvalidInputError("image_bytes cannot be empty")
-            return self._dp["detect"]((bytes(image_bytes), params))
+            return self._dp["detect"]((self._payload(image_bytes), params))
         img = self.decode(image_bytes)
         return self.detect_decoded(img, params)
 
@@ -458,7 +477,7 @@ class MI355XFaceBackend:
         if self._pool is not None:
             if not image_bytes:
                 raise InvalidInputError("image_bytes cannot be empty")
-            return self._dp["det_emb"]((bytes(image_bytes), params, int(max_faces)))
+            return self._dp["det_emb"]((self._payload(image_bytes), params, int(max_faces)))
         img = self.decode(image_bytes)
         faces = self.detect_decoded(img, params)
         if 0 < max_faces < len(faces):
@@ -541,6 +560,11 @@ class MI355XFaceBackend:
                            extra={"det_size": str(self.spec.det_size), "rec_size": str(self.spec.rec_size),
                                   "detector": "scrfd", "max_batch": str(self.max_batch),
                                   "dp_workers": str(len(self.dp_devices) if self._pool is not None else 1)})
+
+
+def engine_spec(resources: GenericResources, max_batch: int = 64) -> tuple:
+    """(factory path, kwargs) of the GPU engine side of this backend (parallel/engine.py)."""
+    return "lumen_amd.services.face.backend:dp_worker", {"resources": resources, "max_batch": max_batch}
 
 
 def create_backend(settings, resources: GenericResources, runtime: Optional[str] = None) -> MI355XFaceBackend:

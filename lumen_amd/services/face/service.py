@@ -68,6 +68,11 @@ class GeneralFaceService(BaseInferenceService):
         self.model = FaceModelManager(backend, resources)
         self._setup_registry()
 
+    def engine_spec(self):
+        from .backend import engine_spec
+
+        return engine_spec(self.resources, self.backend.max_batch)
+
     @classmethod
     def from_config(cls, service_config, cache_dir) -> "GeneralFaceService":
         mc = pick_model(service_config, FACE_KEYS)

@@ -39,6 +39,7 @@ from ...runtime.engine import LLMEngine, SamplingParams
 from ...runtime.kv_cache import PagedKVCache
 from ...runtime.metrics import current_timer, stage
 from ...utils.image import decode_rgb
+from ...utils.jpeg import decode_image
 from ..common import GenericResources, load_safetensors, pick_device, runtime_name
 
 log = logging.getLogger("lumen.vlm.backend")
@@ -458,7 +459,7 @@ class MI355XVLMBackend:
         ids, img = args[0], args[1]
         if len(args) > 2:                    # TP follower: no image here, rank 0 broadcasts its features
             return self.model.build_prefill(ids, [], n_images=args[2])
-        tens = [torch.from_numpy(img)] if img is not None else []
+        tens = [img if isinstance(img, torch.Tensor) else torch.from_numpy(img)] if img is not None else []
         return self.model.build_prefill(ids, tens)
 
     @staticmethod
@@ -486,7 +487,9 @@ class MI355XVLMBackend:
             ids = self.tokenize(prompt)
         try:
             with stage("decode"):
-                img = decode_rgb(req.image_bytes, draft_to=self.jpeg_draft_size())
+                # baseline JPEGs: parallel host entropy decode + GPU reconstruction (utils/jpeg.py);
+                # others: Pillow, DCT-scaled towards the vision input
+                img = decode_image(req.image_bytes, self.device, draft_to=self.jpeg_draft_size())
         except ValueError as e:
             raise InvalidInputError(str(e)) from e
         full, starts = self.model.expand_image_tokens(ids, 1)

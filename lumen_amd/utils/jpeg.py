@@ -211,3 +211,17 @@ def decode_to_device(data: bytes, device, threads: Optional[int] = None, stats: 
             hip_ops().jpeg_reconstruct(cd, qd, ji.meta(), samp, out)
             return out
     return torch.from_numpy(decode_rgb(data)).to(dev)
+
+
+def decode_image(data: bytes, device, draft_to: Optional[tuple] = None, stats: Optional[dict] = None):
+    """Request image -> uint8 [H, W, 3] torch tensor: on a GPU device a baseline JPEG takes
+    :func:`decode_to_device` (full resolution, no DCT-domain shortcut needed: the entropy decode
+    runs on every host thread and the pixels on the GPU); anything else decodes with Pillow
+    (DCT-scaled to ``draft_to`` when given) and stays on the host."""
+    import torch
+
+    from .image import decode_rgb
+
+    if torch.device(device).type == "cuda" and info(data) is not None:
+        return decode_to_device(data, device, stats=stats)
+    return torch.from_numpy(decode_rgb(data, draft_to=draft_to))

@@ -27,6 +27,7 @@ from lumen_amd.models.vlm import VLM, VLM_PRESETS  # noqa: E402
 from lumen_amd.runtime.engine import LLMEngine, SamplingParams  # noqa: E402
 from lumen_amd.runtime.kv_cache import PagedKVCache  # noqa: E402
 from lumen_amd.utils.image import decode_rgb, encode_jpeg  # noqa: E402
+from lumen_amd.utils.jpeg import decode_image  # noqa: E402
 from tools.face_ocr_bench import synth_image  # noqa: E402
 
 
@@ -41,7 +42,8 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--prompt-tokens", type=int, default=48)
     ap.add_argument("--kv-blocks", type=int, default=4096)
-    ap.add_argument("--full-decode", action="store_true", help="decode the JPEG at full resolution")
+    ap.add_argument("--full-decode", action="store_true", help="host decode: the JPEG at full resolution")
+    ap.add_argument("--host-decode", action="store_true", help="Pillow on the host instead of the device JPEG path")
     ap.add_argument("--fp8", action="store_true", help="weight-only OCP e4m3 decoder weights (per-channel scales)")
     ap.add_argument("--kv-fp8", action="store_true", help="OCP e4m3 paged KV cache (unit scale)")
     ap.add_argument("--image-kind", choices=["noise", "photo"], default="noise",
@@ -73,8 +75,11 @@ def main():
         return m.build_prefill(ids, [img])
 
     def decode(jpeg):
+        # as the service: baseline JPEGs -> parallel host entropy decode + GPU reconstruction
+        # (utils/jpeg.py); --host-decode: Pillow on the host (DCT-scaled unless --full-decode)
         t = time.perf_counter()
-        img = torch.from_numpy(decode_rgb(jpeg, draft_to=draft))
+        img = torch.from_numpy(decode_rgb(jpeg, draft_to=draft)) if args.host_decode else \
+            decode_image(jpeg, dev, draft_to=draft)
         dec_ms.append((time.perf_counter() - t) * 1000)
         return img
 
@@ -154,7 +159,9 @@ def main():
            "image_tokens": cfg.num_image_tokens, "max_new_tokens": args.max_new, "batch_max_new_tokens": args.batch_max_new, "n": args.n,
            "preset": args.preset, "kv_cache": "fp8-e4m3" if args.kv_fp8 else "bf16", "dtype": "bf16" if not args.fp8 else "fp8-e4m3 decoder (W8A8 prefill, fp8-weight decode), bf16 vision", "data": f"synthetic (random-init weights, {args.image_kind} 1024x768 JPEG, {len(jpeg) // 1024} KiB)",
            "load_s": load_s, "kv_cache_tokens": kv.capacity_tokens,
-           "jpeg_decode": "full resolution" if args.full_decode else f"DCT-scaled to >= {cfg.vision.image_size}px"}
+           "jpeg_decode": ("host, full resolution" if args.full_decode else
+                           f"host, DCT-scaled to >= {cfg.vision.image_size}px") if args.host_decode else
+                          "parallel host entropy decode + GPU reconstruction, full resolution"}
     print(json.dumps(out))
 
 
