@@ -298,17 +298,29 @@ class MI355XOcrBackend:
         for i, s in enumerate(shapes):
             groups.setdefault(s, []).append(i)
         out: list = [None] * len(images)
+        src, offs = None, None
+        if self.device.type == "cuda":
+            # one pinned H2D for the whole batch; every shape group's resize and the
+            # recogniser's crop warps (recognize) read the images from this upload
+            if getattr(self, "_uploader", None) is None:
+                from ...utils.image import PinnedUploader
+
+                self._uploader = PinnedUploader(self.device)
+            with stage("upload"):
+                src, offs = self._uploader.upload(images)
+            # (strong refs to the images: recognize matches them by identity)
+            self._last_upload = (list(images), src, [int(o) for o in offs])
         for (rh, rw), idx in groups.items():
             geoms, off, tens = [], 0, []
             for i in idx:
                 h, w = images[i].shape[:2]
-                geoms.append(ops.ImageGeom.resize(h, w, off, rh, rw))
+                geoms.append(ops.ImageGeom.resize(h, w, int(offs[i]) if src is not None else off, rh, rw))
                 off += images[i].size
                 tens.append(torch.from_numpy(np.ascontiguousarray(images[i])))
             with stage("det_preprocess"):
                 x = ops.image_prep(tens, (rh, rw), mean=dc["mean"], std=dc["std"], scale=float(dc["scale"]),
                                    filter="cv2_linear", layout="nhwc8", swap_rb=True, geoms=geoms,
-                                   out_dtype=self.dtype, device=self.device)
+                                   out_dtype=self.dtype, device=self.device, src=src)
             with stage("det_forward"):
                 prob = self.det(x)
             with stage("db_post"):
@@ -347,6 +359,10 @@ class MI355XOcrBackend:
         mean = float(np.mean(rc["mean"]))
         std = float(np.mean(rc["std"]))
         scale = float(rc["scale"])
+        src = None
+        last = getattr(self, "_last_upload", None)
+        if last is not None and len(last[0]) == len(images) and all(a is b for a, b in zip(last[0], images)):
+            src = (last[1], last[2])        # the detector's upload of these same images
         for s in range(0, len(order), self.rec_batch):
             chunk = order[s:s + self.rec_batch]
             widths = [maps[k][1] for k in chunk]
@@ -355,7 +371,7 @@ class MI355XOcrBackend:
             with stage("crop_warp"):
                 x = vision.warp_batch(images, [crops[k][0] for k in chunk], minv, (H, Wb), out_w=widths, cpad=8,
                                       scale=scale / std, mean=mean / std, std=1.0, swap_rb=True, cubic=True,
-                                      replicate=True, device=self.device)
+                                      replicate=True, device=self.device, src=src)
                 if x.dtype != self.dtype:
                     x = x.to(self.dtype)
             if hasattr(self.rec, "ctc_from_features"):

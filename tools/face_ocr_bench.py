@@ -172,7 +172,7 @@ def bench_ocr(args):
     def step():
         imgs = nxt[0].result()
         nxt[0] = ahead.submit(dec)
-        t = StageTimer("ocr-bench", gpu=False)
+        t = StageTimer("ocr-bench", gpu=args.gpu_timers)
         with use_timer(t):
             be.detect(imgs, [OcrParams()] * len(imgs))
             crops = [(i, b) for i in range(len(imgs)) for b in boxes]
@@ -207,7 +207,8 @@ def bench_ocr(args):
     return {"metric": "ocr images/s (whole job)", "value": world * args.batch / dt, "unit": "img/s",
             "n_gpus": world, "parallelism": f"dp{world} (SPMD, RCCL all-gather of packed lines)" if world > 1
             else "single GPU", "_rank": rank, "ms_per_batch": dt * 1000,
-            "host_stage_ms_per_batch": {k: round(v / n_steps, 2) for k, v in stages.items()},
+            ("gpu" if args.gpu_timers else "host") + "_stage_ms_per_batch":
+                {k: round(v / n_steps, 2) for k, v in stages.items()},
             "batch": args.batch, "crops_per_image": args.crops, "crops_per_s": world * args.batch * args.crops / dt,
             "jpeg_decode": "excluded (decoded once up front)" if args.predecoded else "included",
             "image_kind": args.image_kind, "jpeg_kb": round(sum(len(j) for j in jpegs) / len(jpegs) / 1024, 1),
@@ -226,6 +227,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1, help="SPMD data parallel over N ranks (torchrun)")
     ap.add_argument("--image-kind", choices=["noise", "photo"], default="noise",
                     help="synthetic JPEG content: uniform noise (worst-case host decode) or photo-like")
+    ap.add_argument("--gpu-timers", action="store_true",
+                    help="OCR stage times from HIP events (device time per stage) instead of host clocks")
     ap.add_argument("--predecoded", action="store_true",
                     help="decode the JPEGs once up front (GPU pipeline throughput without host JPEG decode)")
     a = ap.parse_args()

@@ -17,10 +17,14 @@
 #   prof_ttft      rocprofv3 kernel trace of 3 single-request TTFTs (8B fp8, 2 new tokens)
 #   prof_vlm8b     rocprofv3 kernel stats of the 8B fp8 decode bench (batch 16; prof_vlm8b_b1: single stream)
 #   face_ocr       tools/face_ocr_bench.py face + ocr
+#   ocr            OCR bench pre-decoded (HIP-event stage timers) + JPEG-inclusive
 #   prof_face / prof_ocr   rocprofv3 kernel stats of the face / OCR bench
 #   f8             fp8 tests (tests/test_fp8_gpu.py) + tools/f8_gemm_bench.py ($F8_SHAPES, $F8_M)
 #   pmc_face / pmc_ocr   PMC counters (SQ pass + memory pass) of the face / OCR pipelines
 #   serve          tools/serve_bench.py: gRPC hub end to end (CLIP ViT-L/14 64 clients, face 32 clients)
+#   serve_fe       serving through the engine / front-end topology (CLIP 128 clients, face 64; $SERVE_FE front ends)
+#   jpeg           device JPEG tests + tools/jpeg_bench.py
+#   ttft           VLM TTFT only (8B fp8, 30 requests, device JPEG decode)
 #   pmc_gemm       PMC counters (MFMA, LDS conflicts, busy) of one ViT-L/14 GEMM shape
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -80,6 +84,9 @@ for task in "$@"; do
     face_ocr)
       step face 400 python tools/face_ocr_bench.py --what face
       step ocr 400 python tools/face_ocr_bench.py --what ocr ;;
+    ocr)
+      step ocr_pre 300 python tools/face_ocr_bench.py --what ocr --predecoded --gpu-timers
+      step ocr_jpeg 300 python tools/face_ocr_bench.py --what ocr ;;
     prof_face)
       step prof_face 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_face -o run -- \
         python3 tools/face_ocr_bench.py --what face --iters 3 ;;
@@ -103,6 +110,16 @@ for task in "$@"; do
         --seconds 20
       step serve_face 300 python -u tools/serve_bench.py --service face --model antelopev2 --device cuda --clients 32 \
         --seconds 20 ;;
+    serve_fe)
+      step serve_clip_fe 400 python -u tools/serve_bench.py --service clip --model CLIP-ViT-L-14 --device cuda \
+        --clients "${SERVE_CLIENTS:-128}" --frontends "${SERVE_FE:-6}" --seconds 20
+      step serve_face_fe 400 python -u tools/serve_bench.py --service face --model antelopev2 --device cuda \
+        --clients "${SERVE_FACE_CLIENTS:-64}" --frontends "${SERVE_FE:-6}" --seconds 20 ;;
+    jpeg)
+      step jpeg_tests 200 python -u -m pytest tests/test_jpeg_gpu.py tests/test_jpeg_cpu.py -x -q --timeout 120 \
+        --timeout-method thread
+      step jpeg_bench 200 python -u tools/jpeg_bench.py ;;
+    ttft) step ttft 400 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0 ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
 done

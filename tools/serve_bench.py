@@ -145,6 +145,8 @@ def main():
     ap.add_argument("--server-threads", type=int, default=None)
     ap.add_argument("--client-procs", type=int, default=4, help="client processes (threads spread over them)")
     ap.add_argument("--procs", type=int, default=1, help="hub replica processes on one port (LUMEN_HUB_PROCS)")
+    ap.add_argument("--frontends", type=int, default=0,
+                    help="front-end processes over one GPU engine per device (LUMEN_FRONTENDS); 0 = in-process")
     ap.add_argument("--per-stream", type=int, default=1,
                     help="images per Infer stream (the service handles a stream's requests concurrently); "
                          "latency is then per stream")
@@ -185,7 +187,31 @@ def main():
     res = Downloader(cfg).download_all()
     assert all(r.success for r in res.values()), {k: r.error for k, r in res.items()}
     reps, rep_stop = [], None
-    if args.procs > 1:
+    fe_thread = fe_stop = None
+    if args.frontends > 0:
+        # engine / front-end topology (parallel/engine.py): one GPU engine process per device + K
+        # gRPC front-end processes on one port; this process only supervises and drives clients
+        import socket
+
+        from lumen_amd.hub.server import serve_frontends
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cfg_path = os.path.join(cache, "lumen-config.json")
+        d = cfg.model_dump(mode="json", exclude_none=True)
+        d["server"]["port"] = port
+        with open(cfg_path, "w") as f:
+            json.dump(d, f)
+        ready = ctx.Queue()
+        fe_stop = threading.Event()
+        fe_thread = threading.Thread(target=serve_frontends, args=(cfg_path, port, args.frontends),
+                                     kwargs={"stop_event": fe_stop, "ready_q": ready}, daemon=True)
+        fe_thread.start()
+        for _ in range(args.frontends):
+            ready.get(timeout=900)
+        app = server = None
+    elif args.procs > 1:
         # hub replica processes on one port (hub/server.py start_replicas, SO_REUSEPORT); this process
         # only drives the clients
         import socket
@@ -229,6 +255,9 @@ def main():
     if server is not None:
         server.stop(0)
         app.close()
+    if fe_stop is not None:
+        fe_stop.set()
+        fe_thread.join(timeout=120)
     if rep_stop is not None:
         rep_stop.set()
         for pr in reps:
@@ -239,13 +268,15 @@ def main():
            "p50_ms": round(float(np.percentile(la, 50)), 2), "p99_ms": round(float(np.percentile(la, 99)), 2),
            "mean_ms": round(float(la.mean()), 2), "requests": n, "seconds": round(el, 2), "errors": errors,
            "clients": args.clients, "service": args.service, "model": args.model, "device": args.device,
-           "dp_workers": args.dp, "hub_processes": args.procs, "images_per_stream": args.per_stream, "batch_cap": args.batch, "max_wait_ms": os.environ.get("LUMEN_MAX_WAIT_MS"),
+           "dp_workers": args.dp, "hub_processes": args.procs, "frontends": args.frontends, "images_per_stream": args.per_stream, "batch_cap": args.batch, "max_wait_ms": os.environ.get("LUMEN_MAX_WAIT_MS"),
            "image": f"{args.image_kind} JPEG {args.image_side * 4 // 3}x{args.image_side}, "
                     f"{int(np.mean([len(b) for b in imgs]) / 1024)} KiB mean",
            "load_s": round(load_s, 1),
            "server_stage_ms_p50": {k: round(float(np.median(v)), 2) for k, v in sorted(smeta.items())},
            "data": "synthetic (random-init weights of the named architecture, generated JPEGs)",
-           "path": "gRPC Infer stream -> hub router -> service -> dynamic batcher -> "
+           "path": ("gRPC Infer stream -> front-end process (service, decode, batcher) -> shm channel -> "
+                    "GPU engine process (cross-front-end batch)") if args.frontends > 0 else
+                   "gRPC Infer stream -> hub router -> service -> dynamic batcher -> "
                    + ("GPU worker pool (shm rings)" if args.dp > 1 else "in-process backend")}
     print(json.dumps(out), flush=True)
 
