@@ -21,22 +21,12 @@
 // Q/K/V are read in place from packed projections via strides, and O is
 // written as [b, s, h, d] so the out-projection GEMM consumes it directly.
 #include <cstdlib>
+#include "attention.h"
 #include "common.h"
 
 namespace lumen {
 
-struct AttnArgs {
-  const uint16_t* q; const uint16_t* k; const uint16_t* v; uint16_t* o;
-  int64_t q_sb, q_ss, q_sh;   // strides (elements) batch / seq / head
-  int64_t k_sb, k_ss, k_sh;
-  int64_t v_sb, v_ss, v_sh;
-  int64_t o_sb, o_ss, o_sh;
-  const int* kv_len;          // optional per-batch valid key count
-  int Sq, Sk, H, Hkv;
-  float scale_log2;           // softmax_scale * log2(e)
-  int causal;                 // query i attends keys j <= i + (Sk - Sq)
-};
-
+// AttnArgs: attention.h
 typedef short s16x4v __attribute__((ext_vector_type(4)));
 
 // K image: rows of D bf16; 16-byte chunk XOR so the ds_read_b128 A-fragment
@@ -257,8 +247,8 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
   }
 
   // ---- normalise and store O[b, q, h, d]: lane holds d = 16j + 4g + r for query col
-  if (qi < a.Sq) {
-    const float inv = l4[0] > 0.f ? __builtin_amdgcn_rcpf(l4[0]) : 0.f;
+  const float inv = l4[0] > 0.f ? __builtin_amdgcn_rcpf(l4[0]) : 0.f;
+  if (a.o != nullptr && qi < a.Sq) {
     uint16_t* orow = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qi * a.o_ss;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -266,6 +256,49 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
       w.x = pack2bf(o[j][0] * inv, o[j][1] * inv);
       w.y = pack2bf(o[j][2] * inv, o[j][3] * inv);
       *(uint2*)(orow + j * 16 + 4 * g) = w;
+    }
+  }
+  if constexpr (D >= 64) {
+    if (a.o8 != nullptr) {
+      // MX block m (d = 32m .. 32m+31) = fragments j = 2m, 2m+1 of the 4 lanes {l, l^16, l^32, l^48}
+      // holding this query: amax over the lane's 8 values, then over the lane quartet (whole wave
+      // takes part in the shuffles; lanes of one query share validity)
+      constexpr int NM = D / 32;
+      float am[NM];
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        float x = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x = fmaxf(x, fmaxf(fabsf(o[2 * m][r]), fabsf(o[2 * m + 1][r])));
+        x *= inv;
+        x = fmaxf(x, __shfl_xor(x, 16, 64));
+        am[m] = fmaxf(x, __shfl_xor(x, 32, 64));
+      }
+      if (qi < a.Sq) {
+        uint8_t* o8 = a.o8 + b * a.o8_sb + (int64_t)qi * a.o8_ss + h * D;
+        uint32_t sbytes = 0;
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+          const int e = mx_exp(am[m]);
+          const float sc = inv * mx_inv(e);
+          sbytes |= (uint32_t)(e + 127) << (8 * m);
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const int j = 2 * m + jj;
+            float t[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t[r] = fminf(fmaxf(o[j][r] * sc, -448.f), 448.f);
+            int w = __builtin_amdgcn_cvt_pk_fp8_f32(t[0], t[1], 0, false);
+            w = __builtin_amdgcn_cvt_pk_fp8_f32(t[2], t[3], w, true);
+            *(uint32_t*)(o8 + j * 16 + 4 * g) = (uint32_t)w;
+          }
+        }
+        uint8_t* os = a.os + b * a.os_sb + (int64_t)qi * a.os_ss + h * NM;
+        if (g == 0) {
+          if constexpr (NM == 4) *(uint32_t*)os = sbytes;
+          else *(uint16_t*)os = (uint16_t)sbytes;
+        }
+      }
     }
   }
 }
@@ -489,7 +522,10 @@ static hipError_t launch_res(const AttnArgs& a, int B, int nkc, hipStream_t stre
 hipError_t attn_fwd(const AttnArgs& a, int B, int D, hipStream_t stream) {
   // K/V-resident path when the whole K/V fits in 80 KiB and there are enough (batch, head) pairs
   const int nkc = (a.Sk + 63) / 64;
-  const bool res_ok = (int64_t)B * a.H >= 1024 && (size_t)nkc * 2 * 64 * D * 2 <= 80 * 1024 && a.Sq <= 1024;
+  if (a.o8 != nullptr && D < 64) return hipErrorInvalidValue;
+  if (a.o == nullptr && a.o8 == nullptr) return hipErrorInvalidValue;
+  const bool res_ok = a.o8 == nullptr && (int64_t)B * a.H >= 1024 && (size_t)nkc * 2 * 64 * D * 2 <= 80 * 1024 &&
+                      a.Sq <= 1024;
   if (res_ok) {
     if (D == 64) return launch_res<64>(a, B, nkc, stream);
     if (D == 128) return launch_res<128>(a, B, nkc, stream);

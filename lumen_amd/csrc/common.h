@@ -89,6 +89,30 @@ __device__ __forceinline__ uint8_t f2fp8(float v) {
   return (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false) & 0xff);
 }
 
+// ---- MX fp8 blocks (OCP microscaling): 32 e4m3fn values sharing one E8M0 exponent --------
+// The producers of a W8A8 GEMM operand (GEMM epilogues, attention) quantise each 32-value
+// block with its own power-of-two scale and the consumer feeds that byte straight into the
+// scale operand of v_mfma_scale_f32_16x16x128_f8f6f4 (one byte per lane = per 32 k-values).
+// mx_exp: the smallest e with amax / 2^e <= 448 (the E8M0 byte is e + 127), clamped so 2^-e
+// stays a normal float; amax = 0 gives the smallest scale.
+__device__ __forceinline__ int mx_exp(float amax) {
+  const uint32_t b = __float_as_uint(amax * (1.f / 448.f));
+  int e = (int)((b >> 23) & 0xff) - 127 + ((b & 0x7fffff) != 0);
+  return min(max(e, -127), 126);
+}
+__device__ __forceinline__ float mx_inv(int e) { return __uint_as_float((uint32_t)(127 - e) << 23); }   // 2^-e
+// 8 floats * inv -> 8 e4m3fn bytes, saturated to +-448
+__device__ __forceinline__ uint2 fp8x8_scaled(const float* f, float inv) {
+  float t[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) t[q] = fminf(fmaxf(f[q] * inv, -448.f), 448.f);
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(t[0], t[1], 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(t[2], t[3], lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(t[4], t[5], 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(t[6], t[7], hi, true);
+  return make_uint2((unsigned)lo, (unsigned)hi);
+}
+
 // ---- wave reductions (64 lanes) -----------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

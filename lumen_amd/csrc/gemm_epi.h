@@ -49,6 +49,22 @@ struct GemmEpi {
   const float* col_aff;
 };
 
+// MX operand / outputs of the W8A8 prefill GEMM (gemm_f8.hip::gemm_mx; fields documented there)
+struct MxArgs {
+  const uint8_t* a_bs;
+  int64_t ld_bs;
+  const float* ssq_in;
+  int ssq_in_tiles;
+  float norm_eps;
+  uint8_t* q8;
+  int64_t ldq;
+  uint8_t* qs;
+  int64_t ldqs;
+  float* ssq_out;
+  int ssq_out_tiles;
+  int skip_c;        // SwiGLU with q8: no bf16 output
+};
+
 // Launch plan of an fp8-weight decode GEMM (gemm_w8.hip): column tiles per wave, K splits and
 // the K chunk per split.  The host sizes the split-K slabs / counters from the same plan.
 struct W8DecPlan {

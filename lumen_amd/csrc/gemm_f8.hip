@@ -22,9 +22,13 @@
 // keeps NSTAGE-2 stages in flight across the barrier.  LDS rows are 128 B with the
 // 16-byte chunk XOR swizzle of gemm_epi.h::swz applied on the per-lane *source*
 // address.  Each MFMA lane reads two 16-byte chunks of its row: lane group g = lane/16
-// takes logical chunks g and g+4 (k = 16g..16g+15 and 64+16g..64+16g+15).  The same
-// k permutation is used for A and W, so the dot products are unchanged, and with it
-// every ds_read_b128 lane group hits 64 distinct banks (chunks 2g, 2g+1 would be 2-way).
+// takes chunks g and g+4 (k = 16g..16g+15 and 64+16g..64+16g+15), which is the
+// instruction's own k order -- it runs as two k = 64 halves, VGPRs 0-3 then 4-7, lane
+// group g holding 16 k of each -- and every ds_read_b128 lane group hits 64 distinct banks.
+// In that order the 32-value block b (k = 32b..32b+31) spans lane groups 2(b&1), 2(b&1)+1
+// of half b/2, and its E8M0 scale is the byte lane group b supplies (measured: a
+// contiguous-32-per-lane assumption scaled the wrong k, tests/test_mx_gpu.py), so MX
+// activations (gemm_mx) need no layout change: lane (row, g) passes row's scale of block g.
 #include <algorithm>
 #include <cstdlib>
 #include <map>
@@ -68,11 +72,24 @@ struct SkArgs {
   uint32_t* cnt;    // [tiles] arrival tickets (zero between launches: the last arriver resets)
 };
 
-template <int NSTAGE, int WN, bool F8, int BN = 128, bool SK = false>
+// MX (block-scaled) operand and outputs of the W8A8 prefill chain (ops.linear_mx):
+//  * BS launches read A's E8M0 exponents (one per row per 32 k) and feed them to the MFMA's A
+//    scale operand, so any producer can quantise with block-local scales (no per-row pass);
+//  * ssq_in: the producing GEMM's per-(row, column-tile) sums of squares -> rstd row scale (the
+//    RMSNorm folded into this projection, gamma already folded into W: LLM.fold_norms);
+//  * q8 / qs: an MX fp8 copy of this GEMM's output for the next projection (32-column blocks;
+//    SwiGLU outputs need 64-column wave tiles so one 4-lane group owns a block);
+//  * ssq_out: per-(row, BN tile) sums of squares of the stored bf16 output (residual stream).
+// (MxArgs: gemm_epi.h)
+
+constexpr int MX_SCRATCH = 40960;    // epilogue LDS bytes past the per-wave slabs: rstd[128], ssq[128][WN]
+
+template <int NSTAGE, int WN, bool F8, int BN = 128, bool SK = false, bool BS = false>
 __global__ void __launch_bounds__(128 * WN)
 gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restrict__ sa, const uint8_t* __restrict__ W,
                int64_t ldw, const float* __restrict__ sw, void* __restrict__ C, int64_t ldc, int M, int N, int K,
-               GemmEpi ep, SkArgs sk) {
+               GemmEpi ep, SkArgs sk, MxArgs mx) {
+  static_assert(!BS || F8, "block scales: fp8 operands only");
   constexpr int ES = F8 ? 1 : 2;         // bytes per element
   lda *= ES;
   ldw *= ES;
@@ -82,7 +99,8 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
   constexpr int PER = 16 / NW;           // glds instructions per wave for the A image per stage
   constexpr int PERW = (BN / 8) / NW;    // ... and for the W image
   static_assert(NR >= 1 && PERW >= 1, "tile / wave split");
-  constexpr int STAGE = 128 * 128 + BN * 128;   // bytes: A image then W image
+  constexpr int SCB = BS ? NW * 256 : 0;          // A scale bytes per stage (each wave: 64 rows x 4)
+  constexpr int STAGE = 128 * 128 + BN * 128 + SCB;   // bytes: A image, W image, A scales
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -117,6 +135,9 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
       const int c = (lane & 7) ^ ((r >> 1) & 7);
       src_w[i] = W + (int64_t)min(n0 + r, N - 1) * ldw + c * 16;
     }
+    // BS: every wave stages the 4 scale bytes of one 64-row half per K-step (waves 0 / 1 are the
+    // copies the fragments read; the others keep the per-wave glds count uniform for vmcnt)
+    const uint8_t* src_s = BS ? mx.a_bs + (int64_t)min(m0 + (wid & 1) * 64 + lane, M - 1) * mx.ld_bs : nullptr;
     auto stage = [&](int s, int64_t koff) {
       char* base = smem + s * STAGE;
 #pragma unroll
@@ -127,6 +148,9 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
       for (int i = 0; i < PERW; ++i)
         __builtin_amdgcn_global_load_lds((g_ptr_t)(src_w[i] + koff),
                                          (lds_ptr_t)(base + 128 * 128 + (wid * PERW + i) * 1024), 16, 0, 0);
+      if constexpr (BS)
+        __builtin_amdgcn_global_load_lds((g_ptr_t)(src_s + (koff >> 7) * 4),
+                                         (lds_ptr_t)(base + 128 * 128 + BN * 128 + wid * 256), 4, 0, 0);
     };
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -139,7 +163,7 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
 
     for (int kt = 0; kt < n; ++kt) {
       // stage kt landed for this wave (NSTAGE-2 younger stages may stay in flight) ...
-      if (kt + NSTAGE - 2 < n) f8_vm_wait<(PER + PERW) * (NSTAGE - 2)>();
+      if (kt + NSTAGE - 2 < n) f8_vm_wait<(PER + PERW + (BS ? 1 : 0)) * (NSTAGE - 2)>();
       else f8_vm_wait<0>();
       // ... and for every wave; every wave is also done reading stage kt-1's buffer
       __builtin_amdgcn_s_barrier();
@@ -147,6 +171,7 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
       const char* sA = smem + (kt % NSTAGE) * STAGE;
       const char* sW = sA + 128 * 128;
       u32x4_t fa[4][2], fb[NR][2];
+      int as[4];
 #pragma unroll
       for (int j = 0; j < NR; ++j) {
         const int r = wn * TN + j * 16 + frow;
@@ -158,6 +183,8 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
         const int r = wm * 64 + i * 16 + frow;
         fa[i][0] = *(const u32x4_t*)(sA + swz(r, g));
         fa[i][1] = *(const u32x4_t*)(sA + swz(r, g + 4));
+        if constexpr (BS) as[i] = *(const uint8_t*)(sA + 128 * 128 + BN * 128 + wm * 256 + (i * 16 + frow) * 4 + g);
+        else as[i] = 127;
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -168,7 +195,7 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
                                          (int)fa[i][1][0], (int)fa[i][1][1], (int)fa[i][1][2], (int)fa[i][1][3]};
             const i32x8_t b8 = (i32x8_t){(int)fb[j][0][0], (int)fb[j][0][1], (int)fb[j][0][2], (int)fb[j][0][3],
                                          (int)fb[j][1][0], (int)fb[j][1][1], (int)fb[j][1][2], (int)fb[j][1][3]};
-            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, acc[i][j], 0, 0, 0, 127, 0, 127);
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, acc[i][j], 0, 0, 0, as[i], 0, 127);
           } else {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[i][0]),
                                                                 __builtin_bit_cast(bf16x8_t, fb[j][0]), acc[i][j], 0, 0, 0);
@@ -187,6 +214,18 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
     constexpr int RPP = 64 / LPR;          // rows per pass
     constexpr int NPASS = RPP >= 16 ? 1 : 16 / RPP;
     float* es = (float*)smem + wid * 16 * LDSTR;
+    float* rstd_s = (float*)(smem + MX_SCRATCH);     // [128]
+    float* ssq_s = rstd_s + 128;                      // [128][WN]
+    const bool mx_out = mx.q8 != nullptr || mx.ssq_out != nullptr;
+    if (mx.ssq_in) {   // rstd of the tile's rows from the producer's partial sums of squares
+      if (tid < 128) {
+        const float* p = mx.ssq_in + (int64_t)min(m0 + tid, M - 1) * mx.ssq_in_tiles;
+        float ss = 0.f;
+        for (int j = 0; j < mx.ssq_in_tiles; ++j) ss += p[j];
+        rstd_s[tid] = rsqrtf(ss / (float)K + mx.norm_eps);
+      }
+      __syncthreads();
+    }
     const int cc = (lane % LPR) * 16;
     const int n = n0 + wn * TN + cc;
     float cs[16];
@@ -202,9 +241,10 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
 #pragma unroll
       for (int p = 0; p < NPASS; ++p) {
         const int rr = p * RPP + lane / LPR;
-        if (rr >= 16) continue;
-        const int m = m0 + wm * 64 + i * 16 + rr;
-        const float rs = m < M ? (sa ? sa[m] : 1.f) : 0.f;
+        if (rr >= 16) continue;             // whole LPR-lane row groups skip together
+        const int mt = wm * 64 + i * 16 + rr, m = m0 + mt;
+        float rs = m < M ? (sa ? sa[m] : 1.f) : 0.f;
+        if (mx.ssq_in) rs *= rstd_s[mt];
         float v[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -214,10 +254,72 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
           v[q * 4 + 2] = t[2] * rs * cs[q * 4 + 2];
           v[q * 4 + 3] = t[3] * rs * cs[q * 4 + 3];
         }
-        epi_store16_t<false>(v, m, n, M, N, C, ldc, ep, crs);
+        if (!mx_out) {
+          epi_store16_t<false>(v, m, n, M, N, C, ldc, ep, crs);
+          continue;
+        }
+        const bool valid = m < M && n < N;
+        if (ep.glu) {
+          // SwiGLU -> 8 outputs [n/2, n/2 + 8); a 4-lane row group owns one 32-output MX block
+          if (ep.bias) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+              v[q] += valid ? (ep.bias_f32 ? ((const float*)ep.bias)[n + q] : bf2f(((const uint16_t*)ep.bias)[n + q]))
+                            : 0.f;
+          }
+          float r[8], am = 0.f;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            r[q] = valid ? v[q] * fast_rcp(1.f + __expf(-v[q])) * v[8 + q] : 0.f;
+            am = fmaxf(am, fabsf(r[q]));
+          }
+          if (valid && !mx.skip_c) st16<false>(C, crs, ((int64_t)m * ldc + (n >> 1)) * 2, pack8(r));
+          if constexpr (LPR >= 4) if (mx.q8) {     // host: SwiGLU + q8 only on 64-column wave tiles
+            am = fmaxf(am, __shfl_xor(am, 1, 64));
+            am = fmaxf(am, __shfl_xor(am, 2, 64));
+            const int e = mx_exp(am);
+            if (valid) {
+              *(uint2*)(mx.q8 + (int64_t)m * mx.ldq + (n >> 1)) = fp8x8_scaled(r, mx_inv(e));
+              if ((lane & 3) == 0) mx.qs[(int64_t)m * mx.ldqs + (n >> 6)] = (uint8_t)(e + 127);
+            }
+          }
+          continue;
+        }
+        if (valid) epi_store16_t<false>(v, m, n, M, N, C, ldc, ep, crs);   // v -> the stored values (fp32)
+        float f[16], am = 0.f, ss = 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          f[q] = valid ? bf2f(f2bf(v[q])) : 0.f;     // what the residual stream now holds
+          am = fmaxf(am, fabsf(f[q]));
+          ss += f[q] * f[q];
+        }
+        if (mx.q8) {
+          am = fmaxf(am, __shfl_xor(am, 1, 64));     // lanes 2k, 2k+1: one 32-column block
+          const int e = mx_exp(am);
+          if (valid) {
+            const float inv = mx_inv(e);
+            const uint2 lo = fp8x8_scaled(f, inv), hi = fp8x8_scaled(f + 8, inv);
+            *(u32x4_t*)(mx.q8 + (int64_t)m * mx.ldq + n) = (u32x4_t){lo.x, lo.y, hi.x, hi.y};
+            if ((lane & 1) == 0) mx.qs[(int64_t)m * mx.ldqs + (n >> 5)] = (uint8_t)(e + 127);
+          }
+        }
+        if (mx.ssq_out) {
+          ss += __shfl_xor(ss, 1, 64);
+          if constexpr (LPR >= 4) ss += __shfl_xor(ss, 2, 64);
+          if (lane % LPR == 0) ssq_s[mt * WN + wn] = ss;
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     });
+    if (mx.ssq_out) {   // fixed-order sum over the WN column slices -> one partial per (row, BN tile)
+      __syncthreads();
+      if (tid < 128 && m0 + tid < M) {
+        float ss = 0.f;
+#pragma unroll
+        for (int w = 0; w < WN; ++w) ss += ssq_s[tid * WN + w];
+        mx.ssq_out[(int64_t)(m0 + tid) * mx.ssq_out_tiles + n0 / BN] = ss;
+      }
+    }
   };
 
   if constexpr (!SK) {
@@ -284,20 +386,25 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
   }
 }
 
-template <int NS, int WN, bool F8 = true, int BN = 128>
+template <int NS, int WN, bool BS, int BN>
+static constexpr size_t f8_lds() {
+  return (size_t)NS * (128 * 128 + BN * 128 + (BS ? 2 * WN * 256 : 0));
+}
+
+template <int NS, int WN, bool F8 = true, int BN = 128, bool BS = false>
 static hipError_t launch_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
                             const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep,
-                            hipStream_t stream, int splits = 1) {
-  const size_t lds = (size_t)NS * (128 * 128 + BN * 128);
+                            hipStream_t stream, int splits = 1, const MxArgs& mx = MxArgs{}) {
+  constexpr size_t lds = f8_lds<NS, WN, BS, BN>();
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm_f8_kernel<NS, WN, F8, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)lds);
+    hipFuncSetAttribute((const void*)gemm_f8_kernel<NS, WN, F8, BN, false, BS>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int tiles = ((M + 127) / 128) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8, BN>), dim3(tiles, splits), dim3(128 * WN), lds, stream, A, lda, sa, W,
-                     ldw, sw, C, ldc, M, N, K, ep, SkArgs{});
+  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8, BN, false, BS>), dim3(tiles, splits), dim3(128 * WN), lds, stream, A,
+                     lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, SkArgs{}, mx);
   return hipGetLastError();
 }
 
@@ -308,10 +415,10 @@ static uint32_t* sk_counters(size_t n, hipStream_t stream);
 static float* sk_slabs(size_t bytes, hipStream_t stream);
 static int f8_num_cus();
 
-template <int NS, int WN, bool F8 = true, int BN = 128>
+template <int NS, int WN, bool F8 = true, int BN = 128, bool BS = false>
 static hipError_t launch_f8_sk(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
                                const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep,
-                               hipStream_t stream) {
+                               hipStream_t stream, const MxArgs& mx = MxArgs{}) {
   constexpr int ES = F8 ? 1 : 2;
   const int tiles = ((M + 127) / 128) * ((N + BN - 1) / BN);
   const int nk = K * ES / 128;
@@ -323,16 +430,16 @@ static hipError_t launch_f8_sk(const uint8_t* A, int64_t lda, const float* sa, c
   sk.ws = sk_slabs((size_t)tiles * sk.maxc * 128 * BN * sizeof(float), stream);
   sk.cnt = sk_counters((size_t)tiles, stream);
   if (sk.ws == nullptr || sk.cnt == nullptr) return hipErrorNotReady;
-  const size_t lds = (size_t)NS * (128 * 128 + BN * 128);
+  constexpr size_t lds = f8_lds<NS, WN, BS, BN>();
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm_f8_kernel<NS, WN, F8, BN, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)lds);
+    hipFuncSetAttribute((const void*)gemm_f8_kernel<NS, WN, F8, BN, true, BS>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int used = (total + sk.ipw - 1) / sk.ipw;   // workgroups with work
-  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8, BN, true>), dim3(used), dim3(128 * WN), lds, stream, A, lda, sa, W, ldw,
-                     sw, C, ldc, M, N, K, ep, sk);
+  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8, BN, true, BS>), dim3(used), dim3(128 * WN), lds, stream, A, lda, sa, W,
+                     ldw, sw, C, ldc, M, N, K, ep, sk, mx);
   return hipGetLastError();
 }
 
@@ -516,6 +623,40 @@ hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t
   return launch_variant<true>(multi_wave ? 1 : 2, A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
 }
 
+// W8A8 with MX-scaled activations (ops.linear_mx, the fused prefill chain of LLM._layers_mx).
+// No split-K (its slab reduce has no MX epilogue).  Codes as launch_variant; SwiGLU with an MX
+// output needs 64-column wave tiles (codes 1, 4, 10), a sums-of-squares output 128-column tiles.
+hipError_t gemm_mx(const uint8_t* A, int64_t lda, const uint8_t* a_bs, int64_t ld_bs, const uint8_t* W, int64_t ldw,
+                   const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, MxArgs mx,
+                   hipStream_t stream, int variant) {
+  if (K % 128 != 0 || N % 16 != 0 || M <= 0 || lda % 16 != 0 || ldw % 16 != 0 || ld_bs < K / 32 || ld_bs % 4 != 0)
+    return hipErrorInvalidValue;
+  if (ep.split_koff || ep.out_group || ep.table || ep.prelu || ep.post_act || ep.row_aff) return hipErrorInvalidValue;
+  if (mx.skip_c && !(ep.glu && mx.q8)) return hipErrorInvalidValue;
+  mx.a_bs = a_bs;
+  mx.ld_bs = ld_bs;
+  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  const bool multi_wave = tiles > f8_num_cus();
+  int v = variant > 0 ? variant : (multi_wave ? 1 : 2);
+  if (ep.glu && mx.q8 && !(v == 1 || v == 4 || v == 10)) v = multi_wave ? 1 : 4;
+  hipError_t e = hipErrorNotReady;
+  switch (v) {
+    case 9: e = launch_f8_sk<3, 4, true, 128, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, mx); break;
+    case 10: e = launch_f8_sk<4, 2, true, 128, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, mx); break;
+    case 11: e = launch_f8_sk<4, 4, true, 128, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, mx); break;
+    default: break;
+  }
+  if (e != hipErrorNotReady) return e;
+  if (v >= 9) v = v == 10 ? 4 : 2;    // no stream-K workspace (first call inside a graph capture)
+  switch (v) {
+    case 1: return launch_f8<2, 2, true, 128, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, 1, mx);
+    case 3: return launch_f8<4, 4, true, 128, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, 1, mx);
+    case 4: return launch_f8<4, 2, true, 128, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, 1, mx);
+    case 5: return launch_f8<2, 4, true, 128, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, 1, mx);
+    default: return launch_f8<3, 4, true, 128, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, 1, mx);
+  }
+}
+
 // ============================================================================ quantisers
 // Per-token dynamic quantisation: scale[m] = max|y[m, :]| / 448, out = e4m3(y / scale).
 // One 256-thread workgroup per row; rows are re-read (L2-resident) instead of being held
@@ -637,6 +778,48 @@ __global__ void __launch_bounds__(256) rms_norm_quant_fp8_kernel(const uint16_t*
       *(uint2*)(out + m * ldo + k) = to_fp8x8(v[c]);
     }
   }
+}
+
+// bf16 rows -> MX fp8 (E8M0 per 32 columns) + per-(row, 128-column) sums of squares: the first
+// layer's input of the MX prefill chain (later layers get theirs from the GEMM epilogues).
+// One wave per row slice of 512 columns: lane -> 8 columns, 4 lanes per MX block, 16 per ssq tile.
+__global__ void __launch_bounds__(256) quant_rows_mx_kernel(const uint16_t* __restrict__ x, int64_t ldx,
+                                                            uint8_t* __restrict__ q8, int64_t ldq,
+                                                            uint8_t* __restrict__ qs, int64_t ldqs,
+                                                            float* __restrict__ ssq, int64_t ldss, int M, int K) {
+  const int lane = threadIdx.x & 63;
+  const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);   // (row, 512-column slice)
+  const int slices = (K + 511) / 512;
+  if (item >= (int64_t)M * slices) return;
+  const int64_t m = item / slices;
+  const int k = (int)(item % slices) * 512 + lane * 8;
+  const bool valid = k < K;
+  float f[8], am = 0.f, ss = 0.f;
+  if (valid) unpack8(*(const u32x4_t*)(x + m * ldx + k), f);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    if (!valid) f[q] = 0.f;
+    am = fmaxf(am, fabsf(f[q]));
+    ss += f[q] * f[q];
+  }
+  am = fmaxf(am, __shfl_xor(am, 1, 64));
+  am = fmaxf(am, __shfl_xor(am, 2, 64));
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) ss += __shfl_xor(ss, o, 64);
+  if (!valid) return;
+  const int e = mx_exp(am);
+  *(uint2*)(q8 + m * ldq + k) = fp8x8_scaled(f, mx_inv(e));
+  if ((lane & 3) == 0) qs[m * ldqs + (k >> 5)] = (uint8_t)(e + 127);
+  if (ssq && (lane & 15) == 0) ssq[m * ldss + (k >> 7)] = ss;
+}
+
+hipError_t quant_rows_mx(const uint16_t* x, int64_t ldx, uint8_t* q8, int64_t ldq, uint8_t* qs, int64_t ldqs,
+                         float* ssq, int64_t ldss, int M, int K, hipStream_t stream) {
+  if (K % 128 != 0 || M <= 0 || ldx % 8 != 0) return hipErrorInvalidValue;
+  const int64_t items = (int64_t)M * ((K + 511) / 512);
+  hipLaunchKernelGGL(quant_rows_mx_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, stream, x, ldx, q8, ldq, qs,
+                     ldqs, ssq, ldss, M, K);
+  return hipGetLastError();
 }
 
 hipError_t quant_rows_fp8(const uint16_t* x, int64_t ldx, uint8_t* out, int64_t ldo, float* scale, int M, int K,

@@ -70,8 +70,102 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(RopeKVArgs a, int nrot_blo
   else a.v_cache[vo] = vr[idx];
 }
 
+// Prefill form (T >= 64): one workgroup per (64-token tile, head) with 16-byte accesses.  q / k
+// heads: each thread rotates D/8 pairs of one token (4 threads per token) in place and writes the
+// k cache rows; v heads: the [64 x D] tile goes through LDS and leaves d-major, 8 tokens (16 or
+// 8 bytes) per store when their slots are consecutive in one block.  The per-element kernel above
+// wrote V with 2-byte stores 128 bytes apart (11 us per 8B-prefill layer at 624 tokens).
+template <int D>
+__global__ void __launch_bounds__(256) rope_kv_tile_kernel(RopeKVArgs a) {
+  constexpr int HALF = D / 2, PPT = D / 8;       // rotation pairs per thread
+  __shared__ __attribute__((aligned(16))) uint16_t vt[64][D + 8];
+  __shared__ int64_t sl[64];
+  const int t0 = blockIdx.x * 64, hh = blockIdx.y, tid = threadIdx.x;
+  if (hh < a.H + a.Hkv) {
+    const int tt = tid >> 2, c0 = (tid & 3) * PPT, t = t0 + tt;
+    if (t >= a.T) return;
+    uint16_t* hp = a.qkv + (int64_t)t * a.ld + hh * D;
+    const float2* cs = reinterpret_cast<const float2*>(a.cos_sin) + (int64_t)a.pos[t] * HALF + c0;
+    float y1[PPT], y2[PPT];
+#pragma unroll
+    for (int u = 0; u < PPT; u += 8) {
+      float x1[8], x2[8];
+      unpack8(*(const u32x4_t*)(hp + c0 + u), x1);
+      unpack8(*(const u32x4_t*)(hp + HALF + c0 + u), x2);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float2 c = cs[u + q];
+        y1[u + q] = x1[q] * c.x - x2[q] * c.y;
+        y2[u + q] = x2[q] * c.x + x1[q] * c.y;
+      }
+      *(u32x4_t*)(hp + c0 + u) = pack8(y1 + u);
+      *(u32x4_t*)(hp + HALF + c0 + u) = pack8(y2 + u);
+    }
+    const int64_t slot = a.slots && hh >= a.H ? a.slots[t] : -1;
+    if (slot >= 0) {
+      const int64_t ko = (((slot >> 6) * a.Hkv + (hh - a.H)) * KV_BLOCK + (slot & 63)) * D;
+#pragma unroll
+      for (int u = 0; u < PPT; u += 8) {
+        float r1[8], r2[8];   // the stored (bf16-rounded) values, as the per-element kernel caches them
+        unpack8(pack8(y1 + u), r1);
+        unpack8(pack8(y2 + u), r2);
+        if (a.kv_fp8) {
+          uint8_t* kr = reinterpret_cast<uint8_t*>(a.k_cache) + ko;
+          *(uint2*)(kr + c0 + u) = fp8x8_scaled(r1, 1.f);
+          *(uint2*)(kr + HALF + c0 + u) = fp8x8_scaled(r2, 1.f);
+        } else {
+          *(u32x4_t*)(a.k_cache + ko + c0 + u) = pack8(r1);
+          *(u32x4_t*)(a.k_cache + ko + HALF + c0 + u) = pack8(r2);
+        }
+      }
+    }
+    return;
+  }
+  if (a.slots == nullptr) return;
+  const int kh = hh - a.H - a.Hkv;
+  if (tid < 64) sl[tid] = t0 + tid < a.T ? a.slots[t0 + tid] : -1;
+  constexpr int CPR = D / 8;                       // 16-byte chunks per token row
+  for (int c = tid; c < 64 * CPR; c += 256) {
+    const int tt = c / CPR, ch = c % CPR;
+    if (t0 + tt < a.T)
+      *(u32x4_t*)&vt[tt][ch * 8] = *(const u32x4_t*)(a.qkv + (int64_t)(t0 + tt) * a.ld + (a.H + a.Hkv + kh) * D + ch * 8);
+  }
+  __syncthreads();
+  // thread -> (d, run of 8 tokens)
+  for (int w = tid; w < D * 8; w += 256) {
+    const int d = w % D, g8 = w / D;
+    const int64_t s0 = sl[g8 * 8];
+    bool run = s0 >= 0 && (s0 & 7) == 0;
+#pragma unroll
+    for (int q = 1; q < 8; ++q) run = run && sl[g8 * 8 + q] == s0 + q;
+    if (run) {
+      const int64_t vo = (((s0 >> 6) * a.Hkv + kh) * D + d) * KV_BLOCK + (s0 & 63);
+      float f[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) f[q] = bf2f(vt[g8 * 8 + q][d]);
+      if (a.kv_fp8) *(uint2*)(reinterpret_cast<uint8_t*>(a.v_cache) + vo) = fp8x8_scaled(f, 1.f);
+      else *(u32x4_t*)(a.v_cache + vo) = pack8(f);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int64_t s = sl[g8 * 8 + q];
+        if (s < 0) continue;
+        const int64_t vo = (((s >> 6) * a.Hkv + kh) * D + d) * KV_BLOCK + (s & 63);
+        if (a.kv_fp8) reinterpret_cast<uint8_t*>(a.v_cache)[vo] = f2fp8(bf2f(vt[g8 * 8 + q][d]));
+        else a.v_cache[vo] = vt[g8 * 8 + q][d];
+      }
+    }
+  }
+}
+
 hipError_t rope_kv(const RopeKVArgs& a, hipStream_t stream) {
   if (a.T == 0) return hipSuccess;
+  if (a.T >= 64 && (a.D == 64 || a.D == 128) && a.ld % 8 == 0) {
+    const dim3 grid((a.T + 63) / 64, a.H + 2 * a.Hkv);
+    if (a.D == 128) hipLaunchKernelGGL(rope_kv_tile_kernel<128>, grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL(rope_kv_tile_kernel<64>, grid, dim3(256), 0, stream, a);
+    return hipGetLastError();
+  }
   const int nrot_blocks = ((a.H + a.Hkv) * (a.D / 2) + 255) / 256;
   const int v_blocks = a.slots ? (a.Hkv * a.D + 255) / 256 : 0;
   hipLaunchKernelGGL(rope_kv_kernel, dim3(a.T, nrot_blocks + v_blocks), dim3(256), 0, stream, a, nrot_blocks);

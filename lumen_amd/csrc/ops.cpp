@@ -17,6 +17,7 @@
 #include <algorithm>
 
 #include "gemm_epi.h"
+#include "attention.h"
 #include "conv.h"
 
 namespace lumen {
@@ -30,6 +31,11 @@ hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t
                    int variant = 0);
 hipError_t quant_rows_fp8(const uint16_t* x, int64_t ldx, uint8_t* out, int64_t ldo, float* scale, int M, int K,
                           hipStream_t stream);
+hipError_t gemm_mx(const uint8_t* A, int64_t lda, const uint8_t* a_bs, int64_t ld_bs, const uint8_t* W, int64_t ldw,
+                   const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, MxArgs mx,
+                   hipStream_t stream, int variant);
+hipError_t quant_rows_mx(const uint16_t* x, int64_t ldx, uint8_t* q8, int64_t ldq, uint8_t* qs, int64_t ldqs,
+                         float* ssq, int64_t ldss, int M, int K, hipStream_t stream);
 hipError_t rms_norm_quant_fp8(const uint16_t* x, int64_t ldx, const uint16_t* add, int64_t ldadd, uint16_t* resid_out,
                               int64_t ldr, const uint16_t* gamma, float eps, uint8_t* out, int64_t ldo, float* scale,
                               int M, int K, hipStream_t stream);
@@ -47,12 +53,6 @@ hipError_t cls_fill(uint16_t* x, int64_t seq_stride, const uint16_t* cls, const 
                     hipStream_t stream);
 hipError_t embed_gather(const int64_t* ids, const uint16_t* table, const uint16_t* pos, int S, uint16_t* out,
                         int rows, int D, int64_t vocab, int64_t id_offset, hipStream_t stream);
-struct AttnArgs {
-  const uint16_t* q; const uint16_t* k; const uint16_t* v; uint16_t* o;
-  int64_t q_sb, q_ss, q_sh; int64_t k_sb, k_ss, k_sh; int64_t v_sb, v_ss, v_sh; int64_t o_sb, o_ss, o_sh;
-  const int* kv_len; int Sq, Sk, H, Hkv; float scale_log2; int causal;
-};
-hipError_t attn_fwd(const AttnArgs& a, int B, int D, hipStream_t stream);
 struct ImgGeomRaw;
 struct PrepArgs {
   const uint8_t* src; const ImgGeomRaw* geom; float* tmp; int tmp_h, tmp_w; void* out; int OH, OW;
@@ -380,6 +380,112 @@ void gemm_f8(const at::Tensor& a8, const at::Tensor& sa, const at::Tensor& w8, c
                                  (int)splits, (int)variant));
 }
 
+// ---------------------------------------------------------------- MX W8A8 (block-scaled activations)
+static void check_u8_rows(const at::Tensor& t, int64_t M, int64_t cols, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kByte && t.dim() == 2 && t.stride(1) == 1 && t.size(0) >= M &&
+              t.size(1) >= cols && t.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 4 == 0,
+              name, ": uint8 [rows, >= ", cols, "] with 4-byte aligned rows");
+}
+static void check_f32_rows(const at::Tensor& t, int64_t M, int64_t cols, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.dim() == 2 && t.stride(1) == 1 && t.size(0) >= M &&
+              t.size(1) >= cols, name, ": f32 [rows, >= ", cols, "]");
+}
+
+// out = epi(rstd? * (A . W^T) * sw[n]) with A = a8 [M, K] e4m3fn x 2^(a_bs - 127) per 32 columns;
+// optional MX fp8 copy of the output (q8 / qs), per-(row, 128-column) sums of squares (ssq_out),
+// RMSNorm row scale from the producer's sums of squares (ssq_in [M, K/128], norm_eps).
+void gemm_mx(const at::Tensor& a8, const at::Tensor& a_bs, const at::Tensor& w8, const at::Tensor& sw,
+             const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& residual,
+             const c10::optional<at::Tensor>& out, int64_t glu, const c10::optional<at::Tensor>& ssq_in, double norm_eps,
+             const c10::optional<at::Tensor>& q8, const c10::optional<at::Tensor>& qs,
+             const c10::optional<at::Tensor>& ssq_out, int64_t variant) {
+  check_f8_rows(a8, "gemm_mx: a8");
+  check_f8_rows(w8, "gemm_mx: w8");
+  const int64_t M = a8.size(0), K = a8.size(1), N = w8.size(0);
+  TORCH_CHECK(w8.size(1) == K && K % 128 == 0 && N % 128 == 0, "gemm_mx: K % 128 == 0, N % 128 == 0");
+  TORCH_CHECK(variant >= 0 && variant <= 11 && variant != 6 && variant != 7 && variant != 8, "gemm_mx: variant");
+  check_u8_rows(a_bs, M, K / 32, "gemm_mx: a_bs");
+  TORCH_CHECK(sw.is_cuda() && sw.scalar_type() == at::kFloat && sw.numel() == N && sw.is_contiguous(),
+              "gemm_mx: sw f32 [N]");
+  const int64_t NO = glu ? N / 2 : N;
+  lumen::GemmEpi ep{};
+  ep.alpha = 1.f;
+  ep.glu = (int)glu;
+  lumen::MxArgs mx{};
+  void* cp = nullptr;
+  int64_t ldc = 0;
+  if (out.has_value() && out->defined()) {
+    check_bf16_rows(*out, "out");
+    TORCH_CHECK(out->size(0) >= M && out->size(1) >= NO, "gemm_mx: out [M, N (or N/2 with glu)] bf16");
+    cp = out->data_ptr();
+    ldc = out->stride(0);
+  } else {
+    TORCH_CHECK(glu && q8.has_value() && q8->defined(), "gemm_mx: out may only be omitted for SwiGLU with q8");
+    mx.skip_c = 1;
+  }
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->numel() >= N && bias->is_contiguous() &&
+                (bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16), "gemm_mx: bias");
+    ep.bias = bias->data_ptr();
+    ep.bias_f32 = bias->scalar_type() == at::kFloat;
+  }
+  if (residual.has_value() && residual->defined()) {
+    TORCH_CHECK(!glu, "gemm_mx: residual with glu");
+    check_bf16_rows(*residual, "residual");
+    ep.residual = bf(*residual);
+    ep.ldr = residual->stride(0);
+  }
+  if (ssq_in.has_value() && ssq_in->defined()) {
+    check_f32_rows(*ssq_in, M, K / 128, "gemm_mx: ssq_in");
+    TORCH_CHECK(ssq_in->size(1) == K / 128 && ssq_in->is_contiguous(), "gemm_mx: ssq_in [M, K/128] contiguous");
+    mx.ssq_in = ssq_in->data_ptr<float>();
+    mx.ssq_in_tiles = (int)(K / 128);
+    mx.norm_eps = (float)norm_eps;
+  }
+  if (q8.has_value() && q8->defined()) {
+    check_f8_rows(*q8, "gemm_mx: q8");
+    TORCH_CHECK(q8->size(0) >= M && q8->size(1) == NO, "gemm_mx: q8 [M, out columns]");
+    TORCH_CHECK(qs.has_value() && qs->defined(), "gemm_mx: q8 needs qs");
+    check_u8_rows(*qs, M, NO / 32, "gemm_mx: qs");
+    mx.q8 = reinterpret_cast<uint8_t*>(q8->data_ptr());
+    mx.ldq = q8->stride(0);
+    mx.qs = qs->data_ptr<uint8_t>();
+    mx.ldqs = qs->stride(0);
+  }
+  if (ssq_out.has_value() && ssq_out->defined()) {
+    TORCH_CHECK(!glu && cp != nullptr, "gemm_mx: ssq_out needs the bf16 output");
+    check_f32_rows(*ssq_out, M, N / 128, "gemm_mx: ssq_out");
+    TORCH_CHECK(ssq_out->size(1) == N / 128 && ssq_out->is_contiguous(), "gemm_mx: ssq_out [M, N/128] contiguous");
+    mx.ssq_out = ssq_out->data_ptr<float>();
+    mx.ssq_out_tiles = (int)(N / 128);
+  }
+  const at::DeviceGuard guard(a8.device());
+  LUMEN_CHECK_HIP(lumen::gemm_mx(reinterpret_cast<const uint8_t*>(a8.data_ptr()), a8.stride(0), a_bs.data_ptr<uint8_t>(),
+                                 a_bs.stride(0), reinterpret_cast<const uint8_t*>(w8.data_ptr()), w8.stride(0),
+                                 sw.data_ptr<float>(), cp, ldc, (int)M, (int)N, (int)K, ep, mx, cur_stream(),
+                                 (int)variant));
+}
+
+// bf16 rows -> MX fp8 + E8M0 per 32 columns (+ per-(row, 128-column) sums of squares)
+void quant_rows_mx(const at::Tensor& x, at::Tensor q8, at::Tensor qs, const c10::optional<at::Tensor>& ssq) {
+  check_bf16_rows(x, "x");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(K % 128 == 0 && x.stride(0) % 8 == 0, "quant_rows_mx: K % 128 == 0, 16-byte aligned rows");
+  check_f8_rows(q8, "quant_rows_mx: q8");
+  TORCH_CHECK(q8.size(0) >= M && q8.size(1) == K, "quant_rows_mx: q8 shape");
+  check_u8_rows(qs, M, K / 32, "quant_rows_mx: qs");
+  float* sp = nullptr;
+  int64_t lds = 0;
+  if (ssq.has_value() && ssq->defined()) {
+    check_f32_rows(*ssq, M, K / 128, "quant_rows_mx: ssq");
+    sp = ssq->data_ptr<float>();
+    lds = ssq->stride(0);
+  }
+  const at::DeviceGuard guard(x.device());
+  LUMEN_CHECK_HIP(lumen::quant_rows_mx(bf(x), x.stride(0), reinterpret_cast<uint8_t*>(q8.data_ptr()), q8.stride(0),
+                                       qs.data_ptr<uint8_t>(), qs.stride(0), sp, lds, (int)M, (int)K, cur_stream()));
+}
+
 // per-token fp8 quantisation of bf16 rows: out8 [M, K] e4m3fn, scale [M] = amax / 448
 void quant_rows_fp8(const at::Tensor& x, at::Tensor out8, at::Tensor scale) {
   check_bf16_rows(x, "x");
@@ -527,6 +633,50 @@ void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at
   a.o_sb = o.stride(0); a.o_ss = o.stride(1); a.o_sh = o.stride(2);
   if (kv_len.has_value() && kv_len->defined()) {
     TORCH_CHECK(kv_len->scalar_type() == at::kInt && kv_len->numel() == B, "attention: kv_len int32 [B]");
+    a.kv_len = kv_len->data_ptr<int>();
+  }
+  a.Sq = (int)Sq; a.Sk = (int)Sk; a.H = (int)H; a.Hkv = (int)Hkv;
+  a.scale_log2 = (float)(scale * 1.4426950408889634);
+  a.causal = causal ? 1 : 0;
+  const at::DeviceGuard guard(q.device());
+  LUMEN_CHECK_HIP(lumen::attn_fwd(a, (int)B, (int)D, cur_stream()));
+}
+
+// attention with an MX fp8 output (the W8A8 o-projection's operand): o8 e4m3fn [B, Sq, H*D] (or
+// [Sq, H*D] when B == 1), os uint8 [B, Sq, H*D/32] (or 2-D); o (bf16 [B, Sq, H, D]) optional.
+void attention_mx(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const c10::optional<at::Tensor>& o,
+                  at::Tensor o8, at::Tensor os, const c10::optional<at::Tensor>& kv_len, double scale, bool causal) {
+  for (auto* t : {&q, &k, &v}) {
+    check_gpu(*t, "qkv");
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 4 && t->stride(3) == 1, "attention_mx: bf16 4-D");
+  }
+  const int64_t B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
+  const int64_t Sk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(k.size(3) == D && v.size(3) == D && v.size(1) == Sk && v.size(2) == Hkv && H % Hkv == 0,
+              "attention_mx: kv shape");
+  TORCH_CHECK(D == 64 || D == 128, "attention_mx: head dim 64 / 128");
+  TORCH_CHECK(o8.is_cuda() && o8.scalar_type() == at::kFloat8_e4m3fn && o8.stride(-1) == 1 &&
+              (o8.dim() == 3 || (o8.dim() == 2 && B == 1)) && o8.size(-1) >= H * D && o8.size(-2) >= Sq &&
+              o8.stride(-2) % 4 == 0, "attention_mx: o8 e4m3fn [B, Sq, >= H*D]");
+  TORCH_CHECK(os.is_cuda() && os.scalar_type() == at::kByte && os.stride(-1) == 1 && os.dim() == o8.dim() &&
+              os.size(-1) >= H * D / 32 && os.size(-2) >= Sq && os.stride(-2) % 4 == 0 &&
+              reinterpret_cast<uintptr_t>(os.data_ptr()) % 4 == 0, "attention_mx: os uint8 [B, Sq, >= H*D/32]");
+  lumen::AttnArgs a{};
+  a.q = bf(q); a.k = bf(k); a.v = bf(v);
+  a.q_sb = q.stride(0); a.q_ss = q.stride(1); a.q_sh = q.stride(2);
+  a.k_sb = k.stride(0); a.k_ss = k.stride(1); a.k_sh = k.stride(2);
+  a.v_sb = v.stride(0); a.v_ss = v.stride(1); a.v_sh = v.stride(2);
+  if (o.has_value() && o->defined()) {
+    TORCH_CHECK(o->scalar_type() == at::kBFloat16 && o->dim() == 4 && o->stride(3) == 1, "attention_mx: out");
+    a.o = bfm(*o);
+    a.o_sb = o->stride(0); a.o_ss = o->stride(1); a.o_sh = o->stride(2);
+  }
+  a.o8 = reinterpret_cast<uint8_t*>(o8.data_ptr());
+  a.os = os.data_ptr<uint8_t>();
+  a.o8_sb = o8.dim() == 3 ? o8.stride(0) : 0; a.o8_ss = o8.stride(-2);
+  a.os_sb = os.dim() == 3 ? os.stride(0) : 0; a.os_ss = os.stride(-2);
+  if (kv_len.has_value() && kv_len->defined()) {
+    TORCH_CHECK(kv_len->scalar_type() == at::kInt && kv_len->numel() == B, "attention_mx: kv_len int32 [B]");
     a.kv_len = kv_len->data_ptr<int>();
   }
   a.Sq = (int)Sq; a.Sk = (int)Sk; a.H = (int)H; a.Hkv = (int)Hkv;
@@ -755,11 +905,16 @@ TORCH_LIBRARY(lumen, m) {
   m.def("gemm_f8(Tensor a8, Tensor sa, Tensor w8, Tensor sw, Tensor? bias, Tensor? residual, Tensor(o!) out, "
         "int glu, int splits=-1, int variant=0) -> ()");
   m.def("quant_rows_fp8(Tensor x, Tensor(o!) out8, Tensor(s!) scale) -> ()");
+  m.def("gemm_mx(Tensor a8, Tensor a_bs, Tensor w8, Tensor sw, Tensor? bias, Tensor? residual, Tensor(o!)? out, "
+        "int glu, Tensor? ssq_in, float norm_eps, Tensor(q!)? q8, Tensor(s!)? qs, Tensor(t!)? ssq_out, int variant) -> ()");
+  m.def("quant_rows_mx(Tensor x, Tensor(q!) q8, Tensor(s!) qs, Tensor(t!)? ssq) -> ()");
   m.def("rms_norm_quant_fp8(Tensor x, Tensor? add, Tensor(r!)? resid_out, Tensor gamma, float eps, Tensor(o!) out8, "
         "Tensor(s!) scale) -> ()");
   m.def("cls_fill(Tensor(a!) x, Tensor cls, Tensor pos, int seq) -> ()");
   m.def("embed_gather(Tensor ids, Tensor table, Tensor? pos, Tensor(o!) out, int seq, int id_offset) -> ()");
   m.def("attention(Tensor q, Tensor k, Tensor v, Tensor(o!) o, Tensor? kv_len, float scale, bool causal) -> ()");
+  m.def("attention_mx(Tensor q, Tensor k, Tensor v, Tensor(o!)? o, Tensor(q8!) o8, Tensor(s!) os, Tensor? kv_len, "
+        "float scale, bool causal) -> ()");
   m.def("image_prep(Tensor src, Tensor geom, Tensor(o!) out, Tensor(t!) tmp, int out_h, int out_w, int filter, "
         "bool swap_rb, float[] mean, float[] std, float scale, float pad, int layout, int patch, int kpad, "
         "int max_ch, int max_dw) -> ()");
@@ -788,10 +943,13 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("gemm_f8", &gemm_f8);
   m.impl("gemm_dec", &gemm_dec);
   m.impl("quant_rows_fp8", &quant_rows_fp8);
+  m.impl("gemm_mx", &gemm_mx);
+  m.impl("quant_rows_mx", &quant_rows_mx);
   m.impl("rms_norm_quant_fp8", &rms_norm_quant_fp8);
   m.impl("cls_fill", &cls_fill);
   m.impl("embed_gather", &embed_gather);
   m.impl("attention", &attention);
+  m.impl("attention_mx", &attention_mx);
   m.impl("image_prep", &image_prep2);
   m.impl("row_topk", &row_topk);
   m.impl("conv2d", &conv2d);

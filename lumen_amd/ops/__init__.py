@@ -251,6 +251,101 @@ def linear_f8(x8: torch.Tensor, x_scale: torch.Tensor, w8: torch.Tensor, w_scale
     return out
 
 
+def mx_quant_ref(x: torch.Tensor):
+    """MX fp8 of rows x [M, K] (K % 32 == 0), the arithmetic of the GPU producers: per 32
+    columns e = the smallest exponent with amax / 2^e <= 448 (E8M0 byte e + 127), values
+    x * 2^-e saturated to e4m3fn.  -> (q8 [M, K] float8_e4m3fn, qs [M, K/32] uint8)."""
+    M, K = x.shape
+    xb = x.float().reshape(M, K // 32, 32)
+    t = xb.abs().amax(-1) * torch.tensor(1.0 / 448.0, dtype=torch.float32)
+    m, ex = torch.frexp(t)
+    e = torch.where(m == 0.5, ex - 1, ex)
+    e = torch.where(t == 0, torch.full_like(e, -127), e)
+    e = torch.where((t > 0) & (t < 2.0 ** -126), torch.full_like(e, -126), e).clamp(-127, 126)
+    q = (xb * torch.exp2(-e.float())[..., None]).clamp(-448, 448).to(torch.float8_e4m3fn)
+    return q.reshape(M, K), (e + 127).to(torch.uint8)
+
+
+def mx_dequant(q8: torch.Tensor, qs: torch.Tensor) -> torch.Tensor:
+    """MX fp8 [M, K] + E8M0 [M, >= K/32] -> fp32 [M, K]."""
+    M, K = q8.shape
+    s = torch.exp2(qs[:, :K // 32].float() - 127.0)
+    return (q8.float().reshape(M, K // 32, 32) * s[..., None]).reshape(M, K)
+
+
+def quant_rows_mx(x: torch.Tensor, q8: Optional[torch.Tensor] = None, qs: Optional[torch.Tensor] = None,
+                  ssq: Optional[torch.Tensor] = None):
+    """bf16 rows [M, K] -> MX fp8 (q8 [M, K] e4m3fn, qs [M, K/32] E8M0) and, when ``ssq`` is given,
+    its per-(row, 128-column) sums of squares [M, K/128] (the rstd source of a norm-folded
+    consumer, ops.linear_mx(ssq_in=...)).  Returns (q8, qs)."""
+    M, K = x.shape
+    if q8 is None:
+        q8 = torch.empty((M, K), device=x.device, dtype=torch.float8_e4m3fn)
+    if qs is None:
+        qs = torch.empty((M, K // 32), device=x.device, dtype=torch.uint8)
+    if x.is_cuda:
+        hip_ops().quant_rows_mx(x, q8, qs, ssq)
+        return q8, qs
+    a, b = mx_quant_ref(x)
+    q8[:M].copy_(a)
+    qs[:M, :K // 32].copy_(b)
+    if ssq is not None:
+        ssq[:M, :K // 128] = (x.float() ** 2).reshape(M, K // 128, 128).sum(-1)
+    return q8, qs
+
+
+def linear_mx(x8: torch.Tensor, xs: torch.Tensor, w8: torch.Tensor, w_scale: torch.Tensor,
+              bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
+              out: Optional[torch.Tensor] = None, glu: bool = False, ssq_in: Optional[torch.Tensor] = None,
+              norm_eps: float = 0.0, q_out: Optional[tuple] = None, ssq_out: Optional[torch.Tensor] = None,
+              write_out: bool = True, variant: int = 0) -> Optional[torch.Tensor]:
+    """W8A8 projection with MX (block-scaled) activations on the gfx950 matrix cores
+    (csrc/gemm_f8.hip::gemm_mx): A = x8 * 2^(xs - 127) per 32 columns feeds the MFMA scale operand,
+    so producers quantise with block-local scales and no per-row quantisation pass runs.
+
+    y = epi(rstd[m] * (A @ w8^T) * w_scale[n]): ``ssq_in`` [M, K/128] (the producer's sums of
+    squares) gives rstd = rsqrt(sum / K + norm_eps) -- the RMSNorm whose gamma was folded into w8;
+    then fp32 bias, SwiGLU or + residual.  Outputs: bf16 ``out`` (skipped with ``write_out=False``,
+    SwiGLU only), ``q_out = (q8, qs)`` an MX fp8 copy of the output for the next projection,
+    ``ssq_out`` [M, N/128] per-(row, 128-column) sums of squares of the stored bf16 values."""
+    M, K = x8.shape
+    N = w8.shape[0]
+    NO = N // 2 if glu else N
+    if out is None and write_out:
+        out = torch.empty((M, NO), device=x8.device, dtype=torch.bfloat16)
+    q8, qs = q_out if q_out is not None else (None, None)
+    if x8.is_cuda:
+        hip_ops().gemm_mx(x8, xs, w8, w_scale, bias, residual, out if write_out else None, int(bool(glu)), ssq_in,
+                          float(norm_eps), q8, qs, ssq_out, int(variant))
+        return out
+    y = (mx_dequant(x8, xs) @ w8.float().t()) * w_scale.float()[None, :N]
+    if ssq_in is not None:
+        y = y * torch.rsqrt(ssq_in.float()[:M].sum(1, keepdim=True) / K + norm_eps)
+    if bias is not None:
+        y = y + bias.float()[:N]
+    if glu:
+        gu = y.view(M, N // 16, 2, 8)
+        r = (F.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(M, NO)
+        if write_out:
+            out[:M, :NO] = r.to(out.dtype)
+        if q8 is not None:
+            a, b = mx_quant_ref(r)
+            q8[:M].copy_(a)
+            qs[:M, :NO // 32].copy_(b)
+        return out
+    if residual is not None:
+        y = y + residual.float()[:M, :N]
+    yb = y.to(torch.bfloat16)
+    out[:M, :N] = yb
+    if q8 is not None:
+        a, b = mx_quant_ref(yb.float())
+        q8[:M].copy_(a)
+        qs[:M, :N // 32].copy_(b)
+    if ssq_out is not None:
+        ssq_out[:M, :N // 128] = (yb.float() ** 2).reshape(M, N // 128, 128).sum(-1)
+    return out
+
+
 def glu_interleave(w_gate: torch.Tensor, w_up: torch.Tensor) -> torch.Tensor:
     """[I, K] gate / up projections -> [2I, K] rows grouped [gate 8 | up 8] per 16 (``linear(glu=True)``)."""
     I, K = w_gate.shape
@@ -430,6 +525,31 @@ def attention(q, k, v, scale: Optional[float] = None, causal: bool = False, kv_l
     o = (p @ vf).transpose(1, 2)
     out.copy_(o.to(out.dtype))
     return out
+
+
+def attention_mx(q, k, v, scale: Optional[float] = None, causal: bool = False, kv_len=None,
+                 q_out: Optional[tuple] = None, out=None):
+    """:func:`attention` whose output leaves as MX fp8 (the W8A8 o-projection's operand,
+    :func:`linear_mx`): returns (o8 [B*Sq, H*D] e4m3fn, os [B*Sq, H*D/32] E8M0).  ``out``
+    (bf16 [B, Sq, H, D]) is also written when given.  On the CPU: attention + mx_quant_ref."""
+    B, Sq, H, D = q.shape
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if q_out is None:
+        q_out = (torch.empty((B * Sq, H * D), device=q.device, dtype=torch.float8_e4m3fn),
+                 torch.empty((B * Sq, H * D // 32), device=q.device, dtype=torch.uint8))
+    o8, os_ = q_out
+    if q.is_cuda:
+        kl = kv_len.to(torch.int32) if kv_len is not None else None
+        hip_ops().attention_mx(q, k, v, out, o8.view(B, Sq, -1), os_.view(B, Sq, -1), kl, float(scale), bool(causal))
+        return o8, os_
+    o = attention(q, k, v, scale=scale, causal=causal, kv_len=kv_len)
+    if out is not None:
+        out.copy_(o)
+    of = attention(q.float(), k.float(), v.float(), scale=scale, causal=causal, kv_len=kv_len)
+    a, b = mx_quant_ref(of.reshape(B * Sq, H * D))
+    o8.copy_(a)
+    os_[:, :H * D // 32].copy_(b)
+    return o8, os_
 
 
 # --------------------------------------------------------------------------- top-k

@@ -338,7 +338,8 @@ def dp_worker(device: str, cache_dir: str, model: str, runtime: str, dataset: Op
                 raise RuntimeError("this worker holds no label-bank shard")
             return [bank.topk_local(q, k, scale, sm) for q, k, scale, sm in items]
         if kind == "info":
-            return [{"logit_scale": float(m.logit_scale), "embed_dim": int(cfg.embed_dim)}]
+            # one answer per item: the engine may merge several front ends' info calls in a batch
+            return [{"logit_scale": float(m.logit_scale), "embed_dim": int(cfg.embed_dim)}] * len(items)
         if kind == "image":
             # encoded images (DP workers decode here) or uint8 HWC arrays (decoded by a serving front end)
             raw = [k for k, it in enumerate(items) if not isinstance(it, np.ndarray)]

@@ -608,7 +608,7 @@ def dp_worker(device: str, resources: GenericResources, max_batch: int = 64):
     @torch.no_grad()
     def fn(kind, items):
         if kind == "info":
-            return [{"spec": b.spec, "embedding_dim": int(b.rec.cfg.embedding)}]
+            return [{"spec": b.spec, "embedding_dim": int(b.rec.cfg.embedding)}] * len(items)   # one per requester
         imgs = [load(it[0]) for it in items]
         ok = [k for k, im in enumerate(imgs) if not isinstance(im, BaseException)]
         out: list = [imgs[k] for k in range(len(items))]          # decode errors stay in place

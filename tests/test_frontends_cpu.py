@@ -25,17 +25,21 @@ def echo_engine(device, delay_s: float = 0.0):
             raise ValueError("requested failure")
         if kind == "crash":
             os._exit(3)
-        if delay_s:
+        if kind == "slow":      # occupies the batch loop while the front ends queue work
+            time.sleep(2.0)
+        elif delay_s:
             time.sleep(delay_s)
         return [float(np.asarray(x).sum()) * 2.0 for x in items]
     return fn
 
 
-def _frontend(specs, q, n, start_ev):
+def _frontend(specs, q, n, start_ev, ready_q=None):
     attach_frontend(specs)
     with remote_scope("echo"):
         pool = current_remote()
-    start_ev.wait(30)
+    if ready_q is not None:
+        ready_q.put(os.getpid())
+    start_ev.wait(60)
     outs = []
     futs = [pool.submit("sum", [np.full(4, i, np.float32), np.full(2, i + 1, np.float32)]) for i in range(n)]
     for i, f in enumerate(futs):
@@ -75,21 +79,25 @@ def test_two_frontends_share_one_engines_batches():
                    slot_bytes=1 << 16, result_bytes=1 << 14, threads_per_service=1)
     try:
         ctx = mp.get_context("spawn")
-        q, start = ctx.Queue(), ctx.Event()
-        ps = [ctx.Process(target=_frontend, args=(es.frontend_specs(), q, 12, start)) for _ in range(2)]
+        q, start, ready = ctx.Queue(), ctx.Event(), ctx.Queue()
+        ps = [ctx.Process(target=_frontend, args=(es.frontend_specs(), q, 12, start, ready)) for _ in range(2)]
         for p in ps:
             p.start()
-        time.sleep(1.0)
-        start.set()
+        pool = RemotePool(ChannelGroup([ShmChannel.attach(s) for s in es.frontend_specs()["echo"]]))
+        for _ in ps:                # both front ends attached (spawned imports can take seconds)
+            ready.get(timeout=120)
+        blocker = pool.submit("slow", [np.zeros(1, np.float32)])   # the batch loop sleeps 2 s ...
+        time.sleep(0.2)
+        start.set()                                                 # ... while both front ends queue
         got = [q.get(timeout=120) for _ in ps]
         for p in ps:
             p.join(30)
+        blocker.result(30)
         assert len({pid for pid, _ in got}) == 2
         for _pid, outs in got:
             assert [o for _, o in outs] == [[8.0 * i, 4.0 * (i + 1)] for i in range(12)]
-        pool = RemotePool(ChannelGroup([ShmChannel.attach(s) for s in es.frontend_specs()["echo"]]))
         st = pool.submit("__stats__", [None]).result(30)[0]
-        assert st["items"] == 48 and st["max_frontends_per_batch"] == 2 and st["shared_batches"] >= 1
+        assert st["items"] == 49 and st["max_frontends_per_batch"] >= 2 and st["shared_batches"] >= 1
         with pytest.raises(WorkerTaskError, match="requested failure"):
             pool.submit("boom", [1]).result(30)
         pool.close()

@@ -56,6 +56,36 @@ def test_rope_kv(H, Hkv, D):
     assert torch.equal(vc_g.cpu(), vc_ref)
 
 
+@pytest.mark.parametrize("H,Hkv,D", [(32, 8, 128), (14, 2, 64)])
+@pytest.mark.parametrize("start", [0, 37])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_rope_kv_prefill_tiles(H, Hkv, D, start, fp8):
+    """Prefill-sized rope_kv (64-token tiles, d-major V runs through LDS): a sequence whose slots
+    run through its blocks from an unaligned start, vs the CPU reference."""
+    g = torch.Generator().manual_seed(H + start)
+    T = 200
+    qkv = torch.randn(T, (H + 2 * Hkv) * D, generator=g).bfloat16()
+    pos = torch.arange(start, start + T, dtype=torch.int32)
+    cs = llm.rope_cos_sin(4096, D, 5e5)
+    kc, vc = _cache(8, Hkv, D, g)
+    table = torch.tensor([5, 2, 7, 0, 3, 6, 1, 4])
+    p = torch.arange(start, start + T)
+    slots = (table[p // 64] * 64 + p % 64).long()
+    if fp8:
+        kc, vc = kc.to(torch.float8_e4m3fn), vc.to(torch.float8_e4m3fn)
+    q_ref, kc_ref, vc_ref = qkv.clone(), kc.clone(), vc.clone()
+    llm.rope_kv(q_ref, pos, cs, H, Hkv, D, slots, kc_ref, vc_ref)
+    q_g, kc_g, vc_g = qkv.to(DEV), kc.to(DEV), vc.to(DEV)
+    llm.rope_kv(q_g, pos.to(DEV), cs.to(DEV), H, Hkv, D, slots.to(DEV), kc_g, vc_g)
+    assert (q_g.cpu().float() - q_ref.float()).abs().max().item() < 0.05
+    dk = (kc_g.cpu().float() - kc_ref.float()).abs()
+    if fp8:     # one e4m3 step where the rotated bf16 value itself differs by an ulp
+        assert (dk <= 0.13 * kc_ref.float().abs() + 1e-3).all() and (dk > 0).float().mean().item() < 0.02
+    else:
+        assert dk.max().item() < 0.05
+    assert (vc_g.cpu().float() - vc_ref.float()).abs().max().item() == 0.0
+
+
 @pytest.mark.parametrize("H,Hkv,D", [(14, 2, 64), (32, 8, 128), (32, 32, 128), (16, 1, 64), (4, 2, 32)])
 @pytest.mark.parametrize("lens", [[1, 64, 65], [700, 3, 2048 + 17], [5000], [70, 700, 3, 1, 2048 + 17, 64]])
 def test_paged_decode(H, Hkv, D, lens):

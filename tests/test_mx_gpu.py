@@ -1,0 +1,200 @@
+"""MX (block-scaled) W8A8 prefill chain on the gfx950 scaled matrix cores vs the CPU references:
+quant_rows_mx (bit-exact E8M0 + e4m3 bytes), gemm_mx with every epilogue the fused prefill
+uses (rstd row scale from producer sums of squares, SwiGLU -> MX fp8, residual -> bf16 + MX
+fp8 + sums of squares) and the attention kernel's MX fp8 output."""
+import pytest
+import torch
+
+from lumen_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-6)).item()
+
+
+def _rows(M, K, g, spread=True):
+    x = torch.randn(M, K, generator=g)
+    if spread:   # per-block magnitudes over ~2^-8 .. 2^8 so the E8M0 bytes differ along a row
+        x = x * torch.exp2(torch.randint(-8, 9, (M, K // 32), generator=g).float()).repeat_interleave(32, 1)
+    return x.bfloat16()
+
+
+@pytest.mark.parametrize("M,K", [(1, 128), (37, 896), (624, 4096)])
+def test_quant_rows_mx_bit_exact(M, K):
+    g = torch.Generator().manual_seed(M + K)
+    x = _rows(M, K, g)
+    x[0, :32] = 0     # an all-zero block: smallest scale
+    q_ref, s_ref = ops.mx_quant_ref(x)
+    ssq = torch.empty(M, K // 128, device=DEV)
+    q8, qs = ops.quant_rows_mx(x.to(DEV), ssq=ssq)
+    assert torch.equal(qs.cpu(), s_ref)
+    assert torch.equal(q8.cpu().view(torch.uint8), q_ref.view(torch.uint8))
+    ref_ssq = (x.float() ** 2).reshape(M, K // 128, 128).sum(-1)
+    assert torch.allclose(ssq.cpu(), ref_ssq, rtol=1e-4, atol=1e-6)
+
+
+def _operands(M, N, K, g):
+    x = _rows(M, K, g)
+    x8, xs = ops.mx_quant_ref(x)
+    w8, sw = ops.quantize_fp8_rows(torch.randn(N, K, generator=g) * K ** -0.5)
+    return x8, xs, w8, sw
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 9, 10, 11])
+@pytest.mark.parametrize("M,N,K", [(130, 1024, 512), (624, 2048, 4096), (33, 256, 128)])
+def test_gemm_mx_plain_vs_reference(M, N, K, variant):
+    """A scale bytes reach the MFMA per lane (k 32g .. 32g+31) -- wrong lanes or a wrong k order
+    would scale whole blocks by up to 2^16 and blow the error up."""
+    g = torch.Generator().manual_seed(M * N + K)
+    x8, xs, w8, sw = _operands(M, N, K, g)
+    b = torch.randn(N, generator=g)
+    ref = ops.linear_mx(x8, xs, w8, sw, bias=b)
+    got = ops.linear_mx(x8.to(DEV), xs.to(DEV), w8.to(DEV), sw.to(DEV), bias=b.to(DEV), variant=variant)
+    assert _rel(got, ref) < 1e-2
+
+
+def test_gemm_mx_exact_small_integers():
+    """Integer operands and power-of-two block scales are exact in fp32: bitwise-equal result."""
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 64, 128, 256
+    x8 = torch.randint(-4, 5, (M, K), generator=g).float().to(torch.float8_e4m3fn)
+    xs = torch.randint(124, 131, (M, K // 32), generator=g).to(torch.uint8)
+    w8 = torch.randint(-4, 5, (N, K), generator=g).float().to(torch.float8_e4m3fn)
+    sw = torch.ones(N)
+    ref = ops.mx_dequant(x8, xs) @ w8.float().t()
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.linear_mx(x8.to(DEV), xs.to(DEV), w8.to(DEV), sw.to(DEV), out=out)
+    assert torch.equal(out.cpu().float(), ref.bfloat16().float())
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 10])
+@pytest.mark.parametrize("M,N,K", [(200, 1024, 512), (624, 4096, 4096)])
+def test_gemm_mx_residual_outputs(M, N, K, variant):
+    """o / down projection: bf16 residual stream + its MX fp8 copy + per-128-column sums of squares."""
+    g = torch.Generator().manual_seed(M + 7 * N)
+    x8, xs, w8, sw = _operands(M, N, K, g)
+    r = torch.randn(M, N, generator=g).bfloat16()
+    ref_q, ref_s = torch.empty(M, N, dtype=torch.float8_e4m3fn), torch.empty(M, N // 32, dtype=torch.uint8)
+    ref_ss = torch.empty(M, N // 128)
+    ref = ops.linear_mx(x8, xs, w8, sw, residual=r, out=r.clone(), q_out=(ref_q, ref_s), ssq_out=ref_ss)
+    xg = r.to(DEV)
+    q8 = torch.empty(M, N, device=DEV, dtype=torch.float8_e4m3fn)
+    qs = torch.empty(M, N // 32, device=DEV, dtype=torch.uint8)
+    ss = torch.empty(M, N // 128, device=DEV)
+    ops.linear_mx(x8.to(DEV), xs.to(DEV), w8.to(DEV), sw.to(DEV), residual=xg, out=xg, q_out=(q8, qs),
+                  ssq_out=ss, variant=variant)
+    assert _rel(xg, ref) < 1e-2
+    # the MX copy is the exact quantisation of the stored bf16 rows
+    q_self, s_self = ops.mx_quant_ref(xg.cpu().float())
+    assert torch.equal(qs.cpu(), s_self)
+    assert torch.equal(q8.cpu().view(torch.uint8), q_self.view(torch.uint8))
+    assert torch.allclose(ss.cpu(), (xg.cpu().float() ** 2).reshape(M, N // 128, 128).sum(-1), rtol=1e-4)
+    assert _rel(ss, ref_ss) < 2e-2
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 10])
+@pytest.mark.parametrize("write_out", [True, False])
+def test_gemm_mx_swiglu_mx_output(variant, write_out):
+    """gate|up projection: SwiGLU straight to MX fp8 (the down projection's A operand)."""
+    g = torch.Generator().manual_seed(11 + variant)
+    M, N, K = 300, 2048, 1024
+    x8, xs, w8, sw = _operands(M, N, K, g)
+    ref_q, ref_s = torch.empty(M, N // 2, dtype=torch.float8_e4m3fn), torch.empty(M, N // 64, dtype=torch.uint8)
+    ref = ops.linear_mx(x8, xs, w8, sw, glu=True, q_out=(ref_q, ref_s))
+    q8 = torch.empty(M, N // 2, device=DEV, dtype=torch.float8_e4m3fn)
+    qs = torch.empty(M, N // 64, device=DEV, dtype=torch.uint8)
+    got = ops.linear_mx(x8.to(DEV), xs.to(DEV), w8.to(DEV), sw.to(DEV), glu=True, q_out=(q8, qs),
+                        write_out=write_out, variant=variant)
+    if write_out:
+        assert _rel(got, ref) < 1e-2
+    deq, deq_ref = ops.mx_dequant(q8.cpu(), qs.cpu()), ops.mx_dequant(ref_q, ref_s)
+    assert _rel(deq, deq_ref) < 3e-2
+    assert (qs.cpu().int() - ref_s.int()).abs().max().item() <= 1
+
+
+@pytest.mark.parametrize("M,N,K", [(150, 1024, 1024), (624, 6144, 4096)])
+def test_gemm_mx_rstd_from_producer_ssq(M, N, K):
+    """qkv / gate|up: RMSNorm as the rstd row scale from the producer's sums of squares."""
+    g = torch.Generator().manual_seed(M + N + K)
+    x = _rows(M, K, g, spread=False) * 3
+    ssq = torch.empty(M, K // 128, device=DEV)
+    x8, xs = ops.quant_rows_mx(x.to(DEV), ssq=ssq)
+    w8, sw = ops.quantize_fp8_rows(torch.randn(N, K, generator=g) * K ** -0.5)
+    got = ops.linear_mx(x8, xs, w8.to(DEV), sw.to(DEV), ssq_in=ssq, norm_eps=1e-5)
+    xn = x.float() * torch.rsqrt((x.float() ** 2).mean(1, keepdim=True) + 1e-5)
+    ref = xn @ (w8.float() * sw[:, None]).t()
+    assert _rel(got, ref) < 3e-2
+
+
+def test_gemm_mx_graph_capture_and_repeat():
+    g = torch.Generator().manual_seed(5)
+    M, N, K = 624, 4096, 4096
+    x8, xs, w8, sw = [t.to(DEV) for t in _operands(M, N, K, g)]
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.linear_mx(x8, xs, w8, sw, out=out, variant=10)
+    first = out.clone()
+    for v in (10, 10):
+        ops.linear_mx(x8, xs, w8, sw, out=out, variant=v)
+        assert torch.equal(out, first)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        ops.linear_mx(x8, xs, w8, sw, out=out, variant=10)
+    out.zero_()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, first)
+
+
+@pytest.mark.parametrize("S,H,Hkv,D,causal", [(624, 32, 8, 128, True), (577, 16, 16, 64, False), (70, 4, 2, 128, True)])
+def test_attention_mx_output(S, H, Hkv, D, causal):
+    """The attention kernel's MX fp8 output: the exact MX quantisation of its own fp32 O (checked
+    against the bf16 O of the same launch) and close to the fp32 reference."""
+    g = torch.Generator().manual_seed(S + H)
+    q = torch.randn(1, S, H, D, generator=g).bfloat16()
+    k = torch.randn(1, S, Hkv, D, generator=g).bfloat16()
+    v = torch.randn(1, S, Hkv, D, generator=g).bfloat16()
+    qg, kg, vg = q.to(DEV), k.to(DEV), v.to(DEV)
+    ob = torch.empty(1, S, H, D, device=DEV, dtype=torch.bfloat16)
+    o8, os_ = ops.attention_mx(qg, kg, vg, causal=causal, out=ob)
+    plain = ops.attention(qg, kg, vg, causal=causal)
+    assert torch.equal(ob, plain)
+    deq = ops.mx_dequant(o8.cpu(), os_.cpu())
+    ref = ops.attention(q.float(), k.float(), v.float(), causal=causal).reshape(S, H * D)
+    assert _rel(deq, ref) < 4e-2
+    # scale bytes: those of the (bf16-rounded) kernel output, up to one step at block boundaries
+    _, s_b = ops.mx_quant_ref(ob.cpu().float().reshape(S, H * D))
+    assert (os_.cpu().int() - s_b.int()).abs().max().item() <= 1
+    o8b, osb = ops.attention_mx(qg, kg, vg, causal=causal)     # fp8 only: same bytes
+    assert torch.equal(o8b.view(torch.uint8), o8.view(torch.uint8)) and torch.equal(osb, os_)
+
+
+@pytest.mark.parametrize("T", [100, 300])
+def test_llm_prefill_mx_chain_matches_per_token_chain(T):
+    """LLM prefill through the fused MX chain (6 launches per layer) vs the per-token-scale W8A8
+    chain (rms_norm_quant / quant_rows passes): same logits within fp8 noise, and the MX path
+    really ran (no rms_norm_quant launch would show in a trace; here: the module switch)."""
+    from lumen_amd.models import llm as L
+
+    cfg = L.LLMConfig(vocab_size=2048, hidden_size=512, num_layers=3, num_heads=4, num_kv_heads=2, head_dim=128,
+                      intermediate_size=1024, qkv_bias=False, tie_word_embeddings=False, max_position=2048)
+    m = L.LLM(cfg, device=DEV)
+    m.random_init(0)
+    m.quantize_fp8()
+    g = torch.Generator(device=DEV).manual_seed(T)
+    x = (torch.randn(T, 512, device=DEV, generator=g) * 0.5).bfloat16()
+    m.prefill(x.clone())          # folds the norms (both chains then use the same weights)
+    assert m.norm_folded and m._mx_ok(x)
+    old = L._PREFILL_MX
+    try:
+        L._PREFILL_MX = False
+        ref = m.prefill(x.clone())
+        L._PREFILL_MX = True
+        got = m.prefill(x.clone())
+    finally:
+        L._PREFILL_MX = old
+    assert _rel(got, ref) < 5e-2
+    assert torch.isfinite(got).all()

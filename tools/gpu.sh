@@ -24,6 +24,7 @@
 #   serve          tools/serve_bench.py: gRPC hub end to end (CLIP ViT-L/14 64 clients, face 32 clients)
 #   serve_fe       serving through the engine / front-end topology (CLIP 128 clients, face 64; $SERVE_FE front ends)
 #   jpeg           device JPEG tests + tools/jpeg_bench.py
+#   mx             MX W8A8 chain tests (tests/test_mx_gpu.py) + fp8 GEMM + LLM-op tests
 #   ttft           VLM TTFT only (8B fp8, 30 requests, device JPEG decode)
 #   pmc_gemm       PMC counters (MFMA, LDS conflicts, busy) of one ViT-L/14 GEMM shape
 set -o pipefail
@@ -119,6 +120,9 @@ for task in "$@"; do
       step jpeg_tests 200 python -u -m pytest tests/test_jpeg_gpu.py tests/test_jpeg_cpu.py -x -q --timeout 120 \
         --timeout-method thread
       step jpeg_bench 200 python -u tools/jpeg_bench.py ;;
+    mx)
+      step mx_tests 400 python -u -m pytest tests/test_mx_gpu.py tests/test_fp8_gpu.py tests/test_llm_ops_gpu.py -q \
+        --timeout 120 --timeout-method thread ;;
     ttft) step ttft 400 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0 ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
