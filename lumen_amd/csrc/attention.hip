@@ -293,7 +293,8 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
             *(uint32_t*)(o8 + j * 16 + 4 * g) = (uint32_t)w;
           }
         }
-        uint8_t* os = a.os + b * a.os_sb + (int64_t)qi * a.os_ss + h * NM;
+        // scale planes [H*D/128][rows][4]: head h's NM bytes at plane h*D/128, sub-block (h*NM) % 4
+        uint8_t* os = a.os + b * a.os_sb + (int64_t)((h * D) >> 7) * a.os_ss + (int64_t)qi * 4 + ((h * NM) & 3);
         if (g == 0) {
           if constexpr (NM == 4) *(uint32_t*)os = sbytes;
           else *(uint16_t*)os = (uint16_t)sbytes;

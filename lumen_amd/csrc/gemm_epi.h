@@ -50,6 +50,8 @@ struct GemmEpi {
 };
 
 // MX operand / outputs of the W8A8 prefill GEMM (gemm_f8.hip::gemm_mx; fields documented there)
+// MX scale bytes live in K-step planes: byte (row m, 32-column block b) at [b / 4][m][b % 4], plane
+// stride ld_bs / ldqs bytes (>= 4 M) -- the consumer's per-step load of 64 rows is contiguous.
 struct MxArgs {
   const uint8_t* a_bs;
   int64_t ld_bs;

@@ -137,7 +137,8 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
     }
     // BS: every wave stages the 4 scale bytes of one 64-row half per K-step (waves 0 / 1 are the
     // copies the fragments read; the others keep the per-wave glds count uniform for vmcnt)
-    const uint8_t* src_s = BS ? mx.a_bs + (int64_t)min(m0 + (wid & 1) * 64 + lane, M - 1) * mx.ld_bs : nullptr;
+    // (scale planes [K/128][M][4]: a wave's 64 rows x 4 bytes are 256 contiguous bytes, 2 lines)
+    const uint8_t* src_s = BS ? mx.a_bs + (int64_t)min(m0 + (wid & 1) * 64 + lane, M - 1) * 4 : nullptr;
     auto stage = [&](int s, int64_t koff) {
       char* base = smem + s * STAGE;
 #pragma unroll
@@ -149,7 +150,7 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
         __builtin_amdgcn_global_load_lds((g_ptr_t)(src_w[i] + koff),
                                          (lds_ptr_t)(base + 128 * 128 + (wid * PERW + i) * 1024), 16, 0, 0);
       if constexpr (BS)
-        __builtin_amdgcn_global_load_lds((g_ptr_t)(src_s + (koff >> 7) * 4),
+        __builtin_amdgcn_global_load_lds((g_ptr_t)(src_s + (koff >> 7) * mx.ld_bs),
                                          (lds_ptr_t)(base + 128 * 128 + BN * 128 + wid * 256), 4, 0, 0);
     };
 #pragma unroll
@@ -217,12 +218,24 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
     float* rstd_s = (float*)(smem + MX_SCRATCH);     // [128]
     float* ssq_s = rstd_s + 128;                      // [128][WN]
     const bool mx_out = mx.q8 != nullptr || mx.ssq_out != nullptr;
-    if (mx.ssq_in) {   // rstd of the tile's rows from the producer's partial sums of squares
+    if (mx.ssq_in) {
+      // rstd of the tile's rows from the producer's partial sums of squares: WN threads per row
+      // (128 * WN threads), their loads unrolled so they are all in flight at once, partial sums
+      // in a fixed order through LDS
+      constexpr int PARTS = WN;
+      float* red = ssq_s;                             // [PARTS][128], free until the slab loop
+      const int row = tid & 127, part = tid >> 7;
+      const float* p = mx.ssq_in + (int64_t)min(m0 + row, M - 1) * mx.ssq_in_tiles;
+      float ss = 0.f;
+#pragma unroll 8
+      for (int j = part; j < mx.ssq_in_tiles; j += PARTS) ss += p[j];
+      red[part * 128 + row] = ss;
+      __syncthreads();
       if (tid < 128) {
-        const float* p = mx.ssq_in + (int64_t)min(m0 + tid, M - 1) * mx.ssq_in_tiles;
-        float ss = 0.f;
-        for (int j = 0; j < mx.ssq_in_tiles; ++j) ss += p[j];
-        rstd_s[tid] = rsqrtf(ss / (float)K + mx.norm_eps);
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < PARTS; ++q) t += red[q * 128 + tid];
+        rstd_s[tid] = rsqrtf(t / (float)K + mx.norm_eps);
       }
       __syncthreads();
     }
@@ -280,7 +293,7 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
             const int e = mx_exp(am);
             if (valid) {
               *(uint2*)(mx.q8 + (int64_t)m * mx.ldq + (n >> 1)) = fp8x8_scaled(r, mx_inv(e));
-              if ((lane & 3) == 0) mx.qs[(int64_t)m * mx.ldqs + (n >> 6)] = (uint8_t)(e + 127);
+              if ((lane & 3) == 0) mx.qs[(int64_t)(n >> 8) * mx.ldqs + m * 4 + ((n >> 6) & 3)] = (uint8_t)(e + 127);
             }
           }
           continue;
@@ -300,7 +313,7 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
             const float inv = mx_inv(e);
             const uint2 lo = fp8x8_scaled(f, inv), hi = fp8x8_scaled(f + 8, inv);
             *(u32x4_t*)(mx.q8 + (int64_t)m * mx.ldq + n) = (u32x4_t){lo.x, lo.y, hi.x, hi.y};
-            if ((lane & 1) == 0) mx.qs[(int64_t)m * mx.ldqs + (n >> 5)] = (uint8_t)(e + 127);
+            if ((lane & 1) == 0) mx.qs[(int64_t)(n >> 7) * mx.ldqs + m * 4 + ((n >> 5) & 3)] = (uint8_t)(e + 127);
           }
         }
         if (mx.ssq_out) {
@@ -368,8 +381,13 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
         }
         __syncthreads();
         if (!last_flag) continue;
+        // every slab (this workgroup's own too) summed in contributor order: the result does not
+        // depend on which contributor arrived last (bit-identical launches and graph replays)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
         for (int c = 0; c < nc; ++c) {
-          if (c == l - first) continue;
           const float* src = slabs + (int64_t)c * (128 * BN);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
@@ -629,7 +647,8 @@ hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t
 hipError_t gemm_mx(const uint8_t* A, int64_t lda, const uint8_t* a_bs, int64_t ld_bs, const uint8_t* W, int64_t ldw,
                    const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, MxArgs mx,
                    hipStream_t stream, int variant) {
-  if (K % 128 != 0 || N % 16 != 0 || M <= 0 || lda % 16 != 0 || ldw % 16 != 0 || ld_bs < K / 32 || ld_bs % 4 != 0)
+  if (K % 128 != 0 || N % 16 != 0 || M <= 0 || lda % 16 != 0 || ldw % 16 != 0 || ld_bs < 4 * (int64_t)M ||
+      ld_bs % 4 != 0)
     return hipErrorInvalidValue;
   if (ep.split_koff || ep.out_group || ep.table || ep.prelu || ep.post_act || ep.row_aff) return hipErrorInvalidValue;
   if (mx.skip_c && !(ep.glu && mx.q8)) return hipErrorInvalidValue;
@@ -809,7 +828,7 @@ __global__ void __launch_bounds__(256) quant_rows_mx_kernel(const uint16_t* __re
   if (!valid) return;
   const int e = mx_exp(am);
   *(uint2*)(q8 + m * ldq + k) = fp8x8_scaled(f, mx_inv(e));
-  if ((lane & 3) == 0) qs[m * ldqs + (k >> 5)] = (uint8_t)(e + 127);
+  if ((lane & 3) == 0) qs[(k >> 7) * ldqs + m * 4 + ((k >> 5) & 3)] = (uint8_t)(e + 127);
   if (ssq && (lane & 15) == 0) ssq[m * ldss + (k >> 7)] = ss;
 }
 

@@ -381,10 +381,14 @@ void gemm_f8(const at::Tensor& a8, const at::Tensor& sa, const at::Tensor& w8, c
 }
 
 // ---------------------------------------------------------------- MX W8A8 (block-scaled activations)
-static void check_u8_rows(const at::Tensor& t, int64_t M, int64_t cols, const char* name) {
-  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kByte && t.dim() == 2 && t.stride(1) == 1 && t.size(0) >= M &&
-              t.size(1) >= cols && t.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 4 == 0,
-              name, ": uint8 [rows, >= ", cols, "] with 4-byte aligned rows");
+// MX scale planes: uint8 [K/128, >= M, 4] (byte of row m, 32-column block b at [b/4][m][b%4]); returns
+// the plane stride in bytes
+static int64_t check_planes(const at::Tensor& t, int64_t planes, int64_t M, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kByte && t.dim() == 3 && t.size(0) == planes && t.size(1) >= M &&
+              t.size(2) == 4 && t.stride(2) == 1 && t.stride(1) == 4 && (t.stride(0) % 4 == 0 || t.size(0) == 1) &&
+              reinterpret_cast<uintptr_t>(t.data_ptr()) % 4 == 0, name, ": uint8 scale planes [", planes,
+              ", >= ", M, ", 4]");
+  return t.size(0) == 1 ? std::max<int64_t>(t.stride(0), 4 * t.size(1)) : t.stride(0);   // size-1 dim: any stride
 }
 static void check_f32_rows(const at::Tensor& t, int64_t M, int64_t cols, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.dim() == 2 && t.stride(1) == 1 && t.size(0) >= M &&
@@ -404,7 +408,7 @@ void gemm_mx(const at::Tensor& a8, const at::Tensor& a_bs, const at::Tensor& w8,
   const int64_t M = a8.size(0), K = a8.size(1), N = w8.size(0);
   TORCH_CHECK(w8.size(1) == K && K % 128 == 0 && N % 128 == 0, "gemm_mx: K % 128 == 0, N % 128 == 0");
   TORCH_CHECK(variant >= 0 && variant <= 11 && variant != 6 && variant != 7 && variant != 8, "gemm_mx: variant");
-  check_u8_rows(a_bs, M, K / 32, "gemm_mx: a_bs");
+  const int64_t ld_bs = check_planes(a_bs, K / 128, M, "gemm_mx: a_bs");
   TORCH_CHECK(sw.is_cuda() && sw.scalar_type() == at::kFloat && sw.numel() == N && sw.is_contiguous(),
               "gemm_mx: sw f32 [N]");
   const int64_t NO = glu ? N / 2 : N;
@@ -445,12 +449,11 @@ void gemm_mx(const at::Tensor& a8, const at::Tensor& a_bs, const at::Tensor& w8,
   if (q8.has_value() && q8->defined()) {
     check_f8_rows(*q8, "gemm_mx: q8");
     TORCH_CHECK(q8->size(0) >= M && q8->size(1) == NO, "gemm_mx: q8 [M, out columns]");
-    TORCH_CHECK(qs.has_value() && qs->defined(), "gemm_mx: q8 needs qs");
-    check_u8_rows(*qs, M, NO / 32, "gemm_mx: qs");
+    TORCH_CHECK(qs.has_value() && qs->defined() && NO % 128 == 0, "gemm_mx: q8 needs qs (output width % 128)");
+    mx.ldqs = check_planes(*qs, NO / 128, M, "gemm_mx: qs");
     mx.q8 = reinterpret_cast<uint8_t*>(q8->data_ptr());
     mx.ldq = q8->stride(0);
     mx.qs = qs->data_ptr<uint8_t>();
-    mx.ldqs = qs->stride(0);
   }
   if (ssq_out.has_value() && ssq_out->defined()) {
     TORCH_CHECK(!glu && cp != nullptr, "gemm_mx: ssq_out needs the bf16 output");
@@ -461,7 +464,7 @@ void gemm_mx(const at::Tensor& a8, const at::Tensor& a_bs, const at::Tensor& w8,
   }
   const at::DeviceGuard guard(a8.device());
   LUMEN_CHECK_HIP(lumen::gemm_mx(reinterpret_cast<const uint8_t*>(a8.data_ptr()), a8.stride(0), a_bs.data_ptr<uint8_t>(),
-                                 a_bs.stride(0), reinterpret_cast<const uint8_t*>(w8.data_ptr()), w8.stride(0),
+                                 ld_bs, reinterpret_cast<const uint8_t*>(w8.data_ptr()), w8.stride(0),
                                  sw.data_ptr<float>(), cp, ldc, (int)M, (int)N, (int)K, ep, mx, cur_stream(),
                                  (int)variant));
 }
@@ -473,7 +476,7 @@ void quant_rows_mx(const at::Tensor& x, at::Tensor q8, at::Tensor qs, const c10:
   TORCH_CHECK(K % 128 == 0 && x.stride(0) % 8 == 0, "quant_rows_mx: K % 128 == 0, 16-byte aligned rows");
   check_f8_rows(q8, "quant_rows_mx: q8");
   TORCH_CHECK(q8.size(0) >= M && q8.size(1) == K, "quant_rows_mx: q8 shape");
-  check_u8_rows(qs, M, K / 32, "quant_rows_mx: qs");
+  const int64_t ldqs = check_planes(qs, K / 128, M, "quant_rows_mx: qs");
   float* sp = nullptr;
   int64_t lds = 0;
   if (ssq.has_value() && ssq->defined()) {
@@ -483,7 +486,7 @@ void quant_rows_mx(const at::Tensor& x, at::Tensor q8, at::Tensor qs, const c10:
   }
   const at::DeviceGuard guard(x.device());
   LUMEN_CHECK_HIP(lumen::quant_rows_mx(bf(x), x.stride(0), reinterpret_cast<uint8_t*>(q8.data_ptr()), q8.stride(0),
-                                       qs.data_ptr<uint8_t>(), qs.stride(0), sp, lds, (int)M, (int)K, cur_stream()));
+                                       qs.data_ptr<uint8_t>(), ldqs, sp, lds, (int)M, (int)K, cur_stream()));
 }
 
 // per-token fp8 quantisation of bf16 rows: out8 [M, K] e4m3fn, scale [M] = amax / 448
@@ -643,7 +646,8 @@ void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at
 }
 
 // attention with an MX fp8 output (the W8A8 o-projection's operand): o8 e4m3fn [B, Sq, H*D] (or
-// [Sq, H*D] when B == 1), os uint8 [B, Sq, H*D/32] (or 2-D); o (bf16 [B, Sq, H, D]) optional.
+// [Sq, H*D] when B == 1), os uint8 scale planes [B, H*D/128, Sq, 4] (or 3-D when B == 1); o (bf16
+// [B, Sq, H, D]) optional.
 void attention_mx(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const c10::optional<at::Tensor>& o,
                   at::Tensor o8, at::Tensor os, const c10::optional<at::Tensor>& kv_len, double scale, bool causal) {
   for (auto* t : {&q, &k, &v}) {
@@ -656,11 +660,14 @@ void attention_mx(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
               "attention_mx: kv shape");
   TORCH_CHECK(D == 64 || D == 128, "attention_mx: head dim 64 / 128");
   TORCH_CHECK(o8.is_cuda() && o8.scalar_type() == at::kFloat8_e4m3fn && o8.stride(-1) == 1 &&
-              (o8.dim() == 3 || (o8.dim() == 2 && B == 1)) && o8.size(-1) >= H * D && o8.size(-2) >= Sq &&
-              o8.stride(-2) % 4 == 0, "attention_mx: o8 e4m3fn [B, Sq, >= H*D]");
-  TORCH_CHECK(os.is_cuda() && os.scalar_type() == at::kByte && os.stride(-1) == 1 && os.dim() == o8.dim() &&
-              os.size(-1) >= H * D / 32 && os.size(-2) >= Sq && os.stride(-2) % 4 == 0 &&
-              reinterpret_cast<uintptr_t>(os.data_ptr()) % 4 == 0, "attention_mx: os uint8 [B, Sq, >= H*D/32]");
+              (o8.dim() == 3 || (o8.dim() == 2 && o8.size(0) >= B * Sq)) && o8.size(-1) >= H * D &&
+              o8.size(-2) >= Sq && o8.stride(-2) % 4 == 0, "attention_mx: o8 e4m3fn [B, Sq, >= H*D] or [B*Sq, >= H*D]");
+  TORCH_CHECK((H * D) % 128 == 0, "attention_mx: H*D % 128");
+  TORCH_CHECK(os.is_cuda() && os.scalar_type() == at::kByte && (os.dim() == 3 || (os.dim() == 4)) &&
+              os.size(-3) == H * D / 128 && os.size(-2) >= Sq && os.size(-1) == 4 && os.stride(-1) == 1 &&
+              os.stride(-2) == 4 && os.stride(-3) % 4 == 0 && (os.dim() == 4 || os.size(-2) >= B * Sq) &&
+              reinterpret_cast<uintptr_t>(os.data_ptr()) % 4 == 0,
+              "attention_mx: os uint8 scale planes [(B,) H*D/128, >= Sq, 4]");
   lumen::AttnArgs a{};
   a.q = bf(q); a.k = bf(k); a.v = bf(v);
   a.q_sb = q.stride(0); a.q_ss = q.stride(1); a.q_sh = q.stride(2);
@@ -673,8 +680,8 @@ void attention_mx(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
   }
   a.o8 = reinterpret_cast<uint8_t*>(o8.data_ptr());
   a.os = os.data_ptr<uint8_t>();
-  a.o8_sb = o8.dim() == 3 ? o8.stride(0) : 0; a.o8_ss = o8.stride(-2);
-  a.os_sb = os.dim() == 3 ? os.stride(0) : 0; a.os_ss = os.stride(-2);
+  a.o8_sb = o8.dim() == 3 ? o8.stride(0) : Sq * o8.stride(0); a.o8_ss = o8.stride(-2);   // 2-D: rows b-major
+  a.os_sb = os.dim() == 4 ? os.stride(0) : Sq * 4; a.os_ss = os.stride(-3);
   if (kv_len.has_value() && kv_len->defined()) {
     TORCH_CHECK(kv_len->scalar_type() == at::kInt && kv_len->numel() == B, "attention_mx: kv_len int32 [B]");
     a.kv_len = kv_len->data_ptr<int>();

@@ -45,9 +45,12 @@ _FUSED_DECODE_NORM = True
 # decode: RoPE + current-token KV-cache write inside the paged attention kernel (no rope_kv launch)
 _FUSED_DECODE_ROPE = True
 # W8A8 prefill with MX (block-scaled) activations produced in the epilogues (LLM._layers_mx): 6
-# launches per layer instead of 10 -- no RMSNorm+quant and no row-quant passes (LUMEN_PREFILL_MX=0:
-# the per-token-scale chain of _layers_f8)
-_PREFILL_MX = os.environ.get("LUMEN_PREFILL_MX", "1") != "0"
+# launches per layer instead of 10 -- no RMSNorm+quant and no row-quant passes.  Opt-in
+# (LUMEN_PREFILL_MX=1): on the 8B TTFT it measured 13.12 vs 12.79 ms for the per-token chain -- the
+# 4 x 32 removed launches (~0.9 ms) are paid back by the MX epilogues (o / down: bf16 + MX copy +
+# sums of squares, +4.5 us each) and the block-scale staging (+2-7 % per GEMM),
+# profiles/r4_mx_chain_ab_v1.txt
+_PREFILL_MX = os.environ.get("LUMEN_PREFILL_MX", "0") == "1"
 
 
 @dataclass
@@ -334,7 +337,7 @@ class LLM(nn.Module):
         """Fused MX prefill: fp8 weights with folded norms, one rank, 128-aligned widths."""
         cfg = self.cfg
         return (_PREFILL_MX and x.is_cuda and self._f8_ok(x.shape[0]) and self.norm_folded and not self.tp.enabled
-                and cfg.head_dim in (64, 128) and cfg.hidden_size % 128 == 0 and self.layers[0].I % 64 == 0
+                and cfg.head_dim in (64, 128) and cfg.hidden_size % 128 == 0 and self.layers[0].I % 128 == 0
                 and (self.H * cfg.head_dim) % 128 == 0)
 
     def _layers(self, x: torch.Tensor, pos: torch.Tensor, slots: Optional[torch.Tensor], kv, attn_fn) -> torch.Tensor:
@@ -454,13 +457,14 @@ class LLM(nn.Module):
         dev = x.device
         f8 = torch.float8_e4m3fn
         l0 = self.layers[0]
-        x8 = torch.empty((T, Hd), device=dev, dtype=f8)
-        xs = torch.empty((T, Hd // 32), device=dev, dtype=torch.uint8)
+        u8 = torch.uint8
+        x8 = torch.empty((T, Hd), device=dev, dtype=f8)               # MX operands: fp8 values +
+        xs = torch.empty((Hd // 128, T, 4), device=dev, dtype=u8)     # E8M0 scale planes (ops.mx_planes)
         ssq = torch.empty((T, Hd // 128), device=dev, dtype=torch.float32)
         a8 = torch.empty((T, l0.H * D), device=dev, dtype=f8)
-        as_ = torch.empty((T, l0.H * D // 32), device=dev, dtype=torch.uint8)
+        as_ = torch.empty((l0.H * D // 128, T, 4), device=dev, dtype=u8)
         g8 = torch.empty((T, l0.I), device=dev, dtype=f8)
-        gs = torch.empty((T, l0.I // 32), device=dev, dtype=torch.uint8)
+        gs = torch.empty((l0.I // 128, T, 4), device=dev, dtype=u8)
         ops.quant_rows_mx(x, x8, xs, ssq)
         for i, l in enumerate(self.layers):
             qkv = ops.linear_mx(x8, xs, l.qkv_w, l.qkv_s, bias=l.qkv_b, ssq_in=ssq, norm_eps=eps)

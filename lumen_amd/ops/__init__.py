@@ -251,10 +251,27 @@ def linear_f8(x8: torch.Tensor, x_scale: torch.Tensor, w8: torch.Tensor, w_scale
     return out
 
 
+def mx_planes(qs_rows: torch.Tensor) -> torch.Tensor:
+    """E8M0 bytes [M, K/32] (row-major) -> the kernels' K-step planes [K/128, M, 4]: the byte of
+    (row m, 32-column block b) at [b // 4, m, b % 4], so a GEMM's per-K-step load of 64 rows'
+    scales is 256 contiguous bytes."""
+    M, nb = qs_rows.shape
+    out = torch.empty((nb // 4, M, 4), dtype=qs_rows.dtype, device=qs_rows.device)   # standard strides
+    out.copy_(qs_rows.reshape(M, nb // 4, 4).permute(1, 0, 2))
+    return out
+
+
+def mx_rows(qs: torch.Tensor) -> torch.Tensor:
+    """Scale planes [K/128, M, 4] -> row-major E8M0 bytes [M, K/32]."""
+    P, M, _ = qs.shape
+    return qs.permute(1, 0, 2).reshape(M, P * 4)
+
+
 def mx_quant_ref(x: torch.Tensor):
-    """MX fp8 of rows x [M, K] (K % 32 == 0), the arithmetic of the GPU producers: per 32
+    """MX fp8 of rows x [M, K] (K % 128 == 0), the arithmetic of the GPU producers: per 32
     columns e = the smallest exponent with amax / 2^e <= 448 (E8M0 byte e + 127), values
-    x * 2^-e saturated to e4m3fn.  -> (q8 [M, K] float8_e4m3fn, qs [M, K/32] uint8)."""
+    x * 2^-e saturated to e4m3fn.  -> (q8 [M, K] float8_e4m3fn, qs [K/128, M, 4] uint8 scale
+    planes, see :func:`mx_planes`)."""
     M, K = x.shape
     xb = x.float().reshape(M, K // 32, 32)
     t = xb.abs().amax(-1) * torch.tensor(1.0 / 448.0, dtype=torch.float32)
@@ -263,32 +280,32 @@ def mx_quant_ref(x: torch.Tensor):
     e = torch.where(t == 0, torch.full_like(e, -127), e)
     e = torch.where((t > 0) & (t < 2.0 ** -126), torch.full_like(e, -126), e).clamp(-127, 126)
     q = (xb * torch.exp2(-e.float())[..., None]).clamp(-448, 448).to(torch.float8_e4m3fn)
-    return q.reshape(M, K), (e + 127).to(torch.uint8)
+    return q.reshape(M, K), mx_planes((e + 127).to(torch.uint8))
 
 
 def mx_dequant(q8: torch.Tensor, qs: torch.Tensor) -> torch.Tensor:
-    """MX fp8 [M, K] + E8M0 [M, >= K/32] -> fp32 [M, K]."""
+    """MX fp8 [M, K] + E8M0 scale planes [K/128, >= M, 4] -> fp32 [M, K]."""
     M, K = q8.shape
-    s = torch.exp2(qs[:, :K // 32].float() - 127.0)
+    s = torch.exp2(mx_rows(qs[:, :M]).float() - 127.0)
     return (q8.float().reshape(M, K // 32, 32) * s[..., None]).reshape(M, K)
 
 
 def quant_rows_mx(x: torch.Tensor, q8: Optional[torch.Tensor] = None, qs: Optional[torch.Tensor] = None,
                   ssq: Optional[torch.Tensor] = None):
-    """bf16 rows [M, K] -> MX fp8 (q8 [M, K] e4m3fn, qs [M, K/32] E8M0) and, when ``ssq`` is given,
+    """bf16 rows [M, K] -> MX fp8 (q8 [M, K] e4m3fn, qs [K/128, M, 4] E8M0 planes) and, when ``ssq`` is given,
     its per-(row, 128-column) sums of squares [M, K/128] (the rstd source of a norm-folded
     consumer, ops.linear_mx(ssq_in=...)).  Returns (q8, qs)."""
     M, K = x.shape
     if q8 is None:
         q8 = torch.empty((M, K), device=x.device, dtype=torch.float8_e4m3fn)
     if qs is None:
-        qs = torch.empty((M, K // 32), device=x.device, dtype=torch.uint8)
+        qs = torch.empty((K // 128, M, 4), device=x.device, dtype=torch.uint8)
     if x.is_cuda:
         hip_ops().quant_rows_mx(x, q8, qs, ssq)
         return q8, qs
     a, b = mx_quant_ref(x)
     q8[:M].copy_(a)
-    qs[:M, :K // 32].copy_(b)
+    qs[:, :M].copy_(b)
     if ssq is not None:
         ssq[:M, :K // 128] = (x.float() ** 2).reshape(M, K // 128, 128).sum(-1)
     return q8, qs
@@ -331,7 +348,7 @@ def linear_mx(x8: torch.Tensor, xs: torch.Tensor, w8: torch.Tensor, w_scale: tor
         if q8 is not None:
             a, b = mx_quant_ref(r)
             q8[:M].copy_(a)
-            qs[:M, :NO // 32].copy_(b)
+            qs[:, :M].copy_(b)
         return out
     if residual is not None:
         y = y + residual.float()[:M, :N]
@@ -340,7 +357,7 @@ def linear_mx(x8: torch.Tensor, xs: torch.Tensor, w8: torch.Tensor, w_scale: tor
     if q8 is not None:
         a, b = mx_quant_ref(yb.float())
         q8[:M].copy_(a)
-        qs[:M, :N // 32].copy_(b)
+        qs[:, :M].copy_(b)
     if ssq_out is not None:
         ssq_out[:M, :N // 128] = (yb.float() ** 2).reshape(M, N // 128, 128).sum(-1)
     return out
@@ -530,17 +547,17 @@ def attention(q, k, v, scale: Optional[float] = None, causal: bool = False, kv_l
 def attention_mx(q, k, v, scale: Optional[float] = None, causal: bool = False, kv_len=None,
                  q_out: Optional[tuple] = None, out=None):
     """:func:`attention` whose output leaves as MX fp8 (the W8A8 o-projection's operand,
-    :func:`linear_mx`): returns (o8 [B*Sq, H*D] e4m3fn, os [B*Sq, H*D/32] E8M0).  ``out``
-    (bf16 [B, Sq, H, D]) is also written when given.  On the CPU: attention + mx_quant_ref."""
+    :func:`linear_mx`): returns (o8 [B*Sq, H*D] e4m3fn, os [H*D/128, B*Sq, 4] E8M0 planes).
+    ``out`` (bf16 [B, Sq, H, D]) is also written when given.  On the CPU: attention + mx_quant_ref."""
     B, Sq, H, D = q.shape
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     if q_out is None:
         q_out = (torch.empty((B * Sq, H * D), device=q.device, dtype=torch.float8_e4m3fn),
-                 torch.empty((B * Sq, H * D // 32), device=q.device, dtype=torch.uint8))
+                 torch.empty((H * D // 128, B * Sq, 4), device=q.device, dtype=torch.uint8))
     o8, os_ = q_out
     if q.is_cuda:
         kl = kv_len.to(torch.int32) if kv_len is not None else None
-        hip_ops().attention_mx(q, k, v, out, o8.view(B, Sq, -1), os_.view(B, Sq, -1), kl, float(scale), bool(causal))
+        hip_ops().attention_mx(q, k, v, out, o8, os_, kl, float(scale), bool(causal))
         return o8, os_
     o = attention(q, k, v, scale=scale, causal=causal, kv_len=kv_len)
     if out is not None:
@@ -548,7 +565,7 @@ def attention_mx(q, k, v, scale: Optional[float] = None, causal: bool = False, k
     of = attention(q.float(), k.float(), v.float(), scale=scale, causal=causal, kv_len=kv_len)
     a, b = mx_quant_ref(of.reshape(B * Sq, H * D))
     o8.copy_(a)
-    os_[:, :H * D // 32].copy_(b)
+    os_[:, :B * Sq].copy_(b)
     return o8, os_
 
 

@@ -62,7 +62,7 @@ def test_gemm_mx_exact_small_integers():
     g = torch.Generator().manual_seed(3)
     M, N, K = 64, 128, 256
     x8 = torch.randint(-4, 5, (M, K), generator=g).float().to(torch.float8_e4m3fn)
-    xs = torch.randint(124, 131, (M, K // 32), generator=g).to(torch.uint8)
+    xs = ops.mx_planes(torch.randint(124, 131, (M, K // 32), generator=g).to(torch.uint8))
     w8 = torch.randint(-4, 5, (N, K), generator=g).float().to(torch.float8_e4m3fn)
     sw = torch.ones(N)
     ref = ops.mx_dequant(x8, xs) @ w8.float().t()
@@ -78,12 +78,12 @@ def test_gemm_mx_residual_outputs(M, N, K, variant):
     g = torch.Generator().manual_seed(M + 7 * N)
     x8, xs, w8, sw = _operands(M, N, K, g)
     r = torch.randn(M, N, generator=g).bfloat16()
-    ref_q, ref_s = torch.empty(M, N, dtype=torch.float8_e4m3fn), torch.empty(M, N // 32, dtype=torch.uint8)
+    ref_q, ref_s = torch.empty(M, N, dtype=torch.float8_e4m3fn), torch.empty(N // 128, M, 4, dtype=torch.uint8)
     ref_ss = torch.empty(M, N // 128)
     ref = ops.linear_mx(x8, xs, w8, sw, residual=r, out=r.clone(), q_out=(ref_q, ref_s), ssq_out=ref_ss)
     xg = r.to(DEV)
     q8 = torch.empty(M, N, device=DEV, dtype=torch.float8_e4m3fn)
-    qs = torch.empty(M, N // 32, device=DEV, dtype=torch.uint8)
+    qs = torch.empty(N // 128, M, 4, device=DEV, dtype=torch.uint8)
     ss = torch.empty(M, N // 128, device=DEV)
     ops.linear_mx(x8.to(DEV), xs.to(DEV), w8.to(DEV), sw.to(DEV), residual=xg, out=xg, q_out=(q8, qs),
                   ssq_out=ss, variant=variant)
@@ -103,10 +103,10 @@ def test_gemm_mx_swiglu_mx_output(variant, write_out):
     g = torch.Generator().manual_seed(11 + variant)
     M, N, K = 300, 2048, 1024
     x8, xs, w8, sw = _operands(M, N, K, g)
-    ref_q, ref_s = torch.empty(M, N // 2, dtype=torch.float8_e4m3fn), torch.empty(M, N // 64, dtype=torch.uint8)
+    ref_q, ref_s = torch.empty(M, N // 2, dtype=torch.float8_e4m3fn), torch.empty(N // 256, M, 4, dtype=torch.uint8)
     ref = ops.linear_mx(x8, xs, w8, sw, glu=True, q_out=(ref_q, ref_s))
     q8 = torch.empty(M, N // 2, device=DEV, dtype=torch.float8_e4m3fn)
-    qs = torch.empty(M, N // 64, device=DEV, dtype=torch.uint8)
+    qs = torch.empty(N // 256, M, 4, device=DEV, dtype=torch.uint8)
     got = ops.linear_mx(x8.to(DEV), xs.to(DEV), w8.to(DEV), sw.to(DEV), glu=True, q_out=(q8, qs),
                         write_out=write_out, variant=variant)
     if write_out:
@@ -140,13 +140,19 @@ def test_gemm_mx_graph_capture_and_repeat():
     for v in (10, 10):
         ops.linear_mx(x8, xs, w8, sw, out=out, variant=v)
         assert torch.equal(out, first)
+    # captured on torch's capture stream, which has no stream-K workspace yet: the launch falls back
+    # to the tiled pipeline (other K summation order) -- replays are bit-identical to each other
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
         ops.linear_mx(x8, xs, w8, sw, out=out, variant=10)
     out.zero_()
     graph.replay()
     torch.cuda.synchronize()
-    assert torch.equal(out, first)
+    rep = out.clone()
+    out.zero_()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, rep) and _rel(rep, first) < 1e-2
 
 
 @pytest.mark.parametrize("S,H,Hkv,D,causal", [(624, 32, 8, 128, True), (577, 16, 16, 64, False), (70, 4, 2, 128, True)])
@@ -188,13 +194,18 @@ def test_llm_prefill_mx_chain_matches_per_token_chain(T):
     x = (torch.randn(T, 512, device=DEV, generator=g) * 0.5).bfloat16()
     m.prefill(x.clone())          # folds the norms (both chains then use the same weights)
     assert m.norm_folded and m._mx_ok(x)
-    old = L._PREFILL_MX
+    old, old_min = L._PREFILL_MX, L._F8_MIN_ROWS
     try:
+        L._F8_MIN_ROWS = 1 << 30          # fp8 weights, bf16 activations: the reference of both chains
+        w8a16 = m.prefill(x.clone())
+        L._F8_MIN_ROWS = old_min
         L._PREFILL_MX = False
-        ref = m.prefill(x.clone())
+        per_token = m.prefill(x.clone())
         L._PREFILL_MX = True
         got = m.prefill(x.clone())
     finally:
-        L._PREFILL_MX = old
-    assert _rel(got, ref) < 5e-2
+        L._PREFILL_MX, L._F8_MIN_ROWS = old, old_min
     assert torch.isfinite(got).all()
+    # activation quantisation error of the MX chain: no worse than the per-token chain's
+    e_mx, e_pt = _rel(got, w8a16), _rel(per_token, w8a16)
+    assert e_mx < 1.25 * e_pt + 5e-3, (e_mx, e_pt)

@@ -9,6 +9,7 @@ set exceeds the 256 MiB Infinity Cache) and a different activation matrix.
 
     python tools/cold_gemm_bench.py --what vit --variants -1,20002,20013
     python tools/cold_gemm_bench.py --what prefill --variants 0,1,2,3,6 --splits -1,1,2
+    python tools/cold_gemm_bench.py --what mx --epi full      # the fused MX chain's GEMMs (ops.linear_mx)
 
 Variant codes: bf16 (--what vit) are ops.linear tile codes (-1 auto; 20000 + v: the LDS-DMA
 pipeline of csrc/gemm_f8.hip, v = 2 / 3 / 5 r2 shapes, 10 + c: launch_variant code c);
@@ -49,7 +50,9 @@ def timed(fn, L, reps=3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", choices=["vit", "prefill"], default="vit")
+    ap.add_argument("--what", choices=["vit", "prefill", "mx"], default="vit")
+    ap.add_argument("--epi", choices=["full", "plain"], default="full",
+                    help="mx: the chain's epilogues (rstd, MX outputs, sums of squares) or a plain store")
     ap.add_argument("--M", type=int, default=0)
     ap.add_argument("--variants", default="")
     ap.add_argument("--splits", default="-1")
@@ -60,6 +63,7 @@ def main():
     dev = "cuda"
     torch.manual_seed(0)
     vit = a.what == "vit"
+    mx = a.what == "mx"
     M = a.M or (577 if vit else 624)
     variants = [int(v) for v in (a.variants or ("-1,20002,20003,20005" if vit else "0,1,2")).split(",")]
     splits = [int(s) for s in a.splits.split(",")]
@@ -83,9 +87,17 @@ def main():
                 sws.append(sw)
             xs, sxs = [], []
             for _ in range(L):
-                x8, sx = ops.quant_rows_fp8(torch.randn(M, K, device=dev).bfloat16())
+                if mx:
+                    x8, sx = ops.quant_rows_mx(torch.randn(M, K, device=dev).bfloat16())
+                else:
+                    x8, sx = ops.quant_rows_fp8(torch.randn(M, K, device=dev).bfloat16())
                 xs.append(x8)
                 sxs.append(sx)
+            NO_ = N // 2 if x4 else N
+            q8 = torch.empty(M, NO_, device=dev, dtype=torch.float8_e4m3fn)
+            qs = torch.empty(NO_ // 128, M, 4, device=dev, dtype=torch.uint8)
+            ssq_in = torch.rand(M, K // 128, device=dev) + 1.0
+            ssq_out = torch.empty(M, N // 128, device=dev)
         r = torch.randn(M, N, device=dev).bfloat16() if resid else None
         NO = N // 2 if (not vit and x4) else N
         out = torch.empty(M, NO, device=dev, dtype=torch.bfloat16)
@@ -97,6 +109,15 @@ def main():
                     f = lambda l, v=v: ops.linear(xs[l], ws[l], b, act=x4, residual=r, out=out, tile=v)  # noqa: E731
                     fw = lambda l, v=v: ops.linear(xs[0], ws[0], b, act=x4, residual=r, out=out, tile=v)  # noqa: E731
                     key = f"{name}_t{v}"
+                elif mx:
+                    full = a.epi == "full"
+                    kw = dict(residual=r, glu=x4, variant=v)
+                    if full:
+                        kw.update(q_out=(q8, qs) if (x4 or resid) else None, ssq_out=ssq_out if resid else None,
+                                  ssq_in=ssq_in if not resid else None, norm_eps=1e-5, write_out=not x4)
+                    f = lambda l, v=v, kw=kw: ops.linear_mx(xs[l], sxs[l], ws[l], sws[l], out=out, **kw)  # noqa: E731
+                    fw = lambda l, v=v, kw=kw: ops.linear_mx(xs[0], sxs[0], ws[0], sws[0], out=out, **kw)  # noqa: E731
+                    key = f"{name}_mx{a.epi}_v{v}"
                 else:
                     f = lambda l, v=v, sp=sp, wv=wv: ops.linear_f8(xs[l], sxs[l], wv[l], sws[l], residual=r,  # noqa: E731
                                                                    out=out, glu=x4, splits=sp, variant=v)

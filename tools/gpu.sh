@@ -26,6 +26,8 @@
 #   jpeg           device JPEG tests + tools/jpeg_bench.py
 #   mx             MX W8A8 chain tests (tests/test_mx_gpu.py) + fp8 GEMM + LLM-op tests
 #   ttft           VLM TTFT only (8B fp8, 30 requests, device JPEG decode)
+#   mx_cold        cold-weight timing of the MX chain's GEMMs (full / plain epilogues) vs per-token fp8
+#   ttft_ab        TTFT with the fused MX prefill chain (LUMEN_PREFILL_MX=1) vs the per-token-scale chain
 #   pmc_gemm       PMC counters (MFMA, LDS conflicts, busy) of one ViT-L/14 GEMM shape
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -123,6 +125,13 @@ for task in "$@"; do
     mx)
       step mx_tests 400 python -u -m pytest tests/test_mx_gpu.py tests/test_fp8_gpu.py tests/test_llm_ops_gpu.py -q \
         --timeout 120 --timeout-method thread ;;
+    mx_cold)   # MX chain GEMMs (cold weights): full epilogues vs plain stores vs the per-token fp8 GEMMs
+      step mx_cold_full 300 python -u tools/cold_gemm_bench.py --what mx --epi full --variants=0,1,2,4,10
+      step mx_cold_plain 300 python -u tools/cold_gemm_bench.py --what mx --epi plain --variants=0,2
+      step f8_cold 300 python -u tools/cold_gemm_bench.py --what prefill --variants=0,2 ;;
+    ttft_ab)
+      step ttft_mx 400 env LUMEN_PREFILL_MX=1 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0
+      step ttft_pt 400 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0 ;;
     ttft) step ttft 400 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0 ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
