@@ -84,7 +84,13 @@ struct SkArgs {
 
 constexpr int MX_SCRATCH = 40960;    // epilogue LDS bytes past the per-wave slabs: rstd[128], ssq[128][WN]
 
-template <int NSTAGE, int WN, bool F8, int BN = 128, bool SK = false, bool BS = false>
+__device__ __forceinline__ void pp_bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int NSTAGE, int WN, bool F8, int BN = 128, bool SK = false, bool BS = false, bool PP = false>
 __global__ void __launch_bounds__(128 * WN)
 gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restrict__ sa, const uint8_t* __restrict__ W,
                int64_t ldw, const float* __restrict__ sw, void* __restrict__ C, int64_t ldc, int M, int N, int K,
@@ -162,17 +168,11 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
     for (int s = 0; s < NSTAGE - 1; ++s)
       if (s < n) stage(s, (int64_t)(k0 + s) * 128);
 
-    for (int kt = 0; kt < n; ++kt) {
-      // stage kt landed for this wave (NSTAGE-2 younger stages may stay in flight) ...
-      if (kt + NSTAGE - 2 < n) f8_vm_wait<(PER + PERW + (BS ? 1 : 0)) * (NSTAGE - 2)>();
-      else f8_vm_wait<0>();
-      // ... and for every wave; every wave is also done reading stage kt-1's buffer
-      __builtin_amdgcn_s_barrier();
-      if (kt + NSTAGE - 1 < n) stage((kt + NSTAGE - 1) % NSTAGE, (int64_t)(k0 + kt + NSTAGE - 1) * 128);
+    u32x4_t fa[4][2], fb[NR][2];
+    int as[4];
+    auto frags = [&](const int kt) {
       const char* sA = smem + (kt % NSTAGE) * STAGE;
       const char* sW = sA + 128 * 128;
-      u32x4_t fa[4][2], fb[NR][2];
-      int as[4];
 #pragma unroll
       for (int j = 0; j < NR; ++j) {
         const int r = wn * TN + j * 16 + frow;
@@ -187,6 +187,8 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
         if constexpr (BS) as[i] = *(const uint8_t*)(sA + 128 * 128 + BN * 128 + wm * 256 + (i * 16 + frow) * 4 + g);
         else as[i] = 127;
       }
+    };
+    auto mfmas = [&]() {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -204,6 +206,48 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
                                                                 __builtin_bit_cast(bf16x8_t, fb[j][1]), acc[i][j], 0, 0, 0);
           }
         }
+    };
+    constexpr int P = PER + PERW + (BS ? 1 : 0);   // glds instructions per wave per stage
+    if constexpr (PP) {
+      // Ping-pong: wave group wm = 1 runs one barrier behind group 0, so on every SIMD one wave's
+      // MFMAs overlap its partner's fragment reads and staging issue (the gemm_pp.hip schedule on
+      // this 128 x 128 tile).  Phase kt of a group: read stage kt | issue stage kt + NSTAGE - 1 |
+      // own DMAs of stage kt + 1 landed | barrier | MFMAs | barrier.  With the lag, stage kt + 1's
+      // DMAs of BOTH groups were waited for before a barrier each group passes before reading it,
+      // and the buffer a phase restages (stage kt - 1) was last read by the lagging group before
+      // the barrier the leading group passed just before issuing.  Needs NSTAGE >= 3.
+      static_assert(!PP || NSTAGE >= 3, "ping-pong needs a stage in flight across each phase");
+      if (n > NSTAGE - 2) f8_vm_wait<P * (NSTAGE - 2)>();
+      else f8_vm_wait<0>();
+      pp_bar();
+      if (wm == 1) pp_bar();
+      for (int kt = 0; kt < n; ++kt) {
+        frags(kt);
+        if (kt + NSTAGE - 1 < n) {
+          stage((kt + NSTAGE - 1) % NSTAGE, (int64_t)(k0 + kt + NSTAGE - 1) * 128);
+          f8_vm_wait<P * (NSTAGE - 2)>();
+        } else {
+          f8_vm_wait<0>();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pp_bar();
+        __builtin_amdgcn_s_setprio(1);
+        mfmas();
+        __builtin_amdgcn_s_setprio(0);
+        pp_bar();
+      }
+      if (wm == 0) pp_bar();
+    } else {
+      for (int kt = 0; kt < n; ++kt) {
+        // stage kt landed for this wave (NSTAGE-2 younger stages may stay in flight) ...
+        if (kt + NSTAGE - 2 < n) f8_vm_wait<P * (NSTAGE - 2)>();
+        else f8_vm_wait<0>();
+        // ... and for every wave; every wave is also done reading stage kt-1's buffer
+        __builtin_amdgcn_s_barrier();
+        if (kt + NSTAGE - 1 < n) stage((kt + NSTAGE - 1) % NSTAGE, (int64_t)(k0 + kt + NSTAGE - 1) * 128);
+        frags(kt);
+        mfmas();
+      }
     }
     __syncthreads();   // every wave done with the stage buffers (the epilogue reuses them)
   };
@@ -409,20 +453,20 @@ static constexpr size_t f8_lds() {
   return (size_t)NS * (128 * 128 + BN * 128 + (BS ? 2 * WN * 256 : 0));
 }
 
-template <int NS, int WN, bool F8 = true, int BN = 128, bool BS = false>
+template <int NS, int WN, bool F8 = true, int BN = 128, bool BS = false, bool PP = false>
 static hipError_t launch_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
                             const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep,
                             hipStream_t stream, int splits = 1, const MxArgs& mx = MxArgs{}) {
   constexpr size_t lds = f8_lds<NS, WN, BS, BN>();
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm_f8_kernel<NS, WN, F8, BN, false, BS>,
+    hipFuncSetAttribute((const void*)gemm_f8_kernel<NS, WN, F8, BN, false, BS, PP>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int tiles = ((M + 127) / 128) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8, BN, false, BS>), dim3(tiles, splits), dim3(128 * WN), lds, stream, A,
-                     lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, SkArgs{}, mx);
+  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8, BN, false, BS, PP>), dim3(tiles, splits), dim3(128 * WN), lds, stream,
+                     A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, SkArgs{}, mx);
   return hipGetLastError();
 }
 
@@ -433,7 +477,7 @@ static uint32_t* sk_counters(size_t n, hipStream_t stream);
 static float* sk_slabs(size_t bytes, hipStream_t stream);
 static int f8_num_cus();
 
-template <int NS, int WN, bool F8 = true, int BN = 128, bool BS = false>
+template <int NS, int WN, bool F8 = true, int BN = 128, bool BS = false, bool PP = false>
 static hipError_t launch_f8_sk(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
                                const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep,
                                hipStream_t stream, const MxArgs& mx = MxArgs{}) {
@@ -451,13 +495,13 @@ static hipError_t launch_f8_sk(const uint8_t* A, int64_t lda, const float* sa, c
   constexpr size_t lds = f8_lds<NS, WN, BS, BN>();
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm_f8_kernel<NS, WN, F8, BN, true, BS>,
+    hipFuncSetAttribute((const void*)gemm_f8_kernel<NS, WN, F8, BN, true, BS, PP>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int used = (total + sk.ipw - 1) / sk.ipw;   // workgroups with work
-  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8, BN, true, BS>), dim3(used), dim3(128 * WN), lds, stream, A, lda, sa, W,
-                     ldw, sw, C, ldc, M, N, K, ep, sk, mx);
+  hipLaunchKernelGGL((gemm_f8_kernel<NS, WN, F8, BN, true, BS, PP>), dim3(used), dim3(128 * WN), lds, stream, A, lda,
+                     sa, W, ldw, sw, C, ldc, M, N, K, ep, sk, mx);
   return hipGetLastError();
 }
 
@@ -565,19 +609,29 @@ static hipError_t launch_f8_split(const uint8_t* A, int64_t lda, const float* sa
 // MFMAs of step k: no change); every shape runs ~0.53 us per 128-byte K-step + ~7 us per launch
 // (profiles/r4_cold_gemm_blocked_sp_v1.txt, r4_f8_gemm_time_vs_k_v1.txt).
 //   9 = stream-K <3, 8, 128>   10 = stream-K <4, 4, 128>   11 = stream-K <4, 8, 128>
+//  12 / 13 / 14 = ping-pong <3 / 4 / 5 stages, 8 waves, 128>   15 = stream-K ping-pong <4, 8, 128>
 static int variant_bn(int v) { return v == 6 || v == 7 ? 256 : 128; }
 
 template <bool F8>
 static hipError_t launch_variant(int v, const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
                                  const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, int S,
                                  hipStream_t stream) {
-  if (v >= 9 && v <= 11 && ep.split_koff == 0) {
-    hipError_t e = v == 9 ? launch_f8_sk<3, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream)
-                 : v == 10 ? launch_f8_sk<4, 2, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream)
-                           : launch_f8_sk<4, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
-    if (e != hipErrorNotReady) return e;
-    v = 2;      // no workspace (first call inside a graph capture): the tiled pipeline
+  if ((v >= 9 && v <= 11) || v == 15) {
+    if (ep.split_koff == 0) {
+      hipError_t e = v == 9 ? launch_f8_sk<3, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream)
+                   : v == 10 ? launch_f8_sk<4, 2, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream)
+                   : v == 11 ? launch_f8_sk<4, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream)
+                             : launch_f8_sk<4, 4, F8, 128, false, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep,
+                                                                          stream);
+      if (e != hipErrorNotReady) return e;
+    }
+    v = v == 15 ? 13 : 2;      // no workspace (first call inside a graph capture): the tiled pipeline
     S = 1;
+  }
+  if (v >= 12 && v <= 14) {    // ping-pong forms: no split-K slabs
+    if (v == 12) return launch_f8<3, 4, F8, 128, false, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    if (v == 13) return launch_f8<4, 4, F8, 128, false, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    return launch_f8<5, 4, F8, 128, false, true>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
   }
   if (S > 1) {
     switch (v) {
@@ -663,11 +717,19 @@ hipError_t gemm_mx(const uint8_t* A, int64_t lda, const uint8_t* a_bs, int64_t l
     case 9: e = launch_f8_sk<3, 4, true, 128, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, mx); break;
     case 10: e = launch_f8_sk<4, 2, true, 128, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, mx); break;
     case 11: e = launch_f8_sk<4, 4, true, 128, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, mx); break;
+    case 15:
+      e = launch_f8_sk<4, 4, true, 128, true, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, mx);
+      break;
     default: break;
   }
   if (e != hipErrorNotReady) return e;
-  if (v >= 9) v = v == 10 ? 4 : 2;    // no stream-K workspace (first call inside a graph capture)
+  if (v >= 9 && v <= 11) v = v == 10 ? 4 : 2;    // no stream-K workspace (first call inside a graph capture)
+  if (v == 15) v = 13;
   switch (v) {
+    case 12:
+      return launch_f8<3, 4, true, 128, true, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, 1, mx);
+    case 13:
+      return launch_f8<4, 4, true, 128, true, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, 1, mx);
     case 1: return launch_f8<2, 2, true, 128, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, 1, mx);
     case 3: return launch_f8<4, 4, true, 128, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, 1, mx);
     case 4: return launch_f8<4, 2, true, 128, true>(A, lda, nullptr, W, ldw, sw, C, ldc, M, N, K, ep, stream, 1, mx);

@@ -348,7 +348,7 @@ void gemm_f8(const at::Tensor& a8, const at::Tensor& sa, const at::Tensor& w8, c
   check_f8_rows(w8, "gemm_f8: w8");
   const int64_t M = a8.size(0), K = a8.size(1), N = w8.size(0);
   TORCH_CHECK(w8.size(1) == K && K % 128 == 0 && N % 16 == 0, "gemm_f8: K % 128 == 0, N % 16 == 0");
-  TORCH_CHECK(variant >= 0 && variant <= 11, "gemm_f8: variant 0..11");
+  TORCH_CHECK(variant >= 0 && variant <= 15, "gemm_f8: variant 0..15");
   TORCH_CHECK(sa.is_cuda() && sa.scalar_type() == at::kFloat && sa.numel() >= M && sa.is_contiguous(),
               "gemm_f8: sa f32 [M]");
   TORCH_CHECK(sw.is_cuda() && sw.scalar_type() == at::kFloat && sw.numel() == N && sw.is_contiguous(),
@@ -407,7 +407,8 @@ void gemm_mx(const at::Tensor& a8, const at::Tensor& a_bs, const at::Tensor& w8,
   check_f8_rows(w8, "gemm_mx: w8");
   const int64_t M = a8.size(0), K = a8.size(1), N = w8.size(0);
   TORCH_CHECK(w8.size(1) == K && K % 128 == 0 && N % 128 == 0, "gemm_mx: K % 128 == 0, N % 128 == 0");
-  TORCH_CHECK(variant >= 0 && variant <= 11 && variant != 6 && variant != 7 && variant != 8, "gemm_mx: variant");
+  TORCH_CHECK(variant >= 0 && variant <= 15 && variant != 6 && variant != 7 && variant != 8 && variant != 14,
+              "gemm_mx: variant");
   const int64_t ld_bs = check_planes(a_bs, K / 128, M, "gemm_mx: a_bs");
   TORCH_CHECK(sw.is_cuda() && sw.scalar_type() == at::kFloat && sw.numel() == N && sw.is_contiguous(),
               "gemm_mx: sw f32 [N]");

@@ -157,7 +157,7 @@ def test_gemm_f8_splitk_vs_fp32_reference(M, N, K, glu):
     assert torch.equal(got, again)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("M,N,K,splits", [(624, 6144, 4096, 1), (624, 4096, 4096, 2), (300, 1536, 1024, 1),
                                           (97, 768, 2048, 4), (130, 1040, 1024, 1)])
 def test_gemm_f8_pipeline_variants(M, N, K, splits, variant):
@@ -173,7 +173,8 @@ def test_gemm_f8_pipeline_variants(M, N, K, splits, variant):
     assert _rel(got, ref) < 8e-3
 
 
-@pytest.mark.parametrize("tile", [20011, 20012, 20013, 20014, 20015, 20016, 20017, 20018, 20019, 20020, 20021])
+@pytest.mark.parametrize("tile", [20011, 20012, 20013, 20014, 20015, 20016, 20017, 20018, 20019, 20020, 20021,
+                                  20022, 20023, 20024, 20025])
 @pytest.mark.parametrize("M,N,K,act", [(577, 3072, 1024, None), (577, 1024, 4096, None), (200, 512, 640, "quick_gelu")])
 def test_gemm_bf16_pipeline_variants(M, N, K, act, tile):
     """bf16 operands on every LDS-DMA pipeline shape (tile codes 20010 + launch_variant code)."""

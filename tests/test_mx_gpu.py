@@ -44,7 +44,7 @@ def _operands(M, N, K, g):
     return x8, xs, w8, sw
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 9, 10, 11])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 9, 10, 11, 12, 13, 15])
 @pytest.mark.parametrize("M,N,K", [(130, 1024, 512), (624, 2048, 4096), (33, 256, 128)])
 def test_gemm_mx_plain_vs_reference(M, N, K, variant):
     """A scale bytes reach the MFMA per lane (k 32g .. 32g+31) -- wrong lanes or a wrong k order
@@ -193,9 +193,10 @@ def test_llm_prefill_mx_chain_matches_per_token_chain(T):
     g = torch.Generator(device=DEV).manual_seed(T)
     x = (torch.randn(T, 512, device=DEV, generator=g) * 0.5).bfloat16()
     m.prefill(x.clone())          # folds the norms (both chains then use the same weights)
-    assert m.norm_folded and m._mx_ok(x)
     old, old_min = L._PREFILL_MX, L._F8_MIN_ROWS
     try:
+        L._PREFILL_MX = True
+        assert m.norm_folded and m._mx_ok(x)
         L._F8_MIN_ROWS = 1 << 30          # fp8 weights, bf16 activations: the reference of both chains
         w8a16 = m.prefill(x.clone())
         L._F8_MIN_ROWS = old_min

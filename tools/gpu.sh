@@ -27,6 +27,7 @@
 #   mx             MX W8A8 chain tests (tests/test_mx_gpu.py) + fp8 GEMM + LLM-op tests
 #   ttft           VLM TTFT only (8B fp8, 30 requests, device JPEG decode)
 #   mx_cold        cold-weight timing of the MX chain's GEMMs (full / plain epilogues) vs per-token fp8
+#   pp_cold        ping-pong 128x128 pipeline forms vs the aligned ones (fp8 prefill + bf16 vision shapes)
 #   ttft_ab        TTFT with the fused MX prefill chain (LUMEN_PREFILL_MX=1) vs the per-token-scale chain
 #   pmc_gemm       PMC counters (MFMA, LDS conflicts, busy) of one ViT-L/14 GEMM shape
 set -o pipefail
@@ -129,6 +130,9 @@ for task in "$@"; do
       step mx_cold_full 300 python -u tools/cold_gemm_bench.py --what mx --epi full --variants=0,1,2,4,10
       step mx_cold_plain 300 python -u tools/cold_gemm_bench.py --what mx --epi plain --variants=0,2
       step f8_cold 300 python -u tools/cold_gemm_bench.py --what prefill --variants=0,2 ;;
+    pp_cold)   # ping-pong 128x128 forms (codes 12-15) vs the barrier-aligned ones, cold weights
+      step pp_cold_f8 300 python -u tools/cold_gemm_bench.py --what prefill --variants=1,2,12,13,14,15
+      step pp_cold_vit 300 python -u tools/cold_gemm_bench.py --what vit --variants=-1,20003,20022,20023,20024,20025 ;;
     ttft_ab)
       step ttft_mx 400 env LUMEN_PREFILL_MX=1 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0
       step ttft_pt 400 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0 ;;
