@@ -5,17 +5,11 @@
 // one CPU thread with Pillow (packages/lumen-vlm/src/lumen_vlm/backends/onnxrt_backend.py:661-665,
 // packages/lumen-face/src/lumen_face/backends/onnxrt_backend.py:716-723).
 #include "common.h"
+#include "jpeg.h"
 
 namespace lumen {
 
-struct JpegPlanes {
-  const int16_t* coef;   // all planes, [bh][bw][64] each, natural order, not dequantised
-  const uint16_t* qt;    // [ncomp][64]
-  uint8_t* samp;         // component sample planes [bh * 8][bw * 8] each
-  int64_t coef_off[3], samp_off[3];
-  int bw[3], bh[3], h[3], v[3];
-  int ncomp, hmax, vmax, width, height;
-};
+// JpegPlanes / JpegBatchEntry: jpeg.h
 
 // cos((2x + 1) u pi / 16) * C(u) / 2 with C(0) = 1/sqrt(2)
 __constant__ float kIdctCos[8][8] = {
@@ -28,32 +22,85 @@ __constant__ float kIdctCos[8][8] = {
     {0.19134172f, -0.46193977f, 0.46193977f, -0.19134172f, -0.19134172f, 0.46193977f, -0.46193977f, 0.19134172f},
     {0.09754516f, -0.27778512f, 0.41573481f, -0.49039264f, 0.49039264f, -0.41573481f, 0.27778512f, -0.09754516f}};
 
-// 4 blocks per 256-thread workgroup; thread = (block, row y, column x).  Separable: the row
-// pass (over u) goes through LDS, then the column pass (over v).
-__global__ void __launch_bounds__(256) jpeg_idct_kernel(JpegPlanes P, int64_t nblocks, int64_t b1, int64_t b2) {
-  __shared__ float sc[4][8][8];   // dequantised coefficients [block][v][u]
-  __shared__ float sr[4][8][8];   // after the horizontal pass [block][v][x]
-  const int lb = threadIdx.x >> 6, t = threadIdx.x & 63, y = t >> 3, x = t & 7;
-  const int64_t b = (int64_t)blockIdx.x * 4 + lb;
-  const bool live = b < nblocks;
-  const int c = b < b1 ? 0 : (b < b2 ? 1 : 2);
-  const int64_t lbk = b - (c == 0 ? 0 : (c == 1 ? b1 : b2));
-  if (live) sc[lb][y][x] = (float)P.coef[P.coef_off[c] + lbk * 64 + t] * (float)P.qt[c * 64 + t];
+// 8x8 IDCT of block lbk of component c (threads t = 0..63 of one 64-lane group: row y, column x).
+// Separable: the row pass (over u) goes through LDS, then the column pass (over v).
+__device__ __forceinline__ void idct_block(const JpegPlanes& P, int c, int64_t lbk, bool live, int t,
+                                           float (*sc)[8], float (*sr)[8]) {
+  const int y = t >> 3, x = t & 7;
+  if (live) sc[y][x] = (float)P.coef[P.coef_off[c] + lbk * 64 + t] * (float)P.qt[c * 64 + t];
   __syncthreads();
   if (live) {   // row pass: for row v = y, output column x
     float s = 0.f;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s += kIdctCos[u][x] * sc[lb][y][u];
-    sr[lb][y][x] = s;
+    for (int u = 0; u < 8; ++u) s += kIdctCos[u][x] * sc[y][u];
+    sr[y][x] = s;
   }
   __syncthreads();
   if (!live) return;
   float s = 0.f;   // column pass: pixel (x, y)
 #pragma unroll
-  for (int v = 0; v < 8; ++v) s += kIdctCos[v][y] * sr[lb][v][x];
+  for (int v = 0; v < 8; ++v) s += kIdctCos[v][y] * sr[v][x];
   const int val = min(255, max(0, (int)rintf(s + 128.f)));
   const int bx = (int)(lbk % P.bw[c]), by = (int)(lbk / P.bw[c]);
   P.samp[P.samp_off[c] + (int64_t)(by * 8 + y) * (P.bw[c] * 8) + bx * 8 + x] = (uint8_t)val;
+}
+
+__device__ __forceinline__ void block_comp(const JpegPlanes& P, int64_t b, int& c, int64_t& lbk) {
+  const int64_t n0 = (int64_t)P.bw[0] * P.bh[0], n1 = P.ncomp > 1 ? (int64_t)P.bw[1] * P.bh[1] : 0;
+  c = b < n0 ? 0 : (b < n0 + n1 ? 1 : 2);
+  lbk = b - (c == 0 ? 0 : (c == 1 ? n0 : n0 + n1));
+}
+
+__device__ __forceinline__ int64_t jpeg_blocks(const JpegPlanes& P) {
+  int64_t n = 0;
+  for (int c = 0; c < P.ncomp; ++c) n += (int64_t)P.bw[c] * P.bh[c];
+  return n;
+}
+
+// 4 blocks per 256-thread workgroup; thread = (block, row y, column x)
+__global__ void __launch_bounds__(256) jpeg_idct_kernel(JpegPlanes P, int64_t nblocks, int64_t b1, int64_t b2) {
+  __shared__ float sc[4][8][8];   // dequantised coefficients [block][v][u]
+  __shared__ float sr[4][8][8];   // after the horizontal pass [block][v][x]
+  const int lb = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + lb;
+  const bool live = b < nblocks;
+  int c;
+  int64_t lbk;
+  block_comp(P, live ? b : 0, c, lbk);
+  (void)b1;
+  (void)b2;
+  idct_block(P, c, lbk, live, t, sc[lb], sr[lb]);
+}
+
+// the entry owning global index i of a batch (entries sorted by start)
+template <bool PIX>
+__device__ __forceinline__ int batch_entry(const JpegBatchEntry* __restrict__ e, int n, int64_t i) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((PIX ? e[mid].pix0 : e[mid].blk0) <= i) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Batched form: one launch for every image of a batch (each image's block range padded to 4 so a
+// workgroup never straddles two images)
+__global__ void __launch_bounds__(256) jpeg_idct_batch_kernel(const JpegBatchEntry* __restrict__ entries, int n) {
+  __shared__ float sc[4][8][8];
+  __shared__ float sr[4][8][8];
+  __shared__ int img;
+  const int lb = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const int64_t b0 = (int64_t)blockIdx.x * 4;
+  if (threadIdx.x == 0) img = batch_entry<false>(entries, n, b0);
+  __syncthreads();
+  const JpegPlanes& P = entries[img].P;
+  const int64_t b = b0 - entries[img].blk0 + lb;
+  const bool live = b < jpeg_blocks(P);
+  int c;
+  int64_t lbk;
+  block_comp(P, live ? b : 0, c, lbk);
+  idct_block(P, c, lbk, live, t, sc[lb], sr[lb]);
 }
 
 // libjpeg's fancy upsampling of one chroma sample at output (X, Y) of the full-resolution grid:
@@ -76,8 +123,7 @@ __device__ __forceinline__ int chroma(const uint8_t* pl, int stride, int dw, int
   return (3 * cs + pl[(int64_t)Y * stride + max(c - 1, 0)] + 1) >> 2;
 }
 
-__global__ void __launch_bounds__(256) jpeg_color_kernel(JpegPlanes P, uint8_t* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void color_pixel(const JpegPlanes& P, int64_t i, uint8_t* __restrict__ out) {
   if (i >= (int64_t)P.width * P.height) return;
   const int X = (int)(i % P.width), Y = (int)(i / P.width);
   const int y = P.samp[P.samp_off[0] + (int64_t)Y * (P.bw[0] * 8) + X];
@@ -104,6 +150,20 @@ __global__ void __launch_bounds__(256) jpeg_color_kernel(JpegPlanes P, uint8_t* 
   o[2] = (uint8_t)min(255, max(0, b));
 }
 
+__global__ void __launch_bounds__(256) jpeg_color_kernel(JpegPlanes P, uint8_t* __restrict__ out) {
+  color_pixel(P, (int64_t)blockIdx.x * 256 + threadIdx.x, out);
+}
+
+// batched form (each image's pixel range padded to 256: one image per workgroup)
+__global__ void __launch_bounds__(256) jpeg_color_batch_kernel(const JpegBatchEntry* __restrict__ entries, int n) {
+  __shared__ int img;
+  const int64_t p0 = (int64_t)blockIdx.x * 256;
+  if (threadIdx.x == 0) img = batch_entry<true>(entries, n, p0);
+  __syncthreads();
+  const JpegBatchEntry& e = entries[img];
+  color_pixel(e.P, p0 - e.pix0 + threadIdx.x, e.out);
+}
+
 hipError_t jpeg_reconstruct(const JpegPlanes& P, uint8_t* out, hipStream_t stream) {
   if (P.ncomp != 1 && P.ncomp != 3) return hipErrorInvalidValue;
   int64_t nb[3] = {0, 0, 0};
@@ -112,6 +172,14 @@ hipError_t jpeg_reconstruct(const JpegPlanes& P, uint8_t* out, hipStream_t strea
   hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((total + 3) / 4)), dim3(256), 0, stream, P, total, b1, b2);
   const int64_t px = (int64_t)P.width * P.height;
   hipLaunchKernelGGL(jpeg_color_kernel, dim3((unsigned)((px + 255) / 256)), dim3(256), 0, stream, P, out);
+  return hipGetLastError();
+}
+
+hipError_t jpeg_reconstruct_batch(const JpegBatchEntry* entries, int n, int64_t total_blk, int64_t total_pix,
+                                  hipStream_t stream) {
+  if (n <= 0 || total_blk % 4 != 0 || total_pix % 256 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(jpeg_idct_batch_kernel, dim3((unsigned)(total_blk / 4)), dim3(256), 0, stream, entries, n);
+  hipLaunchKernelGGL(jpeg_color_batch_kernel, dim3((unsigned)(total_pix / 256)), dim3(256), 0, stream, entries, n);
   return hipGetLastError();
 }
 

@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <torch/library.h>
 
+#include <vector>
+
 #include "postproc.h"
 
 namespace lumen {
@@ -15,14 +17,8 @@ hipError_t db_components(const void* prob, int is_bf16, const float* thresh, int
 hipError_t db_quad_score(const void* prob, int is_bf16, int n, int H, int W, const float* quads, const int* img, float* score,
                          double* pre,
                          int m, hipStream_t stream);
-struct JpegPlanes {
-  const int16_t* coef; const uint16_t* qt; uint8_t* samp;
-  int64_t coef_off[3], samp_off[3];
-  int bw[3], bh[3], h[3], v[3];
-  int ncomp, hmax, vmax, width, height;
-};
-hipError_t jpeg_reconstruct(const JpegPlanes& P, uint8_t* out, hipStream_t stream);
 }  // namespace lumen
+#include "jpeg.h"
 
 namespace {
 
@@ -221,10 +217,69 @@ void jpeg_reconstruct(const at::Tensor& coef, const at::Tensor& qt, at::IntArray
   CHECK_HIP2(lumen::jpeg_reconstruct(P, out.data_ptr<uint8_t>(), stream()));
 }
 
+// Batched JPEG pixels: every image of a serving batch in one IDCT and one colour launch.
+// coef_all int16 / samp_all uint8: all images' planes back to back; qt_all int16 [n, 3, 64];
+// meta int64 CPU [n, 21] = (coef_base, samp_base, out_off, ncomp, hmax, vmax, width, height,
+// (h, v, bw, bh) x 3, qt_index); out_flat uint8 (each image [height, width, 3] at out_off);
+// entries: uint8 device scratch >= n * sizeof(JpegBatchEntry); entries_host: pinned uint8 CPU staging of
+// the same size, which the caller keeps (and does not rewrite) until this stream has passed the launch.
+void jpeg_reconstruct_batch(const at::Tensor& coef_all, const at::Tensor& qt_all, const at::Tensor& meta,
+                            at::Tensor samp_all, at::Tensor out_flat, at::Tensor entries, at::Tensor entries_host) {
+  TORCH_CHECK(coef_all.is_cuda() && coef_all.scalar_type() == at::kShort && coef_all.is_contiguous(), "jpeg: coef int16");
+  TORCH_CHECK(qt_all.is_cuda() && qt_all.scalar_type() == at::kShort && qt_all.is_contiguous(), "jpeg: qt int16");
+  TORCH_CHECK(samp_all.is_cuda() && samp_all.scalar_type() == at::kByte && samp_all.is_contiguous(), "jpeg: samp");
+  TORCH_CHECK(out_flat.is_cuda() && out_flat.scalar_type() == at::kByte && out_flat.is_contiguous(), "jpeg: out");
+  TORCH_CHECK(entries.is_cuda() && entries.scalar_type() == at::kByte && entries.is_contiguous(), "jpeg: entries");
+  TORCH_CHECK(!meta.is_cuda() && meta.scalar_type() == at::kLong && meta.dim() == 2 && meta.size(1) == 21 &&
+              meta.is_contiguous(), "jpeg: meta int64 CPU [n, 21]");
+  const int64_t n = meta.size(0);
+  TORCH_CHECK(n > 0 && entries.numel() >= n * (int64_t)sizeof(lumen::JpegBatchEntry), "jpeg: entries scratch");
+  TORCH_CHECK(!entries_host.is_cuda() && entries_host.is_pinned() && entries_host.scalar_type() == at::kByte &&
+              entries_host.is_contiguous() && entries_host.numel() >= n * (int64_t)sizeof(lumen::JpegBatchEntry),
+              "jpeg: entries_host pinned uint8 staging");
+  const int64_t* m = meta.data_ptr<int64_t>();
+  lumen::JpegBatchEntry* es = reinterpret_cast<lumen::JpegBatchEntry*>(entries_host.data_ptr());
+  int64_t blk = 0, pix = 0;
+  for (int64_t i = 0; i < n; ++i, m += 21) {
+    lumen::JpegBatchEntry& e = es[i];
+    lumen::JpegPlanes& P = e.P;
+    P = lumen::JpegPlanes{};
+    P.ncomp = (int)m[3]; P.hmax = (int)m[4]; P.vmax = (int)m[5]; P.width = (int)m[6]; P.height = (int)m[7];
+    TORCH_CHECK(P.ncomp == 1 || P.ncomp == 3, "jpeg: components");
+    int64_t co = 0;
+    for (int c = 0; c < P.ncomp; ++c) {
+      P.h[c] = (int)m[8 + 4 * c]; P.v[c] = (int)m[9 + 4 * c]; P.bw[c] = (int)m[10 + 4 * c]; P.bh[c] = (int)m[11 + 4 * c];
+      TORCH_CHECK(P.bw[c] * 8 >= (P.width * P.h[c] + P.hmax - 1) / P.hmax &&
+                  P.bh[c] * 8 >= (P.height * P.v[c] + P.vmax - 1) / P.vmax, "jpeg: plane smaller than the image");
+      P.coef_off[c] = m[0] + co;
+      P.samp_off[c] = m[1] + co;
+      co += (int64_t)P.bw[c] * P.bh[c] * 64;
+    }
+    TORCH_CHECK(m[0] + co <= coef_all.numel() && m[1] + co <= samp_all.numel() &&
+                m[2] + (int64_t)P.width * P.height * 3 <= out_flat.numel() && (m[20] + 1) * 192 <= qt_all.numel(),
+                "jpeg: image ", i, " exceeds the batch buffers");
+    P.coef = coef_all.data_ptr<int16_t>();
+    P.qt = reinterpret_cast<const uint16_t*>(qt_all.data_ptr<int16_t>()) + m[20] * 192;
+    P.samp = samp_all.data_ptr<uint8_t>();
+    e.out = out_flat.data_ptr<uint8_t>() + m[2];
+    e.blk0 = blk;
+    e.pix0 = pix;
+    blk += (co / 64 + 3) / 4 * 4;
+    pix += ((int64_t)P.width * P.height + 255) / 256 * 256;
+  }
+  const at::DeviceGuard g(coef_all.device());
+  CHECK_HIP2(hipMemcpyAsync(entries.data_ptr(), es, (size_t)n * sizeof(lumen::JpegBatchEntry), hipMemcpyHostToDevice,
+                            stream()));
+  CHECK_HIP2(lumen::jpeg_reconstruct_batch(reinterpret_cast<const lumen::JpegBatchEntry*>(entries.data_ptr()), (int)n,
+                                           blk, pix, stream()));
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(lumen, m) {
   m.def("jpeg_reconstruct(Tensor coef, Tensor qt, int[] meta, Tensor(s!) samp, Tensor(o!) out) -> ()");
+  m.def("jpeg_reconstruct_batch(Tensor coef_all, Tensor qt_all, Tensor meta, Tensor(s!) samp_all, Tensor(o!) out_flat, "
+        "Tensor(e!) entries, Tensor(h!) entries_host) -> ()");
   m.def("db_components(Tensor prob, Tensor thresh, Tensor(l!) lab, Tensor(o!) out, Tensor(c!) count, "
         "int min_size) -> ()");
   m.def("db_quad_score(Tensor prob, Tensor quads, Tensor img, Tensor(s!) score) -> ()");
@@ -242,6 +297,7 @@ TORCH_LIBRARY_FRAGMENT(lumen, m) {
 
 TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("jpeg_reconstruct", &jpeg_reconstruct);
+  m.impl("jpeg_reconstruct_batch", &jpeg_reconstruct_batch);
   m.impl("det_decode", &det_decode);
   m.impl("nms", &nms);
   m.impl("warp_batch", &warp_batch);

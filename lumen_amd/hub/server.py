@@ -192,7 +192,12 @@ def serve_frontends(config_path: str, port: int, frontends: int, mode: str = "hu
         specs[name] = spec
     devs = list(devices or engine_devices())
     log.info("starting %d GPU engine(s) on %s for %s", len(devs), devs, list(specs))
-    engines = EngineSet(specs, devs)
+    # batch loops per (engine, service): one runs its GPU work while the other assembles / decodes the
+    # next merged batch (LUMEN_ENGINE_THREADS); a popped batch lingers LUMEN_ENGINE_LINGER_US for more
+    # front-end batches -- with 3 loops and 1.5 ms the engine ran 320 batches/s of 6.5 images, every
+    # loop busy on per-batch overhead (profiles/r4_serve_fe_v1.txt)
+    engines = EngineSet(specs, devs, threads_per_service=int(os.environ.get("LUMEN_ENGINE_THREADS", "2")),
+                        linger_us=int(os.environ.get("LUMEN_ENGINE_LINGER_US", "5000")))
     ctx = mp.get_context("spawn")
     stop = ctx.Event()
     rq = ready_q if ready_q is not None else ctx.Queue()

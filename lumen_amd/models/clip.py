@@ -387,13 +387,15 @@ class VisionTower(nn.Module):
         x = x.view(B, S, W)
         return x[:, 1:] if drop_cls else x
 
-    def preprocess(self, images, mean, std, filter: str = "pil_bicubic", center_crop: bool = False) -> torch.Tensor:
+    def preprocess(self, images, mean, std, filter: str = "pil_bicubic", center_crop: bool = False,
+                   src: Optional[torch.Tensor] = None) -> torch.Tensor:
         """uint8 HWC images -> patch rows [B*P, kpad]: squash resize (the reference's ONNX
-        runtime) or shortest-side resize + centre crop (its torch / open_clip runtime)."""
+        runtime) or shortest-side resize + centre crop (its torch / open_clip runtime).  ``src``:
+        the images already uploaded back to back (``images`` then only carry the shapes)."""
         s = self.cfg.image_size
         return ops.image_prep(images, (s, s), mean=mean, std=std, filter=filter, layout="patches",
                               patch=self.cfg.patch_size, kpad=self.kpad, out_dtype=self.patch_w.dtype,
-                              device=self.patch_w.device, center_crop=center_crop)
+                              device=self.patch_w.device, center_crop=center_crop, src=src)
 
     def preprocess_nchw_to_patches(self, pix: torch.Tensor) -> torch.Tensor:
         """Already-normalised NCHW float pixels -> patch rows (used for parity tests)."""
@@ -559,15 +561,20 @@ class CLIPModel(nn.Module):
 
     # ---- public API (mirrors the reference backend contract: unit-norm fp32 vectors)
     @torch.no_grad()
-    def encode_image_uint8(self, images) -> torch.Tensor:
+    def encode_image_uint8(self, images, src: Optional[torch.Tensor] = None) -> torch.Tensor:
         """uint8 HWC images -> unit fp32 embeddings.  ``self.center_crop`` picks the
         preprocessor: False = squash resize (reference ONNX runtime, onnxrt_backend.py:410-431),
-        True = shortest side + centre crop (reference torch runtime, torch_backend.py:201-204)."""
+        True = shortest side + centre crop (reference torch runtime, torch_backend.py:201-204).
+        ``src``: the images already on the device, back to back in one flat uint8 tensor
+        (utils.jpeg.decode_batch_to_device); ``images`` then only give the (H, W) shapes."""
         crop = self.center_crop
+        if src is not None:
+            images = [torch.empty((h, w, 3), dtype=torch.uint8, device="meta") for h, w in images]
         if self.cfg.vision_arch == "fastvit":
+            assert src is None, "FastViT preprocessing takes host images"
             x = self.visual.preprocess(images, self.cfg.image_mean, self.cfg.image_std, center_crop=crop)
             return self.visual.forward_embed(x)
-        patches = self.visual.preprocess(images, self.cfg.image_mean, self.cfg.image_std, center_crop=crop)
+        patches = self.visual.preprocess(images, self.cfg.image_mean, self.cfg.image_std, center_crop=crop, src=src)
         B = patches.shape[0] // self.visual.num_patches
         return self.visual.forward_patches(patches, B)
 

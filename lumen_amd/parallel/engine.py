@@ -131,6 +131,9 @@ def current_remote() -> Optional[RemotePool]:
 
 
 # ============================================================================ engine side
+_stats_lock = threading.Lock()
+
+
 def _serve_channel(ch: ShmChannel, fn, stop: threading.Event, max_items: int, linger_us: int,
                    stats: dict) -> None:
     """Batch loop over one channel: pop queued front-end batches, merge by kind, run, complete."""
@@ -157,8 +160,13 @@ def _serve_channel(ch: ShmChannel, fn, stop: threading.Event, max_items: int, li
             flat = [it for _, items in reqs for it in items]
             try:
                 res: list = []
+                t0 = time.perf_counter()
                 for i in range(0, len(flat), max_items):
                     res.extend(fn(kind, flat[i:i + max_items]))
+                with _stats_lock:
+                    stats["fn_s"] = stats.get("fn_s", 0.0) + time.perf_counter() - t0
+                    stats["batches"] = stats.get("batches", 0) + 1
+                    stats["batch_items"] = stats.get("batch_items", 0) + len(flat)
                 if len(res) != len(flat):
                     raise RuntimeError(f"engine fn returned {len(res)} results for {len(flat)} items")
             except Exception:  # noqa: BLE001 - the whole merged batch failed
@@ -220,10 +228,24 @@ def engine_main(services: dict, device: str, ready_q, stop_ev, max_items: int = 
             ths.append(t)
     ready_q.put(("ready", device, os.getpid()))
     # stop_ev: a shared byte, polled (an mp.Event's set() blocks on a waiter that died in its wait)
+    every = float(os.environ.get("LUMEN_ENGINE_STATS_S", "0") or 0)    # periodic load log (serving benches)
+    t_log, last = time.perf_counter(), {}
     while not stop_ev.value:
         for ch in chans.values():
             ch.heartbeat()
         time.sleep(0.25)
+        if every > 0 and time.perf_counter() - t_log >= every:
+            now = time.perf_counter()
+            with _stats_lock:
+                cur = dict(stats)
+            dt = now - t_log
+            db = cur.get("batches", 0) - last.get("batches", 0)
+            di = cur.get("batch_items", 0) - last.get("batch_items", 0)
+            busy = (cur.get("fn_s", 0.0) - last.get("fn_s", 0.0)) / dt
+            log.warning("engine %s: %.0f items/s, %.1f batches/s, %.1f items/batch, batch-fn busy %.2f "
+                        "(loops x fraction), shared batches %d", device, di / dt, db / dt, di / max(db, 1), busy,
+                        cur.get("shared_batches", 0))
+            t_log, last = now, cur
     stop.set()
     for t in ths:
         t.join(timeout=5)

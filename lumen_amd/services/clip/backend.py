@@ -247,6 +247,16 @@ class MI355XClipBackend:
             raise InvalidInputError("empty image payload")
         if self._pool is not None and not self.remote:  # DP workers decode in their own processes
             return self._img_batcher(image_bytes)
+        if self.remote:
+            # serving front end: a baseline JPEG travels as bytes and the engine decodes the whole
+            # merged batch on the GPU (utils.jpeg.decode_batch_to_device); anything else decodes here
+            from ...utils.jpeg import info as jpeg_info
+
+            if jpeg_info(image_bytes) is not None:
+                v = self._img_batcher(bytes(image_bytes))
+                if v is None:
+                    raise InvalidInputError("Failed to decode image")
+                return v
         # decoded on the caller's (gRPC) thread: Pillow releases the GIL, so concurrent requests decode
         # in parallel and the batch's critical path is only the GPU work; a bad payload fails alone
         with stage("decode"):
@@ -341,6 +351,18 @@ def dp_worker(device: str, cache_dir: str, model: str, runtime: str, dataset: Op
             # one answer per item: the engine may merge several front ends' info calls in a batch
             return [{"logit_scale": float(m.logit_scale), "embed_dim": int(cfg.embed_dim)}] * len(items)
         if kind == "image":
+            if dev.type == "cuda" and cfg.vision_arch != "fastvit" and items and \
+                    all(isinstance(it, (bytes, bytearray)) for it in items):
+                # encoded payloads (a serving front end or a DP caller): the whole batch decodes on the
+                # device -- parallel host entropy decode, one IDCT + colour launch -- and the patch
+                # preprocessing reads the decoded pixels in place; an undecodable payload answers None
+                from ...utils.jpeg import decode_batch_to_device
+
+                flat, _offs, shapes, errs = decode_batch_to_device(list(items), dev)
+                out = list(m.encode_image_uint8(shapes, src=flat).float().cpu().numpy())
+                for k in errs:
+                    out[k] = None
+                return out
             # encoded images (DP workers decode here) or uint8 HWC arrays (decoded by a serving front end)
             raw = [k for k, it in enumerate(items) if not isinstance(it, np.ndarray)]
             imgs = list(items)

@@ -213,6 +213,140 @@ def decode_to_device(data: bytes, device, threads: Optional[int] = None, stats: 
     return torch.from_numpy(decode_rgb(data)).to(dev)
 
 
+# ------------------------------------------------------------------ batched device decode (serving engines)
+_ENTRY_BYTES = 256            # >= sizeof(JpegBatchEntry) (168 on gfx950 builds)
+_pool_lock = threading.Lock()
+_decode_pool = None
+
+
+def _pool():
+    global _decode_pool
+    with _pool_lock:
+        if _decode_pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+
+            _decode_pool = ThreadPoolExecutor(max_workers=default_threads(), thread_name_prefix="jpeg-batch")
+        return _decode_pool
+
+
+class _BatchStaging(threading.local):
+    bufs = None       # pinned (coef int16, qt int16, entries uint8, raw uint8)
+    ev = None         # the H2D copies that last read them
+
+
+_bstage = _BatchStaging()
+
+
+def _pinned(t, n: int, dtype):
+    import torch
+
+    if t is None or t.numel() < n:
+        t = torch.empty(max(n, 1 << 16), dtype=dtype).pin_memory()
+    return t
+
+
+def decode_batch_to_device(datas, device):
+    """Encoded images -> one flat uint8 device tensor holding every image as [H, W, 3] back to
+    back, for ``ops.image_prep(src=...)``: returns (flat, offsets, shapes, errors).
+
+    Baseline JPEGs: entropy-decoded on the decode pool (one image per thread, the ctypes call
+    releases the GIL) into one pinned coefficient buffer, one H2D copy, then ONE batched IDCT and
+    ONE colour launch for the whole batch (csrc/jpeg.hip).  Anything else (PNG, progressive, a
+    payload the fast decoder rejects) decodes with Pillow on the same pool and is copied into its
+    slot.  ``errors`` maps the index of an undecodable payload to its exception (its slot is a
+    1 x 1 black image so the batch stays aligned)."""
+    import torch
+
+    from .image import decode_rgb
+
+    dev = torch.device(device)
+    n = len(datas)
+    infos = [info(d) for d in datas]
+    jidx = [i for i, ji in enumerate(infos) if ji is not None]
+    cbase, tot = {}, 0
+    for i in jidx:
+        cbase[i] = tot
+        tot += infos[i].coef_count
+    st = _bstage
+    if st.ev is not None:
+        st.ev.synchronize()          # this thread's previous batch has been copied out of the staging
+    coef_h, qt_h, ent_h, raw_h = st.bufs or (None, None, None, None)
+    coef_h = _pinned(coef_h, tot, torch.int16)
+    qt_h = _pinned(qt_h, max(1, len(jidx)) * 192, torch.int16)
+    ent_h = _pinned(ent_h, max(1, len(jidx)) * _ENTRY_BYTES, torch.uint8)
+    coef_np, qt_np = coef_h.numpy(), qt_h.numpy()
+
+    def ent(k_i):
+        k, i = k_i
+        ji = infos[i]
+        res = decode_coefs(datas[i], 1, ji, out=coef_np[cbase[i]:cbase[i] + ji.coef_count])
+        if res is None:
+            return None
+        q = res[1]
+        qt_np[k * 192:k * 192 + q.size] = q.reshape(-1).view(np.int16)
+        return True
+
+    ok = list(_pool().map(ent, list(enumerate(jidx)))) if jidx else []
+    good = [i for i, r in zip(jidx, ok) if r]
+    good_set = set(good)
+    slow = [i for i in range(n) if i not in good_set]
+
+    def pil(i):
+        try:
+            return decode_rgb(datas[i])
+        except Exception as e:    # noqa: BLE001 -- reported per item
+            return e
+
+    pix = dict(zip(slow, _pool().map(pil, slow))) if slow else {}
+    errors = {i: p for i, p in pix.items() if isinstance(p, BaseException)}
+    shapes, offs, off = [], [], 0
+    for i in range(n):
+        if i in errors:
+            h, w = 1, 1
+        elif i in pix:
+            h, w = pix[i].shape[:2]
+        else:
+            h, w = infos[i].height, infos[i].width
+        shapes.append((h, w))
+        offs.append(off)
+        off += h * w * 3
+    out = torch.zeros(max(off, 1), dtype=torch.uint8, device=dev) if errors else \
+        torch.empty(max(off, 1), dtype=torch.uint8, device=dev)
+    raw_n = sum(p.size for i, p in pix.items() if i not in errors)
+    raw_h = _pinned(raw_h, raw_n, torch.uint8)
+    if raw_n:
+        rnp, r = raw_h.numpy(), 0
+        for i, p in pix.items():
+            if i in errors:
+                continue
+            rnp[r:r + p.size] = np.ascontiguousarray(p).reshape(-1)
+            out[offs[i]:offs[i] + p.size].copy_(raw_h[r:r + p.size], non_blocking=True)
+            r += p.size
+    if good:
+        from ..ops import hip_ops
+
+        meta = np.zeros((len(good), 21), np.int64)
+        sbase = 0
+        for k, i in enumerate(good):
+            ji = infos[i]
+            row = [cbase[i], sbase, offs[i], ji.ncomp, ji.hmax, ji.vmax, ji.width, ji.height]
+            for c in range(3):
+                row += list(ji.comps[c][:2]) + list(ji.comps[c][2:4]) if c < ji.ncomp else [0, 0, 0, 0]
+            row.append(jidx.index(i))
+            meta[k] = row
+            sbase += ji.coef_count
+        coef_d = coef_h[:tot].to(dev, non_blocking=True)
+        qt_d = qt_h[:len(jidx) * 192].to(dev, non_blocking=True)
+        samp = torch.empty(max(sbase, 1), dtype=torch.uint8, device=dev)
+        ent_d = torch.empty(len(good) * _ENTRY_BYTES, dtype=torch.uint8, device=dev)
+        hip_ops().jpeg_reconstruct_batch(coef_d, qt_d, torch.from_numpy(meta), samp, out, ent_d, ent_h)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    st.ev = ev
+    st.bufs = (coef_h, qt_h, ent_h, raw_h)
+    return out, offs, shapes, errors
+
+
 def decode_image(data: bytes, device, draft_to: Optional[tuple] = None, stats: Optional[dict] = None):
     """Request image -> uint8 [H, W, 3] torch tensor: on a GPU device a baseline JPEG takes
     :func:`decode_to_device` (full resolution, no DCT-domain shortcut needed: the entropy decode

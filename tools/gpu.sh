@@ -23,6 +23,7 @@
 #   pmc_face / pmc_ocr   PMC counters (SQ pass + memory pass) of the face / OCR pipelines
 #   serve          tools/serve_bench.py: gRPC hub end to end (CLIP ViT-L/14 64 clients, face 32 clients)
 #   serve_fe       serving through the engine / front-end topology (CLIP 128 clients, face 64; $SERVE_FE front ends)
+#   serve_sweep    CLIP serving through the engine / front ends: 8 / 12 front ends x 128 / 256 clients
 #   jpeg           device JPEG tests + tools/jpeg_bench.py
 #   mx             MX W8A8 chain tests (tests/test_mx_gpu.py) + fp8 GEMM + LLM-op tests
 #   ttft           VLM TTFT only (8B fp8, 30 requests, device JPEG decode)
@@ -116,9 +117,19 @@ for task in "$@"; do
         --seconds 20 ;;
     serve_fe)
       step serve_clip_fe 400 python -u tools/serve_bench.py --service clip --model CLIP-ViT-L-14 --device cuda \
-        --clients "${SERVE_CLIENTS:-128}" --frontends "${SERVE_FE:-6}" --seconds 20
+        --clients "${SERVE_CLIENTS:-256}" --frontends "${SERVE_FE:-10}" --client-procs 12 --seconds 20
       step serve_face_fe 400 python -u tools/serve_bench.py --service face --model antelopev2 --device cuda \
-        --clients "${SERVE_FACE_CLIENTS:-64}" --frontends "${SERVE_FE:-6}" --seconds 20 ;;
+        --clients "${SERVE_FACE_CLIENTS:-128}" --frontends "${SERVE_FE:-10}" --client-procs 12 --seconds 20 ;;
+    serve_sweep)   # CLIP serving through front ends: front-end count x client count
+      for fe in 8 12; do for cl in 128 256; do
+        step serve_clip_fe${fe}_c${cl} 300 python -u tools/serve_bench.py --service clip --model CLIP-ViT-L-14 \
+          --device cuda --clients $cl --frontends $fe --client-procs 6 --seconds 15
+      done; done ;;
+    serve_linger)   # engine merge window sweep (CLIP, 8 front ends, 256 clients)
+      for lg in 2000 5000 10000; do
+        step serve_clip_lg${lg} 300 env LUMEN_ENGINE_STATS_S=4 LUMEN_ENGINE_LINGER_US=$lg python -u tools/serve_bench.py \
+          --service clip --model CLIP-ViT-L-14 --device cuda --clients 256 --frontends 8 --client-procs 6 --seconds 15
+      done ;;
     jpeg)
       step jpeg_tests 200 python -u -m pytest tests/test_jpeg_gpu.py tests/test_jpeg_cpu.py -x -q --timeout 120 \
         --timeout-method thread
