@@ -1006,7 +1006,9 @@ hipError_t gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
     // 16 register-staged 32x64 tiles): the LDS-DMA pipeline with K split over gridDim.y streams W once
     else if (M <= 64 && !(lds_ok && K >= 4096)) tile = 3;
     else if (M <= 64) tile = 20000;
-    else if (t128 >= 144 && lds_ok) tile = 20005;
+    // (r4, cold weights: 577 x 4096 x 1024 + quick_gelu 17.5 us as <4 stages, 8 waves> vs 21.9 us as
+    // <2, 8>, profiles/r4_cold_vit_gemm_variants_v1.txt)
+    else if (t128 >= 144 && lds_ok) tile = 20003;
     // fewer 128x128 tiles (VLM vision tower at 577 tokens: 40-120): the same pipeline with K split
     // over gridDim.y + one reduce/epilogue pass (gemm_f8.hip f8_pick_splits) instead of 64x64 tiles
     else if (lds_ok && M >= 128 && K >= 4096) tile = 20000;

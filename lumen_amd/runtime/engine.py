@@ -149,10 +149,12 @@ class Sampler:
 class TPSync:
     """Step broadcast from rank 0 to the follower ranks of a TP group.
 
-    Every step is ONE broadcast of a fixed-capacity int32 buffer: an 8-int header (op, batch,
-    table width, top-k, graph flag) followed, for decode steps, by the step descriptor -- ids,
-    positions, cache slots, context lengths, block table -- so a follower pays one collective
-    and one small D2H per token (the header decides which graph to replay; nothing is pickled).
+    Every step is ONE broadcast of a 4 KiB prefix of an int32 buffer: an 8-int header (op, batch,
+    table width, top-k, graph flag, message length) followed, for decode steps, by the step
+    descriptor -- ids, positions, cache slots, context lengths, block table -- so a follower pays
+    one collective and one small D2H per token (the header decides which graph to replay; nothing
+    is pickled).  A descriptor longer than the prefix (big batches x long block tables) sends its
+    remainder in a second broadcast sized from the header; the full capacity never travels.
     Prefill / control messages and decode steps whose sampling needs per-row state
     (temperatures, repetition-penalty token sets) add an object broadcast after the header.
     The buffer lives on the device the group's backend moves (GPU for RCCL, host for gloo).
@@ -172,7 +174,8 @@ class TPSync:
         self.device = device
         self.capacity = int(capacity)
         self.buf = torch.zeros(8 + self.capacity, dtype=torch.int32, device=device)
-        self.stats = {"tensor_steps": 0, "object_steps": 0}
+        self.prefix = min(1024, 8 + self.capacity)          # ints per step's first broadcast
+        self.stats = {"tensor_steps": 0, "object_steps": 0, "two_part_steps": 0}
 
     def _bcast(self, t: torch.Tensor) -> None:
         import torch.distributed as dist
@@ -184,7 +187,7 @@ class TPSync:
 
         self.buf[:8].fill_(0)
         self.buf[0] = self.OBJ
-        self._bcast(self.buf)
+        self._bcast(self.buf[:self.prefix])
         obj = [msg]
         dist.broadcast_object_list(obj, src=self.src, group=self.group)
         self.stats["object_steps"] += 1
@@ -194,26 +197,33 @@ class TPSync:
         if spec["inv"] is not None or spec["pen"] is not None or 4 * B + B * W > self.capacity:
             self.send(("decode", ids, pos, slots, bt, ctx, spec, graph))
             return
-        msg = np.zeros(8 + 4 * B + B * W, np.int32)
-        msg[:8] = [self.DECODE, B, W, spec["k"], int(graph), 0, 0, 0]
+        n = 8 + 4 * B + B * W
+        msg = np.zeros(n, np.int32)
+        msg[:8] = [self.DECODE, B, W, spec["k"], int(graph), n, 0, 0]
         msg[8:] = np.concatenate([np.asarray(ids, np.int64).astype(np.int32), np.asarray(pos, np.int32),
                                   np.asarray(slots, np.int64).astype(np.int32), np.asarray(ctx, np.int32),
                                   np.asarray(bt, np.int32).reshape(-1)])
-        self.buf[:len(msg)].copy_(torch.from_numpy(msg), non_blocking=self.device.type == "cuda")
-        self._bcast(self.buf)
+        self.buf[:n].copy_(torch.from_numpy(msg), non_blocking=self.device.type == "cuda")
+        self._bcast(self.buf[:self.prefix])
+        if n > self.prefix:
+            self._bcast(self.buf[self.prefix:n])
+            self.stats["two_part_steps"] += 1
         self.stats["tensor_steps"] += 1
 
     def recv(self):
         import torch.distributed as dist
 
-        self._bcast(self.buf)
-        p = self.buf.cpu().numpy()
+        self._bcast(self.buf[:self.prefix])
+        p = self.buf[:self.prefix].cpu().numpy()
         h = p[:8].tolist()
         if h[0] == self.OBJ:
             obj = [None]
             dist.broadcast_object_list(obj, src=self.src, group=self.group)
             return obj[0]
-        B, W, k, graph = h[1], h[2], h[3], bool(h[4])
+        B, W, k, graph, n = h[1], h[2], h[3], bool(h[4]), h[5]
+        if n > self.prefix:
+            self._bcast(self.buf[self.prefix:n])
+            p = self.buf[:n].cpu().numpy()
         p = p[8:8 + 4 * B + B * W]
         ids = p[:B].astype(np.int64)
         pos = p[B:2 * B].copy()
