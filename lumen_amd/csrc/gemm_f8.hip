@@ -399,11 +399,28 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
           }
           continue;
         }
-        if (valid) epi_store16_t<false>(v, m, n, M, N, C, ldc, ep, crs);   // v -> the stored values (fp32)
+        if (valid && !mx.skip_c) {
+          epi_store16_t<false>(v, m, n, M, N, C, ldc, ep, crs);   // v -> the stored values (fp32)
+        } else if (valid) {      // MX output only: the same transforms, no bf16 store
+          if (ep.row_aff) {
+            const float ra = ep.row_aff[2 * (int64_t)m], rb = ep.row_aff[2 * (int64_t)m + 1];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = v[q] * ra + rb * ep.col_aff[n + q] + ep.col_aff[N + n + q];
+          }
+#pragma unroll
+          for (int q = 0; q < 16; ++q) v[q] *= ep.alpha;
+          if (ep.bias) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+              v[q] += ep.bias_f32 ? ((const float*)ep.bias)[n + q] : bf2f(((const uint16_t*)ep.bias)[n + q]);
+          }
+          if (ep.act) apply_act_n<16>(v, ep.act);
+        }
         float f[16], am = 0.f, ss = 0.f;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          f[q] = valid ? bf2f(f2bf(v[q])) : 0.f;     // what the residual stream now holds
+          // what the bf16 output now holds (the fp32 value when only the MX copy is written)
+          f[q] = valid ? (mx.skip_c ? v[q] : bf2f(f2bf(v[q]))) : 0.f;
           am = fmaxf(am, fabsf(f[q]));
           ss += f[q] * f[q];
         }
@@ -761,8 +778,8 @@ hipError_t gemm_mx(const uint8_t* A, int64_t lda, const uint8_t* a_bs, int64_t l
   if (K % 128 != 0 || N % 16 != 0 || M <= 0 || lda % 16 != 0 || ldw % 16 != 0 || ld_bs < 4 * (int64_t)M ||
       ld_bs % 4 != 0)
     return hipErrorInvalidValue;
-  if (ep.split_koff || ep.out_group || ep.table || ep.prelu || ep.post_act || ep.row_aff) return hipErrorInvalidValue;
-  if (mx.skip_c && !(ep.glu && mx.q8)) return hipErrorInvalidValue;
+  if (ep.split_koff || ep.out_group || ep.table || ep.prelu || ep.post_act) return hipErrorInvalidValue;
+  if (mx.skip_c && !mx.q8) return hipErrorInvalidValue;
   mx.a_bs = a_bs;
   mx.ld_bs = ld_bs;
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);

@@ -26,6 +26,7 @@
 #include <cstdint>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -326,9 +327,7 @@ inline bool decode_block(const uint8_t* p, size_t& pos, const Huff& dc, const Hu
 // ---------------------------------------------------------------------------- thread pool
 class Pool {
  public:
-  explicit Pool(int n) {
-    for (int i = 0; i < n; ++i) th_.emplace_back([this] { run(); });
-  }
+  explicit Pool(int n) { grow(n); }
   ~Pool() {
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -337,35 +336,51 @@ class Pool {
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
-  int size() const { return (int)th_.size(); }
+  int size() {
+    std::lock_guard<std::mutex> g(mu_);
+    return (int)th_.size();
+  }
+  // more worker threads (never fewer: another request may be inside parallel_for)
+  void grow(int n) {
+    std::lock_guard<std::mutex> g(mu_);
+    while ((int)th_.size() < n) th_.emplace_back([this] { run(); });
+  }
   // f(i) for i in [0, n), the calling thread helping; returns when all are done.  Concurrent
-  // callers (several request threads) take turns.
+  // callers (several request threads) take turns.  The job state is shared-owned: a worker that
+  // picked the job up late finds every index taken and leaves without touching f or this frame.
   void parallel_for(int n, const std::function<void(int)>& f) {
     std::lock_guard<std::mutex> turn(run_mu_);
-    std::atomic<int> next{0}, done{0};
-    auto work = [&] {
-      for (int i; (i = next.fetch_add(1)) < n;) {
-        f(i);
-        done.fetch_add(1);
-      }
-    };
+    auto job = std::make_shared<Job>();
+    job->n = n;
+    job->f = &f;
     {
       std::lock_guard<std::mutex> g(mu_);
-      job_ = work;
+      job_ = job;
       ++gen_;
     }
     cv_.notify_all();
-    work();
-    while (done.load() < n) std::this_thread::yield();
+    work(*job);
+    while (job->done.load() < n) std::this_thread::yield();
     std::lock_guard<std::mutex> g(mu_);
-    job_ = nullptr;
+    job_.reset();
   }
 
  private:
+  struct Job {
+    std::atomic<int> next{0}, done{0};
+    int n = 0;
+    const std::function<void(int)>* f = nullptr;
+  };
+  static void work(Job& j) {
+    for (int i; (i = j.next.fetch_add(1)) < j.n;) {
+      (*j.f)(i);
+      j.done.fetch_add(1);
+    }
+  }
   void run() {
     uint64_t seen = 0;
     for (;;) {
-      std::function<void()> job;
+      std::shared_ptr<Job> job;
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return stop_ || (gen_ != seen && job_); });
@@ -373,14 +388,14 @@ class Pool {
         seen = gen_;
         job = job_;
       }
-      job();
+      work(*job);
     }
   }
   std::vector<std::thread> th_;
   std::mutex run_mu_;
   std::mutex mu_;
   std::condition_variable cv_;
-  std::function<void()> job_;
+  std::shared_ptr<Job> job_;
   uint64_t gen_ = 0;
   bool stop_ = false;
 };
@@ -388,11 +403,11 @@ class Pool {
 std::mutex g_pool_mu;
 Pool* g_pool = nullptr;
 
-// created once, with the first caller's thread count (never resized: a resize would tear
-// down threads another request may be using)
+// created with the first caller's thread count and grown when a later caller wants more
 Pool& pool(int want) {
   std::lock_guard<std::mutex> g(g_pool_mu);
   if (g_pool == nullptr) g_pool = new Pool(std::max(0, want - 1));
+  else g_pool->grow(want - 1);
   return *g_pool;
 }
 

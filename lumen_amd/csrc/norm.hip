@@ -222,13 +222,16 @@ hipError_t norm_rows(const uint16_t* x, int64_t x_stride, const int64_t* row_idx
 // LayerNorm statistics only, for a projection with the norm folded in (GemmEpi::row_aff):
 // out[row] = (rstd, -mean * rstd).  Same fp32 two-pass arithmetic as norm_rows_kernel mode 0, but
 // 8 bytes per row are written instead of the normalised row.  One wave per row, D <= 64 * 8 * CPL.
+// With q8 (MX form, the W8A8 vision tower): the raw row also leaves as MX fp8 -- 32-column blocks
+// of 4 lanes, E8M0 bytes in K-step planes [D/128][rows][4] (ldqs = plane stride) -- the A operand of
+// the LN-folded gemm_mx that consumes it.
 template <int CPL>
 __global__ void __launch_bounds__(256)
 ln_row_stats_kernel(const uint16_t* __restrict__ x, int64_t x_stride, float* __restrict__ out, int rows, int D,
-                    float eps) {
+                    float eps, uint8_t* __restrict__ q8, int64_t ldq, uint8_t* __restrict__ qs, int64_t ldqs) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  if (row >= rows) return;      // whole waves: the MX shuffles below stay inside a live wave
   const uint16_t* xr = x + (int64_t)row * x_stride;
   const int nch = D >> 3;
   float v[CPL][8];
@@ -259,16 +262,35 @@ ln_row_stats_kernel(const uint16_t* __restrict__ x, int64_t x_stride, float* __r
   }
   const float rstd = rsqrtf(wave_sum(ss) / (float)D + eps);
   if (lane == 0) *(float2*)(out + 2 * (int64_t)row) = make_float2(rstd, -mean * rstd);
+  if (q8 != nullptr) {
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int ch = lane + c * 64;
+      float am = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(v[c][i]));
+      am = fmaxf(am, __shfl_xor(am, 1, 64));
+      am = fmaxf(am, __shfl_xor(am, 2, 64));
+      if (ch < nch) {
+        const int e = mx_exp(am);
+        *(uint2*)(q8 + (int64_t)row * ldq + ch * 8) = fp8x8_scaled(v[c], mx_inv(e));
+        if ((lane & 3) == 0) qs[(int64_t)(ch >> 4) * ldqs + (int64_t)row * 4 + ((ch >> 2) & 3)] = (uint8_t)(e + 127);
+      }
+    }
+  }
 }
 
 hipError_t ln_row_stats(const uint16_t* x, int64_t x_stride, float* out, int rows, int D, float eps,
-                        hipStream_t stream) {
-  if (D % 8 != 0 || D > 64 * 8 * 8 || rows <= 0) return hipErrorInvalidValue;
+                        hipStream_t stream, uint8_t* q8, int64_t ldq, uint8_t* qs, int64_t ldqs) {
+  if (D % 8 != 0 || D > 64 * 8 * 8 || rows <= 0 || (q8 != nullptr && D % 128 != 0)) return hipErrorInvalidValue;
   const dim3 grid((rows + 3) / 4);
-  if (D <= 512) hipLaunchKernelGGL(ln_row_stats_kernel<1>, grid, dim3(256), 0, stream, x, x_stride, out, rows, D, eps);
-  else if (D <= 1024) hipLaunchKernelGGL(ln_row_stats_kernel<2>, grid, dim3(256), 0, stream, x, x_stride, out, rows, D, eps);
-  else if (D <= 2048) hipLaunchKernelGGL(ln_row_stats_kernel<4>, grid, dim3(256), 0, stream, x, x_stride, out, rows, D, eps);
-  else hipLaunchKernelGGL(ln_row_stats_kernel<8>, grid, dim3(256), 0, stream, x, x_stride, out, rows, D, eps);
+#define LUMEN_LNS(C) \
+  hipLaunchKernelGGL(ln_row_stats_kernel<C>, grid, dim3(256), 0, stream, x, x_stride, out, rows, D, eps, q8, ldq, qs, ldqs)
+  if (D <= 512) LUMEN_LNS(1);
+  else if (D <= 1024) LUMEN_LNS(2);
+  else if (D <= 2048) LUMEN_LNS(4);
+  else LUMEN_LNS(8);
+#undef LUMEN_LNS
   return hipGetLastError();
 }
 

@@ -48,7 +48,8 @@ hipError_t norm_rows(const uint16_t* x, int64_t x_stride, const int64_t* row_idx
                      float eps, int mode, hipStream_t stream);
 hipError_t l2norm_f32(float* x, int rows, int D, float eps, hipStream_t stream);
 hipError_t ln_row_stats(const uint16_t* x, int64_t x_stride, float* out, int rows, int D, float eps,
-                        hipStream_t stream);
+                        hipStream_t stream, uint8_t* q8 = nullptr, int64_t ldq = 0, uint8_t* qs = nullptr,
+                        int64_t ldqs = 0);
 hipError_t cls_fill(uint16_t* x, int64_t seq_stride, const uint16_t* cls, const uint16_t* pos, int B, int D,
                     hipStream_t stream);
 hipError_t embed_gather(const int64_t* ids, const uint16_t* table, const uint16_t* pos, int S, uint16_t* out,
@@ -204,13 +205,31 @@ void gemm_lnf(const at::Tensor& a, const at::Tensor& w, const at::Tensor& col_af
                                    (int)M, (int)N, (int)K, ep, (int)tile, cur_stream()));
 }
 
-void ln_row_stats(const at::Tensor& x, at::Tensor out, double eps) {
+static int64_t check_planes(const at::Tensor& t, int64_t planes, int64_t M, const char* name);
+static void check_f8_rows(const at::Tensor& t, const char* name);
+
+// q8 / qs (optional): the raw rows as MX fp8 + E8M0 planes (the LN-folded gemm_mx operand)
+void ln_row_stats(const at::Tensor& x, at::Tensor out, double eps, const c10::optional<at::Tensor>& q8,
+                  const c10::optional<at::Tensor>& qs) {
   check_bf16_rows(x, "x");
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() >= 2 * x.size(0),
               "ln_row_stats: out must be fp32 [rows, 2]");
+  uint8_t* qp = nullptr;
+  uint8_t* sp = nullptr;
+  int64_t ldq = 0, ldqs = 0;
+  if (q8.has_value() && q8->defined()) {
+    const int64_t M = x.size(0), D = x.size(1);
+    check_f8_rows(*q8, "ln_row_stats: q8");
+    TORCH_CHECK(q8->size(0) >= M && q8->size(1) == D && D % 128 == 0 && qs.has_value() && qs->defined(),
+                "ln_row_stats: q8 [rows, D] (D % 128 == 0) needs qs");
+    ldqs = check_planes(*qs, D / 128, M, "ln_row_stats: qs");
+    qp = reinterpret_cast<uint8_t*>(q8->data_ptr());
+    ldq = q8->stride(0);
+    sp = qs->data_ptr<uint8_t>();
+  }
   const at::DeviceGuard guard(x.device());
   LUMEN_CHECK_HIP(lumen::ln_row_stats(bf(x), x.stride(0), out.data_ptr<float>(), (int)x.size(0), (int)x.size(1),
-                                      (float)eps, cur_stream()));
+                                      (float)eps, cur_stream(), qp, ldq, sp, ldqs));
 }
 
 // ---------------------------------------------------------------- fp8 (e4m3fn) weight GEMM
@@ -402,7 +421,8 @@ void gemm_mx(const at::Tensor& a8, const at::Tensor& a_bs, const at::Tensor& w8,
              const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& residual,
              const c10::optional<at::Tensor>& out, int64_t glu, const c10::optional<at::Tensor>& ssq_in, double norm_eps,
              const c10::optional<at::Tensor>& q8, const c10::optional<at::Tensor>& qs,
-             const c10::optional<at::Tensor>& ssq_out, int64_t variant) {
+             const c10::optional<at::Tensor>& ssq_out, int64_t variant, int64_t act,
+             const c10::optional<at::Tensor>& row_aff, const c10::optional<at::Tensor>& col_aff) {
   check_f8_rows(a8, "gemm_mx: a8");
   check_f8_rows(w8, "gemm_mx: w8");
   const int64_t M = a8.size(0), K = a8.size(1), N = w8.size(0);
@@ -425,8 +445,21 @@ void gemm_mx(const at::Tensor& a8, const at::Tensor& a_bs, const at::Tensor& w8,
     cp = out->data_ptr();
     ldc = out->stride(0);
   } else {
-    TORCH_CHECK(glu && q8.has_value() && q8->defined(), "gemm_mx: out may only be omitted for SwiGLU with q8");
+    TORCH_CHECK(q8.has_value() && q8->defined() && !(residual.has_value() && residual->defined()),
+                "gemm_mx: out may only be omitted with q8 (and no residual)");
     mx.skip_c = 1;
+  }
+  ep.act = (int)act;
+  TORCH_CHECK(!(glu && act), "gemm_mx: act with glu");
+  if (row_aff.has_value() && row_aff->defined()) {
+    TORCH_CHECK(!glu && !(bias.has_value() && bias->defined()) && col_aff.has_value() && col_aff->defined(),
+                "gemm_mx: LN fold (row_aff) takes col_aff, no bias / glu");
+    TORCH_CHECK(row_aff->is_cuda() && row_aff->scalar_type() == at::kFloat && row_aff->is_contiguous() &&
+                row_aff->numel() >= 2 * M, "gemm_mx: row_aff fp32 [M, 2]");
+    TORCH_CHECK(col_aff->is_cuda() && col_aff->scalar_type() == at::kFloat && col_aff->is_contiguous() &&
+                col_aff->numel() == 2 * N, "gemm_mx: col_aff fp32 [2, N]");
+    ep.row_aff = row_aff->data_ptr<float>();
+    ep.col_aff = col_aff->data_ptr<float>();
   }
   if (bias.has_value() && bias->defined()) {
     TORCH_CHECK(bias->numel() >= N && bias->is_contiguous() &&
@@ -904,7 +937,7 @@ TORCH_LIBRARY(lumen, m) {
         "Tensor(o!) out, float eps, int mode) -> ()");
   m.def("l2norm_(Tensor(a!) x, float eps) -> ()");
   m.def("gemm_lnf(Tensor a, Tensor w, Tensor col_aff, Tensor row_aff, int act, Tensor(o!) out, int tile) -> ()");
-  m.def("ln_row_stats(Tensor x, Tensor(o!) out, float eps) -> ()");
+  m.def("ln_row_stats(Tensor x, Tensor(o!) out, float eps, Tensor(q!)? q8=None, Tensor(s!)? qs=None) -> ()");
   m.def("gemm_probe(Tensor a, Tensor w, Tensor(o!) out, Tensor(d!) dbg, int tile) -> ()");
   m.def("gemm_w8(Tensor a, Tensor w8, Tensor scale, Tensor? bias, Tensor? residual, int act, Tensor(o!) out, "
         "int glu) -> ()");
@@ -914,7 +947,8 @@ TORCH_LIBRARY(lumen, m) {
         "int glu, int splits=-1, int variant=0) -> ()");
   m.def("quant_rows_fp8(Tensor x, Tensor(o!) out8, Tensor(s!) scale) -> ()");
   m.def("gemm_mx(Tensor a8, Tensor a_bs, Tensor w8, Tensor sw, Tensor? bias, Tensor? residual, Tensor(o!)? out, "
-        "int glu, Tensor? ssq_in, float norm_eps, Tensor(q!)? q8, Tensor(s!)? qs, Tensor(t!)? ssq_out, int variant) -> ()");
+        "int glu, Tensor? ssq_in, float norm_eps, Tensor(q!)? q8, Tensor(s!)? qs, Tensor(t!)? ssq_out, int variant, "
+        "int act=0, Tensor? row_aff=None, Tensor? col_aff=None) -> ()");
   m.def("quant_rows_mx(Tensor x, Tensor(q!) q8, Tensor(s!) qs, Tensor(t!)? ssq) -> ()");
   m.def("rms_norm_quant_fp8(Tensor x, Tensor? add, Tensor(r!)? resid_out, Tensor gamma, float eps, Tensor(o!) out8, "
         "Tensor(s!) scale) -> ()");

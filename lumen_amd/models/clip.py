@@ -200,6 +200,26 @@ class _Block(nn.Module):
             self._lnf_key = key
         return self._lnf_cache
 
+    def mx_weights(self) -> dict:
+        """W8A8 form for the MX tower chain (run_blocks_mx): OCP e4m3 weights with per-output-channel
+        scales -- qkv / fc1 with their LayerNorms folded in (:meth:`lnf`), colsum(w') taken over the
+        DEQUANTISED fp8 rows the GEMM multiplies with (the fold subtracts mean * colsum exactly) --
+        plus out / fc2 as they are.  Cached like :meth:`lnf`."""
+        qw, qa, fw, fa = self.lnf()
+        key = getattr(self, "_lnf_key", None)
+        if getattr(self, "_mx_key", None) != key:
+            with torch.no_grad():
+                q8, qs = ops.quantize_fp8_rows(qw)
+                f8, fs = ops.quantize_fp8_rows(fw)
+                qa2, fa2 = qa.clone(), fa.clone()
+                qa2[0] = (q8.float() * qs[:, None]).sum(1)
+                fa2[0] = (f8.float() * fs[:, None]).sum(1)
+                o8, os_ = ops.quantize_fp8_rows(self.out_w)
+                c8, cs = ops.quantize_fp8_rows(self.fc2_w)
+            self._mx_cache = dict(qkv=(q8, qs, qa2), fc1=(f8, fs, fa2), out=(o8, os_), fc2=(c8, cs))
+            self._mx_key = key
+        return self._mx_cache
+
     def random_init(self, gen: torch.Generator, layers: int):
         w = self.qkv_w.shape[1]
         attn_std = w ** -0.5
@@ -249,6 +269,49 @@ def _block_steps(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, 
         ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x, tile=tile if res_tile is None else res_tile)
         del f
         yield i
+
+
+def run_blocks_mx(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float) -> torch.Tensor:
+    """W8A8 pre-LN blocks (GPU, width and MLP width % 128 == 0, head dim 64 / 128), every GEMM
+    operand an MX fp8 tensor produced by the kernel before it -- 7 launches per block:
+
+      LN stats + MX copy of x  ->  qkv gemm_mx (LN folded)  ->  attention (MX O)
+      ->  out gemm_mx (+ bias + residual)  ->  LN stats + MX copy  ->  fc1 gemm_mx (LN folded + act,
+      MX output only)  ->  fc2 gemm_mx (+ bias + residual)
+
+    against 8 for the bf16 blocks (two row-stat passes, four bf16 GEMMs, attention and fc2's split-K
+    reduce), at half the K-step bytes per GEMM.  Weights: _Block.mx_weights."""
+    T, W = x.shape
+    D = W // heads
+    dev = x.device
+    f8, u8 = torch.float8_e4m3fn, torch.uint8
+    mlp = blocks[0].fc1_w.shape[0]
+    st = torch.empty((T, 2), device=dev, dtype=torch.float32)
+    x8 = torch.empty((T, W), device=dev, dtype=f8)
+    xs = torch.empty((W // 128, T, 4), device=dev, dtype=u8)
+    a8 = torch.empty((T, W), device=dev, dtype=f8)
+    as_ = torch.empty((W // 128, T, 4), device=dev, dtype=u8)
+    g8 = torch.empty((T, mlp), device=dev, dtype=f8)
+    gs = torch.empty((mlp // 128, T, 4), device=dev, dtype=u8)
+    qkv = torch.empty((T, 3 * W), device=dev, dtype=x.dtype)
+    for blk in blocks:
+        w = blk.mx_weights()
+        ops.ln_row_stats(x, eps, out=st, q_out=(x8, xs))
+        ops.linear_mx(x8, xs, w["qkv"][0], w["qkv"][1], out=qkv, row_aff=st, col_aff=w["qkv"][2])
+        q5 = qkv.view(B, S, 3, heads, D)
+        ops.attention_mx(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], q_out=(a8, as_))
+        ops.linear_mx(a8, as_, w["out"][0], w["out"][1], bias=blk.out_b, residual=x, out=x)
+        ops.ln_row_stats(x, eps, out=st, q_out=(x8, xs))
+        ops.linear_mx(x8, xs, w["fc1"][0], w["fc1"][1], row_aff=st, col_aff=w["fc1"][2], act=act, q_out=(g8, gs),
+                      write_out=False)
+        ops.linear_mx(g8, gs, w["fc2"][0], w["fc2"][1], bias=blk.fc2_b, residual=x, out=x)
+    return x
+
+
+def mx_blocks_ok(x: torch.Tensor, blocks, heads: int) -> bool:
+    W = x.shape[1]
+    return (x.is_cuda and len(blocks) > 0 and W % 128 == 0 and blocks[0].fc1_w.shape[0] % 128 == 0
+            and W // heads in (64, 128))
 
 
 def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float,
@@ -383,7 +446,10 @@ class VisionTower(nn.Module):
         ops.cls_fill(x, self.class_emb, self.pos_emb, S)
         ops.layer_norm(x, self.ln_pre_w, self.ln_pre_b, cfg.ln_eps, out=x)
         n = len(self.blocks) + layer + 1 if layer < 0 else layer
-        run_blocks(x, self.blocks[:n], B, S, cfg.heads, cfg.act, cfg.ln_eps)
+        if getattr(self, "w8a8", False) and mx_blocks_ok(x, self.blocks[:n], cfg.heads):
+            run_blocks_mx(x, self.blocks[:n], B, S, cfg.heads, cfg.act, cfg.ln_eps)
+        else:
+            run_blocks(x, self.blocks[:n], B, S, cfg.heads, cfg.act, cfg.ln_eps)
         x = x.view(B, S, W)
         return x[:, 1:] if drop_cls else x
 

@@ -20,6 +20,8 @@ LLM's prefill embedding buffer that the ``<image>`` token occupies.
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import asdict, dataclass, field
 from typing import Optional, Sequence
 
@@ -125,6 +127,14 @@ class VLM(nn.Module):
         self.proj1_w.copy_((torch.randn(Hd, Wv, generator=g) * Wv ** -0.5).to(self.proj1_w.dtype).to(dev))
         self.proj2_w.copy_((torch.randn(Hd, Hd, generator=g) * Hd ** -0.5).to(self.proj2_w.dtype).to(dev))
         self.llm.random_init(seed)
+
+    @torch.no_grad()
+    def quantize_fp8(self) -> None:
+        """fp8 VLM: the W8A8 / fp8-weight decoder (LLM.quantize_fp8) and, for a ViT tower, the MX W8A8
+        vision chain (clip.run_blocks_mx; LUMEN_VIT_FP8=0 keeps the tower bf16)."""
+        self.llm.quantize_fp8()
+        if self.cfg.vision_arch != "fastvit" and os.environ.get("LUMEN_VIT_FP8", "1") != "0":
+            self.vision.w8a8 = True
 
     @property
     def device(self):

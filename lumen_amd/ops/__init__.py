@@ -315,7 +315,8 @@ def linear_mx(x8: torch.Tensor, xs: torch.Tensor, w8: torch.Tensor, w_scale: tor
               bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
               out: Optional[torch.Tensor] = None, glu: bool = False, ssq_in: Optional[torch.Tensor] = None,
               norm_eps: float = 0.0, q_out: Optional[tuple] = None, ssq_out: Optional[torch.Tensor] = None,
-              write_out: bool = True, variant: int = 0) -> Optional[torch.Tensor]:
+              write_out: bool = True, variant: int = 0, act=None, row_aff: Optional[torch.Tensor] = None,
+              col_aff: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """W8A8 projection with MX (block-scaled) activations on the gfx950 matrix cores
     (csrc/gemm_f8.hip::gemm_mx): A = x8 * 2^(xs - 127) per 32 columns feeds the MFMA scale operand,
     so producers quantise with block-local scales and no per-row quantisation pass runs.
@@ -331,15 +332,20 @@ def linear_mx(x8: torch.Tensor, xs: torch.Tensor, w8: torch.Tensor, w_scale: tor
     if out is None and write_out:
         out = torch.empty((M, NO), device=x8.device, dtype=torch.bfloat16)
     q8, qs = q_out if q_out is not None else (None, None)
+    a = act_id(act)
     if x8.is_cuda:
         hip_ops().gemm_mx(x8, xs, w8, w_scale, bias, residual, out if write_out else None, int(bool(glu)), ssq_in,
-                          float(norm_eps), q8, qs, ssq_out, int(variant))
+                          float(norm_eps), q8, qs, ssq_out, int(variant), a, row_aff, col_aff)
         return out
     y = (mx_dequant(x8, xs) @ w8.float().t()) * w_scale.float()[None, :N]
     if ssq_in is not None:
         y = y * torch.rsqrt(ssq_in.float()[:M].sum(1, keepdim=True) / K + norm_eps)
+    if row_aff is not None:
+        y = y * row_aff[:M, :1] + row_aff[:M, 1:] * col_aff[0] + col_aff[1]
     if bias is not None:
         y = y + bias.float()[:N]
+    if a and not glu:
+        y = _act_ref(y, a)
     if glu:
         gu = y.view(M, N // 16, 2, 8)
         r = (F.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(M, NO)
@@ -352,8 +358,9 @@ def linear_mx(x8: torch.Tensor, xs: torch.Tensor, w8: torch.Tensor, w_scale: tor
         return out
     if residual is not None:
         y = y + residual.float()[:M, :N]
-    yb = y.to(torch.bfloat16)
-    out[:M, :N] = yb
+    yb = y.to(torch.bfloat16) if write_out else y
+    if write_out:
+        out[:M, :N] = yb
     if q8 is not None:
         a, b = mx_quant_ref(yb.float())
         q8[:M].copy_(a)
@@ -414,17 +421,23 @@ def layer_norm(x, w, b=None, eps=1e-5, row_idx=None, out=None, out_dtype=None, a
     return out
 
 
-def ln_row_stats(x: torch.Tensor, eps: float = 1e-5, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def ln_row_stats(x: torch.Tensor, eps: float = 1e-5, out: Optional[torch.Tensor] = None,
+                 q_out: Optional[tuple] = None) -> torch.Tensor:
     """LayerNorm statistics of the rows of x [R, D]: fp32 [R, 2] = (rstd, -mean * rstd), the
-    row half of a LayerNorm folded into the next projection (:func:`linear_lnf`)."""
+    row half of a LayerNorm folded into the next projection (:func:`linear_lnf`).  ``q_out``
+    = (q8 [R, D], qs [D/128, R, 4]): the raw rows also as MX fp8 (the W8A8 :func:`linear_mx`
+    operand of that projection)."""
     x2 = x.reshape(-1, x.shape[-1])
     if out is None:
         out = torch.empty((x2.shape[0], 2), device=x.device, dtype=torch.float32)
     if x.is_cuda:
         if x2.stride(-1) != 1 or x2.stride(0) % 8 != 0:
             x2 = x2.contiguous()
-        hip_ops().ln_row_stats(x2, out, float(eps))
+        q8, qs = q_out if q_out is not None else (None, None)
+        hip_ops().ln_row_stats(x2, out, float(eps), q8, qs)
         return out
+    if q_out is not None:
+        quant_rows_mx(x2, q_out[0], q_out[1])
     xf = x2.float()
     mean = xf.mean(-1)
     rstd = torch.rsqrt(((xf - mean[:, None]) ** 2).mean(-1) + eps)

@@ -299,6 +299,8 @@ class MI355XVLMBackend:
         if cached is not None and shard_cache.valid(*cached):
             extra = shard_cache.load(m, cached[0], self.device)
             m.llm.weight_dtype = extra.get("weight_dtype", m.llm.weight_dtype)
+            if fp8 and cfg.vision_arch != "fastvit" and os.environ.get("LUMEN_VIT_FP8", "1") != "0":
+                m.vision.w8a8 = True      # the MX vision chain quantises its (bf16, cached) weights on first use
             log.info("VLM rank %d/%d weights from shard cache %s", self.tp.rank, self.tp.world, cached[0])
         else:
             pack = onnx_import.find_vlm_pack(root, self.resources.precision)
@@ -314,7 +316,7 @@ class MI355XVLMBackend:
             else:
                 raise ResourceNotFoundError(f"{self.resources.model_name}: model.safetensors / onnx pack missing")
             if fp8:
-                m.llm.quantize_fp8()   # weight-only OCP e4m3 decoder (config precision "fp8")
+                m.quantize_fp8()   # fp8 decoder + W8A8 ViT tower (config precision "fp8")
             if cached is not None:
                 shard_cache.save(m, cached[0], cached[1], cached[2], {"weight_dtype": m.llm.weight_dtype})
         self.model = m.eval()

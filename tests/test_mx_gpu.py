@@ -210,3 +210,61 @@ def test_llm_prefill_mx_chain_matches_per_token_chain(T):
     # activation quantisation error of the MX chain: no worse than the per-token chain's
     e_mx, e_pt = _rel(got, w8a16), _rel(per_token, w8a16)
     assert e_mx < 1.25 * e_pt + 5e-3, (e_mx, e_pt)
+
+
+def test_ln_row_stats_mx_copy():
+    """LayerNorm row statistics + the raw rows' MX copy in one pass (the W8A8 vision tower's qkv / fc1
+    operand): stats as the plain kernel, bytes as mx_quant_ref."""
+    g = torch.Generator().manual_seed(7)
+    x = _rows(577, 1024, g)
+    st0 = ops.ln_row_stats(x.to(DEV), 1e-5)
+    q8 = torch.empty(577, 1024, device=DEV, dtype=torch.float8_e4m3fn)
+    qs = torch.empty(8, 577, 4, device=DEV, dtype=torch.uint8)
+    st = ops.ln_row_stats(x.to(DEV), 1e-5, q_out=(q8, qs))
+    assert torch.equal(st, st0)
+    q_ref, s_ref = ops.mx_quant_ref(x)
+    assert torch.equal(qs.cpu(), s_ref) and torch.equal(q8.cpu().view(torch.uint8), q_ref.view(torch.uint8))
+
+
+@pytest.mark.parametrize("mx_only", [False, True])
+def test_gemm_mx_ln_fold_and_act(mx_only):
+    """qkv / fc1 of the vision chain: LN folded (row_aff, col_aff), quick_gelu, bf16 out or MX out only."""
+    g = torch.Generator().manual_seed(9)
+    M, N, K = 577, 1024, 1024
+    x = (torch.randn(M, K, generator=g) * 2 + 0.5).bfloat16()
+    w = (torch.randn(N, K, generator=g) * K ** -0.5)
+    gamma, beta, b = torch.rand(K, generator=g) + 0.5, torch.randn(K, generator=g) * 0.1, torch.randn(N, generator=g)
+    wf, caff = ops.ln_fold_weights(w.bfloat16(), b, gamma, beta)
+    w8, sw = ops.quantize_fp8_rows(wf)
+    caff[0] = (w8.float() * sw[:, None]).sum(1)
+    xd = x.to(DEV)
+    x8 = torch.empty(M, K, device=DEV, dtype=torch.float8_e4m3fn)
+    xs = torch.empty(K // 128, M, 4, device=DEV, dtype=torch.uint8)
+    st = ops.ln_row_stats(xd, 1e-5, q_out=(x8, xs))
+    q8 = torch.empty(M, N, device=DEV, dtype=torch.float8_e4m3fn)
+    qs = torch.empty(N // 128, M, 4, device=DEV, dtype=torch.uint8)
+    got = ops.linear_mx(x8, xs, w8.to(DEV), sw.to(DEV), row_aff=st, col_aff=caff.to(DEV), act="quick_gelu",
+                        q_out=(q8, qs) if mx_only else None, write_out=not mx_only)
+    ln = torch.nn.functional.layer_norm(x.float(), (K,), gamma, beta, 1e-5)
+    ref = ln @ w.t() + b
+    ref = ref * torch.sigmoid(1.702 * ref)
+    res = ops.mx_dequant(q8.cpu(), qs.cpu()) if mx_only else got
+    assert _rel(res, ref) < 4e-2
+
+
+def test_vision_tower_w8a8_matches_bf16():
+    """The W8A8 MX vision chain (run_blocks_mx) vs the bf16 tower on the same weights."""
+    from lumen_amd.models.clip import VisionConfig, VisionTower
+
+    cfg = VisionConfig(image_size=64, patch_size=16, width=256, layers=3, heads=4)
+    vt = VisionTower(cfg, 16, torch.float32, "cpu")
+    vt.random_init(torch.Generator().manual_seed(0))
+    v = VisionTower(cfg, 16, torch.bfloat16, DEV)
+    v.load_state_dict({k: t.to(v.state_dict()[k].dtype) for k, t in vt.state_dict().items()})
+    imgs = [torch.randint(0, 256, (64, 64, 3), dtype=torch.uint8, device=DEV) for _ in range(3)]
+    patches = v.preprocess(imgs, (0.48, 0.46, 0.41), (0.27, 0.26, 0.28))
+    ref = v.forward_features(patches, 3, -2).float()
+    v.w8a8 = True
+    got = v.forward_features(patches, 3, -2).float()
+    cos = torch.nn.functional.cosine_similarity(got.reshape(-1, 256), ref.reshape(-1, 256)).min().item()
+    assert cos > 0.98, cos

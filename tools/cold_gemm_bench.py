@@ -50,7 +50,7 @@ def timed(fn, L, reps=3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", choices=["vit", "prefill", "mx"], default="vit")
+    ap.add_argument("--what", choices=["vit", "prefill", "mx", "mxvit"], default="vit")
     ap.add_argument("--epi", choices=["full", "plain"], default="full",
                     help="mx: the chain's epilogues (rstd, MX outputs, sums of squares) or a plain store")
     ap.add_argument("--M", type=int, default=0)
@@ -63,11 +63,15 @@ def main():
     dev = "cuda"
     torch.manual_seed(0)
     vit = a.what == "vit"
-    mx = a.what == "mx"
-    M = a.M or (577 if vit else 624)
+    mx = a.what in ("mx", "mxvit")
+    mxvit = a.what == "mxvit"
+    M = a.M or (577 if vit or mxvit else 624)
     variants = [int(v) for v in (a.variants or ("-1,20002,20003,20005" if vit else "0,1,2")).split(",")]
     splits = [int(s) for s in a.splits.split(",")]
     shapes = VIT if vit else PREFILL
+    if mxvit:   # the W8A8 vision chain's GEMMs (clip.run_blocks_mx): act -> MX output for fc1
+        shapes = [("qkv", 3072, 1024, False, False), ("out", 1024, 1024, False, True), ("fc1", 4096, 1024, False, False),
+                  ("fc2", 1024, 4096, False, True)]
     if a.shapes:
         shapes = [s for s in shapes if s[0] in a.shapes.split(",")]
     res = {"what": a.what, "M": M}

@@ -56,7 +56,7 @@ def main():
     m = VLM(cfg, device=dev)
     m.random_init(0)
     if args.fp8:
-        m.llm.quantize_fp8()
+        m.quantize_fp8()
     torch.cuda.synchronize()
     load_s = time.time() - t0
     kv = PagedKVCache(cfg.llm.num_layers, m.llm.Hkv, cfg.llm.head_dim, num_blocks=args.kv_blocks, device=dev,
@@ -157,7 +157,7 @@ def main():
            "B prefills; batch_decode_tok_s = steady-state decode while all B streams run",
            "prompt_tokens": len(full),
            "image_tokens": cfg.num_image_tokens, "max_new_tokens": args.max_new, "batch_max_new_tokens": args.batch_max_new, "n": args.n,
-           "preset": args.preset, "kv_cache": "fp8-e4m3" if args.kv_fp8 else "bf16", "dtype": "bf16" if not args.fp8 else "fp8-e4m3 decoder (W8A8 prefill, fp8-weight decode), bf16 vision", "data": f"synthetic (random-init weights, {args.image_kind} 1024x768 JPEG, {len(jpeg) // 1024} KiB)",
+           "preset": args.preset, "kv_cache": "fp8-e4m3" if args.kv_fp8 else "bf16", "dtype": "bf16" if not args.fp8 else "fp8-e4m3 decoder (W8A8 prefill, fp8-weight decode), " + ("W8A8 MX vision" if getattr(m.vision, "w8a8", False) else "bf16 vision"), "data": f"synthetic (random-init weights, {args.image_kind} 1024x768 JPEG, {len(jpeg) // 1024} KiB)",
            "load_s": load_s, "kv_cache_tokens": kv.capacity_tokens,
            "jpeg_decode": ("host, full resolution" if args.full_decode else
                            f"host, DCT-scaled to >= {cfg.vision.image_size}px") if args.host_decode else
