@@ -30,6 +30,7 @@ import torch
 from torch import nn
 
 from .. import ops
+from ..utils.h2d import h2d
 from .clip import VisionConfig, VisionTower
 from .fastvit import FASTVIT_PRESETS, FastViTConfig, FastViTTower
 from .llm import LLM, LLM_PRESETS, LLMConfig, TPInfo
@@ -199,7 +200,7 @@ class VLM(nn.Module):
         n = len(images) if n_images is None else int(n_images)
         full, starts = self.expand_image_tokens(ids, n)
         dev = self.device
-        t = torch.tensor(full, dtype=torch.long, device=dev)
+        t = h2d(full, dev, torch.long)
         x = self.llm.embed_tokens(t)
         N = self.cfg.num_image_tokens
         if not starts:

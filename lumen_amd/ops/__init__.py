@@ -18,6 +18,7 @@ import torch
 import torch.nn.functional as F
 
 from .._native import hip_ops
+from ..utils.h2d import h2d
 
 ACTS = {
     None: 0, "none": 0, "gelu": 1, "quick_gelu": 2, "relu": 3, "silu": 4, "gelu_tanh": 5,
@@ -777,7 +778,7 @@ def image_prep(
         if src is None:
             src = flat_src if flat_src is not None else torch.cat([im.reshape(-1) for im in imgs])
             src = src.to(device, non_blocking=True)
-        g = torch.tensor([gg.row() for gg in geoms], dtype=torch.long).to(device, non_blocking=True)
+        g = h2d([gg.row() for gg in geoms], device, torch.long)
         max_ch = max(gg.ch for gg in geoms)
         max_dw = max(gg.dw for gg in geoms)
         tmp = torch.empty((B, max_ch, max_dw, 3), device=device, dtype=torch.float32)

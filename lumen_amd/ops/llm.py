@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from .._native import hip_ops
+from ..utils.h2d import h2d
 
 KV_BLOCK = 64
 
@@ -177,8 +178,7 @@ def rep_penalty_(logits: torch.Tensor, token_ids: Sequence[Sequence[int]], penal
     for b, u in enumerate(uniq):
         ids[b, :len(u)] = u
     if logits.is_cuda:
-        hip_ops().rep_penalty_(logits, torch.from_numpy(ids).to(logits.device),
-                               torch.tensor(list(penalty), dtype=torch.float32, device=logits.device))
+        hip_ops().rep_penalty_(logits, h2d(ids, logits.device), h2d(list(penalty), logits.device, torch.float32))
         return logits
     for b, u in enumerate(uniq):
         if not u:

@@ -15,6 +15,7 @@ import torch
 
 from .._native import hip_ops, load_host
 from ..runtime.metrics import stage
+from ..utils.h2d import h2d
 
 # ArcFace 5-point template for 112x112 crops (insightface canonical coordinates)
 ARCFACE_DST = np.array([[38.2946, 51.6963], [73.5318, 51.5014], [56.0252, 71.7366], [41.5493, 92.3655],
@@ -198,10 +199,10 @@ def warp_batch(images: Sequence[np.ndarray], img_index: Sequence[int], minv: np.
                 offs.append(off)
                 flat.append(torch.from_numpy(np.ascontiguousarray(im)).reshape(-1))
                 off += im.size
-            src = torch.cat(flat).to(device, non_blocking=True)
-        meta = torch.tensor([[offs[i], images[i].shape[0], images[i].shape[1], ow[f]] for f, i in enumerate(img_index)],
-                            dtype=torch.long).to(device)
-        mv = torch.from_numpy(np.ascontiguousarray(minv, np.float32).reshape(F, 9)).to(device)
+            src = h2d(torch.cat(flat), device)
+        meta = h2d([[offs[i], images[i].shape[0], images[i].shape[1], ow[f]] for f, i in enumerate(img_index)],
+                   device, torch.long)
+        mv = h2d(np.ascontiguousarray(minv, np.float32).reshape(F, 9), device)
         out = torch.empty((F, OH, OW, cpad), device=device, dtype=torch.bfloat16)
         hip_ops().warp_batch(src, meta, mv, out, float(scale), float(mean), float(std), bool(swap_rb), bool(cubic),
                              bool(replicate))
@@ -290,7 +291,7 @@ def cls_ctc_greedy(h: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
     ids = torch.empty((B, T), dtype=torch.int32, device=dev)
     ln = torch.empty((B,), dtype=torch.int32, device=dev)
     cf = torch.empty((B,), dtype=torch.float32, device=dev)
-    tl = torch.tensor(list(tlen), dtype=torch.int32).to(dev) if tlen is not None else None
+    tl = h2d(list(tlen), dev, torch.int32) if tlen is not None else None
     b = bias.float().contiguous() if bias is not None else None
     hip_ops().cls_ctc(h.contiguous(), w.contiguous(), b, int(num_classes), int(B), int(T), int(blank), tl, i1, c1,
                       ids, ln, cf)
@@ -317,7 +318,7 @@ def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw
     if prob.dtype not in (torch.bfloat16, torch.float32):
         prob = prob.float()
     dev = prob.device
-    thr = torch.tensor([float(p.det_thresh) for p in params], dtype=torch.float32, device=dev)
+    thr = h2d([float(p.det_thresh) for p in params], dev, torch.float32)
     cap = cap or max(1 << 16, n * rh * rw // 4)
     lab = torch.empty(5 * n * rh * rw, dtype=torch.int32, device=dev)     # labels + per-root bbox
     pts = torch.empty((cap, 3), dtype=torch.int32, device=dev)
@@ -359,7 +360,7 @@ def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw
     if len(Q):
         with stage("db_score"):
             sc = torch.empty(3 * len(Q), dtype=torch.float32, device=dev)
-            hip_ops().db_quad_score(prob, torch.from_numpy(Q).to(dev), torch.from_numpy(np.concatenate(all_i)).to(dev),
+            hip_ops().db_quad_score(prob, h2d(Q, dev), h2d(np.concatenate(all_i), dev),
                                     sc)
             scores = sc[:len(Q)].cpu().numpy()
     out, o = [], 0

@@ -39,6 +39,7 @@ import torch
 
 from .. import ops
 from ..ops import llm as lops
+from ..utils.h2d import h2d
 from .kv_cache import BLOCK, PagedKVCache
 
 log = logging.getLogger("lumen.engine")
@@ -112,7 +113,7 @@ class Sampler:
         if spec["pen"] is not None:
             lops.rep_penalty_(logits, [[t - self.llm.v0 for t in ids] for ids in spec["pen_ids"]], spec["pen"])
         if spec["inv"] is not None:
-            logits.mul_(torch.tensor(spec["inv"], device=logits.device, dtype=torch.float32)[:, None])
+            logits.mul_(h2d(spec["inv"], logits.device, torch.float32)[:, None])
         k = spec["k"]
         v, i, lse = ops.row_topk(logits, k, with_lse=True, index_offset=self.llm.v0)
         tp = self.llm.tp
@@ -553,8 +554,8 @@ class LLMEngine:
         spec = Sampler.spec([r]) if last else None
         if self.sync is not None:
             self.sync.send(("pchunk", r.rid, s, e, slots, tab, spec, last))
-        logits = self.llm.prefill(r.x[s:e], self.kv, torch.from_numpy(slots).to(self.device), start_pos=s,
-                                  prefix_blocks=torch.from_numpy(tab).to(self.device) if tab is not None else None)
+        logits = self.llm.prefill(r.x[s:e], self.kv, h2d(slots, self.device), start_pos=s,
+                                  prefix_blocks=h2d(tab, self.device) if tab is not None else None)
         r.done = e
         self.stats["prefill_chunks"] += 1
         if not last:
@@ -747,8 +748,8 @@ def follower_loop(llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.
             elif kind == "pchunk":
                 _, rid, s, e, slots, tab, spec, last = msg
                 x = xs[rid] if not last else xs.pop(rid)
-                logits = llm.prefill(x[s:e], kv, torch.from_numpy(slots).to(dev), start_pos=s,
-                                     prefix_blocks=torch.from_numpy(tab).to(dev) if tab is not None else None)
+                logits = llm.prefill(x[s:e], kv, h2d(slots, dev), start_pos=s,
+                                     prefix_blocks=h2d(tab, dev) if tab is not None else None)
                 if last:
                     sampler.candidates(logits, spec)
             elif kind == "decode":
@@ -756,7 +757,6 @@ def follower_loop(llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.
                 if graph and graphs is not None:
                     logits = graphs.run(ids, pos, slots, bt, ctx)
                 else:
-                    logits = llm.decode(torch.from_numpy(ids).to(dev), torch.from_numpy(pos).to(dev),
-                                        torch.from_numpy(slots).to(dev), kv, torch.from_numpy(bt).to(dev),
-                                        torch.from_numpy(ctx).to(dev), workspace=ws)
+                    logits = llm.decode(h2d(ids, dev), h2d(pos, dev), h2d(slots, dev), kv, h2d(bt, dev),
+                                        h2d(ctx, dev), workspace=ws)
                 sampler.candidates(logits, spec)

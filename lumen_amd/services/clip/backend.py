@@ -30,6 +30,7 @@ import torch
 from ...models.clip import CLIPModel
 from ...runtime.batcher import DynamicBatcher
 from ...runtime.metrics import stage
+from ...utils.h2d import h2d
 from ...utils.image import decode_many, decode_rgb
 from ...resources.exceptions import ResourceError
 from .resources import ModelResources, load_weights
@@ -371,7 +372,7 @@ def dp_worker(device: str, cache_dir: str, model: str, runtime: str, dataset: Op
                     imgs[k] = a
             emb = m.encode_image_uint8([torch.from_numpy(np.ascontiguousarray(i)) for i in imgs])
         elif kind == "text":
-            emb = m.encode_text_ids(torch.from_numpy(np.stack(items)).to(dev))
+            emb = m.encode_text_ids(h2d(np.stack(items), dev))
         else:
             raise ValueError(f"unknown CLIP task kind {kind!r}")
         return list(emb.float().cpu().numpy())

@@ -61,6 +61,7 @@ from ...ops import vision
 from ...resources.exceptions import ResourceNotFoundError
 from ...runtime.batcher import DynamicBatcher
 from ...runtime.metrics import stage
+from ...utils.h2d import h2d
 from ...utils.image import decode_rgb
 from ..common import BackendInfo, GenericResources, load_safetensors, pick_device, runtime_name
 
@@ -302,8 +303,8 @@ class MI355XFaceBackend:
             return self._det_post_inner(images, params, heads, scales, N)
 
     def _det_post_inner(self, images, params, heads, scales, N) -> list[list[FaceDetection]]:
-        img_scale = torch.tensor(scales, dtype=torch.float32, device=self.device)
-        img_hw = torch.tensor([[im.shape[0], im.shape[1]] for im in images], dtype=torch.float32, device=self.device)
+        img_scale = h2d(scales, self.device, torch.float32)
+        img_hw = h2d([[im.shape[0], im.shape[1]] for im in images], self.device, torch.float32)
         A = self.det.cfg.anchors
         results: list[Optional[list[FaceDetection]]] = [None] * N
         groups: dict = {}
@@ -311,7 +312,7 @@ class MI355XFaceBackend:
             groups.setdefault(p.key(), []).append(i)
         for key, idx in groups.items():
             p = params[idx[0]]
-            sel = torch.tensor(idx, device=self.device) if len(groups) > 1 else None
+            sel = h2d(idx, self.device, torch.long) if len(groups) > 1 else None
             n = len(idx)
             cand = torch.zeros((n, MAX_CAND, 16), dtype=torch.float32, device=self.device)
             count = torch.zeros((n,), dtype=torch.int32, device=self.device)

@@ -1,0 +1,42 @@
+"""Small host -> device uploads that never stall the host.
+
+A copy from pageable host memory (``torch.tensor(list).to("cuda")``, ``torch.from_numpy(a).to(dev)``
+and even ``.to(dev, non_blocking=True)`` of a pageable tensor) makes HIP stage the bytes through
+its own pinned bounce buffer: the calling thread blocks until the stream has drained up to the
+copy -- measured 6.4 ms of host time for a 64 KiB copy behind 17.7 ms of queued GEMMs
+(tools/probe_h2d.py) versus 0.06 ms from pinned memory.  In a pipelined loop (decode step i on the
+host while the GPU runs step i - 1, an admitted request's prefill launched while its vision tower
+still runs) that stall serialises host and device.
+
+:func:`h2d` copies the data into a block of torch's caching pinned-host allocator and issues an
+asynchronous copy; the allocator records the copy's stream event and only hands the block out
+again once the copy has completed, so the host buffer's lifetime is safe without any fencing here.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+_SMALL = 1 << 26     # above this a one-off pinned block costs more than it saves
+
+
+def h2d(data, device, dtype=None) -> torch.Tensor:
+    """list / numpy array / CPU tensor -> tensor on ``device`` (asynchronous for CUDA targets)."""
+    dev = torch.device(device)
+    if isinstance(data, torch.Tensor):
+        t = data if dtype is None else data.to(dtype)
+    elif isinstance(data, np.ndarray):
+        t = torch.from_numpy(np.ascontiguousarray(data))
+        if dtype is not None:
+            t = t.to(dtype)
+    else:
+        t = torch.as_tensor(data, dtype=dtype)
+    if dev.type != "cuda":
+        return t.to(dev)
+    if t.device.type == "cuda":
+        return t.to(dev)
+    if t.numel() * t.element_size() > _SMALL or torch.cuda.is_current_stream_capturing():
+        return t.to(dev)
+    pinned = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    pinned.copy_(t)
+    return pinned.to(dev, non_blocking=True)

@@ -200,9 +200,10 @@ def decode_to_device(data: bytes, device, threads: Optional[int] = None, stats: 
             if stats is not None:
                 stats.update(s)
             from ..ops import hip_ops
+            from .h2d import h2d
 
             cd = st[:n].to(dev, non_blocking=True)
-            qd = torch.from_numpy(qt.view(np.int16)).to(dev, non_blocking=True)
+            qd = h2d(qt.view(np.int16), dev)
             samp = torch.empty(n, dtype=torch.uint8, device=dev)
             out = torch.empty((ji.height, ji.width, 3), dtype=torch.uint8, device=dev)
             ev = torch.cuda.Event()
