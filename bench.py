@@ -9,8 +9,10 @@ embeddings -> RCCL all-gather of every rank's embeddings (the DP result
 gather).  Weak scaling: the per-GPU batch is fixed, so the global batch grows
 with N.  JPEG decode is not in the headline timed region.  After it, two side windows
 run by default: a >= 30 s steady-state window of the same step (``--seconds``,
-``steady_state``) and an end-to-end window with JPEG decode on the CPU pool
-(``--include-decode``, ``e2e_with_jpeg_decode``); then the text tower (``texts_per_s``).
+``steady_state``) and two end-to-end windows that include JPEG decode (``--include-decode``):
+``e2e_with_jpeg_decode`` = the framework's device JPEG path (host entropy decode + one batched GPU
+IDCT/colour launch, utils/jpeg.py) and ``e2e_with_pillow_decode`` = Pillow on the CPU pool; then
+the text tower (``texts_per_s``).
 
 Launch: ``python bench.py --gpus 1`` or
 ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``.
@@ -267,8 +269,8 @@ def main():
             "text_config": {"context_length": cfg.text.context_length, "batch_per_gpu": B,
                             "timed": "separately, after the image window"} if text_per_s else None,
             "steady_state": steady,
-            "e2e_with_jpeg_decode": e2e,
-            "e2e_with_device_jpeg_decode": e2e_dev,
+            "e2e_with_jpeg_decode": e2e_dev,
+            "e2e_with_pillow_decode": e2e,
             "finite": ok,
         }
         print(json.dumps(out), flush=True)

@@ -4,7 +4,7 @@ A copy from pageable host memory (``torch.tensor(list).to("cuda")``, ``torch.fro
 and even ``.to(dev, non_blocking=True)`` of a pageable tensor) makes HIP stage the bytes through
 its own pinned bounce buffer: the calling thread blocks until the stream has drained up to the
 copy -- measured 6.4 ms of host time for a 64 KiB copy behind 17.7 ms of queued GEMMs
-(tools/probe_h2d.py) versus 0.06 ms from pinned memory.  In a pipelined loop (decode step i on the
+(tools/probes/h2d_stall.py) versus 0.06 ms from pinned memory.  In a pipelined loop (decode step i on the
 host while the GPU runs step i - 1, an admitted request's prefill launched while its vision tower
 still runs) that stall serialises host and device.
 
