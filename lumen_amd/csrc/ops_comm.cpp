@@ -65,6 +65,16 @@ int64_t ar_error(int64_t ptr) {
   return err;
 }
 
+// Enqueue a copy of the error word into out[0] (int32, device) on the current stream: a decode
+// graph captures it after its last all-reduce, so the step's result D2H carries the flag and the
+// leader can refuse to emit tokens computed from a timed-out (stale) all-reduce.
+void ar_error_into(int64_t ptr, at::Tensor out) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kInt && out.numel() >= 1, "ar_error_into: cuda int32 out");
+  const at::DeviceGuard g(out.device());
+  CHECK_HIPC(hipMemcpyAsync(out.data_ptr(), reinterpret_cast<char*>(ptr) + offsetof(lumen::ArCtl, err), sizeof(uint32_t),
+                            hipMemcpyDeviceToDevice, c10::hip::getCurrentHIPStream().stream()));
+}
+
 // out = sum over ranks of inp (bf16 or fp32, contiguous, bytes % 16 == 0, bytes <= cap)
 void custom_all_reduce(const at::Tensor& inp, at::Tensor out, at::IntArrayRef bases, int64_t rank, int64_t cap) {
   TORCH_CHECK(inp.is_cuda() && out.is_cuda() && inp.is_contiguous() && out.is_contiguous(), "custom_all_reduce: cuda contiguous");
@@ -110,8 +120,10 @@ TORCH_LIBRARY_FRAGMENT(lumen, m) {
   m.def("ar_close(int ptr) -> ()", &ar_close);
   m.def("ar_error(int ptr) -> int", &ar_error);
   m.def("custom_all_reduce(Tensor inp, Tensor(o!) out, int[] bases, int rank, int cap) -> ()");
+  m.def("ar_error_into(int ptr, Tensor(o!) out) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("custom_all_reduce", &custom_all_reduce);
+  m.impl("ar_error_into", &ar_error_into);
 }

@@ -190,13 +190,18 @@ class VLM(nn.Module):
 
     @torch.no_grad()
     def build_prefill(self, ids: Sequence[int], images: Sequence[torch.Tensor],
-                      n_images: Optional[int] = None) -> torch.Tensor:
+                      n_images: Optional[int] = None, shard_images: bool = False) -> torch.Tensor:
         """Token embeddings with image rows spliced in -> x [T, hidden] on the model device.
 
-        Tensor parallel: every rank embeds the text (vocab-parallel lookup + all-reduce), but
-        only TP rank 0 holds the images (``n_images`` tells the others how many) and runs the
-        vision tower + projector; the [N_img, hidden] features are broadcast to the group
-        (one RCCL broadcast instead of N-1 redundant JPEG decodes and vision towers)."""
+        Tensor parallel: every rank embeds the text (vocab-parallel lookup + all-reduce).
+        ``shard_images`` (every rank holds all the images): rank r runs the vision tower +
+        projector on images r, r + world, ... only, and ONE all-reduce of the zero-filled
+        [n * N_img, hidden] block (disjoint rows: the sum is exact) hands every rank all the
+        features -- a multi-image prompt's towers run in parallel across the TP group.
+        Otherwise only TP rank 0 holds the images (``n_images`` tells the others how many) and
+        its features are broadcast (one image cannot be split usefully: the ViT-L/14-336 layer is
+        launch-bound at 577 rows, so 1/world of the rows per rank saves almost nothing and adds a
+        K/V all-gather per layer)."""
         n = len(images) if n_images is None else int(n_images)
         full, starts = self.expand_image_tokens(ids, n)
         dev = self.device
@@ -212,6 +217,18 @@ class VLM(nn.Module):
 
             buf = x[starts[0]:starts[0] + N * len(starts)] if contiguous else \
                 torch.empty((N * len(starts), x.shape[1]), device=dev, dtype=x.dtype)
+            if shard_images:
+                buf.zero_()
+                for i in range(tp.rank, len(starts), tp.world):
+                    self.encode_images([images[i]], out=buf[i * N:(i + 1) * N])
+                staged = buf.cpu() if dist.get_backend(tp.group) == "gloo" and buf.is_cuda else buf
+                dist.all_reduce(staged, group=tp.group)
+                if staged is not buf:
+                    buf.copy_(staged)
+                if not contiguous:
+                    for i, s in enumerate(starts):
+                        x[s:s + N] = buf[i * N:(i + 1) * N]
+                return x
             if tp.rank == 0:
                 self.encode_images(images[:len(starts)], out=buf)
             staged = buf.cpu() if dist.get_backend(tp.group) == "gloo" and buf.is_cuda else buf

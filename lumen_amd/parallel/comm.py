@@ -205,6 +205,14 @@ class Communicator:
         if self.custom is not None and self.custom.error():
             raise TPGroupUnavailable("tensor-parallel peer not responding (IPC all-reduce timed out)")
 
+    def error_into(self, out: torch.Tensor) -> None:
+        """Enqueue the IPC all-reduce error word into ``out[0]`` (int32, device; capturable), so a
+        step's result copy carries it; zero when the IPC path is off."""
+        if self.custom is not None:
+            self.custom.ops.ar_error_into(self.custom.own, out)
+        else:
+            out[:1].zero_()
+
     def close(self) -> None:
         if self.custom is not None:
             self.custom.close()

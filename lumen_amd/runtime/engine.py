@@ -39,6 +39,7 @@ import torch
 
 from .. import ops
 from ..ops import llm as lops
+from ..parallel.comm import TPGroupUnavailable
 from ..utils.h2d import h2d
 from .kv_cache import BLOCK, PagedKVCache
 
@@ -98,6 +99,7 @@ class Sampler:
 
     def __init__(self, llm):
         self.llm = llm
+        self.d2h = 0          # host round trips of the candidate gather (gloo groups only)
 
     @staticmethod
     def spec(reqs: Sequence[GenRequest]) -> dict:
@@ -126,6 +128,7 @@ class Sampler:
             packed = torch.cat([v, i.to(torch.float32), lse.view(B, 1)], 1).contiguous()
             if packed.is_cuda and dist.get_backend(tp.group) == "gloo":    # gloo gathers host tensors only
                 packed = packed.cpu()
+                self.d2h += 1
             parts = [torch.empty_like(packed) for _ in range(tp.world)]
             dist.all_gather(parts, packed, group=tp.group)
             allp = torch.stack(parts, 1)                                   # [B, world, 2k + 1]
@@ -148,24 +151,35 @@ class Sampler:
 
 
 class TPSync:
-    """Step broadcast from rank 0 to the follower ranks of a TP group.
+    """Step channel from rank 0 (the engine) to the follower ranks of a TP group.
 
-    Every step is ONE broadcast of a 4 KiB prefix of an int32 buffer: an 8-int header (op, batch,
-    table width, top-k, graph flag, message length) followed, for decode steps, by the step
-    descriptor -- ids, positions, cache slots, context lengths, block table -- so a follower pays
-    one collective and one small D2H per token (the header decides which graph to replay; nothing
-    is pickled).  A descriptor longer than the prefix (big batches x long block tables) sends its
-    remainder in a second broadcast sized from the header; the full capacity never travels.
-    Prefill / control messages and decode steps whose sampling needs per-row state
-    (temperatures, repetition-penalty token sets) add an object broadcast after the header.
-    The buffer lives on the device the group's backend moves (GPU for RCCL, host for gloo).
+    Transport:
+
+    * ``bus`` (default when every rank of the group is on this node -- always, for
+      :class:`~lumen_amd.parallel.tp.TPServingGroup`): a host shared-memory ring
+      (:mod:`lumen_amd.parallel.step_bus`).  A follower's host reads the step straight from shared
+      memory -- no collective and no device->host copy per token -- and launches its step while
+      the leader launches its own.
+    * ``bcast``: ONE broadcast of a 4 KiB prefix of an int32 buffer per step (GPU buffer for RCCL,
+      host for gloo), plus a sized remainder for long descriptors; the follower copies the prefix
+      to the host to parse it.
+
+    A decode step is an 8-int header (op, batch, table width, top-k, flags, message length)
+    followed by the step descriptor -- ids, positions, cache slots, context lengths, block table;
+    nothing is pickled.  ``flags``: 1 = replay the captured graph, 2 = token ids come from the
+    previous replay's in-graph arg-max (look-ahead step), 4 = the graph's in-graph TP sampler is
+    this step's sampler (the follower does nothing after the replay).  Prefill / control messages
+    and decode steps whose sampling needs per-row state (temperatures, repetition-penalty token
+    sets) travel pickled (bus) or as an object broadcast (bcast).
     ``capacity`` (ints after the header) must hold 4 * batch + batch * table width of the
     largest decode step: :func:`tp_sync_capacity`.
     """
 
-    OBJ, DECODE = 1, 2
+    OBJ, DECODE, OBJ_BIG = 1, 2, 3
+    F_GRAPH, F_DEV_IDS, F_INGRAPH = 1, 2, 4
 
-    def __init__(self, group=None, src: int = 0, device: Optional[torch.device] = None, capacity: int = 1 << 15):
+    def __init__(self, group=None, src: int = 0, device: Optional[torch.device] = None, capacity: int = 1 << 15,
+                 transport: Optional[str] = None):
         import torch.distributed as dist
 
         self.group, self.src = group, src
@@ -176,7 +190,52 @@ class TPSync:
         self.capacity = int(capacity)
         self.buf = torch.zeros(8 + self.capacity, dtype=torch.int32, device=device)
         self.prefix = min(1024, 8 + self.capacity)          # ints per step's first broadcast
-        self.stats = {"tensor_steps": 0, "object_steps": 0, "two_part_steps": 0}
+        self.stats = {"tensor_steps": 0, "object_steps": 0, "two_part_steps": 0, "d2h": 0}
+        self.bus = None
+        transport = transport or os.environ.get("LUMEN_TP_STEP_TRANSPORT", "bus")
+        if transport == "bus":
+            self.bus = self._open_bus()
+        self.transport = "bus" if self.bus is not None else "bcast"
+
+    def _open_bus(self):
+        """Collective: a shared-memory bus when all ranks share this host and the host library
+        has it (every rank agrees, else all fall back to broadcasts)."""
+        import socket
+
+        import torch.distributed as dist
+
+        from ..parallel import step_bus
+
+        rank, world = dist.get_rank(self.group), dist.get_world_size(self.group)
+        hosts = [None] * world
+        dist.all_gather_object(hosts, (socket.gethostname(), step_bus.available()), group=self.group)
+        if len({h for h, _ in hosts}) != 1 or not all(ok for _, ok in hosts):
+            return None
+        slot = max(1 << 18, 4 * (8 + self.capacity) + 64)
+        name = [None]
+        bus, err = None, None
+        if rank == self.src:
+            try:
+                name[0] = step_bus.StepBus.unique_name()
+                bus = step_bus.StepBus(name[0], None, nslots=64, slot_bytes=slot, nreaders=world - 1)
+            except Exception as e:  # noqa: BLE001 - agreed fallback below
+                name[0], err = None, e
+        dist.broadcast_object_list(name, src=self.src, group=self.group)
+        if name[0] is not None and rank != self.src:
+            try:
+                bus = step_bus.StepBus(name[0], rank if rank < self.src else rank - 1)
+            except Exception as e:  # noqa: BLE001
+                bus, err = None, e
+        oks = [None] * world
+        dist.all_gather_object(oks, bus is not None, group=self.group)
+        if rank == self.src and bus is not None:
+            bus.unlink()                       # every rank holds its mapping (or gave up): drop the name
+        if not all(oks):
+            if bus is not None:
+                bus.close()
+            log.warning("TP step bus unavailable (%s); stepping over broadcasts", err)
+            return None
+        return bus
 
     def _bcast(self, t: torch.Tensor) -> None:
         import torch.distributed as dist
@@ -184,54 +243,107 @@ class TPSync:
         dist.broadcast(t, src=self.src, group=self.group)
 
     def send(self, msg) -> None:
+        import pickle
+
         import torch.distributed as dist
 
-        self.buf[:8].fill_(0)
-        self.buf[0] = self.OBJ
-        self._bcast(self.buf[:self.prefix])
-        obj = [msg]
-        dist.broadcast_object_list(obj, src=self.src, group=self.group)
         self.stats["object_steps"] += 1
+        if self.bus is not None:
+            data = pickle.dumps(msg, protocol=pickle.HIGHEST_PROTOCOL)
+            head = np.zeros(8, np.int32)
+            if 32 + len(data) <= self.bus.slot_bytes:
+                head[0] = self.OBJ
+                self.bus.publish(head.tobytes() + data)
+                return
+            head[0] = self.OBJ_BIG
+            self.bus.publish(head)
+        else:
+            self.buf[:8].fill_(0)
+            self.buf[0] = self.OBJ
+            self._bcast(self.buf[:self.prefix])
+        dist.broadcast_object_list([msg], src=self.src, group=self.group)
 
-    def send_decode(self, ids, pos, slots, bt, ctx, spec, graph: bool) -> None:
-        B, W = len(ids), bt.shape[1]
+    def send_decode(self, ids, pos, slots, bt, ctx, spec, graph: bool, ingraph: bool = False) -> None:
+        """``ids`` None: the previous replay's in-graph arg-max feeds this step (look-ahead)."""
+        B, W = len(pos), bt.shape[1]
         if spec["inv"] is not None or spec["pen"] is not None or 4 * B + B * W > self.capacity:
-            self.send(("decode", ids, pos, slots, bt, ctx, spec, graph))
+            self.send(("decode", ids, pos, slots, bt, ctx, spec, graph, ingraph))
             return
         n = 8 + 4 * B + B * W
+        flags = (self.F_GRAPH if graph else 0) | (self.F_DEV_IDS if ids is None else 0) | \
+            (self.F_INGRAPH if ingraph else 0)
         msg = np.zeros(n, np.int32)
-        msg[:8] = [self.DECODE, B, W, spec["k"], int(graph), n, 0, 0]
-        msg[8:] = np.concatenate([np.asarray(ids, np.int64).astype(np.int32), np.asarray(pos, np.int32),
-                                  np.asarray(slots, np.int64).astype(np.int32), np.asarray(ctx, np.int32),
-                                  np.asarray(bt, np.int32).reshape(-1)])
+        msg[:8] = [self.DECODE, B, W, spec["k"], flags, n, 0, 0]
+        if ids is not None:
+            msg[8:8 + B] = np.asarray(ids, np.int64).astype(np.int32)
+        msg[8 + B:] = np.concatenate([np.asarray(pos, np.int32), np.asarray(slots, np.int64).astype(np.int32),
+                                      np.asarray(ctx, np.int32), np.asarray(bt, np.int32).reshape(-1)])
+        self.stats["tensor_steps"] += 1
+        if self.bus is not None:
+            self.bus.publish(msg)
+            return
         self.buf[:n].copy_(torch.from_numpy(msg), non_blocking=self.device.type == "cuda")
         self._bcast(self.buf[:self.prefix])
         if n > self.prefix:
             self._bcast(self.buf[self.prefix:n])
             self.stats["two_part_steps"] += 1
-        self.stats["tensor_steps"] += 1
 
-    def recv(self):
-        import torch.distributed as dist
-
-        self._bcast(self.buf[:self.prefix])
-        p = self.buf[:self.prefix].cpu().numpy()
+    def _parse_decode(self, p: np.ndarray):
         h = p[:8].tolist()
-        if h[0] == self.OBJ:
-            obj = [None]
-            dist.broadcast_object_list(obj, src=self.src, group=self.group)
-            return obj[0]
-        B, W, k, graph, n = h[1], h[2], h[3], bool(h[4]), h[5]
-        if n > self.prefix:
-            self._bcast(self.buf[self.prefix:n])
-            p = self.buf[:n].cpu().numpy()
+        B, W, k, flags = h[1], h[2], h[3], h[4]
         p = p[8:8 + 4 * B + B * W]
-        ids = p[:B].astype(np.int64)
+        ids = None if flags & self.F_DEV_IDS else p[:B].astype(np.int64)
         pos = p[B:2 * B].copy()
         slots = p[2 * B:3 * B].astype(np.int64)
         ctx = p[3 * B:4 * B].copy()
         bt = p[4 * B:].reshape(B, W).copy()
-        return ("decode", ids, pos, slots, bt, ctx, {"k": k, "inv": None, "pen": None, "pen_ids": None}, graph)
+        return ("decode", ids, pos, slots, bt, ctx, {"k": k, "inv": None, "pen": None, "pen_ids": None},
+                bool(flags & self.F_GRAPH), bool(flags & self.F_INGRAPH))
+
+    def _recv_obj(self):
+        import torch.distributed as dist
+
+        obj = [None]
+        dist.broadcast_object_list(obj, src=self.src, group=self.group)
+        return obj[0]
+
+    def recv(self):
+        if self.bus is not None:
+            import pickle
+
+            from ..parallel.step_bus import BusClosed
+
+            while True:
+                try:
+                    m = self.bus.next(timeout_ms=1000)
+                except BusClosed:
+                    return ("stop",)
+                if m is not None:
+                    break
+                if not self.bus.writer_alive():
+                    return ("stop",)
+            op = int(np.frombuffer(m[:4], np.int32)[0])
+            if op == self.OBJ:
+                return pickle.loads(m[32:])     # written by this group's own leader process
+            if op == self.OBJ_BIG:
+                return self._recv_obj()
+            return self._parse_decode(np.frombuffer(m, np.int32))
+        self._bcast(self.buf[:self.prefix])
+        p = self.buf[:self.prefix].cpu().numpy()
+        self.stats["d2h"] += 1
+        if int(p[0]) == self.OBJ:
+            return self._recv_obj()
+        n = int(p[5])
+        if n > self.prefix:
+            self._bcast(self.buf[self.prefix:n])
+            p = self.buf[:n].cpu().numpy()
+            self.stats["d2h"] += 1
+        return self._parse_decode(p)
+
+    def close(self) -> None:
+        if self.bus is not None:
+            self.bus.close()
+            self.bus = None
 
 
 def tp_sync_capacity(max_batch: int, max_position: int) -> int:
@@ -248,11 +360,17 @@ class DecodeGraphs:
     fixed width, cache slots) filled by ONE H2D copy from a pinned staging buffer; padded
     rows use slot -1 (no cache write) and context 1, and their logits are ignored.
 
-    Without TP the graph also holds the greedy sampler: the row top-8 candidates + row lse go
-    to one packed result buffer (one D2H per step) and the arg-max token is written straight
-    into the batch bucket's token-id buffer, which every graph of that bucket embeds from --
-    so the NEXT step can be launched before the host has read this one
-    (:meth:`launch` with ``ids=None``; LLMEngine's look-ahead decode).  Staging and result
+    The graph also holds the greedy sampler: the row top-8 candidates + row lse go to one
+    packed result buffer (one D2H per step) and the arg-max token is written straight into the
+    batch bucket's token-id buffer, which every graph of that bucket embeds from -- so the NEXT
+    step can be launched before the host has read this one (:meth:`launch` with ``ids=None``;
+    LLMEngine's look-ahead decode).  Under TP the vocab-parallel merge is captured too: each
+    rank's shard top-8 + lse go into its row of a [world, B, 20] fp32 block, ONE all-reduce
+    (the IPC one-shot kernel) gives every rank every shard's candidates, and the global top-8,
+    the lse of the shard lse's and the arg-max are computed on every rank identically -- so the
+    followers never read anything back and look-ahead works under TP.  The last word of the
+    result buffer is the IPC all-reduce error flag, copied after the step's last all-reduce:
+    the leader sees it in the same D2H as the tokens, before emitting them.  Staging and result
     buffers are double-buffered and fenced by the event of the launch that last used them.
     """
 
@@ -268,7 +386,7 @@ class DecodeGraphs:
         self.graphs: dict[tuple, dict] = {}
         self.ids: dict[int, torch.Tensor] = {}       # batch bucket -> device token ids (shared by its graphs)
         self.pool = None
-        self.in_graph_sampler = not llm.tp.enabled
+        self.in_graph_sampler = not llm.tp.enabled or os.environ.get("LUMEN_TP_INGRAPH_SAMPLER", "1") == "1"
         self._stream = None     # the capture stream, private to this instance (see _capture_stream)
 
     def _bucket(self, B: int) -> int:
@@ -330,7 +448,12 @@ class DecodeGraphs:
             self.ids[Bp] = torch.zeros(Bp, dtype=torch.long, device=d)
         ids = self.ids[Bp]
         k = self.K_GREEDY
-        res = torch.zeros(2 * Bp * k + Bp, dtype=torch.float32, device=d) if self.in_graph_sampler else None
+        res = torch.zeros(2 * Bp * k + Bp + 1, dtype=torch.float32, device=d) if self.in_graph_sampler else None
+        tp = self.llm.tp
+        KP = 2 * k + 4                      # per-row candidate record: k values, k ids, lse, pad to 16 B
+        gat = torch.zeros((tp.world, Bp, KP), dtype=torch.float32, device=d) if res is not None and tp.enabled \
+            else None
+        loc = torch.zeros(2 * Bp * k + Bp, dtype=torch.float32, device=d) if gat is not None else None
         ws: dict = {}
 
         def run():
@@ -338,8 +461,29 @@ class DecodeGraphs:
             if res is not None:
                 v = res[:Bp * k].view(Bp, k)
                 i = res[Bp * k:2 * Bp * k].view(torch.int32).view(Bp, k)
+                lse = res[2 * Bp * k:2 * Bp * k + Bp]
                 hip = ops.hip_ops()
-                hip.row_topk(logits, k, 1.0, v, i, res[2 * Bp * k:], int(self.llm.v0))
+                if gat is None:
+                    hip.row_topk(logits, k, 1.0, v, i, lse, int(self.llm.v0))
+                else:
+                    lv = loc[:Bp * k].view(Bp, k)
+                    li = loc[Bp * k:2 * Bp * k].view(torch.int32).view(Bp, k)
+                    hip.row_topk(logits, k, 1.0, lv, li, loc[2 * Bp * k:], int(self.llm.v0))
+                    gat.zero_()
+                    own = gat[tp.rank]
+                    own[:, :k].copy_(lv)
+                    own[:, k:2 * k].copy_(li)                 # global vocab ids < 2^24: exact in fp32
+                    own[:, 2 * k].copy_(loc[2 * Bp * k:])
+                    self.llm._all_reduce(gat)
+                    vals = gat[:, :, :k].permute(1, 0, 2).reshape(Bp, tp.world * k)
+                    gids = gat[:, :, k:2 * k].permute(1, 0, 2).reshape(Bp, tp.world * k)
+                    tv, order = torch.topk(vals, k, dim=1)
+                    v.copy_(tv)
+                    i.copy_(torch.gather(gids, 1, order))
+                    lse.copy_(torch.logsumexp(gat[:, :, 2 * k], 0))
+                    comm = getattr(self.llm, "comm", None)
+                    if comm is not None:
+                        comm.error_into(res[2 * Bp * k + Bp:].view(torch.int32))
                 ids.copy_(i[:, 0])                                   # greedy next token, on the device
             return logits
 
@@ -369,10 +513,10 @@ class DecodeGraphs:
         key = (self._bucket(B), self._width(width))
         return self.graphs[key] if key in self.graphs else self._capture(*key)
 
-    def launch(self, ids, pos, slots, bt, ctx) -> dict:
+    def launch(self, ids, pos, slots, bt, ctx, fetch: bool = True) -> dict:
         """Stage + replay one step (host arrays; ``ids=None``: the token ids the previous
         replay of this batch bucket wrote on the device).  Returns a handle for
-        :meth:`tokens` / :meth:`logits`."""
+        :meth:`tokens` / :meth:`logits`.  ``fetch=False`` (TP followers): no result copy."""
         B = len(pos)
         e = self._entry(B, bt.shape[1])
         Bp, W = e["Bp"], e["W"]
@@ -398,7 +542,7 @@ class DecodeGraphs:
             hi[:B] = ids
             self.ids[Bp].copy_(e["h_ids"][par], non_blocking=True)
         e["g"].replay()
-        if e["res"] is not None:
+        if e["res"] is not None and fetch:
             e["h_res"][par].copy_(e["res"], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
@@ -406,11 +550,13 @@ class DecodeGraphs:
         return {"e": e, "par": par, "B": B, "ev": ev}
 
     def tokens(self, h: dict):
-        """(values [B, 8], ids [B, 8], lse [B]) numpy of a launched step (waits for it)."""
+        """(values [B, 8], ids [B, 8], lse [B]) numpy of a launched step (waits for it); sets
+        ``h["err"]`` from the step's all-reduce error word (TP)."""
         e, B = h["e"], h["B"]
         h["ev"].synchronize()
         r = e["h_res"][h["par"]]
         Bp, k = e["Bp"], self.K_GREEDY
+        h["err"] = int(r[2 * Bp * k + Bp:].view(torch.int32)[0])
         v = r[:Bp * k].view(Bp, k)[:B].numpy()
         i = r[Bp * k:2 * Bp * k].view(torch.int32).view(Bp, k)[:B].numpy()
         return v, i, r[2 * Bp * k:2 * Bp * k + B].numpy()
@@ -480,6 +626,7 @@ class LLMEngine:
                 self.sync.send(("stop",))
             except Exception:  # pragma: no cover
                 pass
+            self.sync.close()
 
     # ------------------------------------------------------------------ loop
     def _emit(self, r: GenRequest, tok: int) -> bool:
@@ -591,18 +738,22 @@ class LLMEngine:
                 self._fail([r], e)
 
     def _greedy_graph_ok(self, reqs, spec) -> bool:
-        """the in-graph greedy sampler serves this step: single rank, graphs on, every request
-        greedy without repetition penalty, batch and table within the graph buckets"""
+        """the in-graph greedy sampler serves this step: graphs on, every request greedy without
+        repetition penalty, batch and table within the graph buckets (any TP size)"""
         g = self.graphs
-        return (g is not None and g.in_graph_sampler and self.sync is None and _LOOKAHEAD
+        return (g is not None and g.in_graph_sampler and _LOOKAHEAD
                 and spec["inv"] is None and spec["pen"] is None and spec["k"] <= g.K_GREEDY
                 and len(reqs) <= g.buckets[-1])
 
     def _graph_ready(self, reqs) -> bool:
-        """the step's graph exists or captures now (a capture failure disables graphs)"""
+        """the step's graph exists or captures now (a capture failure disables graphs).  Under
+        TP the capture runs collectives, so it happens inside the launch, after the followers
+        received the step (they capture the same graph at the same point)."""
         w = max(len(self.kv.blocks.table(r.rid)) for r in reqs)
         if w > self.graphs.max_blocks:
             return False
+        if self.sync is not None:
+            return True
         try:
             self.graphs._entry(len(reqs), w)
             return True
@@ -646,9 +797,13 @@ class LLMEngine:
                 h = pend[1]
             else:
                 ids = np.array([r.tokens[-1] for r in reqs], np.int64)
-                h = self.graphs.launch(ids, *self._step_inputs(reqs, 0))
-            nxt = self.graphs.launch(None, *self._step_inputs(reqs, 1)) if self._can_look_ahead(reqs) else None
+                h = self._launch_greedy(ids, self._step_inputs(reqs, 0), spec)
+            nxt = self._launch_greedy(None, self._step_inputs(reqs, 1), spec) if self._can_look_ahead(reqs) else None
             _v, i, _lse = self.graphs.tokens(h)
+            if h.get("err"):
+                # an IPC all-reduce of this step gave up on a peer: its tokens are garbage
+                self._pending = None
+                raise TPGroupUnavailable("tensor-parallel peer not responding (IPC all-reduce timed out)")
             toks = [int(i[b, 0]) for b in range(B)]
             self.stats["decode_steps"] += 1
             still = []
@@ -676,8 +831,8 @@ class LLMEngine:
         toks = self.sampler.pick(self.sampler.candidates(logits, spec), reqs)
         self.stats["decode_steps"] += 1
         comm = getattr(self.llm, "comm", None)
-        if comm is not None and self.stats["decode_steps"] % 16 == 0:
-            comm.check()    # the tokens' D2H already waited for the step: the flag read costs a copy only
+        if comm is not None:
+            comm.check()    # before emitting; the tokens' D2H already waited for the step
         still = []
         for r, t in zip(reqs, toks):
             r.ctx += 1
@@ -686,6 +841,20 @@ class LLMEngine:
             else:
                 still.append(r)
         self._running = still
+
+    def _launch_greedy(self, ids, inputs, spec) -> dict:
+        """One in-graph-sampled step (``ids`` None: look-ahead, ids from the device); under TP the
+        followers get the descriptor first and replay the same graph."""
+        if self.sync is not None:
+            self.sync.send_decode(ids, *inputs, spec, graph=True, ingraph=True)
+        try:
+            return self.graphs.launch(ids, *inputs)
+        except Exception:
+            if self.sync is not None:
+                raise            # TP ranks must not diverge
+            log.warning("hipGraph decode disabled", exc_info=True)
+            self.graphs = None
+            raise
 
     def _decode_step(self, ids, pos, slots, bt, ctx, graph: bool = True) -> torch.Tensor:
         d = self.device
@@ -697,9 +866,8 @@ class LLMEngine:
                     raise            # TP ranks must not diverge: surface instead of falling back
                 log.warning("hipGraph decode disabled: %s", e)
                 self.graphs = None
-        return self.llm.decode(torch.from_numpy(ids).to(d), torch.from_numpy(pos).to(d),
-                               torch.from_numpy(slots).to(d), self.kv, torch.from_numpy(bt).to(d),
-                               torch.from_numpy(ctx).to(d), workspace=self._ws)
+        return self.llm.decode(h2d(ids, d), h2d(pos, d), h2d(slots, d), self.kv, h2d(bt, d), h2d(ctx, d),
+                               workspace=self._ws)
 
     def _loop(self) -> None:
         if self.device.type == "cuda":
@@ -726,8 +894,11 @@ class LLMEngine:
 
 
 def follower_loop(llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.Tensor], sync: TPSync,
-                  max_batch: int = 64) -> None:
-    """Non-zero TP ranks: replay rank 0's steps so every collective is matched."""
+                  max_batch: int = 64) -> dict:
+    """Non-zero TP ranks: replay rank 0's steps so every collective is matched.  Greedy decode
+    steps (flag ``ingraph``) are a descriptor read from the step bus + one graph launch: the
+    graph samples on the device, so the follower never reads a result back.  Returns the
+    follower's counters (also written as JSON to ``$LUMEN_TP_FOLLOWER_STATS`` when set)."""
     sampler = Sampler(llm)
     ws: dict = {}
     xs: dict = {}                            # rid -> prefill embeddings of prompts being chunk-prefilled
@@ -736,11 +907,12 @@ def follower_loop(llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.
     if dev.type == "cuda" and os.environ.get("LUMEN_HIP_GRAPHS", "1") == "1" and \
             os.environ.get("LUMEN_TP_GRAPHS", "1") == "1":
         graphs = DecodeGraphs(llm, kv, max_batch, -(-llm.cfg.max_position // 64))   # the leader's buckets
+    stats = {"decode_steps": 0, "ingraph_steps": 0, "lookahead_steps": 0, "prefill_chunks": 0}
     while True:
         msg = sync.recv()
         kind = msg[0]
         if kind == "stop":
-            return
+            break
         with torch.no_grad():
             if kind == "pbuild":
                 _, rid, args = msg
@@ -750,13 +922,30 @@ def follower_loop(llm, kv: PagedKVCache, prefill_builder: Callable[[Any], torch.
                 x = xs[rid] if not last else xs.pop(rid)
                 logits = llm.prefill(x[s:e], kv, h2d(slots, dev), start_pos=s,
                                      prefix_blocks=h2d(tab, dev) if tab is not None else None)
+                stats["prefill_chunks"] += 1
                 if last:
                     sampler.candidates(logits, spec)
             elif kind == "decode":
-                _, ids, pos, slots, bt, ctx, spec, graph = msg
+                _, ids, pos, slots, bt, ctx, spec, graph, ingraph = msg
+                stats["decode_steps"] += 1
+                if graph and graphs is not None and ingraph:
+                    graphs.launch(ids, pos, slots, bt, ctx, fetch=False)
+                    stats["ingraph_steps"] += 1
+                    stats["lookahead_steps"] += ids is None
+                    continue
                 if graph and graphs is not None:
                     logits = graphs.run(ids, pos, slots, bt, ctx)
                 else:
                     logits = llm.decode(h2d(ids, dev), h2d(pos, dev), h2d(slots, dev), kv, h2d(bt, dev),
                                         h2d(ctx, dev), workspace=ws)
                 sampler.candidates(logits, spec)
+    stats["d2h"] = sync.stats["d2h"] + sampler.d2h
+    stats["transport"] = sync.transport
+    path = os.environ.get("LUMEN_TP_FOLLOWER_STATS")
+    if path:
+        import json
+
+        with open(f"{path}.rank{llm.tp.rank}", "w") as f:
+            json.dump(stats, f)
+    sync.close()
+    return stats

@@ -225,3 +225,49 @@ def test_clip_dp_serving_matches_single_process(tmp_path, monkeypatch):
         assert dp._pool.stats["tasks"] >= 4 and abs(dp.get_temperature() - single.get_temperature()) < 1e-3
     finally:
         dp.close()
+
+
+def _vlm_shard_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                      LOCAL_RANK=str(rank))
+    from lumen_amd.models.vlm import VLM, VLM_PRESETS
+    from lumen_amd.parallel import destroy, init_distributed
+
+    st = init_distributed(tp_size=2, device=torch.device("cpu"), timeout_s=60)
+    try:
+        cfg = VLM_PRESETS["tiny"]
+        m = VLM(cfg, st.tp_info(), dtype=torch.float32, device="cpu")
+        m.random_init(0)
+        g = torch.Generator().manual_seed(5)
+        imgs = [torch.randint(0, 256, (20 + 3 * i, 30, 3), generator=g, dtype=torch.uint8) for i in range(3)]
+        it = cfg.image_token_id
+        ids = [1, it, 5, 6, it, 7, it, 9]                 # three images, not contiguous
+        full = m.build_prefill(ids, imgs if rank == 0 else [], n_images=3)
+        shard = m.build_prefill(ids, imgs, shard_images=True)
+        q.put({"rank": rank, "same": bool(torch.equal(full, shard)), "rows": int(full.shape[0])})
+    finally:
+        destroy()
+
+
+def test_vlm_tp_image_sharding_matches_rank0_tower():
+    """TP=2, a three-image prompt: with ``shard_images`` each rank runs the vision tower on its
+    share of the images and one all-reduce assembles the features -- the prefill input equals the
+    rank-0-tower + broadcast path on both ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_vlm_shard_worker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=180) for _ in ps]
+    for p in ps:
+        p.join(60)
+    assert all(p.exitcode == 0 for p in ps)
+    assert all(r["same"] for r in out), out
+    assert out[0]["rows"] == 5 + 3 * _tiny_image_tokens()
+
+
+def _tiny_image_tokens():
+    from lumen_amd.models.vlm import VLM_PRESETS
+
+    return VLM_PRESETS["tiny"].num_image_tokens

@@ -1,8 +1,10 @@
 """Tensor-parallel VLM decode on MI355X: TP=2 (two ranks sharing the box's one GPU, gloo for the
-host-side step broadcast / candidate gather, the IPC one-shot all-reduce inside the decode
-graphs) with hipGraph-captured decode steps generates the same greedy text as TP=1.  Decode
-steps travel as fixed int32 descriptors; only rank 0 decodes the image and runs the vision
-tower (its features are broadcast).  CPU twin: test_parallel_cpu.py::test_vlm_tensor_parallel_*."""
+control collectives, the IPC one-shot all-reduce inside the decode graphs) with hipGraph-captured
+decode steps generates the same greedy text as TP=1.  Decode steps travel as int32 descriptors
+over the host shared-memory step bus; the greedy sampler (vocab-parallel top-k merge through one
+in-graph all-reduce) runs inside the graph, so the follower makes ZERO device->host copies per
+decode step and the leader runs look-ahead steps under TP.  CPU twin:
+test_parallel_cpu.py::test_vlm_tensor_parallel_*."""
 import multiprocessing as mp
 import os
 
@@ -15,6 +17,7 @@ def _leader(cache, tp, q):
     import json as _json
 
     os.environ["LUMEN_TP_SIZE"] = str(tp)
+    os.environ["LUMEN_TP_FOLLOWER_STATS"] = os.path.join(cache, "follower_stats")
     os.environ["LUMEN_DIST_BACKEND"] = "gloo"          # RCCL refuses two ranks on one device
     from lumen_amd.resources.validator import config_from_dict
     from lumen_amd.services.vlm import GeneralFastVLMService
@@ -38,7 +41,8 @@ def _leader(cache, tp, q):
             outs.append(_json.loads(body)["text"])
         eng = s.backend.engine
         q.put({"texts": outs, "tp": s.backend.tp.world, "graphs": eng.graphs is not None and len(eng.graphs.graphs) > 0,
-               "sync": dict(eng.sync.stats) if eng.sync is not None else None})
+               "sync": dict(eng.sync.stats, transport=eng.sync.transport) if eng.sync is not None else None,
+               "lookahead": eng.stats.get("lookahead_steps", 0)})
     except BaseException as e:  # noqa: BLE001
         q.put({"error": repr(e)})
     finally:
@@ -61,5 +65,14 @@ def test_vlm_tp2_graphs_match_tp1(tmp_path):
         assert p.exitcode == 0
     assert res[2]["tp"] == 2 and res[1]["tp"] == 1
     assert res[1]["graphs"] and res[2]["graphs"]                     # decode replayed from hipGraphs on both
-    assert res[2]["sync"]["tensor_steps"] >= 10
+    assert res[2]["sync"]["tensor_steps"] >= 10 and res[2]["sync"]["transport"] == "bus"
     assert res[2]["texts"] == res[1]["texts"]
+    assert res[2]["lookahead"] > 0                                  # look-ahead steps under TP
+    import json
+
+    fol = json.loads((tmp_path / "follower_stats.rank1").read_text())
+    assert fol["transport"] == "bus" and fol["decode_steps"] >= 10
+    assert fol["ingraph_steps"] >= 10 and fol["lookahead_steps"] > 0
+    # prefill's last chunk still gathers candidates through gloo (one host copy per request);
+    # decode steps add none
+    assert fol["d2h"] <= fol["prefill_chunks"]

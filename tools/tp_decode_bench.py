@@ -45,6 +45,7 @@ def main():
     from lumen_amd.utils.image import encode_jpeg
 
     cache = tempfile.mkdtemp(prefix="lumen_tp_")
+    os.environ["LUMEN_TP_FOLLOWER_STATS"] = os.path.join(cache, "follower_stats")
     write_vlm_model(os.path.join(cache, "models", "vlm-bench"), "vlm-bench", preset=a.preset, weights=False)
     cfg = {"metadata": {"version": "1.0.0", "region": "other", "cache_dir": cache},
            "deployment": {"mode": "single", "service": "vlm"}, "server": {"port": 50559, "host": "127.0.0.1"},
@@ -79,6 +80,12 @@ def main():
                           "data": "synthetic (random-init weights, random 1024x768 JPEG)"}), flush=True)
     finally:
         s.close()
+    fol = {}
+    for r in range(1, a.tp):
+        p = os.path.join(cache, f"follower_stats.rank{r}")
+        if os.path.exists(p):
+            fol[r] = json.load(open(p))
+    print(json.dumps({"follower_stats": fol, "leader_lookahead_steps": eng.stats.get("lookahead_steps", 0)}), flush=True)
 
 
 if __name__ == "__main__":
