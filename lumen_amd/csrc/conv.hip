@@ -171,7 +171,11 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_igemm_kernel(ConvArgs a, Gem
           f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cc + q * 4);
           v[q * 4 + 0] = t[0]; v[q * 4 + 1] = t[1]; v[q * 4 + 2] = t[2]; v[q * 4 + 3] = t[3];
         }
-        epi_store16(v, m0 + wm * TM + i * 16 + rr, n0 + wn * TN + cc, M, Nn, a.out, a.ldo, ep);
+        if (ep.aff_s)
+          epi_store16_t<false, true>(v, m0 + wm * TM + i * 16 + rr, n0 + wn * TN + cc, M, Nn, a.out, a.ldo, ep,
+                                     c_rsrc(a.out));
+        else
+          epi_store16(v, m0 + wm * TM + i * 16 + rr, n0 + wn * TN + cc, M, Nn, a.out, a.ldo, ep);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -174,7 +174,8 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
         const f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cc + q * 4);
         v[q * 4 + 0] = t[0]; v[q * 4 + 1] = t[1]; v[q * 4 + 2] = t[2]; v[q * 4 + 3] = t[3];
       }
-      epi_store16_t<false>(v, m, n, M, N, a.out, a.ldo, ep, crs);
+      if (ep.aff_s) epi_store16_t<false, true>(v, m, n, M, N, a.out, a.ldo, ep, crs);
+      else epi_store16_t<false>(v, m, n, M, N, a.out, a.ldo, ep, crs);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   });
@@ -205,7 +206,8 @@ bool conv_lds_ok(const ConvArgs& a) {
 }
 
 // variant: 0 auto; 1 = 128x128 3 stages 8 waves, 2 = 128x128 2 stages 4 waves, 3 = 128x64 3 stages 4 waves,
-// 4 = 128x64 2 stages 4 waves (two workgroups per CU)
+// 4 = 128x64 2 stages 4 waves (two workgroups per CU), 5 = 128x128 4 stages 4 waves, 6 = 128x128 3 stages
+// 4 waves, 7 = 128x64 4 stages 4 waves, 8 = 128x128 4 stages 8 waves
 hipError_t conv2d_lds(const ConvArgs& a, const GemmEpi& ep, int variant, hipStream_t stream) {
   if (!conv_lds_ok(a)) return hipErrorInvalidValue;
   if (variant == 0) {
@@ -218,6 +220,10 @@ hipError_t conv2d_lds(const ConvArgs& a, const GemmEpi& ep, int variant, hipStre
     case 1: return launch_conv_lds<3, 4, 128>(a, ep, stream);
     case 2: return launch_conv_lds<2, 2, 128>(a, ep, stream);
     case 3: return launch_conv_lds<3, 2, 64>(a, ep, stream);
+    case 5: return launch_conv_lds<4, 2, 128>(a, ep, stream);
+    case 6: return launch_conv_lds<3, 2, 128>(a, ep, stream);
+    case 7: return launch_conv_lds<4, 2, 64>(a, ep, stream);
+    case 8: return launch_conv_lds<4, 4, 128>(a, ep, stream);
     default: return launch_conv_lds<2, 2, 64>(a, ep, stream);
   }
 }

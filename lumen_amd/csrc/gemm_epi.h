@@ -47,6 +47,16 @@ struct GemmEpi {
   //   first, in place of alpha and bias (the host passes neither).
   const float* row_aff;
   const float* col_aff;
+  // ---- per-channel affine of the FINAL value (after residual / post-activation), fp32 [N] scale /
+  // shift, applied to the bf16-rounded output: written to aff_out (second output, ld_aff) or, when
+  // aff_out is null, in place of the plain output.  IResNet: the next block's pre-conv BatchNorm
+  // (it precedes a zero-padded conv, so it cannot fold into weights) produced by the conv that
+  // writes the block input, instead of a separate channel-affine pass.  Honoured by the
+  // implicit-GEMM convolutions (epi_store16_t<WT, true>).
+  const float* aff_s;
+  const float* aff_t;
+  uint16_t* aff_out;
+  int64_t ld_aff;
 };
 
 // MX operand / outputs of the W8A8 prefill GEMM (gemm_f8.hip::gemm_mx; fields documented there)
@@ -177,8 +187,9 @@ __device__ __forceinline__ void add8(float* v, const uint16_t* p) {
   for (int q = 0; q < 8; ++q) v[q] += f[q];
 }
 
-// Apply the epilogue to 16 consecutive columns [n, n+16) of row m and store.
-template <bool WT>
+// Apply the epilogue to 16 consecutive columns [n, n+16) of row m and store.  AFF: the output
+// affine (GemmEpi::aff_s) is live (bf16 output, full 16-column pieces: the conv host code checks).
+template <bool WT, bool AFF = false>
 __device__ __forceinline__ void epi_store16_t(float* v, int m, int n, int M, int N, void* __restrict__ C,
                                               int64_t ldc, const GemmEpi& ep, __amdgpu_buffer_rsrc_t rs) {
   if (m >= M || n >= N) return;
@@ -255,6 +266,25 @@ __device__ __forceinline__ void epi_store16_t(float* v, int m, int n, int M, int
   if (ep.post_act) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) v[q] = fmaxf(v[q], 0.f);
+  }
+  if constexpr (AFF) {
+    float w[16];
+    const f32x4_t* s4 = (const f32x4_t*)(ep.aff_s + n);
+    const f32x4_t* t4 = (const f32x4_t*)(ep.aff_t + n);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4_t sq = s4[q], tq = t4[q];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[4 * q + r] = bf2f(f2bf(v[4 * q + r])) * sq[r] + tq[r];
+    }
+    if (ep.aff_out) {
+      uint16_t* o2 = ep.aff_out + orow * ep.ld_aff + n;
+      *(u32x4_t*)o2 = pack8(w);
+      *(u32x4_t*)(o2 + 8) = pack8(w + 8);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = w[q];
+    }
   }
   if (ep.out_f32) {
     float* o = (float*)C + orow * ldc + n;

@@ -803,7 +803,8 @@ static int64_t pixel_stride(const at::Tensor& t, const char* name) {
 void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
             const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& prelu, int64_t act,
             std::vector<int64_t> stride, std::vector<int64_t> padding, std::vector<int64_t> dilation, at::Tensor out,
-            int64_t tile, int64_t post_act) {
+            int64_t tile, int64_t post_act, const c10::optional<at::Tensor>& aff_scale,
+            const c10::optional<at::Tensor>& aff_shift, const c10::optional<at::Tensor>& aff_out) {
   check_gpu(x, "x");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv2d: bf16");
   const int64_t ldx = pixel_stride(x, "x");
@@ -840,6 +841,23 @@ void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Te
   }
   TORCH_CHECK(post_act == 0 || post_act == 3, "conv2d: post_act supports none / relu");
   ep.post_act = (int)post_act;
+  if (aff_scale.has_value() && aff_scale->defined()) {
+    // output affine (next layer's pre-conv BatchNorm): fp32 [Cout] scale / shift, bf16 output
+    TORCH_CHECK(aff_shift.has_value() && aff_shift->defined(), "conv2d: aff_scale needs aff_shift");
+    for (const at::Tensor* t : {&*aff_scale, &*aff_shift})
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == Cout &&
+                      (reinterpret_cast<uintptr_t>(t->data_ptr()) % 16) == 0,
+                  "conv2d: aff scale / shift fp32 [Cout] contiguous, 16-byte aligned");
+    TORCH_CHECK(out.scalar_type() == at::kBFloat16, "conv2d: output affine needs a bf16 output");
+    ep.aff_s = aff_scale->data_ptr<float>();
+    ep.aff_t = aff_shift->data_ptr<float>();
+    if (aff_out.has_value() && aff_out->defined()) {
+      TORCH_CHECK(aff_out->scalar_type() == at::kBFloat16 && aff_out->size(0) == N && aff_out->size(1) == Ho &&
+                      aff_out->size(2) == Wo && aff_out->size(3) == Cout, "conv2d: aff_out shape / dtype");
+      ep.ld_aff = pixel_stride(*aff_out, "aff_out");
+      ep.aff_out = reinterpret_cast<uint16_t*>(aff_out->data_ptr());
+    }
+  }
   lumen::ConvArgs a{};
   a.x = bf(x); a.w = bf(w); a.out = out.data_ptr(); a.ldx = ldx; a.ldo = ldo;
   a.N = (int)N; a.H = (int)H; a.W = (int)W; a.Cin = (int)Cin; a.Cout = (int)Cout; a.KH = (int)KH; a.KW = (int)KW;
@@ -963,7 +981,8 @@ TORCH_LIBRARY(lumen, m) {
   m.def("row_topk(Tensor scores, int k, float scale, Tensor(v!) out_v, Tensor(i!) out_i, Tensor(l!)? out_lse, "
         "int index_offset) -> ()");
   m.def("conv2d(Tensor x, Tensor w, Tensor? bias, Tensor? residual, Tensor? prelu, int act, int[] stride, "
-        "int[] padding, int[] dilation, Tensor(o!) out, int tile, int post_act=0) -> ()");
+        "int[] padding, int[] dilation, Tensor(o!) out, int tile, int post_act=0, Tensor? aff_scale=None, "
+        "Tensor? aff_shift=None, Tensor(b!)? aff_out=None) -> ()");
   m.def("conv2d_dw(Tensor x, Tensor w, Tensor? bias, int act, int[] stride, int[] padding, int[] dilation, "
         "Tensor(o!) out) -> ()");
   m.def("channel_affine(Tensor x, Tensor scale, Tensor shift, Tensor(o!) out, int act, Tensor? prelu) -> ()");

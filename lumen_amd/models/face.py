@@ -33,6 +33,8 @@ from .. import ops
 from ..ops import cnn
 from .layers import ChannelAffine, ConvBN, Linear, fold_bn
 
+_FUSED_BN = __import__("os").environ.get("LUMEN_IRES_FUSED_BN", "1") != "0"
+
 
 # =============================================================================== recogniser
 @dataclass
@@ -57,11 +59,18 @@ class IBasicBlock(nn.Module):
         self.conv2 = ConvBN(cout, cout, 3, stride)                 # conv2 + bn3 (+ shortcut)
         self.down = ConvBN(cin, cout, 1, stride, pad=0) if (stride != 1 or cin != cout) else None
 
-    def forward(self, x):
+    def forward(self, x, xb=None, next_aff=None, next_in_place: bool = False):
+        """x: block input; xb: bn1(x) when the previous conv's epilogue already produced it.
+        ``next_aff`` (scale, shift): the next layer's pre-conv BN, emitted by conv2's epilogue as
+        a second output (returns (out, bn(out))) or, ``next_in_place``, instead of out."""
         sc = self.down(x) if self.down is not None else x
-        h = self.bn1(x)
+        h = xb if xb is not None else self.bn1(x)
         h = self.conv1(h)
-        return self.conv2(h, residual=sc)
+        if next_aff is None:
+            return self.conv2(h, residual=sc)
+        if next_in_place:
+            return self.conv2(h, residual=sc, aff=next_aff)
+        return self.conv2(h, residual=sc, aff=next_aff, aff_out=True)
 
 
 class IResNet(nn.Module):
@@ -93,11 +102,27 @@ class IResNet(nn.Module):
 
     @torch.no_grad()
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        """x: NHWC8 [F, 112, 112, 8] bf16 -> L2-normalised fp32 [F, 512]."""
-        h = self.stem(x)
-        for b in self.blocks:
-            h = b(h)
-        h = self.bn_out(h)
+        """x: NHWC8 [F, 112, 112, 8] bf16 -> L2-normalised fp32 [F, 512].
+
+        On the GPU every pre-conv BatchNorm (bn1 of each block, the final bn_out) is produced by the
+        epilogue of the conv that writes its input -- the stem / the previous block's conv2 writes
+        the block output AND its affine -- so no channel-affine pass re-reads the activations
+        (``LUMEN_IRES_FUSED_BN=0``: the separate channel_affine kernel)."""
+        if not (x.is_cuda and _FUSED_BN):
+            h = self.stem(x)
+            for b in self.blocks:
+                h = b(h)
+            h = self.bn_out(h)
+        else:
+            b0 = self.blocks[0].bn1
+            h, hb = self.stem(x, aff=(b0.scale, b0.shift), aff_out=True)
+            n = len(self.blocks)
+            for i, b in enumerate(self.blocks):
+                if i + 1 < n:
+                    nb = self.blocks[i + 1].bn1
+                    h, hb = b(h, hb, (nb.scale, nb.shift))
+                else:
+                    h = b(h, hb, (self.bn_out.scale, self.bn_out.shift), next_in_place=True)
         emb = self.fc(h.reshape(h.shape[0], -1), out_dtype=torch.float32)
         return ops.l2_normalize_(emb.contiguous())
 

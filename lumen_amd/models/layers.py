@@ -74,10 +74,13 @@ class ConvBN(nn.Module):
             self.prelu.data[: self.cout] = prelu.float().flatten().to(self.prelu.dtype)
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-                out_dtype=None) -> torch.Tensor:
+                out_dtype=None, aff: Optional[tuple] = None, aff_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``aff`` / ``aff_out``: the next layer's channel affine produced by this conv's epilogue
+        (ops.cnn.conv2d)."""
         assert x.shape[-1] == self.cin_p, f"ConvBN expects {self.cin_p} input channels, got {x.shape[-1]}"
         return cnn.conv2d(x, self.w, self.b, self.stride, self.pad, self.dilation, act=self.act, residual=residual,
-                          prelu=self.prelu, out=out, out_dtype=out_dtype, post_act=self.post_act)
+                          prelu=self.prelu, out=out, out_dtype=out_dtype, post_act=self.post_act, aff=aff,
+                          aff_out=aff_out)
 
 
 class DWConvBN(nn.Module):

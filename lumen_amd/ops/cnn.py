@@ -40,17 +40,28 @@ def conv_out_hw(H, W, KH, KW, stride, padding, dilation):
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride=1, padding=0, dilation=1,
            act=None, residual: Optional[torch.Tensor] = None, prelu: Optional[torch.Tensor] = None,
-           out: Optional[torch.Tensor] = None, out_dtype=None, tile: int = -1, post_act=None) -> torch.Tensor:
-    """out = post_act(prelu(act(conv(x, w) + bias)) + residual)   (NHWC; w [Cout, KH, KW, Cin])."""
+           out: Optional[torch.Tensor] = None, out_dtype=None, tile: int = -1, post_act=None,
+           aff: Optional[tuple] = None, aff_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = post_act(prelu(act(conv(x, w) + bias)) + residual)   (NHWC; w [Cout, KH, KW, Cin]).
+
+    ``aff`` = (scale, shift) fp32 [Cout]: a per-channel affine of the bf16-rounded result -- the
+    next layer's pre-conv BatchNorm -- written to ``aff_out`` (a second output; ``True``: allocate
+    it and return ``(out, aff_out)``) or, when ``aff_out`` is None, to ``out`` in place of the
+    plain result."""
     N, H, W, Cin = x.shape
     Cout, KH, KW, _ = w.shape
     Ho, Wo = conv_out_hw(H, W, KH, KW, stride, padding, dilation)
     if out is None:
         out = torch.empty((N, Ho, Wo, Cout), device=x.device, dtype=out_dtype or x.dtype)
+    if aff_out is True:
+        ao = torch.empty_like(out)
+        conv2d(x, w, bias, stride, padding, dilation, act, residual, prelu, out, out_dtype, tile, post_act, aff, ao)
+        return out, ao
     a = act_id(act)
     if x.is_cuda:
         hip_ops().conv2d(x, w, bias, residual, prelu, a, list(_pair(stride)), _pad_arg(padding),
-                         list(_pair(dilation)), out, int(tile), act_id(post_act))
+                         list(_pair(dilation)), out, int(tile), act_id(post_act),
+                         aff[0] if aff is not None else None, aff[1] if aff is not None else None, aff_out)
         return out
     pt, pl, pb, pr = _pads4(padding)
     y = F.conv2d(F.pad(x.float().permute(0, 3, 1, 2), (pl, pr, pt, pb)), w.float().permute(0, 3, 1, 2), None,
@@ -63,6 +74,12 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if residual is not None:
         y = y + residual.float()
     y = _act_ref(y, act_id(post_act))
+    if aff is not None:
+        z = y.to(out.dtype).float() * aff[0].float() + aff[1].float()
+        if aff_out is None:
+            y = z
+        else:
+            aff_out.copy_(z.to(aff_out.dtype))
     out.copy_(y.to(out.dtype))
     return out
 

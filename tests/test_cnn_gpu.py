@@ -41,7 +41,7 @@ def test_conv2d(N, H, W, Cin, Cout, K, s, p, d, tile):
 @pytest.mark.parametrize("N,H,W,Cin,Cout,K,s,p,d", [
     (2, 20, 20, 64, 128, 1, 1, 0, 1), (3, 28, 28, 128, 256, 3, 2, 1, 1), (2, 7, 7, 512, 512, 3, 1, 1, 1),
     (4, 56, 56, 64, 64, 3, 1, 1, 1), (2, 30, 30, 64, 48, 3, 1, 2, 2), (1, 13, 9, 192, 80, 5, 2, 2, 1)])
-@pytest.mark.parametrize("tile", [-1, 11, 12, 13, 14])
+@pytest.mark.parametrize("tile", [-1, 11, 12, 13, 14, 15, 16, 17, 18])
 def test_conv2d_lds_pipeline(N, H, W, Cin, Cout, K, s, p, d, tile):
     """Cin % 64 == 0: the LDS-DMA implicit-GEMM pipeline (conv_lds.hip; -1 picks it), incl. zero
     padding taps, stride / dilation, residual + PReLU + post-ReLU epilogues."""
@@ -57,6 +57,29 @@ def test_conv2d_lds_pipeline(N, H, W, Cin, Cout, K, s, p, d, tile):
     ref3 = cnn.conv2d(x, w, b, s, p, d, residual=r, post_act="relu")
     got3 = cnn.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), s, p, d, residual=r.to(DEV), tile=tile, post_act="relu")
     assert _rel(got3, ref3) < 1e-2 and got3.min().item() >= 0
+
+
+@pytest.mark.parametrize("Cin,tile", [(8, -1), (64, -1), (64, 12), (128, 15)])
+def test_conv2d_output_affine(Cin, tile):
+    """The next layer's channel affine emitted by the conv epilogue: as a second output next to the
+    plain result, and in place of it (both vs the fp32 reference of conv -> round -> affine)."""
+    g = torch.Generator().manual_seed(Cin + tile)
+    x = torch.randn(2, 18, 18, Cin, generator=g).bfloat16()
+    w = (torch.randn(64, 3, 3, Cin, generator=g) * (9 * Cin) ** -0.5).bfloat16()
+    b = torch.randn(64, generator=g).bfloat16()
+    r = torch.randn(2, 18, 18, 64, generator=g).bfloat16()
+    sc, sh = 1 + 0.1 * torch.randn(64, generator=g), 0.1 * torch.randn(64, generator=g)
+    ref = cnn.conv2d(x, w, b, 1, 1, 1, residual=r)
+    ref_aff = (ref.float() * sc + sh)
+    out, ao = cnn.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), 1, 1, 1, residual=r.to(DEV), tile=tile,
+                         aff=(sc.to(DEV), sh.to(DEV)), aff_out=True)
+    assert _rel(out, ref) < 1e-2 and _rel(ao, ref_aff) < 1e-2
+    # the affine of exactly the stored bf16 output
+    exact = out.float() * sc.to(DEV) + sh.to(DEV)
+    assert (ao.float() - exact).abs().max().item() <= 0.02 * exact.abs().max().item()
+    inplace = cnn.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), 1, 1, 1, residual=r.to(DEV), tile=tile,
+                         aff=(sc.to(DEV), sh.to(DEV)))
+    assert torch.equal(inplace, ao)
 
 
 def test_conv2d_into_channel_slice():

@@ -1,0 +1,68 @@
+"""Implicit-GEMM conv timing on the IResNet-100 / SCRFD layer shapes (face pipeline, batch of
+128 aligned faces = 32 images x 4): every conv_lds variant (tile 10 + v) per shape, cold-ish
+(inputs rotate over 4 buffers), HIP-event timed; prints us and TFLOP/s per (shape, variant).
+
+  python tools/conv_bench.py [--faces 128] [--variants 0,1,2,5,6] [--iters 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from lumen_amd.ops import cnn
+
+SHAPES = {  # name: (H, W, Cin, Cout, K, stride)
+    "ires_s1_112": (112, 112, 64, 64, 3, 1),
+    "ires_s1_56": (56, 56, 64, 64, 3, 1),
+    "ires_s2_28": (28, 28, 128, 128, 3, 1),
+    "ires_s3_14": (14, 14, 256, 256, 3, 1),
+    "ires_s4_7": (7, 7, 512, 512, 3, 1),
+    "ires_s3_down": (28, 28, 128, 256, 3, 2),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--faces", type=int, default=128)
+    ap.add_argument("--variants", default="0,1,2,5,6,8")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--shapes", default=",".join(SHAPES))
+    a = ap.parse_args()
+    dev = "cuda"
+    out = []
+    for name in a.shapes.split(","):
+        H, W, Cin, Cout, K, s = SHAPES[name]
+        xs = [torch.randn(a.faces, H, W, Cin, device=dev).bfloat16() for _ in range(4)]
+        w = (torch.randn(Cout, K, K, Cin, device=dev) * (K * K * Cin) ** -0.5).bfloat16()
+        b = torch.randn(Cout, device=dev).bfloat16()
+        pr = (torch.rand(Cout, device=dev) * 0.3).bfloat16()
+        Ho, Wo = cnn.conv_out_hw(H, W, K, K, s, K // 2, 1)
+        res = torch.randn(a.faces, Ho, Wo, Cout, device=dev).bfloat16()
+        flops = 2.0 * a.faces * Ho * Wo * Cout * K * K * Cin
+        ref = None
+        for v in [int(t) for t in a.variants.split(",")]:
+            tile = -1 if v == 0 else 10 + v
+            y = cnn.conv2d(xs[0], w, b, s, K // 2, 1, prelu=pr, residual=res, tile=tile)
+            if ref is None:
+                ref = y.float()
+            err = ((y.float() - ref).norm() / ref.norm()).item()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for i in range(a.iters):
+                cnn.conv2d(xs[i % 4], w, b, s, K // 2, 1, prelu=pr, residual=res, tile=tile, out=y)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / a.iters
+            r = {"shape": name, "variant": v, "us": round(us, 1), "tflops": round(flops / us / 1e6, 1),
+                 "rel_err_vs_first": round(err, 5)}
+            out.append(r)
+            print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

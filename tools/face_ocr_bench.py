@@ -89,21 +89,30 @@ def bench_face(args):
     dec = (lambda: pre) if pre is not None else (lambda: decode_many(jpegs))  # noqa: E731
     nxt = [ahead.submit(dec)]
 
+    from lumen_amd.runtime.metrics import StageTimer, use_timer
+
+    stages: dict = {}
+
     def step():
         imgs = nxt[0].result()
         nxt[0] = ahead.submit(dec)
-        be.detect_images(imgs, [DetParams(0.5, 0.4, 20, 2000)] * len(imgs))
-        idx = [i for i in range(len(imgs)) for _ in range(args.faces)]
-        emb = be.embed_faces(imgs, idx, np.concatenate([minv] * len(imgs)))
+        t = StageTimer("face-bench", gpu=args.gpu_timers)
+        with use_timer(t):
+            be.detect_images(imgs, [DetParams(0.5, 0.4, 20, 2000)] * len(imgs))
+            idx = [i for i in range(len(imgs)) for _ in range(args.faces)]
+            emb = be.embed_faces(imgs, idx, np.concatenate([minv] * len(imgs)))
         if runner is not None:   # DP result gather: every rank gets every image's faces
             res = [[(FaceDetection(bbox=(490.0 + 3 * k, 280.0, 590.0, 420.0), confidence=1.0,
                                    landmarks=[tuple(p) for p in lms + 3 * k]), emb[i * args.faces + k])
                     for k in range(args.faces)] for i in range(len(imgs))]
             runner.gather(res, len(imgs) * world)
         torch.cuda.synchronize()
+        for k, v in t.finish().items():
+            stages[k] = stages.get(k, 0.0) + v
 
     for _ in range(args.warmup):
         step()
+    stages.clear()
     if runner is not None:
         runner.comm.barrier()
     t0 = time.perf_counter()
@@ -120,6 +129,8 @@ def bench_face(args):
             "n_gpus": world, "parallelism": f"dp{world} (SPMD, RCCL all-gather of packed results)" if world > 1
             else "single GPU", "_rank": rank,
             "ms_per_batch": dt * 1000, "batch": args.batch, "faces_per_image": args.faces,
+            ("gpu" if args.gpu_timers else "host") + "_stage_ms_per_batch":
+                {k: round(v / args.iters, 2) for k, v in stages.items()},
             "faces_per_s": world * args.batch * args.faces / dt, "detector": "SCRFD-10G-shaped 640",
             "recogniser": f"IResNet-{args.rec}", "image": "1280x720 JPEG",
             "jpeg_decode": "excluded (decoded once up front)" if args.predecoded else "included",

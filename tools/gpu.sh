@@ -17,6 +17,8 @@
 #   prof_ttft      rocprofv3 kernel trace of 3 single-request TTFTs (8B fp8, 2 new tokens)
 #   prof_vlm8b     rocprofv3 kernel stats of the 8B fp8 decode bench (batch 16; prof_vlm8b_b1: single stream)
 #   face_ocr       tools/face_ocr_bench.py face + ocr
+#   conv           conv_lds variants on the IResNet shapes (tools/conv_bench.py) + LDS-pipeline tests
+#   face           face bench pre-decoded (HIP-event stage timers, then host timers) + JPEG-inclusive
 #   ocr            OCR bench pre-decoded (HIP-event stage timers) + JPEG-inclusive
 #   prof_face / prof_ocr   rocprofv3 kernel stats of the face / OCR bench
 #   f8             fp8 tests (tests/test_fp8_gpu.py) + tools/f8_gemm_bench.py ($F8_SHAPES, $F8_M)
@@ -89,12 +91,20 @@ for task in "$@"; do
     face_ocr)
       step face 400 python tools/face_ocr_bench.py --what face
       step ocr 400 python tools/face_ocr_bench.py --what ocr ;;
+    conv)   # conv_lds variants on the IResNet shapes (+ the LDS-pipeline numerics tests)
+      step conv_tests 300 python -u -m pytest tests/test_cnn_gpu.py -x -q -k lds_pipeline --timeout 120 \
+        --timeout-method thread
+      step conv_bench 300 python -u tools/conv_bench.py ${CONV_ARGS:-} ;;
+    face)
+      step face_pre 300 python tools/face_ocr_bench.py --what face --predecoded --gpu-timers
+      step face_pre_host 300 python tools/face_ocr_bench.py --what face --predecoded
+      step face_jpeg 300 python tools/face_ocr_bench.py --what face ;;
     ocr)
       step ocr_pre 300 python tools/face_ocr_bench.py --what ocr --predecoded --gpu-timers
       step ocr_jpeg 300 python tools/face_ocr_bench.py --what ocr ;;
     prof_face)
       step prof_face 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_face -o run -- \
-        python3 tools/face_ocr_bench.py --what face --iters 3 ;;
+        python3 tools/face_ocr_bench.py --what face --iters 3 --batch 32 --predecoded ;;
     prof_ocr)
       step prof_ocr 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ocr -o run -- \
         python3 tools/face_ocr_bench.py --what ocr --iters 3 ;;
