@@ -264,9 +264,20 @@ class MI355XFaceBackend:
             raise BackendNotInitializedError("Backend not initialized")
 
     # ------------------------------------------------------------------ batched device work
+    def upload_async(self, images: Sequence[np.ndarray]):
+        """Stage a batch's pixels for :meth:`detect_images` (``pre=``) from a prefetch thread: the
+        pinned staging copy and the H2D run while the GPU works on the previous batch."""
+        if getattr(self, "_pre_uploader", None) is None:
+            from ...utils.image import PinnedUploader
+
+            self._pre_uploader = PinnedUploader(self.device)
+        return self._pre_uploader.upload_async(images)
+
     @torch.no_grad()
-    def detect_images(self, images: Sequence[np.ndarray], params: Sequence[DetParams]) -> list[list[FaceDetection]]:
-        """Batched detection of decoded uint8 RGB images (one DetParams per image)."""
+    def detect_images(self, images: Sequence[np.ndarray], params: Sequence[DetParams], pre=None
+                      ) -> list[list[FaceDetection]]:
+        """Batched detection of decoded uint8 RGB images (one DetParams per image).  ``pre``: the
+        images' device upload from :meth:`upload_async` (else uploaded here)."""
         N = len(images)
         if N == 0:
             return []
@@ -285,7 +296,13 @@ class MI355XFaceBackend:
                 from ...utils.image import PinnedUploader
 
                 self._uploader = PinnedUploader(self.device)
-            dev, offs = self._uploader.upload(images)
+            if pre is not None:
+                from ...utils.image import consume
+
+                dev, offs, ready = pre
+                consume(dev, ready)
+            else:
+                dev, offs = self._uploader.upload(images)
             src = dev
             # (strong refs to the images keep their ids from being reused while the map lives)
             self._last_upload = (dev, {id(im): int(o) for im, o in zip(images, offs)}, list(images))

@@ -71,11 +71,49 @@ class PinnedUploader:
             list(_pool().map(cp, range(len(images))))
         elif images:
             cp(0)
-        dev = buf[:total].to(self.device, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        stream = self.side_stream if getattr(self, "_side", False) else None
+        with torch.cuda.stream(stream) if stream is not None else _null():
+            dev = buf[:total].to(self.device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
         self.events[k] = ev
+        self.last_event = ev
         return dev, offs
+
+    def upload_async(self, images: Sequence[np.ndarray]):
+        """Like :meth:`upload` but the H2D copy runs on this uploader's own stream, so it can be
+        issued from a prefetch thread while the compute stream is busy with the previous batch
+        without queueing behind (or in the middle of) that batch's kernels.  Returns
+        ``(dev, offs, ready)``: the consumer calls :func:`consume` (stream wait + allocator hand-off)
+        before its kernels read ``dev``."""
+        import torch
+
+        if getattr(self, "side_stream", None) is None:
+            self.side_stream = torch.cuda.Stream(self.device)
+        self._side = True
+        try:
+            dev, offs = self.upload(images)
+        finally:
+            self._side = False
+        return dev, offs, self.last_event
+
+
+def consume(dev, ready) -> None:
+    """Make the current stream wait for an :meth:`PinnedUploader.upload_async` copy and tell the
+    caching allocator the buffer is used on it."""
+    import torch
+
+    cur = torch.cuda.current_stream(dev.device)
+    cur.wait_event(ready)
+    dev.record_stream(cur)
+
+
+class _null:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
 
 
 def decode_rgb(data: bytes, draft_to: Optional[tuple[int, int]] = None, exif_transpose: bool = False) -> np.ndarray:

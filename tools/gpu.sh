@@ -96,8 +96,8 @@ for task in "$@"; do
         --timeout-method thread
       step conv_bench 300 python -u tools/conv_bench.py ${CONV_ARGS:-} ;;
     face)
-      step face_pre 300 python tools/face_ocr_bench.py --what face --predecoded --gpu-timers
-      step face_pre_host 300 python tools/face_ocr_bench.py --what face --predecoded
+      step face_pre 300 python tools/face_ocr_bench.py --what face --predecoded --gpu-timers --batch 32
+      step face_pre_host 300 python tools/face_ocr_bench.py --what face --predecoded --batch 32
       step face_jpeg 300 python tools/face_ocr_bench.py --what face ;;
     ocr)
       step ocr_pre 300 python tools/face_ocr_bench.py --what ocr --predecoded --gpu-timers
