@@ -157,6 +157,103 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
   const int cc = (lane % LPR) * 16;
   const int n = n0 + wn * TN + cc;
   const __amdgpu_buffer_rsrc_t crs = c_rsrc(a.out);
+  if (NPASS == 1 && !ep.out_f32 && !ep.bias_f32 && !ep.table && !ep.row_aff && !ep.out_group && !ep.glu &&
+      ep.alpha == 1.f) {
+    // Prefetched epilogue: a lane's 16 columns are the same in all 4 row slabs, so bias / PReLU /
+    // output-affine vectors load once, and the 4 slabs' residual rows are all in flight before the
+    // first slab is finished -- the generic path waits one L2 / HBM round trip per slab.
+    const int rr = lane / LPR;
+    const bool live = rr < 16 && n < N;
+    const uint16_t* zb = nullptr;
+    u32x4_t pb0 = {}, pb1 = {}, pp0 = {}, pp1 = {};
+    u32x4_t pr[4][2];
+    f32x4_t ps[4], pt[4];
+    if (live) {
+      if (ep.bias) {
+        zb = (const uint16_t*)ep.bias + n;
+        pb0 = *(const u32x4_t*)zb;
+        pb1 = *(const u32x4_t*)(zb + 8);
+      }
+      if (ep.prelu) {
+        pp0 = *(const u32x4_t*)(ep.prelu + n);
+        pp1 = *(const u32x4_t*)(ep.prelu + n + 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = min(m0 + wm * 64 + i * 16 + rr, M - 1);
+        if (ep.residual) {
+          const uint16_t* t = ep.residual + (int64_t)m * ep.ldr + n;
+          pr[i][0] = *(const u32x4_t*)t;
+          pr[i][1] = *(const u32x4_t*)(t + 8);
+        }
+      }
+      if (ep.aff_s) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          ps[q] = *(const f32x4_t*)(ep.aff_s + n + 4 * q);
+          pt[q] = *(const f32x4_t*)(ep.aff_t + n + 4 * q);
+        }
+      }
+    }
+    Unroll<0, 4>::run([&](const int i) {
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) es[(g * 4 + r) * LDSTR + j * 16 + frow] = acc[i][j][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int m = m0 + wm * 64 + i * 16 + rr;
+      if (live && m < M) {
+        float v[16], f[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cc + q * 4);
+          v[q * 4 + 0] = t[0]; v[q * 4 + 1] = t[1]; v[q * 4 + 2] = t[2]; v[q * 4 + 3] = t[3];
+        }
+        if (ep.bias) {
+          unpack8(pb0, f);
+          unpack8(pb1, f + 8);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) v[q] += f[q];
+        }
+        if (ep.act) apply_act_n<16>(v, ep.act);
+        if (ep.prelu) {
+          unpack8(pp0, f);
+          unpack8(pp1, f + 8);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) v[q] = v[q] > 0.f ? v[q] : v[q] * f[q];
+        }
+        if (ep.residual) {
+          unpack8(pr[i][0], f);
+          unpack8(pr[i][1], f + 8);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) v[q] += f[q];
+        }
+        if (ep.post_act) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) v[q] = fmaxf(v[q], 0.f);
+        }
+        const int64_t o = (int64_t)m * a.ldo + n;
+        if (ep.aff_s) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) f[4 * q + r] = bf2f(f2bf(v[4 * q + r])) * ps[q][r] + pt[q][r];
+          if (ep.aff_out) {
+            uint16_t* o2 = ep.aff_out + (int64_t)m * ep.ld_aff + n;
+            *(u32x4_t*)o2 = pack8(f);
+            *(u32x4_t*)(o2 + 8) = pack8(f + 8);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = f[q];
+          }
+        }
+        st16<false>(a.out, crs, o * 2, pack8(v));
+        st16<false>(a.out, crs, (o + 8) * 2, pack8(v + 8));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    });
+    return;
+  }
   Unroll<0, 4>::run([&](const int i) {
 #pragma unroll
     for (int j = 0; j < NR; ++j)

@@ -267,11 +267,22 @@ class MI355XFaceBackend:
     def upload_async(self, images: Sequence[np.ndarray]):
         """Stage a batch's pixels for :meth:`detect_images` (``pre=``) from a prefetch thread: the
         pinned staging copy and the H2D run while the GPU works on the previous batch."""
-        if getattr(self, "_pre_uploader", None) is None:
+        tl = self._tl()
+        if getattr(tl, "pre_uploader", None) is None:
             from ...utils.image import PinnedUploader
 
-            self._pre_uploader = PinnedUploader(self.device)
-        return self._pre_uploader.upload_async(images)
+            tl.pre_uploader = PinnedUploader(self.device)
+        return tl.pre_uploader.upload_async(images)
+
+    def _tl(self):
+        """Per-thread staging state (uploaders, the last upload's image map): batches of different
+        threads -- each on its own HIP stream -- may be in flight at once."""
+        t = self.__dict__.get("_tls")
+        if t is None:
+            import threading
+
+            t = self.__dict__.setdefault("_tls", threading.local())
+        return t
 
     @torch.no_grad()
     def detect_images(self, images: Sequence[np.ndarray], params: Sequence[DetParams], pre=None
@@ -292,20 +303,21 @@ class MI355XFaceBackend:
         src = None
         if self.device.type == "cuda":
             # one pinned H2D for the batch, kept for the alignment warps of the same images
-            if getattr(self, "_uploader", None) is None:
+            tl = self._tl()
+            if getattr(tl, "uploader", None) is None:
                 from ...utils.image import PinnedUploader
 
-                self._uploader = PinnedUploader(self.device)
+                tl.uploader = PinnedUploader(self.device)
             if pre is not None:
                 from ...utils.image import consume
 
                 dev, offs, ready = pre
                 consume(dev, ready)
             else:
-                dev, offs = self._uploader.upload(images)
+                dev, offs = tl.uploader.upload(images)
             src = dev
             # (strong refs to the images keep their ids from being reused while the map lives)
-            self._last_upload = (dev, {id(im): int(o) for im, o in zip(images, offs)}, list(images))
+            tl.last_upload = (dev, {id(im): int(o) for im, o in zip(images, offs)}, list(images))
         with stage("det_preprocess"):
             x = ops.image_prep(tens, (S, S), mean=(self.spec.det_mean,) * 3, std=(self.spec.det_std,) * 3, scale=1.0,
                                filter="cv2_linear", layout="nhwc8", pad=0.0, geoms=geoms, out_dtype=self.dtype,
@@ -368,7 +380,7 @@ class MI355XFaceBackend:
         R = self.spec.rec_size
         kw = dict(cpad=8, scale=1.0 / self.spec.rec_std, mean=self.spec.rec_mean / self.spec.rec_std, std=1.0,
                   swap_rb=self.spec.rec_color.lower() == "bgr", device=self.device)
-        last = getattr(self, "_last_upload", None)
+        last = getattr(self._tl(), "last_upload", None)
         if last is not None and self.device.type == "cuda" and all(id(im) in last[1] for im in images):
             kw["src"] = (last[0], [last[1][id(im)] for im in images])     # reuse the detection upload
         if replicate is None or not any(replicate):

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--variants", default="0,1,2,5,6,8")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--shapes", default=",".join(SHAPES))
+    ap.add_argument("--epi", default="prelu_res", choices=["prelu_res", "res_aff"],
+                    help="prelu_res: bias + PReLU + residual; res_aff: IResNet conv2 -- bias + residual + the "
+                         "next block's BN as a second output")
     a = ap.parse_args()
     dev = "cuda"
     out = []
@@ -43,10 +46,13 @@ def main():
         Ho, Wo = cnn.conv_out_hw(H, W, K, K, s, K // 2, 1)
         res = torch.randn(a.faces, Ho, Wo, Cout, device=dev).bfloat16()
         flops = 2.0 * a.faces * Ho * Wo * Cout * K * K * Cin
+        sc, sh = 1 + 0.1 * torch.randn(Cout, device=dev), 0.1 * torch.randn(Cout, device=dev)
+        ao = torch.empty_like(res)
+        kw = dict(prelu=pr, residual=res) if a.epi == "prelu_res" else dict(residual=res, aff=(sc, sh), aff_out=ao)
         ref = None
         for v in [int(t) for t in a.variants.split(",")]:
             tile = -1 if v == 0 else 10 + v
-            y = cnn.conv2d(xs[0], w, b, s, K // 2, 1, prelu=pr, residual=res, tile=tile)
+            y = cnn.conv2d(xs[0], w, b, s, K // 2, 1, tile=tile, **kw)
             if ref is None:
                 ref = y.float()
             err = ((y.float() - ref).norm() / ref.norm()).item()
@@ -54,11 +60,11 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for i in range(a.iters):
-                cnn.conv2d(xs[i % 4], w, b, s, K // 2, 1, prelu=pr, residual=res, tile=tile, out=y)
+                cnn.conv2d(xs[i % 4], w, b, s, K // 2, 1, tile=tile, out=y, **kw)
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / a.iters
-            r = {"shape": name, "variant": v, "us": round(us, 1), "tflops": round(flops / us / 1e6, 1),
+            r = {"shape": name, "variant": v, "epi": a.epi, "us": round(us, 1), "tflops": round(flops / us / 1e6, 1),
                  "rel_err_vs_first": round(err, 5)}
             out.append(r)
             print(json.dumps(r), flush=True)
