@@ -284,6 +284,26 @@ class MI355XFaceBackend:
             t = self.__dict__.setdefault("_tls", threading.local())
         return t
 
+    def decode_device(self, datas: Sequence[bytes]):
+        """A batch of encoded images -> (images, pre): baseline JPEGs entropy-decoded on the host
+        pool and reconstructed on the GPU by one batched launch (utils/jpeg.py), other formats
+        through Pillow, every image in one flat device buffer.  ``images[k]`` is a
+        :class:`~lumen_amd.utils.jpeg.DeviceImage` (pixels stay on the device) or the
+        InvalidInputError of an undecodable payload; ``pre`` feeds :meth:`detect_images`."""
+        from ...utils.jpeg import DeviceImage, decode_batch_to_device
+
+        with stage("decode"):
+            flat, offs, shapes, errors = decode_batch_to_device(list(datas), self.device)
+        images = [InvalidInputError(f"Failed to decode image bytes: {errors[k]}") if k in errors
+                  else DeviceImage(*shapes[k]) for k in range(len(datas))]
+        return images, (flat, offs, None)
+
+    def device_decode_ok(self) -> bool:
+        """Batches of JPEG bytes can take :meth:`decode_device` (GPU device, standard alignment:
+        the reference alignment mode crops host pixels)."""
+        return self.device.type == "cuda" and self.align_mode != "reference" and \
+            os.environ.get("LUMEN_FACE_DEVICE_JPEG", "1") != "0"
+
     @torch.no_grad()
     def detect_images(self, images: Sequence[np.ndarray], params: Sequence[DetParams], pre=None
                       ) -> list[list[FaceDetection]]:
@@ -299,7 +319,8 @@ class MI355XFaceBackend:
             geoms.append(g)
             scales.append(s)
             off += im.size
-        tens = [torch.from_numpy(np.ascontiguousarray(im)) for im in images]
+        tens = [torch.empty(im.shape, dtype=torch.uint8, device="meta") for im in images] if pre is not None \
+            else [torch.from_numpy(np.ascontiguousarray(im)) for im in images]
         src = None
         if self.device.type == "cuda":
             # one pinned H2D for the batch, kept for the alignment warps of the same images
@@ -470,7 +491,15 @@ class MI355XFaceBackend:
         a DP worker pool gets the JPEG and decodes in the worker."""
         from ...parallel.engine import RemotePool
 
-        return self.decode(image_bytes) if isinstance(self._pool, RemotePool) else bytes(image_bytes)
+        if isinstance(self._pool, RemotePool):
+            # baseline JPEGs travel as bytes: the engine decodes its merged batch with one GPU
+            # reconstruction (dp_worker "detect" / "det_emb"); anything else decodes here
+            from ...utils import jpeg
+
+            if os.environ.get("LUMEN_FACE_DEVICE_JPEG", "1") != "0" and jpeg.info(bytes(image_bytes)) is not None:
+                return bytes(image_bytes)
+            return self.decode(image_bytes)
+        return bytes(image_bytes)
 
     def decode(self, image_bytes: bytes) -> np.ndarray:
         if not image_bytes:
@@ -639,16 +668,23 @@ def dp_worker(device: str, resources: GenericResources, max_batch: int = 64):
     def fn(kind, items):
         if kind == "info":
             return [{"spec": b.spec, "embedding_dim": int(b.rec.cfg.embedding)}] * len(items)   # one per requester
-        imgs = [load(it[0]) for it in items]
+        dev_path = kind in ("detect", "det_emb") and b.device_decode_ok() and bool(items) and \
+            all(isinstance(it[0], (bytes, bytearray, memoryview)) for it in items)
+        if dev_path:
+            # the whole batch's JPEGs: host entropy decode on the pool + ONE GPU reconstruction
+            imgs, (flat, offs, _) = b.decode_device([bytes(it[0]) for it in items])
+        else:
+            imgs = [load(it[0]) for it in items]
         ok = [k for k, im in enumerate(imgs) if not isinstance(im, BaseException)]
         out: list = [imgs[k] for k in range(len(items))]          # decode errors stay in place
+        pre = (flat, [offs[k] for k in ok], None) if dev_path else None
         if kind == "embed":
             if ok:
                 embs = b._embed_batch([(imgs[k], items[k][1], items[k][2]) for k in ok])
                 for k, e in zip(ok, embs):
                     out[k] = e
             return out
-        dets = b.detect_images([imgs[k] for k in ok], [items[k][1] for k in ok]) if ok else []
+        dets = b.detect_images([imgs[k] for k in ok], [items[k][1] for k in ok], pre=pre) if ok else []
         if kind == "detect":
             for k, d in zip(ok, dets):
                 out[k] = d

@@ -104,7 +104,8 @@ def consume(dev, ready) -> None:
     import torch
 
     cur = torch.cuda.current_stream(dev.device)
-    cur.wait_event(ready)
+    if ready is not None:
+        cur.wait_event(ready)
     dev.record_stream(cur)
 
 

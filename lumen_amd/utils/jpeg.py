@@ -348,6 +348,21 @@ def decode_batch_to_device(datas, device):
     return out, offs, shapes, errors
 
 
+class DeviceImage:
+    """Shape-only stand-in for a decoded image whose pixels live in a device buffer
+    (:func:`decode_batch_to_device`): the batched pipelines (face detection / alignment) take
+    their geometry from ``shape`` and their pixels from the flat buffer + offset."""
+
+    __slots__ = ("shape",)
+
+    def __init__(self, h: int, w: int):
+        self.shape = (int(h), int(w), 3)
+
+    @property
+    def size(self) -> int:
+        return self.shape[0] * self.shape[1] * 3
+
+
 def decode_image(data: bytes, device, draft_to: Optional[tuple] = None, stats: Optional[dict] = None):
     """Request image -> uint8 [H, W, 3] torch tensor: on a GPU device a baseline JPEG takes
     :func:`decode_to_device` (full resolution, no DCT-domain shortcut needed: the entropy decode

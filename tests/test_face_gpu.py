@@ -131,3 +131,32 @@ def test_reference_alignment_warp_gpu_matches_cpu():
         outs[dev] = b.warp_faces(srcs, list(range(len(srcs))), np.stack(minvs), reps)[..., :3].float().cpu()
     d = (outs["cpu"] - outs["cuda"]).abs()
     assert d.max().item() < 3 / 255 and d.mean().item() < 1e-3
+
+
+def test_face_engine_device_jpeg_matches_pillow(tmp_path, monkeypatch):
+    """The face engine's batched device JPEG path (host entropy decode + one GPU reconstruction,
+    pixels never leave the device) detects and embeds like the Pillow path; an undecodable
+    payload fails alone."""
+    from lumen_amd.resources.exceptions import InvalidInputError
+    from lumen_amd.services.face.backend import DetParams, dp_worker
+
+    write_face_model(tmp_path / "models" / "buffalo_tiny", "buffalo_tiny")
+    cfg = config_from_dict(_cfg(tmp_path, "cuda"))
+    svc = GeneralFaceService.from_config(cfg.services["face"], tmp_path)
+    svc.initialize()
+    try:
+        fn = dp_worker("cuda", svc.backend.resources)
+        rng = np.random.default_rng(7)
+        jpegs = [encode_jpeg(rng.integers(0, 255, (96 + 8 * k, 160 - 4 * k, 3), dtype=np.uint8)) for k in range(3)]
+        items = [(j, DetParams(0.0, 0.3, 0, 10000), 4) for j in jpegs] + [(b"not an image", DetParams(), 4)]
+        monkeypatch.setenv("LUMEN_FACE_DEVICE_JPEG", "1")
+        dev = fn("det_emb", items)
+        monkeypatch.setenv("LUMEN_FACE_DEVICE_JPEG", "0")
+        host = fn("det_emb", items)
+        assert isinstance(dev[3], InvalidInputError) and isinstance(host[3], InvalidInputError)
+        for d, h in zip(dev[:3], host[:3]):
+            assert len(d) > 0 and abs(len(d) - len(h)) <= 1
+            assert np.abs(np.array(d[0][0].bbox) - np.array(h[0][0].bbox)).max() < 4.0
+            assert float(np.dot(d[0][1], h[0][1])) > 0.95
+    finally:
+        svc.close()
