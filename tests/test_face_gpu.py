@@ -137,8 +137,7 @@ def test_face_engine_device_jpeg_matches_pillow(tmp_path, monkeypatch):
     """The face engine's batched device JPEG path (host entropy decode + one GPU reconstruction,
     pixels never leave the device) detects and embeds like the Pillow path; an undecodable
     payload fails alone."""
-    from lumen_amd.resources.exceptions import InvalidInputError
-    from lumen_amd.services.face.backend import DetParams, dp_worker
+    from lumen_amd.services.face.backend import DetParams, InvalidInputError, dp_worker
 
     write_face_model(tmp_path / "models" / "buffalo_tiny", "buffalo_tiny")
     cfg = config_from_dict(_cfg(tmp_path, "cuda"))
