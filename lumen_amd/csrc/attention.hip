@@ -130,7 +130,9 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
   // being re-fetched from HBM by up to 8 different dies.
   const int nqb = gridDim.x;
   const int lin = xcd_remap(blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z), nqb * gridDim.y * gridDim.z);
-  const int qblk = lin % nqb;
+  // causal: a head's query blocks in decreasing work order (the last block sees every key), so
+  // each XCD starts its longest blocks first and the short ones fill in behind them
+  const int qblk = a.causal ? nqb - 1 - lin % nqb : lin % nqb;
   const int h = (lin / nqb) % gridDim.y, b = lin / (nqb * gridDim.y);
   const int hk = h / (a.H / a.Hkv);
   const int q0 = qblk * QB + wid * 16;

@@ -851,6 +851,45 @@ __global__ void __launch_bounds__(256) quant_rows_fp8_kernel(const uint16_t* __r
   __shared__ float red[4];
   const int64_t m = blockIdx.x;
   const uint16_t* xr = x + m * ldx;
+  // the row stays in registers (K <= 16384: 8 chunks of 8 per thread), every chunk's load in
+  // flight at once: one round trip instead of one per 2048 columns per pass, and no second read
+  constexpr int NC = 8;
+  u32x4_t raw[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int k = (threadIdx.x + c * 256) * 8;
+    raw[c] = k < K ? *(const u32x4_t*)(xr + k) : (u32x4_t){0u, 0u, 0u, 0u};
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    float f[8];
+    unpack8(raw[c], f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) amax = fmaxf(amax, fabsf(f[q]));
+  }
+  amax = block_max(amax, red);
+  const float s = fmaxf(amax, 1e-12f) / FP8_MAX;
+  if (threadIdx.x == 0) scale[m] = s;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int k = (threadIdx.x + c * 256) * 8;
+    if (k >= K) break;
+    float f[8];
+    unpack8(raw[c], f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) f[q] = fminf(fmaxf(f[q] / s, -FP8_MAX), FP8_MAX);   // IEEE divide: bit-identical to x / s on the host
+    *(uint2*)(out + m * ldo + k) = to_fp8x8(f);
+  }
+}
+
+// K > 16384: two passes over global memory
+__global__ void __launch_bounds__(256) quant_rows_fp8_wide_kernel(const uint16_t* __restrict__ x, int64_t ldx,
+                                                                  uint8_t* __restrict__ out, int64_t ldo,
+                                                                  float* __restrict__ scale, int K) {
+  __shared__ float red[4];
+  const int64_t m = blockIdx.x;
+  const uint16_t* xr = x + m * ldx;
   float amax = 0.f;
   for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
     float f[8];
@@ -865,7 +904,7 @@ __global__ void __launch_bounds__(256) quant_rows_fp8_kernel(const uint16_t* __r
     float f[8];
     unpack8(*(const u32x4_t*)(xr + k), f);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) f[q] = fminf(fmaxf(f[q] / s, -FP8_MAX), FP8_MAX);   // IEEE divide: bit-identical to x / s on the host
+    for (int q = 0; q < 8; ++q) f[q] = fminf(fmaxf(f[q] / s, -FP8_MAX), FP8_MAX);
     *(uint2*)(out + m * ldo + k) = to_fp8x8(f);
   }
 }
@@ -980,7 +1019,10 @@ hipError_t quant_rows_mx(const uint16_t* x, int64_t ldx, uint8_t* q8, int64_t ld
 hipError_t quant_rows_fp8(const uint16_t* x, int64_t ldx, uint8_t* out, int64_t ldo, float* scale, int M, int K,
                           hipStream_t stream) {
   if (K % 8 != 0 || M <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(quant_rows_fp8_kernel, dim3(M), dim3(256), 0, stream, x, ldx, out, ldo, scale, K);
+  if (K <= 16384)
+    hipLaunchKernelGGL(quant_rows_fp8_kernel, dim3(M), dim3(256), 0, stream, x, ldx, out, ldo, scale, K);
+  else
+    hipLaunchKernelGGL(quant_rows_fp8_wide_kernel, dim3(M), dim3(256), 0, stream, x, ldx, out, ldo, scale, K);
   return hipGetLastError();
 }
 

@@ -108,7 +108,7 @@ def test_gemm_f8_swiglu(M):
     assert got.shape == (M, I) and _rel(got, ref) < 1e-2
 
 
-@pytest.mark.parametrize("M,K", [(1, 896), (37, 4096), (624, 14336)])
+@pytest.mark.parametrize("M,K", [(1, 896), (37, 4096), (624, 14336), (3, 20480)])
 def test_quant_rows_fp8_matches_torch(M, K):
     x = (torch.randn(M, K) * torch.logspace(-2, 2, M)[:, None]).bfloat16()
     ref8, refs = ops.quant_rows_fp8(x)
