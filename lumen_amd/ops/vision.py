@@ -131,8 +131,21 @@ def nms(cand: torch.Tensor, count: torch.Tensor, iou_thr: float, max_out: int = 
         keep = torch.empty((N, max_out), dtype=torch.int32, device=cand.device)
         keep_n = torch.empty((N,), dtype=torch.int32, device=cand.device)
         hip_ops().nms(cand, count, float(iou_thr), keep, keep_n)
-        keep_c, keep_nc, cand_c = keep.cpu(), keep_n.cpu(), cand.cpu()
-        return [cand_c[n, keep_c[n, : int(keep_nc[n])].long()] for n in range(N)]
+        # kept rows gathered on the device, then ONE small copy: the whole candidate block
+        # (N x MC x 64 B, MBs for a batch) never crosses to the host
+        counts = keep_n.cpu().tolist()
+        tot = sum(counts)
+        if tot == 0:
+            return [torch.zeros((0, cand.shape[2]), dtype=cand.dtype) for _ in range(N)]
+        n_idx = np.repeat(np.arange(N, dtype=np.int64), counts)
+        j_idx = np.concatenate([np.arange(c, dtype=np.int64) for c in counts])
+        nd, jd = h2d(n_idx, cand.device), h2d(j_idx, cand.device)
+        rows = cand[nd, keep[nd, jd].long()].cpu()
+        out, o = [], 0
+        for c in counts:
+            out.append(rows[o:o + c])
+            o += c
+        return out
     out = []
     for n in range(N):
         c = min(int(count[n]), MC)

@@ -309,9 +309,22 @@ class MI355XFaceBackend:
                       ) -> list[list[FaceDetection]]:
         """Batched detection of decoded uint8 RGB images (one DetParams per image).  ``pre``: the
         images' device upload from :meth:`upload_async` (else uploaded here)."""
-        N = len(images)
-        if N == 0:
+        if len(images) == 0:
             return []
+        return self.detect_finish(self.detect_launch(images, params, pre))
+
+    def detect_finish(self, st) -> list[list[FaceDetection]]:
+        """Second half of :meth:`detect_images`: decode + NMS kernels, the D2H of the kept rows
+        (synchronises) and the host parse."""
+        images, params, heads, scales = st
+        return self._det_post(images, params, heads, scales)
+
+    @torch.no_grad()
+    def detect_launch(self, images: Sequence[np.ndarray], params: Sequence[DetParams], pre=None):
+        """First half of :meth:`detect_images`: upload / preprocess / detector forward, all queued
+        on the stream without waiting -- a pipelined caller queues batch i + 1's detector behind
+        batch i's recogniser before it waits for batch i's embeddings."""
+        N = len(images)
         S = self.spec.det_size
         geoms, scales, off = [], [], 0
         for im in images:
@@ -345,7 +358,7 @@ class MI355XFaceBackend:
                                device=self.device, src=src)
         with stage("det_forward"):
             heads = self.det(x)
-        return self._det_post(images, params, heads, scales)
+        return images, params, heads, scales
 
     def _det_post(self, images, params, heads, scales) -> list[list[FaceDetection]]:
         N = len(images)
@@ -431,6 +444,26 @@ class MI355XFaceBackend:
                 x = x.to(self.dtype)
         with stage("rec_forward"):
             return self.rec(x).float().cpu().numpy()
+
+    @torch.no_grad()
+    def embed_faces_async(self, images: Sequence[np.ndarray], img_index: Sequence[int], minv: np.ndarray):
+        """:meth:`embed_faces` without the wait: warp + recogniser + a D2H copy into pinned memory
+        are queued; :meth:`embed_wait` returns the [F, D] embeddings."""
+        x = self.warp_faces(images, img_index, minv)
+        if x.dtype != self.dtype:
+            x = x.to(self.dtype)
+        emb = self.rec(x)
+        host = torch.empty(emb.shape, dtype=torch.float32, pin_memory=True)
+        host.copy_(emb, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return host, ev
+
+    @staticmethod
+    def embed_wait(h) -> np.ndarray:
+        host, ev = h
+        ev.synchronize()
+        return host.numpy()
 
     def _detect_batch(self, items):
         imgs = [it[0] for it in items]

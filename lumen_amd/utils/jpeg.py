@@ -231,8 +231,12 @@ def _pool():
 
 
 class _BatchStaging(threading.local):
-    bufs = None       # pinned (coef int16, qt int16, entries uint8, raw uint8)
-    ev = None         # the H2D copies that last read them
+    """Two pinned staging sets per thread, alternating: a caller that queues batch i + 1 before the
+    device has consumed batch i's copies waits only for batch i - 1's."""
+
+    def __init__(self):
+        self.slots = [[None, None], [None, None]]    # [bufs (coef, qt, entries, raw), event of their H2D]
+        self.k = 0
 
 
 _bstage = _BatchStaging()
@@ -269,9 +273,11 @@ def decode_batch_to_device(datas, device):
         cbase[i] = tot
         tot += infos[i].coef_count
     st = _bstage
-    if st.ev is not None:
-        st.ev.synchronize()          # this thread's previous batch has been copied out of the staging
-    coef_h, qt_h, ent_h, raw_h = st.bufs or (None, None, None, None)
+    slot = st.slots[st.k]
+    st.k ^= 1
+    if slot[1] is not None:
+        slot[1].synchronize()        # the batch before last has been copied out of this staging set
+    coef_h, qt_h, ent_h, raw_h = slot[0] or (None, None, None, None)
     coef_h = _pinned(coef_h, tot, torch.int16)
     qt_h = _pinned(qt_h, max(1, len(jidx)) * 192, torch.int16)
     ent_h = _pinned(ent_h, max(1, len(jidx)) * _ENTRY_BYTES, torch.uint8)
@@ -343,8 +349,8 @@ def decode_batch_to_device(datas, device):
         hip_ops().jpeg_reconstruct_batch(coef_d, qt_d, torch.from_numpy(meta), samp, out, ent_d, ent_h)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
-    st.ev = ev
-    st.bufs = (coef_h, qt_h, ent_h, raw_h)
+    slot[1] = ev
+    slot[0] = (coef_h, qt_h, ent_h, raw_h)
     return out, offs, shapes, errors
 
 
