@@ -80,12 +80,18 @@ class SPMDFaceRunner:
             dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=self.comm.group)
         maxf = max(int(mx.item()), 1)
         rows, counts = pack_faces(local, per, maxf, self.dim)
-        rows, counts = rows.to(self.device), counts.to(self.device)
-        all_rows = torch.empty((world * per,) + tuple(rows.shape[1:]), dtype=rows.dtype, device=self.device)
-        all_counts = torch.empty((world * per,), dtype=counts.dtype, device=self.device)
-        self.comm.all_gather_into(all_rows, rows)
-        self.comm.all_gather_into(all_counts, counts)
-        r_np, c_np = all_rows.cpu().numpy(), all_counts.cpu().numpy()
+        # ONE all-gather: each image's face count rides in an extra leading row of its block
+        # (exact in fp32), uploaded through pinned memory
+        blk = torch.zeros((per, maxf + 1, rows.shape[2]), dtype=torch.float32)
+        blk[:, 0, 0] = counts.float()
+        blk[:, 1:] = rows
+        from ...utils.h2d import h2d
+
+        blk = h2d(blk, self.device)
+        all_blk = torch.empty((world * per,) + tuple(blk.shape[1:]), dtype=blk.dtype, device=self.device)
+        self.comm.all_gather_into(all_blk, blk)
+        a_np = all_blk.cpu().numpy()
+        r_np, c_np = a_np[:, 1:], a_np[:, 0, 0].astype(np.int32)
         keep = np.concatenate([np.arange(r * per, r * per + (shard_range(n_global, r, world)[1] -
                                                                shard_range(n_global, r, world)[0]))
                                for r in range(world)])
