@@ -200,7 +200,9 @@ static hipError_t launch_conv(const ConvArgs& a, const GemmEpi& ep, hipStream_t 
 }
 
 bool conv_lds_ok(const ConvArgs& a);
+bool conv_lds_small_ok(const ConvArgs& a);
 hipError_t conv2d_lds(const ConvArgs& a, const GemmEpi& ep, int variant, hipStream_t stream);
+hipError_t conv2d_lds_small(const ConvArgs& a, const GemmEpi& ep, int variant, hipStream_t stream);
 
 // tile: -1 auto, 0..2 register-staged configs, 10 + v the LDS-DMA pipeline (conv_lds.hip, v = variant)
 hipError_t conv2d_igemm(const ConvArgs& a, const GemmEpi& ep, int tile, hipStream_t stream) {
@@ -209,6 +211,12 @@ hipError_t conv2d_igemm(const ConvArgs& a, const GemmEpi& ep, int tile, hipStrea
   // Cin % 64 == 0 layers (IResNet, SCRFD / DBNet trunks): the LDS-DMA pipeline
   // (profiles/r2_conv_lds_v1.txt); other shapes use the register-staged kernels
   if (tile < 0 && conv_lds_ok(a)) return conv2d_lds(a, ep, 0, stream);
+  // Cin 8 / 16 / 32 (stems): the same pipeline with several taps per K step
+  static const bool small_lds = [] {
+    const char* e = std::getenv("LUMEN_CONV_SMALL_LDS");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (tile < 0 && small_lds && conv_lds_small_ok(a)) return conv2d_lds_small(a, ep, 0, stream);
   if (tile < 0) {
     const int64_t t128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
     if (a.Cout >= 128 && t128 >= 256) tile = 0;

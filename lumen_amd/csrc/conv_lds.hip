@@ -19,7 +19,11 @@
 
 namespace lumen {
 
-template <int NSTAGE, int WN, int BN>
+// SMALLC: Cin in {8, 16, 32} (detector / recogniser stems): one 64-wide K step spans 64 / Cin
+// filter taps, so a lane's 16-byte chunk picks its own tap -- tap = step * (64 / Cin) + chunk / (Cin / 8)
+// -- and its offset comes from a per-workgroup LDS table of tap offsets; taps past KH * KW (the
+// last, partial step) read zeros, and the B side's columns past K meet those zeros.
+template <int NSTAGE, int WN, int BN, bool SMALLC = false>
 __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi ep) {
   constexpr int NW = 2 * WN;
   constexpr int TN = BN / WN;
@@ -52,10 +56,17 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
       __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, (int)((int64_t)N * K * 2), 0x00020000);
   int rofs[PERA];
   uint64_t tmask[PERA];
+  int cchunk[PERA];
+  __shared__ int s_tap[SMALLC ? 64 : 1];
+  const int row_step = a.dh * a.W * a.ldx * 2, col_step = a.dw * a.ldx * 2;
+  if constexpr (SMALLC) {
+    if (tid < 64) s_tap[tid] = (tid / a.KW) * row_step + (tid % a.KW) * col_step;
+  }
 #pragma unroll
   for (int i = 0; i < PERA; ++i) {
     const int r = (PERA * wid + i) * 8 + (lane >> 3);
-    const int ca = ((lane & 7) ^ ((r >> 1) & 7)) * 8;             // channel offset of this lane's 16 B
+    cchunk[i] = (lane & 7) ^ ((r >> 1) & 7);                      // logical 16-byte chunk of the row
+    const int ca = SMALLC ? 0 : cchunk[i] * 8;                     // channel offset of this lane's 16 B
     const int m = min(m0 + r, M - 1);
     const int img = m / (a.Ho * a.Wo), rem = m % (a.Ho * a.Wo);
     const int hb = (rem / a.Wo) * a.sh - a.ph, wb = (rem % a.Wo) * a.sw - a.pw;
@@ -78,12 +89,21 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
   // wave-uniform walk over (tap, 64-channel block): advanced once per stage() call, in K order
   int ky = 0, kx = 0, c0 = 0, tofs = 0;
   uint64_t tbit = 1;
-  const int row_step = a.dh * a.W * a.ldx * 2, col_step = a.dw * a.ldx * 2;
+  const int cpt_log = a.Cin == 8 ? 0 : (a.Cin == 16 ? 1 : 2);   // SMALLC: 16-byte chunks per tap (log2)
+  const int khw = a.KH * a.KW;
+  if constexpr (SMALLC) __syncthreads();                       // s_tap
   auto stage = [&](int s, int kt) {
     char* baseA = smem + s * STAGE + wid * PERA * 1024;
 #pragma unroll
     for (int i = 0; i < PERA; ++i) {
-      const int off = (tmask[i] & tbit) ? rofs[i] + tofs : (int)0x80000000;
+      int off;
+      if constexpr (SMALLC) {
+        const int t = (kt << (3 - cpt_log)) + (cchunk[i] >> cpt_log);
+        const int ch = (cchunk[i] & ((1 << cpt_log) - 1)) * 16;
+        off = (t < khw && ((tmask[i] >> t) & 1ull)) ? rofs[i] + s_tap[t] + ch : (int)0x80000000;
+      } else {
+        off = (tmask[i] & tbit) ? rofs[i] + tofs : (int)0x80000000;
+      }
       buf_load_lds16(xr, baseA + i * 1024, off, 0);
     }
     char* baseB = smem + s * STAGE + ASZ + wid * PERB * 1024;
@@ -109,7 +129,7 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
 #pragma unroll
     for (int j = 0; j < NR; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / 64;
+  const int nk = SMALLC ? (K + 63) / 64 : K / 64;
   const int frow = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
@@ -278,19 +298,27 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
   });
 }
 
-template <int NS, int WN, int BN>
+template <int NS, int WN, int BN, bool SMALLC = false>
 static hipError_t launch_conv_lds(const ConvArgs& a, const GemmEpi& ep, hipStream_t stream) {
   const size_t lds = (size_t)NS * (128 + BN) * 128;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_lds_kernel<NS, WN, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)lds);
+    (void)hipFuncSetAttribute((const void*)conv_lds_kernel<NS, WN, BN, SMALLC>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int M = a.N * a.Ho * a.Wo;
   const int tiles = ((M + 127) / 128) * ((a.Cout + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_lds_kernel<NS, WN, BN>), dim3(tiles), dim3(128 * WN), lds, stream, a, ep);
+  hipLaunchKernelGGL((conv_lds_kernel<NS, WN, BN, SMALLC>), dim3(tiles), dim3(128 * WN), lds, stream, a, ep);
   return hipGetLastError();
+}
+
+bool conv_lds_small_ok(const ConvArgs& a) {
+  // the small-Cin form: Cin 8 / 16 / 32, K steps of 64 / Cin taps
+  return (a.Cin == 8 || a.Cin == 16 || a.Cin == 32) && a.Cout % 16 == 0 && a.ldx % 8 == 0 && a.ldo % 8 == 0 &&
+         ((uintptr_t)a.x & 15) == 0 && ((uintptr_t)a.w & 15) == 0 && (int64_t)a.N * a.Ho * a.Wo < (1LL << 31) &&
+         (int64_t)a.N * a.H * a.W * a.ldx * 2 < (1LL << 31) && (int64_t)a.Cout * a.KH * a.KW * a.Cin * 2 < (1LL << 31) &&
+         a.KH * a.KW <= 64;
 }
 
 bool conv_lds_ok(const ConvArgs& a) {
@@ -305,7 +333,20 @@ bool conv_lds_ok(const ConvArgs& a) {
 // variant: 0 auto; 1 = 128x128 3 stages 8 waves, 2 = 128x128 2 stages 4 waves, 3 = 128x64 3 stages 4 waves,
 // 4 = 128x64 2 stages 4 waves (two workgroups per CU), 5 = 128x128 4 stages 4 waves, 6 = 128x128 3 stages
 // 4 waves, 7 = 128x64 4 stages 4 waves, 8 = 128x128 4 stages 8 waves
+// small-Cin form: 9 = 128x32 2 stages 4 waves, 10 = 128x64 2 stages 4 waves, 11 = 128x128 2 stages 4 waves
+hipError_t conv2d_lds_small(const ConvArgs& a, const GemmEpi& ep, int variant, hipStream_t stream) {
+  if (!conv_lds_small_ok(a)) return hipErrorInvalidValue;
+  if (variant == 0) variant = a.Cout <= 32 ? 9 : (a.Cout <= 64 ? 10 : 11);
+  switch (variant) {
+    case 9: return launch_conv_lds<2, 2, 32, true>(a, ep, stream);
+    case 10: return launch_conv_lds<2, 2, 64, true>(a, ep, stream);
+    case 11: return launch_conv_lds<2, 2, 128, true>(a, ep, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 hipError_t conv2d_lds(const ConvArgs& a, const GemmEpi& ep, int variant, hipStream_t stream) {
+  if (variant >= 9) return conv2d_lds_small(a, ep, variant, stream);
   if (!conv_lds_ok(a)) return hipErrorInvalidValue;
   if (variant == 0) {
     const int64_t M = (int64_t)a.N * a.Ho * a.Wo;

@@ -59,6 +59,27 @@ def test_conv2d_lds_pipeline(N, H, W, Cin, Cout, K, s, p, d, tile):
     assert _rel(got3, ref3) < 1e-2 and got3.min().item() >= 0
 
 
+@pytest.mark.parametrize("N,H,W,Cin,Cout,K,s,p", [
+    (2, 33, 31, 8, 32, 3, 2, 1), (1, 40, 40, 32, 32, 3, 1, 1), (2, 21, 19, 32, 64, 3, 2, 1),
+    (3, 28, 28, 8, 64, 3, 1, 1), (1, 17, 23, 16, 48, 5, 1, 2), (2, 12, 12, 32, 128, 1, 1, 0)])
+@pytest.mark.parametrize("tile", [-1, 19, 20, 21])
+def test_conv2d_lds_small_cin(N, H, W, Cin, Cout, K, s, p, tile):
+    """Cin 8 / 16 / 32: the LDS-DMA pipeline with several filter taps per 64-wide K step (per-lane
+    tap offsets, zero taps past KH * KW in the last step), every tile width."""
+    g = torch.Generator().manual_seed(H * Cin + K + Cout)
+    x = torch.randn(N, H, W, Cin, generator=g).bfloat16()
+    w = (torch.randn(Cout, K, K, Cin, generator=g) * (K * K * Cin) ** -0.5).bfloat16()
+    b = torch.randn(Cout, generator=g).bfloat16()
+    pr = (torch.rand(Cout, generator=g) * 0.3).bfloat16()
+    ref = cnn.conv2d(x, w, b, s, p, 1, act="relu", prelu=pr)
+    got = cnn.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), s, p, 1, act="relu", prelu=pr.to(DEV), tile=tile)
+    assert got.shape == ref.shape and _rel(got, ref) < 1e-2
+    r = torch.randn(*ref.shape, generator=g).bfloat16()
+    ref3 = cnn.conv2d(x, w, b, s, p, 1, residual=r, post_act="relu")
+    got3 = cnn.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), s, p, 1, residual=r.to(DEV), tile=tile, post_act="relu")
+    assert _rel(got3, ref3) < 1e-2
+
+
 @pytest.mark.parametrize("Cin,tile", [(8, -1), (64, -1), (64, 12), (128, 15)])
 def test_conv2d_output_affine(Cin, tile):
     """The next layer's channel affine emitted by the conv epilogue: as a second output next to the
