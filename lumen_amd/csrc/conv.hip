@@ -214,7 +214,7 @@ hipError_t conv2d_igemm(const ConvArgs& a, const GemmEpi& ep, int tile, hipStrea
   // Cin 8 / 16 / 32 (stems): the same pipeline with several taps per K step
   static const bool small_lds = [] {
     const char* e = std::getenv("LUMEN_CONV_SMALL_LDS");
-    return e == nullptr || e[0] != '0';
+    return e != nullptr && e[0] == '1';
   }();
   if (tile < 0 && small_lds && conv_lds_small_ok(a)) return conv2d_lds_small(a, ep, 0, stream);
   if (tile < 0) {
