@@ -73,3 +73,16 @@ def test_step_bus_full_ring_times_out_and_rejects_oversize():
     finally:
         w.close()
         w.unlink()
+
+
+def test_h2d_cpu_paths():
+    """utils.h2d on a CPU target: lists, numpy arrays and tensors keep values and dtypes."""
+    import torch
+
+    from lumen_amd.utils.h2d import h2d
+
+    assert torch.equal(h2d([[1, 2], [3, 4]], "cpu", torch.long), torch.tensor([[1, 2], [3, 4]]))
+    a = np.arange(6, dtype=np.float32).reshape(2, 3)[:, ::2]          # non-contiguous view
+    t = h2d(a, "cpu")
+    assert t.dtype == torch.float32 and torch.equal(t, torch.from_numpy(np.ascontiguousarray(a)))
+    assert h2d(torch.ones(3, dtype=torch.int32), "cpu", torch.float32).dtype == torch.float32
