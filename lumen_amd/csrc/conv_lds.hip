@@ -181,16 +181,21 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
       ep.alpha == 1.f) {
     // Prefetched epilogue: a lane's 16 columns are the same in all 4 row slabs, so bias / PReLU /
     // output-affine vectors load once, and the 4 slabs' residual rows are all in flight before the
-    // first slab is finished -- the generic path waits one L2 / HBM round trip per slab.
-    const int rr = lane / LPR;
-    const bool live = rr < 16 && n < N;
-    const uint16_t* zb = nullptr;
+    // first slab is finished -- the generic path waits one L2 / HBM round trip per slab.  SL row
+    // slabs go through LDS per pass, so all 64 lanes work when a wave tile is only 32 (16) columns
+    // wide (RPP = 32 (64) rows per pass): half (a quarter) as many epilogue instructions per output.
+    constexpr int SL = RPP >= 64 ? 4 : (RPP >= 32 ? 2 : 1);
+    constexpr int NP = 4 / SL;
+    constexpr int PR = 16 * SL;                 // rows per pass
+    float* es2 = (float*)smem + wid * PR * LDSTR;
+    const int rr = lane / LPR;                  // row within a pass
+    const bool live = rr < PR && n < N;
     u32x4_t pb0 = {}, pb1 = {}, pp0 = {}, pp1 = {};
-    u32x4_t pr[4][2];
+    u32x4_t pr[NP][2];
     f32x4_t ps[4], pt[4];
     if (live) {
       if (ep.bias) {
-        zb = (const uint16_t*)ep.bias + n;
+        const uint16_t* zb = (const uint16_t*)ep.bias + n;
         pb0 = *(const u32x4_t*)zb;
         pb1 = *(const u32x4_t*)(zb + 8);
       }
@@ -199,12 +204,12 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
         pp1 = *(const u32x4_t*)(ep.prelu + n + 8);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = min(m0 + wm * 64 + i * 16 + rr, M - 1);
+      for (int p = 0; p < NP; ++p) {
+        const int m = min(m0 + wm * 64 + p * PR + rr, M - 1);
         if (ep.residual) {
           const uint16_t* t = ep.residual + (int64_t)m * ep.ldr + n;
-          pr[i][0] = *(const u32x4_t*)t;
-          pr[i][1] = *(const u32x4_t*)(t + 8);
+          pr[p][0] = *(const u32x4_t*)t;
+          pr[p][1] = *(const u32x4_t*)(t + 8);
         }
       }
       if (ep.aff_s) {
@@ -215,18 +220,20 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
         }
       }
     }
-    Unroll<0, 4>::run([&](const int i) {
+    Unroll<0, NP>::run([&](const int p) {
 #pragma unroll
-      for (int j = 0; j < NR; ++j)
+      for (int sl = 0; sl < SL; ++sl)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) es[(g * 4 + r) * LDSTR + j * 16 + frow] = acc[i][j][r];
+        for (int j = 0; j < NR; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) es2[(sl * 16 + g * 4 + r) * LDSTR + j * 16 + frow] = acc[p * SL + sl][j][r];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      const int m = m0 + wm * 64 + i * 16 + rr;
+      const int m = m0 + wm * 64 + p * PR + rr;
       if (live && m < M) {
         float v[16], f[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const f32x4_t t = *(const f32x4_t*)(es + rr * LDSTR + cc + q * 4);
+          const f32x4_t t = *(const f32x4_t*)(es2 + rr * LDSTR + cc + q * 4);
           v[q * 4 + 0] = t[0]; v[q * 4 + 1] = t[1]; v[q * 4 + 2] = t[2]; v[q * 4 + 3] = t[3];
         }
         if (ep.bias) {
@@ -243,8 +250,8 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
           for (int q = 0; q < 16; ++q) v[q] = v[q] > 0.f ? v[q] : v[q] * f[q];
         }
         if (ep.residual) {
-          unpack8(pr[i][0], f);
-          unpack8(pr[i][1], f + 8);
+          unpack8(pr[p][0], f);
+          unpack8(pr[p][1], f + 8);
 #pragma unroll
           for (int q = 0; q < 16; ++q) v[q] += f[q];
         }
