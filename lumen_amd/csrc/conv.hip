@@ -211,16 +211,16 @@ hipError_t conv2d_igemm(const ConvArgs& a, const GemmEpi& ep, int tile, hipStrea
   // Cin % 64 == 0 layers (IResNet, SCRFD / DBNet trunks): the LDS-DMA pipeline
   // (profiles/r2_conv_lds_v1.txt); other shapes use the register-staged kernels
   if (tile < 0 && conv_lds_ok(a)) return conv2d_lds(a, ep, 0, stream);
-  // Cin 8 / 16 / 32 stems with Cout >= 64: the same pipeline with several taps per K step, 128 x 64
-  // tiles (IResNet stem 250 -> 189 us, SCRFD 32 -> 64 stride-2 conv 173 -> 146 us at 128 faces /
-  // 32 images); with Cout 32 the register-staged 128 x 32 kernel stays faster
-  // (profiles/r4_conv_small_cin_v1.jsonl)
-  static const int small_lds = [] {
+  // Cin 8 / 16 / 32 stems: the same pipeline with several taps per K step -- 128 x 64 tiles for
+  // Cout >= 64 (IResNet stem 245 -> 152 us, SCRFD 32 -> 64 stride-2 conv 187 -> 129 us at 128 faces /
+  // 32 images), 128 x 32 for Cout 32 (SCRFD 640 px stems 298 -> 276 and 349 -> 327 us)
+  // (profiles/r4_conv_small_cin_v2.jsonl)
+  static const bool small_lds = [] {
     const char* e = std::getenv("LUMEN_CONV_SMALL_LDS");
-    return e == nullptr ? 1 : (e[0] == '0' ? 0 : 2);     // 1: Cout >= 64 only, 2: always
+    return e == nullptr || e[0] != '0';
   }();
-  if (tile < 0 && small_lds && conv_lds_small_ok(a) && (small_lds == 2 || a.Cout >= 64))
-    return conv2d_lds_small(a, ep, a.Cout >= 64 ? 10 : 0, stream);
+  if (tile < 0 && small_lds && a.KH * a.KW >= 9 && conv_lds_small_ok(a))     // spatial stems, not 1x1 pointwise
+    return conv2d_lds_small(a, ep, a.Cout >= 64 ? 10 : 9, stream);
   if (tile < 0) {
     const int64_t t128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
     if (a.Cout >= 128 && t128 >= 256) tile = 0;
