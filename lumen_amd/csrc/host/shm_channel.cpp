@@ -23,6 +23,12 @@
 // (not process-private) futex on a word of the region with a timeout, so a dead peer costs a
 // timeout, never a hang.  The engine writes a heartbeat; a restarted engine bumps the
 // generation and fails the slots its predecessor left RUNNING.
+//
+// A front end that stops waiting (timeout) ABANDONS its slot instead of leaking it: a slot that
+// is still queued is marked ABANDONED_Q and the engine frees it when it pops it; one that is
+// running is marked ABANDONED_R and the engine frees it at completion (or a restarted engine
+// frees it); one that already finished is freed by the front end on the spot.  Every hand-over
+// is a compare-and-swap on the state word, so exactly one side returns the slot to the free ring.
 #include <linux/futex.h>
 #include <sys/syscall.h>
 #include <time.h>
@@ -40,7 +46,8 @@ namespace {
 constexpr uint32_t kMagic = 0x4c4d4348;   // "LMCH"
 constexpr uint32_t kVersion = 1;
 
-enum State : uint32_t { FREE = 0, FILLING = 1, QUEUED = 2, RUNNING = 3, DONE = 4, ERROR = 5 };
+enum State : uint32_t { FREE = 0, FILLING = 1, QUEUED = 2, RUNNING = 3, DONE = 4, ERROR = 5,
+                       ABANDONED_Q = 6, ABANDONED_R = 7 };
 
 struct alignas(64) Cell {
   std::atomic<uint64_t> seq;
@@ -326,8 +333,14 @@ int lumen_ch_pop_batch(void* base, int* out, int max_n, int wait_ms, int linger_
     const uint32_t seen = h->sq_futex.load(std::memory_order_acquire);
     uint32_t v;
     if (ring_pop(h->sq, sc, &v)) {
+      uint32_t st = QUEUED;
+      if (!sl[v].state.compare_exchange_strong(st, RUNNING, std::memory_order_acq_rel)) {
+        // ABANDONED_Q: its front end gave up while it was queued; free it here
+        h->depth.fetch_sub(1, std::memory_order_relaxed);
+        lumen_ch_release(base, (int)v);
+        continue;
+      }
       sl[v].gen = gen;
-      sl[v].state.store(RUNNING, std::memory_order_release);
       out[n++] = (int)v;
       if (n == 1) linger_deadline = now_ns() + (uint64_t)(linger_us < 0 ? 0 : linger_us) * 1000ull;
       continue;
@@ -345,9 +358,27 @@ void lumen_ch_complete(void* base, int slot, int status) {
   Header* h = H(base);
   Slot& s = slots(base)[slot];
   s.status = (uint32_t)status;
-  s.state.store(status == 0 ? DONE : ERROR, std::memory_order_release);
+  uint32_t st = RUNNING;
+  const bool handed = s.state.compare_exchange_strong(st, status == 0 ? DONE : ERROR, std::memory_order_acq_rel);
   h->depth.fetch_sub(1, std::memory_order_relaxed);
-  futex_wake(&s.state, INT_MAX);
+  if (handed) futex_wake(&s.state, INT_MAX);
+  else if (st == ABANDONED_R) lumen_ch_release(base, slot);   // nobody waits for it any more
+}
+
+// Front end: give up on a submitted slot (after a wait timeout).  Returns 1 when the slot was
+// already finished and is freed here, 0 when the engine will free it (queued / running).
+int lumen_ch_abandon(void* base, int slot) {
+  Slot& s = slots(base)[slot];
+  for (;;) {
+    uint32_t st = s.state.load(std::memory_order_acquire);
+    if (st == DONE || st == ERROR) {
+      lumen_ch_release(base, slot);
+      return 1;
+    }
+    const uint32_t to = st == QUEUED ? ABANDONED_Q : st == RUNNING ? ABANDONED_R : 0;
+    if (to == 0) return -1;   // FREE / FILLING / already abandoned: not a submitted slot
+    if (s.state.compare_exchange_weak(st, to, std::memory_order_acq_rel)) return 0;
+  }
 }
 
 void lumen_ch_heartbeat(void* base, uint32_t pid) {
@@ -371,6 +402,12 @@ int lumen_ch_engine_start(void* base, uint32_t pid) {
   int failed = 0;
   Slot* sl = slots(base);
   for (uint32_t i = 0; i < h->nslots; ++i) {
+    uint32_t ab = ABANDONED_R;   // abandoned while the dead engine ran it: nobody else frees it
+    if (sl[i].state.compare_exchange_strong(ab, FREE, std::memory_order_acq_rel)) {
+      h->depth.fetch_sub(1, std::memory_order_relaxed);
+      lumen_ch_release(base, (int)i);
+      continue;
+    }
     uint32_t st = RUNNING;
     if (sl[i].state.load(std::memory_order_acquire) == RUNNING) {
       char* msg = static_cast<char*>(base) + lumen_ch_result_off(base, (int)i);

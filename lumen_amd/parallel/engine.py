@@ -147,16 +147,15 @@ def _serve_channel(ch: ShmChannel, fn, stop: threading.Event, max_items: int, li
                 _kind, blob, _meta = ch.request(s)
                 kind, items = pickle.loads(bytes(blob))
                 if kind == "__stats__":        # engine counters (tests, tools/serve_bench.py)
-                    ch.complete(s, pickle.dumps([dict(stats)]))
+                    with _stats_lock:
+                        snap = dict(stats)
+                    ch.complete(s, pickle.dumps([snap]))
                     continue
                 groups.setdefault(kind, []).append((s, items))
             except Exception as e:  # noqa: BLE001 - a bad request fails alone
                 ch.complete(s, error=f"bad request: {e}")
         for kind, reqs in groups.items():
             fronts = len({ch.tag(s) >> 32 for s, _ in reqs})
-            stats["max_frontends_per_batch"] = max(stats.get("max_frontends_per_batch", 0), fronts)
-            if fronts > 1:
-                stats["shared_batches"] = stats.get("shared_batches", 0) + 1
             flat = [it for _, items in reqs for it in items]
             try:
                 res: list = []
@@ -167,6 +166,11 @@ def _serve_channel(ch: ShmChannel, fn, stop: threading.Event, max_items: int, li
                     stats["fn_s"] = stats.get("fn_s", 0.0) + time.perf_counter() - t0
                     stats["batches"] = stats.get("batches", 0) + 1
                     stats["batch_items"] = stats.get("batch_items", 0) + len(flat)
+                    stats["items"] = stats.get("items", 0) + len(flat)
+                    stats["slots"] = stats.get("slots", 0) + len(reqs)
+                    stats["max_frontends_per_batch"] = max(stats.get("max_frontends_per_batch", 0), fronts)
+                    if fronts > 1:
+                        stats["shared_batches"] = stats.get("shared_batches", 0) + 1
                 if len(res) != len(flat):
                     raise RuntimeError(f"engine fn returned {len(res)} results for {len(flat)} items")
             except Exception:  # noqa: BLE001 - the whole merged batch failed
@@ -182,9 +186,6 @@ def _serve_channel(ch: ShmChannel, fn, stop: threading.Event, max_items: int, li
                     ch.complete(s, pickle.dumps(part, protocol=pickle.HIGHEST_PROTOCOL))
                 except Exception as e:  # noqa: BLE001 - e.g. a result larger than the slot
                     ch.complete(s, error=f"result: {e}")
-            stats["batches"] = stats.get("batches", 0) + 1
-            stats["items"] = stats.get("items", 0) + len(flat)
-            stats["slots"] = stats.get("slots", 0) + len(reqs)
 
 
 def engine_main(services: dict, device: str, ready_q, stop_ev, max_items: int = 256, linger_us: int = 1500,

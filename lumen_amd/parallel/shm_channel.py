@@ -36,7 +36,7 @@ import numpy as np
 
 from .._native import load_host
 
-FREE, FILLING, QUEUED, RUNNING, DONE, ERROR = range(6)
+FREE, FILLING, QUEUED, RUNNING, DONE, ERROR, ABANDONED_Q, ABANDONED_R = range(8)
 
 _DTYPES = [np.uint8, np.float32, np.int64, np.int32, np.float16, np.int8]
 BYTES = 255            # dtype code of an opaque byte payload / result
@@ -73,6 +73,7 @@ def _lib():
                "lumen_ch_slot_state": (i32, [vp, i32]), "lumen_ch_depth": (i32, [vp]),
                "lumen_ch_acquire": (i32, [vp, i32]), "lumen_ch_submit": (i32, [vp, i32, u64]),
                "lumen_ch_wait": (i32, [vp, i32, i32]), "lumen_ch_release": (None, [vp, i32]),
+               "lumen_ch_abandon": (i32, [vp, i32]),
                "lumen_ch_pop_batch": (i32, [vp, ctypes.POINTER(ctypes.c_int), i32, i32, i32]),
                "lumen_ch_complete": (None, [vp, i32, i32]), "lumen_ch_heartbeat": (None, [vp, u32]),
                "lumen_ch_heartbeat_age_ns": (u64, [vp]), "lumen_ch_engine_start": (i32, [vp, u32])}
@@ -249,8 +250,9 @@ class ShmChannel:
                 raise RuntimeError("shm channel submit failed")
             st = lib.lumen_ch_wait(base, slot, int(timeout * 1000))
             if st < 0:
-                # the engine may still write this slot: leave it out of the free ring (leaked until
-                # an engine restart fails it) rather than hand it to another request
+                # the engine may still write this slot: abandon it (the engine frees it when it
+                # pops or completes it; a finished one is freed here) instead of releasing it
+                lib.lumen_ch_abandon(base, slot)
                 slot = -1
                 raise EngineUnavailable(f"channel {self.name}: no answer in {timeout:.0f} s")
             rb = int(d.rbytes)

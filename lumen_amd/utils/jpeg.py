@@ -76,13 +76,31 @@ class JpegInfo:
         return m
 
 
+def max_pixels() -> int:
+    """Decompression-bomb cap of the device path: Pillow's ``Image.MAX_IMAGE_PIXELS`` (the check
+    the Pillow fallback applies), overridable with ``LUMEN_JPEG_MAX_PIXELS``."""
+    env = os.environ.get("LUMEN_JPEG_MAX_PIXELS")
+    if env:
+        return int(env)
+    try:
+        from PIL import Image
+
+        return int(Image.MAX_IMAGE_PIXELS or (1 << 62))
+    except ImportError:     # pragma: no cover
+        return 89_478_485
+
+
 def info(data: bytes) -> Optional[JpegInfo]:
-    """Header of a baseline JPEG this decoder handles, else None."""
+    """Header of a baseline JPEG this decoder handles, else None.  A frame larger than
+    :func:`max_pixels` is also None: the caller falls back to Pillow, whose bomb check rejects
+    it before any staging buffer is sized from the header."""
     lib = _lib()
     if lib is None or len(data) < 4 or data[:2] != b"\xff\xd8":
         return None
     out = (ctypes.c_int * 32)()
     if lib.lumen_jpeg_info(data, len(data), out) != 0:
+        return None
+    if out[0] * out[1] > max_pixels():
         return None
     nc = out[2]
     comps = [tuple(out[8 + 5 * c + k] for k in range(5)) for c in range(nc)]

@@ -73,6 +73,55 @@ def test_channel_round_trip_in_process():
         ch.close()
 
 
+def test_abandoned_slots_are_reclaimed():
+    """A front end that times out abandons its slot: one abandoned while QUEUED is freed when the
+    engine pops it, one abandoned while RUNNING is freed at completion, so timeouts under load
+    never drain the slot pool."""
+    from lumen_amd.parallel.shm_channel import EngineUnavailable
+
+    ch = ShmChannel.create("ab", ["a"], nslots=2, slot_bytes=1 << 12, result_bytes=1 << 10)
+    try:
+        ch.engine_start()
+        # abandoned while queued (no engine popping): both slots time out
+        for _ in range(2):
+            with pytest.raises(EngineUnavailable):
+                ch.call("a", np.zeros(4, np.int32), timeout=0.05)
+        assert ch.depth() == 2
+        assert ch.pop_batch(4, wait_ms=10) == []        # the engine frees both instead of running them
+        assert ch.depth() == 0
+        # abandoned while running: the engine completes after the front end gave up
+        popped = []
+
+        def slow_engine():
+            while not popped:
+                popped.extend(ch.pop_batch(1, wait_ms=50))
+            time.sleep(0.3)
+            ch.complete(popped[0], np.ones(1, np.float32))
+
+        t = threading.Thread(target=slow_engine, daemon=True)
+        t.start()
+        with pytest.raises(EngineUnavailable):
+            ch.call("a", np.zeros(4, np.int32), timeout=0.1)
+        t.join(5)
+        assert ch.depth() == 0
+        # every slot is usable again
+        stop = threading.Event()
+
+        def eng():
+            while not stop.is_set():
+                for s in ch.pop_batch(2, wait_ms=20):
+                    ch.complete(s, np.asarray([7.0], np.float32))
+
+        t = threading.Thread(target=eng, daemon=True)
+        t.start()
+        for _ in range(6):
+            assert float(ch.call("a", np.zeros(2, np.int32), timeout=5)[0]) == 7.0
+        stop.set()
+        t.join(5)
+    finally:
+        ch.close()
+
+
 def test_two_frontends_share_one_engines_batches():
     # one batch loop, 0.3 s per batch: while the first batch runs, both front ends queue theirs
     es = EngineSet({"echo": ("tests.test_frontends_cpu:echo_engine", {"delay_s": 0.3})}, ["cpu"], nslots=32,
