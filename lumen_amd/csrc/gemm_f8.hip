@@ -579,6 +579,10 @@ static hipError_t launch_f8_sk(const uint8_t* A, int64_t lda, const float* sa, c
   return hipGetLastError();
 }
 
+// intra-workgroup split-K form (csrc/gemm_f8ks.hip)
+hipError_t gemm_f8ks(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw, const float* sw,
+                     void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, hipStream_t stream);
+
 // ---------------------------------------------------------------------------- split-K
 // Mid-size GEMMs whose 128x128 tile count leaves CUs idle (LLaVA vision tower at 577 tokens:
 // 40-160 tiles; 8B prefill o / down at 624 tokens: 160) split K over gridDim.y: each split
@@ -690,6 +694,12 @@ template <bool F8>
 static hipError_t launch_variant(int v, const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
                                  const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, int S,
                                  hipStream_t stream) {
+  if (v == 16) {               // intra-workgroup split-K (fp8 only; its own plain epilogues)
+    if constexpr (F8) {
+      if (ep.split_koff == 0 && S == 1) return gemm_f8ks(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    }
+    v = 2;
+  }
   if ((v >= 9 && v <= 11) || v == 15) {
     if (ep.split_koff == 0) {
       hipError_t e = v == 9 ? launch_f8_sk<3, 4, F8>(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream)

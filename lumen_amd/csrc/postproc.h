@@ -11,7 +11,7 @@ struct DetDecodeArgs {
   const float* bbox;     // [N, H*W*A, 4]        distances (in stride units) or prior deltas
   const float* kps;      // [N, H*W*A, 10] or null
   const float* priors;   // [P, 4] (cx, cy, w, h) normalised, RetinaFace mode; null = SCRFD anchors
-  int N, H, W, A, stride;
+  int N, H, W, A, stride;  // stride < 0 with priors null: already-decoded boxes (x1 y1 x2 y2) * (in_w, in_h)
   int P;                 // candidates per image in this level
   float thresh;
   const float* img_scale;  // [N] letterbox scale (det size / original)

@@ -5,7 +5,8 @@
 //    and face-size filter; survivors are appended to a per-image candidate list
 //    through an atomic counter (reference face onnxrt_backend.py:425-468,
 //    882-1153, 1208-1259; SURVEY F-3/F-5).  Also decodes RetinaFace-style
-//    prior-box outputs (F-4: centre/size regression with variances).
+//    prior-box outputs (F-4: centre/size regression with variances) and already-decoded
+//    (boxes, scores, landmarks) exports (reference onnxrt_backend.py:810-880).
 //  * nms: per-image greedy NMS on the candidate list (one workgroup per image:
 //    bitonic sort by score in LDS, then the kept set is swept in score order
 //    with a block-parallel IoU suppression per kept box; reference _nms
@@ -34,7 +35,18 @@ __global__ void det_decode_kernel(DetDecodeArgs a) {
   if (!(s >= a.thresh)) return;
   const float* bb = strided ? a.bbox + n * a.sN + loc_i * a.sL + anc * 4 : a.bbox + ((int64_t)n * a.P + i) * 4;
   float x1, y1, x2, y2, cx, cy, pw = 0.f, ph = 0.f;
-  if (a.priors == nullptr) {
+  const bool decoded = a.priors == nullptr && a.stride < 0;
+  // decoded mode (generic detector exports that emit boxes directly, reference
+  // _decode_detection_outputs non-SCRFD branch): bbox = (x1, y1, x2, y2) in network-input pixels
+  // times (in_w, in_h), or, with in_w < 0, normalised to the ORIGINAL image (reference
+  // normalized_boxes): scaled by the image size here and by the letterbox scale so the common
+  // "/ sc" below cancels
+  const float fx = decoded ? (a.in_w < 0.f ? a.img_hw[n * 2 + 1] * a.img_scale[n] : a.in_w) : 0.f;
+  const float fy = decoded ? (a.in_h < 0.f ? a.img_hw[n * 2 + 0] * a.img_scale[n] : a.in_h) : 0.f;
+  if (decoded) {
+    cx = cy = 0.f;
+    x1 = bb[0] * fx; y1 = bb[1] * fy; x2 = bb[2] * fx; y2 = bb[3] * fy;
+  } else if (a.priors == nullptr) {
     const int loc = i / a.A;
     cx = (float)((loc % a.W) * a.stride);
     cy = (float)((loc / a.W) * a.stride);
@@ -65,7 +77,9 @@ __global__ void det_decode_kernel(DetDecodeArgs a) {
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       float kx, ky;
-      if (a.priors == nullptr) {
+      if (decoded) {
+        kx = kp[2 * k] * fx; ky = kp[2 * k + 1] * fy;
+      } else if (a.priors == nullptr) {
         kx = cx + kp[2 * k] * a.stride; ky = cy + kp[2 * k + 1] * a.stride;
       } else {
         const float* pr = a.priors + (int64_t)i * 4;

@@ -62,15 +62,63 @@ def det_decode_priors(scores, bbox, kps, priors, thresh, img_scale, img_hw, cand
                 img_scale, img_hw, cand, count, min_size, max_size, priors=priors, var=var, in_wh=in_wh)
 
 
+def det_decode_boxes(scores, bbox, kps, thresh, img_scale, img_hw, cand, count, in_wh=(1.0, 1.0),
+                     min_size=0.0, max_size=1e9):
+    """Already-decoded detector outputs (generic / RetinaFace exports with the decode in the graph;
+    reference onnxrt_backend.py:810-880): scores [N, P] (probabilities), boxes [N, P, 4]
+    (x1, y1, x2, y2) and landmarks [N, P, 10] in network-input pixels times ``in_wh`` -- (1, 1)
+    for pixel outputs, (S, S) for outputs normalised to the input -- or, with ``in_wh`` = (-1, -1),
+    normalised to the ORIGINAL image (reference ``normalized_boxes``).  Same candidate rows,
+    un-letterbox, clip and size filter as the anchor / prior decodes."""
+    N, P = scores.shape
+    if scores.is_cuda:
+        hip_ops().det_decode(scores.float().contiguous(), bbox.float().contiguous(),
+                             kps.float().contiguous() if kps is not None else None, None,
+                             0, 0, 1, -1, float(thresh), img_scale.float().contiguous(), img_hw.float().contiguous(),
+                             float(min_size), float(max_size), 0.0, 0.0, float(in_wh[0]), float(in_wh[1]),
+                             cand, count, int(P), 0, 0, False)
+        return
+    _decode_ref(scores.float(), bbox.float(), kps.float() if kps is not None else None, 0, 0, 1, -1, thresh,
+                img_scale, img_hw, cand, count, min_size, max_size, in_wh=in_wh)
+
+
+def retinaface_priors(in_hw, steps=(8, 16, 32), min_sizes=((16, 32), (64, 128), (256, 512)),
+                      clip: bool = False) -> torch.Tensor:
+    """RetinaFace prior boxes [P, 4] (cx, cy, w, h) normalised to the network input: per level
+    (step, sizes) a ceil(H / step) x ceil(W / step) grid, every cell emitting one square prior per
+    size, in (row, column, size) order -- the layout RetinaFace heads are flattened in."""
+    H, W = int(in_hw[0]), int(in_hw[1])
+    out = []
+    for step, sizes in zip(steps, min_sizes):
+        fh, fw = -(-H // step), -(-W // step)
+        ys, xs = torch.meshgrid(torch.arange(fh, dtype=torch.float32), torch.arange(fw, dtype=torch.float32),
+                                indexing="ij")
+        cx = ((xs + 0.5) * step / W).reshape(-1, 1)
+        cy = ((ys + 0.5) * step / H).reshape(-1, 1)
+        for_sizes = []
+        for ms in sizes:
+            wh = torch.tensor([ms / W, ms / H], dtype=torch.float32).expand(cx.shape[0], 2)
+            for_sizes.append(torch.cat([cx, cy, wh], 1))
+        out.append(torch.stack(for_sizes, 1).reshape(-1, 4))
+    pr = torch.cat(out)
+    return pr.clamp(0, 1) if clip else pr
+
+
 def _decode_ref(sc, bb, kp, H, W, A, stride, thresh, img_scale, img_hw, cand, count, min_size, max_size,
                 priors=None, var=(0.1, 0.2), in_wh=(0.0, 0.0)):
     N, P = sc.shape
+    decoded = priors is None and stride < 0
     for n in range(N):
         s_img = float(img_scale[n])
         ih, iw = float(img_hw[n, 0]), float(img_hw[n, 1])
+        fx = (iw * s_img if in_wh[0] < 0 else in_wh[0]) if decoded else 0.0
+        fy = (ih * s_img if in_wh[1] < 0 else in_wh[1]) if decoded else 0.0
         for i in torch.nonzero(sc[n] >= thresh).flatten().tolist():
             d = bb[n, i]
-            if priors is None:
+            if decoded:
+                cx = cy = 0.0
+                x1, y1, x2, y2 = d[0] * fx, d[1] * fy, d[2] * fx, d[3] * fy
+            elif priors is None:
                 loc = i // A
                 cx, cy = float((loc % W) * stride), float((loc // W) * stride)
                 x1, y1, x2, y2 = cx - d[0] * stride, cy - d[1] * stride, cx + d[2] * stride, cy + d[3] * stride
@@ -93,7 +141,9 @@ def _decode_ref(sc, bb, kp, H, W, A, stride, thresh, img_scale, img_hw, cand, co
             row = [x1, y1, x2, y2, float(sc[n, i])]
             if kp is not None:
                 for k in range(5):
-                    if priors is None:
+                    if decoded:
+                        kx, ky = kp[n, i, 2 * k] * fx, kp[n, i, 2 * k + 1] * fy
+                    elif priors is None:
                         kx, ky = cx + kp[n, i, 2 * k] * stride, cy + kp[n, i, 2 * k + 1] * stride
                     else:
                         pr = priors[i].float()

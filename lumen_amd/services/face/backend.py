@@ -122,6 +122,10 @@ class FaceSpec:
     rec_color: str = "rgb"
     align_landmarks: bool = True
     extra: dict = field(default_factory=dict)
+    # per-channel detector normalisation in the model's channel order (RetinaFace: BGR 104/117/123, std 1)
+    det_mean3: Optional[tuple] = None
+    det_std3: Optional[tuple] = None
+    det_bgr: bool = False
 
 
 def letterbox_geom(h: int, w: int, off: int, S: int):
@@ -210,17 +214,21 @@ class MI355XFaceBackend:
             det_size, rec_size = dcfg.input_size, rcfg.input_size
         else:
             # the reference's InsightFace ONNX pack, run by the MI355X graph executor
-            from .onnx_pack import OnnxArcFace, OnnxSCRFD, find_onnx_pair
+            from .onnx_pack import OnnxArcFace, find_onnx_pair, make_detector
 
             dpath, rpath = find_onnx_pair(r.model_root_path)
             if dpath is None or rpath is None:
                 raise ResourceNotFoundError(
                     f"{r.model_name}: neither lumen_face_config.json (+ safetensors) nor a detection/recognition "
                     f"ONNX pair found in {r.model_root_path}")
-            det, rec = OnnxSCRFD(dpath, self.device, d), OnnxArcFace(rpath, self.device, rc)
+            det, rec = make_detector(dpath, self.device, d), OnnxArcFace(rpath, self.device, rc)
             det_size, rec_size = det.cfg.input_size, rec.cfg.input_size
-        self.spec = FaceSpec(det_size=det_size, det_mean=float(np.mean(d.get("mean", 127.5))),
-                             det_std=float(np.mean(d.get("std", 128.0))), rec_size=rec_size,
+        dm, dsd = d.get("mean", 127.5), d.get("std", 128.0)
+        self.spec = FaceSpec(det_size=det_size, det_mean=float(np.mean(dm)),
+                             det_std=float(np.mean(dsd)), rec_size=rec_size,
+                             det_mean3=tuple(float(v) for v in np.broadcast_to(np.asarray(dm, np.float64), 3)),
+                             det_std3=tuple(float(v) for v in np.broadcast_to(np.asarray(dsd, np.float64), 3)),
+                             det_bgr=str(d.get("color_order", "rgb")).lower() == "bgr",
                              rec_mean=float(np.mean(rc.get("mean", 127.5))), rec_std=float(np.mean(rc.get("std", 127.5))),
                              rec_color=rc.get("color_order", "rgb"), align_landmarks=rc.get("align_landmarks", True))
         self.det, self.rec = det.to(self.device).eval(), rec.to(self.device).eval()
@@ -353,9 +361,11 @@ class MI355XFaceBackend:
             # (strong refs to the images keep their ids from being reused while the map lives)
             tl.last_upload = (dev, {id(im): int(o) for im, o in zip(images, offs)}, list(images))
         with stage("det_preprocess"):
-            x = ops.image_prep(tens, (S, S), mean=(self.spec.det_mean,) * 3, std=(self.spec.det_std,) * 3, scale=1.0,
+            sp = self.spec
+            x = ops.image_prep(tens, (S, S), mean=getattr(sp, "det_mean3", None) or (sp.det_mean,) * 3,
+                               std=getattr(sp, "det_std3", None) or (sp.det_std,) * 3, scale=1.0,
                                filter="cv2_linear", layout="nhwc8", pad=0.0, geoms=geoms, out_dtype=self.dtype,
-                               device=self.device, src=src)
+                               device=self.device, src=src, swap_rb=bool(getattr(sp, "det_bgr", False)))
         with stage("det_forward"):
             heads = self.det(x)
         return images, params, heads, scales
@@ -369,6 +379,7 @@ class MI355XFaceBackend:
         img_scale = h2d(scales, self.device, torch.float32)
         img_hw = h2d([[im.shape[0], im.shape[1]] for im in images], self.device, torch.float32)
         A = self.det.cfg.anchors
+        box_det = hasattr(self.det, "decode")       # RetinaFace-family / generic exports (onnx_pack)
         results: list[Optional[list[FaceDetection]]] = [None] * N
         groups: dict = {}
         for i, p in enumerate(params):
@@ -379,12 +390,16 @@ class MI355XFaceBackend:
             n = len(idx)
             cand = torch.zeros((n, MAX_CAND, 16), dtype=torch.float32, device=self.device)
             count = torch.zeros((n,), dtype=torch.int32, device=self.device)
-            for h, stride in zip(heads, self.det.cfg.strides):
-                hh = h if sel is None else h.index_select(0, sel)
-                vision.det_decode_head(hh, A, stride, p.conf,
-                                       img_scale if sel is None else img_scale.index_select(0, sel),
-                                       img_hw if sel is None else img_hw.index_select(0, sel), cand, count,
-                                       float(p.size_min), float(p.size_max))
+            isc = img_scale if sel is None else img_scale.index_select(0, sel)
+            ihw = img_hw if sel is None else img_hw.index_select(0, sel)
+            if box_det:
+                out = heads if sel is None else self.det.select(heads, sel)
+                self.det.decode(out, p.conf, isc, ihw, cand, count, float(p.size_min), float(p.size_max))
+            else:
+                for h, stride in zip(heads, self.det.cfg.strides):
+                    hh = h if sel is None else h.index_select(0, sel)
+                    vision.det_decode_head(hh, A, stride, p.conf, isc, ihw, cand, count, float(p.size_min),
+                                           float(p.size_max))
             kept = vision.nms(cand, count, p.nms)
             for j, rows in zip(idx, kept):
                 faces = []

@@ -10,6 +10,15 @@ call contract as the native towers:
   reference insightface_specs.py output index map) -> one fused NHWC head per stride
   ``[N, H, W, 15A]`` (score logits | bbox distances | kps distances), which the HIP
   ``det_decode`` + NMS kernels consume unchanged;
+* detector, any other ``type`` (reference ``detector_type`` "retinaface", the default of a
+  non-SCRFD pack; onnxrt_backend.py:810-880): outputs picked by the ``outputs`` index map
+  (``boxes`` / ``scores`` / ``landmarks``) and returned as ``(scores [N, P], boxes [N, P, 4],
+  landmarks [N, P, 10] | None)``.  ``box_encoding`` says what the boxes are:
+  ``"decoded"`` (the reference's contract: corner boxes in input pixels, or normalised to the
+  original image with ``normalized_boxes``) -> ``vision.det_decode_boxes``; ``"priors"`` (a raw
+  RetinaFace export: centre / size regressions against the prior grid of ``steps`` /
+  ``min_sizes`` with ``variance``) -> ``vision.det_decode_priors``.  Two-column class scores
+  (background, face) take the face column (softmax first when they are logits);
 * recogniser: aligned 112x112 crops -> L2-normalised embeddings.
 """
 from __future__ import annotations
@@ -90,6 +99,111 @@ class OnnxSCRFD:
                 m["kps"] < len(outs) else torch.zeros(N, H, W, 10 * A, device=sc.device)
             heads.append(torch.cat([logit, bb, kp], dim=-1).contiguous())
         return heads
+
+
+@dataclass
+class _BoxDetCfg:
+    input_size: int = 640
+    strides: list = field(default_factory=list)
+    anchors: int = 1
+
+
+class OnnxBoxDetector:
+    """Non-SCRFD detector export (RetinaFace family / generic): see the module docstring."""
+
+    def __init__(self, path, device, spec: dict):
+        self.g = OnnxGraph(path, device)
+        self.cfg = _BoxDetCfg(int(spec.get("input_size", (640, 640))[0]))
+        self.kind = "priors" if str(spec.get("box_encoding", "decoded")).lower() == "priors" else "decoded"
+        om = spec.get("outputs")
+        if not isinstance(om, dict):        # a SCRFD-style list does not apply: reference defaults
+            om = {}
+        self.idx = {"boxes": om.get("boxes", 0), "scores": om.get("scores", 1), "landmarks": om.get("landmarks", 2)}
+        self.normalized = bool(spec.get("normalized_boxes", False))
+        self.score_act = str(spec.get("score_activation", "auto")).lower()
+        self.var = tuple(float(v) for v in spec.get("variance", (0.1, 0.2)))
+        self.priors = None
+        if self.kind == "priors":
+            from ...ops.vision import retinaface_priors
+
+            S = self.cfg.input_size
+            self.priors = retinaface_priors((S, S), tuple(spec.get("steps", (8, 16, 32))),
+                                            tuple(tuple(m) for m in spec.get("min_sizes", ((16, 32), (64, 128),
+                                                                                            (256, 512))))
+                                            ).to(device)
+
+    def eval(self):
+        return self
+
+    def to(self, _):
+        return self
+
+    def _run(self, x: torch.Tensor) -> list:
+        return self.g.run({self.g.model.graph.inputs[0]: x})
+
+    def _scores(self, sc: torch.Tensor, N: int) -> torch.Tensor:
+        sc = sc.float().reshape(N, -1, sc.shape[-1]) if sc.dim() >= 2 and sc.shape[-1] in (1, 2) else \
+            sc.float().reshape(N, -1, 1)
+        if sc.shape[-1] == 2:
+            logits = self.score_act == "softmax" or (self.score_act == "auto" and
+                                                     bool(((sc < 0) | (sc > 1)).any()))
+            if logits:
+                sc = torch.softmax(sc, -1)
+            sc = sc[..., 1:]
+        elif self.score_act == "sigmoid":
+            sc = torch.sigmoid(sc)
+        return sc[..., 0].contiguous()
+
+    def __call__(self, x: torch.Tensor):
+        xn = _to_nchw3(x)
+        N = xn.shape[0]
+        outs = self._run(xn)
+        b0 = outs[self.idx["boxes"]]
+        if b0.dim() >= 2 and b0.shape[0] != N and N > 1:    # fixed-batch-1 graph: image by image
+            per = [self._run(xn[i:i + 1]) for i in range(N)]
+            outs = [torch.cat([p[j] for p in per]) for j in range(len(per[0]))]
+        boxes = outs[self.idx["boxes"]].float()
+        C = boxes.shape[-1]
+        boxes = boxes.reshape(N, -1, C)
+        si, li = self.idx["scores"], self.idx["landmarks"]
+        if si is not None and si < len(outs):
+            scores = self._scores(outs[si], N)
+        elif C >= 5:                                          # [x1 y1 x2 y2 score] rows
+            scores = boxes[..., 4].contiguous()
+        else:
+            scores = torch.ones(boxes.shape[:2], device=boxes.device)
+        boxes = boxes[..., :4].contiguous()
+        kps = None
+        if li is not None and li < len(outs):
+            k = outs[li].float()
+            if k.numel() == boxes.shape[0] * boxes.shape[1] * 10:
+                kps = k.reshape(N, -1, 10).contiguous()
+        P = min(boxes.shape[1], scores.shape[1])
+        return scores[:, :P].contiguous(), boxes[:, :P].contiguous(), None if kps is None else kps[:, :P].contiguous()
+
+    def decode(self, out, thresh, img_scale, img_hw, cand, count, min_size, max_size):
+        """Candidate rows of one batch (``vision`` decode kernels), as the SCRFD heads' decode."""
+        from ...ops import vision
+
+        scores, boxes, kps = out
+        if self.kind == "priors":
+            S = float(self.cfg.input_size)
+            vision.det_decode_priors(scores, boxes, kps, self.priors, thresh, img_scale, img_hw, cand, count, (S, S),
+                                     var=self.var, min_size=min_size, max_size=max_size)
+        else:
+            vision.det_decode_boxes(scores, boxes, kps, thresh, img_scale, img_hw, cand, count,
+                                    (-1.0, -1.0) if self.normalized else (1.0, 1.0), min_size, max_size)
+
+    @staticmethod
+    def select(out, sel):
+        return tuple(None if t is None else t.index_select(0, sel) for t in out)
+
+
+def make_detector(path, device, spec: dict):
+    """The ONNX detector adapter for a pack's detection spec (``type``: "scrfd" or any other)."""
+    if str(spec.get("type", "scrfd")).lower() == "scrfd":
+        return OnnxSCRFD(path, device, spec)
+    return OnnxBoxDetector(path, device, spec)
 
 
 class OnnxArcFace:

@@ -157,7 +157,7 @@ def test_gemm_f8_splitk_vs_fp32_reference(M, N, K, glu):
     assert torch.equal(got, again)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
 @pytest.mark.parametrize("M,N,K,splits", [(624, 6144, 4096, 1), (624, 4096, 4096, 2), (300, 1536, 1024, 1),
                                           (97, 768, 2048, 4), (130, 1040, 1024, 1)])
 def test_gemm_f8_pipeline_variants(M, N, K, splits, variant):
@@ -171,6 +171,37 @@ def test_gemm_f8_pipeline_variants(M, N, K, splits, variant):
     got = ops.linear_f8(x8.to(DEV), xs.to(DEV), wd, ws.to(DEV), bias=b.to(DEV), residual=r.to(DEV),
                         splits=splits, variant=variant)
     assert _rel(got, ref) < 8e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(624, 6144, 4096), (624, 4096, 14336), (130, 1040, 128), (200, 512, 256),
+                                   (333, 768, 384), (624, 1024, 1152), (64, 256, 1024)])
+@pytest.mark.parametrize("epi", ["bf16_bias_res", "f32_bias", "glu", "plain"])
+def test_gemm_f8_intra_wg_splitk(M, N, K, epi):
+    """Intra-workgroup split-K fp8 GEMM (variant 16, csrc/gemm_f8ks.hip): both wave groups' K
+    halves (odd and even K-step counts, one K-step), ragged M, the prefetched fast epilogue (bf16
+    bias, residual, SwiGLU) and the generic one (fp32 bias) against the fp32 reference; repeat
+    launches are bitwise identical."""
+    g, x8, xs, w8, ws = _f8_operands(M, N, K, M + N + K)
+    dev_args = (x8.to(DEV), xs.to(DEV), w8.to(DEV), ws.to(DEV))
+    acc = (x8.float() @ w8.float().t()) * xs[:, None] * ws[None, :]
+    if epi == "glu":
+        ref = ops.linear_f8(x8, xs, w8, ws, glu=True)
+        got = ops.linear_f8(*dev_args, glu=True, variant=16)
+        assert got.shape == (M, N // 2) and _rel(got, ref) < 1e-2
+        return
+    kw, ref = {}, acc
+    if epi == "bf16_bias_res":
+        b = torch.randn(N, generator=g).bfloat16()
+        r = torch.randn(M, N, generator=g).bfloat16()
+        kw = {"bias": b.to(DEV), "residual": r.to(DEV)}
+        ref = acc + b.float() + r.float()
+    elif epi == "f32_bias":
+        b = torch.randn(N, generator=g)
+        kw = {"bias": b.to(DEV)}
+        ref = acc + b
+    got = ops.linear_f8(*dev_args, variant=16, **kw)
+    assert _rel(got, ref) < 8e-3
+    assert torch.equal(got, ops.linear_f8(*dev_args, variant=16, **kw))
 
 
 @pytest.mark.parametrize("tile", [20011, 20012, 20013, 20014, 20015, 20016, 20017, 20018, 20019, 20020, 20021,
