@@ -45,11 +45,14 @@ class AppService:
         self.names = names
 
     @classmethod
-    def from_app_config(cls, config: LumenConfig, initialize: bool = True) -> "AppService":
+    def from_app_config(cls, config: LumenConfig, initialize: bool = True, proxies: Optional[dict] = None,
+                        only=None) -> "AppService":
         """Each enabled service is built and initialised under its GPU set
         (runtime/placement.py: disjoint GPUs per service, DP workers per GPU).  In a serving front
         end (parallel/engine.py) a service whose engines are attached finds them through
-        ``remote_scope`` and loads no model here."""
+        ``remote_scope`` and loads no model here; a service in ``proxies`` (name -> address) is a
+        :class:`~lumen_amd.hub.proxy.ProxyService` to the serving parent.  ``only``: build just
+        these services (the parent's share of a mixed topology)."""
         from ..parallel.engine import remote_scope
         from ..runtime import placement
 
@@ -57,6 +60,14 @@ class AppService:
         enabled = config.enabled_services()
         plan = placement.plan_from_env(list(enabled))
         for name, svc_cfg in enabled.items():
+            if only is not None and name not in only:
+                continue
+            if proxies and name in proxies:
+                from .proxy import ProxyService
+
+                services.append(ProxyService(proxies[name], name))
+                names.append(name)
+                continue
             cls_ = ServiceLoader.get_class(svc_cfg.import_info.registry_class)
             with placement.use(plan.get(name)), remote_scope(name):
                 svc = cls_.from_config(svc_cfg, config.cache_path())
@@ -141,15 +152,16 @@ def _replica_main(config_path: str, port: int, mode: str, stop_event, ready_q, i
 
 
 def _frontend_main(config_path: str, port: int, mode: str, stop_event, ready_q, idx: int, parent_pid: int,
-                   specs: dict) -> None:
+                   specs: dict, proxies: Optional[dict] = None) -> None:
     """A serving front-end process (spawned before any GPU use): the services of the config with
-    their GPU work forwarded to the engine processes, gRPC on the shared port (SO_REUSEPORT)."""
+    their GPU work forwarded to the engine processes (or, for ``proxies``, whole requests to the
+    serving parent), gRPC on the shared port (SO_REUSEPORT)."""
     setup_logging(os.environ.get("LUMEN_LOG_LEVEL", "INFO"))
     from ..parallel.engine import attach_frontend
 
     attach_frontend(specs)
     serve(config_path, port, mode=mode, stop_event=stop_event, procs=1, replica=idx, ready_q=ready_q,
-          parent_pid=parent_pid, frontends=0)
+          parent_pid=parent_pid, frontends=0, proxies=proxies)
 
 
 def engine_devices() -> list[str]:
@@ -169,27 +181,36 @@ def engine_devices() -> list[str]:
 def serve_frontends(config_path: str, port: int, frontends: int, mode: str = "hub",
                     stop_event: Optional[threading.Event] = None, ready_q=None, devices=None) -> bool:
     """Engine/front-end topology: one GPU engine process per device holding the models, and
-    ``frontends`` gRPC front-end processes sharing ``port``.  Returns False (nothing started) when
-    a service of the config cannot run on engines -- the caller then serves in-process."""
+    ``frontends`` gRPC front-end processes sharing ``port``.  A service that cannot run on engines
+    (``engine_spec()`` None: a tensor-parallel VLM) is served by THIS process on a private local
+    socket, and the front ends proxy its tasks there (hub/proxy.py): a mixed topology, never an
+    all-or-nothing fallback.  Returns False (nothing started) only when no service can use engines."""
     import multiprocessing as mp
+    import tempfile
 
     from ..parallel.engine import EngineSet
 
     config = load_and_validate_config(config_path)
     handle_download_results(Downloader(config).download_all())
-    specs = {}
+    specs, local = {}, []
+    exclude = {x.strip() for x in os.environ.get("LUMEN_ENGINE_EXCLUDE", "").split(",") if x.strip()}
     for name, svc_cfg in config.enabled_services().items():
         cls_ = ServiceLoader.get_class(svc_cfg.import_info.registry_class)
         svc = cls_.from_config(svc_cfg, config.cache_path())   # not initialised: no model, no GPU
-        spec = svc.engine_spec() if hasattr(svc, "engine_spec") else None
+        spec = svc.engine_spec() if hasattr(svc, "engine_spec") and name not in exclude else None
         try:
             svc.close()
         except Exception:  # noqa: BLE001
             pass
         if spec is None:
-            log.warning("service %s cannot run on GPU engines: serving in-process instead", name)
-            return False
-        specs[name] = spec
+            log.warning("service %s cannot run on GPU engines: served by the parent process, proxied by the "
+                        "front ends", name)
+            local.append(name)
+        else:
+            specs[name] = spec
+    if not specs:
+        log.warning("no service of this config can run on GPU engines: serving in-process instead")
+        return False
     devs = list(devices or engine_devices())
     log.info("starting %d GPU engine(s) on %s for %s", len(devs), devs, list(specs))
     # batch loops per (engine, service): one runs its GPU work while the other assembles / decodes the
@@ -201,11 +222,26 @@ def serve_frontends(config_path: str, port: int, frontends: int, mode: str = "hu
     ctx = mp.get_context("spawn")
     stop = ctx.Event()
     rq = ready_q if ready_q is not None else ctx.Queue()
+    addr = f"unix:{tempfile.gettempdir()}/lumen-hub-{os.getpid()}-{uuid.uuid4().hex[:8]}.sock" if local else None
+    proxies = {name: addr for name in local}
+    # front ends first: they are spawned before this process initialises any GPU (a spawned child
+    # must not start from a GPU-initialised parent); their proxies wait for the local server
     procs = [ctx.Process(target=_frontend_main, args=(config_path, port, mode, stop, rq, i + 1, os.getpid(),
-                                                      engines.frontend_specs()), daemon=False)
+                                                      engines.frontend_specs(), proxies), daemon=False)
              for i in range(frontends)]
     for p in procs:
         p.start()
+    local_app = local_server = None
+    if local:
+        local_app = AppService.from_app_config(config, only=set(local))
+        local_server = grpc.server(futures.ThreadPoolExecutor(max_workers=64),
+                                   options=[("grpc.max_receive_message_length", 64 * 1024 * 1024),
+                                            ("grpc.max_send_message_length", 64 * 1024 * 1024)])
+        HubRouter(local_app.services).attach_to_server(local_server)
+        if local_server.add_insecure_port(addr) == 0:
+            raise RuntimeError(f"cannot bind {addr}")
+        local_server.start()
+        log.info("parent serves %s on %s for the front ends", local, addr)
     if ready_q is None:
         for _ in procs:
             rq.get(timeout=900)
@@ -228,6 +264,13 @@ def serve_frontends(config_path: str, port: int, frontends: int, mode: str = "hu
         p.join(timeout=30)
         if p.is_alive():
             p.kill()
+    if local_server is not None:
+        local_server.stop(grace=2)
+        local_app.close()
+        try:
+            os.unlink(addr[len("unix:"):])
+        except OSError:
+            pass
     engines.close()
     return True
 
@@ -264,7 +307,8 @@ def start_replicas(config_path: str, port: int, n: int, mode: str = "hub", ready
 
 def serve(config_path: str, port_override: Optional[int] = None, mode: str = "hub",
           stop_event: Optional[threading.Event] = None, procs: Optional[int] = None, replica: int = 0,
-          ready_q=None, parent_pid: Optional[int] = None, frontends: Optional[int] = None) -> None:
+          ready_q=None, parent_pid: Optional[int] = None, frontends: Optional[int] = None,
+          proxies: Optional[dict] = None) -> None:
     """Run the server.  ``frontends`` > 0 (or LUMEN_FRONTENDS): GPU engine processes + that many
     front-end processes on one port (:func:`serve_frontends`).  ``procs`` > 1 (or LUMEN_HUB_PROCS):
     this process plus procs - 1 spawned full replicas accept on the same port (SO_REUSEPORT; a
@@ -289,7 +333,7 @@ def serve(config_path: str, port_override: Optional[int] = None, mode: str = "hu
         if not port0:
             raise SystemExit("LUMEN_HUB_PROCS > 1 needs a fixed server.port")
         reps, rep_stop = start_replicas(config_path, port0, nproc - 1, mode)
-    app = AppService.from_app_config(config)
+    app = AppService.from_app_config(config, proxies=proxies)
     if mode == "single":
         target = config.deployment.service
         idx = app.names.index(target) if target in app.names else 0

@@ -105,6 +105,66 @@ class RemotePool:
     def close(self) -> None:
         self._ex.shutdown(wait=False)
 
+    def prefixed(self, prefix: str) -> "PrefixedRemote":
+        """A view of this pool for one model of a multi-model service (SmartCLIP: general CLIP +
+        BioCLIP on one engine, :func:`multi_worker`): every kind is sent as ``prefix:kind``."""
+        return PrefixedRemote(self, prefix)
+
+
+class PrefixedRemote:
+    """:class:`RemotePool` facade whose task kinds carry a model prefix (see :func:`multi_worker`)."""
+
+    def __init__(self, pool: RemotePool, prefix: str):
+        self.pool = pool
+        self.prefix = prefix
+        self.info = pool.info
+
+    @property
+    def size(self) -> int:
+        return self.pool.size
+
+    def submit(self, kind: str, items: list, worker: Optional[int] = None) -> Future:
+        return self.pool.submit(f"{self.prefix}:{kind}", items, worker)
+
+    def run(self, kind: str, items: Sequence, timeout: Optional[float] = None) -> list:
+        return self.pool.run(f"{self.prefix}:{kind}", items, timeout)
+
+    def broadcast(self, kind: str, items: list, timeout: Optional[float] = None) -> list:
+        return self.pool.broadcast(f"{self.prefix}:{kind}", items, timeout)
+
+    def close(self) -> None:       # the shared pool is closed by its owner
+        pass
+
+
+def is_remote(pool) -> bool:
+    return isinstance(pool, (RemotePool, PrefixedRemote))
+
+
+def _call_factory(path: str, device: str, kwargs: dict, rank: int, world: int):
+    fac = _resolve(path)
+    kw = dict(kwargs)
+    params = inspect.signature(fac).parameters
+    if "rank" in params and "rank" not in kw:
+        kw["rank"] = rank
+    if "world" in params and "world" not in kw:
+        kw["world"] = world
+    return fac(device, **kw)
+
+
+def multi_worker(device: str, parts: dict, rank: int = 0, world: int = 1):
+    """Engine factory of a multi-model service: ``parts`` = name -> (factory path, kwargs); the
+    batch function routes kind ``name:kind`` to that part's function (the front end's backends talk
+    to it through :meth:`RemotePool.prefixed`)."""
+    fns = {name: _call_factory(path, device, kw, rank, world) for name, (path, kw) in parts.items()}
+
+    def fn(kind, items):
+        name, sep, sub = kind.partition(":")
+        if not sep or name not in fns:
+            raise ValueError(f"multi-model engine: unknown kind {kind!r} (parts {list(fns)})")
+        return fns[name](sub, items)
+
+    return fn
+
 
 _REMOTE: dict = {}
 _scope = threading.local()
@@ -189,27 +249,26 @@ def _serve_channel(ch: ShmChannel, fn, stop: threading.Event, max_items: int, li
 
 
 def engine_main(services: dict, device: str, ready_q, stop_ev, max_items: int = 256, linger_us: int = 1500,
-                threads_per_service: int = 2) -> None:
-    """Engine process body.  ``services``: name -> (ChannelSpec, factory path, kwargs).  Pins the
-    device, builds every service's batch function, then serves each channel with
-    ``threads_per_service`` batch loops (one batch's host work overlaps the other's GPU work)."""
+                threads_per_service: int = 2, rank: int = 0, world: int = 1) -> None:
+    """Engine process body.  ``services``: name -> (ChannelSpec, factory path, kwargs[, options]).
+    Pins the device, builds every service's batch function (factories taking ``rank`` / ``world``
+    get this engine's index / the engine count: a label bank is sharded over the engines), then
+    serves each channel with ``threads_per_service`` batch loops (one batch's host work overlaps the
+    other's GPU work; a service's ``options["threads"]`` overrides it -- a continuous-batching
+    service keeps one loop per request in flight)."""
     try:
         if device.startswith("cuda"):
             import torch
 
             torch.cuda.set_device(torch.device(device))
-        chans, fns = {}, {}
-        for name, (spec, factory, kwargs) in services.items():
+        chans, fns, nthreads = {}, {}, {}
+        for name, entry in services.items():
+            spec, factory, kwargs = entry[:3]
+            opts = entry[3] if len(entry) > 3 else {}
             ch = ShmChannel.attach(spec)
-            fac = _resolve(factory)
-            kw = dict(kwargs)
-            params = inspect.signature(fac).parameters
-            if "rank" in params and "rank" not in kw:
-                kw["rank"] = 0
-            if "world" in params and "world" not in kw:
-                kw["world"] = 1
-            fns[name] = fac(device, **kw)
+            fns[name] = _call_factory(factory, device, kwargs, rank, world)
             chans[name] = ch
+            nthreads[name] = int(opts.get("threads", threads_per_service))
         for ch in chans.values():
             failed = ch.engine_start()
             if failed:
@@ -222,7 +281,7 @@ def engine_main(services: dict, device: str, ready_q, stop_ev, max_items: int = 
     stats: dict = {}
     ths = []
     for name, ch in chans.items():
-        for i in range(threads_per_service):
+        for i in range(nthreads[name]):
             t = threading.Thread(target=_serve_channel, args=(ch, fns[name], stop, max_items, linger_us, stats),
                                  name=f"lumen-engine-{name}-{i}", daemon=True)
             t.start()
@@ -259,7 +318,7 @@ class EngineSet:
     def __init__(self, services: dict, devices: Sequence[str], nslots: int = 64, slot_bytes: int = 32 << 20,
                  result_bytes: int = 4 << 20, start_timeout_s: float = 900.0, respawn: bool = True,
                  threads_per_service: int = 2, linger_us: int = 1500, max_items: int = 256):
-        """``services``: name -> (factory path, kwargs)."""
+        """``services``: name -> (factory path, kwargs[, options])."""
         self.services = dict(services)
         self.loop_args = (max_items, linger_us, threads_per_service)
         self.devices = list(devices)
@@ -279,8 +338,9 @@ class EngineSet:
         self._mon.start()
 
     def _spawn(self, i: int) -> None:
-        svc = {name: (self.channels[name][i].spec(), fac, kw) for name, (fac, kw) in self.services.items()}
-        p = self._ctx.Process(target=engine_main, args=(svc, self.devices[i], self._ready, self._stop, *self.loop_args),
+        svc = {name: (self.channels[name][i].spec(), *entry) for name, entry in self.services.items()}
+        p = self._ctx.Process(target=engine_main, args=(svc, self.devices[i], self._ready, self._stop, *self.loop_args,
+                                                        i, len(self.devices)),
                               name=f"lumen-engine-{i}", daemon=False)
         p.start()
         self.procs[i] = p
@@ -343,5 +403,5 @@ def engine_factory_of(service_cls, svc_cfg, cache_dir) -> Optional[tuple]:
 
 
 # a ChannelSpec must be importable where pickled objects are rebuilt
-__all__ = ["RemotePool", "EngineSet", "engine_main", "attach_frontend", "install_remote", "remote_scope",
-           "current_remote", "engine_factory_of", "ChannelSpec"]
+__all__ = ["RemotePool", "PrefixedRemote", "EngineSet", "engine_main", "attach_frontend", "install_remote",
+           "remote_scope", "current_remote", "engine_factory_of", "multi_worker", "is_remote", "ChannelSpec"]

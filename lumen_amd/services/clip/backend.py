@@ -119,6 +119,7 @@ class MI355XClipBackend:
         self._img_batcher: Optional[DynamicBatcher] = None
         self._txt_batcher: Optional[DynamicBatcher] = None
         self.shard_bank = False        # BioCLIP: each DP worker holds a slice of the label bank
+        self.remote_key: Optional[str] = None   # multi-model service: this model's part of the engine
         self.is_initialized = False
 
     # ------------------------------------------------------------------ lifecycle
@@ -136,6 +137,8 @@ class MI355XClipBackend:
         from ...parallel.engine import current_remote
 
         remote = current_remote()
+        if remote is not None and self.remote_key:
+            remote = remote.prefixed(self.remote_key)
         if remote is not None:
             # serving front end (parallel/engine.py): the towers live in the GPU engine processes;
             # this process decodes, tokenises and ships batches there
@@ -206,9 +209,9 @@ class MI355XClipBackend:
     @property
     def remote(self) -> bool:
         """True in a serving front end: batches go to the GPU engine processes (decoded here)."""
-        from ...parallel.engine import RemotePool
+        from ...parallel.engine import is_remote
 
-        return isinstance(self._pool, RemotePool)
+        return is_remote(self._pool)
 
     # ------------------------------------------------------------------ batched workers
     def tokenize(self, texts: Sequence[str]) -> torch.Tensor:
@@ -380,12 +383,19 @@ def dp_worker(device: str, cache_dir: str, model: str, runtime: str, dataset: Op
     return fn
 
 
-def engine_spec(resources: ModelResources) -> tuple:
-    """(factory path, kwargs) of the GPU engine side of this backend (parallel/engine.py)."""
+def engine_spec(resources: ModelResources, shard_bank: bool = False) -> tuple:
+    """(factory path, kwargs) of the GPU engine side of this backend (parallel/engine.py).
+    ``shard_bank``: every engine holds its rank / world slice of the stored label bank (BioCLIP's
+    TreeOfLife bank), queried by broadcast from the front ends (runtime/label_bank.PoolShardedBank)."""
     r = resources
     return ("lumen_amd.services.clip.backend:dp_worker",
             {"cache_dir": str(r.model_root_path.parent.parent), "model": r.model_name, "runtime": r.runtime,
-             "dataset": r.dataset, "shard_bank": False})
+             "dataset": r.dataset, "shard_bank": bool(shard_bank)})
+
+
+def bio_shards_bank(resources: ModelResources) -> bool:
+    """A BioCLIP model with a stored bank: sharded over the GPU workers / engines."""
+    return resources.labels is not None and len(resources.labels) > 0 and resources.label_embeddings is not None
 
 
 def create_backend(backend_settings, resources: ModelResources, runtime: Optional[str] = None,

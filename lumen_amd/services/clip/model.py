@@ -141,7 +141,11 @@ class BioCLIPModelManager:
             return
         # with DP workers and a stored bank (TreeOfLife, 10^5-10^6 x 768), every GPU worker
         # holds 1/world of it (K13): queries are broadcast, candidates merged here
-        shard = self.labels and self.resources.label_embeddings is not None and self.backend.dp_size > 1
+        from ...parallel.engine import current_remote
+
+        # serving front end: the engines hold the bank slices (services/clip engine_spec(shard_bank=True))
+        shard = self.labels and self.resources.label_embeddings is not None and \
+            (self.backend.dp_size > 1 or current_remote() is not None)
         self.backend.shard_bank = bool(shard)
         self.backend.initialize()
         if self.labels:
@@ -150,7 +154,7 @@ class BioCLIPModelManager:
                 emb = orient_bank(self.resources.label_embeddings, len(self.labels), dim)
                 self.text_embeddings = emb                  # memory-mapped; never loaded whole here
                 self.bank = PoolShardedBank(self.backend._pool, emb.shape[0])
-                log.info("BioCLIP bank %d x %d sharded over %d DP workers", emb.shape[0], emb.shape[1],
+                log.info("BioCLIP bank %d x %d sharded over %d GPU worker(s) / engine(s)", emb.shape[0], emb.shape[1],
                          self.backend._pool.size)
             else:
                 emb = self.resources.label_embeddings

@@ -159,6 +159,11 @@ class BioCLIPService(BaseInferenceService):
     def _initialize(self):
         self.model.initialize()
 
+    def engine_spec(self):
+        from .backend import bio_shards_bank, engine_spec
+
+        return engine_spec(self.resources, shard_bank=bio_shards_bank(self.resources))
+
     def _handle_text(self, payload: bytes, mime: str, meta: dict):
         if not (mime or "").startswith("text/"):
             raise ValueError(f"embed expects text/* payload, got {mime!r}")
@@ -215,7 +220,16 @@ class SmartCLIPService(BaseInferenceService):
         mb = mb.model_copy(update={"runtime": mc.runtime})
         cb, cr = _make_backend(service_config, mc, cache_dir)
         bb, br = _make_backend(service_config, mb, cache_dir)
+        cb.remote_key, bb.remote_key = "general", "bio"     # their parts of the shared engine
         return cls(cb, cr, bb, br)
+
+    def engine_spec(self):
+        """Both towers on one engine (parallel.engine.multi_worker): kinds "general:*" / "bio:*"."""
+        from .backend import bio_shards_bank, engine_spec
+
+        return ("lumen_amd.parallel.engine:multi_worker",
+                {"parts": {"general": engine_spec(self.clip_resources),
+                           "bio": engine_spec(self.bio_resources, shard_bank=bio_shards_bank(self.bio_resources))}})
 
     def _setup_registry(self):
         r = self.registry

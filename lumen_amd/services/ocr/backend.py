@@ -232,6 +232,25 @@ class MI355XOcrBackend:
             chars.append(" ")
         self.character_str = ["blank"] + chars
         cfgp = r.model_root_path / "lumen_ocr_config.json"
+        from ...parallel.engine import current_remote
+
+        remote = current_remote()
+        if remote is not None:
+            # serving front end (parallel/engine.py): DBNet + SVTR live in the GPU engine processes;
+            # request batches (JPEG bytes + parameters) are shipped there whole
+            self.device = torch.device("cpu")
+            self.dtype = torch.float32
+            self._pool = remote
+
+            def rfn(items):
+                with stage("dp_forward"):
+                    return remote.submit("ocr", list(items)).result()
+
+            self._batcher = DynamicBatcher(rfn, self.max_batch, self.max_wait_ms, "ocr-remote", 2 * remote.size)
+            self.load_time = time.time() - t0
+            self.is_initialized = True
+            log.info("OCR %s served by %d GPU engine(s)", r.model_name, remote.size)
+            return
         self.device = pick_device(self.device_pref)
         self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
         if len(self.dp_devices) > 1:
@@ -460,6 +479,11 @@ def create_backend(settings, resources: GenericResources, runtime: Optional[str]
     dev, dp_devs = placement.resolve(dev, placement.dp_size_env())
     return MI355XOcrBackend(resources, device=dev, max_batch=min(amd.max_batch, 16), max_wait_ms=amd.max_wait_ms,
                             dp_devices=dp_devs)
+
+
+def engine_spec(resources: GenericResources, max_batch: int = 16) -> tuple:
+    """(factory path, kwargs) of the GPU engine side (parallel/engine.py): :func:`dp_worker`."""
+    return "lumen_amd.services.ocr.backend:dp_worker", {"resources": resources, "max_batch": max_batch}
 
 
 def dp_worker(device: str, resources: GenericResources, max_batch: int = 16):

@@ -101,6 +101,14 @@ class GeneralOcrService(BaseInferenceService):
     def _initialize(self):
         self.manager.initialize()
 
+    def engine_spec(self):
+        """DBNet + SVTR on the GPU engines (the front end decodes nothing: JPEG bytes go whole)."""
+        m = self.manager
+        res = m.resources or load_model_resources(m.cache_dir, m.config, ("lumen_ocr_config.json",))
+        from .backend import engine_spec
+
+        return engine_spec(res)
+
     def close(self):
         self.manager.close()
 

@@ -238,6 +238,7 @@ class MI355XVLMBackend:
         self.vision_config = VisionConfigMeta.from_dict(meta.get("vision_config", {}))
         self.model: Optional[VLM] = None
         self.engine: Optional[LLMEngine] = None
+        self._remote = None            # serving front end: generation runs on a GPU engine (engine_worker)
         self.load_time = 0.0
 
     # ------------------------------------------------------------------ lifecycle
@@ -336,6 +337,18 @@ class MI355XVLMBackend:
         if self._initialized:
             return
         t0 = time.time()
+        from ...parallel.engine import current_remote
+
+        remote = current_remote()
+        if remote is not None and self.tp_size <= 1:
+            # serving front end (parallel/engine.py): the VLM and its continuous-batching engine live
+            # in a GPU engine process (:func:`engine_worker`); requests are shipped there whole
+            self._remote = remote
+            self.device = torch.device("cpu")
+            self.load_time = time.time() - t0
+            self._initialized = True
+            log.info("VLM %s served by %d GPU engine(s)", self.resources.model_name, remote.size)
+            return
         sync = None
         if self.tp_size > 1 and not self.tp.enabled:
             from ...parallel.tp import TPServingGroup
@@ -505,7 +518,36 @@ class MI355XVLMBackend:
         r = self.engine.submit((ids, img if starts else None), len(full), sp)
         return r, len(full)
 
+    def _generate_remote(self, request: GenerationRequest) -> GenerationResult:
+        from dataclasses import replace
+
+        res = self._remote.submit("generate", [replace(request, stream=False)]).result()[0]
+        if isinstance(res, BaseException):
+            raise res
+        return res
+
+    def _stream_remote(self, request: GenerationRequest) -> Iterator[GenerationChunk]:
+        """The engine generates the whole answer; its tokens are replayed as the local stream's
+        chunks (one per token, held back on an incomplete UTF-8 tail)."""
+        res = self._generate_remote(request)
+        emitted, step = "", 0
+        for k, tok in enumerate(res.tokens):
+            text = self.detokenize(res.tokens[:k + 1])
+            if len(text) > len(res.text):
+                break                                  # past a stop sequence the engine cut at
+            if text.endswith("�"):
+                continue
+            yield GenerationChunk(text=text[len(emitted):], tokens=[tok], metadata={"step": step})
+            emitted, step = text, step + 1
+        if len(res.text) > len(emitted):
+            yield GenerationChunk(text=res.text[len(emitted):], metadata={"step": step})
+        yield GenerationChunk(text="", is_final=True, metadata={"reason": res.finish_reason,
+                                                               "input_tokens": res.metadata.get("input_tokens")})
+
     def generate(self, request: GenerationRequest):
+        if self._remote is not None:
+            self.ensure_initialized()
+            return self._stream_remote(request) if request.stream else self._generate_remote(request)
         if request.stream:
             return self._generate_stream(request)
         r, n_in = self._submit(request)
@@ -562,7 +604,49 @@ class MI355XVLMBackend:
                            max_context_length=gc.max_position_embeddings, vision_image_size=vc.image_size,
                            vision_patch_size=vc.patch_size, vocab_size=gc.vocab_size,
                            extra={"tp_size": str(self.tp.world),
-                                  "kv_cache_tokens": str(self.kv.capacity_tokens) if self._initialized else "0"})
+                                  "kv_cache_tokens": str(self.kv.capacity_tokens)
+                                  if self._initialized and getattr(self, "kv", None) is not None else "0",
+                                  "served_by": "engine" if self._remote is not None else "in-process"})
+
+
+def engine_spec(backend: "MI355XVLMBackend") -> Optional[tuple]:
+    """GPU engine side of a single-GPU VLM (parallel/engine.py): :func:`engine_worker`, with one
+    engine batch loop per request the continuous-batching engine may hold.  A tensor-parallel VLM
+    leads its TP group from the serving parent instead (None: mixed topology, hub/server.py)."""
+    if backend.tp_size > 1:
+        return None
+    return ("lumen_amd.services.vlm.backend:engine_worker",
+            {"resources": backend.resources, "max_new_tokens": backend._max_new_tokens, "kv_blocks": backend.kv_blocks,
+             "max_batch": backend.max_batch},
+            {"threads": max(2, min(backend.max_batch, 32))})
+
+
+def engine_worker(device: str, resources: GenericResources, max_new_tokens: Optional[int] = None, kv_blocks: int = 0,
+                  max_batch: int = 64):
+    """Engine factory: the VLM on ``device``; fn("generate", [GenerationRequest]) -> GenerationResult
+    per request (an exception object for a request that failed alone).  The requests of one merged
+    batch run concurrently on the continuous-batching LLMEngine, as do other batch loops' requests."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    b = MI355XVLMBackend(resources, device=device, max_new_tokens=max_new_tokens, kv_blocks=kv_blocks,
+                         max_batch=max_batch)
+    b.initialize()
+    ex = ThreadPoolExecutor(max_workers=max(4, max_batch), thread_name_prefix="vlm-engine")
+
+    def one(req):
+        try:
+            return b.generate(req)
+        except Exception as e:  # noqa: BLE001 - reported per request
+            return e
+
+    def fn(kind, items):
+        if kind == "generate":
+            return list(ex.map(one, items))
+        if kind == "info":
+            return [b.get_info().as_dict()] * len(items)
+        raise ValueError(f"unknown VLM task kind {kind!r}")
+
+    return fn
 
 
 def create_backend(settings, resources: GenericResources, runtime: Optional[str] = None) -> MI355XVLMBackend:

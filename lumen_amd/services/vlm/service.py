@@ -172,6 +172,11 @@ class GeneralFastVLMService(BaseInferenceService):
     def _initialize(self):
         self.model.initialize()
 
+    def engine_spec(self):
+        from .backend import engine_spec
+
+        return engine_spec(self.backend)
+
     def close(self):
         self.model.close()
 
