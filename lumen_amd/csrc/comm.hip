@@ -4,8 +4,8 @@
 // Every rank owns ONE uncached device allocation (hipExtMallocWithFlags
 // hipDeviceMallocUncached) that all peers map through hipIpc handles:
 //
-//   [ control (16 KiB): flag[2][64 blocks][8 ranks] u32 | epoch[64 blocks] u32 | err u32 ]
-//   [ data parity 0 (cap bytes) ][ data parity 1 (cap bytes) ]
+//   [ control (16 KiB): flag[2][64 blocks][8 ranks] u32 | flag2 (same) | epoch[64 blocks] u32 | err u32 ]
+//   [ data parity 0 (cap bytes) ][ data parity 1 (cap bytes) ][ reduced parity 0 ][ reduced parity 1 ]
 //
 // Call e (per block b, e = epoch[b] + 1, parity p = e & 1):
 //   1. block b copies its slice of the input into its OWN data[p];
@@ -106,6 +106,123 @@ __global__ void __launch_bounds__(512) custom_ar_kernel(const u32x4v* __restrict
   }
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(&ctl->epoch[b], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Two-shot form for bandwidth-bound messages (a TP prefill all-reduce: 624 x 4096 bf16 = 5 MB per
+// layer at Llama-3-8B), same buffers and epochs.  Block b owns vectors [lo, hi) on every rank and
+// splits them into `world` sub-slices:
+//   1. copy [lo, hi) of the input into my data[p]; signal flag[p][b] to every peer; wait for all;
+//   2. reduce MY sub-slice over all ranks' data[p] (fp32, rank order) -> out and my red[p];
+//   3. signal flag2[p][b] to every peer; wait for all;
+//   4. copy every peer's reduced sub-slice from its red[p] into out.
+// Each rank moves 2 (n-1)/n of the message over its links instead of (n-1) x (one-shot), so at
+// n = 8 and MB-sized messages the links carry 4x less.  Reuse by parity is safe as in the one-shot
+// form: a rank rewrites data[p] / red[p] at call e + 2 only after every peer signalled call
+// e + 1 (or e + 2), i.e. finished reading call e.
+template <int BF16>
+__global__ void __launch_bounds__(512) custom_ar2_kernel(const u32x4v* __restrict__ in, u32x4v* __restrict__ out,
+                                                         ArPeers peers, int rank, int world, int64_t nvec,
+                                                         int64_t vec_per_block, int64_t cap_bytes) {
+  const int b = blockIdx.x;
+  char* mine = peers.base[rank];
+  ArCtl* ctl = reinterpret_cast<ArCtl*>(mine);
+  __shared__ uint32_t s_epoch;
+  if (threadIdx.x == 0) s_epoch = __hip_atomic_load(&ctl->epoch[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  const uint32_t e = s_epoch;
+  const int p = (int)(e & 1u);
+  const int64_t lo = (int64_t)b * vec_per_block;
+  const int64_t hi = lo + vec_per_block < nvec ? lo + vec_per_block : nvec;
+  const int64_t sub = (hi - lo + world - 1) / world;
+  const int64_t doff = AR_CTL_BYTES + (int64_t)p * cap_bytes;         // data[p]
+  const int64_t roff = AR_CTL_BYTES + (int64_t)(2 + p) * cap_bytes;   // red[p]
+
+  // 1. stage [lo, hi) into my data[p], barrier 1
+  u32x4v* my_data = reinterpret_cast<u32x4v*>(mine + doff);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) my_data[i] = in[i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x < (unsigned)world) {
+    ArCtl* pc = reinterpret_cast<ArCtl*>(peers.base[threadIdx.x]);
+    __hip_atomic_store(&pc->flag[p][b][rank], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* f = &ctl->flag[p][b][threadIdx.x];
+    int spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > AR_SPIN_LIMIT) {
+        __hip_atomic_store(&ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+
+  // 2. reduce my sub-slice -> out, my red[p]
+  u32x4v* my_red = reinterpret_cast<u32x4v*>(mine + roff);
+  const int64_t s0 = lo + rank * sub, s1 = s0 + sub < hi ? s0 + sub : hi;
+  for (int64_t i = s0 + threadIdx.x; i < s1; i += blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < world; ++r) add_vec(acc, reinterpret_cast<const u32x4v*>(peers.base[r] + doff)[i], BF16);
+    u32x4v o;
+    if (BF16) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = rne_bf16(acc[2 * k]) | (rne_bf16(acc[2 * k + 1]) << 16);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = __float_as_uint(acc[k]);
+    }
+    my_red[i] = o;
+    out[i] = o;
+  }
+  __threadfence_system();
+  __syncthreads();
+
+  // 3. barrier 2: every rank's reduced sub-slice published
+  if (threadIdx.x < (unsigned)world) {
+    ArCtl* pc = reinterpret_cast<ArCtl*>(peers.base[threadIdx.x]);
+    __hip_atomic_store(&pc->flag2[p][b][rank], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* f = &ctl->flag2[p][b][threadIdx.x];
+    int spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > AR_SPIN_LIMIT) {
+        __hip_atomic_store(&ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+
+  // 4. gather the peers' reduced sub-slices
+  for (int r = 1; r < world; ++r) {
+    const int q = (rank + r) % world;            // start at a different peer on every rank
+    const int64_t q0 = lo + q * sub, q1 = q0 + sub < hi ? q0 + sub : hi;
+    const u32x4v* src = reinterpret_cast<const u32x4v*>(peers.base[q] + roff);
+    for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) out[i] = src[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&ctl->epoch[b], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+hipError_t custom_all_reduce_2shot(const void* in, void* out, const ArPeers& peers, int rank, int world,
+                                   int64_t bytes, int is_bf16, int64_t cap_bytes, hipStream_t stream) {
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world) return hipErrorInvalidValue;
+  if (bytes % 16 != 0 || bytes > cap_bytes) return hipErrorInvalidValue;
+  const int64_t nvec = bytes / 16;
+  if (nvec == 0) return hipSuccess;
+  int64_t blocks = (nvec + 2047) / 2048;      // >= 4 vectors per thread per sub-slice at n = 8
+  if (blocks > AR_MAX_BLOCKS) blocks = AR_MAX_BLOCKS;
+  const int64_t per = (nvec + blocks - 1) / blocks;
+  blocks = (nvec + per - 1) / per;
+  if (is_bf16)
+    hipLaunchKernelGGL(custom_ar2_kernel<1>, dim3((unsigned)blocks), dim3(512), 0, stream, (const u32x4v*)in,
+                       (u32x4v*)out, peers, rank, world, nvec, per, cap_bytes);
+  else
+    hipLaunchKernelGGL(custom_ar2_kernel<0>, dim3((unsigned)blocks), dim3(512), 0, stream, (const u32x4v*)in,
+                       (u32x4v*)out, peers, rank, world, nvec, per, cap_bytes);
+  return hipGetLastError();
 }
 
 hipError_t custom_all_reduce(const void* in, void* out, const ArPeers& peers, int rank, int world, int64_t bytes,

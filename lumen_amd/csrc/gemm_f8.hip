@@ -579,6 +579,9 @@ static hipError_t launch_f8_sk(const uint8_t* A, int64_t lda, const float* sa, c
   return hipGetLastError();
 }
 
+// 256 x 256 ping-pong form (csrc/gemm_f8pp.hip); splits <= 0: automatic
+hipError_t gemm_f8pp(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw, const float* sw,
+                     void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, int splits, hipStream_t stream);
 // intra-workgroup split-K form (csrc/gemm_f8ks.hip)
 hipError_t gemm_f8ks(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw, const float* sw,
                      void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, hipStream_t stream);
@@ -694,6 +697,12 @@ template <bool F8>
 static hipError_t launch_variant(int v, const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw,
                                  const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, int S,
                                  hipStream_t stream) {
+  if (v == 17) {               // 256 x 256 ping-pong (fp8 only; its own split-K)
+    if constexpr (F8) {
+      if (ep.split_koff == 0) return gemm_f8pp(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S > 1 ? S : -1, stream);
+    }
+    v = 2;
+  }
   if (v == 16) {               // intra-workgroup split-K (fp8 only; its own plain epilogues)
     if constexpr (F8) {
       if (ep.split_koff == 0 && S == 1) return gemm_f8ks(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
@@ -776,6 +785,28 @@ hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t
   }
   const bool multi_wave = tiles * S > f8_num_cus();
   if (variant > 0) return launch_variant<true>(variant, A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
+  // r5 (profiles/r5_f8_*): at prefill sizes (M <= 768) the intra-workgroup split-K 128 x 128 form
+  // (code 16) runs the single-round grids (qkv / o / down: 23.7-66.5 us cold vs 26.3-69.8), and a
+  // multi-round grid (gate|up, 1120 tiles of 128 x 128) runs its whole rounds of 256 x 256 ping-pong
+  // tiles (code 17: twice the FLOP per staged byte) and the remaining columns on code 16
+  const bool plain = !(ep.out_group || ep.table || ep.prelu || ep.post_act || ep.split_koff || ep.row_aff ||
+                       (ep.glu && ep.out_f32));
+  if (plain && splits <= 0 && M <= 768 && K >= 1024) {
+    const int cus = f8_num_cus();
+    const int per_round = cus / ((M + 255) / 256);       // 256-column panels per round of 256 x 256 tiles
+    const int panels = N / 256;
+    const int full = panels >= per_round && tiles > cus ? panels / per_round * per_round : 0;
+    if (full == 0) return gemm_f8ks(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+    const int n1 = full * 256;
+    hipError_t e = gemm_f8pp(A, lda, sa, W, ldw, sw, C, ldc, M, n1, K, ep, 1, stream);
+    if (e != hipSuccess || n1 == N) return e;
+    GemmEpi e2 = ep;          // the remaining columns: every per-column operand shifted by n1
+    if (ep.bias) e2.bias = (const char*)ep.bias + (int64_t)n1 * (ep.bias_f32 ? 4 : 2);
+    if (ep.residual) e2.residual = ep.residual + n1;
+    const int64_t cshift = (int64_t)(ep.glu ? n1 / 2 : n1) * (ep.out_f32 ? 4 : 2);
+    return gemm_f8ks(A, lda, sa, W + (int64_t)n1 * ldw, ldw, sw ? sw + n1 : nullptr, (char*)C + cshift, ldc, M,
+                     N - n1, K, e2, stream);
+  }
   return launch_variant<true>(multi_wave ? 1 : 2, A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
 }
 

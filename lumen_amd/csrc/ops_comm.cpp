@@ -20,11 +20,12 @@ namespace {
     TORCH_CHECK(_e == hipSuccess, "lumen HIP error: ", hipGetErrorString(_e), " @ ", #expr); \
   } while (0)
 
-// bytes = control block + 2 parities of `cap` data bytes; zero-filled.
+// bytes = control block + 2 parities of `cap` data bytes + 2 parities of `cap` reduced bytes (the
+// two-shot form's published sub-slices); zero-filled.
 int64_t ar_alloc(int64_t cap) {
   TORCH_CHECK(cap > 0 && cap % 16 == 0, "ar_alloc: capacity must be a positive multiple of 16");
   void* p = nullptr;
-  const size_t total = (size_t)lumen::AR_CTL_BYTES + 2 * (size_t)cap;
+  const size_t total = (size_t)lumen::AR_CTL_BYTES + 4 * (size_t)cap;
   CHECK_HIPC(hipExtMallocWithFlags(&p, total, hipDeviceMallocUncached));
   CHECK_HIPC(hipMemset(p, 0, total));
   CHECK_HIPC(hipDeviceSynchronize());
@@ -76,7 +77,8 @@ void ar_error_into(int64_t ptr, at::Tensor out) {
 }
 
 // out = sum over ranks of inp (bf16 or fp32, contiguous, bytes % 16 == 0, bytes <= cap)
-void custom_all_reduce(const at::Tensor& inp, at::Tensor out, at::IntArrayRef bases, int64_t rank, int64_t cap) {
+void custom_all_reduce(const at::Tensor& inp, at::Tensor out, at::IntArrayRef bases, int64_t rank, int64_t cap,
+                       bool two_shot) {
   TORCH_CHECK(inp.is_cuda() && out.is_cuda() && inp.is_contiguous() && out.is_contiguous(), "custom_all_reduce: cuda contiguous");
   TORCH_CHECK(inp.scalar_type() == out.scalar_type() && inp.numel() == out.numel(), "custom_all_reduce: in/out mismatch");
   TORCH_CHECK(inp.scalar_type() == at::kBFloat16 || inp.scalar_type() == at::kFloat, "custom_all_reduce: bf16 or fp32");
@@ -90,9 +92,9 @@ void custom_all_reduce(const at::Tensor& inp, at::Tensor out, at::IntArrayRef ba
     peers.base[r] = reinterpret_cast<char*>(bases[r]);
   }
   const at::DeviceGuard g(inp.device());
-  CHECK_HIPC(lumen::custom_all_reduce(inp.data_ptr(), out.data_ptr(), peers, (int)rank, (int)world, bytes,
-                                      inp.scalar_type() == at::kBFloat16 ? 1 : 0, cap,
-                                      c10::hip::getCurrentHIPStream().stream()));
+  auto fn = two_shot ? lumen::custom_all_reduce_2shot : lumen::custom_all_reduce;
+  CHECK_HIPC(fn(inp.data_ptr(), out.data_ptr(), peers, (int)rank, (int)world, bytes,
+                inp.scalar_type() == at::kBFloat16 ? 1 : 0, cap, c10::hip::getCurrentHIPStream().stream()));
 }
 
 // A HIP stream owned by the caller for the life of the process (never from PyTorch's
@@ -119,7 +121,7 @@ TORCH_LIBRARY_FRAGMENT(lumen, m) {
   m.def("ar_open(Tensor handle) -> int", &ar_open);
   m.def("ar_close(int ptr) -> ()", &ar_close);
   m.def("ar_error(int ptr) -> int", &ar_error);
-  m.def("custom_all_reduce(Tensor inp, Tensor(o!) out, int[] bases, int rank, int cap) -> ()");
+  m.def("custom_all_reduce(Tensor inp, Tensor(o!) out, int[] bases, int rank, int cap, bool two_shot=False) -> ()");
   m.def("ar_error_into(int ptr, Tensor(o!) out) -> ()");
 }
 

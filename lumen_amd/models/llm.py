@@ -107,6 +107,12 @@ LLM_PRESETS = {
                            eos_token_id=2),
     "tiny": LLMConfig(vocab_size=512, hidden_size=128, num_layers=2, num_heads=4, num_kv_heads=2, head_dim=32,
                       intermediate_size=256, max_position=2048, bos_token_id=1, eos_token_id=2),
+    # TP = 4 / 8 test shapes: 8 query heads over 8 KV heads (one of each per rank at TP = 8) and over
+    # 2 KV heads (GQA: every KV head replicated on TP / 2 ranks, the kv_rep > 1 load path)
+    "tiny-h8": LLMConfig(vocab_size=512, hidden_size=256, num_layers=2, num_heads=8, num_kv_heads=8, head_dim=32,
+                         intermediate_size=512, max_position=2048, bos_token_id=1, eos_token_id=2),
+    "tiny-gqa8": LLMConfig(vocab_size=512, hidden_size=256, num_layers=2, num_heads=8, num_kv_heads=2, head_dim=32,
+                           intermediate_size=512, max_position=2048, bos_token_id=1, eos_token_id=2),
 }
 
 

@@ -95,6 +95,10 @@ VLM_PRESETS = {
                                  image_std=(0.26862954, 0.26130258, 0.27577711), pad_value=116.0),
     "tiny": VLMConfig(vision=VisionConfig(image_size=32, patch_size=8, width=64, layers=2, heads=2, act="gelu"),
                       llm=LLM_PRESETS["tiny"], image_token_id=259),
+    "tiny-h8": VLMConfig(vision=VisionConfig(image_size=32, patch_size=8, width=64, layers=2, heads=2, act="gelu"),
+                         llm=LLM_PRESETS["tiny-h8"], image_token_id=259),
+    "tiny-gqa8": VLMConfig(vision=VisionConfig(image_size=32, patch_size=8, width=64, layers=2, heads=2, act="gelu"),
+                           llm=LLM_PRESETS["tiny-gqa8"], image_token_id=259),
     "tiny-fastvit": VLMConfig(vision=VisionConfig(image_size=64, patch_size=16, width=128, layers=0, heads=1),
                               vision_arch="fastvit", fastvit=FASTVIT_PRESETS["tiny-ln"], llm=LLM_PRESETS["tiny"],
                               image_token_id=259),
@@ -321,7 +325,7 @@ def write_vlm_model(root, name: str, preset: Optional[str] = None, seed: int = 0
                                                             "eos_token": "<|im_end|>", "bos_token": None}, indent=2))
     (root / "lumen_vlm_config.json").write_text(json.dumps(cfg.to_dict(), indent=2))
     if weights is None:
-        weights = preset == "tiny"
+        weights = preset in ("tiny", "tiny-h8", "tiny-gqa8")
     files = ["tokenizer.json", "tokenizer_config.json", "lumen_vlm_config.json"]
     if weights:
         m = VLM(cfg, dtype=torch.float32, device="cpu")

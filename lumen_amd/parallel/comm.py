@@ -28,6 +28,12 @@ import torch
 log = logging.getLogger("lumen.comm")
 
 DEFAULT_IPC_MAX_BYTES = int(os.environ.get("LUMEN_IPC_AR_MAX_BYTES", str(512 * 1024)))
+# two-shot IPC all-reduce (reduce-scatter + all-gather reading every peer at once): messages above the
+# one-shot limit and up to this many bytes, in groups of >= 4 ranks, where it moves 2 (n-1)/n of the
+# message per rank instead of the ring's 2 (n-1)/n in 2 (n-1) serial hops -- the TP prefill
+# all-reduces (624 x 4096 bf16 = 5 MB per layer at Llama-3-8B)
+TWO_SHOT_MAX_BYTES = int(os.environ.get("LUMEN_IPC_AR2_MAX_BYTES", str(16 << 20)))
+TWO_SHOT_MIN_WORLD = int(os.environ.get("LUMEN_IPC_AR2_MIN_WORLD", "4"))
 # without RCCL (gloo groups: several TP ranks sharing one GPU in tests) every message the IPC
 # kernel cannot take is staged through the host; cover prefill-sized all-reduces there too
 GLOO_IPC_MAX_BYTES = 32 << 20
@@ -87,10 +93,11 @@ class CustomAllReduce:
         return (not self.closed and t.is_cuda and t.dtype in (torch.bfloat16, torch.float32) and t.is_contiguous()
                 and nbytes % 16 == 0 and 0 < nbytes <= self.max_bytes)
 
-    def all_reduce(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Sum over the group; in place unless ``out`` is given."""
+    def all_reduce(self, t: torch.Tensor, out: Optional[torch.Tensor] = None, two_shot: bool = False) -> torch.Tensor:
+        """Sum over the group; in place unless ``out`` is given.  ``two_shot``: the reduce-scatter +
+        all-gather form (bandwidth-bound messages); every rank must pass the same value."""
         out = t if out is None else out
-        self.ops.custom_all_reduce(t, out, self.bases, self.rank, self.max_bytes)
+        self.ops.custom_all_reduce(t, out, self.bases, self.rank, self.max_bytes, bool(two_shot))
         return out
 
     def error(self) -> bool:
@@ -115,7 +122,7 @@ class Communicator:
     """
 
     def __init__(self, group=None, device: Optional[torch.device] = None, ipc: Optional[bool] = None,
-                 ipc_max_bytes: int = DEFAULT_IPC_MAX_BYTES):
+                 ipc_max_bytes: int = DEFAULT_IPC_MAX_BYTES, two_shot_max_bytes: int = TWO_SHOT_MAX_BYTES):
         import torch.distributed as dist
 
         self.group = group
@@ -123,15 +130,19 @@ class Communicator:
         self.rank, self.world = _group_ranks(group) if self.enabled else (0, 1)
         self.device = device
         self.custom: Optional[CustomAllReduce] = None
-        self.stats = {"ipc_calls": 0, "rccl_calls": 0, "ipc_bytes": 0, "rccl_bytes": 0}
+        self.stats = {"ipc_calls": 0, "rccl_calls": 0, "ipc_bytes": 0, "rccl_bytes": 0, "ipc2_calls": 0}
+        self.one_shot_max = ipc_max_bytes
         if ipc is None:
             ipc = os.environ.get("LUMEN_IPC_ALLREDUCE", "1") == "1"
             ipc = ipc and self.world > 1 and device is not None and device.type == "cuda"
         if ipc and self.world > 1:
+            cap = ipc_max_bytes
             if self.enabled and dist.get_backend(group) != "nccl":
-                ipc_max_bytes = max(ipc_max_bytes, GLOO_IPC_MAX_BYTES)
+                cap = max(cap, GLOO_IPC_MAX_BYTES)     # (above the one-shot limit: two-shot)
+            if self.world >= TWO_SHOT_MIN_WORLD:
+                cap = max(cap, two_shot_max_bytes)
             try:
-                self.custom = CustomAllReduce(group, device, ipc_max_bytes)
+                self.custom = CustomAllReduce(group, device, cap)
             except Exception as e:  # noqa: BLE001 - fall back to RCCL, loudly
                 log.warning("IPC all-reduce unavailable (%s); using RCCL for every all-reduce", e)
                 self.custom = None
@@ -145,7 +156,9 @@ class Communicator:
         if self.custom is not None and self.custom.eligible(t):
             self.stats["ipc_calls"] += 1
             self.stats["ipc_bytes"] += nbytes
-            return self.custom.all_reduce(t)
+            two = nbytes > self.one_shot_max      # room above it: groups of >= TWO_SHOT_MIN_WORLD / gloo groups
+            self.stats["ipc2_calls"] += int(two)
+            return self.custom.all_reduce(t, two_shot=two)
         import torch.distributed as dist
 
         self.stats["rccl_calls"] += 1

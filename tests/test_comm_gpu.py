@@ -1,6 +1,6 @@
-"""IPC one-shot all-reduce (csrc/comm.hip) on the GPU.
+"""IPC one-shot and two-shot all-reduce (csrc/comm.hip) on the GPU.
 
-The box has one MI355X, so the group is two processes sharing cuda:0: the IPC
+The box has one MI355X, so the group is 2 or 4 processes sharing cuda:0: the IPC
 mapping, flag protocol, parity double-buffering, device-side epochs and hipGraph
 replay are the same code paths as 8 GPUs over xGMI (only the link differs).
 Bootstrap (handle exchange) runs over gloo.  Reference: fp32 sum of the inputs.
@@ -23,7 +23,7 @@ def _port():
     return p
 
 
-def _ar_worker(rank, world, port, q):
+def _ar_worker(rank, world, port, q, one_shot_max=1 << 20):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
@@ -34,11 +34,15 @@ def _ar_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     res = {"rank": rank}
     try:
-        comm = Communicator(None, dev, ipc=True, ipc_max_bytes=1 << 20)
+        comm = Communicator(None, dev, ipc=True, ipc_max_bytes=one_shot_max)
         assert comm.custom is not None
         errs = []
+        # one-shot sizes, then two-shot ones (above one_shot_max: reduce-scatter + all-gather), with
+        # slices that do not divide evenly over the ranks / blocks, interleaved with one-shot calls
         for it, (n, dt) in enumerate([(4096, torch.bfloat16), (8, torch.bfloat16), (4096 * 3, torch.float32),
-                                      (65536 * 4, torch.bfloat16), (1024, torch.float32), (4096, torch.bfloat16)]):
+                                      (65536 * 4, torch.bfloat16), (1024, torch.float32), (4096, torch.bfloat16),
+                                      (624 * 4096, torch.bfloat16), (300008, torch.float32), (8, torch.bfloat16),
+                                      (624 * 4096, torch.bfloat16)]):
             parts = [torch.randn(n, generator=torch.Generator().manual_seed(100 * it + r)) for r in range(world)]
             ref = sum(p.to(dt).float() for p in parts)
             x = parts[rank].to(dt).to(dev)
@@ -75,20 +79,23 @@ def _ar_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_ipc_all_reduce_two_processes_one_gpu():
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_all_reduce_processes_one_gpu(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_ar_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_ar_worker, args=(r, world, port, q, 1 << 18)) for r in range(world)]
     for p in ps:
         p.start()
-    out = sorted([q.get(timeout=100) for _ in range(2)], key=lambda d: d["rank"])
+    out = sorted([q.get(timeout=100) for _ in range(world)], key=lambda d: d["rank"])
     for p in ps:
         p.join(30)
+    graph = [float(sum(r + 1 + k for r in range(world))) for k in range(3)]
     for r in out:
         assert "exc" not in r, r
         assert max(r["errs"]) < 1e-2, r["errs"]
-        assert r["graph"] == [3.0, 5.0, 7.0], r["graph"]
+        assert r["graph"] == graph, r["graph"]
         assert not r["error_flag"]
-        assert r["stats"]["ipc_calls"] >= 7
-    assert out[0]["errs"] == out[1]["errs"]      # both ranks hold the same (bitwise) result
+        assert r["stats"]["ipc_calls"] >= 11 and r["stats"]["ipc2_calls"] == 4
+    for r in out[1:]:
+        assert r["errs"] == out[0]["errs"]       # every rank holds the same (bitwise) result

@@ -176,17 +176,19 @@ def test_gemm_f8_pipeline_variants(M, N, K, splits, variant):
 @pytest.mark.parametrize("M,N,K", [(624, 6144, 4096), (624, 4096, 14336), (130, 1040, 128), (200, 512, 256),
                                    (333, 768, 384), (624, 1024, 1152), (64, 256, 1024)])
 @pytest.mark.parametrize("epi", ["bf16_bias_res", "f32_bias", "glu", "plain"])
-def test_gemm_f8_intra_wg_splitk(M, N, K, epi):
-    """Intra-workgroup split-K fp8 GEMM (variant 16, csrc/gemm_f8ks.hip): both wave groups' K
-    halves (odd and even K-step counts, one K-step), ragged M, the prefetched fast epilogue (bf16
-    bias, residual, SwiGLU) and the generic one (fp32 bias) against the fp32 reference; repeat
-    launches are bitwise identical."""
+@pytest.mark.parametrize("variant", [16, 17])
+def test_gemm_f8_intra_wg_splitk(M, N, K, epi, variant):
+    """Intra-workgroup split-K fp8 GEMM (variant 16, csrc/gemm_f8ks.hip: both wave groups' K
+    halves, odd and even K-step counts, one K-step) and the 256 x 256 ping-pong fp8 GEMM (variant 17,
+    csrc/gemm_f8pp.hip: peeled last K-tiles, automatic split-K with fp32 slabs for narrow grids):
+    ragged M, the fast epilogue (bf16 bias, residual, SwiGLU) and the generic one (fp32 bias)
+    against the fp32 reference; repeat launches are bitwise identical."""
     g, x8, xs, w8, ws = _f8_operands(M, N, K, M + N + K)
     dev_args = (x8.to(DEV), xs.to(DEV), w8.to(DEV), ws.to(DEV))
     acc = (x8.float() @ w8.float().t()) * xs[:, None] * ws[None, :]
     if epi == "glu":
         ref = ops.linear_f8(x8, xs, w8, ws, glu=True)
-        got = ops.linear_f8(*dev_args, glu=True, variant=16)
+        got = ops.linear_f8(*dev_args, glu=True, variant=variant)
         assert got.shape == (M, N // 2) and _rel(got, ref) < 1e-2
         return
     kw, ref = {}, acc
@@ -199,9 +201,31 @@ def test_gemm_f8_intra_wg_splitk(M, N, K, epi):
         b = torch.randn(N, generator=g)
         kw = {"bias": b.to(DEV)}
         ref = acc + b
-    got = ops.linear_f8(*dev_args, variant=16, **kw)
+    got = ops.linear_f8(*dev_args, variant=variant, **kw)
     assert _rel(got, ref) < 8e-3
-    assert torch.equal(got, ops.linear_f8(*dev_args, variant=16, **kw))
+    assert torch.equal(got, ops.linear_f8(*dev_args, variant=variant, **kw))
+
+
+@pytest.mark.parametrize("M,N,glu,resid", [(624, 28672, True, False), (624, 22016 + 4096, False, True),
+                                           (300, 36864, True, False)])
+def test_gemm_f8_auto_prefill_split_columns(M, N, glu, resid):
+    """Auto selection at prefill sizes: a multi-round grid runs whole rounds of 256 x 256 tiles
+    (code 17) and the remaining columns on the 128 x 128 split-K form (code 16) with every per-column
+    operand (weight scale, bias, residual, SwiGLU output column) shifted; same result as the fp32
+    reference."""
+    K = 1024
+    g, x8, xs, w8, ws = _f8_operands(M, N, K, N + M)
+    b = torch.randn(N, generator=g).bfloat16()
+    args = (x8.to(DEV), xs.to(DEV), w8.to(DEV), ws.to(DEV))
+    if glu:
+        ref = ops.linear_f8(x8, xs, w8, ws, bias=b.float(), glu=True)
+        got = ops.linear_f8(*args, bias=b.to(DEV), glu=True)
+        assert got.shape == (M, N // 2) and _rel(got, ref) < 1e-2
+        return
+    r = torch.randn(M, N, generator=g).bfloat16()
+    ref = (x8.float() @ w8.float().t()) * xs[:, None] * ws[None, :] + b.float() + r.float()
+    got = ops.linear_f8(*args, bias=b.to(DEV), residual=r.to(DEV))
+    assert _rel(got, ref) < 8e-3
 
 
 @pytest.mark.parametrize("tile", [20011, 20012, 20013, 20014, 20015, 20016, 20017, 20018, 20019, 20020, 20021,

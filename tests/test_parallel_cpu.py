@@ -138,7 +138,7 @@ def test_worker_pool_task_timeout_kills_hung_worker():
         pool.close()
 
 
-def _vlm_leader(cache, tp, q):
+def _vlm_leader(cache, tp, q, model="fastvlm-tiny"):
     import json as _json
 
     os.environ["LUMEN_TP_SIZE"] = str(tp)
@@ -154,7 +154,7 @@ def _vlm_leader(cache, tp, q):
                                 "import_info": {"registry_class": "lumen_vlm.fastvlm.GeneralFastVLMService",
                                                 "add_to_server": "lumen_vlm.proto.ml_service_pb2_grpc.add_InferenceServicer_to_server"},
                                 "backend_settings": {"device": "cpu"},
-                                "models": {"general": {"model": "fastvlm-tiny", "runtime": "onnx"}}}}}
+                                "models": {"general": {"model": model, "runtime": "onnx"}}}}}
     s = GeneralFastVLMService.from_config(config_from_dict(cfg).services["vlm"], cache)
     s.initialize()
     try:
@@ -190,6 +190,29 @@ def test_vlm_tensor_parallel_serving_matches_tp1(tmp_path):
     assert res[2]["texts"] == res[1]["texts"]
     # greedy decode steps travel as fixed int32 descriptors, prefill/control as objects
     assert res[2]["sync"]["tensor_steps"] >= 8 and res[2]["sync"]["object_steps"] >= 2
+
+
+@pytest.mark.parametrize("preset,tps", [("tiny-h8", (1, 8)), ("tiny-gqa8", (1, 4, 8))])
+def test_vlm_tp4_tp8_greedy_matches_tp1(tmp_path, preset, tps):
+    """TP = 4 and 8 (gloo, one process per rank): the IPC-free CPU collectives with 3 / 7 peers,
+    the step bus with 3 / 7 readers, the 4- / 8-way vocab-parallel candidate merge, and -- for the
+    GQA preset (2 KV heads) -- the kv_rep > 1 weight split (models/llm.py: each KV head replicated
+    on TP / 2 ranks) generate the same greedy text as TP = 1."""
+    from lumen_amd.models.vlm import write_vlm_model
+
+    write_vlm_model(tmp_path / "models" / f"vlm-{preset}", f"vlm-{preset}", preset=preset)
+    ctx = mp.get_context("spawn")
+    res = {}
+    for tp in tps:
+        q = ctx.Queue()
+        p = ctx.Process(target=_vlm_leader, args=(str(tmp_path), tp, q, f"vlm-{preset}"))
+        p.start()
+        res[tp] = q.get(timeout=600)
+        p.join(120)
+        assert p.exitcode == 0
+    for tp in tps[1:]:
+        assert res[tp]["tp"] == tp
+        assert res[tp]["texts"] == res[1]["texts"], (preset, tp)
 
 
 def test_clip_dp_serving_matches_single_process(tmp_path, monkeypatch):

@@ -13,7 +13,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _leader(cache, tp, q):
+def _leader(cache, tp, q, model="fastvlm-tiny"):
     import json as _json
 
     os.environ["LUMEN_TP_SIZE"] = str(tp)
@@ -30,7 +30,7 @@ def _leader(cache, tp, q):
                                 "import_info": {"registry_class": "lumen_vlm.fastvlm.GeneralFastVLMService",
                                                 "add_to_server": "lumen_vlm.proto.ml_service_pb2_grpc.add_InferenceServicer_to_server"},
                                 "backend_settings": {"device": "cuda"},
-                                "models": {"general": {"model": "fastvlm-tiny", "runtime": "onnx"}}}}}
+                                "models": {"general": {"model": model, "runtime": "onnx"}}}}}
     s = GeneralFastVLMService.from_config(config_from_dict(cfg).services["vlm"], cache)
     s.initialize()
     try:
@@ -76,3 +76,31 @@ def test_vlm_tp2_graphs_match_tp1(tmp_path):
     # prefill's last chunk still gathers candidates through gloo (one host copy per request);
     # decode steps add none
     assert fol["d2h"] <= fol["prefill_chunks"]
+
+
+def test_vlm_tp4_gqa_graphs_match_tp1(tmp_path):
+    """TP = 4 on one GPU (4 ranks, gloo control + the IPC all-reduce with 3 peers, one- and two-shot):
+    8 query heads over 2 KV heads, so every KV head is replicated on 2 ranks (the kv_rep > 1 load
+    path); the step bus has 3 readers and the in-graph sampler merges 4 vocab shards.  Same greedy
+    text as TP = 1."""
+    from lumen_amd.models.vlm import write_vlm_model
+
+    write_vlm_model(tmp_path / "models" / "vlm-gqa8", "vlm-gqa8", preset="tiny-gqa8")
+    ctx = mp.get_context("spawn")
+    res = {}
+    for tp in (1, 4):
+        q = ctx.Queue()
+        p = ctx.Process(target=_leader, args=(str(tmp_path), tp, q, "vlm-gqa8"))
+        p.start()
+        res[tp] = q.get(timeout=110)
+        p.join(30)
+        assert "error" not in res[tp], res[tp]
+        assert p.exitcode == 0
+    assert res[4]["tp"] == 4 and res[4]["graphs"]
+    assert res[4]["sync"]["transport"] == "bus" and res[4]["sync"]["tensor_steps"] >= 10
+    assert res[4]["texts"] == res[1]["texts"]
+    import json
+
+    for r in (1, 2, 3):
+        fol = json.loads((tmp_path / f"follower_stats.rank{r}").read_text())
+        assert fol["transport"] == "bus" and fol["ingraph_steps"] >= 10
