@@ -135,12 +135,11 @@ def build(verbose: bool = False, jobs: int | None = None) -> dict:
     host_dir = CSRC / "host"
     hsrcs = sorted(host_dir.glob("*.cpp")) if host_dir.exists() else []
     if hsrcs:
-        hheaders = sorted(host_dir.glob("*.h"))
         hobjs, htodo = [], []
         for s in hsrcs:
             o = BUILD / ("host_" + s.name + ".o")
             hobjs.append(o)
-            if _needs(o, s, [h for h in hheaders if h in _local_deps(s)]):
+            if _needs(o, s, _local_deps(s)):      # host headers and the shared csrc/*.h layouts
                 htodo.append(["g++", "-O3", "-fPIC", "-std=c++17", "-pthread", f"-I{host_dir}", "-c", str(s),
                               "-o", str(o)])
         with cf.ThreadPoolExecutor(jobs) as ex:

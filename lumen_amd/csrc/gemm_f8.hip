@@ -785,27 +785,16 @@ hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t
   }
   const bool multi_wave = tiles * S > f8_num_cus();
   if (variant > 0) return launch_variant<true>(variant, A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
-  // r5 (profiles/r5_f8_*): at prefill sizes (M <= 768) the intra-workgroup split-K 128 x 128 form
-  // (code 16) runs the single-round grids (qkv / o / down: 23.7-66.5 us cold vs 26.3-69.8), and a
-  // multi-round grid (gate|up, 1120 tiles of 128 x 128) runs its whole rounds of 256 x 256 ping-pong
-  // tiles (code 17: twice the FLOP per staged byte) and the remaining columns on code 16
+  // r5 (profiles/r5_f8_variants_cold_v1.txt): at prefill sizes (M <= 768) the intra-workgroup
+  // split-K 128 x 128 form (code 16) runs the single-round grids (qkv / o / down: 23.8-66.1 us cold
+  // vs 26.1-69.5 for code 2), the 256 x 256 ping-pong (code 17: twice the FLOP per staged byte) the
+  // multi-round ones (gate|up, 1120 tiles of 128 x 128: 91.6 us vs 95.0 with its last partial
+  // round on code 16 and 106.4 for code 1)
   const bool plain = !(ep.out_group || ep.table || ep.prelu || ep.post_act || ep.split_koff || ep.row_aff ||
                        (ep.glu && ep.out_f32));
   if (plain && splits <= 0 && M <= 768 && K >= 1024) {
-    const int cus = f8_num_cus();
-    const int per_round = cus / ((M + 255) / 256);       // 256-column panels per round of 256 x 256 tiles
-    const int panels = N / 256;
-    const int full = panels >= per_round && tiles > cus ? panels / per_round * per_round : 0;
-    if (full == 0) return gemm_f8ks(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
-    const int n1 = full * 256;
-    hipError_t e = gemm_f8pp(A, lda, sa, W, ldw, sw, C, ldc, M, n1, K, ep, 1, stream);
-    if (e != hipSuccess || n1 == N) return e;
-    GemmEpi e2 = ep;          // the remaining columns: every per-column operand shifted by n1
-    if (ep.bias) e2.bias = (const char*)ep.bias + (int64_t)n1 * (ep.bias_f32 ? 4 : 2);
-    if (ep.residual) e2.residual = ep.residual + n1;
-    const int64_t cshift = (int64_t)(ep.glu ? n1 / 2 : n1) * (ep.out_f32 ? 4 : 2);
-    return gemm_f8ks(A, lda, sa, W + (int64_t)n1 * ldw, ldw, sw ? sw + n1 : nullptr, (char*)C + cshift, ldc, M,
-                     N - n1, K, e2, stream);
+    if (tiles > f8_num_cus() && N % 256 == 0) return gemm_f8pp(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, 1, stream);
+    return gemm_f8ks(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
   }
   return launch_variant<true>(multi_wave ? 1 : 2, A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
 }

@@ -31,6 +31,9 @@
 #include <thread>
 #include <vector>
 
+#include "../jpeg_huff.h"
+#include "../jpeg_huff_core.h"
+
 namespace {
 
 const int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
@@ -703,6 +706,235 @@ int lumen_jpeg_decode_coefs(const uint8_t* data, uint64_t len, int nthreads, int
   }
   st[0] = nch;
   if (stats) memcpy(stats, st, sizeof(st));
+  return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------- GPU entropy decode
+// The preparation the GPU decoder (csrc/jpeg_huff.hip) needs from the host: header parse, the
+// Huffman tables (same fast tables as above), byte unstuffing and the restart-interval starts,
+// written as one descriptor + stream into the caller's (pinned) upload buffer.  O(bytes) memchr /
+// memcpy work: ~20 us for a 1024 x 768 photo against ~1.5-3 ms for the entropy decode itself.
+namespace {
+
+void copy_dc(lumen::JHuffDc& d, const Huff& h) {
+  memcpy(d.fast, h.fast, sizeof(d.fast));
+  memcpy(d.maxcode, h.maxcode, sizeof(d.maxcode));
+  memcpy(d.valptr, h.valptr, sizeof(d.valptr));
+  memcpy(d.mincode, h.mincode, sizeof(d.mincode));
+  memcpy(d.vals, h.vals, sizeof(d.vals));
+}
+
+void copy_ac(lumen::JHuffAc& d, const Huff& h) {
+  memcpy(d.fast, h.fast, sizeof(d.fast));
+  memcpy(d.fast_ac, h.fast_ac, sizeof(d.fast_ac));
+  memcpy(d.maxcode, h.maxcode, sizeof(d.maxcode));
+  memcpy(d.valptr, h.valptr, sizeof(d.valptr));
+  memcpy(d.mincode, h.mincode, sizeof(d.mincode));
+  memcpy(d.vals, h.vals, sizeof(d.vals));
+}
+
+}  // namespace
+
+extern "C" {
+
+int lumen_jpeg_desc_bytes() { return (int)sizeof(lumen::JHuffDesc); }
+
+// Descriptor + stream of one baseline JPEG into out[0, cap) (out 16-byte aligned), its quantisation
+// tables into qt [ncomp][64] (natural order), split for <= max_lanes decoding lanes (the GPU
+// spreads them over max_lanes / 256 workgroups).  *need = bytes the entry takes.  Returns 0 ok,
+// 1 unsupported, -1 malformed, 2 cap too small (nothing usable written; retry with *need).
+int lumen_jpeg_prepare_gpu(const uint8_t* data, uint64_t len, uint8_t* out, int64_t cap, uint16_t* qt,
+                           int64_t* need, int max_lanes) {
+  Jpeg J;
+  const int r = parse(data, (size_t)len, J);
+  if (r != 0) return r;
+  const Layout L = make_layout(J);
+  const int64_t total = (int64_t)J.mcux * J.mcuy * L.bpm;
+  const size_t ecs = J.ecs_end - J.ecs_begin;
+  if (ecs >= ((size_t)1 << 25) || total >= ((int64_t)1 << 31)) return 1;   // 28-bit bit offsets on the GPU
+  const int64_t dsz = (int64_t)((sizeof(lumen::JHuffDesc) + 255) & ~(size_t)255);
+  const int64_t stream_cap = (int64_t)((ecs + 64 + 3) & ~(size_t)3);
+  *need = dsz + stream_cap;
+  if (*need > cap) return 2;
+  for (int c = 0; c < J.ncomp; ++c) memcpy(qt + 64 * c, J.qt[J.comp[c].tq], 64 * sizeof(uint16_t));
+  auto* Dd = reinterpret_cast<lumen::JHuffDesc*>(out);
+  memset(Dd, 0, sizeof(*Dd));
+  lumen::JHuffHead* D = &Dd->h;
+  // unstuff straight into the upload buffer (as unstuff() above)
+  uint8_t* st = out + dsz;
+  std::vector<int32_t> segs{0};
+  size_t o = 0, i = J.ecs_begin;
+  const size_t e = J.ecs_end;
+  while (i < e) {
+    const uint8_t* ff = static_cast<const uint8_t*>(memchr(data + i, 0xFF, e - i));
+    const size_t run = ff ? (size_t)(ff - (data + i)) : e - i;
+    memcpy(st + o, data + i, run);
+    o += run;
+    i += run;
+    if (i >= e) break;
+    if (i + 1 < e && data[i + 1] == 0x00) {
+      st[o++] = 0xFF;
+      i += 2;
+    } else if (i + 1 < e && data[i + 1] >= 0xD0 && data[i + 1] <= 0xD7) {
+      segs.push_back((int32_t)(o * 8));
+      i += 2;
+    } else {
+      st[o++] = 0xFF;
+      ++i;
+    }
+  }
+  const size_t words = (o + 64 + 3) / 4;
+  memset(st + o, 0, words * 4 - o);
+  // 32-bit words, big-endian within each word: the GPU byte-swaps on load
+  D->nbits = (int32_t)(o * 8);
+  D->nwords = (int32_t)words;
+  D->total = (int32_t)total;
+  D->bpm = L.bpm;
+  D->ncomp = J.ncomp;
+  D->mcux = J.mcux;
+  D->stream_off = (int32_t)dsz;
+  if (J.restart > 0 && segs.size() > 1) {
+    const int64_t per = (int64_t)J.restart * L.bpm;
+    const int nseg = (int)segs.size();
+    if ((int64_t)nseg * per < total) return -1;   // fewer intervals than the frame needs
+    const int64_t seg_off = dsz + (int64_t)words * 4;
+    *need = seg_off + 4 * (int64_t)nseg;
+    if (*need > cap) return 2;
+    memcpy(out + seg_off, segs.data(), 4 * (size_t)nseg);
+    D->restart_blocks = (int32_t)per;
+    D->nseg = nseg;
+    D->seg_off = (int32_t)seg_off;
+  } else {
+    *need = dsz + (int64_t)words * 4;
+  }
+  // synchronising decode: <= max_lanes subsequences of >= 128 bits
+  const int64_t nb = std::max<int64_t>(D->nbits, 1);
+  const int64_t lanes = std::min<int64_t>(std::max(max_lanes, lumen::kJHuffWgLanes), lumen::kJHuffMaxLanes);
+  int64_t sub = std::max<int64_t>(128, (nb + lanes - 1) / lanes);
+  sub = (sub + 31) & ~(int64_t)31;
+  D->sub_bits = (int32_t)sub;
+  D->nsub = (int32_t)((nb + sub - 1) / sub);
+  // tables: one slot per distinct (class, id) the scan uses
+  int dmap[4] = {-1, -1, -1, -1}, amap[4] = {-1, -1, -1, -1};
+  for (int k = 0; k < L.bpm; ++k) {
+    const Comp& cp = J.comp[L.pcomp[k]];
+    if (dmap[cp.td] < 0) {
+      dmap[cp.td] = D->ndc++;
+      copy_dc(Dd->dc[dmap[cp.td]], J.dc[cp.td]);
+    }
+    if (amap[cp.ta] < 0) {
+      amap[cp.ta] = D->nac++;
+      copy_ac(Dd->ac[amap[cp.ta]], J.ac[cp.ta]);
+    }
+    D->pcomp[k] = L.pcomp[k];
+    D->px[k] = L.ph[k];
+    D->py[k] = L.pv[k];
+    D->pdc[k] = dmap[cp.td];
+    D->pac[k] = amap[cp.ta];
+  }
+  for (int c = 0; c < J.ncomp; ++c) {
+    D->bw[c] = J.comp[c].bw;
+    D->hh[c] = J.comp[c].h;
+    D->vv[c] = J.comp[c].v;
+    D->plane_off[c] = (int64_t)L.plane_off[c];
+  }
+  return 0;
+}
+
+// The GPU decoder's schedule run sequentially on the host (csrc/jpeg_huff.hip:jpeg_huff_kernel,
+// lane by lane, round by round, the same per-lane code from jpeg_huff_core.h): the CPU-side
+// oracle of the kernel's synchronisation / prefix-sum / placement logic.  Same blob, coefficient
+// and err ([2n]: malformed flag, rounds) conventions as the kernel.
+// stats (nullable) [4]: round-0 slides and blocks summed over the lanes, the most slides of a lane,
+// the lanes
+int lumen_jpeg_gpu_emulate(const uint8_t* blob, int n, int16_t* coefs, int32_t* err, int64_t* stats) {
+  uint8_t zz[64];
+  for (int k = 0; k < 64; ++k) zz[k] = (uint8_t)kZigzag[k];
+  for (int img = 0; img < n; ++img) {
+    const lumen::JHuffJob job = reinterpret_cast<const lumen::JHuffJob*>(blob)[img];
+    const uint8_t* dp = blob + job.desc_off;
+    const auto* D = reinterpret_cast<const lumen::JHuffDesc*>(dp);
+    const lumen::JHuffHead& H = D->h;
+    const lumen::jh::SrcMem w{reinterpret_cast<const uint32_t*>(dp + H.stream_off), (uint32_t)H.nwords};
+    int16_t* co = coefs + job.coef_off;
+    memset(co, 0, (size_t)H.total * 64 * sizeof(int16_t));   // as the kernel's launcher
+    int bad = 0, rounds = 0;
+    if (H.restart_blocks > 0) {
+      const int32_t* segs = reinterpret_cast<const int32_t*>(dp + H.seg_off);
+      for (int sg = 0; sg < H.nseg; ++sg)
+        if (!lumen::jh::write_interval(H, D->dc, D->ac, w, segs, sg, co, zz)) bad = 1;
+      err[2 * img] = bad;
+      err[2 * img + 1] = 0;
+      continue;
+    }
+    const int nsub = H.nsub;
+    const uint32_t sub = (uint32_t)H.sub_bits;
+    constexpr int kCap = 16;   // jpeg_huff.hip kMarkCap
+    std::vector<uint32_t> epos(nsub);
+    std::vector<int> eph(nsub, 0), dirty(nsub, 0);
+    std::vector<lumen::jh::Span> sp(nsub), s0(nsub);
+    std::vector<lumen::jh::Mark> marks((size_t)nsub * kCap);
+    std::vector<uint32_t> keys((size_t)nsub * kCap);
+    for (int i = 0; i < nsub; ++i) epos[i] = (uint32_t)i * sub;
+    bool chg = false;
+    for (int i = 0; i < nsub; ++i) {   // round 0: guesses, recording marks
+      s0[i] = lumen::jh::run_span<lumen::jh::kRecord>(H, D->dc, D->ac, w, (uint32_t)i * sub, 0, (uint32_t)(i + 1) * sub,
+                                                      zz, &keys[(size_t)i * kCap], 1, &marks[(size_t)i * kCap], kCap);
+      sp[i] = s0[i];
+      if (stats) {
+        stats[0] += s0[i].slides;
+        stats[1] += s0[i].n;
+        stats[2] = std::max<int64_t>(stats[2], s0[i].slides);
+        stats[3] += 1;
+      }
+    }
+    for (int i = 0; i + 1 < nsub; ++i)
+      if (sp[i].pos != epos[i + 1] || sp[i].phase != eph[i + 1]) {
+        epos[i + 1] = sp[i].pos;
+        eph[i + 1] = sp[i].phase;
+        dirty[i + 1] = 1;
+        chg = true;
+      }
+    rounds = 1;
+    for (int r = 1; chg && r <= nsub + 1; ++r) {
+      const std::vector<uint32_t> p0 = epos;
+      const std::vector<int> ph0 = eph, d0 = dirty;
+      std::fill(dirty.begin(), dirty.end(), 0);
+      chg = false;
+      for (int i = 0; i < nsub; ++i) {
+        if (!d0[i]) continue;
+        const uint32_t end = (uint32_t)(i + 1) * sub;
+        sp[i] = i + 1 < nsub ? lumen::jh::run_span<lumen::jh::kSync>(H, D->dc, D->ac, w, p0[i], ph0[i], end, zz,
+                                                                     &keys[(size_t)i * kCap], 1,
+                                                                     &marks[(size_t)i * kCap], 0, &s0[i])
+                             : lumen::jh::run_span<lumen::jh::kPlain>(H, D->dc, D->ac, w, p0[i], ph0[i], end, zz);
+        if (i + 1 < nsub && (sp[i].pos != epos[i + 1] || sp[i].phase != eph[i + 1])) {
+          epos[i + 1] = sp[i].pos;
+          eph[i + 1] = sp[i].phase;
+          dirty[i + 1] = 1;
+          chg = true;
+        }
+      }
+      rounds = r + 1;
+    }
+    int64_t base = 0, a0 = 0, a1 = 0, a2 = 0;
+    for (int i = 0; i < nsub; ++i) {
+      if (sp[i].good < sp[i].n && base + sp[i].good < H.total) bad = 1;
+      if (i == nsub - 1 && base + sp[i].n < H.total) bad = 1;
+      if (base < H.total &&
+          !lumen::jh::write_span(H, D->dc, D->ac, w, epos[i], eph[i], (uint32_t)(i + 1) * sub, base, (int)a0, (int)a1,
+                                 (int)a2, co, zz))
+        bad = 1;
+      base += sp[i].n;
+      a0 += sp[i].d0;
+      a1 += sp[i].d1;
+      a2 += sp[i].d2;
+    }
+    err[2 * img] = bad;
+    err[2 * img + 1] = rounds;
+  }
   return 0;
 }
 

@@ -27,4 +27,13 @@ hipError_t jpeg_reconstruct(const JpegPlanes& P, uint8_t* out, hipStream_t strea
 hipError_t jpeg_reconstruct_batch(const JpegBatchEntry* entries, int n, int64_t total_blk, int64_t total_pix,
                                   hipStream_t stream);
 
+// GPU entropy decode (jpeg_huff.hip): blob = JHuffJob[n] + descriptors / streams (jpeg_huff.h);
+// coefficient planes into coefs; err [2n] int32 zeroed (malformed flag, synchronisation rounds);
+// scratch: jpeg_huff_scratch_bytes(n, lanes) zeroed; max_wg: the most workgroups an image needs
+// (ceil(nsub / 256)); lanes: the most lanes of an image; window: the largest stream window (words);
+// ticks (nullable): [n][128] wall-clock stamps of workgroup 0's phases (profiling)
+hipError_t jpeg_huff_decode(const uint8_t* blob, int n, int max_wg, int16_t* coefs, int32_t* err, void* scratch,
+                            int lanes, int window, int64_t* ticks, hipStream_t stream);
+size_t jpeg_huff_scratch_bytes(int n, int lanes);
+
 }  // namespace lumen

@@ -19,6 +19,7 @@ hipError_t db_quad_score(const void* prob, int is_bf16, int n, int H, int W, con
                          int m, hipStream_t stream);
 }  // namespace lumen
 #include "jpeg.h"
+#include "jpeg_huff.h"
 
 namespace {
 
@@ -274,9 +275,80 @@ void jpeg_reconstruct_batch(const at::Tensor& coef_all, const at::Tensor& qt_all
                                            blk, pix, stream()));
 }
 
+// GPU entropy decode of n prepared JPEGs (host/jpeg_decode.cpp:lumen_jpeg_prepare_gpu).  blob: the
+// device copy of the pinned upload blob_host; every job's descriptor, stream, restart table and
+// coefficient range is bounds-checked on the host copy before the launch.
+void jpeg_huff_decode(const at::Tensor& blob, const at::Tensor& blob_host, int64_t n, at::Tensor coefs,
+                      at::Tensor err, const c10::optional<at::Tensor>& ticks) {
+  TORCH_CHECK(blob.is_cuda() && blob.scalar_type() == at::kByte && blob.is_contiguous(), "jpeg_huff: blob uint8");
+  TORCH_CHECK(!blob_host.is_cuda() && blob_host.scalar_type() == at::kByte && blob_host.is_contiguous() &&
+              blob_host.numel() == blob.numel(), "jpeg_huff: blob_host must be the host copy of blob");
+  TORCH_CHECK(coefs.is_cuda() && coefs.scalar_type() == at::kShort && coefs.is_contiguous(), "jpeg_huff: coefs int16");
+  TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt && err.numel() >= 2 * n, "jpeg_huff: err int32 [2n]");
+  TORCH_CHECK(n > 0 && (int64_t)sizeof(lumen::JHuffJob) * n <= blob.numel(), "jpeg_huff: jobs");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(blob.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(coefs.data_ptr()) % 16 == 0, "jpeg_huff: 16-byte aligned buffers");
+  const uint8_t* hb = blob_host.data_ptr<uint8_t>();
+  const int64_t bn = blob.numel();
+  int max_wg = 1, max_lanes = 1, max_window = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const lumen::JHuffJob& j = reinterpret_cast<const lumen::JHuffJob*>(hb)[i];
+    TORCH_CHECK(j.desc_off >= 0 && j.desc_off % 16 == 0 && j.desc_off + (int64_t)sizeof(lumen::JHuffDesc) <= bn,
+                "jpeg_huff: descriptor ", i, " outside the blob");
+    const lumen::JHuffHead& H = reinterpret_cast<const lumen::JHuffDesc*>(hb + j.desc_off)->h;
+    TORCH_CHECK(H.ncomp >= 1 && H.ncomp <= 3 && H.bpm >= 1 && H.bpm <= 10 && H.mcux >= 1 && H.total >= 0 &&
+                H.nbits >= 0 && H.nwords >= 0 && H.ndc >= 1 && H.ndc <= 3 && H.nac >= 1 && H.nac <= 3,
+                "jpeg_huff: descriptor ", i, " header");
+    TORCH_CHECK(H.stream_off % 16 == 0 && j.desc_off + H.stream_off + 4 * (int64_t)H.nwords <= bn &&
+                4 * (int64_t)H.nwords * 8 >= (int64_t)H.nbits && H.nbits < (1 << 28),
+                "jpeg_huff: stream ", i, " outside the blob");
+    if (H.restart_blocks == 0) {
+      max_wg = std::max(max_wg, (H.nsub + lumen::kJHuffWgLanes - 1) / lumen::kJHuffWgLanes);
+      max_lanes = std::max(max_lanes, H.nsub);
+      max_window = std::max<int64_t>(max_window, std::min<int64_t>(H.nwords, (int64_t)lumen::kJHuffWgLanes * H.sub_bits / 32 + 256));
+    }
+    for (int k = 0; k < H.bpm; ++k)
+      TORCH_CHECK(H.pcomp[k] >= 0 && H.pcomp[k] < H.ncomp && H.pdc[k] >= 0 && H.pdc[k] < H.ndc && H.pac[k] >= 0 &&
+                  H.pac[k] < H.nac && H.px[k] >= 0 && H.px[k] < H.hh[H.pcomp[k]] && H.py[k] >= 0 &&
+                  H.py[k] < H.vv[H.pcomp[k]], "jpeg_huff: MCU layout ", i);
+    int64_t blocks = 0;
+    for (int c = 0; c < H.ncomp; ++c) {
+      TORCH_CHECK(H.hh[c] >= 1 && H.hh[c] <= 2 && H.vv[c] >= 1 && H.vv[c] <= 2 && H.bw[c] == H.mcux * H.hh[c] &&
+                  H.plane_off[c] == 64 * blocks, "jpeg_huff: planes ", i);
+      blocks += (int64_t)H.bw[c] * (H.total / H.bpm / H.mcux) * H.vv[c];
+    }
+    TORCH_CHECK(blocks == H.total && j.coef_off >= 0 && j.coef_off % 64 == 0 && j.coef_off + 64 * blocks <= coefs.numel(),
+                "jpeg_huff: coefficients of image ", i, " outside the buffer");
+    if (H.restart_blocks > 0) {
+      TORCH_CHECK(H.nseg >= 1 && H.seg_off % 4 == 0 && j.desc_off + H.seg_off + 4 * (int64_t)H.nseg <= bn &&
+                  (int64_t)H.nseg * H.restart_blocks >= H.total, "jpeg_huff: restart table ", i);
+    } else {
+      TORCH_CHECK(H.sub_bits >= 32 && H.sub_bits % 32 == 0 && H.nsub >= 1 && H.nsub <= lumen::kJHuffMaxLanes &&
+                  (int64_t)H.nsub * H.sub_bits >= (int64_t)H.nbits, "jpeg_huff: subsequences ", i);
+    }
+  }
+  // the workgroups of an image meet at a spin barrier: all of them must be resident at once
+  int cus = 0;
+  CHECK_HIP2(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, blob.get_device()));
+  TORCH_CHECK(max_wg == 1 || n * max_wg <= cus, "jpeg_huff: ", n, " images x ", max_wg,
+              " workgroups exceed the ", cus, " CUs (prepare with fewer lanes per image)");
+  auto scratch = at::zeros({(int64_t)lumen::jpeg_huff_scratch_bytes((int)n, max_lanes)}, blob.options());
+  err.zero_();
+  coefs.zero_();   // the decoder writes only the nonzero coefficients
+  int64_t* tp = nullptr;
+  if (ticks.has_value()) {
+    TORCH_CHECK(ticks->is_cuda() && ticks->scalar_type() == at::kLong && ticks->numel() >= 128 * n, "jpeg_huff: ticks");
+    tp = ticks->data_ptr<int64_t>();
+  }
+  CHECK_HIP2(lumen::jpeg_huff_decode(blob.data_ptr<uint8_t>(), (int)n, max_wg, coefs.data_ptr<int16_t>(),
+                                     err.data_ptr<int32_t>(), scratch.data_ptr(), max_lanes, max_window, tp, stream()));
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(lumen, m) {
+  m.def("jpeg_huff_decode(Tensor blob, Tensor blob_host, int n, Tensor(c!) coefs, Tensor(e!) err, "
+        "Tensor(t!)? ticks=None) -> ()");
   m.def("jpeg_reconstruct(Tensor coef, Tensor qt, int[] meta, Tensor(s!) samp, Tensor(o!) out) -> ()");
   m.def("jpeg_reconstruct_batch(Tensor coef_all, Tensor qt_all, Tensor meta, Tensor(s!) samp_all, Tensor(o!) out_flat, "
         "Tensor(e!) entries, Tensor(h!) entries_host) -> ()");
@@ -298,6 +370,7 @@ TORCH_LIBRARY_FRAGMENT(lumen, m) {
 TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("jpeg_reconstruct", &jpeg_reconstruct);
   m.impl("jpeg_reconstruct_batch", &jpeg_reconstruct_batch);
+  m.impl("jpeg_huff_decode", &jpeg_huff_decode);
   m.impl("det_decode", &det_decode);
   m.impl("nms", &nms);
   m.impl("warp_batch", &warp_batch);

@@ -20,7 +20,9 @@ LLM's prefill embedding buffer that the ``<image>`` token occupies.
 """
 from __future__ import annotations
 
+import logging
 import os
+import threading
 
 from dataclasses import asdict, dataclass, field
 from typing import Optional, Sequence
@@ -34,6 +36,31 @@ from ..utils.h2d import h2d
 from .clip import VisionConfig, VisionTower
 from .fastvit import FASTVIT_PRESETS, FastViTConfig, FastViTTower
 from .llm import LLM, LLM_PRESETS, LLMConfig, TPInfo
+
+log = logging.getLogger("lumen.vlm")
+
+# The image encoder (patch GEMM -> tower -> projector) of a small image count replayed from a
+# hipGraph: ~170 launches of ~8 us host time each become one, so the tower no longer waits on the
+# host at the start of a request (profiles/r5_ttft_*).  LUMEN_VISION_GRAPH=0: eager launches.
+_VISION_GRAPH = os.environ.get("LUMEN_VISION_GRAPH", "1") == "1"
+_VISION_GRAPH_MAX_B = 4
+# the service / benchmarks encode a request's image in the request's thread (encode_ahead)
+ENCODE_AHEAD = os.environ.get("LUMEN_VLM_ENCODE_AHEAD", "1") == "1"
+
+
+class EncodedImage:
+    """Projected embeddings [N_img, hidden] of one image, encoded ahead of the prefill
+    (:meth:`VLM.encode_ahead`, in the request's thread while the engine admits it); the prefill
+    builder splices the rows instead of running the tower."""
+
+    __slots__ = ("emb",)
+
+    def __init__(self, emb: torch.Tensor):
+        self.emb = emb
+
+    @property
+    def shape(self):
+        return tuple(self.emb.shape)
 
 
 @dataclass
@@ -118,6 +145,14 @@ class VLM(nn.Module):
         self.proj2_w = nn.Parameter(torch.zeros(Hd, Hd, **kw), requires_grad=False)
         self.proj2_b = nn.Parameter(torch.zeros(Hd, dtype=torch.float32, device=device), requires_grad=False)
         self.llm = LLM(cfg.llm, tp, dtype, device)
+        self._vgraphs: dict = {}
+        self._vgraph_lock = threading.Lock()
+
+    def invalidate_graphs(self) -> None:
+        """Drop the captured image-encoder graphs (they hold the weights' tensors; call after any
+        weight load / quantisation)."""
+        with self._vgraph_lock:
+            self._vgraphs.clear()
 
     @torch.no_grad()
     def random_init(self, seed: int = 0):
@@ -132,6 +167,7 @@ class VLM(nn.Module):
         self.proj1_w.copy_((torch.randn(Hd, Wv, generator=g) * Wv ** -0.5).to(self.proj1_w.dtype).to(dev))
         self.proj2_w.copy_((torch.randn(Hd, Hd, generator=g) * Hd ** -0.5).to(self.proj2_w.dtype).to(dev))
         self.llm.random_init(seed)
+        self.invalidate_graphs()
 
     @torch.no_grad()
     def quantize_fp8(self) -> None:
@@ -140,6 +176,7 @@ class VLM(nn.Module):
         self.llm.quantize_fp8()
         if self.cfg.vision_arch != "fastvit" and os.environ.get("LUMEN_VIT_FP8", "1") != "0":
             self.vision.w8a8 = True
+        self.invalidate_graphs()
 
     @property
     def device(self):
@@ -163,19 +200,79 @@ class VLM(nn.Module):
                               kpad=v.kpad, pad=self.cfg.pad_value, geoms=geoms, out_dtype=v.patch_w.dtype,
                               device=self.device)
 
-    @torch.no_grad()
-    def encode_images(self, images: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """-> projected image embeddings [B * N_img, hidden] (or written into ``out`` rows)."""
-        B = len(images)
+    def _encode_tower(self, pre: torch.Tensor, B: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """preprocessed pixels -> projected embeddings [B * N_img, hidden]"""
         if self.cfg.vision_arch == "fastvit":     # conv_exp map [B, 16, 16, 3072]: NHWC rows = image tokens
-            feats = self.vision.forward_features(self.preprocess(images))
+            feats = self.vision.forward_features(pre)
         else:
-            feats = self.vision.forward_features(self.preprocess(images), B, self.cfg.feature_layer)
+            feats = self.vision.forward_features(pre, B, self.cfg.feature_layer)
         f = feats.reshape(B * self.cfg.num_image_tokens, -1)
         if not f.is_contiguous():
             f = f.contiguous()
         h = ops.linear(f, self.proj1_w, self.proj1_b, act="gelu")
         return ops.linear(h, self.proj2_w, self.proj2_b, out=out)
+
+    def _graph_ok(self, pre: torch.Tensor, B: int) -> bool:
+        return _VISION_GRAPH and pre.is_cuda and B <= _VISION_GRAPH_MAX_B and not torch.cuda.is_current_stream_capturing()
+
+    def _graph_encode(self, pre: torch.Tensor, B: int, out: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+        """the tower from the graph of this (B, input shape, tower precision); None when it cannot be
+        captured (eager from then on for this key).  The static input / output are used under the
+        lock, so concurrent requests cannot interleave their copies with another's replay."""
+        key = (B, tuple(pre.shape), pre.dtype, bool(getattr(self.vision, "w8a8", False)))
+        with self._vgraph_lock:
+            ent = self._vgraphs.get(key)
+            if ent is None:
+                ent = self._capture(pre, B)
+                self._vgraphs[key] = ent
+            if ent is False:
+                return None
+            ent["in"].copy_(pre)
+            ent["g"].replay()
+            if out is not None:
+                out.copy_(ent["out"])
+                return out
+            return ent["out"].clone()
+
+    def _capture(self, pre: torch.Tensor, B: int):
+        try:
+            static_in = pre.clone()
+            cur = torch.cuda.current_stream(pre.device)
+            side = torch.cuda.Stream(device=pre.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self._encode_tower(static_in, B)     # warm-up: weight caches, workspaces, autotune
+            cur.wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                static_out = self._encode_tower(static_in, B)
+            return {"g": g, "in": static_in, "out": static_out}
+        except Exception as e:  # noqa: BLE001 - an op that cannot be captured: eager launches
+            log.warning("image encoder graph capture failed (%s); eager launches", e)
+            return False
+
+    @torch.no_grad()
+    def encode_images(self, images: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """-> projected image embeddings [B * N_img, hidden] (or written into ``out`` rows)."""
+        B = len(images)
+        pre = self.preprocess(images)
+        if self._graph_ok(pre, B):
+            r = self._graph_encode(pre, B, out)
+            if r is not None:
+                return r
+        return self._encode_tower(pre, B, out=out)
+
+    @torch.no_grad()
+    def encode_ahead(self, images: Sequence[torch.Tensor]) -> list:
+        """Run the image encoder now (in the caller's thread, on its stream) and return
+        :class:`EncodedImage` stand-ins for :meth:`build_prefill`: the tower's GPU work then starts
+        while the engine is still admitting the request.  Single-rank models only (under tensor
+        parallelism the images follow the TP group's own schedule)."""
+        if self.llm.tp.enabled or not images or self.device.type != "cuda":
+            return list(images)
+        N = self.cfg.num_image_tokens
+        emb = self.encode_images(images)
+        return [EncodedImage(emb[i * N:(i + 1) * N]) for i in range(len(images))]
 
     # ------------------------------------------------------------------ prefill inputs
     def expand_image_tokens(self, ids: Sequence[int], n_images: int) -> tuple[list[int], list[int]]:
@@ -243,10 +340,18 @@ class VLM(nn.Module):
                 for i, s in enumerate(starts):
                     x[s:s + N] = buf[i * N:(i + 1) * N]
             return x
+        imgs = images[:len(starts)]
+        if any(isinstance(im, EncodedImage) for im in imgs):
+            raw = [im for im in imgs if not isinstance(im, EncodedImage)]
+            enc = iter(self.encode_ahead(raw)) if raw else iter(())
+            for i, s in enumerate(starts):
+                im = imgs[i] if isinstance(imgs[i], EncodedImage) else next(enc)
+                x[s:s + N] = im.emb
+            return x
         if contiguous:
-            self.encode_images(images[:len(starts)], out=x[starts[0]:starts[0] + N * len(starts)])
+            self.encode_images(imgs, out=x[starts[0]:starts[0] + N * len(starts)])
         else:
-            emb = self.encode_images(images[:len(starts)])
+            emb = self.encode_images(imgs)
             for i, s in enumerate(starts):
                 x[s:s + N] = emb[i * N:(i + 1) * N]
         return x
@@ -289,6 +394,7 @@ class VLM(nn.Module):
                          (self.proj2_w, "mm_projector.2.weight"), (self.proj2_b, "mm_projector.2.bias")):
             dst.copy_(sd[key].to(dst.dtype))
         self.llm.load_hf_state_dict(sd)
+        self.invalidate_graphs()
 
 
 # ============================================================================= synthetic pack

@@ -44,6 +44,15 @@ def _lib():
             lib.lumen_jpeg_decode_coefs.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p]
             lib.lumen_jpeg_decode_coefs.restype = ctypes.c_int
+            if hasattr(lib, "lumen_jpeg_prepare_gpu"):
+                lib.lumen_jpeg_prepare_gpu.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                       ctypes.c_int64, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
+                                                       ctypes.c_int]
+                lib.lumen_jpeg_prepare_gpu.restype = ctypes.c_int
+                lib.lumen_jpeg_gpu_emulate.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                       ctypes.c_void_p]
+                lib.lumen_jpeg_gpu_emulate.restype = ctypes.c_int
+                lib.lumen_jpeg_desc_bytes.restype = ctypes.c_int
             _typed = True
     return lib
 
@@ -125,6 +134,171 @@ def decode_coefs(data: bytes, threads: Optional[int] = None, jinfo: Optional[Jpe
                           "blocks": int(st[3])}
 
 
+# ------------------------------------------------------------------ GPU entropy decode (csrc/jpeg_huff.hip)
+_HEAD = 512                 # blob header: JHuffJob[n] when n <= 32 (else n * 16 rounded up to 256)
+
+
+def gpu_entropy_enabled() -> bool:
+    """``LUMEN_JPEG_GPU_ENTROPY=1``: baseline JPEGs are entropy-decoded on the GPU
+    (csrc/jpeg_huff.hip) instead of on the host thread pool.  Off by default: a GPU lane decodes a
+    Huffman symbol in ~1 us (a serial dependent chain of ~130 instructions and 3-4 LDS round trips),
+    so the lone-image decode (1.3-1.6 ms for a 1024 x 768 photo, bound by the resynchronisation
+    chain) loses to the 16-thread host decoder (0.9 ms), and a batch-128 decode (7.8k img/s) holds
+    up to 128 CUs for 16 ms that the vision tower would use (profiles/r5_jpeg_gpu_entropy_v1.txt).
+    It pays where host cores are the scarce resource."""
+    return os.environ.get("LUMEN_JPEG_GPU_ENTROPY", "0") == "1"
+
+
+def _desc_bytes() -> int:
+    return (int(_lib().lumen_jpeg_desc_bytes()) + 255) & ~255
+
+
+def _cap1(data: bytes, ji: "JpegInfo") -> int:
+    """blob bytes one payload may take: descriptor + stream words (+ the restart table, at most one
+    4-byte start per 2 payload bytes)"""
+    return (_desc_bytes() + (3 if ji.restart else 1) * len(data) + 1024 + 255) & ~255
+
+
+def _head(n: int) -> int:
+    return max(_HEAD, (16 * n + 255) & ~255)
+
+
+def blob_capacity(datas, infos=None) -> int:
+    """Upper bound of the upload blob for these payloads (job header + per image descriptor,
+    stream words and restart table)."""
+    infos = infos or [info(d) for d in datas]
+    return _head(len(datas)) + sum(_cap1(d, ji) for d, ji in zip(datas, infos) if ji is not None)
+
+
+def single_lanes() -> int:
+    """Lanes for a lone image (``LUMEN_JPEG_LANES``, default 1024 = 4 workgroups): more lanes
+    shorten each lane's span but add synchronisation rounds (~ resync distance / span), each a
+    cross-workgroup barrier (profiles/r5_jpeg_gpu_entropy_*)."""
+    return int(os.environ.get("LUMEN_JPEG_LANES", "1024"))
+
+
+def lanes_for(n_images: int, cus: int = 256) -> int:
+    """Decoding lanes per image for a batch of n: 256-lane workgroups, as many per image (<= 16) as
+    keep every workgroup of the batch resident at once (the image's workgroups meet at a spin
+    barrier), so a lone image spreads over 16 CUs and a batch of >= 256 uses one CU each."""
+    return 256 * max(1, min(16, cus // max(1, n_images)))
+
+
+def prepare_blob(datas, infos, blob: np.ndarray, qt: np.ndarray, pool=None, lanes: Optional[int] = None):
+    """Fill ``blob`` (uint8, >= blob_capacity) with each payload's descriptor + stream at a fixed
+    offset (prepared on ``pool`` when given: the ctypes calls release the GIL) and a job header
+    listing the payloads that prepared; ``qt`` [n, 192] uint16 receives the quantisation tables.
+    Coefficients of payload k start at element sum(coef_count of the payloads before it).
+    -> (bytes to upload, ok flags); the job count is sum(ok)."""
+    lib = _lib()
+    n = len(datas)
+    lanes = lanes or lanes_for(n)
+    offs, coffs, off, coff = [], [], _head(n), 0
+    for d, ji in zip(datas, infos):
+        offs.append(off)
+        coffs.append(coff)
+        if ji is not None:
+            off += _cap1(d, ji)
+            coff += ji.coef_count
+    base = blob.ctypes.data
+
+    def one(k):
+        if infos[k] is None:
+            return False, 0
+        need = ctypes.c_int64(0)
+        cap = _cap1(datas[k], infos[k])
+        r = lib.lumen_jpeg_prepare_gpu(datas[k], len(datas[k]), base + offs[k], cap, qt[k].ctypes.data,
+                                       ctypes.byref(need), int(lanes))
+        return r == 0, int(need.value)
+
+    res = list(pool.map(one, range(n))) if pool is not None and n > 2 else [one(k) for k in range(n)]
+    ok = [r[0] for r in res]
+    jobs = np.array([(offs[k], coffs[k]) for k in range(n) if ok[k]], np.int64).reshape(-1, 2)
+    blob[:16 * len(jobs)].view(np.int64)[:] = jobs.reshape(-1)
+    used = max([_head(n)] + [offs[k] + res[k][1] for k in range(n) if ok[k]])
+    return (used + 15) & ~15, ok
+
+
+def emulate_gpu_decode(data: bytes, lanes: Optional[int] = None, stats: Optional[dict] = None):
+    """The GPU decoder's schedule run on the host (csrc/host/jpeg_decode.cpp:lumen_jpeg_gpu_emulate)
+    -> (coefficients int16 [coef_count], qt [ncomp, 64], JpegInfo, malformed flag, rounds) or None."""
+    ji = info(data)
+    if ji is None:
+        return None
+    blob = np.zeros(blob_capacity([data], [ji]), np.uint8)
+    qt = np.zeros((1, 192), np.uint16)
+    used, ok = prepare_blob([data], [ji], blob, qt, lanes=lanes)
+    if not ok[0]:
+        return None
+    coef = np.full(ji.coef_count, 12345, np.int16)      # zeroed by the emulation, as by the launcher
+    err = np.zeros(2, np.int32)
+    st = np.zeros(4, np.int64)
+    _lib().lumen_jpeg_gpu_emulate(blob.ctypes.data, 1, coef.ctypes.data, err.ctypes.data, st.ctypes.data)
+    if stats is not None:
+        stats.update(slides=int(st[0]), blocks=int(st[1]), max_lane_slides=int(st[2]), lanes=int(st[3]))
+    return coef, qt[0, :64 * ji.ncomp].reshape(ji.ncomp, 64), ji, int(err[0]), int(err[1])
+
+
+class _HuffStaging(threading.local):
+    blob = None
+    qt = None
+    ev = None
+
+
+_hstage = _HuffStaging()
+
+
+def decode_to_device_gpu(data: bytes, device, ji: Optional["JpegInfo"] = None, lanes: Optional[int] = None):
+    """Baseline JPEG -> uint8 [H, W, 3] on ``device`` with the entropy decode on the GPU too:
+    the host parses the header and unstuffs the bytes into a pinned blob (one H2D), then
+    jpeg_huff_decode + jpeg_reconstruct run on the current stream.  The result carries
+    ``jpeg_err`` (device int32 [2]: malformed flag, rounds) for :func:`check_device_error`.
+    None when the payload is not a baseline JPEG this path handles."""
+    import torch
+
+    from ..ops import hip_ops
+
+    dev = torch.device(device)
+    ji = ji or info(data)
+    if ji is None:
+        return None
+    st = _hstage
+    if st.ev is not None:
+        st.ev.synchronize()              # this thread's previous upload has read the staging blob
+    cap = blob_capacity([data], [ji])
+    if st.blob is None or st.blob.numel() < cap:
+        st.blob = torch.empty(max(cap, 1 << 20), dtype=torch.uint8).pin_memory()
+        st.qt = torch.empty((1, 192), dtype=torch.int16).pin_memory()
+    bnp = st.blob.numpy()
+    used, ok = prepare_blob([data], [ji], bnp, st.qt.numpy().view(np.uint16), lanes=lanes or single_lanes())
+    if not ok[0]:
+        return None
+    hb = st.blob[:used]
+    bd = hb.to(dev, non_blocking=True)
+    qd = st.qt[0, :64 * ji.ncomp].to(dev, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    st.ev = ev
+    n = ji.coef_count
+    coef = torch.empty(n, dtype=torch.int16, device=dev)
+    err = torch.empty(2, dtype=torch.int32, device=dev)
+    ops = hip_ops()
+    ops.jpeg_huff_decode(bd, hb, 1, coef, err)
+    samp = torch.empty(n, dtype=torch.uint8, device=dev)
+    out = torch.empty((ji.height, ji.width, 3), dtype=torch.uint8, device=dev)
+    ops.jpeg_reconstruct(coef, qd, ji.meta(), samp, out)
+    out.jpeg_err = err
+    return out
+
+
+def check_device_error(img) -> None:
+    """Raise ValueError when a GPU-entropy-decoded image's stream was malformed (reads the flag:
+    a device sync, so call it where the caller synchronises anyway)."""
+    err = getattr(img, "jpeg_err", None)
+    if err is not None and int(err[0].item()) != 0:
+        raise ValueError("cannot identify image file: malformed JPEG entropy-coded data")
+
+
 # ------------------------------------------------------------------ NumPy reference of csrc/jpeg.hip
 def _idct_matrix() -> np.ndarray:
     k = np.zeros((8, 8), np.float64)
@@ -202,6 +376,10 @@ def decode_to_device(data: bytes, device, threads: Optional[int] = None, stats: 
 
     dev = torch.device(device)
     ji = info(data) if dev.type == "cuda" else None
+    if ji is not None and gpu_entropy_enabled() and threads is None and stats is None:
+        out = decode_to_device_gpu(data, dev, ji)
+        if out is not None:
+            return out
     if ji is not None:
         # coefficients straight into a pinned, per-thread staging buffer -> one async H2D
         n = ji.coef_count
@@ -253,7 +431,7 @@ class _BatchStaging(threading.local):
     device has consumed batch i's copies waits only for batch i - 1's."""
 
     def __init__(self):
-        self.slots = [[None, None], [None, None]]    # [bufs (coef, qt, entries, raw), event of their H2D]
+        self.slots = [[None, None], [None, None]]    # [bufs (coef, qt, entries, raw, blob), event of their H2D]
         self.k = 0
 
 
@@ -295,23 +473,32 @@ def decode_batch_to_device(datas, device):
     st.k ^= 1
     if slot[1] is not None:
         slot[1].synchronize()        # the batch before last has been copied out of this staging set
-    coef_h, qt_h, ent_h, raw_h = slot[0] or (None, None, None, None)
-    coef_h = _pinned(coef_h, tot, torch.int16)
+    coef_h, qt_h, ent_h, raw_h, blob_h = slot[0] or (None, None, None, None, None)
     qt_h = _pinned(qt_h, max(1, len(jidx)) * 192, torch.int16)
     ent_h = _pinned(ent_h, max(1, len(jidx)) * _ENTRY_BYTES, torch.uint8)
-    coef_np, qt_np = coef_h.numpy(), qt_h.numpy()
+    qt_np = qt_h.numpy()
+    gpu_ent = bool(jidx) and gpu_entropy_enabled()
+    if gpu_ent:
+        # entropy decode on the GPU (csrc/jpeg_huff.hip): the host only parses + unstuffs
+        dj, ij = [datas[i] for i in jidx], [infos[i] for i in jidx]
+        blob_h = _pinned(blob_h, blob_capacity(dj, ij), torch.uint8)
+        used, ok = prepare_blob(dj, ij, blob_h.numpy(), qt_np[:len(jidx) * 192].view(np.uint16).reshape(-1, 192),
+                                _pool())
+    else:
+        coef_h = _pinned(coef_h, tot, torch.int16)
+        coef_np = coef_h.numpy()
 
-    def ent(k_i):
-        k, i = k_i
-        ji = infos[i]
-        res = decode_coefs(datas[i], 1, ji, out=coef_np[cbase[i]:cbase[i] + ji.coef_count])
-        if res is None:
-            return None
-        q = res[1]
-        qt_np[k * 192:k * 192 + q.size] = q.reshape(-1).view(np.int16)
-        return True
+        def ent(k_i):
+            k, i = k_i
+            ji = infos[i]
+            res = decode_coefs(datas[i], 1, ji, out=coef_np[cbase[i]:cbase[i] + ji.coef_count])
+            if res is None:
+                return None
+            q = res[1]
+            qt_np[k * 192:k * 192 + q.size] = q.reshape(-1).view(np.int16)
+            return True
 
-    ok = list(_pool().map(ent, list(enumerate(jidx)))) if jidx else []
+        ok = list(_pool().map(ent, list(enumerate(jidx)))) if jidx else []
     good = [i for i, r in zip(jidx, ok) if r]
     good_set = set(good)
     slow = [i for i in range(n) if i not in good_set]
@@ -360,16 +547,36 @@ def decode_batch_to_device(datas, device):
             row.append(jidx.index(i))
             meta[k] = row
             sbase += ji.coef_count
-        coef_d = coef_h[:tot].to(dev, non_blocking=True)
         qt_d = qt_h[:len(jidx) * 192].to(dev, non_blocking=True)
+        if gpu_ent:
+            hb = blob_h[:used]
+            coef_d = torch.empty(max(tot, 1), dtype=torch.int16, device=dev)
+            err_d = torch.empty(2 * len(good), dtype=torch.int32, device=dev)
+            hip_ops().jpeg_huff_decode(hb.to(dev, non_blocking=True), hb, len(good), coef_d, err_d)
+            out.jpeg_err = err_d
+            out.jpeg_err_items = list(good)
+        else:
+            coef_d = coef_h[:tot].to(dev, non_blocking=True)
         samp = torch.empty(max(sbase, 1), dtype=torch.uint8, device=dev)
         ent_d = torch.empty(len(good) * _ENTRY_BYTES, dtype=torch.uint8, device=dev)
         hip_ops().jpeg_reconstruct_batch(coef_d, qt_d, torch.from_numpy(meta), samp, out, ent_d, ent_h)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
     slot[1] = ev
-    slot[0] = (coef_h, qt_h, ent_h, raw_h)
+    slot[0] = (coef_h, qt_h, ent_h, raw_h, blob_h)
     return out, offs, shapes, errors
+
+
+def device_errors(flat) -> dict:
+    """Payloads of a :func:`decode_batch_to_device` batch whose GPU entropy decode found a
+    malformed stream -> {index: ValueError} (reads the flags: a device sync, so call it where the
+    caller synchronises anyway, e.g. after copying its results to the host)."""
+    err = getattr(flat, "jpeg_err", None)
+    if err is None:
+        return {}
+    flags = err.view(-1, 2)[:, 0].cpu().numpy()
+    return {i: ValueError("cannot identify image file: malformed JPEG entropy-coded data")
+            for i, f in zip(flat.jpeg_err_items, flags) if f}
 
 
 class DeviceImage:

@@ -228,3 +228,34 @@ def test_vlm_backend_fp8_shard_cache(tmp_path, monkeypatch):
         finally:
             b.close()
     assert outs[0] == outs[1]
+
+
+@pytest.mark.parametrize("preset,fp8", [("tiny", False), ("tiny", True), ("tiny-fastvit", False)])
+def test_image_encoder_graph_and_encode_ahead(preset, fp8):
+    """The image encoder replayed from its hipGraph (models/vlm.py:_graph_encode) equals the eager
+    launches, and a prompt built from encode_ahead's EncodedImage equals one built from the raw
+    image (the service encodes in the request's thread)."""
+    from lumen_amd.models.vlm import VLM, VLM_PRESETS, EncodedImage
+
+    if preset not in VLM_PRESETS:
+        pytest.skip(f"no {preset} preset")
+    m = VLM(VLM_PRESETS[preset], device="cuda")
+    m.random_init(3)
+    if fp8:
+        m.quantize_fp8()
+    imgs = [torch.randint(0, 256, (40 + 7 * i, 52, 3), dtype=torch.uint8, device="cuda") for i in range(2)]
+    with torch.no_grad():
+        for k in (1, 2):
+            eager = m._encode_tower(m.preprocess(imgs[:k]), k)
+            g1 = m.encode_images(imgs[:k])
+            g2 = m.encode_images(imgs[:k])           # replay
+            assert torch.equal(g1, eager) and torch.equal(g2, eager)
+        assert m._vgraphs and all(v is not False for v in m._vgraphs.values())
+        ids = [5, 6, m.cfg.image_token_id, 7, 8]
+        ref = m.build_prefill(ids, [imgs[0]])
+        enc = m.encode_ahead([imgs[0]])
+        assert isinstance(enc[0], EncodedImage)
+        got = m.build_prefill(ids, enc)
+        assert torch.equal(got, ref)
+        m.invalidate_graphs()
+        assert not m._vgraphs

@@ -32,6 +32,8 @@
 #   mx_cold        cold-weight timing of the MX chain's GEMMs (full / plain epilogues) vs per-token fp8
 #   pp_cold        ping-pong 128x128 pipeline forms vs the aligned ones (fp8 prefill + bf16 vision shapes)
 #   ttft_ab        TTFT with the fused MX prefill chain (LUMEN_PREFILL_MX=1) vs the per-token-scale chain
+#   f8auto         fp8 tests + cold prefill GEMMs (auto vs codes 1, 2, 16, 17)
+#   acc            full-size fp8 accuracy pins (ViT-L/14-336 W8A8, Llama-3-8B first token)
 #   pmc_gemm       PMC counters (MFMA, LDS conflicts, busy) of one ViT-L/14 GEMM shape
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -141,9 +143,9 @@ for task in "$@"; do
           --service clip --model CLIP-ViT-L-14 --device cuda --clients 256 --frontends 8 --client-procs 6 --seconds 15
       done ;;
     jpeg)
-      step jpeg_tests 200 python -u -m pytest tests/test_jpeg_gpu.py tests/test_jpeg_cpu.py -x -q --timeout 120 \
+      step jpeg_tests 200 python -u -m pytest tests/test_jpeg_gpu_entropy_gpu.py tests/test_jpeg_gpu.py tests/test_jpeg_cpu.py -x -q --timeout 120 \
         --timeout-method thread
-      step jpeg_bench 200 python -u tools/jpeg_bench.py ;;
+      step jpeg_bench 300 python -u tools/jpeg_bench.py --n 20 ;;
     mx)
       step mx_tests 400 python -u -m pytest tests/test_mx_gpu.py tests/test_fp8_gpu.py tests/test_llm_ops_gpu.py -q \
         --timeout 120 --timeout-method thread ;;
@@ -157,6 +159,10 @@ for task in "$@"; do
     ttft_ab)
       step ttft_mx 400 env LUMEN_PREFILL_MX=1 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0
       step ttft_pt 400 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0 ;;
+    f8auto)   # fp8 tests + cold-weight prefill GEMMs: auto selection vs the split-K / 256x256 ping-pong forms
+      step f8_tests 400 python -u -m pytest tests/test_fp8_gpu.py -x -q --timeout 120 --timeout-method thread
+      step f8_cold 300 python -u tools/cold_gemm_bench.py --what prefill --variants=0,1,2,16,17 ;;
+    acc) step acc 400 python -u -m pytest tests/test_fp8_accuracy_gpu.py -x -v --timeout 300 --timeout-method thread ;;
     ttft) step ttft 400 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0 ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac

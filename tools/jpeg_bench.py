@@ -1,5 +1,6 @@
 """JPEG decode latency on the bench images: Pillow (full / DCT-scaled) vs the parallel entropy
-decoder (host threads) + GPU reconstruction (utils/jpeg.py), per image, median of N.
+decoder (host threads) + GPU reconstruction vs the GPU entropy decoder (csrc/jpeg_huff.hip) + GPU
+reconstruction (utils/jpeg.py), per image and per batch of 32, median of N.
 
     python tools/jpeg_bench.py [--n 30]
 """
@@ -49,7 +50,21 @@ def main():
             J.decode_to_device(data, "cuda")
             torch.cuda.synchronize()
 
-        r["device_decode_ms"] = med(dev, a.n)
+        def batch():
+            J.decode_batch_to_device([data] * 32, "cuda")
+            torch.cuda.synchronize()
+
+        for mode in ("1", "0"):        # GPU entropy decode, then the host thread-pool decoder
+            os.environ["LUMEN_JPEG_GPU_ENTROPY"] = mode
+            tag = "gpu_entropy" if mode == "1" else "host_entropy"
+            r[f"device_decode_{tag}_ms"] = med(dev, a.n)
+            b = med(batch, max(5, a.n // 4))
+            r[f"batch32_{tag}_ms"] = b
+            r[f"batch32_{tag}_img_s"] = round(32e3 / b, 1)
+        os.environ.pop("LUMEN_JPEG_GPU_ENTROPY")
+        img = J.decode_to_device_gpu(data, "cuda")
+        torch.cuda.synchronize()
+        r["gpu_rounds"] = int(img.jpeg_err[1])
         st = {}
         J.decode_to_device(data, "cuda", stats=st)
         r["stats"] = st

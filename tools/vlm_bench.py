@@ -27,6 +27,7 @@ from lumen_amd.models.vlm import VLM, VLM_PRESETS  # noqa: E402
 from lumen_amd.runtime.engine import LLMEngine, SamplingParams  # noqa: E402
 from lumen_amd.runtime.kv_cache import PagedKVCache  # noqa: E402
 from lumen_amd.utils.image import decode_rgb, encode_jpeg  # noqa: E402
+from lumen_amd.models.vlm import ENCODE_AHEAD  # noqa: E402
 from lumen_amd.utils.jpeg import decode_image  # noqa: E402
 from tools.face_ocr_bench import synth_image  # noqa: E402
 
@@ -81,7 +82,8 @@ def main():
         img = torch.from_numpy(decode_rgb(jpeg, draft_to=draft)) if args.host_decode else \
             decode_image(jpeg, dev, draft_to=draft)
         dec_ms.append((time.perf_counter() - t) * 1000)
-        return img
+        # as the service: the image encoder starts in the request's thread (models/vlm.py:encode_ahead)
+        return m.encode_ahead([img])[0] if ENCODE_AHEAD else img
 
     eng = LLMEngine(m.llm, kv, build, max_batch=max(args.batch, 1))
     rng = np.random.default_rng(0)
