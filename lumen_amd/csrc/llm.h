@@ -66,4 +66,11 @@ hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream);
 hipError_t rep_penalty(float* logits, int64_t ld, const int* ids, int maxn, const float* penalty, int B, int V,
                        hipStream_t stream);
 
+// <= kUploadMax int32 values -> int64 device array, carried in the kernel arguments
+constexpr int kUploadMax = 896;
+struct UploadArgs {
+  int32_t v[kUploadMax];
+};
+hipError_t upload_i64(const UploadArgs& a, int64_t* out, int n, hipStream_t stream);
+
 }  // namespace lumen

@@ -625,4 +625,19 @@ hipError_t rep_penalty(float* logits, int64_t ld, const int* ids, int maxn, cons
   return hipGetLastError();
 }
 
+// Small integer arrays (token ids, cache slots) uploaded through the kernel arguments: no copy
+// engine / blit path, so behind a queue of kernels (a request's prefill inputs behind its image
+// tower) the values land one tiny kernel after the queue drains instead of 20-70 us later per
+// hipMemcpyAsync (profiles/r5_ttft_*).
+__global__ void upload_i64_kernel(UploadArgs a, int64_t* __restrict__ out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = a.v[i];
+}
+
+hipError_t upload_i64(const UploadArgs& a, int64_t* out, int n, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(upload_i64_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a, out, n);
+  return hipGetLastError();
+}
+
 }  // namespace lumen

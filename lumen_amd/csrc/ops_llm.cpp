@@ -147,9 +147,22 @@ void rep_penalty_(at::Tensor logits, const at::Tensor& ids, const at::Tensor& pe
                                 penalty.data_ptr<float>(), (int)B, (int)logits.size(1), cur()));
 }
 
+// int32 CPU values -> int64 device tensor through the kernel arguments (llm.hip:upload_i64)
+void upload_small(const at::Tensor& src, at::Tensor out) {
+  TORCH_CHECK(!src.is_cuda() && src.scalar_type() == at::kInt && src.is_contiguous(), "upload_small: src int32 CPU");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kLong && out.is_contiguous() && out.numel() == src.numel(),
+              "upload_small: out int64 like src");
+  TORCH_CHECK(src.numel() <= lumen::kUploadMax, "upload_small: at most ", lumen::kUploadMax, " values");
+  lumen::UploadArgs a;
+  memcpy(a.v, src.data_ptr<int32_t>(), (size_t)src.numel() * sizeof(int32_t));
+  const at::DeviceGuard g(out.device());
+  CHECK_HIP3(lumen::upload_i64(a, out.data_ptr<int64_t>(), (int)src.numel(), cur()));
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(lumen, m) {
+  m.def("upload_small(Tensor src, Tensor(o!) out) -> ()");
   m.def("rope_kv(Tensor(a!) qkv, Tensor pos, Tensor cos_sin, Tensor? slots, Tensor(k!) k_cache, Tensor(v!) v_cache, "
         "int H, int Hkv, int D) -> ()");
   m.def("paged_decode(Tensor q, Tensor(k!) k_cache, Tensor(v!) v_cache, Tensor block_table, Tensor ctx_len, "
@@ -163,4 +176,5 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("rope_kv", &rope_kv);
   m.impl("paged_decode", &paged_decode);
   m.impl("rep_penalty_", &rep_penalty_);
+  m.impl("upload_small", &upload_small);
 }

@@ -32,7 +32,7 @@ import torch
 from torch import nn
 
 from .. import ops
-from ..utils.h2d import h2d
+from ..utils.h2d import h2d, h2d_ahead
 from .clip import VisionConfig, VisionTower
 from .fastvit import FASTVIT_PRESETS, FastViTConfig, FastViTTower
 from .llm import LLM, LLM_PRESETS, LLMConfig, TPInfo
@@ -46,6 +46,21 @@ _VISION_GRAPH = os.environ.get("LUMEN_VISION_GRAPH", "1") == "1"
 _VISION_GRAPH_MAX_B = 4
 # the service / benchmarks encode a request's image in the request's thread (encode_ahead)
 ENCODE_AHEAD = os.environ.get("LUMEN_VLM_ENCODE_AHEAD", "1") == "1"
+
+
+class PreparedPrefill:
+    """A request's whole prefill input x [T, hidden] (text embeddings + image rows), built in the
+    request's thread (:meth:`VLM.prepare_prefill`) so that its uploads and the image encoder are
+    queued before the engine admits the request; the engine's prefill builder passes it through."""
+
+    __slots__ = ("x",)
+
+    def __init__(self, x: torch.Tensor):
+        self.x = x
+
+    @property
+    def shape(self):
+        return tuple(self.x.shape)
 
 
 class EncodedImage:
@@ -263,6 +278,14 @@ class VLM(nn.Module):
         return self._encode_tower(pre, B, out=out)
 
     @torch.no_grad()
+    def prepare_prefill(self, ids: Sequence[int], images: Sequence[torch.Tensor]):
+        """:meth:`build_prefill` run now, in the caller's thread (single-rank GPU models), wrapped
+        as a :class:`PreparedPrefill`; otherwise None (the engine builds the input itself)."""
+        if self.llm.tp.enabled or self.device.type != "cuda":
+            return None
+        return PreparedPrefill(self.build_prefill(ids, images))
+
+    @torch.no_grad()
     def encode_ahead(self, images: Sequence[torch.Tensor]) -> list:
         """Run the image encoder now (in the caller's thread, on its stream) and return
         :class:`EncodedImage` stand-ins for :meth:`build_prefill`: the tower's GPU work then starts
@@ -306,7 +329,7 @@ class VLM(nn.Module):
         n = len(images) if n_images is None else int(n_images)
         full, starts = self.expand_image_tokens(ids, n)
         dev = self.device
-        t = h2d(full, dev, torch.long)
+        t = h2d_ahead(full, dev, torch.long)
         x = self.llm.embed_tokens(t)
         N = self.cfg.num_image_tokens
         if not starts:

@@ -40,7 +40,7 @@ import torch
 from .. import ops
 from ..ops import llm as lops
 from ..parallel.comm import TPGroupUnavailable
-from ..utils.h2d import h2d
+from ..utils.h2d import h2d, h2d_ahead
 from .kv_cache import BLOCK, PagedKVCache
 
 log = logging.getLogger("lumen.engine")
@@ -701,8 +701,8 @@ class LLMEngine:
         spec = Sampler.spec([r]) if last else None
         if self.sync is not None:
             self.sync.send(("pchunk", r.rid, s, e, slots, tab, spec, last))
-        logits = self.llm.prefill(r.x[s:e], self.kv, h2d(slots, self.device), start_pos=s,
-                                  prefix_blocks=h2d(tab, self.device) if tab is not None else None)
+        logits = self.llm.prefill(r.x[s:e], self.kv, h2d_ahead(slots, self.device), start_pos=s,
+                                  prefix_blocks=h2d_ahead(tab, self.device) if tab is not None else None)
         r.done = e
         self.stats["prefill_chunks"] += 1
         if not last:

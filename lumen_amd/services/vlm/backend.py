@@ -33,7 +33,7 @@ import numpy as np
 import torch
 
 from ...models.llm import TPInfo
-from ...models.vlm import ENCODE_AHEAD, VLM, VLM_PRESETS, EncodedImage, VLMConfig
+from ...models.vlm import ENCODE_AHEAD, VLM, VLM_PRESETS, EncodedImage, PreparedPrefill, VLMConfig
 from ...resources.exceptions import ResourceNotFoundError
 from ...runtime.engine import LLMEngine, SamplingParams
 from ...runtime.kv_cache import PagedKVCache
@@ -472,6 +472,8 @@ class MI355XVLMBackend:
     # ------------------------------------------------------------------ generation
     def _build_prefill(self, args) -> torch.Tensor:
         ids, img = args[0], args[1]
+        if isinstance(img, PreparedPrefill):
+            return img.x
         if len(args) > 2:                    # TP follower: no image here, rank 0 broadcasts its features
             return self.model.build_prefill(ids, [], n_images=args[2])
         tens = [img if isinstance(img, (torch.Tensor, EncodedImage)) else torch.from_numpy(img)] \
@@ -510,9 +512,12 @@ class MI355XVLMBackend:
             raise InvalidInputError(str(e)) from e
         full, starts = self.model.expand_image_tokens(ids, 1)
         if starts and ENCODE_AHEAD and self._tp_group is None and torch.device(self.device).type == "cuda":
-            # the image encoder starts now, in this request's thread, while the engine admits it
+            # the prompt's embeddings and the image encoder are queued now, in this request's
+            # thread, while the engine admits it
             with stage("encode"):
-                img = self.model.encode_ahead([img])[0]
+                pre = self.model.prepare_prefill(ids, [img])
+            if pre is not None:
+                img = pre
         gc = self.generation_config
         stops = {gc.eos_token_id}
         extra_eos = self.resources.extra.get("stop_token_ids") or []

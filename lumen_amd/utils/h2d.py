@@ -40,3 +40,25 @@ def h2d(data, device, dtype=None) -> torch.Tensor:
     pinned = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
     pinned.copy_(t)
     return pinned.to(dev, non_blocking=True)
+
+
+def h2d_ahead(data, device, dtype=None) -> torch.Tensor:
+    """:func:`h2d` for a prefill's small inputs (token ids, cache slots) queued behind other work:
+    an integer array of <= 896 values travels in the arguments of one tiny kernel (ops_llm.cpp:
+    upload_small), so it lands as soon as the queue ahead drains, not 20-70 us later per
+    hipMemcpyAsync (a side-stream copy does not help: the blit kernel waits its turn behind the
+    busy queue's kernels; profiles/r5_ttft_*).  Anything else: :func:`h2d`."""
+    dev = torch.device(device)
+    if dev.type == "cuda" and dtype in (None, torch.long) and not torch.cuda.is_current_stream_capturing():
+        a = data.numpy() if isinstance(data, torch.Tensor) and not data.is_cuda else data
+        if not isinstance(a, torch.Tensor):
+            a = np.asarray(a)
+            if a.dtype.kind in "iu" and 0 < a.size <= 896 and (dtype is not None or a.dtype == np.int64):
+                a32 = a.reshape(-1).astype(np.int32)
+                if int(a32.min()) == int(a.min()) and int(a32.max()) == int(a.max()):
+                    from ..ops import hip_ops
+
+                    out = torch.empty(a.shape, dtype=torch.long, device=dev)
+                    hip_ops().upload_small(torch.from_numpy(a32), out.view(-1))
+                    return out
+    return h2d(data, device, dtype)

@@ -376,3 +376,25 @@ def test_fp8_kv_cache_matches_cpu(H, Hkv, D, fused):
     assert torch.equal(kg.cpu().view(torch.uint8), k_ref.view(torch.uint8))
     assert torch.equal(vg.cpu().view(torch.uint8), v_ref.view(torch.uint8))
     assert _rel(got, ref) < 2e-2
+
+
+def test_upload_small_and_h2d_ahead():
+    """Small integer uploads through kernel arguments (ops_llm.cpp:upload_small) land exactly, in
+    stream order behind queued work; larger / non-integer inputs fall back to the pinned copy."""
+    import numpy as np
+
+    from lumen_amd.utils.h2d import h2d_ahead
+
+    a = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+    for _ in range(4):
+        a = a @ a * 0.01                          # queued work ahead of the uploads
+    ids = list(np.random.default_rng(0).integers(0, 128256, 624))
+    t = h2d_ahead(ids, "cuda", torch.long)
+    slots = np.arange(7, 7 + 896, dtype=np.int64)
+    s = h2d_ahead(slots, "cuda")
+    big = h2d_ahead(np.arange(2000, dtype=np.int64), "cuda")
+    neg = h2d_ahead(np.array([-5, 3, 2 ** 40], dtype=np.int64), "cuda")
+    torch.cuda.synchronize()
+    assert t.dtype == torch.long and t.tolist() == [int(v) for v in ids]
+    assert s.tolist() == slots.tolist() and big.tolist() == list(range(2000))
+    assert neg.tolist() == [-5, 3, 2 ** 40]

@@ -257,5 +257,7 @@ def test_image_encoder_graph_and_encode_ahead(preset, fp8):
         assert isinstance(enc[0], EncodedImage)
         got = m.build_prefill(ids, enc)
         assert torch.equal(got, ref)
+        pre = m.prepare_prefill(ids, [imgs[0]])
+        assert torch.equal(pre.x, ref)
         m.invalidate_graphs()
         assert not m._vgraphs

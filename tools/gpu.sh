@@ -33,6 +33,7 @@
 #   pp_cold        ping-pong 128x128 pipeline forms vs the aligned ones (fp8 prefill + bf16 vision shapes)
 #   ttft_ab        TTFT with the fused MX prefill chain (LUMEN_PREFILL_MX=1) vs the per-token-scale chain
 #   f8auto         fp8 tests + cold prefill GEMMs (auto vs codes 1, 2, 16, 17)
+#   vlm_tests      VLM / engine GPU tests + GPU entropy JPEG tests
 #   acc            full-size fp8 accuracy pins (ViT-L/14-336 W8A8, Llama-3-8B first token)
 #   pmc_gemm       PMC counters (MFMA, LDS conflicts, busy) of one ViT-L/14 GEMM shape
 set -o pipefail
@@ -162,6 +163,8 @@ for task in "$@"; do
     f8auto)   # fp8 tests + cold-weight prefill GEMMs: auto selection vs the split-K / 256x256 ping-pong forms
       step f8_tests 400 python -u -m pytest tests/test_fp8_gpu.py -x -q --timeout 120 --timeout-method thread
       step f8_cold 300 python -u tools/cold_gemm_bench.py --what prefill --variants=0,1,2,16,17 ;;
+    vlm_tests) step vlm_tests 400 python -u -m pytest tests/test_vlm_gpu.py tests/test_jpeg_gpu_entropy_gpu.py -x -q \
+      --timeout 200 --timeout-method thread ;;
     acc) step acc 400 python -u -m pytest tests/test_fp8_accuracy_gpu.py -x -v --timeout 300 --timeout-method thread ;;
     ttft) step ttft 400 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0 ;;
     *) echo "unknown task $task"; exit 2 ;;

@@ -27,7 +27,7 @@ from lumen_amd.models.vlm import VLM, VLM_PRESETS  # noqa: E402
 from lumen_amd.runtime.engine import LLMEngine, SamplingParams  # noqa: E402
 from lumen_amd.runtime.kv_cache import PagedKVCache  # noqa: E402
 from lumen_amd.utils.image import decode_rgb, encode_jpeg  # noqa: E402
-from lumen_amd.models.vlm import ENCODE_AHEAD  # noqa: E402
+from lumen_amd.models.vlm import ENCODE_AHEAD, PreparedPrefill  # noqa: E402
 from lumen_amd.utils.jpeg import decode_image  # noqa: E402
 from tools.face_ocr_bench import synth_image  # noqa: E402
 
@@ -63,7 +63,7 @@ def main():
     kv = PagedKVCache(cfg.llm.num_layers, m.llm.Hkv, cfg.llm.head_dim, num_blocks=args.kv_blocks, device=dev,
                       dtype=torch.float8_e4m3fn if args.kv_fp8 else torch.bfloat16)
 
-    dec_ms = []
+    dec_ms, enc_ms = [], []
     # JPEG decoded with libjpeg DCT scaling down to >= the vision input (as the VLM service does,
     # services/vlm/backend.py:jpeg_draft_size); --full-decode measures the full-resolution decode
     draft = None if args.full_decode else (cfg.vision.image_size, cfg.vision.image_size)
@@ -71,9 +71,14 @@ def main():
     # as in the VLM service (services/vlm/backend.py _submit): the JPEG is decoded in the caller's
     # thread before the request is queued, so the engine thread never blocks on it; TTFT below is
     # still measured from BEFORE the decode (request arrival -> first token)
+    build_ms = []
+
     def build(a):
         ids, img = a
-        return m.build_prefill(ids, [img])
+        t = time.perf_counter()
+        x = img.x if isinstance(img, PreparedPrefill) else m.build_prefill(ids, [img])
+        build_ms.append((time.perf_counter() - t) * 1000)
+        return x
 
     def decode(jpeg):
         # as the service: baseline JPEGs -> parallel host entropy decode + GPU reconstruction
@@ -82,8 +87,17 @@ def main():
         img = torch.from_numpy(decode_rgb(jpeg, draft_to=draft)) if args.host_decode else \
             decode_image(jpeg, dev, draft_to=draft)
         dec_ms.append((time.perf_counter() - t) * 1000)
-        # as the service: the image encoder starts in the request's thread (models/vlm.py:encode_ahead)
-        return m.encode_ahead([img])[0] if ENCODE_AHEAD else img
+        return img
+
+    def prepare(ids, img):
+        # as the service: the prompt embeddings and the image encoder are queued in the request's
+        # thread (models/vlm.py:prepare_prefill) before the engine admits the request
+        if not ENCODE_AHEAD:
+            return img
+        t = time.perf_counter()
+        pre = m.prepare_prefill(ids, [img])
+        enc_ms.append((time.perf_counter() - t) * 1000)
+        return pre if pre is not None else img
 
     eng = LLMEngine(m.llm, kv, build, max_batch=max(args.batch, 1))
     rng = np.random.default_rng(0)
@@ -96,7 +110,7 @@ def main():
 
     def one(max_new):
         t_arrive = time.perf_counter()
-        r = eng.submit((ids, decode(jpeg)), len(full), SamplingParams(max_new_tokens=max_new))
+        r = eng.submit((ids, prepare(ids, decode(jpeg))), len(full), SamplingParams(max_new_tokens=max_new))
         r.t_arrive = t_arrive
         times = []
         for kind, _ in r.stream(timeout=600):
@@ -122,12 +136,14 @@ def main():
         eng.close()
         print(json.dumps({"metric": "VLM p50 TTFT", "value": float(np.percentile(ttft, 50)), "unit": "ms",
                           "admit_to_first_token": float(np.median(admit_first_ms)),
+                          "queue": float(np.median(queue_ms)), "build_host_ms": float(np.median(build_ms[-args.n:])),
+                          "encode_ahead_host_ms": float(np.median(enc_ms[-args.n:])) if enc_ms else None,
                           "jpeg_decode": float(np.median(dec_ms[:args.n])),
                           "decode_tok_s_single": float(np.median(tps)) if tps else None, "n": args.n}))
         return
     t1 = time.perf_counter()
     with ThreadPoolExecutor(max_workers=max(args.batch, 1)) as ex:
-        rs = list(ex.map(lambda _: eng.submit((ids, decode(jpeg)), len(full),
+        rs = list(ex.map(lambda _: eng.submit((ids, prepare(ids, decode(jpeg))), len(full),
                                               SamplingParams(max_new_tokens=args.batch_max_new)), range(args.batch)))
     # steady-state batched decode: per-token arrival times of every stream; the window starts
     # when the LAST request has its first token (all B in the running batch) and ends when the
