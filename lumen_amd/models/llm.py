@@ -44,13 +44,9 @@ _F8_MIN_ROWS = 33
 _FUSED_DECODE_NORM = True
 # decode: RoPE + current-token KV-cache write inside the paged attention kernel (no rope_kv launch)
 _FUSED_DECODE_ROPE = True
-# W8A8 prefill with MX (block-scaled) activations produced in the epilogues (LLM._layers_mx): 6
-# launches per layer instead of 10 -- no RMSNorm+quant and no row-quant passes.  Opt-in
-# (LUMEN_PREFILL_MX=1): on the 8B TTFT it measured 13.12 vs 12.79 ms for the per-token chain -- the
-# 4 x 32 removed launches (~0.9 ms) are paid back by the MX epilogues (o / down: bf16 + MX copy +
-# sums of squares, +4.5 us each) and the block-scale staging (+2-7 % per GEMM),
-# profiles/r4_mx_chain_ab_v1.txt
-_PREFILL_MX = os.environ.get("LUMEN_PREFILL_MX", "0") == "1"
+# (r4's fused MX prefill chain -- block-scaled activations from the epilogues, 6 launches per
+# layer -- lost its A/B to this per-token chain, 13.12 vs 12.79 ms TTFT, profiles/r4_mx_chain_ab_v1.txt,
+# and was removed in r5; the MX W8A8 chain stays for the ViT tower, models/clip.py:run_blocks_mx)
 
 
 @dataclass
@@ -339,17 +335,8 @@ class LLM(nn.Module):
         e = e.view(-1, self.cfg.hidden_size)
         return self._all_reduce(e)
 
-    def _mx_ok(self, x: torch.Tensor) -> bool:
-        """Fused MX prefill: fp8 weights with folded norms, one rank, 128-aligned widths."""
-        cfg = self.cfg
-        return (_PREFILL_MX and x.is_cuda and self._f8_ok(x.shape[0]) and self.norm_folded and not self.tp.enabled
-                and cfg.head_dim in (64, 128) and cfg.hidden_size % 128 == 0 and self.layers[0].I % 128 == 0
-                and (self.H * cfg.head_dim) % 128 == 0)
-
     def _layers(self, x: torch.Tensor, pos: torch.Tensor, slots: Optional[torch.Tensor], kv, attn_fn) -> torch.Tensor:
         """x [T, hidden] residual stream (updated in place); returns x."""
-        if self._mx_ok(x) and getattr(attn_fn, "mx", False):
-            return self._layers_mx(x, pos, slots, kv, attn_fn)
         if self._f8_ok(x.shape[0]):
             return self._layers_f8(x, pos, slots, kv, attn_fn)
         cfg = self.cfg
@@ -446,44 +433,6 @@ class LLM(nn.Module):
             x.add_(self._all_reduce(pending))
         return x
 
-    def _layers_mx(self, x, pos, slots, kv, attn_fn):
-        """W8A8 prefill with MX activations: each projection's fp8 operand (one E8M0 exponent per
-        32 values) comes out of the kernel before it, so a layer is 6 launches --
-
-          qkv GEMM (rstd row scale from the residual's sums of squares)  ->  rope_kv
-          ->  attention (MX fp8 O)  ->  o GEMM (+ residual: bf16 x, its MX copy, sums of squares)
-          ->  gate|up GEMM (rstd; SwiGLU straight to MX fp8)  ->  down GEMM (like o)
-
-        -- against 10 for _layers_f8 (RMSNorm+quant and row-quant passes between the GEMMs).  The
-        norms' gammas are folded into qkv / gate|up (fold_norms), so RMSNorm is the rstd scale the
-        consuming GEMM applies from the producer's per-(row, 128-column) sums of squares of the
-        stored bf16 residual; the first layer's operand comes from one quant_rows_mx pass."""
-        cfg = self.cfg
-        D, eps, T, Hd = cfg.head_dim, cfg.rms_eps, x.shape[0], cfg.hidden_size
-        dev = x.device
-        f8 = torch.float8_e4m3fn
-        l0 = self.layers[0]
-        u8 = torch.uint8
-        x8 = torch.empty((T, Hd), device=dev, dtype=f8)               # MX operands: fp8 values +
-        xs = torch.empty((Hd // 128, T, 4), device=dev, dtype=u8)     # E8M0 scale planes (ops.mx_planes)
-        ssq = torch.empty((T, Hd // 128), device=dev, dtype=torch.float32)
-        a8 = torch.empty((T, l0.H * D), device=dev, dtype=f8)
-        as_ = torch.empty((l0.H * D // 128, T, 4), device=dev, dtype=u8)
-        g8 = torch.empty((T, l0.I), device=dev, dtype=f8)
-        gs = torch.empty((l0.I // 128, T, 4), device=dev, dtype=u8)
-        ops.quant_rows_mx(x, x8, xs, ssq)
-        for i, l in enumerate(self.layers):
-            qkv = ops.linear_mx(x8, xs, l.qkv_w, l.qkv_s, bias=l.qkv_b, ssq_in=ssq, norm_eps=eps)
-            kc, vc = (kv.k[i], kv.v[i]) if kv is not None else (None, None)
-            lops.rope_kv(qkv, pos, self.cos_sin, l.H, l.Hkv, D, slots, kc, vc)
-            attn_fn(qkv, l, kc, vc, mx_out=(a8, as_))
-            ops.linear_mx(a8, as_, l.o_w, l.o_s, residual=x, out=x, q_out=(x8, xs), ssq_out=ssq)
-            ops.linear_mx(x8, xs, l.gu_w, l.gu_s, glu=True, ssq_in=ssq, norm_eps=eps, q_out=(g8, gs),
-                          write_out=False)
-            ops.linear_mx(g8, gs, l.down_w, l.down_s, residual=x, out=x, q_out=(x8, xs), ssq_out=ssq)
-            del qkv
-        return x
-
     def logits(self, x_rows: torch.Tensor, ssq: Optional[torch.Tensor] = None) -> torch.Tensor:
         """final norm + lm_head of rows [B, hidden] -> local-vocab fp32 logits [B, V/tp].
         With folded norms (untied head, <= 32 rows) the norm is the lm_head GEMM's rstd row
@@ -512,7 +461,7 @@ class LLM(nn.Module):
         D = self.cfg.head_dim
         S = start_pos + T
 
-        def attn(qkv, l, kc, vc, mx_out=None):
+        def attn(qkv, l, kc, vc):
             q5 = qkv.view(1, T, l.H + 2 * l.Hkv, D)
             if start_pos > 0:
                 assert prefix_blocks is not None and kc is not None, "chunked prefill needs the KV cache"
@@ -524,12 +473,8 @@ class LLM(nn.Module):
                 v_all = vb.permute(0, 3, 1, 2).reshape(1, -1, l.Hkv, D)[:, :S].contiguous()
             else:
                 k_all, v_all = q5[:, :, l.H:l.H + l.Hkv], q5[:, :, l.H + l.Hkv:]
-            if mx_out is not None:      # _layers_mx: O leaves as the o projection's MX fp8 operand
-                return ops.attention_mx(q5[:, :, :l.H], k_all, v_all, causal=True, q_out=mx_out)
             o = ops.attention(q5[:, :, :l.H], k_all, v_all, causal=True)
             return o.view(T, l.H * D)
-
-        attn.mx = True
 
         self._layers(x, pos, slots, kv, attn)
         return self.logits(x[T - 1:T])

@@ -259,7 +259,7 @@ class VLM(nn.Module):
                 self._encode_tower(static_in, B)     # warm-up: weight caches, workspaces, autotune
             cur.wait_stream(side)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):   # other threads keep launching
                 static_out = self._encode_tower(static_in, B)
             return {"g": g, "in": static_in, "out": static_out}
         except Exception as e:  # noqa: BLE001 - an op that cannot be captured: eager launches

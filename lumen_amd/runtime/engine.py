@@ -498,7 +498,9 @@ class DecodeGraphs:
             self.pool = torch.cuda.graph_pool_handle()
         # captured on the warm-up stream: the split-K tickets / workspaces the kernels key by stream
         # already exist (a first request inside the capture would record its zero-fill into every replay)
-        with torch.cuda.graph(g, pool=self.pool, stream=s):
+        # thread_local: a multi-service engine process runs other services' batch loops on other
+        # threads meanwhile; the default (global) mode would fail their HIP calls during the capture
+        with torch.cuda.graph(g, pool=self.pool, stream=s, capture_error_mode="thread_local"):
             out = run()
         pin = lambda t: torch.empty(t.shape, dtype=t.dtype).pin_memory()  # noqa: E731
         ent = {"g": g, "st": st, "dbuf": dbuf, "out": out, "ws": ws, "res": res, "lay": lay, "Bp": Bp, "W": W,

@@ -61,6 +61,10 @@ class LabelBank:
         self.n_local = emb.shape[0]
         self.device = device
         dt = torch.bfloat16 if device.type == "cuda" else torch.float32
+        if device.type == "cuda" and self.n_local % 16:
+            # the score GEMM tiles N in 16s: zero rows pad the bank, their scores are cut off
+            # before the top-k (ImageNet's 1000 classes, a shard's remainder)
+            emb = torch.cat([emb, emb.new_zeros(16 - self.n_local % 16, emb.shape[1])])
         self.bank = emb.to(device=device, dtype=dt).contiguous()
 
     @torch.no_grad()
@@ -71,6 +75,8 @@ class LabelBank:
         kl = min(k, self.n_local) if self.n_local > 0 else 0
         if kl > 0:
             s = ops.bank_scores(q, self.bank)
+            if s.shape[1] != self.n_local:
+                s = s[:, :self.n_local].contiguous()
             v, i, lse = ops.row_topk(s, kl, scale=scale, with_lse=softmax, index_offset=self.offset)
         else:
             B = q.shape[0]

@@ -282,3 +282,24 @@ def test_gemm_bf16_few_rows_deep_k_vs_fp32(M, N, K):
     ref = ops.linear(x.float(), w.float(), b)
     got = ops.linear(x.to(DEV), w.to(DEV), b.to(DEV), out_dtype=torch.float32)
     assert got.dtype == torch.float32 and _rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("n", [40, 1000, 37])
+def test_label_bank_any_label_count(n):
+    """Label banks of any size on the GPU (the score GEMM tiles N in 16s: the bank is zero-padded
+    and the padded scores cut before the top-k) == the fp32 reference top-k."""
+    import numpy as np
+
+    from lumen_amd.runtime.label_bank import LabelBank
+
+    rng = np.random.default_rng(n)
+    emb = rng.standard_normal((n, 768)).astype(np.float32)
+    q = rng.standard_normal((3, 768)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    bank = LabelBank(emb, torch.device(DEV))
+    p, idx = bank.topk(q, 5, scale=100.0, softmax=True)
+    ref = q @ (emb / np.linalg.norm(emb, axis=1, keepdims=True)).T
+    want = np.argsort(-ref, axis=1)[:, :5]
+    assert np.asarray(idx).shape == (3, 5)
+    assert (np.asarray(idx) < n).all()
+    assert (np.asarray(idx)[:, 0] == want[:, 0]).all()

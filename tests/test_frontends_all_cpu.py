@@ -102,13 +102,13 @@ def _cos(a, b):
     return float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
 
 
-def _same(task, got, ref):
+def _same(task, got, ref, score_atol=1e-4):
     if "vector" in ref:
         assert _cos(got["vector"], ref["vector"]) > 0.9999, task
     elif "labels" in ref:
         assert [x["label"] for x in got["labels"]] == [x["label"] for x in ref["labels"]], task
         np.testing.assert_allclose([x["score"] for x in got["labels"]], [x["score"] for x in ref["labels"]],
-                                   atol=1e-4)
+                                   atol=score_atol)
     elif "faces" in ref:
         assert got["count"] == ref["count"] > 0, task
         for fa, fb in zip(got["faces"], ref["faces"]):
@@ -135,7 +135,7 @@ def _reference(cfg_dict, tasks=None):
         server.stop(0)
 
 
-def _serve(tmp_path, cfg_dict, nfe, tasks, monkeypatch, exclude=""):
+def _serve(tmp_path, cfg_dict, nfe, tasks, monkeypatch, exclude="", devices=("cpu",)):
     from lumen_amd.hub.server import serve_frontends
 
     cfg_path = tmp_path / "cfg.yaml"
@@ -145,7 +145,7 @@ def _serve(tmp_path, cfg_dict, nfe, tasks, monkeypatch, exclude=""):
     ready = mp.get_context("spawn").Queue()
     started = []
     th = threading.Thread(target=lambda: started.append(serve_frontends(
-        str(cfg_path), cfg_dict["server"]["port"], nfe, stop_event=stop, ready_q=ready, devices=["cpu"])))
+        str(cfg_path), cfg_dict["server"]["port"], nfe, stop_event=stop, ready_q=ready, devices=list(devices))))
     th.start()
     try:
         for _ in range(nfe):

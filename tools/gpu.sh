@@ -31,10 +31,12 @@
 #   ttft           VLM TTFT only (8B fp8, 30 requests, device JPEG decode)
 #   mx_cold        cold-weight timing of the MX chain's GEMMs (full / plain epilogues) vs per-token fp8
 #   pp_cold        ping-pong 128x128 pipeline forms vs the aligned ones (fp8 prefill + bf16 vision shapes)
-#   ttft_ab        TTFT with the fused MX prefill chain (LUMEN_PREFILL_MX=1) vs the per-token-scale chain
 #   f8auto         fp8 tests + cold prefill GEMMs (auto vs codes 1, 2, 16, 17)
 #   vlm_tests      VLM / engine GPU tests + GPU entropy JPEG tests
 #   acc            full-size fp8 accuracy pins (ViT-L/14-336 W8A8, Llama-3-8B first token)
+#   vlm_service    service-level TTFT: gRPC vlm_generate_stream first chunk (tools/vlm_service_ttft.py)
+#   serve128       CLIP serving through 8 front ends, 128 clients from 6 client processes
+#   fe_gpu         engine / front-end topology GPU test (tests/test_frontends_gpu.py)
 #   pmc_gemm       PMC counters (MFMA, LDS conflicts, busy) of one ViT-L/14 GEMM shape
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -157,15 +159,17 @@ for task in "$@"; do
     pp_cold)   # ping-pong 128x128 forms (codes 12-15) vs the barrier-aligned ones, cold weights
       step pp_cold_f8 300 python -u tools/cold_gemm_bench.py --what prefill --variants=1,2,12,13,14,15
       step pp_cold_vit 300 python -u tools/cold_gemm_bench.py --what vit --variants=-1,20003,20022,20023,20024,20025 ;;
-    ttft_ab)
-      step ttft_mx 400 env LUMEN_PREFILL_MX=1 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0
-      step ttft_pt 400 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0 ;;
     f8auto)   # fp8 tests + cold-weight prefill GEMMs: auto selection vs the split-K / 256x256 ping-pong forms
       step f8_tests 400 python -u -m pytest tests/test_fp8_gpu.py -x -q --timeout 120 --timeout-method thread
       step f8_cold 300 python -u tools/cold_gemm_bench.py --what prefill --variants=0,1,2,16,17 ;;
     vlm_tests) step vlm_tests 400 python -u -m pytest tests/test_vlm_gpu.py tests/test_jpeg_gpu_entropy_gpu.py -x -q \
       --timeout 200 --timeout-method thread ;;
     acc) step acc 400 python -u -m pytest tests/test_fp8_accuracy_gpu.py -x -v --timeout 300 --timeout-method thread ;;
+    vlm_service) step vlm_service 500 python -u tools/vlm_service_ttft.py --n 30 ;;
+    serve128)   # CLIP through front ends, 128 clients from 6 client processes
+      step serve128 400 python -u tools/serve_bench.py --service clip --model CLIP-ViT-L-14 --device cuda \
+        --clients 128 --frontends "${SERVE_FE:-8}" --client-procs 6 --seconds 20 ;;
+    fe_gpu) step fe_gpu 400 python -u -m pytest tests/test_frontends_gpu.py -x -q --timeout 300 --timeout-method thread ;;
     ttft) step ttft 400 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0 ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac

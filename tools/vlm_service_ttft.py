@@ -1,0 +1,88 @@
+"""Service-level VLM time to first token: the hub's gRPC ``vlm_generate_stream`` task end to end
+(JPEG bytes in the request -> first streamed chunk at the client), the way a Lumen client sees it,
+next to tools/vlm_bench.py's engine-API TTFT.  Synthetic LLaVA-Llama-3-8B pack (random-init
+weights on the device, byte-level tokenizer), fp8 decoder (LUMEN_VLM_FP8=1), one GPU.
+
+    python tools/vlm_service_ttft.py [--n 30] [--warmup 3] [--prompt-chars 40]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--prompt-chars", type=int, default=40)
+    ap.add_argument("--max-new", type=int, default=8)
+    ap.add_argument("--fp8", type=int, default=1)
+    a = ap.parse_args()
+    if a.fp8:
+        os.environ["LUMEN_VLM_FP8"] = "1"
+    import grpc
+
+    from lumen_amd.hub.router import HubRouter
+    from lumen_amd.hub.server import AppService, build_server
+    from lumen_amd.models.vlm import write_vlm_model
+    from lumen_amd.proto import ml_service as pb
+    from lumen_amd.resources.validator import config_from_dict
+    from lumen_amd.utils.image import encode_jpeg
+    from tools.vlm_bench import synth_image
+
+    cache = tempfile.mkdtemp(prefix="lumen-vlm-ttft-")
+    write_vlm_model(os.path.join(cache, "models", "llava-llama3-8b"), "llava-llama3-8b")
+    svc = {"enabled": True, "package": "lumen_vlm",
+           "import_info": {"registry_class": "lumen_vlm.fastvlm.GeneralFastVLMService",
+                           "add_to_server": "lumen_vlm.proto.ml_service_pb2_grpc.add_InferenceServicer_to_server"},
+           "backend_settings": {"device": "cuda", "batch_size": 8},
+           "models": {"general": {"model": "llava-llama3-8b", "runtime": "onnx"}}}
+    cfg = {"metadata": {"version": "1.0.0", "region": "other", "cache_dir": cache},
+           "deployment": {"mode": "hub", "services": ["vlm"]},
+           "server": {"port": 0, "host": "127.0.0.1"}, "services": {"vlm": svc}}
+    t0 = time.time()
+    app = AppService.from_app_config(config_from_dict(cfg))
+    server, port = build_server(HubRouter(app.services), "127.0.0.1", 0)
+    server.start()
+    load_s = time.time() - t0
+    jpeg = encode_jpeg(synth_image(np.random.default_rng(0), 768, 1024, "photo"))
+    prompt = ("Describe the picture " * 8)[:a.prompt_chars]
+    meta = {"prompt": prompt, "max_new_tokens": str(a.max_new)}
+    ttft, total, chunks = [], [], []
+    with grpc.insecure_channel(f"127.0.0.1:{port}") as ch:
+        stub = pb.InferenceStub(ch)
+        for i in range(a.warmup + a.n):
+            t = time.perf_counter()
+            first, n = None, 0
+            for r in stub.Infer(iter([pb.InferRequest(correlation_id=str(i), task="vlm_generate_stream", payload=jpeg,
+                                                      payload_mime="image/jpeg", meta=meta)]), timeout=300):
+                if r.HasField("error"):
+                    raise RuntimeError(r.error.message)
+                if first is None:
+                    first = time.perf_counter()
+                n += 1
+            if i >= a.warmup:
+                ttft.append((first - t) * 1e3)
+                total.append((time.perf_counter() - t) * 1e3)
+                chunks.append(n)
+    server.stop(0)
+    app.close()
+    print(json.dumps({"metric": "VLM p50 TTFT (service: gRPC vlm_generate_stream, first chunk)",
+                      "value": round(float(np.percentile(ttft, 50)), 3), "unit": "ms",
+                      "p99_ms": round(float(np.percentile(ttft, 99)), 3),
+                      "request_ms_p50": round(float(np.percentile(total, 50)), 3),
+                      "chunks_per_request": float(np.median(chunks)), "n": a.n, "load_s": round(load_s, 1),
+                      "config": {"model": "LLaVA-Llama-3-8B (synthetic pack, random-init weights)",
+                                 "decoder": "fp8" if a.fp8 else "bf16", "image": f"1024x768 JPEG {len(jpeg) // 1024} KiB",
+                                 "prompt_chars": a.prompt_chars, "max_new_tokens": a.max_new}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
