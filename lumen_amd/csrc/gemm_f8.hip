@@ -584,7 +584,8 @@ hipError_t gemm_f8pp(const uint8_t* A, int64_t lda, const float* sa, const uint8
                      void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, int splits, hipStream_t stream);
 // intra-workgroup split-K form (csrc/gemm_f8ks.hip)
 hipError_t gemm_f8ks(const uint8_t* A, int64_t lda, const float* sa, const uint8_t* W, int64_t ldw, const float* sw,
-                     void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, hipStream_t stream);
+                     void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, hipStream_t stream,
+                     int stream_k = -1);
 
 // ---------------------------------------------------------------------------- split-K
 // Mid-size GEMMs whose 128x128 tile count leaves CUs idle (LLaVA vision tower at 577 tokens:
@@ -703,9 +704,10 @@ static hipError_t launch_variant(int v, const uint8_t* A, int64_t lda, const flo
     }
     v = 2;
   }
-  if (v == 16) {               // intra-workgroup split-K (fp8 only; its own plain epilogues)
+  if (v == 16 || v == 18) {    // intra-workgroup split-K (fp8 only; its own plain epilogues); 18: + Stream-K
     if constexpr (F8) {
-      if (ep.split_koff == 0 && S == 1) return gemm_f8ks(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream);
+      if (ep.split_koff == 0 && S == 1)
+        return gemm_f8ks(A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, stream, v == 18 ? 1 : 0);
     }
     v = 2;
   }

@@ -367,7 +367,7 @@ void gemm_f8(const at::Tensor& a8, const at::Tensor& sa, const at::Tensor& w8, c
   check_f8_rows(w8, "gemm_f8: w8");
   const int64_t M = a8.size(0), K = a8.size(1), N = w8.size(0);
   TORCH_CHECK(w8.size(1) == K && K % 128 == 0 && N % 16 == 0, "gemm_f8: K % 128 == 0, N % 16 == 0");
-  TORCH_CHECK(variant >= 0 && variant <= 17, "gemm_f8: variant 0..17");
+  TORCH_CHECK(variant >= 0 && variant <= 18, "gemm_f8: variant 0..18");
   TORCH_CHECK(sa.is_cuda() && sa.scalar_type() == at::kFloat && sa.numel() >= M && sa.is_contiguous(),
               "gemm_f8: sa f32 [M]");
   TORCH_CHECK(sw.is_cuda() && sw.scalar_type() == at::kFloat && sw.numel() == N && sw.is_contiguous(),

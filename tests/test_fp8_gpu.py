@@ -176,10 +176,12 @@ def test_gemm_f8_pipeline_variants(M, N, K, splits, variant):
 @pytest.mark.parametrize("M,N,K", [(624, 6144, 4096), (624, 4096, 14336), (130, 1040, 128), (200, 512, 256),
                                    (333, 768, 384), (624, 1024, 1152), (64, 256, 1024)])
 @pytest.mark.parametrize("epi", ["bf16_bias_res", "f32_bias", "glu", "plain"])
-@pytest.mark.parametrize("variant", [16, 17])
+@pytest.mark.parametrize("variant", [16, 17, 18])
 def test_gemm_f8_intra_wg_splitk(M, N, K, epi, variant):
     """Intra-workgroup split-K fp8 GEMM (variant 16, csrc/gemm_f8ks.hip: both wave groups' K
-    halves, odd and even K-step counts, one K-step) and the 256 x 256 ping-pong fp8 GEMM (variant 17,
+    halves, odd and even K-step counts, one K-step), its Stream-K form (variant 18: one workgroup per
+    CU over the (tile, K-step) sequence, tiles finished by their last segment from the others' fp32
+    partials; 64 x 256 x 1024 puts 8 workgroups on one tile) and the 256 x 256 ping-pong fp8 GEMM (variant 17,
     csrc/gemm_f8pp.hip: peeled last K-tiles, automatic split-K with fp32 slabs for narrow grids):
     ragged M, the fast epilogue (bf16 bias, residual, SwiGLU) and the generic one (fp32 bias)
     against the fp32 reference; repeat launches are bitwise identical."""
@@ -209,10 +211,9 @@ def test_gemm_f8_intra_wg_splitk(M, N, K, epi, variant):
 @pytest.mark.parametrize("M,N,glu,resid", [(624, 28672, True, False), (624, 22016 + 4096, False, True),
                                            (300, 36864, True, False)])
 def test_gemm_f8_auto_prefill_split_columns(M, N, glu, resid):
-    """Auto selection at prefill sizes: a multi-round grid runs whole rounds of 256 x 256 tiles
-    (code 17) and the remaining columns on the 128 x 128 split-K form (code 16) with every per-column
-    operand (weight scale, bias, residual, SwiGLU output column) shifted; same result as the fp32
-    reference."""
+    """Auto selection at prefill sizes (multi-round grids on the 256 x 256 ping-pong, code 17;
+    single-round ones on the 128 x 128 split-K form, Stream-K when a quarter of the CUs would idle):
+    same result as the fp32 reference with bias / residual / SwiGLU epilogues."""
     K = 1024
     g, x8, xs, w8, ws = _f8_operands(M, N, K, N + M)
     b = torch.randn(N, generator=g).bfloat16()

@@ -102,7 +102,7 @@ def _cos(a, b):
     return float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
 
 
-def _same(task, got, ref, score_atol=1e-4):
+def _same(task, got, ref, score_atol=1e-4, box_atol=1e-3, emb_cos=0.9999):
     if "vector" in ref:
         assert _cos(got["vector"], ref["vector"]) > 0.9999, task
     elif "labels" in ref:
@@ -112,8 +112,8 @@ def _same(task, got, ref, score_atol=1e-4):
     elif "faces" in ref:
         assert got["count"] == ref["count"] > 0, task
         for fa, fb in zip(got["faces"], ref["faces"]):
-            np.testing.assert_allclose(fa["bbox"], fb["bbox"], atol=1e-3)
-            assert _cos(fa["embedding"], fb["embedding"]) > 0.9999
+            np.testing.assert_allclose(fa["bbox"], fb["bbox"], atol=box_atol)
+            assert _cos(fa["embedding"], fb["embedding"]) > emb_cos
     elif "items" in ref:
         assert got["count"] == ref["count"], task
         assert [i["text"] for i in got["items"]] == [i["text"] for i in ref["items"]], task

@@ -37,6 +37,7 @@
 #   vlm_service    service-level TTFT: gRPC vlm_generate_stream first chunk (tools/vlm_service_ttft.py)
 #   serve128       CLIP serving through 8 front ends, 128 clients from 6 client processes
 #   fe_gpu         engine / front-end topology GPU test (tests/test_frontends_gpu.py)
+#   shrink         rocpd databases under gpurun_out -> kernel-stats / PMC text, databases > 4 MB removed (64 MiB copy-back cap)
 #   pmc_gemm       PMC counters (MFMA, LDS conflicts, busy) of one ViT-L/14 GEMM shape
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -170,6 +171,13 @@ for task in "$@"; do
       step serve128 400 python -u tools/serve_bench.py --service clip --model CLIP-ViT-L-14 --device cuda \
         --clients 128 --frontends "${SERVE_FE:-8}" --client-procs 6 --seconds 20 ;;
     fe_gpu) step fe_gpu 400 python -u -m pytest tests/test_frontends_gpu.py -x -q --timeout 300 --timeout-method thread ;;
+    shrink)   # summarise every rocpd database under gpurun_out (kernel stats, PMC sums), drop the big ones
+      for db in $(find gpurun_out -name "*.db" -size +4M); do
+        python tools/rocpd_stats.py "$db" "${db%.db}_stats.csv" --top 60 > "${db%.db}_stats.txt" 2>&1 || true
+        python tools/rocpd_stats.py "$db" --pmc > "${db%.db}_pmc.txt" 2>&1 || true
+        rm -f "$db"
+      done
+      echo "[shrink] done" ;;
     ttft) step ttft 400 python -u tools/vlm_bench.py --preset llava-llama3-8b --fp8 --n 30 --batch 0 ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac

@@ -37,6 +37,11 @@ def main():
     from lumen_amd.utils.image import encode_jpeg
     from tools.vlm_bench import synth_image
 
+    import socket
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        free_port = so.getsockname()[1]
     cache = tempfile.mkdtemp(prefix="lumen-vlm-ttft-")
     write_vlm_model(os.path.join(cache, "models", "llava-llama3-8b"), "llava-llama3-8b")
     svc = {"enabled": True, "package": "lumen_vlm",
@@ -46,7 +51,7 @@ def main():
            "models": {"general": {"model": "llava-llama3-8b", "runtime": "onnx"}}}
     cfg = {"metadata": {"version": "1.0.0", "region": "other", "cache_dir": cache},
            "deployment": {"mode": "hub", "services": ["vlm"]},
-           "server": {"port": 0, "host": "127.0.0.1"}, "services": {"vlm": svc}}
+           "server": {"port": free_port, "host": "127.0.0.1"}, "services": {"vlm": svc}}
     t0 = time.time()
     app = AppService.from_app_config(config_from_dict(cfg))
     server, port = build_server(HubRouter(app.services), "127.0.0.1", 0)
