@@ -37,6 +37,7 @@
 #   vlm_service    service-level TTFT: gRPC vlm_generate_stream first chunk (tools/vlm_service_ttft.py)
 #   serve128       CLIP serving through 8 front ends, 128 clients from 6 client processes
 #   fe_gpu         engine / front-end topology GPU test (tests/test_frontends_gpu.py)
+#   face_real      face bench on the detector's real output (detect_and_embed_images; SPMD path under torchrun)
 #   shrink         rocpd databases under gpurun_out -> kernel-stats / PMC text, databases > 4 MB removed (64 MiB copy-back cap)
 #   pmc_gemm       PMC counters (MFMA, LDS conflicts, busy) of one ViT-L/14 GEMM shape
 set -o pipefail
@@ -166,11 +167,12 @@ for task in "$@"; do
     vlm_tests) step vlm_tests 400 python -u -m pytest tests/test_vlm_gpu.py tests/test_jpeg_gpu_entropy_gpu.py -x -q \
       --timeout 200 --timeout-method thread ;;
     acc) step acc 400 python -u -m pytest tests/test_fp8_accuracy_gpu.py -x -v --timeout 300 --timeout-method thread ;;
-    vlm_service) step vlm_service 500 python -u tools/vlm_service_ttft.py --n 30 ;;
+    vlm_service) step vlm_service 500 python -u tools/vlm_service_ttft.py --n 30 --max-new 1 ;;
     serve128)   # CLIP through front ends, 128 clients from 6 client processes
       step serve128 400 python -u tools/serve_bench.py --service clip --model CLIP-ViT-L-14 --device cuda \
         --clients 128 --frontends "${SERVE_FE:-8}" --client-procs 6 --seconds 20 ;;
     fe_gpu) step fe_gpu 400 python -u -m pytest tests/test_frontends_gpu.py -x -q --timeout 300 --timeout-method thread ;;
+    face_real) step face_real 300 python -u tools/face_ocr_bench.py --what face --real-dets --iters 5 ;;
     shrink)   # summarise every rocpd database under gpurun_out (kernel stats, PMC sums), drop the big ones
       for db in $(find gpurun_out -name "*.db" -size +4M); do
         python tools/rocpd_stats.py "$db" "${db%.db}_stats.csv" --top 60 > "${db%.db}_stats.txt" 2>&1 || true
