@@ -180,6 +180,19 @@ __device__ __forceinline__ int swz(int row, int chunk) {
   return (row << 7) + (((chunk ^ ((row >> 1) & 7))) << 4);
 }
 
+// Direct-store ping-pong kernels (gemm_pp.hip, DS): the MFMA takes W as its first operand, so a lane's
+// accumulator holds 4 consecutive OUTPUT COLUMNS of one row, and the B fragment of 16x16 block j holds
+// W rows 8 * (f >> 2) + 4 * j + (f & 3) (f = lane & 15): blocks j = 0, 1 together give each lane 8
+// consecutive columns -> one 16-byte store, no LDS round trip in the epilogue.  Those fragment rows
+// ({0-3, 8-11, 16-19, 24-27} + 4j) hit 2-way bank conflicts under swz's XOR of row bits 1..3; this
+// XOR of row bits 1, 3, 4 (searched exhaustively over linear XOR maps) keeps every ds_read_b128 lane
+// group on 16 distinct bank slots.  Applied to the B half-tiles only (DMA source chunk and read).
+__device__ __forceinline__ int ds_bxor(int row) {
+  const int x = row >> 1;
+  return (x & 1) ^ (((x >> 2) & 1) << 1) ^ (((x >> 3) & 1) << 2);
+}
+__device__ __forceinline__ int swzb(int row, int chunk) { return (row << 7) + ((chunk ^ ds_bxor(row)) << 4); }
+
 __device__ __forceinline__ void add8(float* v, const uint16_t* p) {
   float f[8];
   unpack8(*(const u32x4_t*)p, f);

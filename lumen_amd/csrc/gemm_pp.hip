@@ -35,6 +35,82 @@ __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// Direct-store epilogue (DS kernels): the lane holds row m0 + qm*128 + wm*64 + i*16 + (lane & 15),
+// columns n0 + qn*128 + wn*32 + 8*(lane >> 4) + [0, 8) in acc[qm][qn][i][0..1][0..3]; 16 passes of one
+// 16-byte store each.  Bias / residual / LN-fold operands are loaded up front (residual RD passes ahead).
+template <bool WT, int FK>
+__device__ __forceinline__ void pp_epilogue_direct(const f32x4_t (&acc)[2][2][4][2], int m0, int n0, int M, int N,
+                                                   void* __restrict__ C, int64_t ldc, const GemmEpi& ep, int wm,
+                                                   int wn, int lane) {
+  constexpr bool FL = FK == 5;
+  constexpr bool fast = FK > 0 && !FL;
+  constexpr bool FB = fast && ((FK - 1) & 1), FR = fast && ((FK - 1) & 2);
+  constexpr int RD = LUMEN_GEMM_RES_PREFETCH;
+  const __amdgpu_buffer_rsrc_t crs = c_rsrc(C);
+  const int fr = lane & 15, fc = lane >> 4;
+  auto col_of = [&](int qn) { return n0 + qn * 128 + wn * 32 + fc * 8; };
+  auto row_of = [&](int p) { return m0 + (p >> 3) * 128 + wm * 64 + ((p >> 1) & 3) * 16 + fr; };
+  u32x4_t bq[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+  u32x4_t rz[RD];
+  if constexpr (FB) {
+    bq[0] = *(const u32x4_t*)((const uint16_t*)ep.bias + col_of(0));
+    bq[1] = *(const u32x4_t*)((const uint16_t*)ep.bias + col_of(1));
+  }
+  if constexpr (FR) {
+#pragma unroll
+    for (int p = 0; p < RD; ++p) rz[p] = *(const u32x4_t*)(ep.residual + (int64_t)row_of(p) * ep.ldr + col_of(p & 1));
+  }
+  float lcs[FL ? 16 : 1], lcb[FL ? 16 : 1], lrs[FL ? 8 : 1], lro[FL ? 8 : 1];
+  if constexpr (FL) {
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4_t a = *(const f32x4_t*)(ep.col_aff + col_of(qn) + 4 * h);
+        const f32x4_t b = *(const f32x4_t*)(ep.col_aff + N + col_of(qn) + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          lcs[qn * 8 + 4 * h + e] = a[e];
+          lcb[qn * 8 + 4 * h + e] = b[e];
+        }
+      }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int64_t m = row_of(2 * r);
+      lrs[r] = ep.row_aff[2 * m];
+      lro[r] = ep.row_aff[2 * m + 1];
+    }
+  }
+  Unroll<0, 16>::run([&](const int p) __attribute__((always_inline)) {
+    const int qm = p >> 3, i = (p >> 1) & 3, qn = p & 1;
+    float v[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[r] = acc[qm][qn][i][0][r];
+      v[4 + r] = acc[qm][qn][i][1][r];
+    }
+    const int m = row_of(p), n = col_of(qn);
+    if constexpr (FL) {
+      epi_store_lnf<WT, 8>(v, m, n, C, ldc, ep, lrs[p >> 1], lro[p >> 1], lcs + qn * 8, lcb + qn * 8, crs);
+    } else if constexpr (fast) {
+      float f[8];
+      unpack8(bq[qn], f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = v[q] * ep.alpha + f[q];
+      if (ep.act) apply_act_n<8>(v, ep.act);
+      if constexpr (FR) {
+        unpack8(rz[p % RD], f);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] += f[q];
+        if (p + RD < 16) rz[p % RD] = *(const u32x4_t*)(ep.residual + (int64_t)row_of(p + RD) * ep.ldr + col_of((p + RD) & 1));
+      }
+      st16<WT>(C, crs, ((int64_t)m * ldc + n) * 2, pack8(v));
+    } else {
+      epi_store8_t<WT>(v, m, n, M, N, C, ldc, ep, crs);
+    }
+  });
+}
+
 template <int N>
 __device__ __forceinline__ void vm_wait_n() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -45,11 +121,14 @@ __device__ __forceinline__ void vm_wait_n() {
 
 // NPH: phases per K-tile (4 or 2).  PRIO 0: s_setprio(1) around every MFMA cluster;
 // PRIO 1: static priority 1 for the lagging group (MI355X_MICROARCH "Two waves per SIMD" 4).
-template <bool WT, int FK, int PRIO, int NPH>
+// DS: direct-store epilogue (gemm_epi.h swzb): transposed accumulators, 16-byte stores straight
+// from registers, no LDS staging (no SwiGLU).
+template <bool WT, int FK, int PRIO, int NPH, bool DS = false>
 __global__ void __launch_bounds__(512)
 gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                void* __restrict__ C, int64_t ldc, int M, int N, int K, GemmEpi ep, int group_m) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int64_t t_start = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -74,11 +153,12 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     const int g = 2 * wid + i;
     const int r = g * 8 + (lane >> 3);
     const int c = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+    const int cb = DS ? ((lane & 7) ^ ds_bxor(r)) * 8 : c;
     dst[i] = g * 1024;
     src[0][i] = A + (int64_t)min(m0 + r, M - 1) * lda + c;
     src[3][i] = A + (int64_t)min(m0 + 128 + r, M - 1) * lda + c;
-    src[1][i] = W + (int64_t)min(n0 + r, N - 1) * ldw + c;
-    src[2][i] = W + (int64_t)min(n0 + 128 + r, N - 1) * ldw + c;
+    src[1][i] = W + (int64_t)min(n0 + r, N - 1) * ldw + cb;
+    src[2][i] = W + (int64_t)min(n0 + 128 + r, N - 1) * ldw + cb;
   }
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   typedef const __attribute__((address_space(1))) void* g_ptr_t;
@@ -113,14 +193,17 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s)
-        fb[slot][j][s] = *(const bf16x8_t*)(base + G_OP + qn * G_HALF + swz(wn * 32 + j * 16 + frow, s * 4 + fq));
+        fb[slot][j][s] = *(const bf16x8_t*)(base + G_OP + qn * G_HALF +
+                                             (DS ? swzb(wn * 32 + 8 * (frow >> 2) + 4 * j + (frow & 3), s * 4 + fq)
+                                                 : swz(wn * 32 + j * 16 + frow, s * 4 + fq)));
   };
 
 #define LUMEN_PP_CLUSTER(QM, QN, SLOT)                                                                          \
   Unroll<0, 4>::run([&](const int i) {                                                                        \
     _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                              \
     _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                              \
-      acc[QM][QN][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[SLOT][j][s], acc[QM][QN][i][j], 0, 0, 0); \
+      acc[QM][QN][i][j] = DS ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[SLOT][j][s], fa[i][s], acc[QM][QN][i][j], 0, 0, 0) \
+                             : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[SLOT][j][s], acc[QM][QN][i][j], 0, 0, 0); \
   });
 #define LUMEN_PP_SYNC_IN()                                                                                      \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                           \
@@ -161,6 +244,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     }
   }
   pp_barrier();
+  const int64_t t_pro = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
   if (wm == 1) pp_barrier();   // the stagger
   if constexpr (PRIO == 1) { if (wm == 1) __builtin_amdgcn_s_setprio(1); }
 
@@ -238,7 +322,11 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
 #undef LUMEN_PP_SYNC_OUT
   if constexpr (PRIO == 1) { if (wm == 1) __builtin_amdgcn_s_setprio(0); }
   if (wm == 0) pp_barrier();   // re-align the groups: every LDS read of the K loop is done
+  const int64_t t_loop = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
 
+  if constexpr (DS) {
+    pp_epilogue_direct<WT, FK>(acc, m0, n0, M, N, C, ldc, ep, wm, wn, lane);
+  } else {
   // ---- epilogue: per-wave 16-row slabs through LDS (bias / residual prefetched on the FAST path)
   constexpr int LDSTR = 68;
   float* es = (float*)smem + wid * 16 * LDSTR;
@@ -316,29 +404,39 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       epi_store16_t<WT>(v, m, ncol, M, N, C, ldc, ep, crs);
     }
   });
+  }
+  if (ep.dbg && tid == 0) {   // profiling (tools/gemm_timeline.py): wave 0's view of the tile
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int64_t* d = ep.dbg + 4 * (int64_t)blockIdx.x;
+    d[0] = t_start; d[1] = t_pro; d[2] = t_loop; d[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  }
 }
 
-template <bool WT, int FK, int PRIO, int NPH>
+template <bool WT, int FK, int PRIO, int NPH, bool DS = false>
 static void launch_pp_t(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
                         int N, int K, const GemmEpi& ep, int group_m, hipStream_t stream, int splits = 1) {
   const dim3 tiles(((M + 255) / 256) * ((N + 255) / 256), splits);
   const size_t lds = 2 * G_BUF;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm_pp_kernel<WT, FK, PRIO, NPH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipFuncSetAttribute((const void*)gemm_pp_kernel<WT, FK, PRIO, NPH, DS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<WT, FK, PRIO, NPH>), dim3(tiles), dim3(512), lds, stream, A, lda, W, ldw, C, ldc,
-                     M, N, K, ep, group_m);
+  hipLaunchKernelGGL((gemm_pp_kernel<WT, FK, PRIO, NPH, DS>), dim3(tiles), dim3(512), lds, stream, A, lda, W, ldw, C,
+                     ldc, M, N, K, ep, group_m);
 }
 
 template <int FK>
 static void launch_pp_fk(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
-                         int N, int K, const GemmEpi& ep, int group_m, bool wt, bool prio1, bool two,
+                         int N, int K, const GemmEpi& ep, int group_m, bool wt, bool prio1, bool two, bool ds,
                          hipStream_t stream) {
   // write-through stores measured slower on every shape (profiles/r2_gemm_pp_v1.jsonl): not instantiated
   (void)wt;
+  if (ds) {   // direct-store epilogue: the production two-phase, static-priority form only
+    launch_pp_t<false, FK, 1, 2, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
+    return;
+  }
   if (two) {
     if (prio1) launch_pp_t<false, FK, 1, 2>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
     else launch_pp_t<false, FK, 0, 2>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
@@ -373,7 +471,7 @@ constexpr int PPS_STR = 36;                       // epilogue staging row stride
 constexpr int PPS_WAVE = 16 * PPS_STR * 4;        // bytes per wave
 constexpr int PPS_LDS = 2 * G_BUF + 8 * PPS_WAVE;
 
-template <int FK, int PRIO>
+template <int FK, int PRIO, bool DS = false>
 __global__ void __launch_bounds__(512)
 gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                 void* __restrict__ C, int64_t ldc, int M, int N, int K, GemmEpi ep, int group_m) {
@@ -398,11 +496,12 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
     const int g = 2 * wid + i;
     const int r = g * 8 + (lane >> 3);
     const int c = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+    const int cb = DS ? ((lane & 7) ^ ds_bxor(r)) * 8 : c;
     dst[i] = g * 1024;
     off[0][i] = r * (int)lda + c;
     off[3][i] = (128 + r) * (int)lda + c;
-    off[1][i] = r * (int)ldw + c;
-    off[2][i] = (128 + r) * (int)ldw + c;
+    off[1][i] = r * (int)ldw + cb;
+    off[2][i] = (128 + r) * (int)ldw + cb;
   }
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   typedef const __attribute__((address_space(1))) void* g_ptr_t;
@@ -440,15 +539,18 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s)
-        fb[qn][j][s] = *(const bf16x8_t*)(base + G_OP + qn * G_HALF + swz(wn * 32 + j * 16 + frow, s * 4 + fq));
+        fb[qn][j][s] = *(const bf16x8_t*)(base + G_OP + qn * G_HALF +
+                                           (DS ? swzb(wn * 32 + 8 * (frow >> 2) + 4 * j + (frow & 3), s * 4 + fq)
+                                               : swz(wn * 32 + j * 16 + frow, s * 4 + fq)));
   };
 
   constexpr bool FL = FK == 5;   // LN-folded row / column affine, no residual
   constexpr bool fast = FK > 0 && !FL;
   constexpr bool FB = fast && ((FK - 1) & 1), FR = fast && ((FK - 1) & 2);
   // VMEM ops of one epilogue (0: unknown): 16 stores (+ bias / residual loads; LN-folded: 8 column
-  // vectors + 16 row scalars)
-  constexpr int E = FL ? 16 + 8 + 16 : fast ? 16 + (FB ? 2 : 0) + (FR ? 16 : 0) : 0;
+  // vectors + 16 row scalars).  DS: only its 16 stores can still be in flight at the next wait (every
+  // load of the epilogue feeds a store), and an under-stated count only waits longer.
+  constexpr int E = DS ? ((FL || fast) ? 16 : 0) : FL ? 16 + 8 + 16 : fast ? 16 + (FB ? 2 : 0) + (FR ? 16 : 0) : 0;
 
   int m0, n0, kb, ke;
   seg_info(0, m0, n0, kb, ke);
@@ -470,6 +572,7 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
   int T = 0;       // global K-tile counter (LDS buffer parity)
   int after = 0;   // 0: none, 1: a C epilogue since the previous staging
   for (int sg = 0; sg < S; ++sg) {
+    const int64_t t_seg = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
     const bool has_next = sg + 1 < S;
     int nm0 = m0, nn0 = n0, nkb = 0, nke = 0;
     if (has_next) seg_info(sg + 1, nm0, nn0, nkb, nke);
@@ -487,7 +590,8 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
     Unroll<0, 4>::run([&](const int i) {                                                                      \
       _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                            \
       _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                            \
-        acc[QM][QN][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[QN][j][s], acc[QM][QN][i][j], 0, 0, 0); \
+        acc[QM][QN][i][j] = DS ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[QN][j][s], fa[i][s], acc[QM][QN][i][j], 0, 0, 0) \
+                               : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[QN][j][s], acc[QM][QN][i][j], 0, 0, 0); \
     });
     for (int kt = kb; kt < ke; ++kt) {
       const int b = T & 1;
@@ -538,8 +642,12 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
       ++T;
     }
 #undef LUMEN_PPS_CLUSTER
+    const int64_t t_loop = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
 
-    {
+    if constexpr (DS) {
+      pp_epilogue_direct<false, FK>(acc, m0, n0, M, N, C, ldc, ep, wm, wn, lane);
+      after = 1;
+    } else {
       // ---- C epilogue: 16 passes (qm, i, qn) of 16 rows x 32 columns through this wave's
       // staging region; lane (rr, cq) stores 8 columns (16 B) of one row.
       const int rr = lane >> 2, cq = lane & 3;
@@ -614,6 +722,10 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
       });
       after = 1;
     }
+    if (ep.dbg && tid == 0) {   // profiling (tools/gemm_pp_timeline.py): stamps of this tile
+      int64_t* d = ep.dbg + 4 * (int64_t)(lin0 + sg * G);
+      d[0] = t_seg; d[1] = t_seg; d[2] = t_loop; d[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    }
     m0 = nm0;
     n0 = nn0;
     kb = nkb;
@@ -634,22 +746,29 @@ static int pp_num_cus() {
   return n;
 }
 
-template <int FK, int PRIO>
+template <int FK, int PRIO, bool DS = false>
 static void launch_pps_t(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
                          int N, int K, const GemmEpi& ep, int group_m, hipStream_t stream) {
   const int tiles = (M / 256) * (N / 256);
   const int grid = tiles < pp_num_cus() ? tiles : pp_num_cus();
+  const int lds = DS ? 2 * G_BUF : PPS_LDS;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm_pps_kernel<FK, PRIO>, hipFuncAttributeMaxDynamicSharedMemorySize, PPS_LDS);
+    hipFuncSetAttribute((const void*)gemm_pps_kernel<FK, PRIO, DS>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm_pps_kernel<FK, PRIO>), dim3(grid), dim3(512), PPS_LDS, stream, A, lda, W, ldw, C, ldc, M,
+  hipLaunchKernelGGL((gemm_pps_kernel<FK, PRIO, DS>), dim3(grid), dim3(512), lds, stream, A, lda, W, ldw, C, ldc, M,
                      N, K, ep, group_m);
 }
 
 hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
                    int N, int K, const GemmEpi& ep, int group_m, int variant, hipStream_t stream) {
+  // variants 8 / 9: 6 / 7 with the direct-store epilogue (pp_epilogue_direct; not for SwiGLU)
+  bool ds = false;
+  if (variant >= 8) {
+    variant -= 2;
+    ds = !ep.glu;
+  }
   if (variant & 1) {
     // persistent form: interior tiles only, 32-bit in-tile offsets, >= 2 K-tiles
     const bool ok = M % 256 == 0 && N % 256 == 0 && K / BK >= 2 && 255 * lda + K < (1LL << 31) &&
@@ -663,7 +782,8 @@ hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ld
       const bool prio1 = (variant & 2) != 0;
 #define LUMEN_PPS_CASE(FKV)                                                                                     \
       case FKV:                                                                                                 \
-        if (prio1) launch_pps_t<FKV, 1>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);                  \
+        if (ds) launch_pps_t<FKV, 1, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);               \
+        else if (prio1) launch_pps_t<FKV, 1>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);             \
         else launch_pps_t<FKV, 0>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);                        \
         break;
       switch (fk) {
@@ -688,12 +808,12 @@ hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ld
   const int fk = lnf ? 5 : fast && !ep.row_aff ? 1 + (ep.bias ? 1 : 0) + (ep.residual ? 2 : 0) : 0;
   const bool prio1 = (variant & 2) != 0, two = (variant & 4) != 0;
   switch (fk) {
-    case 1: launch_pp_fk<1>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, stream); break;
-    case 2: launch_pp_fk<2>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, stream); break;
-    case 3: launch_pp_fk<3>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, stream); break;
-    case 4: launch_pp_fk<4>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, stream); break;
-    case 5: launch_pp_fk<5>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, stream); break;
-    default: launch_pp_fk<0>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, stream); break;
+    case 1: launch_pp_fk<1>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, ds, stream); break;
+    case 2: launch_pp_fk<2>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, ds, stream); break;
+    case 3: launch_pp_fk<3>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, ds, stream); break;
+    case 4: launch_pp_fk<4>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, ds, stream); break;
+    case 5: launch_pp_fk<5>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, ds, stream); break;
+    default: launch_pp_fk<0>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, wt, prio1, two, ds, stream); break;
   }
   return hipGetLastError();
 }

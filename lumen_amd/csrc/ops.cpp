@@ -89,7 +89,9 @@ uint32_t* splitk_counters(const at::Tensor& like, int64_t tiles) {
 
 namespace {
 
-#define LUMEN_CHECK_HIP(expr)                                                          \
+int64_t* g_gemm_dbg = nullptr;   // profiling only (gemm_set_dbg)
+
+#define LUMEN_CHECK_HIP(expr)                                                        \
   do {                                                                                 \
     hipError_t _e = (expr);                                                            \
     TORCH_CHECK(_e == hipSuccess, "lumen HIP error: ", hipGetErrorString(_e), " @ ", #expr); \
@@ -164,6 +166,7 @@ void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tens
     TORCH_CHECK(prelu->scalar_type() == at::kBFloat16 && prelu->numel() >= N && prelu->is_contiguous(), "gemm: prelu");
     ep.prelu = bf(*prelu);
   }
+  ep.dbg = g_gemm_dbg;
   const at::DeviceGuard guard(a.device());
   // decode-shaped GEMMs (M <= 32): bandwidth-bound split-K kernel (tile -1 = auto, 9 = force)
   if ((tile == -1 || tile == 9) && M <= 32 && M > 0) {
@@ -200,6 +203,7 @@ void gemm_lnf(const at::Tensor& a, const at::Tensor& w, const at::Tensor& col_af
   ep.act = (int)act;
   ep.row_aff = row_aff.data_ptr<float>();
   ep.col_aff = col_aff.data_ptr<float>();
+  ep.dbg = g_gemm_dbg;
   const at::DeviceGuard guard(a.device());
   LUMEN_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
                                    (int)M, (int)N, (int)K, ep, (int)tile, cur_stream()));
@@ -571,6 +575,12 @@ void rms_norm_quant_fp8(const at::Tensor& x, const c10::optional<at::Tensor>& ad
   LUMEN_CHECK_HIP(lumen::rms_norm_quant_fp8(bf(x), x.stride(0), ap, lda, rp, ldr, bf(gamma), (float)eps,
                                             reinterpret_cast<uint8_t*>(out8.data_ptr()), out8.stride(0),
                                             scale.data_ptr<float>(), (int)M, (int)K, cur_stream()));
+}
+
+// profiling: route per-workgroup timestamps of the gemm / gemm_lnf ops into dbg [wg, 4] (empty: off)
+void gemm_set_dbg(const at::Tensor& dbg) {
+  TORCH_CHECK(dbg.is_cuda() && dbg.scalar_type() == at::kLong && dbg.is_contiguous(), "gemm_set_dbg: int64");
+  g_gemm_dbg = dbg.numel() > 0 ? dbg.data_ptr<int64_t>() : nullptr;
 }
 
 // profiling: plain GEMM with per-workgroup timestamps (start, prologue, K-loop, epilogue) in dbg [wg, 4]
@@ -957,6 +967,7 @@ TORCH_LIBRARY(lumen, m) {
   m.def("gemm_lnf(Tensor a, Tensor w, Tensor col_aff, Tensor row_aff, int act, Tensor(o!) out, int tile) -> ()");
   m.def("ln_row_stats(Tensor x, Tensor(o!) out, float eps, Tensor(q!)? q8=None, Tensor(s!)? qs=None) -> ()");
   m.def("gemm_probe(Tensor a, Tensor w, Tensor(o!) out, Tensor(d!) dbg, int tile) -> ()");
+  m.def("gemm_set_dbg(Tensor dbg) -> ()");
   m.def("gemm_w8(Tensor a, Tensor w8, Tensor scale, Tensor? bias, Tensor? residual, int act, Tensor(o!) out, "
         "int glu) -> ()");
   m.def("gemm_dec(Tensor a, Tensor w, Tensor? scale, Tensor? bias, Tensor? residual, Tensor(o!) out, int glu, "
@@ -1000,6 +1011,7 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("gemm_lnf", &gemm_lnf);
   m.impl("ln_row_stats", &ln_row_stats);
   m.impl("gemm_probe", &gemm_probe);
+  m.impl("gemm_set_dbg", &gemm_set_dbg);
   m.impl("gemm_w8", &gemm_w8);
   m.impl("gemm_f8", &gemm_f8);
   m.impl("gemm_dec", &gemm_dec);

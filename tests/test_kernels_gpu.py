@@ -25,7 +25,7 @@ def test_native_library_loaded():
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 768, 1024), (131, 3072, 1024), (512, 4096, 1024),
                                    (37, 64, 128), (4096, 1024, 4096), (2, 512, 512), (2570, 1024, 640)])
 @pytest.mark.parametrize("act", [None, "gelu", "quick_gelu"])
-@pytest.mark.parametrize("tile", [-1, 4, 5, 6, 7, 8, 9, 209, 609, 709, 109, 20000, 20002, 20003])
+@pytest.mark.parametrize("tile", [-1, 4, 5, 6, 7, 8, 9, 209, 609, 709, 809, 909, 109, 20000, 20002, 20003])
 def test_gemm_vs_fp32(M, N, K, act, tile):
     g = torch.Generator().manual_seed(M + N + K)
     x = torch.randn(M, K, generator=g).bfloat16()
@@ -37,7 +37,7 @@ def test_gemm_vs_fp32(M, N, K, act, tile):
     assert _rel(got, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 609, 709, 20002, 20003])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 609, 709, 809, 909, 20002, 20003])
 def test_gemm_tiles_asymmetric(tile):
     # A = I, asymmetric B: catches a transposed C write
     M = N = K = 256
@@ -181,7 +181,7 @@ def test_gemm_activations(act):
 
 
 @pytest.mark.parametrize("M,N,K", [(40 * 256, 2048, 1024), (600 * 256 + 77, 1024, 128), (3000, 768, 256)])
-@pytest.mark.parametrize("tile", [7, 1007, 47, 17, 8, 48, 1008, 609, 709, 1709, 109])
+@pytest.mark.parametrize("tile", [7, 1007, 47, 17, 8, 48, 1008, 609, 709, 1709, 109, 909, 1929, 1829])
 def test_gemm_persistent_multi_tile(M, N, K, tile):
     """Persistent kernel: several tiles per workgroup (cross-tile prefetch), epilogue with
     bias + GELU + residual, bf16 and fp32 outputs, with/without the tail split."""
@@ -203,7 +203,7 @@ def test_gemm_persistent_multi_tile(M, N, K, tile):
 
 @pytest.mark.parametrize("M,N,K", [(40 * 256, 2048, 192), (24 * 256, 3072, 128), (600 * 256, 1024, 1024),
                                    (300 * 256, 768, 64 * 7)])
-@pytest.mark.parametrize("tile", [709, 1709, 609])
+@pytest.mark.parametrize("tile", [709, 1709, 609, 809, 909, 1929])
 @pytest.mark.parametrize("act", [None, "quick_gelu"])
 def test_gemm_pingpong_fast_epilogue(M, N, K, tile, act):
     """Ping-pong kernels on interior tiles (bf16 bias -> FAST epilogue), several tiles per
@@ -280,7 +280,8 @@ def test_image_prep_center_crop_matches_reference():
                                         (16 * 256, 1024, 1024, 709), (24 * 256 + 77, 3072, 1024, -1),
                                         (577, 3072, 1024, -1), (577, 4096, 1024, -1), (40, 768, 768, -1),
                                         (512 * 77, 2304, 768, -1), (300 * 256 + 300, 1024, 512, 609),
-                                        (257 * 256, 3072, 1024, -1)])
+                                        (257 * 256, 3072, 1024, -1), (24 * 256, 3072, 1024, 1829),
+                                        (16 * 256, 4096, 1024, 1929), (300 * 256 + 300, 1024, 512, 809)])
 @pytest.mark.parametrize("act", [None, "quick_gelu"])
 def test_gemm_layernorm_folded(M, N, K, tile, act):
     """LayerNorm folded into the projection (ln_row_stats + gemm_lnf): ping-pong FAST form (interior
