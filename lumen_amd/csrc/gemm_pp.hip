@@ -27,6 +27,8 @@
 #include "gemm_epi.h"
 #include "workspace.h"
 
+#include <cstdlib>
+
 namespace lumen {
 
 __device__ __forceinline__ void pp_barrier() {
@@ -81,6 +83,7 @@ __device__ __forceinline__ void pp_epilogue_direct(const f32x4_t (&acc)[2][2][4]
       lro[r] = ep.row_aff[2 * m + 1];
     }
   }
+  float keep[FR ? 8 : 1];   // LN partials: the row's qn = 0 values until its qn = 1 pass
   Unroll<0, 16>::run([&](const int p) __attribute__((always_inline)) {
     const int qm = p >> 3, i = (p >> 1) & 3, qn = p & 1;
     float v[8];
@@ -104,7 +107,41 @@ __device__ __forceinline__ void pp_epilogue_direct(const f32x4_t (&acc)[2][2][4]
         for (int q = 0; q < 8; ++q) v[q] += f[q];
         if (p + RD < 16) rz[p % RD] = *(const u32x4_t*)(ep.residual + (int64_t)row_of(p + RD) * ep.ldr + col_of((p + RD) & 1));
       }
-      st16<WT>(C, crs, ((int64_t)m * ldc + n) * 2, pack8(v));
+      const u32x4_t pk = pack8(v);
+      st16<WT>(C, crs, ((int64_t)m * ldc + n) * 2, pk);
+      if constexpr (FR) {
+        if (ep.ln_part) {
+          // (mean, M2) of the 64 stored values of row m in this wave's columns: 16 per lane (qn = 0, 1,
+          // two-pass), then Chan merges over the 4 lanes of the row (equal counts: delta^2 * n / 2)
+          float r8[8];
+          unpack8(pk, r8);
+          if (qn == 0) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) keep[q] = r8[q];
+          } else {
+            float s = 0.f;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) s += keep[q] + r8[q];
+            float mean = s * (1.f / 16.f), m2 = 0.f;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const float d0 = keep[q] - mean, d1 = r8[q] - mean;
+              m2 += d0 * d0 + d1 * d1;
+            }
+#pragma unroll
+            for (int o = 16; o <= 32; o *= 2) {
+              const float mb = __shfl_xor(mean, o, 64), m2b = __shfl_xor(m2, o, 64);
+              const float d = mb - mean;
+              m2 = (m2 + m2b) + d * d * (float)(o / 2);
+              mean = 0.5f * (mean + mb);
+            }
+            if (fc == 0) {
+              const int nslot = N >> 6, slot = (n0 >> 8) * 4 + wn;
+              *(float2*)(ep.ln_part + ((int64_t)m * nslot + slot) * 2) = make_float2(mean, m2);
+            }
+          }
+        }
+      }
     } else {
       epi_store8_t<WT>(v, m, n, M, N, C, ldc, ep, crs);
     }
@@ -750,7 +787,13 @@ template <int FK, int PRIO, bool DS = false>
 static void launch_pps_t(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
                          int N, int K, const GemmEpi& ep, int group_m, hipStream_t stream) {
   const int tiles = (M / 256) * (N / 256);
-  const int grid = tiles < pp_num_cus() ? tiles : pp_num_cus();
+  // LUMEN_PPS_TILES_PER_WG = T > 0: ceil(tiles / T) workgroups of ~T tiles each (dispatched as CUs free up,
+  // so kernels of other streams interleave) instead of one workgroup per CU
+  static const int tpw = [] {
+    const char* e = getenv("LUMEN_PPS_TILES_PER_WG");
+    return e ? atoi(e) : 0;
+  }();
+  const int grid = tpw > 0 ? (tiles + tpw - 1) / tpw : (tiles < pp_num_cus() ? tiles : pp_num_cus());
   const int lds = DS ? 2 * G_BUF : PPS_LDS;
   static bool attr_set = false;
   if (!attr_set) {
@@ -768,6 +811,13 @@ hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ld
   if (variant >= 8) {
     variant -= 2;
     ds = !ep.glu;
+  }
+  if (ep.ln_part) {   // row-statistics partials: the direct-store, non-persistent, residual FAST epilogue only
+    const int64_t extent = (int64_t)M * ldc * 2;
+    const bool ok = ds && !(variant & 1) && M % 256 == 0 && N % 256 == 0 && ep.residual && !ep.row_aff &&
+                    !ep.out_group && !ep.table && !ep.prelu && !ep.post_act && !ep.out_f32 &&
+                    !(ep.bias && ep.bias_f32) && extent < ((int64_t)1 << 31);
+    if (!ok) return hipErrorNotSupported;
   }
   if (variant & 1) {
     // persistent form: interior tiles only, 32-bit in-tile offsets, >= 2 K-tiles

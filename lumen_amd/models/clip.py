@@ -247,10 +247,20 @@ def _block_steps(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, 
     # the out-proj / fc2 residual is added in the GEMM epilogue (the MFMA GEMM adds the prefetched
     # residual rows before its single bf16 rounding); a separate add + LayerNorm pass measured
     # 5837 vs 5951 img/s on ViT-L/14 b512 (profiles/r2_bench_resid_paths_v1.txt)
+    # the residual GEMMs (out-proj, fc2) also leave the next LayerNorm's row statistics as partials over 64
+    # columns (direct-store tile codes): one small pass over 128 B per row instead of re-reading x
+    rt = tile if res_tile is None else res_tile
+    part = None
+    if fold and _RES_LN and ops.res_ln_ok(T, W, rt, blocks[0].out_b if len(blocks) else None):
+        part = torch.empty((T, W // 64, 2), device=x.device, dtype=torch.float32)
+    have_part = False
     for i, blk in enumerate(blocks):
         if fold:
             qw, qa, fw, fa = blk.lnf()
-            ops.ln_row_stats(x, eps, out=st)
+            if have_part:
+                ops.ln_part_finalize(part, eps, out=st)
+            else:
+                ops.ln_row_stats(x, eps, out=st)
             qkv = ops.linear_lnf(x, qw, qa, st, tile=tile)
         else:
             ops.layer_norm(x, blk.ln1_w, blk.ln1_b, eps, out=h)
@@ -259,14 +269,19 @@ def _block_steps(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, 
         ops.attention(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], causal=causal, kv_len=kv_len,
                       out=o.view(B, S, heads, D))
         del qkv, q5
-        ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x, tile=tile if res_tile is None else res_tile)
+        ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x, tile=rt, ln_part=part)
         if fold:
-            ops.ln_row_stats(x, eps, out=st)
+            if part is not None:
+                ops.ln_part_finalize(part, eps, out=st)
+            else:
+                ops.ln_row_stats(x, eps, out=st)
             f = ops.linear_lnf(x, fw, fa, st, act=act, tile=tile)
         else:
             ops.layer_norm(x, blk.ln2_w, blk.ln2_b, eps, out=h)
             f = ops.linear(h, blk.fc1_w, blk.fc1_b, act=act, tile=tile)
-        ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x, tile=tile if res_tile is None else res_tile)
+        last = i == len(blocks) - 1
+        ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x, tile=rt, ln_part=None if last else part)
+        have_part = part is not None and not last
         del f
         yield i
 
@@ -330,9 +345,15 @@ def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, ep
 # LayerNorm of one half overlap GEMM tails of the other.
 _VIT_MICRO = int(os.environ.get("LUMEN_VIT_MICRO", "2"))
 _LN_FOLD = True   # GPU blocks: LayerNorms folded into qkv / fc1 (see _block_steps)
-# ping-pong 256x256, 2 phases per K-tile + priority, group_m = 2, no tail split (1629 vs 1609 / 1689:
-# 6209-6222 vs 6203-6204 / 6129-6130 img/s, profiles/r2_vit_micro_streams_v1.txt)
-_VIT_MICRO_TILE = 1629
+# LayerNorm partials from the residual GEMMs (opt-in: in the 2-stream tower the row-statistics pass already
+# hides behind the other stream's GEMMs -- 6248 vs 6251-6268 img/s, profiles/r5_gemm_pp_ds_v1.txt)
+_RES_LN = os.environ.get("LUMEN_RES_LN", "0") == "1"
+# ping-pong 256x256, 2 phases per K-tile + priority, no tail split (r2: group_m 2 = 1629 vs 1609 / 1689:
+# 6209-6222 vs 6203-6204 / 6129-6130 img/s, profiles/r2_vit_micro_streams_v1.txt); r5: the direct-store
+# epilogue with group_m 4 (1849: 6287-6340 vs 1629 6225-6227 img/s same box, the persistent forms lose in
+# the 2-stream tower, profiles/r5_gemm_pp_ds_v1.txt)
+_VIT_MICRO_TILE = int(os.environ.get("LUMEN_VIT_TILE", "1849"))
+_VIT_MICRO_RES_TILE = int(os.environ.get("LUMEN_VIT_RES_TILE", str(_VIT_MICRO_TILE)))
 # text tower (B x 77 rows): micro-batched with the auto tile choice once it has this many rows per
 # half (b512 x 77: 50.4-50.6k -> 56.2-56.4k texts/s, profiles/r2_vit_micro_streams_v1.txt)
 _TEXT_MICRO_MIN_ROWS = 16384
@@ -357,7 +378,7 @@ def run_blocks_micro(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: s
     if not x.is_cuda or n <= 1 or B < n or (B // n) * S < min_rows:
         return run_blocks(x, blocks, B, S, heads, act, eps, causal=causal)
     tile = _VIT_MICRO_TILE if tile is None else tile
-    res_tile = _VIT_MICRO_TILE if res_tile is None else res_tile
+    res_tile = _VIT_MICRO_RES_TILE if res_tile is None else res_tile
     cur = torch.cuda.current_stream(x.device)
     streams = _micro_streams(x.device, n)
     bounds = [B * i // n for i in range(n + 1)]

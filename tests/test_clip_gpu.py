@@ -91,3 +91,22 @@ def test_text_micro_batch_streams_match(monkeypatch):
     t2 = m_gpu.encode_text_ids(ids.cuda()).cpu()
     assert (t1 * t2).sum(-1).min().item() > 0.9995
     assert (t2[:6] * t_ref).sum(-1).min().item() > 0.995
+
+
+def test_vit_residual_ln_partials_match(monkeypatch):
+    """The micro-batched tower with each LayerNorm's row statistics taken from the residual GEMMs'
+    partials (LUMEN_RES_LN=1: direct-store epilogue, ops.ln_part_finalize) == re-reading the rows
+    (ln_row_stats).  ViT-B/32 at 256 images: 128 x 50 = 25 row tiles per micro-batch."""
+    import lumen_amd.models.clip as clip_mod
+
+    m_gpu = CLIPModel.random("ViT-B-32", seed=7, dtype=torch.bfloat16, device="cuda")
+    imgs = torch.randint(0, 256, (256, 224, 224, 3), dtype=torch.uint8,
+                         generator=torch.Generator().manual_seed(8)).cuda()
+    monkeypatch.setattr(clip_mod, "_VIT_MICRO", 2)
+    monkeypatch.setattr(clip_mod, "_VIT_MICRO_MIN_ROWS", 0)
+    monkeypatch.setattr(clip_mod, "_RES_LN", False)
+    e0 = m_gpu.encode_image_uint8(imgs).cpu()
+    monkeypatch.setattr(clip_mod, "_RES_LN", True)
+    e1 = m_gpu.encode_image_uint8(imgs).cpu()
+    assert torch.isfinite(e1).all()
+    assert (e0 * e1).sum(-1).min().item() > 0.9995
