@@ -60,6 +60,8 @@ struct DecodeArgs {
   // itself occupies only a few dozen CUs.  null / 0 = none.
   const uint8_t* pf[2];
   int64_t pf_bytes[2];
+  // profiling only (tools/decode_attn_timeline.py): per-workgroup s_memrealtime stamps [B, Hkv, nsplit, 8]
+  int64_t* dbg;
 };
 hipError_t paged_decode(const DecodeArgs& a, int B, int D, hipStream_t stream);
 

@@ -257,11 +257,11 @@ __global__ void __launch_bounds__(64 * PD_NW) paged_decode_kernel(DecodeArgs a, 
                 (gridDim.z - B) * gridDim.y * gridDim.x);
     return;
   }
+  const int64_t t_start = a.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
   constexpr int KS = D / 32;   // k-steps of S^T over the head dim
   constexpr int NB = D / 16;   // 16-wide d blocks of O^T
   __shared__ float sm_ml[NW][2][16];
   __shared__ float sm_o[NW][D][17];
-  __shared__ float sm_c[2][16][32];   // combine: (m, l) of up to 32 splits per query head
   __shared__ int sm_last;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -498,6 +498,11 @@ __global__ void __launch_bounds__(64 * PD_NW) paged_decode_kernel(DecodeArgs a, 
     }
   }
 
+  int64_t* dbg = a.dbg ? a.dbg + ((((int64_t)b * a.Hkv + hk) * gridDim.x + split) << 3) : nullptr;
+  if (dbg && lane == 0) {   // per wave: when its block loop ended (stamp 1 + wave)
+    dbg[1 + wid] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    if (wid == 0) dbg[0] = t_start;
+  }
   // ---- merge the NW wave states through LDS
   if (g == 0) {
     sm_ml[wid][0][col] = mrow;
@@ -534,11 +539,15 @@ __global__ void __launch_bounds__(64 * PD_NW) paged_decode_kernel(DecodeArgs a, 
       }
     }
   }
-  if (ns == 1) return;
+  if (ns == 1) {
+    if (dbg && tid == 0) dbg[5] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    return;
+  }
 
   // ---- in-launch combine: the last split of (b, hk) to arrive merges all ns splits
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (dbg && tid == 0) dbg[5] = (int64_t)__builtin_amdgcn_s_memrealtime();   // partials published
   if (tid == 0) {
     uint32_t* c = a.split_cnt + (int64_t)b * a.Hkv + hk;
     const uint32_t prev = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -547,41 +556,46 @@ __global__ void __launch_bounds__(64 * PD_NW) paged_decode_kernel(DecodeArgs a, 
     sm_last = last ? 1 : 0;
   }
   __syncthreads();
+  if (dbg && tid == 0) dbg[6] = (int64_t)__builtin_amdgcn_s_memrealtime();   // ticket back
   if (!sm_last) return;
-  for (int i = tid; i < G * ns; i += 64 * NW) {
-    const int q = i / ns, sp = i - q * ns;
-    const int64_t pi = ((int64_t)b * a.H + hk * G + q) * a.nsplit + sp;
-    sm_c[0][q][sp] = __hip_atomic_load(a.part_ml + pi * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sm_c[1][q][sp] = __hip_atomic_load(a.part_ml + pi * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
+  // one round trip per 8 splits: every (m, l) and o partial of a chunk is loaded before any is used
+  // (the chunk's max rescales the running sums, online-softmax style); split order: deterministic
   for (int idx = tid; idx < G * D; idx += 64 * NW) {
     const int q = idx / D, d = idx - q * D;
     const int h = hk * G + q;
     const int64_t pi0 = ((int64_t)b * a.H + h) * a.nsplit;
-    float M = -INFINITY;
-    for (int sp = 0; sp < ns; ++sp) M = fmaxf(M, sm_c[0][q][sp]);
-    float L = 0.f, O = 0.f;
-    if (M != -INFINITY) {
-      // 8 splits' partial loads in flight per round trip; accumulation in split order: deterministic
-      for (int s0 = 0; s0 < ns; s0 += 8) {
-        float pv[8];
+    float M = -INFINITY, L = 0.f, O = 0.f;
+    for (int s0 = 0; s0 < ns; s0 += 8) {
+      float pm[8], pl[8], pv[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int sp = min(s0 + j, ns - 1);
-          pv[j] = __hip_atomic_load(a.part_o + (pi0 + sp) * D + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+      for (int j = 0; j < 8; ++j) {
+        const int64_t pi = pi0 + min(s0 + j, ns - 1);
+        pm[j] = __hip_atomic_load(a.part_ml + pi * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pl[j] = __hip_atomic_load(a.part_ml + pi * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pv[j] = __hip_atomic_load(a.part_o + pi * D + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      float mc = M;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if (s0 + j < ns) {
-            const float e = __builtin_amdgcn_exp2f(sm_c[0][q][s0 + j] - M);
-            L += sm_c[1][q][s0 + j] * e;
-            O += pv[j] * e;
-          }
+      for (int j = 0; j < 8; ++j) mc = s0 + j < ns ? fmaxf(mc, pm[j]) : mc;
+      if (mc == -INFINITY) continue;
+      const float r = __builtin_amdgcn_exp2f(M - mc);   // M = -inf: 0 (L, O still 0)
+      L *= r;
+      O *= r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (s0 + j < ns) {
+          const float e = __builtin_amdgcn_exp2f(pm[j] - mc);
+          L += pl[j] * e;
+          O += pv[j] * e;
         }
       }
+      M = mc;
     }
     a.o[(int64_t)b * a.o_sb + (int64_t)h * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+  }
+  if (dbg && tid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    dbg[7] = (int64_t)__builtin_amdgcn_s_memrealtime();   // combine done (last split only)
   }
 }
 

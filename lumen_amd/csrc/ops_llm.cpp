@@ -14,6 +14,8 @@ uint32_t* splitk_counters(const at::Tensor& like, int64_t tiles);   // ops.cpp
 
 namespace {
 
+int64_t* g_decode_dbg = nullptr;   // profiling only (decode_set_dbg)
+
 #define CHECK_HIP3(expr)                                                                   \
   do {                                                                                     \
     hipError_t _e = (expr);                                                                \
@@ -131,8 +133,15 @@ void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
     }
   }
   if (B == 0) return;
+  a.dbg = g_decode_dbg;
   const at::DeviceGuard g(q.device());
   CHECK_HIP3(lumen::paged_decode(a, (int)B, (int)D, cur()));
+}
+
+// profiling: per-workgroup timestamps of paged_decode into dbg [B, Hkv, nsplit, 8] int64 (empty: off)
+void decode_set_dbg(const at::Tensor& dbg) {
+  TORCH_CHECK(dbg.is_cuda() && dbg.scalar_type() == at::kLong && dbg.is_contiguous(), "decode_set_dbg: int64");
+  g_decode_dbg = dbg.numel() > 0 ? dbg.data_ptr<int64_t>() : nullptr;
 }
 
 void rep_penalty_(at::Tensor logits, const at::Tensor& ids, const at::Tensor& penalty) {
@@ -170,6 +179,7 @@ TORCH_LIBRARY_FRAGMENT(lumen, m) {
         "Tensor(m!)? part_ml=None, Tensor? pos=None, Tensor? cos_sin=None, Tensor? slots=None, Tensor? pf0=None, "
         "Tensor? pf1=None) -> ()");
   m.def("rep_penalty_(Tensor(a!) logits, Tensor ids, Tensor penalty) -> ()");
+  m.def("decode_set_dbg(Tensor dbg) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
@@ -177,4 +187,5 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("paged_decode", &paged_decode);
   m.impl("rep_penalty_", &rep_penalty_);
   m.impl("upload_small", &upload_small);
+  m.impl("decode_set_dbg", &decode_set_dbg);
 }
