@@ -205,7 +205,11 @@ hipError_t conv2d_lds(const ConvArgs& a, const GemmEpi& ep, int variant, hipStre
 hipError_t conv2d_lds_small(const ConvArgs& a, const GemmEpi& ep, int variant, hipStream_t stream);
 
 // tile: -1 auto, 0..2 register-staged configs, 10 + v the LDS-DMA pipeline (conv_lds.hip, v = variant)
-hipError_t conv2d_igemm(const ConvArgs& a, const GemmEpi& ep, int tile, hipStream_t stream) {
+hipError_t conv2d_igemm(const ConvArgs& a0, const GemmEpi& ep, int tile, hipStream_t stream) {
+  ConvArgs a = a0;
+  a.div_hw = make_fastdiv((uint32_t)(a.Ho * a.Wo));
+  a.div_w = make_fastdiv((uint32_t)a.Wo);
+  a.div_kw = make_fastdiv((uint32_t)a.KW);
   const int64_t M = (int64_t)a.N * a.Ho * a.Wo;
   if (tile >= 10) return conv2d_lds(a, ep, tile - 10, stream);
   // Cin % 64 == 0 layers (IResNet, SCRFD / DBNet trunks): the LDS-DMA pipeline

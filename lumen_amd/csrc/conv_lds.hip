@@ -33,6 +33,8 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
   static_assert(PERA >= 1 && PERB >= 1 && NR >= 1, "tiling");
   constexpr int ASZ = 128 * 128, STAGE = ASZ + BN * 128;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int64_t t_start = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  int64_t t_pro = 0, t_loop = 0;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
@@ -57,26 +59,24 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
   int rofs[PERA];
   uint64_t tmask[PERA];
   int cchunk[PERA];
-  __shared__ int s_tap[SMALLC ? 64 : 1];
   const int row_step = a.dh * a.W * a.ldx * 2, col_step = a.dw * a.ldx * 2;
-  if constexpr (SMALLC) {
-    if (tid < 64) s_tap[tid] = (tid / a.KW) * row_step + (tid % a.KW) * col_step;
-  }
 #pragma unroll
   for (int i = 0; i < PERA; ++i) {
     const int r = (PERA * wid + i) * 8 + (lane >> 3);
     cchunk[i] = (lane & 7) ^ ((r >> 1) & 7);                      // logical 16-byte chunk of the row
     const int ca = SMALLC ? 0 : cchunk[i] * 8;                     // channel offset of this lane's 16 B
     const int m = min(m0 + r, M - 1);
-    const int img = m / (a.Ho * a.Wo), rem = m % (a.Ho * a.Wo);
-    const int hb = (rem / a.Wo) * a.sh - a.ph, wb = (rem % a.Wo) * a.sw - a.pw;
+    const int img = (int)fdiv((uint32_t)m, a.div_hw), rem = m - img * (a.Ho * a.Wo);
+    const int ho = (int)fdiv((uint32_t)rem, a.div_w), wo = rem - ho * a.Wo;
+    const int hb = ho * a.sh - a.ph, wb = wo * a.sw - a.pw;
     rofs[i] = (((img * a.H + hb) * a.W + wb) * a.ldx + ca) * 2;   // wraps for padding rows: never used then
+    // tap validity is separable: (row ky inside) x (column kx inside)
+    uint32_t rok = 0, cok = 0;
+    for (int ky = 0; ky < a.KH; ++ky) rok |= (uint32_t)((unsigned)(hb + ky * a.dh) < (unsigned)a.H) << ky;
+    for (int kx = 0; kx < a.KW; ++kx) cok |= (uint32_t)((unsigned)(wb + kx * a.dw) < (unsigned)a.W) << kx;
     uint64_t msk = 0;
-    for (int ky = 0, t = 0; ky < a.KH; ++ky)
-      for (int kx = 0; kx < a.KW; ++kx, ++t) {
-        const int ih = hb + ky * a.dh, iw = wb + kx * a.dw;
-        if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W) msk |= 1ull << t;
-      }
+    for (int ky = 0; ky < a.KH; ++ky)
+      if ((rok >> ky) & 1u) msk |= (uint64_t)cok << (ky * a.KW);
     tmask[i] = msk;
   }
   int wofs[PERB];
@@ -91,7 +91,6 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
   uint64_t tbit = 1;
   const int cpt_log = a.Cin == 8 ? 0 : (a.Cin == 16 ? 1 : 2);   // SMALLC: 16-byte chunks per tap (log2)
   const int khw = a.KH * a.KW;
-  if constexpr (SMALLC) __syncthreads();                       // s_tap
   auto stage = [&](int s, int kt) {
     char* baseA = smem + s * STAGE + wid * PERA * 1024;
 #pragma unroll
@@ -100,7 +99,10 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
       if constexpr (SMALLC) {
         const int t = (kt << (3 - cpt_log)) + (cchunk[i] >> cpt_log);
         const int ch = (cchunk[i] & ((1 << cpt_log) - 1)) * 16;
-        off = (t < khw && ((tmask[i] >> t) & 1ull)) ? rofs[i] + s_tap[t] + ch : (int)0x80000000;
+        // tap t -> (t / KW, t % KW) by multiply-high: no LDS table, so the stage buffers are the whole
+        // LDS footprint (2 x 160 rows x 128 B = 40 KiB for 128 x 32 tiles: 4 workgroups per CU, not 3)
+        const int ty = (int)fdiv((uint32_t)t, a.div_kw), tx = t - ty * a.KW;
+        off = (t < khw && ((tmask[i] >> t) & 1ull)) ? rofs[i] + ty * row_step + tx * col_step + ch : (int)0x80000000;
       } else {
         off = (tmask[i] & tbit) ? rofs[i] + tofs : (int)0x80000000;
       }
@@ -141,6 +143,7 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
+    if (ep.dbg && kt == 0) t_pro = (int64_t)__builtin_amdgcn_s_memrealtime();
     if (kt + NSTAGE - 1 < nk) stage((kt + NSTAGE - 1) % NSTAGE, kt + NSTAGE - 1);
     const char* sA = smem + (kt % NSTAGE) * STAGE;
     const char* sW = sA + ASZ;
@@ -168,6 +171,14 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
       }
   }
   __syncthreads();
+  if (ep.dbg) t_loop = (int64_t)__builtin_amdgcn_s_memrealtime();
+  auto stamp = [&]() {   // profiling (tools/conv_timeline.py): wave 0's view of the tile
+    if (ep.dbg && tid == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int64_t* d = ep.dbg + 4 * (int64_t)blockIdx.x;
+      d[0] = t_start; d[1] = t_pro; d[2] = t_loop; d[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    }
+  };
 
   constexpr int LDSTR = TN + 4;
   constexpr int LPR = TN / 16;
@@ -279,6 +290,7 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     });
+    stamp();
     return;
   }
   Unroll<0, 4>::run([&](const int i) {
@@ -303,6 +315,7 @@ __global__ void __launch_bounds__(128 * WN) conv_lds_kernel(ConvArgs a, GemmEpi 
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   });
+  stamp();
 }
 
 template <int NS, int WN, int BN, bool SMALLC = false>

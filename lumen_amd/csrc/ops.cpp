@@ -895,6 +895,7 @@ void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Te
   a.N = (int)N; a.H = (int)H; a.W = (int)W; a.Cin = (int)Cin; a.Cout = (int)Cout; a.KH = (int)KH; a.KW = (int)KW;
   a.sh = (int)stride[0]; a.sw = (int)stride[1]; a.ph = (int)padding[0]; a.pw = (int)padding[1];
   a.dh = (int)dilation[0]; a.dw = (int)dilation[1]; a.Ho = (int)Ho; a.Wo = (int)Wo;
+  ep.dbg = g_gemm_dbg;
   const at::DeviceGuard guard(x.device());
   LUMEN_CHECK_HIP(lumen::conv2d_igemm(a, ep, (int)tile, cur_stream()));
 }
