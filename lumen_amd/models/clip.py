@@ -380,6 +380,12 @@ def run_blocks_micro(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: s
     tile = _VIT_MICRO_TILE if tile is None else tile
     res_tile = _VIT_MICRO_RES_TILE if res_tile is None else res_tile
     cur = torch.cuda.current_stream(x.device)
+    if _LN_FOLD:
+        # the LN-folded weights are built lazily and cached on the block: build them HERE, on the caller's
+        # stream that every micro-batch stream waits for -- built inside the generators, the first
+        # micro-batch's stream would compute them while the second's GEMMs already read the cache
+        for blk in blocks:
+            blk.lnf()
     streams = _micro_streams(x.device, n)
     bounds = [B * i // n for i in range(n + 1)]
     gens = []
