@@ -159,9 +159,15 @@ def _frontend_main(config_path: str, port: int, mode: str, stop_event, ready_q, 
     setup_logging(os.environ.get("LUMEN_LOG_LEVEL", "INFO"))
     from ..parallel.engine import attach_frontend
 
+    from ..utils.sampler import maybe_start
+
     attach_frontend(specs)
-    serve(config_path, port, mode=mode, stop_event=stop_event, procs=1, replica=idx, ready_q=ready_q,
-          parent_pid=parent_pid, frontends=0, proxies=proxies)
+    stop_sampler = maybe_start(f"frontend{idx}")   # LUMEN_SAMPLE_DIR: stack samples of every thread
+    try:
+        serve(config_path, port, mode=mode, stop_event=stop_event, procs=1, replica=idx, ready_q=ready_q,
+              parent_pid=parent_pid, frontends=0, proxies=proxies)
+    finally:
+        stop_sampler()
 
 
 def engine_devices() -> list[str]:

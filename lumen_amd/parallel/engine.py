@@ -287,6 +287,9 @@ def engine_main(services: dict, device: str, ready_q, stop_ev, max_items: int = 
             t.start()
             ths.append(t)
     ready_q.put(("ready", device, os.getpid()))
+    from ..utils.sampler import maybe_start
+
+    stop_sampler = maybe_start(f"engine-{device.replace(':', '')}")   # LUMEN_SAMPLE_DIR
     # stop_ev: a shared byte, polled (an mp.Event's set() blocks on a waiter that died in its wait)
     every = float(os.environ.get("LUMEN_ENGINE_STATS_S", "0") or 0)    # periodic load log (serving benches)
     t_log, last = time.perf_counter(), {}
@@ -309,6 +312,7 @@ def engine_main(services: dict, device: str, ready_q, stop_ev, max_items: int = 
     stop.set()
     for t in ths:
         t.join(timeout=5)
+    stop_sampler()
 
 
 class EngineSet:
