@@ -17,8 +17,10 @@ OpenAI-style towers (torch_backend.py:340-393).
 """
 from __future__ import annotations
 
+import logging
 import math
 import os
+import threading
 from dataclasses import dataclass, field, asdict
 from typing import Optional
 
@@ -344,6 +346,13 @@ def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, ep
 # tail pass (tile code 1609: ping-pong 256x256, non-persistent, no tail split) and attention /
 # LayerNorm of one half overlap GEMM tails of the other.
 _VIT_MICRO = int(os.environ.get("LUMEN_VIT_MICRO", "2"))
+# serving-sized image batches (<= LUMEN_CLIP_GRAPH_MAX_B) replay the tower from a hipGraph captured per
+# batch bucket (multiples of 8): one launch instead of ~200 Python-dispatched kernels per batch
+# (opt-in: serving A/B 2,897 vs 3,052 img/s eager -- the small-batch tower is GPU-bound, and the graph's
+# static buffers serialise the engine's two batch loops; profiles/r5_clip_graph_serve_v1.txt)
+_CLIP_GRAPH = os.environ.get("LUMEN_CLIP_GRAPH", "0") == "1"
+_CLIP_GRAPH_MAX_B = int(os.environ.get("LUMEN_CLIP_GRAPH_MAX_B", "64"))
+log = logging.getLogger(__name__)
 _LN_FOLD = True   # GPU blocks: LayerNorms folded into qkv / fc1 (see _block_steps)
 # LayerNorm partials from the residual GEMMs (opt-in: in the 2-stream tower the row-statistics pass already
 # hides behind the other stream's GEMMs -- 6248 vs 6251-6268 img/s, profiles/r5_gemm_pp_ds_v1.txt)
@@ -357,7 +366,11 @@ _VIT_MICRO_RES_TILE = int(os.environ.get("LUMEN_VIT_RES_TILE", str(_VIT_MICRO_TI
 # text tower (B x 77 rows): micro-batched with the auto tile choice once it has this many rows per
 # half (b512 x 77: 50.4-50.6k -> 56.2-56.4k texts/s, profiles/r2_vit_micro_streams_v1.txt)
 _TEXT_MICRO_MIN_ROWS = 16384
-_VIT_MICRO_MIN_ROWS = 65536          # per micro-batch: every GEMM stays >= 512 tiles of 256x256
+# per micro-batch rows: from 65536 rows (every GEMM >= 512 tiles of 256x256) on the fixed ping-pong tiles, below
+# that (serving-sized batches) on the auto tile choice (128x128 LDS-DMA tiles): ViT-L/14 at 40 images 3,784 vs
+# 3,116 img/s on one stream, at 64 images 4,127 vs 4,080 (profiles/r5_clip_graph_serve_v1.txt)
+_VIT_MICRO_MIN_ROWS = int(os.environ.get("LUMEN_VIT_MICRO_MIN_ROWS", "4096"))
+_VIT_MICRO_PP_ROWS = 65536
 _MICRO_STREAMS: dict = {}
 
 
@@ -377,8 +390,9 @@ def run_blocks_micro(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: s
     min_rows = _VIT_MICRO_MIN_ROWS if min_rows is None else min_rows
     if not x.is_cuda or n <= 1 or B < n or (B // n) * S < min_rows:
         return run_blocks(x, blocks, B, S, heads, act, eps, causal=causal)
-    tile = _VIT_MICRO_TILE if tile is None else tile
-    res_tile = _VIT_MICRO_RES_TILE if res_tile is None else res_tile
+    small = (B // n) * S < _VIT_MICRO_PP_ROWS
+    tile = (-1 if small else _VIT_MICRO_TILE) if tile is None else tile
+    res_tile = (-1 if small else _VIT_MICRO_RES_TILE) if res_tile is None else res_tile
     cur = torch.cuda.current_stream(x.device)
     if _LN_FOLD:
         # the LN-folded weights are built lazily and cached on the block: build them HERE, on the caller's
@@ -430,8 +444,20 @@ class VisionTower(nn.Module):
         self.ln_post_w = nn.Parameter(torch.ones(W, **kw), requires_grad=False)
         self.ln_post_b = nn.Parameter(torch.zeros(W, **kw), requires_grad=False)
         self.proj_w = nn.Parameter(torch.zeros(embed_dim, W, **kw), requires_grad=False)  # [E, W]
+        self._graphs: dict = {}
+        self._graph_lock = threading.Lock()
+
+    def invalidate_graphs(self) -> None:
+        """Drop the captured tower graphs (they hold the weights' and folded weights' addresses)."""
+        with self._graph_lock:
+            self._graphs.clear()
+
+    def _apply(self, fn, *args, **kwargs):   # .to() / .half() / ... re-home the parameters: recapture
+        self.invalidate_graphs()
+        return super()._apply(fn, *args, **kwargs)
 
     def random_init(self, gen: torch.Generator):
+        self.invalidate_graphs()
         W = self.cfg.width
         s = W ** -0.5
         w = torch.randn(W, self.kdim, generator=gen) * (self.kdim ** -0.5)
@@ -446,6 +472,50 @@ class VisionTower(nn.Module):
     @torch.no_grad()
     def forward_patches(self, patches: torch.Tensor, B: int) -> torch.Tensor:
         """patches [B*P, kpad] (bf16) -> L2-normalised fp32 embeddings [B, E]."""
+        if _CLIP_GRAPH and patches.is_cuda and 0 < B <= _CLIP_GRAPH_MAX_B and \
+                not torch.cuda.is_current_stream_capturing():
+            r = self._graph_forward(patches, B)
+            if r is not None:
+                return r
+        return self._forward_patches(patches, B)
+
+    def _graph_forward(self, patches: torch.Tensor, B: int) -> Optional[torch.Tensor]:
+        """The tower replayed from the graph of B's bucket (B rounded up to 8; the pad images' rows
+        keep whatever the bucket's input held: finite, their embeddings are dropped).  Copy-in, replay
+        and copy-out run under the lock: the serving engine's batch loops share the static buffers."""
+        Bp = -(-B // 8) * 8
+        P = self.num_patches
+        key = (Bp, patches.shape[1], patches.dtype, patches.device)
+        with self._graph_lock:
+            ent = self._graphs.get(key)
+            if ent is None:
+                ent = self._capture(Bp, patches)
+                self._graphs[key] = ent
+            if ent is False:
+                return None
+            ent["in"][:B * P].copy_(patches)
+            ent["g"].replay()
+            return ent["out"][:B].clone()
+
+    def _capture(self, Bp: int, patches: torch.Tensor):
+        try:
+            static_in = torch.zeros((Bp * self.num_patches, patches.shape[1]), device=patches.device,
+                                    dtype=patches.dtype)
+            cur = torch.cuda.current_stream(patches.device)
+            side = torch.cuda.Stream(device=patches.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self._forward_patches(static_in, Bp)     # warm-up: folded weights, kernel attributes, workspaces
+            cur.wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):   # the other batch loop keeps launching
+                static_out = self._forward_patches(static_in, Bp)
+            return {"g": g, "in": static_in, "out": static_out}
+        except Exception as e:  # noqa: BLE001 - an op that cannot be captured: eager launches for this bucket
+            log.warning("CLIP image tower graph capture failed (%s); eager launches", e)
+            return False
+
+    def _forward_patches(self, patches: torch.Tensor, B: int) -> torch.Tensor:
         cfg = self.cfg
         S, P, W = self.seq, self.num_patches, cfg.width
         dev, dt = patches.device, self.patch_w.dtype
@@ -679,6 +749,8 @@ class CLIPModel(nn.Module):
     # ---- weight ingestion
     def load_state_dict_any(self, sd: dict) -> None:
         """Load OpenCLIP / OpenAI (``visual.*``), HF ``CLIPModel`` or HF ``ChineseCLIPModel`` naming."""
+        if hasattr(self.visual, "invalidate_graphs"):
+            self.visual.invalidate_graphs()
         if self.cfg.text_arch == "bert" and any(k.startswith("text_model.encoder.layer.") for k in sd):
             _load_bert_text(self.text, sd) if self.text is not None else None
             sd = {k: v for k, v in sd.items() if not k.startswith("text_model.") and k != "text_projection.weight"}

@@ -116,3 +116,28 @@ def test_vit_residual_ln_partials_match(monkeypatch):
     m2 = CLIPModel.random("ViT-B-32", seed=7, dtype=torch.bfloat16, device="cuda")
     e2 = m2.encode_image_uint8(imgs).cpu()
     assert (e2 * e1).sum(-1).min().item() > 0.9995
+
+
+def test_vit_graph_buckets_match_eager(monkeypatch):
+    """Serving-sized image batches replay the tower from a hipGraph per 8-image bucket
+    (VisionTower._graph_forward): same embeddings as the eager launches for a partial bucket and a full
+    one, and new weights (load / random_init) recapture instead of replaying the old addresses."""
+    import lumen_amd.models.clip as clip_mod
+
+    m = CLIPModel.random("ViT-B-32", seed=11, dtype=torch.bfloat16, device="cuda")
+    imgs = torch.randint(0, 256, (16, 224, 224, 3), dtype=torch.uint8,
+                         generator=torch.Generator().manual_seed(12)).cuda()
+    for n in (5, 16, 5):
+        monkeypatch.setattr(clip_mod, "_CLIP_GRAPH", False)
+        e_eager = m.encode_image_uint8(imgs[:n]).cpu()
+        monkeypatch.setattr(clip_mod, "_CLIP_GRAPH", True)
+        e_graph = m.encode_image_uint8(imgs[:n]).cpu()
+        assert (e_eager * e_graph).sum(-1).min().item() > 0.9999
+    assert len(m.visual._graphs) == 2
+    m.visual.random_init(torch.Generator().manual_seed(13))
+    assert len(m.visual._graphs) == 0
+    monkeypatch.setattr(clip_mod, "_CLIP_GRAPH", False)
+    e_eager = m.encode_image_uint8(imgs[:5]).cpu()
+    monkeypatch.setattr(clip_mod, "_CLIP_GRAPH", True)
+    e_graph = m.encode_image_uint8(imgs[:5]).cpu()
+    assert (e_eager * e_graph).sum(-1).min().item() > 0.9999
