@@ -34,6 +34,12 @@ from ..ops import cnn
 from .layers import ChannelAffine, ConvBN, Linear, fold_bn
 
 _FUSED_BN = __import__("os").environ.get("LUMEN_IRES_FUSED_BN", "1") != "0"
+# LUMEN_IRES_MICRO = 2: recogniser batches of >= 2 x LUMEN_IRES_MICRO_MIN faces as 2 halves on 2 HIP streams,
+# block-interleaved (opt-in: the face pipeline already overlaps the next batch's detector with this batch's
+# recogniser -- 3,318-3,346 vs 3,325-3,344 img/s, profiles/r5_face_micro_v1.txt)
+_IRES_MICRO = int(__import__("os").environ.get("LUMEN_IRES_MICRO", "1"))
+_IRES_MICRO_MIN = int(__import__("os").environ.get("LUMEN_IRES_MICRO_MIN", "32"))
+_IRES_STREAMS: dict = {}
 
 
 # =============================================================================== recogniser
@@ -114,17 +120,62 @@ class IResNet(nn.Module):
                 h = b(h)
             h = self.bn_out(h)
         else:
-            b0 = self.blocks[0].bn1
-            h, hb = self.stem(x, aff=(b0.scale, b0.shift), aff_out=True)
-            n = len(self.blocks)
-            for i, b in enumerate(self.blocks):
-                if i + 1 < n:
-                    nb = self.blocks[i + 1].bn1
-                    h, hb = b(h, hb, (nb.scale, nb.shift))
-                else:
-                    h = b(h, hb, (self.bn_out.scale, self.bn_out.shift), next_in_place=True)
+            F = x.shape[0]
+            n = _IRES_MICRO
+            if n > 1 and F >= n * _IRES_MICRO_MIN:
+                return self._forward_micro(x, n)
+            for h in self._fused_steps(x):
+                pass
         emb = self.fc(h.reshape(h.shape[0], -1), out_dtype=torch.float32)
         return ops.l2_normalize_(emb.contiguous())
+
+    def _fused_steps(self, x: torch.Tensor):
+        """The fused-BN block chain over x, one ``yield`` per block (the last yields the output rows)."""
+        b0 = self.blocks[0].bn1
+        h, hb = self.stem(x, aff=(b0.scale, b0.shift), aff_out=True)
+        n = len(self.blocks)
+        for i, b in enumerate(self.blocks):
+            if i + 1 < n:
+                nb = self.blocks[i + 1].bn1
+                h, hb = b(h, hb, (nb.scale, nb.shift))
+            else:
+                h = b(h, hb, (self.bn_out.scale, self.bn_out.shift), next_in_place=True)
+            yield h
+
+    def _forward_micro(self, x: torch.Tensor, n: int) -> torch.Tensor:
+        """Faces split into n row ranges, each on its own stream, blocks issued interleaved; each range
+        writes its embeddings into the shared output (allocated on the caller's stream, joined at the end)."""
+        F = x.shape[0]
+        cur = torch.cuda.current_stream(x.device)
+        key = (x.device.index, n)
+        if key not in _IRES_STREAMS:
+            _IRES_STREAMS[key] = [torch.cuda.Stream(device=x.device) for _ in range(n)]
+        streams = _IRES_STREAMS[key]
+        out = torch.empty((F, self.cfg.embedding), device=x.device, dtype=torch.float32)
+        bounds = [F * i // n for i in range(n + 1)]
+        gens = []
+        for i, st in enumerate(streams):
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                gens.append(self._fused_steps(x[bounds[i]:bounds[i + 1]]))
+        last = [None] * n
+        live = list(range(n))
+        while live:
+            nxt = []
+            for i in live:
+                with torch.cuda.stream(streams[i]):
+                    h = next(gens[i], None)
+                    if h is not None:
+                        last[i] = h
+                        nxt.append(i)
+                    else:   # chain done: this range's embeddings on its own stream
+                        hl = last[i]
+                        out[bounds[i]:bounds[i + 1]].copy_(self.fc(hl.reshape(hl.shape[0], -1), out_dtype=torch.float32))
+                        last[i] = None
+            live = nxt
+        for st in streams:
+            cur.wait_stream(st)
+        return ops.l2_normalize_(out)
 
     def load_insightface_state_dict(self, sd: dict) -> None:
         """insightface ``iresnet`` PyTorch weights (conv1/bn1/prelu, layerX.Y.*, bn2, fc, features)."""
