@@ -43,7 +43,7 @@ __device__ __forceinline__ void pp_barrier() {
 template <bool WT, int FK>
 __device__ __forceinline__ void pp_epilogue_direct(const f32x4_t (&acc)[2][2][4][2], int m0, int n0, int M, int N,
                                                    void* __restrict__ C, int64_t ldc, const GemmEpi& ep, int wm,
-                                                   int wn, int lane) {
+                                                   int wn, int lane, const float* aff_lds = nullptr) {
   constexpr bool FL = FK == 5;
   constexpr bool fast = FK > 0 && !FL;
   constexpr bool FB = fast && ((FK - 1) & 1), FR = fast && ((FK - 1) & 2);
@@ -64,23 +64,45 @@ __device__ __forceinline__ void pp_epilogue_direct(const f32x4_t (&acc)[2][2][4]
   }
   float lcs[FL ? 16 : 1], lcb[FL ? 16 : 1], lrs[FL ? 8 : 1], lro[FL ? 8 : 1];
   if constexpr (FL) {
+    if (aff_lds) {   // staged by the kernel ahead of its K loop: [col scale 256 | col shift 256 | rstd 256 | -mean*rstd 256]
 #pragma unroll
-    for (int qn = 0; qn < 2; ++qn)
+      for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const f32x4_t a = *(const f32x4_t*)(ep.col_aff + col_of(qn) + 4 * h);
-        const f32x4_t b = *(const f32x4_t*)(ep.col_aff + N + col_of(qn) + 4 * h);
+        for (int h = 0; h < 2; ++h) {
+          const int c = col_of(qn) - n0 + 4 * h;
+          const f32x4_t a = *(const f32x4_t*)(aff_lds + c);
+          const f32x4_t b = *(const f32x4_t*)(aff_lds + 256 + c);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          lcs[qn * 8 + 4 * h + e] = a[e];
-          lcb[qn * 8 + 4 * h + e] = b[e];
+          for (int e = 0; e < 4; ++e) {
+            lcs[qn * 8 + 4 * h + e] = a[e];
+            lcb[qn * 8 + 4 * h + e] = b[e];
+          }
         }
-      }
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int64_t m = row_of(2 * r);
-      lrs[r] = ep.row_aff[2 * m];
-      lro[r] = ep.row_aff[2 * m + 1];
+      for (int r = 0; r < 8; ++r) {
+        const int lr = row_of(2 * r) - m0;
+        lrs[r] = aff_lds[512 + lr];
+        lro[r] = aff_lds[768 + lr];
+      }
+    } else {
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4_t a = *(const f32x4_t*)(ep.col_aff + col_of(qn) + 4 * h);
+          const f32x4_t b = *(const f32x4_t*)(ep.col_aff + N + col_of(qn) + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            lcs[qn * 8 + 4 * h + e] = a[e];
+            lcb[qn * 8 + 4 * h + e] = b[e];
+          }
+        }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int64_t m = row_of(2 * r);
+        lrs[r] = ep.row_aff[2 * m];
+        lro[r] = ep.row_aff[2 * m + 1];
+      }
     }
   }
   float keep[FR ? 8 : 1];   // LN partials: the row's qn = 0 values until its qn = 1 pass
@@ -250,6 +272,23 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);                                                      \
   pp_barrier();
 
+  // direct store + LN fold: the epilogue's column / row affine operands staged in LDS past the pipeline
+  // buffers, loaded ahead of the K loop -- loaded after it, their round trip sat between the last MFMA
+  // and the first store of every tile
+  constexpr bool PRE = DS && FK == 5;
+  float* aff_lds = (float*)(smem + 2 * G_BUF);
+  float pre0 = 0.f, pre1 = 0.f;
+  if constexpr (PRE) {
+    if (tid < 256) {
+      pre0 = ep.col_aff[n0 + tid];
+      pre1 = ep.col_aff[N + n0 + tid];
+    } else {
+      const int64_t r = m0 + tid - 256;
+      pre0 = ep.row_aff[2 * r];
+      pre1 = ep.row_aff[2 * r + 1];
+    }
+    asm volatile("" ::: "memory");   // issued before the prologue's staging loads
+  }
   const int nk = K / BK;
   if constexpr (NPH == 4) {
     // prologue: tile 0 whole, then A0, B1, A1 of tile 1 (B0(1) goes out at phase 0 of tile 0)
@@ -279,6 +318,10 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     } else {
       vm_wait_n<2>();
     }
+  }
+  if constexpr (PRE) {   // older than every staging load: landed by the wait above
+    aff_lds[(tid & 255) + (tid < 256 ? 0 : 512)] = pre0;
+    aff_lds[(tid & 255) + (tid < 256 ? 256 : 768)] = pre1;
   }
   pp_barrier();
   const int64_t t_pro = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
@@ -362,7 +405,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   const int64_t t_loop = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
 
   if constexpr (DS) {
-    pp_epilogue_direct<WT, FK>(acc, m0, n0, M, N, C, ldc, ep, wm, wn, lane);
+    pp_epilogue_direct<WT, FK>(acc, m0, n0, M, N, C, ldc, ep, wm, wn, lane, PRE ? aff_lds : nullptr);
   } else {
   // ---- epilogue: per-wave 16-row slabs through LDS (bias / residual prefetched on the FAST path)
   constexpr int LDSTR = 68;
@@ -453,7 +496,7 @@ template <bool WT, int FK, int PRIO, int NPH, bool DS = false>
 static void launch_pp_t(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
                         int N, int K, const GemmEpi& ep, int group_m, hipStream_t stream, int splits = 1) {
   const dim3 tiles(((M + 255) / 256) * ((N + 255) / 256), splits);
-  const size_t lds = 2 * G_BUF;
+  const size_t lds = 2 * G_BUF + (DS && FK == 5 ? 4096 : 0);   // + the LN-fold affine stage
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)gemm_pp_kernel<WT, FK, PRIO, NPH, DS>, hipFuncAttributeMaxDynamicSharedMemorySize,
