@@ -281,7 +281,8 @@ def test_image_prep_center_crop_matches_reference():
                                         (577, 3072, 1024, -1), (577, 4096, 1024, -1), (40, 768, 768, -1),
                                         (512 * 77, 2304, 768, -1), (300 * 256 + 300, 1024, 512, 609),
                                         (257 * 256, 3072, 1024, -1), (24 * 256, 3072, 1024, 1829),
-                                        (16 * 256, 4096, 1024, 1929), (300 * 256 + 300, 1024, 512, 809)])
+                                        (16 * 256, 4096, 1024, 1929), (300 * 256 + 300, 1024, 512, 809),
+                                        (24 * 256, 4096, 1024, 1839)])
 @pytest.mark.parametrize("act", [None, "quick_gelu"])
 def test_gemm_layernorm_folded(M, N, K, tile, act):
     """LayerNorm folded into the projection (ln_row_stats + gemm_lnf): ping-pong FAST form (interior
