@@ -514,7 +514,13 @@ static void launch_pp_fk(const uint16_t* A, int64_t lda, const uint16_t* W, int6
   // write-through stores measured slower on every shape (profiles/r2_gemm_pp_v1.jsonl): not instantiated
   (void)wt;
   if (ds) {   // direct-store epilogue: the production two-phase, static-priority form only
-    launch_pp_t<false, FK, 1, 2, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
+    // LUMEN_PP_DS_WT=1: write-through (sc1) C stores (A/B knob, profiles/r5_gemm_pp_ds_v1.txt)
+    static const bool ds_wt = [] {
+      const char* e = getenv("LUMEN_PP_DS_WT");
+      return e != nullptr && e[0] == '1';
+    }();
+    if (ds_wt) launch_pp_t<true, FK, 1, 2, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
+    else launch_pp_t<false, FK, 1, 2, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
     return;
   }
   if (two) {
