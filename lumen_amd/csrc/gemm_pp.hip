@@ -40,14 +40,14 @@ __device__ __forceinline__ void pp_barrier() {
 // Direct-store epilogue (DS kernels): the lane holds row m0 + qm*128 + wm*64 + i*16 + (lane & 15),
 // columns n0 + qn*128 + wn*32 + 8*(lane >> 4) + [0, 8) in acc[qm][qn][i][0..1][0..3]; 16 passes of one
 // 16-byte store each.  Bias / residual / LN-fold operands are loaded up front (residual RD passes ahead).
-template <bool WT, int FK>
+template <bool WT, int FK, int RDD = LUMEN_GEMM_RES_PREFETCH>
 __device__ __forceinline__ void pp_epilogue_direct(const f32x4_t (&acc)[2][2][4][2], int m0, int n0, int M, int N,
                                                    void* __restrict__ C, int64_t ldc, const GemmEpi& ep, int wm,
                                                    int wn, int lane, const float* aff_lds = nullptr) {
   constexpr bool FL = FK == 5;
   constexpr bool fast = FK > 0 && !FL;
   constexpr bool FB = fast && ((FK - 1) & 1), FR = fast && ((FK - 1) & 2);
-  constexpr int RD = LUMEN_GEMM_RES_PREFETCH;
+  constexpr int RD = RDD;   // residual passes in flight (16: every residual load issued before the first store)
   const __amdgpu_buffer_rsrc_t crs = c_rsrc(C);
   const int fr = lane & 15, fc = lane >> 4;
   auto col_of = [&](int qn) { return n0 + qn * 128 + wn * 32 + fc * 8; };
@@ -182,7 +182,7 @@ __device__ __forceinline__ void vm_wait_n() {
 // PRIO 1: static priority 1 for the lagging group (MI355X_MICROARCH "Two waves per SIMD" 4).
 // DS: direct-store epilogue (gemm_epi.h swzb): transposed accumulators, 16-byte stores straight
 // from registers, no LDS staging (no SwiGLU).
-template <bool WT, int FK, int PRIO, int NPH, bool DS = false>
+template <bool WT, int FK, int PRIO, int NPH, bool DS = false, int RDD = LUMEN_GEMM_RES_PREFETCH>
 __global__ void __launch_bounds__(512)
 gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                void* __restrict__ C, int64_t ldc, int M, int N, int K, GemmEpi ep, int group_m) {
@@ -405,7 +405,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   const int64_t t_loop = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
 
   if constexpr (DS) {
-    pp_epilogue_direct<WT, FK>(acc, m0, n0, M, N, C, ldc, ep, wm, wn, lane, PRE ? aff_lds : nullptr);
+    pp_epilogue_direct<WT, FK, RDD>(acc, m0, n0, M, N, C, ldc, ep, wm, wn, lane, PRE ? aff_lds : nullptr);
   } else {
   // ---- epilogue: per-wave 16-row slabs through LDS (bias / residual prefetched on the FAST path)
   constexpr int LDSTR = 68;
@@ -492,19 +492,19 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   }
 }
 
-template <bool WT, int FK, int PRIO, int NPH, bool DS = false>
+template <bool WT, int FK, int PRIO, int NPH, bool DS = false, int RDD = LUMEN_GEMM_RES_PREFETCH>
 static void launch_pp_t(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
                         int N, int K, const GemmEpi& ep, int group_m, hipStream_t stream, int splits = 1) {
   const dim3 tiles(((M + 255) / 256) * ((N + 255) / 256), splits);
   const size_t lds = 2 * G_BUF + (DS && FK == 5 ? 4096 : 0);   // + the LN-fold affine stage
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm_pp_kernel<WT, FK, PRIO, NPH, DS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)lds);
+    hipFuncSetAttribute((const void*)gemm_pp_kernel<WT, FK, PRIO, NPH, DS, RDD>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<WT, FK, PRIO, NPH, DS>), dim3(tiles), dim3(512), lds, stream, A, lda, W, ldw, C,
-                     ldc, M, N, K, ep, group_m);
+  hipLaunchKernelGGL((gemm_pp_kernel<WT, FK, PRIO, NPH, DS, RDD>), dim3(tiles), dim3(512), lds, stream, A, lda, W, ldw,
+                     C, ldc, M, N, K, ep, group_m);
 }
 
 template <int FK>
@@ -519,7 +519,15 @@ static void launch_pp_fk(const uint16_t* A, int64_t lda, const uint16_t* W, int6
       const char* e = getenv("LUMEN_PP_DS_WT");
       return e != nullptr && e[0] == '1';
     }();
+    // LUMEN_PP_DS_RD = 8 / 16: residual passes in flight in the residual epilogues (A/B knob)
+    static const int ds_rd = [] {
+      const char* e = getenv("LUMEN_PP_DS_RD");
+      return e ? atoi(e) : 0;
+    }();
+    constexpr bool RES = FK == 3 || FK == 4;
     if (ds_wt) launch_pp_t<true, FK, 1, 2, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
+    else if (RES && ds_rd == 8) launch_pp_t<false, FK, 1, 2, true, 8>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
+    else if (RES && ds_rd == 16) launch_pp_t<false, FK, 1, 2, true, 16>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
     else launch_pp_t<false, FK, 1, 2, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
     return;
   }
