@@ -24,6 +24,13 @@
 // timeout, never a hang.  The engine writes a heartbeat; a restarted engine bumps the
 // generation and fails the slots its predecessor left RUNNING.
 //
+// Streaming requests (VLM token streams): while a slot is RUNNING the engine may APPEND partial
+// records ([u32 length][bytes], 8-byte aligned) to the slot's result area (lumen_ch_partial); the
+// front end waits on the slot's pseq futex word (bumped by every append and by completion) and
+// hands each record on as it lands (lumen_ch_wait_partial).  The final result then goes after the
+// log (Slot::roff), so nothing the front end has not read yet is overwritten.  An append to a slot
+// its front end abandoned returns -2: the engine stops generating for it.
+//
 // A front end that stops waiting (timeout) ABANDONS its slot instead of leaking it: a slot that
 // is still queued is marked ABANDONED_Q and the engine frees it when it pops it; one that is
 // running is marked ABANDONED_R and the engine frees it at completion (or a restarted engine
@@ -44,7 +51,7 @@
 namespace {
 
 constexpr uint32_t kMagic = 0x4c4d4348;   // "LMCH"
-constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersion = 2;
 
 enum State : uint32_t { FREE = 0, FILLING = 1, QUEUED = 2, RUNNING = 3, DONE = 4, ERROR = 5,
                        ABANDONED_Q = 6, ABANDONED_R = 7 };
@@ -91,6 +98,10 @@ struct alignas(64) Slot {
   uint32_t gen;                  // engine generation that ran it
   uint64_t tag;                  // submitter tag (pid << 32 | sequence), diagnostics
   char meta[128];                // small per-request options (UTF-8 JSON), NUL-terminated
+  std::atomic<uint32_t> pseq;    // futex word: bumped by every partial append and by completion
+  uint32_t pflags;               // reserved
+  std::atomic<uint64_t> plen;    // bytes of partial records in the result area
+  uint64_t roff;                 // offset of the final result in the result area (after the log)
 };
 
 inline uint64_t now_ns() {
@@ -269,6 +280,8 @@ int lumen_ch_acquire(void* base, int timeout_ms) {
       s.rbytes = 0;
       s.rndim = 0;
       s.meta[0] = 0;
+      s.plen.store(0, std::memory_order_relaxed);
+      s.roff = 0;
       s.state.store(FILLING, std::memory_order_release);
       return (int)v;
     }
@@ -361,8 +374,53 @@ void lumen_ch_complete(void* base, int slot, int status) {
   uint32_t st = RUNNING;
   const bool handed = s.state.compare_exchange_strong(st, status == 0 ? DONE : ERROR, std::memory_order_acq_rel);
   h->depth.fetch_sub(1, std::memory_order_relaxed);
-  if (handed) futex_wake(&s.state, INT_MAX);
-  else if (st == ABANDONED_R) lumen_ch_release(base, slot);   // nobody waits for it any more
+  if (handed) {
+    futex_wake(&s.state, INT_MAX);
+    s.pseq.fetch_add(1, std::memory_order_release);   // a streaming waiter sleeps on pseq
+    futex_wake(&s.pseq, INT_MAX);
+  } else if (st == ABANDONED_R) {
+    lumen_ch_release(base, slot);   // nobody waits for it any more
+  }
+}
+
+// Engine: append one partial record to a RUNNING slot.  0 ok, -1 no room left in the result
+// area (the record is dropped: the final result must carry everything), -2 the slot is no longer
+// RUNNING (abandoned by its front end, or failed by a restart): stop producing for it.
+int lumen_ch_partial(void* base, int slot, const void* data, uint64_t n) {
+  Header* h = H(base);
+  Slot& s = slots(base)[slot];
+  if (s.state.load(std::memory_order_acquire) != RUNNING) return -2;
+  const uint64_t at = s.plen.load(std::memory_order_relaxed);
+  const uint64_t rec = (4 + n + 7) & ~uint64_t(7);
+  if (n > 0xffffffffull || at + rec > h->result_bytes) return -1;
+  char* dst = static_cast<char*>(base) + lumen_ch_result_off(base, slot) + at;
+  const uint32_t len = (uint32_t)n;
+  std::memcpy(dst, &len, 4);
+  if (n) std::memcpy(dst + 4, data, n);
+  s.plen.store(at + rec, std::memory_order_release);
+  s.pseq.fetch_add(1, std::memory_order_release);
+  futex_wake(&s.pseq, INT_MAX);
+  return 0;
+}
+
+uint64_t lumen_ch_plen(void* base, int slot) {
+  return slots(base)[slot].plen.load(std::memory_order_acquire);
+}
+
+// Front end of a streaming slot: wait until it has partial bytes past seen_plen (returns RUNNING)
+// or is DONE / ERROR (returns that state); -1 after timeout_ms.
+int lumen_ch_wait_partial(void* base, int slot, uint64_t seen_plen, int timeout_ms) {
+  Slot& s = slots(base)[slot];
+  const uint64_t deadline = now_ns() + (uint64_t)(timeout_ms < 0 ? 0 : timeout_ms) * 1000000ull;
+  for (;;) {
+    const uint32_t seq = s.pseq.load(std::memory_order_acquire);
+    if (s.plen.load(std::memory_order_acquire) > seen_plen) return RUNNING;
+    const uint32_t st = s.state.load(std::memory_order_acquire);
+    if (st == DONE || st == ERROR) return (int)st;
+    const uint64_t t = now_ns();
+    if (t >= deadline) return -1;
+    futex_wait(&s.pseq, seq, (int64_t)(deadline - t));
+  }
 }
 
 // Front end: give up on a submitted slot (after a wait timeout).  Returns 1 when the slot was
@@ -410,14 +468,20 @@ int lumen_ch_engine_start(void* base, uint32_t pid) {
     }
     uint32_t st = RUNNING;
     if (sl[i].state.load(std::memory_order_acquire) == RUNNING) {
-      char* msg = static_cast<char*>(base) + lumen_ch_result_off(base, (int)i);
       const char text[] = "engine restarted while this request was running";
+      // after any partial records a streaming front end may still be reading
+      uint64_t at = (sl[i].plen.load(std::memory_order_acquire) + 63) & ~uint64_t(63);
+      if (at + sizeof(text) > h->result_bytes) at = 0;
+      char* msg = static_cast<char*>(base) + lumen_ch_result_off(base, (int)i) + at;
       std::memcpy(msg, text, sizeof(text));
       sl[i].rbytes = sizeof(text) - 1;
       sl[i].status = 1;
+      sl[i].roff = at;
       if (sl[i].state.compare_exchange_strong(st, ERROR, std::memory_order_acq_rel)) {
         h->depth.fetch_sub(1, std::memory_order_relaxed);
         futex_wake(&sl[i].state, INT_MAX);
+        sl[i].pseq.fetch_add(1, std::memory_order_release);
+        futex_wake(&sl[i].pseq, INT_MAX);
         ++failed;
       }
     }

@@ -95,6 +95,34 @@ class RemotePool:
     def run(self, kind: str, items: Sequence, timeout: Optional[float] = None) -> list:
         return self.submit(kind, list(items)).result(timeout)
 
+    def stream(self, kind: str, item):
+        """Generator over ONE streaming request (the engine factory lists ``kind`` in its
+        ``solo_kinds``): yields every partial object the engine emits as it lands and returns the
+        final result (``final = yield from pool.stream(...)``).  Closing it early abandons the
+        request on the engine."""
+        blob = pickle.dumps((kind, [item]), protocol=pickle.HIGHEST_PROTOCOL)
+        ch = self.group.pick()
+        self.stats["tasks"] += 1
+        self.stats["items"] += 1
+        try:
+            for tag, val in ch.call_stream("call", blob, timeout=self.timeout_s):
+                if tag == "partial":
+                    yield pickle.loads(val)
+                    continue
+                out = pickle.loads(val)
+                if isinstance(out, BaseException):
+                    raise out
+                if isinstance(out[0], BaseException):
+                    raise out[0]
+                return out[0]
+        except EngineUnavailable as e:
+            raise WorkerLostError(str(e)) from e
+        except ChannelError as e:
+            msg = str(e)
+            if msg.startswith("engine restarted"):
+                raise WorkerLostError(msg) from e
+            raise WorkerTaskError(msg) from e
+
     def broadcast(self, kind: str, items: list, timeout: Optional[float] = None) -> list:
         futs = []
         for ch in self.group.channels:
@@ -128,6 +156,9 @@ class PrefixedRemote:
 
     def run(self, kind: str, items: Sequence, timeout: Optional[float] = None) -> list:
         return self.pool.run(f"{self.prefix}:{kind}", items, timeout)
+
+    def stream(self, kind: str, item):
+        return (yield from self.pool.stream(f"{self.prefix}:{kind}", item))
 
     def broadcast(self, kind: str, items: list, timeout: Optional[float] = None) -> list:
         return self.pool.broadcast(f"{self.prefix}:{kind}", items, timeout)
@@ -163,6 +194,13 @@ def multi_worker(device: str, parts: dict, rank: int = 0, world: int = 1):
             raise ValueError(f"multi-model engine: unknown kind {kind!r} (parts {list(fns)})")
         return fns[name](sub, items)
 
+    solo = tuple(f"{name}:{k}" for name, f in fns.items() for k in getattr(f, "solo_kinds", ()))
+    if solo:
+        def stream(kind, item, emit):
+            name, _, sub = kind.partition(":")
+            return fns[name].stream(sub, item, emit)
+
+        fn.stream, fn.solo_kinds = stream, solo
     return fn
 
 
@@ -194,9 +232,37 @@ def current_remote() -> Optional[RemotePool]:
 _stats_lock = threading.Lock()
 
 
+def _run_solo(ch: ShmChannel, fn, slot: int, kind: str, items: list, stats: dict) -> None:
+    """One slot of a ``solo`` kind on its own thread: ``fn.stream(kind, item, emit)`` per item, each
+    ``emit(obj)`` appending a partial record the front end receives at once (False once the front
+    end abandoned the request); the slot completes on its own, not with a merged batch."""
+    def emit(obj) -> bool:
+        return ch.partial(slot, pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)) != -2
+
+    try:
+        t0 = time.perf_counter()
+        res = []
+        for it in items:
+            try:
+                res.append(fn.stream(kind, it, emit))
+            except Exception as e:  # noqa: BLE001 - reported per request
+                res.append(e)
+        with _stats_lock:
+            stats["fn_s"] = stats.get("fn_s", 0.0) + time.perf_counter() - t0
+            stats["solo"] = stats.get("solo", 0) + 1
+            stats["items"] = stats.get("items", 0) + len(items)
+            stats["slots"] = stats.get("slots", 0) + 1
+        ch.complete(slot, pickle.dumps(res, protocol=pickle.HIGHEST_PROTOCOL))
+    except Exception:  # noqa: BLE001 - e.g. an unpicklable result
+        ch.complete(slot, error=traceback.format_exc()[-4000:])
+
+
 def _serve_channel(ch: ShmChannel, fn, stop: threading.Event, max_items: int, linger_us: int,
-                   stats: dict) -> None:
-    """Batch loop over one channel: pop queued front-end batches, merge by kind, run, complete."""
+                   stats: dict, solo_ex: Optional[ThreadPoolExecutor] = None) -> None:
+    """Batch loop over one channel: pop queued front-end batches, merge by kind, run, complete.
+    Kinds the factory lists in ``fn.solo_kinds`` (a VLM's generations) are not merged: each slot
+    runs on ``solo_ex`` and may stream partial results."""
+    solo = set(getattr(fn, "solo_kinds", ()))
     while not stop.is_set():
         slots = ch.pop_batch(ch.nslots, wait_ms=100, linger_us=linger_us)
         if not slots:
@@ -210,6 +276,9 @@ def _serve_channel(ch: ShmChannel, fn, stop: threading.Event, max_items: int, li
                     with _stats_lock:
                         snap = dict(stats)
                     ch.complete(s, pickle.dumps([snap]))
+                    continue
+                if kind in solo and solo_ex is not None:
+                    solo_ex.submit(_run_solo, ch, fn, s, kind, items, stats)
                     continue
                 groups.setdefault(kind, []).append((s, items))
             except Exception as e:  # noqa: BLE001 - a bad request fails alone
@@ -261,10 +330,11 @@ def engine_main(services: dict, device: str, ready_q, stop_ev, max_items: int = 
             import torch
 
             torch.cuda.set_device(torch.device(device))
-        chans, fns, nthreads = {}, {}, {}
+        chans, fns, nthreads, opts_of = {}, {}, {}, {}
         for name, entry in services.items():
             spec, factory, kwargs = entry[:3]
             opts = entry[3] if len(entry) > 3 else {}
+            opts_of[name] = opts
             ch = ShmChannel.attach(spec)
             fns[name] = _call_factory(factory, device, kwargs, rank, world)
             chans[name] = ch
@@ -280,9 +350,16 @@ def engine_main(services: dict, device: str, ready_q, stop_ev, max_items: int = 
     stop = threading.Event()
     stats: dict = {}
     ths = []
+    solo_exs = []
     for name, ch in chans.items():
+        sx = None
+        if getattr(fns[name], "solo_kinds", ()):
+            # one thread per request in flight (a continuous-batching engine holds many at once)
+            sx = ThreadPoolExecutor(max_workers=int(opts_of[name].get("solo_threads", 64)),
+                                    thread_name_prefix=f"lumen-solo-{name}")
+            solo_exs.append(sx)
         for i in range(nthreads[name]):
-            t = threading.Thread(target=_serve_channel, args=(ch, fns[name], stop, max_items, linger_us, stats),
+            t = threading.Thread(target=_serve_channel, args=(ch, fns[name], stop, max_items, linger_us, stats, sx),
                                  name=f"lumen-engine-{name}-{i}", daemon=True)
             t.start()
             ths.append(t)
@@ -312,6 +389,8 @@ def engine_main(services: dict, device: str, ready_q, stop_ev, max_items: int = 
     stop.set()
     for t in ths:
         t.join(timeout=5)
+    for sx in solo_exs:
+        sx.shutdown(wait=False, cancel_futures=True)
     stop_sampler()
 
 

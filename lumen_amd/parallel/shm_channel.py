@@ -18,6 +18,10 @@ Engine::
         arr, meta = ch.request(slot)                       # zero-copy view into the slot
         ...; ch.complete(slot, result_array)
 
+Streaming (a VLM's tokens): the engine appends partial records to a running slot
+(``ch.partial(slot, b"...")``) and the front end iterates ``ch.call_stream(...)``, which yields
+``("partial", bytes)`` as each record lands and ends with ``("result", value)``.
+
 The reference has no cross-process serving path at all (``src/lumen/server.py:232-235``: one
 process, a 10-thread gRPC pool, batch 1).
 """
@@ -56,7 +60,9 @@ class _SlotDesc(ctypes.Structure):
                 ("ndim", ctypes.c_uint32), ("shape", ctypes.c_uint32 * 4), ("nbytes", ctypes.c_uint64),
                 ("rdtype", ctypes.c_uint32), ("rndim", ctypes.c_uint32), ("rshape", ctypes.c_uint32 * 4),
                 ("rbytes", ctypes.c_uint64), ("status", ctypes.c_uint32), ("gen", ctypes.c_uint32),
-                ("tag", ctypes.c_uint64), ("meta", ctypes.c_char * 128), ("_pad", ctypes.c_char * 40)]
+                ("tag", ctypes.c_uint64), ("meta", ctypes.c_char * 128), ("pseq", ctypes.c_uint32),
+                ("pflags", ctypes.c_uint32), ("plen", ctypes.c_uint64), ("roff", ctypes.c_uint64),
+                ("_pad", ctypes.c_char * 16)]
 
 
 def _lib():
@@ -76,7 +82,9 @@ def _lib():
                "lumen_ch_abandon": (i32, [vp, i32]),
                "lumen_ch_pop_batch": (i32, [vp, ctypes.POINTER(ctypes.c_int), i32, i32, i32]),
                "lumen_ch_complete": (None, [vp, i32, i32]), "lumen_ch_heartbeat": (None, [vp, u32]),
-               "lumen_ch_heartbeat_age_ns": (u64, [vp]), "lumen_ch_engine_start": (i32, [vp, u32])}
+               "lumen_ch_heartbeat_age_ns": (u64, [vp]), "lumen_ch_engine_start": (i32, [vp, u32]),
+               "lumen_ch_partial": (i32, [vp, i32, vp, u64]), "lumen_ch_plen": (u64, [vp, i32]),
+               "lumen_ch_wait_partial": (i32, [vp, i32, u64, i32])}
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
             f.restype, f.argtypes = res, args
@@ -191,8 +199,8 @@ class ShmChannel:
     def _payload(self, slot: int, nbytes: int) -> np.ndarray:
         return np.frombuffer(self.mm, np.uint8, nbytes, self._pay[slot])
 
-    def _result(self, slot: int, nbytes: int) -> np.ndarray:
-        return np.frombuffer(self.mm, np.uint8, nbytes, self._res[slot])
+    def _result(self, slot: int, nbytes: int, off: int = 0) -> np.ndarray:
+        return np.frombuffer(self.mm, np.uint8, nbytes, self._res[slot] + off)
 
     @staticmethod
     def _code(x) -> tuple:
@@ -212,9 +220,8 @@ class ShmChannel:
         return a.copy() if copy else a
 
     # ------------------------------------------------------------------ front end
-    def call(self, kind: str, payload, meta: Optional[dict] = None, timeout: float = 120.0):
-        """Submit one request and wait for its result (array or bytes).  Raises
-        :class:`ChannelError` with the engine's message, :class:`EngineUnavailable` on timeout."""
+    def _fill_submit(self, kind: str, payload, meta: Optional[dict], timeout: float) -> int:
+        """Acquire a slot, write the request and queue it; returns the slot (released on error)."""
         lib, base = self.lib, self.base
         slot = lib.lumen_ch_acquire(base, int(timeout * 1000))
         if slot < 0:
@@ -248,6 +255,25 @@ class ShmChannel:
             tag = (os.getpid() << 32) | (next(self._seq) & 0xFFFFFFFF)
             if lib.lumen_ch_submit(base, slot, tag) != 0:
                 raise RuntimeError("shm channel submit failed")
+        except BaseException:
+            lib.lumen_ch_release(base, slot)
+            raise
+        return slot
+
+    def _final(self, slot: int, st: int):
+        d = self._desc[slot]
+        rb = int(d.rbytes)
+        buf = np.frombuffer(self.mm, np.uint8, rb, self._res[slot] + int(d.roff))
+        if st == ERROR:
+            raise ChannelError(bytes(buf).decode("utf-8", "replace"))
+        return self._decode(buf, d.rdtype, tuple(d.rshape[:d.rndim]), copy=True)
+
+    def call(self, kind: str, payload, meta: Optional[dict] = None, timeout: float = 120.0):
+        """Submit one request and wait for its result (array or bytes).  Raises
+        :class:`ChannelError` with the engine's message, :class:`EngineUnavailable` on timeout."""
+        lib, base = self.lib, self.base
+        slot = self._fill_submit(kind, payload, meta, timeout)
+        try:
             st = lib.lumen_ch_wait(base, slot, int(timeout * 1000))
             if st < 0:
                 # the engine may still write this slot: abandon it (the engine frees it when it
@@ -255,13 +281,41 @@ class ShmChannel:
                 lib.lumen_ch_abandon(base, slot)
                 slot = -1
                 raise EngineUnavailable(f"channel {self.name}: no answer in {timeout:.0f} s")
-            rb = int(d.rbytes)
-            if st == ERROR:
-                raise ChannelError(bytes(self._result(slot, rb)).decode("utf-8", "replace"))
-            return self._decode(self._result(slot, rb), d.rdtype, tuple(d.rshape[:d.rndim]), copy=True)
+            return self._final(slot, st)
         finally:
             if slot >= 0:
                 lib.lumen_ch_release(base, slot)
+
+    def call_stream(self, kind: str, payload, meta: Optional[dict] = None, timeout: float = 120.0):
+        """Submit one streaming request; yields ``("partial", bytes)`` for every record the engine
+        appends, as it lands, then ``("result", value)``.  ``timeout`` bounds the wait for EACH
+        record.  Closing the generator early (a cancelled client) abandons the slot: the engine's
+        next append to it fails and it stops generating."""
+        lib, base = self.lib, self.base
+        slot = self._fill_submit(kind, payload, meta, timeout)
+        done = False
+        seen = 0
+        try:
+            while True:
+                st = lib.lumen_ch_wait_partial(base, slot, seen, int(timeout * 1000))
+                if st < 0:
+                    raise EngineUnavailable(f"channel {self.name}: no answer in {timeout:.0f} s")
+                end = int(lib.lumen_ch_plen(base, slot))
+                off = self._res[slot]
+                while seen < end:
+                    n = int(np.frombuffer(self.mm, np.uint32, 1, off + seen)[0])
+                    yield "partial", bytes(self.mm[off + seen + 4: off + seen + 4 + n])
+                    seen += (4 + n + 7) & ~7
+                if st in (DONE, ERROR) and int(lib.lumen_ch_plen(base, slot)) == seen:
+                    done = True
+                    value = self._final(slot, st)
+                    yield "result", value
+                    return
+        finally:
+            if done:
+                lib.lumen_ch_release(base, slot)
+            else:
+                lib.lumen_ch_abandon(base, slot)
 
     # ------------------------------------------------------------------ engine
     def engine_start(self) -> int:
@@ -289,11 +343,21 @@ class ShmChannel:
         meta = json.loads(d.meta.decode()) if d.meta else {}
         return self.kinds[d.kind], self._decode(buf, d.dtype, tuple(d.shape[:d.ndim]), copy=False), meta
 
+    def partial(self, slot: int, data: bytes) -> int:
+        """Engine: append one partial record to a running slot (streaming).  0 ok, -1 the result
+        area is full (record dropped), -2 the front end abandoned the request: stop producing."""
+        data = bytes(data)
+        return int(self.lib.lumen_ch_partial(self.base, slot, data if data else None, len(data)))
+
     def complete(self, slot: int, result=None, error: Optional[str] = None) -> None:
         d = self._desc[slot]
+        # the final result goes after any partial records (a streaming front end may still read them)
+        roff = (int(self.lib.lumen_ch_plen(self.base, slot)) + 63) & ~63
+        room = self.result_bytes - roff
         if error is not None:
-            msg = error.encode("utf-8", "replace")[: self.result_bytes]
-            self._result(slot, len(msg))[:] = np.frombuffer(msg, np.uint8)
+            msg = error.encode("utf-8", "replace")[: max(room, 0)]
+            self._result(slot, len(msg), roff)[:] = np.frombuffer(msg, np.uint8)
+            d.roff = roff
             d.rbytes, d.rdtype, d.rndim = len(msg), BYTES, 0
             self.lib.lumen_ch_complete(self.base, slot, 1)
             return
@@ -301,17 +365,18 @@ class ShmChannel:
         if code == BYTES:
             raw = bytes(result or b"")
             nb = len(raw)
-            if nb > self.result_bytes:
+            if nb > room:
                 return self.complete(slot, error=f"result {nb} B exceeds the channel result area")
-            self._result(slot, nb)[:] = np.frombuffer(raw, np.uint8)
+            self._result(slot, nb, roff)[:] = np.frombuffer(raw, np.uint8)
         else:
             a = np.ascontiguousarray(result)
             nb = a.nbytes
-            if nb > self.result_bytes or a.ndim > 4:
+            if nb > room or a.ndim > 4:
                 return self.complete(slot, error=f"result {a.shape} exceeds the channel result area")
-            self._result(slot, nb)[:] = a.reshape(-1).view(np.uint8)
+            self._result(slot, nb, roff)[:] = a.reshape(-1).view(np.uint8)
             for i, s in enumerate(a.shape):
                 d.rshape[i] = s
+        d.roff = roff
         d.rbytes, d.rdtype, d.rndim = nb, code, len(shape)
         self.lib.lumen_ch_complete(self.base, slot, 0)
 

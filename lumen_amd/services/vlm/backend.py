@@ -199,6 +199,42 @@ def stop_on_sequences(text: str, stop_sequences: Optional[Sequence[str]]) -> tup
     return text, ""
 
 
+class IncrementalText:
+    """Streaming detokenization at O(window) per token: the text of the tokens since the previous
+    emission boundary, decoded together with the token before it (so a leading-space piece keeps
+    its space), minus that prefix's own text, is the new text; a tail ending in U+FFFD (an
+    incomplete UTF-8 sequence) is held back until a later token completes it."""
+
+    def __init__(self, detok):
+        self.detok = detok
+        self.tokens: list = []
+        self.prefix = 0        # window start
+        self.read = 0          # tokens whose text is in self.text
+        self.text = ""
+
+    def push(self, tok) -> str:
+        self.tokens.append(int(tok))
+        return self._advance(hold=True)
+
+    def flush(self) -> str:
+        return self._advance(hold=False)
+
+    def _advance(self, hold: bool) -> str:
+        if self.read == len(self.tokens):
+            return ""
+        prev = self.detok(self.tokens[self.prefix:self.read])
+        cur = self.detok(self.tokens[self.prefix:])
+        if (hold and cur.endswith("\ufffd")) or len(cur) <= len(prev) or not cur.startswith(prev):
+            if not hold and not cur.startswith(prev):   # tokenizer re-spelled the window: resync
+                self.text = self.detok(self.tokens)
+                self.prefix = self.read = len(self.tokens)
+            return ""
+        delta = cur[len(prev):]
+        self.text += delta
+        self.prefix, self.read = self.read, len(self.tokens)
+        return delta
+
+
 def _engine_stages(r) -> None:
     """Engine-side stage times of a finished request onto the request's timer: admission
     queue, prefill (incl. vision tower) to first token, and the decode phase."""
@@ -528,36 +564,29 @@ class MI355XVLMBackend:
         r = self.engine.submit((ids, img if starts else None), len(full), sp)
         return r, len(full)
 
-    def _generate_remote(self, request: GenerationRequest) -> GenerationResult:
+    def _remote_result(self, request: GenerationRequest) -> GenerationResult:
+        """One generation on the engine, completed on its own (not with a merged batch)."""
         from dataclasses import replace
 
-        res = self._remote.submit("generate", [replace(request, stream=False)]).result()[0]
-        if isinstance(res, BaseException):
-            raise res
-        return res
+        gen = self._remote.stream("generate", replace(request, stream=False))
+        try:
+            while True:
+                next(gen)
+        except StopIteration as e:
+            return e.value
 
     def _stream_remote(self, request: GenerationRequest) -> Iterator[GenerationChunk]:
-        """The engine generates the whole answer; its tokens are replayed as the local stream's
-        chunks (one per token, held back on an incomplete UTF-8 tail)."""
-        res = self._generate_remote(request)
-        emitted, step = "", 0
-        for k, tok in enumerate(res.tokens):
-            text = self.detokenize(res.tokens[:k + 1])
-            if len(text) > len(res.text):
-                break                                  # past a stop sequence the engine cut at
-            if text.endswith("�"):
-                continue
-            yield GenerationChunk(text=text[len(emitted):], tokens=[tok], metadata={"step": step})
-            emitted, step = text, step + 1
-        if len(res.text) > len(emitted):
-            yield GenerationChunk(text=res.text[len(emitted):], metadata={"step": step})
-        yield GenerationChunk(text="", is_final=True, metadata={"reason": res.finish_reason,
-                                                               "input_tokens": res.metadata.get("input_tokens")})
+        """The engine's token stream: every chunk is yielded as the engine produces it (shm
+        channel partial records, parallel/shm_channel.py); closing this generator (a cancelled
+        client) abandons the request and the engine stops generating it."""
+        from dataclasses import replace
+
+        yield from self._remote.stream("generate_stream", replace(request, stream=True))
 
     def generate(self, request: GenerationRequest):
         if self._remote is not None:
             self.ensure_initialized()
-            return self._stream_remote(request) if request.stream else self._generate_remote(request)
+            return self._stream_remote(request) if request.stream else self._remote_result(request)
         if request.stream:
             return self._generate_stream(request)
         r, n_in = self._submit(request)
@@ -573,34 +602,49 @@ class MI355XVLMBackend:
 
     def _generate_stream(self, request: GenerationRequest) -> Iterator[GenerationChunk]:
         r, n_in = self._submit(request)
-        emitted = ""
+        inc = IncrementalText(self.detokenize)
+        stops = [x for x in (request.stop_sequences or []) if x]
+        longest = max((len(x) for x in stops), default=0)
+        emitted = 0                     # characters of inc.text already yielded
+        pending: list = []              # tokens not yet carried by a chunk (text held back)
         step = 0
-        for kind, val in r.stream():
-            if kind == "token":
-                text = self.detokenize(r.tokens)
-                cut, stop = stop_on_sequences(text, request.stop_sequences)
-                if stop:
-                    if len(cut) > len(emitted):
-                        yield GenerationChunk(text=cut[len(emitted):], tokens=[val], metadata={"step": step})
-                    self.engine.cancel(r)
-                    for _ in r.stream():
-                        pass
+        finished = False
+        try:
+            for kind, val in r.stream():
+                if kind == "token":
+                    pending.append(val)
+                    inc.push(val)
+                    if stops:
+                        # a stop sequence can only end inside the new text: search the tail
+                        lo = max(0, emitted - longest)
+                        cut, stop = stop_on_sequences(inc.text[lo:], stops)
+                        if stop:
+                            cut = inc.text[:lo] + cut
+                            if len(cut) > emitted:
+                                yield GenerationChunk(text=cut[emitted:], tokens=pending, metadata={"step": step})
+                            self.engine.cancel(r)
+                            for _ in r.stream():
+                                pass
+                            finished = True
+                            _engine_stages(r)
+                            yield GenerationChunk(text="", is_final=True, metadata={"reason": "stop_sequence",
+                                                                                   "input_tokens": n_in})
+                            return
+                    if len(inc.text) == emitted:
+                        continue                # held back: an incomplete UTF-8 tail
+                    yield GenerationChunk(text=inc.text[emitted:], tokens=pending, metadata={"step": step})
+                    emitted, pending = len(inc.text), []
+                    step += 1
+                else:
+                    finished = True
+                    inc.flush()
+                    if len(inc.text) > emitted or pending:
+                        yield GenerationChunk(text=inc.text[emitted:], tokens=pending, metadata={"step": step})
                     _engine_stages(r)
-                    yield GenerationChunk(text="", is_final=True, metadata={"reason": "stop_sequence",
-                                                                           "input_tokens": n_in})
-                    return
-                # hold back text that may be an incomplete UTF-8 sequence
-                if text.endswith("�"):
-                    continue
-                yield GenerationChunk(text=text[len(emitted):], tokens=[val], metadata={"step": step})
-                emitted = text
-                step += 1
-            else:
-                tail = self.detokenize(r.tokens)
-                if len(tail) > len(emitted):
-                    yield GenerationChunk(text=tail[len(emitted):], metadata={"step": step})
-                _engine_stages(r)
-                yield GenerationChunk(text="", is_final=True, metadata={"reason": val, "input_tokens": n_in})
+                    yield GenerationChunk(text="", is_final=True, metadata={"reason": val, "input_tokens": n_in})
+        finally:
+            if not finished:            # the consumer went away (client cancel): stop generating
+                self.engine.cancel(r)
 
     def get_info(self) -> BackendInfo:
         gc, vc = self.generation_config, self.vision_config
@@ -633,29 +677,44 @@ def engine_spec(backend: "MI355XVLMBackend") -> Optional[tuple]:
 
 def engine_worker(device: str, resources: GenericResources, max_new_tokens: Optional[int] = None, kv_blocks: int = 0,
                   max_batch: int = 64):
-    """Engine factory: the VLM on ``device``; fn("generate", [GenerationRequest]) -> GenerationResult
-    per request (an exception object for a request that failed alone).  The requests of one merged
-    batch run concurrently on the continuous-batching LLMEngine, as do other batch loops' requests."""
-    from concurrent.futures import ThreadPoolExecutor
+    """Engine factory: the VLM on ``device``.  Generations are ``solo`` kinds (parallel/engine.py):
+    each request's slot runs on its own thread on the continuous-batching LLMEngine and completes
+    alone -- a short answer does not wait for a long one that arrived in the same front-end batch --
+    and ``generate_stream`` hands every chunk to the front end as it is produced."""
+    from dataclasses import replace
 
     b = MI355XVLMBackend(resources, device=device, max_new_tokens=max_new_tokens, kv_blocks=kv_blocks,
                          max_batch=max_batch)
     b.initialize()
-    ex = ThreadPoolExecutor(max_workers=max(4, max_batch), thread_name_prefix="vlm-engine")
-
-    def one(req):
-        try:
-            return b.generate(req)
-        except Exception as e:  # noqa: BLE001 - reported per request
-            return e
 
     def fn(kind, items):
         if kind == "generate":
-            return list(ex.map(one, items))
+            out = []
+            for req in items:
+                try:
+                    out.append(b.generate(replace(req, stream=False)))
+                except Exception as e:  # noqa: BLE001 - reported per request
+                    out.append(e)
+            return out
         if kind == "info":
             return [b.get_info().as_dict()] * len(items)
         raise ValueError(f"unknown VLM task kind {kind!r}")
 
+    def stream(kind, req, emit):
+        if kind == "generate":
+            return b.generate(replace(req, stream=False))
+        if kind != "generate_stream":
+            raise ValueError(f"unknown VLM stream kind {kind!r}")
+        gen = b.generate(replace(req, stream=True))
+        try:
+            for chunk in gen:
+                if not emit(chunk):     # the front end abandoned the request
+                    break
+        finally:
+            gen.close()                 # cancels the engine request if it is still running
+        return None
+
+    fn.stream, fn.solo_kinds = stream, ("generate", "generate_stream")
     return fn
 
 

@@ -42,3 +42,11 @@ def test_engine_set_on_gpu_answers_like_in_process_hub(tmp_path, cache, monkeypa
     for t, _, _, _ in REQS:
         # bf16 tower: batch composition moves the softmax(100 cos) scores by a few 1e-4
         _same(t, got[t], ref[t], score_atol=3e-3, box_atol=0.05, emb_cos=0.999)
+
+
+def test_vlm_engine_streams_tokens_on_gpu(tmp_path, cache, monkeypatch):
+    """The VLM on a GPU engine behind 2 front ends streams: chunks arrive while the engine still
+    generates (first chunk < 50 % of the request time), text equal to the in-process stream."""
+    from test_vlm_stream_cpu import engine_stream_check
+
+    engine_stream_check(tmp_path, cache, monkeypatch, "cuda:0", 128)

@@ -127,6 +127,12 @@ for task in "$@"; do
         --pmc SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
         -d gpurun_out/pmc_gemm -o run -- python3 tools/gemm_bench_tiles.py --tiles=609 --rounds 1 --iters 2 \
         --shapes "${GEMM_SHAPES:-131584x3072x1024}" ;;
+    pmc_mfma)   # MFMA-busy / LDS / clock counters of the ViT GEMM tiles ($GEMM_TILES, $GEMM_SHAPES)
+      step pmc_mfma 120 timeout -s KILL 100 rocprofv3 --kernel-trace \
+        --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU \
+        SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
+        -d gpurun_out/pmc_mfma -o run -- python3 tools/gemm_bench_tiles.py --tiles="${GEMM_TILES:-1839}" --rounds 1 \
+        --iters 2 --shapes "${GEMM_SHAPES:-65792x3072x1024,65792x1024x4096}" ;;
     serve)
       step serve_clip 300 python -u tools/serve_bench.py --service clip --model CLIP-ViT-L-14 --device cuda --clients 64 \
         --seconds 20

@@ -42,6 +42,19 @@ def pmc(db, kernels=None):
             d["mfma_inst_fraction"] = d.get("SQ_INSTS_MFMA", 0) / tot
         if d.get("SQ_WAVE_CYCLES"):
             d["wait_inst_fraction"] = d.get("SQ_WAIT_INST_ANY", 0) / d["SQ_WAVE_CYCLES"]
+    try:   # kernel time under the profiler -> effective clock from GRBM_GUI_ACTIVE
+        dur = dict(c.execute("select name, sum(end - start) from kernels group by name").fetchall())
+    except sqlite3.Error:
+        dur = {}
+    for n, d in out.items():
+        if n in dur:
+            d["kernel_ns"] = dur[n]
+        if d.get("GRBM_GUI_ACTIVE") and d.get("SQ_VALU_MFMA_BUSY_CYCLES"):
+            # MFMA-busy share of every SIMD's cycles over the dispatches (1,024 SIMDs; the GRBM counter
+            # is summed over the 8 XCDs, so per-XCD active cycles = GRBM_GUI_ACTIVE / 8)
+            d["mfma_busy_per_simd"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / (d["GRBM_GUI_ACTIVE"] / 8 * 1024)
+            if n in dur:
+                d["clock_ghz_grbm"] = d["GRBM_GUI_ACTIVE"] / 8 / dur[n]
     return out
 
 
