@@ -6,15 +6,17 @@
 namespace lumen {
 
 constexpr int AR_MAX_RANKS = 8;
-constexpr int AR_MAX_BLOCKS = 64;
-constexpr int64_t AR_CTL_BYTES = 16384;
+constexpr int AR_MAX_BLOCKS = 128;
+constexpr int64_t AR_CTL_BYTES = 32768;
 constexpr int AR_SPIN_LIMIT = 2000000;   // ~1-4 s of polling before a peer is declared missing
 
 // control block at the start of every rank's buffer
 struct ArCtl {
   uint32_t flag[2][AR_MAX_BLOCKS][AR_MAX_RANKS];   // flag[parity][block][src rank], written by the peers
   uint32_t flag2[2][AR_MAX_BLOCKS][AR_MAX_RANKS];  // two-shot phase 2 (reduced slices published)
-  uint32_t epoch[AR_MAX_BLOCKS];                    // this rank's per-block call counter
+  uint32_t epoch;                                   // this rank's call counter (ONE for every block of
+                                                    // every call: all blocks agree on the parity)
+  uint32_t done;                                    // blocks of the current call that finished
   uint32_t err;                                     // set when a peer never arrived
 };
 static_assert(sizeof(ArCtl) <= AR_CTL_BYTES, "control block too large");

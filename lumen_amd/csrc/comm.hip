@@ -4,10 +4,10 @@
 // Every rank owns ONE uncached device allocation (hipExtMallocWithFlags
 // hipDeviceMallocUncached) that all peers map through hipIpc handles:
 //
-//   [ control (16 KiB): flag[2][64 blocks][8 ranks] u32 | flag2 (same) | epoch[64 blocks] u32 | err u32 ]
+//   [ control (32 KiB): flag[2][128 blocks][8 ranks] u32 | flag2 (same) | epoch u32 | done u32 | err u32 ]
 //   [ data parity 0 (cap bytes) ][ data parity 1 (cap bytes) ][ reduced parity 0 ][ reduced parity 1 ]
 //
-// Call e (per block b, e = epoch[b] + 1, parity p = e & 1):
+// Call e (e = epoch + 1, parity p = e & 1, the same for every block of the call):
 //   1. block b copies its slice of the input into its OWN data[p];
 //   2. system-scope release: flag[p][b][rank] = e stored into EVERY peer's control
 //      block (each xGMI link carries one 4-byte write);
@@ -16,10 +16,15 @@
 //      fp32 in fixed rank order (bitwise identical on every rank), writes `out`.
 // Double-buffering by parity makes an end barrier unnecessary: rank r can only
 // rewrite data[p] at call e+2 after every peer passed call e+1's barrier, i.e.
-// finished reading call e.  The epoch lives in device memory (each block bumps
-// its own counter), so the kernel takes no per-call arguments and a captured
-// hipGraph replays it correctly.  Every spin has a bounded budget: a missing
-// peer sets `err` and the kernel drains instead of hanging the GPU.
+// finished reading call e (kernels of one stream are ordered, so once ANY block of rank r's call
+// e + 1 saw a peer's e + 1 flag, that peer's whole call-e kernel is done).  This needs every block
+// of a call to use the same parity whatever partition the call uses (one-shot and two-shot slice
+// the buffer differently, and the block count follows the message size): the epoch is ONE device
+// counter per rank, advanced by the last block of each call to finish (per-block epochs
+// diverged when consecutive calls used different block counts, so a block could reuse the parity
+// a peer was still reading).  It lives in device memory, so the kernel takes no per-call arguments
+// and a captured hipGraph replays it correctly.  Every spin has a bounded budget: a missing peer
+// sets `err` and the kernel drains instead of hanging the GPU.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -47,6 +52,16 @@ __device__ __forceinline__ uint32_t rne_bf16(float f) {
   return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
 }
 
+// The last block of a call to finish advances the rank's epoch (the next call is the next kernel on
+// the stream: every one of its blocks reads the new value).
+__device__ __forceinline__ void end_call(ArCtl* ctl, uint32_t e) {
+  const uint32_t d = __hip_atomic_fetch_add(&ctl->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (d + 1u == gridDim.x) {
+    __hip_atomic_store(&ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ctl->epoch, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // BF16 = 1: bf16 elements (8 per 16-byte vector); 0: fp32 (4 per vector).
 template <int BF16>
 __global__ void __launch_bounds__(512) custom_ar_kernel(const u32x4v* __restrict__ in, u32x4v* __restrict__ out,
@@ -56,7 +71,7 @@ __global__ void __launch_bounds__(512) custom_ar_kernel(const u32x4v* __restrict
   char* mine = peers.base[rank];
   ArCtl* ctl = reinterpret_cast<ArCtl*>(mine);
   __shared__ uint32_t s_epoch;
-  if (threadIdx.x == 0) s_epoch = __hip_atomic_load(&ctl->epoch[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  if (threadIdx.x == 0) s_epoch = __hip_atomic_load(&ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   __syncthreads();
   const uint32_t e = s_epoch;
   const int p = (int)(e & 1u);
@@ -105,7 +120,7 @@ __global__ void __launch_bounds__(512) custom_ar_kernel(const u32x4v* __restrict
     out[i] = o;
   }
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(&ctl->epoch[b], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) end_call(ctl, e);
 }
 
 // Two-shot form for bandwidth-bound messages (a TP prefill all-reduce: 624 x 4096 bf16 = 5 MB per
@@ -127,7 +142,7 @@ __global__ void __launch_bounds__(512) custom_ar2_kernel(const u32x4v* __restric
   char* mine = peers.base[rank];
   ArCtl* ctl = reinterpret_cast<ArCtl*>(mine);
   __shared__ uint32_t s_epoch;
-  if (threadIdx.x == 0) s_epoch = __hip_atomic_load(&ctl->epoch[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  if (threadIdx.x == 0) s_epoch = __hip_atomic_load(&ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   __syncthreads();
   const uint32_t e = s_epoch;
   const int p = (int)(e & 1u);
@@ -203,7 +218,7 @@ __global__ void __launch_bounds__(512) custom_ar2_kernel(const u32x4v* __restric
     for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) out[i] = src[i];
   }
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(&ctl->epoch[b], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) end_call(ctl, e);
 }
 
 hipError_t custom_all_reduce_2shot(const void* in, void* out, const ArPeers& peers, int rank, int world,
@@ -212,7 +227,9 @@ hipError_t custom_all_reduce_2shot(const void* in, void* out, const ArPeers& pee
   if (bytes % 16 != 0 || bytes > cap_bytes) return hipErrorInvalidValue;
   const int64_t nvec = bytes / 16;
   if (nvec == 0) return hipSuccess;
-  int64_t blocks = (nvec + 2047) / 2048;      // >= 4 vectors per thread per sub-slice at n = 8
+  // >= 2 vectors per thread per sub-slice at n = 8: up to 128 workgroups keep more remote reads in
+  // flight over the 7 links (a 5 MB prefill message: 128 x 40 KB)
+  int64_t blocks = (nvec + 1023) / 1024;
   if (blocks > AR_MAX_BLOCKS) blocks = AR_MAX_BLOCKS;
   const int64_t per = (nvec + blocks - 1) / blocks;
   blocks = (nvec + per - 1) / per;

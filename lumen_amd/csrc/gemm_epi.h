@@ -26,10 +26,6 @@ struct GemmEpi {
   int glu;                   // SwiGLU: columns interleaved [gate 8 | up 8] per 16; writes silu(g) * u to
                              // column n/2 .. n/2+8 of C (C has N/2 columns)
   int64_t* dbg;              // profiling only: per-workgroup s_memrealtime stamps (null in production)
-  // LayerNorm statistics of the OUTPUT rows (direct-store ping-pong kernel, residual epilogue only):
-  // per row, N / 64 partials (mean, M2) over 64 columns each, of the bf16 values stored; finished by
-  // ln_part_finalize into ln_row_stats' (rstd, -mean * rstd) -- the next LayerNorm without re-reading C
-  float* ln_part;
   int64_t split_koff;        // split-K launches (gridDim.y = splits): A, W advance by y * split_koff
   int64_t split_cstride;     // elements; C (fp32 slabs) advances by y * split_cstride
   // ---- decode (skinny) GEMMs only: RMSNorm folded into the projection.  gamma is folded

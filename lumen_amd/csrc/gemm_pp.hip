@@ -40,14 +40,14 @@ __device__ __forceinline__ void pp_barrier() {
 // Direct-store epilogue (DS kernels): the lane holds row m0 + qm*128 + wm*64 + i*16 + (lane & 15),
 // columns n0 + qn*128 + wn*32 + 8*(lane >> 4) + [0, 8) in acc[qm][qn][i][0..1][0..3]; 16 passes of one
 // 16-byte store each.  Bias / residual / LN-fold operands are loaded up front (residual RD passes ahead).
-template <bool WT, int FK, int RDD = LUMEN_GEMM_RES_PREFETCH>
+template <bool WT, int FK>
 __device__ __forceinline__ void pp_epilogue_direct(const f32x4_t (&acc)[2][2][4][2], int m0, int n0, int M, int N,
                                                    void* __restrict__ C, int64_t ldc, const GemmEpi& ep, int wm,
                                                    int wn, int lane, const float* aff_lds = nullptr) {
   constexpr bool FL = FK == 5;
   constexpr bool fast = FK > 0 && !FL;
   constexpr bool FB = fast && ((FK - 1) & 1), FR = fast && ((FK - 1) & 2);
-  constexpr int RD = RDD;   // residual passes in flight (16: every residual load issued before the first store)
+  constexpr int RD = LUMEN_GEMM_RES_PREFETCH;   // residual passes in flight
   const __amdgpu_buffer_rsrc_t crs = c_rsrc(C);
   const int fr = lane & 15, fc = lane >> 4;
   auto col_of = [&](int qn) { return n0 + qn * 128 + wn * 32 + fc * 8; };
@@ -105,7 +105,6 @@ __device__ __forceinline__ void pp_epilogue_direct(const f32x4_t (&acc)[2][2][4]
       }
     }
   }
-  float keep[FR ? 8 : 1];   // LN partials: the row's qn = 0 values until its qn = 1 pass
   Unroll<0, 16>::run([&](const int p) __attribute__((always_inline)) {
     const int qm = p >> 3, i = (p >> 1) & 3, qn = p & 1;
     float v[8];
@@ -129,41 +128,7 @@ __device__ __forceinline__ void pp_epilogue_direct(const f32x4_t (&acc)[2][2][4]
         for (int q = 0; q < 8; ++q) v[q] += f[q];
         if (p + RD < 16) rz[p % RD] = *(const u32x4_t*)(ep.residual + (int64_t)row_of(p + RD) * ep.ldr + col_of((p + RD) & 1));
       }
-      const u32x4_t pk = pack8(v);
-      st16<WT>(C, crs, ((int64_t)m * ldc + n) * 2, pk);
-      if constexpr (FR) {
-        if (ep.ln_part) {
-          // (mean, M2) of the 64 stored values of row m in this wave's columns: 16 per lane (qn = 0, 1,
-          // two-pass), then Chan merges over the 4 lanes of the row (equal counts: delta^2 * n / 2)
-          float r8[8];
-          unpack8(pk, r8);
-          if (qn == 0) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) keep[q] = r8[q];
-          } else {
-            float s = 0.f;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) s += keep[q] + r8[q];
-            float mean = s * (1.f / 16.f), m2 = 0.f;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              const float d0 = keep[q] - mean, d1 = r8[q] - mean;
-              m2 += d0 * d0 + d1 * d1;
-            }
-#pragma unroll
-            for (int o = 16; o <= 32; o *= 2) {
-              const float mb = __shfl_xor(mean, o, 64), m2b = __shfl_xor(m2, o, 64);
-              const float d = mb - mean;
-              m2 = (m2 + m2b) + d * d * (float)(o / 2);
-              mean = 0.5f * (mean + mb);
-            }
-            if (fc == 0) {
-              const int nslot = N >> 6, slot = (n0 >> 8) * 4 + wn;
-              *(float2*)(ep.ln_part + ((int64_t)m * nslot + slot) * 2) = make_float2(mean, m2);
-            }
-          }
-        }
-      }
+      st16<WT>(C, crs, ((int64_t)m * ldc + n) * 2, pack8(v));
     } else {
       epi_store8_t<WT>(v, m, n, M, N, C, ldc, ep, crs);
     }
@@ -182,7 +147,7 @@ __device__ __forceinline__ void vm_wait_n() {
 // PRIO 1: static priority 1 for the lagging group (MI355X_MICROARCH "Two waves per SIMD" 4).
 // DS: direct-store epilogue (gemm_epi.h swzb): transposed accumulators, 16-byte stores straight
 // from registers, no LDS staging (no SwiGLU).
-template <bool WT, int FK, int PRIO, int NPH, bool DS = false, int RDD = LUMEN_GEMM_RES_PREFETCH>
+template <bool WT, int FK, int PRIO, int NPH, bool DS = false>
 __global__ void __launch_bounds__(512)
 gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                void* __restrict__ C, int64_t ldc, int M, int N, int K, GemmEpi ep, int group_m) {
@@ -405,7 +370,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   const int64_t t_loop = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
 
   if constexpr (DS) {
-    pp_epilogue_direct<WT, FK, RDD>(acc, m0, n0, M, N, C, ldc, ep, wm, wn, lane, PRE ? aff_lds : nullptr);
+    pp_epilogue_direct<WT, FK>(acc, m0, n0, M, N, C, ldc, ep, wm, wn, lane, PRE ? aff_lds : nullptr);
   } else {
   // ---- epilogue: per-wave 16-row slabs through LDS (bias / residual prefetched on the FAST path)
   constexpr int LDSTR = 68;
@@ -492,18 +457,18 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   }
 }
 
-template <bool WT, int FK, int PRIO, int NPH, bool DS = false, int RDD = LUMEN_GEMM_RES_PREFETCH>
+template <bool WT, int FK, int PRIO, int NPH, bool DS = false>
 static void launch_pp_t(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
                         int N, int K, const GemmEpi& ep, int group_m, hipStream_t stream, int splits = 1) {
   const dim3 tiles(((M + 255) / 256) * ((N + 255) / 256), splits);
   const size_t lds = 2 * G_BUF + (DS && FK == 5 ? 4096 : 0);   // + the LN-fold affine stage
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm_pp_kernel<WT, FK, PRIO, NPH, DS, RDD>,
+    hipFuncSetAttribute((const void*)gemm_pp_kernel<WT, FK, PRIO, NPH, DS>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<WT, FK, PRIO, NPH, DS, RDD>), dim3(tiles), dim3(512), lds, stream, A, lda, W, ldw,
+  hipLaunchKernelGGL((gemm_pp_kernel<WT, FK, PRIO, NPH, DS>), dim3(tiles), dim3(512), lds, stream, A, lda, W, ldw,
                      C, ldc, M, N, K, ep, group_m);
 }
 
@@ -514,21 +479,9 @@ static void launch_pp_fk(const uint16_t* A, int64_t lda, const uint16_t* W, int6
   // write-through stores measured slower on every shape (profiles/r2_gemm_pp_v1.jsonl): not instantiated
   (void)wt;
   if (ds) {   // direct-store epilogue: the production two-phase, static-priority form only
-    // LUMEN_PP_DS_WT=1: write-through (sc1) C stores (A/B knob, profiles/r5_gemm_pp_ds_v1.txt)
-    static const bool ds_wt = [] {
-      const char* e = getenv("LUMEN_PP_DS_WT");
-      return e != nullptr && e[0] == '1';
-    }();
-    // LUMEN_PP_DS_RD = 8 / 16: residual passes in flight in the residual epilogues (A/B knob)
-    static const int ds_rd = [] {
-      const char* e = getenv("LUMEN_PP_DS_RD");
-      return e ? atoi(e) : 0;
-    }();
-    constexpr bool RES = FK == 3 || FK == 4;
-    if (ds_wt) launch_pp_t<true, FK, 1, 2, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
-    else if (RES && ds_rd == 8) launch_pp_t<false, FK, 1, 2, true, 8>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
-    else if (RES && ds_rd == 16) launch_pp_t<false, FK, 1, 2, true, 16>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
-    else launch_pp_t<false, FK, 1, 2, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
+    // (r5 A/Bs, profiles/r5_gemm_pp_ds_v1.txt: write-through C stores and 8 / 16 residual rows in flight
+    // both lost to plain stores with 4 rows in flight; those variants were removed in r6)
+    launch_pp_t<false, FK, 1, 2, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);
     return;
   }
   if (two) {
@@ -844,13 +797,9 @@ template <int FK, int PRIO, bool DS = false>
 static void launch_pps_t(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, void* C, int64_t ldc, int M,
                          int N, int K, const GemmEpi& ep, int group_m, hipStream_t stream) {
   const int tiles = (M / 256) * (N / 256);
-  // LUMEN_PPS_TILES_PER_WG = T > 0: ceil(tiles / T) workgroups of ~T tiles each (dispatched as CUs free up,
-  // so kernels of other streams interleave) instead of one workgroup per CU
-  static const int tpw = [] {
-    const char* e = getenv("LUMEN_PPS_TILES_PER_WG");
-    return e ? atoi(e) : 0;
-  }();
-  const int grid = tpw > 0 ? (tiles + tpw - 1) / tpw : (tiles < pp_num_cus() ? tiles : pp_num_cus());
+  // one workgroup per CU (r5: fewer tiles per workgroup, dispatched as CUs free up, lost in the 2-stream
+  // tower -- a workgroup's next tile shares no L2 panels with its neighbours', profiles/r5_gemm_pp_ds_v1.txt)
+  const int grid = tiles < pp_num_cus() ? tiles : pp_num_cus();
   const int lds = DS ? 2 * G_BUF : PPS_LDS;
   static bool attr_set = false;
   if (!attr_set) {
@@ -868,13 +817,6 @@ hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ld
   if (variant >= 8) {
     variant -= 2;
     ds = !ep.glu;
-  }
-  if (ep.ln_part) {   // row-statistics partials: the direct-store, non-persistent, residual FAST epilogue only
-    const int64_t extent = (int64_t)M * ldc * 2;
-    const bool ok = ds && !(variant & 1) && M % 256 == 0 && N % 256 == 0 && ep.residual && !ep.row_aff &&
-                    !ep.out_group && !ep.table && !ep.prelu && !ep.post_act && !ep.out_f32 &&
-                    !(ep.bias && ep.bias_f32) && extent < ((int64_t)1 << 31);
-    if (!ok) return hipErrorNotSupported;
   }
   if (variant & 1) {
     // persistent form: interior tiles only, 32-bit in-tile offsets, >= 2 K-tiles

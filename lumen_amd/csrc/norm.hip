@@ -280,34 +280,6 @@ ln_row_stats_kernel(const uint16_t* __restrict__ x, int64_t x_stride, float* __r
   }
 }
 
-// LayerNorm row statistics from the (mean, M2) partials a residual GEMM wrote (GemmEpi::ln_part, 64 columns
-// each): Chan's merge with equal counts, M2 = sum M2_i + 64 * sum (mean_i - mean)^2, then ln_row_stats' output.
-__global__ void __launch_bounds__(256)
-ln_part_finalize_kernel(const float* __restrict__ part, int nslot, int rows, int D, float eps, float* __restrict__ out) {
-  const int row = blockIdx.x * 256 + threadIdx.x;
-  if (row >= rows) return;
-  const float2* p = (const float2*)(part + (int64_t)row * nslot * 2);
-  float s = 0.f;
-  for (int i = 0; i < nslot; ++i) s += p[i].x;
-  const float mean = s / (float)nslot;
-  float m2 = 0.f, dd = 0.f;
-  for (int i = 0; i < nslot; ++i) {
-    const float2 t = p[i];
-    const float d = t.x - mean;
-    m2 += t.y;
-    dd += d * d;
-  }
-  const float rstd = rsqrtf((m2 + 64.f * dd) / (float)D + eps);
-  *(float2*)(out + 2 * (int64_t)row) = make_float2(rstd, -mean * rstd);
-}
-
-hipError_t ln_part_finalize(const float* part, int rows, int D, float eps, float* out, hipStream_t stream) {
-  if (D % 64 != 0 || rows <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ln_part_finalize_kernel, dim3((rows + 255) / 256), dim3(256), 0, stream, part, D / 64, rows, D,
-                     eps, out);
-  return hipGetLastError();
-}
-
 hipError_t ln_row_stats(const uint16_t* x, int64_t x_stride, float* out, int rows, int D, float eps,
                         hipStream_t stream, uint8_t* q8, int64_t ldq, uint8_t* qs, int64_t ldqs) {
   if (D % 8 != 0 || D > 64 * 8 * 8 || rows <= 0 || (q8 != nullptr && D % 128 != 0)) return hipErrorInvalidValue;

@@ -50,7 +50,6 @@ hipError_t l2norm_f32(float* x, int rows, int D, float eps, hipStream_t stream);
 hipError_t ln_row_stats(const uint16_t* x, int64_t x_stride, float* out, int rows, int D, float eps,
                         hipStream_t stream, uint8_t* q8 = nullptr, int64_t ldq = 0, uint8_t* qs = nullptr,
                         int64_t ldqs = 0);
-hipError_t ln_part_finalize(const float* part, int rows, int D, float eps, float* out, hipStream_t stream);
 hipError_t cls_fill(uint16_t* x, int64_t seq_stride, const uint16_t* cls, const uint16_t* pos, int B, int D,
                     hipStream_t stream);
 hipError_t embed_gather(const int64_t* ids, const uint16_t* table, const uint16_t* pos, int S, uint16_t* out,
@@ -120,7 +119,7 @@ void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tens
           const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& table,
           int64_t table_period, int64_t table_offset, int64_t act, double alpha, at::Tensor out,
           int64_t out_group, int64_t out_group_stride, int64_t out_row_offset, int64_t tile,
-          const c10::optional<at::Tensor>& prelu, int64_t glu, const c10::optional<at::Tensor>& ln_part) {
+          const c10::optional<at::Tensor>& prelu, int64_t glu) {
   check_bf16_rows(a, "a");
   check_bf16_rows(w, "w");
   const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
@@ -168,15 +167,6 @@ void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tens
     ep.prelu = bf(*prelu);
   }
   ep.dbg = g_gemm_dbg;
-  if (ln_part.has_value() && ln_part->defined()) {
-    // LayerNorm partials of the output rows: the direct-store ping-pong residual epilogue (gemm_pp errors out
-    // on any other path, so a caller that asked for them never silently gets none)
-    TORCH_CHECK(ln_part->is_cuda() && ln_part->scalar_type() == at::kFloat && ln_part->is_contiguous() &&
-                    ln_part->numel() == M * (N / 64) * 2 && N % 64 == 0,
-                "gemm: ln_part must be fp32 [M, N / 64, 2]");
-    TORCH_CHECK(tile >= 1000 && (tile / 100) % 10 == 8 && tile % 10 == 9, "gemm: ln_part needs a direct-store ping-pong tile code (1809..1899)");
-    ep.ln_part = ln_part->data_ptr<float>();
-  }
   const at::DeviceGuard guard(a.device());
   // decode-shaped GEMMs (M <= 32): bandwidth-bound split-K kernel (tile -1 = auto, 9 = force)
   if ((tile == -1 || tile == 9) && M <= 32 && M > 0) {
@@ -587,18 +577,6 @@ void rms_norm_quant_fp8(const at::Tensor& x, const c10::optional<at::Tensor>& ad
                                             scale.data_ptr<float>(), (int)M, (int)K, cur_stream()));
 }
 
-// LayerNorm row statistics [rows, 2] = (rstd, -mean * rstd) from a residual GEMM's ln_part partials
-void ln_part_finalize(const at::Tensor& part, at::Tensor out, double eps) {
-  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3 &&
-                  part.size(2) == 2, "ln_part_finalize: part fp32 [rows, D / 64, 2]");
-  const int64_t rows = part.size(0), D = part.size(1) * 64;
-  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() >= 2 * rows,
-              "ln_part_finalize: out fp32 [rows, 2]");
-  const at::DeviceGuard guard(part.device());
-  LUMEN_CHECK_HIP(lumen::ln_part_finalize(part.data_ptr<float>(), (int)rows, (int)D, (float)eps,
-                                          out.data_ptr<float>(), cur_stream()));
-}
-
 // profiling: route per-workgroup timestamps of the gemm / gemm_lnf ops into dbg [wg, 4] (empty: off)
 void gemm_set_dbg(const at::Tensor& dbg) {
   TORCH_CHECK(dbg.is_cuda() && dbg.scalar_type() == at::kLong && dbg.is_contiguous(), "gemm_set_dbg: int64");
@@ -983,8 +961,7 @@ void pixel_shuffle_up(const at::Tensor& y, at::Tensor out, int64_t factor) {
 TORCH_LIBRARY(lumen, m) {
   m.def("gemm(Tensor a, Tensor w, Tensor? bias, Tensor? residual, Tensor? table, int table_period, "
         "int table_offset, int act, float alpha, Tensor(o!) out, int out_group, int out_group_stride, "
-        "int out_row_offset, int tile, Tensor? prelu=None, int glu=0, Tensor(p!)? ln_part=None) -> ()");
-  m.def("ln_part_finalize(Tensor part, Tensor(o!) out, float eps) -> ()");
+        "int out_row_offset, int tile, Tensor? prelu=None, int glu=0) -> ()");
   m.def("norm(Tensor x, Tensor? row_idx, Tensor? add, Tensor(r!)? resid_out, Tensor w, Tensor? b, "
         "Tensor(o!) out, float eps, int mode) -> ()");
   m.def("l2norm_(Tensor(a!) x, float eps) -> ()");
@@ -1034,7 +1011,6 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("l2norm_", &l2norm_);
   m.impl("gemm_lnf", &gemm_lnf);
   m.impl("ln_row_stats", &ln_row_stats);
-  m.impl("ln_part_finalize", &ln_part_finalize);
   m.impl("gemm_probe", &gemm_probe);
   m.impl("gemm_set_dbg", &gemm_set_dbg);
   m.impl("gemm_w8", &gemm_w8);

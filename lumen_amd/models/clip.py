@@ -20,7 +20,6 @@ from __future__ import annotations
 import logging
 import math
 import os
-import threading
 from dataclasses import dataclass, field, asdict
 from typing import Optional
 
@@ -249,20 +248,11 @@ def _block_steps(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, 
     # the out-proj / fc2 residual is added in the GEMM epilogue (the MFMA GEMM adds the prefetched
     # residual rows before its single bf16 rounding); a separate add + LayerNorm pass measured
     # 5837 vs 5951 img/s on ViT-L/14 b512 (profiles/r2_bench_resid_paths_v1.txt)
-    # the residual GEMMs (out-proj, fc2) also leave the next LayerNorm's row statistics as partials over 64
-    # columns (direct-store tile codes): one small pass over 128 B per row instead of re-reading x
     rt = tile if res_tile is None else res_tile
-    part = None
-    if fold and _RES_LN and ops.res_ln_ok(T, W, rt, blocks[0].out_b if len(blocks) else None):
-        part = torch.empty((T, W // 64, 2), device=x.device, dtype=torch.float32)
-    have_part = False
     for i, blk in enumerate(blocks):
         if fold:
             qw, qa, fw, fa = blk.lnf()
-            if have_part:
-                ops.ln_part_finalize(part, eps, out=st)
-            else:
-                ops.ln_row_stats(x, eps, out=st)
+            ops.ln_row_stats(x, eps, out=st)
             qkv = ops.linear_lnf(x, qw, qa, st, tile=tile)
         else:
             ops.layer_norm(x, blk.ln1_w, blk.ln1_b, eps, out=h)
@@ -271,19 +261,14 @@ def _block_steps(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, 
         ops.attention(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], causal=causal, kv_len=kv_len,
                       out=o.view(B, S, heads, D))
         del qkv, q5
-        ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x, tile=rt, ln_part=part)
+        ops.linear(o, blk.out_w, blk.out_b, residual=x, out=x, tile=rt)
         if fold:
-            if part is not None:
-                ops.ln_part_finalize(part, eps, out=st)
-            else:
-                ops.ln_row_stats(x, eps, out=st)
+            ops.ln_row_stats(x, eps, out=st)
             f = ops.linear_lnf(x, fw, fa, st, act=act, tile=tile)
         else:
             ops.layer_norm(x, blk.ln2_w, blk.ln2_b, eps, out=h)
             f = ops.linear(h, blk.fc1_w, blk.fc1_b, act=act, tile=tile)
-        last = i == len(blocks) - 1
-        ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x, tile=rt, ln_part=None if last else part)
-        have_part = part is not None and not last
+        ops.linear(f, blk.fc2_w, blk.fc2_b, residual=x, out=x, tile=rt)
         del f
         yield i
 
@@ -346,17 +331,13 @@ def run_blocks(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, ep
 # tail pass (tile code 1609: ping-pong 256x256, non-persistent, no tail split) and attention /
 # LayerNorm of one half overlap GEMM tails of the other.
 _VIT_MICRO = int(os.environ.get("LUMEN_VIT_MICRO", "2"))
-# serving-sized image batches (<= LUMEN_CLIP_GRAPH_MAX_B) replay the tower from a hipGraph captured per
-# batch bucket (multiples of 8): one launch instead of ~200 Python-dispatched kernels per batch
-# (opt-in: serving A/B 2,897 vs 3,052 img/s eager -- the small-batch tower is GPU-bound, and the graph's
-# static buffers serialise the engine's two batch loops; profiles/r5_clip_graph_serve_v1.txt)
-_CLIP_GRAPH = os.environ.get("LUMEN_CLIP_GRAPH", "0") == "1"
-_CLIP_GRAPH_MAX_B = int(os.environ.get("LUMEN_CLIP_GRAPH_MAX_B", "64"))
+# (r5's per-bucket hipGraph replay of serving-sized batches lost its serving A/B, 2,897 vs 3,052 img/s
+# eager -- the small-batch tower is GPU-bound and the graph's static buffers serialise the engine's two
+# batch loops, profiles/r5_clip_graph_serve_v1.txt -- and was removed in r6)
 log = logging.getLogger(__name__)
 _LN_FOLD = True   # GPU blocks: LayerNorms folded into qkv / fc1 (see _block_steps)
-# LayerNorm partials from the residual GEMMs (opt-in: in the 2-stream tower the row-statistics pass already
-# hides behind the other stream's GEMMs -- 6248 vs 6251-6268 img/s, profiles/r5_gemm_pp_ds_v1.txt)
-_RES_LN = os.environ.get("LUMEN_RES_LN", "0") == "1"
+# (r5's LayerNorm partials from the residual GEMMs -- no gain: the row-statistics pass already hides behind
+# the other stream's GEMMs, 6248 vs 6251-6268 img/s, profiles/r5_gemm_pp_ds_v1.txt -- were removed in r6)
 # ping-pong 256x256, 2 phases per K-tile + priority, no tail split (r2: group_m 2 = 1629 vs 1609 / 1689:
 # 6209-6222 vs 6203-6204 / 6129-6130 img/s, profiles/r2_vit_micro_streams_v1.txt); r5: the direct-store
 # epilogue (1849: 6287-6340 vs 1629 6225-6227 img/s same box, the persistent forms lose in the 2-stream
@@ -384,10 +365,12 @@ def _micro_streams(dev: torch.device, n: int):
 
 def run_blocks_micro(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float,
                      causal: bool = False, min_rows: Optional[int] = None, tile: Optional[int] = None,
-                     res_tile: Optional[int] = None) -> torch.Tensor:
+                     res_tile: Optional[int] = None, streams: Optional[list] = None) -> torch.Tensor:
     """run_blocks over micro-batches on separate streams (falls back to run_blocks when the
-    batch is too small to split or x is on the CPU)."""
-    n = _VIT_MICRO
+    batch is too small to split or x is on the CPU).  ``streams``: the micro-batch streams to use
+    (a graph capture passes its own private ones: the shared module-level streams may at the same
+    time carry another thread's eager tower, whose kernels would join the capture -- ADVICE r5)."""
+    n = len(streams) if streams else _VIT_MICRO
     min_rows = _VIT_MICRO_MIN_ROWS if min_rows is None else min_rows
     if not x.is_cuda or n <= 1 or B < n or (B // n) * S < min_rows:
         return run_blocks(x, blocks, B, S, heads, act, eps, causal=causal)
@@ -401,7 +384,7 @@ def run_blocks_micro(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: s
         # micro-batch's stream would compute them while the second's GEMMs already read the cache
         for blk in blocks:
             blk.lnf()
-    streams = _micro_streams(x.device, n)
+    streams = streams or _micro_streams(x.device, n)
     bounds = [B * i // n for i in range(n + 1)]
     gens = []
     for i, st in enumerate(streams):
@@ -445,20 +428,8 @@ class VisionTower(nn.Module):
         self.ln_post_w = nn.Parameter(torch.ones(W, **kw), requires_grad=False)
         self.ln_post_b = nn.Parameter(torch.zeros(W, **kw), requires_grad=False)
         self.proj_w = nn.Parameter(torch.zeros(embed_dim, W, **kw), requires_grad=False)  # [E, W]
-        self._graphs: dict = {}
-        self._graph_lock = threading.Lock()
-
-    def invalidate_graphs(self) -> None:
-        """Drop the captured tower graphs (they hold the weights' and folded weights' addresses)."""
-        with self._graph_lock:
-            self._graphs.clear()
-
-    def _apply(self, fn, *args, **kwargs):   # .to() / .half() / ... re-home the parameters: recapture
-        self.invalidate_graphs()
-        return super()._apply(fn, *args, **kwargs)
 
     def random_init(self, gen: torch.Generator):
-        self.invalidate_graphs()
         W = self.cfg.width
         s = W ** -0.5
         w = torch.randn(W, self.kdim, generator=gen) * (self.kdim ** -0.5)
@@ -473,48 +444,7 @@ class VisionTower(nn.Module):
     @torch.no_grad()
     def forward_patches(self, patches: torch.Tensor, B: int) -> torch.Tensor:
         """patches [B*P, kpad] (bf16) -> L2-normalised fp32 embeddings [B, E]."""
-        if _CLIP_GRAPH and patches.is_cuda and 0 < B <= _CLIP_GRAPH_MAX_B and \
-                not torch.cuda.is_current_stream_capturing():
-            r = self._graph_forward(patches, B)
-            if r is not None:
-                return r
         return self._forward_patches(patches, B)
-
-    def _graph_forward(self, patches: torch.Tensor, B: int) -> Optional[torch.Tensor]:
-        """The tower replayed from the graph of B's bucket (B rounded up to 8; the pad images' rows
-        keep whatever the bucket's input held: finite, their embeddings are dropped).  Copy-in, replay
-        and copy-out run under the lock: the serving engine's batch loops share the static buffers."""
-        Bp = -(-B // 8) * 8
-        P = self.num_patches
-        key = (Bp, patches.shape[1], patches.dtype, patches.device)
-        with self._graph_lock:
-            ent = self._graphs.get(key)
-            if ent is None:
-                ent = self._capture(Bp, patches)
-                self._graphs[key] = ent
-            if ent is False:
-                return None
-            ent["in"][:B * P].copy_(patches)
-            ent["g"].replay()
-            return ent["out"][:B].clone()
-
-    def _capture(self, Bp: int, patches: torch.Tensor):
-        try:
-            static_in = torch.zeros((Bp * self.num_patches, patches.shape[1]), device=patches.device,
-                                    dtype=patches.dtype)
-            cur = torch.cuda.current_stream(patches.device)
-            side = torch.cuda.Stream(device=patches.device)
-            side.wait_stream(cur)
-            with torch.cuda.stream(side):
-                self._forward_patches(static_in, Bp)     # warm-up: folded weights, kernel attributes, workspaces
-            cur.wait_stream(side)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):   # the other batch loop keeps launching
-                static_out = self._forward_patches(static_in, Bp)
-            return {"g": g, "in": static_in, "out": static_out}
-        except Exception as e:  # noqa: BLE001 - an op that cannot be captured: eager launches for this bucket
-            log.warning("CLIP image tower graph capture failed (%s); eager launches", e)
-            return False
 
     def _forward_patches(self, patches: torch.Tensor, B: int) -> torch.Tensor:
         cfg = self.cfg
@@ -750,8 +680,6 @@ class CLIPModel(nn.Module):
     # ---- weight ingestion
     def load_state_dict_any(self, sd: dict) -> None:
         """Load OpenCLIP / OpenAI (``visual.*``), HF ``CLIPModel`` or HF ``ChineseCLIPModel`` naming."""
-        if hasattr(self.visual, "invalidate_graphs"):
-            self.visual.invalidate_graphs()
         if self.cfg.text_arch == "bert" and any(k.startswith("text_model.encoder.layer.") for k in sd):
             _load_bert_text(self.text, sd) if self.text is not None else None
             sd = {k: v for k, v in sd.items() if not k.startswith("text_model.") and k != "text_projection.weight"}

@@ -44,6 +44,10 @@ _F8_MIN_ROWS = 33
 _FUSED_DECODE_NORM = True
 # decode: RoPE + current-token KV-cache write inside the paged attention kernel (no rope_kv launch)
 _FUSED_DECODE_ROPE = True
+# TP prefill from this many rows up: the rows run as two halves whose row-parallel all-reduces go
+# to a communication stream, so half A's all-reduce overlaps half B's GEMMs (624-token
+# LLaVA prompts at TP 8: 64 x 5 MB all-reduces on the time-to-first-token path)
+_TP_OVERLAP_MIN_ROWS = 256
 # (r4's fused MX prefill chain -- block-scaled activations from the epilogues, 6 launches per
 # layer -- lost its A/B to this per-token chain, 13.12 vs 12.79 ms TTFT, profiles/r4_mx_chain_ab_v1.txt,
 # and was removed in r5; the MX W8A8 chain stays for the ViT tower, models/clip.py:run_blocks_mx)
@@ -327,6 +331,35 @@ class LLM(nn.Module):
             dist.all_reduce(t, group=self.tp.group)
         return t
 
+    def _comm_stream(self, dev: torch.device):
+        """The TP group's communication stream (private: graph-safe, never PyTorch's pool)."""
+        cs = getattr(self, "_cstream", None)
+        if cs is None or cs.device != dev:
+            cs = self._cstream = ops.private_stream(dev)
+        return cs
+
+    def _all_reduce_async(self, t: torch.Tensor):
+        """Start the all-reduce of ``t`` (in place) on the communication stream once the work issued
+        so far on the current stream (t's producer) is done; returns the event to wait for before
+        reading ``t`` (None: it completed synchronously, e.g. on the CPU)."""
+        if not t.is_cuda:
+            self._all_reduce(t)
+            return None
+        cur = torch.cuda.current_stream(t.device)
+        cs = self._comm_stream(t.device)
+        cs.wait_stream(cur)
+        with torch.cuda.stream(cs):
+            self._all_reduce(t)
+        ev = torch.cuda.Event()
+        ev.record(cs)
+        t.record_stream(cs)
+        return ev
+
+    @staticmethod
+    def _wait(ev) -> None:
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+
     # ------------------------------------------------------------------ pieces
     def embed_tokens(self, ids: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """ids [T] -> [T, hidden] (vocab-parallel: masked local lookup + all-reduce)."""
@@ -350,6 +383,8 @@ class LLM(nn.Module):
         # wrote (TP keeps the norm kernel: it also adds the all-reduced row-parallel partial)
         if x.is_cuda and T <= 32 and not tp and self.norm_folded:
             return self._layers_dec(x, pos, slots, kv, attn_fn)
+        if tp and T >= _TP_OVERLAP_MIN_ROWS:
+            return self._layers_tp_overlap(x, pos, slots, kv, attn_fn, f8=False)
         pending: Optional[torch.Tensor] = None   # TP: row-parallel partial to add before the next norm
         for i, l in enumerate(self.layers):
             if pending is None:
@@ -407,6 +442,8 @@ class LLM(nn.Module):
         h8 = torch.empty((T, x.shape[1]), device=dev, dtype=torch.float8_e4m3fn)
         hs = torch.empty((T,), device=dev, dtype=torch.float32)
         tp = self.tp.enabled
+        if tp and T >= _TP_OVERLAP_MIN_ROWS:
+            return self._layers_tp_overlap(x, pos, slots, kv, attn_fn, f8=True)
         pending: Optional[torch.Tensor] = None
         for i, l in enumerate(self.layers):
             add = self._all_reduce(pending) if pending is not None else None
@@ -431,6 +468,82 @@ class LLM(nn.Module):
             del qkv, att, a8, g, g8
         if pending is not None:
             x.add_(self._all_reduce(pending))
+        return x
+
+    def _layers_tp_overlap(self, x, pos, slots, kv, attn_fn, f8: bool):
+        """TP prefill with the row-parallel all-reduces off the critical path.  The rows run as two
+        halves A / B through every projection; each half's o / down partial is all-reduced on the
+        communication stream (:meth:`_all_reduce_async`) while the compute stream carries on with
+        the other half:
+
+            o(A) -> AR(o A) | o(B) -> AR(o B) | norm(A) gu(A) down(A) -> AR(down A) | norm(B) ...
+
+        so AR(o A) hides under o(B), AR(o B) under A's MLP, AR(down A) under B's MLP and AR(down B)
+        under the next layer's A norm + qkv.  RoPE and attention run over all rows at once (every
+        query needs the keys of both halves).  Same arithmetic as :meth:`_layers` / :meth:`_layers_f8`
+        row for row (the reductions are per row), so TP results do not depend on the split."""
+        cfg = self.cfg
+        D, eps, T = cfg.head_dim, cfg.rms_eps, x.shape[0]
+        dev = x.device
+        # split on a 64-row boundary (GEMM row tiles), the halves as equal as that allows
+        t0 = max(64, min(T - 64, (T // 2 + 32) // 64 * 64))
+        halves = ((0, t0), (t0, T))
+        if f8:
+            h8 = torch.empty((T, x.shape[1]), device=dev, dtype=torch.float8_e4m3fn)
+            hs = torch.empty((T,), device=dev, dtype=torch.float32)
+        else:
+            h = torch.empty_like(x)
+        pend = [None, None]      # per half: row-parallel partial still to be added to x
+        evs = [None, None]       # per half: its all-reduce's completion event
+
+        def norm(i_half, gamma):
+            a, b = halves[i_half]
+            add = pend[i_half]
+            if add is not None:
+                self._wait(evs[i_half])
+            xs = x[a:b]
+            kw = dict(add=add, resid_out=xs) if add is not None else {}
+            if f8:
+                ops.rms_norm_quant_fp8(xs, gamma, eps, out=h8[a:b], scale=hs[a:b], **kw)
+            else:
+                ops.rms_norm(xs, gamma, eps, out=h[a:b], **kw)
+            pend[i_half] = None
+
+        def lin(i_half, l, name, inp, inp_s=None, **kw):
+            a, b = halves[i_half]
+            if f8:
+                return self._lin8(inp[a:b], inp_s[a:b], l, name, **kw)
+            return self._lin(inp[a:b], l, name, **kw)
+
+        for i, l in enumerate(self.layers):
+            nq = (l.H + 2 * l.Hkv) * D
+            qkv = torch.empty((T, nq), device=dev, dtype=x.dtype)
+            for c, (a, b) in enumerate(halves):
+                norm(c, l.ln1)
+                lin(c, l, "qkv", h8 if f8 else h, hs if f8 else None, bias=l.qkv_b, out=qkv[a:b])
+            kc, vc = (kv.k[i], kv.v[i]) if kv is not None else (None, None)
+            if not getattr(attn_fn, "fuses_rope", False):
+                lops.rope_kv(qkv, pos, self.cos_sin, l.H, l.Hkv, D, slots, kc, vc)
+            att = attn_fn(qkv, l, kc, vc)                            # [T, H*D]
+            if f8:
+                a8, as_ = ops.quant_rows_fp8(att)
+            for c in range(2):
+                pend[c] = lin(c, l, "o", a8 if f8 else att, as_ if f8 else None)
+                evs[c] = self._all_reduce_async(pend[c])
+            for c in range(2):
+                norm(c, l.ln2)
+                a, b = halves[c]
+                g = lin(c, l, "gu", h8 if f8 else h, hs if f8 else None, glu=True)
+                if f8:
+                    g8, gs = ops.quant_rows_fp8(g)
+                    pend[c] = self._lin8(g8, gs, l, "down")
+                else:
+                    pend[c] = self._lin(g, l, "down")
+                evs[c] = self._all_reduce_async(pend[c])
+            del qkv, att
+        for c, (a, b) in enumerate(halves):
+            self._wait(evs[c])
+            x[a:b].add_(pend[c])
         return x
 
     def logits(self, x_rows: torch.Tensor, ssq: Optional[torch.Tensor] = None) -> torch.Tensor:

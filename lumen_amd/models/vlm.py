@@ -242,24 +242,37 @@ class VLM(nn.Module):
                 self._vgraphs[key] = ent
             if ent is False:
                 return None
+            # the lock orders the host-side enqueues only: wait on the device for the previous user's
+            # replay / copy-out (possibly on another stream) before reusing the static buffers
+            cur = torch.cuda.current_stream(pre.device)
+            if ent.get("ev") is not None:
+                cur.wait_event(ent["ev"])
             ent["in"].copy_(pre)
             ent["g"].replay()
             if out is not None:
                 out.copy_(ent["out"])
-                return out
-            return ent["out"].clone()
+            else:
+                out = ent["out"].clone()
+            ent["ev"] = torch.cuda.Event()
+            ent["ev"].record(cur)
+            return out
 
     def _capture(self, pre: torch.Tensor, B: int):
         try:
             static_in = pre.clone()
             cur = torch.cuda.current_stream(pre.device)
-            side = torch.cuda.Stream(device=pre.device)
+            # this model's own capture stream: the split-K tickets / workspaces keyed by the
+            # stream are baked into the graph, so no other graph or eager thread may ever use it
+            if getattr(self, "_cap_stream", None) is None:
+                self._cap_stream = ops.private_stream(pre.device)
+            side = self._cap_stream
             side.wait_stream(cur)
             with torch.cuda.stream(side):
                 self._encode_tower(static_in, B)     # warm-up: weight caches, workspaces, autotune
             cur.wait_stream(side)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):   # other threads keep launching
+            # thread_local: other threads keep launching meanwhile
+            with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
                 static_out = self._encode_tower(static_in, B)
             return {"g": g, "in": static_in, "out": static_out}
         except Exception as e:  # noqa: BLE001 - an op that cannot be captured: eager launches

@@ -26,6 +26,19 @@ ACTS = {
 }
 
 
+def private_stream(device) -> "torch.cuda.Stream":
+    """A HIP stream that nothing else in the process uses (never from PyTorch's recycled pool):
+    kernels key their split-K tickets / workspaces by stream (csrc/workspace.h), and a hipGraph
+    captured on a stream keeps those buffers; a pool stream could later be handed to another
+    thread's eager work, or another model's graph, that would then share them."""
+    d = torch.device(device)
+    idx = d.index if d.index is not None else torch.cuda.current_device()
+    try:
+        return torch.cuda.ExternalStream(int(hip_ops().private_stream(idx)), device=torch.device("cuda", idx))
+    except (AttributeError, RuntimeError):   # extension without the op
+        return torch.cuda.Stream(device=torch.device("cuda", idx))
+
+
 def _act_ref(x: torch.Tensor, act: int) -> torch.Tensor:
     if act == 0:
         return x
@@ -80,7 +93,6 @@ def linear(
     tile: int = -1,
     glu: bool = False,
     w_scale: Optional[torch.Tensor] = None,
-    ln_part: Optional[torch.Tensor] = None,
 ) -> torch.Tensor:
     """y = epi(alpha * x @ w.T): (+bias) -> act -> (+table[m % P + off]) -> (+residual[orow]).
 
@@ -93,10 +105,6 @@ def linear(
     buffer).  ``residual`` is indexed by the *output* row.  ``glu``: the rows of ``w``
     interleave [gate 8 | up 8] per 16 (see :func:`glu_interleave`) and the output is
     silu(gate) * up with N/2 columns (SwiGLU fused into the epilogue).
-
-    ``ln_part`` fp32 [M, N/64, 2]: the residual epilogue also leaves LayerNorm partials of the
-    stored rows (:func:`ln_part_finalize` turns them into :func:`ln_row_stats`' output) -- GPU:
-    direct-store ping-pong tile codes only (:func:`res_ln_ok`), an error on any other path.
     """
     lead = x.shape[:-1]
     x2 = x.reshape(-1, x.shape[-1])
@@ -126,8 +134,7 @@ def linear(
             x2 = x2.contiguous()
         res2 = residual.reshape(-1, residual.shape[-1]) if residual is not None else None
         hip_ops().gemm(x2, w, bias, res2, table, int(table_period), int(table_offset), a, float(alpha), out2,
-                       int(out_group), int(out_group_stride), int(out_row_offset), int(tile), None, int(bool(glu)),
-                       ln_part)
+                       int(out_group), int(out_group_stride), int(out_row_offset), int(tile), None, int(bool(glu)))
     else:
         y = (x2.float() @ w.float().t()) * alpha
         if bias is not None:
@@ -145,8 +152,6 @@ def linear(
             r2 = residual.reshape(-1, residual.shape[-1])
             y = y + r2.float()[orow, :N]
         out2[orow, :N] = y.to(out2.dtype)
-        if ln_part is not None:
-            _ln_part_ref(out2[orow, :N].float(), ln_part)
     if ret_shape is not None:
         return out.view(ret_shape)
     return out
@@ -452,46 +457,6 @@ def ln_row_stats(x: torch.Tensor, eps: float = 1e-5, out: Optional[torch.Tensor]
     rstd = torch.rsqrt(((xf - mean[:, None]) ** 2).mean(-1) + eps)
     out[:, 0] = rstd
     out[:, 1] = -mean * rstd
-    return out
-
-
-def _ln_slot_cols(N: int) -> torch.Tensor:
-    """Column index [N/64, 64] of each LayerNorm partial slot of the direct-store GEMM epilogue: slot
-    4 * t + w holds columns 256 t + 32 w + [0, 32) and 256 t + 128 + 32 w + [0, 32)."""
-    t = torch.arange(N // 256)[:, None, None]
-    w = torch.arange(4)[None, :, None]
-    c = torch.arange(32)[None, None, :]
-    lo = 256 * t + 32 * w + c
-    return torch.cat([lo, lo + 128], -1).reshape(N // 64, 64)
-
-
-def _ln_part_ref(y: torch.Tensor, part: torch.Tensor):
-    g = y[:, _ln_slot_cols(y.shape[1])]                      # [M, S, 64]
-    mean = g.mean(-1)
-    part[..., 0] = mean
-    part[..., 1] = ((g - mean[..., None]) ** 2).sum(-1)
-
-
-def res_ln_ok(M: int, N: int, tile: int, bias: Optional[torch.Tensor] = None) -> bool:
-    """Whether a residual GEMM on tile code ``tile`` can leave LayerNorm partials (``ln_part``)."""
-    return (tile >= 1000 and (tile // 100) % 10 == 8 and tile % 10 == 9 and M % 256 == 0 and N % 256 == 0
-            and (bias is None or bias.dtype == torch.bfloat16))
-
-
-def ln_part_finalize(part: torch.Tensor, eps: float = 1e-5, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """LayerNorm row statistics (:func:`ln_row_stats` layout: (rstd, -mean * rstd)) from the
-    (mean, M2)-over-64-columns partials a residual GEMM wrote (:func:`linear` ``ln_part``)."""
-    R, S = part.shape[0], part.shape[1]
-    if out is None:
-        out = torch.empty((R, 2), device=part.device, dtype=torch.float32)
-    if part.is_cuda:
-        hip_ops().ln_part_finalize(part, out, float(eps))
-        return out
-    mean = part[..., 0].mean(-1)
-    m2 = part[..., 1].sum(-1) + 64.0 * ((part[..., 0] - mean[:, None]) ** 2).sum(-1)
-    rstd = torch.rsqrt(m2 / (64 * S) + eps)
-    out[:R, 0] = rstd
-    out[:R, 1] = -mean * rstd
     return out
 
 

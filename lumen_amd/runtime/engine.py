@@ -418,12 +418,7 @@ class DecodeGraphs:
         stream from PyTorch's recycled pool could later be handed to another thread's eager
         split-K work while a graph replays, and the two would share counters."""
         if self._stream is None:
-            try:
-                ptr = int(ops.hip_ops().private_stream(d.index if d.index is not None else
-                                                       torch.cuda.current_device()))
-                self._stream = torch.cuda.ExternalStream(ptr, device=d)
-            except (AttributeError, RuntimeError):   # extension without the op (CPU-only builds)
-                self._stream = torch.cuda.Stream(d)
+            self._stream = ops.private_stream(d)
         return self._stream
 
     def _capture(self, Bp: int, W: int) -> dict:

@@ -91,53 +91,3 @@ def test_text_micro_batch_streams_match(monkeypatch):
     t2 = m_gpu.encode_text_ids(ids.cuda()).cpu()
     assert (t1 * t2).sum(-1).min().item() > 0.9995
     assert (t2[:6] * t_ref).sum(-1).min().item() > 0.995
-
-
-def test_vit_residual_ln_partials_match(monkeypatch):
-    """The micro-batched tower with each LayerNorm's row statistics taken from the residual GEMMs'
-    partials (LUMEN_RES_LN=1: direct-store epilogue, ops.ln_part_finalize) == re-reading the rows
-    (ln_row_stats).  ViT-B/32 at 256 images: 128 x 50 = 25 row tiles per micro-batch.  The first
-    encode of a fresh model is the one compared: it builds the LN-folded weights, which must be ready
-    before the second micro-batch's stream reads them (run_blocks_micro builds them up front)."""
-    import lumen_amd.models.clip as clip_mod
-
-    m_gpu = CLIPModel.random("ViT-B-32", seed=7, dtype=torch.bfloat16, device="cuda")
-    imgs = torch.randint(0, 256, (256, 224, 224, 3), dtype=torch.uint8,
-                         generator=torch.Generator().manual_seed(8)).cuda()
-    monkeypatch.setattr(clip_mod, "_VIT_MICRO", 2)
-    monkeypatch.setattr(clip_mod, "_VIT_MICRO_MIN_ROWS", 0)
-    monkeypatch.setattr(clip_mod, "_RES_LN", False)
-    e0 = m_gpu.encode_image_uint8(imgs).cpu()
-    monkeypatch.setattr(clip_mod, "_RES_LN", True)
-    e1 = m_gpu.encode_image_uint8(imgs).cpu()
-    assert torch.isfinite(e1).all()
-    assert (e0 * e1).sum(-1).min().item() > 0.9995
-    # and a fresh model's first encode == a warm one's (the folded-weight cache across the streams)
-    m2 = CLIPModel.random("ViT-B-32", seed=7, dtype=torch.bfloat16, device="cuda")
-    e2 = m2.encode_image_uint8(imgs).cpu()
-    assert (e2 * e1).sum(-1).min().item() > 0.9995
-
-
-def test_vit_graph_buckets_match_eager(monkeypatch):
-    """Serving-sized image batches replay the tower from a hipGraph per 8-image bucket
-    (VisionTower._graph_forward): same embeddings as the eager launches for a partial bucket and a full
-    one, and new weights (load / random_init) recapture instead of replaying the old addresses."""
-    import lumen_amd.models.clip as clip_mod
-
-    m = CLIPModel.random("ViT-B-32", seed=11, dtype=torch.bfloat16, device="cuda")
-    imgs = torch.randint(0, 256, (16, 224, 224, 3), dtype=torch.uint8,
-                         generator=torch.Generator().manual_seed(12)).cuda()
-    for n in (5, 16, 5):
-        monkeypatch.setattr(clip_mod, "_CLIP_GRAPH", False)
-        e_eager = m.encode_image_uint8(imgs[:n]).cpu()
-        monkeypatch.setattr(clip_mod, "_CLIP_GRAPH", True)
-        e_graph = m.encode_image_uint8(imgs[:n]).cpu()
-        assert (e_eager * e_graph).sum(-1).min().item() > 0.9999
-    assert len(m.visual._graphs) == 2
-    m.visual.random_init(torch.Generator().manual_seed(13))
-    assert len(m.visual._graphs) == 0
-    monkeypatch.setattr(clip_mod, "_CLIP_GRAPH", False)
-    e_eager = m.encode_image_uint8(imgs[:5]).cpu()
-    monkeypatch.setattr(clip_mod, "_CLIP_GRAPH", True)
-    e_graph = m.encode_image_uint8(imgs[:5]).cpu()
-    assert (e_eager * e_graph).sum(-1).min().item() > 0.9999

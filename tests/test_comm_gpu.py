@@ -68,6 +68,35 @@ def _ar_worker(rank, world, port, q, one_shot_max=1 << 20):
             torch.cuda.synchronize()
             vals.append(float(x[0]))
         res["graph"] = vals
+        # one-shot and two-shot calls of varying sizes (different block partitions of the
+        # buffer) alternating inside ONE graph, replayed back to back: every block of a call must use
+        # the same parity (a single per-rank epoch)
+        sizes = [(2048, torch.bfloat16), (200000, torch.bfloat16), (8, torch.bfloat16), (130000, torch.float32),
+                 (40000, torch.bfloat16), (300000, torch.bfloat16), (16, torch.float32)]
+        xs = [torch.zeros(n, dtype=dt, device=dev) for n, dt in sizes]
+        with torch.cuda.stream(s):
+            for t in xs:
+                comm.all_reduce(t)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g2):
+            for t in xs:
+                comm.all_reduce(t)
+        mix = []
+        for k in range(4):
+            for j, t in enumerate(xs):
+                t.copy_(torch.arange(t.numel(), device=dev, dtype=torch.float32).remainder(7).to(t.dtype)
+                        * (rank + 1) + k + j)
+            g2.replay()
+            torch.cuda.synchronize()
+            ok = True
+            for j, t in enumerate(xs):
+                base = torch.arange(t.numel(), device=dev, dtype=torch.float32).remainder(7)
+                want = base * sum(r + 1 for r in range(world)) + world * (k + j)
+                ok = ok and bool(torch.equal(t.float(), want.to(t.dtype).float()))
+            mix.append(ok)
+        res["graph_mix"] = mix
         res["error_flag"] = comm.custom.error()
         res["stats"] = dict(comm.stats)
         dist.barrier()
@@ -95,7 +124,8 @@ def test_ipc_all_reduce_processes_one_gpu(world):
         assert "exc" not in r, r
         assert max(r["errs"]) < 1e-2, r["errs"]
         assert r["graph"] == graph, r["graph"]
+        assert r["graph_mix"] == [True] * 4, r["graph_mix"]
         assert not r["error_flag"]
-        assert r["stats"]["ipc_calls"] >= 11 and r["stats"]["ipc2_calls"] == 4
+        assert r["stats"]["ipc_calls"] >= 11 and r["stats"]["ipc2_calls"] >= 4
     for r in out[1:]:
         assert r["errs"] == out[0]["errs"]       # every rank holds the same (bitwise) result

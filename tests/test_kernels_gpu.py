@@ -304,28 +304,3 @@ def test_gemm_layernorm_folded(M, N, K, tile, act):
     got = ops.linear_lnf(xd, wf, ca, st, act=act, tile=tile).cpu().float()
     assert _rel(got[rows], ref) < 1e-2
     assert torch.isfinite(got).all()
-
-
-@pytest.mark.parametrize("M,N,K,tile", [(24 * 256, 1024, 1024, 1849), (8 * 256, 2048, 512, 1829)])
-def test_gemm_residual_ln_partials(M, N, K, tile):
-    """Residual GEMM (direct-store ping-pong) leaving LayerNorm partials of its stored rows: partials
-    vs the fp32 reference over the GPU's own bf16 output, ln_part_finalize vs ln_row_stats of it."""
-    g = torch.Generator().manual_seed(M + N)
-    x = torch.randn(M, K, generator=g).bfloat16()
-    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16()
-    b = torch.randn(N, generator=g).bfloat16()
-    r = (torch.randn(M, N, generator=g) * 3 + 0.7).bfloat16()
-    part = torch.empty(M, N // 64, 2, device=DEV)
-    assert ops.res_ln_ok(M, N, tile, b)
-    got = ops.linear(x.to(DEV), w.to(DEV), b.to(DEV), residual=r.to(DEV), tile=tile, ln_part=part).cpu()
-    ref = ops.linear(x, w, b, residual=r)
-    assert _rel(got, ref) < 1e-2
-    pref = torch.empty(M, N // 64, 2)
-    ops._ln_part_ref(got.float(), pref)
-    assert torch.allclose(part.cpu()[..., 0], pref[..., 0], rtol=1e-5, atol=1e-5)
-    assert torch.allclose(part.cpu()[..., 1], pref[..., 1], rtol=1e-4, atol=1e-3)
-    st = ops.ln_part_finalize(part, 1e-5)
-    st_ref = ops.ln_row_stats(got.to(DEV), 1e-5)
-    assert torch.allclose(st.cpu(), st_ref.cpu(), rtol=1e-4, atol=1e-5)
-    with pytest.raises(RuntimeError):
-        ops.linear(x.to(DEV), w.to(DEV), b.to(DEV), residual=r.to(DEV), tile=1629, ln_part=part)

@@ -108,3 +108,87 @@ def test_vlm_tp4_gqa_graphs_match_tp1(tmp_path):
     for r in (1, 2, 3):
         fol = json.loads((tmp_path / f"follower_stats.rank{r}").read_text())
         assert fol["transport"] == "bus" and fol["ingraph_steps"] >= 10
+
+
+def _tf_rank(rank, world, port, cfg, T, steps, f8, q):
+    """One TP rank on the shared GPU: teacher-forced logits (overlapped prefill + decode steps)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    from lumen_amd.models.llm import LLM, TPInfo
+    from lumen_amd.parallel.comm import Communicator
+    from test_tp_overlap_cpu import hf_state_dict, teacher_forced_logits
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = LLM(cfg, TPInfo(rank, world, None), dtype=torch.bfloat16, device=dev)
+        m.load_hf_state_dict(hf_state_dict(cfg, seed=5))
+        if f8:
+            m.quantize_fp8()
+        m.comm = Communicator(None, dev, ipc=True)
+        ids = torch.randint(3, cfg.vocab_size, (T + steps,), generator=torch.Generator().manual_seed(9))
+
+        def gather(t):                       # the vocab shards, over gloo (host copies)
+            t = t.cpu().contiguous()
+            parts = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(parts, t)
+            return torch.cat(parts, dim=-1)
+
+        out = teacher_forced_logits(m, ids, T, steps, dev, torch.bfloat16, gather)
+        torch.cuda.synchronize()
+        q.put({"rank": rank, "logits": [o.numpy() for o in out], "ipc": m.comm.stats["ipc_calls"],
+               "err": m.comm.custom.error()})
+        dist.barrier()
+        m.comm.close()
+    except BaseException as e:  # noqa: BLE001
+        q.put({"rank": rank, "error": repr(e)})
+    finally:
+        dist.destroy_process_group()
+
+
+F8_CFG = dict(vocab_size=1024, hidden_size=1024, num_layers=2, num_heads=8, num_kv_heads=4, head_dim=128,
+              intermediate_size=2048, max_position=2048, tie_word_embeddings=False, qkv_bias=False)
+
+
+@pytest.mark.parametrize("world,preset,f8", [(4, "tiny-gqa8", False), (2, "tiny-h8", False), (4, "f8", True)])
+def test_tp_teacher_forced_logits_match_tp1(world, preset, f8):
+    """TP = 2 / 4 ranks sharing the GPU (IPC one- / two-shot all-reduce, the overlapped prefill's
+    communication stream): a 300-token prefill + 4 teacher-forced decode steps give per-step
+    full-vocab logits with cosine >= 0.999 (bf16; W8A8 fp8 >= 0.995: the row-parallel shards quantise
+    their weight rows over fewer columns) against TP = 1 on the same GPU and weights -- a reduction-order
+    or shard bug that moves any step's logits fails here, not only one that changes a greedy token."""
+    import numpy as np
+    import torch
+
+    from lumen_amd.models.llm import LLM, LLM_PRESETS, LLMConfig
+    from test_tp_overlap_cpu import _port, hf_state_dict, teacher_forced_logits
+
+    cfg = LLMConfig(**F8_CFG) if preset == "f8" else LLM_PRESETS[preset]
+    T, steps = 300, 4
+    ref_m = LLM(cfg, dtype=torch.bfloat16, device="cuda")
+    ref_m.load_hf_state_dict(hf_state_dict(cfg, seed=5))
+    if f8:
+        ref_m.quantize_fp8()
+    ids = torch.randint(3, cfg.vocab_size, (T + steps,), generator=torch.Generator().manual_seed(9))
+    ref = teacher_forced_logits(ref_m, ids, T, steps, "cuda", torch.bfloat16)
+    del ref_m
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_tf_rank, args=(r, world, port, cfg, T, steps, f8, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = sorted([q.get(timeout=110) for _ in ps], key=lambda d: d["rank"])
+    for p in ps:
+        p.join(30)
+    bound = 0.995 if f8 else 0.999
+    for r in out:
+        assert "error" not in r, r
+        assert r["ipc"] > 0 and not r["err"]
+        for k, (a, b) in enumerate(zip(r["logits"], ref)):
+            a = torch.from_numpy(np.asarray(a))
+            cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
+            assert cos >= bound, (world, preset, k, cos)

@@ -4,6 +4,7 @@
 # times out ends the script (no retries).  Outputs land in gpurun_out/.
 #
 #   tests          pytest -m gpu (one process, 120 s per test)
+#   tsel           pytest -m gpu on $TESTS only (one process)
 #   smoke          __graft_entry__.smoke()
 #   bench          headline bench.py (defaults)
 #   prof_bench     rocprofv3 kernel stats of the headline bench (3 steps)
@@ -58,6 +59,8 @@ step() {   # step NAME SECONDS CMD...  (stdout+stderr -> gpurun_out/NAME.log)
 for task in "$@"; do
   case $task in
     tests) step tests 900 python -u -m pytest tests -m gpu --maxfail=15 -q --timeout 120 --timeout-method thread ;;
+    tsel) step tsel 600 python -u -m pytest ${TESTS:-tests/test_comm_gpu.py} -m gpu -x -v --timeout 120 \
+        --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 400 python bench.py ;;
     prof_bench)
