@@ -9,7 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define LUMEN_WAVE 64
+#define LM_WAVE 64
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x8_t __attribute__((ext_vector_type(8)));
@@ -163,23 +163,23 @@ __device__ __forceinline__ float act_fn(float x) {
 // per-element switch: if-converted, that evaluates every activation).
 template <int N>
 __device__ __forceinline__ void apply_act_n(float* v, int act) {
-#define LUMEN_ACT_CASE(A)                                 \
+#define LM_ACT_CASE(A)                                 \
   case A:                                                 \
     _Pragma("unroll") for (int q = 0; q < N; ++q) v[q] = act_fn<A>(v[q]); \
     break;
   switch (act) {
-    LUMEN_ACT_CASE(ACT_GELU)
-    LUMEN_ACT_CASE(ACT_QUICK_GELU)
-    LUMEN_ACT_CASE(ACT_RELU)
-    LUMEN_ACT_CASE(ACT_SILU)
-    LUMEN_ACT_CASE(ACT_GELU_TANH)
-    LUMEN_ACT_CASE(ACT_HARDSWISH)
-    LUMEN_ACT_CASE(ACT_SIGMOID)
-    LUMEN_ACT_CASE(ACT_LEAKY)
-    LUMEN_ACT_CASE(ACT_HARDSIGMOID)
+    LM_ACT_CASE(ACT_GELU)
+    LM_ACT_CASE(ACT_QUICK_GELU)
+    LM_ACT_CASE(ACT_RELU)
+    LM_ACT_CASE(ACT_SILU)
+    LM_ACT_CASE(ACT_GELU_TANH)
+    LM_ACT_CASE(ACT_HARDSWISH)
+    LM_ACT_CASE(ACT_SIGMOID)
+    LM_ACT_CASE(ACT_LEAKY)
+    LM_ACT_CASE(ACT_HARDSIGMOID)
     default: break;
   }
-#undef LUMEN_ACT_CASE
+#undef LM_ACT_CASE
 }
 
 __device__ __forceinline__ float apply_act(float x, int act) {

@@ -219,11 +219,7 @@ hipError_t conv2d_igemm(const ConvArgs& a0, const GemmEpi& ep, int tile, hipStre
   // Cout >= 64 (IResNet stem 245 -> 152 us, SCRFD 32 -> 64 stride-2 conv 187 -> 129 us at 128 faces /
   // 32 images), 128 x 32 for Cout 32 (SCRFD 640 px stems 298 -> 276 and 349 -> 327 us)
   // (profiles/r4_conv_small_cin_v2.jsonl)
-  static const bool small_lds = [] {
-    const char* e = std::getenv("LUMEN_CONV_SMALL_LDS");
-    return e == nullptr || e[0] != '0';
-  }();
-  if (tile < 0 && small_lds && a.KH * a.KW >= 9 && conv_lds_small_ok(a))     // spatial stems, not 1x1 pointwise
+  if (tile < 0 && a.KH * a.KW >= 9 && conv_lds_small_ok(a))     // spatial stems, not 1x1 pointwise
     return conv2d_lds_small(a, ep, a.Cout >= 64 ? 10 : 9, stream);
   if (tile < 0) {
     const int64_t t128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
@@ -371,15 +367,15 @@ hipError_t conv2d_depthwise(const uint16_t* x, const uint16_t* w, const void* bi
                             int H, int W, int C, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw,
                             int Ho, int Wo, int act, int out_f32, hipStream_t stream) {
   if (dh == 1 && dw == 1 && (sw == 1 || sw == 2)) {
-#define LUMEN_DW_CASE(K)                                                                                       \
+#define LM_DW_CASE(K)                                                                                       \
     if (KW == K) return sw == 1 ? launch_dw_rb<K, 1>(x, w, bias, bias_f32, out, N, H, W, C, KH, sh, ph, pw, Ho, Wo, act, \
                                                      out_f32, stream)                                          \
                                 : launch_dw_rb<K, 2>(x, w, bias, bias_f32, out, N, H, W, C, KH, sh, ph, pw, Ho, Wo, act, \
                                                      out_f32, stream);
-    LUMEN_DW_CASE(3)
-    LUMEN_DW_CASE(5)
-    LUMEN_DW_CASE(7)
-#undef LUMEN_DW_CASE
+    LM_DW_CASE(3)
+    LM_DW_CASE(5)
+    LM_DW_CASE(7)
+#undef LM_DW_CASE
   }
   const int64_t total = (int64_t)N * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(dw_conv_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, x, w, bias,

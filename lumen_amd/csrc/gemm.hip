@@ -299,7 +299,7 @@ gemm_glds_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     const int buf = kt & 1, nbuf = buf ^ 1;
     const int koff = (kt + 1) * BK;
     const char* base = smem + buf * G_BUF;
-#define LUMEN_QUAD(QM, QN)                                                                                     \
+#define LM_QUAD(QM, QN)                                                                                     \
     if constexpr (MODE >= 1) __builtin_amdgcn_s_setprio(1);                                                    \
     Unroll<0, 4>::run([&](const int i) {                                                                      \
       _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                            \
@@ -315,7 +315,7 @@ gemm_glds_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     }
     load_a(base, 0);
     load_b(base, 0);
-    LUMEN_QUAD(0, 0)
+    LM_QUAD(0, 0)
     if constexpr (MODE != 2) {
       if (more) vm_wait4(); else vm_wait0();   // B1(t) landed
       __builtin_amdgcn_s_barrier();
@@ -323,7 +323,7 @@ gemm_glds_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     }
     // ---- phase 1: quadrant (0,1)
     load_b(base, 1);
-    LUMEN_QUAD(0, 1)
+    LM_QUAD(0, 1)
     if constexpr (MODE != 2) {
       if (more) vm_wait4(); else vm_wait0();   // A1(t) landed
       __builtin_amdgcn_s_barrier();
@@ -331,14 +331,14 @@ gemm_glds_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     }
     // ---- phase 2: quadrant (1,1)
     load_a(base, 1);
-    LUMEN_QUAD(1, 1)
+    LM_QUAD(1, 1)
     // ---- phase 3: quadrant (1,0)   (B0(t) already resident)
     if constexpr (MODE != 2) {
       if (more) stage(0, 1, nbuf, koff);
     }
     load_b(base, 0);
-    LUMEN_QUAD(1, 0)
-#undef LUMEN_QUAD
+    LM_QUAD(1, 0)
+#undef LM_QUAD
     if constexpr (MODE != 2) {
       if (more) vm_wait4(); else vm_wait0();   // A0(t+1), B0(t+1) landed
     } else {
@@ -551,7 +551,7 @@ gemm_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t*
       // exactly the loads (stores and loads share the in-order vmcnt counter).
       const bool relax = FK > 0 && after_epi && kt == 0 && more;
       const char* base = smem + buf * G_BUF;
-#define LUMEN_PQUAD(QM, QN)                                                                                    \
+#define LM_PQUAD(QM, QN)                                                                                    \
       __builtin_amdgcn_s_setprio(1);                                                                           \
       Unroll<0, 4>::run([&](const int i) {                                                                    \
         _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                          \
@@ -563,26 +563,26 @@ gemm_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t*
       if (more) stageA(0, nbuf, pm0, koff);
       load_a(base, 0);
       load_b(base, 0);
-      LUMEN_PQUAD(0, 0)
+      LM_PQUAD(0, 0)
       if (relax) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
       else if (more) vm_wait4(); else vm_wait0();   // B1 landed
       __builtin_amdgcn_s_barrier();
       if (more) stageB(0, nbuf, pn0, koff);
       // phase 1: quadrant (0,1)
       load_b(base, 1);
-      LUMEN_PQUAD(0, 1)
+      LM_PQUAD(0, 1)
       if (relax) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
       else if (more) vm_wait4(); else vm_wait0();   // A1 landed
       __builtin_amdgcn_s_barrier();
       if (more) stageB(1, nbuf, pn0, koff);
       // phase 2: quadrant (1,1)
       load_a(base, 1);
-      LUMEN_PQUAD(1, 1)
+      LM_PQUAD(1, 1)
       // phase 3: quadrant (1,0)
       if (more) stageA(1, nbuf, pm0, koff);
       load_b(base, 0);
-      LUMEN_PQUAD(1, 0)
-#undef LUMEN_PQUAD
+      LM_PQUAD(1, 0)
+#undef LM_PQUAD
       if (more) vm_wait4(); else vm_wait0();   // next A0, B0 landed
       __builtin_amdgcn_s_barrier();
       buf = nbuf;
@@ -600,7 +600,7 @@ gemm_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t*
     // (residual RD slabs ahead) instead of being loaded inside each slab's store
     constexpr bool fast = FK > 0;
     constexpr bool FB = fast && ((FK - 1) & 1), FR = fast && ((FK - 1) & 2);
-    constexpr int RD = LUMEN_GEMM_RES_PREFETCH;
+    constexpr int RD = LM_GEMM_RES_PREFETCH;
     u32x4_t bz0 = {0u, 0u, 0u, 0u}, bz1 = {0u, 0u, 0u, 0u};
     u32x4_t rz[RD][2];
     auto res_ptr = [&](int s) {
@@ -777,7 +777,7 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     const int sA0 = s0, sB0 = s0 + 1 >= R_SLOTS ? s0 + 1 - R_SLOTS : s0 + 1;
     const int sB1 = sB0 + 1 >= R_SLOTS ? sB0 + 1 - R_SLOTS : sB0 + 1;
     const int sA1 = sB1 + 1 >= R_SLOTS ? sB1 + 1 - R_SLOTS : sB1 + 1;
-#define LUMEN_RQUAD(QM, QN)                                                                                    \
+#define LM_RQUAD(QM, QN)                                                                                    \
     __builtin_amdgcn_s_setprio(1);                                                                             \
     Unroll<0, 4>::run([&](const int i) {                                                                      \
       _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                            \
@@ -785,7 +785,7 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
         acc[QM][QN][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[j][s], acc[QM][QN][i][j], 0, 0, 0); \
     });                                                                                                        \
     __builtin_amdgcn_s_setprio(0);
-#define LUMEN_RISSUE(PP)                                                                                       \
+#define LM_RISSUE(PP)                                                                                       \
     if ((PP) + R_DIST < nh) {                                                                                  \
       issue((PP) + R_DIST, islot);                                                                             \
       last = (PP) + R_DIST;                                                                                    \
@@ -794,28 +794,28 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     // phase 0: quadrant (0,0) needs A0 (P) and B0 (P + 1)
     vm_wait_halves(last - (P + 1));
     __builtin_amdgcn_s_barrier();
-    LUMEN_RISSUE(P)
+    LM_RISSUE(P)
     load_a(sA0);
     load_b(sB0);
-    LUMEN_RQUAD(0, 0)
+    LM_RQUAD(0, 0)
     // phase 1: quadrant (0,1) needs B1 (P + 2)
     vm_wait_halves(last - (P + 2));
     __builtin_amdgcn_s_barrier();
-    LUMEN_RISSUE(P + 1)
+    LM_RISSUE(P + 1)
     load_b(sB1);
-    LUMEN_RQUAD(0, 1)
+    LM_RQUAD(0, 1)
     // phase 2: quadrant (1,1) needs A1 (P + 3)
     vm_wait_halves(last - (P + 3));
     __builtin_amdgcn_s_barrier();
-    LUMEN_RISSUE(P + 2)
+    LM_RISSUE(P + 2)
     load_a(sA1);
-    LUMEN_RQUAD(1, 1)
+    LM_RQUAD(1, 1)
     // phase 3: quadrant (1,0): B0 again (resident), no wait / barrier
-    LUMEN_RISSUE(P + 3)
+    LM_RISSUE(P + 3)
     load_b(sB0);
-    LUMEN_RQUAD(1, 0)
-#undef LUMEN_RQUAD
-#undef LUMEN_RISSUE
+    LM_RQUAD(1, 0)
+#undef LM_RQUAD
+#undef LM_RISSUE
     s0 = s0 + 4 >= R_SLOTS ? s0 + 4 - R_SLOTS : s0 + 4;
   }
 

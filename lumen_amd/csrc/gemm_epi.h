@@ -120,8 +120,8 @@ constexpr int G_HALF = 128 * 128;       // bytes per half-tile image (128 rows x
 constexpr int G_OP = 2 * G_HALF;
 constexpr int G_BUF = 2 * G_OP;
 
-#ifndef LUMEN_GEMM_RES_PREFETCH
-#define LUMEN_GEMM_RES_PREFETCH 4
+#ifndef LM_GEMM_RES_PREFETCH
+#define LM_GEMM_RES_PREFETCH 4
 #endif
 
 __device__ __forceinline__ void vm_wait4() { asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }

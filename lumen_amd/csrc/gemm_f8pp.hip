@@ -117,7 +117,7 @@ gemm_f8pp_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __rest
       for (int s = 0; s < 2; ++s)
         fb[qn][j][s] = *(const u32x4_t*)(base + G_OP + qn * G_HALF + swz(wn * 32 + j * 16 + frow, s * 4 + fq));
   };
-#define LUMEN_F8PP_CLUSTER(QM, QN)                                                                                \
+#define LM_F8PP_CLUSTER(QM, QN)                                                                                \
   Unroll<0, 4>::run([&](const int i) {                                                                          \
     const i32x8_t a8 = cat8(fa[i][0], fa[i][1]);                                                                \
     _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                                \
@@ -163,8 +163,8 @@ gemm_f8pp_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __rest
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     f8pp_bar();
-    LUMEN_F8PP_CLUSTER(0, 0)
-    LUMEN_F8PP_CLUSTER(0, 1)
+    LM_F8PP_CLUSTER(0, 0)
+    LM_F8PP_CLUSTER(0, 1)
     f8pp_bar();
     // phase 1: rows qm = 1 <- A1 (B fragments kept); stage A0, B0, B1 of t+2; retire those of t+1
     load_a(base, 1);
@@ -180,8 +180,8 @@ gemm_f8pp_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __rest
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     f8pp_bar();
-    LUMEN_F8PP_CLUSTER(1, 0)
-    LUMEN_F8PP_CLUSTER(1, 1)
+    LM_F8PP_CLUSTER(1, 0)
+    LM_F8PP_CLUSTER(1, 1)
     f8pp_bar();
   };
   using T_ = std::true_type;
@@ -193,7 +193,7 @@ gemm_f8pp_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __rest
     ++kt;
   }
   ktile(kt, F_{}, F_{});
-#undef LUMEN_F8PP_CLUSTER
+#undef LM_F8PP_CLUSTER
   if (wm == 1) __builtin_amdgcn_s_setprio(0);
   if (wm == 0) f8pp_bar();   // re-align the groups: every LDS read of the K loop is done
 

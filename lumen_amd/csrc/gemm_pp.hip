@@ -47,7 +47,7 @@ __device__ __forceinline__ void pp_epilogue_direct(const f32x4_t (&acc)[2][2][4]
   constexpr bool FL = FK == 5;
   constexpr bool fast = FK > 0 && !FL;
   constexpr bool FB = fast && ((FK - 1) & 1), FR = fast && ((FK - 1) & 2);
-  constexpr int RD = LUMEN_GEMM_RES_PREFETCH;   // residual passes in flight
+  constexpr int RD = LM_GEMM_RES_PREFETCH;   // residual passes in flight
   const __amdgpu_buffer_rsrc_t crs = c_rsrc(C);
   const int fr = lane & 15, fc = lane >> 4;
   auto col_of = [&](int qn) { return n0 + qn * 128 + wn * 32 + fc * 8; };
@@ -222,18 +222,18 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
                                                  : swz(wn * 32 + j * 16 + frow, s * 4 + fq)));
   };
 
-#define LUMEN_PP_CLUSTER(QM, QN, SLOT)                                                                          \
+#define LM_PP_CLUSTER(QM, QN, SLOT)                                                                          \
   Unroll<0, 4>::run([&](const int i) {                                                                        \
     _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                              \
     _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                              \
       acc[QM][QN][i][j] = DS ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[SLOT][j][s], fa[i][s], acc[QM][QN][i][j], 0, 0, 0) \
                              : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[SLOT][j][s], acc[QM][QN][i][j], 0, 0, 0); \
   });
-#define LUMEN_PP_SYNC_IN()                                                                                      \
+#define LM_PP_SYNC_IN()                                                                                      \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                           \
   pp_barrier();                                                                                                \
   if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
-#define LUMEN_PP_SYNC_OUT()                                                                                     \
+#define LM_PP_SYNC_OUT()                                                                                     \
   if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);                                                      \
   pp_barrier();
 
@@ -302,21 +302,21 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       load_a(base, 0);
       load_b(base, 0, 0);
       if (n1) issue(1, b ^ 1, kt + 1);
-      LUMEN_PP_SYNC_IN()
-      LUMEN_PP_CLUSTER(0, 0, 0)
-      LUMEN_PP_SYNC_OUT()
+      LM_PP_SYNC_IN()
+      LM_PP_CLUSTER(0, 0, 0)
+      LM_PP_SYNC_OUT()
       // phase 1: quadrant (0,1) <- B1; stage A0(t+2) (A0(t) last read at phase 0)
       load_b(base, 1, 1);
       if (n2) issue(0, b, kt + 2);
-      LUMEN_PP_SYNC_IN()
-      LUMEN_PP_CLUSTER(0, 1, 1)
-      LUMEN_PP_SYNC_OUT()
+      LM_PP_SYNC_IN()
+      LM_PP_CLUSTER(0, 1, 1)
+      LM_PP_SYNC_OUT()
       // phase 2: quadrant (1,1) <- A1; stage B1(t+2)
       load_a(base, 1);
       if (n2) issue(2, b, kt + 2);
-      LUMEN_PP_SYNC_IN()
-      LUMEN_PP_CLUSTER(1, 1, 1)
-      LUMEN_PP_SYNC_OUT()
+      LM_PP_SYNC_IN()
+      LM_PP_CLUSTER(1, 1, 1)
+      LM_PP_SYNC_OUT()
       // phase 3: quadrant (1,0) <- B0 (still in fb slot 0); stage A1(t+2); retire tile t+1
       if (n2) {
         issue(3, b, kt + 2);
@@ -324,9 +324,9 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       } else {
         vm_wait_n<0>();
       }
-      LUMEN_PP_SYNC_IN()
-      LUMEN_PP_CLUSTER(1, 0, 0)
-      LUMEN_PP_SYNC_OUT()
+      LM_PP_SYNC_IN()
+      LM_PP_CLUSTER(1, 0, 0)
+      LM_PP_SYNC_OUT()
     } else {
       // phase 0: rows qm = 0 x all columns <- A0, B0, B1; stage A1(t+1) (A1(t-1) read last
       // phase); retire A1(t)
@@ -339,10 +339,10 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       } else {
         vm_wait_n<0>();
       }
-      LUMEN_PP_SYNC_IN()
-      LUMEN_PP_CLUSTER(0, 0, 0)
-      LUMEN_PP_CLUSTER(0, 1, 1)
-      LUMEN_PP_SYNC_OUT()
+      LM_PP_SYNC_IN()
+      LM_PP_CLUSTER(0, 0, 0)
+      LM_PP_CLUSTER(0, 1, 1)
+      LM_PP_SYNC_OUT()
       // phase 1: rows qm = 1 <- A1 (B fragments kept); stage A0, B0, B1 of t+2 (read last
       // at phase 0); retire A0, B0, B1 of t+1
       load_a(base, 1);
@@ -356,15 +356,15 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       } else {
         vm_wait_n<0>();
       }
-      LUMEN_PP_SYNC_IN()
-      LUMEN_PP_CLUSTER(1, 0, 0)
-      LUMEN_PP_CLUSTER(1, 1, 1)
-      LUMEN_PP_SYNC_OUT()
+      LM_PP_SYNC_IN()
+      LM_PP_CLUSTER(1, 0, 0)
+      LM_PP_CLUSTER(1, 1, 1)
+      LM_PP_SYNC_OUT()
     }
   }
-#undef LUMEN_PP_CLUSTER
-#undef LUMEN_PP_SYNC_IN
-#undef LUMEN_PP_SYNC_OUT
+#undef LM_PP_CLUSTER
+#undef LM_PP_SYNC_IN
+#undef LM_PP_SYNC_OUT
   if constexpr (PRIO == 1) { if (wm == 1) __builtin_amdgcn_s_setprio(0); }
   if (wm == 0) pp_barrier();   // re-align the groups: every LDS read of the K loop is done
   const int64_t t_loop = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
@@ -381,7 +381,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   constexpr bool FL = FK == 5;   // LN-folded row / column affine (GemmEpi::row_aff), no residual
   constexpr bool fast = FK > 0 && !FL;
   constexpr bool FB = fast && ((FK - 1) & 1), FR = fast && ((FK - 1) & 2);
-  constexpr int RD = LUMEN_GEMM_RES_PREFETCH;
+  constexpr int RD = LM_GEMM_RES_PREFETCH;
   u32x4_t bz0 = {0u, 0u, 0u, 0u}, bz1 = {0u, 0u, 0u, 0u};
   u32x4_t rz[RD][2];
   float lcs[FL ? 16 : 1], lcb[FL ? 16 : 1], lrs[FL ? 8 : 1], lro[FL ? 8 : 1];
@@ -633,7 +633,7 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[a][bq][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-#define LUMEN_PPS_CLUSTER(QM, QN)                                                                               \
+#define LM_PPS_CLUSTER(QM, QN)                                                                               \
     Unroll<0, 4>::run([&](const int i) {                                                                      \
       _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                            \
       _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                            \
@@ -662,8 +662,8 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       pp_barrier();
       if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
-      LUMEN_PPS_CLUSTER(0, 0)
-      LUMEN_PPS_CLUSTER(0, 1)
+      LM_PPS_CLUSTER(0, 0)
+      LM_PPS_CLUSTER(0, 1)
       if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
       pp_barrier();
       // phase 1: rows qm = 1 <- A1; stage A0, B0, B1 of T+2; retire A0, B0, B1 of T+1
@@ -682,13 +682,13 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       pp_barrier();
       if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
-      LUMEN_PPS_CLUSTER(1, 0)
-      LUMEN_PPS_CLUSTER(1, 1)
+      LM_PPS_CLUSTER(1, 0)
+      LM_PPS_CLUSTER(1, 1)
       if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
       pp_barrier();
       ++T;
     }
-#undef LUMEN_PPS_CLUSTER
+#undef LM_PPS_CLUSTER
     const int64_t t_loop = ep.dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
 
     if constexpr (DS) {
@@ -698,7 +698,7 @@ gemm_pps_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
       // ---- C epilogue: 16 passes (qm, i, qn) of 16 rows x 32 columns through this wave's
       // staging region; lane (rr, cq) stores 8 columns (16 B) of one row.
       const int rr = lane >> 2, cq = lane & 3;
-      constexpr int RD = LUMEN_GEMM_RES_PREFETCH;
+      constexpr int RD = LM_GEMM_RES_PREFETCH;
       u32x4_t bq[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
       u32x4_t rz[RD];
       auto col_of = [&](int qn) { return n0 + qn * 128 + wn * 32 + cq * 8; };
@@ -829,22 +829,22 @@ hipError_t gemm_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ld
       const bool lnf = ep.row_aff && !ep.bias && !ep.residual && ep.alpha == 1.f && fast;
       const int fk = lnf ? 5 : fast && !ep.row_aff ? 1 + (ep.bias ? 1 : 0) + (ep.residual ? 2 : 0) : 0;
       const bool prio1 = (variant & 2) != 0;
-#define LUMEN_PPS_CASE(FKV)                                                                                     \
+#define LM_PPS_CASE(FKV)                                                                                     \
       case FKV:                                                                                                 \
         if (ds) launch_pps_t<FKV, 1, true>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);               \
         else if (prio1) launch_pps_t<FKV, 1>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);             \
         else launch_pps_t<FKV, 0>(A, lda, W, ldw, C, ldc, M, N, K, ep, group_m, stream);                        \
         break;
       switch (fk) {
-        LUMEN_PPS_CASE(1)
-        LUMEN_PPS_CASE(2)
-        LUMEN_PPS_CASE(3)
-        LUMEN_PPS_CASE(4)
-        LUMEN_PPS_CASE(5)
+        LM_PPS_CASE(1)
+        LM_PPS_CASE(2)
+        LM_PPS_CASE(3)
+        LM_PPS_CASE(4)
+        LM_PPS_CASE(5)
         default:
-        LUMEN_PPS_CASE(0)
+        LM_PPS_CASE(0)
       }
-#undef LUMEN_PPS_CASE
+#undef LM_PPS_CASE
       return hipGetLastError();
     }
     variant |= 4;   // two-phase non-persistent form otherwise

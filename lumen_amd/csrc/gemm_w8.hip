@@ -27,7 +27,7 @@ typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
 // row-streaming decode weights (M <= 4): read once per launch by one CU -> non-temporal
-// (LUMEN_W8_NT, default on: 8B fp8 single-stream decode 428 -> 452 tok/s).  The batched kernels
+// (8B fp8 single-stream decode 428 -> 452 tok/s, r3).  The batched kernels
 // (M > 4) keep the default policy: nt measured 5 % slower there (r3_w8_nt_ab_v1.txt).
 template <bool NT>
 __device__ __forceinline__ u32x4_t wload(const uint8_t* p) {
@@ -759,19 +759,11 @@ hipError_t gemm_w8(const uint16_t* A, int64_t lda, const uint8_t* W, int64_t ldw
                    int64_t ldc, int M, int N, int K, const GemmEpi& ep, float* ws, uint32_t* cnt, int ksplit,
                    hipStream_t stream) {
   if (K % 64 != 0 || M <= 0) return hipErrorInvalidValue;
-  static const bool nt = [] {
-    const char* e = std::getenv("LUMEN_W8_NT");
-    return e == nullptr || e[0] != '0';
-  }();
-  if (M <= 4) {   // row-streaming GEMV
+  if (M <= 4) {   // row-streaming GEMV, non-temporal weight loads
     const dim3 grid((N + 15) / 16);
 #define ROWS_LAUNCH(MR_, U_)                                                                                      \
-  do {                                                                                                         \
-    if (nt) hipLaunchKernelGGL((gemv_w8_rows_kernel<MR_, U_, true>), grid, dim3(256), 0, stream, A, lda, W, ldw,  \
-                               scale, C, ldc, M, N, K, ep);                                                     \
-    else hipLaunchKernelGGL((gemv_w8_rows_kernel<MR_, U_, false>), grid, dim3(256), 0, stream, A, lda, W, ldw,    \
-                            scale, C, ldc, M, N, K, ep);                                                        \
-  } while (0)
+  hipLaunchKernelGGL((gemv_w8_rows_kernel<MR_, U_, true>), grid, dim3(256), 0, stream, A, lda, W, ldw, scale, C, \
+                     ldc, M, N, K, ep)
     if (M == 1) ROWS_LAUNCH(1, 2);
     else if (M == 2) ROWS_LAUNCH(2, 2);
     else ROWS_LAUNCH(4, 1);

@@ -284,13 +284,13 @@ hipError_t ln_row_stats(const uint16_t* x, int64_t x_stride, float* out, int row
                         hipStream_t stream, uint8_t* q8, int64_t ldq, uint8_t* qs, int64_t ldqs) {
   if (D % 8 != 0 || D > 64 * 8 * 8 || rows <= 0 || (q8 != nullptr && D % 128 != 0)) return hipErrorInvalidValue;
   const dim3 grid((rows + 3) / 4);
-#define LUMEN_LNS(C) \
+#define LM_LNS(C) \
   hipLaunchKernelGGL(ln_row_stats_kernel<C>, grid, dim3(256), 0, stream, x, x_stride, out, rows, D, eps, q8, ldq, qs, ldqs)
-  if (D <= 512) LUMEN_LNS(1);
-  else if (D <= 1024) LUMEN_LNS(2);
-  else if (D <= 2048) LUMEN_LNS(4);
-  else LUMEN_LNS(8);
-#undef LUMEN_LNS
+  if (D <= 512) LM_LNS(1);
+  else if (D <= 1024) LM_LNS(2);
+  else if (D <= 2048) LM_LNS(4);
+  else LM_LNS(8);
+#undef LM_LNS
   return hipGetLastError();
 }
 

@@ -91,7 +91,7 @@ namespace {
 
 int64_t* g_gemm_dbg = nullptr;   // profiling only (gemm_set_dbg)
 
-#define LUMEN_CHECK_HIP(expr)                                                        \
+#define LM_CHECK_HIP(expr)                                                        \
   do {                                                                                 \
     hipError_t _e = (expr);                                                            \
     TORCH_CHECK(_e == hipSuccess, "lumen HIP error: ", hipGetErrorString(_e), " @ ", #expr); \
@@ -174,12 +174,12 @@ void gemm(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tens
     at::Tensor ws;
     if (ks > 1) ws = at::empty({ks, M, N}, a.options().dtype(at::kFloat));   // per-split slabs, no zero-fill
     uint32_t* cnt = ks > 1 ? splitk_counters(a, (N + 15) / 16) : nullptr;
-    LUMEN_CHECK_HIP(lumen::gemm_skinny(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0), (int)M,
+    LM_CHECK_HIP(lumen::gemm_skinny(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0), (int)M,
                                        (int)N, (int)K, ep, ks > 1 ? ws.data_ptr<float>() : nullptr, cnt, ks,
                                        cur_stream()));
     return;
   }
-  LUMEN_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
+  LM_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
                                    (int)M, (int)N, (int)K, ep, (int)tile, cur_stream()));
 }
 
@@ -205,7 +205,7 @@ void gemm_lnf(const at::Tensor& a, const at::Tensor& w, const at::Tensor& col_af
   ep.col_aff = col_aff.data_ptr<float>();
   ep.dbg = g_gemm_dbg;
   const at::DeviceGuard guard(a.device());
-  LUMEN_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
+  LM_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
                                    (int)M, (int)N, (int)K, ep, (int)tile, cur_stream()));
 }
 
@@ -232,7 +232,7 @@ void ln_row_stats(const at::Tensor& x, at::Tensor out, double eps, const c10::op
     sp = qs->data_ptr<uint8_t>();
   }
   const at::DeviceGuard guard(x.device());
-  LUMEN_CHECK_HIP(lumen::ln_row_stats(bf(x), x.stride(0), out.data_ptr<float>(), (int)x.size(0), (int)x.size(1),
+  LM_CHECK_HIP(lumen::ln_row_stats(bf(x), x.stride(0), out.data_ptr<float>(), (int)x.size(0), (int)x.size(1),
                                       (float)eps, cur_stream(), qp, ldq, sp, ldqs));
 }
 
@@ -278,7 +278,7 @@ void gemm_w8(const at::Tensor& a, const at::Tensor& w8, const at::Tensor& scale,
       cnt = splitk_counters(a, (N + 15) / 16);
     }
   }
-  LUMEN_CHECK_HIP(lumen::gemm_w8(bf(a), a.stride(0), reinterpret_cast<const uint8_t*>(w8.data_ptr()), w8.stride(0),
+  LM_CHECK_HIP(lumen::gemm_w8(bf(a), a.stride(0), reinterpret_cast<const uint8_t*>(w8.data_ptr()), w8.stride(0),
                                  scale.data_ptr<float>(), out.data_ptr(), out.stride(0), (int)M, (int)N, (int)K, ep,
                                  ks > 1 ? ws.data_ptr<float>() : nullptr, cnt, ks, cur_stream()));
 }
@@ -346,12 +346,12 @@ void gemm_dec(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::
     TORCH_CHECK(scale.has_value() && scale->defined() && scale->scalar_type() == at::kFloat && scale->numel() == N,
                 "gemm_dec: fp8 weights need scale f32 [N]");
     TORCH_CHECK(K % 64 == 0 && w.stride(0) % 16 == 0, "gemm_dec: fp8 K % 64");
-    LUMEN_CHECK_HIP(lumen::gemm_w8(bf(a), a.stride(0), reinterpret_cast<const uint8_t*>(w.data_ptr()), w.stride(0),
+    LM_CHECK_HIP(lumen::gemm_w8(bf(a), a.stride(0), reinterpret_cast<const uint8_t*>(w.data_ptr()), w.stride(0),
                                    scale->data_ptr<float>(), out.data_ptr(), out.stride(0), (int)M, (int)N, (int)K, ep,
                                    wsp, cnt, ks, cur_stream()));
   } else {
     TORCH_CHECK(w.scalar_type() == at::kBFloat16 && K % 32 == 0, "gemm_dec: bf16 weights, K % 32");
-    LUMEN_CHECK_HIP(lumen::gemm_skinny(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0), (int)M,
+    LM_CHECK_HIP(lumen::gemm_skinny(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0), (int)M,
                                        (int)N, (int)K, ep, wsp, cnt, ks, cur_stream()));
   }
 }
@@ -397,7 +397,7 @@ void gemm_f8(const at::Tensor& a8, const at::Tensor& sa, const at::Tensor& w8, c
     ep.ldr = residual->stride(0);
   }
   const at::DeviceGuard guard(a8.device());
-  LUMEN_CHECK_HIP(lumen::gemm_f8(reinterpret_cast<const uint8_t*>(a8.data_ptr()), a8.stride(0), sa.data_ptr<float>(),
+  LM_CHECK_HIP(lumen::gemm_f8(reinterpret_cast<const uint8_t*>(a8.data_ptr()), a8.stride(0), sa.data_ptr<float>(),
                                  reinterpret_cast<const uint8_t*>(w8.data_ptr()), w8.stride(0), sw.data_ptr<float>(),
                                  out.data_ptr(), out.stride(0), (int)M, (int)N, (int)K, ep, cur_stream(),
                                  (int)splits, (int)variant));
@@ -501,7 +501,7 @@ void gemm_mx(const at::Tensor& a8, const at::Tensor& a_bs, const at::Tensor& w8,
     mx.ssq_out_tiles = (int)(N / 128);
   }
   const at::DeviceGuard guard(a8.device());
-  LUMEN_CHECK_HIP(lumen::gemm_mx(reinterpret_cast<const uint8_t*>(a8.data_ptr()), a8.stride(0), a_bs.data_ptr<uint8_t>(),
+  LM_CHECK_HIP(lumen::gemm_mx(reinterpret_cast<const uint8_t*>(a8.data_ptr()), a8.stride(0), a_bs.data_ptr<uint8_t>(),
                                  ld_bs, reinterpret_cast<const uint8_t*>(w8.data_ptr()), w8.stride(0),
                                  sw.data_ptr<float>(), cp, ldc, (int)M, (int)N, (int)K, ep, mx, cur_stream(),
                                  (int)variant));
@@ -523,7 +523,7 @@ void quant_rows_mx(const at::Tensor& x, at::Tensor q8, at::Tensor qs, const c10:
     lds = ssq->stride(0);
   }
   const at::DeviceGuard guard(x.device());
-  LUMEN_CHECK_HIP(lumen::quant_rows_mx(bf(x), x.stride(0), reinterpret_cast<uint8_t*>(q8.data_ptr()), q8.stride(0),
+  LM_CHECK_HIP(lumen::quant_rows_mx(bf(x), x.stride(0), reinterpret_cast<uint8_t*>(q8.data_ptr()), q8.stride(0),
                                        qs.data_ptr<uint8_t>(), ldqs, sp, lds, (int)M, (int)K, cur_stream()));
 }
 
@@ -537,7 +537,7 @@ void quant_rows_fp8(const at::Tensor& x, at::Tensor out8, at::Tensor scale) {
   TORCH_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale.numel() >= M && scale.is_contiguous(),
               "quant_rows_fp8: scale f32 [M]");
   const at::DeviceGuard guard(x.device());
-  LUMEN_CHECK_HIP(lumen::quant_rows_fp8(bf(x), x.stride(0), reinterpret_cast<uint8_t*>(out8.data_ptr()), out8.stride(0),
+  LM_CHECK_HIP(lumen::quant_rows_fp8(bf(x), x.stride(0), reinterpret_cast<uint8_t*>(out8.data_ptr()), out8.stride(0),
                                         scale.data_ptr<float>(), (int)M, (int)K, cur_stream()));
 }
 
@@ -572,7 +572,7 @@ void rms_norm_quant_fp8(const at::Tensor& x, const c10::optional<at::Tensor>& ad
     ldr = resid_out->stride(0);
   }
   const at::DeviceGuard guard(x.device());
-  LUMEN_CHECK_HIP(lumen::rms_norm_quant_fp8(bf(x), x.stride(0), ap, lda, rp, ldr, bf(gamma), (float)eps,
+  LM_CHECK_HIP(lumen::rms_norm_quant_fp8(bf(x), x.stride(0), ap, lda, rp, ldr, bf(gamma), (float)eps,
                                             reinterpret_cast<uint8_t*>(out8.data_ptr()), out8.stride(0),
                                             scale.data_ptr<float>(), (int)M, (int)K, cur_stream()));
 }
@@ -594,7 +594,7 @@ void gemm_probe(const at::Tensor& a, const at::Tensor& w, at::Tensor out, at::Te
   ep.alpha = 1.f;
   ep.dbg = dbg.data_ptr<int64_t>();
   const at::DeviceGuard guard(a.device());
-  LUMEN_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
+  LM_CHECK_HIP(lumen::gemm_bf16(bf(a), a.stride(0), bf(w), w.stride(0), out.data_ptr(), out.stride(0),
                                    (int)M, (int)N, (int)K, ep, (int)tile, cur_stream()));
 }
 
@@ -622,7 +622,7 @@ void norm(const at::Tensor& x, const c10::optional<at::Tensor>& row_idx, const c
   if (b.has_value() && b->defined()) { TORCH_CHECK(b->scalar_type() == at::kBFloat16 && b->numel() == D); bp = bf(*b); }
   TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) == D, "norm: out");
   const at::DeviceGuard guard(x.device());
-  LUMEN_CHECK_HIP(lumen::norm_rows(bf(x), x.stride(0), idx, addp, add_stride, rp, r_stride, bf(w), bp,
+  LM_CHECK_HIP(lumen::norm_rows(bf(x), x.stride(0), idx, addp, add_stride, rp, r_stride, bf(w), bp,
                                    out.data_ptr(), out.stride(0), out.scalar_type() == at::kFloat, (int)rows,
                                    (int)D, (float)eps, (int)mode, cur_stream()));
 }
@@ -631,7 +631,7 @@ void l2norm_(at::Tensor x, double eps) {
   check_gpu(x, "x");
   TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 2, "l2norm_: f32 2-D contiguous");
   const at::DeviceGuard guard(x.device());
-  LUMEN_CHECK_HIP(lumen::l2norm_f32(x.data_ptr<float>(), (int)x.size(0), (int)x.size(1), (float)eps, cur_stream()));
+  LM_CHECK_HIP(lumen::l2norm_f32(x.data_ptr<float>(), (int)x.size(0), (int)x.size(1), (float)eps, cur_stream()));
 }
 
 void cls_fill(at::Tensor x, const at::Tensor& cls, const at::Tensor& pos, int64_t seq) {
@@ -640,7 +640,7 @@ void cls_fill(at::Tensor x, const at::Tensor& cls, const at::Tensor& pos, int64_
   TORCH_CHECK(x.size(0) % seq == 0, "cls_fill: rows % seq");
   TORCH_CHECK(cls.numel() == D && pos.size(-1) == D, "cls_fill: shapes");
   const at::DeviceGuard guard(x.device());
-  LUMEN_CHECK_HIP(lumen::cls_fill(bfm(x), seq * x.stride(0), bf(cls), bf(pos), (int)(x.size(0) / seq), (int)D,
+  LM_CHECK_HIP(lumen::cls_fill(bfm(x), seq * x.stride(0), bf(cls), bf(pos), (int)(x.size(0) / seq), (int)D,
                                   cur_stream()));
 }
 
@@ -654,7 +654,7 @@ void embed_gather(const at::Tensor& ids, const at::Tensor& table, const c10::opt
   const uint16_t* pp = nullptr;
   if (pos.has_value() && pos->defined()) { TORCH_CHECK(pos->is_contiguous() && pos->size(-1) == D); pp = bf(*pos); }
   const at::DeviceGuard guard(ids.device());
-  LUMEN_CHECK_HIP(lumen::embed_gather(ids.data_ptr<int64_t>(), bf(table), pp, (int)seq, bfm(out), (int)ids.numel(),
+  LM_CHECK_HIP(lumen::embed_gather(ids.data_ptr<int64_t>(), bf(table), pp, (int)seq, bfm(out), (int)ids.numel(),
                                       (int)D, table.size(0), id_offset, cur_stream()));
 }
 
@@ -686,7 +686,7 @@ void attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at
   a.scale_log2 = (float)(scale * 1.4426950408889634);
   a.causal = causal ? 1 : 0;
   const at::DeviceGuard guard(q.device());
-  LUMEN_CHECK_HIP(lumen::attn_fwd(a, (int)B, (int)D, cur_stream()));
+  LM_CHECK_HIP(lumen::attn_fwd(a, (int)B, (int)D, cur_stream()));
 }
 
 // attention with an MX fp8 output (the W8A8 o-projection's operand): o8 e4m3fn [B, Sq, H*D] (or
@@ -734,7 +734,7 @@ void attention_mx(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
   a.scale_log2 = (float)(scale * 1.4426950408889634);
   a.causal = causal ? 1 : 0;
   const at::DeviceGuard guard(q.device());
-  LUMEN_CHECK_HIP(lumen::attn_fwd(a, (int)B, (int)D, cur_stream()));
+  LM_CHECK_HIP(lumen::attn_fwd(a, (int)B, (int)D, cur_stream()));
 }
 
 // ---------------------------------------------------------------- image prep
@@ -774,7 +774,7 @@ void image_prep2(const at::Tensor& src, const at::Tensor& geom, at::Tensor out, 
   a.scale = (float)scale; a.pad = (float)pad;
   a.layout = (int)layout; a.patch = (int)patch; a.kpad = (int)kpad;
   const at::DeviceGuard guard(src.device());
-  LUMEN_CHECK_HIP(lumen::image_prep(a, (int)B, (int)max_ch, (int)max_dw, cur_stream()));
+  LM_CHECK_HIP(lumen::image_prep(a, (int)B, (int)max_ch, (int)max_dw, cur_stream()));
 }
 
 // ---------------------------------------------------------------- top-k
@@ -795,7 +795,7 @@ void row_topk(const at::Tensor& scores, int64_t k, double scale, at::Tensor out_
   const int nch = lumen::topk_chunks((int)scores.size(1));
   at::Tensor ws;
   if (nch > 1) ws = at::empty({B * nch * (2 * k + 2)}, scores.options());
-  LUMEN_CHECK_HIP(lumen::row_topk(scores.data_ptr<float>(), scores.stride(0), (int)B, (int)scores.size(1), (int)k,
+  LM_CHECK_HIP(lumen::row_topk(scores.data_ptr<float>(), scores.stride(0), (int)B, (int)scores.size(1), (int)k,
                                   (float)scale, out_v.data_ptr<float>(), out_i.data_ptr<int>(), lse, (int)index_offset,
                                   nch > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
 }
@@ -875,7 +875,7 @@ void conv2d(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Te
   a.dh = (int)dilation[0]; a.dw = (int)dilation[1]; a.Ho = (int)Ho; a.Wo = (int)Wo;
   ep.dbg = g_gemm_dbg;
   const at::DeviceGuard guard(x.device());
-  LUMEN_CHECK_HIP(lumen::conv2d_igemm(a, ep, (int)tile, cur_stream()));
+  LM_CHECK_HIP(lumen::conv2d_igemm(a, ep, (int)tile, cur_stream()));
 }
 
 void conv2d_dw(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t act,
@@ -890,7 +890,7 @@ void conv2d_dw(const at::Tensor& x, const at::Tensor& w, const c10::optional<at:
   const void* bp = nullptr; int bf32 = 0;
   if (bias.has_value() && bias->defined()) { bp = bias->data_ptr(); bf32 = bias->scalar_type() == at::kFloat; }
   const at::DeviceGuard guard(x.device());
-  LUMEN_CHECK_HIP(lumen::conv2d_depthwise(bf(x), bf(w), bp, bf32, out.data_ptr(), (int)N, (int)H, (int)W, (int)C,
+  LM_CHECK_HIP(lumen::conv2d_depthwise(bf(x), bf(w), bp, bf32, out.data_ptr(), (int)N, (int)H, (int)W, (int)C,
                                           (int)w.size(0), (int)w.size(1), (int)stride[0], (int)stride[1],
                                           (int)padding[0], (int)padding[1], (int)dilation[0], (int)dilation[1],
                                           (int)out.size(1), (int)out.size(2), (int)act,
@@ -906,7 +906,7 @@ void channel_affine(const at::Tensor& x, const at::Tensor& scale, const at::Tens
   const uint16_t* pp = nullptr;
   if (prelu.has_value() && prelu->defined()) pp = bf(*prelu);
   const at::DeviceGuard guard(x.device());
-  LUMEN_CHECK_HIP(lumen::channel_affine(bf(x), scale.data_ptr<float>(), shift.data_ptr<float>(), bfm(out),
+  LM_CHECK_HIP(lumen::channel_affine(bf(x), scale.data_ptr<float>(), shift.data_ptr<float>(), bfm(out),
                                         x.numel() / C, (int)C, (int)act, pp, cur_stream()));
 }
 
@@ -915,7 +915,7 @@ void pool2d(const at::Tensor& x, at::Tensor out, std::vector<int64_t> kernel, st
   check_gpu(x, "x");
   TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.dim() == 4 && x.size(3) % 8 == 0, "pool2d: NHWC");
   const at::DeviceGuard guard(x.device());
-  LUMEN_CHECK_HIP(lumen::pool2d(bf(x), bfm(out), (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3),
+  LM_CHECK_HIP(lumen::pool2d(bf(x), bfm(out), (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3),
                                 (int)kernel[0], (int)kernel[1], (int)stride[0], (int)stride[1], (int)padding[0],
                                 (int)padding[1], (int)out.size(1), (int)out.size(2), is_max ? 1 : 0, cur_stream()));
 }
@@ -924,7 +924,7 @@ void global_avgpool(const at::Tensor& x, at::Tensor out) {
   check_gpu(x, "x");
   TORCH_CHECK(x.is_contiguous() && x.dim() == 4 && out.scalar_type() == at::kFloat, "global_avgpool");
   const at::DeviceGuard guard(x.device());
-  LUMEN_CHECK_HIP(lumen::global_avgpool(bf(x), out.data_ptr<float>(), (int)x.size(0), (int)(x.size(1) * x.size(2)),
+  LM_CHECK_HIP(lumen::global_avgpool(bf(x), out.data_ptr<float>(), (int)x.size(0), (int)(x.size(1) * x.size(2)),
                                         (int)x.size(3), cur_stream()));
 }
 
@@ -935,7 +935,7 @@ void upsample_add(const at::Tensor& x, const c10::optional<at::Tensor>& add, at:
   const uint16_t* ap = nullptr;
   if (add.has_value() && add->defined()) { TORCH_CHECK(add->is_contiguous()); ap = bf(*add); }
   const at::DeviceGuard guard(x.device());
-  LUMEN_CHECK_HIP(lumen::upsample_add(bf(x), ap, bfm(out), (int)x.size(0), (int)x.size(1), (int)x.size(2),
+  LM_CHECK_HIP(lumen::upsample_add(bf(x), ap, bfm(out), (int)x.size(0), (int)x.size(1), (int)x.size(2),
                                       (int)x.size(3), (int)factor, ldo, cur_stream()));
 }
 
@@ -943,7 +943,7 @@ void channel_scale_(at::Tensor x, const at::Tensor& s) {
   check_gpu(x, "x");
   TORCH_CHECK(x.is_contiguous() && x.dim() == 4 && s.scalar_type() == at::kFloat, "channel_scale_");
   const at::DeviceGuard guard(x.device());
-  LUMEN_CHECK_HIP(lumen::channel_scale(bfm(x), s.data_ptr<float>(), (int)x.size(0), (int)(x.size(1) * x.size(2)),
+  LM_CHECK_HIP(lumen::channel_scale(bfm(x), s.data_ptr<float>(), (int)x.size(0), (int)(x.size(1) * x.size(2)),
                                        (int)x.size(3), cur_stream()));
 }
 
@@ -952,7 +952,7 @@ void pixel_shuffle_up(const at::Tensor& y, at::Tensor out, int64_t factor) {
   TORCH_CHECK(y.is_contiguous() && out.is_contiguous(), "pixel_shuffle_up");
   const int64_t C = out.size(3);
   const at::DeviceGuard guard(y.device());
-  LUMEN_CHECK_HIP(lumen::pixel_shuffle_up(bf(y), bfm(out), (int)y.size(0), (int)y.size(1), (int)y.size(2), (int)C,
+  LM_CHECK_HIP(lumen::pixel_shuffle_up(bf(y), bfm(out), (int)y.size(0), (int)y.size(1), (int)y.size(2), (int)C,
                                           (int)factor, cur_stream()));
 }
 

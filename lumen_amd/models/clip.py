@@ -344,7 +344,7 @@ _LN_FOLD = True   # GPU blocks: LayerNorms folded into qkv / fc1 (see _block_ste
 # tower), group_m 3 (1839: 6388.6 / 6390.6 vs 1849 6336.6 / 6354.6 and 1629 6383.4 / 6380.4 on a later box),
 # profiles/r5_gemm_pp_ds_v1.txt
 _VIT_MICRO_TILE = int(os.environ.get("LUMEN_VIT_TILE", "1839"))
-_VIT_MICRO_RES_TILE = int(os.environ.get("LUMEN_VIT_RES_TILE", str(_VIT_MICRO_TILE)))
+_VIT_MICRO_RES_TILE = _VIT_MICRO_TILE
 # text tower (B x 77 rows): micro-batched with the auto tile choice once it has this many rows per
 # half (b512 x 77: 50.4-50.6k -> 56.2-56.4k texts/s, profiles/r2_vit_micro_streams_v1.txt)
 _TEXT_MICRO_MIN_ROWS = 16384

@@ -33,13 +33,9 @@ from .. import ops
 from ..ops import cnn
 from .layers import ChannelAffine, ConvBN, Linear, fold_bn
 
-_FUSED_BN = __import__("os").environ.get("LUMEN_IRES_FUSED_BN", "1") != "0"
-# LUMEN_IRES_MICRO = 2: recogniser batches of >= 2 x LUMEN_IRES_MICRO_MIN faces as 2 halves on 2 HIP streams,
-# block-interleaved (opt-in: the face pipeline already overlaps the next batch's detector with this batch's
-# recogniser -- 3,318-3,346 vs 3,325-3,344 img/s, profiles/r5_face_micro_v1.txt)
-_IRES_MICRO = int(__import__("os").environ.get("LUMEN_IRES_MICRO", "1"))
-_IRES_MICRO_MIN = int(__import__("os").environ.get("LUMEN_IRES_MICRO_MIN", "32"))
-_IRES_STREAMS: dict = {}
+# (r5's 2-stream recogniser -- batch halves block-interleaved on two HIP streams -- tied the single stream,
+# 3,318-3,346 vs 3,325-3,344 img/s: the face pipeline already overlaps the next batch's detector with this
+# batch's recogniser, profiles/r5_face_micro_v1.txt; it was removed in r6)
 
 
 # =============================================================================== recogniser
@@ -112,18 +108,14 @@ class IResNet(nn.Module):
 
         On the GPU every pre-conv BatchNorm (bn1 of each block, the final bn_out) is produced by the
         epilogue of the conv that writes its input -- the stem / the previous block's conv2 writes
-        the block output AND its affine -- so no channel-affine pass re-reads the activations
-        (``LUMEN_IRES_FUSED_BN=0``: the separate channel_affine kernel)."""
-        if not (x.is_cuda and _FUSED_BN):
+        the block output AND its affine -- so no channel-affine pass re-reads the activations (the CPU
+        reference runs the separate channel affine)."""
+        if not x.is_cuda:
             h = self.stem(x)
             for b in self.blocks:
                 h = b(h)
             h = self.bn_out(h)
         else:
-            F = x.shape[0]
-            n = _IRES_MICRO
-            if n > 1 and F >= n * _IRES_MICRO_MIN:
-                return self._forward_micro(x, n)
             for h in self._fused_steps(x):
                 pass
         emb = self.fc(h.reshape(h.shape[0], -1), out_dtype=torch.float32)
@@ -141,41 +133,6 @@ class IResNet(nn.Module):
             else:
                 h = b(h, hb, (self.bn_out.scale, self.bn_out.shift), next_in_place=True)
             yield h
-
-    def _forward_micro(self, x: torch.Tensor, n: int) -> torch.Tensor:
-        """Faces split into n row ranges, each on its own stream, blocks issued interleaved; each range
-        writes its embeddings into the shared output (allocated on the caller's stream, joined at the end)."""
-        F = x.shape[0]
-        cur = torch.cuda.current_stream(x.device)
-        key = (x.device.index, n)
-        if key not in _IRES_STREAMS:
-            _IRES_STREAMS[key] = [torch.cuda.Stream(device=x.device) for _ in range(n)]
-        streams = _IRES_STREAMS[key]
-        out = torch.empty((F, self.cfg.embedding), device=x.device, dtype=torch.float32)
-        bounds = [F * i // n for i in range(n + 1)]
-        gens = []
-        for i, st in enumerate(streams):
-            st.wait_stream(cur)
-            with torch.cuda.stream(st):
-                gens.append(self._fused_steps(x[bounds[i]:bounds[i + 1]]))
-        last = [None] * n
-        live = list(range(n))
-        while live:
-            nxt = []
-            for i in live:
-                with torch.cuda.stream(streams[i]):
-                    h = next(gens[i], None)
-                    if h is not None:
-                        last[i] = h
-                        nxt.append(i)
-                    else:   # chain done: this range's embeddings on its own stream
-                        hl = last[i]
-                        out[bounds[i]:bounds[i + 1]].copy_(self.fc(hl.reshape(hl.shape[0], -1), out_dtype=torch.float32))
-                        last[i] = None
-            live = nxt
-        for st in streams:
-            cur.wait_stream(st)
-        return ops.l2_normalize_(out)
 
     def load_insightface_state_dict(self, sd: dict) -> None:
         """insightface ``iresnet`` PyTorch weights (conv1/bn1/prelu, layerX.Y.*, bn2, fc, features)."""

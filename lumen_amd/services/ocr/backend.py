@@ -352,7 +352,7 @@ class MI355XOcrBackend:
         """DB post-processing of a [n, rh, rw] probability batch -> boxes in reading order.
         On the GPU: threshold + connected components + boundary extraction + box scores run on
         the device (ops.vision.db_boxes_gpu), only boundary pixels and scores come back."""
-        if prob.is_cuda and os.environ.get("LUMEN_OCR_GPU_DB", "1") != "0":
+        if prob.is_cuda:
             return [sorted_boxes(list(b)) for b, _ in vision.db_boxes_gpu(prob, params, hw, rh, rw)]
         pm = prob.float().cpu().numpy()
         res = []

@@ -30,42 +30,6 @@ def test_iresnet50_full_size():
     assert _cos(got, ref).min() > 0.99
 
 
-def test_iresnet_fused_bn_matches_channel_affine(monkeypatch):
-    """Pre-conv BatchNorms produced by the previous conv's epilogue (second output) == the separate
-    channel-affine pass: the same bf16-rounded block outputs feed the same affine."""
-    import lumen_amd.models.face as face
-
-    g = torch.Generator().manual_seed(3)
-    m = IResNet(IRESNET_PRESETS["r18"])
-    m.random_init(g)
-    m = m.to("cuda")
-    x = torch.randn(6, 112, 112, 8, generator=g).to("cuda", torch.bfloat16)
-    monkeypatch.setattr(face, "_FUSED_BN", True)
-    fused = m(x)
-    monkeypatch.setattr(face, "_FUSED_BN", False)
-    plain = m(x)
-    assert (fused - plain).abs().max().item() < 2e-3
-
-
-def test_iresnet_two_stream_halves_match(monkeypatch):
-    """Recogniser batches split into 2 halves on 2 HIP streams, block-interleaved (IResNet._forward_micro)
-    == the single-stream chain: same kernels on the same rows, so the embeddings agree to rounding."""
-    import lumen_amd.models.face as face
-
-    g = torch.Generator().manual_seed(4)
-    m = IResNet(IRESNET_PRESETS["r18"])
-    m.random_init(g)
-    m = m.to("cuda")
-    x = torch.randn(70, 112, 112, 8, generator=g).to("cuda", torch.bfloat16)
-    monkeypatch.setattr(face, "_IRES_MICRO", 1)
-    one = m(x).cpu()
-    monkeypatch.setattr(face, "_IRES_MICRO", 2)
-    monkeypatch.setattr(face, "_IRES_MICRO_MIN", 8)
-    two = m(x).cpu()
-    assert torch.isfinite(two).all()
-    assert (one * two).sum(-1).min().item() > 0.9999
-
-
 def test_scrfd_10g_full_size():
     g = torch.Generator().manual_seed(1)
     m = SCRFD(SCRFD_PRESETS["10g"])
