@@ -3,7 +3,12 @@
 next to tools/vlm_bench.py's engine-API TTFT.  Synthetic LLaVA-Llama-3-8B pack (random-init
 weights on the device, byte-level tokenizer), fp8 decoder (LUMEN_VLM_FP8=1), one GPU.
 
-    python tools/vlm_service_ttft.py [--n 30] [--warmup 3] [--prompt-chars 40]
+    python tools/vlm_service_ttft.py [--n 30] [--warmup 3] [--prompt-chars 40] [--max-new 32] [--frontends 2]
+
+``--frontends K``: the serving topology (hub/server.py serve_frontends): K gRPC front-end processes
+feeding one GPU engine process that holds the model; the engine streams each token back over the
+shared-memory channel as it is produced (partial records), so the first chunk does not wait for the
+last token.  Without it: an in-process hub.
 """
 import argparse
 import json
@@ -24,6 +29,7 @@ def main():
     ap.add_argument("--prompt-chars", type=int, default=40)
     ap.add_argument("--max-new", type=int, default=8)
     ap.add_argument("--fp8", type=int, default=1)
+    ap.add_argument("--frontends", type=int, default=0)
     a = ap.parse_args()
     if a.fp8:
         os.environ["LUMEN_VLM_FP8"] = "1"
@@ -53,9 +59,30 @@ def main():
            "deployment": {"mode": "hub", "services": ["vlm"]},
            "server": {"port": free_port, "host": "127.0.0.1"}, "services": {"vlm": svc}}
     t0 = time.time()
-    app = AppService.from_app_config(config_from_dict(cfg))
-    server, port = build_server(HubRouter(app.services), "127.0.0.1", 0)
-    server.start()
+    app = server = th = stop = None
+    if a.frontends > 0:
+        import multiprocessing as mp
+        import threading
+
+        import yaml
+
+        from lumen_amd.hub.server import serve_frontends
+
+        cfg_path = os.path.join(cache, "cfg.yaml")
+        with open(cfg_path, "w") as f:
+            yaml.safe_dump(cfg, f)
+        stop = threading.Event()
+        ready = mp.get_context("spawn").Queue()
+        th = threading.Thread(target=serve_frontends, args=(cfg_path, free_port, a.frontends),
+                              kwargs={"stop_event": stop, "ready_q": ready, "devices": ["cuda:0"]})
+        th.start()
+        for _ in range(a.frontends):
+            ready.get(timeout=1200)
+        port = free_port
+    else:
+        app = AppService.from_app_config(config_from_dict(cfg))
+        server, port = build_server(HubRouter(app.services), "127.0.0.1", 0)
+        server.start()
     load_s = time.time() - t0
     jpeg = encode_jpeg(synth_image(np.random.default_rng(0), 768, 1024, "photo"))
     prompt = ("Describe the picture " * 8)[:a.prompt_chars]
@@ -77,8 +104,12 @@ def main():
                 ttft.append((first - t) * 1e3)
                 total.append((time.perf_counter() - t) * 1e3)
                 chunks.append(n)
-    server.stop(0)
-    app.close()
+    if server is not None:
+        server.stop(0)
+        app.close()
+    else:
+        stop.set()
+        th.join(300)
     print(json.dumps({"metric": "VLM p50 TTFT (service: gRPC vlm_generate_stream, first chunk)",
                       "value": round(float(np.percentile(ttft, 50)), 3), "unit": "ms",
                       "p99_ms": round(float(np.percentile(ttft, 99)), 3),
@@ -86,7 +117,9 @@ def main():
                       "chunks_per_request": float(np.median(chunks)), "n": a.n, "load_s": round(load_s, 1),
                       "config": {"model": "LLaVA-Llama-3-8B (synthetic pack, random-init weights)",
                                  "decoder": "fp8" if a.fp8 else "bf16", "image": f"1024x768 JPEG {len(jpeg) // 1024} KiB",
-                                 "prompt_chars": a.prompt_chars, "max_new_tokens": a.max_new}}), flush=True)
+                                 "prompt_chars": a.prompt_chars, "max_new_tokens": a.max_new,
+                                 "topology": f"{a.frontends} front ends + 1 GPU engine (token stream over the shm "
+                                             f"channel)" if a.frontends else "in-process hub"}}), flush=True)
 
 
 if __name__ == "__main__":
