@@ -18,6 +18,7 @@
 //  * ctc_greedy: per (sequence, timestep) arg-max over the class axis and the
 //    blank/repeat collapse with the mean confidence (O-8).
 #include "common.h"
+#include "workspace.h"
 #include "postproc.h"
 
 namespace lumen {
@@ -314,11 +315,20 @@ __global__ void ctc_collapse_kernel(const int* __restrict__ idx, const float* __
 // states; one 16-lane reduction at the end gives idx[row] and conf[row] = 1 / sum (the softmax
 // probability of the arg-max, what ctc_argmax_kernel computes from stored logits).  Ties keep the
 // smaller class index.  K in {64, 128, 256}; classes >= C (padding) never win.
+// Split form (gridDim.y = S > 1): workgroup (x, y) folds the class tiles of split y only and writes its
+// per-row (max, sum, arg-max) state to part[y][row]; cls_argmax_combine merges the S states per row.  A
+// batch of 320 crops x 40 steps is 100 row blocks: one workgroup per CU for a fifth of the CUs and
+// 104 class tiles each (VALU-bound fold, one wave per SIMD) -- S = 8 spreads it over the chip.
+struct ClsPart {
+  float m, s;
+  int idx, pad;
+};
+
 template <int K>
 __global__ void __launch_bounds__(256) cls_argmax_kernel(const uint16_t* __restrict__ h, int64_t ldh,
                                                          const uint16_t* __restrict__ w, const float* __restrict__ bias,
                                                          int M, int N, int C, int* __restrict__ idx_out,
-                                                         float* __restrict__ conf_out) {
+                                                         float* __restrict__ conf_out, ClsPart* __restrict__ part) {
   constexpr int KS = K / 32;          // MFMA k-steps
   constexpr int CPR = K / 8;          // 16-byte chunks per W row
   constexpr int TILE = 64 * K * 2;    // bytes of one 64-class W tile
@@ -335,8 +345,12 @@ __global__ void __launch_bounds__(256) cls_argmax_kernel(const uint16_t* __restr
 #pragma unroll
     for (int t = 0; t < KS; ++t) fa[i][t] = *(const bf16x8_t*)(h + (int64_t)r * ldh + t * 32 + g * 8);
   }
-  const int ntile = (N + 63) / 64;
-  auto load_tile = [&](int nt, u32x4_t (&v)[LPT]) {
+  const int ntile_all = (N + 63) / 64;
+  const int tps = (ntile_all + (int)gridDim.y - 1) / (int)gridDim.y;   // class tiles of this split
+  const int t0 = (int)blockIdx.y * tps;
+  const int ntile = max(0, min(ntile_all - t0, tps));
+  auto load_tile = [&](int nt_, u32x4_t (&v)[LPT]) {
+    const int nt = t0 + nt_;
 #pragma unroll
     for (int q = 0; q < LPT; ++q) {
       const int c = tid + q * 256;                 // 16-byte chunk of the tile
@@ -365,12 +379,15 @@ __global__ void __launch_bounds__(256) cls_argmax_kernel(const uint16_t* __restr
       bi[i][r] = 0;
     }
   u32x4_t stage[LPT];
-  load_tile(0, stage);
-  store_tile(0, stage);
+  if (ntile > 0) {
+    load_tile(0, stage);
+    store_tile(0, stage);
+  }
   __syncthreads();
-  for (int nt = 0; nt < ntile; ++nt) {
-    const int buf = nt & 1;
-    if (nt + 1 < ntile) load_tile(nt + 1, stage);   // lands while this tile computes
+  for (int nt_ = 0; nt_ < ntile; ++nt_) {
+    const int buf = nt_ & 1;
+    const int nt = t0 + nt_;
+    if (nt_ + 1 < ntile) load_tile(nt_ + 1, stage);   // lands while this tile computes
     f32x4_t acc[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -406,7 +423,7 @@ __global__ void __launch_bounds__(256) cls_argmax_kernel(const uint16_t* __restr
           }
         }
     }
-    if (nt + 1 < ntile) {
+    if (nt_ + 1 < ntile) {
       __syncthreads();                 // every wave is done reading buf ^ 1 (tile nt - 1)
       store_tile(buf ^ 1, stage);
       __syncthreads();
@@ -432,22 +449,59 @@ __global__ void __launch_bounds__(256) cls_argmax_kernel(const uint16_t* __restr
       }
       const int row = row0 + i * 16 + 4 * g + r;
       if (frow == 0 && row < M) {
-        idx_out[row] = bx;
-        conf_out[row] = bs > 0.f ? 1.f / bs : 0.f;
+        if (part != nullptr) {
+          part[(int64_t)blockIdx.y * M + row] = ClsPart{bm, bs, bx, 0};
+        } else {
+          idx_out[row] = bx;
+          conf_out[row] = bs > 0.f ? 1.f / bs : 0.f;
+        }
       }
     }
+}
+
+// merge the S split states of every row (split order: deterministic; ties keep the smaller class)
+__global__ void __launch_bounds__(256) cls_argmax_combine_kernel(const ClsPart* __restrict__ part, int S, int M,
+                                                                 int* __restrict__ idx_out,
+                                                                 float* __restrict__ conf_out) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= M) return;
+  float bm = -INFINITY, bs = 0.f;
+  int bx = 0;
+  for (int y = 0; y < S; ++y) {
+    const ClsPart p = part[(int64_t)y * M + row];
+    if (p.m == -INFINITY) continue;
+    const float mm = fmaxf(bm, p.m);
+    bs = (bm == -INFINITY ? 0.f : bs * __builtin_amdgcn_exp2f(bm - mm)) + p.s * __builtin_amdgcn_exp2f(p.m - mm);
+    if (p.m > bm || (p.m == bm && p.idx < bx)) bx = p.idx;
+    bm = mm;
+  }
+  idx_out[row] = bx;
+  conf_out[row] = bs > 0.f ? 1.f / bs : 0.f;
 }
 
 hipError_t cls_argmax(const uint16_t* h, int64_t ldh, const uint16_t* w, const float* bias, int M, int N, int K, int C,
                       int* idx_out, float* conf_out, hipStream_t stream) {
   if (M <= 0) return hipSuccess;
-  const dim3 grid((M + 127) / 128);
+  const int rb = (M + 127) / 128, ntile = (N + 63) / 64;
+  // class splits: ~3 workgroups per CU of 256, at least 4 class tiles each
+  int S = (768 + rb - 1) / rb;
+  S = S < 1 ? 1 : S > 16 ? 16 : S;
+  while (S > 1 && ntile / S < 4) --S;
+  ClsPart* part = nullptr;
+  if (S > 1) {
+    part = (ClsPart*)stream_workspace((size_t)S * M * sizeof(ClsPart), stream, WS_CLS_PART, (size_t)1 << 20);
+    if (part == nullptr) S = 1;
+  }
+  const dim3 grid(rb, S);
   switch (K) {
-    case 64: hipLaunchKernelGGL(cls_argmax_kernel<64>, grid, dim3(256), 0, stream, h, ldh, w, bias, M, N, C, idx_out, conf_out); break;
-    case 128: hipLaunchKernelGGL(cls_argmax_kernel<128>, grid, dim3(256), 0, stream, h, ldh, w, bias, M, N, C, idx_out, conf_out); break;
-    case 256: hipLaunchKernelGGL(cls_argmax_kernel<256>, grid, dim3(256), 0, stream, h, ldh, w, bias, M, N, C, idx_out, conf_out); break;
+    case 64: hipLaunchKernelGGL(cls_argmax_kernel<64>, grid, dim3(256), 0, stream, h, ldh, w, bias, M, N, C, idx_out, conf_out, part); break;
+    case 128: hipLaunchKernelGGL(cls_argmax_kernel<128>, grid, dim3(256), 0, stream, h, ldh, w, bias, M, N, C, idx_out, conf_out, part); break;
+    case 256: hipLaunchKernelGGL(cls_argmax_kernel<256>, grid, dim3(256), 0, stream, h, ldh, w, bias, M, N, C, idx_out, conf_out, part); break;
     default: return hipErrorInvalidValue;
   }
+  if (part != nullptr)
+    hipLaunchKernelGGL(cls_argmax_combine_kernel, dim3((M + 255) / 256), dim3(256), 0, stream, part, S, M, idx_out,
+                       conf_out);
   return hipGetLastError();
 }
 

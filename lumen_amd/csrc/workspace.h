@@ -17,7 +17,7 @@
 
 namespace lumen {
 
-enum WorkspaceTag : int { WS_F8_SPLIT = 0, WS_PP_TAIL = 1, WS_SK_SLAB = 2, WS_SK_CNT = 3 };
+enum WorkspaceTag : int { WS_F8_SPLIT = 0, WS_PP_TAIL = 1, WS_SK_SLAB = 2, WS_SK_CNT = 3, WS_CLS_PART = 4 };
 
 // zero: a fresh allocation is zero-filled on the stream (arrival counters)
 inline void* stream_workspace(size_t bytes, hipStream_t stream, int tag, size_t min_bytes, bool zero = false) {

@@ -221,6 +221,55 @@ class _Block(nn.Module):
             self._mx_key = key
         return self._mx_cache
 
+    def tp_shard(self, rank: int, world: int, heads: int, mx: bool = False) -> dict:
+        """This rank's slice of the block for tensor-parallel blocks (:func:`run_blocks_tp`):
+        column-parallel qkv (the rank's heads of q, k and v) and fc1 (its 1/world of the MLP
+        columns), row-parallel out / fc2 (the matching input columns; the biases on rank 0 only).
+        GPU: from the LayerNorm-folded weights (:meth:`lnf`) or, ``mx``, their W8A8 form
+        (:meth:`mx_weights`, per-output-row scales: a column slice keeps its rows' scales).
+        Cached per (rank, world, form) until a source weight changes."""
+        gpu = self.qkv_w.is_cuda
+        src_key = getattr(self, "_lnf_key", None) if gpu else None
+        if gpu:
+            self.lnf()
+            src_key = self._lnf_key
+        key = (rank, world, heads, mx, gpu, src_key,
+               tuple((p.data_ptr(), p._version) for p in (self.qkv_w, self.out_w, self.fc1_w, self.fc2_w)))
+        cache = getattr(self, "_tp_cache", None)
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        W = self.qkv_w.shape[1]
+        mlp = self.fc1_w.shape[0]
+        assert heads % world == 0 and mlp % world == 0, "TP tower: heads / MLP width not divisible"
+        wr, mr = W // world, mlp // world
+        rows = torch.cat([torch.arange(j * W + rank * wr, j * W + (rank + 1) * wr) for j in range(3)]).to(self.qkv_w.device)
+        fcr = slice(rank * mr, (rank + 1) * mr)
+        d: dict = {}
+        with torch.no_grad():
+            if gpu:
+                qw, qa, fw, fa = self.lnf()
+                if mx:
+                    m = self.mx_weights()
+                    d["qkv"] = (m["qkv"][0].index_select(0, rows).contiguous(), m["qkv"][1][rows].contiguous(),
+                                m["qkv"][2][:, rows].contiguous())
+                    d["fc1"] = (m["fc1"][0][fcr].contiguous(), m["fc1"][1][fcr].contiguous(),
+                                m["fc1"][2][:, fcr].contiguous())
+                    d["out"] = (m["out"][0][:, rank * wr:(rank + 1) * wr].contiguous(), m["out"][1])
+                    d["fc2"] = (m["fc2"][0][:, fcr].contiguous(), m["fc2"][1])
+                else:
+                    d["qkv"] = (qw.index_select(0, rows).contiguous(), qa[:, rows].contiguous())
+                    d["fc1"] = (fw[fcr].contiguous(), fa[:, fcr].contiguous())
+            else:
+                d["qkv"] = (self.qkv_w.index_select(0, rows.cpu()).contiguous(), self.qkv_b[rows.cpu()].contiguous())
+                d["fc1"] = (self.fc1_w[fcr].contiguous(), self.fc1_b[fcr].contiguous())
+            if not (gpu and mx):
+                d["out_w"] = self.out_w[:, rank * wr:(rank + 1) * wr].contiguous()
+                d["fc2_w"] = self.fc2_w[:, fcr].contiguous()
+        d["out_b"] = self.out_b if rank == 0 else None
+        d["fc2_b"] = self.fc2_b if rank == 0 else None
+        self._tp_cache = (key, d)
+        return d
+
     def random_init(self, gen: torch.Generator, layers: int):
         w = self.qkv_w.shape[1]
         attn_std = w ** -0.5
@@ -308,6 +357,81 @@ def run_blocks_mx(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str,
                       write_out=False)
         ops.linear_mx(g8, gs, w["fc2"][0], w["fc2"][1], bias=blk.fc2_b, residual=x, out=x)
     return x
+
+
+def run_blocks_tp(x: torch.Tensor, blocks, B: int, S: int, heads: int, act: str, eps: float, rank: int,
+                  world: int, all_reduce, mx: bool = False) -> torch.Tensor:
+    """Tensor-parallel pre-LN blocks (Megatron split): every rank holds the whole residual stream
+    x [B*S, W] and runs its heads of attention and its 1/world of the MLP; the row-parallel out /
+    fc2 partials are summed by ``all_reduce`` (in place; the IPC one- / two-shot kernels under a TP
+    group) -- 2 all-reduces per block.  A single image's tower then runs on every GPU of the TP group
+    instead of on rank 0 alone, and the features need no broadcast (VLM.build_prefill).  ``mx``: the
+    W8A8 MX chain of :func:`run_blocks_mx` on the shards (GPU; W / world a multiple of 128)."""
+    T, W = x.shape
+    hr = heads // world
+    D = W // heads
+    dev = x.device
+    gpu = x.is_cuda
+    if gpu:
+        st = torch.empty((T, 2), device=dev, dtype=torch.float32)
+    else:
+        h = torch.empty_like(x)
+    o = torch.empty((B, S, hr, D), device=dev, dtype=x.dtype)
+    if mx:
+        f8, u8 = torch.float8_e4m3fn, torch.uint8
+        mlp_r = blocks[0].fc1_w.shape[0] // world
+        x8 = torch.empty((T, W), device=dev, dtype=f8)
+        xs = torch.empty((W // 128, T, 4), device=dev, dtype=u8)
+        a8 = torch.empty((T, hr * D), device=dev, dtype=f8)
+        as_ = torch.empty((hr * D // 128, T, 4), device=dev, dtype=u8)
+        g8 = torch.empty((T, mlp_r), device=dev, dtype=f8)
+        gs = torch.empty((mlp_r // 128, T, 4), device=dev, dtype=u8)
+    for blk in blocks:
+        d = blk.tp_shard(rank, world, heads, mx=mx)
+        if mx:
+            ops.ln_row_stats(x, eps, out=st, q_out=(x8, xs))
+            qkv = ops.linear_mx(x8, xs, d["qkv"][0], d["qkv"][1], row_aff=st, col_aff=d["qkv"][2])
+            q5 = qkv.view(B, S, 3, hr, D)
+            ops.attention_mx(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], q_out=(a8, as_))
+            part = ops.linear_mx(a8, as_, d["out"][0], d["out"][1], bias=d["out_b"])
+        else:
+            if gpu:
+                ops.ln_row_stats(x, eps, out=st)
+                qkv = ops.linear_lnf(x, d["qkv"][0], d["qkv"][1], st)
+            else:
+                ops.layer_norm(x, blk.ln1_w, blk.ln1_b, eps, out=h)
+                qkv = ops.linear(h, d["qkv"][0], d["qkv"][1])
+            q5 = qkv.view(B, S, 3, hr, D)
+            ops.attention(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], out=o)
+            part = ops.linear(o.view(T, hr * D), d["out_w"], d["out_b"])
+        x.add_(all_reduce(part))
+        if mx:
+            ops.ln_row_stats(x, eps, out=st, q_out=(x8, xs))
+            ops.linear_mx(x8, xs, d["fc1"][0], d["fc1"][1], row_aff=st, col_aff=d["fc1"][2], act=act,
+                          q_out=(g8, gs), write_out=False)
+            part = ops.linear_mx(g8, gs, d["fc2"][0], d["fc2"][1], bias=d["fc2_b"])
+        else:
+            if gpu:
+                ops.ln_row_stats(x, eps, out=st)
+                f = ops.linear_lnf(x, d["fc1"][0], d["fc1"][1], st, act=act)
+            else:
+                ops.layer_norm(x, blk.ln2_w, blk.ln2_b, eps, out=h)
+                f = ops.linear(h, d["fc1"][0], d["fc1"][1], act=act)
+            part = ops.linear(f, d["fc2_w"], d["fc2_b"])
+        x.add_(all_reduce(part))
+        del qkv, part
+    return x
+
+
+def tp_blocks_ok(x: torch.Tensor, blocks, heads: int, world: int, mx: bool) -> bool:
+    """Whether :func:`run_blocks_tp` can split these blocks ``world`` ways."""
+    if not blocks:
+        return False
+    W = x.shape[1]
+    mlp = blocks[0].fc1_w.shape[0]
+    if heads % world or mlp % world or (W // world) % 64 or (mlp // world) % 64:
+        return False
+    return not mx or (x.is_cuda and (W // world) % 128 == 0 and (mlp // world) % 128 == 0 and W // heads in (64, 128))
 
 
 def mx_blocks_ok(x: torch.Tensor, blocks, heads: int) -> bool:
@@ -463,9 +587,12 @@ class VisionTower(nn.Module):
         return ops.l2_normalize_(emb)
 
     @torch.no_grad()
-    def forward_features(self, patches: torch.Tensor, B: int, layer: int = -2, drop_cls: bool = True) -> torch.Tensor:
+    def forward_features(self, patches: torch.Tensor, B: int, layer: int = -2, drop_cls: bool = True,
+                         tp: Optional[tuple] = None) -> torch.Tensor:
         """Hidden states after block ``layer`` (LLaVA ``mm_vision_select_layer``; -1 = last,
-        -2 = penultimate) -> [B, P(+1), W] bf16 patch features (CLS dropped)."""
+        -2 = penultimate) -> [B, P(+1), W] bf16 patch features (CLS dropped).  ``tp`` = (rank, world,
+        all_reduce): the blocks run tensor-parallel over the group (:func:`run_blocks_tp`); every rank
+        passes the same patches and gets the full features."""
         cfg = self.cfg
         S, P, W = self.seq, self.num_patches, cfg.width
         x = torch.empty((B * S, W), device=patches.device, dtype=self.patch_w.dtype)
@@ -474,7 +601,11 @@ class VisionTower(nn.Module):
         ops.cls_fill(x, self.class_emb, self.pos_emb, S)
         ops.layer_norm(x, self.ln_pre_w, self.ln_pre_b, cfg.ln_eps, out=x)
         n = len(self.blocks) + layer + 1 if layer < 0 else layer
-        if getattr(self, "w8a8", False) and mx_blocks_ok(x, self.blocks[:n], cfg.heads):
+        mx = getattr(self, "w8a8", False) and mx_blocks_ok(x, self.blocks[:n], cfg.heads)
+        if tp is not None and tp[1] > 1:
+            run_blocks_tp(x, self.blocks[:n], B, S, cfg.heads, cfg.act, cfg.ln_eps, tp[0], tp[1], tp[2],
+                          mx=mx and tp_blocks_ok(x, self.blocks[:n], cfg.heads, tp[1], True))
+        elif mx:
             run_blocks_mx(x, self.blocks[:n], B, S, cfg.heads, cfg.act, cfg.ln_eps)
         else:
             run_blocks(x, self.blocks[:n], B, S, cfg.heads, cfg.act, cfg.ln_eps)

@@ -364,7 +364,7 @@ def cls_ctc_greedy(h: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
 
 # --------------------------------------------------------------------------- DB post-processing (GPU + host)
 def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw: int, max_candidates: int = 1000,
-                 min_size: int = 3, max_boxes: int = 1000, cap: Optional[int] = None) -> list:
+                 min_size: int = 3, max_boxes: int = 1000, cap: Optional[int] = None, on_gpu_done=None) -> list:
     """Batched DB post-processing of a device probability batch [n, rh, rw]: GPU threshold +
     connected components + boundary extraction (db_post.hip), host hull / min-area rect on
     the boundary pixels, GPU box score, host unclip / order / rescale.  ``params[j]`` has
@@ -390,7 +390,10 @@ def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw
         hip_ops().db_components(prob, thr, lab, pts, cnt, int(min_size))
         K = int(cnt.item())
     if K > cap:                                      # pathological maps: retry with room for every pixel
-        return db_boxes_gpu(prob, params, hw, rh, rw, max_candidates, min_size, max_boxes, cap=n * rh * rw)
+        return db_boxes_gpu(prob, params, hw, rh, rw, max_candidates, min_size, max_boxes, cap=n * rh * rw,
+                            on_gpu_done=on_gpu_done)
+    if on_gpu_done is not None:                      # the device-heavy part is done: e.g. queue the next batch
+        on_gpu_done()
     with stage("db_points"):
         dp = pts[:K]
         if K > 1:                                    # group by component on the device (radix sort)

@@ -27,6 +27,8 @@ softmax is fused into the CTC arg-max kernel.
 """
 from __future__ import annotations
 
+import contextlib
+
 import json
 import os
 import logging
@@ -310,50 +312,90 @@ class MI355XOcrBackend:
     @torch.no_grad()
     def detect(self, images: Sequence[np.ndarray], params: Sequence[OcrParams]) -> list[list[np.ndarray]]:
         """decoded RGB images -> per image list of int boxes [4, 2] in reading order."""
+        return self.detect_finish(self.detect_submit(images, params))
+
+    @torch.no_grad()
+    def detect_submit(self, images: Sequence[np.ndarray], params: Sequence[OcrParams], stream=None) -> dict:
+        """The device half of :meth:`detect`, queued without waiting: one pinned upload of the batch,
+        the resize / normalise and the detector forward per shape group, on ``stream`` (default: the
+        current one).  :meth:`detect_finish` runs the DB post-processing.  Submitting batch i + 1 on its
+        own stream while batch i is post-processed and recognised overlaps the detector with the host
+        geometry and the recogniser (tools/face_ocr_bench.py --what ocr)."""
         dc = self.det_config
         limit = int(dc["limit_side_len"])
         shapes = [det_resize_shape(im.shape[0], im.shape[1], limit) for im in images]
         groups: dict = {}
         for i, s in enumerate(shapes):
             groups.setdefault(s, []).append(i)
-        out: list = [None] * len(images)
-        src, offs = None, None
-        if self.device.type == "cuda":
-            # one pinned H2D for the whole batch; every shape group's resize and the
-            # recogniser's crop warps (recognize) read the images from this upload
-            if getattr(self, "_uploader", None) is None:
-                from ...utils.image import PinnedUploader
+        h = {"images": list(images), "params": list(params), "groups": [], "upload": None, "event": None}
+        cuda = self.device.type == "cuda"
+        ctx = torch.cuda.stream(stream) if (cuda and stream is not None) else contextlib.nullcontext()
+        with ctx:
+            src, offs = None, None
+            if cuda:
+                # one pinned H2D for the whole batch; every shape group's resize and the
+                # recogniser's crop warps (recognize) read the images from this upload
+                if getattr(self, "_uploader", None) is None:
+                    from ...utils.image import PinnedUploader
 
-                self._uploader = PinnedUploader(self.device)
-            with stage("upload"):
-                src, offs = self._uploader.upload(images)
-            # (strong refs to the images: recognize matches them by identity)
-            self._last_upload = (list(images), src, [int(o) for o in offs])
-        for (rh, rw), idx in groups.items():
-            geoms, off, tens = [], 0, []
-            for i in idx:
-                h, w = images[i].shape[:2]
-                geoms.append(ops.ImageGeom.resize(h, w, int(offs[i]) if src is not None else off, rh, rw))
-                off += images[i].size
-                tens.append(torch.from_numpy(np.ascontiguousarray(images[i])))
-            with stage("det_preprocess"):
-                x = ops.image_prep(tens, (rh, rw), mean=dc["mean"], std=dc["std"], scale=float(dc["scale"]),
-                                   filter="cv2_linear", layout="nhwc8", swap_rb=True, geoms=geoms,
-                                   out_dtype=self.dtype, device=self.device, src=src)
-            with stage("det_forward"):
-                prob = self.det(x)
+                    self._uploader = PinnedUploader(self.device)
+                with stage("upload"):
+                    src, offs = self._uploader.upload(images)
+                # (strong refs to the images: recognize matches them by identity)
+                h["upload"] = (list(images), src, [int(o) for o in offs])
+                self._last_upload = h["upload"]
+            for (rh, rw), idx in groups.items():
+                geoms, off, tens = [], 0, []
+                for i in idx:
+                    hh, ww = images[i].shape[:2]
+                    geoms.append(ops.ImageGeom.resize(hh, ww, int(offs[i]) if src is not None else off, rh, rw))
+                    off += images[i].size
+                    tens.append(torch.from_numpy(np.ascontiguousarray(images[i])))
+                with stage("det_preprocess"):
+                    x = ops.image_prep(tens, (rh, rw), mean=dc["mean"], std=dc["std"], scale=float(dc["scale"]),
+                                       filter="cv2_linear", layout="nhwc8", swap_rb=True, geoms=geoms,
+                                       out_dtype=self.dtype, device=self.device, src=src)
+                with stage("det_forward"):
+                    prob = self.det(x)
+                h["groups"].append((rh, rw, idx, prob))
+            if cuda:
+                h["event"] = torch.cuda.Event()
+                h["event"].record()
+        return h
+
+    @torch.no_grad()
+    def detect_finish(self, h: dict, on_gpu_done=None) -> list[list[np.ndarray]]:
+        """DB post-processing of a :meth:`detect_submit` handle on the current stream -> per image list
+        of int boxes.  ``on_gpu_done()`` is called once the first group's connected components are
+        back on the host (the GPU is then free for the next batch's detector)."""
+        images, params = h["images"], h["params"]
+        out: list = [None] * len(images)
+        if h["event"] is not None:
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(h["event"])
+            for _, _, _, prob in h["groups"]:
+                prob.record_stream(cur)
+            if h["upload"] is not None:
+                h["upload"][1].record_stream(cur)
+        for gi, (rh, rw, idx, prob) in enumerate(h["groups"]):
             with stage("db_post"):
-                out_g = self._db_post(prob, [images[i].shape[:2] for i in idx], [params[i] for i in idx], rh, rw)
+                out_g = self._db_post(prob, [images[i].shape[:2] for i in idx], [params[i] for i in idx], rh, rw,
+                                      on_gpu_done=on_gpu_done if gi == 0 else None)
             for i, bx in zip(idx, out_g):
                 out[i] = bx
+        if on_gpu_done is not None and not h["groups"]:
+            on_gpu_done()
         return out
 
-    def _db_post(self, prob: torch.Tensor, hw, params, rh: int, rw: int) -> list:
+    def _db_post(self, prob: torch.Tensor, hw, params, rh: int, rw: int, on_gpu_done=None) -> list:
         """DB post-processing of a [n, rh, rw] probability batch -> boxes in reading order.
         On the GPU: threshold + connected components + boundary extraction + box scores run on
         the device (ops.vision.db_boxes_gpu), only boundary pixels and scores come back."""
         if prob.is_cuda:
-            return [sorted_boxes(list(b)) for b, _ in vision.db_boxes_gpu(prob, params, hw, rh, rw)]
+            return [sorted_boxes(list(b)) for b, _ in vision.db_boxes_gpu(prob, params, hw, rh, rw,
+                                                                          on_gpu_done=on_gpu_done)]
+        if on_gpu_done is not None:
+            on_gpu_done()
         pm = prob.float().cpu().numpy()
         res = []
         for j, ((h, w), p) in enumerate(zip(hw, params)):
@@ -364,9 +406,10 @@ class MI355XOcrBackend:
 
     # ------------------------------------------------------------------ recognition
     @torch.no_grad()
-    def recognize(self, images: Sequence[np.ndarray], crops: Sequence[tuple[int, np.ndarray]]
-                  ) -> list[tuple[str, float]]:
-        """crops: (image index, box [4, 2]) -> (text, confidence) per crop."""
+    def recognize(self, images: Sequence[np.ndarray], crops: Sequence[tuple[int, np.ndarray]],
+                  upload: Optional[tuple] = None) -> list[tuple[str, float]]:
+        """crops: (image index, box [4, 2]) -> (text, confidence) per crop.  ``upload``: the
+        :meth:`detect_submit` handle's upload of these images (default: the last one)."""
         if not crops:
             return []
         rc = self.rec_config
@@ -379,7 +422,7 @@ class MI355XOcrBackend:
         std = float(np.mean(rc["std"]))
         scale = float(rc["scale"])
         src = None
-        last = getattr(self, "_last_upload", None)
+        last = upload if upload is not None else getattr(self, "_last_upload", None)
         if last is not None and len(last[0]) == len(images) and all(a is b for a, b in zip(last[0], images)):
             src = (last[1], last[2])        # the detector's upload of these same images
         for s in range(0, len(order), self.rec_batch):

@@ -192,3 +192,67 @@ def test_tp_teacher_forced_logits_match_tp1(world, preset, f8):
             a = torch.from_numpy(np.asarray(a))
             cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
             assert cos >= bound, (world, preset, k, cos)
+
+
+def _tp_tower_rank(rank, world, port, fp8, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    import lumen_amd.models.vlm as vlm_mod
+    from lumen_amd.models.clip import VisionConfig
+    from lumen_amd.models.llm import LLM_PRESETS, TPInfo
+    from lumen_amd.models.vlm import VLM, VLMConfig
+    from lumen_amd.parallel.comm import Communicator
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = VLMConfig(vision=VisionConfig(image_size=224, patch_size=14, width=256, layers=3, heads=4, act="gelu"),
+                        llm=LLM_PRESETS["tiny-h8"], image_token_id=259)
+        m = VLM(cfg, TPInfo(rank, world, dist.group.WORLD), device=dev)
+        m.random_init(0)
+        if fp8:
+            m.quantize_fp8()
+        m.llm.comm = Communicator(None, dev, ipc=True)
+        g = torch.Generator().manual_seed(5)
+        img = torch.randint(0, 256, (180, 240, 3), generator=g, dtype=torch.uint8).to(dev)
+        it = cfg.image_token_id
+        ids = [1, 2, it, 5, 6]
+        mine = [img] if rank == 0 else []
+        vlm_mod.TP_TOWER = False
+        ref = m.build_prefill(ids, mine, n_images=1).float()
+        vlm_mod.TP_TOWER = True
+        got = m.build_prefill(ids, mine, n_images=1).float()
+        torch.cuda.synchronize()
+        cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0).item()
+        q.put({"rank": rank, "ok": m.tp_tower_ok(), "cos": cos, "sig": float(got.double().sum())})
+        dist.barrier()
+        m.llm.comm.close()
+    except BaseException as e:  # noqa: BLE001
+        q.put({"rank": rank, "error": repr(e)})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_vlm_tp_tower_gpu_matches_rank0_tower(fp8):
+    """The tensor-parallel image tower at TP = 2 on the shared GPU (bf16 LN-folded blocks, or the MX
+    W8A8 chain on the shards with fp8) equals the rank-0 tower + broadcast, with identical prefill
+    inputs on both ranks."""
+    from test_tp_overlap_cpu import _port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_tp_tower_rank, args=(r, 2, port, fp8, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = sorted([q.get(timeout=110) for _ in ps], key=lambda d: d["rank"])
+    for p in ps:
+        p.join(30)
+    for r in out:
+        assert "error" not in r, r
+        assert r["ok"] and r["cos"] > (0.995 if fp8 else 0.9995), r
+    assert out[0]["sig"] == out[1]["sig"]

@@ -184,7 +184,9 @@ for task in "$@"; do
       step serve128 400 python -u tools/serve_bench.py --service clip --model CLIP-ViT-L-14 --device cuda \
         --clients 128 --frontends "${SERVE_FE:-8}" --client-procs 6 --seconds 20 ;;
     fe_gpu) step fe_gpu 400 python -u -m pytest tests/test_frontends_gpu.py -x -q --timeout 300 --timeout-method thread ;;
-    face_real) step face_real 300 python -u tools/face_ocr_bench.py --what face --real-dets --iters 5 ;;
+    face_real)   # real detections at batch 32 (GPU stage timers, then host timers)
+      step face_real_gpu 300 python -u tools/face_ocr_bench.py --what face --real-dets --batch 32 --iters 5 --gpu-timers
+      step face_real 300 python -u tools/face_ocr_bench.py --what face --real-dets --batch 32 --iters 10 ;;
     shrink)   # summarise every rocpd database under gpurun_out (kernel stats, PMC sums), drop the big ones
       for db in $(find gpurun_out -name "*.db" -size +4M); do
         python tools/rocpd_stats.py "$db" "${db%.db}_stats.csv" --top 60 > "${db%.db}_stats.txt" 2>&1 || true
