@@ -372,103 +372,35 @@ __global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc) 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int qbk = wid; qbk < nq16; qbk += NW) {
-    const int q0 = qbk * 16;
-    const int qi = q0 + col;
-    bf16x8_t qf[KS];
+  // One 64-key chunk of S^T, online softmax, O^T += V^T P^T for the 16 queries of block q0 (qf).
+  auto full_chunk = [&](int kc, const bf16x8_t (&qf)[KS], f32x4_t (&o)[NB], f32x4_t& l4, float& mrow, int q0,
+                        int qi) __attribute__((always_inline)) {
+    const int k0 = kc * KC;
+    const char* sK = smem + kc * 2 * IMG;
+    const char* sV = sK + IMG;
+    f32x4_t sc[4];
 #pragma unroll
-    for (int t = 0; t < KS; ++t) qf[t] = qn[t];
-    if (qbk + NW < nq16) load_q(qbk + NW);
-    f32x4_t o[NB];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) o[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    float mrow = -INFINITY;
-    f32x4_t l4 = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    const int wave_kend = a.causal ? min(kv_len, min(q0 + 16, a.Sq) + causal_off) : kv_len;
-    const int nc = min(nkc, (wave_kend + KC - 1) / KC);
-    // a ragged last chunk with <= 16 live keys (ViT S = 257: 1 key; CLIP text S = 77: 13)
-    // runs a 16-key tail step below: 7 MFMAs and 4 scores per lane instead of 18 and 16
-    const bool tail1 = nc > 0 && wave_kend - (nc - 1) * KC <= 16;
-    const int nfull = tail1 ? nc - 1 : nc;
-    for (int kc = 0; kc < nfull; ++kc) {
-      const int k0 = kc * KC;
-      const char* sK = smem + kc * 2 * IMG;
-      const char* sV = sK + IMG;
-      f32x4_t sc[4];
-#pragma unroll
-      for (int kb16 = 0; kb16 < 4; ++kb16) {
-        sc[kb16] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-        const int kr = kb16 * 16 + col;
-#pragma unroll
-        for (int t = 0; t < KS; ++t) {
-          bf16x8_t kf = *(const bf16x8_t*)(sK + kr * D * 2 + (k_phys<D>(kr, t * 4 + g) << 4));
-          sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[t], sc[kb16], 0, 0, 0);
-        }
-      }
-      const bool need_mask = (k0 + KC > kv_len) || (a.causal && k0 + KC - 1 > q0 + causal_off);
-      softmax_chunk<NB>(sc, o, l4, mrow, a, need_mask, k0, g, qi, kv_len, causal_off);
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-          bf16x8_t pf;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pf[r] = (__bf16)sc[2 * s][r];
-          pf[4 + r] = (__bf16)sc[2 * s + 1][r];
-        }
-        const int q = col >> 2, p = col & 3;
-        const int r0 = s * 32 + 4 * g + q, r1 = r0 + 16;
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          const int c0 = j * 16 + 4 * p;
-          const char* a0 = sV + r0 * D * 2 + (v_phys<D>(r0, c0 >> 3) << 4) + (c0 & 7) * 2;
-          const char* a1 = sV + r1 * D * 2 + (v_phys<D>(r1, c0 >> 3) << 4) + (c0 & 7) * 2;
-          const s16x4v lo = ds_read_tr16(a0);
-          const s16x4v hi = ds_read_tr16(a1);
-          s16x8_t vv = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, vv), pf, o[j], 0, 0, 0);
-        }
-        l4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones_bf16x8(), pf, l4, 0, 0, 0);   // row sums of P
-      }
-    }
-    if (tail1) {
-      const int k0 = nfull * KC;
-      const char* sK = smem + nfull * 2 * IMG;
-      const char* sV = sK + IMG;
-      f32x4_t s0 = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int kb16 = 0; kb16 < 4; ++kb16) {
+      sc[kb16] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      const int kr = kb16 * 16 + col;
 #pragma unroll
       for (int t = 0; t < KS; ++t) {
-        bf16x8_t kf = *(const bf16x8_t*)(sK + col * D * 2 + (k_phys<D>(col, t * 4 + g) << 4));
-        s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[t], s0, 0, 0, 0);
+        bf16x8_t kf = *(const bf16x8_t*)(sK + kr * D * 2 + (k_phys<D>(kr, t * 4 + g) << 4));
+        sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[t], sc[kb16], 0, 0, 0);
       }
-      float mx = -INFINITY;
+    }
+    const bool need_mask = (k0 + KC > kv_len) || (a.causal && k0 + KC - 1 > q0 + causal_off);
+    softmax_chunk<NB>(sc, o, l4, mrow, a, need_mask, k0, g, qi, kv_len, causal_off);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kj = k0 + g * 4 + r;
-        bool ok = kj < kv_len;
-        if (a.causal) ok = ok && (kj <= qi + causal_off);
-        s0[r] = ok ? s0[r] : -INFINITY;
-        mx = fmaxf(mx, s0[r]);
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mcand = fmaxf(mrow, mx * a.scale_log2);
-      if (__any(mcand > mrow + 8.f)) {
-        const float mb = mcand == -INFINITY ? 0.f : mcand;
-        const float alpha = __builtin_amdgcn_exp2f(mrow - mb);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) o[j] *= alpha;
-        l4 *= alpha;
-        mrow = mcand;
-      }
-      const float nmb = mrow == -INFINITY ? 0.f : -mrow;
+    for (int s = 0; s < 2; ++s) {
       bf16x8_t pf;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        pf[r] = (__bf16)__builtin_amdgcn_exp2f(__builtin_fmaf(s0[r], a.scale_log2, nmb));
-        pf[4 + r] = (__bf16)0.f;                  // keys 16..31 of the chunk: past the tail
+        pf[r] = (__bf16)sc[2 * s][r];
+        pf[4 + r] = (__bf16)sc[2 * s + 1][r];
       }
       const int q = col >> 2, p = col & 3;
-      const int r0 = 4 * g + q, r1 = r0 + 16;
+      const int r0 = s * 32 + 4 * g + q, r1 = r0 + 16;
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const int c0 = j * 16 + 4 * p;
@@ -479,23 +411,156 @@ __global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc) 
         s16x8_t vv = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, vv), pf, o[j], 0, 0, 0);
       }
-      l4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones_bf16x8(), pf, l4, 0, 0, 0);
+      l4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones_bf16x8(), pf, l4, 0, 0, 0);   // row sums of P
     }
-    // Branch-free store through a per-(batch, head) buffer descriptor whose range ends at
-    // the last valid query row: lanes of the ragged last block (qi >= Sq) are dropped by
-    // the range check.  A divergent `if (qi < Sq)` store made hipcc merge its vmcnt
-    // bookkeeping conservatively and wait vmcnt(0) for the prefetched Q at every block.
-    {
-      const float inv = l4[0] > 0.f ? __builtin_amdgcn_rcpf(l4[0]) : 0.f;
-      const int row_off = qi * (int)a.o_ss * 2;
+  };
+  // a ragged last chunk with <= 16 live keys (ViT S = 257: 1 key; CLIP text S = 77: 13): a 16-key
+  // step, 7 MFMAs and 4 scores per lane instead of 18 and 16
+  auto tail_chunk = [&](int kc, const bf16x8_t (&qf)[KS], f32x4_t (&o)[NB], f32x4_t& l4, float& mrow,
+                        int qi) __attribute__((always_inline)) {
+    const int k0 = kc * KC;
+    const char* sK = smem + kc * 2 * IMG;
+    const char* sV = sK + IMG;
+    f32x4_t s0 = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
-        const u32x2v w = {pack2bf(o[j][0] * inv, o[j][1] * inv), pack2bf(o[j][2] * inv, o[j][3] * inv)};
-        __builtin_amdgcn_raw_buffer_store_b64(w, o_rs, row_off + (j * 16 + 4 * g) * 2, 0, 0);
-      }
+    for (int t = 0; t < KS; ++t) {
+      bf16x8_t kf = *(const bf16x8_t*)(sK + col * D * 2 + (k_phys<D>(col, t * 4 + g) << 4));
+      s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[t], s0, 0, 0, 0);
     }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int kj = k0 + g * 4 + r;
+      bool ok = kj < kv_len;
+      if (a.causal) ok = ok && (kj <= qi + causal_off);
+      s0[r] = ok ? s0[r] : -INFINITY;
+      mx = fmaxf(mx, s0[r]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mcand = fmaxf(mrow, mx * a.scale_log2);
+    if (__any(mcand > mrow + 8.f)) {
+      const float mb = mcand == -INFINITY ? 0.f : mcand;
+      const float alpha = __builtin_amdgcn_exp2f(mrow - mb);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) o[j] *= alpha;
+      l4 *= alpha;
+      mrow = mcand;
+    }
+    const float nmb = mrow == -INFINITY ? 0.f : -mrow;
+    bf16x8_t pf;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      pf[r] = (__bf16)__builtin_amdgcn_exp2f(__builtin_fmaf(s0[r], a.scale_log2, nmb));
+      pf[4 + r] = (__bf16)0.f;                  // keys 16..31 of the chunk: past the tail
+    }
+    const int q = col >> 2, p = col & 3;
+    const int r0 = 4 * g + q, r1 = r0 + 16;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int c0 = j * 16 + 4 * p;
+      const char* a0 = sV + r0 * D * 2 + (v_phys<D>(r0, c0 >> 3) << 4) + (c0 & 7) * 2;
+      const char* a1 = sV + r1 * D * 2 + (v_phys<D>(r1, c0 >> 3) << 4) + (c0 & 7) * 2;
+      const s16x4v lo = ds_read_tr16(a0);
+      const s16x4v hi = ds_read_tr16(a1);
+      s16x8_t vv = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, vv), pf, o[j], 0, 0, 0);
+    }
+    l4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones_bf16x8(), pf, l4, 0, 0, 0);
+  };
+  // Branch-free store through a per-(batch, head) buffer descriptor whose range ends at the last valid
+  // query row: lanes of the ragged last block (qi >= Sq) are dropped by the range check.  A divergent
+  // `if (qi < Sq)` store made hipcc merge its vmcnt bookkeeping conservatively and wait vmcnt(0) for the
+  // prefetched Q at every block.
+  auto store_o = [&](const f32x4_t (&o)[NB], float lsum, int qi) __attribute__((always_inline)) {
+    const float inv = lsum > 0.f ? __builtin_amdgcn_rcpf(lsum) : 0.f;
+    const int row_off = qi * (int)a.o_ss * 2;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+      const u32x2v w = {pack2bf(o[j][0] * inv, o[j][1] * inv), pack2bf(o[j][2] * inv, o[j][3] * inv)};
+      __builtin_amdgcn_raw_buffer_store_b64(w, o_rs, row_off + (j * 16 + 4 * g) * 2, 0, 0);
+    }
+  };
+
+  // Ragged split (non-causal, full-length keys, the last query block the only one left over after
+  // equal shares, <= NW chunks -- ViT S = 257 at NW = 8: 16 blocks + 1 query): every wave takes its equal
+  // share of blocks, then wave w < nkc computes chunk w of the LAST block and the partial softmax
+  // states merge through LDS, instead of one wave running a third whole block while seven idle
+  // (2.2 instead of 3 block-times per workgroup)
+  const bool split_tail = !a.causal && kv_len == a.Sk && nq16 > NW && (nq16 - 1) % NW == 0 && nkc <= NW;
+  const int nq_main = split_tail ? nq16 - 1 : nq16;
+  const int nc_all = (kv_len + KC - 1) / KC;
+  const bool tail1_all = nc_all > 0 && kv_len - (nc_all - 1) * KC <= 16;
+
+  for (int qbk = wid; qbk < nq_main; qbk += NW) {
+    const int q0 = qbk * 16;
+    const int qi = q0 + col;
+    bf16x8_t qf[KS];
+#pragma unroll
+    for (int t = 0; t < KS; ++t) qf[t] = qn[t];
+    if (qbk + NW < nq_main) load_q(qbk + NW);
+    else if (split_tail) load_q(nq16 - 1);          // the split tail block's queries, every wave
+    f32x4_t o[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) o[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    float mrow = -INFINITY;
+    f32x4_t l4 = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const int wave_kend = a.causal ? min(kv_len, min(q0 + 16, a.Sq) + causal_off) : kv_len;
+    const int nc = min(nkc, (wave_kend + KC - 1) / KC);
+    const bool tail1 = nc > 0 && wave_kend - (nc - 1) * KC <= 16;
+    const int nfull = tail1 ? nc - 1 : nc;
+    for (int kc = 0; kc < nfull; ++kc) full_chunk(kc, qf, o, l4, mrow, q0, qi);
+    if (tail1) tail_chunk(nfull, qf, o, l4, mrow, qi);
+    store_o(o, l4[0], qi);
   }
+  if (!split_tail) return;
+
+  // ---- the split tail block: wave w < nc_all runs chunk w for its 16 queries (one valid at S = 257)
+  const int q0t = (nq16 - 1) * 16, qit = q0t + col;
+  bf16x8_t qft[KS];
+#pragma unroll
+  for (int t = 0; t < KS; ++t) qft[t] = qn[t];
+  f32x4_t ot[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) ot[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  float mt = -INFINITY;
+  f32x4_t lt = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  if (wid < nc_all) {
+    if (wid == nc_all - 1 && tail1_all) tail_chunk(wid, qft, ot, lt, mt, qit);
+    else full_chunk(wid, qft, ot, lt, mt, q0t, qit);
+  }
+  __syncthreads();                                   // every wave is done with the K / V images
+  // partial states into the (now free) K / V region: [wave][m 16 | l 16 | o D x 16] floats
+  float* ps = (float*)smem + wid * (32 + D * 16);
+  if (wid < nc_all) {
+    if (g == 0) {
+      ps[col] = mt;
+      ps[16 + col] = lt[0];
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ps[32 + (j * 16 + 4 * g + r) * 16 + col] = ot[j][r];
+  }
+  __syncthreads();
+  if (wid != 0) return;
+  float M = -INFINITY;
+  for (int w = 0; w < nc_all; ++w) M = fmaxf(M, ((const float*)smem)[w * (32 + D * 16) + col]);
+  float L = 0.f;
+  f32x4_t om[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) om[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  for (int w = 0; w < nc_all; ++w) {
+    const float* pw = (const float*)smem + w * (32 + D * 16);
+    const float e = pw[col] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(pw[col] - M);
+    L += pw[16 + col] * e;
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) om[j][r] += pw[32 + (j * 16 + 4 * g + r) * 16 + col] * e;
+  }
+  store_o(om, L, qit);
 }
 
 template <int D, int NW>

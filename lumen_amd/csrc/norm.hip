@@ -280,9 +280,63 @@ ln_row_stats_kernel(const uint16_t* __restrict__ x, int64_t x_stride, float* __r
   }
 }
 
+// Statistics only, R rows per wave: every row's loads are issued before the first reduction, so a
+// wave pays one memory round trip per R rows (ViT-L/14 b256: 65,792 rows of 1,024 -- one row per wave
+// left 257 waves per CU each waiting out its own load).
+template <int CPL, int R>
+__global__ void __launch_bounds__(256)
+ln_row_stats_multi_kernel(const uint16_t* __restrict__ x, int64_t x_stride, float* __restrict__ out, int rows, int D,
+                          float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (row0 >= rows) return;
+  const int nch = D >> 3;
+  u32x4_t raw[R][CPL];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint16_t* xr = x + (int64_t)min(row0 + r, rows - 1) * x_stride;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int ch = lane + c * 64;
+      raw[r][c] = ch < nch ? *(const u32x4_t*)(xr + ch * 8) : (u32x4_t){0u, 0u, 0u, 0u};
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    float v[CPL][8];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      unpack8(raw[r][c], v[c]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[c][i];
+    }
+    const float mean = wave_sum(s) / (float)D;
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      if (lane + c * 64 < nch) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float d = v[c][i] - mean;
+          ss += d * d;
+        }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / (float)D + eps);
+    if (lane == 0 && row0 + r < rows) *(float2*)(out + 2 * (int64_t)(row0 + r)) = make_float2(rstd, -mean * rstd);
+  }
+}
+
 hipError_t ln_row_stats(const uint16_t* x, int64_t x_stride, float* out, int rows, int D, float eps,
                         hipStream_t stream, uint8_t* q8, int64_t ldq, uint8_t* qs, int64_t ldqs) {
   if (D % 8 != 0 || D > 64 * 8 * 8 || rows <= 0 || (q8 != nullptr && D % 128 != 0)) return hipErrorInvalidValue;
+  if (q8 == nullptr && D <= 1024 && rows >= 16384) {   // large row counts: 4 rows per wave
+    const dim3 g4((rows + 15) / 16);
+    if (D <= 512) hipLaunchKernelGGL((ln_row_stats_multi_kernel<1, 4>), g4, dim3(256), 0, stream, x, x_stride, out, rows, D, eps);
+    else hipLaunchKernelGGL((ln_row_stats_multi_kernel<2, 4>), g4, dim3(256), 0, stream, x, x_stride, out, rows, D, eps);
+    return hipGetLastError();
+  }
   const dim3 grid((rows + 3) / 4);
 #define LM_LNS(C) \
   hipLaunchKernelGGL(ln_row_stats_kernel<C>, grid, dim3(256), 0, stream, x, x_stride, out, rows, D, eps, q8, ldq, qs, ldqs)

@@ -499,8 +499,11 @@ def write_vlm_model(root, name: str, preset: Optional[str] = None, seed: int = 0
     n = name.lower()
     preset = preset or ("tiny" if "tiny" in n else "llava-llama3-8b" if ("llava" in n or "8b" in n) else "fastvlm-0.5b")
     cfg = copy.deepcopy(VLM_PRESETS[preset])
+    # full-size presets: the tokenizer covers the decoder's whole vocabulary (random-init decoders then
+    # generate decodable text, so service benchmarks see real streamed chunks); tiny ones stay byte-only
     tok = write_byte_bpe_tokenizer(root / "tokenizer.json", bos="<|im_start|>", eos="<|im_end|>",
-                                   extra_special=["<|endoftext|>", "<image>"], add_bos_eos=False)
+                                   extra_special=["<|endoftext|>", "<image>"], add_bos_eos=False,
+                                   fill_vocab=0 if "tiny" in preset else cfg.llm.vocab_size)
     from tokenizers import Tokenizer
 
     t = Tokenizer.from_file(str(root / "tokenizer.json"))

@@ -34,9 +34,13 @@ def _bytes_to_unicode():
 
 
 def write_byte_bpe_tokenizer(path: Path, bos: str = "<start_of_text>", eos: str = "<end_of_text>",
-                             extra_special: Optional[list[str]] = None, add_bos_eos: bool = True) -> dict:
+                             extra_special: Optional[list[str]] = None, add_bos_eos: bool = True,
+                             fill_vocab: int = 0) -> dict:
     """A dependency-free byte-level BPE tokenizer.json (no merges): ids 0..255 = bytes,
-    then the special tokens; EOS gets the largest id (CLIP's EOT-argmax pooling)."""
+    then the special tokens; EOS gets the largest id (CLIP's EOT-argmax pooling).
+    ``fill_vocab``: pad the vocabulary with word tokens " w<k>" up to that many ids (after the
+    specials), so a random-init decoder over a real-sized vocabulary (128,256 for Llama-3) produces
+    readable text instead of ids the tokenizer does not know (service-level streaming benchmarks)."""
     from tokenizers import Tokenizer, decoders, models, pre_tokenizers, processors
 
     b2u = _bytes_to_unicode()
@@ -44,6 +48,11 @@ def write_byte_bpe_tokenizer(path: Path, bos: str = "<start_of_text>", eos: str 
     specials = (extra_special or []) + [bos, eos]
     for s in specials:
         vocab[s] = len(vocab)
+    sp = b2u[ord(" ")]
+    k = 0
+    while len(vocab) < fill_vocab:
+        vocab[f"{sp}w{k}"] = len(vocab)
+        k += 1
     tok = Tokenizer(models.BPE(vocab=vocab, merges=[]))
     tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
     tok.decoder = decoders.ByteLevel()

@@ -358,8 +358,11 @@ class MI355XFaceBackend:
             else:
                 dev, offs = tl.uploader.upload(images)
             src = dev
-            # (strong refs to the images keep their ids from being reused while the map lives)
-            tl.last_upload = (dev, {id(im): int(o) for im, o in zip(images, offs)}, list(images))
+            # (strong refs to the images keep their ids from being reused while the map lives); the two
+            # most recent uploads are kept: a pipelined caller launches batch i + 1's detector before it
+            # aligns batch i's faces (tools/face_ocr_bench.py --real-dets)
+            up = (dev, {id(im): int(o) for im, o in zip(images, offs)}, list(images))
+            tl.uploads = [up] + list(getattr(tl, "uploads", []))[:1]
         with stage("det_preprocess"):
             sp = self.spec
             x = ops.image_prep(tens, (S, S), mean=getattr(sp, "det_mean3", None) or (sp.det_mean,) * 3,
@@ -429,9 +432,11 @@ class MI355XFaceBackend:
         R = self.spec.rec_size
         kw = dict(cpad=8, scale=1.0 / self.spec.rec_std, mean=self.spec.rec_mean / self.spec.rec_std, std=1.0,
                   swap_rb=self.spec.rec_color.lower() == "bgr", device=self.device)
-        last = getattr(self._tl(), "last_upload", None)
-        if last is not None and self.device.type == "cuda" and all(id(im) in last[1] for im in images):
-            kw["src"] = (last[0], [last[1][id(im)] for im in images])     # reuse the detection upload
+        if self.device.type == "cuda":
+            for last in getattr(self._tl(), "uploads", []):
+                if all(id(im) in last[1] for im in images):
+                    kw["src"] = (last[0], [last[1][id(im)] for im in images])     # reuse the detection upload
+                    break
         if replicate is None or not any(replicate):
             return vision.warp_batch(images, img_index, minv, (R, R), **kw)
         rep = np.asarray(replicate, bool)

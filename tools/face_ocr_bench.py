@@ -137,6 +137,7 @@ def bench_face(args):
             stages[k] = stages.get(k, 0.0) + v
 
     found = []
+    pend: list = []
 
     def step_real():
         # --real-dets: the detector's own output drives the recogniser (no fabricated rows); under
@@ -147,6 +148,16 @@ def bench_face(args):
         with use_timer(t):
             if runner is not None:
                 res = runner.run(imgs, [params[0]] * len(imgs), args.faces)
+            elif args.pipeline:
+                # pipelined: batch i + 1's upload + detector are queued as soon as batch i's detections are
+                # on the host, ahead of batch i's alignment / recogniser (detect_launch / detect_finish)
+                if not pend:
+                    pend.append(be.detect_launch(imgs, params[:len(imgs)]))
+                st0 = pend.pop()
+                dets = be.detect_finish(st0)
+                nimgs = [np.asarray(im) for im in dec()]
+                pend.append(be.detect_launch(nimgs, params[:len(nimgs)]))
+                res = be.embed_batch_detections(st0[0], dets, [args.faces] * len(st0[0]))
             else:
                 res = be.detect_and_embed_images(imgs, params[:len(imgs)], args.faces)
         found.append(sum(len(f) for f in res) / max(len(res), 1))
@@ -199,8 +210,11 @@ def bench_face(args):
                 ("included (Pillow, host pool)" if args.pillow else
                  "included (device JPEG: host entropy decode pool + one batched GPU reconstruction)"),
             "image_kind": args.image_kind, "jpeg_kb": round(sum(len(j) for j in jpegs) / len(jpegs) / 1024, 1),
-            "pipeline": ("real detections: detect_and_embed_images / SPMDFaceRunner.run on the detector's own output, "
-                         "images pre-decoded" if args.real_dets else
+            "pipeline": ("real detections on the detector's own output, images pre-decoded, " +
+                         ("SPMDFaceRunner.run" if runner is not None else
+                          "batch i+1's detector queued before batch i's alignment + recogniser (detect_launch / "
+                          "detect_finish / embed_batch_detections)" if args.pipeline else "detect_and_embed_images")
+                         if args.real_dets else
                          "JPEG decode + pinned staging + H2D (own stream) of batch i+1 overlapped with the GPU "
                          "work of batch i; batch i+1's detector queued before batch i's embeddings are read"),
             "faces_found_per_image": round(float(np.mean(found)), 2) if found else None}
@@ -253,21 +267,37 @@ def bench_ocr(args):
     # and its recogniser (MI355XOcrBackend.detect_submit / detect_finish)
     det_stream = torch.cuda.Stream(dev) if args.pipeline and runner is None else None
     pending = [None]
+    # JPEG-inclusive: the prefetch thread decodes batch i + 1 AND queues its upload + detector, so the
+    # decode never waits in the main thread; pre-decoded: batch i + 1 goes out once batch i's connected
+    # components are back (its detector then does not compete with batch i's labelling kernels)
+    in_thread = det_stream is not None and pre is None
+
+    def dec_submit():
+        nimgs = dec()
+        return be.detect_submit(nimgs, [OcrParams()] * len(nimgs), stream=det_stream)
+
+    if in_thread:
+        nxt[0] = ahead.submit(dec_submit)
 
     def step():
         t = StageTimer("ocr-bench", gpu=args.gpu_timers)
         if det_stream is not None:
             with use_timer(t):
-                if pending[0] is None:
-                    imgs0 = nxt[0].result()
-                    nxt[0] = ahead.submit(dec)
-                    pending[0] = be.detect_submit(imgs0, [OcrParams()] * len(imgs0), stream=det_stream)
-                h = pending[0]
+                if in_thread:
+                    h = nxt[0].result()
+                    nxt[0] = ahead.submit(dec_submit)
+                    launch_next = None
+                else:
+                    if pending[0] is None:
+                        imgs0 = nxt[0].result()
+                        nxt[0] = ahead.submit(dec)
+                        pending[0] = be.detect_submit(imgs0, [OcrParams()] * len(imgs0), stream=det_stream)
+                    h = pending[0]
 
-                def launch_next():
-                    nimgs = nxt[0].result()
-                    nxt[0] = ahead.submit(dec)
-                    pending[0] = be.detect_submit(nimgs, [OcrParams()] * len(nimgs), stream=det_stream)
+                    def launch_next():
+                        nimgs = nxt[0].result()
+                        nxt[0] = ahead.submit(dec)
+                        pending[0] = be.detect_submit(nimgs, [OcrParams()] * len(nimgs), stream=det_stream)
 
                 be.detect_finish(h, on_gpu_done=launch_next)
                 imgs = h["images"]
@@ -340,7 +370,8 @@ def main():
     ap.add_argument("--pillow", action="store_true",
                     help="face, JPEG-inclusive: decode with Pillow on the host pool instead of the device JPEG path")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
-                    help="ocr: one batch at a time (no detector / recogniser overlap across batches)")
+                    help="ocr / face --real-dets: one batch at a time (no detector / recogniser overlap across "
+                         "batches)")
     ap.add_argument("--real-dets", action="store_true",
                     help="face: the recogniser embeds the detector's real output (seeded head bias), SPMD via "
                          "SPMDFaceRunner.run")
