@@ -22,6 +22,7 @@
 // written as [b, s, h, d] so the out-projection GEMM consumes it directly.
 #include <cstdlib>
 #include "attention.h"
+#include "tuning.h"
 #include "common.h"
 
 namespace lumen {
@@ -318,7 +319,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
 // SIMD to hide the LDS / MFMA latencies of the query-block walk (ViT S = 257: 17 blocks -> at most
 // 3 per wave instead of 5).
 template <int D, int NW>
-__global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc) {
+__global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc, int allow_split) {
   constexpr int NCH = D / 8;
   constexpr int KS = D / 32;
   constexpr int NB = D / 16;
@@ -488,7 +489,8 @@ __global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc) 
   // share of blocks, then wave w < nkc computes chunk w of the LAST block and the partial softmax
   // states merge through LDS, instead of one wave running a third whole block while seven idle
   // (2.2 instead of 3 block-times per workgroup)
-  const bool split_tail = !a.causal && kv_len == a.Sk && nq16 > NW && (nq16 - 1) % NW == 0 && nkc <= NW;
+  const bool split_tail = allow_split && !a.causal && kv_len == a.Sk && nq16 > NW && (nq16 - 1) % NW == 0 &&
+                          nkc <= NW;
   const int nq_main = split_tail ? nq16 - 1 : nq16;
   const int nc_all = (kv_len + KC - 1) / KC;
   const bool tail1_all = nc_all > 0 && kv_len - (nc_all - 1) * KC <= 16;
@@ -571,7 +573,8 @@ static hipError_t launch_res_nw(const AttnArgs& a, int B, int nkc, hipStream_t s
     hipFuncSetAttribute((const void*)attn_res_kernel<D, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((attn_res_kernel<D, NW>), dim3(a.H, B), dim3(64 * NW), lds, stream, a, nkc);
+  hipLaunchKernelGGL((attn_res_kernel<D, NW>), dim3(a.H, B), dim3(64 * NW), lds, stream, a, nkc,
+                     tuning(TUNE_ATTN_SPLIT_TAIL));
   return hipGetLastError();
 }
 

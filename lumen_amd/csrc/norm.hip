@@ -7,6 +7,7 @@
 // packages/lumen-clip/src/lumen_clip/backends/onnxrt_backend.py:458,545-546 and
 // packages/lumen-face/src/lumen_face/backends/onnxrt_backend.py:1341-1343.
 #include "common.h"
+#include "tuning.h"
 
 namespace lumen {
 
@@ -331,7 +332,7 @@ ln_row_stats_multi_kernel(const uint16_t* __restrict__ x, int64_t x_stride, floa
 hipError_t ln_row_stats(const uint16_t* x, int64_t x_stride, float* out, int rows, int D, float eps,
                         hipStream_t stream, uint8_t* q8, int64_t ldq, uint8_t* qs, int64_t ldqs) {
   if (D % 8 != 0 || D > 64 * 8 * 8 || rows <= 0 || (q8 != nullptr && D % 128 != 0)) return hipErrorInvalidValue;
-  if (q8 == nullptr && D <= 1024 && rows >= 16384) {   // large row counts: 4 rows per wave
+  if (q8 == nullptr && D <= 1024 && rows >= 16384 && tuning(TUNE_LN_MULTI_ROW)) {   // large row counts: 4 rows per wave
     const dim3 g4((rows + 15) / 16);
     if (D <= 512) hipLaunchKernelGGL((ln_row_stats_multi_kernel<1, 4>), g4, dim3(256), 0, stream, x, x_stride, out, rows, D, eps);
     else hipLaunchKernelGGL((ln_row_stats_multi_kernel<2, 4>), g4, dim3(256), 0, stream, x, x_stride, out, rows, D, eps);

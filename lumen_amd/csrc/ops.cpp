@@ -18,6 +18,7 @@
 
 #include "gemm_epi.h"
 #include "attention.h"
+#include "tuning.h"
 #include "conv.h"
 
 namespace lumen {
@@ -84,6 +85,11 @@ uint32_t* splitk_counters(const at::Tensor& like, int64_t tiles) {
   if (!t.defined() || t.numel() < tiles)
     t = at::zeros({std::max<int64_t>(tiles, 16384)}, like.options().dtype(at::kInt));
   return reinterpret_cast<uint32_t*>(t.data_ptr());
+}
+static int g_tuning[TUNE_COUNT] = {1, 1};
+int tuning(int flag) { return flag >= 0 && flag < TUNE_COUNT ? g_tuning[flag] : 0; }
+void set_tuning(int flag, int value) {
+  if (flag >= 0 && flag < TUNE_COUNT) g_tuning[flag] = value;
 }
 }  // namespace lumen
 
@@ -578,6 +584,13 @@ void rms_norm_quant_fp8(const at::Tensor& x, const c10::optional<at::Tensor>& ad
 }
 
 // profiling: route per-workgroup timestamps of the gemm / gemm_lnf ops into dbg [wg, 4] (empty: off)
+// in-process A/B switch of a kernel variant (csrc/tuning.h); returns the previous value
+int64_t set_tuning_op(int64_t flag, int64_t value) {
+  const int prev = lumen::tuning((int)flag);
+  lumen::set_tuning((int)flag, (int)value);
+  return prev;
+}
+
 void gemm_set_dbg(const at::Tensor& dbg) {
   TORCH_CHECK(dbg.is_cuda() && dbg.scalar_type() == at::kLong && dbg.is_contiguous(), "gemm_set_dbg: int64");
   g_gemm_dbg = dbg.numel() > 0 ? dbg.data_ptr<int64_t>() : nullptr;
@@ -969,6 +982,7 @@ TORCH_LIBRARY(lumen, m) {
   m.def("ln_row_stats(Tensor x, Tensor(o!) out, float eps, Tensor(q!)? q8=None, Tensor(s!)? qs=None) -> ()");
   m.def("gemm_probe(Tensor a, Tensor w, Tensor(o!) out, Tensor(d!) dbg, int tile) -> ()");
   m.def("gemm_set_dbg(Tensor dbg) -> ()");
+  m.def("set_tuning(int flag, int value) -> int", &set_tuning_op);
   m.def("gemm_w8(Tensor a, Tensor w8, Tensor scale, Tensor? bias, Tensor? residual, int act, Tensor(o!) out, "
         "int glu) -> ()");
   m.def("gemm_dec(Tensor a, Tensor w, Tensor? scale, Tensor? bias, Tensor? residual, Tensor(o!) out, int glu, "

@@ -3,6 +3,7 @@
 module flag of lumen_amd.models.clip off and on.
 
     python tools/tower_ab.py --flag _LN_FOLD [--model ViT-L-14] [--batch 512] [--rounds 5] [--steps 10]
+    python tools/tower_ab.py --tuning attn_split_tail     # a kernel-variant switch (csrc/tuning.h) instead
 """
 import argparse
 import json
@@ -24,18 +25,32 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--tuning", default=None, help="csrc/tuning.h switch: attn_split_tail | ln_multi_row")
     args = ap.parse_args()
     load_hip(required=True)
     dev = torch.device("cuda")
     m = clip_mod.CLIPModel.random(clip_mod.PRESETS[args.model], seed=0, device=dev, with_text=False)
     imgs = torch.randint(0, 256, (args.batch, 256, 256, 3), dtype=torch.uint8, device=dev)
-    base = getattr(clip_mod, args.flag)
+    tune = {"attn_split_tail": 0, "ln_multi_row": 1}.get(args.tuning) if args.tuning else None
+    ops = load_hip(required=True) if tune is not None else None
+    if tune is not None:
+        from lumen_amd._native import hip_ops
+
+        def setter(v):
+            hip_ops().set_tuning(tune, int(v))
+        base = True
+        args.flag = f"tuning:{args.tuning}"
+    else:
+        base = getattr(clip_mod, args.flag)
+
+        def setter(v):
+            setattr(clip_mod, args.flag, v)
     arms = {"off": False if isinstance(base, bool) else 0, "on": True if isinstance(base, bool) else 1}
     res = {k: [] for k in arms}
     outs = {}
     for r in range(args.rounds + 1):
         for name, val in arms.items():
-            setattr(clip_mod, args.flag, val)
+            setter(val)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(args.steps):
@@ -45,7 +60,7 @@ def main():
             if r > 0:                                   # round 0 = warm-up of both arms
                 res[name].append(args.batch * args.steps / dt)
             outs[name] = e.float().cpu()
-    setattr(clip_mod, args.flag, base)
+    setter(base)
     cos = float((outs["off"] * outs["on"]).sum(-1).min())
     print(json.dumps({"flag": args.flag, "model": args.model, "batch": args.batch,
                       "images_per_s": {k: [round(x, 1) for x in v] for k, v in res.items()},
