@@ -174,28 +174,53 @@ def nms_ref(boxes: np.ndarray, scores: np.ndarray, thr: float) -> np.ndarray:
     return np.array(keep, dtype=np.int32)
 
 
+NMS_ASYNC_ROWS = 64     # kept rows per image gathered + copied before the host looks at the counts
+
+
+def nms_async(cand: torch.Tensor, count: torch.Tensor, iou_thr: float, max_out: int = 1024):
+    """Queue per-image NMS on the stream without waiting: the kernel, a device gather of each
+    image's first NMS_ASYNC_ROWS kept rows and ONE non-blocking D2H of (counts, rows) into pinned
+    memory.  :func:`nms_wait` returns what :func:`nms` does; only an image that kept more rows
+    than the gathered window costs a second (synchronous) copy.  A pipelined caller queues batch
+    i + 1's detector behind this and parses batch i on the host while it runs."""
+    N, MC, C = cand.shape
+    keep = torch.empty((N, max_out), dtype=torch.int32, device=cand.device)
+    keep_n = torch.empty((N,), dtype=torch.int32, device=cand.device)
+    hip_ops().nms(cand, count, float(iou_thr), keep, keep_n)
+    w = min(NMS_ASYNC_ROWS, max_out)
+    # slots past an image's count hold stale indices: clamp them into range, the host drops them
+    idx = keep[:, :w].long().clamp_(0, MC - 1)
+    rows = torch.gather(cand, 1, idx.unsqueeze(-1).expand(N, w, C))
+    host_rows = torch.empty((N, w, C), dtype=cand.dtype, pin_memory=True)
+    host_n = torch.empty((N,), dtype=torch.int32, pin_memory=True)
+    host_rows.copy_(rows, non_blocking=True)
+    host_n.copy_(keep_n, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    return cand, keep, host_rows, host_n, ev
+
+
+def nms_wait(h):
+    """Host half of :func:`nms_async`: waits for the copy, per image kept rows [k, 16]."""
+    cand, keep, host_rows, host_n, ev = h
+    ev.synchronize()
+    counts = host_n.tolist()
+    w = host_rows.shape[1]
+    out = [host_rows[n, :min(c, w)] for n, c in enumerate(counts)]
+    big = [n for n, c in enumerate(counts) if c > w]
+    for n in big:       # rare: an image kept more rows than the window -- fetch the rest
+        rest = cand[n, keep[n, w:counts[n]].long()].cpu()
+        out[n] = torch.cat([out[n], rest])
+    return out
+
+
 def nms(cand: torch.Tensor, count: torch.Tensor, iou_thr: float, max_out: int = 1024):
     """Per-image NMS -> list (per image) of kept candidate rows [k, 16] (score-descending)."""
     N, MC, _ = cand.shape
     if cand.is_cuda:
-        keep = torch.empty((N, max_out), dtype=torch.int32, device=cand.device)
-        keep_n = torch.empty((N,), dtype=torch.int32, device=cand.device)
-        hip_ops().nms(cand, count, float(iou_thr), keep, keep_n)
         # kept rows gathered on the device, then ONE small copy: the whole candidate block
         # (N x MC x 64 B, MBs for a batch) never crosses to the host
-        counts = keep_n.cpu().tolist()
-        tot = sum(counts)
-        if tot == 0:
-            return [torch.zeros((0, cand.shape[2]), dtype=cand.dtype) for _ in range(N)]
-        n_idx = np.repeat(np.arange(N, dtype=np.int64), counts)
-        j_idx = np.concatenate([np.arange(c, dtype=np.int64) for c in counts])
-        nd, jd = h2d(n_idx, cand.device), h2d(j_idx, cand.device)
-        rows = cand[nd, keep[nd, jd].long()].cpu()
-        out, o = [], 0
-        for c in counts:
-            out.append(rows[o:o + c])
-            o += c
-        return out
+        return nms_wait(nms_async(cand, count, iou_thr, max_out))
     out = []
     for n in range(N):
         c = min(int(count[n]), MC)

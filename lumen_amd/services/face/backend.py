@@ -322,10 +322,11 @@ class MI355XFaceBackend:
         return self.detect_finish(self.detect_launch(images, params, pre))
 
     def detect_finish(self, st) -> list[list[FaceDetection]]:
-        """Second half of :meth:`detect_images`: decode + NMS kernels, the D2H of the kept rows
-        (synchronises) and the host parse."""
-        images, params, heads, scales = st
-        return self._det_post(images, params, heads, scales)
+        """Second half of :meth:`detect_images`: waits for the kept rows' D2H (queued by
+        :meth:`detect_launch`) and parses them on the host."""
+        images, pend = st
+        with stage("det_parse"):
+            return self._det_parse(len(images), pend)
 
     @torch.no_grad()
     def detect_launch(self, images: Sequence[np.ndarray], params: Sequence[DetParams], pre=None):
@@ -371,19 +372,16 @@ class MI355XFaceBackend:
                                device=self.device, src=src, swap_rb=bool(getattr(sp, "det_bgr", False)))
         with stage("det_forward"):
             heads = self.det(x)
-        return images, params, heads, scales
+        with stage("det_decode_nms"):      # decode + NMS kernels + the kept rows' async D2H
+            return images, self._det_post_launch(images, params, heads, scales)
 
-    def _det_post(self, images, params, heads, scales) -> list[list[FaceDetection]]:
-        N = len(images)
-        with stage("det_decode_nms"):      # decode + NMS kernels, the D2H of kept rows synchronises
-            return self._det_post_inner(images, params, heads, scales, N)
-
-    def _det_post_inner(self, images, params, heads, scales, N) -> list[list[FaceDetection]]:
+    def _det_post_launch(self, images, params, heads, scales):
+        """Queue decode + NMS per parameter group; -> [(image indices, NMS handle or rows)]."""
         img_scale = h2d(scales, self.device, torch.float32)
         img_hw = h2d([[im.shape[0], im.shape[1]] for im in images], self.device, torch.float32)
         A = self.det.cfg.anchors
         box_det = hasattr(self.det, "decode")       # RetinaFace-family / generic exports (onnx_pack)
-        results: list[Optional[list[FaceDetection]]] = [None] * N
+        pend = []
         groups: dict = {}
         for i, p in enumerate(params):
             groups.setdefault(p.key(), []).append(i)
@@ -403,7 +401,15 @@ class MI355XFaceBackend:
                     hh = h if sel is None else h.index_select(0, sel)
                     vision.det_decode_head(hh, A, stride, p.conf, isc, ihw, cand, count, float(p.size_min),
                                            float(p.size_max))
-            kept = vision.nms(cand, count, p.nms)
+            pend.append((idx, vision.nms_async(cand, count, p.nms) if cand.is_cuda
+                         else vision.nms(cand, count, p.nms)))
+        return pend
+
+    @staticmethod
+    def _det_parse(N, pend) -> list[list[FaceDetection]]:
+        results: list[Optional[list[FaceDetection]]] = [None] * N
+        for idx, h in pend:
+            kept = vision.nms_wait(h) if isinstance(h, tuple) else h
             for j, rows in zip(idx, kept):
                 faces = []
                 for r in rows.tolist():
@@ -526,6 +532,12 @@ class MI355XFaceBackend:
             emb = self.embed_faces(srcs, list(range(len(srcs))), np.stack(minvs), reps) if srcs else None
             dim = self.rec.cfg.embedding
             return [emb[k] if k >= 0 else np.zeros(dim, np.float32) for k in slot]
+        emb = self.embed_faces(*self._standard_geom(items))
+        return list(emb)
+
+    def _standard_geom(self, items):
+        """(unique images, per-face image index, [F, 2, 3] dst->src maps) of (image, landmarks,
+        bbox) items; identical image objects are listed (and uploaded) once."""
         uniq: dict = {}
         images, index, minvs = [], [], []
         for img, lm, bb in items:
@@ -535,8 +547,7 @@ class MI355XFaceBackend:
                 images.append(img)
             index.append(uniq[k])
             minvs.append(self._minv_for(img, lm, bb))
-        emb = self.embed_faces(images, index, np.stack(minvs))
-        return list(emb)
+        return images, index, np.stack(minvs)
 
     # ------------------------------------------------------------------ public API (reference contract)
     def _payload(self, image_bytes: bytes):
@@ -629,6 +640,18 @@ class MI355XFaceBackend:
         """Every face of a batch of decoded images (detections capped at max_faces[i] when > 0)
         aligned + embedded as ONE recogniser batch -> per image [(FaceDetection, embedding)].
         A failed embedding yields zero vectors like the reference (face_model.py:357-364)."""
+        kept, flat, owner = self._flatten_dets(images, dets, max_faces)
+        embs: list = []
+        if flat:
+            try:
+                embs = self._embed_batch(flat)
+            except Exception as e:  # noqa: BLE001
+                log.warning("face embedding failed: %s", e)
+                embs = [np.zeros((self.rec.cfg.embedding,), np.float32) for _ in flat]
+        return self._per_image(kept, owner, embs)
+
+    @staticmethod
+    def _flatten_dets(images, dets, max_faces):
         kept, flat, owner = [], [], []
         for k, (img, d) in enumerate(zip(images, dets)):
             mf = int(max_faces[k])
@@ -637,17 +660,37 @@ class MI355XFaceBackend:
             for f in d:
                 flat.append((img, f.landmarks, f.bbox))
                 owner.append(k)
-        embs: list = []
-        if flat:
-            try:
-                embs = self._embed_batch(flat)
-            except Exception as e:  # noqa: BLE001
-                log.warning("face embedding failed: %s", e)
-                embs = [np.zeros((self.rec.cfg.embedding,), np.float32) for _ in flat]
-        per: list = [[] for _ in images]
+        return kept, flat, owner
+
+    @staticmethod
+    def _per_image(kept, owner, embs):
+        per: list = [[] for _ in kept]
         for k, e in zip(owner, embs):
             per[k].append(e)
-        return [list(zip(kept[k], per[k])) for k in range(len(images))]
+        return [list(zip(kept[k], per[k])) for k in range(len(kept))]
+
+    @torch.no_grad()
+    def embed_batch_detections_async(self, images: Sequence[np.ndarray], dets: Sequence[Sequence[FaceDetection]],
+                                     max_faces: Sequence[int]):
+        """:meth:`embed_batch_detections` without the wait (standard alignment on a GPU): the
+        host geometry runs here, warp + recogniser + the embeddings' D2H are queued, and
+        :meth:`embed_batch_detections_wait` assembles the per-image result.  A pipelined caller
+        queues batch i + 1's detector between the two (tools/face_ocr_bench.py --real-dets)."""
+        kept, flat, owner = self._flatten_dets(images, dets, max_faces)
+        if flat and self.align_mode != "reference" and self.device.type == "cuda":
+            try:
+                with stage("align_rec_launch"):
+                    return "pend", self.embed_faces_async(*self._standard_geom(flat)), kept, owner
+            except Exception as e:  # noqa: BLE001 -- the synchronous path below logs + zero-fills
+                log.warning("async face embedding launch failed (%s); embedding synchronously", e)
+        return "done", self.embed_batch_detections(images, dets, max_faces)
+
+    def embed_batch_detections_wait(self, h) -> list[list[tuple[FaceDetection, np.ndarray]]]:
+        if h[0] == "done":
+            return h[1]
+        _, eh, kept, owner = h
+        with stage("rec_wait"):
+            return self._per_image(kept, owner, list(self.embed_wait(eh)))
 
     def detect_and_embed_images(self, images: Sequence[np.ndarray], params: Sequence[DetParams],
                                 max_faces: int = -1) -> list[list[tuple[FaceDetection, np.ndarray]]]:

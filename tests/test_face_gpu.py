@@ -142,3 +142,34 @@ def test_face_engine_device_jpeg_matches_pillow(tmp_path, monkeypatch):
             assert float(np.dot(d[0][1], h[0][1])) > 0.95
     finally:
         svc.close()
+
+
+def test_pipelined_detect_embed_matches_sync(tmp_path):
+    """Two detector batches in flight (detect_launch x2, detect_finish, the async batch embedding
+    queued behind the second detector) give the synchronous detect_and_embed_images result."""
+    from lumen_amd.services.face.backend import DetParams
+
+    write_face_model(tmp_path / "models" / "buffalo_tiny", "buffalo_tiny")
+    cfg = config_from_dict(_cfg(tmp_path, "cuda"))
+    svc = GeneralFaceService.from_config(cfg.services["face"], tmp_path)
+    svc.initialize()
+    try:
+        be = svc.backend
+        rng = np.random.default_rng(11)
+        batches = [[rng.integers(0, 255, (96 + 8 * k, 160 - 4 * k, 3), dtype=np.uint8) for k in range(3)]
+                   for _ in range(2)]
+        p = [DetParams(0.0, 0.3, 0, 10000)] * 3
+        ref = [be.detect_and_embed_images(b, p, 4) for b in batches]
+        st = [be.detect_launch(b, p) for b in batches]
+        got = []
+        for b, s in zip(batches, st):
+            h = be.embed_batch_detections_async(b, be.detect_finish(s), [4] * len(b))
+            got.append(be.embed_batch_detections_wait(h))
+        for g_, r_ in zip(got, ref):
+            for gi, ri in zip(g_, r_):
+                assert len(gi) == len(ri) > 0
+                for (fg, eg), (fr, er) in zip(gi, ri):
+                    assert np.abs(np.array(fg.bbox) - np.array(fr.bbox)).max() < 1e-3
+                    assert float(np.dot(eg, er)) > 0.999
+    finally:
+        svc.close()

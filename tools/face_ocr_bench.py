@@ -149,15 +149,18 @@ def bench_face(args):
             if runner is not None:
                 res = runner.run(imgs, [params[0]] * len(imgs), args.faces)
             elif args.pipeline:
-                # pipelined: batch i + 1's upload + detector are queued as soon as batch i's detections are
-                # on the host, ahead of batch i's alignment / recogniser (detect_launch / detect_finish)
-                if not pend:
+                # pipelined, two detector batches in flight: batch i's kept rows are parsed while batch
+                # i + 1's detector runs; batch i's warp + recogniser are queued behind it, then batch
+                # i + 2's detector, and only then are batch i's embeddings waited for -- the GPU always
+                # has the next batch queued while the host parses / builds the alignment geometry
+                while len(pend) < 2:
                     pend.append(be.detect_launch(imgs, params[:len(imgs)]))
-                st0 = pend.pop()
+                st0 = pend.pop(0)
                 dets = be.detect_finish(st0)
+                h = be.embed_batch_detections_async(st0[0], dets, [args.faces] * len(st0[0]))
                 nimgs = [np.asarray(im) for im in dec()]
                 pend.append(be.detect_launch(nimgs, params[:len(nimgs)]))
-                res = be.embed_batch_detections(st0[0], dets, [args.faces] * len(st0[0]))
+                res = be.embed_batch_detections_wait(h)
             else:
                 res = be.detect_and_embed_images(imgs, params[:len(imgs)], args.faces)
         found.append(sum(len(f) for f in res) / max(len(res), 1))
@@ -212,8 +215,8 @@ def bench_face(args):
             "image_kind": args.image_kind, "jpeg_kb": round(sum(len(j) for j in jpegs) / len(jpegs) / 1024, 1),
             "pipeline": ("real detections on the detector's own output, images pre-decoded, " +
                          ("SPMDFaceRunner.run" if runner is not None else
-                          "batch i+1's detector queued before batch i's alignment + recogniser (detect_launch / "
-                          "detect_finish / embed_batch_detections)" if args.pipeline else "detect_and_embed_images")
+                          "two detector batches in flight: batch i+2's detector queued behind batch i's recogniser (detect_launch / "
+                          "detect_finish / embed_batch_detections_async)" if args.pipeline else "detect_and_embed_images")
                          if args.real_dets else
                          "JPEG decode + pinned staging + H2D (own stream) of batch i+1 overlapped with the GPU "
                          "work of batch i; batch i+1's detector queued before batch i's embeddings are read"),
