@@ -49,5 +49,7 @@ hipError_t upsample_add(const uint16_t* x, const uint16_t* add, uint16_t* out, i
                         int64_t ldo, hipStream_t stream);
 hipError_t channel_scale(uint16_t* x, const float* s, int N, int HW, int C, hipStream_t stream);
 hipError_t pixel_shuffle_up(const uint16_t* y, uint16_t* out, int N, int H, int W, int C, int f, hipStream_t stream);
+hipError_t db_head_up(const uint16_t* h, const uint16_t* w1, const float* b1, const uint16_t* w2p, const float* b2,
+                      float* out, int N, int H4, int W4, int C, hipStream_t stream);
 
 }  // namespace lumen

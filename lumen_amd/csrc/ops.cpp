@@ -583,7 +583,6 @@ void rms_norm_quant_fp8(const at::Tensor& x, const c10::optional<at::Tensor>& ad
                                             scale.data_ptr<float>(), (int)M, (int)K, cur_stream()));
 }
 
-// profiling: route per-workgroup timestamps of the gemm / gemm_lnf ops into dbg [wg, 4] (empty: off)
 // in-process A/B switch of a kernel variant (csrc/tuning.h); returns the previous value
 int64_t set_tuning_op(int64_t flag, int64_t value) {
   const int prev = lumen::tuning((int)flag);
@@ -591,6 +590,7 @@ int64_t set_tuning_op(int64_t flag, int64_t value) {
   return prev;
 }
 
+// profiling: route per-workgroup timestamps of the gemm / gemm_lnf ops into dbg [wg, 4] (empty: off)
 void gemm_set_dbg(const at::Tensor& dbg) {
   TORCH_CHECK(dbg.is_cuda() && dbg.scalar_type() == at::kLong && dbg.is_contiguous(), "gemm_set_dbg: int64");
   g_gemm_dbg = dbg.numel() > 0 ? dbg.data_ptr<int64_t>() : nullptr;
@@ -969,6 +969,28 @@ void pixel_shuffle_up(const at::Tensor& y, at::Tensor out, int64_t factor) {
                                           (int)factor, cur_stream()));
 }
 
+// DBNet head tail (csrc/conv.hip db_head_up): h [N, H4, W4, C] bf16 -> prob [N, 4*H4, 4*W4] fp32
+void db_head_up(const at::Tensor& h, const at::Tensor& w1, const at::Tensor& b1, const at::Tensor& w2p,
+                const at::Tensor& b2, at::Tensor out) {
+  check_gpu(h, "h");
+  TORCH_CHECK(h.dim() == 4 && h.is_contiguous() && h.scalar_type() == at::kBFloat16, "db_head_up: h NHWC bf16");
+  const int64_t N = h.size(0), H4 = h.size(1), W4 = h.size(2), C = h.size(3);
+  TORCH_CHECK(C == 16 || C == 32, "db_head_up: C must be 16 or 32");
+  TORCH_CHECK(w1.is_contiguous() && w1.scalar_type() == at::kBFloat16 && w1.size(0) == 4 * C && w1.size(1) == C,
+              "db_head_up: w1 [4C, C] bf16");
+  TORCH_CHECK(b1.is_contiguous() && b1.scalar_type() == at::kFloat && b1.numel() == 4 * C, "db_head_up: b1 [4C] fp32");
+  TORCH_CHECK(w2p.is_contiguous() && w2p.scalar_type() == at::kBFloat16 && w2p.numel() == 4 * 64 * 8,
+              "db_head_up: w2p [4, 64, 8] bf16");
+  TORCH_CHECK(b2.is_contiguous() && b2.scalar_type() == at::kFloat && b2.numel() >= 4, "db_head_up: b2 [4] fp32");
+  TORCH_CHECK(out.is_contiguous() && out.scalar_type() == at::kFloat && out.dim() == 3 && out.size(0) == N &&
+              out.size(1) == 4 * H4 && out.size(2) == 4 * W4, "db_head_up: out [N, 4*H4, 4*W4] fp32");
+  for (const at::Tensor* t : {&w1, &b1, &w2p, &b2, (const at::Tensor*)&out})
+    TORCH_CHECK(t->device() == h.device(), "db_head_up: device");
+  const at::DeviceGuard guard(h.device());
+  LM_CHECK_HIP(lumen::db_head_up(bf(h), bf(w1), b1.data_ptr<float>(), bf(w2p), b2.data_ptr<float>(),
+                                 out.data_ptr<float>(), (int)N, (int)H4, (int)W4, (int)C, cur_stream()));
+}
+
 }  // namespace
 
 TORCH_LIBRARY(lumen, m) {
@@ -1017,6 +1039,7 @@ TORCH_LIBRARY(lumen, m) {
   m.def("upsample_add(Tensor x, Tensor? add, Tensor(o!) out, int factor) -> ()");
   m.def("channel_scale_(Tensor(a!) x, Tensor s) -> ()");
   m.def("pixel_shuffle_up(Tensor y, Tensor(o!) out, int factor) -> ()");
+  m.def("db_head_up(Tensor h, Tensor w1, Tensor b1, Tensor w2p, Tensor b2, Tensor(o!) out) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
@@ -1048,4 +1071,5 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("upsample_add", &upsample_add);
   m.impl("channel_scale_", &channel_scale_);
   m.impl("pixel_shuffle_up", &pixel_shuffle_up);
+  m.impl("db_head_up", &db_head_up);
 }

@@ -147,6 +147,22 @@ class DBNet(nn.Module):
             elif isinstance(m, (SE, ConvT2)):
                 m.random_init(g)
 
+    def _head_weights(self, device):
+        """(w1 [4C, C], b1 [4C], w2p [4, 64, 8], b2 [4]) of the fused head tail, rebuilt when the
+        ConvT2 weights change (load / random_init bump the parameters' versions)."""
+        g1, g2 = self.up1.g, self.up2.g
+        key = (str(device), g1.w.data_ptr(), g1.w._version, g1.b._version, g2.w.data_ptr(), g2.w._version,
+               g2.b._version)
+        c = getattr(self, "_head_cache", None)
+        if c is None or c[0] != key:
+            C = self.up1.cout
+            w1 = g1.w[:4 * C, :C].to(device=device, dtype=torch.bfloat16).contiguous()
+            b1 = g1.b[:4 * C].to(device=device, dtype=torch.float32).contiguous()
+            w2p = cnn.db_head_pack_up2(g2.w[:4, :C]).to(device)
+            b2 = g2.b[:4].to(device=device, dtype=torch.float32).contiguous()
+            c = self._head_cache = (key, (w1, b1, w2p, b2))
+        return c[1]
+
     @torch.no_grad()
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """x NHWC8 [N, H, W, 8] (H, W multiples of 32) -> probability map fp32 [N, H, W]."""
@@ -171,6 +187,9 @@ class DBNet(nn.Module):
             else:
                 cnn.upsample_add(self.smooth[i](p), None, 2 ** i, out=sl)
         h = self.head_conv(cat)
+        if h.is_cuda and h.shape[-1] in (16, 32) and self.up1.cout == h.shape[-1] and self.up2.cout == 1:
+            # up1 + ReLU + shuffle + up2 + sigmoid + the final interleave in one MFMA pass (ops.cnn.db_head_up)
+            return cnn.db_head_up(h, *self._head_weights(h.device))
         h = self.up1(h)
         y = self.up2.gemm(h)                         # [N, H/2, W/2, 4] fp32, sigmoid applied
         N, Hh, Wh, _ = y.shape

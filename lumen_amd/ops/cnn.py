@@ -8,6 +8,7 @@ from __future__ import annotations
 
 from typing import Optional
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -179,6 +180,36 @@ def pixel_shuffle_up(y, C, factor=2):
     t = y.reshape(N, H, W, factor, factor, C).permute(0, 1, 3, 2, 4, 5).reshape(N, H * factor, W * factor, C)
     out.copy_(t)
     return out
+
+
+def db_head_up(h, w1, b1, w2p, b2):
+    """DBNet head tail fused (csrc/conv.hip db_head_up): h [N, H4, W4, C] bf16 (C 16 or 32) through
+    up1 (2x2 s2 ConvTranspose C -> C + ReLU, weights w1 [4C, C] bf16 / b1 [4C] fp32) and up2 (2x2 s2
+    ConvTranspose C -> 1 + sigmoid, MFMA-packed w2p [4, 64, 8] from :func:`db_head_pack_up2`, b2 [4])
+    -> probability map [N, 4*H4, 4*W4] fp32."""
+    N, H4, W4, _ = h.shape
+    out = torch.empty((N, 4 * H4, 4 * W4), device=h.device, dtype=torch.float32)
+    hip_ops().db_head_up(h, w1, b1, w2p, b2, out)
+    return out
+
+
+def db_head_pack_up2(w2: torch.Tensor) -> torch.Tensor:
+    """up2's weights [4 (kh*2 + kw), C] -> the A fragments of db_head_up's four k-steps [4, 64, 8] bf16:
+    k-step s1, lane l holds row l & 15 (= 4*s1 + s2 when nonzero) at the permuted channels
+    c(l >> 4, j) = 4*(l >> 4) + j for j < 4, 12 + 4*(l >> 4) + j for j >= 4 (see the kernel)."""
+    C = w2.shape[1]
+    lane = np.arange(64)
+    row, hq = lane & 15, lane >> 4
+    j = np.arange(8)
+    c = np.where(j[None, :] < 4, 4 * hq[:, None] + j[None, :], 12 + 4 * hq[:, None] + j[None, :])    # [64, 8]
+    w = w2.float().cpu().numpy()
+    out = np.zeros((4, 64, 8), np.float32)
+    for s1 in range(4):
+        sel = (row >> 2) == s1
+        ok = sel[:, None] & (c < C)
+        vals = w[(row & 3)[:, None].repeat(8, 1), np.minimum(c, C - 1)]
+        out[s1] = np.where(ok, vals, 0.0)
+    return torch.from_numpy(out).to(torch.bfloat16)
 
 
 def conv_weight_from_torch(w: torch.Tensor, cin_pad: Optional[int] = None) -> torch.Tensor:

@@ -26,6 +26,36 @@ def test_dbnet_mobile_full_size():
     assert ((got > 0.3) == (ref > 0.3)).float().mean().item() > 0.98
 
 
+@pytest.mark.parametrize("C", [16, 32])
+def test_db_head_up_fused_vs_fp32(C):
+    """csrc/conv.hip db_head_up (up1 + ReLU + shuffle + up2 + sigmoid in one MFMA pass) against the
+    fp32 CPU path of the same head tail; 7 x 9 pixels per image: a partial 16-pixel group and groups
+    that span image rows and images."""
+    from lumen_amd.models.ocr import ConvT2
+    from lumen_amd.ops import cnn
+
+    g = torch.Generator().manual_seed(C)
+    up1 = ConvT2(C, C, act="relu")
+    up2 = ConvT2(C, 1, act="sigmoid", out_dtype=torch.float32)
+    up1.random_init(g)
+    up2.random_init(g)
+    up1.g.b.data[:4 * C] = torch.randn(4 * C, generator=g) * 0.1
+    up2.g.b.data[:4] = torch.randn(4, generator=g) * 0.1
+    N, H4, W4 = 3, 7, 9
+    h = torch.randn(N, H4, W4, C, generator=g).bfloat16()
+    y = up2.gemm(up1(h.float()))
+    ref = y.view(N, 2 * H4, 2 * W4, 2, 2).permute(0, 1, 3, 2, 4).reshape(N, 4 * H4, 4 * W4).float()
+    dev = torch.device("cuda")
+    w1 = up1.g.w[:4 * C, :C].to(dev, torch.bfloat16).contiguous()
+    b1 = up1.g.b[:4 * C].to(dev, torch.float32).contiguous()
+    w2p = cnn.db_head_pack_up2(up2.g.w[:4, :C]).to(dev)
+    b2 = up2.g.b[:4].to(dev, torch.float32).contiguous()
+    got = cnn.db_head_up(h.to(dev), w1, b1, w2p, b2).cpu()
+    assert got.shape == ref.shape
+    # bf16 up1 output (as in the unfused GPU path) vs fp32: sigmoid outputs agree to ~1e-2
+    assert (got - ref).abs().max().item() < 2e-2
+
+
 def test_svtr_mobile():
     g = torch.Generator().manual_seed(1)
     m = SVTRRecognizer(REC_PRESETS["mobile"])

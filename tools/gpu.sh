@@ -37,6 +37,8 @@
 #   acc            full-size fp8 accuracy pins (ViT-L/14-336 W8A8, Llama-3-8B first token)
 #   vlm_service    service-level TTFT: gRPC vlm_generate_stream first chunk (tools/vlm_service_ttft.py)
 #   vlm_service_fe the same through 2 front ends + 1 GPU engine, 32 streamed tokens
+#   vlm_service32  in-process hub, 32 streamed tokens (inter-chunk time, engine counters)
+#   attn           tools/attn_bench.py (ViT / text / prefill shapes; split-tail switch A/B)
 #   serve128       CLIP serving through 8 front ends, 128 clients from 6 client processes
 #   fe_gpu         engine / front-end topology GPU test (tests/test_frontends_gpu.py)
 #   face_real      face bench on the detector's real output (detect_and_embed_images; SPMD path under torchrun)
@@ -178,6 +180,9 @@ for task in "$@"; do
       --timeout 200 --timeout-method thread ;;
     acc) step acc 400 python -u -m pytest tests/test_fp8_accuracy_gpu.py -x -v --timeout 300 --timeout-method thread ;;
     vlm_service) step vlm_service 500 python -u tools/vlm_service_ttft.py --n 30 --max-new 1 ;;
+    vlm_service32)   # in-process hub, 32 new tokens streamed (inter-chunk time + engine counters)
+      step vlm_service32 500 python -u tools/vlm_service_ttft.py --n 20 --max-new 32 ;;
+    attn) step attn 200 python -u tools/attn_bench.py ;;
     vlm_service_fe)   # service TTFT through 2 front ends + 1 engine, 32 new tokens streamed
       step vlm_service_fe 600 python -u tools/vlm_service_ttft.py --n 30 --max-new 32 --frontends 2 ;;
     serve128)   # CLIP through front ends, 128 clients from 6 client processes

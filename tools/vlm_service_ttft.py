@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--max-new", type=int, default=8)
     ap.add_argument("--fp8", type=int, default=1)
     ap.add_argument("--frontends", type=int, default=0)
+    ap.add_argument("--preset", default="llava-llama3-8b")
+    ap.add_argument("--device", default="cuda")
     a = ap.parse_args()
     if a.fp8:
         os.environ["LUMEN_VLM_FP8"] = "1"
@@ -49,12 +51,12 @@ def main():
         so.bind(("127.0.0.1", 0))
         free_port = so.getsockname()[1]
     cache = tempfile.mkdtemp(prefix="lumen-vlm-ttft-")
-    write_vlm_model(os.path.join(cache, "models", "llava-llama3-8b"), "llava-llama3-8b")
+    write_vlm_model(os.path.join(cache, "models", a.preset), a.preset)
     svc = {"enabled": True, "package": "lumen_vlm",
            "import_info": {"registry_class": "lumen_vlm.fastvlm.GeneralFastVLMService",
                            "add_to_server": "lumen_vlm.proto.ml_service_pb2_grpc.add_InferenceServicer_to_server"},
-           "backend_settings": {"device": "cuda", "batch_size": 8},
-           "models": {"general": {"model": "llava-llama3-8b", "runtime": "onnx"}}}
+           "backend_settings": {"device": a.device, "batch_size": 8},
+           "models": {"general": {"model": a.preset, "runtime": "onnx"}}}
     cfg = {"metadata": {"version": "1.0.0", "region": "other", "cache_dir": cache},
            "deployment": {"mode": "hub", "services": ["vlm"]},
            "server": {"port": free_port, "host": "127.0.0.1"}, "services": {"vlm": svc}}
@@ -74,7 +76,8 @@ def main():
         stop = threading.Event()
         ready = mp.get_context("spawn").Queue()
         th = threading.Thread(target=serve_frontends, args=(cfg_path, free_port, a.frontends),
-                              kwargs={"stop_event": stop, "ready_q": ready, "devices": ["cuda:0"]})
+                              kwargs={"stop_event": stop, "ready_q": ready,
+                                      "devices": ["cuda:0" if a.device == "cuda" else a.device]})
         th.start()
         for _ in range(a.frontends):
             ready.get(timeout=1200)
@@ -87,24 +90,35 @@ def main():
     jpeg = encode_jpeg(synth_image(np.random.default_rng(0), 768, 1024, "photo"))
     prompt = ("Describe the picture " * 8)[:a.prompt_chars]
     meta = {"prompt": prompt, "max_new_tokens": str(a.max_new)}
-    ttft, total, chunks = [], [], []
+    ttft, total, chunks, gaps = [], [], [], []
     with grpc.insecure_channel(f"127.0.0.1:{port}") as ch:
         stub = pb.InferenceStub(ch)
         for i in range(a.warmup + a.n):
             t = time.perf_counter()
-            first, n = None, 0
+            first, n, last = None, 0, None
             for r in stub.Infer(iter([pb.InferRequest(correlation_id=str(i), task="vlm_generate_stream", payload=jpeg,
                                                       payload_mime="image/jpeg", meta=meta)]), timeout=300):
                 if r.HasField("error"):
                     raise RuntimeError(r.error.message)
+                now = time.perf_counter()
                 if first is None:
-                    first = time.perf_counter()
+                    first = now
+                elif i >= a.warmup:
+                    gaps.append((now - last) * 1e3)
+                last = now
                 n += 1
             if i >= a.warmup:
                 ttft.append((first - t) * 1e3)
                 total.append((time.perf_counter() - t) * 1e3)
                 chunks.append(n)
+    eng_stats = None
     if server is not None:
+        try:
+            svc_obj = app.services["vlm"] if isinstance(app.services, dict) else app.services[0]
+            eng = svc_obj.backend.engine
+            eng_stats = dict(eng.stats, graphs=sorted(eng.graphs.graphs) if eng.graphs is not None else None)
+        except Exception as e:  # noqa: BLE001 - diagnostics only
+            eng_stats = repr(e)
         server.stop(0)
         app.close()
     else:
@@ -114,8 +128,10 @@ def main():
                       "value": round(float(np.percentile(ttft, 50)), 3), "unit": "ms",
                       "p99_ms": round(float(np.percentile(ttft, 99)), 3),
                       "request_ms_p50": round(float(np.percentile(total, 50)), 3),
-                      "chunks_per_request": float(np.median(chunks)), "n": a.n, "load_s": round(load_s, 1),
-                      "config": {"model": "LLaVA-Llama-3-8B (synthetic pack, random-init weights)",
+                      "chunks_per_request": float(np.median(chunks)), "n": a.n,
+                      "engine_stats": eng_stats,
+                      "inter_chunk_ms_p50": round(float(np.percentile(gaps, 50)), 3) if gaps else None, "load_s": round(load_s, 1),
+                      "config": {"model": f"{a.preset} (synthetic pack, random-init weights)", "device": a.device,
                                  "decoder": "fp8" if a.fp8 else "bf16", "image": f"1024x768 JPEG {len(jpeg) // 1024} KiB",
                                  "prompt_chars": a.prompt_chars, "max_new_tokens": a.max_new,
                                  "topology": f"{a.frontends} front ends + 1 GPU engine (token stream over the shm "
