@@ -358,8 +358,10 @@ def engine_main(services: dict, device: str, ready_q, stop_ev, max_items: int = 
             sx = ThreadPoolExecutor(max_workers=int(opts_of[name].get("solo_threads", 64)),
                                     thread_name_prefix=f"lumen-solo-{name}")
             solo_exs.append(sx)
+        # a solo service's requests never merge, so waiting for more to arrive only delays them
+        lg = 0 if sx is not None else linger_us
         for i in range(nthreads[name]):
-            t = threading.Thread(target=_serve_channel, args=(ch, fns[name], stop, max_items, linger_us, stats, sx),
+            t = threading.Thread(target=_serve_channel, args=(ch, fns[name], stop, max_items, lg, stats, sx),
                                  name=f"lumen-engine-{name}-{i}", daemon=True)
             t.start()
             ths.append(t)
