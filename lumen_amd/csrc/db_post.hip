@@ -5,7 +5,7 @@
 // (cv2.findContours on the thresholded bitmap, cv2.minAreaRect, box_score_fast).  Labels are
 // global pixel indices; every component's root is its smallest pixel index -- the raster-order
 // first pixel, i.e. the component order of the host two-pass labelling (max_candidates cuts
-// identically).  Four launches, bounded work per pixel:
+// identically).  Five launches, bounded work per pixel:
 //
 //   db_tile_ccl       one workgroup per 32x32 tile: threshold into LDS, union-find over the
 //                     4 "earlier" 8-neighbours INSIDE the tile with LDS atomics, flatten, and
@@ -13,7 +13,8 @@
 //                     record of every local root).  All but the tile-border unions stay in LDS.
 //   db_border_merge   the 8-neighbour pairs that cross a tile border (each tile: its left column
 //                     and top row) are unioned in global memory (atomicMin on roots; trees are
-//                     one level deep after the tile pass)
+//                     one level deep after the tile pass), one union per distinct root pair
+//   db_root_compress  every border tile-root points straight at its final root
 //   db_flatten_bbox   lab[p] = root(p) and the pixel-centre bounding box of every component from
 //                     its boundary pixels (LDS reduction for the workgroup's dominant component)
 //   db_row_extremes   (root, x, y) of the leftmost / rightmost pixel of every row of every
@@ -156,28 +157,70 @@ __global__ void __launch_bounds__(256) db_tile_ccl_kernel(const T* __restrict__ 
 }
 
 // grid (tiles_x, tiles_y, n), 64 threads: the 8-neighbour pairs crossing this tile's left column
-// (W, NW, SW) and top row (N, NW, NE) -- every cross-tile pair is some tile's left or top pair
+// (W, NW, SW) and top row (N, NW, NE) -- every cross-tile pair is some tile's left or top pair.
+// Every pixel's label is still (a node of the set of) its tile-local root, so a border of one blob
+// repeats the same (root, neighbour root) pair ~32 x 3 times: a pair equal to the previous lane's
+// (same direction) or to one of this lane's earlier directions is skipped -- one union per distinct
+// pair instead of one per pixel pair (the untrained map's giant blob serialised ~1.5M global-atomic
+// unions on a handful of roots: 336 us per 16-map batch, profiles/r6_ocr_kernel_stats_v1.txt).
 __global__ void __launch_bounds__(64) db_border_merge_kernel(int* __restrict__ lab, int H, int W) {
   const int img = blockIdx.z, tx = blockIdx.x, ty = blockIdx.y;
   const int64_t base = img * (int64_t)H * W;
   const int t = threadIdx.x & 31;
-  if (threadIdx.x < 32) {   // left column
+  const bool left = threadIdx.x < 32;
+  int la = -1, nb[3] = {-1, -1, -1};
+  if (left) {   // left column: W, NW, SW
     const int x = tx * DB_T, y = ty * DB_T + t;
-    if (x == 0 || y >= H) return;
-    const int i = (int)(base + (int64_t)y * W + x);
-    if (lab[i] < 0) return;
-    if (lab[i - 1] >= 0) db_union(lab, i, i - 1);
-    if (y > 0 && lab[i - W - 1] >= 0) db_union(lab, i, i - W - 1);
-    if (y + 1 < H && lab[i + W - 1] >= 0) db_union(lab, i, i + W - 1);
-  } else {                  // top row
+    if (x > 0 && y < H) {
+      const int i = (int)(base + (int64_t)y * W + x);
+      la = db_ld(lab, i);
+      if (la >= 0) {
+        nb[0] = db_ld(lab, i - 1);
+        if (y > 0) nb[1] = db_ld(lab, i - W - 1);
+        if (y + 1 < H) nb[2] = db_ld(lab, i + W - 1);
+      }
+    }
+  } else {      // top row: N, NW, NE
     const int x = tx * DB_T + t, y = ty * DB_T;
-    if (y == 0 || x >= W) return;
-    const int i = (int)(base + (int64_t)y * W + x);
-    if (lab[i] < 0) return;
-    if (lab[i - W] >= 0) db_union(lab, i, i - W);
-    if (x > 0 && lab[i - W - 1] >= 0) db_union(lab, i, i - W - 1);
-    if (x + 1 < W && lab[i - W + 1] >= 0) db_union(lab, i, i - W + 1);
+    if (y > 0 && x < W) {
+      const int i = (int)(base + (int64_t)y * W + x);
+      la = db_ld(lab, i);
+      if (la >= 0) {
+        nb[0] = db_ld(lab, i - W);
+        if (x > 0) nb[1] = db_ld(lab, i - W - 1);
+        if (x + 1 < W) nb[2] = db_ld(lab, i - W + 1);
+      }
+    }
   }
+  const int pa = __shfl_up(la, 1, 64);
+  const bool first = t == 0;   // lanes 0 and 32 start their own edge
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const int pb = __shfl_up(nb[d], 1, 64);
+    if (la < 0 || nb[d] < 0) continue;
+    if (!first && pa == la && pb == nb[d]) continue;              // the previous lane unions this pair
+    if (d >= 1 && nb[d] == nb[0]) continue;                       // this lane's earlier direction does
+    if (d == 2 && nb[2] == nb[1]) continue;
+    db_union(lab, la, nb[d]);
+  }
+}
+
+// grid (tiles_x, tiles_y, n), 64 threads, after db_border_merge: every border pixel's tile-local
+// root is pointed straight at its final root (db_find's path compression; no union runs any
+// more), so db_flatten_bbox's finds are <= 2 hops instead of walking the chains the merges built
+// (a blob's root chain crosses many tiles: 294 us for the flatten pass before this)
+__global__ void __launch_bounds__(64) db_root_compress_kernel(int* __restrict__ lab, int H, int W) {
+  const int img = blockIdx.z, tx = blockIdx.x, ty = blockIdx.y;
+  const int64_t base = img * (int64_t)H * W;
+  const int t = threadIdx.x & 31;
+  const int x = threadIdx.x < 32 ? tx * DB_T : tx * DB_T + t;
+  const int y = threadIdx.x < 32 ? ty * DB_T + t : ty * DB_T;
+  if (x >= W || y >= H) return;
+  const int la = db_ld(lab, (int)(base + (int64_t)y * W + x));
+  if (la < 0) return;
+  const int pa = __shfl_up(la, 1, 64);
+  if ((t != 0 && pa == la) || db_ld(lab, la) == la) return;      // the previous lane does it / a root already
+  db_find(lab, la);
 }
 
 __device__ __forceinline__ bool db_is_boundary(const int* lab, int64_t i, int x, int y, int H, int W) {
@@ -467,6 +510,7 @@ hipError_t db_components(const void* prob, int is_bf16, const float* thresh, int
     hipLaunchKernelGGL(db_tile_ccl_kernel<float>, tiles, dim3(256), 0, stream, (const float*)prob, thresh, lab, bb, H,
                        W);
   hipLaunchKernelGGL(db_border_merge_kernel, tiles, dim3(64), 0, stream, lab, H, W);
+  hipLaunchKernelGGL(db_root_compress_kernel, tiles, dim3(64), 0, stream, lab, H, W);
   hipLaunchKernelGGL(db_flatten_bbox_kernel, dim3((int)((total + 1023) / 1024)), dim3(1024), 0, stream, lab, bb, H, W,
                      total);
   (void)blocks;

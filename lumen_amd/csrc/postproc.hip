@@ -374,7 +374,7 @@ __global__ void __launch_bounds__(256) cls_argmax_kernel(const uint16_t* __restr
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      m[i][r] = -INFINITY;
+      m[i][r] = -1e30f;      // finite: the branch-free fold never forms -inf - -inf
       s[i][r] = 0.f;
       bi[i][r] = 0;
     }
@@ -403,26 +403,35 @@ __global__ void __launch_bounds__(256) cls_argmax_kernel(const uint16_t* __restr
         for (int i = 0; i < 2; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][t], fb, acc[i][j], 0, 0, 0);
       }
     }
-    // fold the tile: lane column n = nt*64 + 16j + frow, rows 16i + 4g + r (increasing n per lane)
+    // fold the tile, branch-free: lane column n_j = nt*64 + 16j + frow, rows 16i + 4g + r.  Per row slot
+    // the 4 columns' max / first arg-max and the rescaled sum of exp; a per-value branch (the old form)
+    // put ~50 instructions of exec-mask juggling on every logit (profiles/r6_ocr_kernel_stats).
+    int col[4];
+    float bl[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int n = nt * 64 + j * 16 + frow;
-      const bool ok = n < C;
-      const float b = (ok && bias) ? bias[n] : 0.f;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = ok ? (acc[i][j][r] + b) * L2E : -INFINITY;
-          if (v > m[i][r]) {
-            s[i][r] = (m[i][r] == -INFINITY ? 0.f : s[i][r] * __builtin_amdgcn_exp2f(m[i][r] - v)) + 1.f;
-            m[i][r] = v;
-            bi[i][r] = n;
-          } else if (ok) {
-            s[i][r] += __builtin_amdgcn_exp2f(v - m[i][r]);
-          }
-        }
+      col[j] = nt * 64 + j * 16 + frow;
+      bl[j] = col[j] < C ? (bias ? bias[col[j]] * L2E : 0.f) : -INFINITY;   // padding classes never win
     }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fmaf(acc[i][j][r], L2E, bl[j]);
+        const float tm = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+        int tc = col[3];
+        tc = v[2] == tm ? col[2] : tc;
+        tc = v[1] == tm ? col[1] : tc;
+        tc = v[0] == tm ? col[0] : tc;
+        const float mo = m[i][r], mn = fmaxf(mo, tm);
+        bi[i][r] = tm > mo ? tc : bi[i][r];      // strict: an equal later column keeps the earlier index
+        s[i][r] = s[i][r] * __builtin_amdgcn_exp2f(mo - mn) + __builtin_amdgcn_exp2f(v[0] - mn) +
+                  __builtin_amdgcn_exp2f(v[1] - mn) + __builtin_amdgcn_exp2f(v[2] - mn) +
+                  __builtin_amdgcn_exp2f(v[3] - mn);
+        m[i][r] = mn;
+      }
     if (nt_ + 1 < ntile) {
       __syncthreads();                 // every wave is done reading buf ^ 1 (tile nt - 1)
       store_tile(buf ^ 1, stage);
