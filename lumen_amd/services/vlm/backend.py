@@ -621,7 +621,7 @@ class MI355XVLMBackend:
                         if stop:
                             cut = inc.text[:lo] + cut
                             if len(cut) > emitted:
-                                yield GenerationChunk(text=cut[emitted:], tokens=pending, metadata={"step": step})
+                                yield GenerationChunk(text=cut[emitted:], tokens=pending, metadata={"step": step, "t_wall": time.time()})
                             self.engine.cancel(r)
                             for _ in r.stream():
                                 pass
@@ -632,14 +632,14 @@ class MI355XVLMBackend:
                             return
                     if len(inc.text) == emitted:
                         continue                # held back: an incomplete UTF-8 tail
-                    yield GenerationChunk(text=inc.text[emitted:], tokens=pending, metadata={"step": step})
+                    yield GenerationChunk(text=inc.text[emitted:], tokens=pending, metadata={"step": step, "t_wall": time.time()})
                     emitted, pending = len(inc.text), []
                     step += 1
                 else:
                     finished = True
                     inc.flush()
                     if len(inc.text) > emitted or pending:
-                        yield GenerationChunk(text=inc.text[emitted:], tokens=pending, metadata={"step": step})
+                        yield GenerationChunk(text=inc.text[emitted:], tokens=pending, metadata={"step": step, "t_wall": time.time()})
                     _engine_stages(r)
                     yield GenerationChunk(text="", is_final=True, metadata={"reason": val, "input_tokens": n_in})
         finally:

@@ -263,8 +263,10 @@ class GeneralFastVLMService(BaseInferenceService):
                 if ch.text:
                     text.append(ch.text)
                     n_chunks += 1
-                    yield ch.text.encode("utf-8"), "text/plain;charset=utf-8", \
-                        {"step": str(ch.metadata.get("step", n_chunks)), "tokens": str(n_tok)}, False
+                    m = {"step": str(ch.metadata.get("step", n_chunks)), "tokens": str(n_tok)}
+                    if "t_wall" in ch.metadata:     # when the generating process produced the chunk
+                        m["t_emit"] = f"{ch.metadata['t_wall']:.6f}"
+                    yield ch.text.encode("utf-8"), "text/plain;charset=utf-8", m, False
 
         return gen()
 

@@ -90,17 +90,24 @@ def main():
     jpeg = encode_jpeg(synth_image(np.random.default_rng(0), 768, 1024, "photo"))
     prompt = ("Describe the picture " * 8)[:a.prompt_chars]
     meta = {"prompt": prompt, "max_new_tokens": str(a.max_new)}
-    ttft, total, chunks, gaps = [], [], [], []
+    ttft, total, chunks, gaps, lag, egaps = [], [], [], [], [], []
     with grpc.insecure_channel(f"127.0.0.1:{port}") as ch:
         stub = pb.InferenceStub(ch)
         for i in range(a.warmup + a.n):
             t = time.perf_counter()
-            first, n, last = None, 0, None
+            first, n, last, last_te = None, 0, None, None
             for r in stub.Infer(iter([pb.InferRequest(correlation_id=str(i), task="vlm_generate_stream", payload=jpeg,
                                                       payload_mime="image/jpeg", meta=meta)]), timeout=300):
                 if r.HasField("error"):
                     raise RuntimeError(r.error.message)
                 now = time.perf_counter()
+                te = r.meta.get("t_emit")
+                if te is not None and i >= a.warmup:
+                    tw = time.time()
+                    lag.append((tw - float(te)) * 1e3)          # engine emit -> client receive
+                    if last_te is not None:
+                        egaps.append((float(te) - last_te) * 1e3)
+                    last_te = float(te)
                 if first is None:
                     first = now
                 elif i >= a.warmup:
@@ -130,7 +137,9 @@ def main():
                       "request_ms_p50": round(float(np.percentile(total, 50)), 3),
                       "chunks_per_request": float(np.median(chunks)), "n": a.n,
                       "engine_stats": eng_stats,
-                      "inter_chunk_ms_p50": round(float(np.percentile(gaps, 50)), 3) if gaps else None, "load_s": round(load_s, 1),
+                      "inter_chunk_ms_p50": round(float(np.percentile(gaps, 50)), 3) if gaps else None,
+                      "engine_inter_emit_ms_p50": round(float(np.percentile(egaps, 50)), 3) if egaps else None,
+                      "emit_to_client_ms_p50": round(float(np.percentile(lag, 50)), 3) if lag else None, "load_s": round(load_s, 1),
                       "config": {"model": f"{a.preset} (synthetic pack, random-init weights)", "device": a.device,
                                  "decoder": "fp8" if a.fp8 else "bf16", "image": f"1024x768 JPEG {len(jpeg) // 1024} KiB",
                                  "prompt_chars": a.prompt_chars, "max_new_tokens": a.max_new,
