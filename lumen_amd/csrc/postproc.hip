@@ -283,28 +283,40 @@ __global__ void ctc_argmax_kernel(const float* __restrict__ probs, int rows, int
   if (lane == 0) { idx[row] = bi; conf[row] = from_logits ? 1.f / sum : best; }
 }
 
-// collapse: one thread per sequence; out_ids [B, T] (-1 padded), out_len [B], out_conf [B] (mean prob).
-// tlen (optional) = valid time steps per sequence (width-bucketed batches).
-__global__ void ctc_collapse_kernel(const int* __restrict__ idx, const float* __restrict__ conf, int B, int T,
-                                    int blank, const int* __restrict__ tlen, int* __restrict__ out_ids,
-                                    int* __restrict__ out_len, float* __restrict__ out_conf) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+// collapse: one wave per sequence (4 per workgroup); out_ids [B, T] (-1 padded), out_len [B],
+// out_conf [B] (mean prob).  tlen (optional) = valid time steps per sequence (width-bucketed
+// batches).  64 time steps per pass: keep = not blank and not the previous step's class, the kept
+// steps' output slots from a ballot prefix count.  (The former thread-per-sequence loop was a chain
+// of ~T dependent global round trips: ~85 us for 64 crops x 108 steps, more than the classifier.)
+__global__ void __launch_bounds__(256) ctc_collapse_kernel(const int* __restrict__ idx, const float* __restrict__ conf,
+                                                           int B, int T, int blank, const int* __restrict__ tlen,
+                                                           int* __restrict__ out_ids, int* __restrict__ out_len,
+                                                           float* __restrict__ out_conf) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;      // wave-uniform
   const int Tb = tlen ? min(max(tlen[b], 0), T) : T;
-  int n = 0, prev = -1;
+  const int64_t row = (int64_t)b * T;
+  int n = 0, carry = -1;   // carry: the class of the step before this pass
   float s = 0.f;
-  for (int t = 0; t < Tb; ++t) {
-    const int c = idx[b * T + t];
-    if (c != blank && c != prev) {
-      out_ids[b * T + n] = c;
-      s += conf[b * T + t];
-      ++n;
-    }
-    prev = c;
+  for (int t0 = 0; t0 < Tb; t0 += 64) {
+    const int t = t0 + lane;
+    const bool in = t < Tb;
+    const int c = in ? idx[row + t] : blank;
+    int cp = __shfl_up(c, 1, 64);
+    if (lane == 0) cp = carry;
+    const bool keep = in && c != blank && c != cp;
+    const unsigned long long mask = __ballot(keep);
+    if (keep) out_ids[row + n + __popcll(mask & ((1ull << lane) - 1ull))] = c;
+    s += wave_sum(keep ? conf[row + t] : 0.f);
+    n += __popcll(mask);
+    carry = __shfl(c, 63, 64);
   }
-  for (int t = n; t < T; ++t) out_ids[b * T + t] = -1;
-  out_len[b] = n;
-  out_conf[b] = n > 0 ? s / n : 0.f;
+  for (int t = n + lane; t < T; t += 64) out_ids[row + t] = -1;
+  if (lane == 0) {
+    out_len[b] = n;
+    out_conf[b] = n > 0 ? s / n : 0.f;
+  }
 }
 
 // Recogniser classifier fused with the CTC arg-max (O-8): logits = h . W^T + bias are never
@@ -516,7 +528,7 @@ hipError_t cls_argmax(const uint16_t* h, int64_t ldh, const uint16_t* w, const f
 
 hipError_t ctc_collapse(const int* idx, const float* conf, int B, int T, int blank, const int* tlen, int* out_ids,
                         int* out_len, float* out_conf, hipStream_t stream) {
-  hipLaunchKernelGGL(ctc_collapse_kernel, dim3((B + 63) / 64), dim3(64), 0, stream, idx, conf, B, T, blank, tlen,
+  hipLaunchKernelGGL(ctc_collapse_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, idx, conf, B, T, blank, tlen,
                      out_ids, out_len, out_conf);
   return hipGetLastError();
 }
@@ -526,7 +538,7 @@ hipError_t ctc_greedy(const float* probs, int B, int T, int C, int blank, int fr
   const int rows = B * T;
   hipLaunchKernelGGL(ctc_argmax_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, probs, rows, C, from_logits,
                      tmp_idx, tmp_conf);
-  hipLaunchKernelGGL(ctc_collapse_kernel, dim3((B + 63) / 64), dim3(64), 0, stream, tmp_idx, tmp_conf, B, T, blank,
+  hipLaunchKernelGGL(ctc_collapse_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, tmp_idx, tmp_conf, B, T, blank,
                      tlen, out_ids, out_len, out_conf);
   return hipGetLastError();
 }
