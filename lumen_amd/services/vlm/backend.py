@@ -467,7 +467,12 @@ class MI355XVLMBackend:
 
     def detokenize(self, ids: Sequence[int]) -> str:
         tok = self.tokenizer()
-        V = tok.get_vocab_size(with_added_tokens=True)
+        # Tokenizer.get_vocab_size materialises the whole vocabulary: ~12-60 ms for a 128k-token
+        # (Llama-3) vocab, paid on every streamed token before it was cached per tokenizer object
+        cv = self.__dict__.get("_vocab_size")
+        if cv is None or cv[0] is not tok:
+            cv = self._vocab_size = (tok, tok.get_vocab_size(with_added_tokens=True))
+        V = cv[1]
         try:
             return tok.decode([int(i) for i in ids if 0 <= int(i) < V], skip_special_tokens=True)
         except Exception as e:
