@@ -22,7 +22,6 @@
 // written as [b, s, h, d] so the out-projection GEMM consumes it directly.
 #include <cstdlib>
 #include "attention.h"
-#include "tuning.h"
 #include "common.h"
 
 namespace lumen {
@@ -319,7 +318,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
 // SIMD to hide the LDS / MFMA latencies of the query-block walk (ViT S = 257: 17 blocks -> at most
 // 3 per wave instead of 5).
 template <int D, int NW>
-__global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc, int allow_split) {
+__global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc) {
   constexpr int NCH = D / 8;
   constexpr int KS = D / 32;
   constexpr int NB = D / 16;
@@ -484,25 +483,13 @@ __global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc, 
     }
   };
 
-  // Ragged split (non-causal, full-length keys, the last query block the only one left over after
-  // equal shares, <= NW chunks -- ViT S = 257 at NW = 8: 16 blocks + 1 query): every wave takes its equal
-  // share of blocks, then wave w < nkc computes chunk w of the LAST block and the partial softmax
-  // states merge through LDS, instead of one wave running a third whole block while seven idle
-  // (2.2 instead of 3 block-times per workgroup)
-  const bool split_tail = allow_split && !a.causal && kv_len == a.Sk && nq16 > NW && (nq16 - 1) % NW == 0 &&
-                          nkc <= NW;
-  const int nq_main = split_tail ? nq16 - 1 : nq16;
-  const int nc_all = (kv_len + KC - 1) / KC;
-  const bool tail1_all = nc_all > 0 && kv_len - (nc_all - 1) * KC <= 16;
-
-  for (int qbk = wid; qbk < nq_main; qbk += NW) {
+  for (int qbk = wid; qbk < nq16; qbk += NW) {
     const int q0 = qbk * 16;
     const int qi = q0 + col;
     bf16x8_t qf[KS];
 #pragma unroll
     for (int t = 0; t < KS; ++t) qf[t] = qn[t];
-    if (qbk + NW < nq_main) load_q(qbk + NW);
-    else if (split_tail) load_q(nq16 - 1);          // the split tail block's queries, every wave
+    if (qbk + NW < nq16) load_q(qbk + NW);
     f32x4_t o[NB];
 #pragma unroll
     for (int j = 0; j < NB; ++j) o[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
@@ -516,53 +503,6 @@ __global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc, 
     if (tail1) tail_chunk(nfull, qf, o, l4, mrow, qi);
     store_o(o, l4[0], qi);
   }
-  if (!split_tail) return;
-
-  // ---- the split tail block: wave w < nc_all runs chunk w for its 16 queries (one valid at S = 257)
-  const int q0t = (nq16 - 1) * 16, qit = q0t + col;
-  bf16x8_t qft[KS];
-#pragma unroll
-  for (int t = 0; t < KS; ++t) qft[t] = qn[t];
-  f32x4_t ot[NB];
-#pragma unroll
-  for (int j = 0; j < NB; ++j) ot[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  float mt = -INFINITY;
-  f32x4_t lt = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  if (wid < nc_all) {
-    if (wid == nc_all - 1 && tail1_all) tail_chunk(wid, qft, ot, lt, mt, qit);
-    else full_chunk(wid, qft, ot, lt, mt, q0t, qit);
-  }
-  __syncthreads();                                   // every wave is done with the K / V images
-  // partial states into the (now free) K / V region: [wave][m 16 | l 16 | o D x 16] floats
-  float* ps = (float*)smem + wid * (32 + D * 16);
-  if (wid < nc_all) {
-    if (g == 0) {
-      ps[col] = mt;
-      ps[16 + col] = lt[0];
-    }
-#pragma unroll
-    for (int j = 0; j < NB; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ps[32 + (j * 16 + 4 * g + r) * 16 + col] = ot[j][r];
-  }
-  __syncthreads();
-  if (wid != 0) return;
-  float M = -INFINITY;
-  for (int w = 0; w < nc_all; ++w) M = fmaxf(M, ((const float*)smem)[w * (32 + D * 16) + col]);
-  float L = 0.f;
-  f32x4_t om[NB];
-#pragma unroll
-  for (int j = 0; j < NB; ++j) om[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  for (int w = 0; w < nc_all; ++w) {
-    const float* pw = (const float*)smem + w * (32 + D * 16);
-    const float e = pw[col] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(pw[col] - M);
-    L += pw[16 + col] * e;
-#pragma unroll
-    for (int j = 0; j < NB; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) om[j][r] += pw[32 + (j * 16 + 4 * g + r) * 16 + col] * e;
-  }
-  store_o(om, L, qit);
 }
 
 template <int D, int NW>
@@ -573,8 +513,7 @@ static hipError_t launch_res_nw(const AttnArgs& a, int B, int nkc, hipStream_t s
     hipFuncSetAttribute((const void*)attn_res_kernel<D, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((attn_res_kernel<D, NW>), dim3(a.H, B), dim3(64 * NW), lds, stream, a, nkc,
-                     tuning(TUNE_ATTN_SPLIT_TAIL));
+  hipLaunchKernelGGL((attn_res_kernel<D, NW>), dim3(a.H, B), dim3(64 * NW), lds, stream, a, nkc);
   return hipGetLastError();
 }
 

@@ -5,10 +5,11 @@
 
 namespace lumen {
 
+// (r6: the ViT attention split-tail variant lost its A/B -- 6,316 vs 6,339 img/s, 0.301 vs 0.299 ms per
+// b512 layer, profiles/r6_tower_ab_tuning_v1.txt, r6_attn_bench_v1.txt -- and was deleted)
 enum TuningFlag : int {
-  TUNE_ATTN_SPLIT_TAIL = 0,   // attn_res_kernel: split the ragged last query block over the waves (1)
-  TUNE_LN_MULTI_ROW = 1,      // ln_row_stats: 4 rows per wave for large row counts (1)
-  TUNE_COUNT = 2,
+  TUNE_LN_MULTI_ROW = 0,      // ln_row_stats: 4 rows per wave for large row counts (1; +0.3 %, same A/B file)
+  TUNE_COUNT = 1,
 };
 
 int tuning(int flag);

@@ -33,21 +33,6 @@ for (B, S, H, D, causal) in [(512, 257, 16, 64, False), (512, 77, 12, 64, True),
         ms = s.elapsed_time(e) / 10
         r[name + "_ms"] = round(ms, 3)
         r[name + "_tflops"] = round(flops / ms / 1e9, 1)
-    if not causal:      # csrc/tuning.h TUNE_ATTN_SPLIT_TAIL (0): the ragged tail query block split over waves
-        hip = ops.hip_ops()
-        base = hip.set_tuning(0, 0)
-        for val in (0, 1, 0, 1):
-            hip.set_tuning(0, val)
-            for _ in range(3):
-                run_l()
-            s.record()
-            for _ in range(20):
-                run_l()
-            e.record()
-            torch.cuda.synchronize()
-            key = "split_tail_" + ("on" if val else "off") + "_ms"
-            r[key] = min(r.get(key, 1e9), round(s.elapsed_time(e) / 20, 4))
-        hip.set_tuning(0, base)
     ref = F.scaled_dot_product_attention(qt[:2].float(), kt[:2].float(), vt[:2].float(), is_causal=causal).transpose(1, 2)
     run_l()
     r["rel_err"] = float(((out[:2].float() - ref).norm() / ref.norm()).item())

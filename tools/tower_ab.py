@@ -3,7 +3,7 @@
 module flag of lumen_amd.models.clip off and on.
 
     python tools/tower_ab.py --flag _LN_FOLD [--model ViT-L-14] [--batch 512] [--rounds 5] [--steps 10]
-    python tools/tower_ab.py --tuning attn_split_tail     # a kernel-variant switch (csrc/tuning.h) instead
+    python tools/tower_ab.py --tuning ln_multi_row        # a kernel-variant switch (csrc/tuning.h) instead
 """
 import argparse
 import json
@@ -25,13 +25,13 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--tuning", default=None, help="csrc/tuning.h switch: attn_split_tail | ln_multi_row")
+    ap.add_argument("--tuning", default=None, help="csrc/tuning.h switch: ln_multi_row")
     args = ap.parse_args()
     load_hip(required=True)
     dev = torch.device("cuda")
     m = clip_mod.CLIPModel.random(clip_mod.PRESETS[args.model], seed=0, device=dev, with_text=False)
     imgs = torch.randint(0, 256, (args.batch, 256, 256, 3), dtype=torch.uint8, device=dev)
-    tune = {"attn_split_tail": 0, "ln_multi_row": 1}.get(args.tuning) if args.tuning else None
+    tune = {"ln_multi_row": 0}.get(args.tuning) if args.tuning else None
     ops = load_hip(required=True) if tune is not None else None
     if tune is not None:
         from lumen_amd._native import hip_ops
