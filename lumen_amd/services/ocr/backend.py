@@ -315,12 +315,29 @@ class MI355XOcrBackend:
         return self.detect_finish(self.detect_submit(images, params))
 
     @torch.no_grad()
-    def detect_submit(self, images: Sequence[np.ndarray], params: Sequence[OcrParams], stream=None) -> dict:
+    def decode_device(self, datas: Sequence[bytes]):
+        """A batch of encoded images -> (images, pre): baseline JPEGs entropy-decoded on the host
+        pool and reconstructed on the GPU in one batched launch (utils/jpeg.py), other formats through
+        Pillow, every image in one flat device buffer -- the pixels never come back to the host.
+        ``images[k]`` is a shape-only :class:`~lumen_amd.utils.jpeg.DeviceImage` (or the
+        InvalidInputError of an undecodable payload); ``pre`` feeds :meth:`detect_submit`, whose
+        upload the recogniser's crop warps then read as well."""
+        from ...utils.jpeg import DeviceImage, decode_batch_to_device
+
+        with stage("decode"):
+            flat, offs, shapes, errors = decode_batch_to_device(list(datas), self.device)
+        images = [InvalidInputError(f"Failed to decode image bytes: {errors[k]}") if k in errors
+                  else DeviceImage(*shapes[k]) for k in range(len(datas))]
+        return images, (flat, [int(o) for o in offs])
+
+    def detect_submit(self, images: Sequence[np.ndarray], params: Sequence[OcrParams], stream=None,
+                      pre=None) -> dict:
         """The device half of :meth:`detect`, queued without waiting: one pinned upload of the batch,
         the resize / normalise and the detector forward per shape group, on ``stream`` (default: the
         current one).  :meth:`detect_finish` runs the DB post-processing.  Submitting batch i + 1 on its
         own stream while batch i is post-processed and recognised overlaps the detector with the host
-        geometry and the recogniser (tools/face_ocr_bench.py --what ocr)."""
+        geometry and the recogniser (tools/face_ocr_bench.py --what ocr).  ``pre``: the (flat device
+        buffer, offsets) of :meth:`decode_device` (queued on the same stream) instead of an upload."""
         dc = self.det_config
         limit = int(dc["limit_side_len"])
         shapes = [det_resize_shape(im.shape[0], im.shape[1], limit) for im in images]
@@ -335,12 +352,15 @@ class MI355XOcrBackend:
             if cuda:
                 # one pinned H2D for the whole batch; every shape group's resize and the
                 # recogniser's crop warps (recognize) read the images from this upload
-                if getattr(self, "_uploader", None) is None:
-                    from ...utils.image import PinnedUploader
+                if pre is not None:
+                    src, offs = pre
+                else:
+                    if getattr(self, "_uploader", None) is None:
+                        from ...utils.image import PinnedUploader
 
-                    self._uploader = PinnedUploader(self.device)
-                with stage("upload"):
-                    src, offs = self._uploader.upload(images)
+                        self._uploader = PinnedUploader(self.device)
+                    with stage("upload"):
+                        src, offs = self._uploader.upload(images)
                 # (strong refs to the images: recognize matches them by identity)
                 h["upload"] = (list(images), src, [int(o) for o in offs])
                 self._last_upload = h["upload"]
@@ -350,7 +370,8 @@ class MI355XOcrBackend:
                     hh, ww = images[i].shape[:2]
                     geoms.append(ops.ImageGeom.resize(hh, ww, int(offs[i]) if src is not None else off, rh, rw))
                     off += images[i].size
-                    tens.append(torch.from_numpy(np.ascontiguousarray(images[i])))
+                    tens.append(torch.empty(images[i].shape, dtype=torch.uint8, device="meta") if pre is not None
+                                else torch.from_numpy(np.ascontiguousarray(images[i])))
                 with stage("det_preprocess"):
                     x = ops.image_prep(tens, (rh, rw), mean=dc["mean"], std=dc["std"], scale=float(dc["scale"]),
                                        filter="cv2_linear", layout="nhwc8", swap_rb=True, geoms=geoms,
@@ -453,12 +474,15 @@ class MI355XOcrBackend:
         return res
 
     # ------------------------------------------------------------------ end to end
-    def _predict_batch(self, items):
+    def _predict_batch(self, items, pre=None):
+        """(image, OcrParams) items -> per image list of OcrResult; ``pre``: the images' device buffer
+        from :meth:`decode_device` (the images are then its shape-only stand-ins)."""
         imgs = [it[0] for it in items]
         params = [it[1] for it in items]
-        boxes = self.detect(imgs, params)
+        h = self.detect_submit(imgs, params, pre=pre)
+        boxes = self.detect_finish(h)
         crops = [(i, b) for i, bs in enumerate(boxes) for b in bs]
-        texts = self.recognize(imgs, crops)
+        texts = self.recognize(imgs, crops, upload=h["upload"])
         outs: list = [[] for _ in items]
         for (i, b), (text, score) in zip(crops, texts):
             if score >= params[i].rec_thresh:
@@ -539,6 +563,19 @@ def dp_worker(device: str, resources: GenericResources, max_batch: int = 16):
         if kind != "ocr":
             raise ValueError(f"unknown OCR task kind {kind!r}")
         out: list = [None] * len(items)
+        if b.device.type == "cuda" and items and all(not isinstance(p, np.ndarray) for p, _ in items):
+            # a merged batch of encoded images: one device JPEG decode (host entropy decode + one GPU
+            # reconstruction), the detector and the crop warps read the pixels where they landed
+            imgs, (flat, offs) = b.decode_device([bytes(p) for p, _ in items])
+            ok = [k for k, im in enumerate(imgs) if not isinstance(im, Exception)]
+            for k, im in enumerate(imgs):
+                if isinstance(im, Exception):
+                    out[k] = im
+            if ok:
+                res = b._predict_batch([(imgs[k], items[k][1]) for k in ok], pre=(flat, [offs[k] for k in ok]))
+                for k, r in zip(ok, res):
+                    out[k] = r
+            return out
         ok = []
         for k, (payload, _) in enumerate(items):
             if isinstance(payload, np.ndarray):

@@ -100,3 +100,30 @@ def test_ocr_service_gpu_vs_cpu(tmp_path):
     finally:
         for s in svcs.values():
             s.close()
+
+
+def test_ocr_engine_device_jpeg_matches_host_decode(tmp_path):
+    """The OCR engine's merged batch of encoded images takes the device JPEG path (host entropy
+    decode + one GPU reconstruction; detector and crop warps read the device buffer): same boxes and
+    texts as the host-decoded arrays; an undecodable payload fails alone."""
+    from lumen_amd.services.ocr.backend import InvalidInputError, OcrParams, dp_worker
+    from lumen_amd.utils.image import decode_rgb, encode_jpeg
+
+    write_ocr_model(tmp_path / "models" / "ppocr-tiny", "ppocr-tiny")
+    svc = GeneralOcrService.from_config(config_from_dict(_cfg(tmp_path, "cuda")).services["ocr"], tmp_path)
+    try:
+        svc.manager.initialize()
+        fn = dp_worker("cuda", svc.manager.resources)
+        rng = np.random.default_rng(5)
+        jpegs = [encode_jpeg(rng.integers(0, 255, (90 + 8 * k, 200 - 6 * k, 3), dtype=np.uint8)) for k in range(3)]
+        p = OcrParams(det_thresh=0.0, box_thresh=0.0, rec_thresh=0.0)
+        dev = fn("ocr", [(j, p) for j in jpegs] + [(b"not an image", p)])
+        host = fn("ocr", [(decode_rgb(j), p) for j in jpegs])
+        assert isinstance(dev[3], InvalidInputError)
+        for d, h in zip(dev[:3], host):
+            assert len(d) == len(h) >= 1
+            for a, b in zip(d, h):
+                assert np.abs(np.array(a.box) - np.array(b.box)).max() <= 2
+                assert a.text == b.text
+    finally:
+        svc.close()
