@@ -242,14 +242,25 @@ __global__ void __launch_bounds__(1024) db_flatten_bbox_kernel(int* __restrict__
   __shared__ int sL;
   const int64_t base = (int64_t)blockIdx.x * blockDim.x;
   const int64_t i = min(base + threadIdx.x, total - 1);   // whole waves stay active
+  // no unions run any more and db_root_compress pointed every tile root at its final root: a
+  // read-only find (<= 2 hops) and a plain store of the root -- the compressing find's atomicMin
+  // plus the flatten atomic were two global atomics per blob pixel (~320 us per 16-map batch)
   const int l0 = db_ld(lab, (int)i);
-  const int l = l0 >= 0 ? db_find(lab, (int)i) : -1;
+  int l = l0;
+  if (l0 >= 0) {
+    int p = db_ld(lab, l);
+    while (p != l) {
+      l = p;
+      p = db_ld(lab, l);
+    }
+  }
   if (threadIdx.x == 0) {
     sb[0] = W; sb[1] = -1; sb[2] = H; sb[3] = -1;
     sL = l;                                               // the workgroup's first pixel's component
   }
   __syncthreads();
-  if (base + threadIdx.x < total && l0 >= 0 && l != l0) atomicMin(lab + i, l);
+  if (base + threadIdx.x < total && l0 >= 0 && l != l0)
+    __hip_atomic_store(lab + i, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int L = sL;
   const int p = (int)(i % ((int64_t)H * W)), x = p % W, y = p / W;
   const bool act = l >= 0 && db_is_boundary(lab, i, x, y, H, W);
@@ -293,36 +304,42 @@ constexpr int DB_HASH = 4096;   // > W / 2 + 1 distinct labels per row for W <= 
 
 __global__ void __launch_bounds__(256) db_row_extremes_kernel(const int* __restrict__ lab, const int* __restrict__ bb,
                                                               int H, int W, int min_size, int* __restrict__ out,
-                                                              int* __restrict__ count, int cap) {
+                                                              int* __restrict__ count, int cap, int hs) {
   __shared__ int key[DB_HASH], mn[DB_HASH], mx[DB_HASH];
   const int64_t row = blockIdx.x;                  // map * H + y
   const int y = (int)(row % H);
   const int* lr = lab + row * W;
-  for (int i = threadIdx.x; i < DB_HASH; i += blockDim.x) {
+  const int lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < hs; i += blockDim.x) {
     key[i] = -1;
     mn[i] = INT32_MAX;
     mx[i] = -1;
   }
   __syncthreads();
-  for (int x = threadIdx.x; x < W; x += blockDim.x) {
-    const int l = lr[x];
-    if (l < 0) continue;
+  // a wave covers 64 consecutive pixels: only the head (min x) and tail (max x) of each run of one
+  // label touch the hash -- a blob row's wave does 2 inserts instead of 64 same-address atomics x 3
+  for (int x0 = 0; x0 < W; x0 += blockDim.x) {
+    const int x = x0 + threadIdx.x;
+    const int l = x < W ? lr[x] : -1;
+    const int lp = __shfl_up(l, 1, 64), ln = __shfl_down(l, 1, 64);
+    const bool head = l >= 0 && (lane == 0 || lp != l);
+    const bool tail = l >= 0 && (lane == 63 || ln != l);
+    if (!head && !tail) continue;
     const int* b = bb + 4 * (int64_t)l;
     if (!((b[1] - b[0]) >= min_size || (b[3] - b[2]) >= min_size)) continue;
-    uint32_t h = ((uint32_t)l * 2654435761u) & (DB_HASH - 1);
-    for (int probe = 0; probe < DB_HASH; ++probe) {
+    uint32_t h = ((uint32_t)l * 2654435761u) & (uint32_t)(hs - 1);
+    for (int probe = 0; probe < hs; ++probe) {
       const int old = atomicCAS(&key[h], -1, l);
       if (old == -1 || old == l) {
-        atomicMin(&mn[h], x);
-        atomicMax(&mx[h], x);
+        if (head) atomicMin(&mn[h], x);
+        if (tail) atomicMax(&mx[h], x);
         break;
       }
-      h = (h + 1) & (DB_HASH - 1);
+      h = (h + 1) & (uint32_t)(hs - 1);
     }
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  for (int s0 = 0; s0 < DB_HASH; s0 += blockDim.x) {   // every lane of the block runs every round
+  for (int s0 = 0; s0 < hs; s0 += blockDim.x) {   // every lane of the block runs every round
     const int slot = s0 + threadIdx.x;
     const int l = key[slot];
     const int a = mn[slot], z = mx[slot];
@@ -515,8 +532,10 @@ hipError_t db_components(const void* prob, int is_bf16, const float* thresh, int
                      total);
   (void)blocks;
   if (W > 2 * DB_HASH - 4) return hipErrorInvalidValue;
+  int hs = 256;                 // hash slots: a power of two >= W + 2 (> 2x the W / 2 + 1 labels a row can hold)
+  while (hs < W + 2 && hs < DB_HASH) hs <<= 1;
   hipLaunchKernelGGL(db_row_extremes_kernel, dim3(n * H), dim3(256), 0, stream, lab, bb, H, W, min_size, out, count,
-                     cap);
+                     cap, hs);
   return hipGetLastError();
 }
 

@@ -208,6 +208,40 @@ int lumen_db_boxes(const float* prob, int H, int W, float thresh, float box_thre
 }
 
 // ---- split form for the GPU labelling path (csrc/db_post.hip) ----------------------------
+// pts: int32 [K, 3] rows (root, x, y) as the GPU appended them (atomic order) -> sorted by root in
+// place, stable (LSD radix sort, 11-bit digits, passes for the largest root only): replaces a
+// device radix sort + gather + copy (torch.sort) between the labelling kernels and the D2H.
+void lumen_sort_points_by_root(int* pts, int K) {
+  if (K < 2) return;
+  int maxk = 0;
+  for (int i = 0; i < K; ++i) maxk = std::max(maxk, pts[3 * i]);
+  // (key, row) pairs sorted on 12-bit digits (2 passes for the < 2^24 pixel indices of a 16-map
+  // batch), then one gather of the 12-byte rows
+  std::vector<uint64_t> a((size_t)K), b((size_t)K);
+  for (int i = 0; i < K; ++i) a[i] = ((uint64_t)(uint32_t)pts[3 * i] << 32) | (uint32_t)i;
+  std::vector<int> cnt(4096);
+  for (int shift = 0; shift == 0 || (maxk >> shift) > 0; shift += 12) {
+    std::fill(cnt.begin(), cnt.end(), 0);
+    for (int i = 0; i < K; ++i) ++cnt[(a[i] >> (32 + shift)) & 4095];
+    int run = 0;
+    for (int d = 0; d < 4096; ++d) {
+      const int c = cnt[d];
+      cnt[d] = run;
+      run += c;
+    }
+    for (int i = 0; i < K; ++i) b[cnt[(a[i] >> (32 + shift)) & 4095]++] = a[i];
+    a.swap(b);
+  }
+  std::vector<int> rows((size_t)3 * K);
+  for (int i = 0; i < K; ++i) {
+    const uint32_t r = (uint32_t)(a[i] & 0xffffffffu);
+    rows[3 * i] = pts[3 * r];
+    rows[3 * i + 1] = pts[3 * r + 1];
+    rows[3 * i + 2] = pts[3 * r + 2];
+  }
+  std::memcpy(pts, rows.data(), sizeof(int) * 3 * (size_t)K);
+}
+
 // pts: int32 [K, 3] boundary pixels (component root, x, y) grouped by root in ascending
 // root order (== the raster order of the components' first pixels, as above).  For the
 // first max_candidates components: hull -> min-area rect; rects below min_size dropped.

@@ -420,10 +420,9 @@ def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw
     if on_gpu_done is not None:                      # the device-heavy part is done: e.g. queue the next batch
         on_gpu_done()
     with stage("db_points"):
-        dp = pts[:K]
-        if K > 1:                                    # group by component on the device (radix sort)
-            dp = dp.index_select(0, torch.sort(dp[:, 0], stable=True).indices)
-        P = dp.cpu().numpy()
+        P = np.ascontiguousarray(pts[:K].cpu().numpy())
+        if K > 1:                                    # group by component: host radix sort (csrc/host/geometry.cpp)
+            lib.lumen_sort_points_by_root(P.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), ctypes.c_int(K))
     HW = rh * rw
     ip = ctypes.POINTER(ctypes.c_int)
     fp = ctypes.POINTER(ctypes.c_float)
