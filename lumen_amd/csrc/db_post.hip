@@ -265,11 +265,21 @@ __global__ void __launch_bounds__(1024) db_flatten_bbox_kernel(int* __restrict__
   const int p = (int)(i % ((int64_t)H * W)), x = p % W, y = p / W;
   const bool act = l >= 0 && db_is_boundary(lab, i, x, y, H, W);
   const bool dom = act && l == L;
-  if (dom) {
-    atomicMin(sb, x); atomicMax(sb + 1, x);
-    atomicMin(sb + 2, y); atomicMax(sb + 3, y);
+  // the dominant component's boundary lanes reduce in the wave first: one lane issues the 4 LDS
+  // atomics instead of every boundary lane hitting the same 4 addresses
+  int rx0 = dom ? x : INT32_MAX, rx1 = dom ? x : -1, ry0 = dom ? y : INT32_MAX, ry1 = dom ? y : -1;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    rx0 = min(rx0, __shfl_xor(rx0, o, 64));
+    rx1 = max(rx1, __shfl_xor(rx1, o, 64));
+    ry0 = min(ry0, __shfl_xor(ry0, o, 64));
+    ry1 = max(ry1, __shfl_xor(ry1, o, 64));
   }
   const int lane = threadIdx.x & 63;
+  if (lane == 0 && rx1 >= 0) {
+    atomicMin(sb, rx0); atomicMax(sb + 1, rx1);
+    atomicMin(sb + 2, ry0); atomicMax(sb + 3, ry1);
+  }
   const bool oth = act && !dom;
   const int lp = __shfl_up(l, 1, 64), ap = __shfl_up((int)oth, 1, 64), yp = __shfl_up(y, 1, 64);
   const int ln = __shfl_down(l, 1, 64), an = __shfl_down((int)oth, 1, 64), yn = __shfl_down(y, 1, 64);
