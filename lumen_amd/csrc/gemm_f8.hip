@@ -116,7 +116,6 @@ gemm_f8_kernel(const uint8_t* __restrict__ A, int64_t lda, const float* __restri
     A += blockIdx.y * ep.split_koff * ES;
     W += blockIdx.y * ep.split_koff * ES;
     C = (float*)C + blockIdx.y * ep.split_cstride;
-    if constexpr (BS) mx.a_bs += blockIdx.y * (ep.split_koff >> 7) * mx.ld_bs;   // the slice's scale planes
   }
   const int nk = K * ES / 128;
   const int frow = lane & 15, g = lane >> 4;
@@ -802,34 +801,9 @@ hipError_t gemm_f8(const uint8_t* A, int64_t lda, const float* sa, const uint8_t
   return launch_variant<true>(multi_wave ? 1 : 2, A, lda, sa, W, ldw, sw, C, ldc, M, N, K, ep, S, stream);
 }
 
-// split-K of an MX GEMM with a plain output (the W8A8 vision tower's out-projection / fc2: bf16 +
-// bias + residual): the slab GEMM applies the block scales of its K slice, splitk_reduce16 the
-// real epilogue.  hipErrorNotReady without a workspace (first call inside a graph capture).
-template <int NS, int WN>
-static hipError_t launch_mx_split(const uint8_t* A, int64_t lda, const uint8_t* W, int64_t ldw, const float* sw,
-                                  void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, int S,
-                                  hipStream_t stream, const MxArgs& mx) {
-  float* slabs = split_workspace((size_t)S * M * N * sizeof(float), stream);
-  if (slabs == nullptr) return hipErrorNotReady;
-  GemmEpi e{};
-  e.alpha = 1.f;
-  e.out_f32 = 1;
-  e.split_koff = (int64_t)(K / S);
-  e.split_cstride = (int64_t)M * N;
-  hipError_t err = launch_f8<NS, WN, true, 128, true>(A, lda, nullptr, W, ldw, sw, slabs, N, M, N, K / S, e, stream, S,
-                                                     mx);
-  if (err != hipSuccess) return err;
-  const int64_t work = (int64_t)M * (N / 16);
-  hipLaunchKernelGGL(splitk_reduce16_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, stream, slabs, S, M,
-                     N, C, ldc, ep);
-  return hipGetLastError();
-}
-
-// W8A8 with MX-scaled activations (ops.linear_mx: the W8A8 vision tower, the fused prefill chain).
-// Codes as launch_variant; SwiGLU with an MX output needs 64-column wave tiles (codes 1, 4, 10), a
-// sums-of-squares output 128-column tiles.  Plain outputs (bf16 + bias / residual, no MX output,
-// no sums of squares, no folded norm) of single-round grids split K like gemm_f8 (f8_pick_splits);
-// variant + 100 * S forces S splits (benchmarks).
+// W8A8 with MX-scaled activations (ops.linear_mx, the fused prefill chain of LLM._layers_mx).
+// No split-K (its slab reduce has no MX epilogue).  Codes as launch_variant; SwiGLU with an MX
+// output needs 64-column wave tiles (codes 1, 4, 10), a sums-of-squares output 128-column tiles.
 hipError_t gemm_mx(const uint8_t* A, int64_t lda, const uint8_t* a_bs, int64_t ld_bs, const uint8_t* W, int64_t ldw,
                    const float* sw, void* C, int64_t ldc, int M, int N, int K, const GemmEpi& ep, MxArgs mx,
                    hipStream_t stream, int variant) {
@@ -842,19 +816,6 @@ hipError_t gemm_mx(const uint8_t* A, int64_t lda, const uint8_t* a_bs, int64_t l
   mx.ld_bs = ld_bs;
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
   const bool multi_wave = tiles > f8_num_cus();
-  const bool plain = !ep.glu && !ep.norm && !ep.ssq_out && !ep.row_aff && !ep.col_aff && !mx.q8 && !mx.skip_c &&
-                     !mx.ssq_out && !mx.ssq_in && N % 16 == 0;
-  int S = variant >= 100 ? variant / 100 : (plain && variant == 0 ? f8_pick_splits(tiles, K / 128, ep) : 1);
-  variant %= 100;
-  if (S > 1 && plain) {
-    while (S > 1 && ((K / 128) % S != 0 || (K / 128) / S < 2)) --S;
-    if (S > 1) {
-      hipError_t e = hipErrorNotReady;
-      if (variant == 4) e = launch_mx_split<4, 2>(A, lda, W, ldw, sw, C, ldc, M, N, K, ep, S, stream, mx);
-      else e = launch_mx_split<3, 4>(A, lda, W, ldw, sw, C, ldc, M, N, K, ep, S, stream, mx);
-      if (e != hipErrorNotReady) return e;
-    }
-  }
   int v = variant > 0 ? variant : (multi_wave ? 1 : 2);
   if (ep.glu && mx.q8 && !(v == 1 || v == 4 || v == 10)) v = multi_wave ? 1 : 4;
   hipError_t e = hipErrorNotReady;
