@@ -141,7 +141,6 @@ class AmdRuntimeSettings(BaseModel):
     max_batch: int = 256
     max_wait_ms: float = 2.0
     kv_blocks: int = 0
-    kv_block_size: int = 16
     synthetic: bool = False
 
     @staticmethod
@@ -155,6 +154,5 @@ class AmdRuntimeSettings(BaseModel):
             max_batch=_i("LUMEN_MAX_BATCH", 256),
             max_wait_ms=float(os.environ.get("LUMEN_MAX_WAIT_MS", 2.0)),
             kv_blocks=_i("LUMEN_KV_BLOCKS", 0),
-            kv_block_size=_i("LUMEN_KV_BLOCK_SIZE", 16),
             synthetic=os.environ.get("LUMEN_SYNTHETIC", "0") == "1",
         )
