@@ -8,6 +8,7 @@ serves the DB-net contour geometry and the 5-point similarity transform on both 
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Sequence
 
 import numpy as np
@@ -429,9 +430,7 @@ def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw
     per_img = []
     all_q, all_r, all_i = [], [], []
     starts = np.searchsorted(P[:, 0], np.arange(n + 1) * HW) if K else np.zeros(n + 1, np.int64)
-    t_cand = stage("db_cand")
-    t_cand.__enter__()
-    for j in range(n):
+    def cand(j):
         seg = np.ascontiguousarray(P[starts[j]:starts[j + 1]])
         mx = max_candidates
         q = np.zeros((mx, 8), np.float32)
@@ -440,11 +439,15 @@ def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw
         m = lib.lumen_db_candidates(seg.ctypes.data_as(ip), ctypes.c_int(len(seg)), ctypes.c_int(max_candidates),
                                     ctypes.c_int(min_size), q.ctypes.data_as(fp), r.ctypes.data_as(fp),
                                     roots.ctypes.data_as(ip), ctypes.c_int(mx)) if len(seg) else 0
-        all_q.append(q[:m])
-        all_r.append(r[:m])
+        return q[:m], r[:m], m
+
+    with stage("db_cand"):   # per-image hulls / min-area rects: the C++ calls release the GIL
+        res = list(_host_pool().map(cand, range(n))) if n > 1 else [cand(0)]
+    for j, (q, r, m) in enumerate(res):
+        all_q.append(q)
+        all_r.append(r)
         all_i.append(np.full(m, j, np.int32))
         per_img.append(m)
-    t_cand.__exit__(None, None, None)
     Q = np.concatenate(all_q) if all_q else np.zeros((0, 8), np.float32)
     scores = np.zeros((len(Q),), np.float32)
     if len(Q):
@@ -453,22 +456,37 @@ def db_boxes_gpu(prob: torch.Tensor, params: Sequence, hw: Sequence, rh: int, rw
             hip_ops().db_quad_score(prob, h2d(Q, dev), h2d(np.concatenate(all_i), dev),
                                     sc)
             scores = sc[:len(Q)].cpu().numpy()
-    out, o = [], 0
-    for j in range(n):
+    offs = np.concatenate([[0], np.cumsum(per_img)]).astype(np.int64)
+
+    def fin(j):
         m = per_img[j]
         h, w = hw[j]
         boxes = np.zeros((max_boxes, 8), np.float32)
         bs = np.zeros((max_boxes,), np.float32)
         R = np.ascontiguousarray(all_r[j])
-        S = np.ascontiguousarray(scores[o:o + m])
+        S = np.ascontiguousarray(scores[offs[j]:offs[j] + m])
         k = lib.lumen_db_finalize(R.ctypes.data_as(fp), S.ctypes.data_as(fp), ctypes.c_int(m),
                                   ctypes.c_float(params[j].box_thresh), ctypes.c_float(params[j].unclip_ratio),
                                   ctypes.c_int(min_size), ctypes.c_float(w / rw), ctypes.c_float(h / rh),
                                   ctypes.c_int(w), ctypes.c_int(h), boxes.ctypes.data_as(fp), bs.ctypes.data_as(fp),
                                   ctypes.c_int(max_boxes)) if m else 0
-        out.append((boxes[:k].reshape(k, 4, 2).astype(np.int32), bs[:k]))
-        o += m
-    return out
+        return boxes[:k].reshape(k, 4, 2).astype(np.int32), bs[:k]
+
+    return list(_host_pool().map(fin, range(n))) if n > 1 else [fin(0)]
+
+
+_HOST_POOL = None
+
+
+def _host_pool():
+    """Threads for the per-image DB host geometry (hull, min-area rect, unclip: C++ calls that
+    release the GIL).  Its own pool: a caller may itself be running on the image decode pool."""
+    global _HOST_POOL
+    if _HOST_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+
+        _HOST_POOL = ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4), thread_name_prefix="lumen-db")
+    return _HOST_POOL
 
 
 # --------------------------------------------------------------------------- DB post-processing (host C++)
