@@ -223,7 +223,7 @@ def serve_frontends(config_path: str, port: int, frontends: int, mode: str = "hu
     # next merged batch (LUMEN_ENGINE_THREADS); a popped batch lingers LUMEN_ENGINE_LINGER_US for more
     # front-end batches -- with 3 loops and 1.5 ms the engine ran 320 batches/s of 6.5 images, every
     # loop busy on per-batch overhead (profiles/r4_serve_fe_v1.txt)
-    engines = EngineSet(specs, devs, threads_per_service=int(os.environ.get("LUMEN_ENGINE_THREADS", "2")),
+    engines = EngineSet(specs, devs, threads_per_service=int(os.environ.get("LUMEN_ENGINE_THREADS", "3")),
                         linger_us=int(os.environ.get("LUMEN_ENGINE_LINGER_US", "5000")))
     ctx = mp.get_context("spawn")
     stop = ctx.Event()
