@@ -28,6 +28,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <array>
 #include <thread>
 #include <vector>
 
@@ -683,24 +684,54 @@ int lumen_jpeg_decode_coefs(const uint8_t* data, uint64_t len, int nthreads, int
     phase = phase + 1 == L.bpm ? 0 : phase + 1;
     ++st[2];
   }
-  // placement (parallel), then the DC integration in decode order (sequential, cheap)
+  // placement with chunk-local DC integration (parallel), the chunks' DC offsets (sequential, one
+  // add per chunk and component), then the offsets applied (parallel).  The former sequential DC
+  // pass over every block ran cache-cold after a parallel placement: ~180 of ~520 us on the GPU
+  // box at 8 threads (profiles/r6_jpeg_host_phases_v1.txt).
   std::vector<int64_t> base(nch + 1, 0);
   for (int i = 0; i < nch; ++i) base[i + 1] = base[i] + ch[i].count;
   const int64_t tail0 = base[nch];
+  std::vector<std::array<int, 4>> dsum(nch + 1, std::array<int, 4>{0, 0, 0, 0});
   auto place = [&](int i) {
     const Chunk& C = ch[i];
     int64_t b = base[i];
+    int acc[4] = {0, 0, 0, 0};
+    auto put = [&](const int16_t* src) {
+      const int c = L.pcomp[b % L.bpm];
+      int16_t* out = block_ptr(J, L, coefs, b);
+      memcpy(out, src, 128);
+      acc[c] += out[0];
+      out[0] = (int16_t)acc[c];
+      ++b;
+    };
     const int npre = (int)(C.pre.size() / 64);
-    for (int k = 0; k < npre; ++k, ++b) memcpy(block_ptr(J, L, coefs, b), &C.pre[64 * k], 128);
-    for (int k = C.take_from; k < C.take_to; ++k, ++b) memcpy(block_ptr(J, L, coefs, b), &C.blk[64 * (size_t)k], 128);
+    for (int k = 0; k < npre; ++k) put(&C.pre[64 * k]);
+    for (int k = C.take_from; k < C.take_to; ++k) put(&C.blk[64 * (size_t)k]);
+    for (int c = 0; c < 4; ++c) dsum[i][c] = acc[c];
   };
   if (nch > 1) pool(nthreads).parallel_for(nch, place);
   else place(0);
-  for (size_t k = 0; k < tail.size() / 64; ++k) memcpy(block_ptr(J, L, coefs, tail0 + (int64_t)k), &tail[64 * k], 128);
-  int pred[4] = {0, 0, 0, 0};
-  for (int64_t b = 0; b < total; ++b) {
+  // DC offset entering chunk i = the sum of every earlier chunk's DC differences (int wrap-around as
+  // in the sequential form: the final int16 store keeps the low 16 bits either way)
+  std::vector<std::array<int, 4>> off(nch + 1, std::array<int, 4>{0, 0, 0, 0});
+  for (int i = 0; i < nch; ++i)
+    for (int c = 0; c < 4; ++c) off[i + 1][c] = off[i][c] + dsum[i][c];
+  auto shift = [&](int i) {
+    const std::array<int, 4>& o = off[i];
+    if (o[0] == 0 && o[1] == 0 && o[2] == 0 && o[3] == 0) return;
+    for (int64_t b = base[i]; b < base[i + 1]; ++b) {
+      int16_t* out = block_ptr(J, L, coefs, b);
+      out[0] = (int16_t)(out[0] + o[L.pcomp[b % L.bpm]]);
+    }
+  };
+  if (nch > 1) pool(nthreads).parallel_for(nch, shift);
+  int pred[4];
+  for (int c = 0; c < 4; ++c) pred[c] = off[nch][c];
+  for (size_t k = 0; k < tail.size() / 64; ++k) {
+    const int64_t b = tail0 + (int64_t)k;
     const int c = L.pcomp[b % L.bpm];
     int16_t* out = block_ptr(J, L, coefs, b);
+    memcpy(out, &tail[64 * k], 128);
     pred[c] += out[0];
     out[0] = (int16_t)pred[c];
   }
