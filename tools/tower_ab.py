@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--values", default="", help="the two arms of an int flag, e.g. 2,3 (default off / on)")
     ap.add_argument("--tuning", default=None, help="csrc/tuning.h switch: ln_multi_row")
     args = ap.parse_args()
     load_hip(required=True)
@@ -46,6 +47,9 @@ def main():
         def setter(v):
             setattr(clip_mod, args.flag, v)
     arms = {"off": False if isinstance(base, bool) else 0, "on": True if isinstance(base, bool) else 1}
+    if args.values:       # two explicit values of an int flag (e.g. --flag _VIT_MICRO --values 2,3)
+        a, b = (int(v) for v in args.values.split(","))
+        arms = {f"v{a}": a, f"v{b}": b}
     res = {k: [] for k in arms}
     outs = {}
     for r in range(args.rounds + 1):
@@ -61,7 +65,8 @@ def main():
                 res[name].append(args.batch * args.steps / dt)
             outs[name] = e.float().cpu()
     setter(base)
-    cos = float((outs["off"] * outs["on"]).sum(-1).min())
+    o1, o2 = (outs[k] for k in arms)
+    cos = float((o1 * o2).sum(-1).min())
     print(json.dumps({"flag": args.flag, "model": args.model, "batch": args.batch,
                       "images_per_s": {k: [round(x, 1) for x in v] for k, v in res.items()},
                       "median": {k: round(sorted(v)[len(v) // 2], 1) for k, v in res.items()},
