@@ -43,6 +43,7 @@
 #   fe_gpu         engine / front-end topology GPU test (tests/test_frontends_gpu.py)
 #   face_real      face bench on the detector's real output (detect_and_embed_images; SPMD path under torchrun)
 #   shrink         rocpd databases under gpurun_out -> kernel-stats / PMC text, databases > 4 MB removed (64 MiB copy-back cap)
+#   pmc_attn       PMC counters (MFMA-busy, LDS, VALU, clock) of tools/attn_bench.py
 #   pmc_gemm       PMC counters (MFMA, LDS conflicts, busy) of one ViT-L/14 GEMM shape
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -139,6 +140,11 @@ for task in "$@"; do
         SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
         -d gpurun_out/pmc_mfma -o run -- python3 tools/gemm_bench_tiles.py --tiles="${GEMM_TILES:-1839}" --rounds 1 \
         --iters 2 --shapes "${GEMM_SHAPES:-65792x3072x1024,65792x1024x4096}" ;;
+    pmc_attn)   # MFMA-busy / LDS / VALU / clock counters of the attention bench kernels
+      step pmc_attn 120 timeout -s KILL 100 rocprofv3 --kernel-trace \
+        --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU \
+        SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
+        -d gpurun_out/pmc_attn -o run -- python3 tools/attn_bench.py ;;
     serve)
       step serve_clip 300 python -u tools/serve_bench.py --service clip --model CLIP-ViT-L-14 --device cuda --clients 64 \
         --seconds 20
