@@ -21,6 +21,7 @@
 // Q/K/V are read in place from packed projections via strides, and O is
 // written as [b, s, h, d] so the out-projection GEMM consumes it directly.
 #include <cstdlib>
+#include <type_traits>
 #include "attention.h"
 #include "common.h"
 
@@ -61,12 +62,15 @@ __device__ __forceinline__ s16x4v ds_read_tr16(const char* p) {
 // lane's max grew by more than 8 in log2 units (lazy rescale: p <= 256 is exact enough in
 // fp32 accumulators and bf16 P).
 // ----------------------------------------------------------------------------------------------
-template <int NB>
+template <int NB, bool MASK>
 __device__ __forceinline__ void softmax_chunk(f32x4_t (&sc)[4], f32x4_t (&o)[NB], f32x4_t& l4, float& mrow,
                                               const AttnArgs& a, bool need_mask, int k0, int g, int qi,
                                               int kv_len, int causal_off) {
   float mx = -INFINITY;
-  if (need_mask) {
+  // MASK is a template argument: as a runtime flag hipcc if-converted the masked path into every
+  // chunk (~80 extra VALU per 18 MFMAs of the ViT K/V-resident kernel, profiles/r6_attn_pmc_v1.txt)
+  (void)need_mask;
+  if constexpr (MASK) {
 #pragma unroll
     for (int kb16 = 0; kb16 < 4; ++kb16)
 #pragma unroll
@@ -220,7 +224,8 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
     }
     // mask (only on chunks that need it) + online softmax (per lane = per query)
     const bool need_mask = (k0 + KC > kv_len) || (a.causal && k0 + KC - 1 > q0 + causal_off);
-    softmax_chunk<NB>(sc, o, l4, mrow, a, need_mask, k0, g, qi, kv_len, causal_off);
+    if (need_mask) softmax_chunk<NB, true>(sc, o, l4, mrow, a, need_mask, k0, g, qi, kv_len, causal_off);
+    else softmax_chunk<NB, false>(sc, o, l4, mrow, a, need_mask, k0, g, qi, kv_len, causal_off);
 
     // O^T += V^T P^T over two 32-key steps
 #pragma unroll
@@ -373,8 +378,8 @@ __global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc) 
   __syncthreads();
 
   // One 64-key chunk of S^T, online softmax, O^T += V^T P^T for the 16 queries of block q0 (qf).
-  auto full_chunk = [&](int kc, const bf16x8_t (&qf)[KS], f32x4_t (&o)[NB], f32x4_t& l4, float& mrow, int q0,
-                        int qi) __attribute__((always_inline)) {
+  auto full_chunk = [&](auto maskc, int kc, const bf16x8_t (&qf)[KS], f32x4_t (&o)[NB], f32x4_t& l4, float& mrow,
+                        int q0, int qi) __attribute__((always_inline)) {
     const int k0 = kc * KC;
     const char* sK = smem + kc * 2 * IMG;
     const char* sV = sK + IMG;
@@ -389,8 +394,7 @@ __global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc) 
         sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[t], sc[kb16], 0, 0, 0);
       }
     }
-    const bool need_mask = (k0 + KC > kv_len) || (a.causal && k0 + KC - 1 > q0 + causal_off);
-    softmax_chunk<NB>(sc, o, l4, mrow, a, need_mask, k0, g, qi, kv_len, causal_off);
+    softmax_chunk<NB, decltype(maskc)::value>(sc, o, l4, mrow, a, true, k0, g, qi, kv_len, causal_off);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8_t pf;
@@ -499,7 +503,12 @@ __global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc) 
     const int nc = min(nkc, (wave_kend + KC - 1) / KC);
     const bool tail1 = nc > 0 && wave_kend - (nc - 1) * KC <= 16;
     const int nfull = tail1 ? nc - 1 : nc;
-    for (int kc = 0; kc < nfull; ++kc) full_chunk(kc, qf, o, l4, mrow, q0, qi);
+    // chunks needing no mask come first (key-length and causal masks grow with the chunk index):
+    // an unmasked loop, then the masked remainder
+    int nclean = nfull;
+    while (nclean > 0 && ((nclean * KC > kv_len) || (a.causal && nclean * KC - 1 > q0 + causal_off))) --nclean;
+    for (int kc = 0; kc < nclean; ++kc) full_chunk(std::false_type{}, kc, qf, o, l4, mrow, q0, qi);
+    for (int kc = nclean; kc < nfull; ++kc) full_chunk(std::true_type{}, kc, qf, o, l4, mrow, q0, qi);
     if (tail1) tail_chunk(nfull, qf, o, l4, mrow, qi);
     store_o(o, l4[0], qi);
   }

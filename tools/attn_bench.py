@@ -21,16 +21,18 @@ for (B, S, H, D, causal) in [(512, 257, 16, 64, False), (512, 77, 12, 64, True),
     r = {"B": B, "S": S, "H": H, "D": D, "causal": causal}
     flops = 4 * B * H * S * S * D * (0.5 if causal else 1.0)
     for name, fn in (("lumen", run_l), ("sdpa", run_t)):
-        for _ in range(3):
-            fn()
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
         for _ in range(10):
             fn()
-        e.record()
         torch.cuda.synchronize()
-        ms = s.elapsed_time(e) / 10
+        ms = 1e9
+        for _ in range(3):     # best of 3 windows of 30 launches (clock / warm-up noise)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(30):
+                fn()
+            e.record()
+            torch.cuda.synchronize()
+            ms = min(ms, s.elapsed_time(e) / 30)
         r[name + "_ms"] = round(ms, 3)
         r[name + "_tflops"] = round(flops / ms / 1e9, 1)
     ref = F.scaled_dot_product_attention(qt[:2].float(), kt[:2].float(), vt[:2].float(), is_causal=causal).transpose(1, 2)
