@@ -24,6 +24,7 @@
 #include <type_traits>
 #include "attention.h"
 #include "common.h"
+#include "tuning.h"
 
 namespace lumen {
 
@@ -323,7 +324,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
 // SIMD to hide the LDS / MFMA latencies of the query-block walk (ViT S = 257: 17 blocks -> at most
 // 3 per wave instead of 5).
 template <int D, int NW>
-__global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc) {
+__global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc, int clean_split) {
   constexpr int NCH = D / 8;
   constexpr int KS = D / 32;
   constexpr int NB = D / 16;
@@ -505,7 +506,7 @@ __global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc) 
     const int nfull = tail1 ? nc - 1 : nc;
     // chunks needing no mask come first (key-length and causal masks grow with the chunk index):
     // an unmasked loop, then the masked remainder
-    int nclean = nfull;
+    int nclean = clean_split ? nfull : 0;   // (0: every chunk takes the masked form -- the A/B arm)
     while (nclean > 0 && ((nclean * KC > kv_len) || (a.causal && nclean * KC - 1 > q0 + causal_off))) --nclean;
     for (int kc = 0; kc < nclean; ++kc) full_chunk(std::false_type{}, kc, qf, o, l4, mrow, q0, qi);
     for (int kc = nclean; kc < nfull; ++kc) full_chunk(std::true_type{}, kc, qf, o, l4, mrow, q0, qi);
@@ -522,7 +523,8 @@ static hipError_t launch_res_nw(const AttnArgs& a, int B, int nkc, hipStream_t s
     hipFuncSetAttribute((const void*)attn_res_kernel<D, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((attn_res_kernel<D, NW>), dim3(a.H, B), dim3(64 * NW), lds, stream, a, nkc);
+  hipLaunchKernelGGL((attn_res_kernel<D, NW>), dim3(a.H, B), dim3(64 * NW), lds, stream, a, nkc,
+                     tuning(TUNE_ATTN_CLEAN_CHUNKS));
   return hipGetLastError();
 }
 

@@ -86,7 +86,7 @@ uint32_t* splitk_counters(const at::Tensor& like, int64_t tiles) {
     t = at::zeros({std::max<int64_t>(tiles, 16384)}, like.options().dtype(at::kInt));
   return reinterpret_cast<uint32_t*>(t.data_ptr());
 }
-static int g_tuning[TUNE_COUNT] = {1};
+static int g_tuning[TUNE_COUNT] = {1, 1};
 int tuning(int flag) { return flag >= 0 && flag < TUNE_COUNT ? g_tuning[flag] : 0; }
 void set_tuning(int flag, int value) {
   if (flag >= 0 && flag < TUNE_COUNT) g_tuning[flag] = value;

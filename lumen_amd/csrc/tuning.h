@@ -9,7 +9,8 @@ namespace lumen {
 // b512 layer, profiles/r6_tower_ab_tuning_v1.txt, r6_attn_bench_v1.txt -- and was deleted)
 enum TuningFlag : int {
   TUNE_LN_MULTI_ROW = 0,      // ln_row_stats: 4 rows per wave for large row counts (1; +0.3 %, same A/B file)
-  TUNE_COUNT = 1,
+  TUNE_ATTN_CLEAN_CHUNKS = 1, // attn_res_kernel: chunks needing no key mask run the mask-free form (1)
+  TUNE_COUNT = 2,
 };
 
 int tuning(int flag);

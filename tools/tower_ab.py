@@ -26,13 +26,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--values", default="", help="the two arms of an int flag, e.g. 2,3 (default off / on)")
-    ap.add_argument("--tuning", default=None, help="csrc/tuning.h switch: ln_multi_row")
+    ap.add_argument("--tuning", default=None, help="csrc/tuning.h switch: ln_multi_row | attn_clean_chunks")
     args = ap.parse_args()
     load_hip(required=True)
     dev = torch.device("cuda")
     m = clip_mod.CLIPModel.random(clip_mod.PRESETS[args.model], seed=0, device=dev, with_text=False)
     imgs = torch.randint(0, 256, (args.batch, 256, 256, 3), dtype=torch.uint8, device=dev)
-    tune = {"ln_multi_row": 0}.get(args.tuning) if args.tuning else None
+    tune = {"ln_multi_row": 0, "attn_clean_chunks": 1}.get(args.tuning) if args.tuning else None
     ops = load_hip(required=True) if tune is not None else None
     if tune is not None:
         from lumen_amd._native import hip_ops
