@@ -63,15 +63,16 @@ __device__ __forceinline__ s16x4v ds_read_tr16(const char* p) {
 // lane's max grew by more than 8 in log2 units (lazy rescale: p <= 256 is exact enough in
 // fp32 accumulators and bf16 P).
 // ----------------------------------------------------------------------------------------------
-template <int NB, bool MASK>
+template <int NB, int MASK>
 __device__ __forceinline__ void softmax_chunk(f32x4_t (&sc)[4], f32x4_t (&o)[NB], f32x4_t& l4, float& mrow,
                                               const AttnArgs& a, bool need_mask, int k0, int g, int qi,
                                               int kv_len, int causal_off) {
   float mx = -INFINITY;
-  // MASK is a template argument: as a runtime flag hipcc if-converted the masked path into every
-  // chunk (~80 extra VALU per 18 MFMAs of the ViT K/V-resident kernel, profiles/r6_attn_pmc_v1.txt)
-  (void)need_mask;
-  if constexpr (MASK) {
+  // MASK: 0 = no key mask, 1 = masked, 2 = runtime need_mask.  As a runtime flag hipcc if-converts
+  // the masked path into every chunk (~80 extra VALU per 18 MFMAs of the ViT K/V-resident kernel,
+  // profiles/r6_attn_pmc_v1.txt): attn_res_kernel runs its clean chunks with 0; the streaming
+  // attn_fwd_kernel keeps 2 (two inlined copies behind a branch measured worse there: 431 -> 577 VALU)
+  if (MASK == 1 || (MASK == 2 && need_mask)) {
 #pragma unroll
     for (int kb16 = 0; kb16 < 4; ++kb16)
 #pragma unroll
@@ -225,8 +226,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnArgs a) {
     }
     // mask (only on chunks that need it) + online softmax (per lane = per query)
     const bool need_mask = (k0 + KC > kv_len) || (a.causal && k0 + KC - 1 > q0 + causal_off);
-    if (need_mask) softmax_chunk<NB, true>(sc, o, l4, mrow, a, need_mask, k0, g, qi, kv_len, causal_off);
-    else softmax_chunk<NB, false>(sc, o, l4, mrow, a, need_mask, k0, g, qi, kv_len, causal_off);
+    softmax_chunk<NB, 2>(sc, o, l4, mrow, a, need_mask, k0, g, qi, kv_len, causal_off);
 
     // O^T += V^T P^T over two 32-key steps
 #pragma unroll
@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc, 
         sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[t], sc[kb16], 0, 0, 0);
       }
     }
-    softmax_chunk<NB, decltype(maskc)::value>(sc, o, l4, mrow, a, true, k0, g, qi, kv_len, causal_off);
+    softmax_chunk<NB, decltype(maskc)::value ? 1 : 0>(sc, o, l4, mrow, a, true, k0, g, qi, kv_len, causal_off);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8_t pf;
