@@ -48,7 +48,29 @@ __device__ __forceinline__ int v_phys(int row, int chunk) {
   else return chunk ^ (((row >> 2) & 1) << 1);
 }
 
+// max over the 4 lane groups (lane, lane ^ 16, lane ^ 32, lane ^ 48) with the gfx950 row swaps:
+// v_permlane16_swap / v_permlane32_swap stay in the VALU (the __shfl_xor form is two
+// ds_bpermute LDS round trips, each waited with lgkmcnt(0), in every chunk).  The max itself is
+// a bare v_max_f32: the swapped values are finite or -inf scores, so the IEEE-mode
+// canonicalisations hipcc inserts around fmaxf of an opaque value are not needed.
+__device__ __forceinline__ float vmax_raw(float a, float b) {
+  float r;
+  asm("v_max_f32_e32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float group4_max(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = vmax_raw(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return vmax_raw(__uint_as_float(s[0]), __uint_as_float(s[1]));
+}
+
 __device__ __forceinline__ s16x4v ds_read_tr16(const char* p) {
+  typedef __attribute__((address_space(3))) s16x4v* lp;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(p));
+}
+typedef __attribute__((address_space(3))) const char lds_char;
+__device__ __forceinline__ s16x4v ds_read_tr16(const lds_char* p) {
   typedef __attribute__((address_space(3))) s16x4v* lp;
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(p));
 }
@@ -90,9 +112,8 @@ __device__ __forceinline__ void softmax_chunk(f32x4_t (&sc)[4], f32x4_t (&o)[NB]
 #pragma unroll
       for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sc[kb16][r]);
   }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  const float mcand = fmaxf(mrow, mx * a.scale_log2);          // scale > 0 commutes with max
+  mx = group4_max(mx);
+  const float mcand = vmax_raw(mrow, mx * a.scale_log2);       // scale > 0 commutes with max
   if (__any(mcand > mrow + 8.f)) {                              // wave-uniform; first chunk: mrow = -inf
     const float mb = mcand == -INFINITY ? 0.f : mcand;
     const float alpha = __builtin_amdgcn_exp2f(mrow - mb);
@@ -378,20 +399,37 @@ __global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc, 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
+  // Per-lane byte offsets inside one chunk's K / V image (chunk independent: K rows kb16 * 16 + col
+  // and V rows 32 s + 4 g + (col >> 2) (+ 16) differ from the kb16 = s = 0 rows by multiples of 16,
+  // which leave the XOR swizzles unchanged), so every LDS address in the chunk loop is the chunk
+  // base plus one of these plus an immediate.
+  // the dynamic-LDS base as an opaque SGPR: with the symbol itself hipcc keeps one running pointer
+  // per lane offset and re-adds the (zero) symbol to each in every chunk (12 VALU per chunk)
+  int lds0 = (int)(size_t)(const lds_char*)smem;
+  asm volatile("" : "+s"(lds0));
+  int kofs[KS], vofs[NB];
+#pragma unroll
+  for (int t = 0; t < KS; ++t) kofs[t] = col * D * 2 + (k_phys<D>(col, t * 4 + g) << 4);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int r0 = 4 * g + (col >> 2), c0 = j * 16 + 4 * (col & 3);
+    vofs[j] = r0 * D * 2 + (v_phys<D>(r0, c0 >> 3) << 4) + (c0 & 7) * 2;
+  }
   // One 64-key chunk of S^T, online softmax, O^T += V^T P^T for the 16 queries of block q0 (qf).
   auto full_chunk = [&](auto maskc, int kc, const bf16x8_t (&qf)[KS], f32x4_t (&o)[NB], f32x4_t& l4, float& mrow,
                         int q0, int qi) __attribute__((always_inline)) {
     const int k0 = kc * KC;
-    const char* sK = smem + kc * 2 * IMG;
-    const char* sV = sK + IMG;
+    const int cb = lds0 + kc * 2 * IMG;   // wave-uniform chunk base (SGPR) + the hoisted lane offsets
+    const lds_char* sK = (const lds_char*)(size_t)cb;
+    const lds_char* sV = sK + IMG;
     f32x4_t sc[4];
 #pragma unroll
     for (int kb16 = 0; kb16 < 4; ++kb16) {
       sc[kb16] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-      const int kr = kb16 * 16 + col;
 #pragma unroll
       for (int t = 0; t < KS; ++t) {
-        bf16x8_t kf = *(const bf16x8_t*)(sK + kr * D * 2 + (k_phys<D>(kr, t * 4 + g) << 4));
+        // row kb16 * 16 + col: the swizzle term of k_phys repeats every 16 rows
+        bf16x8_t kf = *(const __attribute__((address_space(3))) bf16x8_t*)(sK + kofs[t] + kb16 * 16 * D * 2);
         sc[kb16] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[t], sc[kb16], 0, 0, 0);
       }
     }
@@ -404,15 +442,11 @@ __global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc, 
         pf[r] = (__bf16)sc[2 * s][r];
         pf[4 + r] = (__bf16)sc[2 * s + 1][r];
       }
-      const int q = col >> 2, p = col & 3;
-      const int r0 = s * 32 + 4 * g + q, r1 = r0 + 16;
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        const int c0 = j * 16 + 4 * p;
-        const char* a0 = sV + r0 * D * 2 + (v_phys<D>(r0, c0 >> 3) << 4) + (c0 & 7) * 2;
-        const char* a1 = sV + r1 * D * 2 + (v_phys<D>(r1, c0 >> 3) << 4) + (c0 & 7) * 2;
-        const s16x4v lo = ds_read_tr16(a0);
-        const s16x4v hi = ds_read_tr16(a1);
+        // rows r0 = 32 s + 4 g + (col >> 2) and r0 + 16: the swizzle term of v_phys repeats every 8 rows
+        const s16x4v lo = ds_read_tr16(sV + vofs[j] + s * 32 * D * 2);
+        const s16x4v hi = ds_read_tr16(sV + vofs[j] + (s * 32 + 16) * D * 2);
         s16x8_t vv = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, vv), pf, o[j], 0, 0, 0);
       }
@@ -441,8 +475,7 @@ __global__ void __launch_bounds__(64 * NW) attn_res_kernel(AttnArgs a, int nkc, 
       s0[r] = ok ? s0[r] : -INFINITY;
       mx = fmaxf(mx, s0[r]);
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = group4_max(mx);
     const float mcand = fmaxf(mrow, mx * a.scale_log2);
     if (__any(mcand > mrow + 8.f)) {
       const float mb = mcand == -INFINITY ? 0.f : mcand;
