@@ -276,8 +276,8 @@ class VLM(nn.Module):
                 self._encode_tower(static_in, B)     # warm-up: weight caches, workspaces, autotune
             cur.wait_stream(side)
             g = torch.cuda.CUDAGraph()
-            # thread_local: other threads keep launching meanwhile
-            with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
+            # thread_local: other threads keep launching meanwhile; one capture at a time per process
+            with ops.CAPTURE_LOCK, torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
                 static_out = self._encode_tower(static_in, B)
             return {"g": g, "in": static_in, "out": static_out}
         except Exception as e:  # noqa: BLE001 - an op that cannot be captured: eager launches

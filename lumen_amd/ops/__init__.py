@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import functools
 import math
+import threading
 from typing import Optional, Sequence
 
 import torch
@@ -24,6 +25,12 @@ ACTS = {
     None: 0, "none": 0, "gelu": 1, "quick_gelu": 2, "relu": 3, "silu": 4, "gelu_tanh": 5,
     "hardswish": 6, "sigmoid": 7, "leaky": 8, "hardsigmoid": 9,
 }
+
+
+# Held around every hipGraph capture in the process (models/vlm.py, runtime/engine.py):
+# torch.cuda.graph() enters with a device-wide synchronize + empty_cache, which fails (or
+# invalidates) a capture another thread has in progress, thread_local mode or not.
+CAPTURE_LOCK = threading.RLock()
 
 
 def private_stream(device) -> "torch.cuda.Stream":

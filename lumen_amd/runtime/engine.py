@@ -495,7 +495,8 @@ class DecodeGraphs:
         # already exist (a first request inside the capture would record its zero-fill into every replay)
         # thread_local: a multi-service engine process runs other services' batch loops on other
         # threads meanwhile; the default (global) mode would fail their HIP calls during the capture
-        with torch.cuda.graph(g, pool=self.pool, stream=s, capture_error_mode="thread_local"):
+        # (ops.CAPTURE_LOCK: one capture at a time in the process, see there)
+        with ops.CAPTURE_LOCK, torch.cuda.graph(g, pool=self.pool, stream=s, capture_error_mode="thread_local"):
             out = run()
         pin = lambda t: torch.empty(t.shape, dtype=t.dtype).pin_memory()  # noqa: E731
         ent = {"g": g, "st": st, "dbuf": dbuf, "out": out, "ws": ws, "res": res, "lay": lay, "Bp": Bp, "W": W,

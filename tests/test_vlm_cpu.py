@@ -2,6 +2,7 @@
 Llama, prefill + paged decode, TP=2 over gloo), engine batching invariance, service."""
 import json
 import os
+import socket
 
 import numpy as np
 import pytest
@@ -108,7 +109,9 @@ def _tp_worker(rank, world, port, kind, q):
 def test_tensor_parallel_gloo(kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29611 + (kind == "llama")
+    with socket.socket() as s:                 # a free port: a fixed one collides with earlier runs
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
     procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, kind, q)) for r in range(2)]
     for p in procs:
         p.start()
