@@ -5,6 +5,7 @@ arm "x1" is the production step; interleaved rounds in one process.  The differe
 fusing the statistics into the residual GEMM epilogues could save.
 
     python tools/probes/ln_stats_cost.py [--op ln_row_stats | attention] [--rounds 5] [--steps 10]
+    python tools/probes/ln_stats_cost.py --op linear_lnf --drop-act     # cost of the fc1 activation epilogue
 """
 import argparse
 import json
@@ -24,6 +25,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--op", default="ln_row_stats", help="lumen_amd.ops function to double (ln_row_stats | attention)")
+    ap.add_argument("--drop-act", action="store_true",
+                    help="arm x2 runs the op (linear_lnf) WITHOUT its activation instead: the epilogue's activation cost")
     args = ap.parse_args()
     load_hip(required=True)
     dev = torch.device("cuda")
@@ -33,6 +36,10 @@ def main():
     state = {"n": 1}
 
     def stats(*a, **k):
+        if args.drop_act:
+            if state["n"] == 2:
+                k = dict(k, act=None)
+            return orig(*a, **k)
         for _ in range(state["n"] - 1):
             orig(*a, **k)
         return orig(*a, **k)
@@ -54,7 +61,7 @@ def main():
         setattr(clip_mod.ops, args.op, orig)
     med = {k: sorted(v)[len(v) // 2] for k, v in res.items()}
     ms = {k: 512 / v * 1e3 for k, v in med.items()}
-    print(json.dumps({"op": args.op, "images_per_s": {k: [round(x, 1) for x in v] for k, v in res.items()},
+    print(json.dumps({"op": args.op, "drop_act": args.drop_act, "images_per_s": {k: [round(x, 1) for x in v] for k, v in res.items()},
                       "median": {k: round(v, 1) for k, v in med.items()},
                       "ms_per_step": {k: round(v, 3) for k, v in ms.items()},
                       "extra_pass_cost_ms_per_step": round(ms["x2"] - ms["x1"], 3)}))
