@@ -35,11 +35,15 @@ for (B, S, H, D, causal) in [(512, 257, 16, 64, False), (512, 77, 12, 64, True),
             ms = min(ms, s.elapsed_time(e) / 30)
         r[name + "_ms"] = round(ms, 3)
         r[name + "_tflops"] = round(flops / ms / 1e9, 1)
-    if S in (197, 257, 577) and not causal:   # csrc/tuning.h TUNE_ATTN_CLEAN_CHUNKS (1): mask-free clean chunks
+    # csrc/tuning.h A/B of the K/V-resident kernel: TUNE_ATTN_CLEAN_CHUNKS (1) mask-free clean chunks
+    # (a hashed rotation of the query-block walk, switch 2, lost: profiles/r6_attn_rotate_ab_v1.txt)
+    for flag, name in ((1, "clean_chunks"),):
+        if not (S in (197, 257, 577) and not causal):
+            continue
         hip = ops.hip_ops()
-        base = hip.set_tuning(1, 1)
-        for val in (0, 1, 0, 1):
-            hip.set_tuning(1, val)
+        base = hip.set_tuning(flag, 1)
+        for val in (0, 1, 0, 1, 0, 1):
+            hip.set_tuning(flag, val)
             for _ in range(5):
                 run_l()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -48,9 +52,9 @@ for (B, S, H, D, causal) in [(512, 257, 16, 64, False), (512, 77, 12, 64, True),
                 run_l()
             e.record()
             torch.cuda.synchronize()
-            key = "clean_chunks_" + ("on" if val else "off") + "_ms"
+            key = name + ("_on" if val else "_off") + "_ms"
             r[key] = min(r.get(key, 1e9), round(s.elapsed_time(e) / 30, 4))
-        hip.set_tuning(1, base)
+        hip.set_tuning(flag, base)
     ref = F.scaled_dot_product_attention(qt[:2].float(), kt[:2].float(), vt[:2].float(), is_causal=causal).transpose(1, 2)
     run_l()
     r["rel_err"] = float(((out[:2].float() - ref).norm() / ref.norm()).item())
