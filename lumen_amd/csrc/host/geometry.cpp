@@ -209,18 +209,18 @@ int lumen_db_boxes(const float* prob, int H, int W, float thresh, float box_thre
 
 // ---- split form for the GPU labelling path (csrc/db_post.hip) ----------------------------
 // pts: int32 [K, 3] rows (root, x, y) as the GPU appended them (atomic order) -> sorted by root in
-// place, stable (LSD radix sort, 11-bit digits, passes for the largest root only): replaces a
+// place, stable (LSD radix sort, 12-bit digits, passes for the largest root only): replaces a
 // device radix sort + gather + copy (torch.sort) between the labelling kernels and the D2H.
 void lumen_sort_points_by_root(int* pts, int K) {
   if (K < 2) return;
   int maxk = 0;
   for (int i = 0; i < K; ++i) maxk = std::max(maxk, pts[3 * i]);
   // (key, row) pairs sorted on 12-bit digits (2 passes for the < 2^24 pixel indices of a 16-map
-  // batch), then one gather of the 12-byte rows
+  // batch, 3 at most: shift < 32 also keeps `maxk >> shift` defined), then one gather of the 12-byte rows
   std::vector<uint64_t> a((size_t)K), b((size_t)K);
   for (int i = 0; i < K; ++i) a[i] = ((uint64_t)(uint32_t)pts[3 * i] << 32) | (uint32_t)i;
   std::vector<int> cnt(4096);
-  for (int shift = 0; shift == 0 || (maxk >> shift) > 0; shift += 12) {
+  for (int shift = 0; shift < 32 && (shift == 0 || (maxk >> shift) > 0); shift += 12) {
     std::fill(cnt.begin(), cnt.end(), 0);
     for (int i = 0; i < K; ++i) ++cnt[(a[i] >> (32 + shift)) & 4095];
     int run = 0;

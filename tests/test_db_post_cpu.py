@@ -78,3 +78,18 @@ def test_split_host_path_matches_one_shot(seed):
     assert k == len(ref_b) > 0
     np.testing.assert_array_equal(boxes[:k].reshape(k, 4, 2).astype(np.int32), ref_b)
     np.testing.assert_allclose(bs[:k], ref_s, rtol=1e-5)
+
+
+@pytest.mark.parametrize("K,maxroot", [(1, 5), (2, 1), (1000, 4095), (5000, 4096), (20000, 1 << 23), (3000, (1 << 24) + 7)])
+def test_host_point_sort_is_stable_by_root(K, maxroot):
+    """csrc/host/geometry.cpp lumen_sort_points_by_root (the LSD radix sort that replaced a device
+    torch.sort of the DB points): rows grouped by root in ascending order, atomic append order kept
+    within a root (np.argsort kind="stable" is the reference), every digit-pass count covered."""
+    rng = np.random.default_rng(K)
+    roots = rng.integers(0, maxroot + 1, K).astype(np.int32)
+    roots[rng.integers(0, K)] = maxroot
+    P = np.stack([roots, rng.integers(0, 4096, K), np.arange(K)], 1).astype(np.int32)   # y = append order
+    ref = P[np.argsort(P[:, 0], kind="stable")]
+    got = np.ascontiguousarray(P.copy())
+    load_host().lumen_sort_points_by_root(got.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), ctypes.c_int(K))
+    np.testing.assert_array_equal(got, ref)
