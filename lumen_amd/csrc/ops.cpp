@@ -62,6 +62,7 @@ struct PrepArgs {
   int kpad; int out_bf16;
 };
 hipError_t image_prep(const PrepArgs& a, int B, int max_ch, int max_dw, hipStream_t stream);
+hipError_t image_prep_band(const PrepArgs& a, int B, int rcap, int cwcap, int T, hipStream_t stream);
 hipError_t row_topk(const float* scores, int64_t ld, int B, int N, int k, float scale, float* out_v, int* out_i,
                     float* out_lse, int index_offset, float* ws, hipStream_t stream);
 int topk_chunks(int N);
@@ -790,6 +791,37 @@ void image_prep2(const at::Tensor& src, const at::Tensor& geom, at::Tensor out, 
   LM_CHECK_HIP(lumen::image_prep(a, (int)B, (int)max_ch, (int)max_dw, cur_stream()));
 }
 
+// ViT patch rows, PIL filters: the fused per-band kernel (csrc/image.hip prep_band_kernel); rcap / taps are
+// the host's bounds over the batch (ops.image_prep)
+void image_prep_band(const at::Tensor& src, const at::Tensor& geom, at::Tensor out, int64_t out_h, int64_t out_w,
+                     int64_t filter, bool swap_rb, std::vector<double> mean, std::vector<double> std_, double scale,
+                     double pad, int64_t patch, int64_t kpad, int64_t rcap, int64_t cwcap, int64_t taps) {
+  check_gpu(src, "src");
+  check_gpu(out, "out");
+  TORCH_CHECK(src.scalar_type() == at::kByte, "image_prep_band: uint8 src");
+  TORCH_CHECK(geom.is_cuda() && geom.scalar_type() == at::kLong && geom.dim() == 2 && geom.size(1) == 11 &&
+                  geom.is_contiguous(), "image_prep_band: geom int64 [B, 11] on device");
+  TORCH_CHECK(mean.size() == 3 && std_.size() == 3, "image_prep_band: mean/std");
+  TORCH_CHECK(out.is_contiguous() && out.scalar_type() == at::kBFloat16, "image_prep_band: bf16 contiguous out");
+  TORCH_CHECK(filter == 0 || filter == 1, "image_prep_band: PIL filters only");
+  TORCH_CHECK(patch > 0 && out_h % patch == 0 && out_w % patch == 0 && kpad >= 3 * patch * patch && kpad % 8 == 0,
+              "image_prep_band: patch grid / kpad");
+  const int64_t B = geom.size(0);
+  TORCH_CHECK(out.numel() == B * (out_h / patch) * (out_w / patch) * kpad, "image_prep_band: patch out size");
+  lumen::PrepArgs a{};
+  a.src = src.data_ptr<uint8_t>();
+  a.geom = reinterpret_cast<const lumen::ImgGeomRaw*>(geom.data_ptr<int64_t>());
+  a.out = out.data_ptr();
+  a.out_bf16 = 1;
+  a.OH = (int)out_h; a.OW = (int)out_w;
+  a.filter = (int)filter; a.swap_rb = swap_rb ? 1 : 0;
+  for (int i = 0; i < 3; ++i) { a.mean[i] = (float)mean[i]; a.inv_std[i] = (float)(1.0 / std_[i]); }
+  a.scale = (float)scale; a.pad = (float)pad;
+  a.layout = 2; a.patch = (int)patch; a.kpad = (int)kpad;
+  const at::DeviceGuard guard(src.device());
+  LM_CHECK_HIP(lumen::image_prep_band(a, (int)B, (int)rcap, (int)cwcap, (int)taps, cur_stream()));
+}
+
 // ---------------------------------------------------------------- top-k
 void row_topk(const at::Tensor& scores, int64_t k, double scale, at::Tensor out_v, at::Tensor out_i,
               const c10::optional<at::Tensor>& out_lse, int64_t index_offset) {
@@ -1026,6 +1058,8 @@ TORCH_LIBRARY(lumen, m) {
   m.def("image_prep(Tensor src, Tensor geom, Tensor(o!) out, Tensor(t!) tmp, int out_h, int out_w, int filter, "
         "bool swap_rb, float[] mean, float[] std, float scale, float pad, int layout, int patch, int kpad, "
         "int max_ch, int max_dw) -> ()");
+  m.def("image_prep_band(Tensor src, Tensor geom, Tensor(o!) out, int out_h, int out_w, int filter, bool swap_rb, "
+        "float[] mean, float[] std, float scale, float pad, int patch, int kpad, int rcap, int cwcap, int taps) -> ()");
   m.def("row_topk(Tensor scores, int k, float scale, Tensor(v!) out_v, Tensor(i!) out_i, Tensor(l!)? out_lse, "
         "int index_offset) -> ()");
   m.def("conv2d(Tensor x, Tensor w, Tensor? bias, Tensor? residual, Tensor? prelu, int act, int[] stride, "
@@ -1062,6 +1096,7 @@ TORCH_LIBRARY_IMPL(lumen, CUDA, m) {
   m.impl("attention", &attention);
   m.impl("attention_mx", &attention_mx);
   m.impl("image_prep", &image_prep2);
+  m.impl("image_prep_band", &image_prep_band);
   m.impl("row_topk", &row_topk);
   m.impl("conv2d", &conv2d);
   m.impl("conv2d_dw", &conv2d_dw);

@@ -733,6 +733,40 @@ def _filt(x, f):
     return 1 - x if x < 1 else 0.0
 
 
+# the fused band kernel only where three workgroups fit a CU's 160 KB of LDS: ViT-L/14 b512 0.63 -> 0.35 ms;
+# at one workgroup per CU (ViT-B/32: 43 KB patch image + 43 staged rows) it lost to the two passes, 0.77 vs
+# 0.58 ms (profiles/r6_prep_band_v1.txt)
+_PREP_BAND_LDS = 53 * 1024
+
+
+def _prep_band_bounds(geoms, filt: int, lay: int, patch: int, kpad: int, OW: int, out_dtype,
+                      pad: float = 0.0) -> Optional[tuple]:
+    """(rcap, cwcap, taps) for the fused per-band prep kernel, or None when it does not apply: canvas rows
+    one band of ``patch`` output rows reads, staged canvas columns, and taps per resampling window,
+    bounded over the batch
+    (windows span < 2 * support * max(scale, 1) + 1 samples; a band's windows start and end within
+    (patch - 1) * scale of each other)."""
+    if lay != 2 or filt not in (0, 1) or out_dtype != torch.bfloat16 or kpad % 8 or patch <= 0 or OW % patch:
+        return None
+    if not (float(pad).is_integer() and 0 <= pad <= 255):   # the canvas is staged as bytes
+        return None
+    sup = 2.0 if filt == 0 else 1.0
+    taps = rcap = cwcap = 0
+    for cw, dw, ch, dh in {(gg.cw, gg.dw, gg.ch, gg.dh) for gg in geoms}:
+        sx, sy = cw / dw, ch / dh
+        supx, supy = sup * max(sx, 1.0), sup * max(sy, 1.0)
+        taps = max(taps, int(math.floor(2 * supx)) + 2, int(math.floor(2 * supy)) + 2)
+        rcap = max(rcap, int(math.ceil((patch - 1) * sy + 2 * supy)) + 2)   # rows < (patch-1)s + 2 sup + 1
+        cwcap = max(cwcap, cw)
+    if taps > 16:
+        return None
+    tm = 8 if taps <= 8 else 16
+    r16 = lambda n: (n + 15) // 16 * 16  # noqa: E731
+    ra = r16(OW * (tm + 3) * 4) + rcap * cwcap * 4                        # csrc/image.hip image_prep_band_lds
+    lds = r16(patch * (tm + 3) * 4) + r16(max(ra, (OW // patch) * kpad * 2)) + rcap * OW * 4 + 16
+    return (rcap, cwcap, taps) if lds <= _PREP_BAND_LDS else None
+
+
 def image_prep(
     images: Sequence[torch.Tensor] | torch.Tensor,
     out_hw: tuple[int, int],
@@ -799,6 +833,12 @@ def image_prep(
             src = flat_src if flat_src is not None else torch.cat([im.reshape(-1) for im in imgs])
             src = src.to(device, non_blocking=True)
         g = h2d([gg.row() for gg in geoms], device, torch.long)
+        band = _prep_band_bounds(geoms, filt, lay, patch, kpad, OW, out_dtype, pad)
+        if band is not None:          # ViT patch rows, PIL filters: one fused launch (csrc/image.hip)
+            hip_ops().image_prep_band(src, g, out, OH, OW, filt, bool(swap_rb), [float(m) for m in mean],
+                                      [float(s) for s in std], float(scale), float(pad), int(patch), int(kpad),
+                                      band[0], band[1], band[2])
+            return out
         max_ch = max(gg.ch for gg in geoms)
         max_dw = max(gg.dw for gg in geoms)
         tmp = torch.empty((B, max_ch, max_dw, 3), device=device, dtype=torch.float32)

@@ -304,3 +304,54 @@ def test_gemm_layernorm_folded(M, N, K, tile, act):
     got = ops.linear_lnf(xd, wf, ca, st, act=act, tile=tile).cpu().float()
     assert _rel(got[rows], ref) < 1e-2
     assert torch.isfinite(got).all()
+
+
+@pytest.mark.parametrize("case", ["vit_l14", "vit_b32", "ragged", "center_crop", "bilinear_swap", "upscale",
+                                  "big_downscale", "pad_square", "odd_offsets"])
+def test_image_prep_band_kernel_bit_identical_to_two_pass(case, monkeypatch):
+    """csrc/image.hip prep_band_kernel (fused per-band ViT prep: uint8 row pass in LDS) against the
+    two-pass prep_h / prep_v path it replaces for patch rows with the PIL filters: same weights,
+    same accumulation order -> identical bf16 bits."""
+    g = torch.Generator().manual_seed(11)
+    r = lambda h, w: torch.randint(0, 256, (h, w, 3), generator=g, dtype=torch.uint8)  # noqa: E731
+    kw = dict(mean=(0.48, 0.46, 0.41), std=(0.27, 0.26, 0.28), layout="patches", out_dtype=torch.bfloat16)
+    out, patch, kpad = (224, 14, 640)
+    if case == "vit_l14":
+        imgs = torch.randint(0, 256, (6, 256, 256, 3), generator=g, dtype=torch.uint8)
+    elif case == "vit_b32":
+        imgs, (out, patch, kpad) = torch.randint(0, 256, (3, 256, 256, 3), generator=g, dtype=torch.uint8), (224, 32, 3072)
+    elif case == "ragged":
+        imgs = [r(300, 200), r(97, 411), r(224, 224), r(640, 480)]
+    elif case == "center_crop":
+        imgs, kw["center_crop"] = [r(300, 200), r(97, 411), r(500, 500)], True
+    elif case == "bilinear_swap":
+        imgs, kw["filter"], kw["swap_rb"] = [r(333, 250), r(120, 90)], "pil_bilinear", True
+    elif case == "upscale":
+        imgs, (out, patch, kpad) = [r(40, 30), r(17, 64)], (336, 14, 640)
+    elif case == "pad_square":           # VLM pad-to-square canvas with an integral pad value
+        imgs, kw["pad"], (out, patch, kpad) = [r(200, 150), r(90, 160)], 122.0, (336, 14, 640)
+        kw["geoms"] = None
+    elif case == "odd_offsets":          # ragged flat buffer: rows start at unaligned byte offsets
+        imgs = [r(37, 53), r(101, 77), r(64, 65)]
+    else:
+        imgs = [r(1024, 768), r(900, 1400)]
+    if case == "pad_square":
+        geoms, off = [], 0
+        for im in imgs:
+            geoms.append(ops.ImageGeom.pad_square(im.shape[0], im.shape[1], off, out))
+            off += im.numel()
+        kw["geoms"] = geoms
+    if isinstance(imgs, torch.Tensor):
+        dimgs = imgs.to(DEV)
+    else:
+        dimgs = [i.to(DEV) for i in imgs]
+    monkeypatch.setattr(ops, "_PREP_BAND_LDS", 96 * 1024)   # every case through the band kernel
+    assert ops._prep_band_bounds([ops.ImageGeom.resize(8, 8, 0, out, out)], 0, 2, patch, kpad, out,
+                                 torch.bfloat16) is not None
+    band = ops.image_prep(dimgs, (out, out), patch=patch, kpad=kpad, **kw)
+    monkeypatch.setattr(ops, "_prep_band_bounds", lambda *a, **k: None)
+    two = ops.image_prep(dimgs, (out, out), patch=patch, kpad=kpad, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(band.view(torch.int16), two.view(torch.int16))
+    ref = ops.image_prep(imgs, (out, out), patch=patch, kpad=kpad, **kw)          # CPU reference
+    assert (band.cpu().float() - ref.float()).abs().max().item() <= 0.05

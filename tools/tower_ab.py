@@ -4,6 +4,7 @@ module flag of lumen_amd.models.clip off and on.
 
     python tools/tower_ab.py --flag _LN_FOLD [--model ViT-L-14] [--batch 512] [--rounds 5] [--steps 10]
     python tools/tower_ab.py --tuning ln_multi_row        # a kernel-variant switch (csrc/tuning.h) instead
+    python tools/tower_ab.py --flag ops._PREP_BAND_LDS --values 0,54272   # a lumen_amd.ops module flag
 """
 import argparse
 import json
@@ -42,10 +43,12 @@ def main():
         base = True
         args.flag = f"tuning:{args.tuning}"
     else:
-        base = getattr(clip_mod, args.flag)
+        from lumen_amd import ops as ops_mod
+        mod, name = (ops_mod, args.flag[4:]) if args.flag.startswith("ops.") else (clip_mod, args.flag)
+        base = getattr(mod, name)
 
         def setter(v):
-            setattr(clip_mod, args.flag, v)
+            setattr(mod, name, v)
     arms = {"off": False if isinstance(base, bool) else 0, "on": True if isinstance(base, bool) else 1}
     if args.values:       # two explicit values of an int flag (e.g. --flag _VIT_MICRO --values 2,3)
         a, b = (int(v) for v in args.values.split(","))
