@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--host-decode", action="store_true", help="Pillow on the host instead of the device JPEG path")
     ap.add_argument("--fp8", action="store_true", help="weight-only OCP e4m3 decoder weights (per-channel scales)")
     ap.add_argument("--kv-fp8", action="store_true", help="OCP e4m3 paged KV cache (unit scale)")
+    ap.add_argument("--gap-ms", type=float, default=0.0,
+                    help="idle time between the TTFT requests (0: back to back, the next request arrives as the "
+                         "previous stream ends)")
     ap.add_argument("--image-kind", choices=["noise", "photo"], default="noise",
                     help="synthetic JPEG content: uniform noise (worst-case host decode) or photo-like")
     args = ap.parse_args()
@@ -122,6 +125,8 @@ def main():
     ttft, tps, queue_ms, admit_first_ms = [], [], [], []
     dec_ms.clear()
     for _ in range(args.n):
+        if args.gap_ms > 0:
+            time.sleep(args.gap_ms / 1000)
         r, times = one(args.max_new)
         ttft.append((r.t_first - r.t_arrive) * 1000)
         queue_ms.append((r.t_admit - r.t_submit) * 1000)
@@ -139,7 +144,8 @@ def main():
                           "queue": float(np.median(queue_ms)), "build_host_ms": float(np.median(build_ms[-args.n:])),
                           "encode_ahead_host_ms": float(np.median(enc_ms[-args.n:])) if enc_ms else None,
                           "jpeg_decode": float(np.median(dec_ms[:args.n])),
-                          "decode_tok_s_single": float(np.median(tps)) if tps else None, "n": args.n}))
+                          "decode_tok_s_single": float(np.median(tps)) if tps else None, "n": args.n,
+                          "gap_ms": args.gap_ms}))
         return
     t1 = time.perf_counter()
     with ThreadPoolExecutor(max_workers=max(args.batch, 1)) as ex:
