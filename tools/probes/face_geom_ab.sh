@@ -1,5 +1,6 @@
 set -o pipefail
 # same-box A/B of the batched face alignment geometry (arm slow: the per-face similarity + inverse loop)
+# (the "fast" arm needs the batched geometry that lost this A/B and was reverted: profiles/r6_face_geom_ab_v1.txt)
 for arm in slow fast slow fast; do
   timeout -k 10 300 python -c "
 import sys, runpy, numpy as np
